@@ -1,0 +1,491 @@
+// BatchNorm (training + eval), fused MaskConv epilogue (mask + Hardtanh + the
+// NCDT -> T,N,(C*D) collapse) and their backward passes.  HBM-bound.
+//
+// Reductions accumulate in fp64 per workgroup and combine the partials in a
+// fixed order (deterministic; no atomics).  Two reduction shapes:
+//   rows   : x is [R][C] (SequenceWise BatchNorm1d, model.py:28-43,89,336)
+//            block = 64 columns x 4 row groups, grid = column blocks x row chunks
+//   planes : x is [outer][C][D][T] (BatchNorm2d, model.py:210,213)
+//            block = one (outer, channel) plane slice, threads stride along T
+#include "common.h"
+
+namespace ds2 {
+
+constexpr int kRowChunks = 64;    // row chunks for the [R][C] reduction
+constexpr int kPlaneSplit = 4;    // slices per (outer, channel) plane
+
+enum RedMode { RED_STATS = 0, RED_BWD = 1 };
+
+struct BnBwdArgs {
+  const float* mean;
+  const float* invstd;
+  const float* gamma;
+  const float* beta;
+  const int* lens;
+  float lo, hi;
+  int masked;
+};
+
+// g (the upstream gradient after the mask/hardtanh backward) at one element.
+__device__ __forceinline__ float bwd_g(float dy, float x, int c, int t, int len,
+                                       const BnBwdArgs& a, float* xhat_out) {
+  const float xhat = (x - a.mean[c]) * a.invstd[c];
+  *xhat_out = xhat;
+  if (!a.masked) return dy;
+  if (t >= len) return 0.f;
+  const float y2 = a.gamma[c] * xhat + a.beta[c];
+  // torch hardtanh_backward: pass where min_val < x < max_val (strict)
+  return (y2 > a.lo && y2 < a.hi) ? dy : 0.f;
+}
+
+// ---- rows reduction ---------------------------------------------------------
+template <int MODE>
+__global__ __launch_bounds__(256) void reduce_rows_kernel(const float* __restrict__ x,
+                                                          const float* __restrict__ dy, int R,
+                                                          int C, BnBwdArgs a,
+                                                          double* __restrict__ partial) {
+  __shared__ double s0[4][64], s1[4][64];
+  const int lane = threadIdx.x & 63;
+  const int grp = threadIdx.x >> 6;
+  const int col = blockIdx.x * 64 + lane;
+  const int chunk = blockIdx.y;
+  const int per = (R + gridDim.y - 1) / gridDim.y;
+  const int r0 = chunk * per;
+  const int r1 = min(R, r0 + per);
+  double acc0 = 0.0, acc1 = 0.0;
+  if (col < C) {
+    for (int r = r0 + grp; r < r1; r += 4) {
+      const float v = x[(int64_t)r * C + col];
+      if (MODE == RED_STATS) {
+        acc0 += v;
+        acc1 += (double)v * v;
+      } else {
+        float xhat;
+        const float g = bwd_g(dy[(int64_t)r * C + col], v, col, 0, 1, a, &xhat);
+        acc0 += g;
+        acc1 += (double)g * xhat;
+      }
+    }
+  }
+  s0[grp][lane] = acc0;
+  s1[grp][lane] = acc1;
+  __syncthreads();
+  if (grp == 0 && col < C) {
+    double t0 = s0[0][lane] + s0[1][lane] + s0[2][lane] + s0[3][lane];
+    double t1 = s1[0][lane] + s1[1][lane] + s1[2][lane] + s1[3][lane];
+    partial[((int64_t)chunk * C + col) * 2 + 0] = t0;
+    partial[((int64_t)chunk * C + col) * 2 + 1] = t1;
+  }
+}
+
+// ---- planes reduction -------------------------------------------------------
+// grid (C, outer, kPlaneSplit); the plane [D][T] is split by D-rows.
+template <int MODE>
+__global__ __launch_bounds__(256) void reduce_planes_kernel(const float* __restrict__ x,
+                                                            const float* __restrict__ dy, int C,
+                                                            int D, int T, BnBwdArgs a,
+                                                            double* __restrict__ partial) {
+  const int c = blockIdx.x;
+  const int o = blockIdx.y;
+  const int sl = blockIdx.z;
+  const int per = (D + gridDim.z - 1) / gridDim.z;
+  const int d0 = sl * per;
+  const int d1 = min(D, d0 + per);
+  const int64_t base = ((int64_t)o * C + c) * D * T;
+  const int len = (MODE == RED_BWD && a.masked) ? a.lens[o] : T;
+  double acc0 = 0.0, acc1 = 0.0;
+  for (int d = d0; d < d1; ++d) {
+    const int64_t rb = base + (int64_t)d * T;
+    for (int t = threadIdx.x; t < T; t += blockDim.x) {
+      const float v = x[rb + t];
+      if (MODE == RED_STATS) {
+        acc0 += v;
+        acc1 += (double)v * v;
+      } else {
+        float xhat;
+        const float g = bwd_g(dy[rb + t], v, c, t, len, a, &xhat);
+        acc0 += g;
+        acc1 += (double)g * xhat;
+      }
+    }
+  }
+  __shared__ double r0[4], r1[4];
+  acc0 = wave_sum_d(acc0);
+  acc1 = wave_sum_d(acc1);
+  if ((threadIdx.x & 63) == 0) {
+    r0[threadIdx.x >> 6] = acc0;
+    r1[threadIdx.x >> 6] = acc1;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int64_t pidx = ((int64_t)o * gridDim.z + sl) * C + c;
+    partial[pidx * 2 + 0] = r0[0] + r0[1] + r0[2] + r0[3];
+    partial[pidx * 2 + 1] = r1[0] + r1[1] + r1[2] + r1[3];
+  }
+}
+
+// ---- finalize ---------------------------------------------------------------
+__global__ void stats_final_kernel(const double* __restrict__ partial, int nparts, int C,
+                                   double count, float eps, float momentum,
+                                   float* __restrict__ save_mean, float* __restrict__ save_invstd,
+                                   float* __restrict__ running_mean,
+                                   float* __restrict__ running_var) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s = 0.0, ss = 0.0;
+  for (int p = 0; p < nparts; ++p) {
+    s += partial[((int64_t)p * C + c) * 2 + 0];
+    ss += partial[((int64_t)p * C + c) * 2 + 1];
+  }
+  const double mean = s / count;
+  double var = ss / count - mean * mean;
+  if (var < 0.0) var = 0.0;
+  save_mean[c] = static_cast<float>(mean);
+  save_invstd[c] = static_cast<float>(1.0 / sqrt(var + (double)eps));
+  if (running_mean != nullptr) {
+    const double unbiased = count > 1.0 ? var * count / (count - 1.0) : var;
+    running_mean[c] = static_cast<float>((1.0 - momentum) * running_mean[c] + momentum * mean);
+    running_var[c] = static_cast<float>((1.0 - momentum) * running_var[c] + momentum * unbiased);
+  }
+}
+
+__global__ void eval_stats_kernel(const float* __restrict__ rm, const float* __restrict__ rv,
+                                  int C, float eps, float* __restrict__ mean,
+                                  float* __restrict__ invstd) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  mean[c] = rm[c];
+  invstd[c] = static_cast<float>(1.0 / sqrt((double)rv[c] + (double)eps));
+}
+
+// sums -> per-channel coefficients for the backward apply:
+//   dx = k1 * g - k2 - k3 * xhat  with k1 = gamma*invstd, k2 = k1*mean(g),
+//   k3 = k1*mean(g*xhat); also dgamma = sum(g*xhat), dbeta = sum(g) and the
+//   closed-form bias gradient (see ds2_bn_backward).
+__global__ void bwd_final_kernel(const double* __restrict__ partial, int nparts, int C,
+                                 double count, BnBwdArgs a, int n_outer, int D, int T,
+                                 float* __restrict__ coef, float* __restrict__ dgamma,
+                                 float* __restrict__ dbeta, float* __restrict__ dbias) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double sg = 0.0, sgx = 0.0;
+  for (int p = 0; p < nparts; ++p) {
+    sg += partial[((int64_t)p * C + c) * 2 + 0];
+    sgx += partial[((int64_t)p * C + c) * 2 + 1];
+  }
+  const double gbar = sg / count;
+  const double gxbar = sgx / count;
+  const double k1 = (double)a.gamma[c] * a.invstd[c];
+  coef[c * 3 + 0] = static_cast<float>(k1);
+  coef[c * 3 + 1] = static_cast<float>(k1 * gbar);
+  coef[c * 3 + 2] = static_cast<float>(k1 * gxbar);
+  if (dgamma != nullptr) dgamma[c] = static_cast<float>(sgx);
+  if (dbeta != nullptr) dbeta[c] = static_cast<float>(sg);
+  if (dbias != nullptr) {
+    // d bias = sum over unmasked positions of d x1
+    //        = gamma*invstd*(M - cnt_u)*(gbar - gxbar*invstd*mean)
+    double cnt_u = 0.0;
+    if (a.masked) {
+      for (int o = 0; o < n_outer; ++o) cnt_u += (double)max(0, min(a.lens[o], T)) * D;
+    } else {
+      cnt_u = count;
+    }
+    const double v = k1 * (count - cnt_u) * (gbar - gxbar * (double)a.invstd[c] * a.mean[c]);
+    dbias[c] = static_cast<float>(v);
+  }
+}
+
+// ---- apply ------------------------------------------------------------------
+__global__ void apply_rows_kernel(const float* __restrict__ x, int64_t R, int C,
+                                  const float* __restrict__ mean, const float* __restrict__ invstd,
+                                  const float* __restrict__ gamma, const float* __restrict__ beta,
+                                  float* __restrict__ y) {
+  // vectorised: C % 4 == 0
+  const int64_t total4 = R * C / 4;
+  const int C4 = C / 4;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total4;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int c = static_cast<int>(i % C4) * 4;
+    float4 v = reinterpret_cast<const float4*>(x)[i];
+    v.x = gamma[c + 0] * ((v.x - mean[c + 0]) * invstd[c + 0]) + beta[c + 0];
+    v.y = gamma[c + 1] * ((v.y - mean[c + 1]) * invstd[c + 1]) + beta[c + 1];
+    v.z = gamma[c + 2] * ((v.z - mean[c + 2]) * invstd[c + 2]) + beta[c + 2];
+    v.w = gamma[c + 3] * ((v.w - mean[c + 3]) * invstd[c + 3]) + beta[c + 3];
+    reinterpret_cast<float4*>(y)[i] = v;
+  }
+}
+
+__global__ void apply_generic_kernel(const float* __restrict__ x, int64_t total, int C,
+                                     int64_t inner, const float* __restrict__ mean,
+                                     const float* __restrict__ invstd,
+                                     const float* __restrict__ gamma,
+                                     const float* __restrict__ beta, float* __restrict__ y) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int c = static_cast<int>((i / inner) % C);
+    y[i] = gamma[c] * ((x[i] - mean[c]) * invstd[c]) + beta[c];
+  }
+}
+
+// MaskConv epilogue, NCDT output.  grid (ceil(T/256), D, N*C)
+__global__ void apply_mask_htanh_ncdt_kernel(const float* __restrict__ x, int N, int C, int D,
+                                             int T, const float* __restrict__ mean,
+                                             const float* __restrict__ invstd,
+                                             const float* __restrict__ gamma,
+                                             const float* __restrict__ beta,
+                                             const int* __restrict__ lens, float lo, float hi,
+                                             float* __restrict__ y) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  const int d = blockIdx.y;
+  const int nc = blockIdx.z;
+  const int n = nc / C;
+  const int c = nc - n * C;
+  if (t >= T) return;
+  const int64_t idx = ((int64_t)nc * D + d) * T + t;
+  const int len = lens != nullptr ? lens[n] : T;
+  float v = gamma[c] * ((x[idx] - mean[c]) * invstd[c]) + beta[c];
+  if (t >= len) v = 0.f;
+  v = fminf(fmaxf(v, lo), hi);
+  if (t >= len) v = 0.f;
+  y[idx] = v;
+}
+
+// MaskConv epilogue with the TxNx(C*D) collapse.  64(f) x 64(t) LDS tile.
+// grid (ceil(T/64), ceil(F/64), N) with F = C*D, block 256.
+__global__ __launch_bounds__(256) void apply_mask_htanh_tnf_kernel(
+    const float* __restrict__ x, int N, int C, int D, int T, const float* __restrict__ mean,
+    const float* __restrict__ invstd, const float* __restrict__ gamma,
+    const float* __restrict__ beta, const int* __restrict__ lens, float lo, float hi,
+    float* __restrict__ y) {
+  __shared__ float tile[64][65];
+  const int t0 = blockIdx.x * 64;
+  const int f0 = blockIdx.y * 64;
+  const int n = blockIdx.z;
+  const int F = C * D;
+  const int len = lens != nullptr ? lens[n] : T;
+  const int tl = threadIdx.x & 63;
+  const int q = threadIdx.x >> 6;
+#pragma unroll 4
+  for (int i = 0; i < 16; ++i) {
+    const int fl = i * 4 + q;
+    const int f = f0 + fl;
+    const int t = t0 + tl;
+    float v = 0.f;
+    if (f < F && t < T) {
+      const int c = f / D;
+      v = gamma[c] * ((x[((int64_t)n * F + f) * T + t] - mean[c]) * invstd[c]) + beta[c];
+      if (t >= len) v = 0.f;
+      v = fminf(fmaxf(v, lo), hi);
+      if (t >= len) v = 0.f;
+    }
+    tile[fl][tl] = v;
+  }
+  __syncthreads();
+#pragma unroll 4
+  for (int i = 0; i < 16; ++i) {
+    const int tt = i * 4 + q;
+    const int t = t0 + tt;
+    const int f = f0 + tl;
+    if (t < T && f < F) y[((int64_t)t * N + n) * F + f] = tile[tl][tt];
+  }
+}
+
+// dst[n][f][t] = src[t][n][f]  (inverse of the collapse), 64x64 tiles.
+__global__ __launch_bounds__(256) void tnf_to_nft_kernel(const float* __restrict__ src, int N,
+                                                         int F, int T, float* __restrict__ dst) {
+  __shared__ float tile[64][65];
+  const int t0 = blockIdx.x * 64;
+  const int f0 = blockIdx.y * 64;
+  const int n = blockIdx.z;
+  const int l = threadIdx.x & 63;
+  const int q = threadIdx.x >> 6;
+#pragma unroll 4
+  for (int i = 0; i < 16; ++i) {
+    const int tt = i * 4 + q;
+    const int t = t0 + tt;
+    const int f = f0 + l;
+    tile[tt][l] = (t < T && f < F) ? src[((int64_t)t * N + n) * F + f] : 0.f;
+  }
+  __syncthreads();
+#pragma unroll 4
+  for (int i = 0; i < 16; ++i) {
+    const int fl = i * 4 + q;
+    const int f = f0 + fl;
+    const int t = t0 + l;
+    if (t < T && f < F) dst[((int64_t)n * F + f) * T + t] = tile[l][fl];
+  }
+}
+
+// backward apply over [outer][C][D][T] (rows case: D = T = 1 -> inner = 1)
+__global__ void bwd_apply_planes_kernel(const float* __restrict__ dy, const float* __restrict__ x,
+                                        int C, int D, int T, BnBwdArgs a,
+                                        const float* __restrict__ coef, float* __restrict__ dx) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  const int d = blockIdx.y;
+  const int oc = blockIdx.z;
+  const int o = oc / C;
+  const int c = oc - o * C;
+  if (t >= T) return;
+  const int64_t idx = ((int64_t)oc * D + d) * T + t;
+  const int len = a.masked ? a.lens[o] : T;
+  float xhat;
+  const float g = bwd_g(dy[idx], x[idx], c, t, len, a, &xhat);
+  float v = coef[c * 3 + 0] * g - coef[c * 3 + 1] - coef[c * 3 + 2] * xhat;
+  if (a.masked && t >= len) v = 0.f;
+  dx[idx] = v;
+}
+
+__global__ void bwd_apply_rows_kernel(const float* __restrict__ dy, const float* __restrict__ x,
+                                      int64_t R, int C, BnBwdArgs a,
+                                      const float* __restrict__ coef, float* __restrict__ dx) {
+  const int64_t total = R * C;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int c = static_cast<int>(i % C);
+    const float xhat = (x[i] - a.mean[c]) * a.invstd[c];
+    dx[i] = coef[c * 3 + 0] * dy[i] - coef[c * 3 + 1] - coef[c * 3 + 2] * xhat;
+  }
+}
+
+static inline int grid_cap(int64_t work, int block) {
+  int64_t g = (work + block - 1) / block;
+  return static_cast<int>(g > 2048 ? 2048 : (g < 1 ? 1 : g));
+}
+
+static inline size_t partial_parts(int outer, int c, int inner) {
+  (void)c;
+  if (inner == 1) return kRowChunks;
+  return (size_t)outer * kPlaneSplit;
+}
+
+}  // namespace ds2
+
+using namespace ds2;
+
+extern "C" {
+
+size_t ds2_bn_workspace_size(int outer, int c, int inner) {
+  return partial_parts(outer, c, inner) * (size_t)c * 2 * sizeof(double) +
+         (size_t)c * 3 * sizeof(float) + 256;
+}
+
+ds2_status_t ds2_bn_train_stats(const float* x, int outer, int c, int inner, float eps,
+                                float momentum, float* save_mean, float* save_invstd,
+                                float* running_mean, float* running_var, void* ws,
+                                size_t ws_bytes, ds2_stream_t stream) {
+  if (outer < 1 || c < 1 || inner < 1) return DS2_INVALID_VALUE;
+  if (ws == nullptr || ws_bytes < ds2_bn_workspace_size(outer, c, inner))
+    return DS2_WORKSPACE_TOO_SMALL;
+  hipStream_t st = as_stream(stream);
+  double* partial = static_cast<double*>(ws);
+  BnBwdArgs a{};
+  int nparts;
+  if (inner == 1) {
+    nparts = kRowChunks;
+    hipLaunchKernelGGL(reduce_rows_kernel<RED_STATS>, dim3(cdiv(c, 64), kRowChunks), dim3(256), 0,
+                       st, x, nullptr, outer, c, a, partial);
+  } else {
+    nparts = outer * kPlaneSplit;
+    hipLaunchKernelGGL(reduce_planes_kernel<RED_STATS>, dim3(c, outer, kPlaneSplit), dim3(256), 0,
+                       st, x, nullptr, c, 1, inner, a, partial);
+  }
+  hipLaunchKernelGGL(stats_final_kernel, dim3(cdiv(c, 256)), dim3(256), 0, st, partial, nparts, c,
+                     (double)outer * inner, eps, momentum, save_mean, save_invstd, running_mean,
+                     running_var);
+  return launch_status("ds2_bn_train_stats");
+}
+
+ds2_status_t ds2_bn_eval_stats(const float* running_mean, const float* running_var, int c,
+                               float eps, float* save_mean, float* save_invstd,
+                               ds2_stream_t stream) {
+  if (c < 1) return DS2_INVALID_VALUE;
+  hipLaunchKernelGGL(eval_stats_kernel, dim3(cdiv(c, 256)), dim3(256), 0, as_stream(stream),
+                     running_mean, running_var, c, eps, save_mean, save_invstd);
+  return launch_status("ds2_bn_eval_stats");
+}
+
+ds2_status_t ds2_bn_apply(const float* x, int outer, int c, int inner, const float* mean,
+                          const float* invstd, const float* gamma, const float* beta, float* y,
+                          ds2_stream_t stream) {
+  if (outer < 0 || c < 1 || inner < 1) return DS2_INVALID_VALUE;
+  const int64_t total = (int64_t)outer * c * inner;
+  if (total == 0) return DS2_OK;
+  hipStream_t st = as_stream(stream);
+  const bool vec = inner == 1 && (c % 4 == 0) &&
+                   ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y)) & 15) == 0;
+  if (vec)
+    hipLaunchKernelGGL(apply_rows_kernel, dim3(grid_cap(total / 4, 256)), dim3(256), 0, st, x,
+                       (int64_t)outer, c, mean, invstd, gamma, beta, y);
+  else
+    hipLaunchKernelGGL(apply_generic_kernel, dim3(grid_cap(total, 256)), dim3(256), 0, st, x,
+                       total, c, (int64_t)inner, mean, invstd, gamma, beta, y);
+  return launch_status("ds2_bn_apply");
+}
+
+ds2_status_t ds2_bn_apply_mask_htanh(const float* x, int n, int c, int d, int t,
+                                     const float* mean, const float* invstd, const float* gamma,
+                                     const float* beta, const int* lens, float lo, float hi,
+                                     float* y, int out_layout, ds2_stream_t stream) {
+  if (n < 0 || c < 1 || d < 1 || t < 0) return DS2_INVALID_VALUE;
+  if ((int64_t)n * c * d * t == 0) return DS2_OK;
+  hipStream_t st = as_stream(stream);
+  if (out_layout == 0) {
+    hipLaunchKernelGGL(apply_mask_htanh_ncdt_kernel, dim3(cdiv(t, 256), d, n * c), dim3(256), 0,
+                       st, x, n, c, d, t, mean, invstd, gamma, beta, lens, lo, hi, y);
+  } else if (out_layout == 1) {
+    hipLaunchKernelGGL(apply_mask_htanh_tnf_kernel, dim3(cdiv(t, 64), cdiv(c * d, 64), n),
+                       dim3(256), 0, st, x, n, c, d, t, mean, invstd, gamma, beta, lens, lo, hi,
+                       y);
+  } else {
+    return DS2_INVALID_VALUE;
+  }
+  return launch_status("ds2_bn_apply_mask_htanh");
+}
+
+ds2_status_t ds2_bn_backward(const float* dy, int dy_layout, const float* x, int outer, int c,
+                             int d, int t, const float* mean, const float* invstd,
+                             const float* gamma, const float* beta, int masked,
+                             const int* lens, float lo, float hi, float* dx, float* dgamma,
+                             float* dbeta, float* dbias_in, void* ws, size_t ws_bytes,
+                             ds2_stream_t stream) {
+  if (outer < 1 || c < 1 || d < 1 || t < 1) return DS2_INVALID_VALUE;
+  if (dy_layout == 1 && !masked) return DS2_INVALID_VALUE;
+  if (masked && lens == nullptr) return DS2_INVALID_VALUE;
+  const int inner = d * t;
+  if (ws == nullptr || ws_bytes < ds2_bn_workspace_size(outer, c, inner))
+    return DS2_WORKSPACE_TOO_SMALL;
+  hipStream_t st = as_stream(stream);
+  const size_t nparts = partial_parts(outer, c, inner);
+  double* partial = static_cast<double*>(ws);
+  float* coef = reinterpret_cast<float*>(partial + nparts * c * 2);
+  BnBwdArgs a{mean, invstd, gamma, beta, lens, lo, hi, masked};
+
+  const float* g_src = dy;
+  if (dy_layout == 1) {
+    // bring dy into the [n][c*d][t] layout of x, inside dx (same size)
+    hipLaunchKernelGGL(tnf_to_nft_kernel, dim3(cdiv(t, 64), cdiv(c * d, 64), outer), dim3(256),
+                       0, st, dy, outer, c * d, t, dx);
+    g_src = dx;
+  }
+  if (inner == 1) {
+    hipLaunchKernelGGL(reduce_rows_kernel<RED_BWD>, dim3(cdiv(c, 64), kRowChunks), dim3(256), 0,
+                       st, x, g_src, outer, c, a, partial);
+  } else {
+    hipLaunchKernelGGL(reduce_planes_kernel<RED_BWD>, dim3(c, outer, kPlaneSplit), dim3(256), 0,
+                       st, x, g_src, c, d, t, a, partial);
+  }
+  hipLaunchKernelGGL(bwd_final_kernel, dim3(cdiv(c, 256)), dim3(256), 0, st, partial,
+                     (int)nparts, c, (double)outer * inner, a, outer, d, t, coef, dgamma, dbeta,
+                     dbias_in);
+  if (inner == 1) {
+    hipLaunchKernelGGL(bwd_apply_rows_kernel, dim3(grid_cap((int64_t)outer * c, 256)), dim3(256),
+                       0, st, g_src, x, (int64_t)outer, c, a, coef, dx);
+  } else {
+    // elementwise and position-local: safe in place when g_src == dx
+    hipLaunchKernelGGL(bwd_apply_planes_kernel, dim3(cdiv(t, 256), d, outer * c), dim3(256), 0,
+                       st, g_src, x, c, d, t, a, coef, dx);
+  }
+  return launch_status("ds2_bn_backward");
+}
+
+}  // extern "C"

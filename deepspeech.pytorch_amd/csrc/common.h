@@ -1,0 +1,67 @@
+// Shared helpers for the libds2hip kernels (gfx950 / CDNA4 only).
+//
+// Conventions (see include/ds2hip.h):
+//   * every entry point is extern "C", returns ds2_status_t, enqueues work on
+//     the caller's stream and never allocates, synchronises or throws;
+//   * device buffers are caller-owned; scratch comes in through (ws, ws_bytes).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+
+#include "../../include/ds2hip.h"
+
+namespace ds2 {
+
+// Wave width is fixed at 64 on CDNA; never use warpSize-derived 32 idioms.
+constexpr int kWave = 64;
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+inline hipStream_t as_stream(ds2_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+// Records the last HIP error string for ds2_last_error().
+void set_last_error(const char* where, hipError_t e);
+
+inline ds2_status_t launch_status(const char* where) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_last_error(where, e);
+    return DS2_HIP_ERROR;
+  }
+  return DS2_OK;
+}
+
+inline int cdiv(int64_t a, int64_t b) { return static_cast<int>((a + b - 1) / b); }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
+  return v;
+}
+
+// log(exp(a) + exp(b)) with -inf handling (CTC recursions).
+__device__ __forceinline__ float log_add(float a, float b) {
+  if (a == -INFINITY) return b;
+  if (b == -INFINITY) return a;
+  float m = fmaxf(a, b);
+  return m + log1pf(expf(-fabsf(a - b)));
+}
+
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+}  // namespace ds2

@@ -1,0 +1,437 @@
+// Conv2d (NCHW, fp32) as implicit GEMM on v_mfma_f32_32x32x2_f32.
+// ref model.py:208-215: conv1 W[32,1,41,11] s(2,2) p(20,5); conv2 W[32,32,21,11]
+// s(2,1) p(10,5); MaskConv (model.py:63-79) zeroes output columns w >= len.
+//
+//   fwd  : Y[co][p]  = sum_k W[co][k] * X[k][p]          p = (n, ho, wo) tile of one output row
+//   dgrad: DX[ci][q] = sum_k W'[ci][k] * DY[k][q]         q = (n, hi, wi) tile of one input row,
+//          k = (co, kh, kw) restricted to the kh of matching stride parity
+//   wgrad: DW[co][k] = sum_p DY[co][p] * X[k][p]          split over samples, slab reduce
+//
+// All three stage a [16][32] A tile and a [16][256 or 128] B tile k-major in LDS
+// (conflict-free fragment reads), double-buffered through registers: the
+// gathers of K-step i+1 are in flight while the MFMAs of step i run.
+#include "common.h"
+
+namespace ds2 {
+
+constexpr int CBK = 16;       // K per stage
+constexpr int CBN = 256;      // positions per workgroup (fwd / dgrad)
+constexpr int CBNW = 128;     // k-columns per workgroup (wgrad)
+
+struct ConvDims {
+  int n, ci, hi, wi, co, kh, kw, sh, sw, ph, pw, ho, wo;
+};
+
+// ---------------------------------------------------------------------------
+// forward. grid (ceil(Wo/256), Ho, N * ceil(Co/32)); block 256 (4 waves, each
+// 32 co x 64 positions = 2 MFMA tiles).
+__global__ __launch_bounds__(256) void conv_fwd_kernel(const float* __restrict__ x,
+                                                       const float* __restrict__ w,
+                                                       const float* __restrict__ bias,
+                                                       float* __restrict__ y, ConvDims g,
+                                                       const int* __restrict__ out_lens) {
+  __shared__ float As[2][CBK][32];
+  __shared__ float Bs[2][CBK][CBN];
+  const int cob = (g.co + 31) / 32;
+  const int n = blockIdx.z / cob;
+  const int co0 = (blockIdx.z - n * cob) * 32;
+  const int ho = blockIdx.y;
+  const int wo0 = blockIdx.x * CBN;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int K = g.ci * g.kh * g.kw;
+  const int KHW = g.kh * g.kw;
+
+  const int wo = wo0 + tid;           // this thread's B column
+  const int wi_base = wo * g.sw - g.pw;
+  const int hi_base = ho * g.sh - g.ph;
+  const float* xn = x + (int64_t)n * g.ci * g.hi * g.wi;
+
+  float rb[CBK], ra[2];
+  auto load = [&](int k0) {
+    // (ci, kh, kw) of k0 once (wave-uniform), then stepped: no per-element division
+    int ci = k0 / KHW;
+    int khh = (k0 - ci * KHW) / g.kw;
+    int kww = k0 - ci * KHW - khh * g.kw;
+#pragma unroll
+    for (int kk = 0; kk < CBK; ++kk) {
+      const int k = k0 + kk;
+      float v = 0.f;
+      const int hi = hi_base + khh;
+      const int wi = wi_base + kww;
+      if (k < K && wo < g.wo && hi >= 0 && hi < g.hi && wi >= 0 && wi < g.wi)
+        v = xn[((int64_t)ci * g.hi + hi) * g.wi + wi];
+      rb[kk] = v;
+      if (++kww == g.kw) { kww = 0; if (++khh == g.kh) { khh = 0; ++ci; } }
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int e = tid + 256 * q;      // 512 = 16 k x 32 co
+      const int kk = e & 15;
+      const int c = e >> 4;
+      const int k = k0 + kk;
+      ra[q] = (k < K && co0 + c < g.co) ? w[(int64_t)(co0 + c) * K + k] : 0.f;
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int kk = 0; kk < CBK; ++kk) Bs[buf][kk][tid] = rb[kk];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int e = tid + 256 * q;
+      As[buf][e & 15][e >> 4] = ra[q];
+    }
+  };
+
+  f32x16 acc0, acc1;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) { acc0[r] = 0.f; acc1[r] = 0.f; }
+  const int lr = lane & 31, lk = lane >> 5;
+  const int wn = wave * 64;
+  const int nk = (K + CBK - 1) / CBK;
+  load(0);
+  store(0);
+  __syncthreads();
+  for (int it = 0; it < nk; ++it) {
+    const int cur = it & 1;
+    if (it + 1 < nk) load((it + 1) * CBK);
+#pragma unroll
+    for (int kk = 0; kk < CBK; kk += 2) {
+      const float a = As[cur][kk + lk][lr];
+      const float b0 = Bs[cur][kk + lk][wn + lr];
+      const float b1 = Bs[cur][kk + lk][wn + 32 + lr];
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b0, acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b1, acc1, 0, 0, 0);
+    }
+    if (it + 1 < nk) store(cur ^ 1);
+    __syncthreads();
+  }
+  const int len = out_lens != nullptr ? out_lens[n] : g.wo;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int col = wo0 + wn + 32 * j + lr;
+    if (col >= g.wo) continue;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int c = co0 + (r & 3) + 8 * (r >> 2) + 4 * lk;
+      if (c < g.co) {
+        float v = (j == 0 ? acc0[r] : acc1[r]) + (bias != nullptr ? bias[c] : 0.f);
+        if (col >= len) v = 0.f;
+        y[(((int64_t)n * g.co + c) * g.ho + ho) * g.wo + col] = v;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// dgrad. grid (ceil(Wi/256), Hi, N * ceil(Ci/32)).
+__global__ __launch_bounds__(256) void conv_dgrad_kernel(const float* __restrict__ dy,
+                                                         const float* __restrict__ w,
+                                                         float* __restrict__ dx, ConvDims g) {
+  __shared__ float As[2][CBK][32];
+  __shared__ float Bs[2][CBK][CBN];
+  const int cib = (g.ci + 31) / 32;
+  const int n = blockIdx.z / cib;
+  const int ci0 = (blockIdx.z - n * cib) * 32;
+  const int hi = blockIdx.y;
+  const int wi0 = blockIdx.x * CBN;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  // valid kh: (hi + ph - kh) % sh == 0 and 0 <= (hi + ph - kh)/sh < ho
+  const int kh_first = (hi + g.ph) % g.sh;
+  const int nkh = kh_first < g.kh ? (g.kh - kh_first + g.sh - 1) / g.sh : 0;
+  const int K = g.co * nkh * g.kw;
+  const int KHW = nkh * g.kw;
+  const int wi = wi0 + tid;
+  const float* dyn = dy + (int64_t)n * g.co * g.ho * g.wo;
+
+  float rb[CBK], ra[2];
+  auto load = [&](int k0) {
+    int c = K > 0 ? k0 / KHW : 0;
+    int khi = K > 0 ? (k0 - c * KHW) / g.kw : 0;
+    int kww = K > 0 ? k0 - c * KHW - khi * g.kw : 0;
+#pragma unroll
+    for (int kk = 0; kk < CBK; ++kk) {
+      const int k = k0 + kk;
+      float v = 0.f;
+      const int khh = kh_first + khi * g.sh;
+      const int hnum = hi + g.ph - khh;             // divisible by sh by construction
+      const int hq = hnum / g.sh;
+      const int wnum = wi + g.pw - kww;
+      if (k < K && wi < g.wi && hnum >= 0 && hq < g.ho && wnum >= 0) {
+        if (g.sw == 1) {
+          if (wnum < g.wo) v = dyn[((int64_t)c * g.ho + hq) * g.wo + wnum];
+        } else if ((wnum % g.sw) == 0) {
+          const int wq = wnum / g.sw;
+          if (wq < g.wo) v = dyn[((int64_t)c * g.ho + hq) * g.wo + wq];
+        }
+      }
+      rb[kk] = v;
+      if (++kww == g.kw) { kww = 0; if (++khi == nkh) { khi = 0; ++c; } }
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int e = tid + 256 * q;
+      const int kk = e & 15;
+      const int cc = e >> 4;
+      const int k = k0 + kk;
+      float v = 0.f;
+      if (k < K && ci0 + cc < g.ci) {
+        const int c = k / KHW;
+        const int r = k - c * KHW;
+        const int khi = r / g.kw;
+        const int kww = r - khi * g.kw;
+        const int khh = kh_first + khi * g.sh;
+        v = w[(((int64_t)c * g.ci + ci0 + cc) * g.kh + khh) * g.kw + kww];
+      }
+      ra[q] = v;
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int kk = 0; kk < CBK; ++kk) Bs[buf][kk][tid] = rb[kk];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int e = tid + 256 * q;
+      As[buf][e & 15][e >> 4] = ra[q];
+    }
+  };
+
+  f32x16 acc0, acc1;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) { acc0[r] = 0.f; acc1[r] = 0.f; }
+  const int lr = lane & 31, lk = lane >> 5;
+  const int wn = wave * 64;
+  const int nk = (K + CBK - 1) / CBK;
+  if (nk > 0) {
+    load(0);
+    store(0);
+  }
+  __syncthreads();
+  for (int it = 0; it < nk; ++it) {
+    const int cur = it & 1;
+    if (it + 1 < nk) load((it + 1) * CBK);
+#pragma unroll
+    for (int kk = 0; kk < CBK; kk += 2) {
+      const float a = As[cur][kk + lk][lr];
+      const float b0 = Bs[cur][kk + lk][wn + lr];
+      const float b1 = Bs[cur][kk + lk][wn + 32 + lr];
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b0, acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b1, acc1, 0, 0, 0);
+    }
+    if (it + 1 < nk) store(cur ^ 1);
+    __syncthreads();
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int col = wi0 + wn + 32 * j + lr;
+    if (col >= g.wi) continue;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int c = ci0 + (r & 3) + 8 * (r >> 2) + 4 * lk;
+      if (c < g.ci) dx[(((int64_t)n * g.ci + c) * g.hi + hi) * g.wi + col] = j == 0 ? acc0[r] : acc1[r];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// wgrad partials. grid (ceil(Kc/128), N, ceil(Co/32)); block 256 (4 waves, each
+// 32 co x 32 k-columns).  Reduction over (ho, wo) of one sample in steps of 16
+// consecutive wo inside one output row.  partial[n][co][Kc].
+__global__ __launch_bounds__(256) void conv_wgrad_kernel(const float* __restrict__ dy,
+                                                         const float* __restrict__ x,
+                                                         float* __restrict__ partial,
+                                                         ConvDims g) {
+  __shared__ float As[2][CBK][32];
+  __shared__ float Bs[2][CBK][CBNW];
+  const int kc0 = blockIdx.x * CBNW;
+  const int n = blockIdx.y;
+  const int co0 = blockIdx.z * 32;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int Kc = g.ci * g.kh * g.kw;
+  const int KHW = g.kh * g.kw;
+  // this thread's B column and its (ci, kh, kw)
+  const int bcol = tid & (CBNW - 1);
+  const int bq = tid >> 7;     // 0..1 -> positions bq*8 .. bq*8+7
+  const int kcol = kc0 + bcol;
+  int ci = 0, khh = 0, kww = 0;
+  const bool kvalid = kcol < Kc;
+  if (kvalid) {
+    ci = kcol / KHW;
+    const int r = kcol - ci * KHW;
+    khh = r / g.kw;
+    kww = r - khh * g.kw;
+  }
+  const float* xn = x + ((int64_t)n * g.ci + ci) * g.hi * g.wi;
+  const float* dyn = dy + (int64_t)n * g.co * g.ho * g.wo;
+  const int wtiles = (g.wo + CBK - 1) / CBK;
+  const int nsteps = g.ho * wtiles;
+
+  float rb[8], ra[2];
+  auto load = [&](int step) {
+    const int ho = step / wtiles;
+    const int wo0 = (step - ho * wtiles) * CBK;
+    const int hi = ho * g.sh - g.ph + khh;
+    const bool hok = kvalid && hi >= 0 && hi < g.hi;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int pp = bq * 8 + i;
+      const int wo = wo0 + pp;
+      const int wi = wo * g.sw - g.pw + kww;
+      float v = 0.f;
+      if (hok && wo < g.wo && wi >= 0 && wi < g.wi) v = xn[(int64_t)hi * g.wi + wi];
+      rb[i] = v;
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int e = tid + 256 * q;     // 16 positions x 32 co, position fastest
+      const int pp = e & 15;
+      const int c = e >> 4;
+      const int wo = wo0 + pp;
+      ra[q] = (wo < g.wo && co0 + c < g.co) ? dyn[((int64_t)(co0 + c) * g.ho + ho) * g.wo + wo] : 0.f;
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) Bs[buf][bq * 8 + i][bcol] = rb[i];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int e = tid + 256 * q;
+      As[buf][e & 15][e >> 4] = ra[q];
+    }
+  };
+
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  const int lr = lane & 31, lk = lane >> 5;
+  const int wn = wave * 32;
+  load(0);
+  store(0);
+  __syncthreads();
+  for (int it = 0; it < nsteps; ++it) {
+    const int cur = it & 1;
+    if (it + 1 < nsteps) load(it + 1);
+#pragma unroll
+    for (int kk = 0; kk < CBK; kk += 2) {
+      const float a = As[cur][kk + lk][lr];
+      const float b = Bs[cur][kk + lk][wn + lr];
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
+    }
+    if (it + 1 < nsteps) store(cur ^ 1);
+    __syncthreads();
+  }
+  const int col = kc0 + wn + lr;
+  if (col < Kc) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int c = co0 + (r & 3) + 8 * (r >> 2) + 4 * lk;
+      if (c < g.co) partial[((int64_t)n * g.co + c) * Kc + col] = acc[r];
+    }
+  }
+}
+
+// dw[i] = sum_n partial[n][i]  (fixed order -> deterministic)
+__global__ void wgrad_reduce_kernel(const float* __restrict__ partial, int N, int64_t per,
+                                    float* __restrict__ dw) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < per;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int n = 0; n < N; ++n) s += partial[(int64_t)n * per + i];
+    dw[i] = s;
+  }
+}
+
+// dbias[co] = sum over (n, ho, wo) of dy; one block per channel.
+__global__ void bias_grad_kernel(const float* __restrict__ dy, int N, int C, int64_t plane,
+                                 float* __restrict__ db) {
+  const int c = blockIdx.x;
+  double acc = 0.0;
+  for (int n = 0; n < N; ++n) {
+    const float* p = dy + ((int64_t)n * C + c) * plane;
+    for (int64_t i = threadIdx.x; i < plane; i += blockDim.x) acc += p[i];
+  }
+  __shared__ double red[4];
+  acc = wave_sum_d(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) db[c] = static_cast<float>(red[0] + red[1] + red[2] + red[3]);
+}
+
+static inline bool make_dims(ConvDims& g, int n, int c_in, int h_in, int w_in, int c_out, int kh,
+                             int kw, int sh, int sw, int ph, int pw) {
+  if (n < 0 || c_in < 1 || h_in < 1 || w_in < 1 || c_out < 1 || kh < 1 || kw < 1 || sh < 1 ||
+      sw < 1 || ph < 0 || pw < 0)
+    return false;
+  g = ConvDims{n, c_in, h_in, w_in, c_out, kh, kw, sh, sw, ph, pw, 0, 0};
+  g.ho = (h_in + 2 * ph - kh) / sh + 1;
+  g.wo = (w_in + 2 * pw - kw) / sw + 1;
+  return g.ho >= 1 && g.wo >= 1;
+}
+
+}  // namespace ds2
+
+using namespace ds2;
+
+extern "C" {
+
+ds2_status_t ds2_conv2d_fwd(const float* x, const float* w, const float* bias, float* y, int n,
+                            int c_in, int h_in, int w_in, int c_out, int kh, int kw, int sh,
+                            int sw, int ph, int pw, const int* out_lens, ds2_stream_t stream) {
+  ConvDims g;
+  if (!make_dims(g, n, c_in, h_in, w_in, c_out, kh, kw, sh, sw, ph, pw)) return DS2_INVALID_VALUE;
+  if (n == 0) return DS2_OK;
+  if (g.ho > 65535) return DS2_UNSUPPORTED_SHAPE;
+  dim3 grid(cdiv(g.wo, CBN), g.ho, n * cdiv(c_out, 32));
+  hipLaunchKernelGGL(conv_fwd_kernel, grid, dim3(256), 0, as_stream(stream), x, w, bias, y, g,
+                     out_lens);
+  return launch_status("ds2_conv2d_fwd");
+}
+
+ds2_status_t ds2_conv2d_dgrad(const float* dy, const float* w, float* dx, int n, int c_in,
+                              int h_in, int w_in, int c_out, int kh, int kw, int sh, int sw,
+                              int ph, int pw, ds2_stream_t stream) {
+  ConvDims g;
+  if (!make_dims(g, n, c_in, h_in, w_in, c_out, kh, kw, sh, sw, ph, pw)) return DS2_INVALID_VALUE;
+  if (n == 0) return DS2_OK;
+  dim3 grid(cdiv(w_in, CBN), h_in, n * cdiv(c_in, 32));
+  hipLaunchKernelGGL(conv_dgrad_kernel, grid, dim3(256), 0, as_stream(stream), dy, w, dx, g);
+  return launch_status("ds2_conv2d_dgrad");
+}
+
+size_t ds2_conv2d_wgrad_workspace_size(int n, int c_in, int h_in, int w_in, int c_out, int kh,
+                                       int kw, int sh, int sw, int ph, int pw) {
+  (void)h_in; (void)w_in; (void)sh; (void)sw; (void)ph; (void)pw;
+  return (size_t)n * c_out * c_in * kh * kw * sizeof(float) + 256;
+}
+
+ds2_status_t ds2_conv2d_wgrad(const float* dy, const float* x, float* dw, float* dbias, int n,
+                              int c_in, int h_in, int w_in, int c_out, int kh, int kw, int sh,
+                              int sw, int ph, int pw, void* ws, size_t ws_bytes,
+                              ds2_stream_t stream) {
+  ConvDims g;
+  if (!make_dims(g, n, c_in, h_in, w_in, c_out, kh, kw, sh, sw, ph, pw)) return DS2_INVALID_VALUE;
+  if (n == 0) return DS2_OK;
+  if (ws == nullptr ||
+      ws_bytes < ds2_conv2d_wgrad_workspace_size(n, c_in, h_in, w_in, c_out, kh, kw, sh, sw, ph, pw))
+    return DS2_WORKSPACE_TOO_SMALL;
+  hipStream_t st = as_stream(stream);
+  const int Kc = c_in * kh * kw;
+  float* partial = static_cast<float*>(ws);
+  dim3 grid(cdiv(Kc, CBNW), n, cdiv(c_out, 32));
+  hipLaunchKernelGGL(conv_wgrad_kernel, grid, dim3(256), 0, st, dy, x, partial, g);
+  const int64_t per = (int64_t)c_out * Kc;
+  int rg = cdiv(per, 256);
+  if (rg > 2048) rg = 2048;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(rg), dim3(256), 0, st, partial, n, per, dw);
+  if (dbias != nullptr)
+    hipLaunchKernelGGL(bias_grad_kernel, dim3(c_out), dim3(256), 0, st, dy, n, c_out,
+                       (int64_t)g.ho * g.wo, dbias);
+  return launch_status("ds2_conv2d_wgrad");
+}
+
+}  // extern "C"

@@ -1,0 +1,238 @@
+// fp32 GEMM on CDNA4 matrix cores: v_mfma_f32_32x32x2_f32 (exact fp32 products,
+// fp32 accumulation — the same arithmetic class as the reference's cuBLAS SGEMM;
+// gfx950 has no xf32/TF32 shortcut).
+//
+// Tile 128x128x16 per 256-thread workgroup, 4 waves in a 2x2 grid, each wave a
+// 64x64 sub-tile = 2x2 MFMA tiles (64 accumulator VGPRs).  Both operands are
+// staged k-major in LDS ([k][m] / [k][n]) so a half-wave's MFMA fragment read is
+// 32 consecutive floats (conflict-free ds_read_b32).  Global->register loads of
+// tile k+1 are issued before the MFMAs of tile k (register double buffering).
+// Operands that are k-contiguous are transposed on the LDS write; the row pad
+// (+2 floats) makes those 8 ds_write_b32 per thread conflict-free.
+#include "common.h"
+
+namespace ds2 {
+
+constexpr int BM = 128, BN = 128, BK = 16;
+constexpr int LDS_PAD_T = 2;   // k-contiguous source -> transposed ds_write_b32
+constexpr int LDS_PAD_N = 4;   // m/n-contiguous source -> ds_write_b128 (16 B aligned rows)
+
+template <bool KCONTIG>
+struct OperandTile {
+  static constexpr int LD = (KCONTIG ? (BM + LDS_PAD_T) : (BM + LDS_PAD_N));
+};
+
+// Loads the BK x 128 slice of an operand into 8 registers per thread.
+//   KCONTIG: element (r, kk) at p[(r0 + r) * ld + k0 + kk]   (r = m or n)
+//  !KCONTIG: element (r, kk) at p[(k0 + kk) * ld + r0 + r]
+template <bool KCONTIG, bool VEC>
+__device__ __forceinline__ void load_tile(const float* __restrict__ p, int64_t ld, int rows,
+                                          int K, int r0, int k0, float (&v)[8]) {
+  const int t = threadIdx.x;
+  if (KCONTIG) {
+    const int r = t >> 1;
+    const int kb = (t & 1) * 8;
+    const int gr = r0 + r;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int gk = k0 + kb + 4 * q;
+      if (VEC) {
+        float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (gr < rows && gk < K) x = *reinterpret_cast<const float4*>(p + (int64_t)gr * ld + gk);
+        v[4 * q + 0] = x.x; v[4 * q + 1] = x.y; v[4 * q + 2] = x.z; v[4 * q + 3] = x.w;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          v[4 * q + e] = (gr < rows && gk + e < K) ? p[(int64_t)gr * ld + gk + e] : 0.f;
+      }
+    }
+  } else {
+    const int c4 = (t & 31) * 4;
+    const int gr = r0 + c4;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int kk = (t >> 5) + 8 * q;
+      const int gk = k0 + kk;
+      if (VEC) {
+        float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (gk < K && gr < rows) x = *reinterpret_cast<const float4*>(p + (int64_t)gk * ld + gr);
+        v[4 * q + 0] = x.x; v[4 * q + 1] = x.y; v[4 * q + 2] = x.z; v[4 * q + 3] = x.w;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          v[4 * q + e] = (gk < K && gr + e < rows) ? p[(int64_t)gk * ld + gr + e] : 0.f;
+      }
+    }
+  }
+}
+
+template <bool KCONTIG>
+__device__ __forceinline__ void store_tile(float* __restrict__ s, const float (&v)[8]) {
+  constexpr int LD = OperandTile<KCONTIG>::LD;
+  const int t = threadIdx.x;
+  if (KCONTIG) {
+    const int r = t >> 1;
+    const int kb = (t & 1) * 8;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s[(kb + e) * LD + r] = v[e];
+  } else {
+    const int c4 = (t & 31) * 4;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int kk = (t >> 5) + 8 * q;
+      *reinterpret_cast<float4*>(s + kk * LD + c4) =
+          make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+    }
+  }
+}
+
+template <int TA, int TB, bool VA, bool VB>
+__global__ __launch_bounds__(256) void sgemm_kernel(
+    int M, int N, int K, float alpha, const float* __restrict__ A, int64_t lda, int64_t sA,
+    const float* __restrict__ B, int64_t ldb, int64_t sB, float beta, float* __restrict__ C,
+    int64_t ldc, int64_t sC, const float* __restrict__ bias) {
+  // op(A) is k-contiguous when TA == 0 ([m][k] storage); op(B) is k-contiguous
+  // when TB == 1 ([n][k] storage).
+  constexpr bool AK = (TA == 0);
+  constexpr bool BKc = (TB == 1);
+  constexpr int LDA_S = OperandTile<AK>::LD;
+  constexpr int LDB_S = OperandTile<BKc>::LD;
+  __shared__ __attribute__((aligned(16))) float As[2][BK * LDA_S];
+  __shared__ __attribute__((aligned(16))) float Bs[2][BK * LDB_S];
+
+  const int bz = blockIdx.z;
+  A += bz * sA;
+  B += bz * sB;
+  C += bz * sC;
+  const int m0 = blockIdx.y * BM;
+  const int n0 = blockIdx.x * BN;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int wm = (wave >> 1) * 64;
+  const int wn = (wave & 1) * 64;
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  float ra[8], rb[8];
+  const int ktiles = (K + BK - 1) / BK;
+  load_tile<AK, VA>(A, lda, M, K, m0, 0, ra);
+  load_tile<BKc, VB>(B, ldb, N, K, n0, 0, rb);
+  store_tile<AK>(As[0], ra);
+  store_tile<BKc>(Bs[0], rb);
+  __syncthreads();
+
+  const int lr = lane & 31;
+  const int lk = lane >> 5;
+  for (int kt = 0; kt < ktiles; ++kt) {
+    const int cur = kt & 1;
+    const bool more = (kt + 1) < ktiles;
+    if (more) {
+      load_tile<AK, VA>(A, lda, M, K, m0, (kt + 1) * BK, ra);
+      load_tile<BKc, VB>(B, ldb, N, K, n0, (kt + 1) * BK, rb);
+    }
+    const float* as = As[cur];
+    const float* bs = Bs[cur];
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 2) {
+      float a0 = as[(kk + lk) * LDA_S + wm + lr];
+      float a1 = as[(kk + lk) * LDA_S + wm + 32 + lr];
+      float b0 = bs[(kk + lk) * LDB_S + wn + lr];
+      float b1 = bs[(kk + lk) * LDB_S + wn + 32 + lr];
+      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+    }
+    if (more) {
+      store_tile<AK>(As[cur ^ 1], ra);
+      store_tile<BKc>(Bs[cur ^ 1], rb);
+    }
+    __syncthreads();
+  }
+
+  // epilogue: C/D map of the 32x32 MFMA: col = lane & 31,
+  // row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int col = n0 + wn + 32 * j + lr;
+      if (col >= N) continue;
+      const float bv = bias != nullptr ? bias[col] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lk;
+        if (row < M) {
+          float* cp = C + (int64_t)row * ldc + col;
+          float v = alpha * acc[i][j][r] + bv;
+          if (beta != 0.f) v += beta * *cp;
+          *cp = v;
+        }
+      }
+    }
+  }
+}
+
+template <int TA, int TB>
+static void launch_sgemm_t(bool va, bool vb, dim3 grid, hipStream_t st, int M, int N, int K,
+                           float alpha, const float* A, int64_t lda, int64_t sA, const float* B,
+                           int64_t ldb, int64_t sB, float beta, float* C, int64_t ldc,
+                           int64_t sC, const float* bias) {
+#define DS2_L(VA, VB)                                                                      \
+  hipLaunchKernelGGL((sgemm_kernel<TA, TB, VA, VB>), grid, dim3(256), 0, st, M, N, K, alpha, A, \
+                     lda, sA, B, ldb, sB, beta, C, ldc, sC, bias)
+  if (va && vb) DS2_L(true, true);
+  else if (va) DS2_L(true, false);
+  else if (vb) DS2_L(false, true);
+  else DS2_L(false, false);
+#undef DS2_L
+}
+
+static inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+}  // namespace ds2
+
+using namespace ds2;
+
+extern "C" ds2_status_t ds2_sgemm(int trans_a, int trans_b, int m, int n, int k, float alpha,
+                                  const float* a, int64_t lda, int64_t stride_a, const float* b,
+                                  int64_t ldb, int64_t stride_b, float beta, float* c,
+                                  int64_t ldc, int64_t stride_c, int batch, const float* bias,
+                                  ds2_stream_t stream) {
+  if (m < 0 || n < 0 || k < 0 || batch < 0) return DS2_INVALID_VALUE;
+  if (m == 0 || n == 0 || batch == 0) return DS2_OK;
+  if (ldc < n) return DS2_INVALID_VALUE;
+  if (trans_a ? lda < m : lda < k) return DS2_INVALID_VALUE;
+  if (trans_b ? ldb < k : ldb < n) return DS2_INVALID_VALUE;
+  if (m > 65535 * BM) return DS2_UNSUPPORTED_SHAPE;
+  // vector (float4) staging is legal when every float4 is fully in or out of bounds
+  const bool va = aligned16(a) && (lda % 4 == 0) && (stride_a % 4 == 0) &&
+                  (trans_a ? (m % 4 == 0) : (k % 4 == 0));
+  const bool vb = aligned16(b) && (ldb % 4 == 0) && (stride_b % 4 == 0) &&
+                  (trans_b ? (k % 4 == 0) : (n % 4 == 0));
+  dim3 grid(cdiv(n, BN), cdiv(m, BM), batch);
+  hipStream_t st = as_stream(stream);
+  if (k == 0) {
+    // degenerate: C = beta*C + bias; run the kernel with zero k-tiles semantics
+    // via K=0 (loads are fully masked), which still applies the epilogue.
+  }
+  if (!trans_a && !trans_b)
+    launch_sgemm_t<0, 0>(va, vb, grid, st, m, n, k, alpha, a, lda, stride_a, b, ldb, stride_b,
+                         beta, c, ldc, stride_c, bias);
+  else if (!trans_a && trans_b)
+    launch_sgemm_t<0, 1>(va, vb, grid, st, m, n, k, alpha, a, lda, stride_a, b, ldb, stride_b,
+                         beta, c, ldc, stride_c, bias);
+  else if (trans_a && !trans_b)
+    launch_sgemm_t<1, 0>(va, vb, grid, st, m, n, k, alpha, a, lda, stride_a, b, ldb, stride_b,
+                         beta, c, ldc, stride_c, bias);
+  else
+    launch_sgemm_t<1, 1>(va, vb, grid, st, m, n, k, alpha, a, lda, stride_a, b, ldb, stride_b,
+                         beta, c, ldc, stride_c, bias);
+  return launch_status("ds2_sgemm");
+}

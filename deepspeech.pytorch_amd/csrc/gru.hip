@@ -1,0 +1,348 @@
+// Bidirectional GRU recurrence on MFMA (v_mfma_f32_16x16x4_f32), fp32.
+//
+// The input projection (x @ W_ih^T + b_ih, both directions) is a separate big
+// GEMM; this file only runs the sequential part.  One launch per time step
+// (kernel boundaries give the step-to-step ordering/visibility for free); both
+// directions advance in the same launch: direction 0 processes t = s, direction
+// 1 processes t = T-1-s, so a sample of length len starts its reverse pass at
+// t = len-1 from h = 0 exactly like pack_padded_sequence (model.py:103-105).
+//
+// Work split per launch: workgroup = (16 hidden units, direction, 16 samples).
+//   forward : gh[16 x 48] = h_prev[16 x H] @ W_hh[48 rows (r,z,n of the 16 units)]^T
+//   backward: rec[16 x 16] = dgh[16 x 3H] @ W_hh[:, 16 units]
+// The K dimension is split over the 4 waves, partial tiles reduced through LDS,
+// then one thread per (sample, unit) applies the gate math.  W_hh is repacked
+// once per call into MFMA-fragment order so every B-operand load of a wave is a
+// single coalesced 256-byte read.
+//
+// Gate math follows ATen's GRU cell (gate rows ordered r, z, n):
+//   r = sigmoid(hr + xr), z = sigmoid(hz + xz), n = tanh(xn + r*hn),
+//   h' = (h - n) * z + n
+#include "common.h"
+
+namespace ds2 {
+
+constexpr int GU = 16;      // hidden units per workgroup
+constexpr int GB = 16;      // samples per workgroup
+constexpr int GKC = 1024;   // K chunk staged in LDS
+constexpr int GPAD = GKC + 2;
+
+// Wp[d][ub][ks][g][64]: lane l of k-step ks, gate g ->
+//   W_hh_d[g*H + ub*16 + (l&15)][4*ks + (l>>4)]
+__global__ void pack_fwd_kernel(const float* __restrict__ w_f, const float* __restrict__ w_r,
+                                int H, int D, int UB, int KS, float* __restrict__ wp) {
+  const int64_t total = (int64_t)D * UB * KS * 3 * 64;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t r = i;
+    const int l = r % 64; r /= 64;
+    const int g = r % 3; r /= 3;
+    const int ks = r % KS; r /= KS;
+    const int ub = r % UB; r /= UB;
+    const int d = static_cast<int>(r);
+    const float* w = d == 0 ? w_f : w_r;
+    const int u = ub * GU + (l & 15);
+    const int k = 4 * ks + (l >> 4);
+    wp[i] = (u < H && k < H) ? w[(int64_t)(g * H + u) * H + k] : 0.f;
+  }
+}
+
+// WpT[d][ub][ks][64]: lane l of k-step ks -> W_hh_d[4*ks + (l>>4)][ub*16 + (l&15)]
+__global__ void pack_bwd_kernel(const float* __restrict__ w_f, const float* __restrict__ w_r,
+                                int H, int D, int UB, int KS, float* __restrict__ wp) {
+  const int64_t total = (int64_t)D * UB * KS * 64;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t r = i;
+    const int l = r % 64; r /= 64;
+    const int ks = r % KS; r /= KS;
+    const int ub = r % UB; r /= UB;
+    const int d = static_cast<int>(r);
+    const float* w = d == 0 ? w_f : w_r;
+    const int u = ub * GU + (l & 15);
+    const int k = 4 * ks + (l >> 4);
+    wp[i] = (u < H && k < 3 * H) ? w[(int64_t)k * H + u] : 0.f;
+  }
+}
+
+// Stage rows [n0, n0+16) x cols [kc0, kc1) of a row-major matrix (row stride
+// ld, valid rows < N) into hs[m][GPAD], zero-filled.  8-byte accesses.
+__device__ __forceinline__ void stage_rows(const float* __restrict__ src, int64_t ld, int N,
+                                           int n0, int kc0, int kc1, float* __restrict__ hs) {
+  const int width = kc1 - kc0;           // even (H, 3H chunks are multiples of 2 here)
+  const int pairs = (width + 1) >> 1;
+  for (int i = threadIdx.x; i < GB * pairs; i += blockDim.x) {
+    const int m = i / pairs;
+    const int kp = (i - m * pairs) * 2;
+    const int n = n0 + m;
+    float2 v = make_float2(0.f, 0.f);
+    if (n < N) {
+      const float* p = src + (int64_t)n * ld + kc0 + kp;
+      v.x = p[0];
+      v.y = (kp + 1 < width) ? p[1] : 0.f;
+    }
+    *reinterpret_cast<float2*>(hs + m * GPAD + kp) = v;
+  }
+}
+
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void gru_fwd_step_kernel(
+    int s, int T, int N, int H, int D, const float* __restrict__ xproj,
+    const float* __restrict__ wp, const float* __restrict__ b_f, const float* __restrict__ b_r,
+    const int* __restrict__ lens, float* __restrict__ h_all, float* __restrict__ gates) {
+  __shared__ __attribute__((aligned(16))) float hs[GB * GPAD];
+  __shared__ float red[4][GB][3 * GU + 1];
+  const int ub = blockIdx.x;
+  const int d = blockIdx.y;
+  const int n0 = blockIdx.z * GB;
+  const int UB = gridDim.x;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int t = d == 0 ? s : T - 1 - s;
+  const int tp = d == 0 ? t - 1 : t + 1;
+  const int KS = (H + 3) / 4;
+
+  f32x4 acc[3];
+#pragma unroll
+  for (int g = 0; g < 3; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (s > 0) {
+    const float* hprev = h_all + ((int64_t)tp * N * D + d) * H;   // row n at + n*D*H
+    const float* wpd = wp + ((int64_t)d * UB + ub) * KS * 3 * 64;
+    for (int kc0 = 0; kc0 < H; kc0 += GKC) {
+      const int kc1 = min(H, kc0 + GKC);
+      __syncthreads();
+      stage_rows(hprev, (int64_t)D * H, N, n0, kc0, kc1, hs);
+      __syncthreads();
+      const int ks0 = kc0 / 4;
+      const int ks1 = (kc1 + 3) / 4;
+      const int per = (ks1 - ks0 + 3) / 4;
+      const int a_ks = ks0 + wave * per;
+      const int b_ks = min(ks1, a_ks + per);
+      const float* hrow = hs + (lane & 15) * GPAD + (lane >> 4) - kc0;
+      for (int ks = a_ks; ks < b_ks; ++ks) {
+        const int k = 4 * ks;
+        const float a = (k + (lane >> 4) < kc1) ? hrow[k] : 0.f;
+        const float* bp = wpd + (int64_t)ks * 3 * 64 + lane;
+        acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bp[0], acc[0], 0, 0, 0);
+        acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bp[64], acc[1], 0, 0, 0);
+        acc[2] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bp[128], acc[2], 0, 0, 0);
+      }
+    }
+  }
+  // C/D map (16x16): col = lane & 15, row = (lane >> 4) * 4 + r
+#pragma unroll
+  for (int g = 0; g < 3; ++g)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[wave][(lane >> 4) * 4 + r][g * GU + (lane & 15)] = acc[g][r];
+  __syncthreads();
+
+  const int m = threadIdx.x >> 4;       // sample within the tile
+  const int u = threadIdx.x & 15;       // unit within the block
+  const int n = n0 + m;
+  const int j = ub * GU + u;
+  if (n >= N || j >= H) return;
+  const float* bh = d == 0 ? b_f : b_r;
+  float ghr = red[0][m][u] + red[1][m][u] + red[2][m][u] + red[3][m][u] + bh[j];
+  float ghz = red[0][m][GU + u] + red[1][m][GU + u] + red[2][m][GU + u] + red[3][m][GU + u] +
+              bh[H + j];
+  float ghn = red[0][m][2 * GU + u] + red[1][m][2 * GU + u] + red[2][m][2 * GU + u] +
+              red[3][m][2 * GU + u] + bh[2 * H + j];
+  const int64_t row = ((int64_t)t * N + n) * D + d;
+  const bool active = t < lens[n];
+  float hout = 0.f, r = 0.f, z = 0.f, nn = 0.f;
+  if (active) {
+    const float* xp = xproj + row * 3 * H;
+    const float hp = s > 0 ? h_all[(((int64_t)tp * N + n) * D + d) * H + j] : 0.f;
+    r = sigmoidf_(ghr + xp[j]);
+    z = sigmoidf_(ghz + xp[H + j]);
+    nn = tanhf(xp[2 * H + j] + r * ghn);
+    hout = (hp - nn) * z + nn;
+  } else {
+    ghn = 0.f;
+  }
+  h_all[row * H + j] = hout;
+  if (gates != nullptr) {
+    float* gp = gates + row * 4 * H;
+    gp[j] = r;
+    gp[H + j] = z;
+    gp[2 * H + j] = nn;
+    gp[3 * H + j] = ghn;
+  }
+}
+
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void gru_bwd_step_kernel(
+    int s, int T, int N, int H, int D, const float* __restrict__ dy, int dyd,
+    const float* __restrict__ wpt, const float* __restrict__ h_all,
+    const float* __restrict__ gates, const int* __restrict__ lens, float* __restrict__ dgx,
+    float* __restrict__ dgh, float* __restrict__ dhs) {
+  __shared__ __attribute__((aligned(16))) float hs[GB * GPAD];
+  __shared__ float red[4][GB][GU + 1];
+  const int ub = blockIdx.x;
+  const int d = blockIdx.y;
+  const int n0 = blockIdx.z * GB;
+  const int UB = gridDim.x;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int t = d == 0 ? T - 1 - s : s;      // time processed now
+  const int tq = d == 0 ? t + 1 : t - 1;     // time processed at step s-1
+  const int H3 = 3 * H;
+  const int KS = (H3 + 3) / 4;
+
+  f32x4 acc0 = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 acc1 = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (s > 0) {
+    const float* dghq = dgh + ((int64_t)tq * N * D + d) * H3;
+    const float* wpd = wpt + ((int64_t)d * UB + ub) * KS * 64;
+    for (int kc0 = 0; kc0 < H3; kc0 += GKC) {
+      const int kc1 = min(H3, kc0 + GKC);
+      __syncthreads();
+      stage_rows(dghq, (int64_t)D * H3, N, n0, kc0, kc1, hs);
+      __syncthreads();
+      const int ks0 = kc0 / 4;
+      const int ks1 = (kc1 + 3) / 4;
+      const int per = (ks1 - ks0 + 3) / 4;
+      const int a_ks = ks0 + wave * per;
+      const int b_ks = min(ks1, a_ks + per);
+      const float* hrow = hs + (lane & 15) * GPAD + (lane >> 4) - kc0;
+      int ks = a_ks;
+      for (; ks + 1 < b_ks; ks += 2) {
+        const int k = 4 * ks;
+        const float a0 = (k + (lane >> 4) < kc1) ? hrow[k] : 0.f;
+        const float a1 = (k + 4 + (lane >> 4) < kc1) ? hrow[k + 4] : 0.f;
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, wpd[(int64_t)ks * 64 + lane], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, wpd[(int64_t)(ks + 1) * 64 + lane], acc1, 0,
+                                                   0, 0);
+      }
+      if (ks < b_ks) {
+        const int k = 4 * ks;
+        const float a0 = (k + (lane >> 4) < kc1) ? hrow[k] : 0.f;
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, wpd[(int64_t)ks * 64 + lane], acc0, 0, 0, 0);
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) red[wave][(lane >> 4) * 4 + r][lane & 15] = acc0[r] + acc1[r];
+  __syncthreads();
+
+  const int m = threadIdx.x >> 4;
+  const int u = threadIdx.x & 15;
+  const int n = n0 + m;
+  const int j = ub * GU + u;
+  if (n >= N || j >= H) return;
+  const int len = lens[n];
+  const int64_t row = ((int64_t)t * N + n) * D + d;
+  float* dhcur = dhs + ((int64_t)(s & 1) * N * D + (int64_t)n * D + d) * H;
+  const float* dhprv = dhs + ((int64_t)((s + 1) & 1) * N * D + (int64_t)n * D + d) * H;
+  float dh = 0.f;
+  if (t < len) {
+    float carry = 0.f;
+    if (s > 0) {
+      const float zq = gates[(((int64_t)tq * N + n) * D + d) * 4 * H + H + j];
+      carry = dhprv[j] * zq + (red[0][m][u] + red[1][m][u] + red[2][m][u] + red[3][m][u]);
+    }
+    dh = dy[(((int64_t)t * N + n) * dyd + (dyd > 1 ? d : 0)) * H + j] + carry;
+  }
+  float dar = 0.f, daz = 0.f, dan = 0.f, dghn = 0.f;
+  if (t < len) {
+    const float* gp = gates + row * 4 * H;
+    const float r = gp[j], z = gp[H + j], nn = gp[2 * H + j], ghn = gp[3 * H + j];
+    float hp = 0.f;
+    const int tp = d == 0 ? t - 1 : t + 1;
+    if (tp >= 0 && tp < T) hp = h_all[(((int64_t)tp * N + n) * D + d) * H + j];
+    dan = dh * (1.f - z) * (1.f - nn * nn);
+    daz = dh * (hp - nn) * z * (1.f - z);
+    dar = dan * ghn * r * (1.f - r);
+    dghn = dan * r;
+  }
+  float* gx = dgx + row * H3;
+  float* gh = dgh + row * H3;
+  gx[j] = dar;
+  gx[H + j] = daz;
+  gx[2 * H + j] = dan;
+  gh[j] = dar;
+  gh[H + j] = daz;
+  gh[2 * H + j] = dghn;
+  dhcur[j] = dh;
+}
+
+static inline int grid_cap(int64_t work) {
+  int64_t g = (work + 255) / 256;
+  return static_cast<int>(g > 2048 ? 2048 : (g < 1 ? 1 : g));
+}
+
+}  // namespace ds2
+
+using namespace ds2;
+
+extern "C" {
+
+size_t ds2_gru_fwd_workspace_size(int n, int h, int num_dirs) {
+  (void)n;
+  const int64_t UB = (h + GU - 1) / GU;
+  const int64_t KS = (h + 3) / 4;
+  return (size_t)(num_dirs * UB * KS * 3 * 64) * sizeof(float) + 256;
+}
+
+ds2_status_t ds2_gru_fwd(int t_max, int n, int h, int num_dirs, const float* xproj,
+                         const float* w_hh_f, const float* w_hh_r, const float* b_hh_f,
+                         const float* b_hh_r, const int* lens, float* h_all, float* gates,
+                         void* ws, size_t ws_bytes, ds2_stream_t stream) {
+  if (t_max < 0 || n < 0 || h < 1 || (num_dirs != 1 && num_dirs != 2)) return DS2_INVALID_VALUE;
+  if (t_max == 0 || n == 0) return DS2_OK;
+  if (ws == nullptr || ws_bytes < ds2_gru_fwd_workspace_size(n, h, num_dirs))
+    return DS2_WORKSPACE_TOO_SMALL;
+  if (num_dirs == 1) {
+    w_hh_r = w_hh_f;
+    b_hh_r = b_hh_f;
+  }
+  hipStream_t st = as_stream(stream);
+  const int UB = (h + GU - 1) / GU;
+  const int KS = (h + 3) / 4;
+  float* wp = static_cast<float*>(ws);
+  hipLaunchKernelGGL(pack_fwd_kernel, dim3(grid_cap((int64_t)num_dirs * UB * KS * 192)),
+                     dim3(256), 0, st, w_hh_f, w_hh_r, h, num_dirs, UB, KS, wp);
+  dim3 grid(UB, num_dirs, (n + GB - 1) / GB);
+  for (int s = 0; s < t_max; ++s) {
+    hipLaunchKernelGGL(gru_fwd_step_kernel, grid, dim3(256), 0, st, s, t_max, n, h, num_dirs,
+                       xproj, wp, b_hh_f, b_hh_r, lens, h_all, gates);
+  }
+  return launch_status("ds2_gru_fwd");
+}
+
+size_t ds2_gru_bwd_workspace_size(int n, int h, int num_dirs) {
+  const int64_t UB = (h + GU - 1) / GU;
+  const int64_t KS = (3 * h + 3) / 4;
+  return (size_t)(num_dirs * UB * KS * 64) * sizeof(float) +
+         (size_t)2 * n * num_dirs * h * sizeof(float) + 512;
+}
+
+ds2_status_t ds2_gru_bwd(int t_max, int n, int h, int num_dirs, const float* dy, int dy_dirs,
+                         const float* w_hh_f, const float* w_hh_r, const float* h_all,
+                         const float* gates, const int* lens, float* dgates_x, float* dgates_h,
+                         void* ws, size_t ws_bytes, ds2_stream_t stream) {
+  if (t_max < 0 || n < 0 || h < 1 || (num_dirs != 1 && num_dirs != 2)) return DS2_INVALID_VALUE;
+  if (t_max == 0 || n == 0) return DS2_OK;
+  if (gates == nullptr) return DS2_INVALID_VALUE;
+  if (dy_dirs != 1 && dy_dirs != num_dirs) return DS2_INVALID_VALUE;
+  if (ws == nullptr || ws_bytes < ds2_gru_bwd_workspace_size(n, h, num_dirs))
+    return DS2_WORKSPACE_TOO_SMALL;
+  if (num_dirs == 1) w_hh_r = w_hh_f;
+  hipStream_t st = as_stream(stream);
+  const int UB = (h + GU - 1) / GU;
+  const int KS = (3 * h + 3) / 4;
+  float* wpt = static_cast<float*>(ws);
+  size_t off = ((size_t)num_dirs * UB * KS * 64 * sizeof(float) + 255) & ~(size_t)255;
+  float* dhs = reinterpret_cast<float*>(static_cast<char*>(ws) + off);
+  hipLaunchKernelGGL(pack_bwd_kernel, dim3(grid_cap((int64_t)num_dirs * UB * KS * 64)),
+                     dim3(256), 0, st, w_hh_f, w_hh_r, h, num_dirs, UB, KS, wpt);
+  dim3 grid(UB, num_dirs, (n + GB - 1) / GB);
+  for (int s = 0; s < t_max; ++s) {
+    hipLaunchKernelGGL(gru_bwd_step_kernel, grid, dim3(256), 0, st, s, t_max, n, h, num_dirs, dy,
+                       dy_dirs, wpt, h_all, gates, lens, dgates_x, dgates_h, dhs);
+  }
+  return launch_status("ds2_gru_bwd");
+}
+
+}  // extern "C"

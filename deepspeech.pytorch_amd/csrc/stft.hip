@@ -1,0 +1,194 @@
+// Spectrogram front-end: SpectrogramParser.audio_to_stft + normalize_audio.
+// ref data/data_loader.py:201-220,245-284 (legacy, cited by north_star) and
+// data/data_loader_aug.py:220-249,274-313 (the one train.py imports).
+//
+// librosa.stft semantics restated (librosa < 0.10, implied by the positional API
+// used in data/audio_aug.py:20,74): center=True with reflect padding of n_fft/2,
+// frames of n_fft every hop, window = the caller's n_fft taps (scipy hamming,
+// symmetric), real FFT evaluated in float64, stored complex64, |.| in float32.
+// The DFT is evaluated directly in fp64 (161 bins x 320 taps per frame,
+// twiddles from an LDS table indexed by (k*m) mod n_fft): ~13 GFLOP of fp64 for
+// a 32 x 10 s batch, far below the fp64 roof, and bit-for-bit free of the
+// float32 round-off a fp32 DFT would add to near-silent bins after the x2^20
+// gain of 'max_frame'.
+#include "common.h"
+
+namespace ds2 {
+
+constexpr int SF = 8;          // frames per workgroup
+constexpr int SMAXN = 1024;    // max n_fft
+
+__device__ __forceinline__ int reflect_idx(int i, int n) {
+  // numpy 'reflect' (edge sample not repeated); assumes n > 1
+  const int period = 2 * (n - 1);
+  i = i % period;
+  if (i < 0) i += period;
+  return i < n ? i : period - i;
+}
+
+__device__ __forceinline__ int scipy_reflect(int i, int n) {
+  // scipy.ndimage mode='reflect' (half-sample symmetric): d c b a | a b c d
+  const int period = 2 * n;
+  i = i % period;
+  if (i < 0) i += period;
+  return i < n ? i : period - 1 - i;
+}
+
+// grid (ceil(max_frames / SF), batch); block 256 (thread = frequency bin)
+__global__ __launch_bounds__(256) void stft_kernel(const float* __restrict__ pcm,
+                                                   const int* __restrict__ n_samples,
+                                                   int max_samples, int n_fft, int hop,
+                                                   const double* __restrict__ window,
+                                                   int normalize, float* __restrict__ out,
+                                                   int max_frames, float* __restrict__ frame_mean) {
+  __shared__ double cs[SMAXN], sn[SMAXN];
+  __shared__ double fr[SF][SMAXN];
+  __shared__ double red[SF][4];
+  const int b = blockIdx.y;
+  const int t0 = blockIdx.x * SF;
+  const int nb = n_samples[b];
+  const int T = 1 + nb / hop;
+  const int F = n_fft / 2 + 1;
+  const int pad = n_fft / 2;
+  const float* y = pcm + (int64_t)b * max_samples;
+  for (int m = threadIdx.x; m < n_fft; m += blockDim.x) {
+    double s, c;
+    sincospi(2.0 * m / n_fft, &s, &c);
+    cs[m] = c;
+    sn[m] = s;
+  }
+  for (int i = threadIdx.x; i < SF * n_fft; i += blockDim.x) {
+    const int f = i / n_fft;
+    const int m = i - f * n_fft;
+    const int t = t0 + f;
+    double v = 0.0;
+    if (t < T) v = window[m] * (double)y[reflect_idx(t * hop + m - pad, nb)];
+    fr[f][m] = v;
+  }
+  __syncthreads();
+  const int k = threadIdx.x;
+  double lsum[SF];
+#pragma unroll
+  for (int f = 0; f < SF; ++f) lsum[f] = 0.0;
+  if (k < F) {
+    double re[SF], im[SF];
+#pragma unroll
+    for (int f = 0; f < SF; ++f) { re[f] = 0.0; im[f] = 0.0; }
+    int idx = 0;   // (k * m) mod n_fft
+    for (int m = 0; m < n_fft; ++m) {
+      const double c = cs[idx], s = sn[idx];
+#pragma unroll
+      for (int f = 0; f < SF; ++f) {
+        const double v = fr[f][m];
+        re[f] = fma(v, c, re[f]);
+        im[f] = fma(-v, s, im[f]);
+      }
+      idx += k;
+      if (idx >= n_fft) idx -= n_fft;
+    }
+#pragma unroll
+    for (int f = 0; f < SF; ++f) {
+      const int t = t0 + f;
+      if (t >= max_frames) continue;
+      float val = 0.f;
+      if (t < T) {
+        const float mag = hypotf(static_cast<float>(re[f]), static_cast<float>(im[f]));
+        val = normalize ? log1pf(mag * 1048576.0f) : log1pf(mag);
+        lsum[f] = val;
+      }
+      out[((int64_t)b * F + k) * max_frames + t] = val;
+    }
+  }
+  // mean over the F bins of every frame (torch spect.mean(dim=0))
+#pragma unroll
+  for (int f = 0; f < SF; ++f) {
+    double v = wave_sum_d(lsum[f]);
+    if ((threadIdx.x & 63) == 0) red[f][threadIdx.x >> 6] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < SF) {
+    const int f = threadIdx.x;
+    const int t = t0 + f;
+    if (t < T && t < max_frames) {
+      const double s = red[f][0] + red[f][1] + red[f][2] + red[f][3];
+      frame_mean[(int64_t)b * max_frames + t] = static_cast<float>(s / F);
+    }
+  }
+}
+
+// One block per utterance: max_mean = mean_t(gaussian_filter1d(frame_mean, sigma)).
+__global__ void maxframe_offset_kernel(const int* __restrict__ n_samples, int hop,
+                                       int max_frames, const float* __restrict__ frame_mean,
+                                       const float* __restrict__ taps, int radius,
+                                       float* __restrict__ offset) {
+  const int b = blockIdx.x;
+  int T = 1 + n_samples[b] / hop;
+  if (T > max_frames) T = max_frames;
+  const float* m = frame_mean + (int64_t)b * max_frames;
+  double acc = 0.0;
+  for (int t = threadIdx.x; t < T; t += blockDim.x) {
+    double s = 0.0;
+    for (int j = -radius; j <= radius; ++j) s += (double)taps[j + radius] * m[scipy_reflect(t + j, T)];
+    acc += (double)static_cast<float>(s);   // scipy writes the float32 filtered signal
+  }
+  __shared__ double red[4];
+  acc = wave_sum_d(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) offset[b] = static_cast<float>((red[0] + red[1] + red[2] + red[3]) / T);
+}
+
+__global__ void subtract_offset_kernel(const int* __restrict__ n_samples, int hop, int F,
+                                       int max_frames, const float* __restrict__ offset,
+                                       float* __restrict__ out) {
+  const int b = blockIdx.y;
+  int T = 1 + n_samples[b] / hop;
+  if (T > max_frames) T = max_frames;
+  const float o = offset[b];
+  const int64_t total = (int64_t)F * max_frames;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int t = static_cast<int>(i % max_frames);
+    if (t < T) out[(int64_t)b * total + i] -= o;
+  }
+}
+
+}  // namespace ds2
+
+using namespace ds2;
+
+extern "C" {
+
+size_t ds2_stft_workspace_size(int batch, int max_frames) {
+  return (size_t)batch * max_frames * sizeof(float) + (size_t)batch * sizeof(float) + 512;
+}
+
+ds2_status_t ds2_stft_logmag(const float* pcm, const int* n_samples, int batch, int max_samples,
+                             int n_fft, int hop, const double* window, int normalize,
+                             const float* gauss_taps, int gauss_radius, float* out,
+                             int max_frames, void* ws, size_t ws_bytes, ds2_stream_t stream) {
+  if (batch < 0 || n_fft < 2 || n_fft > SMAXN || hop < 1 || max_frames < 1) return DS2_INVALID_VALUE;
+  if (n_fft / 2 + 1 > 256) return DS2_UNSUPPORTED_SHAPE;
+  if (normalize == 1 && (gauss_taps == nullptr || gauss_radius < 0)) return DS2_INVALID_VALUE;
+  if (batch == 0) return DS2_OK;
+  if (ws == nullptr || ws_bytes < ds2_stft_workspace_size(batch, max_frames))
+    return DS2_WORKSPACE_TOO_SMALL;
+  hipStream_t st = as_stream(stream);
+  float* frame_mean = static_cast<float*>(ws);
+  float* offset = frame_mean + (size_t)batch * max_frames;
+  const int F = n_fft / 2 + 1;
+  hipLaunchKernelGGL(stft_kernel, dim3(cdiv(max_frames, SF), batch), dim3(256), 0, st, pcm,
+                     n_samples, max_samples, n_fft, hop, window, normalize, out, max_frames,
+                     frame_mean);
+  if (normalize == 1) {
+    hipLaunchKernelGGL(maxframe_offset_kernel, dim3(batch), dim3(256), 0, st, n_samples, hop,
+                       max_frames, frame_mean, gauss_taps, gauss_radius, offset);
+    int g = cdiv((int64_t)F * max_frames, 256);
+    if (g > 512) g = 512;
+    hipLaunchKernelGGL(subtract_offset_kernel, dim3(g, batch), dim3(256), 0, st, n_samples, hop, F,
+                       max_frames, offset, out);
+  }
+  return launch_status("ds2_stft_logmag");
+}
+
+}  // extern "C"

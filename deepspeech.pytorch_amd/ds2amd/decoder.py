@@ -1,0 +1,162 @@
+"""Decoders — drop-in for the reference ``decoder.py``.
+
+``GreedyDecoder.decode`` runs argmax + CTC collapse in one HIP kernel
+(ds2_greedy_decode) and copies back only the compacted label ids/offsets, instead
+of the reference's per-frame ``.item()`` loop (ref decoder.py:165-197).  The
+string semantics are the reference's: first maximum wins, blanks dropped, a
+frame equal to the previous *frame* is dropped, the space label maps to ' ' and
+'2' is emitted literally.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import ops
+
+
+def _levenshtein(a, b) -> int:
+    """Edit distance (python-Levenshtein's Lev.distance semantics)."""
+    if len(a) < len(b):
+        a, b = b, a
+    prev = list(range(len(b) + 1))
+    for i, ca in enumerate(a, 1):
+        cur = [i]
+        for j, cb in enumerate(b, 1):
+            cur.append(min(prev[j] + 1, cur[j - 1] + 1, prev[j - 1] + (ca != cb)))
+        prev = cur
+    return prev[-1]
+
+
+class Decoder(object):
+    """Base decoder (ref decoder.py:23-87)."""
+
+    def __init__(self, labels, blank_index=0):
+        self.labels = labels
+        self.int_to_char = dict([(i, c) for (i, c) in enumerate(labels)])
+        self.blank_index = blank_index
+        space_index = len(labels)
+        if ' ' in labels:
+            space_index = labels.index(' ')
+        self.space_index = space_index
+
+    def wer(self, s1, s2):
+        b = set(s1.split() + s2.split())
+        word2char = dict(zip(b, range(len(b))))
+        w1 = [chr(word2char[w]) for w in s1.split()]
+        w2 = [chr(word2char[w]) for w in s2.split()]
+        return _levenshtein(''.join(w1), ''.join(w2))
+
+    def cer(self, s1, s2):
+        s1, s2, = s1.replace(' ', ''), s2.replace(' ', '')
+        return _levenshtein(s1, s2)
+
+    def decode(self, probs, sizes=None):
+        raise NotImplementedError
+
+
+class BeamCTCDecoder(Decoder):
+    """Wraps ctcdecode.CTCBeamDecoder exactly like ref decoder.py:90-143 (external, unpinned)."""
+
+    def __init__(self, labels, lm_path=None, alpha=0, beta=0, cutoff_top_n=40, cutoff_prob=1.0,
+                 beam_width=100, num_processes=4, blank_index=0):
+        super().__init__(labels)
+        try:
+            from ctcdecode import CTCBeamDecoder
+        except ImportError:
+            raise ImportError("BeamCTCDecoder requires paddledecoder package.")
+        self._decoder = CTCBeamDecoder(labels, lm_path, alpha, beta, cutoff_top_n, cutoff_prob,
+                                       beam_width, num_processes, blank_index)
+
+    def convert_to_strings(self, out, seq_len):
+        results = []
+        for b, batch in enumerate(out):
+            utterances = []
+            for p, utt in enumerate(batch):
+                size = seq_len[b][p]
+                if size > 0:
+                    transcript = ''.join(map(lambda x: self.int_to_char[x.item()], utt[0:size]))
+                else:
+                    transcript = ''
+                utterances.append(transcript)
+            results.append(utterances)
+        return results
+
+    def convert_tensor(self, offsets, sizes):
+        results = []
+        for b, batch in enumerate(offsets):
+            utterances = []
+            for p, utt in enumerate(batch):
+                size = sizes[b][p]
+                if sizes[b][p] > 0:
+                    utterances.append(utt[0:size])
+                else:
+                    utterances.append(torch.tensor([], dtype=torch.int))
+            results.append(utterances)
+        return results
+
+    def decode(self, probs, sizes=None):
+        probs = probs.cpu()
+        out, scores, offsets, seq_lens = self._decoder.decode(probs, sizes)
+        strings = self.convert_to_strings(out, seq_lens)
+        offsets = self.convert_tensor(offsets, seq_lens)
+        return strings, offsets
+
+
+class GreedyDecoder(Decoder):
+    def __init__(self, labels, blank_index=0):
+        super().__init__(labels, blank_index)
+
+    def convert_to_strings(self, sequences, sizes=None, remove_repetitions=False,
+                           return_offsets=False):
+        """Host conversion of id sequences (targets) to strings (ref decoder.py:150-163)."""
+        strings = []
+        offsets = [] if return_offsets else None
+        for x in range(len(sequences)):
+            seq_len = sizes[x] if sizes is not None else len(sequences[x])
+            string, string_offsets = self.process_string(sequences[x], seq_len, remove_repetitions)
+            strings.append([string])
+            if return_offsets:
+                offsets.append([string_offsets])
+        if return_offsets:
+            return strings, offsets
+        return strings
+
+    def process_string(self, sequence, size, remove_repetitions=False):
+        seq = [int(v) for v in (sequence.tolist() if torch.is_tensor(sequence) else sequence)]
+        size = int(size)
+        string = ''
+        offsets = []
+        blank = self.int_to_char[self.blank_index]
+        for i in range(size):
+            char = self.int_to_char[seq[i]]
+            if char != blank:
+                if remove_repetitions and i != 0 and char == self.int_to_char[seq[i - 1]]:
+                    pass
+                elif char == self.labels[self.space_index] if self.space_index < len(self.labels) else False:
+                    string += ' '
+                    offsets.append(i)
+                else:
+                    string = string + char
+                    offsets.append(i)
+        return string, torch.tensor(offsets, dtype=torch.int)
+
+    def decode_ids(self, probs, sizes=None):
+        """Device-side greedy decode; returns (ids, offsets, counts) int32 device tensors."""
+        ids, offs, counts, _ = ops.greedy_decode_raw(probs, sizes, blank=self.blank_index)
+        return ids, offs, counts
+
+    def decode(self, probs, sizes=None):
+        """Returns (strings, offsets) like ref decoder.py:182-197."""
+        if not probs.is_cuda:
+            raise RuntimeError("ds2amd GreedyDecoder.decode runs on the GPU (HIP kernel)")
+        ids, offs, counts = self.decode_ids(probs, sizes)
+        ids, offs, counts = ids.cpu(), offs.cpu(), counts.cpu()
+        strings, offsets = [], []
+        for b in range(ids.shape[0]):
+            k = int(counts[b])
+            row = ids[b, :k].tolist()
+            s = ''.join(' ' if (self.space_index < len(self.labels) and c == self.space_index)
+                        else self.int_to_char[c] for c in row)
+            strings.append([s])
+            offsets.append([offs[b, :k].to(torch.int).clone()])
+        return strings, offsets

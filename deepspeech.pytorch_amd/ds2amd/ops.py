@@ -1,0 +1,435 @@
+"""Device ops over the libds2hip C ABI, plus their autograd wrappers.
+
+Every function here hands raw device pointers to a HIP kernel through
+``_lib.call``; torch supplies only memory (caching allocator), the current HIP
+stream and autograd bookkeeping.  Inputs must be CUDA (HIP) float32/int32
+tensors; there is no CPU path (the CPU restatement lives in ``oracle/`` and is
+used only by the tests and the bench's cpu_baseline leg).
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+
+from . import _lib
+
+_F32 = torch.float32
+_I32 = torch.int32
+
+
+# ----------------------------------------------------------------------------
+# plumbing
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _p(t: Optional[torch.Tensor]) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+def _need(t: torch.Tensor, name: str, dtype=_F32) -> torch.Tensor:
+    if not t.is_cuda:
+        raise _lib.Ds2Error(f"{name}: expected a device tensor (got {t.device}); "
+                            "the ds2amd product path runs only on the GPU")
+    if t.dtype != dtype:
+        raise _lib.Ds2Error(f"{name}: expected {dtype}, got {t.dtype}")
+    return t.contiguous()
+
+
+def _ws(nbytes: int, device) -> torch.Tensor:
+    return torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=device)
+
+
+# ----------------------------------------------------------------------------
+# raw ops
+def sgemm(a: torch.Tensor, b: torch.Tensor, c: torch.Tensor, *, m: int, n: int, k: int,
+          trans_a: bool = False, trans_b: bool = False, lda: int, ldb: int, ldc: int,
+          alpha: float = 1.0, beta: float = 0.0, bias: Optional[torch.Tensor] = None,
+          a_off: int = 0, b_off: int = 0, c_off: int = 0) -> torch.Tensor:
+    """C = alpha*op(A)@op(B) + beta*C (+bias) on raw row-major storage.
+
+    ``*_off`` are element offsets into the (contiguous) storage of a/b/c.
+    """
+    es = 4
+    _lib.call("ds2_sgemm", int(trans_a), int(trans_b), m, n, k, float(alpha),
+              a.data_ptr() + es * a_off, lda, 0, b.data_ptr() + es * b_off, ldb, 0,
+              float(beta), c.data_ptr() + es * c_off, ldc, 0, 1, _p(bias), _stream())
+    return c
+
+
+def matmul_nt(x2d: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None,
+              out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """x2d[M,K] @ w[N,K]^T (+bias) -> [M,N] (nn.Linear forward)."""
+    m, k = x2d.shape
+    n = w.shape[0]
+    if out is None:
+        out = torch.empty(m, n, device=x2d.device, dtype=_F32)
+    return sgemm(x2d, w, out, m=m, n=n, k=k, trans_b=True, lda=k, ldb=k, ldc=n, bias=bias)
+
+
+def conv_out_shape(h: int, w: int, kh: int, kw: int, sh: int, sw: int, ph: int, pw: int):
+    return (h + 2 * ph - kh) // sh + 1, (w + 2 * pw - kw) // sw + 1
+
+
+def conv2d_fwd(x, weight, bias, stride, padding, out_lens=None):
+    x = _need(x, "conv2d.x")
+    weight = _need(weight, "conv2d.weight")
+    n, ci, h, w = x.shape
+    co, _, kh, kw = weight.shape
+    ho, wo = conv_out_shape(h, w, kh, kw, stride[0], stride[1], padding[0], padding[1])
+    y = torch.empty(n, co, ho, wo, device=x.device, dtype=_F32)
+    _lib.call("ds2_conv2d_fwd", x.data_ptr(), weight.data_ptr(),
+              _p(None if bias is None else _need(bias, "conv2d.bias")), y.data_ptr(), n, ci, h, w,
+              co, kh, kw, stride[0], stride[1], padding[0], padding[1], _p(out_lens), _stream())
+    return y
+
+
+def conv2d_dgrad(dy, weight, x_shape, stride, padding):
+    dy = _need(dy, "conv2d.dy")
+    n, ci, h, w = x_shape
+    co, _, kh, kw = weight.shape
+    dx = torch.empty(n, ci, h, w, device=dy.device, dtype=_F32)
+    _lib.call("ds2_conv2d_dgrad", dy.data_ptr(), weight.data_ptr(), dx.data_ptr(), n, ci, h, w, co,
+              kh, kw, stride[0], stride[1], padding[0], padding[1], _stream())
+    return dx
+
+
+def conv2d_wgrad(dy, x, w_shape, stride, padding, with_bias: bool):
+    dy = _need(dy, "conv2d.dy")
+    x = _need(x, "conv2d.x")
+    n, ci, h, w = x.shape
+    co, _, kh, kw = w_shape
+    dw = torch.empty(w_shape, device=x.device, dtype=_F32)
+    db = torch.empty(co, device=x.device, dtype=_F32) if with_bias else None
+    dims = (n, ci, h, w, co, kh, kw, stride[0], stride[1], padding[0], padding[1])
+    nbytes = _lib.size("ds2_conv2d_wgrad_workspace_size", *dims)
+    ws = _ws(nbytes, x.device)
+    _lib.call("ds2_conv2d_wgrad", dy.data_ptr(), x.data_ptr(), dw.data_ptr(), _p(db), *dims,
+              ws.data_ptr(), ws.numel(), _stream())
+    return dw, db
+
+
+def bn_stats(x, outer, c, inner, eps, momentum, running_mean, running_var, training):
+    mean = torch.empty(c, device=x.device, dtype=_F32)
+    invstd = torch.empty(c, device=x.device, dtype=_F32)
+    if training:
+        ws = _ws(_lib.size("ds2_bn_workspace_size", outer, c, inner), x.device)
+        _lib.call("ds2_bn_train_stats", x.data_ptr(), outer, c, inner, float(eps), float(momentum),
+                  mean.data_ptr(), invstd.data_ptr(), _p(running_mean), _p(running_var),
+                  ws.data_ptr(), ws.numel(), _stream())
+    else:
+        _lib.call("ds2_bn_eval_stats", running_mean.data_ptr(), running_var.data_ptr(), c,
+                  float(eps), mean.data_ptr(), invstd.data_ptr(), _stream())
+    return mean, invstd
+
+
+def bn_apply(x, outer, c, inner, mean, invstd, gamma, beta):
+    y = torch.empty_like(x)
+    _lib.call("ds2_bn_apply", x.data_ptr(), outer, c, inner, mean.data_ptr(), invstd.data_ptr(),
+              gamma.data_ptr(), beta.data_ptr(), y.data_ptr(), _stream())
+    return y
+
+
+def bn_backward(dy, dy_layout, x, outer, c, d, t, mean, invstd, gamma, beta, masked=False,
+                lens=None, lo=0.0, hi=20.0, want_dbias=False):
+    dx = torch.empty(outer, c, d, t, device=x.device, dtype=_F32)
+    dgamma = torch.empty(c, device=x.device, dtype=_F32)
+    dbeta = torch.empty(c, device=x.device, dtype=_F32)
+    dbias = torch.empty(c, device=x.device, dtype=_F32) if want_dbias else None
+    ws = _ws(_lib.size("ds2_bn_workspace_size", outer, c, d * t), x.device)
+    _lib.call("ds2_bn_backward", dy.data_ptr(), dy_layout, x.data_ptr(), outer, c, d, t,
+              mean.data_ptr(), invstd.data_ptr(), gamma.data_ptr(), beta.data_ptr(), int(masked),
+              _p(lens), float(lo), float(hi), dx.data_ptr(), dgamma.data_ptr(), dbeta.data_ptr(),
+              _p(dbias), ws.data_ptr(), ws.numel(), _stream())
+    return dx, dgamma, dbeta, dbias
+
+
+def colsum(x2d_storage, rows, cols, ld, out, accumulate=False, off=0):
+    _lib.call("ds2_colsum", x2d_storage.data_ptr() + 4 * off, rows, cols, ld, out.data_ptr(),
+              int(accumulate), _stream())
+    return out
+
+
+def softmax_tnc(logits_tnc: torch.Tensor) -> torch.Tensor:
+    """probs[N,T,C] = softmax over C of logits stored [T,N,C]."""
+    x = _need(logits_tnc, "softmax.logits")
+    t, n, c = x.shape
+    probs = torch.empty(n, t, c, device=x.device, dtype=_F32)
+    _lib.call("ds2_softmax_tnc", x.data_ptr(), t, n, c, probs.data_ptr(), _stream())
+    return probs
+
+
+def ctc_loss_raw(acts_tnc, labels, act_lens, label_lens, max_label_len, blank=0,
+                 zero_infinity=False, want_grad=True):
+    acts = _need(acts_tnc, "ctc.acts")
+    t, n, c = acts.shape
+    costs = torch.empty(n, device=acts.device, dtype=_F32)
+    grads = torch.empty_like(acts) if want_grad else None
+    ws = _ws(_lib.size("ds2_ctc_workspace_size", t, n, max_label_len), acts.device)
+    _lib.call("ds2_ctc_loss", acts.data_ptr(), t, n, c, labels.data_ptr(), label_lens.data_ptr(),
+              act_lens.data_ptr(), int(max_label_len), int(blank), int(zero_infinity),
+              costs.data_ptr(), _p(grads), ws.data_ptr(), ws.numel(), _stream())
+    return costs, grads
+
+
+def greedy_decode_raw(probs: torch.Tensor, sizes: Optional[torch.Tensor], blank: int = 0,
+                      want_argmax: bool = False):
+    """Device argmax + CTC collapse.  probs [N,T,C] (any strides, fp32).
+
+    Returns (ids [N,T] int32, offsets [N,T] int32, counts [N] int32, argmax or None);
+    row n holds counts[n] valid entries.
+    """
+    if not probs.is_cuda or probs.dtype != _F32:
+        raise _lib.Ds2Error("greedy_decode: expected a float32 device tensor")
+    n, t, c = probs.shape
+    if probs.stride(2) != 1:
+        probs = probs.contiguous()
+    ids = torch.empty(n, t, device=probs.device, dtype=_I32)
+    offs = torch.empty(n, t, device=probs.device, dtype=_I32)
+    counts = torch.empty(n, device=probs.device, dtype=_I32)
+    am = torch.empty(n, t, device=probs.device, dtype=_I32) if want_argmax else None
+    if sizes is not None:
+        sizes = sizes.to(device=probs.device, dtype=_I32).contiguous()
+    _lib.call("ds2_greedy_decode", probs.data_ptr(), n, t, c, probs.stride(0), probs.stride(1),
+              _p(sizes), int(blank), ids.data_ptr(), offs.data_ptr(), counts.data_ptr(), _p(am),
+              _stream())
+    return ids, offs, counts, am
+
+
+def stft_logmag(pcm: torch.Tensor, n_samples: torch.Tensor, n_fft: int, hop: int,
+                window: torch.Tensor, normalize: int, gauss_taps: Optional[torch.Tensor],
+                max_frames: int) -> torch.Tensor:
+    pcm = _need(pcm, "stft.pcm")
+    n_samples = _need(n_samples, "stft.n_samples", _I32)
+    window = _need(window, "stft.window", torch.float64)
+    b, max_samples = pcm.shape
+    f = n_fft // 2 + 1
+    out = torch.empty(b, f, max_frames, device=pcm.device, dtype=_F32)
+    ws = _ws(_lib.size("ds2_stft_workspace_size", b, max_frames), pcm.device)
+    radius = 0 if gauss_taps is None else (gauss_taps.numel() - 1) // 2
+    _lib.call("ds2_stft_logmag", pcm.data_ptr(), n_samples.data_ptr(), b, max_samples, n_fft, hop,
+              window.data_ptr(), int(normalize), _p(gauss_taps), radius, out.data_ptr(),
+              max_frames, ws.data_ptr(), ws.numel(), _stream())
+    return out
+
+
+# ----------------------------------------------------------------------------
+# autograd functions
+class ConvBlockFn(torch.autograd.Function):
+    """Conv2d -> mask -> BatchNorm2d -> mask -> Hardtanh -> mask (model.py:208-215,63-79).
+
+    out_layout 0 returns [N, C, D, T'] like MaskConv; 1 returns the T'xNx(C*D)
+    collapse of model.py:360-362 directly.
+    """
+
+    @staticmethod
+    def forward(ctx, x, lens, weight, bias, gamma, beta, running_mean, running_var, training,
+                momentum, eps, stride, padding, lo, hi, out_layout):
+        z = conv2d_fwd(x, weight, bias, stride, padding, out_lens=lens)
+        n, c, d, t = z.shape
+        mean, invstd = bn_stats(z, n, c, d * t, eps, momentum, running_mean, running_var, training)
+        if out_layout == 1:
+            y = torch.empty(t, n, c * d, device=z.device, dtype=_F32)
+        else:
+            y = torch.empty_like(z)
+        _lib.call("ds2_bn_apply_mask_htanh", z.data_ptr(), n, c, d, t, mean.data_ptr(),
+                  invstd.data_ptr(), gamma.data_ptr(), beta.data_ptr(), _p(lens), float(lo),
+                  float(hi), y.data_ptr(), int(out_layout), _stream())
+        ctx.save_for_backward(x, z, lens, weight, gamma, beta, mean, invstd)
+        ctx.cfg = (stride, padding, lo, hi, out_layout, bias is not None, training)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, z, lens, weight, gamma, beta, mean, invstd = ctx.saved_tensors
+        stride, padding, lo, hi, out_layout, has_bias, training = ctx.cfg
+        if not training:
+            raise _lib.Ds2Error("ConvBlockFn backward in eval mode is not supported")
+        dy = dy.contiguous()
+        n, c, d, t = z.shape
+        dz, dgamma, dbeta, dbias = bn_backward(dy, out_layout, z, n, c, d, t, mean, invstd, gamma,
+                                               beta, masked=True, lens=lens, lo=lo, hi=hi,
+                                               want_dbias=has_bias)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = conv2d_dgrad(dz, weight, x.shape, stride, padding)
+        dw, _ = conv2d_wgrad(dz, x, weight.shape, stride, padding, with_bias=False)
+        return (dx, None, dw, dbias, dgamma, dbeta) + (None,) * 10
+
+
+class SeqBatchNormFn(torch.autograd.Function):
+    """SequenceWise(BatchNorm1d) on x viewed [R, C] (model.py:28-43, 89, 336)."""
+
+    @staticmethod
+    def forward(ctx, x2d, gamma, beta, running_mean, running_var, training, momentum, eps):
+        x2d = x2d.contiguous()
+        r, c = x2d.shape
+        mean, invstd = bn_stats(x2d, r, c, 1, eps, momentum, running_mean, running_var, training)
+        y = bn_apply(x2d, r, c, 1, mean, invstd, gamma, beta)
+        ctx.save_for_backward(x2d, gamma, beta, mean, invstd)
+        ctx.training = training
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2d, gamma, beta, mean, invstd = ctx.saved_tensors
+        if not ctx.training:
+            raise _lib.Ds2Error("SeqBatchNormFn backward in eval mode is not supported")
+        r, c = x2d.shape
+        dx, dgamma, dbeta, _ = bn_backward(dy.contiguous(), 0, x2d, r, c, 1, 1, mean, invstd,
+                                           gamma, beta)
+        return dx.view(r, c), dgamma, dbeta, None, None, None, None, None
+
+
+class LinearFn(torch.autograd.Function):
+    """y = x @ W^T (no bias; model.py:337)."""
+
+    @staticmethod
+    def forward(ctx, x2d, weight):
+        x2d = x2d.contiguous()
+        ctx.save_for_backward(x2d, weight)
+        return matmul_nt(x2d, weight)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2d, weight = ctx.saved_tensors
+        dy = dy.contiguous()
+        m, k = x2d.shape
+        n = weight.shape[0]
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty_like(x2d)
+            sgemm(dy, weight, dx, m=m, n=k, k=n, lda=n, ldb=k, ldc=k)
+        dw = torch.empty_like(weight)
+        sgemm(dy, x2d, dw, m=n, n=k, k=m, trans_a=True, lda=n, ldb=k, ldc=k)
+        return dx, dw
+
+
+class GRULayerFn(torch.autograd.Function):
+    """One (bi)directional GRU layer over padded [T, N, In] input with lengths.
+
+    Equals pack_padded_sequence -> nn.GRU -> pad_packed_sequence (model.py:103-105);
+    with sum_dirs it also folds the direction sum of model.py:107.
+    """
+
+    @staticmethod
+    def forward(ctx, x, lens, sum_dirs, hidden, *weights):
+        x = x.contiguous()
+        t, n, inp = x.shape
+        h = hidden
+        nd = len(weights) // 4
+        dev = x.device
+        x2d = x.view(t * n, inp)
+        h3 = 3 * h
+        xproj = torch.empty(t, n, nd, h3, device=dev, dtype=_F32)
+        for d in range(nd):
+            w_ih, _, b_ih, _ = weights[4 * d: 4 * d + 4]
+            sgemm(x2d, w_ih, xproj, m=t * n, n=h3, k=inp, trans_b=True, lda=inp, ldb=inp,
+                  ldc=nd * h3, bias=b_ih, c_off=d * h3)
+        h_all = torch.empty(t, n, nd, h, device=dev, dtype=_F32)
+        need_grad = torch.is_grad_enabled() and any(ctx.needs_input_grad)
+        gates = torch.empty(t, n, nd, 4 * h, device=dev, dtype=_F32) if need_grad else None
+        w_hh_f, b_hh_f = weights[1], weights[3]
+        w_hh_r = weights[5] if nd == 2 else None
+        b_hh_r = weights[7] if nd == 2 else None
+        ws = _ws(_lib.size("ds2_gru_fwd_workspace_size", n, h, nd), dev)
+        _lib.call("ds2_gru_fwd", t, n, h, nd, xproj.data_ptr(), w_hh_f.data_ptr(), _p(w_hh_r),
+                  b_hh_f.data_ptr(), _p(b_hh_r), lens.data_ptr(), h_all.data_ptr(), _p(gates),
+                  ws.data_ptr(), ws.numel(), _stream())
+        if sum_dirs and nd == 2:
+            y = torch.empty(t, n, h, device=dev, dtype=_F32)
+            _lib.call("ds2_dirsum", h_all.data_ptr(), t * n, nd, h, y.data_ptr(), _stream())
+        else:
+            y = h_all.view(t, n, nd * h)
+        ctx.save_for_backward(x, lens, h_all, gates, *weights)
+        ctx.cfg = (sum_dirs, h, nd)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, lens, h_all, gates, *weights = ctx.saved_tensors
+        sum_dirs, h, nd = ctx.cfg
+        t, n, inp = x.shape
+        dev = x.device
+        h3 = 3 * h
+        dy = dy.contiguous()
+        dy_dirs = 1 if (sum_dirs and nd == 2) else nd
+        dgx = torch.empty(t, n, nd, h3, device=dev, dtype=_F32)
+        dgh = torch.empty(t, n, nd, h3, device=dev, dtype=_F32)
+        w_hh_f = weights[1]
+        w_hh_r = weights[5] if nd == 2 else None
+        ws = _ws(_lib.size("ds2_gru_bwd_workspace_size", n, h, nd), dev)
+        _lib.call("ds2_gru_bwd", t, n, h, nd, dy.data_ptr(), dy_dirs, w_hh_f.data_ptr(),
+                  _p(w_hh_r), h_all.data_ptr(), gates.data_ptr(), lens.data_ptr(), dgx.data_ptr(),
+                  dgh.data_ptr(), ws.data_ptr(), ws.numel(), _stream())
+        x2d = x.view(t * n, inp)
+        tn = t * n
+        ld = nd * h3
+        grads = []
+        dx = torch.empty(t, n, inp, device=dev, dtype=_F32) if ctx.needs_input_grad[0] else None
+        for d in range(nd):
+            w_ih, w_hh, b_ih, b_hh = weights[4 * d: 4 * d + 4]
+            dw_ih = torch.empty_like(w_ih)
+            sgemm(dgx, x2d, dw_ih, m=h3, n=inp, k=tn, trans_a=True, lda=ld, ldb=inp, ldc=inp,
+                  a_off=d * h3)
+            db_ih = torch.empty_like(b_ih)
+            colsum(dgx, tn, h3, ld, db_ih, off=d * h3)
+            dw_hh = torch.empty_like(w_hh)
+            if t > 1:
+                # sum_t dgh_t^T h_{t-1} (fwd) / h_{t+1} (rev); h_prev = 0 at the start
+                a_off = (n * ld if d == 0 else 0) + d * h3
+                b_off = (0 if d == 0 else n * nd * h) + d * h
+                sgemm(dgh, h_all, dw_hh, m=h3, n=h, k=(t - 1) * n, trans_a=True, lda=ld,
+                      ldb=nd * h, ldc=h, a_off=a_off, b_off=b_off)
+            else:
+                dw_hh.zero_()
+            db_hh = torch.empty_like(b_hh)
+            colsum(dgh, tn, h3, ld, db_hh, off=d * h3)
+            if dx is not None:
+                sgemm(dgx, w_ih, dx, m=tn, n=inp, k=h3, lda=ld, ldb=inp, ldc=inp,
+                      beta=0.0 if d == 0 else 1.0, a_off=d * h3)
+            grads += [dw_ih, dw_hh, db_ih, db_hh]
+        return (dx, None, None, None, *grads)
+
+
+class CTCLossFn(torch.autograd.Function):
+    """warp-ctc semantics: summed cost, gradient wrt pre-softmax activations."""
+
+    @staticmethod
+    def forward(ctx, acts, labels, act_lens, label_lens, max_label_len, blank, zero_infinity,
+                size_average):
+        costs, grads = ctc_loss_raw(acts, labels, act_lens, label_lens, max_label_len, blank,
+                                    zero_infinity, want_grad=True)
+        loss = costs.sum()
+        if size_average:
+            n = acts.shape[1]
+            loss = loss / n
+            grads.mul_(1.0 / n)
+        ctx.save_for_backward(grads)
+        return loss
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        (grads,) = ctx.saved_tensors
+        g = grads.clone()
+        go = grad_out.reshape(1).to(dtype=_F32).contiguous()
+        _lib.call("ds2_scale_by_device_scalar", g.data_ptr(), g.numel(), go.data_ptr(), _stream())
+        return g, None, None, None, None, None, None, None
+
+
+class SoftmaxTNCFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits_tnc):
+        probs = softmax_tnc(logits_tnc)
+        ctx.save_for_backward(probs)
+        return probs
+
+    @staticmethod
+    def backward(ctx, dprobs):
+        (probs,) = ctx.saved_tensors
+        n, t, c = probs.shape
+        d = torch.empty(t, n, c, device=probs.device, dtype=_F32)
+        _lib.call("ds2_softmax_tnc_bwd", probs.data_ptr(), dprobs.contiguous().data_ptr(), t, n, c,
+                  d.data_ptr(), 0, _stream())
+        return d

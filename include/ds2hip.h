@@ -1,0 +1,216 @@
+/*
+ * libds2hip — MI355X-native (gfx950 / CDNA4) DeepSpeech2 hot path, C ABI.
+ *
+ * The reference (vadimkantorov/deepspeech.pytorch) has no C ABI of its own: its
+ * pluggable seams are Python objects whose kernels come from third-party
+ * libraries (librosa FFT, cuDNN conv/BN/RNN, cuBLAS, warp-ctc, ATen argmax).
+ * Every entry point below replaces one of those implicit kernels; the comment
+ * above each names the reference call site (file:line) it stands in for.
+ *
+ * Conventions:
+ *   - every function returns ds2_status_t; no exception crosses the ABI;
+ *   - all buffers are caller-owned device pointers (fp32 unless noted, int32
+ *     for lengths/labels), dense row-major unless a leading dimension is given;
+ *   - work is enqueued on `stream` (a hipStream_t, NULL = legacy default);
+ *     nothing synchronises the device, allocates, or touches host memory;
+ *   - scratch memory comes in through (ws, ws_bytes); query the size with the
+ *     matching *_workspace_size() function.
+ */
+#ifndef DS2HIP_H
+#define DS2HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum ds2_status_t {
+  DS2_OK = 0,
+  DS2_INVALID_VALUE = 1,
+  DS2_UNSUPPORTED_SHAPE = 2,
+  DS2_HIP_ERROR = 3,
+  DS2_RCCL_ERROR = 4,
+  DS2_WORKSPACE_TOO_SMALL = 5
+} ds2_status_t;
+
+typedef void* ds2_stream_t; /* hipStream_t */
+
+const char* ds2_status_string(ds2_status_t status);
+const char* ds2_last_error(void);  /* text of the last HIP error seen (thread-local) */
+const char* ds2_version(void);
+
+/* ------------------------------------------------------------------------ */
+/* Features: SpectrogramParser.audio_to_stft + normalize_audio('max_frame') */
+/* ref data/data_loader.py:201-220,276-284; data/data_loader_aug.py:220-249,297-307 */
+/* pcm:  [batch][max_samples] float32, utterance b has n_samples[b] valid samples   */
+/* out:  [batch][n_fft/2+1][max_frames], frames t >= 1 + n_samples[b]/hop are zero  */
+/* window: n_fft doubles (symmetric Hamming in the reference).                     */
+/* normalize: 0 = log1p(|X|), 1 = 'max_frame' (log1p(|X|*2^20) - mean(gauss20(mean_f))) */
+size_t ds2_stft_workspace_size(int batch, int max_frames);
+ds2_status_t ds2_stft_logmag(const float* pcm, const int* n_samples, int batch, int max_samples,
+                             int n_fft, int hop, const double* window, int normalize,
+                             const float* gauss_taps, int gauss_radius,
+                             float* out, int max_frames, void* ws, size_t ws_bytes,
+                             ds2_stream_t stream);
+
+/* ------------------------------------------------------------------------ */
+/* Dense fp32 GEMM on MFMA (v_mfma_f32_32x32x2_f32), strided-batched, row-major.
+ * C[b] = alpha * op(A[b]) @ op(B[b]) + beta * C[b] (+ bias[n] if bias != NULL)
+ * trans_a = 0: A is [m][lda];  1: A is stored [k][lda] (A^T)
+ * trans_b = 0: B is [k][ldb];  1: B is stored [n][ldb] (B^T)
+ * Replaces cuBLAS behind cuDNN's RNN input projection / BPTT weight gradients
+ * (ref model.py:90-91,104 nn.GRU) and nn.Linear (ref model.py:337).          */
+ds2_status_t ds2_sgemm(int trans_a, int trans_b, int m, int n, int k, float alpha,
+                       const float* a, int64_t lda, int64_t stride_a,
+                       const float* b, int64_t ldb, int64_t stride_b, float beta,
+                       float* c, int64_t ldc, int64_t stride_c, int batch,
+                       const float* bias, ds2_stream_t stream);
+
+/* ------------------------------------------------------------------------ */
+/* Conv2d, NCHW fp32, implicit GEMM on MFMA. ref model.py:209,212 (nn.Conv2d via
+ * cuDNN), masked by MaskConv model.py:63-79 when out_lens != NULL: output
+ * columns w >= out_lens[n] are written as 0.                                  */
+ds2_status_t ds2_conv2d_fwd(const float* x, const float* w, const float* bias, float* y,
+                            int n, int c_in, int h_in, int w_in, int c_out, int kh, int kw,
+                            int sh, int sw, int ph, int pw, const int* out_lens,
+                            ds2_stream_t stream);
+ds2_status_t ds2_conv2d_dgrad(const float* dy, const float* w, float* dx,
+                              int n, int c_in, int h_in, int w_in, int c_out, int kh, int kw,
+                              int sh, int sw, int ph, int pw, ds2_stream_t stream);
+size_t ds2_conv2d_wgrad_workspace_size(int n, int c_in, int h_in, int w_in, int c_out, int kh,
+                                       int kw, int sh, int sw, int ph, int pw);
+/* dw = sum over (n, ho, wo) of dy * im2col(x); dbias = sum of dy (if dbias != NULL). */
+ds2_status_t ds2_conv2d_wgrad(const float* dy, const float* x, float* dw, float* dbias,
+                              int n, int c_in, int h_in, int w_in, int c_out, int kh, int kw,
+                              int sh, int sw, int ph, int pw, void* ws, size_t ws_bytes,
+                              ds2_stream_t stream);
+
+/* ------------------------------------------------------------------------ */
+/* BatchNorm (training statistics), x viewed as [outer][c][inner].
+ * ref model.py:210,213 (BatchNorm2d), model.py:89,336 (SequenceWise BatchNorm1d).
+ * Batch statistics include padded (zeroed) positions, as in the reference.
+ * Computes save_mean / save_invstd and updates the running stats in place
+ * (running_var uses the unbiased variance, momentum as in torch).            */
+size_t ds2_bn_workspace_size(int outer, int c, int inner);
+ds2_status_t ds2_bn_train_stats(const float* x, int outer, int c, int inner, float eps,
+                                float momentum, float* save_mean, float* save_invstd,
+                                float* running_mean, float* running_var, void* ws,
+                                size_t ws_bytes, ds2_stream_t stream);
+ds2_status_t ds2_bn_eval_stats(const float* running_mean, const float* running_var, int c,
+                               float eps, float* save_mean, float* save_invstd,
+                               ds2_stream_t stream);
+/* y = gamma * (x - mean) * invstd + beta over [outer][c][inner]. */
+ds2_status_t ds2_bn_apply(const float* x, int outer, int c, int inner, const float* mean,
+                          const float* invstd, const float* gamma, const float* beta, float* y,
+                          ds2_stream_t stream);
+/* Conv-block epilogue (MaskConv, model.py:69-78): x is [n][c][d][t];
+ * y = mask(hardtanh(mask(bn(x)), lo, hi)) where mask zeroes t >= lens[n].
+ * out_layout 0: y is [n][c][d][t];  1: y is [t][n][c*d] (the TxNxH collapse of
+ * model.py:360-362, fused).                                                   */
+ds2_status_t ds2_bn_apply_mask_htanh(const float* x, int n, int c, int d, int t,
+                                     const float* mean, const float* invstd, const float* gamma,
+                                     const float* beta, const int* lens, float lo, float hi,
+                                     float* y, int out_layout, ds2_stream_t stream);
+/* Backward of bn_apply (masked == 0, x viewed [outer][c][d*t]) or of
+ * bn_apply_mask_htanh (masked != 0, x is [outer=n][c][d][t], lens/lo/hi as in
+ * the forward).  dy has the layout of the forward output (dy_layout as
+ * out_layout above; layout 1 only with masked != 0).  Writes dx
+ * ([outer][c][d][t]), dgamma, dbeta (overwritten) and, if dbias_in != NULL, the
+ * gradient of the per-channel bias added before the masked BN (the conv bias;
+ * exact closed form, see bn.hip).  dx may not alias dy.                      */
+ds2_status_t ds2_bn_backward(const float* dy, int dy_layout, const float* x, int outer, int c,
+                             int d, int t, const float* mean, const float* invstd,
+                             const float* gamma, const float* beta, int masked,
+                             const int* lens, float lo, float hi, float* dx, float* dgamma,
+                             float* dbeta, float* dbias_in, void* ws, size_t ws_bytes,
+                             ds2_stream_t stream);
+
+/* ------------------------------------------------------------------------ */
+/* Bidirectional GRU recurrence (torch gate order r, z, n), packed-sequence
+ * semantics: direction 0 runs t = 0..len-1, direction 1 runs t = len-1..0,
+ * both from h = 0; outputs at t >= len are 0.  ref model.py:97-109 (BatchRNN
+ * pack -> nn.GRU -> pad), model.py:16 (supported_rnns['gru']).
+ *   xproj : [T][N][D][3H]  x @ W_ih^T + b_ih for each direction
+ *   h_all : [T][N][D][H]   per-direction hidden states (output)
+ *   gates : [T][N][D][4H]  (r, z, n, W_hn h + b_hn) cache for backward, or NULL
+ * num_dirs = 1 or 2; w_hh_r / b_hh_r ignored when num_dirs == 1.              */
+size_t ds2_gru_fwd_workspace_size(int n, int h, int num_dirs);
+ds2_status_t ds2_gru_fwd(int t_max, int n, int h, int num_dirs, const float* xproj,
+                         const float* w_hh_f, const float* w_hh_r, const float* b_hh_f,
+                         const float* b_hh_r, const int* lens, float* h_all, float* gates,
+                         void* ws, size_t ws_bytes, ds2_stream_t stream);
+size_t ds2_gru_bwd_workspace_size(int n, int h, int num_dirs);
+/* dy: [T][N][dy_dirs][H]; dy_dirs = 1: gradient of the direction-summed output
+ * (model.py:107), dy_dirs = num_dirs: per-direction output gradient.
+ * dgates_x: [T][N][D][3H] grad wrt xproj;  dgates_h: [T][N][D][3H] grad wrt
+ * W_hh h + b_hh.  Weight gradients are then plain GEMMs (see ds2amd/ops.py). */
+ds2_status_t ds2_gru_bwd(int t_max, int n, int h, int num_dirs, const float* dy, int dy_dirs,
+                         const float* w_hh_f, const float* w_hh_r, const float* h_all,
+                         const float* gates, const int* lens, float* dgates_x, float* dgates_h,
+                         void* ws, size_t ws_bytes, ds2_stream_t stream);
+
+/* y[t][n][j] = sum_d h_all[t][n][d][j]   (model.py:107 view(T,N,2,H).sum(2)) */
+ds2_status_t ds2_dirsum(const float* h_all, int rows, int num_dirs, int h, float* y,
+                        ds2_stream_t stream);
+/* out[j] (+)= sum_i x[i*ld + j]  for i < rows, j < cols (bias gradients). */
+ds2_status_t ds2_colsum(const float* x, int rows, int cols, int64_t ld, float* out,
+                        int accumulate, ds2_stream_t stream);
+
+/* ------------------------------------------------------------------------ */
+/* Softmax over C of logits stored [T][N][C] -> probs [N][T][C] (model.py:375-377). */
+ds2_status_t ds2_softmax_tnc(const float* logits, int t_max, int n, int c, float* probs,
+                             ds2_stream_t stream);
+/* Backward of ds2_softmax_tnc: dlogits[T][N][C] (+)= y * (dy - sum(y*dy)). */
+ds2_status_t ds2_softmax_tnc_bwd(const float* probs, const float* dprobs, int t_max, int n,
+                                 int c, float* dlogits, int accumulate, ds2_stream_t stream);
+
+/* ------------------------------------------------------------------------ */
+/* CTC loss, warp-ctc semantics (ref train.py:12,600-602 warpctc_pytorch.CTCLoss):
+ * softmax is applied internally to acts [T][N][C]; costs[b] = -log p(l_b | x_b);
+ * grads [T][N][C] = d cost_b / d acts (softmax - posterior), zero for t >= len.
+ * labels: concatenated int32 targets; label_lens[b] their lengths.
+ * Infeasible samples (L + repeats > act_len) get cost +inf and zero gradient,
+ * or cost 0 when zero_infinity != 0.                                          */
+size_t ds2_ctc_workspace_size(int t_max, int n, int max_label_len);
+ds2_status_t ds2_ctc_loss(const float* acts, int t_max, int n, int c, const int* labels,
+                          const int* label_lens, const int* act_lens, int max_label_len,
+                          int blank, int zero_infinity, float* costs, float* grads, void* ws,
+                          size_t ws_bytes, ds2_stream_t stream);
+
+/* ------------------------------------------------------------------------ */
+/* GreedyDecoder.decode (ref decoder.py:182-197, process_string :165-180):
+ * argmax over C (first maximum) of probs[n][t][c] (strides in elements), then
+ * drop blanks and frames equal to the previous frame.  Emits compacted label
+ * ids and their frame offsets per utterance plus counts[n].                   */
+ds2_status_t ds2_greedy_decode(const float* probs, int n, int t_max, int c, int64_t stride_n,
+                               int64_t stride_t, const int* sizes, int blank, int* out_ids,
+                               int* out_offsets, int* out_counts, int* argmax_out,
+                               ds2_stream_t stream);
+
+/* ------------------------------------------------------------------------ */
+/* Training-step tail (ref train.py:595-632): clip_grad_norm_(max_norm) then
+ * SGD(momentum, nesterov) on flat fp32 buffers.  The global L2 norm is reduced
+ * on device (fp64), nothing returns to the host.  If skip_flag != NULL and
+ * *skip_flag != 0 the step is skipped (NaN guard, train.py:625-630).          */
+size_t ds2_optim_workspace_size(int64_t numel);
+ds2_status_t ds2_grad_norm(const float* grads, int64_t numel, float* out_norm, void* ws,
+                           size_t ws_bytes, ds2_stream_t stream);
+ds2_status_t ds2_clip_sgd_nesterov(float* params, const float* grads, float* momentum_buf,
+                                   int64_t numel, float lr, float momentum, float max_norm,
+                                   const float* norm, const int* skip_flag,
+                                   ds2_stream_t stream);
+/* *flag = 1 if any x is NaN (flag must be zeroed by the caller first);
+ * if zero_nans, NaNs are replaced by 0 in place (train.py:595-598).           */
+ds2_status_t ds2_nan_guard(float* x, int64_t numel, int zero_nans, int* flag,
+                           ds2_stream_t stream);
+/* x[i] *= *scalar (device scalar, e.g. autograd's grad_output). */
+ds2_status_t ds2_scale_by_device_scalar(float* x, int64_t numel, const float* scalar,
+                                        ds2_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DS2HIP_H */

@@ -1,0 +1,61 @@
+"""CPU: the C-ABI library builds, loads and exports every symbol include/ds2hip.h declares.
+
+No compute is launched here (no GPU in the build container); only the pure host
+queries (status strings, version, workspace sizes) are called.
+"""
+import os
+import re
+
+import pytest
+
+import torch  # noqa: F401  (load torch's HIP runtime first: one libamdhip64 per process)
+from ds2amd import _lib
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(REPO, "include", "ds2hip.h")
+
+
+def declared_symbols():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(ds2_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_library_present():
+    assert os.path.exists(_lib.LIB_PATH), "run make -C deepspeech.pytorch_amd/csrc"
+
+
+def test_every_declared_symbol_is_exported_and_bound():
+    lib = _lib.load()
+    syms = declared_symbols()
+    assert len(syms) >= 30
+    for s in syms:
+        assert hasattr(lib, s), f"{s} declared in ds2hip.h but not exported"
+        assert s in _lib.EXPORTED_SYMBOLS, f"{s} has no ctypes prototype"
+    for s in _lib.EXPORTED_SYMBOLS:
+        assert s in syms, f"{s} bound in _lib but not declared in the header"
+
+
+def test_host_queries():
+    lib = _lib.load()
+    assert lib.ds2_status_string(0) == b"DS2_OK"
+    assert lib.ds2_status_string(5) == b"DS2_WORKSPACE_TOO_SMALL"
+    assert b"gfx950" in lib.ds2_version()
+    assert _lib.size("ds2_ctc_workspace_size", 501, 32, 150) >= 32 * 501 * 301 * 4
+    assert _lib.size("ds2_bn_workspace_size", 16032, 800, 1) > 0
+    assert _lib.size("ds2_gru_fwd_workspace_size", 32, 800, 2) >= 2 * 800 * 800 * 3 * 4
+    assert _lib.size("ds2_gru_bwd_workspace_size", 32, 800, 2) >= 2 * 800 * 2400 * 4
+    assert _lib.size("ds2_conv2d_wgrad_workspace_size", 32, 32, 81, 501, 32, 21, 11, 2, 1, 10,
+                     5) >= 32 * 32 * 7392 * 4
+    assert _lib.size("ds2_stft_workspace_size", 32, 1001) >= 32 * 1001 * 4
+
+
+def test_invalid_args_rejected_without_launch():
+    lib = _lib.load()
+    # negative sizes are rejected before any HIP call
+    assert lib.ds2_sgemm(0, 0, -1, 4, 4, 1.0, None, 4, 0, None, 4, 0, 0.0, None, 4, 0, 1, None,
+                         None) == 1
+    assert lib.ds2_ctc_loss(None, 10, 2, 100, None, None, None, 5, 0, 0, None, None, None, 0,
+                            None) == 1
+    with pytest.raises(_lib.Ds2Error):
+        _lib.call("ds2_dirsum", None, -1, 2, 4, None, None)

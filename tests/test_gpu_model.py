@@ -1,0 +1,142 @@
+"""GPU: the whole DS2 hot path (ds2amd.DeepSpeech + CTCLoss + decoder + Trainer)
+against the reference goldens and the CPU oracle.
+
+Tolerance (north_star): logits within 1e-4 relative of the CPU reference
+(max |diff| <= 1e-4 * max |ref|); greedy strings/offsets and lengths bit-exact.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from ds2amd import model as dsm
+from ds2amd.decoder import GreedyDecoder
+from ds2amd.ctc import CTCLoss
+from oracle import ds2_oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+LABELS = orc.LABELS
+CONF = dict(sample_rate=16000, window_size=0.02, window_stride=0.01, window='hamming')
+REL = 1e-4
+
+
+def _rel(got, ref):
+    got = got.detach().double().cpu()
+    ref = ref.detach().double().cpu() if torch.is_tensor(ref) else torch.from_numpy(ref).double()
+    return (got - ref).abs().max().item() / max(ref.abs().max().item(), 1e-30)
+
+
+def build(seed, hidden, layers):
+    torch.manual_seed(seed)
+    return dsm.DeepSpeech(rnn_type='gru', labels=LABELS, rnn_hidden_size=hidden, nb_layers=layers,
+                          audio_conf=CONF, bidirectional=True)
+
+
+def test_tiny_forward_matches_reference_golden(dev, golden_dir):
+    g = np.load(os.path.join(golden_dir, 'tiny_ds2.npz'))
+    m = build(int(g['seed']), int(g['hidden']), int(g['layers'])).to(dev).train()
+    x = torch.from_numpy(g['x']).to(dev)
+    logits, probs, out_lens = m(x, torch.from_numpy(g['input_sizes']))
+    np.testing.assert_array_equal(out_lens.cpu().numpy(), g['out_lens'])
+    assert _rel(logits, g['logits']) < REL
+    assert _rel(probs, g['probs']) < REL
+    for k in g.files:
+        if k.startswith('after_fwd/'):
+            assert _rel(m.state_dict()[k[len('after_fwd/'):]], g[k]) < 1e-5, k
+    dec = GreedyDecoder(LABELS)
+    strings, _ = dec.decode(probs, out_lens)
+    ref_strings, _ = orc.greedy_decode(probs.cpu(), out_lens.cpu().tolist())
+    assert strings == ref_strings          # bit-exact decode of the same probs
+
+
+def test_tiny_train_step_matches_reference_golden(dev, golden_dir):
+    from ds2amd.trainer import Trainer
+    g = np.load(os.path.join(golden_dir, 'tiny_ds2.npz'))
+    m = build(int(g['seed']), int(g['hidden']), int(g['layers']))
+    tr = Trainer(m, LABELS, lr=3e-4, momentum=0.9, max_norm=100.0, device=dev)
+    data = (torch.from_numpy(g['x']), torch.from_numpy(g['targets']), None,
+            torch.from_numpy(g['pct']).clone(), torch.from_numpy(g['target_sizes']))
+    loss = tr.train_batch(data, return_item=True)
+    assert abs(loss - float(g['loss'])) <= 1e-4 * abs(float(g['loss']))
+    gn = float(tr.optimizer.norm.item())
+    assert abs(gn - float(g['grad_norm'])) <= 1e-4 * float(g['grad_norm'])
+    sd = m.state_dict()
+    for k in g.files:
+        if k.startswith('after_step/'):
+            name = k[len('after_step/'):]
+            ref = torch.from_numpy(g[k])
+            before = None
+            assert (sd[name].cpu() - ref).abs().max().item() <= 1e-6 + 1e-5 * ref.abs().max().item(), name
+
+
+def test_tiny_grads_match_reference_golden(dev, golden_dir):
+    g = np.load(os.path.join(golden_dir, 'tiny_ds2.npz'))
+    m = build(int(g['seed']), int(g['hidden']), int(g['layers'])).to(dev).train()
+    x = torch.from_numpy(g['x']).to(dev)
+    logits, probs, out_lens = m(x, torch.from_numpy(g['input_sizes']))
+    loss = CTCLoss()(logits.transpose(0, 1), torch.from_numpy(g['targets']), out_lens,
+                     torch.from_numpy(g['target_sizes'])) / x.shape[0]
+    loss.backward()
+    for name, p in m.named_parameters():
+        ref = g['grad/' + name]
+        assert _rel(p.grad, ref) < 5e-4, name
+
+
+def test_cfg1_eval_forward_and_decode(dev, golden_dir):
+    g = np.load(os.path.join(golden_dir, 'cfg1_ds2.npz'))
+    m = build(int(g['seed']), 256, 2).to(dev).eval()
+    from ds2amd.data_loader import SpectrogramParser
+    parser = SpectrogramParser(CONF, normalize='max_frame', device=dev)
+    spect, frames = parser.parse_batch([g['wav']])
+    with torch.no_grad():
+        logits, probs, out_lens = m(spect, frames)
+    assert _rel(logits, g['logits']) < REL
+    strings, offsets = GreedyDecoder(LABELS).decode(probs, out_lens)
+    assert strings[0][0] == str(g['decoded'][0])
+    np.testing.assert_array_equal(offsets[0][0].numpy(), g['offsets'])
+
+
+def test_ds2_800_forward_matches_oracle(dev):
+    """5 x BiGRU-800 (the benchmark architecture), bs 4, variable lengths, train mode."""
+    m = build(123456, 800, 5).to(dev).train()
+    o = orc.OracleDS2({k: v.detach().cpu() for k, v in m.state_dict().items()}, 5, 800)
+    g = torch.Generator().manual_seed(0)
+    t_list = [241, 200, 173, 120]
+    x = torch.zeros(4, 1, 161, 241)
+    for i, t in enumerate(t_list):
+        x[i, 0, :, :t] = torch.randn(161, t, generator=g)
+    sizes = torch.IntTensor(t_list)
+    logits, probs, out_lens = m(x.to(dev), sizes)
+    with torch.no_grad():
+        rl, rp, ro, _ = o.forward(x, sizes, training=True)
+    np.testing.assert_array_equal(out_lens.cpu().numpy(), ro.numpy())
+    assert _rel(logits, rl) < REL
+    assert _rel(probs, rp) < REL
+
+
+def test_cfg2_shape_step_properties(dev):
+    """Full benchmark shape (bs32, 10 s): a train step is finite, deterministic and
+    decodes identically to the oracle decoder on the same probs."""
+    from ds2amd.trainer import Trainer
+    torch.manual_seed(123456)
+    m = build(123456, 800, 5)
+    tr = Trainer(m, LABELS, device=dev)
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(32, 1, 161, 1001, generator=g)
+    tl = torch.full((32,), 150, dtype=torch.int32)
+    tg = torch.randint(1, 29, (32 * 150,), generator=g, dtype=torch.int32)
+    pct = torch.ones(32)
+    l1 = tr.train_batch((x, tg, None, pct.clone(), tl), return_item=True)
+    assert np.isfinite(l1)
+    with torch.no_grad():
+        m.eval()
+        _, p1, ol = m(x.to(dev), torch.full((32,), 1001, dtype=torch.int32))
+        _, p2, _ = m(x.to(dev), torch.full((32,), 1001, dtype=torch.int32))
+    assert torch.equal(p1, p2)                                   # deterministic kernels
+    s_gpu, _ = GreedyDecoder(LABELS).decode(p1, ol)
+    s_ref, _ = orc.greedy_decode(p1.cpu(), ol.cpu().tolist())
+    assert s_gpu == s_ref
+    s = p1.sum(-1)
+    assert torch.allclose(s, torch.ones_like(s), atol=1e-5)

@@ -1,0 +1,332 @@
+"""GPU: every HIP kernel against a CPU reference of the same op (fp64 where cheap).
+
+Tolerances (fp32 kernels): relative to the magnitude of the result, 1e-5..1e-4;
+integer/index outputs (greedy decode, lengths) bit-exact.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from ds2amd import ops, _lib
+from oracle import ds2_oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+
+def _close(got, ref, rel=1e-5, name=""):
+    got = got.detach().double().cpu()
+    ref = ref.detach().double().cpu()
+    scale = max(ref.abs().max().item(), 1e-30)
+    err = (got - ref).abs().max().item()
+    assert err <= rel * scale, f"{name}: max err {err:.3e} > {rel:.1e} * {scale:.3e}"
+
+
+# ---------------------------------------------------------------------------- GEMM
+@pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
+@pytest.mark.parametrize("m,n,k", [(1, 1, 1), (37, 53, 29), (128, 128, 16), (300, 257, 513),
+                                   (515, 2400, 132)])
+def test_sgemm(dev, ta, tb, m, n, k):
+    g = torch.Generator().manual_seed(m * 7 + n * 3 + k)
+    a = torch.randn(k, m, generator=g) if ta else torch.randn(m, k, generator=g)
+    b = torch.randn(n, k, generator=g) if tb else torch.randn(k, n, generator=g)
+    c0 = torch.randn(m, n, generator=g)
+    bias = torch.randn(n, generator=g)
+    ref = 0.5 * ((a.t() if ta else a).double() @ (b.t() if tb else b).double()) \
+        + 0.25 * c0.double() + bias.double()
+    ad, bd, cd = a.to(dev), b.to(dev), c0.to(dev).clone()
+    ops.sgemm(ad, bd, cd, m=m, n=n, k=k, trans_a=bool(ta), trans_b=bool(tb),
+              lda=ad.shape[1], ldb=bd.shape[1], ldc=n, alpha=0.5, beta=0.25, bias=bias.to(dev))
+    torch.cuda.synchronize()
+    _close(cd, ref, 1e-5, "sgemm")
+
+
+# ---------------------------------------------------------------------------- conv
+CONVS = [  # (n, ci, h, w, co, kh, kw, sh, sw, ph, pw)
+    (2, 1, 161, 37, 32, 41, 11, 2, 2, 20, 5),
+    (2, 32, 81, 23, 32, 21, 11, 2, 1, 10, 5),
+    (3, 3, 17, 300, 40, 5, 3, 1, 2, 2, 1),
+]
+
+
+@pytest.mark.parametrize("cfg", CONVS)
+def test_conv_fwd_bwd(dev, cfg):
+    n, ci, h, w, co, kh, kw, sh, sw, ph, pw = cfg
+    g = torch.Generator().manual_seed(sum(cfg))
+    x = torch.randn(n, ci, h, w, generator=g, dtype=torch.float64)
+    wt = torch.randn(co, ci, kh, kw, generator=g, dtype=torch.float64) * 0.1
+    bias = torch.randn(co, generator=g, dtype=torch.float64)
+    x.requires_grad_(True)
+    wt.requires_grad_(True)
+    y = F.conv2d(x, wt, bias, stride=(sh, sw), padding=(ph, pw))
+    ho, wo = y.shape[2], y.shape[3]
+    lens = torch.tensor([wo - 3 * i for i in range(n)], dtype=torch.int32)
+    yd = ops.conv2d_fwd(x.detach().float().to(dev), wt.detach().float().to(dev),
+                        bias.float().to(dev), (sh, sw), (ph, pw), out_lens=lens.to(dev))
+    ref = y.detach().clone()
+    for i in range(n):
+        ref[i, :, :, int(lens[i]):] = 0
+    _close(yd, ref, 1e-5, "conv fwd")
+    dy = torch.randn(y.shape, generator=g, dtype=torch.float64)
+    y.backward(dy)
+    dx = ops.conv2d_dgrad(dy.float().to(dev), wt.detach().float().to(dev), x.shape, (sh, sw),
+                          (ph, pw))
+    dw, db = ops.conv2d_wgrad(dy.float().to(dev), x.detach().float().to(dev), tuple(wt.shape),
+                              (sh, sw), (ph, pw), with_bias=True)
+    _close(dx, x.grad, 1e-5, "conv dgrad")
+    _close(dw, wt.grad, 1e-5, "conv wgrad")
+    _close(db, dy.sum((0, 2, 3)), 1e-5, "conv dbias")
+
+
+# ---------------------------------------------------------------------------- BN
+def test_seq_bn_fwd_bwd(dev):
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(777, 96, generator=g, dtype=torch.float64) * 3 + 1
+    gamma = torch.rand(96, generator=g, dtype=torch.float64) + 0.5
+    beta = torch.randn(96, generator=g, dtype=torch.float64)
+    rm, rv = torch.zeros(96), torch.ones(96)
+    rm_d, rv_d = rm.clone().to(dev), rv.clone().to(dev)
+    xr = x.clone().requires_grad_(True)
+    gr, br = gamma.clone().requires_grad_(True), beta.clone().requires_grad_(True)
+    y = F.batch_norm(xr, rm.double(), rv.double(), gr, br, training=True, momentum=0.1, eps=1e-5)
+    dy = torch.randn(y.shape, generator=g, dtype=torch.float64)
+    y.backward(dy)
+    xd = x.float().to(dev).requires_grad_(True)
+    gd = gamma.float().to(dev).requires_grad_(True)
+    bd = beta.float().to(dev).requires_grad_(True)
+    yd = ops.SeqBatchNormFn.apply(xd, gd, bd, rm_d, rv_d, True, 0.1, 1e-5)
+    yd.backward(dy.float().to(dev))
+    _close(yd, y, 1e-5, "bn y")
+    _close(xd.grad, xr.grad, 1e-4, "bn dx")
+    _close(gd.grad, gr.grad, 1e-5, "bn dgamma")
+    _close(bd.grad, br.grad, 1e-5, "bn dbeta")
+    _close(rm_d, 0.1 * x.mean(0), 1e-5, "running_mean")
+    _close(rv_d, 0.9 + 0.1 * x.var(0, unbiased=True), 1e-5, "running_var")
+
+
+@pytest.mark.parametrize("layout", [0, 1])
+def test_conv_block_fwd_bwd(dev, layout):
+    """ConvBlockFn vs conv2d -> mask -> BN -> mask -> hardtanh -> mask (model.py:63-79)."""
+    g = torch.Generator().manual_seed(11 + layout)
+    n, ci, h, w = 3, 4, 21, 30
+    co, kh, kw, sh, sw, ph, pw = 8, 5, 3, 2, 1, 2, 1
+    x = torch.randn(n, ci, h, w, generator=g, dtype=torch.float64)
+    wt = torch.randn(co, ci, kh, kw, generator=g, dtype=torch.float64) * 0.3
+    b = torch.randn(co, generator=g, dtype=torch.float64)
+    gamma = torch.rand(co, generator=g, dtype=torch.float64) * 4 + 2
+    beta = torch.randn(co, generator=g, dtype=torch.float64) * 3 + 4
+    lens = torch.tensor([w, w - 7, w - 13], dtype=torch.int32)
+    params = [t.clone().requires_grad_(True) for t in (x, wt, b, gamma, beta)]
+    xr, wr, brr, gr, ber = params
+    rm, rv = torch.zeros(co, dtype=torch.float64), torch.ones(co, dtype=torch.float64)
+
+    def mask(t):
+        m = torch.arange(t.shape[-1])[None, :] >= lens[:, None].long()
+        return t.masked_fill(m[:, None, None, :], 0)
+    z = mask(F.conv2d(xr, wr, brr, stride=(sh, sw), padding=(ph, pw)))
+    z = mask(F.batch_norm(z, rm, rv, gr, ber, training=True, momentum=0.1, eps=1e-5))
+    y = mask(F.hardtanh(z, 0, 20))
+    nn_, c_, d_, t_ = y.shape
+    yref = y if layout == 0 else y.reshape(nn_, c_ * d_, t_).permute(2, 0, 1)
+    dy = torch.randn(yref.shape, generator=g, dtype=torch.float64)
+    yref.backward(dy)
+    dparams = [p.detach().float().to(dev).requires_grad_(True) for p in params]
+    xd, wd, bd, gd, bed = dparams
+    rm_d, rv_d = torch.zeros(co, device=dev), torch.ones(co, device=dev)
+    yd = ops.ConvBlockFn.apply(xd, lens.to(dev), wd, bd, gd, bed, rm_d, rv_d, True, 0.1, 1e-5,
+                               (sh, sw), (ph, pw), 0.0, 20.0, layout)
+    yd.backward(dy.float().to(dev))
+    _close(yd, yref, 1e-5, "block y")
+    for name, pd, pr in zip(["dx", "dw", "dbias", "dgamma", "dbeta"], dparams, params):
+        _close(pd.grad, pr.grad, 2e-4, name)
+
+
+# ---------------------------------------------------------------------------- GRU
+@pytest.mark.parametrize("n,t,inp,h,bidir", [(5, 23, 40, 24, True), (19, 9, 33, 400, True),
+                                             (3, 17, 20, 16, False)])
+def test_gru_layer(dev, n, t, inp, h, bidir):
+    g = torch.Generator().manual_seed(n * 100 + h)
+    gru = torch.nn.GRU(inp, h, bidirectional=bidir).double()
+    with torch.no_grad():
+        for p in gru.parameters():
+            p.copy_(torch.rand(p.shape, generator=g, dtype=torch.float64) * 0.6 - 0.3)
+    lens = torch.tensor(sorted([t] + [max(1, t - 3 * i - 1) for i in range(n - 1)], reverse=True),
+                        dtype=torch.int32)
+    x = torch.randn(t, n, inp, generator=g, dtype=torch.float64)
+    for i in range(n):
+        x[int(lens[i]):, i] = 0
+    xr = x.clone().requires_grad_(True)
+    packed = torch.nn.utils.rnn.pack_padded_sequence(xr, lens.numpy())
+    out, _ = gru(packed)
+    out, _ = torch.nn.utils.rnn.pad_packed_sequence(out, total_length=t)
+    nd = 2 if bidir else 1
+    summed = out.view(t, n, nd, h).sum(2) if bidir else out
+    dy = torch.randn(summed.shape, generator=g, dtype=torch.float64)
+    summed.backward(dy)
+    weights = [p.detach().float().to(dev).requires_grad_(True) for p in gru.parameters()]
+    xd = x.float().to(dev).requires_grad_(True)
+    yd = ops.GRULayerFn.apply(xd, lens.to(dev), True, h, *weights)
+    yd.backward(dy.float().to(dev))
+    _close(yd, summed, 1e-5, "gru y")
+    _close(xd.grad, xr.grad, 1e-4, "gru dx")
+    for (name, p), wd in zip(gru.named_parameters(), weights):
+        _close(wd.grad, p.grad, 1e-4, "gru " + name)
+
+
+def test_gru_per_direction_output(dev):
+    n, t, inp, h = 4, 11, 8, 16
+    g = torch.Generator().manual_seed(5)
+    gru = torch.nn.GRU(inp, h, bidirectional=True).double()
+    lens = torch.tensor([11, 9, 4, 1], dtype=torch.int32)
+    x = torch.randn(t, n, inp, generator=g, dtype=torch.float64)
+    xr = x.clone().requires_grad_(True)
+    out, _ = gru(torch.nn.utils.rnn.pack_padded_sequence(xr, lens.numpy()))
+    out, _ = torch.nn.utils.rnn.pad_packed_sequence(out, total_length=t)
+    dy = torch.randn(out.shape, generator=g, dtype=torch.float64)
+    out.backward(dy)
+    weights = [p.detach().float().to(dev).requires_grad_(True) for p in gru.parameters()]
+    xd = x.float().to(dev).requires_grad_(True)
+    yd = ops.GRULayerFn.apply(xd, lens.to(dev), False, h, *weights)
+    yd.backward(dy.float().to(dev))
+    _close(yd, out, 1e-5, "gru y")
+    _close(xd.grad, xr.grad, 1e-4, "gru dx")
+
+
+# ---------------------------------------------------------------------------- CTC
+def test_ctc_vs_torch(dev):
+    g = torch.Generator().manual_seed(9)
+    t, n, c = 60, 6, 30
+    acts = torch.randn(t, n, c, generator=g) * 3
+    act_lens = torch.tensor([60, 55, 40, 12, 30, 5], dtype=torch.int32)
+    label_lens = torch.tensor([20, 1, 0, 5, 14, 2], dtype=torch.int32)
+    labels = torch.randint(1, c, (int(label_lens.sum()),), generator=g, dtype=torch.int32)
+    labels[3:6] = 7                       # repeats inside sample 0
+    loss_ref, grad_ref = orc.ctc_loss(acts.double(), labels, act_lens, label_lens)
+    costs_ref = orc.ctc_costs(acts, labels, act_lens, label_lens)
+    costs, grads = ops.ctc_loss_raw(acts.to(dev), labels.to(dev), act_lens.to(dev),
+                                    label_lens.to(dev), int(label_lens.max()))
+    _close(costs, costs_ref, 1e-5, "ctc costs")
+    _close(grads, grad_ref, 1e-5, "ctc grads")
+
+
+def test_ctc_infeasible_and_module(dev):
+    from ds2amd.ctc import CTCLoss
+    acts = torch.randn(4, 2, 5)
+    labels = torch.tensor([1, 2, 3, 1, 1], dtype=torch.int32)   # sample1 '1 1' needs 3 frames
+    act_lens = torch.tensor([4, 2], dtype=torch.int32)
+    label_lens = torch.tensor([3, 2], dtype=torch.int32)
+    costs, grads = ops.ctc_loss_raw(acts.to(dev), labels.to(dev), act_lens.to(dev),
+                                    label_lens.to(dev), 3)
+    assert torch.isinf(costs[1]).item() and torch.isfinite(costs[0]).item()
+    assert grads[:, 1].abs().sum().item() == 0
+    crit = CTCLoss(zero_infinity=True)
+    a = acts.to(dev).requires_grad_(True)
+    loss = crit(a, labels, act_lens, label_lens)
+    loss.backward()
+    ref0 = orc.ctc_costs(acts[:, :1], labels[:3], act_lens[:1], label_lens[:1])
+    _close(loss, ref0, 1e-5, "zero_infinity sum")
+    assert torch.isfinite(a.grad).all().item()
+
+
+# ---------------------------------------------------------------------------- softmax / greedy
+def test_softmax_tnc(dev):
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(17, 5, 30, generator=g, dtype=torch.float64) * 4
+    xd = x.float().to(dev).requires_grad_(True)
+    p = ops.SoftmaxTNCFn.apply(xd)
+    ref = F.softmax(x.transpose(0, 1), -1)
+    _close(p, ref, 1e-6, "softmax")
+    dp = torch.randn(ref.shape, generator=g, dtype=torch.float64)
+    p.backward(dp.float().to(dev))
+    xr = x.clone().requires_grad_(True)
+    F.softmax(xr.transpose(0, 1), -1).backward(dp)
+    _close(xd.grad, xr.grad, 1e-5, "softmax bwd")
+
+
+def test_greedy_decode_bit_exact(dev, golden_dir):
+    import os
+    gd = np.load(os.path.join(golden_dir, "greedy_decoder.npz"))
+    probs = torch.from_numpy(gd["probs"])
+    sizes = torch.from_numpy(gd["sizes"])
+    ids, offs, counts, am = ops.greedy_decode_raw(probs.to(dev), sizes.to(dev), want_argmax=True)
+    np.testing.assert_array_equal(am.cpu().numpy(), torch.max(probs, 2)[1].numpy())
+    np.testing.assert_array_equal(counts.cpu().numpy(), gd["counts"])
+    for i in range(probs.shape[0]):
+        k = int(gd["counts"][i])
+        np.testing.assert_array_equal(offs[i, :k].cpu().numpy(), gd["offsets"][i][:k])
+    from ds2amd.decoder import GreedyDecoder
+    dec = GreedyDecoder(orc.LABELS)
+    strings, offsets = dec.decode(probs.to(dev), sizes)
+    assert [s[0] for s in strings] == [str(s) for s in gd["strings"]]
+    hs, ho = dec.decode(torch.from_numpy(gd["hand_probs"]).to(dev), torch.IntTensor([6]))
+    assert hs[0][0] == "AA " and ho[0][0].tolist() == [1, 4, 5]
+    # long utterance crossing several 64-frame chunks, strided (transposed) probs
+    g = torch.Generator().manual_seed(2)
+    big = torch.rand(501, 7, 30, generator=g)
+    big[:, :, 0] += 0.3
+    view = big.to(dev).transpose(0, 1)           # [N, T, C] non-contiguous
+    s2, o2 = dec.decode(view, torch.IntTensor([501, 500, 499, 64, 63, 65, 1]))
+    r2, ro2 = orc.greedy_decode(big.transpose(0, 1), [501, 500, 499, 64, 63, 65, 1])
+    assert s2 == r2
+    for a, b in zip(o2, ro2):
+        assert a[0].tolist() == b[0].tolist()
+
+
+# ---------------------------------------------------------------------------- STFT
+def test_stft_vs_oracle(dev, golden_dir):
+    import os
+    from ds2amd.data_loader import SpectrogramParser
+    gd = np.load(os.path.join(golden_dir, "cfg1_ds2.npz"))
+    parser = SpectrogramParser(dict(sample_rate=16000, window_size=0.02, window_stride=0.01,
+                                    window='hamming'), normalize='max_frame', device=dev)
+    rng = np.random.default_rng(0)
+    wavs = [gd["wav"], (rng.standard_normal(23456) * 0.3).astype(np.float32),
+            np.sin(np.arange(4000) * 0.3).astype(np.float32)]
+    out, frames = parser.parse_batch(wavs)
+    for i, y in enumerate(wavs):
+        ref = orc.spectrogram(y)
+        assert int(frames[i]) == ref.shape[1]
+        got = out[i, 0, :, :ref.shape[1]].cpu()
+        err = (got - ref).abs().max().item()
+        assert err < 2e-4, f"wav {i}: max abs err {err}"
+        assert out[i, 0, :, ref.shape[1]:].abs().sum().item() == 0
+    np.testing.assert_allclose(out[0, 0].cpu().numpy(), gd["spect"], atol=2e-4, rtol=0)
+
+
+# ---------------------------------------------------------------------------- optimizer
+def test_fused_sgd_matches_torch(dev):
+    from ds2amd.optim import FlatParams, FusedSGD
+    g = torch.Generator().manual_seed(4)
+    shapes = [(30, 7), (13,), (5, 5, 3), (1,)]
+    init = [torch.randn(s, generator=g) for s in shapes]
+    ref = [torch.nn.Parameter(t.clone()) for t in init]
+    opt = torch.optim.SGD(ref, lr=0.01, momentum=0.9, nesterov=True)
+    mine = [torch.nn.Parameter(t.clone().to(dev)) for t in init]
+    flat = FlatParams(mine, dev)
+    fopt = FusedSGD(flat, lr=0.01, momentum=0.9, max_norm=1.0)
+    for step in range(3):
+        grads = [torch.randn(s, generator=g) * (3 if step == 1 else 0.1) for s in shapes]
+        for p, gr in zip(ref, grads):
+            p.grad = gr.clone()
+        torch.nn.utils.clip_grad_norm_(ref, 1.0)
+        opt.step()
+        fopt.zero_grad()
+        for p, gr in zip(mine, grads):
+            p.grad.copy_(gr.to(dev))
+        fopt.step()
+        for p, r in zip(mine, ref):
+            _close(p, r, 1e-6, f"sgd step {step}")
+
+
+def test_nan_guard_and_skip(dev):
+    from ds2amd.optim import FlatParams, FusedSGD
+    x = torch.tensor([1.0, float('nan'), 3.0], device=dev)
+    flag = torch.zeros(1, dtype=torch.int32, device=dev)
+    _lib.call("ds2_nan_guard", x.data_ptr(), 3, 1, flag.data_ptr(), ops._stream())
+    assert flag.item() == 1 and x.tolist() == [1.0, 0.0, 3.0]
+    p = torch.nn.Parameter(torch.ones(8, device=dev))
+    flat = FlatParams([p], dev)
+    opt = FusedSGD(flat, lr=1.0, momentum=0.9)
+    p.grad.fill_(1.0)
+    opt.step(skip_flag=flag)
+    assert torch.all(p == 1).item()

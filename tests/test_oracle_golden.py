@@ -1,0 +1,160 @@
+"""CPU: the oracle (and the host-side model constructor) against the reference's goldens.
+
+The goldens were produced by tests/golden/make_golden.py from the reference's
+own model.py / decoder.py.  These tests pin the oracle before any GPU result is
+compared against it.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import ds2_oracle as orc
+from ds2amd import model as dsm
+
+LABELS = orc.LABELS
+CONF = dict(sample_rate=16000, window_size=0.02, window_stride=0.01, window='hamming')
+
+
+def _load(golden_dir, name):
+    return np.load(os.path.join(golden_dir, name))
+
+
+def build_model(seed, hidden, layers):
+    torch.manual_seed(seed)
+    return dsm.DeepSpeech(rnn_type='gru', labels=LABELS, rnn_hidden_size=hidden, nb_layers=layers,
+                          audio_conf=CONF, bidirectional=True)
+
+
+def _checksum(sd, keys):
+    return np.array([float(sd[k].double().sum()) for k in keys])
+
+
+def test_constructor_draws_reference_weights(golden_dir):
+    g = _load(golden_dir, 'tiny_ds2.npz')
+    m = build_model(int(g['seed']), int(g['hidden']), int(g['layers']))
+    keys = [str(k) for k in g['checksum_keys']]
+    assert sorted(k for k, v in m.state_dict().items() if v.is_floating_point()) == sorted(keys)
+    np.testing.assert_array_equal(_checksum(m.state_dict(), keys), g['checksum'])
+
+
+def test_state_dict_keys_match_reference_cfg1(golden_dir):
+    g = _load(golden_dir, 'cfg1_ds2.npz')
+    m = build_model(int(g['seed']), 256, 2)
+    keys = [str(k) for k in g['checksum_keys']]
+    np.testing.assert_array_equal(_checksum(m.state_dict(), keys), g['checksum'])
+
+
+def test_oracle_forward_tiny(golden_dir):
+    g = _load(golden_dir, 'tiny_ds2.npz')
+    m = build_model(int(g['seed']), int(g['hidden']), int(g['layers']))
+    o = orc.OracleDS2(m.state_dict(), int(g['layers']), int(g['hidden']))
+    x = torch.from_numpy(g['x'])
+    sizes = orc.input_sizes_quirk(torch.from_numpy(g['pct']), x.shape[3])
+    np.testing.assert_array_equal(sizes.numpy(), g['input_sizes'])
+    logits, probs, out_lens, acts = o.forward(x, sizes, training=True, keep=True)
+    np.testing.assert_array_equal(out_lens.numpy(), g['out_lens'])
+    np.testing.assert_allclose(acts['conv1'].numpy(), g['conv1'], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(acts['conv2'].numpy(), g['conv2'], rtol=1e-5, atol=1e-5)
+    for i in range(int(g['layers'])):
+        np.testing.assert_allclose(acts[f'rnn{i}'].numpy(), g[f'rnn{i}'], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(logits.numpy(), g['logits'], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(probs.numpy(), g['probs'], rtol=1e-5, atol=1e-6)
+    for k in g.files:
+        if k.startswith('after_fwd/'):
+            np.testing.assert_allclose(o.sd[k[len('after_fwd/'):]].numpy(), g[k], rtol=1e-5,
+                                       atol=1e-6)
+    strings, _ = orc.greedy_decode(probs, out_lens)
+    assert [s[0] for s in strings] == [str(s) for s in g['decoded']]
+
+
+def test_oracle_train_step_tiny(golden_dir):
+    g = _load(golden_dir, 'tiny_ds2.npz')
+    m = build_model(int(g['seed']), int(g['hidden']), int(g['layers']))
+    o = orc.OracleDS2(m.state_dict(), int(g['layers']), int(g['hidden']))
+    loss, new, bufs, grads, gnorm = orc.train_step(
+        o, torch.from_numpy(g['x']), torch.from_numpy(g['pct']), torch.from_numpy(g['targets']),
+        torch.from_numpy(g['target_sizes']))
+    np.testing.assert_allclose(float(loss), float(g['loss']), rtol=1e-5)
+    np.testing.assert_allclose(float(gnorm), float(g['grad_norm']), rtol=1e-4)
+    for k, v in grads.items():
+        np.testing.assert_allclose(v.numpy(), g['grad/' + k], rtol=1e-4, atol=1e-6, err_msg=k)
+    for k, v in new.items():
+        np.testing.assert_allclose(v.numpy(), g['after_step/' + k], rtol=1e-6, atol=1e-7, err_msg=k)
+
+
+def test_oracle_cfg1(golden_dir):
+    g = _load(golden_dir, 'cfg1_ds2.npz')
+    spect = orc.spectrogram(g['wav'])
+    np.testing.assert_allclose(spect.numpy(), g['spect'], rtol=0, atol=0)
+    m = build_model(int(g['seed']), 256, 2)
+    m.eval()
+    o = orc.OracleDS2(m.state_dict(), 2, 256)
+    x = spect.view(1, 1, spect.size(0), spect.size(1))
+    with torch.no_grad():
+        logits, probs, out_lens, _ = o.forward(x, torch.IntTensor([spect.size(1)]), training=False)
+    np.testing.assert_allclose(logits.numpy(), g['logits'], rtol=1e-5, atol=1e-5)
+    strings, offsets = orc.greedy_decode(probs, out_lens)
+    assert strings[0][0] == str(g['decoded'][0])
+    np.testing.assert_array_equal(offsets[0][0].numpy(), g['offsets'])
+
+
+def test_oracle_greedy_known_answers(golden_dir):
+    g = _load(golden_dir, 'greedy_decoder.npz')
+    strings, offsets = orc.greedy_decode(torch.from_numpy(g['probs']), g['sizes'].tolist())
+    assert [s[0] for s in strings] == [str(s) for s in g['strings']]
+    for i, o in enumerate(offsets):
+        np.testing.assert_array_equal(o[0].numpy(), g['offsets'][i][:int(g['counts'][i])])
+    hs, ho = orc.greedy_decode(torch.from_numpy(g['hand_probs']), [6])
+    assert hs[0][0] == 'AA ' == str(g['hand_string'][0])
+    np.testing.assert_array_equal(ho[0][0].numpy(), [1, 4, 5])
+
+
+def test_seq_lens_and_input_size_quirk(golden_dir):
+    g = _load(golden_dir, 'seq_lens.npz')
+    out = orc.get_seq_lens(torch.from_numpy(g['lengths']))
+    np.testing.assert_array_equal(out.numpy(), g['seq_lens'])
+    m = build_model(0, 8, 1)
+    np.testing.assert_array_equal(m.get_seq_lens(torch.from_numpy(g['lengths'])).numpy(),
+                                  g['seq_lens'])
+    tmax = int(g['tmax'])
+    pct = torch.FloatTensor([l / float(tmax) for l in range(1, tmax + 1)])
+    np.testing.assert_array_equal(orc.input_sizes_quirk(pct, tmax).numpy(), g['pct_sizes'])
+    # the survey's lossy lengths
+    lossy = {127: 126, 254: 253, 255: 254, 508: 507, 510: 509}
+    for k, v in lossy.items():
+        assert int(g['pct_sizes'][k - 1]) == v
+
+
+def test_ctc_oracle_hand_case():
+    # T=2, C=2 (blank 0, 'a' 1), label 'a': paths "a_", "_a", "aa"
+    acts = torch.log(torch.tensor([[[0.4, 0.6]], [[0.7, 0.3]]]))   # softmax == these probs
+    loss, grad = orc.ctc_loss(acts, torch.IntTensor([1]), torch.IntTensor([2]),
+                              torch.IntTensor([1]))
+    p = 0.6 * 0.7 + 0.4 * 0.3 + 0.6 * 0.3
+    assert abs(float(loss) + np.log(p)) < 1e-6
+    # posterior of 'a' at t=0: (0.6*0.7 + 0.6*0.3)/p ; grad = y - posterior
+    post_a0 = (0.6 * 0.7 + 0.6 * 0.3) / p
+    assert abs(float(grad[0, 0, 1]) - (0.6 - post_a0)) < 1e-6
+
+
+def test_stft_oracle_known_answers():
+    sr, n = 16000, 16000
+    t = np.arange(n) / sr
+    k = 40                              # bin 40 = 2000 Hz (bins are 50 Hz apart)
+    y = np.cos(2 * np.pi * k * 50 * t).astype(np.float32)
+    mag = orc.stft_magnitude(y)
+    assert mag.shape == (161, 101)
+    w = orc.hamming(320)
+    # interior frame: |X_k| = sum(w)/2 for a unit cosine exactly on bin k
+    np.testing.assert_allclose(mag[k, 50], w.sum() / 2, rtol=1e-4)
+    assert mag[:, 50].argmax() == k
+    assert np.all(orc.stft_magnitude(np.zeros(3200, np.float32)) == 0)
+    dc = orc.stft_magnitude(np.ones(3200, np.float32))
+    np.testing.assert_allclose(dc[0, 5], w.sum(), rtol=1e-6)
+
+
+def test_hamming_matches_scipy():
+    from scipy.signal import windows
+    np.testing.assert_allclose(orc.hamming(320), windows.hamming(320, sym=True), rtol=0, atol=1e-15)
