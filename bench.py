@@ -1,0 +1,215 @@
+#!/usr/bin/env python
+"""DS2 training throughput on MI355X: audio-seconds/sec, 5xBiGRU-800, 32 x 10 s per GPU.
+
+python bench.py [--gpus N --steps K --warmup W]          (N=1: plain process)
+python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+
+One step = the reference's train_batch (train.py:555-632) on the HIP path:
+forward (conv/BN/5 BiGRU/FC/softmax), greedy decode, CTC (+grad), backward,
+bucketed RCCL gradient all-reduce overlapped with backward (N > 1), clip 100 +
+SGD-Nesterov.  Synthetic 10 s spectrograms [32, 1, 161, 1001] resident in HBM,
+random-init weights (seed 123456), 150-label targets.  Weak scaling: 32
+utterances per GPU.  Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "deepspeech.pytorch_amd"))
+sys.path.insert(0, REPO)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+LABELS = "_'ABCDEFGHIJKLMNOPQRSTUVWXYZ2 "
+CONF = dict(sample_rate=16000, window_size=0.02, window_stride=0.01, window='hamming')
+BATCH, T_FRAMES, SECONDS, HIDDEN, LAYERS, LABEL_LEN = 32, 1001, 10.0, 800, 5, 150
+# fp32 algorithmic work per training step at this shape (BASELINE.md §3 / SURVEY §8d)
+TRAIN_FLOP_PER_STEP = 4.940e12
+PEAK_F32_MFMA_TFLOPS = 157.3     # MI355X dense fp32 (MI355X_MICROARCH.md)
+
+
+def synthetic_batch(rank: int):
+    g = torch.Generator().manual_seed(1234 + rank)
+    x = torch.randn(BATCH, 1, 161, T_FRAMES, generator=g)
+    tg = []
+    for _ in range(BATCH):
+        prev = -1
+        for _ in range(LABEL_LEN):
+            v = int(torch.randint(1, 29, (1,), generator=g))
+            while v == prev:
+                v = int(torch.randint(1, 29, (1,), generator=g))
+            tg.append(v)
+            prev = v
+    targets = torch.tensor(tg, dtype=torch.int32)
+    target_sizes = torch.full((BATCH,), LABEL_LEN, dtype=torch.int32)
+    pct = torch.ones(BATCH)
+    return x, targets, pct, target_sizes
+
+
+class KernelProbe:
+    """Brackets every launch of one C-ABI entry point with HIP events on the stream the
+    kernel runs on (torch's current stream), to time it live inside the bench."""
+
+    def __init__(self, name, flop_fn):
+        self.name = name
+        self.flop_fn = flop_fn
+        self.events = []
+        self.flops = []
+        self.active = False
+
+    def install(self):
+        from ds2amd import _lib
+        orig = _lib.call
+        probe = self
+
+        def call(name, *args):
+            if probe.active and name == probe.name:
+                s = torch.cuda.Event(enable_timing=True)
+                e = torch.cuda.Event(enable_timing=True)
+                s.record()
+                orig(name, *args)
+                e.record()
+                probe.events.append((s, e))
+                probe.flops.append(probe.flop_fn(args))
+            else:
+                orig(name, *args)
+        _lib.call = call
+
+    def summary(self):
+        torch.cuda.synchronize()
+        if not self.events:
+            return None
+        ms = [s.elapsed_time(e) for s, e in self.events]
+        return sum(ms) / len(ms), sum(self.flops) / len(self.flops), len(ms)
+
+
+def sgemm_flops(args):
+    m, n, k = args[2], args[3], args[4]
+    return 2.0 * m * n * k
+
+
+def cpu_baseline(seconds_budget: float = 20.0):
+    """The oracle (stock torch CPU ops, the reference's op set) on the host cores: one
+    bounded train step of the same architecture on 2 x 10 s utterances."""
+    from oracle import ds2_oracle as orc
+    from ds2amd import model as dsm
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    torch.manual_seed(123456)
+    m = dsm.DeepSpeech(rnn_type='gru', labels=LABELS, rnn_hidden_size=HIDDEN, nb_layers=LAYERS,
+                       audio_conf=CONF, bidirectional=True)
+    o = orc.OracleDS2({k: v.detach() for k, v in m.state_dict().items()}, LAYERS, HIDDEN)
+    nb = 4
+    x, tg, pct, ts = synthetic_batch(0)
+    x, pct, ts = x[:nb], pct[:nb], ts[:nb]
+    tg = tg[:nb * LABEL_LEN]
+    t0 = time.perf_counter()
+    orc.train_step(o, x, pct.clone(), tg, ts)
+    dt = time.perf_counter() - t0
+    return {"value": round(nb * SECONDS / dt, 4), "unit": "audio-seconds/sec",
+            "cores": threads, "kind": "port",
+            "sample": f"1 oracle train step (fwd+CTC+bwd+clip+SGD), 5xBiGRU-800, {nb} x 10 s "
+                      f"utterances, torch CPU fp32, {dt:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--probe", default="ds2_sgemm")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+
+    from ds2amd import model as dsm
+    from ds2amd.trainer import Trainer
+
+    torch.manual_seed(123456)
+    m = dsm.DeepSpeech(rnn_type='gru', labels=LABELS, rnn_hidden_size=HIDDEN, nb_layers=LAYERS,
+                       audio_conf=CONF, bidirectional=True)
+    tr = Trainer(m, LABELS, lr=3e-4, momentum=0.9, max_norm=100.0, device=dev)
+    x, tg, pct, ts = synthetic_batch(rank)
+    x = x.to(dev)                                      # inputs resident in HBM
+
+    probe = KernelProbe(args.probe, sgemm_flops)
+    probe.install()
+
+    def step():
+        return tr.train_batch((x, tg, None, pct.clone(), ts))
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    probe.active = True
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    probe.active = False
+    if world > 1:
+        tt = torch.tensor([dt], device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    final_loss = float(loss.item())
+    pk = probe.summary()
+
+    if rank == 0:
+        audio = world * BATCH * SECONDS * args.steps
+        value = audio / dt
+        ms_per_step = dt * 1000.0 / args.steps
+        roof = None
+        if pk is not None:
+            avg_ms, flop, count = pk
+            achieved = flop / (avg_ms * 1e-3) / 1e12
+            roof = {"bound": "mfma", "kernel": args.probe, "launches": count,
+                    "avg_launch_ms": round(avg_ms, 5), "achieved": round(achieved, 3),
+                    "peak": PEAK_F32_MFMA_TFLOPS, "unit": "TFLOP/s",
+                    "frac": round(achieved / PEAK_F32_MFMA_TFLOPS, 4), "traffic": None,
+                    "step_achieved_tflops": round(TRAIN_FLOP_PER_STEP / (ms_per_step * 1e-3) / 1e12, 3)}
+        cpu = None
+        if not args.no_cpu_baseline and world == 1:
+            cpu = cpu_baseline()
+        out = {
+            "metric": "audio-seconds/sec training, DS2 5x BiGRU-800 bs32, at 1/2/4/8 MI355X",
+            "value": round(value, 2), "unit": "audio-seconds/sec", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic 10 s spectrograms [32,1,161,1001] + 150-label targets, random init",
+            "config": {"workload": "DS2 5x BiGRU-800, 10 s utterances, batch 32 per GPU, "
+                                   "CTC training step (cfg2/cfg3)",
+                       "global_batch": BATCH * world, "seq_len": T_FRAMES,
+                       "parallelism": f"dp{world}"},
+            "loss": round(final_loss, 4),
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -328,7 +328,7 @@ class GRULayerFn(torch.autograd.Function):
             sgemm(x2d, w_ih, xproj, m=t * n, n=h3, k=inp, trans_b=True, lda=inp, ldb=inp,
                   ldc=nd * h3, bias=b_ih, c_off=d * h3)
         h_all = torch.empty(t, n, nd, h, device=dev, dtype=_F32)
-        need_grad = torch.is_grad_enabled() and any(ctx.needs_input_grad)
+        need_grad = any(ctx.needs_input_grad)   # forward() itself runs under no_grad
         gates = torch.empty(t, n, nd, 4 * h, device=dev, dtype=_F32) if need_grad else None
         w_hh_f, b_hh_f = weights[1], weights[3]
         w_hh_r = weights[5] if nd == 2 else None

@@ -117,30 +117,22 @@ class GradAllReducer:
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         cap = int(bucket_mb * 1024 * 1024 / 4)
-        self.buckets = []          # (start, end) element ranges
+        self.buckets = []          # (start, end, n_params) element ranges
         self.param_bucket = {}
-        start = 0
-        cur_end = 0
-        members = []
-        for p, o, n in flat.slices():
+        start, members = 0, []
+        plist = list(flat.slices())
+        for i, (p, o, n) in enumerate(plist):
             members.append(p)
-            cur_end = o + n
-            if cur_end - start >= cap:
-                self._close(start, cur_end, members)
-                start, members = self._next_start(flat, p), []
-        if members:
-            self._close(start, flat.numel, members)
+            nxt = plist[i + 1][1] if i + 1 < len(plist) else flat.numel
+            if nxt - start >= cap or i + 1 == len(plist):
+                self._close(start, nxt, members)
+                start, members = nxt, []
         self.pending = [0] * len(self.buckets)
         self.handles = [None] * len(self.buckets)
         self._hooks = []
         if self.world > 1:
             for p in flat.params:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._on_ready))
-
-    @staticmethod
-    def _next_start(flat, p):
-        i = flat.params.index(p)
-        return flat.offsets[i + 1] if i + 1 < len(flat.params) else flat.numel
 
     def _close(self, start, end, members):
         b = len(self.buckets)
