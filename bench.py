@@ -124,7 +124,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--probe", default="ds2_sgemm")
+    ap.add_argument("--probe", default="ds2_sgemm_ws")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))

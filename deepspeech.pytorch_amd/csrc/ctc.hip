@@ -17,160 +17,194 @@
 
 namespace ds2 {
 
-constexpr int kCtcThreads = 256;
-constexpr int kCtcMaxS = 2 * 1024 + 1;  // max label length 1024
-
-struct CtcWs {
-  float* lp;      // [n][t_max][c]
-  float* alpha;   // [n][t_max][s_max]
-  int s_max;
-};
+constexpr int kScanThreads = 512;
+constexpr int kMaxLabel = 1024;
+constexpr int kCtcMaxS = 2 * kMaxLabel + 1;
 
 __device__ __forceinline__ int label_at(const int* lab, int s, int blank) {
   return (s & 1) ? lab[s >> 1] : blank;
 }
 
-__global__ __launch_bounds__(kCtcThreads) void ctc_kernel(
-    const float* __restrict__ acts, int t_max, int n, int c, const int* __restrict__ labels,
-    const int* __restrict__ label_lens, const int* __restrict__ act_lens, int blank,
-    int zero_infinity, float* __restrict__ costs, float* __restrict__ grads,
-    float* __restrict__ lp_ws, float* __restrict__ alpha_ws, int s_max) {
-  const int b = blockIdx.x;
-  const int tid = threadIdx.x;
-  __shared__ float row_a[kCtcMaxS];
-  __shared__ float row_b[kCtcMaxS];
-  __shared__ int lab_s[1024];
-  __shared__ int cls_count[64];
-  __shared__ int cls_start[65];
-  __shared__ int cls_states[kCtcMaxS];
-  __shared__ float nll_s;
+struct CtcWs {
+  float* lp;         // [n][t_max][c]       log-softmax
+  float* alpha;      // [n][t_max][s_max]
+  float* beta;       // [n][t_max][s_max]
+  float* nll;        // [n]
+  int* offs;         // [n]                 label offsets
+  int* cls_start;    // [n][65]             per-class start into cls_pos
+  int* cls_pos;      // [n][max_label_len]  label positions grouped by class
+};
 
+// 1) log-softmax of every (t, n) row, one wave per row (C <= 64)
+__global__ void ctc_logsoftmax_kernel(const float* __restrict__ acts, int t_max, int n, int c,
+                                      float* __restrict__ lp) {
+  const int row = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;   // row = t*n + b
+  const int lane = threadIdx.x & 63;
+  if (row >= t_max * n) return;
+  const int t = row / n;
+  const int b = row - t * n;
+  const float v = lane < c ? acts[(int64_t)row * c + lane] : -INFINITY;
+  const float m = wave_max(v);
+  const float e = lane < c ? expf(v - m) : 0.f;
+  const float lse = m + logf(wave_sum(e));
+  if (lane < c) lp[((int64_t)b * t_max + t) * c + lane] = v - lse;
+}
+
+// 2) per utterance: label offset and the class -> label-position lists
+__global__ void ctc_prep_kernel(const int* __restrict__ labels, const int* __restrict__ label_lens,
+                                int n, int c, int max_l, int* __restrict__ offs,
+                                int* __restrict__ cls_start, int* __restrict__ cls_pos) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= n) return;
   int off = 0;
   for (int i = 0; i < b; ++i) off += label_lens[i];
+  offs[b] = off;
+  const int L = label_lens[b];
+  const int* lab = labels + off;
+  int* cs = cls_start + b * 65;
+  int* cp = cls_pos + (int64_t)b * max_l;
+  for (int k = 0; k <= c; ++k) cs[k] = 0;
+  for (int i = 0; i < L; ++i) cs[lab[i] + 1]++;
+  for (int k = 0; k < c; ++k) cs[k + 1] += cs[k];
+  int fill[64];
+  for (int k = 0; k < c; ++k) fill[k] = cs[k];
+  for (int i = 0; i < L; ++i) cp[fill[lab[i]]++] = i;
+}
+
+// 3) alpha (blockIdx.y == 0) and beta (blockIdx.y == 1) scans run concurrently,
+//    one workgroup each per utterance; one LDS row per time step.
+__global__ __launch_bounds__(kScanThreads) void ctc_scan_kernel(
+    const float* __restrict__ lp_all, int t_max, int c, const int* __restrict__ labels,
+    const int* __restrict__ label_lens, const int* __restrict__ act_lens,
+    const int* __restrict__ offs, int blank, int s_max, float* __restrict__ alpha_all,
+    float* __restrict__ beta_all, float* __restrict__ nll_out) {
+  __shared__ float rows[2][kCtcMaxS];
+  __shared__ int lab_s[kMaxLabel];
+  const int b = blockIdx.x;
+  const bool is_beta = blockIdx.y == 1;
+  const int tid = threadIdx.x;
   const int L = label_lens[b];
   int T = act_lens[b];
-  if (T > t_max) T = t_max;
-  if (T < 0) T = 0;
+  T = T > t_max ? t_max : (T < 0 ? 0 : T);
   const int S = 2 * L + 1;
-  const int* lab_g = labels + off;
-  for (int i = tid; i < L; i += blockDim.x) lab_s[i] = lab_g[i];
-  if (tid < 64) cls_count[tid] = 0;
+  for (int i = tid; i < L; i += blockDim.x) lab_s[i] = labels[offs[b] + i];
   __syncthreads();
-
-  // class -> state lists (deterministic order: by state index)
-  if (tid == 0) {
-    for (int s = 0; s < S; ++s) cls_count[label_at(lab_s, s, blank)]++;
-    int acc = 0;
-    for (int k = 0; k < c; ++k) {
-      cls_start[k] = acc;
-      acc += cls_count[k];
-    }
-    cls_start[c] = acc;
-    for (int k = 0; k < c; ++k) cls_count[k] = 0;
-    for (int s = 0; s < S; ++s) {
-      int k = label_at(lab_s, s, blank);
-      cls_states[cls_start[k] + cls_count[k]++] = s;
-    }
-  }
-
-  float* lp = lp_ws + (int64_t)b * t_max * c;
-  float* alpha = alpha_ws + (int64_t)b * t_max * s_max;
-
-  // log-softmax of every valid frame (one thread per frame, C is small).
-  for (int t = tid; t < T; t += blockDim.x) {
-    const float* a = acts + ((int64_t)t * n + b) * c;
-    float m = -INFINITY;
-    for (int k = 0; k < c; ++k) m = fmaxf(m, a[k]);
-    float sum = 0.f;
-    for (int k = 0; k < c; ++k) sum += expf(a[k] - m);
-    float lse = m + logf(sum);
-    for (int k = 0; k < c; ++k) lp[(int64_t)t * c + k] = a[k] - lse;
-  }
-  __syncthreads();
-
-  // ---- alpha -------------------------------------------------------------
-  float* cur = row_a;
-  float* prv = row_b;
-  if (T > 0) {
-    for (int s = tid; s < S; s += blockDim.x) {
-      float v = -INFINITY;
-      if (s == 0) v = lp[blank];
-      else if (s == 1) v = lp[label_at(lab_s, 1, blank)];
-      cur[s] = v;
-      alpha[s] = v;
-    }
-  }
-  __syncthreads();
-  for (int t = 1; t < T; ++t) {
-    float* tmp = prv; prv = cur; cur = tmp;
-    const float* lpt = lp + (int64_t)t * c;
-    for (int s = tid; s < S; s += blockDim.x) {
-      const int ls = label_at(lab_s, s, blank);
-      float v = prv[s];
-      if (s >= 1) v = log_add(v, prv[s - 1]);
-      if (s >= 2 && ls != blank && ls != label_at(lab_s, s - 2, blank)) v = log_add(v, prv[s - 2]);
-      v = (v == -INFINITY) ? -INFINITY : v + lpt[ls];
-      cur[s] = v;
-      alpha[(int64_t)t * s_max + s] = v;
-    }
-    __syncthreads();
-  }
-  if (tid == 0) {
-    float ll;
-    if (T == 0) ll = (L == 0) ? 0.f : -INFINITY;
-    else {
-      ll = cur[S - 1];
-      if (S >= 2) ll = log_add(ll, cur[S - 2]);
-    }
-    nll_s = -ll;
-  }
-  __syncthreads();
-  const float nll = nll_s;
-  const bool feasible = (nll != INFINITY) && (nll == nll);
-  if (tid == 0) costs[b] = feasible ? nll : (zero_infinity ? 0.f : INFINITY);
-
-  if (grads == nullptr) return;
-  // zero rows outside [0, T) and every row of an infeasible utterance
-  for (int i = tid; i < t_max * c; i += blockDim.x) {
-    const int t = i / c;
-    if (t >= T || !feasible) grads[((int64_t)t * n + b) * c + (i - t * c)] = 0.f;
-  }
-  if (!feasible || T == 0) return;
-
-  // ---- beta + gradient ---------------------------------------------------
-  // reuse row_a/row_b as beta rows; e = exp(alpha + beta + nll) per state.
-  float* bcur = row_a;
-  float* bprv = row_b;
-  for (int t = T - 1; t >= 0; --t) {
-    const float* lpt = lp + (int64_t)t * c;
-    for (int s = tid; s < S; s += blockDim.x) {
-      const int ls = label_at(lab_s, s, blank);
-      float v;
-      if (t == T - 1) {
-        v = (s == S - 1 || s == S - 2) ? lpt[ls] : -INFINITY;
-      } else {
-        v = bprv[s];
-        if (s + 1 < S) v = log_add(v, bprv[s + 1]);
-        if (s + 2 < S && ls != blank && ls != label_at(lab_s, s + 2, blank))
-          v = log_add(v, bprv[s + 2]);
-        v = (v == -INFINITY) ? -INFINITY : v + lpt[ls];
+  const float* lp = lp_all + (int64_t)b * t_max * c;
+  float* out = (is_beta ? beta_all : alpha_all) + (int64_t)b * t_max * s_max;
+  int cur = 0;
+  if (!is_beta) {
+    for (int t = 0; t < T; ++t) {
+      const float* lpt = lp + (int64_t)t * c;
+      const float* prv = rows[cur ^ 1];
+      for (int s = tid; s < S; s += blockDim.x) {
+        const int ls = label_at(lab_s, s, blank);
+        float v;
+        if (t == 0) {
+          v = (s <= 1) ? lpt[ls] : -INFINITY;
+        } else {
+          v = prv[s];
+          if (s >= 1) v = log_add(v, prv[s - 1]);
+          if (s >= 2 && ls != blank && ls != label_at(lab_s, s - 2, blank))
+            v = log_add(v, prv[s - 2]);
+          v = (v == -INFINITY) ? -INFINITY : v + lpt[ls];
+        }
+        rows[cur][s] = v;
+        out[(int64_t)t * s_max + s] = v;
       }
-      bcur[s] = v;
+      __syncthreads();
+      cur ^= 1;
     }
-    __syncthreads();
-    // gradient row t: thread k < c walks the states of class k
-    for (int k = tid; k < c; k += blockDim.x) {
-      const float lpk = lpt[k];
-      float acc = 0.f;
-      for (int i = cls_start[k]; i < cls_start[k + 1]; ++i) {
-        const int s = cls_states[i];
-        const float ab = alpha[(int64_t)t * s_max + s] + bcur[s];
+    if (tid == 0) {
+      float ll;
+      if (T == 0) {
+        ll = (L == 0) ? 0.f : -INFINITY;
+      } else {
+        const float* last = rows[cur ^ 1];
+        ll = last[S - 1];
+        if (S >= 2) ll = log_add(ll, last[S - 2]);
+      }
+      nll_out[b] = -ll;
+    }
+  } else {
+    for (int t = T - 1; t >= 0; --t) {
+      const float* lpt = lp + (int64_t)t * c;
+      const float* prv = rows[cur ^ 1];
+      for (int s = tid; s < S; s += blockDim.x) {
+        const int ls = label_at(lab_s, s, blank);
+        float v;
+        if (t == T - 1) {
+          v = (s >= S - 2) ? lpt[ls] : -INFINITY;
+        } else {
+          v = prv[s];
+          if (s + 1 < S) v = log_add(v, prv[s + 1]);
+          if (s + 2 < S && ls != blank && ls != label_at(lab_s, s + 2, blank))
+            v = log_add(v, prv[s + 2]);
+          v = (v == -INFINITY) ? -INFINITY : v + lpt[ls];
+        }
+        rows[cur][s] = v;
+        out[(int64_t)t * s_max + s] = v;
+      }
+      __syncthreads();
+      cur ^= 1;
+    }
+  }
+}
+
+// 4) gradient rows, one wave per (t, n):
+//    grad[t][n][k] = exp(lp_k) - sum_{s: l'_s = k} exp(alpha_t(s) + beta_t(s) + nll - lp_k)
+//    blank states summed by the whole wave, label classes by lane k over its list.
+__global__ void ctc_grad_kernel(int t_max, int n, int c, int blank, int zero_infinity,
+                                const int* __restrict__ act_lens, const int* __restrict__ label_lens,
+                                const float* __restrict__ lp_all, const float* __restrict__ alpha_all,
+                                const float* __restrict__ beta_all, const float* __restrict__ nll_all,
+                                const int* __restrict__ cls_start, const int* __restrict__ cls_pos,
+                                int s_max, int max_l, float* __restrict__ costs,
+                                float* __restrict__ grads) {
+  const int row = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;   // row = t*n + b
+  const int lane = threadIdx.x & 63;
+  if (row >= t_max * n) return;
+  const int t = row / n;
+  const int b = row - t * n;
+  int T = act_lens[b];
+  T = T > t_max ? t_max : (T < 0 ? 0 : T);
+  const float nll = nll_all[b];
+  const bool feasible = (nll != INFINITY) && (nll == nll);
+  if (t == 0 && lane == 0 && costs != nullptr)
+    costs[b] = feasible ? nll : (zero_infinity ? 0.f : INFINITY);
+  if (grads == nullptr) return;
+  float* g = grads + (int64_t)row * c;
+  if (t >= T || !feasible) {
+    if (lane < c) g[lane] = 0.f;
+    return;
+  }
+  const int L = label_lens[b];
+  const int S = 2 * L + 1;
+  const float* lpt = lp_all + ((int64_t)b * t_max + t) * c;
+  const float* al = alpha_all + ((int64_t)b * t_max + t) * s_max;
+  const float* be = beta_all + ((int64_t)b * t_max + t) * s_max;
+  const float lpb = lpt[blank];
+  float accb = 0.f;
+  for (int s = 2 * lane; s < S; s += 128) {
+    const float ab = al[s] + be[s];
+    if (ab != -INFINITY) accb += expf(ab + nll - lpb);
+  }
+  accb = wave_sum(accb);
+  if (lane < c) {
+    const float lpk = lpt[lane];
+    float acc;
+    if (lane == blank) {
+      acc = accb;
+    } else {
+      acc = 0.f;
+      const int* cs = cls_start + b * 65;
+      const int* cp = cls_pos + (int64_t)b * max_l;
+      for (int i = cs[lane]; i < cs[lane + 1]; ++i) {
+        const int s = 2 * cp[i] + 1;
+        const float ab = al[s] + be[s];
         if (ab != -INFINITY) acc += expf(ab + nll - lpk);
       }
-      grads[((int64_t)t * n + b) * c + k] = expf(lpk) - acc;
     }
-    __syncthreads();
-    float* tmp = bprv; bprv = bcur; bcur = tmp;
+    g[lane] = expf(lpk) - acc;
   }
 }
 
@@ -227,10 +261,15 @@ using namespace ds2;
 
 extern "C" {
 
+static inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
+
 size_t ds2_ctc_workspace_size(int t_max, int n, int max_label_len) {
-  const int64_t s_max = 2 * (int64_t)max_label_len + 1;
-  // lp uses c <= 64 classes; size for 64 to keep the query independent of c.
-  return (size_t)n * t_max * 64 * sizeof(float) + (size_t)n * t_max * s_max * sizeof(float) + 256;
+  const size_t s_max = 2 * (size_t)max_label_len + 1;
+  const size_t ml = max_label_len > 0 ? max_label_len : 1;
+  return al256((size_t)n * t_max * 64 * sizeof(float)) +
+         2 * al256((size_t)n * t_max * s_max * sizeof(float)) + al256((size_t)n * sizeof(float)) +
+         al256((size_t)n * sizeof(int)) + al256((size_t)n * 65 * sizeof(int)) +
+         al256((size_t)n * ml * sizeof(int)) + 256;
 }
 
 ds2_status_t ds2_ctc_loss(const float* acts, int t_max, int n, int c, const int* labels,
@@ -238,16 +277,32 @@ ds2_status_t ds2_ctc_loss(const float* acts, int t_max, int n, int c, const int*
                           int blank, int zero_infinity, float* costs, float* grads, void* ws,
                           size_t ws_bytes, ds2_stream_t stream) {
   if (t_max < 0 || n < 0 || c < 1 || c > 64 || blank < 0 || blank >= c) return DS2_INVALID_VALUE;
-  if (max_label_len < 0 || max_label_len > 1024) return DS2_UNSUPPORTED_SHAPE;
+  if (max_label_len < 0 || max_label_len > kMaxLabel) return DS2_UNSUPPORTED_SHAPE;
   if (n == 0) return DS2_OK;
   if (ws == nullptr || ws_bytes < ds2_ctc_workspace_size(t_max, n, max_label_len))
     return DS2_WORKSPACE_TOO_SMALL;
+  hipStream_t st = as_stream(stream);
   const int s_max = 2 * max_label_len + 1;
-  float* lp = static_cast<float*>(ws);
-  float* alpha = lp + (size_t)n * t_max * 64;
-  hipLaunchKernelGGL(ctc_kernel, dim3(n), dim3(kCtcThreads), 0, as_stream(stream), acts, t_max,
-                     n, c, labels, label_lens, act_lens, blank, zero_infinity, costs, grads, lp,
-                     alpha, s_max);
+  const int ml = max_label_len > 0 ? max_label_len : 1;
+  char* p = static_cast<char*>(ws);
+  float* lp = reinterpret_cast<float*>(p); p += al256((size_t)n * t_max * 64 * sizeof(float));
+  float* alpha = reinterpret_cast<float*>(p); p += al256((size_t)n * t_max * s_max * sizeof(float));
+  float* beta = reinterpret_cast<float*>(p); p += al256((size_t)n * t_max * s_max * sizeof(float));
+  float* nll = reinterpret_cast<float*>(p); p += al256((size_t)n * sizeof(float));
+  int* offs = reinterpret_cast<int*>(p); p += al256((size_t)n * sizeof(int));
+  int* cls_start = reinterpret_cast<int*>(p); p += al256((size_t)n * 65 * sizeof(int));
+  int* cls_pos = reinterpret_cast<int*>(p);
+  const int rows = t_max * n;
+  if (rows > 0)
+    hipLaunchKernelGGL(ctc_logsoftmax_kernel, dim3(cdiv(rows, 4)), dim3(256), 0, st, acts, t_max,
+                       n, c, lp);
+  hipLaunchKernelGGL(ctc_prep_kernel, dim3(cdiv(n, 64)), dim3(64), 0, st, labels, label_lens, n, c,
+                     ml, offs, cls_start, cls_pos);
+  hipLaunchKernelGGL(ctc_scan_kernel, dim3(n, 2), dim3(kScanThreads), 0, st, lp, t_max, c, labels,
+                     label_lens, act_lens, offs, blank, s_max, alpha, beta, nll);
+  hipLaunchKernelGGL(ctc_grad_kernel, dim3(cdiv(rows > 0 ? rows : 1, 4)), dim3(256), 0, st, t_max,
+                     n, c, blank, zero_infinity, act_lens, label_lens, lp, alpha, beta, nll,
+                     cls_start, cls_pos, s_max, ml, costs, grads);
   return launch_status("ds2_ctc_loss");
 }
 

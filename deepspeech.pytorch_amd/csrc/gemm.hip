@@ -11,6 +11,8 @@
 // (+2 floats) makes those 8 ds_write_b32 per thread conflict-free.
 #include "common.h"
 
+#include <algorithm>
+
 namespace ds2 {
 
 constexpr int BM = 128, BN = 128, BK = 16;
@@ -90,7 +92,8 @@ template <int TA, int TB, bool VA, bool VB>
 __global__ __launch_bounds__(256) void sgemm_kernel(
     int M, int N, int K, float alpha, const float* __restrict__ A, int64_t lda, int64_t sA,
     const float* __restrict__ B, int64_t ldb, int64_t sB, float beta, float* __restrict__ C,
-    int64_t ldc, int64_t sC, const float* __restrict__ bias) {
+    int64_t ldc, int64_t sC, const float* __restrict__ bias, int nsplit, int kchunk,
+    float* __restrict__ partial) {
   // op(A) is k-contiguous when TA == 0 ([m][k] storage); op(B) is k-contiguous
   // when TB == 1 ([n][k] storage).
   constexpr bool AK = (TA == 0);
@@ -100,10 +103,14 @@ __global__ __launch_bounds__(256) void sgemm_kernel(
   __shared__ __attribute__((aligned(16))) float As[2][BK * LDA_S];
   __shared__ __attribute__((aligned(16))) float Bs[2][BK * LDB_S];
 
-  const int bz = blockIdx.z;
+  // blockIdx.z = batch * nsplit + split; split-K partials go to partial[z][m][n]
+  const int bz = blockIdx.z / nsplit;
+  const int sp = blockIdx.z - bz * nsplit;
   A += bz * sA;
   B += bz * sB;
   C += bz * sC;
+  const int kbeg = sp * kchunk;
+  const int kend = min(K, kbeg + kchunk);
   const int m0 = blockIdx.y * BM;
   const int n0 = blockIdx.x * BN;
   const int lane = threadIdx.x & 63;
@@ -120,9 +127,9 @@ __global__ __launch_bounds__(256) void sgemm_kernel(
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   float ra[8], rb[8];
-  const int ktiles = (K + BK - 1) / BK;
-  load_tile<AK, VA>(A, lda, M, K, m0, 0, ra);
-  load_tile<BKc, VB>(B, ldb, N, K, n0, 0, rb);
+  const int ktiles = (kend - kbeg + BK - 1) / BK;
+  load_tile<AK, VA>(A, lda, M, kend, m0, kbeg, ra);
+  load_tile<BKc, VB>(B, ldb, N, kend, n0, kbeg, rb);
   store_tile<AK>(As[0], ra);
   store_tile<BKc>(Bs[0], rb);
   __syncthreads();
@@ -133,8 +140,8 @@ __global__ __launch_bounds__(256) void sgemm_kernel(
     const int cur = kt & 1;
     const bool more = (kt + 1) < ktiles;
     if (more) {
-      load_tile<AK, VA>(A, lda, M, K, m0, (kt + 1) * BK, ra);
-      load_tile<BKc, VB>(B, ldb, N, K, n0, (kt + 1) * BK, rb);
+      load_tile<AK, VA>(A, lda, M, kend, m0, kbeg + (kt + 1) * BK, ra);
+      load_tile<BKc, VB>(B, ldb, N, kend, n0, kbeg + (kt + 1) * BK, rb);
     }
     const float* as = As[cur];
     const float* bs = Bs[cur];
@@ -164,6 +171,15 @@ __global__ __launch_bounds__(256) void sgemm_kernel(
     for (int j = 0; j < 2; ++j) {
       const int col = n0 + wn + 32 * j + lr;
       if (col >= N) continue;
+      if (partial != nullptr) {
+        float* pp = partial + (int64_t)blockIdx.z * M * N;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lk;
+          if (row < M) pp[(int64_t)row * N + col] = acc[i][j][r];
+        }
+        continue;
+      }
       const float bv = bias != nullptr ? bias[col] : 0.f;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
@@ -179,14 +195,35 @@ __global__ __launch_bounds__(256) void sgemm_kernel(
   }
 }
 
+// C[b] = alpha * sum_s partial[b*nsplit + s] + beta * C[b] + bias (fixed order)
+__global__ void splitk_reduce_kernel(const float* __restrict__ partial, int M, int N, int nsplit,
+                                     int batch, float alpha, float beta, float* __restrict__ C,
+                                     int64_t ldc, int64_t sC, const float* __restrict__ bias) {
+  const int64_t per = (int64_t)M * N;
+  const int64_t total = per * batch;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int b = static_cast<int>(i / per);
+    const int64_t e = i - b * per;
+    const int row = static_cast<int>(e / N);
+    const int col = static_cast<int>(e - (int64_t)row * N);
+    float acc = 0.f;
+    for (int sp = 0; sp < nsplit; ++sp) acc += partial[((int64_t)b * nsplit + sp) * per + e];
+    float* cp = C + b * sC + (int64_t)row * ldc + col;
+    float v = alpha * acc + (bias != nullptr ? bias[col] : 0.f);
+    if (beta != 0.f) v += beta * *cp;
+    *cp = v;
+  }
+}
+
 template <int TA, int TB>
 static void launch_sgemm_t(bool va, bool vb, dim3 grid, hipStream_t st, int M, int N, int K,
                            float alpha, const float* A, int64_t lda, int64_t sA, const float* B,
                            int64_t ldb, int64_t sB, float beta, float* C, int64_t ldc,
-                           int64_t sC, const float* bias) {
+                           int64_t sC, const float* bias, int nsplit, int kchunk, float* partial) {
 #define DS2_L(VA, VB)                                                                      \
   hipLaunchKernelGGL((sgemm_kernel<TA, TB, VA, VB>), grid, dim3(256), 0, st, M, N, K, alpha, A, \
-                     lda, sA, B, ldb, sB, beta, C, ldc, sC, bias)
+                     lda, sA, B, ldb, sB, beta, C, ldc, sC, bias, nsplit, kchunk, partial)
   if (va && vb) DS2_L(true, true);
   else if (va) DS2_L(true, false);
   else if (vb) DS2_L(false, true);
@@ -200,11 +237,29 @@ static inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t
 
 using namespace ds2;
 
-extern "C" ds2_status_t ds2_sgemm(int trans_a, int trans_b, int m, int n, int k, float alpha,
-                                  const float* a, int64_t lda, int64_t stride_a, const float* b,
-                                  int64_t ldb, int64_t stride_b, float beta, float* c,
-                                  int64_t ldc, int64_t stride_c, int batch, const float* bias,
-                                  ds2_stream_t stream) {
+// Split-K only when the output grid is too small to fill the chip (4 resident
+// 256-thread workgroups per CU x 256 CUs) and K is long: weight gradients such as
+// dW_hh = dG^T h (M = 2400, N = 800, K = T*N = 16032) have only 133 output tiles.
+static int choose_split(int m, int n, int k, int batch) {
+  const int64_t tiles = (int64_t)cdiv(m, BM) * cdiv(n, BN) * batch;
+  if (tiles >= 768 || k < 2048) return 1;
+  int s = static_cast<int>((1024 + tiles - 1) / tiles);
+  s = std::min(s, std::max(1, k / 1024));
+  return std::max(1, std::min(s, 32));
+}
+
+extern "C" size_t ds2_sgemm_workspace_size(int m, int n, int k, int batch) {
+  if (m <= 0 || n <= 0 || k <= 0 || batch <= 0) return 0;
+  const int s = choose_split(m, n, k, batch);
+  return s > 1 ? (size_t)s * batch * m * n * sizeof(float) + 256 : 0;
+}
+
+extern "C" ds2_status_t ds2_sgemm_ws(int trans_a, int trans_b, int m, int n, int k, float alpha,
+                                     const float* a, int64_t lda, int64_t stride_a,
+                                     const float* b, int64_t ldb, int64_t stride_b, float beta,
+                                     float* c, int64_t ldc, int64_t stride_c, int batch,
+                                     const float* bias, void* ws, size_t ws_bytes,
+                                     ds2_stream_t stream) {
   if (m < 0 || n < 0 || k < 0 || batch < 0) return DS2_INVALID_VALUE;
   if (m == 0 || n == 0 || batch == 0) return DS2_OK;
   if (ldc < n) return DS2_INVALID_VALUE;
@@ -216,23 +271,37 @@ extern "C" ds2_status_t ds2_sgemm(int trans_a, int trans_b, int m, int n, int k,
                   (trans_a ? (m % 4 == 0) : (k % 4 == 0));
   const bool vb = aligned16(b) && (ldb % 4 == 0) && (stride_b % 4 == 0) &&
                   (trans_b ? (k % 4 == 0) : (n % 4 == 0));
-  dim3 grid(cdiv(n, BN), cdiv(m, BM), batch);
+  int nsplit = 1;
+  if (ws != nullptr && ws_bytes >= ds2_sgemm_workspace_size(m, n, k, batch))
+    nsplit = choose_split(m, n, k, batch);
+  const int kchunk = nsplit > 1 ? cdiv(cdiv(k, nsplit), BK) * BK : std::max(k, 1);
+  nsplit = nsplit > 1 ? cdiv(k, kchunk) : 1;
+  float* partial = nsplit > 1 ? static_cast<float*>(ws) : nullptr;
+  dim3 grid(cdiv(n, BN), cdiv(m, BM), batch * nsplit);
   hipStream_t st = as_stream(stream);
-  if (k == 0) {
-    // degenerate: C = beta*C + bias; run the kernel with zero k-tiles semantics
-    // via K=0 (loads are fully masked), which still applies the epilogue.
+#define DS2_G(TA_, TB_)                                                                       \
+  launch_sgemm_t<TA_, TB_>(va, vb, grid, st, m, n, k, alpha, a, lda, stride_a, b, ldb, stride_b, \
+                           beta, c, ldc, stride_c, bias, nsplit, kchunk, partial)
+  if (!trans_a && !trans_b) DS2_G(0, 0);
+  else if (!trans_a && trans_b) DS2_G(0, 1);
+  else if (trans_a && !trans_b) DS2_G(1, 0);
+  else DS2_G(1, 1);
+#undef DS2_G
+  if (nsplit > 1) {
+    int64_t total = (int64_t)m * n * batch;
+    int g = cdiv(total, 256);
+    if (g > 2048) g = 2048;
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(g), dim3(256), 0, st, partial, m, n, nsplit,
+                       batch, alpha, beta, c, ldc, stride_c, bias);
   }
-  if (!trans_a && !trans_b)
-    launch_sgemm_t<0, 0>(va, vb, grid, st, m, n, k, alpha, a, lda, stride_a, b, ldb, stride_b,
-                         beta, c, ldc, stride_c, bias);
-  else if (!trans_a && trans_b)
-    launch_sgemm_t<0, 1>(va, vb, grid, st, m, n, k, alpha, a, lda, stride_a, b, ldb, stride_b,
-                         beta, c, ldc, stride_c, bias);
-  else if (trans_a && !trans_b)
-    launch_sgemm_t<1, 0>(va, vb, grid, st, m, n, k, alpha, a, lda, stride_a, b, ldb, stride_b,
-                         beta, c, ldc, stride_c, bias);
-  else
-    launch_sgemm_t<1, 1>(va, vb, grid, st, m, n, k, alpha, a, lda, stride_a, b, ldb, stride_b,
-                         beta, c, ldc, stride_c, bias);
   return launch_status("ds2_sgemm");
+}
+
+extern "C" ds2_status_t ds2_sgemm(int trans_a, int trans_b, int m, int n, int k, float alpha,
+                                  const float* a, int64_t lda, int64_t stride_a, const float* b,
+                                  int64_t ldb, int64_t stride_b, float beta, float* c,
+                                  int64_t ldc, int64_t stride_c, int batch, const float* bias,
+                                  ds2_stream_t stream) {
+  return ds2_sgemm_ws(trans_a, trans_b, m, n, k, alpha, a, lda, stride_a, b, ldb, stride_b, beta,
+                      c, ldc, stride_c, batch, bias, nullptr, 0, stream);
 }

@@ -20,12 +20,16 @@
 //   h' = (h - n) * z + n
 #include "common.h"
 
+#include <algorithm>
+
 namespace ds2 {
 
 constexpr int GU = 16;      // hidden units per workgroup
 constexpr int GB = 16;      // samples per workgroup
-constexpr int GKC = 1024;   // K chunk staged in LDS
-constexpr int GPAD = GKC + 2;
+constexpr int GW = 8;       // waves per workgroup (K split 8 ways)
+constexpr int GT = GW * 64; // threads per workgroup
+constexpr int KC_FWD = 1024;   // max H staged in LDS (forward)
+constexpr int KC_BWD = 2400;   // max 3H chunk staged in LDS (backward)
 
 // Wp[d][ub][ks][g][64]: lane l of k-step ks, gate g ->
 //   W_hh_d[g*H + ub*16 + (l&15)][4*ks + (l>>4)]
@@ -65,11 +69,12 @@ __global__ void pack_bwd_kernel(const float* __restrict__ w_f, const float* __re
   }
 }
 
-// Stage rows [n0, n0+16) x cols [kc0, kc1) of a row-major matrix (row stride
-// ld, valid rows < N) into hs[m][GPAD], zero-filled.  8-byte accesses.
+// Stage rows [n0, n0+16) x cols [kc0, kc1) of a row-major matrix (row stride ld,
+// valid rows < N) into hs[m][pitch], zero-filled.  8-byte accesses.
 __device__ __forceinline__ void stage_rows(const float* __restrict__ src, int64_t ld, int N,
-                                           int n0, int kc0, int kc1, float* __restrict__ hs) {
-  const int width = kc1 - kc0;           // even (H, 3H chunks are multiples of 2 here)
+                                           int n0, int kc0, int kc1, float* __restrict__ hs,
+                                           int pitch) {
+  const int width = kc1 - kc0;
   const int pairs = (width + 1) >> 1;
   for (int i = threadIdx.x; i < GB * pairs; i += blockDim.x) {
     const int m = i / pairs;
@@ -81,73 +86,108 @@ __device__ __forceinline__ void stage_rows(const float* __restrict__ src, int64_
       v.x = p[0];
       v.y = (kp + 1 < width) ? p[1] : 0.f;
     }
-    *reinterpret_cast<float2*>(hs + m * GPAD + kp) = v;
+    *reinterpret_cast<float2*>(hs + m * pitch + kp) = v;
   }
 }
 
+// XCD-aware work mapping: the batch tiles of one (unit block, direction) pair run
+// on the same XCD (blocks b and b+8 share one under the observed round-robin
+// dispatch), and a pair keeps its XCD across the per-step launches, so its W_hh
+// slice stays resident in that XCD's L2.  Speed only, never correctness.
+__device__ __forceinline__ bool map_work(int P, int BT, int UB, int& ub, int& d, int& bt) {
+  const int wg = blockIdx.x;
+  const int xcd = wg & 7;
+  const int slot = wg >> 3;
+  const int pair = xcd + 8 * (slot / BT);
+  bt = slot - (slot / BT) * BT;
+  if (pair >= P) return false;
+  ub = pair % UB;
+  d = pair / UB;
+  return true;
+}
+
+static inline int mapped_grid(int P, int BT) { return 8 * ((P + 7) / 8) * BT; }
+
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void gru_fwd_step_kernel(
-    int s, int T, int N, int H, int D, const float* __restrict__ xproj,
+// forward step.  KSW = k-steps of W prefetched into registers per wave.
+template <int KSW>
+__global__ __launch_bounds__(GT) void gru_fwd_step_kernel(
+    int s, int T, int N, int H, int D, int UB, int BT, const float* __restrict__ xproj,
     const float* __restrict__ wp, const float* __restrict__ b_f, const float* __restrict__ b_r,
     const int* __restrict__ lens, float* __restrict__ h_all, float* __restrict__ gates) {
-  __shared__ __attribute__((aligned(16))) float hs[GB * GPAD];
-  __shared__ float red[4][GB][3 * GU + 1];
-  const int ub = blockIdx.x;
-  const int d = blockIdx.y;
-  const int n0 = blockIdx.z * GB;
-  const int UB = gridDim.x;
+  constexpr int PITCH = KC_FWD + 2;
+  __shared__ __attribute__((aligned(16))) float hs[GB * PITCH];
+  int ub, d, bt;
+  if (!map_work(UB * D, BT, UB, ub, d, bt)) return;
+  const int n0 = bt * GB;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int t = d == 0 ? s : T - 1 - s;
   const int tp = d == 0 ? t - 1 : t + 1;
   const int KS = (H + 3) / 4;
+  const int per = (KS + GW - 1) / GW;
+  const int a_ks = wave * per;
+  const int b_ks = min(KS, a_ks + per);
 
   f32x4 acc[3];
 #pragma unroll
   for (int g = 0; g < 3; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   if (s > 0) {
+    // W fragments first: every load of this wave is in flight before the h staging
+    float w[3][KSW];
+    const float* wpd = wp + ((int64_t)d * UB + ub) * KS * 3 * 64 + lane;
+#pragma unroll
+    for (int i = 0; i < KSW; ++i) {
+      const int ks = a_ks + i;
+#pragma unroll
+      for (int g = 0; g < 3; ++g) w[g][i] = ks < b_ks ? wpd[((int64_t)ks * 3 + g) * 64] : 0.f;
+    }
     const float* hprev = h_all + ((int64_t)tp * N * D + d) * H;   // row n at + n*D*H
-    const float* wpd = wp + ((int64_t)d * UB + ub) * KS * 3 * 64;
-    for (int kc0 = 0; kc0 < H; kc0 += GKC) {
-      const int kc1 = min(H, kc0 + GKC);
-      __syncthreads();
-      stage_rows(hprev, (int64_t)D * H, N, n0, kc0, kc1, hs);
-      __syncthreads();
-      const int ks0 = kc0 / 4;
-      const int ks1 = (kc1 + 3) / 4;
-      const int per = (ks1 - ks0 + 3) / 4;
-      const int a_ks = ks0 + wave * per;
-      const int b_ks = min(ks1, a_ks + per);
-      const float* hrow = hs + (lane & 15) * GPAD + (lane >> 4) - kc0;
-      for (int ks = a_ks; ks < b_ks; ++ks) {
+    stage_rows(hprev, (int64_t)D * H, N, n0, 0, H, hs, PITCH);
+    __syncthreads();
+    const float* hrow = hs + (lane & 15) * PITCH + (lane >> 4);
+#pragma unroll
+    for (int i = 0; i < KSW; ++i) {
+      const int ks = a_ks + i;
+      if (ks < b_ks) {
         const int k = 4 * ks;
-        const float a = (k + (lane >> 4) < kc1) ? hrow[k] : 0.f;
-        const float* bp = wpd + (int64_t)ks * 3 * 64 + lane;
-        acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bp[0], acc[0], 0, 0, 0);
-        acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bp[64], acc[1], 0, 0, 0);
-        acc[2] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bp[128], acc[2], 0, 0, 0);
+        const float a = (k + (lane >> 4) < H) ? hrow[k] : 0.f;
+        acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, w[0][i], acc[0], 0, 0, 0);
+        acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, w[1][i], acc[1], 0, 0, 0);
+        acc[2] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, w[2][i], acc[2], 0, 0, 0);
       }
     }
+    __syncthreads();   // hs is reused as the reduction buffer below
   }
-  // C/D map (16x16): col = lane & 15, row = (lane >> 4) * 4 + r
+  // partial tiles -> LDS: red[wave][m][g*16+u], C/D map col = lane&15, row = (lane>>4)*4+r
+  float* red = hs;
+  constexpr int RP = 3 * GU + 1;
 #pragma unroll
   for (int g = 0; g < 3; ++g)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) red[wave][(lane >> 4) * 4 + r][g * GU + (lane & 15)] = acc[g][r];
+    for (int r = 0; r < 4; ++r)
+      red[(wave * GB + (lane >> 4) * 4 + r) * RP + g * GU + (lane & 15)] = acc[g][r];
   __syncthreads();
+  if (threadIdx.x >= GB * GU) return;
 
   const int m = threadIdx.x >> 4;       // sample within the tile
   const int u = threadIdx.x & 15;       // unit within the block
   const int n = n0 + m;
   const int j = ub * GU + u;
   if (n >= N || j >= H) return;
+  float gh[3];
+#pragma unroll
+  for (int g = 0; g < 3; ++g) {
+    float v = 0.f;
+#pragma unroll
+    for (int w8 = 0; w8 < GW; ++w8) v += red[(w8 * GB + m) * RP + g * GU + u];
+    gh[g] = v;
+  }
   const float* bh = d == 0 ? b_f : b_r;
-  float ghr = red[0][m][u] + red[1][m][u] + red[2][m][u] + red[3][m][u] + bh[j];
-  float ghz = red[0][m][GU + u] + red[1][m][GU + u] + red[2][m][GU + u] + red[3][m][GU + u] +
-              bh[H + j];
-  float ghn = red[0][m][2 * GU + u] + red[1][m][2 * GU + u] + red[2][m][2 * GU + u] +
-              red[3][m][2 * GU + u] + bh[2 * H + j];
+  const float ghr = gh[0] + bh[j];
+  const float ghz = gh[1] + bh[H + j];
+  float ghn = gh[2] + bh[2 * H + j];
   const int64_t row = ((int64_t)t * N + n) * D + d;
   const bool active = t < lens[n];
   float hout = 0.f, r = 0.f, z = 0.f, nn = 0.f;
@@ -172,17 +212,18 @@ __global__ __launch_bounds__(256) void gru_fwd_step_kernel(
 }
 
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void gru_bwd_step_kernel(
-    int s, int T, int N, int H, int D, const float* __restrict__ dy, int dyd,
+// backward step (BPTT).  KSW = k-steps of W^T prefetched per wave per chunk.
+template <int KSW>
+__global__ __launch_bounds__(GT) void gru_bwd_step_kernel(
+    int s, int T, int N, int H, int D, int UB, int BT, const float* __restrict__ dy, int dyd,
     const float* __restrict__ wpt, const float* __restrict__ h_all,
     const float* __restrict__ gates, const int* __restrict__ lens, float* __restrict__ dgx,
     float* __restrict__ dgh, float* __restrict__ dhs) {
-  __shared__ __attribute__((aligned(16))) float hs[GB * GPAD];
-  __shared__ float red[4][GB][GU + 1];
-  const int ub = blockIdx.x;
-  const int d = blockIdx.y;
-  const int n0 = blockIdx.z * GB;
-  const int UB = gridDim.x;
+  constexpr int PITCH = KC_BWD + 2;
+  __shared__ __attribute__((aligned(16))) float hs[GB * PITCH];
+  int ub, d, bt;
+  if (!map_work(UB * D, BT, UB, ub, d, bt)) return;
+  const int n0 = bt * GB;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int t = d == 0 ? T - 1 - s : s;      // time processed now
@@ -194,37 +235,48 @@ __global__ __launch_bounds__(256) void gru_bwd_step_kernel(
   f32x4 acc1 = f32x4{0.f, 0.f, 0.f, 0.f};
   if (s > 0) {
     const float* dghq = dgh + ((int64_t)tq * N * D + d) * H3;
-    const float* wpd = wpt + ((int64_t)d * UB + ub) * KS * 64;
-    for (int kc0 = 0; kc0 < H3; kc0 += GKC) {
-      const int kc1 = min(H3, kc0 + GKC);
-      __syncthreads();
-      stage_rows(dghq, (int64_t)D * H3, N, n0, kc0, kc1, hs);
-      __syncthreads();
+    const float* wpd = wpt + ((int64_t)d * UB + ub) * KS * 64 + lane;
+    for (int kc0 = 0; kc0 < H3; kc0 += KC_BWD) {
+      const int kc1 = min(H3, kc0 + KC_BWD);
       const int ks0 = kc0 / 4;
       const int ks1 = (kc1 + 3) / 4;
-      const int per = (ks1 - ks0 + 3) / 4;
+      const int per = (ks1 - ks0 + GW - 1) / GW;
       const int a_ks = ks0 + wave * per;
       const int b_ks = min(ks1, a_ks + per);
-      const float* hrow = hs + (lane & 15) * GPAD + (lane >> 4) - kc0;
-      int ks = a_ks;
-      for (; ks + 1 < b_ks; ks += 2) {
-        const int k = 4 * ks;
-        const float a0 = (k + (lane >> 4) < kc1) ? hrow[k] : 0.f;
-        const float a1 = (k + 4 + (lane >> 4) < kc1) ? hrow[k + 4] : 0.f;
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, wpd[(int64_t)ks * 64 + lane], acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, wpd[(int64_t)(ks + 1) * 64 + lane], acc1, 0,
-                                                   0, 0);
+      float w[KSW];
+#pragma unroll
+      for (int i = 0; i < KSW; ++i) {
+        const int ks = a_ks + i;
+        w[i] = ks < b_ks ? wpd[(int64_t)ks * 64] : 0.f;
       }
-      if (ks < b_ks) {
-        const int k = 4 * ks;
-        const float a0 = (k + (lane >> 4) < kc1) ? hrow[k] : 0.f;
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, wpd[(int64_t)ks * 64 + lane], acc0, 0, 0, 0);
+      if (kc0 > 0) __syncthreads();
+      stage_rows(dghq, (int64_t)D * H3, N, n0, kc0, kc1, hs, PITCH);
+      __syncthreads();
+      const float* hrow = hs + (lane & 15) * PITCH + (lane >> 4) - kc0;
+#pragma unroll
+      for (int i = 0; i < KSW; i += 2) {
+        const int ks = a_ks + i;
+        if (ks < b_ks) {
+          const int k = 4 * ks;
+          const float a0 = (k + (lane >> 4) < kc1) ? hrow[k] : 0.f;
+          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, w[i], acc0, 0, 0, 0);
+        }
+        if (i + 1 < KSW && ks + 1 < b_ks) {
+          const int k = 4 * (ks + 1);
+          const float a1 = (k + (lane >> 4) < kc1) ? hrow[k] : 0.f;
+          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, w[i + 1], acc1, 0, 0, 0);
+        }
       }
     }
+    __syncthreads();
   }
+  float* red = hs;
+  constexpr int RP = GU + 1;
 #pragma unroll
-  for (int r = 0; r < 4; ++r) red[wave][(lane >> 4) * 4 + r][lane & 15] = acc0[r] + acc1[r];
+  for (int r = 0; r < 4; ++r)
+    red[(wave * GB + (lane >> 4) * 4 + r) * RP + (lane & 15)] = acc0[r] + acc1[r];
   __syncthreads();
+  if (threadIdx.x >= GB * GU) return;
 
   const int m = threadIdx.x >> 4;
   const int u = threadIdx.x & 15;
@@ -239,8 +291,11 @@ __global__ __launch_bounds__(256) void gru_bwd_step_kernel(
   if (t < len) {
     float carry = 0.f;
     if (s > 0) {
+      float rec = 0.f;
+#pragma unroll
+      for (int w8 = 0; w8 < GW; ++w8) rec += red[(w8 * GB + m) * RP + u];
       const float zq = gates[(((int64_t)tq * N + n) * D + d) * 4 * H + H + j];
-      carry = dhprv[j] * zq + (red[0][m][u] + red[1][m][u] + red[2][m][u] + red[3][m][u]);
+      carry = dhprv[j] * zq + rec;
     }
     dh = dy[(((int64_t)t * N + n) * dyd + (dyd > 1 ? d : 0)) * H + j] + carry;
   }
@@ -285,11 +340,25 @@ size_t ds2_gru_fwd_workspace_size(int n, int h, int num_dirs) {
   return (size_t)(num_dirs * UB * KS * 3 * 64) * sizeof(float) + 256;
 }
 
+#define DS2_FWD_CASE(K)                                                                    \
+  case K:                                                                                  \
+    hipLaunchKernelGGL(gru_fwd_step_kernel<K>, dim3(grid), dim3(GT), 0, st, s, t_max, n, h, \
+                       num_dirs, UB, BT, xproj, wp, b_hh_f, b_hh_r, lens, h_all, gates);    \
+    break;
+
+static int pick_ksw(int per) {
+  const int opts[] = {8, 16, 32, 48, 64, 80, 96};
+  for (int k : opts)
+    if (per <= k) return k;
+  return -1;
+}
+
 ds2_status_t ds2_gru_fwd(int t_max, int n, int h, int num_dirs, const float* xproj,
                          const float* w_hh_f, const float* w_hh_r, const float* b_hh_f,
                          const float* b_hh_r, const int* lens, float* h_all, float* gates,
                          void* ws, size_t ws_bytes, ds2_stream_t stream) {
   if (t_max < 0 || n < 0 || h < 1 || (num_dirs != 1 && num_dirs != 2)) return DS2_INVALID_VALUE;
+  if (h > KC_FWD) return DS2_UNSUPPORTED_SHAPE;
   if (t_max == 0 || n == 0) return DS2_OK;
   if (ws == nullptr || ws_bytes < ds2_gru_fwd_workspace_size(n, h, num_dirs))
     return DS2_WORKSPACE_TOO_SMALL;
@@ -300,13 +369,18 @@ ds2_status_t ds2_gru_fwd(int t_max, int n, int h, int num_dirs, const float* xpr
   hipStream_t st = as_stream(stream);
   const int UB = (h + GU - 1) / GU;
   const int KS = (h + 3) / 4;
+  const int BT = (n + GB - 1) / GB;
+  const int ksw = pick_ksw((KS + GW - 1) / GW);
+  if (ksw < 0) return DS2_UNSUPPORTED_SHAPE;
   float* wp = static_cast<float*>(ws);
   hipLaunchKernelGGL(pack_fwd_kernel, dim3(grid_cap((int64_t)num_dirs * UB * KS * 192)),
                      dim3(256), 0, st, w_hh_f, w_hh_r, h, num_dirs, UB, KS, wp);
-  dim3 grid(UB, num_dirs, (n + GB - 1) / GB);
+  const int grid = mapped_grid(UB * num_dirs, BT);
   for (int s = 0; s < t_max; ++s) {
-    hipLaunchKernelGGL(gru_fwd_step_kernel, grid, dim3(256), 0, st, s, t_max, n, h, num_dirs,
-                       xproj, wp, b_hh_f, b_hh_r, lens, h_all, gates);
+    switch (ksw) {
+      DS2_FWD_CASE(8) DS2_FWD_CASE(16) DS2_FWD_CASE(32) DS2_FWD_CASE(48) DS2_FWD_CASE(64)
+      DS2_FWD_CASE(80) DS2_FWD_CASE(96)
+    }
   }
   return launch_status("ds2_gru_fwd");
 }
@@ -317,6 +391,13 @@ size_t ds2_gru_bwd_workspace_size(int n, int h, int num_dirs) {
   return (size_t)(num_dirs * UB * KS * 64) * sizeof(float) +
          (size_t)2 * n * num_dirs * h * sizeof(float) + 512;
 }
+
+#define DS2_BWD_CASE(K)                                                                     \
+  case K:                                                                                   \
+    hipLaunchKernelGGL(gru_bwd_step_kernel<K>, dim3(grid), dim3(GT), 0, st, s, t_max, n, h,  \
+                       num_dirs, UB, BT, dy, dy_dirs, wpt, h_all, gates, lens, dgates_x,     \
+                       dgates_h, dhs);                                                       \
+    break;
 
 ds2_status_t ds2_gru_bwd(int t_max, int n, int h, int num_dirs, const float* dy, int dy_dirs,
                          const float* w_hh_f, const float* w_hh_r, const float* h_all,
@@ -332,15 +413,21 @@ ds2_status_t ds2_gru_bwd(int t_max, int n, int h, int num_dirs, const float* dy,
   hipStream_t st = as_stream(stream);
   const int UB = (h + GU - 1) / GU;
   const int KS = (3 * h + 3) / 4;
+  const int BT = (n + GB - 1) / GB;
+  const int chunk_ks = (std::min(3 * h, KC_BWD) + 3) / 4;
+  const int ksw = pick_ksw((chunk_ks + GW - 1) / GW + 1);
+  if (ksw < 0) return DS2_UNSUPPORTED_SHAPE;
   float* wpt = static_cast<float*>(ws);
   size_t off = ((size_t)num_dirs * UB * KS * 64 * sizeof(float) + 255) & ~(size_t)255;
   float* dhs = reinterpret_cast<float*>(static_cast<char*>(ws) + off);
   hipLaunchKernelGGL(pack_bwd_kernel, dim3(grid_cap((int64_t)num_dirs * UB * KS * 64)),
                      dim3(256), 0, st, w_hh_f, w_hh_r, h, num_dirs, UB, KS, wpt);
-  dim3 grid(UB, num_dirs, (n + GB - 1) / GB);
+  const int grid = mapped_grid(UB * num_dirs, BT);
   for (int s = 0; s < t_max; ++s) {
-    hipLaunchKernelGGL(gru_bwd_step_kernel, grid, dim3(256), 0, st, s, t_max, n, h, num_dirs, dy,
-                       dy_dirs, wpt, h_all, gates, lens, dgates_x, dgates_h, dhs);
+    switch (ksw) {
+      DS2_BWD_CASE(8) DS2_BWD_CASE(16) DS2_BWD_CASE(32) DS2_BWD_CASE(48) DS2_BWD_CASE(64)
+      DS2_BWD_CASE(80) DS2_BWD_CASE(96)
+    }
   }
   return launch_status("ds2_gru_bwd");
 }

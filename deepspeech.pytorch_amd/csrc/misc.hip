@@ -36,28 +36,40 @@ __global__ void dirsum_kernel(const float* __restrict__ h_all, int64_t rows, int
   }
 }
 
-// Column sums: one thread per column slice, rows split over blockIdx.y; partial
-// results combined with atomics into a zeroed fp32 output would be
-// nondeterministic, so instead each block reduces a full column range over
-// all rows (rows are <= a few 10^4 here; bias grads are tiny GEMV-like work).
-__global__ void colsum_kernel(const float* __restrict__ x, int rows, int cols, int64_t ld,
-                              float* __restrict__ out, int accumulate) {
-  // block: 256 threads = 64 columns x 4 row-groups
+// Column sums (bias gradients): stage 1 reduces a chunk of rows for 64 columns per
+// block in fp64 (grid = column blocks x row chunks, enough blocks to fill the chip),
+// stage 2 adds the chunk partials in a fixed order (deterministic, no atomics).
+constexpr int kColChunks = 64;
+
+__global__ __launch_bounds__(256) void colsum_partial_kernel(const float* __restrict__ x,
+                                                             int rows, int cols, int64_t ld,
+                                                             double* __restrict__ partial) {
   __shared__ double part[4][64];
   const int lane = threadIdx.x & 63;
   const int grp = threadIdx.x >> 6;
   const int col = blockIdx.x * 64 + lane;
+  const int per = (rows + gridDim.y - 1) / gridDim.y;
+  const int r0 = blockIdx.y * per;
+  const int r1 = min(rows, r0 + per);
   double acc = 0.0;
   if (col < cols) {
-    for (int r = grp; r < rows; r += 4) acc += (double)x[(int64_t)r * ld + col];
+    for (int r = r0 + grp; r < r1; r += 4) acc += (double)x[(int64_t)r * ld + col];
   }
   part[grp][lane] = acc;
   __syncthreads();
-  if (grp == 0 && col < cols) {
-    double s = part[0][lane] + part[1][lane] + part[2][lane] + part[3][lane];
-    float v = static_cast<float>(s);
-    out[col] = accumulate ? out[col] + v : v;
-  }
+  if (grp == 0 && col < cols)
+    partial[(int64_t)blockIdx.y * cols + col] = part[0][lane] + part[1][lane] + part[2][lane] +
+                                                part[3][lane];
+}
+
+__global__ void colsum_final_kernel(const double* __restrict__ partial, int chunks, int cols,
+                                    float* __restrict__ out, int accumulate) {
+  const int col = blockIdx.x * blockDim.x + threadIdx.x;
+  if (col >= cols) return;
+  double s = 0.0;
+  for (int c = 0; c < chunks; ++c) s += partial[(int64_t)c * cols + col];
+  const float v = static_cast<float>(s);
+  out[col] = accumulate ? out[col] + v : v;
 }
 
 // ---------------------------------------------------------------------------
@@ -232,12 +244,24 @@ ds2_status_t ds2_dirsum(const float* h_all, int rows, int num_dirs, int h, float
   return launch_status("ds2_dirsum");
 }
 
+size_t ds2_colsum_workspace_size(int rows, int cols) {
+  (void)rows;
+  return (size_t)kColChunks * (cols > 0 ? cols : 0) * sizeof(double) + 256;
+}
+
 ds2_status_t ds2_colsum(const float* x, int rows, int cols, int64_t ld, float* out,
-                        int accumulate, ds2_stream_t stream) {
+                        int accumulate, void* ws, size_t ws_bytes, ds2_stream_t stream) {
   if (rows < 0 || cols < 0 || ld < cols) return DS2_INVALID_VALUE;
   if (cols == 0) return DS2_OK;
-  hipLaunchKernelGGL(colsum_kernel, dim3(cdiv(cols, 64)), dim3(256), 0, as_stream(stream), x,
-                     rows, cols, ld, out, accumulate);
+  if (ws == nullptr || ws_bytes < ds2_colsum_workspace_size(rows, cols))
+    return DS2_WORKSPACE_TOO_SMALL;
+  int chunks = rows / 64;
+  chunks = chunks < 1 ? 1 : (chunks > kColChunks ? kColChunks : chunks);
+  double* partial = static_cast<double*>(ws);
+  hipLaunchKernelGGL(colsum_partial_kernel, dim3(cdiv(cols, 64), chunks), dim3(256), 0,
+                     as_stream(stream), x, rows, cols, ld, partial);
+  hipLaunchKernelGGL(colsum_final_kernel, dim3(cdiv(cols, 256)), dim3(256), 0, as_stream(stream),
+                     partial, chunks, cols, out, accumulate);
   return launch_status("ds2_colsum");
 }
 

@@ -30,6 +30,10 @@ _PROTOS = {
                                  _c_int, _vp, _c_int, _vp, _sz, _vp]),
     "ds2_sgemm": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _c_f, _vp, _c_i64, _c_i64,
                            _vp, _c_i64, _c_i64, _c_f, _vp, _c_i64, _c_i64, _c_int, _vp, _vp]),
+    "ds2_sgemm_workspace_size": (_sz, [_c_int, _c_int, _c_int, _c_int]),
+    "ds2_sgemm_ws": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _c_f, _vp, _c_i64, _c_i64,
+                              _vp, _c_i64, _c_i64, _c_f, _vp, _c_i64, _c_i64, _c_int, _vp, _vp,
+                              _sz, _vp]),
     "ds2_conv2d_fwd": (_c_int, [_vp, _vp, _vp, _vp] + [_c_int] * 11 + [_vp, _vp]),
     "ds2_conv2d_dgrad": (_c_int, [_vp, _vp, _vp] + [_c_int] * 11 + [_vp]),
     "ds2_conv2d_wgrad_workspace_size": (_sz, [_c_int] * 11),
@@ -51,7 +55,8 @@ _PROTOS = {
     "ds2_gru_bwd": (_c_int, [_c_int, _c_int, _c_int, _c_int, _vp, _c_int, _vp, _vp, _vp, _vp,
                              _vp, _vp, _vp, _vp, _sz, _vp]),
     "ds2_dirsum": (_c_int, [_vp, _c_int, _c_int, _c_int, _vp, _vp]),
-    "ds2_colsum": (_c_int, [_vp, _c_int, _c_int, _c_i64, _vp, _c_int, _vp]),
+    "ds2_colsum_workspace_size": (_sz, [_c_int, _c_int]),
+    "ds2_colsum": (_c_int, [_vp, _c_int, _c_int, _c_i64, _vp, _c_int, _vp, _sz, _vp]),
     "ds2_softmax_tnc": (_c_int, [_vp, _c_int, _c_int, _c_int, _vp, _vp]),
     "ds2_softmax_tnc_bwd": (_c_int, [_vp, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _vp]),
     "ds2_ctc_workspace_size": (_sz, [_c_int, _c_int, _c_int]),

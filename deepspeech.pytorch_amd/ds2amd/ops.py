@@ -52,9 +52,12 @@ def sgemm(a: torch.Tensor, b: torch.Tensor, c: torch.Tensor, *, m: int, n: int, 
     ``*_off`` are element offsets into the (contiguous) storage of a/b/c.
     """
     es = 4
-    _lib.call("ds2_sgemm", int(trans_a), int(trans_b), m, n, k, float(alpha),
+    nbytes = _lib.size("ds2_sgemm_workspace_size", m, n, k, 1)
+    ws = _ws(nbytes, c.device) if nbytes > 0 else None
+    _lib.call("ds2_sgemm_ws", int(trans_a), int(trans_b), m, n, k, float(alpha),
               a.data_ptr() + es * a_off, lda, 0, b.data_ptr() + es * b_off, ldb, 0,
-              float(beta), c.data_ptr() + es * c_off, ldc, 0, 1, _p(bias), _stream())
+              float(beta), c.data_ptr() + es * c_off, ldc, 0, 1, _p(bias), _p(ws),
+              0 if ws is None else ws.numel(), _stream())
     return c
 
 
@@ -146,8 +149,9 @@ def bn_backward(dy, dy_layout, x, outer, c, d, t, mean, invstd, gamma, beta, mas
 
 
 def colsum(x2d_storage, rows, cols, ld, out, accumulate=False, off=0):
+    ws = _ws(_lib.size("ds2_colsum_workspace_size", rows, cols), out.device)
     _lib.call("ds2_colsum", x2d_storage.data_ptr() + 4 * off, rows, cols, ld, out.data_ptr(),
-              int(accumulate), _stream())
+              int(accumulate), ws.data_ptr(), ws.numel(), _stream())
     return out
 
 

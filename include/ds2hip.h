@@ -67,6 +67,15 @@ ds2_status_t ds2_sgemm(int trans_a, int trans_b, int m, int n, int k, float alph
                        const float* b, int64_t ldb, int64_t stride_b, float beta,
                        float* c, int64_t ldc, int64_t stride_c, int batch,
                        const float* bias, ds2_stream_t stream);
+/* Same with a workspace: when the output grid cannot fill the chip and K is long
+ * (weight gradients: M = 3H, N = In, K = T*N), K is split across workgroups and
+ * the fp32 partials are reduced in a fixed order (deterministic).           */
+size_t ds2_sgemm_workspace_size(int m, int n, int k, int batch);
+ds2_status_t ds2_sgemm_ws(int trans_a, int trans_b, int m, int n, int k, float alpha,
+                          const float* a, int64_t lda, int64_t stride_a,
+                          const float* b, int64_t ldb, int64_t stride_b, float beta,
+                          float* c, int64_t ldc, int64_t stride_c, int batch,
+                          const float* bias, void* ws, size_t ws_bytes, ds2_stream_t stream);
 
 /* ------------------------------------------------------------------------ */
 /* Conv2d, NCHW fp32, implicit GEMM on MFMA. ref model.py:209,212 (nn.Conv2d via
@@ -155,8 +164,9 @@ ds2_status_t ds2_gru_bwd(int t_max, int n, int h, int num_dirs, const float* dy,
 ds2_status_t ds2_dirsum(const float* h_all, int rows, int num_dirs, int h, float* y,
                         ds2_stream_t stream);
 /* out[j] (+)= sum_i x[i*ld + j]  for i < rows, j < cols (bias gradients). */
+size_t ds2_colsum_workspace_size(int rows, int cols);
 ds2_status_t ds2_colsum(const float* x, int rows, int cols, int64_t ld, float* out,
-                        int accumulate, ds2_stream_t stream);
+                        int accumulate, void* ws, size_t ws_bytes, ds2_stream_t stream);
 
 /* ------------------------------------------------------------------------ */
 /* Softmax over C of logits stored [T][N][C] -> probs [N][T][C] (model.py:375-377). */

@@ -25,7 +25,7 @@ def _close(got, ref, rel=1e-5, name=""):
 # ---------------------------------------------------------------------------- GEMM
 @pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
 @pytest.mark.parametrize("m,n,k", [(1, 1, 1), (37, 53, 29), (128, 128, 16), (300, 257, 513),
-                                   (515, 2400, 132)])
+                                   (515, 2400, 132), (257, 300, 5000)])   # last: split-K path
 def test_sgemm(dev, ta, tb, m, n, k):
     g = torch.Generator().manual_seed(m * 7 + n * 3 + k)
     a = torch.randn(k, m, generator=g) if ta else torch.randn(m, k, generator=g)
