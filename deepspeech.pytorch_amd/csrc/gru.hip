@@ -21,6 +21,7 @@
 #include "common.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace ds2 {
 
@@ -121,7 +122,7 @@ __global__ __launch_bounds__(GT) void gru_fwd_step_kernel(
   if (!map_work(UB * D, BT, UB, ub, d, bt)) return;
   const int n0 = bt * GB;
   const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // provably uniform
   const int t = d == 0 ? s : T - 1 - s;
   const int tp = d == 0 ? t - 1 : t + 1;
   const int KS = (H + 3) / 4;
@@ -225,7 +226,7 @@ __global__ __launch_bounds__(GT) void gru_bwd_step_kernel(
   if (!map_work(UB * D, BT, UB, ub, d, bt)) return;
   const int n0 = bt * GB;
   const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // provably uniform
   const int t = d == 0 ? T - 1 - s : s;      // time processed now
   const int tq = d == 0 ? t + 1 : t - 1;     // time processed at step s-1
   const int H3 = 3 * H;
@@ -322,6 +323,372 @@ __global__ __launch_bounds__(GT) void gru_bwd_step_kernel(
   dhcur[j] = dh;
 }
 
+// ===========================================================================
+// Persistent variants: one launch per layer and direction pair.  Each workgroup
+// keeps its W_hh fragments in registers for all T steps; the per-step hand-off of
+// the new hidden states (forward) / gate gradients (backward) between the UB
+// workgroups of a (direction, batch tile) group follows the write-through form
+// of MI355X_MICROARCH.md "Valid forms" row 1: payload stored sc1 (agent-scope
+// relaxed atomic stores), every storing wave drains vmcnt, workgroup barrier,
+// one lane adds to the group's arrival counter (agent atomic); consumers poll
+// that counter relaxed (one lane, s_sleep, bounded), barrier, then load the
+// payload with sc1 (agent-scope relaxed atomic) loads.  Counters are zeroed by
+// a hipMemsetAsync before every launch; a spin that exceeds its bound sets the
+// error word and the workgroup leaves (no hang, results invalid).
+constexpr unsigned kSpinLimit = 1u << 21;
+
+__device__ __forceinline__ void st_sc1(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ unsigned long long ld_sc1_u64(const float* p) {
+  return __hip_atomic_load(reinterpret_cast<const unsigned long long*>(p), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ float ld_sc1(const float* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// thread 0 waits until *ctr >= target; returns false (for the whole workgroup) on timeout
+__device__ __forceinline__ bool group_wait(unsigned* ctr, unsigned target, unsigned* err,
+                                           int* lds_flag) {
+  if (threadIdx.x == 0) {
+    unsigned spins = 0;
+    int ok = 1;
+    while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++spins > kSpinLimit || __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+        __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ok = 0;
+        break;
+      }
+    }
+    *lds_flag = ok;
+  }
+  __syncthreads();
+  return *lds_flag != 0;
+}
+
+__device__ __forceinline__ void group_arrive(unsigned* ctr) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains first
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+constexpr int kSc1 = 16;   // buffer-op aux bit: sc1 (write-through store / L1-bypassing load)
+
+// Stage rows [n0, n0+16) x [0, cols) of a row-major slab (row stride ld floats, N
+// valid rows, `width` valid columns) into hs[m][pitch] with 16-byte sc1 buffer loads.
+// Rows >= N and columns >= width read as zero (out-of-range buffer offsets return
+// 0), so the MFMA loop needs no bounds checks.  All MAXI loads of a thread are
+// issued before the first LDS store.  width, cols and ld are multiples of 4.
+template <int MAXI>
+__device__ __forceinline__ void stage_rows_sc1(const float* src, int ld, int N, int n0,
+                                               int width, int cols, float* __restrict__ hs,
+                                               int pitch) {
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(src), (short)0, N * ld * 4, 0x00020000);
+  const int q = cols >> 2;
+  const int total = GB * q;
+  u32x4 v[MAXI];
+#pragma unroll
+  for (int r = 0; r < MAXI; ++r) {
+    const int i = threadIdx.x + r * GT;
+    int off = 0x7ffffff0;
+    if (i < total) {
+      const int m = i / q;
+      const int k = (i - m * q) * 4;
+      if (k < width) off = ((n0 + m) * ld + k) * 4;
+    }
+    v[r] = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, kSc1);
+  }
+#pragma unroll
+  for (int r = 0; r < MAXI; ++r) {
+    const int i = threadIdx.x + r * GT;
+    if (i < total) {
+      const int m = i / q;
+      const int k = (i - m * q) * 4;
+      *reinterpret_cast<u32x4*>(hs + m * pitch + k) = v[r];
+    }
+  }
+}
+
+// phase stamps (diagnostic, DS2_GRU_STAMPS=1): workgroup 0, thread 0 accumulates
+// s_memtime deltas per phase into stamps[0..7] (units: shader clocks)
+__device__ __forceinline__ unsigned long long stamp_now() { return __builtin_amdgcn_s_memtime(); }
+
+template <int KSW>
+__global__ __launch_bounds__(GT) void gru_fwd_persist_kernel(
+    int T, int N, int H, int D, int UB, int BT, const float* __restrict__ xproj,
+    const float* __restrict__ wp, const float* __restrict__ b_f, const float* __restrict__ b_r,
+    const int* __restrict__ lens, float* __restrict__ h_all, float* __restrict__ gates,
+    unsigned* __restrict__ counters, unsigned* __restrict__ err,
+    unsigned long long* __restrict__ stamps) {
+  constexpr int PITCH = KC_FWD + 4;
+  __shared__ __attribute__((aligned(16))) float hs[GB * PITCH];
+  __shared__ int flag;
+  int ub, d, bt;
+  if (!map_work(UB * D, BT, UB, ub, d, bt)) return;
+  const int n0 = bt * GB;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // provably uniform
+  const int KS = (H + 3) / 4;
+  const int a_ks = wave * KSW;           // host guarantees GW * KSW >= KS
+  const int b_ks = min(KS, a_ks + KSW);
+  unsigned* ctr = counters + d * BT + bt;
+  const __amdgpu_buffer_rsrc_t h_rs = __builtin_amdgcn_make_buffer_rsrc(
+      h_all, (short)0, T * N * D * H * 4, 0x00020000);
+  const bool stamping = stamps != nullptr && blockIdx.x == 0 && threadIdx.x == 0;
+  unsigned long long acc_t[6] = {0, 0, 0, 0, 0, 0};
+  unsigned long long t0 = 0, t1 = 0;
+
+  // W_hh fragments for the whole sequence
+  float w[3][KSW];
+  {
+    const float* wpd = wp + ((int64_t)d * UB + ub) * KS * 3 * 64 + lane;
+#pragma unroll
+    for (int i = 0; i < KSW; ++i) {
+      const int ks = a_ks + i;
+#pragma unroll
+      for (int g = 0; g < 3; ++g) w[g][i] = ks < b_ks ? wpd[((int64_t)ks * 3 + g) * 64] : 0.f;
+    }
+  }
+  const float* bh = d == 0 ? b_f : b_r;
+  const int m = threadIdx.x >> 4;
+  const int u = threadIdx.x & 15;
+  const int n = n0 + m;
+  const int j = ub * GU + u;
+  const bool owner = threadIdx.x < GB * GU && n < N && j < H;
+  float bias_r = 0.f, bias_z = 0.f, bias_n = 0.f;
+  int len = 0;
+  if (owner) {
+    bias_r = bh[j];
+    bias_z = bh[H + j];
+    bias_n = bh[2 * H + j];
+    len = lens[n];
+  }
+  constexpr int RP = 3 * GU + 1;
+  __shared__ float red[GW * GB * RP];
+  float g_r = 0.f, g_z = 0.f, g_n = 0.f, g_hn = 0.f;   // gate cache of the previous step
+  int64_t g_row = -1;
+  for (int s = 0; s < T; ++s) {
+    const int t = d == 0 ? s : T - 1 - s;
+    const int tp = d == 0 ? t - 1 : t + 1;
+    const int64_t row = ((int64_t)t * N + n) * D + d;
+    // inputs of this step that do not depend on other workgroups: issue first
+    float xr = 0.f, xz = 0.f, xn = 0.f;
+    if (owner && t < len) {
+      const float* xp = xproj + row * 3 * H;
+      xr = xp[j];
+      xz = xp[H + j];
+      xn = xp[2 * H + j];
+    }
+    f32x4 acc[3];
+#pragma unroll
+    for (int g = 0; g < 3; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float hp = 0.f;
+    if (stamping) t0 = stamp_now();
+    if (s > 0) {
+      if (!group_wait(ctr, (unsigned)s * UB, err, &flag)) return;
+      if (stamping) { t1 = stamp_now(); acc_t[0] += t1 - t0; t0 = t1; }
+      const float* hprev = h_all + ((int64_t)tp * N * D + d) * H;
+      stage_rows_sc1<(GB * KC_FWD / 4 + GT - 1) / GT>(hprev, D * H, N, n0, H, 4 * GW * KSW, hs,
+                                                       PITCH);
+      __syncthreads();
+      if (stamping) { t1 = stamp_now(); acc_t[1] += t1 - t0; t0 = t1; }
+      // every wave runs exactly KSW k-steps; steps past H read zero-staged columns and
+      // zero W registers, so there is no branch between the LDS reads and the MFMAs
+      const float* hrow = hs + (lane & 15) * PITCH + (lane >> 4) + 4 * a_ks;
+#pragma unroll
+      for (int i = 0; i < KSW; ++i) {
+        const float a = hrow[4 * i];
+        acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, w[0][i], acc[0], 0, 0, 0);
+        acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, w[1][i], acc[1], 0, 0, 0);
+        acc[2] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, w[2][i], acc[2], 0, 0, 0);
+      }
+      if (owner) hp = hs[m * PITCH + j];
+    }
+#pragma unroll
+    for (int g = 0; g < 3; ++g)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        red[(wave * GB + (lane >> 4) * 4 + r) * RP + g * GU + (lane & 15)] = acc[g][r];
+    __syncthreads();
+    if (stamping) { t1 = stamp_now(); acc_t[2] += t1 - t0; t0 = t1; }
+    if (owner) {
+      float gh[3];
+#pragma unroll
+      for (int g = 0; g < 3; ++g) {
+        float v = 0.f;
+#pragma unroll
+        for (int w8 = 0; w8 < GW; ++w8) v += red[(w8 * GB + m) * RP + g * GU + u];
+        gh[g] = v;
+      }
+      const float ghr = gh[0] + bias_r;
+      const float ghz = gh[1] + bias_z;
+      float ghn = gh[2] + bias_n;
+      float hout = 0.f, r = 0.f, z = 0.f, nn = 0.f;
+      if (t < len) {
+        r = sigmoidf_(ghr + xr);
+        z = sigmoidf_(ghz + xz);
+        nn = tanhf(xn + r * ghn);
+        hout = (hp - nn) * z + nn;
+      } else {
+        ghn = 0.f;
+      }
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, hout), h_rs,
+                                            static_cast<int>((row * H + j) * 4), 0, kSc1);
+      g_r = r; g_z = z; g_n = nn; g_hn = ghn; g_row = row;
+    }
+    if (stamping) { t1 = stamp_now(); acc_t[3] += t1 - t0; t0 = t1; }
+    group_arrive(ctr);
+    if (stamping) { t1 = stamp_now(); acc_t[4] += t1 - t0; t0 = t1; }
+    // the gate cache is consumed only by the backward kernel: store it off the
+    // critical path, after this step's hand-off has been signalled
+    if (owner && gates != nullptr) {
+      float* gp = gates + g_row * 4 * H;
+      gp[j] = g_r;
+      gp[H + j] = g_z;
+      gp[2 * H + j] = g_n;
+      gp[3 * H + j] = g_hn;
+    }
+  }
+  if (stamping)
+    for (int i = 0; i < 5; ++i) stamps[i] = acc_t[i];
+}
+
+template <int KSW>
+__global__ __launch_bounds__(GT) void gru_bwd_persist_kernel(
+    int T, int N, int H, int D, int UB, int BT, const float* __restrict__ dy, int dyd,
+    const float* __restrict__ wpt, const float* __restrict__ h_all,
+    const float* __restrict__ gates, const int* __restrict__ lens, float* __restrict__ dgx,
+    float* __restrict__ dgh, unsigned* __restrict__ counters, unsigned* __restrict__ err) {
+  constexpr int PITCH = KC_BWD + 4;
+  __shared__ __attribute__((aligned(16))) float hs[GB * PITCH];
+  float* red = hs;                          // reduction buffer aliases the staged rows
+  __shared__ int flag;
+  int ub, d, bt;
+  if (!map_work(UB * D, BT, UB, ub, d, bt)) return;
+  const int n0 = bt * GB;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // provably uniform
+  const int H3 = 3 * H;
+  const int KS = (H3 + 3) / 4;             // single chunk: 32 * KSW <= KC_BWD (host-checked)
+  const int a_ks = wave * KSW;
+  const int b_ks = min(KS, a_ks + KSW);
+  unsigned* ctr = counters + d * BT + bt;
+  const __amdgpu_buffer_rsrc_t g_rs = __builtin_amdgcn_make_buffer_rsrc(
+      dgh, (short)0, T * N * D * H3 * 4, 0x00020000);
+
+  float w[KSW];
+  {
+    const float* wpd = wpt + ((int64_t)d * UB + ub) * KS * 64 + lane;
+#pragma unroll
+    for (int i = 0; i < KSW; ++i) {
+      const int ks = a_ks + i;
+      w[i] = ks < b_ks ? wpd[(int64_t)ks * 64] : 0.f;
+    }
+  }
+  const int m = threadIdx.x >> 4;
+  const int u = threadIdx.x & 15;
+  const int n = n0 + m;
+  const int j = ub * GU + u;
+  const bool owner = threadIdx.x < GB * GU && n < N && j < H;
+  const int len = owner ? lens[n] : 0;
+  constexpr int RP = GU + 1;
+  float dh_prev = 0.f, z_prev = 0.f;        // this thread's unit, carried in registers
+
+  for (int s = 0; s < T; ++s) {
+    const int t = d == 0 ? T - 1 - s : s;
+    f32x4 acc0 = f32x4{0.f, 0.f, 0.f, 0.f};
+    f32x4 acc1 = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (s > 0) {
+      const int tq = d == 0 ? t + 1 : t - 1;
+      if (!group_wait(ctr, (unsigned)s * UB, err, &flag)) return;
+      const float* dghq = dgh + ((int64_t)tq * N * D + d) * H3;
+      stage_rows_sc1<(GB * KC_BWD / 4 + GT - 1) / GT>(dghq, D * H3, N, n0, H3, 4 * GW * KSW, hs,
+                                                       PITCH);
+      __syncthreads();
+      const float* hrow = hs + (lane & 15) * PITCH + (lane >> 4) + 4 * a_ks;
+#pragma unroll
+      for (int i = 0; i < KSW; i += 2) {
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(hrow[4 * i], w[i], acc0, 0, 0, 0);
+        if (i + 1 < KSW)
+          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(hrow[4 * i + 4], w[i + 1], acc1, 0, 0, 0);
+      }
+      __syncthreads();                      // all reads of hs done before red overwrites it
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      red[(wave * GB + (lane >> 4) * 4 + r) * RP + (lane & 15)] = acc0[r] + acc1[r];
+    __syncthreads();
+    if (owner) {
+      const int64_t row = ((int64_t)t * N + n) * D + d;
+      float dh = 0.f;
+      float dar = 0.f, daz = 0.f, dan = 0.f, dghn = 0.f, zc = 0.f;
+      if (t < len) {
+        float carry = 0.f;
+        if (s > 0) {
+          float rec = 0.f;
+#pragma unroll
+          for (int w8 = 0; w8 < GW; ++w8) rec += red[(w8 * GB + m) * RP + u];
+          carry = dh_prev * z_prev + rec;
+        }
+        dh = dy[(((int64_t)t * N + n) * dyd + (dyd > 1 ? d : 0)) * H + j] + carry;
+        const float* gp = gates + row * 4 * H;
+        const float r = gp[j], nn = gp[2 * H + j], ghn = gp[3 * H + j];
+        zc = gp[H + j];
+        float hp = 0.f;
+        const int tp = d == 0 ? t - 1 : t + 1;
+        if (tp >= 0 && tp < T) hp = h_all[(((int64_t)tp * N + n) * D + d) * H + j];
+        dan = dh * (1.f - zc) * (1.f - nn * nn);
+        daz = dh * (hp - nn) * zc * (1.f - zc);
+        dar = dan * ghn * r * (1.f - r);
+        dghn = dan * r;
+      }
+      float* gx = dgx + row * H3;
+      gx[j] = dar;
+      gx[H + j] = daz;
+      gx[2 * H + j] = dan;
+      const int go = static_cast<int>((row * H3 + j) * 4);
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, dar), g_rs, go, 0, kSc1);
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, daz), g_rs, go + 4 * H, 0,
+                                            kSc1);
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, dghn), g_rs, go + 8 * H,
+                                            0, kSc1);
+      dh_prev = dh;
+      z_prev = zc;
+    }
+    group_arrive(ctr);
+  }
+}
+
+static int g_num_cus = -1;
+static int num_cus() {
+  if (g_num_cus < 0) {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) v = 0;
+    g_num_cus = v;
+  }
+  return g_num_cus;
+}
+
+// smallest instantiated k-steps-per-wave >= per whose zero-padded span fits the LDS pitch
+static int persist_ksw(int per, int kc) {
+  const int opts[] = {8, 16, 25, 32, 48, 64, 75};
+  for (int k : opts)
+    if (per <= k && 4 * GW * k <= kc) return k;
+  return -1;
+}
+
+static bool persistent_enabled() {
+  const char* e = getenv("DS2_GRU_PERSISTENT");
+  return !(e != nullptr && e[0] == '0');
+}
+
 static inline int grid_cap(int64_t work) {
   int64_t g = (work + 255) / 256;
   return static_cast<int>(g > 2048 ? 2048 : (g < 1 ? 1 : g));
@@ -333,11 +700,24 @@ using namespace ds2;
 
 extern "C" {
 
+static inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+static inline size_t counter_bytes(int n, int num_dirs) {
+  return align256((size_t)(num_dirs * ((n + GB - 1) / GB) + 1) * sizeof(unsigned)) +
+         16 * sizeof(unsigned long long);
+}
+static inline unsigned long long* stamp_slots(unsigned* ctrs, int n, int num_dirs) {
+  const char* e = getenv("DS2_GRU_STAMPS");
+  if (e == nullptr || e[0] != '1') return nullptr;
+  return reinterpret_cast<unsigned long long*>(
+      reinterpret_cast<char*>(ctrs) +
+      align256((size_t)(num_dirs * ((n + GB - 1) / GB) + 1) * sizeof(unsigned)));
+}
+
 size_t ds2_gru_fwd_workspace_size(int n, int h, int num_dirs) {
-  (void)n;
   const int64_t UB = (h + GU - 1) / GU;
   const int64_t KS = (h + 3) / 4;
-  return (size_t)(num_dirs * UB * KS * 3 * 64) * sizeof(float) + 256;
+  return align256((size_t)(num_dirs * UB * KS * 3 * 64) * sizeof(float)) +
+         counter_bytes(n, num_dirs) + 256;
 }
 
 #define DS2_FWD_CASE(K)                                                                    \
@@ -376,6 +756,31 @@ ds2_status_t ds2_gru_fwd(int t_max, int n, int h, int num_dirs, const float* xpr
   hipLaunchKernelGGL(pack_fwd_kernel, dim3(grid_cap((int64_t)num_dirs * UB * KS * 192)),
                      dim3(256), 0, st, w_hh_f, w_hh_r, h, num_dirs, UB, KS, wp);
   const int grid = mapped_grid(UB * num_dirs, BT);
+  if (persistent_enabled() && (h % 4) == 0 && grid <= num_cus() &&
+      (int64_t)t_max * n * num_dirs * h * 4 < (1ll << 31)) {
+    unsigned* ctrs = reinterpret_cast<unsigned*>(
+        static_cast<char*>(ws) + align256((size_t)num_dirs * UB * KS * 3 * 64 * sizeof(float)));
+    unsigned* err = ctrs + num_dirs * BT;
+    if (hipMemsetAsync(ctrs, 0, counter_bytes(n, num_dirs), st) != hipSuccess)
+      return launch_status("ds2_gru counters");
+    int T_ = t_max, N_ = n, H_ = h, D_ = num_dirs, UB_ = UB, BT_ = BT;
+    unsigned long long* stamps = stamp_slots(ctrs, n, num_dirs);
+    void* args[] = {&T_, &N_, &H_, &D_, &UB_, &BT_, &xproj, &wp, &b_hh_f, &b_hh_r, &lens,
+                    &h_all, &gates, &ctrs, &err, &stamps};
+    const void* fn = nullptr;
+    const int kp = persist_ksw((KS + GW - 1) / GW, KC_FWD);
+    switch (kp) {
+      case 8: fn = reinterpret_cast<const void*>(gru_fwd_persist_kernel<8>); break;
+      case 16: fn = reinterpret_cast<const void*>(gru_fwd_persist_kernel<16>); break;
+      case 25: fn = reinterpret_cast<const void*>(gru_fwd_persist_kernel<25>); break;
+      case 32: fn = reinterpret_cast<const void*>(gru_fwd_persist_kernel<32>); break;
+      default: break;
+    }
+    if (fn != nullptr &&
+        hipLaunchCooperativeKernel(fn, dim3(grid), dim3(GT), args, 0, st) == hipSuccess)
+      return launch_status("ds2_gru_fwd");
+    (void)hipGetLastError();   // fall back to one launch per step
+  }
   for (int s = 0; s < t_max; ++s) {
     switch (ksw) {
       DS2_FWD_CASE(8) DS2_FWD_CASE(16) DS2_FWD_CASE(32) DS2_FWD_CASE(48) DS2_FWD_CASE(64)
@@ -388,8 +793,9 @@ ds2_status_t ds2_gru_fwd(int t_max, int n, int h, int num_dirs, const float* xpr
 size_t ds2_gru_bwd_workspace_size(int n, int h, int num_dirs) {
   const int64_t UB = (h + GU - 1) / GU;
   const int64_t KS = (3 * h + 3) / 4;
-  return (size_t)(num_dirs * UB * KS * 64) * sizeof(float) +
-         (size_t)2 * n * num_dirs * h * sizeof(float) + 512;
+  return align256((size_t)(num_dirs * UB * KS * 64) * sizeof(float)) +
+         align256((size_t)2 * n * num_dirs * h * sizeof(float)) + counter_bytes(n, num_dirs) +
+         512;
 }
 
 #define DS2_BWD_CASE(K)                                                                     \
@@ -418,11 +824,38 @@ ds2_status_t ds2_gru_bwd(int t_max, int n, int h, int num_dirs, const float* dy,
   const int ksw = pick_ksw((chunk_ks + GW - 1) / GW + 1);
   if (ksw < 0) return DS2_UNSUPPORTED_SHAPE;
   float* wpt = static_cast<float*>(ws);
-  size_t off = ((size_t)num_dirs * UB * KS * 64 * sizeof(float) + 255) & ~(size_t)255;
+  size_t off = align256((size_t)num_dirs * UB * KS * 64 * sizeof(float));
   float* dhs = reinterpret_cast<float*>(static_cast<char*>(ws) + off);
   hipLaunchKernelGGL(pack_bwd_kernel, dim3(grid_cap((int64_t)num_dirs * UB * KS * 64)),
                      dim3(256), 0, st, w_hh_f, w_hh_r, h, num_dirs, UB, KS, wpt);
   const int grid = mapped_grid(UB * num_dirs, BT);
+  if (persistent_enabled() && 3 * h <= KC_BWD && (h % 4) == 0 && grid <= num_cus() &&
+      (int64_t)t_max * n * num_dirs * 3 * h * 4 < (1ll << 31)) {
+    unsigned* ctrs = reinterpret_cast<unsigned*>(
+        reinterpret_cast<char*>(dhs) + align256((size_t)2 * n * num_dirs * h * sizeof(float)));
+    unsigned* err = ctrs + num_dirs * BT;
+    if (hipMemsetAsync(ctrs, 0, counter_bytes(n, num_dirs), st) != hipSuccess)
+      return launch_status("ds2_gru counters");
+    int T_ = t_max, N_ = n, H_ = h, D_ = num_dirs, UB_ = UB, BT_ = BT, DYD_ = dy_dirs;
+    void* args[] = {&T_, &N_, &H_, &D_, &UB_, &BT_, &dy, &DYD_, &wpt, &h_all, &gates, &lens,
+                    &dgates_x, &dgates_h, &ctrs, &err};
+    const void* fn = nullptr;
+    const int kp = persist_ksw((KS + GW - 1) / GW, KC_BWD);
+    switch (kp) {
+      case 8: fn = reinterpret_cast<const void*>(gru_bwd_persist_kernel<8>); break;
+      case 16: fn = reinterpret_cast<const void*>(gru_bwd_persist_kernel<16>); break;
+      case 25: fn = reinterpret_cast<const void*>(gru_bwd_persist_kernel<25>); break;
+      case 32: fn = reinterpret_cast<const void*>(gru_bwd_persist_kernel<32>); break;
+      case 48: fn = reinterpret_cast<const void*>(gru_bwd_persist_kernel<48>); break;
+      case 64: fn = reinterpret_cast<const void*>(gru_bwd_persist_kernel<64>); break;
+      case 75: fn = reinterpret_cast<const void*>(gru_bwd_persist_kernel<75>); break;
+      default: break;
+    }
+    if (fn != nullptr &&
+        hipLaunchCooperativeKernel(fn, dim3(grid), dim3(GT), args, 0, st) == hipSuccess)
+      return launch_status("ds2_gru_bwd");
+    (void)hipGetLastError();
+  }
   for (int s = 0; s < t_max; ++s) {
     switch (ksw) {
       DS2_BWD_CASE(8) DS2_BWD_CASE(16) DS2_BWD_CASE(32) DS2_BWD_CASE(48) DS2_BWD_CASE(64)

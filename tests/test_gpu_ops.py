@@ -173,6 +173,30 @@ def test_gru_layer(dev, n, t, inp, h, bidir):
         _close(wd.grad, p.grad, 1e-4, "gru " + name)
 
 
+@pytest.mark.parametrize("h", [24, 400])
+def test_gru_persistent_equals_per_step(dev, h, monkeypatch):
+    """The persistent (one launch per layer) and per-step-launch recurrences agree (their
+    K split over waves may differ, so the fp32 summation order can differ)."""
+    n, t, inp = 21, 37, 48
+    g = torch.Generator().manual_seed(h)
+    weights = [torch.rand(s, generator=g) * 0.4 - 0.2 for s in
+               [(3 * h, inp), (3 * h, h), (3 * h,), (3 * h,)] * 2]
+    lens = torch.tensor(sorted([t - (i % 7) * 3 for i in range(n)], reverse=True), dtype=torch.int32)
+    x = torch.randn(t, n, inp, generator=g)
+    dy = torch.randn(t, n, h, generator=g)
+    outs = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("DS2_GRU_PERSISTENT", flag)
+        ws = [w.to(dev).requires_grad_(True) for w in weights]
+        xd = x.to(dev).requires_grad_(True)
+        y = ops.GRULayerFn.apply(xd, lens.to(dev), True, h, *ws)
+        y.backward(dy.to(dev))
+        torch.cuda.synchronize()
+        outs.append([y.detach().cpu(), xd.grad.cpu()] + [w.grad.cpu() for w in ws])
+    for a, b in zip(*outs):
+        _close(a, b, 1e-5, "persistent vs per-step")
+
+
 def test_gru_per_direction_output(dev):
     n, t, inp, h = 4, 11, 8, 16
     g = torch.Generator().manual_seed(5)
