@@ -103,16 +103,33 @@ __global__ __launch_bounds__(256) void sgemm_kernel(
   __shared__ __attribute__((aligned(16))) float As[2][BK * LDA_S];
   __shared__ __attribute__((aligned(16))) float Bs[2][BK * LDB_S];
 
-  // blockIdx.z = batch * nsplit + split; split-K partials go to partial[z][m][n]
-  const int bz = blockIdx.z / nsplit;
-  const int sp = blockIdx.z - bz * nsplit;
+  // 1-D grid, XCD-aware (bijective) remap: the blocks the dispatcher deals to one
+  // XCD (ids congruent mod 8) get a contiguous run of tiles, n-tile fastest, so the
+  // workgroups sharing an A row panel (and a k-range) share that XCD's L2.
+  const int tn = (N + BN - 1) / BN;
+  const int tm = (M + BM - 1) / BM;
+  const int nwg = gridDim.x;
+  int wgid;
+  {
+    const int orig = blockIdx.x;
+    const int xcd = orig & 7;
+    const int q = nwg >> 3, r = nwg & 7;
+    wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+  }
+  const int z = wgid / (tm * tn);
+  const int rem = wgid - z * tm * tn;
+  const int tile_m = rem / tn;
+  const int tile_n = rem - tile_m * tn;
+  // z = batch * nsplit + split; split-K partials go to partial[z][m][n]
+  const int bz = z / nsplit;
+  const int sp = z - bz * nsplit;
   A += bz * sA;
   B += bz * sB;
   C += bz * sC;
   const int kbeg = sp * kchunk;
   const int kend = min(K, kbeg + kchunk);
-  const int m0 = blockIdx.y * BM;
-  const int n0 = blockIdx.x * BN;
+  const int m0 = tile_m * BM;
+  const int n0 = tile_n * BN;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int wm = (wave >> 1) * 64;
@@ -172,7 +189,7 @@ __global__ __launch_bounds__(256) void sgemm_kernel(
       const int col = n0 + wn + 32 * j + lr;
       if (col >= N) continue;
       if (partial != nullptr) {
-        float* pp = partial + (int64_t)blockIdx.z * M * N;
+        float* pp = partial + (int64_t)z * M * N;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int row = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lk;
@@ -265,7 +282,6 @@ extern "C" ds2_status_t ds2_sgemm_ws(int trans_a, int trans_b, int m, int n, int
   if (ldc < n) return DS2_INVALID_VALUE;
   if (trans_a ? lda < m : lda < k) return DS2_INVALID_VALUE;
   if (trans_b ? ldb < k : ldb < n) return DS2_INVALID_VALUE;
-  if (m > 65535 * BM) return DS2_UNSUPPORTED_SHAPE;
   // vector (float4) staging is legal when every float4 is fully in or out of bounds
   const bool va = aligned16(a) && (lda % 4 == 0) && (stride_a % 4 == 0) &&
                   (trans_a ? (m % 4 == 0) : (k % 4 == 0));
@@ -277,7 +293,9 @@ extern "C" ds2_status_t ds2_sgemm_ws(int trans_a, int trans_b, int m, int n, int
   const int kchunk = nsplit > 1 ? cdiv(cdiv(k, nsplit), BK) * BK : std::max(k, 1);
   nsplit = nsplit > 1 ? cdiv(k, kchunk) : 1;
   float* partial = nsplit > 1 ? static_cast<float*>(ws) : nullptr;
-  dim3 grid(cdiv(n, BN), cdiv(m, BM), batch * nsplit);
+  const int64_t nwg = (int64_t)cdiv(n, BN) * cdiv(m, BM) * batch * nsplit;
+  if (nwg > 0x7fffffff) return DS2_UNSUPPORTED_SHAPE;
+  dim3 grid(static_cast<unsigned>(nwg));
   hipStream_t st = as_stream(stream);
 #define DS2_G(TA_, TB_)                                                                       \
   launch_sgemm_t<TA_, TB_>(va, vb, grid, st, m, n, k, alpha, a, lda, stride_a, b, ldb, stride_b, \

@@ -1,0 +1,651 @@
+// (Bi)directional LSTM recurrence on MFMA (v_mfma_f32_16x16x4_f32), fp32 —
+// SURVEY §8 row a8' (reference model.py:14 supported_rnns['lstm'] = nn.LSTM).
+//
+// Same structure as gru.hip: the input projection x @ W_ih^T + b_ih (both
+// directions, 4H gate rows i, f, g, o) is a separate GEMM; this file runs the
+// sequential part.  Workgroup = (16 hidden units, direction, 16 samples); the
+// forward product is gh[16 x 64] = h_prev[16 x H] @ W_hh[64 rows (i,f,g,o of
+// the 16 units)]^T, the backward one rec[16 x 16] = dg[16 x 4H] @ W_hh[:, 16
+// units].  K is split over the 8 waves; partial tiles are reduced through LDS.
+//
+// Gate math follows ATen's LSTM cell:
+//   i = sigmoid(.), f = sigmoid(.), g = tanh(.), o = sigmoid(.)
+//   c' = f*c + i*g,  h' = o*tanh(c')
+// Packed-sequence semantics as in gru.hip: direction 1 of a sample of length len
+// starts at t = len-1 from (h, c) = 0; outputs past len are 0.
+//
+// Persistent variants (one cooperative launch per layer, W_hh in registers, the
+// hand-off of gru.hip) run when the grid fits the chip; otherwise one launch per
+// time step carries the cell state through a ping-pong buffer.
+#include "rnn_common.h"
+
+#include <algorithm>
+
+namespace ds2 {
+
+constexpr int LKC_FWD = 1024;   // max H staged in LDS (forward)
+constexpr int LKC_BWD = 2048;   // 4H columns staged per chunk (backward)
+constexpr int LRP = 4 * GU + 1; // forward reduction row pitch (4 gates x 16 units)
+
+// ---------------------------------------------------------------------------
+// shared pointwise pieces
+struct LstmFwdOut {
+  float i, f, g, o, c, h;
+};
+
+__device__ __forceinline__ LstmFwdOut lstm_cell(float ai, float af, float ag, float ao, float cp) {
+  LstmFwdOut r;
+  r.i = sigmoidf_(ai);
+  r.f = sigmoidf_(af);
+  r.g = tanhf(ag);
+  r.o = sigmoidf_(ao);
+  r.c = r.f * cp + r.i * r.g;
+  r.h = r.o * tanhf(r.c);
+  return r;
+}
+
+// d(gate pre-activations) from dh, the carried dc (= dc_{t+1} * f_{t+1}), the cached
+// activations and c_t, c_{t-1}; returns the new carry dc_t * f_t.
+__device__ __forceinline__ float lstm_cell_bwd(float dh, float dc_carry, float gi, float gf,
+                                               float gg, float go, float c, float cp,
+                                               float& dai, float& daf, float& dag, float& dao) {
+  const float tc = tanhf(c);
+  const float dc = dc_carry + dh * go * (1.f - tc * tc);
+  dao = dh * tc * go * (1.f - go);
+  dai = dc * gg * gi * (1.f - gi);
+  dag = dc * gi * (1.f - gg * gg);
+  daf = dc * cp * gf * (1.f - gf);
+  return dc * gf;
+}
+
+// ---------------------------------------------------------------------------
+// forward step (one launch per time step)
+template <int KSW>
+__global__ __launch_bounds__(GT) void lstm_fwd_step_kernel(
+    int s, int T, int N, int H, int D, int UB, int BT, const float* __restrict__ xproj,
+    const float* __restrict__ wp, const float* __restrict__ b_f, const float* __restrict__ b_r,
+    const int* __restrict__ lens, float* __restrict__ h_all, float* __restrict__ c_all,
+    float* __restrict__ gates, float* __restrict__ cs) {
+  constexpr int PITCH = LKC_FWD + 2;
+  __shared__ __attribute__((aligned(16))) float hs[GB * PITCH];
+  int ub, d, bt;
+  if (!map_work(UB * D, BT, UB, ub, d, bt)) return;
+  const int n0 = bt * GB;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int t = d == 0 ? s : T - 1 - s;
+  const int tp = d == 0 ? t - 1 : t + 1;
+  const int KS = (H + 3) / 4;
+  const int per = (KS + GW - 1) / GW;
+  const int a_ks = wave * per;
+  const int b_ks = min(KS, a_ks + per);
+
+  f32x4 acc[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (s > 0) {
+    float w[4][KSW];
+    const float* wpd = wp + ((int64_t)d * UB + ub) * KS * 4 * 64 + lane;
+#pragma unroll
+    for (int i = 0; i < KSW; ++i) {
+      const int ks = a_ks + i;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) w[g][i] = ks < b_ks ? wpd[((int64_t)ks * 4 + g) * 64] : 0.f;
+    }
+    stage_rows(h_all + ((int64_t)tp * N * D + d) * H, (int64_t)D * H, N, n0, 0, H, hs, PITCH);
+    __syncthreads();
+    const float* hrow = hs + (lane & 15) * PITCH + (lane >> 4);
+#pragma unroll
+    for (int i = 0; i < KSW; ++i) {
+      const int ks = a_ks + i;
+      if (ks < b_ks) {
+        const int k = 4 * ks;
+        const float a = (k + (lane >> 4) < H) ? hrow[k] : 0.f;
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, w[g][i], acc[g], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+  float* red = hs;
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      red[(wave * GB + (lane >> 4) * 4 + r) * LRP + g * GU + (lane & 15)] = acc[g][r];
+  __syncthreads();
+  if (threadIdx.x >= GB * GU) return;
+  const int m = threadIdx.x >> 4;
+  const int u = threadIdx.x & 15;
+  const int n = n0 + m;
+  const int j = ub * GU + u;
+  if (n >= N || j >= H) return;
+  const int64_t row = ((int64_t)t * N + n) * D + d;
+  const int64_t cidx = (int64_t)n * D * H + (int64_t)d * H + j;
+  const int64_t plane = (int64_t)N * D * H;
+  LstmFwdOut o{0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (t < lens[n]) {
+    float gh[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      float v = 0.f;
+#pragma unroll
+      for (int w8 = 0; w8 < GW; ++w8) v += red[(w8 * GB + m) * LRP + g * GU + u];
+      gh[g] = v;
+    }
+    const float* bh = d == 0 ? b_f : b_r;
+    const float* xp = xproj + row * 4 * H;
+    const float cp = s > 0 ? cs[((s + 1) & 1) * plane + cidx] : 0.f;
+    o = lstm_cell(gh[0] + bh[j] + xp[j], gh[1] + bh[H + j] + xp[H + j],
+                  gh[2] + bh[2 * H + j] + xp[2 * H + j], gh[3] + bh[3 * H + j] + xp[3 * H + j],
+                  cp);
+  }
+  cs[(s & 1) * plane + cidx] = o.c;
+  h_all[row * H + j] = o.h;
+  if (c_all != nullptr) c_all[row * H + j] = o.c;
+  if (gates != nullptr) {
+    float* gp = gates + row * 4 * H;
+    gp[j] = o.i;
+    gp[H + j] = o.f;
+    gp[2 * H + j] = o.g;
+    gp[3 * H + j] = o.o;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// backward step (BPTT, one launch per time step)
+template <int KSW>
+__global__ __launch_bounds__(GT) void lstm_bwd_step_kernel(
+    int s, int T, int N, int H, int D, int UB, int BT, const float* __restrict__ dy, int dyd,
+    const float* __restrict__ wpt, const float* __restrict__ c_all,
+    const float* __restrict__ gates, const int* __restrict__ lens, float* __restrict__ dg,
+    float* __restrict__ dcs) {
+  constexpr int PITCH = LKC_BWD + 2;
+  __shared__ __attribute__((aligned(16))) float hs[GB * PITCH];
+  int ub, d, bt;
+  if (!map_work(UB * D, BT, UB, ub, d, bt)) return;
+  const int n0 = bt * GB;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int t = d == 0 ? T - 1 - s : s;
+  const int tq = d == 0 ? t + 1 : t - 1;
+  const int H4 = 4 * H;
+  const int KS = H;   // (4H + 3) / 4
+
+  f32x4 acc0 = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 acc1 = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (s > 0) {
+    const float* dgq = dg + ((int64_t)tq * N * D + d) * H4;
+    const float* wpd = wpt + ((int64_t)d * UB + ub) * KS * 64 + lane;
+    for (int kc0 = 0; kc0 < H4; kc0 += LKC_BWD) {
+      const int kc1 = min(H4, kc0 + LKC_BWD);
+      const int ks0 = kc0 / 4;
+      const int ks1 = kc1 / 4;
+      const int per = (ks1 - ks0 + GW - 1) / GW;
+      const int a_ks = ks0 + wave * per;
+      const int b_ks = min(ks1, a_ks + per);
+      float w[KSW];
+#pragma unroll
+      for (int i = 0; i < KSW; ++i) {
+        const int ks = a_ks + i;
+        w[i] = ks < b_ks ? wpd[(int64_t)ks * 64] : 0.f;
+      }
+      if (kc0 > 0) __syncthreads();
+      stage_rows(dgq, (int64_t)D * H4, N, n0, kc0, kc1, hs, PITCH);
+      __syncthreads();
+      const float* hrow = hs + (lane & 15) * PITCH + (lane >> 4) - kc0;
+#pragma unroll
+      for (int i = 0; i < KSW; i += 2) {
+        const int ks = a_ks + i;
+        if (ks < b_ks) acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(hrow[4 * ks], w[i], acc0, 0, 0, 0);
+        if (i + 1 < KSW && ks + 1 < b_ks)
+          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(hrow[4 * ks + 4], w[i + 1], acc1, 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+  float* red = hs;
+  constexpr int RP = GU + 1;
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+    red[(wave * GB + (lane >> 4) * 4 + r) * RP + (lane & 15)] = acc0[r] + acc1[r];
+  __syncthreads();
+  if (threadIdx.x >= GB * GU) return;
+  const int m = threadIdx.x >> 4;
+  const int u = threadIdx.x & 15;
+  const int n = n0 + m;
+  const int j = ub * GU + u;
+  if (n >= N || j >= H) return;
+  const int64_t row = ((int64_t)t * N + n) * D + d;
+  const int64_t cidx = (int64_t)n * D * H + (int64_t)d * H + j;
+  const int64_t plane = (int64_t)N * D * H;
+  float dai = 0.f, daf = 0.f, dag = 0.f, dao = 0.f, carry = 0.f;
+  if (t < lens[n]) {
+    float rec = 0.f, dcc = 0.f;
+    if (s > 0) {
+#pragma unroll
+      for (int w8 = 0; w8 < GW; ++w8) rec += red[(w8 * GB + m) * RP + u];
+      dcc = dcs[((s + 1) & 1) * plane + cidx];
+    }
+    const float dh = dy[(((int64_t)t * N + n) * dyd + (dyd > 1 ? d : 0)) * H + j] + rec;
+    const float* gp = gates + row * 4 * H;
+    const int tp = d == 0 ? t - 1 : t + 1;
+    const float cp = (tp >= 0 && tp < T) ? c_all[(((int64_t)tp * N + n) * D + d) * H + j] : 0.f;
+    carry = lstm_cell_bwd(dh, dcc, gp[j], gp[H + j], gp[2 * H + j], gp[3 * H + j],
+                          c_all[row * H + j], cp, dai, daf, dag, dao);
+  }
+  dcs[(s & 1) * plane + cidx] = carry;
+  float* go = dg + row * H4;
+  go[j] = dai;
+  go[H + j] = daf;
+  go[2 * H + j] = dag;
+  go[3 * H + j] = dao;
+}
+
+// ---------------------------------------------------------------------------
+// persistent forward: W_hh fragments (4 gates x KSW k-steps) in registers, cell
+// state in a register of the owning thread, h hand-off through sc1 stores +
+// per-(direction, batch tile) arrival counters.
+template <int KSW>
+__global__ __launch_bounds__(GT) void lstm_fwd_persist_kernel(
+    int T, int N, int H, int D, int UB, int BT, const float* __restrict__ xproj,
+    const float* __restrict__ wp, const float* __restrict__ b_f, const float* __restrict__ b_r,
+    const int* __restrict__ lens, float* __restrict__ h_all, float* __restrict__ c_all,
+    float* __restrict__ gates, unsigned* __restrict__ counters, unsigned* __restrict__ err) {
+  constexpr int PITCH = LKC_FWD + 4;
+  __shared__ __attribute__((aligned(16))) float hs[GB * PITCH];
+  __shared__ float red[GW * GB * LRP];
+  __shared__ int flag;
+  int ub, d, bt;
+  if (!map_work(UB * D, BT, UB, ub, d, bt)) return;
+  const int n0 = bt * GB;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int KS = H / 4;                    // host guarantees H % 4 == 0, GW * KSW >= KS
+  const int a_ks = wave * KSW;
+  const int b_ks = min(KS, a_ks + KSW);
+  unsigned* ctr = counters + d * BT + bt;
+  const __amdgpu_buffer_rsrc_t h_rs = __builtin_amdgcn_make_buffer_rsrc(
+      h_all, (short)0, T * N * D * H * 4, 0x00020000);
+
+  float w[4][KSW];
+  {
+    const float* wpd = wp + ((int64_t)d * UB + ub) * KS * 4 * 64 + lane;
+#pragma unroll
+    for (int i = 0; i < KSW; ++i) {
+      const int ks = a_ks + i;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) w[g][i] = ks < b_ks ? wpd[((int64_t)ks * 4 + g) * 64] : 0.f;
+    }
+  }
+  const float* bh = d == 0 ? b_f : b_r;
+  const int m = threadIdx.x >> 4;
+  const int u = threadIdx.x & 15;
+  const int n = n0 + m;
+  const int j = ub * GU + u;
+  const bool owner = threadIdx.x < GB * GU && n < N && j < H;
+  float bias[4] = {0.f, 0.f, 0.f, 0.f};
+  int len = 0;
+  if (owner) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) bias[g] = bh[g * H + j];
+    len = lens[n];
+  }
+  float c = 0.f;
+  LstmFwdOut prev{0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  int64_t prev_row = -1;
+  for (int s = 0; s < T; ++s) {
+    const int t = d == 0 ? s : T - 1 - s;
+    const int tp = d == 0 ? t - 1 : t + 1;
+    const int64_t row = ((int64_t)t * N + n) * D + d;
+    float xg[4] = {0.f, 0.f, 0.f, 0.f};
+    if (owner && t < len) {
+      const float* xp = xproj + row * 4 * H;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) xg[g] = xp[g * H + j];
+    }
+    f32x4 acc[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (s > 0) {
+      if (!group_wait(ctr, (unsigned)s * UB, err, &flag)) return;
+      stage_rows_sc1<(GB * LKC_FWD / 4 + GT - 1) / GT>(h_all + ((int64_t)tp * N * D + d) * H,
+                                                        D * H, N, n0, H, 4 * GW * KSW, hs, PITCH);
+      __syncthreads();
+      const float* hrow = hs + (lane & 15) * PITCH + (lane >> 4) + 4 * a_ks;
+#pragma unroll
+      for (int i = 0; i < KSW; ++i) {
+        const float a = hrow[4 * i];
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, w[g][i], acc[g], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        red[(wave * GB + (lane >> 4) * 4 + r) * LRP + g * GU + (lane & 15)] = acc[g][r];
+    __syncthreads();
+    if (owner) {
+      LstmFwdOut o{0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if (t < len) {
+        float gh[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          float v = 0.f;
+#pragma unroll
+          for (int w8 = 0; w8 < GW; ++w8) v += red[(w8 * GB + m) * LRP + g * GU + u];
+          gh[g] = v + bias[g] + xg[g];
+        }
+        o = lstm_cell(gh[0], gh[1], gh[2], gh[3], c);
+      }
+      c = o.c;
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, o.h), h_rs,
+                                            static_cast<int>((row * H + j) * 4), 0, kSc1);
+      prev = o;
+      prev_row = row;
+    }
+    group_arrive(ctr);
+    // backward-only caches, off the critical path
+    if (owner) {
+      if (c_all != nullptr) c_all[prev_row * H + j] = prev.c;
+      if (gates != nullptr) {
+        float* gp = gates + prev_row * 4 * H;
+        gp[j] = prev.i;
+        gp[H + j] = prev.f;
+        gp[2 * H + j] = prev.g;
+        gp[3 * H + j] = prev.o;
+      }
+    }
+  }
+}
+
+// persistent backward: W_hh^T fragments for NCH chunks of 4*GW*KSWC gate columns in
+// registers; dc carried in a register; gate gradients handed off through sc1 stores.
+template <int KSWC, int NCH>
+__global__ __launch_bounds__(GT) void lstm_bwd_persist_kernel(
+    int T, int N, int H, int D, int UB, int BT, const float* __restrict__ dy, int dyd,
+    const float* __restrict__ wpt, const float* __restrict__ c_all,
+    const float* __restrict__ gates, const int* __restrict__ lens, float* __restrict__ dg,
+    unsigned* __restrict__ counters, unsigned* __restrict__ err) {
+  constexpr int CW = 4 * GW * KSWC;         // gate columns per chunk (<= LKC_BWD)
+  constexpr int PITCH = CW + 4;
+  __shared__ __attribute__((aligned(16))) float hs[GB * PITCH];
+  float* red = hs;                          // reduction buffer aliases the staged rows
+  __shared__ int flag;
+  int ub, d, bt;
+  if (!map_work(UB * D, BT, UB, ub, d, bt)) return;
+  const int n0 = bt * GB;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int H4 = 4 * H;
+  const int KS = H;
+  unsigned* ctr = counters + d * BT + bt;
+  const __amdgpu_buffer_rsrc_t g_rs = __builtin_amdgcn_make_buffer_rsrc(
+      dg, (short)0, T * N * D * H4 * 4, 0x00020000);
+
+  float w[NCH][KSWC];
+  {
+    const float* wpd = wpt + ((int64_t)d * UB + ub) * KS * 64 + lane;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c)
+#pragma unroll
+      for (int i = 0; i < KSWC; ++i) {
+        const int ks = c * (CW / 4) + wave * KSWC + i;
+        w[c][i] = ks < KS ? wpd[(int64_t)ks * 64] : 0.f;
+      }
+  }
+  const int m = threadIdx.x >> 4;
+  const int u = threadIdx.x & 15;
+  const int n = n0 + m;
+  const int j = ub * GU + u;
+  const bool owner = threadIdx.x < GB * GU && n < N && j < H;
+  const int len = owner ? lens[n] : 0;
+  constexpr int RP = GU + 1;
+  float carry = 0.f;
+
+  for (int s = 0; s < T; ++s) {
+    const int t = d == 0 ? T - 1 - s : s;
+    // inputs of this step that do not depend on other workgroups: issue first
+    float dyv = 0.f, gi = 0.f, gf = 0.f, gg = 0.f, go = 0.f, cc = 0.f, cp = 0.f;
+    const int64_t row = ((int64_t)t * N + n) * D + d;
+    if (owner && t < len) {
+      dyv = dy[(((int64_t)t * N + n) * dyd + (dyd > 1 ? d : 0)) * H + j];
+      const float* gp = gates + row * 4 * H;
+      gi = gp[j];
+      gf = gp[H + j];
+      gg = gp[2 * H + j];
+      go = gp[3 * H + j];
+      cc = c_all[row * H + j];
+      const int tp = d == 0 ? t - 1 : t + 1;
+      if (tp >= 0 && tp < T) cp = c_all[(((int64_t)tp * N + n) * D + d) * H + j];
+    }
+    f32x4 acc0 = f32x4{0.f, 0.f, 0.f, 0.f};
+    f32x4 acc1 = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (s > 0) {
+      const int tq = d == 0 ? t + 1 : t - 1;
+      if (!group_wait(ctr, (unsigned)s * UB, err, &flag)) return;
+      const float* dgq = dg + ((int64_t)tq * N * D + d) * H4;
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) {
+        if (c > 0) __syncthreads();
+        const int c0 = c * CW;
+        // two half-chunk stagings keep the in-flight load registers bounded
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+          const int off = c0 + hh * (CW / 2);
+          stage_rows_sc1<(GB * CW / 8 + GT - 1) / GT>(dgq + off, D * H4, N, n0,
+                                                      max(0, min(H4 - off, CW / 2)), CW / 2,
+                                                      hs + hh * (CW / 2), PITCH);
+        }
+        __syncthreads();
+        const float* hrow = hs + (lane & 15) * PITCH + (lane >> 4) + 4 * wave * KSWC;
+#pragma unroll
+        for (int i = 0; i < KSWC; i += 2) {
+          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(hrow[4 * i], w[c][i], acc0, 0, 0, 0);
+          if (i + 1 < KSWC)
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(hrow[4 * i + 4], w[c][i + 1], acc1, 0, 0,
+                                                        0);
+        }
+      }
+      __syncthreads();                      // all reads of hs done before red overwrites it
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      red[(wave * GB + (lane >> 4) * 4 + r) * RP + (lane & 15)] = acc0[r] + acc1[r];
+    __syncthreads();
+    if (owner) {
+      float dai = 0.f, daf = 0.f, dag = 0.f, dao = 0.f;
+      if (t < len) {
+        float rec = 0.f;
+#pragma unroll
+        for (int w8 = 0; w8 < GW; ++w8) rec += red[(w8 * GB + m) * RP + u];
+        carry = lstm_cell_bwd(dyv + rec, carry, gi, gf, gg, go, cc, cp, dai, daf, dag, dao);
+      } else {
+        carry = 0.f;
+      }
+      const int o = static_cast<int>((row * H4 + j) * 4);
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, dai), g_rs, o, 0, kSc1);
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, daf), g_rs, o + 4 * H, 0,
+                                            kSc1);
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, dag), g_rs, o + 8 * H, 0,
+                                            kSc1);
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, dao), g_rs, o + 12 * H, 0,
+                                            kSc1);
+    }
+    group_arrive(ctr);
+  }
+}
+
+// per-step kernels: forward needs <= 32 (H <= 1024), backward <= 64 (2048-column chunks)
+static int lstm_pick_ksw(int per) {
+  const int opts[] = {8, 16, 32, 64};
+  for (int k : opts)
+    if (per <= k) return k;
+  return -1;
+}
+
+}  // namespace ds2
+
+using namespace ds2;
+
+extern "C" {
+
+static inline size_t lstm_counter_bytes(int n, int num_dirs) {
+  return align256((size_t)(num_dirs * ((n + GB - 1) / GB) + 1) * sizeof(unsigned));
+}
+
+size_t ds2_lstm_fwd_workspace_size(int n, int h, int num_dirs) {
+  const int64_t UB = (h + GU - 1) / GU;
+  const int64_t KS = (h + 3) / 4;
+  return align256((size_t)(num_dirs * UB * KS * 4 * 64) * sizeof(float)) +
+         align256((size_t)2 * n * num_dirs * h * sizeof(float)) + lstm_counter_bytes(n, num_dirs) +
+         256;
+}
+
+#define DS2_LFWD_CASE(K)                                                                    \
+  case K:                                                                                   \
+    hipLaunchKernelGGL(lstm_fwd_step_kernel<K>, dim3(grid), dim3(GT), 0, st, s, t_max, n, h, \
+                       num_dirs, UB, BT, xproj, wp, b_hh_f, b_hh_r, lens, h_all, c_all, gates, \
+                       cs);                                                                 \
+    break;
+
+ds2_status_t ds2_lstm_fwd(int t_max, int n, int h, int num_dirs, const float* xproj,
+                          const float* w_hh_f, const float* w_hh_r, const float* b_hh_f,
+                          const float* b_hh_r, const int* lens, float* h_all, float* c_all,
+                          float* gates, void* ws, size_t ws_bytes, ds2_stream_t stream) {
+  if (t_max < 0 || n < 0 || h < 1 || (num_dirs != 1 && num_dirs != 2)) return DS2_INVALID_VALUE;
+  if (h > LKC_FWD) return DS2_UNSUPPORTED_SHAPE;
+  if (t_max == 0 || n == 0) return DS2_OK;
+  if (ws == nullptr || ws_bytes < ds2_lstm_fwd_workspace_size(n, h, num_dirs))
+    return DS2_WORKSPACE_TOO_SMALL;
+  if (num_dirs == 1) {
+    w_hh_r = w_hh_f;
+    b_hh_r = b_hh_f;
+  }
+  hipStream_t st = as_stream(stream);
+  const int UB = (h + GU - 1) / GU;
+  const int KS = (h + 3) / 4;
+  const int BT = (n + GB - 1) / GB;
+  const int ksw = lstm_pick_ksw((KS + GW - 1) / GW);
+  if (ksw < 0 || ksw > 32) return DS2_UNSUPPORTED_SHAPE;
+  float* wp = static_cast<float*>(ws);
+  size_t off = align256((size_t)num_dirs * UB * KS * 4 * 64 * sizeof(float));
+  float* cs = reinterpret_cast<float*>(static_cast<char*>(ws) + off);
+  off += align256((size_t)2 * n * num_dirs * h * sizeof(float));
+  unsigned* ctrs = reinterpret_cast<unsigned*>(static_cast<char*>(ws) + off);
+  hipLaunchKernelGGL(pack_fwd_kernel<4>, dim3(grid_cap((int64_t)num_dirs * UB * KS * 256)),
+                     dim3(256), 0, st, w_hh_f, w_hh_r, h, num_dirs, UB, KS, wp);
+  const int grid = mapped_grid(UB * num_dirs, BT);
+  const int kp = persist_ksw((KS + GW - 1) / GW, LKC_FWD);
+  if (persistent_enabled() && (h % 4) == 0 && grid <= num_cus() && kp > 0 && kp <= 32 &&
+      (int64_t)t_max * n * num_dirs * h * 4 < (1ll << 31)) {
+    unsigned* err = ctrs + num_dirs * BT;
+    if (hipMemsetAsync(ctrs, 0, lstm_counter_bytes(n, num_dirs), st) != hipSuccess)
+      return launch_status("ds2_lstm counters");
+    int T_ = t_max, N_ = n, H_ = h, D_ = num_dirs, UB_ = UB, BT_ = BT;
+    void* args[] = {&T_, &N_, &H_, &D_, &UB_, &BT_, &xproj, &wp, &b_hh_f, &b_hh_r, &lens,
+                    &h_all, &c_all, &gates, &ctrs, &err};
+    const void* fn = nullptr;
+    switch (kp) {
+      case 8: fn = reinterpret_cast<const void*>(lstm_fwd_persist_kernel<8>); break;
+      case 16: fn = reinterpret_cast<const void*>(lstm_fwd_persist_kernel<16>); break;
+      case 25: fn = reinterpret_cast<const void*>(lstm_fwd_persist_kernel<25>); break;
+      case 32: fn = reinterpret_cast<const void*>(lstm_fwd_persist_kernel<32>); break;
+      default: break;
+    }
+    if (fn != nullptr &&
+        hipLaunchCooperativeKernel(fn, dim3(grid), dim3(GT), args, 0, st) == hipSuccess)
+      return launch_status("ds2_lstm_fwd");
+    (void)hipGetLastError();   // fall back to one launch per step
+  }
+  for (int s = 0; s < t_max; ++s) {
+    switch (ksw) {
+      DS2_LFWD_CASE(8) DS2_LFWD_CASE(16) DS2_LFWD_CASE(32)
+    }
+  }
+  return launch_status("ds2_lstm_fwd");
+}
+
+size_t ds2_lstm_bwd_workspace_size(int n, int h, int num_dirs) {
+  const int64_t UB = (h + GU - 1) / GU;
+  const int64_t KS = h;
+  return align256((size_t)(num_dirs * UB * KS * 64) * sizeof(float)) +
+         align256((size_t)2 * n * num_dirs * h * sizeof(float)) + lstm_counter_bytes(n, num_dirs) +
+         256;
+}
+
+#define DS2_LBWD_CASE(K)                                                                    \
+  case K:                                                                                   \
+    hipLaunchKernelGGL(lstm_bwd_step_kernel<K>, dim3(grid), dim3(GT), 0, st, s, t_max, n, h, \
+                       num_dirs, UB, BT, dy, dy_dirs, wpt, c_all, gates, lens, dgates, dcs);  \
+    break;
+
+ds2_status_t ds2_lstm_bwd(int t_max, int n, int h, int num_dirs, const float* dy, int dy_dirs,
+                          const float* w_hh_f, const float* w_hh_r, const float* c_all,
+                          const float* gates, const int* lens, float* dgates, void* ws,
+                          size_t ws_bytes, ds2_stream_t stream) {
+  if (t_max < 0 || n < 0 || h < 1 || (num_dirs != 1 && num_dirs != 2)) return DS2_INVALID_VALUE;
+  if (t_max == 0 || n == 0) return DS2_OK;
+  if (gates == nullptr || c_all == nullptr) return DS2_INVALID_VALUE;
+  if (dy_dirs != 1 && dy_dirs != num_dirs) return DS2_INVALID_VALUE;
+  if (ws == nullptr || ws_bytes < ds2_lstm_bwd_workspace_size(n, h, num_dirs))
+    return DS2_WORKSPACE_TOO_SMALL;
+  if (num_dirs == 1) w_hh_r = w_hh_f;
+  hipStream_t st = as_stream(stream);
+  const int UB = (h + GU - 1) / GU;
+  const int KS = h;
+  const int BT = (n + GB - 1) / GB;
+  const int chunk_ks = std::min(4 * h, LKC_BWD) / 4;
+  const int ksw = lstm_pick_ksw((chunk_ks + GW - 1) / GW);
+  if (ksw < 0) return DS2_UNSUPPORTED_SHAPE;
+  float* wpt = static_cast<float*>(ws);
+  size_t off = align256((size_t)num_dirs * UB * KS * 64 * sizeof(float));
+  float* dcs = reinterpret_cast<float*>(static_cast<char*>(ws) + off);
+  off += align256((size_t)2 * n * num_dirs * h * sizeof(float));
+  unsigned* ctrs = reinterpret_cast<unsigned*>(static_cast<char*>(ws) + off);
+  hipLaunchKernelGGL(pack_bwd_kernel<4>, dim3(grid_cap((int64_t)num_dirs * UB * KS * 64)),
+                     dim3(256), 0, st, w_hh_f, w_hh_r, h, num_dirs, UB, KS, wpt);
+  const int grid = mapped_grid(UB * num_dirs, BT);
+  if (persistent_enabled() && (h % 4) == 0 && grid <= num_cus() &&
+      (int64_t)t_max * n * num_dirs * 4 * h * 4 < (1ll << 31)) {
+    // smallest (k-steps per wave per chunk, chunks) covering 4H gate columns
+    const int opts[] = {8, 16, 25, 32, 48, 64};
+    int kswc = -1, nch = -1;
+    for (int c = 1; c <= 2 && kswc < 0; ++c)
+      for (int k : opts)
+        if (c * 4 * GW * k >= 4 * h) {
+          kswc = k;
+          nch = c;
+          break;
+        }
+    const void* fn = nullptr;
+#define DS2_LBP(K, C)                                                      \
+  if (kswc == K && nch == C)                                               \
+    fn = reinterpret_cast<const void*>(lstm_bwd_persist_kernel<K, C>);
+    DS2_LBP(8, 1) DS2_LBP(16, 1) DS2_LBP(25, 1) DS2_LBP(32, 1) DS2_LBP(48, 1) DS2_LBP(64, 1)
+    DS2_LBP(48, 2) DS2_LBP(64, 2)
+#undef DS2_LBP
+    if (fn != nullptr) {
+      unsigned* err = ctrs + num_dirs * BT;
+      if (hipMemsetAsync(ctrs, 0, lstm_counter_bytes(n, num_dirs), st) != hipSuccess)
+        return launch_status("ds2_lstm counters");
+      int T_ = t_max, N_ = n, H_ = h, D_ = num_dirs, UB_ = UB, BT_ = BT, DYD_ = dy_dirs;
+      void* args[] = {&T_, &N_, &H_, &D_, &UB_, &BT_, &dy, &DYD_, &wpt, &c_all, &gates, &lens,
+                      &dgates, &ctrs, &err};
+      if (hipLaunchCooperativeKernel(fn, dim3(grid), dim3(GT), args, 0, st) == hipSuccess)
+        return launch_status("ds2_lstm_bwd");
+      (void)hipGetLastError();
+    }
+  }
+  for (int s = 0; s < t_max; ++s) {
+    switch (ksw) {
+      DS2_LBWD_CASE(8) DS2_LBWD_CASE(16) DS2_LBWD_CASE(32) DS2_LBWD_CASE(64)
+    }
+  }
+  return launch_status("ds2_lstm_bwd");
+}
+
+}  // extern "C"

@@ -1,0 +1,227 @@
+// Shared pieces of the recurrent kernels (gru.hip, lstm.hip): the workgroup
+// tiling constants, W_hh repacking into MFMA-fragment order, XCD-aware work
+// mapping, LDS staging, and the inter-workgroup hand-off of the persistent
+// kernels (MI355X_MICROARCH.md "Valid forms" row 1).
+#pragma once
+
+#include "common.h"
+
+#include <cstdlib>
+
+namespace ds2 {
+
+constexpr int GU = 16;      // hidden units per workgroup
+constexpr int GB = 16;      // samples per workgroup
+constexpr int GW = 8;       // waves per workgroup (K split 8 ways)
+constexpr int GT = GW * 64; // threads per workgroup
+
+// Wp[d][ub][ks][g][64] (G gates): lane l of k-step ks, gate g ->
+//   W_hh_d[g*H + ub*16 + (l&15)][4*ks + (l>>4)]
+template <int G>
+__global__ void pack_fwd_kernel(const float* __restrict__ w_f, const float* __restrict__ w_r,
+                                int H, int D, int UB, int KS, float* __restrict__ wp) {
+  const int64_t total = (int64_t)D * UB * KS * G * 64;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t r = i;
+    const int l = r % 64; r /= 64;
+    const int g = r % G; r /= G;
+    const int ks = r % KS; r /= KS;
+    const int ub = r % UB; r /= UB;
+    const int d = static_cast<int>(r);
+    const float* w = d == 0 ? w_f : w_r;
+    const int u = ub * GU + (l & 15);
+    const int k = 4 * ks + (l >> 4);
+    wp[i] = (u < H && k < H) ? w[(int64_t)(g * H + u) * H + k] : 0.f;
+  }
+}
+
+// WpT[d][ub][ks][64] (W_hh has G*H rows): lane l of k-step ks ->
+//   W_hh_d[4*ks + (l>>4)][ub*16 + (l&15)]
+template <int G>
+__global__ void pack_bwd_kernel(const float* __restrict__ w_f, const float* __restrict__ w_r,
+                                int H, int D, int UB, int KS, float* __restrict__ wp) {
+  const int64_t total = (int64_t)D * UB * KS * 64;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t r = i;
+    const int l = r % 64; r /= 64;
+    const int ks = r % KS; r /= KS;
+    const int ub = r % UB; r /= UB;
+    const int d = static_cast<int>(r);
+    const float* w = d == 0 ? w_f : w_r;
+    const int u = ub * GU + (l & 15);
+    const int k = 4 * ks + (l >> 4);
+    wp[i] = (u < H && k < G * H) ? w[(int64_t)k * H + u] : 0.f;
+  }
+}
+
+// Stage rows [n0, n0+16) x cols [kc0, kc1) of a row-major matrix (row stride ld,
+// valid rows < N) into hs[m][pitch], zero-filled.  8-byte accesses.
+__device__ __forceinline__ void stage_rows(const float* __restrict__ src, int64_t ld, int N,
+                                           int n0, int kc0, int kc1, float* __restrict__ hs,
+                                           int pitch) {
+  const int width = kc1 - kc0;
+  const int pairs = (width + 1) >> 1;
+  for (int i = threadIdx.x; i < GB * pairs; i += blockDim.x) {
+    const int m = i / pairs;
+    const int kp = (i - m * pairs) * 2;
+    const int n = n0 + m;
+    float2 v = make_float2(0.f, 0.f);
+    if (n < N) {
+      const float* p = src + (int64_t)n * ld + kc0 + kp;
+      v.x = p[0];
+      v.y = (kp + 1 < width) ? p[1] : 0.f;
+    }
+    *reinterpret_cast<float2*>(hs + m * pitch + kp) = v;
+  }
+}
+
+// XCD-aware work mapping: the batch tiles of one (unit block, direction) pair run
+// on the same XCD (blocks b and b+8 share one under the observed round-robin
+// dispatch), and a pair keeps its XCD across the per-step launches, so its W_hh
+// slice stays resident in that XCD's L2.  Speed only, never correctness.
+__device__ __forceinline__ bool map_work(int P, int BT, int UB, int& ub, int& d, int& bt) {
+  const int wg = blockIdx.x;
+  const int xcd = wg & 7;
+  const int slot = wg >> 3;
+  const int pair = xcd + 8 * (slot / BT);
+  bt = slot - (slot / BT) * BT;
+  if (pair >= P) return false;
+  ub = pair % UB;
+  d = pair / UB;
+  return true;
+}
+
+static inline int mapped_grid(int P, int BT) { return 8 * ((P + 7) / 8) * BT; }
+
+
+// ===========================================================================
+// Persistent variants: one launch per layer and direction pair.  Each workgroup
+// keeps its W_hh fragments in registers for all T steps; the per-step hand-off of
+// the new hidden states (forward) / gate gradients (backward) between the UB
+// workgroups of a (direction, batch tile) group follows the write-through form
+// of MI355X_MICROARCH.md "Valid forms" row 1: payload stored sc1 (agent-scope
+// relaxed atomic stores), every storing wave drains vmcnt, workgroup barrier,
+// one lane adds to the group's arrival counter (agent atomic); consumers poll
+// that counter relaxed (one lane, s_sleep, bounded), barrier, then load the
+// payload with sc1 (agent-scope relaxed atomic) loads.  Counters are zeroed by
+// a hipMemsetAsync before every launch; a spin that exceeds its bound sets the
+// error word and the workgroup leaves (no hang, results invalid).
+constexpr unsigned kSpinLimit = 1u << 21;
+
+__device__ __forceinline__ void st_sc1(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ unsigned long long ld_sc1_u64(const float* p) {
+  return __hip_atomic_load(reinterpret_cast<const unsigned long long*>(p), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ float ld_sc1(const float* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// thread 0 waits until *ctr >= target; returns false (for the whole workgroup) on timeout
+__device__ __forceinline__ bool group_wait(unsigned* ctr, unsigned target, unsigned* err,
+                                           int* lds_flag) {
+  if (threadIdx.x == 0) {
+    unsigned spins = 0;
+    int ok = 1;
+    while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++spins > kSpinLimit || __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+        __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ok = 0;
+        break;
+      }
+    }
+    *lds_flag = ok;
+  }
+  __syncthreads();
+  return *lds_flag != 0;
+}
+
+__device__ __forceinline__ void group_arrive(unsigned* ctr) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains first
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+constexpr int kSc1 = 16;   // buffer-op aux bit: sc1 (write-through store / L1-bypassing load)
+
+// Stage rows [n0, n0+16) x [0, cols) of a row-major slab (row stride ld floats, N
+// valid rows, `width` valid columns) into hs[m][pitch] with 16-byte sc1 buffer loads.
+// Rows >= N and columns >= width read as zero (out-of-range buffer offsets return
+// 0), so the MFMA loop needs no bounds checks.  All MAXI loads of a thread are
+// issued before the first LDS store.  width, cols and ld are multiples of 4.
+template <int MAXI>
+__device__ __forceinline__ void stage_rows_sc1(const float* src, int ld, int N, int n0,
+                                               int width, int cols, float* __restrict__ hs,
+                                               int pitch) {
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(src), (short)0, N * ld * 4, 0x00020000);
+  const int q = cols >> 2;
+  const int total = GB * q;
+  u32x4 v[MAXI];
+#pragma unroll
+  for (int r = 0; r < MAXI; ++r) {
+    const int i = threadIdx.x + r * GT;
+    int off = 0x7ffffff0;
+    if (i < total) {
+      const int m = i / q;
+      const int k = (i - m * q) * 4;
+      if (k < width) off = ((n0 + m) * ld + k) * 4;
+    }
+    v[r] = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, kSc1);
+  }
+#pragma unroll
+  for (int r = 0; r < MAXI; ++r) {
+    const int i = threadIdx.x + r * GT;
+    if (i < total) {
+      const int m = i / q;
+      const int k = (i - m * q) * 4;
+      *reinterpret_cast<u32x4*>(hs + m * pitch + k) = v[r];
+    }
+  }
+}
+
+// phase stamps (diagnostic, DS2_GRU_STAMPS=1): workgroup 0, thread 0 accumulates
+// s_memtime deltas per phase into stamps[0..7] (units: shader clocks)
+__device__ __forceinline__ unsigned long long stamp_now() { return __builtin_amdgcn_s_memtime(); }
+
+static int g_num_cus = -1;
+static int num_cus() {
+  if (g_num_cus < 0) {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) v = 0;
+    g_num_cus = v;
+  }
+  return g_num_cus;
+}
+
+// smallest instantiated k-steps-per-wave >= per whose zero-padded span fits the LDS pitch
+static int persist_ksw(int per, int kc) {
+  const int opts[] = {8, 16, 25, 32, 48, 64, 75};
+  for (int k : opts)
+    if (per <= k && 4 * GW * k <= kc) return k;
+  return -1;
+}
+
+static bool persistent_enabled() {
+  const char* e = getenv("DS2_RNN_PERSISTENT");
+  return !(e != nullptr && e[0] == '0');
+}
+
+static inline int grid_cap(int64_t work) {
+  int64_t g = (work + 255) / 256;
+  return static_cast<int>(g > 2048 ? 2048 : (g < 1 ? 1 : g));
+}
+
+static inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+
+}  // namespace ds2

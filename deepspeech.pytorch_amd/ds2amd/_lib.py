@@ -54,6 +54,17 @@ _PROTOS = {
     "ds2_gru_bwd_workspace_size": (_sz, [_c_int, _c_int, _c_int]),
     "ds2_gru_bwd": (_c_int, [_c_int, _c_int, _c_int, _c_int, _vp, _c_int, _vp, _vp, _vp, _vp,
                              _vp, _vp, _vp, _vp, _sz, _vp]),
+    "ds2_lstm_fwd_workspace_size": (_sz, [_c_int, _c_int, _c_int]),
+    "ds2_lstm_fwd": (_c_int, [_c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                              _vp, _vp, _vp, _sz, _vp]),
+    "ds2_lstm_bwd_workspace_size": (_sz, [_c_int, _c_int, _c_int]),
+    "ds2_lstm_bwd": (_c_int, [_c_int, _c_int, _c_int, _c_int, _vp, _c_int, _vp, _vp, _vp, _vp,
+                              _vp, _vp, _vp, _sz, _vp]),
+    "ds2_lookahead_fwd": (_c_int, [_vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_f,
+                                   _c_f, _vp, _vp]),
+    "ds2_lookahead_bwd_workspace_size": (_sz, [_c_int, _c_int, _c_int, _c_int]),
+    "ds2_lookahead_bwd": (_c_int, [_vp, _vp, _c_f, _c_f, _vp, _c_int, _c_int, _c_int, _vp,
+                                   _c_int, _vp, _vp, _vp, _sz, _vp]),
     "ds2_dirsum": (_c_int, [_vp, _c_int, _c_int, _c_int, _vp, _vp]),
     "ds2_colsum_workspace_size": (_sz, [_c_int, _c_int]),
     "ds2_colsum": (_c_int, [_vp, _c_int, _c_int, _c_i64, _vp, _c_int, _vp, _sz, _vp]),

@@ -24,23 +24,27 @@ from . import ops
 
 # ----------------------------------------------------------------------------
 # RNN op seam (ref model.py:13-25 supported_rnns)
-class GRU(nn.Module):
-    """Single-layer (bi)directional GRU with nn.GRU's parameter names, order and init.
+class _HipRNN(nn.Module):
+    """Single-layer (bi)directional recurrent layer with nn.GRU / nn.LSTM's parameter
+    names, order and init.
 
     ``forward(x, lengths)`` takes padded [T, N, In] + int lengths (sorted or not)
     and returns padded [T, N, D*H]; a PackedSequence input is also accepted and
-    answered with a PackedSequence, like nn.GRU.
+    answered with a PackedSequence, like the torch modules.
     """
+    GATES = 0
+    FN = None
 
     def __init__(self, input_size, hidden_size, bidirectional=False, bias=True, num_layers=1):
         super().__init__()
         if num_layers != 1 or not bias:
-            raise ValueError("ds2amd.GRU supports num_layers=1, bias=True (what BatchRNN builds)")
+            raise ValueError(f"ds2amd.{type(self).__name__} supports num_layers=1, bias=True "
+                             "(what BatchRNN builds)")
         self.input_size = input_size
         self.hidden_size = hidden_size
         self.bidirectional = bidirectional
         self.num_directions = 2 if bidirectional else 1
-        g = 3 * hidden_size
+        g = self.GATES * hidden_size
         for sfx in [""] + (["_reverse"] if bidirectional else []):
             self.register_parameter("weight_ih_l0" + sfx, nn.Parameter(torch.empty(g, input_size)))
             self.register_parameter("weight_hh_l0" + sfx, nn.Parameter(torch.empty(g, hidden_size)))
@@ -53,7 +57,7 @@ class GRU(nn.Module):
         for w in self.parameters():
             nn.init.uniform_(w, -stdv, stdv)
 
-    def flatten_parameters(self):  # API parity with nn.GRU (model.py:94-95)
+    def flatten_parameters(self):  # API parity with nn.GRU/nn.LSTM (model.py:94-95)
         return None
 
     def _weights(self):
@@ -64,7 +68,7 @@ class GRU(nn.Module):
         return ws
 
     def run(self, x, lens_dev, sum_dirs=False):
-        return ops.GRULayerFn.apply(x, lens_dev, sum_dirs, self.hidden_size, *self._weights())
+        return self.FN.apply(x, lens_dev, sum_dirs, self.hidden_size, *self._weights())
 
     def forward(self, x, lengths=None):
         if isinstance(x, PackedSequence):
@@ -76,7 +80,20 @@ class GRU(nn.Module):
         return self.run(x, lengths.to(x.device, torch.int32)), None
 
 
+class GRU(_HipRNN):
+    """nn.GRU drop-in (gates r, z, n) on the HIP recurrence kernels (gru.hip)."""
+    GATES = 3
+    FN = ops.GRULayerFn
+
+
+class LSTM(_HipRNN):
+    """nn.LSTM drop-in (gates i, f, g, o) on the HIP recurrence kernels (lstm.hip)."""
+    GATES = 4
+    FN = ops.LSTMLayerFn
+
+
 supported_rnns = {
+    'lstm': LSTM,
     'gru': GRU,
 }
 supported_rnns_inv = dict((v, k) for k, v in supported_rnns.items())
@@ -209,8 +226,12 @@ class Lookahead(nn.Module):
         self.weight.data.uniform_(-stdv, stdv)
 
     def forward(self, input):
-        raise NotImplementedError(
-            "Lookahead (unidirectional DS2, cfg 4) has no HIP kernel yet; see DESIGN.md §next")
+        """[T, N, H] -> [T, N, H] (ds2_lookahead_fwd)."""
+        return ops.LookaheadFn.apply(input, self.weight, None)
+
+    def forward_htanh(self, input, lo, hi):
+        """Lookahead followed by Hardtanh(lo, hi), fused into one kernel."""
+        return ops.LookaheadFn.apply(input, self.weight, (float(lo), float(hi)))
 
     def __repr__(self):
         return (self.__class__.__name__ + '(n_features=' + str(self.n_features)
@@ -297,7 +318,8 @@ class DeepSpeech(nn.Module):
         for rnn in self.rnns:
             x = rnn(x, lens_dev)
         if not self._bidirectional:
-            x = self.lookahead(x)
+            la, ht = self.lookahead[0], self.lookahead[1]
+            x = la.forward_htanh(x, ht.min_val, ht.max_val)      # model.py:369-371
         x = self.fc(x)                                         # T' x N x C
         x_tnc = x
         x = x.transpose(0, 1)

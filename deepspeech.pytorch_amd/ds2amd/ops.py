@@ -310,6 +310,69 @@ class LinearFn(torch.autograd.Function):
         return dx, dw
 
 
+def _rnn_input_proj(x, weights, nd, g):
+    """xproj[T, N, D, g] = x @ W_ih^T + b_ih for every direction (one GEMM each)."""
+    t, n, inp = x.shape
+    x2d = x.view(t * n, inp)
+    xproj = torch.empty(t, n, nd, g, device=x.device, dtype=_F32)
+    for d in range(nd):
+        w_ih, _, b_ih, _ = weights[4 * d: 4 * d + 4]
+        sgemm(x2d, w_ih, xproj, m=t * n, n=g, k=inp, trans_b=True, lda=inp, ldb=inp,
+              ldc=nd * g, bias=b_ih, c_off=d * g)
+    return xproj
+
+
+def _rnn_output(h_all, sum_dirs, nd):
+    t, n, _, h = h_all.shape
+    if sum_dirs and nd == 2:
+        y = torch.empty(t, n, h, device=h_all.device, dtype=_F32)
+        _lib.call("ds2_dirsum", h_all.data_ptr(), t * n, nd, h, y.data_ptr(), _stream())
+        return y
+    return h_all.view(t, n, nd * h)
+
+
+def _rnn_param_grads(x, h_all, dgx, dgh, weights, nd, g, need_dx):
+    """Weight/bias/input gradients of one recurrent layer from the gate gradients.
+
+    dgx = d/d(x W_ih^T + b_ih), dgh = d/d(h W_hh^T + b_hh), both [T, N, D, g]
+    (the same tensor for LSTM).  All plain GEMMs + column sums.
+    """
+    t, n, inp = x.shape
+    h = h_all.shape[-1]
+    dev = x.device
+    x2d = x.view(t * n, inp)
+    tn = t * n
+    ld = nd * g
+    grads = []
+    dx = torch.empty(t, n, inp, device=dev, dtype=_F32) if need_dx else None
+    for d in range(nd):
+        w_ih, w_hh, b_ih, b_hh = weights[4 * d: 4 * d + 4]
+        dw_ih = torch.empty_like(w_ih)
+        sgemm(dgx, x2d, dw_ih, m=g, n=inp, k=tn, trans_a=True, lda=ld, ldb=inp, ldc=inp,
+              a_off=d * g)
+        db_ih = torch.empty_like(b_ih)
+        colsum(dgx, tn, g, ld, db_ih, off=d * g)
+        dw_hh = torch.empty_like(w_hh)
+        if t > 1:
+            # sum_t dgh_t^T h_{t-1} (fwd) / h_{t+1} (rev); h_prev = 0 at the start
+            a_off = (n * ld if d == 0 else 0) + d * g
+            b_off = (0 if d == 0 else n * nd * h) + d * h
+            sgemm(dgh, h_all, dw_hh, m=g, n=h, k=(t - 1) * n, trans_a=True, lda=ld,
+                  ldb=nd * h, ldc=h, a_off=a_off, b_off=b_off)
+        else:
+            dw_hh.zero_()
+        if dgh is dgx:
+            db_hh = db_ih.clone()
+        else:
+            db_hh = torch.empty_like(b_hh)
+            colsum(dgh, tn, g, ld, db_hh, off=d * g)
+        if dx is not None:
+            sgemm(dgx, w_ih, dx, m=tn, n=inp, k=g, lda=ld, ldb=inp, ldc=inp,
+                  beta=0.0 if d == 0 else 1.0, a_off=d * g)
+        grads += [dw_ih, dw_hh, db_ih, db_hh]
+    return dx, grads
+
+
 class GRULayerFn(torch.autograd.Function):
     """One (bi)directional GRU layer over padded [T, N, In] input with lengths.
 
@@ -320,17 +383,11 @@ class GRULayerFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, lens, sum_dirs, hidden, *weights):
         x = x.contiguous()
-        t, n, inp = x.shape
+        t, n, _ = x.shape
         h = hidden
         nd = len(weights) // 4
         dev = x.device
-        x2d = x.view(t * n, inp)
-        h3 = 3 * h
-        xproj = torch.empty(t, n, nd, h3, device=dev, dtype=_F32)
-        for d in range(nd):
-            w_ih, _, b_ih, _ = weights[4 * d: 4 * d + 4]
-            sgemm(x2d, w_ih, xproj, m=t * n, n=h3, k=inp, trans_b=True, lda=inp, ldb=inp,
-                  ldc=nd * h3, bias=b_ih, c_off=d * h3)
+        xproj = _rnn_input_proj(x, weights, nd, 3 * h)
         h_all = torch.empty(t, n, nd, h, device=dev, dtype=_F32)
         need_grad = any(ctx.needs_input_grad)   # forward() itself runs under no_grad
         gates = torch.empty(t, n, nd, 4 * h, device=dev, dtype=_F32) if need_grad else None
@@ -341,20 +398,15 @@ class GRULayerFn(torch.autograd.Function):
         _lib.call("ds2_gru_fwd", t, n, h, nd, xproj.data_ptr(), w_hh_f.data_ptr(), _p(w_hh_r),
                   b_hh_f.data_ptr(), _p(b_hh_r), lens.data_ptr(), h_all.data_ptr(), _p(gates),
                   ws.data_ptr(), ws.numel(), _stream())
-        if sum_dirs and nd == 2:
-            y = torch.empty(t, n, h, device=dev, dtype=_F32)
-            _lib.call("ds2_dirsum", h_all.data_ptr(), t * n, nd, h, y.data_ptr(), _stream())
-        else:
-            y = h_all.view(t, n, nd * h)
         ctx.save_for_backward(x, lens, h_all, gates, *weights)
         ctx.cfg = (sum_dirs, h, nd)
-        return y
+        return _rnn_output(h_all, sum_dirs, nd)
 
     @staticmethod
     def backward(ctx, dy):
         x, lens, h_all, gates, *weights = ctx.saved_tensors
         sum_dirs, h, nd = ctx.cfg
-        t, n, inp = x.shape
+        t, n, _ = x.shape
         dev = x.device
         h3 = 3 * h
         dy = dy.contiguous()
@@ -367,34 +419,90 @@ class GRULayerFn(torch.autograd.Function):
         _lib.call("ds2_gru_bwd", t, n, h, nd, dy.data_ptr(), dy_dirs, w_hh_f.data_ptr(),
                   _p(w_hh_r), h_all.data_ptr(), gates.data_ptr(), lens.data_ptr(), dgx.data_ptr(),
                   dgh.data_ptr(), ws.data_ptr(), ws.numel(), _stream())
-        x2d = x.view(t * n, inp)
-        tn = t * n
-        ld = nd * h3
-        grads = []
-        dx = torch.empty(t, n, inp, device=dev, dtype=_F32) if ctx.needs_input_grad[0] else None
-        for d in range(nd):
-            w_ih, w_hh, b_ih, b_hh = weights[4 * d: 4 * d + 4]
-            dw_ih = torch.empty_like(w_ih)
-            sgemm(dgx, x2d, dw_ih, m=h3, n=inp, k=tn, trans_a=True, lda=ld, ldb=inp, ldc=inp,
-                  a_off=d * h3)
-            db_ih = torch.empty_like(b_ih)
-            colsum(dgx, tn, h3, ld, db_ih, off=d * h3)
-            dw_hh = torch.empty_like(w_hh)
-            if t > 1:
-                # sum_t dgh_t^T h_{t-1} (fwd) / h_{t+1} (rev); h_prev = 0 at the start
-                a_off = (n * ld if d == 0 else 0) + d * h3
-                b_off = (0 if d == 0 else n * nd * h) + d * h
-                sgemm(dgh, h_all, dw_hh, m=h3, n=h, k=(t - 1) * n, trans_a=True, lda=ld,
-                      ldb=nd * h, ldc=h, a_off=a_off, b_off=b_off)
-            else:
-                dw_hh.zero_()
-            db_hh = torch.empty_like(b_hh)
-            colsum(dgh, tn, h3, ld, db_hh, off=d * h3)
-            if dx is not None:
-                sgemm(dgx, w_ih, dx, m=tn, n=inp, k=h3, lda=ld, ldb=inp, ldc=inp,
-                      beta=0.0 if d == 0 else 1.0, a_off=d * h3)
-            grads += [dw_ih, dw_hh, db_ih, db_hh]
+        dx, grads = _rnn_param_grads(x, h_all, dgx, dgh, weights, nd, h3,
+                                     ctx.needs_input_grad[0])
         return (dx, None, None, None, *grads)
+
+
+class LSTMLayerFn(torch.autograd.Function):
+    """One (bi)directional LSTM layer (nn.LSTM semantics, gates i, f, g, o) over padded
+    [T, N, In] + lengths: pack -> nn.LSTM -> pad of model.py:103-105 (rnn_type 'lstm',
+    model.py:14); with sum_dirs the direction sum of model.py:107."""
+
+    @staticmethod
+    def forward(ctx, x, lens, sum_dirs, hidden, *weights):
+        x = x.contiguous()
+        t, n, _ = x.shape
+        h = hidden
+        nd = len(weights) // 4
+        dev = x.device
+        xproj = _rnn_input_proj(x, weights, nd, 4 * h)
+        h_all = torch.empty(t, n, nd, h, device=dev, dtype=_F32)
+        need_grad = any(ctx.needs_input_grad)
+        c_all = torch.empty(t, n, nd, h, device=dev, dtype=_F32) if need_grad else None
+        gates = torch.empty(t, n, nd, 4 * h, device=dev, dtype=_F32) if need_grad else None
+        w_hh_f, b_hh_f = weights[1], weights[3]
+        w_hh_r = weights[5] if nd == 2 else None
+        b_hh_r = weights[7] if nd == 2 else None
+        ws = _ws(_lib.size("ds2_lstm_fwd_workspace_size", n, h, nd), dev)
+        _lib.call("ds2_lstm_fwd", t, n, h, nd, xproj.data_ptr(), w_hh_f.data_ptr(), _p(w_hh_r),
+                  b_hh_f.data_ptr(), _p(b_hh_r), lens.data_ptr(), h_all.data_ptr(), _p(c_all),
+                  _p(gates), ws.data_ptr(), ws.numel(), _stream())
+        ctx.save_for_backward(x, lens, h_all, c_all, gates, *weights)
+        ctx.cfg = (sum_dirs, h, nd)
+        return _rnn_output(h_all, sum_dirs, nd)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, lens, h_all, c_all, gates, *weights = ctx.saved_tensors
+        sum_dirs, h, nd = ctx.cfg
+        t, n, _ = x.shape
+        dev = x.device
+        dy = dy.contiguous()
+        dy_dirs = 1 if (sum_dirs and nd == 2) else nd
+        dg = torch.empty(t, n, nd, 4 * h, device=dev, dtype=_F32)
+        w_hh_f = weights[1]
+        w_hh_r = weights[5] if nd == 2 else None
+        ws = _ws(_lib.size("ds2_lstm_bwd_workspace_size", n, h, nd), dev)
+        _lib.call("ds2_lstm_bwd", t, n, h, nd, dy.data_ptr(), dy_dirs, w_hh_f.data_ptr(),
+                  _p(w_hh_r), c_all.data_ptr(), gates.data_ptr(), lens.data_ptr(), dg.data_ptr(),
+                  ws.data_ptr(), ws.numel(), _stream())
+        dx, grads = _rnn_param_grads(x, h_all, dg, dg, weights, nd, 4 * h,
+                                     ctx.needs_input_grad[0])
+        return (dx, None, None, None, *grads)
+
+
+class LookaheadFn(torch.autograd.Function):
+    """Lookahead conv (model.py:140-177) on [T, N, H], optionally fused with the
+    Hardtanh(lo, hi) that follows it in DeepSpeech (model.py:329-333)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, clamp):
+        x = _need(x, "lookahead x").contiguous()
+        w = _need(weight, "lookahead weight").contiguous()
+        t, n, h = x.shape
+        context = w.shape[1] - 1
+        y = torch.empty_like(x)
+        lo, hi = clamp if clamp is not None else (0.0, 0.0)
+        _lib.call("ds2_lookahead_fwd", x.data_ptr(), t, n, h, w.data_ptr(), context,
+                  int(clamp is not None), lo, hi, y.data_ptr(), _stream())
+        ctx.save_for_backward(x, w, y if clamp is not None else None)
+        ctx.clamp = clamp
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, y = ctx.saved_tensors
+        t, n, h = x.shape
+        context = w.shape[1] - 1
+        lo, hi = ctx.clamp if ctx.clamp is not None else (0.0, 0.0)
+        dy = dy.contiguous()
+        dx = torch.empty_like(x) if ctx.needs_input_grad[0] else None
+        dw = torch.empty_like(w) if ctx.needs_input_grad[1] else None
+        ws = _ws(_lib.size("ds2_lookahead_bwd_workspace_size", t, n, h, context), x.device)
+        _lib.call("ds2_lookahead_bwd", dy.data_ptr(), _p(y), lo, hi, x.data_ptr(), t, n, h,
+                  w.data_ptr(), context, _p(dx), _p(dw), ws.data_ptr(), ws.numel(), _stream())
+        return dx, dw, None
 
 
 class CTCLossFn(torch.autograd.Function):

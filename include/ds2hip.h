@@ -160,6 +160,44 @@ ds2_status_t ds2_gru_bwd(int t_max, int n, int h, int num_dirs, const float* dy,
                          const float* gates, const int* lens, float* dgates_x, float* dgates_h,
                          void* ws, size_t ws_bytes, ds2_stream_t stream);
 
+/* ------------------------------------------------------------------------ */
+/* (Bi)directional LSTM recurrence (torch gate order i, f, g, o), same packed-
+ * sequence semantics as the GRU.  ref model.py:14 (supported_rnns['lstm'] =
+ * nn.LSTM) inside BatchRNN model.py:97-109.
+ *   xproj : [T][N][D][4H]  x @ W_ih^T + b_ih for each direction
+ *   h_all : [T][N][D][H]   hidden states (output)
+ *   c_all : [T][N][D][H]   cell states (backward cache, or NULL)
+ *   gates : [T][N][D][4H]  activated (i, f, g, o) cache for backward, or NULL  */
+size_t ds2_lstm_fwd_workspace_size(int n, int h, int num_dirs);
+ds2_status_t ds2_lstm_fwd(int t_max, int n, int h, int num_dirs, const float* xproj,
+                          const float* w_hh_f, const float* w_hh_r, const float* b_hh_f,
+                          const float* b_hh_r, const int* lens, float* h_all, float* c_all,
+                          float* gates, void* ws, size_t ws_bytes, ds2_stream_t stream);
+size_t ds2_lstm_bwd_workspace_size(int n, int h, int num_dirs);
+/* dy as for ds2_gru_bwd.  dgates: [T][N][D][4H] gradient wrt the gate
+ * pre-activations (= wrt xproj and wrt W_hh h + b_hh).                       */
+ds2_status_t ds2_lstm_bwd(int t_max, int n, int h, int num_dirs, const float* dy, int dy_dirs,
+                          const float* w_hh_f, const float* w_hh_r, const float* c_all,
+                          const float* gates, const int* lens, float* dgates, void* ws,
+                          size_t ws_bytes, ds2_stream_t stream);
+
+/* ------------------------------------------------------------------------ */
+/* Lookahead convolution, ref model.py:140-177 (Lookahead.forward), optionally
+ * fused with the Hardtanh that follows it (model.py:329-333):
+ *   y[t][n][h] = sum_{j=0..context} w[h][j] * x[t+j][n][h]  (0 past T)
+ *   clamp != 0: y = min(max(y, lo), hi).   x, y: [T][N][H]; w: [H][context+1];
+ *   context + 1 <= 32.                                                       */
+ds2_status_t ds2_lookahead_fwd(const float* x, int t, int n, int h, const float* w, int context,
+                               int clamp, float lo, float hi, float* y, ds2_stream_t stream);
+/* Backward: y = the clamped forward output (or NULL when not clamped: dz = dy,
+ * else dz = dy where lo < y < hi).  dx (or NULL) overwritten; dw (or NULL)
+ * overwritten, deterministic.                                                 */
+size_t ds2_lookahead_bwd_workspace_size(int t, int n, int h, int context);
+ds2_status_t ds2_lookahead_bwd(const float* dy, const float* y, float lo, float hi,
+                               const float* x, int t, int n, int h, const float* w, int context,
+                               float* dx, float* dw, void* ws, size_t ws_bytes,
+                               ds2_stream_t stream);
+
 /* y[t][n][j] = sum_d h_all[t][n][d][j]   (model.py:107 view(T,N,2,H).sum(2)) */
 ds2_status_t ds2_dirsum(const float* h_all, int rows, int num_dirs, int h, float* y,
                         ds2_stream_t stream);

@@ -103,13 +103,14 @@ class OracleDS2:
     """Functional DS2 forward on CPU from a (reference-compatible) state_dict."""
 
     def __init__(self, state_dict: Dict[str, torch.Tensor], nb_layers: int, hidden: int,
-                 bidirectional: bool = True, bnm: float = 0.1):
+                 bidirectional: bool = True, bnm: float = 0.1, rnn_type: str = 'gru'):
         self.sd = {k: v.detach().clone().float() if v.is_floating_point() else v.clone()
                    for k, v in state_dict.items()}
         self.nb_layers = nb_layers
         self.hidden = hidden
         self.bidirectional = bidirectional
         self.bnm = bnm
+        self.rnn_type = rnn_type
 
     def parameters(self) -> Dict[str, torch.Tensor]:
         return {k: v for k, v in self.sd.items()
@@ -155,6 +156,10 @@ class OracleDS2:
             x = self._gru(x, out_lens, pre + '.rnn')
             if keep:
                 acts[f'rnn{i}'] = x
+        if not self.bidirectional:   # model.py:369-371: Lookahead + Hardtanh(0, 20)
+            x = F.hardtanh(lookahead(x, p['lookahead.0.weight']), 0, 20)
+            if keep:
+                acts['lookahead'] = x
         tt, nn_ = x.shape[0], x.shape[1]
         y = self._bn(x.reshape(tt * nn_, -1), 'fc.0.module.0', training)
         y = y @ p['fc.0.module.1.weight'].t()
@@ -163,11 +168,12 @@ class OracleDS2:
         return x, probs, out_lens, acts
 
     def _gru(self, x, lens, pre):
-        """pack -> nn.GRU -> pad -> sum directions (model.py:97-109)."""
+        """pack -> nn.GRU / nn.LSTM -> pad -> sum directions (model.py:97-109)."""
         p = self.params
         t = x.shape[0]
         inp = x.shape[2]
-        gru = torch.nn.GRU(inp, self.hidden, bidirectional=self.bidirectional, bias=True)
+        cls = {'gru': torch.nn.GRU, 'lstm': torch.nn.LSTM}[self.rnn_type]
+        gru = cls(inp, self.hidden, bidirectional=self.bidirectional, bias=True)
         names = ['weight_ih_l0', 'weight_hh_l0', 'bias_ih_l0', 'bias_hh_l0']
         if self.bidirectional:
             names += [nm + '_reverse' for nm in names]
@@ -179,6 +185,16 @@ class OracleDS2:
         if self.bidirectional:
             out = out.view(out.size(0), out.size(1), 2, -1).sum(2).view(out.size(0), out.size(1), -1)
         return out
+
+
+def lookahead(x: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
+    """Lookahead.forward (model.py:158-172): zero-pad `context` steps at the end, stack
+    the [t, t+context] windows, weight per feature and sum.  x [T, N, H], weight [H, C+1]."""
+    context = weight.shape[1] - 1
+    seq_len = x.size(0)
+    padded = torch.cat((x, x.new_zeros(context, *x.shape[1:])), 0)
+    win = torch.stack([padded[i:i + context + 1] for i in range(seq_len)])   # T x L x N x H
+    return torch.mul(win.permute(0, 2, 3, 1), weight).sum(dim=3)
 
 
 # ----------------------------------------------------------------------------

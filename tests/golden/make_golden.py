@@ -75,16 +75,19 @@ def ref_forward(m, x, lengths, keep=None):
             keep.append(x.detach().clone())
     if not m._bidirectional:
         x = m.lookahead(x)
+        if keep is not None:
+            keep.append(x.detach().clone())
     x = m.fc(x)
     x = x.transpose(0, 1)
     outs = F.softmax(x, dim=-1)
     return x, outs, output_lengths
 
 
-def make_ref(seed, hidden, layers, bidir=True):
+def make_ref(seed, hidden, layers, bidir=True, rnn_type='gru', context=20):
     torch.manual_seed(seed)
-    return ref_model.DeepSpeech(rnn_type='gru', labels=LABELS, rnn_hidden_size=hidden,
-                                nb_layers=layers, audio_conf=AUDIO_CONF, bidirectional=bidir)
+    return ref_model.DeepSpeech(rnn_type=rnn_type, labels=LABELS, rnn_hidden_size=hidden,
+                                nb_layers=layers, audio_conf=AUDIO_CONF, bidirectional=bidir,
+                                context=context)
 
 
 def checksum(sd):
@@ -108,8 +111,9 @@ def targets_for(out_lens, rng, n_classes=30):
     return np.array(tg, np.int32), np.array(tl, np.int32)
 
 
-def golden_tiny(path, seed=1234, hidden=16, layers=2, t_list=(64, 50, 31)):
-    m = make_ref(seed, hidden, layers)
+def golden_tiny(path, seed=1234, hidden=16, layers=2, t_list=(64, 50, 31), rnn_type='gru',
+                bidir=True, context=20):
+    m = make_ref(seed, hidden, layers, bidir, rnn_type, context)
     m.train()
     sd0 = {k: v.detach().clone() for k, v in m.state_dict().items()}
     cs, keys = checksum(sd0)
@@ -126,7 +130,7 @@ def golden_tiny(path, seed=1234, hidden=16, layers=2, t_list=(64, 50, 31)):
     rng = np.random.default_rng(seed)
     tg, tl = targets_for(out_lens.tolist(), rng)
     # one reference training step (train.py:600-632), CTC via the F.ctc_loss stand-in
-    m2 = make_ref(seed, hidden, layers)
+    m2 = make_ref(seed, hidden, layers, bidir, rnn_type, context)
     m2.train()
     opt = torch.optim.SGD(m2.parameters(), lr=3e-4, momentum=0.9, nesterov=True)
     lg, pr, ol = ref_forward(m2, x, input_sizes)
@@ -141,7 +145,8 @@ def golden_tiny(path, seed=1234, hidden=16, layers=2, t_list=(64, 50, 31)):
     after = {k: v.detach().clone() for k, v in m2.state_dict().items()}
     dec = ref_decoder.GreedyDecoder(LABELS)
     strings, offsets = dec.decode(probs, out_lens)
-    out = dict(seed=seed, hidden=hidden, layers=layers, x=x.numpy(), pct=pct.numpy(),
+    out = dict(seed=seed, hidden=hidden, layers=layers, rnn_type=rnn_type, bidirectional=bidir,
+               context=context, x=x.numpy(), pct=pct.numpy(),
                input_sizes=input_sizes.numpy(), logits=logits.detach().numpy(),
                probs=probs.detach().numpy(), out_lens=out_lens.numpy(), targets=tg,
                target_sizes=tl, loss=np.float32(loss.item()), grad_norm=np.float32(gnorm),
@@ -150,6 +155,8 @@ def golden_tiny(path, seed=1234, hidden=16, layers=2, t_list=(64, 50, 31)):
                conv1=keep[0].numpy(), conv2=keep[1].numpy())
     for i in range(layers):
         out[f'rnn{i}'] = keep[2 + i].numpy()
+    if not bidir:
+        out['lookahead'] = keep[2 + layers].numpy()
     for k, v in m.state_dict().items():            # running stats after one train forward
         if 'running' in k:
             out['after_fwd/' + k] = v.numpy()
@@ -232,6 +239,11 @@ def golden_seq_lens(path):
 if __name__ == '__main__':
     torch.set_num_threads(8)
     golden_tiny(os.path.join(HERE, 'tiny_ds2.npz'))
+    golden_tiny(os.path.join(HERE, 'tiny_lstm_bi.npz'), seed=2024, rnn_type='lstm')
+    golden_tiny(os.path.join(HERE, 'tiny_lstm_uni.npz'), seed=2025, rnn_type='lstm', bidir=False,
+                context=20)
+    golden_tiny(os.path.join(HERE, 'tiny_gru_uni.npz'), seed=2026, rnn_type='gru', bidir=False,
+                context=3)
     golden_cfg1(os.path.join(HERE, 'cfg1_ds2.npz'))
     golden_decoder(os.path.join(HERE, 'greedy_decoder.npz'))
     golden_seq_lens(os.path.join(HERE, 'seq_lens.npz'))

@@ -28,15 +28,29 @@ def _rel(got, ref):
     return (got - ref).abs().max().item() / max(ref.abs().max().item(), 1e-30)
 
 
-def build(seed, hidden, layers):
+TINY = ['tiny_ds2.npz', 'tiny_lstm_bi.npz', 'tiny_lstm_uni.npz', 'tiny_gru_uni.npz']
+
+
+def build(seed, hidden, layers, rnn_type='gru', bidirectional=True, context=20):
     torch.manual_seed(seed)
-    return dsm.DeepSpeech(rnn_type='gru', labels=LABELS, rnn_hidden_size=hidden, nb_layers=layers,
-                          audio_conf=CONF, bidirectional=True)
+    return dsm.DeepSpeech(rnn_type=rnn_type, labels=LABELS, rnn_hidden_size=hidden,
+                          nb_layers=layers, audio_conf=CONF, bidirectional=bidirectional,
+                          context=context)
 
 
-def test_tiny_forward_matches_reference_golden(dev, golden_dir):
-    g = np.load(os.path.join(golden_dir, 'tiny_ds2.npz'))
-    m = build(int(g['seed']), int(g['hidden']), int(g['layers'])).to(dev).train()
+def build_tiny(g):
+    """The model a tiny golden was made from (BiGRU / BiLSTM / uni + Lookahead)."""
+    kw = {}
+    if 'rnn_type' in g.files:
+        kw = dict(rnn_type=str(g['rnn_type']), bidirectional=bool(g['bidirectional']),
+                  context=int(g['context']))
+    return build(int(g['seed']), int(g['hidden']), int(g['layers']), **kw)
+
+
+@pytest.mark.parametrize("name", TINY)
+def test_tiny_forward_matches_reference_golden(dev, golden_dir, name):
+    g = np.load(os.path.join(golden_dir, name))
+    m = build_tiny(g).to(dev).train()
     x = torch.from_numpy(g['x']).to(dev)
     logits, probs, out_lens = m(x, torch.from_numpy(g['input_sizes']))
     np.testing.assert_array_equal(out_lens.cpu().numpy(), g['out_lens'])
@@ -51,10 +65,11 @@ def test_tiny_forward_matches_reference_golden(dev, golden_dir):
     assert strings == ref_strings          # bit-exact decode of the same probs
 
 
-def test_tiny_train_step_matches_reference_golden(dev, golden_dir):
+@pytest.mark.parametrize("name", TINY)
+def test_tiny_train_step_matches_reference_golden(dev, golden_dir, name):
     from ds2amd.trainer import Trainer
-    g = np.load(os.path.join(golden_dir, 'tiny_ds2.npz'))
-    m = build(int(g['seed']), int(g['hidden']), int(g['layers']))
+    g = np.load(os.path.join(golden_dir, name))
+    m = build_tiny(g)
     tr = Trainer(m, LABELS, lr=3e-4, momentum=0.9, max_norm=100.0, device=dev)
     data = (torch.from_numpy(g['x']), torch.from_numpy(g['targets']), None,
             torch.from_numpy(g['pct']).clone(), torch.from_numpy(g['target_sizes']))
@@ -71,9 +86,10 @@ def test_tiny_train_step_matches_reference_golden(dev, golden_dir):
             assert (sd[name].cpu() - ref).abs().max().item() <= 1e-6 + 1e-5 * ref.abs().max().item(), name
 
 
-def test_tiny_grads_match_reference_golden(dev, golden_dir):
-    g = np.load(os.path.join(golden_dir, 'tiny_ds2.npz'))
-    m = build(int(g['seed']), int(g['hidden']), int(g['layers'])).to(dev).train()
+@pytest.mark.parametrize("name", TINY)
+def test_tiny_grads_match_reference_golden(dev, golden_dir, name):
+    g = np.load(os.path.join(golden_dir, name))
+    m = build_tiny(g).to(dev).train()
     x = torch.from_numpy(g['x']).to(dev)
     logits, probs, out_lens = m(x, torch.from_numpy(g['input_sizes']))
     loss = CTCLoss()(logits.transpose(0, 1), torch.from_numpy(g['targets']), out_lens,
@@ -105,6 +121,28 @@ def test_ds2_800_forward_matches_oracle(dev):
     g = torch.Generator().manual_seed(0)
     t_list = [241, 200, 173, 120]
     x = torch.zeros(4, 1, 161, 241)
+    for i, t in enumerate(t_list):
+        x[i, 0, :, :t] = torch.randn(161, t, generator=g)
+    sizes = torch.IntTensor(t_list)
+    logits, probs, out_lens = m(x.to(dev), sizes)
+    with torch.no_grad():
+        rl, rp, ro, _ = o.forward(x, sizes, training=True)
+    np.testing.assert_array_equal(out_lens.cpu().numpy(), ro.numpy())
+    assert _rel(logits, rl) < REL
+    assert _rel(probs, rp) < REL
+
+
+@pytest.mark.parametrize("bidir", [False, True])
+def test_lstm_1024_forward_matches_oracle(dev, bidir):
+    """cfg4 layer type (LSTM-1024; unidirectional = with Lookahead + Hardtanh), 2 layers,
+    bs 4, variable lengths, train mode, against the CPU oracle (pinned by the tiny LSTM
+    goldens)."""
+    m = build(77, 1024, 2, rnn_type='lstm', bidirectional=bidir).to(dev).train()
+    o = orc.OracleDS2({k: v.detach().cpu() for k, v in m.state_dict().items()}, 2, 1024,
+                      bidirectional=bidir, rnn_type='lstm')
+    g = torch.Generator().manual_seed(1)
+    t_list = [161, 140, 99, 64]
+    x = torch.zeros(4, 1, 161, 161)
     for i, t in enumerate(t_list):
         x[i, 0, :, :t] = torch.randn(161, t, generator=g)
     sizes = torch.IntTensor(t_list)

@@ -186,7 +186,7 @@ def test_gru_persistent_equals_per_step(dev, h, monkeypatch):
     dy = torch.randn(t, n, h, generator=g)
     outs = []
     for flag in ("1", "0"):
-        monkeypatch.setenv("DS2_GRU_PERSISTENT", flag)
+        monkeypatch.setenv("DS2_RNN_PERSISTENT", flag)
         ws = [w.to(dev).requires_grad_(True) for w in weights]
         xd = x.to(dev).requires_grad_(True)
         y = ops.GRULayerFn.apply(xd, lens.to(dev), True, h, *ws)
@@ -214,6 +214,94 @@ def test_gru_per_direction_output(dev):
     yd.backward(dy.float().to(dev))
     _close(yd, out, 1e-5, "gru y")
     _close(xd.grad, xr.grad, 1e-4, "gru dx")
+
+
+# ---------------------------------------------------------------------------- LSTM
+def _lstm_case(n, t, inp, h, bidir, seed):
+    g = torch.Generator().manual_seed(seed)
+    lstm = torch.nn.LSTM(inp, h, bidirectional=bidir).double()
+    with torch.no_grad():
+        for p in lstm.parameters():
+            p.copy_(torch.rand(p.shape, generator=g, dtype=torch.float64) * 0.2 - 0.1)
+    lens = torch.tensor(sorted([t] + [max(1, t - 2 * i - 1) for i in range(n - 1)], reverse=True),
+                        dtype=torch.int32)
+    x = torch.randn(t, n, inp, generator=g, dtype=torch.float64)
+    for i in range(n):
+        x[int(lens[i]):, i] = 0
+    return lstm, lens, x, g
+
+
+@pytest.mark.parametrize("n,t,inp,h,bidir", [(5, 23, 40, 24, True), (19, 9, 33, 400, True),
+                                             (3, 17, 20, 16, False),
+                                             (64, 5, 64, 1024, True),     # cfg4 shape: per-step path
+                                             (32, 6, 48, 1024, False)])   # persistent, 2 bwd chunks
+def test_lstm_layer(dev, n, t, inp, h, bidir):
+    """ds2amd LSTM layer == pack -> nn.LSTM -> pad (-> direction sum), fwd and bwd."""
+    lstm, lens, x, g = _lstm_case(n, t, inp, h, bidir, n * 100 + h)
+    xr = x.clone().requires_grad_(True)
+    out, _ = lstm(torch.nn.utils.rnn.pack_padded_sequence(xr, lens.numpy()))
+    out, _ = torch.nn.utils.rnn.pad_packed_sequence(out, total_length=t)
+    nd = 2 if bidir else 1
+    summed = out.view(t, n, nd, h).sum(2) if bidir else out
+    dy = torch.randn(summed.shape, generator=g, dtype=torch.float64)
+    summed.backward(dy)
+    weights = [p.detach().float().to(dev).requires_grad_(True) for p in lstm.parameters()]
+    xd = x.float().to(dev).requires_grad_(True)
+    yd = ops.LSTMLayerFn.apply(xd, lens.to(dev), True, h, *weights)
+    yd.backward(dy.float().to(dev))
+    _close(yd, summed, 1e-5, "lstm y")
+    _close(xd.grad, xr.grad, 1e-4, "lstm dx")
+    for (name, p), wd in zip(lstm.named_parameters(), weights):
+        _close(wd.grad, p.grad, 1e-4, "lstm " + name)
+
+
+@pytest.mark.parametrize("h", [24, 800])
+def test_lstm_persistent_equals_per_step(dev, h, monkeypatch):
+    n, t, inp = 21, 19, 40
+    lstm, lens, x, g = _lstm_case(n, t, inp, h, True, h)
+    weights = [p.detach().float() for p in lstm.parameters()]
+    x = x.float()
+    dy = torch.randn(t, n, h, generator=g)
+    outs = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("DS2_RNN_PERSISTENT", flag)
+        ws = [w.to(dev).requires_grad_(True) for w in weights]
+        xd = x.to(dev).requires_grad_(True)
+        y = ops.LSTMLayerFn.apply(xd, lens.to(dev), True, h, *ws)
+        y.backward(dy.to(dev))
+        torch.cuda.synchronize()
+        outs.append([y.detach().cpu(), xd.grad.cpu()] + [w.grad.cpu() for w in ws])
+    for a, b in zip(*outs):
+        _close(a, b, 1e-5, "lstm persistent vs per-step")
+
+
+# ---------------------------------------------------------------------------- Lookahead
+@pytest.mark.parametrize("t,n,h,context", [(37, 3, 20, 20), (7, 2, 33, 20), (50, 5, 130, 3),
+                                           (1, 1, 1, 1)])
+@pytest.mark.parametrize("fused", [False, True])
+def test_lookahead(dev, t, n, h, context, fused):
+    """ds2_lookahead_fwd/bwd vs the reference formulation (oracle.lookahead, model.py:158-172),
+    optionally fused with Hardtanh(0, 20) (model.py:329-333)."""
+    g = torch.Generator().manual_seed(t * 31 + h)
+    x = (torch.randn(t, n, h, generator=g, dtype=torch.float64) * 8 + 4)
+    w = torch.rand(h, context + 1, generator=g, dtype=torch.float64) - 0.3
+    xr, wr = x.clone().requires_grad_(True), w.clone().requires_grad_(True)
+    yr = orc.lookahead(xr, wr)
+    if fused:
+        yr = torch.nn.functional.hardtanh(yr, 0, 20)
+    dy = torch.randn(yr.shape, generator=g, dtype=torch.float64)
+    yr.backward(dy)
+    xd = x.float().to(dev).requires_grad_(True)
+    wd = w.float().to(dev).requires_grad_(True)
+    yd = ops.LookaheadFn.apply(xd, wd, (0.0, 20.0) if fused else None)
+    yd.backward(dy.float().to(dev))
+    _close(yd, yr, 1e-5, "lookahead y")
+    if fused:
+        # the clamp's gradient mask must agree exactly where the output is not at a bound
+        inside = (yr.detach() > 0) & (yr.detach() < 20)
+        assert torch.equal((yd.detach().cpu() > 0) & (yd.detach().cpu() < 20), inside)
+    _close(xd.grad, xr.grad, 1e-5, "lookahead dx")
+    _close(wd.grad, wr.grad, 1e-5, "lookahead dw")
 
 
 # ---------------------------------------------------------------------------- CTC

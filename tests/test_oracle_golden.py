@@ -21,19 +21,36 @@ def _load(golden_dir, name):
     return np.load(os.path.join(golden_dir, name))
 
 
-def build_model(seed, hidden, layers):
+TINY = ['tiny_ds2.npz', 'tiny_lstm_bi.npz', 'tiny_lstm_uni.npz', 'tiny_gru_uni.npz']
+
+
+def build_model(seed, hidden, layers, rnn_type='gru', bidirectional=True, context=20):
     torch.manual_seed(seed)
-    return dsm.DeepSpeech(rnn_type='gru', labels=LABELS, rnn_hidden_size=hidden, nb_layers=layers,
-                          audio_conf=CONF, bidirectional=True)
+    return dsm.DeepSpeech(rnn_type=rnn_type, labels=LABELS, rnn_hidden_size=hidden,
+                          nb_layers=layers, audio_conf=CONF, bidirectional=bidirectional,
+                          context=context)
+
+
+def tiny_spec(g):
+    """(model kwargs, oracle kwargs) of a tiny golden (older files: BiGRU, context 20)."""
+    rnn_type = str(g['rnn_type']) if 'rnn_type' in g.files else 'gru'
+    bidir = bool(g['bidirectional']) if 'bidirectional' in g.files else True
+    context = int(g['context']) if 'context' in g.files else 20
+    mk = dict(seed=int(g['seed']), hidden=int(g['hidden']), layers=int(g['layers']),
+              rnn_type=rnn_type, bidirectional=bidir, context=context)
+    ok = dict(nb_layers=int(g['layers']), hidden=int(g['hidden']), bidirectional=bidir,
+              rnn_type=rnn_type)
+    return mk, ok
 
 
 def _checksum(sd, keys):
     return np.array([float(sd[k].double().sum()) for k in keys])
 
 
-def test_constructor_draws_reference_weights(golden_dir):
-    g = _load(golden_dir, 'tiny_ds2.npz')
-    m = build_model(int(g['seed']), int(g['hidden']), int(g['layers']))
+@pytest.mark.parametrize("name", TINY)
+def test_constructor_draws_reference_weights(golden_dir, name):
+    g = _load(golden_dir, name)
+    m = build_model(**tiny_spec(g)[0])
     keys = [str(k) for k in g['checksum_keys']]
     assert sorted(k for k, v in m.state_dict().items() if v.is_floating_point()) == sorted(keys)
     np.testing.assert_array_equal(_checksum(m.state_dict(), keys), g['checksum'])
@@ -46,10 +63,12 @@ def test_state_dict_keys_match_reference_cfg1(golden_dir):
     np.testing.assert_array_equal(_checksum(m.state_dict(), keys), g['checksum'])
 
 
-def test_oracle_forward_tiny(golden_dir):
-    g = _load(golden_dir, 'tiny_ds2.npz')
-    m = build_model(int(g['seed']), int(g['hidden']), int(g['layers']))
-    o = orc.OracleDS2(m.state_dict(), int(g['layers']), int(g['hidden']))
+@pytest.mark.parametrize("name", TINY)
+def test_oracle_forward_tiny(golden_dir, name):
+    g = _load(golden_dir, name)
+    mk, ok = tiny_spec(g)
+    m = build_model(**mk)
+    o = orc.OracleDS2(m.state_dict(), **ok)
     x = torch.from_numpy(g['x'])
     sizes = orc.input_sizes_quirk(torch.from_numpy(g['pct']), x.shape[3])
     np.testing.assert_array_equal(sizes.numpy(), g['input_sizes'])
@@ -59,6 +78,8 @@ def test_oracle_forward_tiny(golden_dir):
     np.testing.assert_allclose(acts['conv2'].numpy(), g['conv2'], rtol=1e-5, atol=1e-5)
     for i in range(int(g['layers'])):
         np.testing.assert_allclose(acts[f'rnn{i}'].numpy(), g[f'rnn{i}'], rtol=1e-5, atol=1e-5)
+    if 'lookahead' in g.files:
+        np.testing.assert_allclose(acts['lookahead'].numpy(), g['lookahead'], rtol=1e-5, atol=1e-5)
     np.testing.assert_allclose(logits.numpy(), g['logits'], rtol=1e-5, atol=1e-5)
     np.testing.assert_allclose(probs.numpy(), g['probs'], rtol=1e-5, atol=1e-6)
     for k in g.files:
@@ -69,10 +90,12 @@ def test_oracle_forward_tiny(golden_dir):
     assert [s[0] for s in strings] == [str(s) for s in g['decoded']]
 
 
-def test_oracle_train_step_tiny(golden_dir):
-    g = _load(golden_dir, 'tiny_ds2.npz')
-    m = build_model(int(g['seed']), int(g['hidden']), int(g['layers']))
-    o = orc.OracleDS2(m.state_dict(), int(g['layers']), int(g['hidden']))
+@pytest.mark.parametrize("name", TINY)
+def test_oracle_train_step_tiny(golden_dir, name):
+    g = _load(golden_dir, name)
+    mk, ok = tiny_spec(g)
+    m = build_model(**mk)
+    o = orc.OracleDS2(m.state_dict(), **ok)
     loss, new, bufs, grads, gnorm = orc.train_step(
         o, torch.from_numpy(g['x']), torch.from_numpy(g['pct']), torch.from_numpy(g['targets']),
         torch.from_numpy(g['target_sizes']))
