@@ -12,6 +12,8 @@
 // gathers of K-step i+1 are in flight while the MFMAs of step i run.
 #include "common.h"
 
+#include <cstdlib>
+
 namespace ds2 {
 
 constexpr int CBK = 16;       // K per stage
@@ -362,6 +364,283 @@ __global__ void bias_grad_kernel(const float* __restrict__ dy, int N, int C, int
   if (threadIdx.x == 0) db[c] = static_cast<float>(red[0] + red[1] + red[2] + red[3]);
 }
 
+// ---------------------------------------------------------------------------
+// Direct convolution from an LDS input patch (width stride 1): forward and dgrad.
+//
+// A workgroup owns 32 output channels x PT_ROWS output rows x PT_COLS output
+// columns of one sample; wave w computes row w with four 32x32 MFMA tiles.  For
+// each input ("loop") channel the input patch those outputs need — rows
+// PR0 + w*RSI + a, columns PC0 + j + b — and the channel's filter taps Wl[t][m]
+// (t = a*B + b) are staged once in LDS; every tap is then one A read (weights),
+// four B reads (patch, consecutive columns across lanes) and four MFMAs.  Versus
+// the im2col gather this reads each input element from global memory once per
+// workgroup instead of once per tap.  The next channel's patch and taps are
+// loaded into registers while the current channel's MFMAs run.
+//
+//   fwd  : out = y[n][co][ho][wo], loop over ci, taps (kh, kw),
+//          input row = ho*sh - ph + kh, col = wo - pw + kw
+//   dgrad: out = dx[n][ci][hi][wi] for the rows hi of one stride class
+//          (hi + ph) % sh == q; loop over co, taps = the kh of that class
+//          (reversed) x the kw (reversed), input = dy row
+//          (hi + ph - kh) / sh, col = wi + pw - kw
+constexpr int PT_ROWS = 4;          // output rows per workgroup (one per wave)
+constexpr int PT_COLS = 128;        // output columns per workgroup
+constexpr int PT_PITCH = 144;       // patch row pitch (>= PT_COLS + kw - 1)
+constexpr int PT_PROWS = 28;        // max patch rows incl. one zero row
+constexpr int PT_TMAX = 232;        // max taps (padded to even)
+constexpr int PT_WP = 33;           // tap-row pitch of the weight tile (conflict-free)
+constexpr int PT_PREG = (PT_PROWS * (PT_PITCH - 6) + 255) / 256;
+constexpr int PT_WREG4 = (PT_TMAX * PT_WP / 4 + 255) / 256;
+
+struct PatchGeom {
+  int taps_a;     // A: tap rows
+  int tpad;       // A*B rounded up to even
+  int prows;      // patch rows actually used (incl. the zero row)
+  int pcols;      // patch columns actually used (PT_COLS + B - 1)
+  int rsi;        // patch-row step between consecutive output rows of the tile
+  int pr0;        // first patch row (input row index)
+  int pc0;        // first patch column (input column index)
+  int kh_class;   // dgrad: stride class q
+  int r_first;    // first output row of the tile
+  int r_step;     // output-row step between waves (1 fwd, sh dgrad)
+};
+
+__host__ __device__ inline int class_taps(const ConvDims& g, int q) {
+  return q < g.kh ? (g.kh - 1 - q) / g.sh + 1 : 0;
+}
+
+// weight-image geometry shared by host and device: tap rows padded to even, 33-float rows,
+// tiles padded to 16 bytes
+__host__ __device__ inline int wimg_tstride(const ConvDims& g, bool dgrad) {
+  const int a = dgrad ? class_taps(g, 0) : g.kh;   // class 0 has the most taps
+  return ((a * g.kw) + 1) & ~1;
+}
+__host__ __device__ inline int64_t wimg_tile(int tstride) {
+  return ((int64_t)tstride * PT_WP + 3) & ~(int64_t)3;
+}
+
+template <bool DGRAD>
+__device__ __forceinline__ PatchGeom patch_geom(const ConvDims& g, int ty, int wo0) {
+  PatchGeom p;
+  if (!DGRAD) {
+    p.taps_a = g.kh;
+    p.rsi = g.sh;
+    p.r_first = ty * PT_ROWS;
+    p.r_step = 1;
+    p.pr0 = p.r_first * g.sh - g.ph;
+    p.pc0 = wo0 - g.pw;
+    p.kh_class = 0;
+  } else {
+    // decode (class q, tile) from ty: classes in order, ceil(count_q / PT_ROWS) tiles each
+    int q = 0, t = ty, hq = 0;
+    for (q = 0; q < g.sh; ++q) {
+      hq = ((q - g.ph) % g.sh + g.sh) % g.sh;
+      const int cnt = hq < g.hi ? (g.hi - 1 - hq) / g.sh + 1 : 0;
+      const int tiles = (cnt + PT_ROWS - 1) / PT_ROWS;
+      if (t < tiles) break;
+      t -= tiles;
+    }
+    const int aq = class_taps(g, q);
+    p.taps_a = aq;
+    p.rsi = 1;
+    p.r_first = hq + g.sh * PT_ROWS * t;
+    p.r_step = g.sh;
+    p.pr0 = (p.r_first + g.ph - q) / g.sh - (aq - 1);
+    p.pc0 = wo0 + g.pw - g.kw + 1;
+    p.kh_class = q;
+  }
+  const int taps = p.taps_a * g.kw;
+  p.tpad = (taps + 1) & ~1;
+  p.prows = (PT_ROWS - 1) * p.rsi + p.taps_a + 1;
+  p.pcols = PT_COLS + g.kw - 1;
+  return p;
+}
+
+// Weight images, one [tstride][33] tile per (class, 32-channel output block, loop
+// channel): img[t][m] = the weight of output channel m0+m for tap t (0 past the
+// taps / channels).  fwd taps t = kh*kw + kw; dgrad taps of class q reversed.
+template <bool DGRAD>
+__global__ void conv_wimg_kernel(const float* __restrict__ w, ConvDims g, int tstride,
+                                 float* __restrict__ img) {
+  const int M = DGRAD ? g.ci : g.co;
+  const int L = DGRAD ? g.co : g.ci;
+  const int mbn = (M + 31) / 32;
+  const int classes = DGRAD ? g.sh : 1;
+  const int64_t tile = wimg_tile(tstride);
+  const int64_t total = (int64_t)classes * mbn * L * tile;
+  const int KHW = g.kh * g.kw;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t r = i;
+    const int e = static_cast<int>(r % tile); r /= tile;
+    const int c = static_cast<int>(r % L); r /= L;
+    const int mb = static_cast<int>(r % mbn); r /= mbn;
+    const int q = static_cast<int>(r);
+    const int t = e / PT_WP;
+    const int m = mb * 32 + (e - t * PT_WP);
+    float v = 0.f;
+    if (t < tstride && e - t * PT_WP < 32 && m < M) {
+      const int a = t / g.kw;
+      const int b = t - a * g.kw;
+      if (!DGRAD) {
+        if (a < g.kh) v = w[((int64_t)m * g.ci + c) * KHW + a * g.kw + b];
+      } else {
+        const int aq = class_taps(g, q);
+        if (a < aq) {
+          const int khi = q + g.sh * (aq - 1 - a);
+          v = w[((int64_t)c * g.ci + m) * KHW + khi * g.kw + (g.kw - 1 - b)];
+        }
+      }
+    }
+    img[i] = v;
+  }
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t conv_rsrc(const float* p, int64_t elems) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), (short)0,
+                                           static_cast<int>(elems * 4), 0x00020000);
+}
+
+typedef unsigned int cu32x4 __attribute__((ext_vector_type(4)));
+
+template <bool DGRAD>
+__global__ __launch_bounds__(256) void conv_patch_kernel(const float* __restrict__ in,
+                                                         const float* __restrict__ img,
+                                                         const float* __restrict__ bias,
+                                                         float* __restrict__ out, ConvDims g,
+                                                         const int* __restrict__ out_lens,
+                                                         int tstride) {
+  __shared__ __attribute__((aligned(16))) float ps[PT_PROWS * PT_PITCH];
+  __shared__ __attribute__((aligned(16))) float wl[PT_TMAX * PT_WP];
+  const int M = DGRAD ? g.ci : g.co;            // output channels
+  const int L = DGRAD ? g.co : g.ci;            // loop channels
+  const int in_h = DGRAD ? g.ho : g.hi;
+  const int in_w = DGRAD ? g.wo : g.wi;
+  const int out_h = DGRAD ? g.hi : g.ho;
+  const int out_w = DGRAD ? g.wi : g.wo;
+  const int mbn = (M + 31) / 32;
+  const int n = blockIdx.z / mbn;
+  const int mb = blockIdx.z - n * mbn;
+  const int m0 = mb * 32;
+  const int c0 = blockIdx.x * PT_COLS;
+  const PatchGeom p = patch_geom<DGRAD>(g, blockIdx.y, c0);
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int B = g.kw;
+  const int plane = in_h * in_w;
+  const float* inn = in + (int64_t)n * L * plane;
+  const int64_t tile = wimg_tile(tstride);
+  const float* wimg = img + ((int64_t)p.kh_class * mbn + mb) * L * tile;
+  const int wq = (p.tpad * PT_WP + 3) / 4;      // 16-byte chunks of the used tap rows
+  const int pe = p.prows * p.pcols;
+
+  // channel-invariant part of this thread's patch offsets: (row, col) of idx = tid + 256 r
+  float rp[PT_PREG];
+  cu32x4 rw[PT_WREG4];
+  auto load = [&](int c) {
+    const __amdgpu_buffer_rsrc_t rs = conv_rsrc(inn + (int64_t)c * plane, plane);
+    int row = tid / p.pcols, col = tid - (tid / p.pcols) * p.pcols;
+#pragma unroll
+    for (int r = 0; r < PT_PREG; ++r) {
+      const int ir = p.pr0 + row, ic = p.pc0 + col;
+      const bool ok = tid + 256 * r < pe && row < p.prows - 1 && ir >= 0 && ir < in_h &&
+                      ic >= 0 && ic < in_w;
+      rp[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                            rs, ok ? (ir * in_w + ic) * 4 : 0x7ffffff0, 0, 0));
+      col += 256;
+      while (col >= p.pcols) {
+        col -= p.pcols;
+        ++row;
+      }
+    }
+    const __amdgpu_buffer_rsrc_t ws = conv_rsrc(wimg + (int64_t)c * tile, tile);
+#pragma unroll
+    for (int r = 0; r < PT_WREG4; ++r) {
+      const int i = tid + 256 * r;
+      rw[r] = __builtin_amdgcn_raw_buffer_load_b128(ws, i < wq ? i * 16 : 0x7ffffff0, 0, 0);
+    }
+  };
+  auto store = [&]() {
+    int row = tid / p.pcols, col = tid - (tid / p.pcols) * p.pcols;
+#pragma unroll
+    for (int r = 0; r < PT_PREG; ++r) {
+      if (tid + 256 * r < pe) ps[row * PT_PITCH + col] = rp[r];
+      col += 256;
+      while (col >= p.pcols) {
+        col -= p.pcols;
+        ++row;
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < PT_WREG4; ++r) {
+      const int i = tid + 256 * r;
+      if (i < wq) *reinterpret_cast<cu32x4*>(wl + 4 * i) = rw[r];
+    }
+  };
+
+  f32x16 acc[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+  const int lr = lane & 31, lk = lane >> 5;
+  // this lane's first tap (t = lk) as (a, b) and its patch offset
+  const int a0 = lk / B, b0 = lk - (lk / B) * B;
+  const int po_start = (wave * p.rsi + a0) * PT_PITCH + b0 + lr;
+  const int steps = p.tpad >> 1;
+
+  load(0);
+  store();
+  __syncthreads();
+  for (int c = 0; c < L; ++c) {
+    if (c + 1 < L) load(c + 1);
+    int po = po_start, bb = b0;
+    const float* wrow = wl + lk * PT_WP + lr;
+    for (int s = 0; s < steps; ++s) {
+      const float av = wrow[s * 2 * PT_WP];
+      const float* pp = ps + po;
+      const float v0 = pp[0], v1 = pp[32], v2 = pp[64], v3 = pp[96];
+      acc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, v0, acc[0], 0, 0, 0);
+      acc[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, v1, acc[1], 0, 0, 0);
+      acc[2] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, v2, acc[2], 0, 0, 0);
+      acc[3] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, v3, acc[3], 0, 0, 0);
+      bb += 2;
+      po += 2;
+      if (bb >= B) {            // kw >= 2 (host-checked): at most one wrap per step
+        bb -= B;
+        po += PT_PITCH - B;
+      }
+    }
+    __syncthreads();
+    if (c + 1 < L) {
+      store();
+      __syncthreads();
+    }
+  }
+
+  const int orow = p.r_first + wave * p.r_step;
+  if (orow >= out_h) return;
+  const int len = (!DGRAD && out_lens != nullptr) ? out_lens[n] : out_w;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = c0 + 32 * j + lr;
+    if (col >= out_w) continue;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int m = m0 + (r & 3) + 8 * (r >> 2) + 4 * lk;
+      if (m < M) {
+        float v = acc[j][r];
+        if (!DGRAD) {
+          if (bias != nullptr) v += bias[m];
+          if (col >= len) v = 0.f;
+        }
+        out[(((int64_t)n * M + m) * out_h + orow) * out_w + col] = v;
+      }
+    }
+  }
+}
+
 static inline bool make_dims(ConvDims& g, int n, int c_in, int h_in, int w_in, int c_out, int kh,
                              int kw, int sh, int sw, int ph, int pw) {
   if (n < 0 || c_in < 1 || h_in < 1 || w_in < 1 || c_out < 1 || kh < 1 || kw < 1 || sh < 1 ||
@@ -373,19 +652,76 @@ static inline bool make_dims(ConvDims& g, int n, int c_in, int h_in, int w_in, i
   return g.ho >= 1 && g.wo >= 1;
 }
 
+// the LDS-patch kernel covers width stride 1 with patches / tap tiles that fit its LDS
+static inline bool patch_ok(const ConvDims& g, bool dgrad) {
+  if (getenv("DS2_CONV_PATCH") != nullptr && getenv("DS2_CONV_PATCH")[0] == '0') return false;
+  if (g.sw != 1 || g.kw < 2 || g.kw > PT_PITCH - PT_COLS + 1) return false;
+  const int a = dgrad ? (g.kh + g.sh - 1) / g.sh : g.kh;
+  const int rows = (PT_ROWS - 1) * (dgrad ? 1 : g.sh) + a + 1;
+  const int taps = ((a * g.kw) + 1) & ~1;
+  const int64_t plane = dgrad ? (int64_t)g.ho * g.wo : (int64_t)g.hi * g.wi;
+  return rows <= PT_PROWS && taps <= PT_TMAX && plane * 4 < (1ll << 31) - 64;
+}
+
+static size_t patch_ws_bytes(const ConvDims& g, bool dgrad) {
+  if (!patch_ok(g, dgrad)) return 0;
+  const int M = dgrad ? g.ci : g.co;
+  const int L = dgrad ? g.co : g.ci;
+  const int classes = dgrad ? g.sh : 1;
+  return (size_t)classes * ((M + 31) / 32) * L * wimg_tile(wimg_tstride(g, dgrad)) * sizeof(float);
+}
+
+template <bool DGRAD>
+static ds2_status_t launch_patch(const float* in, const float* w, const float* bias, float* out,
+                                 const ConvDims& g, const int* out_lens, void* ws, hipStream_t st) {
+  const int tstride = wimg_tstride(g, DGRAD);
+  float* img = static_cast<float*>(ws);
+  const int64_t total = (int64_t)patch_ws_bytes(g, DGRAD) / sizeof(float);
+  hipLaunchKernelGGL(conv_wimg_kernel<DGRAD>, dim3(cdiv(total, 256) > 2048 ? 2048 : cdiv(total, 256)),
+                     dim3(256), 0, st, w, g, tstride, img);
+  int ty = 0;
+  if (!DGRAD) {
+    ty = cdiv(g.ho, PT_ROWS);
+  } else {
+    for (int q = 0; q < g.sh; ++q) {
+      const int hq = ((q - g.ph) % g.sh + g.sh) % g.sh;
+      const int cnt = hq < g.hi ? (g.hi - 1 - hq) / g.sh + 1 : 0;
+      ty += cdiv(cnt, PT_ROWS);
+    }
+  }
+  const int M = DGRAD ? g.ci : g.co;
+  dim3 grid(cdiv(DGRAD ? g.wi : g.wo, PT_COLS), ty, g.n * cdiv(M, 32));
+  hipLaunchKernelGGL(conv_patch_kernel<DGRAD>, grid, dim3(256), 0, st, in, img, bias, out, g,
+                     out_lens, tstride);
+  return launch_status(DGRAD ? "ds2_conv2d_dgrad" : "ds2_conv2d_fwd");
+}
+
 }  // namespace ds2
 
 using namespace ds2;
 
 extern "C" {
 
+size_t ds2_conv2d_workspace_size(int n, int c_in, int h_in, int w_in, int c_out, int kh, int kw,
+                                 int sh, int sw, int ph, int pw) {
+  ConvDims g;
+  if (!make_dims(g, n, c_in, h_in, w_in, c_out, kh, kw, sh, sw, ph, pw)) return 0;
+  const size_t a = patch_ws_bytes(g, false), b = patch_ws_bytes(g, true);
+  return (a > b ? a : b) + 256;
+}
+
 ds2_status_t ds2_conv2d_fwd(const float* x, const float* w, const float* bias, float* y, int n,
                             int c_in, int h_in, int w_in, int c_out, int kh, int kw, int sh,
-                            int sw, int ph, int pw, const int* out_lens, ds2_stream_t stream) {
+                            int sw, int ph, int pw, const int* out_lens, void* ws,
+                            size_t ws_bytes, ds2_stream_t stream) {
   ConvDims g;
   if (!make_dims(g, n, c_in, h_in, w_in, c_out, kh, kw, sh, sw, ph, pw)) return DS2_INVALID_VALUE;
   if (n == 0) return DS2_OK;
   if (g.ho > 65535) return DS2_UNSUPPORTED_SHAPE;
+  if (patch_ok(g, false)) {
+    if (ws == nullptr || ws_bytes < patch_ws_bytes(g, false)) return DS2_WORKSPACE_TOO_SMALL;
+    return launch_patch<false>(x, w, bias, y, g, out_lens, ws, as_stream(stream));
+  }
   dim3 grid(cdiv(g.wo, CBN), g.ho, n * cdiv(c_out, 32));
   hipLaunchKernelGGL(conv_fwd_kernel, grid, dim3(256), 0, as_stream(stream), x, w, bias, y, g,
                      out_lens);
@@ -394,10 +730,14 @@ ds2_status_t ds2_conv2d_fwd(const float* x, const float* w, const float* bias, f
 
 ds2_status_t ds2_conv2d_dgrad(const float* dy, const float* w, float* dx, int n, int c_in,
                               int h_in, int w_in, int c_out, int kh, int kw, int sh, int sw,
-                              int ph, int pw, ds2_stream_t stream) {
+                              int ph, int pw, void* ws, size_t ws_bytes, ds2_stream_t stream) {
   ConvDims g;
   if (!make_dims(g, n, c_in, h_in, w_in, c_out, kh, kw, sh, sw, ph, pw)) return DS2_INVALID_VALUE;
   if (n == 0) return DS2_OK;
+  if (patch_ok(g, true)) {
+    if (ws == nullptr || ws_bytes < patch_ws_bytes(g, true)) return DS2_WORKSPACE_TOO_SMALL;
+    return launch_patch<true>(dy, w, nullptr, dx, g, nullptr, ws, as_stream(stream));
+  }
   dim3 grid(cdiv(w_in, CBN), h_in, n * cdiv(c_in, 32));
   hipLaunchKernelGGL(conv_dgrad_kernel, grid, dim3(256), 0, as_stream(stream), dy, w, dx, g);
   return launch_status("ds2_conv2d_dgrad");

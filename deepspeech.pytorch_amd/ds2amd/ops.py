@@ -82,9 +82,11 @@ def conv2d_fwd(x, weight, bias, stride, padding, out_lens=None):
     co, _, kh, kw = weight.shape
     ho, wo = conv_out_shape(h, w, kh, kw, stride[0], stride[1], padding[0], padding[1])
     y = torch.empty(n, co, ho, wo, device=x.device, dtype=_F32)
+    dims = (n, ci, h, w, co, kh, kw, stride[0], stride[1], padding[0], padding[1])
+    ws = _ws(_lib.size("ds2_conv2d_workspace_size", *dims), x.device)
     _lib.call("ds2_conv2d_fwd", x.data_ptr(), weight.data_ptr(),
-              _p(None if bias is None else _need(bias, "conv2d.bias")), y.data_ptr(), n, ci, h, w,
-              co, kh, kw, stride[0], stride[1], padding[0], padding[1], _p(out_lens), _stream())
+              _p(None if bias is None else _need(bias, "conv2d.bias")), y.data_ptr(), *dims,
+              _p(out_lens), ws.data_ptr(), ws.numel(), _stream())
     return y
 
 
@@ -93,8 +95,10 @@ def conv2d_dgrad(dy, weight, x_shape, stride, padding):
     n, ci, h, w = x_shape
     co, _, kh, kw = weight.shape
     dx = torch.empty(n, ci, h, w, device=dy.device, dtype=_F32)
-    _lib.call("ds2_conv2d_dgrad", dy.data_ptr(), weight.data_ptr(), dx.data_ptr(), n, ci, h, w, co,
-              kh, kw, stride[0], stride[1], padding[0], padding[1], _stream())
+    dims = (n, ci, h, w, co, kh, kw, stride[0], stride[1], padding[0], padding[1])
+    ws = _ws(_lib.size("ds2_conv2d_workspace_size", *dims), dy.device)
+    _lib.call("ds2_conv2d_dgrad", dy.data_ptr(), weight.data_ptr(), dx.data_ptr(), *dims,
+              ws.data_ptr(), ws.numel(), _stream())
     return dx
 
 

@@ -78,16 +78,21 @@ ds2_status_t ds2_sgemm_ws(int trans_a, int trans_b, int m, int n, int k, float a
                           const float* bias, void* ws, size_t ws_bytes, ds2_stream_t stream);
 
 /* ------------------------------------------------------------------------ */
-/* Conv2d, NCHW fp32, implicit GEMM on MFMA. ref model.py:209,212 (nn.Conv2d via
- * cuDNN), masked by MaskConv model.py:63-79 when out_lens != NULL: output
- * columns w >= out_lens[n] are written as 0.                                  */
+/* Conv2d, NCHW fp32, on MFMA. ref model.py:209,212 (nn.Conv2d via cuDNN), masked
+ * by MaskConv model.py:63-79 when out_lens != NULL: output columns w >= out_lens[n]
+ * are written as 0.  Width-stride-1 convolutions (conv2) run as direct
+ * convolutions from LDS input patches and need the workspace (re-laid-out
+ * filter taps); others (conv1) run as an implicit GEMM and ignore it.        */
+size_t ds2_conv2d_workspace_size(int n, int c_in, int h_in, int w_in, int c_out, int kh, int kw,
+                                 int sh, int sw, int ph, int pw);
 ds2_status_t ds2_conv2d_fwd(const float* x, const float* w, const float* bias, float* y,
                             int n, int c_in, int h_in, int w_in, int c_out, int kh, int kw,
-                            int sh, int sw, int ph, int pw, const int* out_lens,
-                            ds2_stream_t stream);
+                            int sh, int sw, int ph, int pw, const int* out_lens, void* ws,
+                            size_t ws_bytes, ds2_stream_t stream);
 ds2_status_t ds2_conv2d_dgrad(const float* dy, const float* w, float* dx,
                               int n, int c_in, int h_in, int w_in, int c_out, int kh, int kw,
-                              int sh, int sw, int ph, int pw, ds2_stream_t stream);
+                              int sh, int sw, int ph, int pw, void* ws, size_t ws_bytes,
+                              ds2_stream_t stream);
 size_t ds2_conv2d_wgrad_workspace_size(int n, int c_in, int h_in, int w_in, int c_out, int kh,
                                        int kw, int sh, int sw, int ph, int pw);
 /* dw = sum over (n, ho, wo) of dy * im2col(x); dbias = sum of dy (if dbias != NULL). */

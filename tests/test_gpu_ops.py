@@ -46,6 +46,12 @@ CONVS = [  # (n, ci, h, w, co, kh, kw, sh, sw, ph, pw)
     (2, 1, 161, 37, 32, 41, 11, 2, 2, 20, 5),
     (2, 32, 81, 23, 32, 21, 11, 2, 1, 10, 5),
     (3, 3, 17, 300, 40, 5, 3, 1, 2, 2, 1),
+    # width stride 1 -> LDS-patch direct kernels (several column tiles, two output-channel
+    # blocks, 3 stride classes in dgrad, odd tap counts, edge rows / columns)
+    (2, 32, 81, 200, 32, 21, 11, 2, 1, 10, 5),
+    (3, 5, 19, 140, 40, 3, 3, 1, 1, 1, 1),
+    (2, 4, 30, 50, 8, 7, 5, 3, 1, 3, 2),
+    (1, 2, 9, 7, 3, 4, 2, 2, 1, 3, 0),
 ]
 
 
