@@ -641,6 +641,158 @@ __global__ __launch_bounds__(256) void conv_patch_kernel(const float* __restrict
   }
 }
 
+// ---------------------------------------------------------------------------
+// Weight gradient from LDS tiles: for one (sample n, input channel ci, band of
+// output rows) a workgroup accumulates
+//   dW[co][ci][t] += sum_pos dy[n][co][pos] * x[n][ci][row(pos, kh)][col(pos, kw)]
+// for all 32 co and all taps t = kh*kw + kw, as MFMA tiles with M = co, N = 32
+// taps, K = output positions.  Per chunk of WG_RW x WG_CW output positions the
+// dy tile (position-major, 33-float rows: conflict-free A reads) and the x patch
+// those positions touch are staged once in LDS; a lane's tap is fixed, so every
+// B read is the lane's tap offset plus the position offset.  Partials per
+// (n, band) are reduced in a fixed order by wgrad_reduce_kernel (deterministic).
+constexpr int WG_RW = 2;            // output rows per chunk
+constexpr int WG_CW = 128;          // output columns per chunk
+constexpr int WG_DYP = 33;          // dy tile row pitch
+
+template <int NT, int XS>
+__global__ __launch_bounds__(256) void conv_wgrad_patch_kernel(const float* __restrict__ dy,
+                                                               const float* __restrict__ x,
+                                                               float* __restrict__ partial,
+                                                               ConvDims g, int bands, int xpitch) {
+  __shared__ __attribute__((aligned(16))) float dys[WG_RW * WG_CW * WG_DYP];
+  __shared__ __attribute__((aligned(16))) float xs[XS];
+  constexpr int DYREG = WG_RW * WG_CW * 32 / 256;
+  constexpr int XREG = (XS + 255) / 256;
+  const int band = blockIdx.x;
+  const int ci = blockIdx.y;
+  const int mbn = (g.co + 31) / 32;
+  const int n = blockIdx.z / mbn;
+  const int m0 = (blockIdx.z - n * mbn) * 32;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int lr = lane & 31, lk = lane >> 5;
+  const int T = g.kh * g.kw;
+  const int Kc = g.ci * T;
+  const int prow = (WG_RW - 1) * g.sh + g.kh;          // patch rows
+  const int pcol = (WG_CW - 1) * g.sw + g.kw;          // patch columns
+  const int pe = prow * pcol;
+  const int rchunks = (g.ho + WG_RW - 1) / WG_RW;
+  const int per_band = (rchunks + bands - 1) / bands;
+  const int rc0 = band * per_band;
+  const int rc1 = min(rchunks, rc0 + per_band);
+  const int ctiles = (g.wo + WG_CW - 1) / WG_CW;
+  const int nchunks = (rc1 - rc0) * ctiles;
+  const int dplane = g.ho * g.wo;
+  const int xplane = g.hi * g.wi;
+  const __amdgpu_buffer_rsrc_t drs =
+      conv_rsrc(dy + ((int64_t)n * g.co + m0) * dplane, (int64_t)min(32, g.co - m0) * dplane);
+  const __amdgpu_buffer_rsrc_t xrs = conv_rsrc(x + ((int64_t)n * g.ci + ci) * xplane, xplane);
+
+  // this lane's taps (one per tile) as patch offsets; invalid taps read offset 0
+  int tb[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    const int t = (wave * NT + j) * 32 + lr;
+    tb[j] = t < T ? (t / g.kw) * xpitch + (t - (t / g.kw) * g.kw) : 0;
+  }
+
+  float rd[DYREG], rx[XREG];
+  auto load = [&](int k) {
+    const int rc = rc0 + k / ctiles;
+    const int ho0 = rc * WG_RW;
+    const int wo0 = (k - (k / ctiles) * ctiles) * WG_CW;
+#pragma unroll
+    for (int r = 0; r < DYREG; ++r) {
+      const int idx = tid + 256 * r;                  // (co, row, col), col fastest
+      const int co = idx / (WG_RW * WG_CW);
+      const int rr = (idx / WG_CW) % WG_RW;
+      const int cc = idx % WG_CW;
+      const int ho = ho0 + rr, wo = wo0 + cc;
+      const bool ok = m0 + co < g.co && ho < g.ho && wo < g.wo;
+      rd[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                            drs, ok ? (co * dplane + ho * g.wo + wo) * 4 : 0x7ffffff0, 0, 0));
+    }
+    const int ir0 = ho0 * g.sh - g.ph, ic0 = wo0 * g.sw - g.pw;
+    int row = tid / pcol, col = tid - (tid / pcol) * pcol;
+#pragma unroll
+    for (int r = 0; r < XREG; ++r) {
+      const int ir = ir0 + row, ic = ic0 + col;
+      const bool ok = tid + 256 * r < pe && ir >= 0 && ir < g.hi && ic >= 0 && ic < g.wi;
+      rx[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                            xrs, ok ? (ir * g.wi + ic) * 4 : 0x7ffffff0, 0, 0));
+      col += 256;
+      while (col >= pcol) {
+        col -= pcol;
+        ++row;
+      }
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int r = 0; r < DYREG; ++r) {
+      const int idx = tid + 256 * r;
+      const int co = idx / (WG_RW * WG_CW);
+      const int pos = idx % (WG_RW * WG_CW);
+      dys[pos * WG_DYP + co] = rd[r];
+    }
+    int row = tid / pcol, col = tid - (tid / pcol) * pcol;
+#pragma unroll
+    for (int r = 0; r < XREG; ++r) {
+      if (tid + 256 * r < pe) xs[row * xpitch + col] = rx[r];
+      col += 256;
+      while (col >= pcol) {
+        col -= pcol;
+        ++row;
+      }
+    }
+  };
+
+  f32x16 acc[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+  if (nchunks > 0) {
+    load(0);
+    store();
+  }
+  __syncthreads();
+  const int rstep = g.sh * xpitch;
+  for (int k = 0; k < nchunks; ++k) {
+    if (k + 1 < nchunks) load(k + 1);
+    const float* arow = dys + lk * WG_DYP + lr;
+#pragma unroll 4
+    for (int s2 = 0; s2 < WG_RW * WG_CW / 2; ++s2) {
+      const int pos = 2 * s2;                        // + lk (folded into arow / boff)
+      const int rr = pos / WG_CW;
+      const int cc = pos - rr * WG_CW + lk;
+      const float av = arow[pos * WG_DYP];
+      const int boff = rr * rstep + cc * g.sw;
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, xs[tb[j] + boff], acc[j], 0, 0, 0);
+    }
+    __syncthreads();
+    if (k + 1 < nchunks) {
+      store();
+      __syncthreads();
+    }
+  }
+  float* out = partial + ((int64_t)n * bands + band) * g.co * Kc;
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    const int t = (wave * NT + j) * 32 + lr;
+    if (t >= T) continue;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int m = m0 + (r & 3) + 8 * (r >> 2) + 4 * lk;
+      if (m < g.co) out[(int64_t)m * Kc + ci * T + t] = acc[j][r];
+    }
+  }
+}
+
 static inline bool make_dims(ConvDims& g, int n, int c_in, int h_in, int w_in, int c_out, int kh,
                              int kw, int sh, int sw, int ph, int pw) {
   if (n < 0 || c_in < 1 || h_in < 1 || w_in < 1 || c_out < 1 || kh < 1 || kw < 1 || sh < 1 ||
@@ -696,6 +848,40 @@ static ds2_status_t launch_patch(const float* in, const float* w, const float* b
   return launch_status(DGRAD ? "ds2_conv2d_dgrad" : "ds2_conv2d_fwd");
 }
 
+constexpr int WG_XS_SMALL = 3200;    // x patch floats, <= 8 tap tiles (conv2: 23 x 139)
+constexpr int WG_XS_LARGE = 11520;   // x patch floats, <= 16 tap tiles (conv1: 43 x 267)
+
+struct WgradPlan {
+  int nt;        // tap tiles per wave (0: use the implicit-GEMM kernel)
+  int bands;     // output-row bands per (n, ci): more workgroups, more partial slabs
+  int xpitch;    // x patch row pitch (== 11 mod 32 spreads the 3 tap rows of a tile over banks)
+};
+
+static inline WgradPlan wgrad_plan(const ConvDims& g) {
+  WgradPlan pl{0, 1, 0};
+  if (getenv("DS2_CONV_PATCH") != nullptr && getenv("DS2_CONV_PATCH")[0] == '0') return pl;
+  const int T = g.kh * g.kw;
+  const int prow = (WG_RW - 1) * g.sh + g.kh;
+  const int pcol = (WG_CW - 1) * g.sw + g.kw;
+  int pitch = pcol + ((11 - pcol % 32) + 32) % 32;
+  const int64_t dplane = (int64_t)g.ho * g.wo, xplane = (int64_t)g.hi * g.wi;
+  if (32 * dplane * 4 >= (1ll << 31) - 64 || xplane * 4 >= (1ll << 31) - 64) return pl;
+  if (T <= 8 * 32 && prow * pitch <= WG_XS_SMALL) {
+    pl.nt = 2;
+  } else if (T <= 16 * 32 && prow * pitch <= WG_XS_LARGE) {
+    pl.nt = 4;
+  } else {
+    return pl;
+  }
+  pl.xpitch = pitch;
+  // enough workgroups to fill the chip about three times over
+  const int64_t wgs = (int64_t)g.n * g.ci * ((g.co + 31) / 32);
+  const int rchunks = (g.ho + WG_RW - 1) / WG_RW;
+  int bands = static_cast<int>((768 + wgs - 1) / wgs);
+  pl.bands = bands < 1 ? 1 : (bands > rchunks ? rchunks : bands);
+  return pl;
+}
+
 }  // namespace ds2
 
 using namespace ds2;
@@ -745,8 +931,10 @@ ds2_status_t ds2_conv2d_dgrad(const float* dy, const float* w, float* dx, int n,
 
 size_t ds2_conv2d_wgrad_workspace_size(int n, int c_in, int h_in, int w_in, int c_out, int kh,
                                        int kw, int sh, int sw, int ph, int pw) {
-  (void)h_in; (void)w_in; (void)sh; (void)sw; (void)ph; (void)pw;
-  return (size_t)n * c_out * c_in * kh * kw * sizeof(float) + 256;
+  ConvDims g;
+  if (!make_dims(g, n, c_in, h_in, w_in, c_out, kh, kw, sh, sw, ph, pw)) return 0;
+  const WgradPlan pl = wgrad_plan(g);
+  return (size_t)n * (pl.nt > 0 ? pl.bands : 1) * c_out * c_in * kh * kw * sizeof(float) + 256;
 }
 
 ds2_status_t ds2_conv2d_wgrad(const float* dy, const float* x, float* dw, float* dbias, int n,
@@ -762,12 +950,25 @@ ds2_status_t ds2_conv2d_wgrad(const float* dy, const float* x, float* dw, float*
   hipStream_t st = as_stream(stream);
   const int Kc = c_in * kh * kw;
   float* partial = static_cast<float*>(ws);
-  dim3 grid(cdiv(Kc, CBNW), n, cdiv(c_out, 32));
-  hipLaunchKernelGGL(conv_wgrad_kernel, grid, dim3(256), 0, st, dy, x, partial, g);
+  const WgradPlan pl = wgrad_plan(g);
+  int slabs = n;
+  if (pl.nt > 0) {
+    dim3 grid(pl.bands, c_in, n * cdiv(c_out, 32));
+    if (pl.nt == 2)
+      hipLaunchKernelGGL((conv_wgrad_patch_kernel<2, WG_XS_SMALL>), grid, dim3(256), 0, st, dy, x,
+                         partial, g, pl.bands, pl.xpitch);
+    else
+      hipLaunchKernelGGL((conv_wgrad_patch_kernel<4, WG_XS_LARGE>), grid, dim3(256), 0, st, dy, x,
+                         partial, g, pl.bands, pl.xpitch);
+    slabs = n * pl.bands;
+  } else {
+    dim3 grid(cdiv(Kc, CBNW), n, cdiv(c_out, 32));
+    hipLaunchKernelGGL(conv_wgrad_kernel, grid, dim3(256), 0, st, dy, x, partial, g);
+  }
   const int64_t per = (int64_t)c_out * Kc;
   int rg = cdiv(per, 256);
   if (rg > 2048) rg = 2048;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(rg), dim3(256), 0, st, partial, n, per, dw);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(rg), dim3(256), 0, st, partial, slabs, per, dw);
   if (dbias != nullptr)
     hipLaunchKernelGGL(bias_grad_kernel, dim3(c_out), dim3(256), 0, st, dy, n, c_out,
                        (int64_t)g.ho * g.wo, dbias);
