@@ -92,8 +92,8 @@ template <int TA, int TB, bool VA, bool VB>
 __global__ __launch_bounds__(256) void sgemm_kernel(
     int M, int N, int K, float alpha, const float* __restrict__ A, int64_t lda, int64_t sA,
     const float* __restrict__ B, int64_t ldb, int64_t sB, float beta, float* __restrict__ C,
-    int64_t ldc, int64_t sC, const float* __restrict__ bias, int nsplit, int kchunk,
-    float* __restrict__ partial) {
+    int64_t ldc, int64_t sC, const float* __restrict__ bias, int main_wgs, int tail_tile0,
+    int tail_tiles, int nsplit, int kchunk, float* __restrict__ partial) {
   // op(A) is k-contiguous when TA == 0 ([m][k] storage); op(B) is k-contiguous
   // when TB == 1 ([n][k] storage).
   constexpr bool AK = (TA == 0);
@@ -103,31 +103,39 @@ __global__ __launch_bounds__(256) void sgemm_kernel(
   __shared__ __attribute__((aligned(16))) float As[2][BK * LDA_S];
   __shared__ __attribute__((aligned(16))) float Bs[2][BK * LDB_S];
 
-  // 1-D grid, XCD-aware (bijective) remap: the blocks the dispatcher deals to one
-  // XCD (ids congruent mod 8) get a contiguous run of tiles, n-tile fastest, so the
-  // workgroups sharing an A row panel (and a k-range) share that XCD's L2.
+  // Work items (blockIdx.x in dispatch order):
+  //   [0, main_wgs)       one whole output tile each (batch == 1), XCD-aware order;
+  //   [main_wgs, grid)    "tail" pieces: (batch, split, tile) of the tiles from tail_tile0
+  //                       on, K range split nsplit ways; dispatched last, they fill the
+  //                       slots the whole tiles leave in the final round.
+  // XCD-aware (bijective) remap of the whole-tile range: the blocks the dispatcher deals
+  // to one XCD (ids congruent mod 8) get a contiguous run of tiles, n-tile fastest, so
+  // workgroups sharing an A row panel share that XCD's L2.
   const int tn = (N + BN - 1) / BN;
-  const int tm = (M + BM - 1) / BM;
-  const int nwg = gridDim.x;
-  int wgid;
-  {
-    const int orig = blockIdx.x;
+  const int orig = blockIdx.x;
+  int tile, z = 0;
+  float* __restrict__ part = nullptr;
+  if (orig < main_wgs) {
+    const int q = main_wgs >> 3, r = main_wgs & 7;
     const int xcd = orig & 7;
-    const int q = nwg >> 3, r = nwg & 7;
-    wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+    tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+  } else {
+    const int pidx = orig - main_wgs;
+    z = pidx / tail_tiles;
+    const int lt = pidx - z * tail_tiles;
+    tile = tail_tile0 + lt;
+    if (nsplit > 1) part = partial + ((int64_t)z * tail_tiles + lt) * (BM * BN);
   }
-  const int z = wgid / (tm * tn);
-  const int rem = wgid - z * tm * tn;
-  const int tile_m = rem / tn;
-  const int tile_n = rem - tile_m * tn;
-  // z = batch * nsplit + split; split-K partials go to partial[z][m][n]
+  const int tile_m = tile / tn;
+  const int tile_n = tile - tile_m * tn;
+  // z = batch * nsplit + split
   const int bz = z / nsplit;
   const int sp = z - bz * nsplit;
   A += bz * sA;
   B += bz * sB;
   C += bz * sC;
-  const int kbeg = sp * kchunk;
-  const int kend = min(K, kbeg + kchunk);
+  const int kbeg = orig < main_wgs ? 0 : sp * kchunk;
+  const int kend = orig < main_wgs ? K : min(K, kbeg + kchunk);
   const int m0 = tile_m * BM;
   const int n0 = tile_n * BN;
   const int lane = threadIdx.x & 63;
@@ -188,12 +196,11 @@ __global__ __launch_bounds__(256) void sgemm_kernel(
     for (int j = 0; j < 2; ++j) {
       const int col = n0 + wn + 32 * j + lr;
       if (col >= N) continue;
-      if (partial != nullptr) {
-        float* pp = partial + (int64_t)z * M * N;
+      if (part != nullptr) {              // tile-local [BM][BN] partial slab
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int row = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lk;
-          if (row < M) pp[(int64_t)row * N + col] = acc[i][j][r];
+          const int rl = wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lk;
+          part[rl * BN + wn + 32 * j + lr] = acc[i][j][r];
         }
         continue;
       }
@@ -212,20 +219,27 @@ __global__ __launch_bounds__(256) void sgemm_kernel(
   }
 }
 
-// C[b] = alpha * sum_s partial[b*nsplit + s] + beta * C[b] + bias (fixed order)
+// Tail tiles: C[b] = alpha * sum_s partial[b][s][tile] + beta * C[b] + bias (fixed order)
 __global__ void splitk_reduce_kernel(const float* __restrict__ partial, int M, int N, int nsplit,
-                                     int batch, float alpha, float beta, float* __restrict__ C,
-                                     int64_t ldc, int64_t sC, const float* __restrict__ bias) {
-  const int64_t per = (int64_t)M * N;
-  const int64_t total = per * batch;
+                                     int batch, int tail_tile0, int tail_tiles, float alpha,
+                                     float beta, float* __restrict__ C, int64_t ldc, int64_t sC,
+                                     const float* __restrict__ bias) {
+  constexpr int TE = BM * BN;
+  const int tn = (N + BN - 1) / BN;
+  const int64_t total = (int64_t)batch * tail_tiles * TE;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * blockDim.x) {
-    const int b = static_cast<int>(i / per);
-    const int64_t e = i - b * per;
-    const int row = static_cast<int>(e / N);
-    const int col = static_cast<int>(e - (int64_t)row * N);
+    const int e = static_cast<int>(i % TE);
+    const int64_t bt = i / TE;
+    const int lt = static_cast<int>(bt % tail_tiles);
+    const int b = static_cast<int>(bt / tail_tiles);
+    const int tile = tail_tile0 + lt;
+    const int row = (tile / tn) * BM + e / BN;
+    const int col = (tile % tn) * BN + e % BN;
+    if (row >= M || col >= N) continue;
     float acc = 0.f;
-    for (int sp = 0; sp < nsplit; ++sp) acc += partial[((int64_t)b * nsplit + sp) * per + e];
+    for (int sp = 0; sp < nsplit; ++sp)
+      acc += partial[(((int64_t)b * nsplit + sp) * tail_tiles + lt) * TE + e];
     float* cp = C + b * sC + (int64_t)row * ldc + col;
     float v = alpha * acc + (bias != nullptr ? bias[col] : 0.f);
     if (beta != 0.f) v += beta * *cp;
@@ -237,10 +251,12 @@ template <int TA, int TB>
 static void launch_sgemm_t(bool va, bool vb, dim3 grid, hipStream_t st, int M, int N, int K,
                            float alpha, const float* A, int64_t lda, int64_t sA, const float* B,
                            int64_t ldb, int64_t sB, float beta, float* C, int64_t ldc,
-                           int64_t sC, const float* bias, int nsplit, int kchunk, float* partial) {
+                           int64_t sC, const float* bias, int main_wgs, int tail_tile0,
+                           int tail_tiles, int nsplit, int kchunk, float* partial) {
 #define DS2_L(VA, VB)                                                                      \
   hipLaunchKernelGGL((sgemm_kernel<TA, TB, VA, VB>), grid, dim3(256), 0, st, M, N, K, alpha, A, \
-                     lda, sA, B, ldb, sB, beta, C, ldc, sC, bias, nsplit, kchunk, partial)
+                     lda, sA, B, ldb, sB, beta, C, ldc, sC, bias, main_wgs, tail_tile0,        \
+                     tail_tiles, nsplit, kchunk, partial)
   if (va && vb) DS2_L(true, true);
   else if (va) DS2_L(true, false);
   else if (vb) DS2_L(false, true);
@@ -254,21 +270,68 @@ static inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t
 
 using namespace ds2;
 
-// Split-K only when the output grid is too small to fill the chip (4 resident
-// 256-thread workgroups per CU x 256 CUs) and K is long: weight gradients such as
-// dW_hh = dG^T h (M = 2400, N = 800, K = T*N = 16032) have only 133 output tiles.
-static int choose_split(int m, int n, int k, int batch) {
-  const int64_t tiles = (int64_t)cdiv(m, BM) * cdiv(n, BN) * batch;
-  if (tiles >= 768 || k < 2048) return 1;
-  int s = static_cast<int>((1024 + tiles - 1) / tiles);
-  s = std::min(s, std::max(1, k / 1024));
-  return std::max(1, std::min(s, 32));
+static int g_cus = -1;
+static int device_cus() {
+  if (g_cus < 0) {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        v <= 0)
+      v = 256;
+    g_cus = v;
+  }
+  return g_cus;
+}
+
+// Work plan.  Whole tiles run in full rounds of `slots` resident workgroups (3 per CU);
+// the tiles of a last, partial round ("tail") have their K range split so that the
+// round is filled: e.g. the input projection 16032 x 2400 = 2394 tiles = 3 rounds of
+// 768 + 90 tail tiles x 8 splits; the weight gradient 2400 x 800 (133 tiles, K = 16032)
+// becomes 133 tiles x 5 splits.  Split partials are reduced in a fixed order.
+struct GemmPlan {
+  int main_wgs, tail_tile0, tail_tiles, nsplit, kchunk;
+};
+
+static GemmPlan gemm_plan(int m, int n, int k, int batch) {
+  const int tiles = cdiv(m, BM) * cdiv(n, BN);
+  GemmPlan p{0, 0, tiles, 1, std::max(k, 1)};
+  const int slots = 3 * device_cus();
+  if (batch == 1) {
+    p.main_wgs = (tiles / slots) * slots;
+    p.tail_tile0 = p.main_wgs;
+    p.tail_tiles = tiles - p.main_wgs;
+    if (p.tail_tiles == 0) {   // full rounds only
+      p.main_wgs = 0;
+      p.tail_tile0 = 0;
+      p.tail_tiles = tiles;
+      return p;
+    }
+  }
+  const int64_t tail = (int64_t)p.tail_tiles * batch;
+  const int smax = std::max(1, std::min(32, k / 256));
+  double best = 1e30;
+  int bs = 1;
+  for (int s = 1; s <= smax; ++s) {
+    const double rounds = (double)((tail * s + slots - 1) / slots);
+    const double cost = rounds / s + (s > 1 ? 0.005 * s : 0.0);
+    if (cost < best - 1e-9) {
+      best = cost;
+      bs = s;
+    }
+  }
+  if (bs > 1) {
+    p.kchunk = cdiv(cdiv(k, bs), BK) * BK;
+    p.nsplit = cdiv(k, p.kchunk);
+  }
+  return p;
 }
 
 extern "C" size_t ds2_sgemm_workspace_size(int m, int n, int k, int batch) {
   if (m <= 0 || n <= 0 || k <= 0 || batch <= 0) return 0;
-  const int s = choose_split(m, n, k, batch);
-  return s > 1 ? (size_t)s * batch * m * n * sizeof(float) + 256 : 0;
+  const GemmPlan p = gemm_plan(m, n, k, batch);
+  return p.nsplit > 1
+             ? (size_t)p.nsplit * batch * p.tail_tiles * BM * BN * sizeof(float) + 256
+             : 0;
 }
 
 extern "C" ds2_status_t ds2_sgemm_ws(int trans_a, int trans_b, int m, int n, int k, float alpha,
@@ -287,30 +350,31 @@ extern "C" ds2_status_t ds2_sgemm_ws(int trans_a, int trans_b, int m, int n, int
                   (trans_a ? (m % 4 == 0) : (k % 4 == 0));
   const bool vb = aligned16(b) && (ldb % 4 == 0) && (stride_b % 4 == 0) &&
                   (trans_b ? (k % 4 == 0) : (n % 4 == 0));
-  int nsplit = 1;
-  if (ws != nullptr && ws_bytes >= ds2_sgemm_workspace_size(m, n, k, batch))
-    nsplit = choose_split(m, n, k, batch);
-  const int kchunk = nsplit > 1 ? cdiv(cdiv(k, nsplit), BK) * BK : std::max(k, 1);
-  nsplit = nsplit > 1 ? cdiv(k, kchunk) : 1;
-  float* partial = nsplit > 1 ? static_cast<float*>(ws) : nullptr;
-  const int64_t nwg = (int64_t)cdiv(n, BN) * cdiv(m, BM) * batch * nsplit;
+  GemmPlan p = gemm_plan(m, n, k, batch);
+  if (p.nsplit > 1 && (ws == nullptr || ws_bytes < ds2_sgemm_workspace_size(m, n, k, batch))) {
+    p.nsplit = 1;                       // no workspace: whole-K pieces
+    p.kchunk = std::max(k, 1);
+  }
+  float* partial = p.nsplit > 1 ? static_cast<float*>(ws) : nullptr;
+  const int64_t nwg = p.main_wgs + (int64_t)p.tail_tiles * batch * p.nsplit;
   if (nwg > 0x7fffffff) return DS2_UNSUPPORTED_SHAPE;
   dim3 grid(static_cast<unsigned>(nwg));
   hipStream_t st = as_stream(stream);
 #define DS2_G(TA_, TB_)                                                                       \
   launch_sgemm_t<TA_, TB_>(va, vb, grid, st, m, n, k, alpha, a, lda, stride_a, b, ldb, stride_b, \
-                           beta, c, ldc, stride_c, bias, nsplit, kchunk, partial)
+                           beta, c, ldc, stride_c, bias, p.main_wgs, p.tail_tile0, p.tail_tiles,  \
+                           p.nsplit, p.kchunk, partial)
   if (!trans_a && !trans_b) DS2_G(0, 0);
   else if (!trans_a && trans_b) DS2_G(0, 1);
   else if (trans_a && !trans_b) DS2_G(1, 0);
   else DS2_G(1, 1);
 #undef DS2_G
-  if (nsplit > 1) {
-    int64_t total = (int64_t)m * n * batch;
+  if (p.nsplit > 1) {
+    const int64_t total = (int64_t)batch * p.tail_tiles * BM * BN;
     int g = cdiv(total, 256);
-    if (g > 2048) g = 2048;
-    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(g), dim3(256), 0, st, partial, m, n, nsplit,
-                       batch, alpha, beta, c, ldc, stride_c, bias);
+    if (g > 4096) g = 4096;
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(g), dim3(256), 0, st, partial, m, n, p.nsplit,
+                       batch, p.tail_tile0, p.tail_tiles, alpha, beta, c, ldc, stride_c, bias);
   }
   return launch_status("ds2_sgemm");
 }

@@ -41,6 +41,25 @@ def test_sgemm(dev, ta, tb, m, n, k):
     _close(cd, ref, 1e-5, "sgemm")
 
 
+@pytest.mark.parametrize("ta,tb", [(0, 1), (1, 0)])
+def test_sgemm_full_rounds_plus_split_tail(dev, ta, tb):
+    """783 output tiles = one full round of resident workgroups + 15 tail tiles whose K
+    range is split (one launch) and reduced in a fixed order; alpha/beta/bias applied once."""
+    m, n, k = 128 * 29, 128 * 27, 2048
+    g = torch.Generator().manual_seed(5)
+    a = torch.randn(k, m, generator=g) if ta else torch.randn(m, k, generator=g)
+    b = torch.randn(n, k, generator=g) if tb else torch.randn(k, n, generator=g)
+    c0 = torch.randn(m, n, generator=g)
+    bias = torch.randn(n, generator=g)
+    ref = 0.5 * ((a.t() if ta else a).double() @ (b.t() if tb else b).double()) \
+        + 0.25 * c0.double() + bias.double()
+    ad, bd, cd = a.to(dev), b.to(dev), c0.to(dev).clone()
+    ops.sgemm(ad, bd, cd, m=m, n=n, k=k, trans_a=bool(ta), trans_b=bool(tb),
+              lda=ad.shape[1], ldb=bd.shape[1], ldc=n, alpha=0.5, beta=0.25, bias=bias.to(dev))
+    torch.cuda.synchronize()
+    _close(cd, ref, 1e-5, "sgemm main+tail")
+
+
 # ---------------------------------------------------------------------------- conv
 CONVS = [  # (n, ci, h, w, co, kh, kw, sh, sw, ph, pw)
     (2, 1, 161, 37, 32, 41, 11, 2, 2, 20, 5),
