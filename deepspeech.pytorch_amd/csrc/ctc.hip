@@ -255,6 +255,240 @@ __global__ void greedy_kernel(const float* __restrict__ probs, int n, int t_max,
   if (lane == 0) out_counts[wave] = count;
 }
 
+
+// ---------------------------------------------------------------------------
+// CTC prefix beam search without a language model (BeamCTCDecoder, decoder.py:90-143,
+// wrapping ctcdecode's ctc_beam_search_decoder with lm_path=None).  One 64-lane
+// workgroup per utterance; the beam (<= BEAM_MAX prefixes) lives in LDS, the prefix
+// trie (parent, char, timestep, best char log-prob) in the workspace.  Per frame:
+// prune the vocabulary (cutoff_top_n / cutoff_prob), score every candidate
+// (prefix x char: blank / repeat "stay" terms, extensions, extensions that land on a
+// prefix already in the beam are merged into it), then keep the beam_width best by
+// (score desc, last char asc, candidate index asc).  oracle/ctc_beam.py restates the
+// same algorithm (parity with ctcdecode itself is unpinned: it is not available).
+constexpr int BEAM_MAX = 32;
+constexpr int BEAM_CMAX = 64;
+
+__device__ __forceinline__ float beam_lse(float a, float b) {
+  if (a == -INFINITY) return b;
+  if (b == -INFINITY) return a;
+  const float m = fmaxf(a, b);
+  return logf(expf(a - m) + expf(b - m)) + m;
+}
+
+// lexicographic "better": higher score, then lower char, then lower candidate index
+__device__ __forceinline__ bool beam_better(float s1, int key1, float s2, int key2) {
+  return s1 > s2 || (s1 == s2 && key1 < key2);
+}
+
+__global__ __launch_bounds__(64) void ctc_beam_kernel(
+    const float* __restrict__ probs, int t_max, int C, int64_t stride_n, int64_t stride_t,
+    const int* __restrict__ sizes, int blank, int beam, int cutoff_top_n, double cutoff_prob,
+    int top_paths, int* __restrict__ node_parent, int* __restrict__ node_ch,
+    int* __restrict__ node_ts, float* __restrict__ node_lpc, int64_t node_cap,
+    int* __restrict__ out_ids, int* __restrict__ out_ts, int* __restrict__ out_lens,
+    float* __restrict__ out_scores) {
+  __shared__ float lp[BEAM_CMAX];
+  __shared__ int allowed[BEAM_CMAX];
+  __shared__ int order[BEAM_CMAX];
+  __shared__ int b_node[2][BEAM_MAX], b_last[2][BEAM_MAX];
+  __shared__ float b_pb[2][BEAM_MAX], b_pnb[2][BEAM_MAX];
+  __shared__ float score[BEAM_MAX];
+  __shared__ int pidx[BEAM_MAX];
+  __shared__ signed char child_of[BEAM_MAX * BEAM_CMAX];
+  __shared__ float cs[BEAM_MAX * BEAM_CMAX], cpb[BEAM_MAX * BEAM_CMAX], cpnb[BEAM_MAX * BEAM_CMAX];
+  __shared__ int sel_k[BEAM_MAX];
+  __shared__ int s_nb, s_nodes;
+
+  const int n = blockIdx.x;
+  const int lane = threadIdx.x;
+  int size = sizes != nullptr ? sizes[n] : t_max;
+  size = size < 0 ? 0 : (size > t_max ? t_max : size);
+  const float* pn = probs + (int64_t)n * stride_n;
+  int* par = node_parent + (int64_t)n * node_cap;
+  int* chr = node_ch + (int64_t)n * node_cap;
+  int* tst = node_ts + (int64_t)n * node_cap;
+  float* lpcv = node_lpc + (int64_t)n * node_cap;
+  const bool prune = cutoff_prob < 1.0 || cutoff_top_n < C;
+
+  if (lane == 0) {
+    b_node[0][0] = 0; b_last[0][0] = -1; b_pb[0][0] = 0.f; b_pnb[0][0] = -INFINITY;
+    par[0] = -1; chr[0] = -1; tst[0] = -1; lpcv[0] = -INFINITY;
+    s_nb = 1;
+    s_nodes = 1;
+  }
+  __syncthreads();
+  int cur = 0;
+  for (int t = 0; t < size; ++t) {
+    const int nb = s_nb;
+    if (nb == 0) break;
+    // ---- vocabulary pruning and log probs
+    float pv = 0.f;
+    if (lane < C) {
+      pv = pn[(int64_t)t * stride_t + lane];
+      lp[lane] = logf(pv + 1.17549435e-38f);
+    }
+    if (prune) {
+      int rank = 0;
+      for (int k = 0; k < C; ++k) {
+        const float q = __shfl(pv, k, 64);
+        rank += (q > pv || (q == pv && k < lane)) ? 1 : 0;
+      }
+      if (lane < C) order[rank] = lane;
+      __syncthreads();
+      if (lane < C) {
+        int ok = rank < cutoff_top_n;
+        if (ok && cutoff_prob < 1.0) {
+          double cum = 0.0;
+          for (int r = 0; r < rank; ++r) cum += (double)pn[(int64_t)t * stride_t + order[r]];
+          ok = cum < cutoff_prob;
+        }
+        allowed[lane] = ok;
+      }
+    } else if (lane < C) {
+      allowed[lane] = 1;
+    }
+    // ---- beam bookkeeping: scores, parent index in the beam, child map
+    if (lane < nb) {
+      score[lane] = beam_lse(b_pb[cur][lane], b_pnb[cur][lane]);
+      const int nd = b_node[cur][lane];
+      const int pnode = nd > 0 ? par[nd] : -1;
+      int j = -1;
+      for (int i = 0; i < nb; ++i)
+        if (pnode >= 0 && b_node[cur][i] == pnode) j = i;
+      pidx[lane] = j;
+    }
+    for (int e = lane; e < nb * C; e += 64) child_of[e] = -1;
+    __syncthreads();
+    if (lane < nb && pidx[lane] >= 0) child_of[pidx[lane] * C + b_last[cur][lane]] = lane;
+    __syncthreads();
+    // ---- candidates
+    for (int k = lane; k < nb * C; k += 64) {
+      const int i = k / C;
+      const int c = k - i * C;
+      const int last_i = b_last[cur][i];
+      const float pb_i = b_pb[cur][i];
+      float sc = -INFINITY, pb = -INFINITY, pnb = -INFINITY;
+      if (c == blank) {
+        pb = allowed[blank] ? lp[blank] + score[i] : -INFINITY;
+        pnb = (last_i >= 0 && allowed[last_i]) ? lp[last_i] + b_pnb[cur][i] : -INFINITY;
+        const int j = pidx[i];
+        if (j >= 0 && allowed[last_i]) {
+          const float e = (last_i == b_last[cur][j])
+                              ? (b_pb[cur][j] != -INFINITY ? lp[last_i] + b_pb[cur][j] : -INFINITY)
+                              : lp[last_i] + score[j];
+          pnb = beam_lse(pnb, e);
+          const int nd = b_node[cur][i];
+          if (lp[last_i] > lpcv[nd]) {
+            lpcv[nd] = lp[last_i];
+            tst[nd] = t;
+          }
+        }
+        sc = beam_lse(pb, pnb);
+      } else if (allowed[c] && child_of[k] < 0) {
+        pnb = (c == last_i) ? (pb_i != -INFINITY ? lp[c] + pb_i : -INFINITY) : lp[c] + score[i];
+        sc = pnb;
+      }
+      cs[k] = sc;
+      cpb[k] = pb;
+      cpnb[k] = pnb;
+    }
+    __syncthreads();
+    // ---- keep the best `beam` candidates
+    int nsel = 0;
+    for (int r = 0; r < beam; ++r) {
+      float bs = -INFINITY;
+      int bkey = 0x7fffffff;
+      for (int k = lane; k < nb * C; k += 64) {
+        const float sk = cs[k];
+        if (sk == -INFINITY) continue;
+        const int i = k / C;
+        const int c = k - i * C;
+        const int ch = c == blank ? b_last[cur][i] : c;
+        const int key = (ch + 1) * 4096 + k;
+        if (beam_better(sk, key, bs, bkey)) {
+          bs = sk;
+          bkey = key;
+        }
+      }
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) {
+        const float os = __shfl_xor(bs, off, 64);
+        const int ok = __shfl_xor(bkey, off, 64);
+        if (beam_better(os, ok, bs, bkey)) {
+          bs = os;
+          bkey = ok;
+        }
+      }
+      if (bs == -INFINITY) break;
+      const int k = bkey & 4095;
+      if (lane == 0) {
+        sel_k[r] = k;
+        cs[k] = -INFINITY;
+      }
+      __syncthreads();
+      ++nsel;
+    }
+    // ---- new beam (new prefixes get trie nodes in rank order)
+    const int nxt = cur ^ 1;
+    if (lane == 0) {
+      int nodes = s_nodes;
+      for (int r = 0; r < nsel; ++r) {
+        const int k = sel_k[r];
+        const int i = k / C;
+        const int c = k - i * C;
+        if (c == blank) {
+          b_node[nxt][r] = b_node[cur][i];
+          b_last[nxt][r] = b_last[cur][i];
+        } else {
+          par[nodes] = b_node[cur][i];
+          chr[nodes] = c;
+          tst[nodes] = t;
+          lpcv[nodes] = lp[c];
+          b_node[nxt][r] = nodes;
+          b_last[nxt][r] = c;
+          ++nodes;
+        }
+        b_pb[nxt][r] = cpb[k];
+        b_pnb[nxt][r] = cpnb[k];
+      }
+      s_nodes = nodes;
+      s_nb = nsel;
+    }
+    __syncthreads();
+    cur = nxt;
+  }
+  // ---- final ranking and back-tracking (one lane per returned path)
+  const int nb = s_nb;
+  if (lane < nb) score[lane] = beam_lse(b_pb[cur][lane], b_pnb[cur][lane]);
+  __syncthreads();
+  if (lane < nb) {
+    int rank = 0;
+    const float s0 = score[lane];
+    const int key0 = (b_last[cur][lane] + 1) * 4096 + lane;
+    for (int i = 0; i < nb; ++i)
+      if (i != lane && beam_better(score[i], (b_last[cur][i] + 1) * 4096 + i, s0, key0)) ++rank;
+    if (rank < top_paths) {
+      int len = 0;
+      for (int nd = b_node[cur][lane]; nd > 0; nd = par[nd]) ++len;
+      int* ids = out_ids + ((int64_t)n * top_paths + rank) * t_max;
+      int* tsp = out_ts + ((int64_t)n * top_paths + rank) * t_max;
+      int pos = len;
+      for (int nd = b_node[cur][lane]; nd > 0; nd = par[nd]) {
+        --pos;
+        ids[pos] = chr[nd];
+        tsp[pos] = tst[nd];
+      }
+      out_lens[n * top_paths + rank] = len;
+      out_scores[n * top_paths + rank] = s0;
+    }
+  }
+  for (int r = nb + lane; r < top_paths; r += 64) {   // fewer prefixes than paths asked for
+    out_lens[n * top_paths + r] = 0;
+    out_scores[n * top_paths + r] = -INFINITY;
+  }
+}
+
 }  // namespace ds2
 
 using namespace ds2;
@@ -316,6 +550,39 @@ ds2_status_t ds2_greedy_decode(const float* probs, int n, int t_max, int c, int6
                      t_max, c, stride_n, stride_t, sizes, blank, out_ids, out_offsets, out_counts,
                      argmax_out);
   return launch_status("ds2_greedy_decode");
+}
+
+size_t ds2_ctc_beam_workspace_size(int n, int t_max, int beam) {
+  const size_t cap = (size_t)t_max * (beam > 0 ? beam : 1) + 1;
+  return 4 * al256((size_t)n * cap * 4) + 256;
+}
+
+ds2_status_t ds2_ctc_beam_decode(const float* probs, int n, int t_max, int c, int64_t stride_n,
+                                 int64_t stride_t, const int* sizes, int blank, int beam_width,
+                                 int cutoff_top_n, double cutoff_prob, int top_paths,
+                                 int* out_ids, int* out_offsets, int* out_lens,
+                                 float* out_scores, void* ws, size_t ws_bytes,
+                                 ds2_stream_t stream) {
+  if (n < 0 || t_max < 0 || c < 1 || blank < 0 || blank >= c || beam_width < 1 ||
+      top_paths < 1 || top_paths > beam_width || cutoff_top_n < 1)
+    return DS2_INVALID_VALUE;
+  if (c > BEAM_CMAX || beam_width > BEAM_MAX || (int64_t)beam_width * c > 4096)
+    return DS2_UNSUPPORTED_SHAPE;
+  if (n == 0) return DS2_OK;
+  if (ws == nullptr || ws_bytes < ds2_ctc_beam_workspace_size(n, t_max, beam_width))
+    return DS2_WORKSPACE_TOO_SMALL;
+  const int64_t cap = (int64_t)t_max * beam_width + 1;
+  char* w = static_cast<char*>(ws);
+  const size_t plane = al256((size_t)n * cap * 4);
+  int* par = reinterpret_cast<int*>(w);
+  int* chr = reinterpret_cast<int*>(w + plane);
+  int* tst = reinterpret_cast<int*>(w + 2 * plane);
+  float* lpc = reinterpret_cast<float*>(w + 3 * plane);
+  hipLaunchKernelGGL(ctc_beam_kernel, dim3(n), dim3(64), 0, as_stream(stream), probs, t_max, c,
+                     stride_n, stride_t, sizes, blank, beam_width, cutoff_top_n, cutoff_prob,
+                     top_paths, par, chr, tst, lpc, cap, out_ids, out_offsets, out_lens,
+                     out_scores);
+  return launch_status("ds2_ctc_beam_decode");
 }
 
 }  // extern "C"

@@ -55,50 +55,45 @@ class Decoder(object):
 
 
 class BeamCTCDecoder(Decoder):
-    """Wraps ctcdecode.CTCBeamDecoder exactly like ref decoder.py:90-143 (external, unpinned)."""
+    """CTC prefix beam search on the GPU (ds2_ctc_beam_decode), drop-in for ref
+    decoder.py:90-143 without a language model.
+
+    Same constructor and ``decode(probs, sizes) -> (strings, offsets)`` as the
+    reference, whose ctcdecode backend returns every beam: strings[n][p] /
+    offsets[n][p] for p < beam_width, best first.  KenLM scoring (lm_path, alpha,
+    beta) is not available; without an LM ctcdecode ignores alpha/beta too.
+    """
 
     def __init__(self, labels, lm_path=None, alpha=0, beta=0, cutoff_top_n=40, cutoff_prob=1.0,
                  beam_width=100, num_processes=4, blank_index=0):
-        super().__init__(labels)
-        try:
-            from ctcdecode import CTCBeamDecoder
-        except ImportError:
-            raise ImportError("BeamCTCDecoder requires paddledecoder package.")
-        self._decoder = CTCBeamDecoder(labels, lm_path, alpha, beta, cutoff_top_n, cutoff_prob,
-                                       beam_width, num_processes, blank_index)
+        super().__init__(labels, blank_index=blank_index)
+        if lm_path is not None:
+            raise NotImplementedError("ds2amd.BeamCTCDecoder: KenLM language-model scoring is "
+                                      "not supported (lm_path must be None)")
+        if beam_width > 32:
+            raise ValueError("ds2amd.BeamCTCDecoder: beam_width <= 32")
+        self.beam_width = int(beam_width)
+        self.cutoff_top_n = int(cutoff_top_n)
+        self.cutoff_prob = float(cutoff_prob)
 
-    def convert_to_strings(self, out, seq_len):
-        results = []
-        for b, batch in enumerate(out):
-            utterances = []
-            for p, utt in enumerate(batch):
-                size = seq_len[b][p]
-                if size > 0:
-                    transcript = ''.join(map(lambda x: self.int_to_char[x.item()], utt[0:size]))
-                else:
-                    transcript = ''
-                utterances.append(transcript)
-            results.append(utterances)
-        return results
-
-    def convert_tensor(self, offsets, sizes):
-        results = []
-        for b, batch in enumerate(offsets):
-            utterances = []
-            for p, utt in enumerate(batch):
-                size = sizes[b][p]
-                if sizes[b][p] > 0:
-                    utterances.append(utt[0:size])
-                else:
-                    utterances.append(torch.tensor([], dtype=torch.int))
-            results.append(utterances)
-        return results
+    def decode_raw(self, probs, sizes=None):
+        """Device tensors (ids [N,P,T], offsets [N,P,T], lens [N,P], scores [N,P])."""
+        return ops.ctc_beam_decode_raw(probs, sizes, self.beam_width, self.beam_width,
+                                       blank=self.blank_index, cutoff_top_n=self.cutoff_top_n,
+                                       cutoff_prob=self.cutoff_prob)
 
     def decode(self, probs, sizes=None):
-        probs = probs.cpu()
-        out, scores, offsets, seq_lens = self._decoder.decode(probs, sizes)
-        strings = self.convert_to_strings(out, seq_lens)
-        offsets = self.convert_tensor(offsets, seq_lens)
+        ids, offs, lens, _ = self.decode_raw(probs, sizes)
+        ids, offs, lens = ids.cpu(), offs.cpu(), lens.cpu()
+        strings, offsets = [], []
+        for b in range(ids.shape[0]):
+            sb, ob = [], []
+            for p in range(ids.shape[1]):
+                k = int(lens[b, p])
+                sb.append(''.join(self.int_to_char[int(x)] for x in ids[b, p, :k]))
+                ob.append(offs[b, p, :k].clone() if k > 0 else torch.tensor([], dtype=torch.int))
+            strings.append(sb)
+            offsets.append(ob)
         return strings, offsets
 
 

@@ -205,6 +205,34 @@ def greedy_decode_raw(probs: torch.Tensor, sizes: Optional[torch.Tensor], blank:
     return ids, offs, counts, am
 
 
+def ctc_beam_decode_raw(probs: torch.Tensor, sizes: Optional[torch.Tensor], beam_width: int,
+                        top_paths: int, blank: int = 0, cutoff_top_n: int = 40,
+                        cutoff_prob: float = 1.0):
+    """Device CTC prefix beam search (no LM).  probs [N,T,C] fp32 (any strides).
+
+    Returns (ids [N,P,T] int32, offsets [N,P,T] int32, lens [N,P] int32, scores [N,P]
+    fp32), paths best first; row (n, p) holds lens[n, p] valid entries.
+    """
+    if not probs.is_cuda or probs.dtype != _F32:
+        raise _lib.Ds2Error("ctc_beam_decode: expected a float32 device tensor")
+    n, t, c = probs.shape
+    if probs.stride(2) != 1:
+        probs = probs.contiguous()
+    dev = probs.device
+    ids = torch.empty(n, top_paths, t, device=dev, dtype=_I32)
+    offs = torch.empty(n, top_paths, t, device=dev, dtype=_I32)
+    lens = torch.empty(n, top_paths, device=dev, dtype=_I32)
+    scores = torch.empty(n, top_paths, device=dev, dtype=_F32)
+    if sizes is not None:
+        sizes = sizes.to(device=dev, dtype=_I32).contiguous()
+    ws = _ws(_lib.size("ds2_ctc_beam_workspace_size", n, t, beam_width), dev)
+    _lib.call("ds2_ctc_beam_decode", probs.data_ptr(), n, t, c, probs.stride(0), probs.stride(1),
+              _p(sizes), int(blank), int(beam_width), int(cutoff_top_n), float(cutoff_prob),
+              int(top_paths), ids.data_ptr(), offs.data_ptr(), lens.data_ptr(), scores.data_ptr(),
+              ws.data_ptr(), ws.numel(), _stream())
+    return ids, offs, lens, scores
+
+
 def stft_logmag(pcm: torch.Tensor, n_samples: torch.Tensor, n_fft: int, hop: int,
                 window: torch.Tensor, normalize: int, gauss_taps: Optional[torch.Tensor],
                 max_frames: int) -> torch.Tensor:

@@ -242,6 +242,21 @@ ds2_status_t ds2_greedy_decode(const float* probs, int n, int t_max, int c, int6
                                int* out_offsets, int* out_counts, int* argmax_out,
                                ds2_stream_t stream);
 
+/* CTC prefix beam search without a language model: BeamCTCDecoder.decode
+ * (decoder.py:90-143, ctcdecode.CTCBeamDecoder with lm_path=None; opts.py beam
+ * defaults).  probs as for ds2_greedy_decode; per utterance the top_paths best
+ * prefixes (best first): out_ids / out_offsets [n][top_paths][t_max] (char ids and
+ * the frame of each char), out_lens [n][top_paths], out_scores [n][top_paths]
+ * (log prob).  cutoff_top_n / cutoff_prob prune the vocabulary per frame as
+ * ctcdecode does.  beam_width <= 32, c <= 64.                                  */
+size_t ds2_ctc_beam_workspace_size(int n, int t_max, int beam_width);
+ds2_status_t ds2_ctc_beam_decode(const float* probs, int n, int t_max, int c, int64_t stride_n,
+                                 int64_t stride_t, const int* sizes, int blank, int beam_width,
+                                 int cutoff_top_n, double cutoff_prob, int top_paths,
+                                 int* out_ids, int* out_offsets, int* out_lens,
+                                 float* out_scores, void* ws, size_t ws_bytes,
+                                 ds2_stream_t stream);
+
 /* ------------------------------------------------------------------------ */
 /* Training-step tail (ref train.py:595-632): clip_grad_norm_(max_norm) then
  * SGD(momentum, nesterov) on flat fp32 buffers.  The global L2 norm is reduced

@@ -470,3 +470,47 @@ def test_nan_guard_and_skip(dev):
     p.grad.fill_(1.0)
     opt.step(skip_flag=flag)
     assert torch.all(p == 1).item()
+
+
+# ---------------------------------------------------------------------------- beam search
+def _beam_check(dev, probs, sizes, beam, top_n=40, cutoff=1.0):
+    from oracle import ctc_beam
+    ids, offs, lens, scores = ops.ctc_beam_decode_raw(
+        torch.from_numpy(probs).to(dev), torch.tensor(sizes, dtype=torch.int32).to(dev), beam,
+        beam, cutoff_top_n=top_n, cutoff_prob=cutoff)
+    ids, offs, lens, scores = ids.cpu(), offs.cpu(), lens.cpu(), scores.cpu()
+    ref = ctc_beam.beam_decode(probs, sizes, beam, cutoff_top_n=top_n, cutoff_prob=cutoff)
+    for n, paths in enumerate(ref):
+        for p in range(beam):
+            if p >= len(paths):
+                assert int(lens[n, p]) == 0
+                continue
+            s, rid, rts = paths[p]
+            k = int(lens[n, p])
+            assert ids[n, p, :k].tolist() == rid, (n, p)
+            assert offs[n, p, :k].tolist() == rts, (n, p)
+            assert abs(float(scores[n, p]) - s) <= 1e-5 * max(1.0, abs(s)), (n, p)
+
+
+@pytest.mark.parametrize("beam,top_n,cutoff", [(8, 40, 1.0), (4, 5, 1.0), (6, 40, 0.95),
+                                               (1, 40, 1.0)])
+def test_ctc_beam_vs_oracle(dev, beam, top_n, cutoff):
+    """ds2_ctc_beam_decode == oracle/ctc_beam.py (prefix beam search, no LM): ids, char
+    frames and lengths bit-exact for every returned beam, scores to 1e-5 rel."""
+    g = np.random.default_rng(beam * 10 + top_n)
+    n, t, c = 5, 37, 30
+    logits = g.standard_normal((n, t, c)).astype(np.float32) * 3
+    logits[:, :, 0] += 1.5                                  # blank-heavy, like a trained model
+    probs = np.exp(logits - logits.max(-1, keepdims=True))
+    probs = (probs / probs.sum(-1, keepdims=True)).astype(np.float32)
+    _beam_check(dev, probs, [37, 30, 1, 0, 22], beam, top_n, cutoff)
+
+
+def test_ctc_beam_hand_case_and_decoder(dev):
+    from ds2amd.decoder import BeamCTCDecoder
+    probs = np.array([[[0.6, 0.4], [0.6, 0.4]]], np.float32)
+    _beam_check(dev, probs, [2], 4)
+    dec = BeamCTCDecoder("_a", beam_width=2)
+    strings, offsets = dec.decode(torch.from_numpy(probs).to(dev), torch.IntTensor([2]))
+    assert strings == [["a", ""]]
+    assert offsets[0][0].tolist() == [0]

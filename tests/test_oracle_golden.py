@@ -181,3 +181,29 @@ def test_stft_oracle_known_answers():
 def test_hamming_matches_scipy():
     from scipy.signal import windows
     np.testing.assert_allclose(orc.hamming(320), windows.hamming(320, sym=True), rtol=0, atol=1e-15)
+
+
+def test_beam_oracle_hand_case():
+    """Prefix beam search sums over alignments: T=2, probs (blank .6, 'a' .4) per frame.
+    'a' = aa + a_ + _a = .16 + .24 + .24 = .64 beats '' = .36 (greedy would say '')."""
+    from oracle import ctc_beam
+    probs = np.array([[0.6, 0.4], [0.6, 0.4]], np.float32)
+    res = ctc_beam.beam_decode_one(probs, 2, beam=4, blank=0)
+    assert res[0][1] == [1] and abs(res[0][0] - np.log(0.64)) < 1e-6
+    assert res[1][1] == [] and abs(res[1][0] - np.log(0.36)) < 1e-6
+    assert res[0][2] == [0]                       # best extension event of 'a' at frame 0 (tie -> first)
+    # vocabulary pruning: with cutoff_top_n = 1 only the blank survives each frame
+    res = ctc_beam.beam_decode_one(probs, 2, beam=4, blank=0, cutoff_top_n=1)
+    assert len(res) == 1 and res[0][1] == []
+
+
+def test_beam_oracle_beam1_peaked_equals_greedy():
+    from oracle import ctc_beam
+    g = np.random.default_rng(3)
+    t, c = 40, 30
+    ids = g.integers(0, c, t)
+    probs = np.full((t, c), 0.1 / (c - 1), np.float32)
+    probs[np.arange(t), ids] = 0.9
+    res = ctc_beam.beam_decode_one(probs, t, beam=1)
+    strings, _ = orc.greedy_decode(torch.from_numpy(probs[None]), [t])
+    assert ''.join(LABELS[k] for k in res[0][1]) == strings[0][0]
