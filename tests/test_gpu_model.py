@@ -178,3 +178,39 @@ def test_cfg2_shape_step_properties(dev):
     assert s_gpu == s_ref
     s = p1.sum(-1)
     assert torch.allclose(s, torch.ones_like(s), atol=1e-5)
+
+
+def test_batched_transcribe_beam_and_greedy(dev):
+    """cfg5-style batched inference (smaller model / 3 s clips): batched transcribe equals
+    per-utterance transcribe; the device beam search equals the oracle restatement on the
+    model's own probs; beam width 1 keeps the greedy string on these peaked outputs."""
+    from ds2amd.data_loader import SpectrogramParser
+    from ds2amd.decoder import BeamCTCDecoder
+    from ds2amd.transcribe import transcribe_batch, decode_results
+    from oracle import ctc_beam
+    m = build(4321, 256, 2).to(dev).eval()
+    parser = SpectrogramParser(CONF, normalize='max_frame', device=dev)
+    rng = np.random.default_rng(9)
+    clips = []
+    for k, secs in enumerate([3.0, 2.2, 1.3]):
+        n = int(16000 * secs)
+        t = np.arange(n) / 16000.0
+        y = 0.1 * rng.standard_normal(n) + np.sin(2 * np.pi * (300 + 200 * k) * t)
+        clips.append((y / np.abs(y).max()).astype(np.float32))
+    greedy = GreedyDecoder(LABELS)
+    out_b, _ = transcribe_batch(clips, parser, m, greedy)
+    for i, y in enumerate(clips):
+        out_1, _ = transcribe_batch([y], parser, m, greedy)
+        assert out_1[0] == out_b[i]
+    beam = BeamCTCDecoder(LABELS, beam_width=8, cutoff_top_n=40)
+    spect, frames = parser.parse_batch(clips)
+    with torch.no_grad():
+        _, probs, out_lens = m(spect, frames)
+    strings, offsets = beam.decode(probs, out_lens)
+    ref = ctc_beam.beam_decode(probs.cpu().numpy(), out_lens.cpu().tolist(), 8)
+    for i, paths in enumerate(ref):
+        for p, (s, ids, ts) in enumerate(paths):
+            assert strings[i][p] == ''.join(LABELS[k] for k in ids)
+            assert offsets[i][p].tolist() == ts
+    res = decode_results(strings, offsets, top_paths=2, offsets=True)
+    assert len(res['output']) == 6 and 'offsets' in res['output'][0]
