@@ -489,6 +489,147 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// Batched CER / WER edit distances (data/utils.py:47-57 get_cer_wer with
+// decoder.py Decoder.wer / .cer): for each utterance, a = decoded ids (row n of a
+// [N][a_stride] array, a_lens[n] valid), b = reference ids (flat, b_offsets/b_lens).
+//   cer = Levenshtein(a without spaces, b without spaces)
+//   wer = Levenshtein(words(a), words(b)), words = maximal runs of non-space ids
+// out[n] = {wer, cer, max(#words(b), 1), max(#non-space(b), 1)} (ints).  Words are
+// mapped to exact ids (equal length and equal ids) before the DP.  One 64-lane
+// workgroup per utterance; DP rows use D[i][j] = j + prefix-min_k<=j (E[k] - k) with
+// E[k] = min(D[i-1][k] + 1, D[i-1][k-1] + (x != y)), a wave scan per 64 columns.
+constexpr int ED_MAXC = 2048;   // ids per sequence
+constexpr int ED_MAXW = 1024;   // words per sequence
+
+__device__ __forceinline__ int wave_incl_min(int v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int o = __shfl_up(v, off, 64);
+    if (lane >= off) v = min(v, o);
+  }
+  return v;
+}
+
+__device__ __forceinline__ int wave_excl_count(bool p, int& total) {
+  const unsigned long long m = __ballot(p);
+  total = __popcll(m);
+  return __builtin_amdgcn_mbcnt_hi(static_cast<unsigned>(m >> 32),
+                                   __builtin_amdgcn_mbcnt_lo(static_cast<unsigned>(m), 0));
+}
+
+// Levenshtein distance of x[0..m) and y[0..n) (all lanes participate)
+__device__ int ed_levenshtein(const int* x, int m, const int* y, int n, int* r0, int* r1) {
+  const int lane = threadIdx.x;
+  for (int j = lane; j <= n; j += 64) r0[j] = j;
+  __syncthreads();
+  int* prev = r0;
+  int* cur = r1;
+  for (int i = 1; i <= m; ++i) {
+    const int xi = x[i - 1];
+    int carry = 0x3fffffff;
+    for (int j0 = 0; j0 <= n; j0 += 64) {
+      const int j = j0 + lane;
+      int e = 0x3fffffff;
+      if (j <= n) e = j == 0 ? i : min(prev[j] + 1, prev[j - 1] + (xi != y[j - 1] ? 1 : 0));
+      int v = wave_incl_min(j <= n ? e - j : 0x3fffffff);
+      v = min(v, carry);
+      if (j <= n) cur[j] = v + j;
+      carry = __shfl(v, 63, 64);
+    }
+    __syncthreads();
+    int* tmp = prev;
+    prev = cur;
+    cur = tmp;
+  }
+  return prev[n];
+}
+
+// compact non-space ids and word starts of one sequence into LDS
+__device__ void ed_tokens(const int* __restrict__ src, int len, int space, int* chars, int& nch,
+                          int* wstart, int* wlen, int& nw) {
+  const int lane = threadIdx.x;
+  int cbase = 0, wbase = 0;
+  for (int p0 = 0; p0 < len; p0 += 64) {
+    const int p = p0 + lane;
+    const int c = p < len ? src[p] : space;
+    const int prevc = (p > 0 && p - 1 < len) ? src[p - 1] : space;
+    const bool isc = p < len && c != space;
+    const bool isw = isc && prevc == space;
+    int tc, tw;
+    const int rc = wave_excl_count(isc, tc);
+    const int rw = wave_excl_count(isw, tw);
+    if (isc && cbase + rc < ED_MAXC) chars[cbase + rc] = c;
+    if (isw && wbase + rw < ED_MAXW) {
+      int l = 0;
+      while (p + l < len && src[p + l] != space) ++l;
+      wstart[wbase + rw] = p;
+      wlen[wbase + rw] = l;
+    }
+    cbase += tc;
+    wbase += tw;
+  }
+  nch = cbase;
+  nw = wbase;
+}
+
+__global__ __launch_bounds__(64) void edit_distance_kernel(
+    const int* __restrict__ a, int64_t a_stride, const int* __restrict__ a_lens,
+    const int* __restrict__ b, const int* __restrict__ b_offsets, const int* __restrict__ b_lens,
+    int space, int* __restrict__ out, int* __restrict__ err) {
+  __shared__ int ca[ED_MAXC], cb[ED_MAXC];
+  __shared__ int r0[ED_MAXC + 1], r1[ED_MAXC + 1];
+  __shared__ int wsa[ED_MAXW], wla[ED_MAXW], wsb[ED_MAXW], wlb[ED_MAXW];
+  __shared__ int wida[ED_MAXW], widb[ED_MAXW];
+  const int n = blockIdx.x;
+  const int lane = threadIdx.x;
+  const int* pa = a + (int64_t)n * a_stride;
+  const int* pb = b + b_offsets[n];
+  const int la = a_lens[n], lb = b_lens[n];
+  int nca, ncb, nwa, nwb;
+  ed_tokens(pa, la, space, ca, nca, wsa, wla, nwa);
+  ed_tokens(pb, lb, space, cb, ncb, wsb, wlb, nwb);
+  __syncthreads();
+  if (nca > ED_MAXC || ncb > ED_MAXC || nwa > ED_MAXW || nwb > ED_MAXW) {
+    if (lane == 0) {
+      atomicOr(err, 1);
+      out[4 * n + 0] = out[4 * n + 1] = -1;
+      out[4 * n + 2] = max(nwb, 1);
+      out[4 * n + 3] = max(ncb, 1);
+    }
+    return;
+  }
+  // exact word ids: the index (over a's words then b's) of the first equal word
+  for (int w = lane; w < nwa + nwb; w += 64) {
+    const bool in_a = w < nwa;
+    const int s0 = in_a ? wsa[w] : wsb[w - nwa];
+    const int l0 = in_a ? wla[w] : wlb[w - nwa];
+    const int* q0 = in_a ? pa + s0 : pb + s0;
+    int id = w;
+    for (int v = 0; v < w && id == w; ++v) {
+      const bool va = v < nwa;
+      const int l1 = va ? wla[v] : wlb[v - nwa];
+      if (l1 != l0) continue;
+      const int* q1 = va ? pa + wsa[v] : pb + wsb[v - nwa];
+      bool eq = true;
+      for (int k = 0; k < l0 && eq; ++k) eq = q0[k] == q1[k];
+      if (eq) id = v;
+    }
+    if (in_a) wida[w] = id; else widb[w - nwa] = id;
+  }
+  __syncthreads();
+  const int wer = ed_levenshtein(wida, nwa, widb, nwb, r0, r1);
+  __syncthreads();
+  const int cer = ed_levenshtein(ca, nca, cb, ncb, r0, r1);
+  if (lane == 0) {
+    out[4 * n + 0] = wer;
+    out[4 * n + 1] = cer;
+    out[4 * n + 2] = max(nwb, 1);
+    out[4 * n + 3] = max(ncb, 1);
+  }
+}
+
 }  // namespace ds2
 
 using namespace ds2;
@@ -583,6 +724,19 @@ ds2_status_t ds2_ctc_beam_decode(const float* probs, int n, int t_max, int c, in
                      top_paths, par, chr, tst, lpc, cap, out_ids, out_offsets, out_lens,
                      out_scores);
   return launch_status("ds2_ctc_beam_decode");
+}
+
+ds2_status_t ds2_edit_distance(const int* a_ids, int64_t a_stride, const int* a_lens,
+                               const int* b_ids, const int* b_offsets, const int* b_lens, int n,
+                               int space_id, int* out, int* err, ds2_stream_t stream) {
+  if (n < 0 || a_stride < 0) return DS2_INVALID_VALUE;
+  if (n == 0) return DS2_OK;
+  if (a_ids == nullptr || a_lens == nullptr || b_ids == nullptr || b_offsets == nullptr ||
+      b_lens == nullptr || out == nullptr || err == nullptr)
+    return DS2_INVALID_VALUE;
+  hipLaunchKernelGGL(edit_distance_kernel, dim3(n), dim3(64), 0, as_stream(stream), a_ids,
+                     a_stride, a_lens, b_ids, b_offsets, b_lens, space_id, out, err);
+  return launch_status("ds2_edit_distance");
 }
 
 }  // extern "C"

@@ -76,6 +76,8 @@ _PROTOS = {
                               _vp, _vp, _vp, _sz, _vp]),
     "ds2_greedy_decode": (_c_int, [_vp, _c_int, _c_int, _c_int, _c_i64, _c_i64, _vp, _c_int, _vp,
                                    _vp, _vp, _vp, _vp]),
+    "ds2_edit_distance": (_c_int, [_vp, _c_i64, _vp, _vp, _vp, _vp, _c_int, _c_int, _vp, _vp,
+                                   _vp]),
     "ds2_ctc_beam_workspace_size": (_sz, [_c_int, _c_int, _c_int]),
     "ds2_ctc_beam_decode": (_c_int, [_vp, _c_int, _c_int, _c_int, _c_i64, _c_i64, _vp, _c_int,
                                      _c_int, _c_int, ctypes.c_double, _c_int, _vp, _vp, _vp, _vp,

@@ -205,6 +205,28 @@ def greedy_decode_raw(probs: torch.Tensor, sizes: Optional[torch.Tensor], blank:
     return ids, offs, counts, am
 
 
+def edit_distance_raw(a_ids: torch.Tensor, a_lens: torch.Tensor, b_ids: torch.Tensor,
+                      b_lens: torch.Tensor, space_id: int):
+    """Device CER/WER distances.  a_ids [N, S] int32 rows with a_lens valid; b_ids flat int32
+    (concatenated references), b_lens [N].  Returns int32 [N, 4] = (word dist, char dist,
+    max(#ref words, 1), max(#ref chars, 1)); raises if a sequence exceeds the kernel limits."""
+    dev = a_ids.device
+    if not a_ids.is_cuda:
+        raise _lib.Ds2Error("edit_distance: expected device tensors")
+    a_ids = a_ids.to(_I32).contiguous()
+    a_lens = a_lens.to(device=dev, dtype=_I32).contiguous()
+    b_ids = b_ids.to(device=dev, dtype=_I32).contiguous()
+    b_lens = b_lens.to(device=dev, dtype=_I32).contiguous()
+    b_off = (torch.cumsum(b_lens, 0) - b_lens).to(_I32).contiguous()
+    n = a_ids.shape[0]
+    out = torch.empty(n, 4, device=dev, dtype=_I32)
+    err = torch.zeros(1, device=dev, dtype=_I32)
+    _lib.call("ds2_edit_distance", a_ids.data_ptr(), a_ids.stride(0), a_lens.data_ptr(),
+              b_ids.data_ptr(), b_off.data_ptr(), b_lens.data_ptr(), n, int(space_id),
+              out.data_ptr(), err.data_ptr(), _stream())
+    return out, err
+
+
 def ctc_beam_decode_raw(probs: torch.Tensor, sizes: Optional[torch.Tensor], beam_width: int,
                         top_paths: int, blank: int = 0, cutoff_top_n: int = 40,
                         cutoff_prob: float = 1.0):

@@ -14,7 +14,7 @@ from typing import Optional
 import torch
 import torch.distributed as dist
 
-from . import _lib
+from . import _lib, ops
 from .ctc import CTCLoss
 from .decoder import GreedyDecoder
 from .ops import _stream
@@ -59,10 +59,25 @@ class Trainer:
         self.decode = decode
         self.score = score
         self.nan_flag = torch.zeros(1, dtype=torch.int32, device=self.device)
-        self.train_wer = 0.0
-        self.train_cer = 0.0
-        self.num_words = 0.0
-        self.num_chars = 0.0
+        # device accumulators of (wer, cer, words, chars): no host sync per batch
+        self._score_acc = torch.zeros(4, dtype=torch.float64, device=self.device)
+
+    # train.py:584-587 running sums, read lazily (one device->host copy)
+    @property
+    def train_wer(self):
+        return float(self._score_acc[0])
+
+    @property
+    def train_cer(self):
+        return float(self._score_acc[1])
+
+    @property
+    def num_words(self):
+        return float(self._score_acc[2])
+
+    @property
+    def num_chars(self):
+        return float(self._score_acc[3])
 
     def train_batch(self, data, return_item: bool = False):
         inputs, targets, filenames, input_percentages, target_sizes = data
@@ -97,17 +112,7 @@ class Trainer:
         return loss.detach()
 
     def _score(self, ids, counts, targets, target_sizes):
-        ids, counts = ids.cpu(), counts.cpu()
-        off = 0
-        for b in range(ids.shape[0]):
-            k = int(counts[b])
-            transcript = ''.join(' ' if c == self.decoder.space_index else
-                                 self.decoder.int_to_char[c] for c in ids[b, :k].tolist())
-            size = int(target_sizes[b])
-            ref = self.decoder.convert_to_strings([targets[off:off + size]])[0][0]
-            off += size
-            wer, cer, wer_ref, cer_ref = get_cer_wer(self.decoder, transcript, ref)
-            self.train_wer += wer
-            self.train_cer += cer
-            self.num_words += wer_ref
-            self.num_chars += cer_ref
+        """get_cer_wer over the batch (train.py:575-587) on the device: ds2_edit_distance
+        on the compact greedy ids vs the flat targets."""
+        d, _ = ops.edit_distance_raw(ids, counts, targets, target_sizes, self.decoder.space_index)
+        self._score_acc += d.sum(0, dtype=torch.float64)

@@ -249,6 +249,16 @@ ds2_status_t ds2_greedy_decode(const float* probs, int n, int t_max, int c, int6
  * the frame of each char), out_lens [n][top_paths], out_scores [n][top_paths]
  * (log prob).  cutoff_top_n / cutoff_prob prune the vocabulary per frame as
  * ctcdecode does.  beam_width <= 32, c <= 64.                                  */
+/* Batched CER / WER edit distances (data/utils.py:47-57 get_cer_wer, decoder.py
+ * Decoder.cer / .wer) over id sequences: a = decoded ids [n][a_stride] with a_lens,
+ * b = reference ids flat with b_offsets / b_lens.  out[4*i .. 4*i+3] = {word
+ * distance, char distance (spaces removed), max(#reference words, 1),
+ * max(#reference non-space chars, 1)}.  Sequences longer than 2048 ids / 1024 words
+ * set *err != 0 and distance -1 (err must be zeroed by the caller).           */
+ds2_status_t ds2_edit_distance(const int* a_ids, int64_t a_stride, const int* a_lens,
+                               const int* b_ids, const int* b_offsets, const int* b_lens, int n,
+                               int space_id, int* out, int* err, ds2_stream_t stream);
+
 size_t ds2_ctc_beam_workspace_size(int n, int t_max, int beam_width);
 ds2_status_t ds2_ctc_beam_decode(const float* probs, int n, int t_max, int c, int64_t stride_n,
                                  int64_t stride_t, const int* sizes, int blank, int beam_width,

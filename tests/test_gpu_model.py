@@ -214,3 +214,29 @@ def test_batched_transcribe_beam_and_greedy(dev):
             assert offsets[i][p].tolist() == ts
     res = decode_results(strings, offsets, top_paths=2, offsets=True)
     assert len(res['output']) == 6 and 'offsets' in res['output'][0]
+
+
+def test_trainer_scores_cer_wer_on_device(dev, golden_dir):
+    """Trainer(score=True) accumulates get_cer_wer (train.py:575-587) through
+    ds2_edit_distance; equal to the host strings' Levenshtein on the same decode."""
+    from ds2amd.trainer import Trainer, get_cer_wer
+    g = np.load(os.path.join(golden_dir, 'tiny_ds2.npz'))
+    m = build_tiny(g)
+    tr = Trainer(m, LABELS, lr=3e-4, device=dev, score=True)
+    x = torch.from_numpy(g['x'])
+    data = (x, torch.from_numpy(g['targets']), None, torch.from_numpy(g['pct']).clone(),
+            torch.from_numpy(g['target_sizes']))
+    tr.train_batch(data)
+    # recompute on the host from the train-mode forward the trainer decoded
+    m2 = build_tiny(g).to(dev).train()
+    _, probs, out_lens = m2(x.to(dev), torch.from_numpy(g['input_sizes']))
+    strings, _ = GreedyDecoder(LABELS).decode(probs, out_lens)
+    tg, ts = g['targets'].tolist(), g['target_sizes'].tolist()
+    tot = [0.0, 0.0, 0.0, 0.0]
+    off = 0
+    for i, s in enumerate(ts):
+        ref = ''.join(LABELS[k] for k in tg[off:off + s])
+        off += s
+        for j, v in enumerate(get_cer_wer(GreedyDecoder(LABELS), strings[i][0], ref)):
+            tot[j] += v
+    assert [tr.train_wer, tr.train_cer, tr.num_words, tr.num_chars] == tot

@@ -514,3 +514,42 @@ def test_ctc_beam_hand_case_and_decoder(dev):
     strings, offsets = dec.decode(torch.from_numpy(probs).to(dev), torch.IntTensor([2]))
     assert strings == [["a", ""]]
     assert offsets[0][0].tolist() == [0]
+
+
+# ---------------------------------------------------------------------------- CER / WER
+def test_edit_distance_vs_reference_semantics(dev):
+    """ds2_edit_distance == get_cer_wer (data/utils.py:47-57) with Decoder.wer/.cer's
+    Levenshtein on the same strings: random id strings with runs of spaces, leading /
+    trailing spaces, empty sequences, identical pairs and long sequences."""
+    from ds2amd.decoder import Decoder
+    from ds2amd.trainer import get_cer_wer
+    labels = orc.LABELS
+    space = labels.index(' ')
+    dec = Decoder(labels)
+    g = np.random.default_rng(17)
+    a_rows, b_rows = [], []
+    for i in range(40):
+        la = int(g.integers(0, 120)) if i % 10 else 0
+        lb = int(g.integers(0, 90)) if i % 7 else 0
+        alphabet = [space, space, 1, 2, 3, 4, 5] if i % 3 == 0 else list(range(1, len(labels)))
+        a_rows.append([int(alphabet[k]) for k in g.integers(0, len(alphabet), la)])
+        b_rows.append([int(alphabet[k]) for k in g.integers(0, len(alphabet), lb)])
+    a_rows.append(list(range(1, 29)) * 40)          # 1120 ids
+    b_rows.append(list(range(1, 29)) * 35)
+    a_rows.append([5, space, 6, space, space, 5])   # identical after strip / split
+    b_rows.append([space, 5, space, 6, space, 5, space])
+    n = len(a_rows)
+    width = max(len(r) for r in a_rows)
+    a = torch.zeros(n, width, dtype=torch.int32)
+    for i, r in enumerate(a_rows):
+        a[i, :len(r)] = torch.tensor(r, dtype=torch.int32)
+    a_lens = torch.tensor([len(r) for r in a_rows], dtype=torch.int32)
+    b = torch.tensor([x for r in b_rows for x in r], dtype=torch.int32)
+    b_lens = torch.tensor([len(r) for r in b_rows], dtype=torch.int32)
+    out, err = ops.edit_distance_raw(a.to(dev), a_lens, b, b_lens, space)
+    out = out.cpu()
+    assert int(err.item()) == 0
+    to_s = lambda r: ''.join(labels[k] for k in r)
+    for i in range(n):
+        wer, cer, wref, cref = get_cer_wer(dec, to_s(a_rows[i]), to_s(b_rows[i]))
+        assert out[i].tolist() == [wer, cer, int(wref), int(cref)], i
