@@ -364,6 +364,20 @@ __global__ void bias_grad_kernel(const float* __restrict__ dy, int N, int C, int
   if (threadIdx.x == 0) db[c] = static_cast<float>(red[0] + red[1] + red[2] + red[3]);
 }
 
+// XCD-aware decode of a 3-D grid launched as gx*gy*gz 1-D blocks: the blocks one XCD
+// is dealt (ids congruent mod 8) get a contiguous run of (x fastest, y, z) tiles, so
+// tiles that share input rows / samples share that XCD's L2.  Speed only.
+__device__ __forceinline__ void xcd_tile(int gx, int gy, int& bx, int& by, int& bz) {
+  const int nwg = gridDim.x;
+  const int o = blockIdx.x;
+  const int q = nwg >> 3, r = nwg & 7;
+  const int xcd = o & 7;
+  const int id = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (o >> 3);
+  bx = id % gx;
+  by = (id / gx) % gy;
+  bz = id / (gx * gy);
+}
+
 // ---------------------------------------------------------------------------
 // Direct convolution from an LDS input patch (width stride 1): forward and dgrad.
 //
@@ -509,7 +523,7 @@ __global__ __launch_bounds__(256) void conv_patch_kernel(const float* __restrict
                                                          const float* __restrict__ bias,
                                                          float* __restrict__ out, ConvDims g,
                                                          const int* __restrict__ out_lens,
-                                                         int tstride) {
+                                                         int tstride, int gx, int gy) {
   __shared__ __attribute__((aligned(16))) float ps[PT_PROWS * PT_PITCH];
   __shared__ __attribute__((aligned(16))) float wl[PT_TMAX * PT_WP];
   const int M = DGRAD ? g.ci : g.co;            // output channels
@@ -519,11 +533,13 @@ __global__ __launch_bounds__(256) void conv_patch_kernel(const float* __restrict
   const int out_h = DGRAD ? g.hi : g.ho;
   const int out_w = DGRAD ? g.wi : g.wo;
   const int mbn = (M + 31) / 32;
-  const int n = blockIdx.z / mbn;
-  const int mb = blockIdx.z - n * mbn;
+  int bx, by, bz;
+  xcd_tile(gx, gy, bx, by, bz);
+  const int n = bz / mbn;
+  const int mb = bz - n * mbn;
   const int m0 = mb * 32;
-  const int c0 = blockIdx.x * PT_COLS;
-  const PatchGeom p = patch_geom<DGRAD>(g, blockIdx.y, c0);
+  const int c0 = bx * PT_COLS;
+  const PatchGeom p = patch_geom<DGRAD>(g, by, c0);
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
@@ -660,15 +676,17 @@ __global__ __launch_bounds__(256) void conv_wgrad_patch_kernel(const float* __re
                                                                const float* __restrict__ x,
                                                                float* __restrict__ partial,
                                                                ConvDims g, int bands, int xpitch) {
+  int bx, by, bz;
+  xcd_tile(bands, g.ci, bx, by, bz);
   __shared__ __attribute__((aligned(16))) float dys[WG_RW * WG_CW * WG_DYP];
   __shared__ __attribute__((aligned(16))) float xs[XS];
   constexpr int DYREG = WG_RW * WG_CW * 32 / 256;
   constexpr int XREG = (XS + 255) / 256;
-  const int band = blockIdx.x;
-  const int ci = blockIdx.y;
+  const int band = bx;
+  const int ci = by;
   const int mbn = (g.co + 31) / 32;
-  const int n = blockIdx.z / mbn;
-  const int m0 = (blockIdx.z - n * mbn) * 32;
+  const int n = bz / mbn;
+  const int m0 = (bz - n * mbn) * 32;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
@@ -842,9 +860,11 @@ static ds2_status_t launch_patch(const float* in, const float* w, const float* b
     }
   }
   const int M = DGRAD ? g.ci : g.co;
-  dim3 grid(cdiv(DGRAD ? g.wi : g.wo, PT_COLS), ty, g.n * cdiv(M, 32));
-  hipLaunchKernelGGL(conv_patch_kernel<DGRAD>, grid, dim3(256), 0, st, in, img, bias, out, g,
-                     out_lens, tstride);
+  const int gx = cdiv(DGRAD ? g.wi : g.wo, PT_COLS);
+  const int64_t nwg = (int64_t)gx * ty * g.n * cdiv(M, 32);
+  if (nwg > 0x7fffffff) return DS2_UNSUPPORTED_SHAPE;
+  hipLaunchKernelGGL(conv_patch_kernel<DGRAD>, dim3(static_cast<unsigned>(nwg)), dim3(256), 0, st,
+                     in, img, bias, out, g, out_lens, tstride, gx, ty);
   return launch_status(DGRAD ? "ds2_conv2d_dgrad" : "ds2_conv2d_fwd");
 }
 
@@ -953,7 +973,7 @@ ds2_status_t ds2_conv2d_wgrad(const float* dy, const float* x, float* dw, float*
   const WgradPlan pl = wgrad_plan(g);
   int slabs = n;
   if (pl.nt > 0) {
-    dim3 grid(pl.bands, c_in, n * cdiv(c_out, 32));
+    dim3 grid(static_cast<unsigned>((int64_t)pl.bands * c_in * n * cdiv(c_out, 32)));
     if (pl.nt == 2)
       hipLaunchKernelGGL((conv_wgrad_patch_kernel<2, WG_XS_SMALL>), grid, dim3(256), 0, st, dy, x,
                          partial, g, pl.bands, pl.xpitch);

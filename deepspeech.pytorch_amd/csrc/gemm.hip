@@ -120,7 +120,13 @@ __global__ __launch_bounds__(256) void sgemm_kernel(
     const int xcd = orig & 7;
     tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
   } else {
-    const int pidx = orig - main_wgs;
+    // same XCD-aware remap over the tail pieces: one XCD gets a contiguous run of
+    // (split, tile) pieces, so the pieces sharing an operand panel share its L2
+    const int np = gridDim.x - main_wgs;
+    const int o = orig - main_wgs;
+    const int q = np >> 3, r = np & 7;
+    const int xcd = o & 7;
+    const int pidx = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (o >> 3);
     z = pidx / tail_tiles;
     const int lt = pidx - z * tail_tiles;
     tile = tail_tile0 + lt;
