@@ -89,6 +89,29 @@ class KernelProbe:
         return sum(ms) / len(ms), sum(self.flops) / len(self.flops), len(ms)
 
 
+def pmc_traffic_per_launch(prefix="sgemm_kernel", extra=("splitk_reduce_kernel",)):
+    """HBM bytes per ds2_sgemm_ws launch from the newest committed PMC summary
+    (profiles/r*_pmc_traffic.csv, made by scripts/pmc_traffic.sh + pmc_summary.py:
+    FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE, one pass per counter)."""
+    import csv
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_traffic.csv")))
+    if not files:
+        return None, None
+    launches, total = 0, 0.0
+    for r in csv.DictReader(open(files[-1])):
+        name = r["kernel"]
+        calls = int(r["calls"])
+        if prefix in name:
+            launches += calls
+            total += calls * float(r["avg_total_MB"])
+        elif any(e in name for e in extra):
+            total += calls * float(r["avg_total_MB"])
+    if launches == 0:
+        return None, None
+    return total / launches * 1e6, os.path.relpath(files[-1], REPO)
+
+
 def sgemm_flops(args):
     m, n, k = args[2], args[3], args[4]
     return 2.0 * m * n * k
@@ -130,7 +153,9 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    # DS2_FORCE_DIST=1 under torchrun exercises the RCCL path even at world size 1
+    distributed = world > 1 or os.environ.get("DS2_FORCE_DIST") == "1"
+    if distributed:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -155,7 +180,7 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    if world > 1:
+    if distributed:
         dist.barrier()
     torch.cuda.synchronize()
     probe.active = True
@@ -163,12 +188,12 @@ def main():
     for _ in range(args.steps):
         loss = step()
     torch.cuda.synchronize()
-    if world > 1:
+    if distributed:
         dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     probe.active = False
-    if world > 1:
+    if distributed:
         tt = torch.tensor([dt], device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
@@ -180,13 +205,16 @@ def main():
         value = audio / dt
         ms_per_step = dt * 1000.0 / args.steps
         roof = None
+        traffic, traffic_src = pmc_traffic_per_launch()
         if pk is not None:
             avg_ms, flop, count = pk
             achieved = flop / (avg_ms * 1e-3) / 1e12
             roof = {"bound": "mfma", "kernel": args.probe, "launches": count,
                     "avg_launch_ms": round(avg_ms, 5), "achieved": round(achieved, 3),
                     "peak": PEAK_F32_MFMA_TFLOPS, "unit": "TFLOP/s",
-                    "frac": round(achieved / PEAK_F32_MFMA_TFLOPS, 4), "traffic": None,
+                    "frac": round(achieved / PEAK_F32_MFMA_TFLOPS, 4),
+                    "traffic": None if traffic is None else round(traffic),
+                    "traffic_unit": "bytes/launch (HBM, PMC)", "traffic_source": traffic_src,
                     "step_achieved_tflops": round(TRAIN_FLOP_PER_STEP / (ms_per_step * 1e-3) / 1e12, 3)}
         cpu = None
         if not args.no_cpu_baseline and world == 1:
@@ -206,7 +234,7 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if distributed:
         dist.barrier()
         dist.destroy_process_group()
 

@@ -26,6 +26,7 @@ namespace ds2 {
 
 constexpr int KC_FWD = 1024;   // max H staged in LDS (forward)
 constexpr int KC_BWD = 2400;   // max 3H chunk staged in LDS (backward)
+constexpr int kTraceS0 = 100, kTraceSteps = 16;   // DS2_GRU_STAMPS=2 trace window
 
 // ---------------------------------------------------------------------------
 // forward step.  KSW = k-steps of W prefetched into registers per wave.
@@ -247,7 +248,7 @@ __global__ __launch_bounds__(GT) void gru_fwd_persist_kernel(
     const float* __restrict__ wp, const float* __restrict__ b_f, const float* __restrict__ b_r,
     const int* __restrict__ lens, float* __restrict__ h_all, float* __restrict__ gates,
     unsigned* __restrict__ counters, unsigned* __restrict__ err,
-    unsigned long long* __restrict__ stamps) {
+    unsigned long long* __restrict__ stamps, int trace) {
   constexpr int PITCH = KC_FWD + 4;
   __shared__ __attribute__((aligned(16))) float hs[GB * PITCH];
   __shared__ int flag;
@@ -262,7 +263,16 @@ __global__ __launch_bounds__(GT) void gru_fwd_persist_kernel(
   unsigned* ctr = counters + d * BT + bt;
   const __amdgpu_buffer_rsrc_t h_rs = __builtin_amdgcn_make_buffer_rsrc(
       h_all, (short)0, T * N * D * H * 4, 0x00020000);
-  const bool stamping = stamps != nullptr && blockIdx.x == 0 && threadIdx.x == 0;
+  const bool stamping = stamps != nullptr && !trace && blockIdx.x == 0 && threadIdx.x == 0;
+  // trace mode (DS2_GRU_STAMPS=2): every workgroup's thread 0 records s_memrealtime
+  // (100 MHz) at {step start, wait done, staged, mfma+red done, arrived} for steps
+  // [kTraceS0, kTraceS0 + kTraceSteps)
+  const bool tracing = stamps != nullptr && trace && threadIdx.x == 0;
+  auto trace_at = [&](int s, int p) {
+    if (tracing && s >= kTraceS0 && s < kTraceS0 + kTraceSteps)
+      stamps[((int64_t)(s - kTraceS0) * gridDim.x + blockIdx.x) * 5 + p] =
+          __builtin_amdgcn_s_memrealtime();
+  };
   unsigned long long acc_t[6] = {0, 0, 0, 0, 0, 0};
   unsigned long long t0 = 0, t1 = 0;
 
@@ -312,13 +322,16 @@ __global__ __launch_bounds__(GT) void gru_fwd_persist_kernel(
     for (int g = 0; g < 3; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
     float hp = 0.f;
     if (stamping) t0 = stamp_now();
+    trace_at(s, 0);
     if (s > 0) {
       if (!group_wait(ctr, (unsigned)s * UB, err, &flag)) return;
+      trace_at(s, 1);
       if (stamping) { t1 = stamp_now(); acc_t[0] += t1 - t0; t0 = t1; }
       const float* hprev = h_all + ((int64_t)tp * N * D + d) * H;
       stage_rows_sc1<(GB * KC_FWD / 4 + GT - 1) / GT>(hprev, D * H, N, n0, H, 4 * GW * KSW, hs,
                                                        PITCH);
       __syncthreads();
+      trace_at(s, 2);
       if (stamping) { t1 = stamp_now(); acc_t[1] += t1 - t0; t0 = t1; }
       // every wave runs exactly KSW k-steps; steps past H read zero-staged columns and
       // zero W registers, so there is no branch between the LDS reads and the MFMAs
@@ -338,6 +351,7 @@ __global__ __launch_bounds__(GT) void gru_fwd_persist_kernel(
       for (int r = 0; r < 4; ++r)
         red[(wave * GB + (lane >> 4) * 4 + r) * RP + g * GU + (lane & 15)] = acc[g][r];
     __syncthreads();
+    trace_at(s, 3);
     if (stamping) { t1 = stamp_now(); acc_t[2] += t1 - t0; t0 = t1; }
     if (owner) {
       float gh[3];
@@ -366,6 +380,7 @@ __global__ __launch_bounds__(GT) void gru_fwd_persist_kernel(
     }
     if (stamping) { t1 = stamp_now(); acc_t[3] += t1 - t0; t0 = t1; }
     group_arrive(ctr);
+    trace_at(s, 4);
     if (stamping) { t1 = stamp_now(); acc_t[4] += t1 - t0; t0 = t1; }
     // the gate cache is consumed only by the backward kernel: store it off the
     // critical path, after this step's hand-off has been signalled
@@ -493,13 +508,17 @@ using namespace ds2;
 
 extern "C" {
 
+static inline int stamp_mode() {
+  const char* e = getenv("DS2_GRU_STAMPS");
+  return e == nullptr ? 0 : (e[0] == '1' ? 1 : (e[0] == '2' ? 2 : 0));
+}
 static inline size_t counter_bytes(int n, int num_dirs) {
+  const size_t trace = stamp_mode() == 2 ? (size_t)kTraceSteps * 1024 * 5 : 16;
   return align256((size_t)(num_dirs * ((n + GB - 1) / GB) + 1) * sizeof(unsigned)) +
-         16 * sizeof(unsigned long long);
+         trace * sizeof(unsigned long long);
 }
 static inline unsigned long long* stamp_slots(unsigned* ctrs, int n, int num_dirs) {
-  const char* e = getenv("DS2_GRU_STAMPS");
-  if (e == nullptr || e[0] != '1') return nullptr;
+  if (stamp_mode() == 0) return nullptr;
   return reinterpret_cast<unsigned long long*>(
       reinterpret_cast<char*>(ctrs) +
       align256((size_t)(num_dirs * ((n + GB - 1) / GB) + 1) * sizeof(unsigned)));
@@ -557,8 +576,9 @@ ds2_status_t ds2_gru_fwd(int t_max, int n, int h, int num_dirs, const float* xpr
       return launch_status("ds2_gru counters");
     int T_ = t_max, N_ = n, H_ = h, D_ = num_dirs, UB_ = UB, BT_ = BT;
     unsigned long long* stamps = stamp_slots(ctrs, n, num_dirs);
+    int trace_ = stamp_mode() == 2 ? 1 : 0;
     void* args[] = {&T_, &N_, &H_, &D_, &UB_, &BT_, &xproj, &wp, &b_hh_f, &b_hh_r, &lens,
-                    &h_all, &gates, &ctrs, &err, &stamps};
+                    &h_all, &gates, &ctrs, &err, &stamps, &trace_};
     const void* fn = nullptr;
     const int kp = persist_ksw((KS + GW - 1) / GW, KC_FWD);
     switch (kp) {

@@ -130,7 +130,9 @@ class GradAllReducer:
         self.pending = [0] * len(self.buckets)
         self.handles = [None] * len(self.buckets)
         self._hooks = []
-        if self.world > 1:
+        # hooks whenever a process group exists (world 1 included: that exercises the
+        # RCCL path on a single-GPU box; the all-reduce is then a no-op copy)
+        if dist.is_initialized():
             for p in flat.params:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._on_ready))
 
@@ -153,11 +155,12 @@ class GradAllReducer:
                                               async_op=True)
 
     def finish(self):
-        if self.world <= 1:
+        if not self._hooks:
             return
         for b, h in enumerate(self.handles):
             if h is None:     # a bucket whose params received no gradient this step
                 s, e, _ = self.buckets[b]
                 h = dist.all_reduce(self.flat.grad[s:e], group=self.group, async_op=True)
             h.wait()
-        self.flat.grad.mul_(1.0 / self.world)
+        if self.world > 1:
+            self.flat.grad.mul_(1.0 / self.world)

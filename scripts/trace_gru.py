@@ -1,0 +1,82 @@
+"""Diagnostic: per-workgroup timeline of the persistent GRU forward (DS2_GRU_STAMPS=2).
+
+Every workgroup stamps s_memrealtime (10 ns ticks) at {step start, wait done, staged,
+mfma+red done, arrived} for 16 steps; this prints the arrival skew inside each
+(direction, batch tile) group, the latency from the group's last arrival to the
+first / median / last consumer leaving its wait, and the phase lengths."""
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "deepspeech.pytorch_amd"))
+os.environ["DS2_GRU_STAMPS"] = "2"
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+from ds2amd import _lib, ops  # noqa: E402
+
+T, N, H, D = 501, 32, 800, 2
+S0, NS = 100, 16
+dev = torch.device("cuda")
+g = torch.Generator(device="cpu").manual_seed(0)
+xproj = (torch.randn(T, N, D, 3 * H, generator=g) * 0.5).to(dev)
+w = [(torch.rand(3 * H, H, generator=g) * 0.06 - 0.03).to(dev) for _ in range(2)]
+b = [(torch.rand(3 * H, generator=g) * 0.06 - 0.03).to(dev) for _ in range(2)]
+lens = torch.full((N,), T, dtype=torch.int32, device=dev)
+h_all = torch.empty(T, N, D, H, device=dev)
+gates = torch.empty(T, N, D, 4 * H, device=dev)
+ws = torch.zeros(_lib.size("ds2_gru_fwd_workspace_size", N, H, D), dtype=torch.uint8, device=dev)
+UB, KS, BT = (H + 15) // 16, (H + 3) // 4, (N + 15) // 16
+al = lambda x: (x + 255) & ~255
+off = al(D * UB * KS * 3 * 64 * 4) + al((D * BT + 1) * 4)
+P = UB * D
+grid = 8 * ((P + 7) // 8) * BT
+for it in range(3):
+    _lib.call("ds2_gru_fwd", T, N, H, D, xproj.data_ptr(), w[0].data_ptr(), w[1].data_ptr(),
+              b[0].data_ptr(), b[1].data_ptr(), lens.data_ptr(), h_all.data_ptr(),
+              gates.data_ptr(), ws.data_ptr(), ws.numel(), ops._stream())
+    torch.cuda.synchronize()
+tr = ws[off:off + NS * grid * 5 * 8].view(torch.int64).cpu().numpy().reshape(NS, grid, 5)
+groups = {}
+for wg in range(grid):
+    xcd, slot = wg & 7, wg >> 3
+    pair = xcd + 8 * (slot // BT)
+    bt = slot % BT
+    if pair >= P:
+        continue
+    d = pair // UB
+    groups.setdefault((d, bt), []).append(wg)
+ticks_us = 0.01
+rows = []
+for s in range(NS - 1):
+    for key, wgs in groups.items():
+        arr = tr[s, wgs, 4].astype(np.float64)
+        nxt_wait = tr[s + 1, wgs, 1].astype(np.float64)
+        last = arr.max()
+        rows.append(((arr.max() - arr.min()) * ticks_us, (np.sort(arr)[-2] - np.median(arr)) * ticks_us,
+                     (nxt_wait.min() - last) * ticks_us, (np.median(nxt_wait) - last) * ticks_us,
+                     (nxt_wait.max() - last) * ticks_us))
+r = np.array(rows)
+print("per group-step (us): arrival skew max-min %.2f | 2nd-last minus median arrival %.2f | "
+      "last arrival -> first consumer %.2f, median %.2f, last %.2f" % tuple(r.mean(0)))
+ph = tr[1:NS - 1]
+valid = ph[..., 0] > 0
+def mean_phase(a, b_):
+    return float(((ph[..., b_] - ph[..., a]) * ticks_us)[valid].mean())
+print("phases (us, mean over WGs/steps): wait %.2f, stage %.2f, mfma+red %.2f, pointwise+arrive %.2f"
+      % (mean_phase(0, 1), mean_phase(1, 2), mean_phase(2, 3), mean_phase(3, 4)))
+v2 = tr[1:NS - 1, :, 0] > 0
+step_len = (tr[2:NS, :, 0] - tr[1:NS - 1, :, 0])[v2] * ticks_us
+print("step length (us): mean %.2f" % step_len.mean())
+# which WGs arrive last most often (systematic skew?)
+last_counts = {}
+for s in range(NS):
+    for key, wgs in groups.items():
+        wl = wgs[int(np.argmax(tr[s, wgs, 4]))]
+        last_counts[wl] = last_counts.get(wl, 0) + 1
+top = sorted(last_counts.items(), key=lambda kv: -kv[1])[:8]
+print("most frequent last arrivers (wg: count, xcd):", [(k, v, k & 7) for k, v in top])
+# per-WG mean stage time by XCD
+st = ((ph[..., 2] - ph[..., 1]) * ticks_us)
+for x in range(8):
+    cols = [wg for wg in range(grid) if (wg & 7) == x and any(wg in v for v in groups.values())]
+    print(f"xcd {x}: stage {st[:, cols].mean():.2f} us, mfma {((ph[..., 3] - ph[..., 2]) * ticks_us)[:, cols].mean():.2f} us, wait {((ph[..., 1] - ph[..., 0]) * ticks_us)[:, cols].mean():.2f}")
