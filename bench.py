@@ -99,9 +99,16 @@ def pmc_traffic_per_launch(prefix="sgemm_kernel", extra=("splitk_reduce_kernel",
     if not files:
         return None, None
     launches, total = 0, 0.0
-    for r in csv.DictReader(open(files[-1])):
-        name = r["kernel"]
-        calls = int(r["calls"])
+    try:
+        rows = list(csv.DictReader(open(files[-1])))
+    except (OSError, csv.Error):
+        return None, None
+    for r in rows:
+        name = r.get("kernel", "")
+        try:
+            calls = int(r["calls"])
+        except (KeyError, TypeError, ValueError):
+            continue
         if prefix in name:
             launches += calls
             total += calls * float(r["avg_total_MB"])

@@ -248,7 +248,7 @@ __global__ __launch_bounds__(GT) void gru_fwd_persist_kernel(
     const float* __restrict__ wp, const float* __restrict__ b_f, const float* __restrict__ b_r,
     const int* __restrict__ lens, float* __restrict__ h_all, float* __restrict__ gates,
     unsigned* __restrict__ counters, unsigned* __restrict__ err,
-    unsigned long long* __restrict__ stamps, int trace) {
+    unsigned long long* __restrict__ stamps, int trace, int use_flags) {
   constexpr int PITCH = KC_FWD + 4;
   __shared__ __attribute__((aligned(16))) float hs[GB * PITCH];
   __shared__ int flag;
@@ -261,6 +261,7 @@ __global__ __launch_bounds__(GT) void gru_fwd_persist_kernel(
   const int a_ks = wave * KSW;           // host guarantees GW * KSW >= KS
   const int b_ks = min(KS, a_ks + KSW);
   unsigned* ctr = counters + d * BT + bt;
+  unsigned* gflags = counters + (D * BT + 1) + (d * BT + bt) * UB;   // flag variant
   const __amdgpu_buffer_rsrc_t h_rs = __builtin_amdgcn_make_buffer_rsrc(
       h_all, (short)0, T * N * D * H * 4, 0x00020000);
   const bool stamping = stamps != nullptr && !trace && blockIdx.x == 0 && threadIdx.x == 0;
@@ -324,7 +325,9 @@ __global__ __launch_bounds__(GT) void gru_fwd_persist_kernel(
     if (stamping) t0 = stamp_now();
     trace_at(s, 0);
     if (s > 0) {
-      if (!group_wait(ctr, (unsigned)s * UB, err, &flag)) return;
+      if (!(use_flags ? flags_wait(gflags, UB, (unsigned)s, err, &flag)
+                      : group_wait(ctr, (unsigned)s * UB, err, &flag)))
+        return;
       trace_at(s, 1);
       if (stamping) { t1 = stamp_now(); acc_t[0] += t1 - t0; t0 = t1; }
       const float* hprev = h_all + ((int64_t)tp * N * D + d) * H;
@@ -379,7 +382,8 @@ __global__ __launch_bounds__(GT) void gru_fwd_persist_kernel(
       g_r = r; g_z = z; g_n = nn; g_hn = ghn; g_row = row;
     }
     if (stamping) { t1 = stamp_now(); acc_t[3] += t1 - t0; t0 = t1; }
-    group_arrive(ctr);
+    if (use_flags) flags_arrive(gflags + ub, (unsigned)s + 1);
+    else group_arrive(ctr);
     trace_at(s, 4);
     if (stamping) { t1 = stamp_now(); acc_t[4] += t1 - t0; t0 = t1; }
     // the gate cache is consumed only by the backward kernel: store it off the
@@ -401,7 +405,8 @@ __global__ __launch_bounds__(GT) void gru_bwd_persist_kernel(
     int T, int N, int H, int D, int UB, int BT, const float* __restrict__ dy, int dyd,
     const float* __restrict__ wpt, const float* __restrict__ h_all,
     const float* __restrict__ gates, const int* __restrict__ lens, float* __restrict__ dgx,
-    float* __restrict__ dgh, unsigned* __restrict__ counters, unsigned* __restrict__ err) {
+    float* __restrict__ dgh, unsigned* __restrict__ counters, unsigned* __restrict__ err,
+    int use_flags) {
   constexpr int PITCH = KC_BWD + 4;
   __shared__ __attribute__((aligned(16))) float hs[GB * PITCH];
   float* red = hs;                          // reduction buffer aliases the staged rows
@@ -416,6 +421,7 @@ __global__ __launch_bounds__(GT) void gru_bwd_persist_kernel(
   const int a_ks = wave * KSW;
   const int b_ks = min(KS, a_ks + KSW);
   unsigned* ctr = counters + d * BT + bt;
+  unsigned* gflags = counters + (D * BT + 1) + (d * BT + bt) * UB;   // flag variant
   const __amdgpu_buffer_rsrc_t g_rs = __builtin_amdgcn_make_buffer_rsrc(
       dgh, (short)0, T * N * D * H3 * 4, 0x00020000);
 
@@ -443,7 +449,9 @@ __global__ __launch_bounds__(GT) void gru_bwd_persist_kernel(
     f32x4 acc1 = f32x4{0.f, 0.f, 0.f, 0.f};
     if (s > 0) {
       const int tq = d == 0 ? t + 1 : t - 1;
-      if (!group_wait(ctr, (unsigned)s * UB, err, &flag)) return;
+      if (!(use_flags ? flags_wait(gflags, UB, (unsigned)s, err, &flag)
+                      : group_wait(ctr, (unsigned)s * UB, err, &flag)))
+        return;
       const float* dghq = dgh + ((int64_t)tq * N * D + d) * H3;
       stage_rows_sc1<(GB * KC_BWD / 4 + GT - 1) / GT>(dghq, D * H3, N, n0, H3, 4 * GW * KSW, hs,
                                                        PITCH);
@@ -498,7 +506,8 @@ __global__ __launch_bounds__(GT) void gru_bwd_persist_kernel(
       dh_prev = dh;
       z_prev = zc;
     }
-    group_arrive(ctr);
+    if (use_flags) flags_arrive(gflags + ub, (unsigned)s + 1);
+    else group_arrive(ctr);
   }
 }
 
@@ -512,16 +521,24 @@ static inline int stamp_mode() {
   const char* e = getenv("DS2_GRU_STAMPS");
   return e == nullptr ? 0 : (e[0] == '1' ? 1 : (e[0] == '2' ? 2 : 0));
 }
+// per-producer flags (default) or one arrival counter per group (DS2_RNN_FLAGS=0)
+static inline int flags_mode() {
+  const char* e = getenv("DS2_RNN_FLAGS");
+  return !(e != nullptr && e[0] == '0');
+}
+// counters (one per group) + error word + per-producer flags (64 per group), then stamps
+static inline size_t ctr_words(int n, int num_dirs) {
+  const int groups = num_dirs * ((n + GB - 1) / GB);
+  return (size_t)groups + 1 + (size_t)groups * 64;
+}
 static inline size_t counter_bytes(int n, int num_dirs) {
   const size_t trace = stamp_mode() == 2 ? (size_t)kTraceSteps * 1024 * 5 : 16;
-  return align256((size_t)(num_dirs * ((n + GB - 1) / GB) + 1) * sizeof(unsigned)) +
-         trace * sizeof(unsigned long long);
+  return align256(ctr_words(n, num_dirs) * sizeof(unsigned)) + trace * sizeof(unsigned long long);
 }
 static inline unsigned long long* stamp_slots(unsigned* ctrs, int n, int num_dirs) {
   if (stamp_mode() == 0) return nullptr;
-  return reinterpret_cast<unsigned long long*>(
-      reinterpret_cast<char*>(ctrs) +
-      align256((size_t)(num_dirs * ((n + GB - 1) / GB) + 1) * sizeof(unsigned)));
+  return reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(ctrs) +
+                                               align256(ctr_words(n, num_dirs) * sizeof(unsigned)));
 }
 
 size_t ds2_gru_fwd_workspace_size(int n, int h, int num_dirs) {
@@ -577,8 +594,9 @@ ds2_status_t ds2_gru_fwd(int t_max, int n, int h, int num_dirs, const float* xpr
     int T_ = t_max, N_ = n, H_ = h, D_ = num_dirs, UB_ = UB, BT_ = BT;
     unsigned long long* stamps = stamp_slots(ctrs, n, num_dirs);
     int trace_ = stamp_mode() == 2 ? 1 : 0;
+    int flags_ = flags_mode();
     void* args[] = {&T_, &N_, &H_, &D_, &UB_, &BT_, &xproj, &wp, &b_hh_f, &b_hh_r, &lens,
-                    &h_all, &gates, &ctrs, &err, &stamps, &trace_};
+                    &h_all, &gates, &ctrs, &err, &stamps, &trace_, &flags_};
     const void* fn = nullptr;
     const int kp = persist_ksw((KS + GW - 1) / GW, KC_FWD);
     switch (kp) {
@@ -649,8 +667,9 @@ ds2_status_t ds2_gru_bwd(int t_max, int n, int h, int num_dirs, const float* dy,
     if (hipMemsetAsync(ctrs, 0, counter_bytes(n, num_dirs), st) != hipSuccess)
       return launch_status("ds2_gru counters");
     int T_ = t_max, N_ = n, H_ = h, D_ = num_dirs, UB_ = UB, BT_ = BT, DYD_ = dy_dirs;
+    int flags_ = flags_mode();
     void* args[] = {&T_, &N_, &H_, &D_, &UB_, &BT_, &dy, &DYD_, &wpt, &h_all, &gates, &lens,
-                    &dgates_x, &dgates_h, &ctrs, &err};
+                    &dgates_x, &dgates_h, &ctrs, &err, &flags_};
     const void* fn = nullptr;
     const int kp = persist_ksw((KS + GW - 1) / GW, KC_BWD);
     switch (kp) {

@@ -252,7 +252,8 @@ __global__ __launch_bounds__(GT) void lstm_fwd_persist_kernel(
     int T, int N, int H, int D, int UB, int BT, const float* __restrict__ xproj,
     const float* __restrict__ wp, const float* __restrict__ b_f, const float* __restrict__ b_r,
     const int* __restrict__ lens, float* __restrict__ h_all, float* __restrict__ c_all,
-    float* __restrict__ gates, unsigned* __restrict__ counters, unsigned* __restrict__ err) {
+    float* __restrict__ gates, unsigned* __restrict__ counters, unsigned* __restrict__ err,
+    int use_flags) {
   constexpr int PITCH = LKC_FWD + 4;
   __shared__ __attribute__((aligned(16))) float hs[GB * PITCH];
   __shared__ float red[GW * GB * LRP];
@@ -266,6 +267,7 @@ __global__ __launch_bounds__(GT) void lstm_fwd_persist_kernel(
   const int a_ks = wave * KSW;
   const int b_ks = min(KS, a_ks + KSW);
   unsigned* ctr = counters + d * BT + bt;
+  unsigned* gflags = counters + (D * BT + 1) + (d * BT + bt) * UB;   // flag variant
   const __amdgpu_buffer_rsrc_t h_rs = __builtin_amdgcn_make_buffer_rsrc(
       h_all, (short)0, T * N * D * H * 4, 0x00020000);
 
@@ -309,7 +311,9 @@ __global__ __launch_bounds__(GT) void lstm_fwd_persist_kernel(
 #pragma unroll
     for (int g = 0; g < 4; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
     if (s > 0) {
-      if (!group_wait(ctr, (unsigned)s * UB, err, &flag)) return;
+      if (!(use_flags ? flags_wait(gflags, UB, (unsigned)s, err, &flag)
+                      : group_wait(ctr, (unsigned)s * UB, err, &flag)))
+        return;
       stage_rows_sc1<(GB * LKC_FWD / 4 + GT - 1) / GT>(h_all + ((int64_t)tp * N * D + d) * H,
                                                         D * H, N, n0, H, 4 * GW * KSW, hs, PITCH);
       __syncthreads();
@@ -347,7 +351,8 @@ __global__ __launch_bounds__(GT) void lstm_fwd_persist_kernel(
       prev = o;
       prev_row = row;
     }
-    group_arrive(ctr);
+    if (use_flags) flags_arrive(gflags + ub, (unsigned)s + 1);
+    else group_arrive(ctr);
     // backward-only caches, off the critical path
     if (owner) {
       if (c_all != nullptr) c_all[prev_row * H + j] = prev.c;
@@ -369,7 +374,7 @@ __global__ __launch_bounds__(GT) void lstm_bwd_persist_kernel(
     int T, int N, int H, int D, int UB, int BT, const float* __restrict__ dy, int dyd,
     const float* __restrict__ wpt, const float* __restrict__ c_all,
     const float* __restrict__ gates, const int* __restrict__ lens, float* __restrict__ dg,
-    unsigned* __restrict__ counters, unsigned* __restrict__ err) {
+    unsigned* __restrict__ counters, unsigned* __restrict__ err, int use_flags) {
   constexpr int CW = 4 * GW * KSWC;         // gate columns per chunk (<= LKC_BWD)
   constexpr int PITCH = CW + 4;
   __shared__ __attribute__((aligned(16))) float hs[GB * PITCH];
@@ -383,6 +388,7 @@ __global__ __launch_bounds__(GT) void lstm_bwd_persist_kernel(
   const int H4 = 4 * H;
   const int KS = H;
   unsigned* ctr = counters + d * BT + bt;
+  unsigned* gflags = counters + (D * BT + 1) + (d * BT + bt) * UB;   // flag variant
   const __amdgpu_buffer_rsrc_t g_rs = __builtin_amdgcn_make_buffer_rsrc(
       dg, (short)0, T * N * D * H4 * 4, 0x00020000);
 
@@ -426,7 +432,9 @@ __global__ __launch_bounds__(GT) void lstm_bwd_persist_kernel(
     f32x4 acc1 = f32x4{0.f, 0.f, 0.f, 0.f};
     if (s > 0) {
       const int tq = d == 0 ? t + 1 : t - 1;
-      if (!group_wait(ctr, (unsigned)s * UB, err, &flag)) return;
+      if (!(use_flags ? flags_wait(gflags, UB, (unsigned)s, err, &flag)
+                      : group_wait(ctr, (unsigned)s * UB, err, &flag)))
+        return;
       const float* dgq = dg + ((int64_t)tq * N * D + d) * H4;
 #pragma unroll
       for (int c = 0; c < NCH; ++c) {
@@ -475,7 +483,8 @@ __global__ __launch_bounds__(GT) void lstm_bwd_persist_kernel(
       __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, dao), g_rs, o + 12 * H, 0,
                                             kSc1);
     }
-    group_arrive(ctr);
+    if (use_flags) flags_arrive(gflags + ub, (unsigned)s + 1);
+    else group_arrive(ctr);
   }
 }
 
@@ -493,8 +502,14 @@ using namespace ds2;
 
 extern "C" {
 
+// counters (one per group) + error word + per-producer flags (64 per group)
 static inline size_t lstm_counter_bytes(int n, int num_dirs) {
-  return align256((size_t)(num_dirs * ((n + GB - 1) / GB) + 1) * sizeof(unsigned));
+  const size_t groups = (size_t)num_dirs * ((n + GB - 1) / GB);
+  return align256((groups + 1 + groups * 64) * sizeof(unsigned));
+}
+static inline int lstm_flags_mode() {
+  const char* e = getenv("DS2_RNN_FLAGS");
+  return !(e != nullptr && e[0] == '0');
 }
 
 size_t ds2_lstm_fwd_workspace_size(int n, int h, int num_dirs) {
@@ -546,8 +561,9 @@ ds2_status_t ds2_lstm_fwd(int t_max, int n, int h, int num_dirs, const float* xp
     if (hipMemsetAsync(ctrs, 0, lstm_counter_bytes(n, num_dirs), st) != hipSuccess)
       return launch_status("ds2_lstm counters");
     int T_ = t_max, N_ = n, H_ = h, D_ = num_dirs, UB_ = UB, BT_ = BT;
+    int flags_ = lstm_flags_mode();
     void* args[] = {&T_, &N_, &H_, &D_, &UB_, &BT_, &xproj, &wp, &b_hh_f, &b_hh_r, &lens,
-                    &h_all, &c_all, &gates, &ctrs, &err};
+                    &h_all, &c_all, &gates, &ctrs, &err, &flags_};
     const void* fn = nullptr;
     switch (kp) {
       case 8: fn = reinterpret_cast<const void*>(lstm_fwd_persist_kernel<8>); break;
@@ -633,8 +649,9 @@ ds2_status_t ds2_lstm_bwd(int t_max, int n, int h, int num_dirs, const float* dy
       if (hipMemsetAsync(ctrs, 0, lstm_counter_bytes(n, num_dirs), st) != hipSuccess)
         return launch_status("ds2_lstm counters");
       int T_ = t_max, N_ = n, H_ = h, D_ = num_dirs, UB_ = UB, BT_ = BT, DYD_ = dy_dirs;
+      int flags_ = lstm_flags_mode();
       void* args[] = {&T_, &N_, &H_, &D_, &UB_, &BT_, &dy, &DYD_, &wpt, &c_all, &gates, &lens,
-                      &dgates, &ctrs, &err};
+                      &dgates, &ctrs, &err, &flags_};
       if (hipLaunchCooperativeKernel(fn, dim3(grid), dim3(GT), args, 0, st) == hipSuccess)
         return launch_status("ds2_lstm_bwd");
       (void)hipGetLastError();

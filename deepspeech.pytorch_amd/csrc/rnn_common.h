@@ -143,6 +143,41 @@ __device__ __forceinline__ bool group_wait(unsigned* ctr, unsigned target, unsig
   return *lds_flag != 0;
 }
 
+// Per-producer flag variant of the hand-off (same valid form, row 1: one lane of each
+// storing workgroup publishes with an sc1 store; the consumer polls every shard).  The
+// group's UB flags sit in one or two cache lines; wave 0 polls them with one vector sc1
+// load (lane i <- producer i) and a ballot, so no atomic read-modify-write serialises
+// the arrivals.  flags[i] holds the number of steps producer i has published.
+__device__ __forceinline__ bool flags_wait(const unsigned* flags, int count, unsigned target,
+                                           unsigned* err, int* lds_flag) {
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    unsigned spins = 0;
+    int ok = 1;
+    for (;;) {
+      const unsigned v = lane < count ? __hip_atomic_load(flags + lane, __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT)
+                                      : target;
+      if (__ballot(v < target) == 0ull) break;
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > kSpinLimit) {
+        if (lane == 0) __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ok = 0;
+        break;
+      }
+    }
+    if (lane == 0) *lds_flag = ok;
+  }
+  __syncthreads();
+  return *lds_flag != 0;
+}
+
+__device__ __forceinline__ void flags_arrive(unsigned* flag, unsigned value) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains first
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(flag, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __device__ __forceinline__ void group_arrive(unsigned* ctr) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains first
   __syncthreads();

@@ -22,7 +22,7 @@ nbytes = _lib.size("ds2_gru_fwd_workspace_size", N, H, D)
 ws = torch.zeros(nbytes, dtype=torch.uint8, device=dev)
 UB, KS, BT = (H + 15) // 16, (H + 3) // 4, (N + 15) // 16
 al = lambda x: (x + 255) & ~255
-off = al(D * UB * KS * 3 * 64 * 4) + al((D * BT + 1) * 4)
+off = al(D * UB * KS * 3 * 64 * 4) + al((D * BT + 1 + D * BT * 64) * 4)
 for it in range(3):
     s0 = torch.cuda.Event(enable_timing=True); s1 = torch.cuda.Event(enable_timing=True)
     s0.record()

@@ -19,7 +19,8 @@ for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
         seen[name] += 1
     for k, v in seen.items():
         acc[k]["calls"] = max(acc[k]["calls"], v)
-print("kernel,calls,avg_read_MB,avg_write_MB,avg_total_MB")
+w = csv.writer(sys.stdout)
+w.writerow(["kernel", "calls", "avg_read_MB", "avg_write_MB", "avg_total_MB"])
 rows = []
 for k, v in acc.items():
     c = max(v["calls"], 1)
@@ -27,4 +28,4 @@ for k, v in acc.items():
     wr = v["WRITE_SIZE"] * 1024 / c / 1e6
     rows.append((rd + wr, k, c, rd, wr))
 for tot, k, c, rd, wr in sorted(rows, reverse=True):
-    print(f"{k},{c},{rd:.2f},{wr:.2f},{tot:.2f}")
+    w.writerow([k, c, f"{rd:.2f}", f"{wr:.2f}", f"{tot:.2f}"])

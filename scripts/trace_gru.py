@@ -27,7 +27,7 @@ gates = torch.empty(T, N, D, 4 * H, device=dev)
 ws = torch.zeros(_lib.size("ds2_gru_fwd_workspace_size", N, H, D), dtype=torch.uint8, device=dev)
 UB, KS, BT = (H + 15) // 16, (H + 3) // 4, (N + 15) // 16
 al = lambda x: (x + 255) & ~255
-off = al(D * UB * KS * 3 * 64 * 4) + al((D * BT + 1) * 4)
+off = al(D * UB * KS * 3 * 64 * 4) + al((D * BT + 1 + D * BT * 64) * 4)
 P = UB * D
 grid = 8 * ((P + 7) // 8) * BT
 for it in range(3):

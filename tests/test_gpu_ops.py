@@ -222,6 +222,32 @@ def test_gru_persistent_equals_per_step(dev, h, monkeypatch):
         _close(a, b, 1e-5, "persistent vs per-step")
 
 
+@pytest.mark.parametrize("cell", ["gru", "lstm"])
+def test_rnn_flag_handoff_equals_counter_handoff(dev, cell, monkeypatch):
+    """The per-producer-flag and the arrival-counter hand-offs of the persistent kernels
+    synchronise differently but compute the same thing: bit-identical outputs and grads."""
+    n, t, inp, h = 32, 29, 48, 64
+    gm = 3 if cell == "gru" else 4
+    g = torch.Generator().manual_seed(77)
+    weights = [torch.rand(s, generator=g) * 0.4 - 0.2 for s in
+               [(gm * h, inp), (gm * h, h), (gm * h,), (gm * h,)] * 2]
+    lens = torch.tensor(sorted([t - (i % 5) * 4 for i in range(n)], reverse=True), dtype=torch.int32)
+    x = torch.randn(t, n, inp, generator=g)
+    dy = torch.randn(t, n, h, generator=g)
+    fn = ops.GRULayerFn if cell == "gru" else ops.LSTMLayerFn
+    outs = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("DS2_RNN_FLAGS", flag)
+        ws = [w.to(dev).requires_grad_(True) for w in weights]
+        xd = x.to(dev).requires_grad_(True)
+        y = fn.apply(xd, lens.to(dev), True, h, *ws)
+        y.backward(dy.to(dev))
+        torch.cuda.synchronize()
+        outs.append([y.detach().cpu(), xd.grad.cpu()] + [w.grad.cpu() for w in ws])
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
 def test_gru_per_direction_output(dev):
     n, t, inp, h = 4, 11, 8, 16
     g = torch.Generator().manual_seed(5)
