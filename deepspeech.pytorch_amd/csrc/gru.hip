@@ -406,7 +406,7 @@ __global__ __launch_bounds__(GT) void gru_bwd_persist_kernel(
     const float* __restrict__ wpt, const float* __restrict__ h_all,
     const float* __restrict__ gates, const int* __restrict__ lens, float* __restrict__ dgx,
     float* __restrict__ dgh, unsigned* __restrict__ counters, unsigned* __restrict__ err,
-    int use_flags) {
+    int use_flags, unsigned long long* __restrict__ stamps) {
   constexpr int PITCH = KC_BWD + 4;
   __shared__ __attribute__((aligned(16))) float hs[GB * PITCH];
   float* red = hs;                          // reduction buffer aliases the staged rows
@@ -442,20 +442,45 @@ __global__ __launch_bounds__(GT) void gru_bwd_persist_kernel(
   const int len = owner ? lens[n] : 0;
   constexpr int RP = GU + 1;
   float dh_prev = 0.f, z_prev = 0.f;        // this thread's unit, carried in registers
+  // trace mode (DS2_GRU_STAMPS=2, as in the forward kernel)
+  const bool tracing = stamps != nullptr && threadIdx.x == 0;
+  auto trace_at = [&](int s, int p) {
+    if (tracing && s >= kTraceS0 && s < kTraceS0 + kTraceSteps)
+      stamps[((int64_t)(s - kTraceS0) * gridDim.x + blockIdx.x) * 5 + p] =
+          __builtin_amdgcn_s_memrealtime();
+  };
 
+  float px_dar = 0.f, px_daz = 0.f, px_dan = 0.f;   // dgx of the previous step (deferred)
+  int64_t px_row = -1;
   for (int s = 0; s < T; ++s) {
     const int t = d == 0 ? T - 1 - s : s;
     f32x4 acc0 = f32x4{0.f, 0.f, 0.f, 0.f};
     f32x4 acc1 = f32x4{0.f, 0.f, 0.f, 0.f};
+    trace_at(s, 0);
+    // this step's inputs that do not depend on other workgroups: issue before the wait
+    float dyv = 0.f, g_r = 0.f, g_z = 0.f, g_n = 0.f, g_hn = 0.f, hp = 0.f;
+    const int64_t row = ((int64_t)t * N + n) * D + d;
+    if (owner && t < len) {
+      dyv = dy[(((int64_t)t * N + n) * dyd + (dyd > 1 ? d : 0)) * H + j];
+      const float* gp = gates + row * 4 * H;
+      g_r = gp[j];
+      g_z = gp[H + j];
+      g_n = gp[2 * H + j];
+      g_hn = gp[3 * H + j];
+      const int tp = d == 0 ? t - 1 : t + 1;
+      if (tp >= 0 && tp < T) hp = h_all[(((int64_t)tp * N + n) * D + d) * H + j];
+    }
     if (s > 0) {
       const int tq = d == 0 ? t + 1 : t - 1;
       if (!(use_flags ? flags_wait(gflags, UB, (unsigned)s, err, &flag)
                       : group_wait(ctr, (unsigned)s * UB, err, &flag)))
         return;
+      trace_at(s, 1);
       const float* dghq = dgh + ((int64_t)tq * N * D + d) * H3;
       stage_rows_sc1<(GB * KC_BWD / 4 + GT - 1) / GT>(dghq, D * H3, N, n0, H3, 4 * GW * KSW, hs,
                                                        PITCH);
       __syncthreads();
+      trace_at(s, 2);
       const float* hrow = hs + (lane & 15) * PITCH + (lane >> 4) + 4 * a_ks;
 #pragma unroll
       for (int i = 0; i < KSW; i += 2) {
@@ -469,8 +494,8 @@ __global__ __launch_bounds__(GT) void gru_bwd_persist_kernel(
     for (int r = 0; r < 4; ++r)
       red[(wave * GB + (lane >> 4) * 4 + r) * RP + (lane & 15)] = acc0[r] + acc1[r];
     __syncthreads();
+    trace_at(s, 3);
     if (owner) {
-      const int64_t row = ((int64_t)t * N + n) * D + d;
       float dh = 0.f;
       float dar = 0.f, daz = 0.f, dan = 0.f, dghn = 0.f, zc = 0.f;
       if (t < len) {
@@ -481,22 +506,13 @@ __global__ __launch_bounds__(GT) void gru_bwd_persist_kernel(
           for (int w8 = 0; w8 < GW; ++w8) rec += red[(w8 * GB + m) * RP + u];
           carry = dh_prev * z_prev + rec;
         }
-        dh = dy[(((int64_t)t * N + n) * dyd + (dyd > 1 ? d : 0)) * H + j] + carry;
-        const float* gp = gates + row * 4 * H;
-        const float r = gp[j], nn = gp[2 * H + j], ghn = gp[3 * H + j];
-        zc = gp[H + j];
-        float hp = 0.f;
-        const int tp = d == 0 ? t - 1 : t + 1;
-        if (tp >= 0 && tp < T) hp = h_all[(((int64_t)tp * N + n) * D + d) * H + j];
-        dan = dh * (1.f - zc) * (1.f - nn * nn);
-        daz = dh * (hp - nn) * zc * (1.f - zc);
-        dar = dan * ghn * r * (1.f - r);
-        dghn = dan * r;
+        dh = dyv + carry;
+        zc = g_z;
+        dan = dh * (1.f - zc) * (1.f - g_n * g_n);
+        daz = dh * (hp - g_n) * zc * (1.f - zc);
+        dar = dan * g_hn * g_r * (1.f - g_r);
+        dghn = dan * g_r;
       }
-      float* gx = dgx + row * H3;
-      gx[j] = dar;
-      gx[H + j] = daz;
-      gx[2 * H + j] = dan;
       const int go = static_cast<int>((row * H3 + j) * 4);
       __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, dar), g_rs, go, 0, kSc1);
       __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, daz), g_rs, go + 4 * H, 0,
@@ -505,9 +521,18 @@ __global__ __launch_bounds__(GT) void gru_bwd_persist_kernel(
                                             0, kSc1);
       dh_prev = dh;
       z_prev = zc;
+      px_dar = dar; px_daz = daz; px_dan = dan; px_row = row;
     }
     if (use_flags) flags_arrive(gflags + ub, (unsigned)s + 1);
     else group_arrive(ctr);
+    trace_at(s, 4);
+    // dgx is consumed only by later kernels: store it after the hand-off is signalled
+    if (owner) {
+      float* gx = dgx + px_row * H3;
+      gx[j] = px_dar;
+      gx[H + j] = px_daz;
+      gx[2 * H + j] = px_dan;
+    }
   }
 }
 
@@ -668,8 +693,9 @@ ds2_status_t ds2_gru_bwd(int t_max, int n, int h, int num_dirs, const float* dy,
       return launch_status("ds2_gru counters");
     int T_ = t_max, N_ = n, H_ = h, D_ = num_dirs, UB_ = UB, BT_ = BT, DYD_ = dy_dirs;
     int flags_ = flags_mode();
+    unsigned long long* stamps = stamp_mode() == 2 ? stamp_slots(ctrs, n, num_dirs) : nullptr;
     void* args[] = {&T_, &N_, &H_, &D_, &UB_, &BT_, &dy, &DYD_, &wpt, &h_all, &gates, &lens,
-                    &dgates_x, &dgates_h, &ctrs, &err, &flags_};
+                    &dgates_x, &dgates_h, &ctrs, &err, &flags_, &stamps};
     const void* fn = nullptr;
     const int kp = persist_ksw((KS + GW - 1) / GW, KC_BWD);
     switch (kp) {

@@ -35,48 +35,66 @@ for it in range(3):
               b[0].data_ptr(), b[1].data_ptr(), lens.data_ptr(), h_all.data_ptr(),
               gates.data_ptr(), ws.data_ptr(), ws.numel(), ops._stream())
     torch.cuda.synchronize()
-tr = ws[off:off + NS * grid * 5 * 8].view(torch.int64).cpu().numpy().reshape(NS, grid, 5)
-groups = {}
-for wg in range(grid):
-    xcd, slot = wg & 7, wg >> 3
-    pair = xcd + 8 * (slot // BT)
-    bt = slot % BT
-    if pair >= P:
-        continue
-    d = pair // UB
-    groups.setdefault((d, bt), []).append(wg)
-ticks_us = 0.01
-rows = []
-for s in range(NS - 1):
-    for key, wgs in groups.items():
-        arr = tr[s, wgs, 4].astype(np.float64)
-        nxt_wait = tr[s + 1, wgs, 1].astype(np.float64)
-        last = arr.max()
-        rows.append(((arr.max() - arr.min()) * ticks_us, (np.sort(arr)[-2] - np.median(arr)) * ticks_us,
-                     (nxt_wait.min() - last) * ticks_us, (np.median(nxt_wait) - last) * ticks_us,
-                     (nxt_wait.max() - last) * ticks_us))
-r = np.array(rows)
-print("per group-step (us): arrival skew max-min %.2f | 2nd-last minus median arrival %.2f | "
-      "last arrival -> first consumer %.2f, median %.2f, last %.2f" % tuple(r.mean(0)))
-ph = tr[1:NS - 1]
-valid = ph[..., 0] > 0
-def mean_phase(a, b_):
-    return float(((ph[..., b_] - ph[..., a]) * ticks_us)[valid].mean())
-print("phases (us, mean over WGs/steps): wait %.2f, stage %.2f, mfma+red %.2f, pointwise+arrive %.2f"
-      % (mean_phase(0, 1), mean_phase(1, 2), mean_phase(2, 3), mean_phase(3, 4)))
-v2 = tr[1:NS - 1, :, 0] > 0
-step_len = (tr[2:NS, :, 0] - tr[1:NS - 1, :, 0])[v2] * ticks_us
-print("step length (us): mean %.2f" % step_len.mean())
-# which WGs arrive last most often (systematic skew?)
-last_counts = {}
-for s in range(NS):
-    for key, wgs in groups.items():
-        wl = wgs[int(np.argmax(tr[s, wgs, 4]))]
-        last_counts[wl] = last_counts.get(wl, 0) + 1
-top = sorted(last_counts.items(), key=lambda kv: -kv[1])[:8]
-print("most frequent last arrivers (wg: count, xcd):", [(k, v, k & 7) for k, v in top])
-# per-WG mean stage time by XCD
-st = ((ph[..., 2] - ph[..., 1]) * ticks_us)
-for x in range(8):
-    cols = [wg for wg in range(grid) if (wg & 7) == x and any(wg in v for v in groups.values())]
-    print(f"xcd {x}: stage {st[:, cols].mean():.2f} us, mfma {((ph[..., 3] - ph[..., 2]) * ticks_us)[:, cols].mean():.2f} us, wait {((ph[..., 1] - ph[..., 0]) * ticks_us)[:, cols].mean():.2f}")
+
+
+def analyse(tr, label):
+    print(f"--- {label}")
+    groups = {}
+    for wg in range(grid):
+        xcd, slot = wg & 7, wg >> 3
+        pair = xcd + 8 * (slot // BT)
+        bt = slot % BT
+        if pair >= P:
+            continue
+        d = pair // UB
+        groups.setdefault((d, bt), []).append(wg)
+    ticks_us = 0.01
+    rows = []
+    for s in range(NS - 1):
+        for key, wgs in groups.items():
+            arr = tr[s, wgs, 4].astype(np.float64)
+            nxt_wait = tr[s + 1, wgs, 1].astype(np.float64)
+            last = arr.max()
+            rows.append(((arr.max() - arr.min()) * ticks_us, (np.sort(arr)[-2] - np.median(arr)) * ticks_us,
+                         (nxt_wait.min() - last) * ticks_us, (np.median(nxt_wait) - last) * ticks_us,
+                         (nxt_wait.max() - last) * ticks_us))
+    r = np.array(rows)
+    print("per group-step (us): arrival skew max-min %.2f | 2nd-last minus median arrival %.2f | "
+          "last arrival -> first consumer %.2f, median %.2f, last %.2f" % tuple(r.mean(0)))
+    ph = tr[1:NS - 1]
+    valid = ph[..., 0] > 0
+    def mean_phase(a, b_):
+        return float(((ph[..., b_] - ph[..., a]) * ticks_us)[valid].mean())
+    print("phases (us, mean over WGs/steps): wait %.2f, stage %.2f, mfma+red %.2f, pointwise+arrive %.2f"
+          % (mean_phase(0, 1), mean_phase(1, 2), mean_phase(2, 3), mean_phase(3, 4)))
+    v2 = tr[1:NS - 1, :, 0] > 0
+    step_len = (tr[2:NS, :, 0] - tr[1:NS - 1, :, 0])[v2] * ticks_us
+    print("step length (us): mean %.2f" % step_len.mean())
+    # which WGs arrive last most often (systematic skew?)
+    last_counts = {}
+    for s in range(NS):
+        for key, wgs in groups.items():
+            wl = wgs[int(np.argmax(tr[s, wgs, 4]))]
+            last_counts[wl] = last_counts.get(wl, 0) + 1
+    top = sorted(last_counts.items(), key=lambda kv: -kv[1])[:8]
+    print("most frequent last arrivers (wg: count, xcd):", [(k, v, k & 7) for k, v in top])
+    # per-WG mean stage time by XCD
+    st = ((ph[..., 2] - ph[..., 1]) * ticks_us)
+    for x in range(8):
+        cols = [wg for wg in range(grid) if (wg & 7) == x and any(wg in v for v in groups.values())]
+        print(f"xcd {x}: stage {st[:, cols].mean():.2f} us, mfma {((ph[..., 3] - ph[..., 2]) * ticks_us)[:, cols].mean():.2f} us, wait {((ph[..., 1] - ph[..., 0]) * ticks_us)[:, cols].mean():.2f}")
+
+
+analyse(ws[off:off + NS * grid * 5 * 8].view(torch.int64).cpu().numpy().reshape(NS, grid, 5), "forward")
+dy = torch.randn(T, N, H, device=dev)
+dgx = torch.empty(T, N, D, 3 * H, device=dev)
+dgh = torch.empty(T, N, D, 3 * H, device=dev)
+wsb = torch.zeros(_lib.size("ds2_gru_bwd_workspace_size", N, H, D), dtype=torch.uint8, device=dev)
+for it in range(3):
+    _lib.call("ds2_gru_bwd", T, N, H, D, dy.data_ptr(), 1, w[0].data_ptr(), w[1].data_ptr(),
+              h_all.data_ptr(), gates.data_ptr(), lens.data_ptr(), dgx.data_ptr(), dgh.data_ptr(),
+              wsb.data_ptr(), wsb.numel(), ops._stream())
+    torch.cuda.synchronize()
+KS3 = (3 * H + 3) // 4
+offb = al(D * UB * KS3 * 64 * 4) + al(2 * N * D * H * 4) + al((D * BT + 1 + D * BT * 64) * 4)
+analyse(wsb[offb:offb + NS * grid * 5 * 8].view(torch.int64).cpu().numpy().reshape(NS, grid, 5), "backward")
