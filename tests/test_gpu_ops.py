@@ -579,3 +579,18 @@ def test_edit_distance_vs_reference_semantics(dev):
     for i in range(n):
         wer, cer, wref, cref = get_cer_wer(dec, to_s(a_rows[i]), to_s(b_rows[i]))
         assert out[i].tolist() == [wer, cer, int(wref), int(cref)], i
+
+
+# ---------------------------------------------------------------------------- colsum
+@pytest.mark.parametrize("rows,cols,ld,off", [(16032, 2400, 4800, 0), (16032, 2400, 4800, 2400),
+                                              (37, 5, 7, 1), (1000, 260, 260, 0)])
+@pytest.mark.parametrize("accumulate", [0, 1])
+def test_colsum(dev, rows, cols, ld, off, accumulate):
+    """ds2_colsum (bias gradients): vector and scalar paths vs a float64 reference."""
+    g = torch.Generator().manual_seed(rows + cols + off)
+    x = torch.randn(rows, ld, generator=g)
+    out0 = torch.randn(cols, generator=g)
+    ref = x[:, off:off + cols].double().sum(0) + (out0.double() if accumulate else 0.0)
+    out = out0.to(dev).clone()
+    ops.colsum(x.to(dev), rows, cols, ld, out, accumulate=bool(accumulate), off=off)
+    _close(out, ref, 1e-6, "colsum")
