@@ -12,6 +12,7 @@
 #include "common.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace ds2 {
 
@@ -88,6 +89,85 @@ __device__ __forceinline__ void store_tile(float* __restrict__ s, const float (&
   }
 }
 
+// Work items (blockIdx.x in dispatch order):
+//   [0, main_wgs)       one whole output tile each (batch == 1), XCD-aware order;
+//   [main_wgs, grid)    "tail" pieces: (batch, split, tile) of the tiles from tail_tile0
+//                       on, K range split nsplit ways; dispatched last, they fill the
+//                       slots the whole tiles leave in the final round.
+// XCD-aware (bijective) remap of both ranges: the blocks the dispatcher deals to one XCD
+// (ids congruent mod 8) get a contiguous run of tiles (pieces), n-tile fastest, so
+// workgroups sharing an operand panel share that XCD's L2.
+__device__ __forceinline__ void decode_work(int M, int N, int K, int main_wgs, int tail_tile0,
+                                            int tail_tiles, int nsplit, int kchunk,
+                                            float* partial, int& m0, int& n0, int& kbeg,
+                                            int& kend, int& bz, float*& part) {
+  const int tn = (N + BN - 1) / BN;
+  const int orig = blockIdx.x;
+  int tile, z = 0;
+  part = nullptr;
+  if (orig < main_wgs) {
+    const int q = main_wgs >> 3, r = main_wgs & 7;
+    const int xcd = orig & 7;
+    tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+  } else {
+    const int np = gridDim.x - main_wgs;
+    const int o = orig - main_wgs;
+    const int q = np >> 3, r = np & 7;
+    const int xcd = o & 7;
+    const int pidx = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (o >> 3);
+    z = pidx / tail_tiles;
+    const int lt = pidx - z * tail_tiles;
+    tile = tail_tile0 + lt;
+    if (nsplit > 1) part = partial + ((int64_t)z * tail_tiles + lt) * (BM * BN);
+  }
+  const int tile_m = tile / tn;
+  const int tile_n = tile - tile_m * tn;
+  // z = batch * nsplit + split
+  bz = z / nsplit;
+  const int sp = z - bz * nsplit;
+  kbeg = orig < main_wgs ? 0 : sp * kchunk;
+  kend = orig < main_wgs ? K : min(K, kbeg + kchunk);
+  m0 = tile_m * BM;
+  n0 = tile_n * BN;
+}
+
+// Epilogue: C/D map of the 32x32 MFMA: col = lane & 31, row = (r & 3) + 8 * (r >> 2) +
+// 4 * (lane >> 5).  Split pieces write a tile-local [BM][BN] partial slab.
+__device__ __forceinline__ void store_acc(const f32x16 (&acc)[2][2], int M, int N, float alpha,
+                                          float beta, float* __restrict__ C, int64_t ldc,
+                                          const float* __restrict__ bias, float* __restrict__ part,
+                                          int m0, int n0, int wm, int wn, int lane) {
+  const int lr = lane & 31;
+  const int lk = lane >> 5;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int col = n0 + wn + 32 * j + lr;
+      if (part != nullptr) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int rl = wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lk;
+          part[rl * BN + wn + 32 * j + lr] = acc[i][j][r];
+        }
+        continue;
+      }
+      if (col >= N) continue;
+      const float bv = bias != nullptr ? bias[col] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lk;
+        if (row < M) {
+          float* cp = C + (int64_t)row * ldc + col;
+          float v = alpha * acc[i][j][r] + bv;
+          if (beta != 0.f) v += beta * *cp;
+          *cp = v;
+        }
+      }
+    }
+  }
+}
+
 template <int TA, int TB, bool VA, bool VB>
 __global__ __launch_bounds__(256) void sgemm_kernel(
     int M, int N, int K, float alpha, const float* __restrict__ A, int64_t lda, int64_t sA,
@@ -103,47 +183,13 @@ __global__ __launch_bounds__(256) void sgemm_kernel(
   __shared__ __attribute__((aligned(16))) float As[2][BK * LDA_S];
   __shared__ __attribute__((aligned(16))) float Bs[2][BK * LDB_S];
 
-  // Work items (blockIdx.x in dispatch order):
-  //   [0, main_wgs)       one whole output tile each (batch == 1), XCD-aware order;
-  //   [main_wgs, grid)    "tail" pieces: (batch, split, tile) of the tiles from tail_tile0
-  //                       on, K range split nsplit ways; dispatched last, they fill the
-  //                       slots the whole tiles leave in the final round.
-  // XCD-aware (bijective) remap of the whole-tile range: the blocks the dispatcher deals
-  // to one XCD (ids congruent mod 8) get a contiguous run of tiles, n-tile fastest, so
-  // workgroups sharing an A row panel share that XCD's L2.
-  const int tn = (N + BN - 1) / BN;
-  const int orig = blockIdx.x;
-  int tile, z = 0;
-  float* __restrict__ part = nullptr;
-  if (orig < main_wgs) {
-    const int q = main_wgs >> 3, r = main_wgs & 7;
-    const int xcd = orig & 7;
-    tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
-  } else {
-    // same XCD-aware remap over the tail pieces: one XCD gets a contiguous run of
-    // (split, tile) pieces, so the pieces sharing an operand panel share its L2
-    const int np = gridDim.x - main_wgs;
-    const int o = orig - main_wgs;
-    const int q = np >> 3, r = np & 7;
-    const int xcd = o & 7;
-    const int pidx = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (o >> 3);
-    z = pidx / tail_tiles;
-    const int lt = pidx - z * tail_tiles;
-    tile = tail_tile0 + lt;
-    if (nsplit > 1) part = partial + ((int64_t)z * tail_tiles + lt) * (BM * BN);
-  }
-  const int tile_m = tile / tn;
-  const int tile_n = tile - tile_m * tn;
-  // z = batch * nsplit + split
-  const int bz = z / nsplit;
-  const int sp = z - bz * nsplit;
+  int m0, n0, kbeg, kend, bz;
+  float* part;
+  decode_work(M, N, K, main_wgs, tail_tile0, tail_tiles, nsplit, kchunk, partial, m0, n0, kbeg,
+              kend, bz, part);
   A += bz * sA;
   B += bz * sB;
   C += bz * sC;
-  const int kbeg = orig < main_wgs ? 0 : sp * kchunk;
-  const int kend = orig < main_wgs ? K : min(K, kbeg + kchunk);
-  const int m0 = tile_m * BM;
-  const int n0 = tile_n * BN;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int wm = (wave >> 1) * 64;
@@ -194,36 +240,9 @@ __global__ __launch_bounds__(256) void sgemm_kernel(
     __syncthreads();
   }
 
-  // epilogue: C/D map of the 32x32 MFMA: col = lane & 31,
-  // row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int col = n0 + wn + 32 * j + lr;
-      if (col >= N) continue;
-      if (part != nullptr) {              // tile-local [BM][BN] partial slab
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int rl = wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lk;
-          part[rl * BN + wn + 32 * j + lr] = acc[i][j][r];
-        }
-        continue;
-      }
-      const float bv = bias != nullptr ? bias[col] : 0.f;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lk;
-        if (row < M) {
-          float* cp = C + (int64_t)row * ldc + col;
-          float v = alpha * acc[i][j][r] + bv;
-          if (beta != 0.f) v += beta * *cp;
-          *cp = v;
-        }
-      }
-    }
-  }
+  store_acc(acc, M, N, alpha, beta, C, ldc, bias, part, m0, n0, wm, wn, lane);
 }
+
 
 // Tail tiles: C[b] = alpha * sum_s partial[b][s][tile] + beta * C[b] + bias (fixed order)
 __global__ void splitk_reduce_kernel(const float* __restrict__ partial, int M, int N, int nsplit,

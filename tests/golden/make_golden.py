@@ -236,6 +236,18 @@ def golden_seq_lens(path):
     print('wrote', path)
 
 
+def golden_package(path, seed=1234):
+    """A reference-format model package (model.py:426-468 serialize) of the tiny golden
+    model, for checkpoint compatibility (SURVEY §8f#3)."""
+    m = make_ref(seed, 16, 2)
+    pkg = ref_model.DeepSpeech.serialize(
+        m, epoch=2, iteration=5, loss_results=torch.tensor([3.0, 2.5, 2.0]),
+        cer_results=torch.tensor([90.0, 80.0, 70.0]), wer_results=torch.tensor([99.0, 95.0, 90.0]),
+        avg_loss=2.0, checkpoint=True)
+    torch.save(pkg, path)
+    print('wrote', path, sorted(pkg))
+
+
 if __name__ == '__main__':
     torch.set_num_threads(8)
     golden_tiny(os.path.join(HERE, 'tiny_ds2.npz'))
@@ -247,3 +259,4 @@ if __name__ == '__main__':
     golden_cfg1(os.path.join(HERE, 'cfg1_ds2.npz'))
     golden_decoder(os.path.join(HERE, 'greedy_decoder.npz'))
     golden_seq_lens(os.path.join(HERE, 'seq_lens.npz'))
+    golden_package(os.path.join(HERE, 'tiny_ref_package.pth'))

@@ -207,3 +207,38 @@ def test_beam_oracle_beam1_peaked_equals_greedy():
     res = ctc_beam.beam_decode_one(probs, t, beam=1)
     strings, _ = orc.greedy_decode(torch.from_numpy(probs[None]), [t])
     assert ''.join(LABELS[k] for k in res[0][1]) == strings[0][0]
+
+
+def test_reference_package_round_trip(golden_dir, tmp_path):
+    """Checkpoint compatibility (model.py:395-468): a package written by the
+    reference's DeepSpeech.serialize loads into ds2amd (torch.load weights_only=True) with
+    identical weights and metadata; ds2amd's serialize writes the same structure back."""
+    path = os.path.join(golden_dir, 'tiny_ref_package.pth')
+    m = dsm.DeepSpeech.load_model(path)
+    ref_pkg = torch.load(path, map_location='cpu', weights_only=True)
+    g = _load(golden_dir, 'tiny_ds2.npz')
+    fresh = build_model(**tiny_spec(g)[0])
+    for k, v in fresh.state_dict().items():
+        assert torch.equal(m.state_dict()[k], v), k
+    assert (m._hidden_size, m._hidden_layers, m._rnn_type, m._bidirectional) == \
+        (ref_pkg['hidden_size'], ref_pkg['hidden_layers'], ref_pkg['rnn_type'],
+         ref_pkg['bidirectional'])
+    ours = dsm.DeepSpeech.serialize(m, epoch=ref_pkg['epoch'] - 1, iteration=ref_pkg['iteration'],
+                                    loss_results=ref_pkg['loss_results'],
+                                    cer_results=ref_pkg['cer_results'],
+                                    wer_results=ref_pkg['wer_results'],
+                                    avg_loss=ref_pkg['avg_loss'], checkpoint=ref_pkg['checkpoint'])
+    assert sorted(ours) == sorted(ref_pkg)
+    for k in ref_pkg:
+        a, b = ours[k], ref_pkg[k]
+        if k == 'state_dict':
+            assert sorted(a) == sorted(b)
+            assert all(torch.equal(a[n], b[n]) for n in a)
+        elif torch.is_tensor(b):
+            assert torch.equal(a, b), k
+        else:
+            assert a == b, k
+    out = tmp_path / 'ours.pth'
+    torch.save(ours, out)
+    m2 = dsm.DeepSpeech.load_model(str(out))
+    assert all(torch.equal(m2.state_dict()[n], v) for n, v in m.state_dict().items())
