@@ -326,8 +326,10 @@ __global__ __launch_bounds__(GT) void gru_fwd_persist_kernel(
     trace_at(s, 0);
     if (s > 0) {
       if (!(use_flags ? flags_wait(gflags, UB, (unsigned)s, err, &flag)
-                      : group_wait(ctr, (unsigned)s * UB, err, &flag)))
+                      : group_wait(ctr, (unsigned)s * UB, err, &flag))) {
+        poison_rest(h_all, s, T, d != 0, N, D, n, d, H, j, H, 1, owner);
         return;
+      }
       trace_at(s, 1);
       if (stamping) { t1 = stamp_now(); acc_t[0] += t1 - t0; t0 = t1; }
       const float* hprev = h_all + ((int64_t)tp * N * D + d) * H;
@@ -398,6 +400,182 @@ __global__ __launch_bounds__(GT) void gru_fwd_persist_kernel(
   }
   if (stamping)
     for (int i = 0; i < 5; ++i) stamps[i] = acc_t[i];
+}
+
+// Direct-operand forward recurrence (H % 16 == 0, per-producer flags).
+//
+// Hand-off layout: besides h_all (row-major, for the GEMMs that follow), every producer
+// publishes its 16 units x 16 samples of h_t as ONE 1-KB tile in a two-slot ring,
+//   hx[slot = step & 1][d][bt][unit block][q][r][c]   (unit 4 q + c, sample n0 + r),
+// written by wave 0 with one 16-byte sc1 store per lane after a transpose through LDS.
+// The K range of W_hh h_{t-1} is split between the 8 waves in whole producer blocks
+// (wave w owns blocks [b0, b0 + nb)); lane (r, q) of a wave reads its four A operands of
+// block b (the k values 16 b + 4 q + 0..3 of sample r) as one 16-byte sc1 load, so each
+// load instruction is one contiguous 1-KB tile -- no LDS staging of h, no barrier between
+// the loads and the MFMAs.  W_hh fragments follow the same k order and are read once
+// from the unpacked weight.  Wave 0 polls the producer flags (flags_wait) and releases
+// the workgroup with a barrier (MI355X_MICROARCH.md "Valid forms" row 1).  A slot is
+// rewritten two steps later, after every consumer of the group has published the step
+// in between, i.e. after all its loads of the slot have returned.
+template <int NBW>
+__global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void gru_fwd_dop_kernel(
+    int T, int N, int H, int D, int UB, int BT, const float* __restrict__ xproj,
+    const float* __restrict__ w_f, const float* __restrict__ w_r, const float* __restrict__ b_f,
+    const float* __restrict__ b_r, const int* __restrict__ lens, float* __restrict__ h_all,
+    float* __restrict__ gates, float* __restrict__ hx, unsigned* __restrict__ counters,
+    unsigned* __restrict__ err, unsigned long long* __restrict__ stamps) {
+  constexpr int RP = 3 * GU + 1;
+  __shared__ float red[GW * GB * RP];
+  __shared__ __attribute__((aligned(16))) float tile[GB * GU];
+  __shared__ int flag;
+  int ub, d, bt;
+  if (!map_work(UB * D, BT, UB, ub, d, bt)) return;
+  const int n0 = bt * GB;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int b0 = (wave * UB) / GW;
+  const int nb = ((wave + 1) * UB) / GW - b0;   // host guarantees nb <= NBW
+  const unsigned* gflags = counters + (D * BT + 1) + (d * BT + bt) * UB;
+  unsigned* myflag = counters + (D * BT + 1) + (d * BT + bt) * UB + ub;
+  const int slot_floats = D * BT * UB * 256;
+  const __amdgpu_buffer_rsrc_t x_rs =
+      __builtin_amdgcn_make_buffer_rsrc(hx, (short)0, 2 * slot_floats * 4, 0x00020000);
+  const int grp_off = (d * BT + bt) * UB * 256;            // this group's tiles in a slot
+  const bool tracing = stamps != nullptr && threadIdx.x == 0;
+  auto trace_at = [&](int s, int p) {
+    if (tracing && s >= kTraceS0 && s < kTraceS0 + kTraceSteps)
+      stamps[((int64_t)(s - kTraceS0) * gridDim.x + blockIdx.x) * 5 + p] =
+          __builtin_amdgcn_s_memrealtime();
+  };
+
+  // W_hh fragments: w[g][i][c] = W_hh[g H + ub 16 + (lane & 15)][16 (b0 + i) + 4 (lane >> 4) + c]
+  f32x4 w[3][NBW];
+  {
+    const float* W = d == 0 ? w_f : w_r;
+    const float* wr = W + (int64_t)(ub * GU + (lane & 15)) * H + 16 * b0 + 4 * (lane >> 4);
+#pragma unroll
+    for (int i = 0; i < NBW; ++i)
+#pragma unroll
+      for (int g = 0; g < 3; ++g)
+        w[g][i] = i < nb ? *reinterpret_cast<const f32x4*>(wr + (int64_t)g * H * H + 16 * i)
+                         : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  const float* bh = d == 0 ? b_f : b_r;
+  const int m = threadIdx.x >> 4;
+  const int u = threadIdx.x & 15;
+  const int n = n0 + m;
+  const int j = ub * GU + u;
+  const bool owner = threadIdx.x < GB * GU && n < N;
+  float bias_r = 0.f, bias_z = 0.f, bias_n = 0.f;
+  int len = 0;
+  if (owner) {
+    bias_r = bh[j];
+    bias_z = bh[H + j];
+    bias_n = bh[2 * H + j];
+    len = lens[n];
+  }
+  // this thread's slot in the transposed tile: (q = u >> 2, r = m, c = u & 3)
+  const int tpos = ((u >> 2) * GB + m) * 4 + (u & 3);
+  float g_r = 0.f, g_z = 0.f, g_n = 0.f, g_hn = 0.f, h_own = 0.f;
+  int64_t g_row = -1;
+  for (int s = 0; s < T; ++s) {
+    const int t = d == 0 ? s : T - 1 - s;
+    const int64_t row = ((int64_t)t * N + n) * D + d;
+    float xr = 0.f, xz = 0.f, xn = 0.f;
+    if (owner && t < len) {
+      const float* xp = xproj + row * 3 * H;
+      xr = xp[j];
+      xz = xp[H + j];
+      xn = xp[2 * H + j];
+    }
+    f32x4 acc[3];
+#pragma unroll
+    for (int g = 0; g < 3; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+    trace_at(s, 0);
+    if (s > 0) {
+      if (!flags_wait(gflags, UB, (unsigned)s, err, &flag)) {
+        poison_rest(h_all, s, T, d != 0, N, D, n, d, H, j, H, 1, owner);
+        return;
+      }
+      trace_at(s, 1);
+      const int base = (((s - 1) & 1) * slot_floats + grp_off + b0 * 256 + lane * 4) * 4;
+      f32x4 hv[NBW];
+#pragma unroll
+      for (int i = 0; i < NBW; ++i) {
+        const int off = i < nb ? base + i * 1024 : 0x7ffffff0;
+        hv[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(x_rs, off, 0, kSc1));
+      }
+      // all loads in flight before the first MFMA (the scheduler would otherwise
+      // interleave them with the MFMAs and expose one load latency per block)
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < NBW; ++i)
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+          for (int g = 0; g < 3; ++g)
+            acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(hv[i][c], w[g][i][c], acc[g], 0, 0, 0);
+      trace_at(s, 2);
+    }
+#pragma unroll
+    for (int g = 0; g < 3; ++g)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        red[(wave * GB + (lane >> 4) * 4 + r) * RP + g * GU + (lane & 15)] = acc[g][r];
+    __syncthreads();
+    trace_at(s, 3);
+    if (threadIdx.x < GB * GU) {
+      float hout = 0.f;
+      if (owner) {
+        float gh[3];
+#pragma unroll
+        for (int g = 0; g < 3; ++g) {
+          float v = 0.f;
+#pragma unroll
+          for (int w8 = 0; w8 < GW; ++w8) v += red[(w8 * GB + m) * RP + g * GU + u];
+          gh[g] = v;
+        }
+        const float ghr = gh[0] + bias_r;
+        const float ghz = gh[1] + bias_z;
+        float ghn = gh[2] + bias_n;
+        float r = 0.f, z = 0.f, nn = 0.f;
+        if (t < len) {
+          r = sigmoidf_(ghr + xr);
+          z = sigmoidf_(ghz + xz);
+          nn = tanhf(xn + r * ghn);
+          hout = (h_own - nn) * z + nn;
+        } else {
+          ghn = 0.f;
+        }
+        h_own = hout;
+        g_r = r; g_z = z; g_n = nn; g_hn = ghn; g_row = row;
+      }
+      tile[tpos] = hout;
+    }
+    __syncthreads();
+    // publish: wave 0 stores the tile (one 16-B sc1 store per lane), drains, flags
+    if (wave == 0) {
+      const u32x4 v = *reinterpret_cast<const u32x4*>(tile + lane * 4);
+      __builtin_amdgcn_raw_buffer_store_b128(v, x_rs, ((s & 1) * slot_floats + grp_off +
+                                                       ub * 256 + lane * 4) * 4, 0, kSc1);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0)
+        __hip_atomic_store(myflag, (unsigned)s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    trace_at(s, 4);
+    // outputs consumed only by later kernels, off the critical path
+    if (owner) {
+      h_all[row * H + j] = h_own;
+      if (gates != nullptr) {
+        float* gp = gates + g_row * 4 * H;
+        gp[j] = g_r;
+        gp[H + j] = g_z;
+        gp[2 * H + j] = g_n;
+        gp[3 * H + j] = g_hn;
+      }
+    }
+  }
 }
 
 template <int KSW>
@@ -473,8 +651,10 @@ __global__ __launch_bounds__(GT) void gru_bwd_persist_kernel(
     if (s > 0) {
       const int tq = d == 0 ? t + 1 : t - 1;
       if (!(use_flags ? flags_wait(gflags, UB, (unsigned)s, err, &flag)
-                      : group_wait(ctr, (unsigned)s * UB, err, &flag)))
+                      : group_wait(ctr, (unsigned)s * UB, err, &flag))) {
+        poison_rest(dgx, s, T, d == 0, N, D, n, d, H, j, H3, 3, owner);
         return;
+      }
       trace_at(s, 1);
       const float* dghq = dgh + ((int64_t)tq * N * D + d) * H3;
       stage_rows_sc1<(GB * KC_BWD / 4 + GT - 1) / GT>(dghq, D * H3, N, n0, H3, 4 * GW * KSW, hs,
@@ -536,6 +716,165 @@ __global__ __launch_bounds__(GT) void gru_bwd_persist_kernel(
   }
 }
 
+// Direct-operand backward recurrence (H % 16 == 0, per-producer flags).  Same scheme
+// as gru_fwd_dop_kernel over K = 3H: each producer publishes its gate gradients
+// (dar, daz, dghn) as three 1-KB tiles, tile g * UB + ub of the ring
+//   gx[slot][d][bt][3 UB blocks][q][r][c],
+// whose block order is the k order of dgh; wave w owns blocks [b0, b0 + nb) of the 3 UB.
+// dgh (for the weight-gradient GEMM) and dgx are stored after the flag.
+template <int NBW>
+__global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void gru_bwd_dop_kernel(
+    int T, int N, int H, int D, int UB, int BT, const float* __restrict__ dy, int dyd,
+    const float* __restrict__ w_f, const float* __restrict__ w_r,
+    const float* __restrict__ h_all, const float* __restrict__ gates,
+    const int* __restrict__ lens, float* __restrict__ dgx, float* __restrict__ dgh,
+    float* __restrict__ gx, unsigned* __restrict__ counters, unsigned* __restrict__ err,
+    unsigned long long* __restrict__ stamps) {
+  constexpr int RP = GU + 1;
+  __shared__ float red[GW * GB * RP];
+  __shared__ __attribute__((aligned(16))) float tile[3 * GB * GU];
+  __shared__ int flag;
+  int ub, d, bt;
+  if (!map_work(UB * D, BT, UB, ub, d, bt)) return;
+  const int n0 = bt * GB;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int H3 = 3 * H;
+  const int NB3 = 3 * UB;
+  const int b0 = (wave * NB3) / GW;
+  const int nb = ((wave + 1) * NB3) / GW - b0;   // host guarantees nb <= NBW
+  const unsigned* gflags = counters + (D * BT + 1) + (d * BT + bt) * UB;
+  unsigned* myflag = counters + (D * BT + 1) + (d * BT + bt) * UB + ub;
+  const int slot_floats = D * BT * NB3 * 256;
+  const __amdgpu_buffer_rsrc_t x_rs =
+      __builtin_amdgcn_make_buffer_rsrc(gx, (short)0, 2 * slot_floats * 4, 0x00020000);
+  const int grp_off = (d * BT + bt) * NB3 * 256;
+  const bool tracing = stamps != nullptr && threadIdx.x == 0;
+  auto trace_at = [&](int s, int p) {
+    if (tracing && s >= kTraceS0 && s < kTraceS0 + kTraceSteps)
+      stamps[((int64_t)(s - kTraceS0) * gridDim.x + blockIdx.x) * 5 + p] =
+          __builtin_amdgcn_s_memrealtime();
+  };
+
+  // W_hh^T fragments: w[i][c] = W_hh[16 (b0 + i) + 4 (lane >> 4) + c][ub 16 + (lane & 15)]
+  f32x4 w[NBW];
+  {
+    const float* W = d == 0 ? w_f : w_r;
+    const float* wc = W + (int64_t)(16 * b0 + 4 * (lane >> 4)) * H + ub * GU + (lane & 15);
+#pragma unroll
+    for (int i = 0; i < NBW; ++i)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) w[i][c] = i < nb ? wc[(int64_t)(16 * i + c) * H] : 0.f;
+  }
+  const int m = threadIdx.x >> 4;
+  const int u = threadIdx.x & 15;
+  const int n = n0 + m;
+  const int j = ub * GU + u;
+  const bool owner = threadIdx.x < GB * GU && n < N;
+  const int len = owner ? lens[n] : 0;
+  const int tpos = ((u >> 2) * GB + m) * 4 + (u & 3);
+  float dh_prev = 0.f, z_prev = 0.f;
+  float px_dar = 0.f, px_daz = 0.f, px_dan = 0.f, px_dghn = 0.f;
+  int64_t px_row = -1;
+  for (int s = 0; s < T; ++s) {
+    const int t = d == 0 ? T - 1 - s : s;
+    f32x4 acc0 = f32x4{0.f, 0.f, 0.f, 0.f};
+    f32x4 acc1 = f32x4{0.f, 0.f, 0.f, 0.f};
+    trace_at(s, 0);
+    float dyv = 0.f, g_r = 0.f, g_z = 0.f, g_n = 0.f, g_hn = 0.f, hp = 0.f;
+    const int64_t row = ((int64_t)t * N + n) * D + d;
+    if (owner && t < len) {
+      dyv = dy[(((int64_t)t * N + n) * dyd + (dyd > 1 ? d : 0)) * H + j];
+      const float* gp = gates + row * 4 * H;
+      g_r = gp[j];
+      g_z = gp[H + j];
+      g_n = gp[2 * H + j];
+      g_hn = gp[3 * H + j];
+      const int tp = d == 0 ? t - 1 : t + 1;
+      if (tp >= 0 && tp < T) hp = h_all[(((int64_t)tp * N + n) * D + d) * H + j];
+    }
+    if (s > 0) {
+      if (!flags_wait(gflags, UB, (unsigned)s, err, &flag)) {
+        poison_rest(dgx, s, T, d == 0, N, D, n, d, H, j, H3, 3, owner);
+        return;
+      }
+      trace_at(s, 1);
+      const int base = (((s - 1) & 1) * slot_floats + grp_off + b0 * 256 + lane * 4) * 4;
+      f32x4 gv[NBW];
+#pragma unroll
+      for (int i = 0; i < NBW; ++i) {
+        const int off = i < nb ? base + i * 1024 : 0x7ffffff0;
+        gv[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(x_rs, off, 0, kSc1));
+      }
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < NBW; ++i) {
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(gv[i][0], w[i][0], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(gv[i][1], w[i][1], acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(gv[i][2], w[i][2], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(gv[i][3], w[i][3], acc1, 0, 0, 0);
+      }
+      trace_at(s, 2);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      red[(wave * GB + (lane >> 4) * 4 + r) * RP + (lane & 15)] = acc0[r] + acc1[r];
+    __syncthreads();
+    trace_at(s, 3);
+    if (threadIdx.x < GB * GU) {
+      float dar = 0.f, daz = 0.f, dan = 0.f, dghn = 0.f;
+      if (owner) {
+        float dh = 0.f, zc = 0.f;
+        if (t < len) {
+          float carry = 0.f;
+          if (s > 0) {
+            float rec = 0.f;
+#pragma unroll
+            for (int w8 = 0; w8 < GW; ++w8) rec += red[(w8 * GB + m) * RP + u];
+            carry = dh_prev * z_prev + rec;
+          }
+          dh = dyv + carry;
+          zc = g_z;
+          dan = dh * (1.f - zc) * (1.f - g_n * g_n);
+          daz = dh * (hp - g_n) * zc * (1.f - zc);
+          dar = dan * g_hn * g_r * (1.f - g_r);
+          dghn = dan * g_r;
+        }
+        dh_prev = dh;
+        z_prev = zc;
+        px_dar = dar; px_daz = daz; px_dan = dan; px_dghn = dghn; px_row = row;
+      }
+      tile[tpos] = dar;
+      tile[GB * GU + tpos] = daz;
+      tile[2 * GB * GU + tpos] = dghn;
+    }
+    __syncthreads();
+    if (wave == 0) {
+      const int so = ((s & 1) * slot_floats + grp_off + ub * 256 + lane * 4) * 4;
+#pragma unroll
+      for (int g = 0; g < 3; ++g) {
+        const u32x4 v = *reinterpret_cast<const u32x4*>(tile + g * GB * GU + lane * 4);
+        __builtin_amdgcn_raw_buffer_store_b128(v, x_rs, so + g * UB * 1024, 0, kSc1);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0)
+        __hip_atomic_store(myflag, (unsigned)s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    trace_at(s, 4);
+    if (owner) {
+      float* gxr = dgx + px_row * H3;
+      gxr[j] = px_dar;
+      gxr[H + j] = px_daz;
+      gxr[2 * H + j] = px_dan;
+      float* ghr = dgh + px_row * H3;
+      ghr[j] = px_dar;
+      ghr[H + j] = px_daz;
+      ghr[2 * H + j] = px_dghn;
+    }
+  }
+}
+
 }  // namespace ds2
 
 using namespace ds2;
@@ -552,6 +891,21 @@ static inline int flags_mode() {
   return !(e != nullptr && e[0] == '0');
 }
 // counters (one per group) + error word + per-producer flags (64 per group), then stamps
+// direct-operand recurrence kernels (default; DS2_GRU_DOP=0 selects the LDS-staged ones)
+static inline int dop_enabled() {
+  const char* e = getenv("DS2_GRU_DOP");
+  return !(e != nullptr && e[0] == '0');
+}
+constexpr unsigned kDopPadLds = 80 * 1024;
+// smallest instantiated blocks-per-wave >= need (extra blocks are predicated off)
+static const void* bwd_dop_fn(int need) {
+#define DS2_BDOP(K) \
+  if (need <= K) return reinterpret_cast<const void*>(gru_bwd_dop_kernel<K>);
+  DS2_BDOP(1) DS2_BDOP(2) DS2_BDOP(3) DS2_BDOP(4) DS2_BDOP(6) DS2_BDOP(8) DS2_BDOP(10)
+  DS2_BDOP(13) DS2_BDOP(16) DS2_BDOP(19) DS2_BDOP(22) DS2_BDOP(24)
+#undef DS2_BDOP
+  return nullptr;
+}
 static inline size_t ctr_words(int n, int num_dirs) {
   const int groups = num_dirs * ((n + GB - 1) / GB);
   return (size_t)groups + 1 + (size_t)groups * 64;
@@ -566,11 +920,18 @@ static inline unsigned long long* stamp_slots(unsigned* ctrs, int n, int num_dir
                                                align256(ctr_words(n, num_dirs) * sizeof(unsigned)));
 }
 
+// two-slot ring of 1-KB hand-off tiles for the direct-operand kernels (gates tiles per
+// unit block: 1 forward, 3 backward)
+static inline size_t ring_bytes(int n, int h, int num_dirs, int tiles) {
+  const size_t UB = (h + GU - 1) / GU, BT = (n + GB - 1) / GB;
+  return align256(2 * (size_t)num_dirs * BT * UB * tiles * 256 * sizeof(float));
+}
+
 size_t ds2_gru_fwd_workspace_size(int n, int h, int num_dirs) {
   const int64_t UB = (h + GU - 1) / GU;
   const int64_t KS = (h + 3) / 4;
   return align256((size_t)(num_dirs * UB * KS * 3 * 64) * sizeof(float)) +
-         counter_bytes(n, num_dirs) + 256;
+         align256(counter_bytes(n, num_dirs)) + ring_bytes(n, h, num_dirs, 1) + 256;
 }
 
 #define DS2_FWD_CASE(K)                                                                    \
@@ -606,9 +967,40 @@ ds2_status_t ds2_gru_fwd(int t_max, int n, int h, int num_dirs, const float* xpr
   const int ksw = pick_ksw((KS + GW - 1) / GW);
   if (ksw < 0) return DS2_UNSUPPORTED_SHAPE;
   float* wp = static_cast<float*>(ws);
+  const int grid = mapped_grid(UB * num_dirs, BT);
+  if (dop_enabled() && flags_mode() && (h % GU) == 0 && UB <= 8 * GW && grid <= num_cus() &&
+      (int64_t)t_max * n * num_dirs * h * 4 < (1ll << 31)) {
+    unsigned* ctrs = reinterpret_cast<unsigned*>(
+        static_cast<char*>(ws) + align256((size_t)num_dirs * UB * KS * 3 * 64 * sizeof(float)));
+    unsigned* err = ctrs + num_dirs * BT;
+    if (hipMemsetAsync(ctrs, 0, counter_bytes(n, num_dirs), st) != hipSuccess)
+      return launch_status("ds2_gru counters");
+    int T_ = t_max, N_ = n, H_ = h, D_ = num_dirs, UB_ = UB, BT_ = BT;
+    unsigned long long* stamps = stamp_mode() == 2 ? stamp_slots(ctrs, n, num_dirs) : nullptr;
+    float* ring = reinterpret_cast<float*>(reinterpret_cast<char*>(ctrs) +
+                                           align256(counter_bytes(n, num_dirs)));
+    void* args[] = {&T_, &N_, &H_, &D_, &UB_, &BT_, &xproj, &w_hh_f, &w_hh_r, &b_hh_f,
+                    &b_hh_r, &lens, &h_all, &gates, &ring, &ctrs, &err, &stamps};
+    const void* fn = nullptr;
+    switch ((UB + GW - 1) / GW) {
+      case 1: fn = reinterpret_cast<const void*>(gru_fwd_dop_kernel<1>); break;
+      case 2: fn = reinterpret_cast<const void*>(gru_fwd_dop_kernel<2>); break;
+      case 3: fn = reinterpret_cast<const void*>(gru_fwd_dop_kernel<3>); break;
+      case 4: fn = reinterpret_cast<const void*>(gru_fwd_dop_kernel<4>); break;
+      case 5: fn = reinterpret_cast<const void*>(gru_fwd_dop_kernel<5>); break;
+      case 6: fn = reinterpret_cast<const void*>(gru_fwd_dop_kernel<6>); break;
+      case 7: fn = reinterpret_cast<const void*>(gru_fwd_dop_kernel<7>); break;
+      case 8: fn = reinterpret_cast<const void*>(gru_fwd_dop_kernel<8>); break;
+      default: break;
+    }
+    // the dynamic LDS keeps one workgroup per CU (every workgroup gets a whole CU's SIMDs)
+    if (fn != nullptr &&
+        hipLaunchCooperativeKernel(fn, dim3(grid), dim3(GT), args, kDopPadLds, st) == hipSuccess)
+      return launch_status("ds2_gru_fwd");
+    (void)hipGetLastError();
+  }
   hipLaunchKernelGGL(pack_fwd_kernel<3>, dim3(grid_cap((int64_t)num_dirs * UB * KS * 192)),
                      dim3(256), 0, st, w_hh_f, w_hh_r, h, num_dirs, UB, KS, wp);
-  const int grid = mapped_grid(UB * num_dirs, BT);
   if (persistent_enabled() && (h % 4) == 0 && grid <= num_cus() &&
       (int64_t)t_max * n * num_dirs * h * 4 < (1ll << 31)) {
     unsigned* ctrs = reinterpret_cast<unsigned*>(
@@ -649,8 +1041,8 @@ size_t ds2_gru_bwd_workspace_size(int n, int h, int num_dirs) {
   const int64_t UB = (h + GU - 1) / GU;
   const int64_t KS = (3 * h + 3) / 4;
   return align256((size_t)(num_dirs * UB * KS * 64) * sizeof(float)) +
-         align256((size_t)2 * n * num_dirs * h * sizeof(float)) + counter_bytes(n, num_dirs) +
-         512;
+         align256((size_t)2 * n * num_dirs * h * sizeof(float)) +
+         align256(counter_bytes(n, num_dirs)) + ring_bytes(n, h, num_dirs, 3) + 512;
 }
 
 #define DS2_BWD_CASE(K)                                                                     \
@@ -681,9 +1073,28 @@ ds2_status_t ds2_gru_bwd(int t_max, int n, int h, int num_dirs, const float* dy,
   float* wpt = static_cast<float*>(ws);
   size_t off = align256((size_t)num_dirs * UB * KS * 64 * sizeof(float));
   float* dhs = reinterpret_cast<float*>(static_cast<char*>(ws) + off);
+  const int grid = mapped_grid(UB * num_dirs, BT);
+  if (dop_enabled() && flags_mode() && (h % GU) == 0 && UB <= 8 * GW && grid <= num_cus() &&
+      (int64_t)t_max * n * num_dirs * 3 * h * 4 < (1ll << 31)) {
+    unsigned* ctrs = reinterpret_cast<unsigned*>(
+        reinterpret_cast<char*>(dhs) + align256((size_t)2 * n * num_dirs * h * sizeof(float)));
+    unsigned* err = ctrs + num_dirs * BT;
+    if (hipMemsetAsync(ctrs, 0, counter_bytes(n, num_dirs), st) != hipSuccess)
+      return launch_status("ds2_gru counters");
+    int T_ = t_max, N_ = n, H_ = h, D_ = num_dirs, UB_ = UB, BT_ = BT, DYD_ = dy_dirs;
+    unsigned long long* stamps = stamp_mode() == 2 ? stamp_slots(ctrs, n, num_dirs) : nullptr;
+    float* ring = reinterpret_cast<float*>(reinterpret_cast<char*>(ctrs) +
+                                           align256(counter_bytes(n, num_dirs)));
+    void* args[] = {&T_, &N_, &H_, &D_, &UB_, &BT_, &dy, &DYD_, &w_hh_f, &w_hh_r, &h_all,
+                    &gates, &lens, &dgates_x, &dgates_h, &ring, &ctrs, &err, &stamps};
+    const void* fn = bwd_dop_fn((3 * UB + GW - 1) / GW);
+    if (fn != nullptr &&
+        hipLaunchCooperativeKernel(fn, dim3(grid), dim3(GT), args, kDopPadLds, st) == hipSuccess)
+      return launch_status("ds2_gru_bwd");
+    (void)hipGetLastError();
+  }
   hipLaunchKernelGGL(pack_bwd_kernel<3>, dim3(grid_cap((int64_t)num_dirs * UB * KS * 64)),
                      dim3(256), 0, st, w_hh_f, w_hh_r, h, num_dirs, UB, KS, wpt);
-  const int grid = mapped_grid(UB * num_dirs, BT);
   if (persistent_enabled() && 3 * h <= KC_BWD && (h % 4) == 0 && grid <= num_cus() &&
       (int64_t)t_max * n * num_dirs * 3 * h * 4 < (1ll << 31)) {
     unsigned* ctrs = reinterpret_cast<unsigned*>(

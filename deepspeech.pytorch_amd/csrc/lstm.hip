@@ -312,8 +312,10 @@ __global__ __launch_bounds__(GT) void lstm_fwd_persist_kernel(
     for (int g = 0; g < 4; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
     if (s > 0) {
       if (!(use_flags ? flags_wait(gflags, UB, (unsigned)s, err, &flag)
-                      : group_wait(ctr, (unsigned)s * UB, err, &flag)))
+                      : group_wait(ctr, (unsigned)s * UB, err, &flag))) {
+        poison_rest(h_all, s, T, d != 0, N, D, n, d, H, j, H, 1, owner);
         return;
+      }
       stage_rows_sc1<(GB * LKC_FWD / 4 + GT - 1) / GT>(h_all + ((int64_t)tp * N * D + d) * H,
                                                         D * H, N, n0, H, 4 * GW * KSW, hs, PITCH);
       __syncthreads();
@@ -433,8 +435,10 @@ __global__ __launch_bounds__(GT) void lstm_bwd_persist_kernel(
     if (s > 0) {
       const int tq = d == 0 ? t + 1 : t - 1;
       if (!(use_flags ? flags_wait(gflags, UB, (unsigned)s, err, &flag)
-                      : group_wait(ctr, (unsigned)s * UB, err, &flag)))
+                      : group_wait(ctr, (unsigned)s * UB, err, &flag))) {
+        poison_rest(dg, s, T, d == 0, N, D, n, d, H, j, H4, 4, owner);
         return;
+      }
       const float* dgq = dg + ((int64_t)tq * N * D + d) * H4;
 #pragma unroll
       for (int c = 0; c < NCH; ++c) {

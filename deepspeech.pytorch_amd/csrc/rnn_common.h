@@ -172,6 +172,42 @@ __device__ __forceinline__ bool flags_wait(const unsigned* flags, int count, uns
   return *lds_flag != 0;
 }
 
+// After a hand-off timeout the workgroup leaves its step loop; its owning lanes first
+// fill their unit's outputs for every remaining step with NaN (`groups` slices of H
+// columns per row of `width` floats), so the failure reaches the loss instead of
+// leaving stale memory behind.  `rev` is true when direction d walks t downwards.
+__device__ __forceinline__ void poison_rest(float* out, int s, int T, bool rev, int N, int D,
+                                            int n, int d, int H, int j, int width, int groups,
+                                            bool owner) {
+  if (!owner || out == nullptr) return;
+  for (int q = s; q < T; ++q) {
+    const int t = rev ? T - 1 - q : q;
+    float* o = out + (((int64_t)t * N + n) * D + d) * width + j;
+    for (int g = 0; g < groups; ++g) o[(int64_t)g * H] = __builtin_nanf("");
+  }
+}
+
+// Per-wave form of flags_wait for the direct-operand kernels: the calling wave polls
+// only the `count` (<= 64) producers whose payload it loads itself (flags[i] for lane
+// i < count), so it loads right after its own poll has matched (row 1 of the table:
+// "the wave that polled loads only after its poll has matched").  No barrier.
+__device__ __forceinline__ bool wave_flags_wait(const unsigned* flags, int count,
+                                                unsigned target, unsigned* err) {
+  const int lane = threadIdx.x & 63;
+  unsigned spins = 0;
+  for (;;) {
+    const unsigned v = lane < count ? __hip_atomic_load(flags + lane, __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_AGENT)
+                                    : target;
+    if (__ballot(v < target) == 0ull) return true;
+    __builtin_amdgcn_s_sleep(1);
+    if (++spins > kSpinLimit) {
+      if (lane == 0) __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+  }
+}
+
 __device__ __forceinline__ void flags_arrive(unsigned* flag, unsigned value) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains first
   __syncthreads();

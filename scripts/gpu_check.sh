@@ -6,8 +6,11 @@ TAG=${1:-run}
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
 timeout -k 10 600 python -m pytest tests -q -m gpu -p no:cacheprovider > gpurun_out/$TAG.tests.log 2>&1
-echo "TESTS EXIT $?" >> gpurun_out/$TAG.tests.log
+RC=$?
+echo "TESTS EXIT $RC" >> gpurun_out/$TAG.tests.log
 tail -3 gpurun_out/$TAG.tests.log
+# a fault, abort or time limit ends the call here (nothing more runs on the GPU)
+if [ $RC -gt 1 ] && [ $RC -ne 5 ]; then echo "STOP after tests rc=$RC"; exit $RC; fi
 timeout -k 10 600 python bench.py ${BENCH_ARGS:---steps 5 --warmup 2} > gpurun_out/$TAG.bench.log 2>&1 || { echo "BENCH FAILED"; tail -30 gpurun_out/$TAG.bench.log; exit 1; }
 tail -1 gpurun_out/$TAG.bench.log
 cd /tmp && export TMPDIR=/tmp

@@ -1,0 +1,66 @@
+"""A/B timing of the GRU recurrence variants at the bench shape (T=501, N=32, H=800,
+bidirectional): LDS-staged vs direct-operand kernels and their polling forms, selected
+through the environment switches the library reads at every call."""
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "deepspeech.pytorch_amd"))
+import torch  # noqa: E402
+from ds2amd import _lib, ops  # noqa: E402
+
+T, N, H, D = 501, 32, 800, 2
+dev = torch.device("cuda")
+g = torch.Generator(device="cpu").manual_seed(0)
+xproj = (torch.randn(T, N, D, 3 * H, generator=g) * 0.5).to(dev)
+w = [(torch.rand(3 * H, H, generator=g) * 0.06 - 0.03).to(dev) for _ in range(2)]
+b = [(torch.rand(3 * H, generator=g) * 0.06 - 0.03).to(dev) for _ in range(2)]
+lens = torch.full((N,), T, dtype=torch.int32, device=dev)
+h_all = torch.empty(T, N, D, H, device=dev)
+gates = torch.empty(T, N, D, 4 * H, device=dev)
+dy = torch.randn(T, N, H, generator=g).to(dev)
+dgx = torch.empty(T, N, D, 3 * H, device=dev)
+dgh = torch.empty(T, N, D, 3 * H, device=dev)
+wsf = torch.zeros(_lib.size("ds2_gru_fwd_workspace_size", N, H, D), dtype=torch.uint8, device=dev)
+wsb = torch.zeros(_lib.size("ds2_gru_bwd_workspace_size", N, H, D), dtype=torch.uint8, device=dev)
+
+
+def fwd():
+    _lib.call("ds2_gru_fwd", T, N, H, D, xproj.data_ptr(), w[0].data_ptr(), w[1].data_ptr(),
+              b[0].data_ptr(), b[1].data_ptr(), lens.data_ptr(), h_all.data_ptr(),
+              gates.data_ptr(), wsf.data_ptr(), wsf.numel(), ops._stream())
+
+
+def bwd():
+    _lib.call("ds2_gru_bwd", T, N, H, D, dy.data_ptr(), 1, w[0].data_ptr(), w[1].data_ptr(),
+              h_all.data_ptr(), gates.data_ptr(), lens.data_ptr(), dgx.data_ptr(),
+              dgh.data_ptr(), wsb.data_ptr(), wsb.numel(), ops._stream())
+
+
+def timed(fn, reps=5):
+    fn()
+    torch.cuda.synchronize()
+    st = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(reps):
+        fn()
+    e1.record(st)
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+variants = {"staged": {"DS2_GRU_DOP": "0"}, "direct-operand": {"DS2_GRU_DOP": "1"}}
+ref = None
+for name, env in variants.items():
+    os.environ.update(env)
+    tf = timed(fwd)
+    out_h = h_all.clone()
+    tb = timed(bwd)
+    out_g = dgx.clone()
+    if ref is None:
+        ref = (out_h, out_g)
+    dh = (out_h - ref[0]).abs().max().item()
+    dg = (out_g - ref[1]).abs().max().item() / max(ref[1].abs().max().item(), 1e-30)
+    print(f"{name:12s} fwd {tf * 1e3:8.1f} us ({tf * 1e3 / T:5.2f}/step)  bwd {tb * 1e3:8.1f} us "
+          f"({tb * 1e3 / T:5.2f}/step)  max|dh| {dh:.2e} rel|ddgx| {dg:.2e}", flush=True)

@@ -168,13 +168,16 @@ def test_conv_block_fwd_bwd(dev, layout):
 
 # ---------------------------------------------------------------------------- GRU
 @pytest.mark.parametrize("n,t,inp,h,bidir", [(5, 23, 40, 24, True), (19, 9, 33, 400, True),
-                                             (3, 17, 20, 16, False)])
+                                             (3, 17, 20, 16, False), (20, 30, 64, 800, True)])
 def test_gru_layer(dev, n, t, inp, h, bidir):
     g = torch.Generator().manual_seed(n * 100 + h)
     gru = torch.nn.GRU(inp, h, bidirectional=bidir).double()
+    # +-0.3 for the small layers; the PyTorch default range 1/sqrt(h) for h = 800, where
+    # +-0.3 makes the recurrence chaotic enough that fp32 and fp64 trajectories separate
+    a = 0.3 if h <= 400 else h ** -0.5
     with torch.no_grad():
         for p in gru.parameters():
-            p.copy_(torch.rand(p.shape, generator=g, dtype=torch.float64) * 0.6 - 0.3)
+            p.copy_((torch.rand(p.shape, generator=g, dtype=torch.float64) * 2 - 1) * a)
     lens = torch.tensor(sorted([t] + [max(1, t - 3 * i - 1) for i in range(n - 1)], reverse=True),
                         dtype=torch.int32)
     x = torch.randn(t, n, inp, generator=g, dtype=torch.float64)
@@ -236,6 +239,7 @@ def test_rnn_flag_handoff_equals_counter_handoff(dev, cell, monkeypatch):
     dy = torch.randn(t, n, h, generator=g)
     fn = ops.GRULayerFn if cell == "gru" else ops.LSTMLayerFn
     outs = []
+    monkeypatch.setenv("DS2_GRU_DOP", "0")   # both forms of the LDS-staged kernels
     for flag in ("1", "0"):
         monkeypatch.setenv("DS2_RNN_FLAGS", flag)
         ws = [w.to(dev).requires_grad_(True) for w in weights]
@@ -246,6 +250,34 @@ def test_rnn_flag_handoff_equals_counter_handoff(dev, cell, monkeypatch):
         outs.append([y.detach().cpu(), xd.grad.cpu()] + [w.grad.cpu() for w in ws])
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("n,h,bidir", [(32, 64, True), (20, 800, True), (7, 48, False)])
+def test_gru_direct_operand_equals_staged(dev, n, h, bidir, monkeypatch):
+    """The direct-operand recurrences (per-wave producer polls, A operands loaded straight
+    into registers) and the LDS-staged ones agree; they sum the K range in a different
+    order, so within fp32 rounding."""
+    t, inp = 31, 40
+    nd = 2 if bidir else 1
+    g = torch.Generator().manual_seed(h + n)
+    weights = [torch.rand(s, generator=g) * 0.4 - 0.2 for s in
+               [(3 * h, inp), (3 * h, h), (3 * h,), (3 * h,)] * nd]
+    lens = torch.tensor(sorted([t - (i % 6) * 5 for i in range(n)], reverse=True),
+                        dtype=torch.int32)
+    x = torch.randn(t, n, inp, generator=g)
+    dy = torch.randn(t, n, h, generator=g)
+    outs = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("DS2_GRU_DOP", flag)
+        ws = [w.to(dev).requires_grad_(True) for w in weights]
+        xd = x.to(dev).requires_grad_(True)
+        y = ops.GRULayerFn.apply(xd, lens.to(dev), True, h, *ws)
+        y.backward(dy.to(dev))
+        torch.cuda.synchronize()
+        outs.append([y.detach().cpu(), xd.grad.cpu()] + [w.grad.cpu() for w in ws])
+    for a, b in zip(*outs):
+        assert torch.isfinite(a).all()
+        _close(a, b, 2e-5, "direct-operand vs staged")
 
 
 def test_gru_per_direction_output(dev):
