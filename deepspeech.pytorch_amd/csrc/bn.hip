@@ -125,18 +125,37 @@ __global__ __launch_bounds__(256) void reduce_planes_kernel(const float* __restr
 }
 
 // ---- finalize ---------------------------------------------------------------
-__global__ void stats_final_kernel(const double* __restrict__ partial, int nparts, int C,
-                                   double count, float eps, float momentum,
-                                   float* __restrict__ save_mean, float* __restrict__ save_invstd,
-                                   float* __restrict__ running_mean,
-                                   float* __restrict__ running_var) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+// Fixed-order sum of the (s, ss) partial pairs of column c = blockIdx.x * 64 + lane:
+// the 4 waves of a 256-thread block sum interleaved part subsets, wave 0 combines.
+// Returns false for the threads that do not finish a column.
+__device__ __forceinline__ bool sum_pairs(const double* __restrict__ partial, int nparts, int C,
+                                          int& c, double& s, double& ss) {
+  __shared__ double red[2][4][64];
+  const int lane = threadIdx.x & 63;
+  const int grp = threadIdx.x >> 6;
+  c = blockIdx.x * 64 + lane;
+  double a = 0.0, b = 0.0;
+  if (c < C)
+    for (int p = grp; p < nparts; p += 4) {
+      a += partial[((int64_t)p * C + c) * 2 + 0];
+      b += partial[((int64_t)p * C + c) * 2 + 1];
+    }
+  red[0][grp][lane] = a;
+  red[1][grp][lane] = b;
+  __syncthreads();
+  if (grp != 0 || c >= C) return false;
+  s = (red[0][0][lane] + red[0][1][lane]) + (red[0][2][lane] + red[0][3][lane]);
+  ss = (red[1][0][lane] + red[1][1][lane]) + (red[1][2][lane] + red[1][3][lane]);
+  return true;
+}
+
+__global__ __launch_bounds__(256) void stats_final_kernel(
+    const double* __restrict__ partial, int nparts, int C, double count, float eps,
+    float momentum, float* __restrict__ save_mean, float* __restrict__ save_invstd,
+    float* __restrict__ running_mean, float* __restrict__ running_var) {
+  int c;
   double s = 0.0, ss = 0.0;
-  for (int p = 0; p < nparts; ++p) {
-    s += partial[((int64_t)p * C + c) * 2 + 0];
-    ss += partial[((int64_t)p * C + c) * 2 + 1];
-  }
+  if (!sum_pairs(partial, nparts, C, c, s, ss)) return;
   const double mean = s / count;
   double var = ss / count - mean * mean;
   if (var < 0.0) var = 0.0;
@@ -162,17 +181,13 @@ __global__ void eval_stats_kernel(const float* __restrict__ rm, const float* __r
 //   dx = k1 * g - k2 - k3 * xhat  with k1 = gamma*invstd, k2 = k1*mean(g),
 //   k3 = k1*mean(g*xhat); also dgamma = sum(g*xhat), dbeta = sum(g) and the
 //   closed-form bias gradient (see ds2_bn_backward).
-__global__ void bwd_final_kernel(const double* __restrict__ partial, int nparts, int C,
-                                 double count, BnBwdArgs a, int n_outer, int D, int T,
-                                 float* __restrict__ coef, float* __restrict__ dgamma,
-                                 float* __restrict__ dbeta, float* __restrict__ dbias) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+__global__ __launch_bounds__(256) void bwd_final_kernel(
+    const double* __restrict__ partial, int nparts, int C, double count, BnBwdArgs a,
+    int n_outer, int D, int T, float* __restrict__ coef, float* __restrict__ dgamma,
+    float* __restrict__ dbeta, float* __restrict__ dbias) {
+  int c;
   double sg = 0.0, sgx = 0.0;
-  for (int p = 0; p < nparts; ++p) {
-    sg += partial[((int64_t)p * C + c) * 2 + 0];
-    sgx += partial[((int64_t)p * C + c) * 2 + 1];
-  }
+  if (!sum_pairs(partial, nparts, C, c, sg, sgx)) return;
   const double gbar = sg / count;
   const double gxbar = sgx / count;
   const double k1 = (double)a.gamma[c] * a.invstd[c];
@@ -389,7 +404,7 @@ ds2_status_t ds2_bn_train_stats(const float* x, int outer, int c, int inner, flo
     hipLaunchKernelGGL(reduce_planes_kernel<RED_STATS>, dim3(c, outer, kPlaneSplit), dim3(256), 0,
                        st, x, nullptr, c, 1, inner, a, partial);
   }
-  hipLaunchKernelGGL(stats_final_kernel, dim3(cdiv(c, 256)), dim3(256), 0, st, partial, nparts, c,
+  hipLaunchKernelGGL(stats_final_kernel, dim3(cdiv(c, 64)), dim3(256), 0, st, partial, nparts, c,
                      (double)outer * inner, eps, momentum, save_mean, save_invstd, running_mean,
                      running_var);
   return launch_status("ds2_bn_train_stats");
@@ -474,7 +489,7 @@ ds2_status_t ds2_bn_backward(const float* dy, int dy_layout, const float* x, int
     hipLaunchKernelGGL(reduce_planes_kernel<RED_BWD>, dim3(c, outer, kPlaneSplit), dim3(256), 0,
                        st, x, g_src, c, d, t, a, partial);
   }
-  hipLaunchKernelGGL(bwd_final_kernel, dim3(cdiv(c, 256)), dim3(256), 0, st, partial,
+  hipLaunchKernelGGL(bwd_final_kernel, dim3(cdiv(c, 64)), dim3(256), 0, st, partial,
                      (int)nparts, c, (double)outer * inner, a, outer, d, t, coef, dgamma, dbeta,
                      dbias_in);
   if (inner == 1) {

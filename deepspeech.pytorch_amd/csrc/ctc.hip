@@ -51,24 +51,38 @@ __global__ void ctc_logsoftmax_kernel(const float* __restrict__ acts, int t_max,
 }
 
 // 2) per utterance: label offset and the class -> label-position lists
-__global__ void ctc_prep_kernel(const int* __restrict__ labels, const int* __restrict__ label_lens,
-                                int n, int c, int max_l, int* __restrict__ offs,
-                                int* __restrict__ cls_start, int* __restrict__ cls_pos) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= n) return;
-  int off = 0;
-  for (int i = 0; i < b; ++i) off += label_lens[i];
-  offs[b] = off;
-  const int L = label_lens[b];
-  const int* lab = labels + off;
+__global__ __launch_bounds__(64) void ctc_prep_kernel(
+    const int* __restrict__ labels, const int* __restrict__ label_lens, int n, int c, int max_l,
+    int* __restrict__ offs, int* __restrict__ cls_start, int* __restrict__ cls_pos) {
+  // one wave per utterance; lane k owns class k (c <= 64)
+  __shared__ int lab_s[kMaxLabel];
+  const int b = blockIdx.x;
+  const int lane = threadIdx.x;
+  int part = 0;
+  for (int i = lane; i < b; i += 64) part += label_lens[i];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o);
+  const int off = part;
+  const int L = min(label_lens[b], kMaxLabel);   // host: label lengths <= max_l <= kMaxLabel
+  for (int i = lane; i < L; i += 64) lab_s[i] = labels[off + i];
+  __syncthreads();
+  int cnt = 0;
+  for (int i = 0; i < L; ++i) cnt += lab_s[i] == lane;
+  int incl = cnt;                           // inclusive scan over the classes
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int v = __shfl_up(incl, o);
+    if (lane >= o) incl += v;
+  }
+  const int start = incl - cnt;             // labels of a smaller class
+  if (lane == 0) offs[b] = off;
   int* cs = cls_start + b * 65;
+  if (lane <= c) cs[lane] = start;
+  if (lane == 0 && c == 64) cs[64] = L;
   int* cp = cls_pos + (int64_t)b * max_l;
-  for (int k = 0; k <= c; ++k) cs[k] = 0;
-  for (int i = 0; i < L; ++i) cs[lab[i] + 1]++;
-  for (int k = 0; k < c; ++k) cs[k + 1] += cs[k];
-  int fill[64];
-  for (int k = 0; k < c; ++k) fill[k] = cs[k];
-  for (int i = 0; i < L; ++i) cp[fill[lab[i]]++] = i;
+  int w = start;
+  for (int i = 0; i < L; ++i)
+    if (lab_s[i] == lane) cp[w++] = i;
 }
 
 // 3) alpha (blockIdx.y == 0) and beta (blockIdx.y == 1) scans run concurrently,
@@ -671,7 +685,7 @@ ds2_status_t ds2_ctc_loss(const float* acts, int t_max, int n, int c, const int*
   if (rows > 0)
     hipLaunchKernelGGL(ctc_logsoftmax_kernel, dim3(cdiv(rows, 4)), dim3(256), 0, st, acts, t_max,
                        n, c, lp);
-  hipLaunchKernelGGL(ctc_prep_kernel, dim3(cdiv(n, 64)), dim3(64), 0, st, labels, label_lens, n, c,
+  hipLaunchKernelGGL(ctc_prep_kernel, dim3(n), dim3(64), 0, st, labels, label_lens, n, c,
                      ml, offs, cls_start, cls_pos);
   hipLaunchKernelGGL(ctc_scan_kernel, dim3(n, 2), dim3(kScanThreads), 0, st, lp, t_max, c, labels,
                      label_lens, act_lens, offs, blank, s_max, alpha, beta, nll);

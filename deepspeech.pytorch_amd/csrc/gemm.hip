@@ -100,8 +100,8 @@ __device__ __forceinline__ void store_tile(float* __restrict__ s, const float (&
 __device__ __forceinline__ void decode_work(int M, int N, int K, int main_wgs, int tail_tile0,
                                             int tail_tiles, int nsplit, int kchunk,
                                             float* partial, int& m0, int& n0, int& kbeg,
-                                            int& kend, int& bz, float*& part) {
-  const int tn = (N + BN - 1) / BN;
+                                            int& kend, int& bz, float*& part, int bn = BN) {
+  const int tn = (N + bn - 1) / bn;
   const int orig = blockIdx.x;
   int tile, z = 0;
   part = nullptr;
@@ -118,7 +118,7 @@ __device__ __forceinline__ void decode_work(int M, int N, int K, int main_wgs, i
     z = pidx / tail_tiles;
     const int lt = pidx - z * tail_tiles;
     tile = tail_tile0 + lt;
-    if (nsplit > 1) part = partial + ((int64_t)z * tail_tiles + lt) * (BM * BN);
+    if (nsplit > 1) part = partial + ((int64_t)z * tail_tiles + lt) * (BM * bn);
   }
   const int tile_m = tile / tn;
   const int tile_n = tile - tile_m * tn;
@@ -128,7 +128,7 @@ __device__ __forceinline__ void decode_work(int M, int N, int K, int main_wgs, i
   kbeg = orig < main_wgs ? 0 : sp * kchunk;
   kend = orig < main_wgs ? K : min(K, kbeg + kchunk);
   m0 = tile_m * BM;
-  n0 = tile_n * BN;
+  n0 = tile_n * bn;
 }
 
 // Epilogue: C/D map of the 32x32 MFMA: col = lane & 31, row = (r & 3) + 8 * (r >> 2) +
@@ -244,13 +244,189 @@ __global__ __launch_bounds__(256) void sgemm_kernel(
 }
 
 
+// ---------------------------------------------------------------------------------------
+// Deep-K variant (float4-aligned operands): same work plan and epilogue semantics as
+// sgemm_kernel, but BK = 64 per LDS stage and v_mfma_f32_16x16x4_f32 with a 4 x WN grid
+// of 16x16 tiles per wave (tile 128 x 32 WN: WN = 4 -> 128, WN = 5 -> 160, which divides
+// the model's N = 800 / 1600 / 2400 exactly).  Within a k-group of 16, lane (r, q) feeds
+// its four MFMAs c = 0..3 with the k values 16 g + 4 q + c of row r: one ds_read_b128
+// from a k-contiguous image ([row][64 k], float4 slot XOR (row & 15): conflict-free for
+// the b128 lane groups and for the b128 stores) or four ds_read_b32 from a
+// row-contiguous image ([k][row], pitch rows + 4: the two 16-lane row groups of a
+// half-wave land on disjoint bank halves).  Each operand keeps the orientation of its
+// global layout, so every global load and LDS store is a contiguous float4.  One LDS
+// stage (<= 76 KB) per workgroup, two workgroups per CU: one computes while the other
+// refills; 16 WN MFMAs per wave per k-group, 64 WN between barriers.
+constexpr int K64 = 64;
+
+template <bool KC, int ROWS>
+struct Img64 {
+  static constexpr int PITCH = KC ? K64 : ROWS + 4;
+  static constexpr int FLOATS = KC ? ROWS * K64 : K64 * (ROWS + 4);
+  static constexpr int LOADS = ROWS * K64 / 4 / 256;   // float4 per thread
+};
+
+// ROWS rows x 64 k of one operand through a buffer resource; an element outside
+// [rows) x [k, kend) gets an out-of-range offset and reads as zero (no branches)
+template <bool KC, int ROWS>
+__device__ __forceinline__ void load64(__amdgpu_buffer_rsrc_t rs, int ld, int rows, int kend,
+                                       int r0, int k0, f32x4 (&v)[Img64<KC, ROWS>::LOADS]) {
+  constexpr int kOob = 0x7ffffff0;
+  constexpr int L = Img64<KC, ROWS>::LOADS;
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int q = 0; q < L; ++q) {
+    int r, k;
+    if (KC) {
+      r = r0 + (t >> 4) + 16 * q;
+      k = k0 + (t & 15) * 4;
+    } else {
+      const int i = t + 256 * q;
+      k = k0 + i / (ROWS / 4);
+      r = r0 + (i % (ROWS / 4)) * 4;
+    }
+    const int off = (r < rows && k < kend) ? (KC ? r * ld + k : k * ld + r) * 4 : kOob;
+    v[q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+  }
+}
+
+template <bool KC, int ROWS>
+__device__ __forceinline__ void store64(float* __restrict__ s,
+                                        const f32x4 (&v)[Img64<KC, ROWS>::LOADS]) {
+  constexpr int L = Img64<KC, ROWS>::LOADS;
+  constexpr int P = Img64<KC, ROWS>::PITCH;
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int q = 0; q < L; ++q) {
+    if (KC) {
+      const int r = (t >> 4) + 16 * q;
+      *reinterpret_cast<f32x4*>(s + r * P + 4 * ((t & 15) ^ (r & 15))) = v[q];
+    } else {
+      const int i = t + 256 * q;
+      *reinterpret_cast<f32x4*>(s + (i / (ROWS / 4)) * P + (i % (ROWS / 4)) * 4) = v[q];
+    }
+  }
+}
+
+// fragment of rows [rb, rb + 16) (rb % 16 == 0) for k-group g
+template <bool KC, int ROWS>
+__device__ __forceinline__ f32x4 frag64(const float* __restrict__ s, int rb, int g, int lane) {
+  constexpr int P = Img64<KC, ROWS>::PITCH;
+  const int r = lane & 15, q = lane >> 4;
+  if (KC) return *reinterpret_cast<const f32x4*>(s + (rb + r) * P + 4 * ((4 * g + q) ^ r));
+  const float* p = s + (16 * g + 4 * q) * P + rb + r;
+  return f32x4{p[0], p[P], p[2 * P], p[3 * P]};
+}
+
+template <int TA, int TB, int WN>
+__global__ __launch_bounds__(256, 2) void sgemm64_kernel(
+    int M, int N, int K, float alpha, const float* __restrict__ A, int64_t lda, int64_t sA,
+    const float* __restrict__ B, int64_t ldb, int64_t sB, float beta, float* __restrict__ C,
+    int64_t ldc, int64_t sC, const float* __restrict__ bias, int main_wgs, int tail_tile0,
+    int tail_tiles, int nsplit, int kchunk, float* __restrict__ partial) {
+  constexpr bool AK = (TA == 0);
+  constexpr bool BKc = (TB == 1);
+  constexpr int TBN = 32 * WN;              // tile width
+  using IA = Img64<AK, BM>;
+  using IB = Img64<BKc, TBN>;
+  __shared__ __attribute__((aligned(16))) float As[IA::FLOATS];
+  __shared__ __attribute__((aligned(16))) float Bs[IB::FLOATS];
+
+  int m0, n0, kbeg, kend, bz;
+  float* part;
+  decode_work(M, N, K, main_wgs, tail_tile0, tail_tiles, nsplit, kchunk, partial, m0, n0, kbeg,
+              kend, bz, part, TBN);
+  A += bz * sA;
+  B += bz * sB;
+  C += bz * sC;
+  // host: every operand spans < 2^31 bytes (32-bit buffer offsets)
+  const int a_rows = AK ? M : K, b_rows = BKc ? N : K;
+  const __amdgpu_buffer_rsrc_t a_rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(A), (short)0, static_cast<int>(a_rows * lda * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t b_rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(B), (short)0, static_cast<int>(b_rows * ldb * 4), 0x00020000);
+  const int ilda = static_cast<int>(lda), ildb = static_cast<int>(ldb);
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int wm = (wave >> 1) * 64;
+  const int wn = (wave & 1) * 16 * WN;
+
+  f32x4 acc[4][WN];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < WN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  f32x4 ra[IA::LOADS], rb[IB::LOADS];
+  const int ktiles = (kend - kbeg + K64 - 1) / K64;
+  load64<AK, BM>(a_rs, ilda, M, kend, m0, kbeg, ra);
+  load64<BKc, TBN>(b_rs, ildb, N, kend, n0, kbeg, rb);
+  for (int kt = 0; kt < ktiles; ++kt) {
+    store64<AK, BM>(As, ra);
+    store64<BKc, TBN>(Bs, rb);
+    __syncthreads();
+    if (kt + 1 < ktiles) {   // next stage's global loads fly during this stage's MFMAs
+      load64<AK, BM>(a_rs, ilda, M, kend, m0, kbeg + (kt + 1) * K64, ra);
+      load64<BKc, TBN>(b_rs, ildb, N, kend, n0, kbeg + (kt + 1) * K64, rb);
+    }
+    // k-groups past kend hold zeros: skip them (K = 800, 1312, 2400 end on half stages)
+    const int ng = min(K64 / 16, (kend - kbeg - kt * K64 + 15) / 16);
+#pragma unroll
+    for (int g = 0; g < K64 / 16; ++g) {
+      if (g >= ng) break;
+      f32x4 a[4], b[WN];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] = frag64<AK, BM>(As, wm + 16 * i, g, lane);
+#pragma unroll
+      for (int j = 0; j < WN; ++j) b[j] = frag64<BKc, TBN>(Bs, wn + 16 * j, g, lane);
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < WN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][c], b[j][c], acc[i][j], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+
+  // epilogue (16x16 C/D map: col = lane & 15, row = 4 * (lane >> 4) + r)
+  const int lc = lane & 15;
+  const int lr = 4 * (lane >> 4);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int j = 0; j < WN; ++j) {
+      const int cl = wn + 16 * j + lc;
+      if (part != nullptr) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) part[(wm + 16 * i + lr + r) * TBN + cl] = acc[i][j][r];
+        continue;
+      }
+      const int col = n0 + cl;
+      if (col >= N) continue;
+      const float bv = bias != nullptr ? bias[col] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wm + 16 * i + lr + r;
+        if (row < M) {
+          float* cp = C + (int64_t)row * ldc + col;
+          float v = alpha * acc[i][j][r] + bv;
+          if (beta != 0.f) v += beta * *cp;
+          *cp = v;
+        }
+      }
+    }
+  }
+}
+
 // Tail tiles: C[b] = alpha * sum_s partial[b][s][tile] + beta * C[b] + bias (fixed order)
 __global__ void splitk_reduce_kernel(const float* __restrict__ partial, int M, int N, int nsplit,
                                      int batch, int tail_tile0, int tail_tiles, float alpha,
                                      float beta, float* __restrict__ C, int64_t ldc, int64_t sC,
-                                     const float* __restrict__ bias) {
-  constexpr int TE = BM * BN;
-  const int tn = (N + BN - 1) / BN;
+                                     const float* __restrict__ bias, int bn) {
+  const int TE = BM * bn;
+  const int tn = (N + bn - 1) / bn;
   const int64_t total = (int64_t)batch * tail_tiles * TE;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * blockDim.x) {
@@ -259,8 +435,8 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ partial, int M, i
     const int lt = static_cast<int>(bt % tail_tiles);
     const int b = static_cast<int>(bt / tail_tiles);
     const int tile = tail_tile0 + lt;
-    const int row = (tile / tn) * BM + e / BN;
-    const int col = (tile % tn) * BN + e % BN;
+    const int row = (tile / tn) * BM + e / bn;
+    const int col = (tile % tn) * bn + e % bn;
     if (row >= M || col >= N) continue;
     float acc = 0.f;
     for (int sp = 0; sp < nsplit; ++sp)
@@ -314,13 +490,34 @@ static int device_cus() {
 // 768 + 90 tail tiles x 8 splits; the weight gradient 2400 x 800 (133 tiles, K = 16032)
 // becomes 133 tiles x 5 splits.  Split partials are reduced in a fixed order.
 struct GemmPlan {
-  int main_wgs, tail_tile0, tail_tiles, nsplit, kchunk;
+  int main_wgs, tail_tile0, tail_tiles, nsplit, kchunk, bn;
 };
 
-static GemmPlan gemm_plan(int m, int n, int k, int batch) {
-  const int tiles = cdiv(m, BM) * cdiv(n, BN);
-  GemmPlan p{0, 0, tiles, 1, std::max(k, 1)};
-  const int slots = 3 * device_cus();
+// the deep-K kernel (sgemm64_kernel) runs 2 workgroups per CU and BK = 64, the
+// original one 3 per CU and BK = 16
+static bool use_k64(bool va, bool vb) {
+  const char* e = getenv("DS2_GEMM64");
+  return va && vb && !(e != nullptr && e[0] == '0');
+}
+
+// 32-bit buffer offsets: each operand (one batch entry) must span < 2^31 bytes
+static bool fits_rsrc(int64_t rows, int64_t ld) { return rows * ld * 4 < (1ll << 31); }
+
+// tile width of the deep-K kernel: 160 where it wastes less of the last tile column
+// (N = 800, 1600, 2400 are multiples of 160), else 128
+static int pick_bn(int n) {
+  const char* e = getenv("DS2_GEMM_BN");
+  if (e != nullptr) return e[0] == '1' && e[1] == '6' ? 160 : 128;
+  const double w128 = (double)cdiv(n, 128) * 128, w160 = (double)cdiv(n, 160) * 160;
+  return w160 < w128 * 0.995 ? 160 : 128;
+}
+
+static GemmPlan gemm_plan(int m, int n, int k, int batch, bool k64) {
+  const int bn = k64 ? pick_bn(n) : BN;
+  const int tiles = cdiv(m, BM) * cdiv(n, bn);
+  GemmPlan p{0, 0, tiles, 1, std::max(k, 1), bn};
+  const int slots = (k64 ? 2 : 3) * device_cus();
+  const int bk = k64 ? K64 : BK;
   if (batch == 1) {
     p.main_wgs = (tiles / slots) * slots;
     p.tail_tile0 = p.main_wgs;
@@ -345,18 +542,22 @@ static GemmPlan gemm_plan(int m, int n, int k, int batch) {
     }
   }
   if (bs > 1) {
-    p.kchunk = cdiv(cdiv(k, bs), BK) * BK;
+    p.kchunk = cdiv(cdiv(k, bs), bk) * bk;
     p.nsplit = cdiv(k, p.kchunk);
   }
   return p;
 }
 
+static size_t plan_ws(const GemmPlan& p, int batch) {
+  return p.nsplit > 1 ? (size_t)p.nsplit * batch * p.tail_tiles * BM * p.bn * sizeof(float) + 256
+                      : 0;
+}
+
+// large enough for either kernel's plan (the choice depends on operand alignment)
 extern "C" size_t ds2_sgemm_workspace_size(int m, int n, int k, int batch) {
   if (m <= 0 || n <= 0 || k <= 0 || batch <= 0) return 0;
-  const GemmPlan p = gemm_plan(m, n, k, batch);
-  return p.nsplit > 1
-             ? (size_t)p.nsplit * batch * p.tail_tiles * BM * BN * sizeof(float) + 256
-             : 0;
+  return std::max(plan_ws(gemm_plan(m, n, k, batch, false), batch),
+                  plan_ws(gemm_plan(m, n, k, batch, true), batch));
 }
 
 extern "C" ds2_status_t ds2_sgemm_ws(int trans_a, int trans_b, int m, int n, int k, float alpha,
@@ -375,8 +576,10 @@ extern "C" ds2_status_t ds2_sgemm_ws(int trans_a, int trans_b, int m, int n, int
                   (trans_a ? (m % 4 == 0) : (k % 4 == 0));
   const bool vb = aligned16(b) && (ldb % 4 == 0) && (stride_b % 4 == 0) &&
                   (trans_b ? (k % 4 == 0) : (n % 4 == 0));
-  GemmPlan p = gemm_plan(m, n, k, batch);
-  if (p.nsplit > 1 && (ws == nullptr || ws_bytes < ds2_sgemm_workspace_size(m, n, k, batch))) {
+  const bool k64 = use_k64(va, vb) && fits_rsrc(trans_a ? k : m, lda) &&
+                   fits_rsrc(trans_b ? n : k, ldb);
+  GemmPlan p = gemm_plan(m, n, k, batch, k64);
+  if (p.nsplit > 1 && (ws == nullptr || ws_bytes < plan_ws(p, batch))) {
     p.nsplit = 1;                       // no workspace: whole-K pieces
     p.kchunk = std::max(k, 1);
   }
@@ -386,20 +589,35 @@ extern "C" ds2_status_t ds2_sgemm_ws(int trans_a, int trans_b, int m, int n, int
   dim3 grid(static_cast<unsigned>(nwg));
   hipStream_t st = as_stream(stream);
 #define DS2_G(TA_, TB_)                                                                       \
-  launch_sgemm_t<TA_, TB_>(va, vb, grid, st, m, n, k, alpha, a, lda, stride_a, b, ldb, stride_b, \
-                           beta, c, ldc, stride_c, bias, p.main_wgs, p.tail_tile0, p.tail_tiles,  \
-                           p.nsplit, p.kchunk, partial)
-  if (!trans_a && !trans_b) DS2_G(0, 0);
-  else if (!trans_a && trans_b) DS2_G(0, 1);
-  else if (trans_a && !trans_b) DS2_G(1, 0);
-  else DS2_G(1, 1);
+  if (k64 && p.bn == 160)                                                                    \
+    hipLaunchKernelGGL((sgemm64_kernel<TA_, TB_, 5>), grid, dim3(256), 0, st, m, n, k, alpha,  \
+                       a, lda, stride_a, b, ldb, stride_b, beta, c, ldc, stride_c, bias,       \
+                       p.main_wgs, p.tail_tile0, p.tail_tiles, p.nsplit, p.kchunk, partial);  \
+  else if (k64)                                                                               \
+    hipLaunchKernelGGL((sgemm64_kernel<TA_, TB_, 4>), grid, dim3(256), 0, st, m, n, k, alpha,  \
+                       a, lda, stride_a, b, ldb, stride_b, beta, c, ldc, stride_c, bias,       \
+                       p.main_wgs, p.tail_tile0, p.tail_tiles, p.nsplit, p.kchunk, partial);  \
+  else                                                                                        \
+    launch_sgemm_t<TA_, TB_>(va, vb, grid, st, m, n, k, alpha, a, lda, stride_a, b, ldb,       \
+                             stride_b, beta, c, ldc, stride_c, bias, p.main_wgs, p.tail_tile0, \
+                             p.tail_tiles, p.nsplit, p.kchunk, partial)
+  if (!trans_a && !trans_b) {
+    DS2_G(0, 0);
+  } else if (!trans_a && trans_b) {
+    DS2_G(0, 1);
+  } else if (trans_a && !trans_b) {
+    DS2_G(1, 0);
+  } else {
+    DS2_G(1, 1);
+  }
 #undef DS2_G
   if (p.nsplit > 1) {
-    const int64_t total = (int64_t)batch * p.tail_tiles * BM * BN;
+    const int64_t total = (int64_t)batch * p.tail_tiles * BM * p.bn;
     int g = cdiv(total, 256);
     if (g > 4096) g = 4096;
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3(g), dim3(256), 0, st, partial, m, n, p.nsplit,
-                       batch, p.tail_tile0, p.tail_tiles, alpha, beta, c, ldc, stride_c, bias);
+                       batch, p.tail_tile0, p.tail_tiles, alpha, beta, c, ldc, stride_c, bias,
+                       p.bn);
   }
   return launch_status("ds2_sgemm");
 }

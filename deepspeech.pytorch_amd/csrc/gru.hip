@@ -433,8 +433,8 @@ __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   const int n0 = bt * GB;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int b0 = (wave * UB) / GW;
-  const int nb = ((wave + 1) * UB) / GW - b0;   // host guarantees nb <= NBW
+  int b0, nb;
+  simd_split(UB, wave, b0, nb);                 // host guarantees nb <= NBW
   const unsigned* gflags = counters + (D * BT + 1) + (d * BT + bt) * UB;
   unsigned* myflag = counters + (D * BT + 1) + (d * BT + bt) * UB + ub;
   const int slot_floats = D * BT * UB * 256;
@@ -741,8 +741,8 @@ __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int H3 = 3 * H;
   const int NB3 = 3 * UB;
-  const int b0 = (wave * NB3) / GW;
-  const int nb = ((wave + 1) * NB3) / GW - b0;   // host guarantees nb <= NBW
+  int b0, nb;
+  simd_split(NB3, wave, b0, nb);                // host guarantees nb <= NBW
   const unsigned* gflags = counters + (D * BT + 1) + (d * BT + bt) * UB;
   unsigned* myflag = counters + (D * BT + 1) + (d * BT + bt) * UB + ub;
   const int slot_floats = D * BT * NB3 * 256;

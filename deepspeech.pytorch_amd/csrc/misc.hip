@@ -100,14 +100,26 @@ __global__ __launch_bounds__(256) void colsum_partial4_kernel(const float* __res
         part[0][threadIdx.x] + part[1][threadIdx.x] + part[2][threadIdx.x] + part[3][threadIdx.x];
 }
 
-__global__ void colsum_final_kernel(const double* __restrict__ partial, int chunks, int cols,
-                                    float* __restrict__ out, int accumulate) {
-  const int col = blockIdx.x * blockDim.x + threadIdx.x;
-  if (col >= cols) return;
+// 64 columns per block; the 4 waves sum interleaved chunk subsets, combined in a
+// fixed order (deterministic)
+__global__ __launch_bounds__(256) void colsum_final_kernel(const double* __restrict__ partial,
+                                                           int chunks, int cols,
+                                                           float* __restrict__ out,
+                                                           int accumulate) {
+  __shared__ double part[4][64];
+  const int lane = threadIdx.x & 63;
+  const int grp = threadIdx.x >> 6;
+  const int col = blockIdx.x * 64 + lane;
   double s = 0.0;
-  for (int c = 0; c < chunks; ++c) s += partial[(int64_t)c * cols + col];
-  const float v = static_cast<float>(s);
-  out[col] = accumulate ? out[col] + v : v;
+  if (col < cols)
+    for (int c = grp; c < chunks; c += 4) s += partial[(int64_t)c * cols + col];
+  part[grp][lane] = s;
+  __syncthreads();
+  if (grp == 0 && col < cols) {
+    const float v = static_cast<float>((part[0][lane] + part[1][lane]) +
+                                       (part[2][lane] + part[3][lane]));
+    out[col] = accumulate ? out[col] + v : v;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -302,7 +314,7 @@ ds2_status_t ds2_colsum(const float* x, int rows, int cols, int64_t ld, float* o
   else
     hipLaunchKernelGGL(colsum_partial_kernel, dim3(cdiv(cols, 64), chunks), dim3(256), 0,
                        as_stream(stream), x, rows, cols, ld, partial);
-  hipLaunchKernelGGL(colsum_final_kernel, dim3(cdiv(cols, 256)), dim3(256), 0, as_stream(stream),
+  hipLaunchKernelGGL(colsum_final_kernel, dim3(cdiv(cols, 64)), dim3(256), 0, as_stream(stream),
                      partial, chunks, cols, out, accumulate);
   return launch_status("ds2_colsum");
 }

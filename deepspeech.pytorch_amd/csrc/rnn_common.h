@@ -187,25 +187,20 @@ __device__ __forceinline__ void poison_rest(float* out, int s, int T, bool rev, 
   }
 }
 
-// Per-wave form of flags_wait for the direct-operand kernels: the calling wave polls
-// only the `count` (<= 64) producers whose payload it loads itself (flags[i] for lane
-// i < count), so it loads right after its own poll has matched (row 1 of the table:
-// "the wave that polled loads only after its poll has matched").  No barrier.
-__device__ __forceinline__ bool wave_flags_wait(const unsigned* flags, int count,
-                                                unsigned target, unsigned* err) {
-  const int lane = threadIdx.x & 63;
-  unsigned spins = 0;
-  for (;;) {
-    const unsigned v = lane < count ? __hip_atomic_load(flags + lane, __ATOMIC_RELAXED,
-                                                        __HIP_MEMORY_SCOPE_AGENT)
-                                    : target;
-    if (__ballot(v < target) == 0ull) return true;
-    __builtin_amdgcn_s_sleep(1);
-    if (++spins > kSpinLimit) {
-      if (lane == 0) __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return false;
-    }
-  }
+// K split of the direct-operand kernels: `nblk` 16-wide blocks over the GW = 8 waves,
+// balanced per SIMD (waves w and w + 4 share SIMD w % 4): SIMD s gets its share of the
+// blocks, split between its two waves; wave w owns the contiguous blocks [b0, b0 + nb).
+__device__ __forceinline__ void simd_split(int nblk, int wave, int& b0, int& nb) {
+  auto simd_lo = [&](int s) { return (nblk * s) / 4; };
+  auto wave_cnt = [&](int w) {
+    const int s = w & 3;
+    const int c = simd_lo(s + 1) - simd_lo(s);
+    return w < 4 ? (c + 1) / 2 : c / 2;
+  };
+  int start = 0;
+  for (int w = 0; w < wave; ++w) start += wave_cnt(w);
+  b0 = start;
+  nb = wave_cnt(wave);
 }
 
 __device__ __forceinline__ void flags_arrive(unsigned* flag, unsigned value) {

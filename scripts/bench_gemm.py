@@ -41,7 +41,19 @@ for name, ta, tb, m, n, k in SHAPES:
     at = a.t() if ta else a
     bt = b.t() if tb else b
     f2 = lambda: torch.mm(at, bt, out=c)
-    t1, t2 = timeit(f1), timeit(f2)
     fl = 2.0 * m * n * k
-    print(f"{name:9s} {m:6d}x{n:5d}x{k:6d}: ds2 {t1*1e3:8.1f} us {fl/t1/1e9:6.1f} TF | "
-          f"torch {t2*1e3:8.1f} us {fl/t2/1e9:6.1f} TF")
+    os.environ["DS2_GEMM64"] = "0"
+    t0 = timeit(f1)
+    r0 = c.clone()
+    os.environ["DS2_GEMM64"] = "1"
+    res = []
+    for bn in ("128", "160"):
+        os.environ["DS2_GEMM_BN"] = bn
+        t1 = timeit(f1)
+        rel = ((c - r0).abs().max() / r0.abs().max()).item()
+        res.append(f"bk64/{bn} {fl/t1/1e9:6.1f} TF ({rel:.0e})")
+    del os.environ["DS2_GEMM_BN"]
+    t1 = timeit(f1)
+    t2 = timeit(f2)
+    print(f"{name:9s} {m:6d}x{n:5d}x{k:6d}: bk16 {fl/t0/1e9:6.1f} | " + " | ".join(res) +
+          f" | auto {t1*1e3:7.1f} us {fl/t1/1e9:6.1f} | torch {fl/t2/1e9:6.1f} TF", flush=True)
