@@ -259,29 +259,37 @@ __global__ __launch_bounds__(256) void sgemm_kernel(
 // refills; 16 WN MFMAs per wave per k-group, 64 WN between barriers.
 constexpr int K64 = 64;
 
-template <bool KC, int ROWS>
-struct Img64 {
-  static constexpr int PITCH = KC ? K64 : ROWS + 4;
-  static constexpr int FLOATS = KC ? ROWS * K64 : K64 * (ROWS + 4);
-  static constexpr int LOADS = ROWS * K64 / 4 / 256;   // float4 per thread
+// LDS image of ROWS rows x KS k of one operand.  k-contiguous ([row][KS]): float4 slot
+// s of row r stored at slot s ^ swz(r), swz = r & 15 (KS = 64) or (r >> 1) & 7 (KS = 32),
+// which keeps both the ds_read_b128 fragment reads (16-lane groups, 64 banks) and the
+// ds_write_b128 stores (8-lane groups, 32 banks) conflict-free without padding.
+// Row-contiguous ([KS][ROWS + 4]).
+template <bool KC, int ROWS, int KS>
+struct Img {
+  static constexpr int PITCH = KC ? KS : ROWS + 4;
+  static constexpr int FLOATS = KC ? ROWS * KS : KS * (ROWS + 4);
+  static constexpr int LOADS = ROWS * KS / 4 / 256;   // float4 per thread
+  static constexpr int SLOTS = KS / 4;                // float4 per k-contiguous row
+  __device__ static __forceinline__ int swz(int r) { return KS == 64 ? (r & 15) : ((r >> 1) & 7); }
 };
 
-// ROWS rows x 64 k of one operand through a buffer resource; an element outside
-// [rows) x [k, kend) gets an out-of-range offset and reads as zero (no branches)
-template <bool KC, int ROWS>
-__device__ __forceinline__ void load64(__amdgpu_buffer_rsrc_t rs, int ld, int rows, int kend,
-                                       int r0, int k0, f32x4 (&v)[Img64<KC, ROWS>::LOADS]) {
+// one stage of an operand through a buffer resource; an element outside [rows) x
+// [k, kend) gets an out-of-range offset and reads as zero (no branches)
+template <bool KC, int ROWS, int KS>
+__device__ __forceinline__ void load_stage(__amdgpu_buffer_rsrc_t rs, int ld, int rows, int kend,
+                                           int r0, int k0,
+                                           f32x4 (&v)[Img<KC, ROWS, KS>::LOADS]) {
+  using I = Img<KC, ROWS, KS>;
   constexpr int kOob = 0x7ffffff0;
-  constexpr int L = Img64<KC, ROWS>::LOADS;
   const int t = threadIdx.x;
 #pragma unroll
-  for (int q = 0; q < L; ++q) {
+  for (int q = 0; q < I::LOADS; ++q) {
+    const int i = t + 256 * q;
     int r, k;
     if (KC) {
-      r = r0 + (t >> 4) + 16 * q;
-      k = k0 + (t & 15) * 4;
+      r = r0 + i / I::SLOTS;
+      k = k0 + (i % I::SLOTS) * 4;
     } else {
-      const int i = t + 256 * q;
       k = k0 + i / (ROWS / 4);
       r = r0 + (i % (ROWS / 4)) * 4;
     }
@@ -290,35 +298,47 @@ __device__ __forceinline__ void load64(__amdgpu_buffer_rsrc_t rs, int ld, int ro
   }
 }
 
-template <bool KC, int ROWS>
-__device__ __forceinline__ void store64(float* __restrict__ s,
-                                        const f32x4 (&v)[Img64<KC, ROWS>::LOADS]) {
-  constexpr int L = Img64<KC, ROWS>::LOADS;
-  constexpr int P = Img64<KC, ROWS>::PITCH;
+template <bool KC, int ROWS, int KS>
+__device__ __forceinline__ void store_stage(float* __restrict__ s,
+                                            const f32x4 (&v)[Img<KC, ROWS, KS>::LOADS]) {
+  using I = Img<KC, ROWS, KS>;
   const int t = threadIdx.x;
 #pragma unroll
-  for (int q = 0; q < L; ++q) {
+  for (int q = 0; q < I::LOADS; ++q) {
+    const int i = t + 256 * q;
     if (KC) {
-      const int r = (t >> 4) + 16 * q;
-      *reinterpret_cast<f32x4*>(s + r * P + 4 * ((t & 15) ^ (r & 15))) = v[q];
+      const int r = i / I::SLOTS;
+      *reinterpret_cast<f32x4*>(s + r * I::PITCH + 4 * ((i % I::SLOTS) ^ I::swz(r))) = v[q];
     } else {
-      const int i = t + 256 * q;
-      *reinterpret_cast<f32x4*>(s + (i / (ROWS / 4)) * P + (i % (ROWS / 4)) * 4) = v[q];
+      *reinterpret_cast<f32x4*>(s + (i / (ROWS / 4)) * I::PITCH + (i % (ROWS / 4)) * 4) = v[q];
     }
   }
 }
 
-// fragment of rows [rb, rb + 16) (rb % 16 == 0) for k-group g
-template <bool KC, int ROWS>
-__device__ __forceinline__ f32x4 frag64(const float* __restrict__ s, int rb, int g, int lane) {
-  constexpr int P = Img64<KC, ROWS>::PITCH;
+// fragment of rows [rb, rb + 16) (rb % 16 == 0) for k-group g of the stage
+template <bool KC, int ROWS, int KS>
+__device__ __forceinline__ f32x4 frag(const float* __restrict__ s, int rb, int g, int lane) {
+  using I = Img<KC, ROWS, KS>;
   const int r = lane & 15, q = lane >> 4;
-  if (KC) return *reinterpret_cast<const f32x4*>(s + (rb + r) * P + 4 * ((4 * g + q) ^ r));
-  const float* p = s + (16 * g + 4 * q) * P + rb + r;
-  return f32x4{p[0], p[P], p[2 * P], p[3 * P]};
+  if (KC)
+    return *reinterpret_cast<const f32x4*>(s + (rb + r) * I::PITCH +
+                                           4 * ((4 * g + q) ^ I::swz(rb + r)));
+  const float* p = s + (16 * g + 4 * q) * I::PITCH + rb + r;
+  return f32x4{p[0], p[I::PITCH], p[2 * I::PITCH], p[3 * I::PITCH]};
 }
 
-template <int TA, int TB, int WN>
+// Deep-K variant (float4-aligned operands): same work plan and epilogue semantics as
+// sgemm_kernel; v_mfma_f32_16x16x4_f32 with a 4 x WN grid of 16x16 tiles per wave (tile
+// 128 x 32 WN: WN = 4 -> 128, WN = 5 -> 160, which divides the model's N = 800 / 1600 /
+// 2400 exactly).  Within a k-group of 16, lane (r, q) feeds its four MFMAs c = 0..3 with
+// the k values 16 g + 4 q + c of row r: one ds_read_b128 from a k-contiguous image or
+// four ds_read_b32 from a row-contiguous one.  Each operand keeps the orientation of its
+// global layout, so every global load and LDS store is a contiguous float4.
+//   NBUF = 1: one LDS stage of KS = 64 per workgroup (<= 76 KB, two workgroups per CU);
+//             store, barrier, MFMAs, barrier.
+//   NBUF = 2: two stages of KS = 32; the next stage is stored into the other buffer at
+//             the top of each stage, one barrier per stage.
+template <int TA, int TB, int WN, int KS, int NBUF>
 __global__ __launch_bounds__(256, 2) void sgemm64_kernel(
     int M, int N, int K, float alpha, const float* __restrict__ A, int64_t lda, int64_t sA,
     const float* __restrict__ B, int64_t ldb, int64_t sB, float beta, float* __restrict__ C,
@@ -327,10 +347,10 @@ __global__ __launch_bounds__(256, 2) void sgemm64_kernel(
   constexpr bool AK = (TA == 0);
   constexpr bool BKc = (TB == 1);
   constexpr int TBN = 32 * WN;              // tile width
-  using IA = Img64<AK, BM>;
-  using IB = Img64<BKc, TBN>;
-  __shared__ __attribute__((aligned(16))) float As[IA::FLOATS];
-  __shared__ __attribute__((aligned(16))) float Bs[IB::FLOATS];
+  using IA = Img<AK, BM, KS>;
+  using IB = Img<BKc, TBN, KS>;
+  __shared__ __attribute__((aligned(16))) float As[NBUF][IA::FLOATS];
+  __shared__ __attribute__((aligned(16))) float Bs[NBUF][IB::FLOATS];
 
   int m0, n0, kbeg, kend, bz;
   float* part;
@@ -357,28 +377,17 @@ __global__ __launch_bounds__(256, 2) void sgemm64_kernel(
 #pragma unroll
     for (int j = 0; j < WN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  f32x4 ra[IA::LOADS], rb[IB::LOADS];
-  const int ktiles = (kend - kbeg + K64 - 1) / K64;
-  load64<AK, BM>(a_rs, ilda, M, kend, m0, kbeg, ra);
-  load64<BKc, TBN>(b_rs, ildb, N, kend, n0, kbeg, rb);
-  for (int kt = 0; kt < ktiles; ++kt) {
-    store64<AK, BM>(As, ra);
-    store64<BKc, TBN>(Bs, rb);
-    __syncthreads();
-    if (kt + 1 < ktiles) {   // next stage's global loads fly during this stage's MFMAs
-      load64<AK, BM>(a_rs, ilda, M, kend, m0, kbeg + (kt + 1) * K64, ra);
-      load64<BKc, TBN>(b_rs, ildb, N, kend, n0, kbeg + (kt + 1) * K64, rb);
-    }
+  auto compute = [&](const float* as, const float* bs, int k0) {
     // k-groups past kend hold zeros: skip them (K = 800, 1312, 2400 end on half stages)
-    const int ng = min(K64 / 16, (kend - kbeg - kt * K64 + 15) / 16);
+    const int ng = min(KS / 16, (kend - k0 + 15) / 16);
 #pragma unroll
-    for (int g = 0; g < K64 / 16; ++g) {
+    for (int g = 0; g < KS / 16; ++g) {
       if (g >= ng) break;
       f32x4 a[4], b[WN];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) a[i] = frag64<AK, BM>(As, wm + 16 * i, g, lane);
+      for (int i = 0; i < 4; ++i) a[i] = frag<AK, BM, KS>(as, wm + 16 * i, g, lane);
 #pragma unroll
-      for (int j = 0; j < WN; ++j) b[j] = frag64<BKc, TBN>(Bs, wn + 16 * j, g, lane);
+      for (int j = 0; j < WN; ++j) b[j] = frag<BKc, TBN, KS>(bs, wn + 16 * j, g, lane);
 #pragma unroll
       for (int c = 0; c < 4; ++c)
 #pragma unroll
@@ -387,7 +396,45 @@ __global__ __launch_bounds__(256, 2) void sgemm64_kernel(
           for (int j = 0; j < WN; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][c], b[j][c], acc[i][j], 0, 0, 0);
     }
-    __syncthreads();
+  };
+
+  f32x4 ra[IA::LOADS], rb[IB::LOADS];
+  const int ktiles = (kend - kbeg + KS - 1) / KS;
+  load_stage<AK, BM, KS>(a_rs, ilda, M, kend, m0, kbeg, ra);
+  load_stage<BKc, TBN, KS>(b_rs, ildb, N, kend, n0, kbeg, rb);
+  if (NBUF == 1) {
+    for (int kt = 0; kt < ktiles; ++kt) {
+      store_stage<AK, BM, KS>(As[0], ra);
+      store_stage<BKc, TBN, KS>(Bs[0], rb);
+      __syncthreads();
+      if (kt + 1 < ktiles) {   // next stage's global loads fly during this stage's MFMAs
+        load_stage<AK, BM, KS>(a_rs, ilda, M, kend, m0, kbeg + (kt + 1) * KS, ra);
+        load_stage<BKc, TBN, KS>(b_rs, ildb, N, kend, n0, kbeg + (kt + 1) * KS, rb);
+      }
+      compute(As[0], Bs[0], kbeg + kt * KS);
+      __syncthreads();
+    }
+  } else {
+    store_stage<AK, BM, KS>(As[0], ra);
+    store_stage<BKc, TBN, KS>(Bs[0], rb);
+    if (ktiles > 1) {
+      load_stage<AK, BM, KS>(a_rs, ilda, M, kend, m0, kbeg + KS, ra);
+      load_stage<BKc, TBN, KS>(b_rs, ildb, N, kend, n0, kbeg + KS, rb);
+    }
+    for (int kt = 0; kt < ktiles; ++kt) {
+      // stage kt visible; every wave is done with the other buffer (stage kt - 1)
+      __syncthreads();
+      const int cur = kt & 1;
+      if (kt + 1 < ktiles) {
+        store_stage<AK, BM, KS>(As[cur ^ 1], ra);
+        store_stage<BKc, TBN, KS>(Bs[cur ^ 1], rb);
+        if (kt + 2 < ktiles) {
+          load_stage<AK, BM, KS>(a_rs, ilda, M, kend, m0, kbeg + (kt + 2) * KS, ra);
+          load_stage<BKc, TBN, KS>(b_rs, ildb, N, kend, n0, kbeg + (kt + 2) * KS, rb);
+        }
+      }
+      compute(As[cur], Bs[cur], kbeg + kt * KS);
+    }
   }
 
   // epilogue (16x16 C/D map: col = lane & 15, row = 4 * (lane >> 4) + r)
@@ -465,6 +512,24 @@ static void launch_sgemm_t(bool va, bool vb, dim3 grid, hipStream_t st, int M, i
 #undef DS2_L
 }
 
+template <int TA, int TB>
+static void launch_k64(int bn, bool db, dim3 grid, hipStream_t st, int M, int N, int K,
+                       float alpha, const float* A, int64_t lda, int64_t sA, const float* B,
+                       int64_t ldb, int64_t sB, float beta, float* C, int64_t ldc, int64_t sC,
+                       const float* bias, int main_wgs, int tail_tile0, int tail_tiles,
+                       int nsplit, int kchunk, float* partial) {
+#define DS2_K(WN, KS, NB)                                                                   \
+  hipLaunchKernelGGL((sgemm64_kernel<TA, TB, WN, KS, NB>), grid, dim3(256), 0, st, M, N, K,    \
+                     alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC, bias, main_wgs,          \
+                     tail_tile0, tail_tiles, nsplit, kchunk, partial)
+  if (bn == 160) {
+    if (db) DS2_K(5, 32, 2); else DS2_K(5, 64, 1);
+  } else {
+    if (db) DS2_K(4, 32, 2); else DS2_K(4, 64, 1);
+  }
+#undef DS2_K
+}
+
 static inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 }  // namespace ds2
@@ -503,21 +568,21 @@ static bool use_k64(bool va, bool vb) {
 // 32-bit buffer offsets: each operand (one batch entry) must span < 2^31 bytes
 static bool fits_rsrc(int64_t rows, int64_t ld) { return rows * ld * 4 < (1ll << 31); }
 
-// tile width of the deep-K kernel: 160 where it wastes less of the last tile column
-// (N = 800, 1600, 2400 are multiples of 160), else 128
-static int pick_bn(int n) {
-  const char* e = getenv("DS2_GEMM_BN");
-  if (e != nullptr) return e[0] == '1' && e[1] == '6' ? 160 : 128;
-  const double w128 = (double)cdiv(n, 128) * 128, w160 = (double)cdiv(n, 160) * 160;
-  return w160 < w128 * 0.995 ? 160 : 128;
-}
+// Plan for tile width bn.  The split count s of the tail is chosen by a time model in
+// units of one workgroup slot's MFMA time per (128-row x k) tile step: whole rounds
+// cost k each, the tail ceil(pieces / slots) * kchunk; a split adds its partial-slab
+// write + read (8 B per element at ~4 TB/s) and the reduce launch.  `eff` is the tile's
+// relative MFMA efficiency (160-wide tiles: 5 B fragments per 4 A, measured ~7 % faster
+// per unit of work than 128-wide).
+struct PlanChoice {
+  GemmPlan p;
+  double t;   // seconds (model)
+};
 
-static GemmPlan gemm_plan(int m, int n, int k, int batch, bool k64) {
-  const int bn = k64 ? pick_bn(n) : BN;
+static PlanChoice plan_bn(int m, int n, int k, int batch, int bn, int slots, int bk,
+                          double eff) {
   const int tiles = cdiv(m, BM) * cdiv(n, bn);
   GemmPlan p{0, 0, tiles, 1, std::max(k, 1), bn};
-  const int slots = (k64 ? 2 : 3) * device_cus();
-  const int bk = k64 ? K64 : BK;
   if (batch == 1) {
     p.main_wgs = (tiles / slots) * slots;
     p.tail_tile0 = p.main_wgs;
@@ -526,26 +591,42 @@ static GemmPlan gemm_plan(int m, int n, int k, int batch, bool k64) {
       p.main_wgs = 0;
       p.tail_tile0 = 0;
       p.tail_tiles = tiles;
-      return p;
     }
   }
+  // seconds per unit (one k step of one BM x bn tile on one slot)
+  const double unit = 2.0 * BM * bn / (157.3e12 * eff / slots);
+  const double main_t = (double)(p.main_wgs / slots) * k * unit;
   const int64_t tail = (int64_t)p.tail_tiles * batch;
   const int smax = std::max(1, std::min(32, k / 256));
   double best = 1e30;
   int bs = 1;
   for (int s = 1; s <= smax; ++s) {
-    const double rounds = (double)((tail * s + slots - 1) / slots);
-    const double cost = rounds / s + (s > 1 ? 0.005 * s : 0.0);
-    if (cost < best - 1e-9) {
-      best = cost;
-      bs = s;
+    const int kc = cdiv(cdiv(k, s), bk) * bk;
+    const int ns = cdiv(k, kc);
+    if (s > 1 && ns != s) continue;
+    const int64_t pieces = tail * ns;
+    double t = (double)((pieces + slots - 1) / slots) * kc * unit;
+    if (ns > 1) t += (double)pieces * BM * bn * 8.0 / 4e12 + 6e-6;
+    if (t < best - 1e-12) {
+      best = t;
+      bs = ns;
     }
   }
   if (bs > 1) {
     p.kchunk = cdiv(cdiv(k, bs), bk) * bk;
     p.nsplit = cdiv(k, p.kchunk);
   }
-  return p;
+  return {p, main_t + best};
+}
+
+static GemmPlan gemm_plan(int m, int n, int k, int batch, bool k64) {
+  const int cus = device_cus();
+  if (!k64) return plan_bn(m, n, k, batch, BN, 3 * cus, BK, 1.0).p;
+  const char* e = getenv("DS2_GEMM_BN");
+  if (e != nullptr) return plan_bn(m, n, k, batch, e[1] == '6' ? 160 : 128, 2 * cus, K64, 1.0).p;
+  const PlanChoice a = plan_bn(m, n, k, batch, 128, 2 * cus, K64, 1.0);
+  const PlanChoice b = plan_bn(m, n, k, batch, 160, 2 * cus, K64, 1.07);
+  return b.t < a.t ? b.p : a.p;
 }
 
 static size_t plan_ws(const GemmPlan& p, int batch) {
@@ -578,6 +659,8 @@ extern "C" ds2_status_t ds2_sgemm_ws(int trans_a, int trans_b, int m, int n, int
                   (trans_b ? (k % 4 == 0) : (n % 4 == 0));
   const bool k64 = use_k64(va, vb) && fits_rsrc(trans_a ? k : m, lda) &&
                    fits_rsrc(trans_b ? n : k, ldb);
+  const char* dbe = getenv("DS2_GEMM_DB");
+  const bool db = dbe != nullptr && dbe[0] == '1';
   GemmPlan p = gemm_plan(m, n, k, batch, k64);
   if (p.nsplit > 1 && (ws == nullptr || ws_bytes < plan_ws(p, batch))) {
     p.nsplit = 1;                       // no workspace: whole-K pieces
@@ -589,14 +672,10 @@ extern "C" ds2_status_t ds2_sgemm_ws(int trans_a, int trans_b, int m, int n, int
   dim3 grid(static_cast<unsigned>(nwg));
   hipStream_t st = as_stream(stream);
 #define DS2_G(TA_, TB_)                                                                       \
-  if (k64 && p.bn == 160)                                                                    \
-    hipLaunchKernelGGL((sgemm64_kernel<TA_, TB_, 5>), grid, dim3(256), 0, st, m, n, k, alpha,  \
-                       a, lda, stride_a, b, ldb, stride_b, beta, c, ldc, stride_c, bias,       \
-                       p.main_wgs, p.tail_tile0, p.tail_tiles, p.nsplit, p.kchunk, partial);  \
-  else if (k64)                                                                               \
-    hipLaunchKernelGGL((sgemm64_kernel<TA_, TB_, 4>), grid, dim3(256), 0, st, m, n, k, alpha,  \
-                       a, lda, stride_a, b, ldb, stride_b, beta, c, ldc, stride_c, bias,       \
-                       p.main_wgs, p.tail_tile0, p.tail_tiles, p.nsplit, p.kchunk, partial);  \
+  if (k64)                                                                                    \
+    launch_k64<TA_, TB_>(p.bn, db, grid, st, m, n, k, alpha, a, lda, stride_a, b, ldb, stride_b, \
+                         beta, c, ldc, stride_c, bias, p.main_wgs, p.tail_tile0, p.tail_tiles,  \
+                         p.nsplit, p.kchunk, partial);                                         \
   else                                                                                        \
     launch_sgemm_t<TA_, TB_>(va, vb, grid, st, m, n, k, alpha, a, lda, stride_a, b, ldb,       \
                              stride_b, beta, c, ldc, stride_c, bias, p.main_wgs, p.tail_tile0, \

@@ -42,18 +42,21 @@ for name, ta, tb, m, n, k in SHAPES:
     bt = b.t() if tb else b
     f2 = lambda: torch.mm(at, bt, out=c)
     fl = 2.0 * m * n * k
-    os.environ["DS2_GEMM64"] = "0"
-    t0 = timeit(f1)
-    r0 = c.clone()
-    os.environ["DS2_GEMM64"] = "1"
-    res = []
-    for bn in ("128", "160"):
-        os.environ["DS2_GEMM_BN"] = bn
+    variants = [("bk16", {"DS2_GEMM64": "0"}), ("sb128", {"DS2_GEMM_BN": "128"}),
+                ("sb160", {"DS2_GEMM_BN": "160"}), ("db128", {"DS2_GEMM_BN": "128", "DS2_GEMM_DB": "1"}),
+                ("db160", {"DS2_GEMM_BN": "160", "DS2_GEMM_DB": "1"})]
+    res, ref = [], None
+    for vname, env in variants:
+        for key in ("DS2_GEMM64", "DS2_GEMM_BN", "DS2_GEMM_DB"):
+            os.environ.pop(key, None)
+        os.environ.update(env)
         t1 = timeit(f1)
-        rel = ((c - r0).abs().max() / r0.abs().max()).item()
-        res.append(f"bk64/{bn} {fl/t1/1e9:6.1f} TF ({rel:.0e})")
-    del os.environ["DS2_GEMM_BN"]
-    t1 = timeit(f1)
+        if ref is None:
+            ref = c.clone()
+        rel = ((c - ref).abs().max() / ref.abs().max()).item()
+        res.append(f"{vname} {fl/t1/1e9:6.1f}" + ("" if rel < 1e-5 else f" (rel {rel:.0e}!)"))
+    for key in ("DS2_GEMM64", "DS2_GEMM_BN", "DS2_GEMM_DB"):
+        os.environ.pop(key, None)
     t2 = timeit(f2)
-    print(f"{name:9s} {m:6d}x{n:5d}x{k:6d}: bk16 {fl/t0/1e9:6.1f} | " + " | ".join(res) +
-          f" | auto {t1*1e3:7.1f} us {fl/t1/1e9:6.1f} | torch {fl/t2/1e9:6.1f} TF", flush=True)
+    print(f"{name:9s} {m:6d}x{n:5d}x{k:6d} TF: " + " | ".join(res) + f" | torch {fl/t2/1e9:6.1f}",
+          flush=True)

@@ -41,7 +41,7 @@ def test_sgemm(dev, ta, tb, m, n, k):
     _close(cd, ref, 1e-5, "sgemm")
 
 
-@pytest.mark.parametrize("mode", ["bk16", "128", "160"])
+@pytest.mark.parametrize("mode", ["bk16", "128", "160", "db128", "db160"])
 @pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0)])
 def test_sgemm_full_rounds_plus_split_tail(dev, ta, tb, mode, monkeypatch):
     """Whole rounds of resident workgroups + a tail whose K range is split (one launch) and
@@ -49,7 +49,8 @@ def test_sgemm_full_rounds_plus_split_tail(dev, ta, tb, mode, monkeypatch):
     32x32x2 (DS2_GEMM64=0) and BK = 64 / 16x16x4 with 128- and 160-wide tiles."""
     monkeypatch.setenv("DS2_GEMM64", "0" if mode == "bk16" else "1")
     if mode != "bk16":
-        monkeypatch.setenv("DS2_GEMM_BN", mode)
+        monkeypatch.setenv("DS2_GEMM_BN", mode[-3:])
+        monkeypatch.setenv("DS2_GEMM_DB", "1" if mode.startswith("db") else "0")
     m, n, k = 128 * 29, 128 * 27 + 52, 2080
     g = torch.Generator().manual_seed(5)
     a = torch.randn(k, m, generator=g) if ta else torch.randn(m, k, generator=g)
