@@ -613,20 +613,41 @@ __global__ __launch_bounds__(256) void conv_patch_kernel(const float* __restrict
     if (c + 1 < L) load(c + 1);
     int po = po_start, bb = b0;
     const float* wrow = wl + lk * PT_WP + lr;
-    for (int s = 0; s < steps; ++s) {
-      const float av = wrow[s * 2 * PT_WP];
-      const float* pp = ps + po;
-      const float v0 = pp[0], v1 = pp[32], v2 = pp[64], v3 = pp[96];
-      acc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, v0, acc[0], 0, 0, 0);
-      acc[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, v1, acc[1], 0, 0, 0);
-      acc[2] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, v2, acc[2], 0, 0, 0);
-      acc[3] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, v3, acc[3], 0, 0, 0);
+    // Two operand sets in ping-pong: the reads of step s + 1 are issued before the MFMAs
+    // of step s (sched barriers keep that order), so the LDS latency hides behind this
+    // wave's own MFMAs.  A step past the end re-reads a valid address with A = 0.
+    auto advance = [&]() {
       bb += 2;
       po += 2;
       if (bb >= B) {            // kw >= 2 (host-checked): at most one wrap per step
         bb -= B;
         po += PT_PITCH - B;
       }
+    };
+    auto read = [&](int st, float& av, float (&v)[4]) {
+      const bool ok = st < steps;
+      const float* pp = ps + (ok ? po : po_start);
+      av = ok ? wrow[st * 2 * PT_WP] : 0.f;
+      v[0] = pp[0]; v[1] = pp[32]; v[2] = pp[64]; v[3] = pp[96];
+    };
+    auto mma = [&](float av, const float (&v)[4]) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, v[j], acc[j], 0, 0, 0);
+    };
+    float aA, aB, vA[4], vB[4];
+    read(0, aA, vA);
+    for (int s = 0; s < steps; s += 2) {
+      advance();
+      read(s + 1, aB, vB);
+      __builtin_amdgcn_sched_barrier(0);
+      mma(aA, vA);
+      __builtin_amdgcn_sched_barrier(0);
+      advance();
+      read(s + 2, aA, vA);
+      __builtin_amdgcn_sched_barrier(0);
+      mma(aB, vB);
+      __builtin_amdgcn_sched_barrier(0);
     }
     __syncthreads();
     if (c + 1 < L) {

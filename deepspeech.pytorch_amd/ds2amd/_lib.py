@@ -12,7 +12,7 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libds2hip.so")
+LIB_PATH = os.environ.get("DS2_LIB_PATH") or os.path.join(_HERE, "libds2hip.so")
 
 _c_int = ctypes.c_int
 _c_i64 = ctypes.c_int64
