@@ -89,7 +89,7 @@ class KernelProbe:
         return sum(ms) / len(ms), sum(self.flops) / len(self.flops), len(ms)
 
 
-def pmc_traffic_per_launch(prefix="sgemm_kernel", extra=("splitk_reduce_kernel",)):
+def pmc_traffic_per_launch(prefix="sgemm", extra=("splitk_reduce_kernel",)):
     """HBM bytes per ds2_sgemm_ws launch from the newest committed PMC summary
     (profiles/r*_pmc_traffic.csv, made by scripts/pmc_traffic.sh + pmc_summary.py:
     FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE, one pass per counter)."""
@@ -109,7 +109,7 @@ def pmc_traffic_per_launch(prefix="sgemm_kernel", extra=("splitk_reduce_kernel",
             calls = int(r["calls"])
         except (KeyError, TypeError, ValueError):
             continue
-        if prefix in name:
+        if prefix in name and not any(e in name for e in extra):
             launches += calls
             total += calls * float(r["avg_total_MB"])
         elif any(e in name for e in extra):
