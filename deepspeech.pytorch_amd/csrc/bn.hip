@@ -11,7 +11,7 @@
 
 namespace ds2 {
 
-constexpr int kRowChunks = 64;    // row chunks for the [R][C] reduction
+constexpr int kRowChunks = 256;   // row chunks for the [R][C] reduction (>= 4 workgroups per CU)
 constexpr int kPlaneSplit = 4;    // slices per (outer, channel) plane
 
 enum RedMode { RED_STATS = 0, RED_BWD = 1 };
@@ -76,6 +76,88 @@ __global__ __launch_bounds__(256) void reduce_rows_kernel(const float* __restric
     partial[((int64_t)chunk * C + col) * 2 + 0] = t0;
     partial[((int64_t)chunk * C + col) * 2 + 1] = t1;
   }
+}
+
+// Vector variant (C % 4 == 0, 16-B aligned rows): each lane owns 4 adjacent columns
+// (float4 loads, two rows in flight per row group), per-column BN parameters held in
+// registers; same partial layout as reduce_rows_kernel.
+template <int MODE>
+__global__ __launch_bounds__(256) void reduce_rows4_kernel(const float* __restrict__ x,
+                                                           const float* __restrict__ dy, int R,
+                                                           int C, BnBwdArgs a,
+                                                           double* __restrict__ partial) {
+  __shared__ double s0[4][256], s1[4][256];
+  const int lane = threadIdx.x & 63;
+  const int grp = threadIdx.x >> 6;
+  const int col = blockIdx.x * 256 + lane * 4;
+  const int chunk = blockIdx.y;
+  const int per = (R + gridDim.y - 1) / gridDim.y;
+  const int r0 = chunk * per;
+  const int r1 = min(R, r0 + per);
+  double acc0[4] = {0.0, 0.0, 0.0, 0.0}, acc1[4] = {0.0, 0.0, 0.0, 0.0};
+  if (col < C) {
+    float mu[4] = {0.f, 0.f, 0.f, 0.f}, is[4] = {0.f, 0.f, 0.f, 0.f};
+    float ga[4] = {0.f, 0.f, 0.f, 0.f}, be[4] = {0.f, 0.f, 0.f, 0.f};
+    if (MODE == RED_BWD) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        mu[e] = a.mean[col + e];
+        is[e] = a.invstd[col + e];
+        if (a.masked) {
+          ga[e] = a.gamma[col + e];
+          be[e] = a.beta[col + e];
+        }
+      }
+    }
+    auto add = [&](int r) {
+      const float4 v = *reinterpret_cast<const float4*>(x + (int64_t)r * C + col);
+      const float vv[4] = {v.x, v.y, v.z, v.w};
+      if (MODE == RED_STATS) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          acc0[e] += vv[e];
+          acc1[e] += (double)vv[e] * vv[e];
+        }
+      } else {
+        const float4 d = *reinterpret_cast<const float4*>(dy + (int64_t)r * C + col);
+        const float dd[4] = {d.x, d.y, d.z, d.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float xhat = (vv[e] - mu[e]) * is[e];
+          float g = dd[e];
+          if (a.masked) {
+            const float y2 = ga[e] * xhat + be[e];
+            g = (y2 > a.lo && y2 < a.hi) ? g : 0.f;
+          }
+          acc0[e] += g;
+          acc1[e] += (double)g * xhat;
+        }
+      }
+    };
+    int r = r0 + grp;
+    for (; r + 4 < r1; r += 8) {
+      add(r);
+      add(r + 4);
+    }
+    if (r < r1) add(r);
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    s0[grp][lane * 4 + e] = acc0[e];
+    s1[grp][lane * 4 + e] = acc1[e];
+  }
+  __syncthreads();
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c < C) {
+    const int t = threadIdx.x;
+    partial[((int64_t)chunk * C + c) * 2 + 0] = s0[0][t] + s0[1][t] + s0[2][t] + s0[3][t];
+    partial[((int64_t)chunk * C + c) * 2 + 1] = s1[0][t] + s1[1][t] + s1[2][t] + s1[3][t];
+  }
+}
+
+static inline bool rows_vec(const float* x, const float* dy, int c) {
+  return (c % 4) == 0 &&
+         ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(dy)) & 15) == 0;
 }
 
 // ---- planes reduction -------------------------------------------------------
@@ -397,8 +479,12 @@ ds2_status_t ds2_bn_train_stats(const float* x, int outer, int c, int inner, flo
   int nparts;
   if (inner == 1) {
     nparts = kRowChunks;
-    hipLaunchKernelGGL(reduce_rows_kernel<RED_STATS>, dim3(cdiv(c, 64), kRowChunks), dim3(256), 0,
-                       st, x, nullptr, outer, c, a, partial);
+    if (rows_vec(x, nullptr, c))
+      hipLaunchKernelGGL(reduce_rows4_kernel<RED_STATS>, dim3(cdiv(c, 256), kRowChunks),
+                         dim3(256), 0, st, x, nullptr, outer, c, a, partial);
+    else
+      hipLaunchKernelGGL(reduce_rows_kernel<RED_STATS>, dim3(cdiv(c, 64), kRowChunks),
+                         dim3(256), 0, st, x, nullptr, outer, c, a, partial);
   } else {
     nparts = outer * kPlaneSplit;
     hipLaunchKernelGGL(reduce_planes_kernel<RED_STATS>, dim3(c, outer, kPlaneSplit), dim3(256), 0,
@@ -483,8 +569,12 @@ ds2_status_t ds2_bn_backward(const float* dy, int dy_layout, const float* x, int
     g_src = dx;
   }
   if (inner == 1) {
-    hipLaunchKernelGGL(reduce_rows_kernel<RED_BWD>, dim3(cdiv(c, 64), kRowChunks), dim3(256), 0,
-                       st, x, g_src, outer, c, a, partial);
+    if (rows_vec(x, g_src, c))
+      hipLaunchKernelGGL(reduce_rows4_kernel<RED_BWD>, dim3(cdiv(c, 256), kRowChunks),
+                         dim3(256), 0, st, x, g_src, outer, c, a, partial);
+    else
+      hipLaunchKernelGGL(reduce_rows_kernel<RED_BWD>, dim3(cdiv(c, 64), kRowChunks),
+                         dim3(256), 0, st, x, g_src, outer, c, a, partial);
   } else {
     hipLaunchKernelGGL(reduce_planes_kernel<RED_BWD>, dim3(c, outer, kPlaneSplit), dim3(256), 0,
                        st, x, g_src, c, d, t, a, partial);

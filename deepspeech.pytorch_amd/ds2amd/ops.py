@@ -71,6 +71,25 @@ def matmul_nt(x2d: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] =
     return sgemm(x2d, w, out, m=m, n=n, k=k, trans_b=True, lda=k, ldb=k, ldc=n, bias=bias)
 
 
+# Gradient slots (optim.FlatParams): a registered parameter whose .grad is None gets its
+# gradient written straight into its slice of the flat gradient buffer; autograd then
+# adopts that view as p.grad (no accumulate kernel, no copy).  With p.grad already set
+# (backward without zero_grad) a fresh tensor is returned and autograd accumulates.
+_GRAD_SLOTS = {}
+
+
+def register_grad_slot(param, flat_grad, offset):
+    _GRAD_SLOTS[param.data_ptr()] = (flat_grad, int(offset), tuple(param.shape))
+
+
+def grad_like(param):
+    slot = _GRAD_SLOTS.get(param.data_ptr())
+    if slot is not None and param.grad is None and slot[2] == tuple(param.shape):
+        buf, off, shape = slot
+        return buf.narrow(0, off, param.numel()).view(shape)
+    return torch.empty_like(param)
+
+
 def conv_out_shape(h: int, w: int, kh: int, kw: int, sh: int, sw: int, ph: int, pw: int):
     return (h + 2 * ph - kh) // sh + 1, (w + 2 * pw - kw) // sw + 1
 
@@ -102,13 +121,15 @@ def conv2d_dgrad(dy, weight, x_shape, stride, padding):
     return dx
 
 
-def conv2d_wgrad(dy, x, w_shape, stride, padding, with_bias: bool):
+def conv2d_wgrad(dy, x, w_shape, stride, padding, with_bias: bool, out_dw=None, out_db=None):
     dy = _need(dy, "conv2d.dy")
     x = _need(x, "conv2d.x")
     n, ci, h, w = x.shape
     co, _, kh, kw = w_shape
-    dw = torch.empty(w_shape, device=x.device, dtype=_F32)
-    db = torch.empty(co, device=x.device, dtype=_F32) if with_bias else None
+    dw = out_dw if out_dw is not None else torch.empty(w_shape, device=x.device, dtype=_F32)
+    db = None
+    if with_bias:
+        db = out_db if out_db is not None else torch.empty(co, device=x.device, dtype=_F32)
     dims = (n, ci, h, w, co, kh, kw, stride[0], stride[1], padding[0], padding[1])
     nbytes = _lib.size("ds2_conv2d_wgrad_workspace_size", *dims)
     ws = _ws(nbytes, x.device)
@@ -139,11 +160,16 @@ def bn_apply(x, outer, c, inner, mean, invstd, gamma, beta):
 
 
 def bn_backward(dy, dy_layout, x, outer, c, d, t, mean, invstd, gamma, beta, masked=False,
-                lens=None, lo=0.0, hi=20.0, want_dbias=False):
+                lens=None, lo=0.0, hi=20.0, want_dbias=False, bias=None):
+    """dgamma / dbeta (/ dbias of the preceding conv) land in the parameters' gradient
+    slots when they have one (grad_like)."""
     dx = torch.empty(outer, c, d, t, device=x.device, dtype=_F32)
-    dgamma = torch.empty(c, device=x.device, dtype=_F32)
-    dbeta = torch.empty(c, device=x.device, dtype=_F32)
-    dbias = torch.empty(c, device=x.device, dtype=_F32) if want_dbias else None
+    dgamma = grad_like(gamma)
+    dbeta = grad_like(beta)
+    dbias = None
+    if want_dbias:
+        dbias = grad_like(bias) if bias is not None else torch.empty(c, device=x.device,
+                                                                      dtype=_F32)
     ws = _ws(_lib.size("ds2_bn_workspace_size", outer, c, d * t), x.device)
     _lib.call("ds2_bn_backward", dy.data_ptr(), dy_layout, x.data_ptr(), outer, c, d, t,
               mean.data_ptr(), invstd.data_ptr(), gamma.data_ptr(), beta.data_ptr(), int(masked),
@@ -295,6 +321,7 @@ class ConvBlockFn(torch.autograd.Function):
                   invstd.data_ptr(), gamma.data_ptr(), beta.data_ptr(), _p(lens), float(lo),
                   float(hi), y.data_ptr(), int(out_layout), _stream())
         ctx.save_for_backward(x, z, lens, weight, gamma, beta, mean, invstd)
+        ctx.bias = bias   # only its identity (gradient slot) is used in backward
         ctx.cfg = (stride, padding, lo, hi, out_layout, bias is not None, training)
         return y
 
@@ -308,11 +335,12 @@ class ConvBlockFn(torch.autograd.Function):
         n, c, d, t = z.shape
         dz, dgamma, dbeta, dbias = bn_backward(dy, out_layout, z, n, c, d, t, mean, invstd, gamma,
                                                beta, masked=True, lens=lens, lo=lo, hi=hi,
-                                               want_dbias=has_bias)
+                                               want_dbias=has_bias, bias=ctx.bias)
         dx = None
         if ctx.needs_input_grad[0]:
             dx = conv2d_dgrad(dz, weight, x.shape, stride, padding)
-        dw, _ = conv2d_wgrad(dz, x, weight.shape, stride, padding, with_bias=False)
+        dw, _ = conv2d_wgrad(dz, x, weight.shape, stride, padding, with_bias=False,
+                             out_dw=grad_like(weight))
         return (dx, None, dw, dbias, dgamma, dbeta) + (None,) * 10
 
 
@@ -359,7 +387,7 @@ class LinearFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x2d)
             sgemm(dy, weight, dx, m=m, n=k, k=n, lda=n, ldb=k, ldc=k)
-        dw = torch.empty_like(weight)
+        dw = grad_like(weight)
         sgemm(dy, x2d, dw, m=n, n=k, k=m, trans_a=True, lda=n, ldb=k, ldc=k)
         return dx, dw
 
@@ -401,12 +429,12 @@ def _rnn_param_grads(x, h_all, dgx, dgh, weights, nd, g, need_dx):
     dx = torch.empty(t, n, inp, device=dev, dtype=_F32) if need_dx else None
     for d in range(nd):
         w_ih, w_hh, b_ih, b_hh = weights[4 * d: 4 * d + 4]
-        dw_ih = torch.empty_like(w_ih)
+        dw_ih = grad_like(w_ih)
         sgemm(dgx, x2d, dw_ih, m=g, n=inp, k=tn, trans_a=True, lda=ld, ldb=inp, ldc=inp,
               a_off=d * g)
-        db_ih = torch.empty_like(b_ih)
+        db_ih = grad_like(b_ih)
         colsum(dgx, tn, g, ld, db_ih, off=d * g)
-        dw_hh = torch.empty_like(w_hh)
+        dw_hh = grad_like(w_hh)
         if t > 1:
             # sum_t dgh_t^T h_{t-1} (fwd) / h_{t+1} (rev); h_prev = 0 at the start
             a_off = (n * ld if d == 0 else 0) + d * g
@@ -415,10 +443,10 @@ def _rnn_param_grads(x, h_all, dgx, dgh, weights, nd, g, need_dx):
                   ldb=nd * h, ldc=h, a_off=a_off, b_off=b_off)
         else:
             dw_hh.zero_()
+        db_hh = grad_like(b_hh)
         if dgh is dgx:
-            db_hh = db_ih.clone()
+            db_hh.copy_(db_ih)
         else:
-            db_hh = torch.empty_like(b_hh)
             colsum(dgh, tn, g, ld, db_hh, off=d * g)
         if dx is not None:
             sgemm(dgx, w_ih, dx, m=tn, n=inp, k=g, lda=ld, ldb=inp, ldc=inp,
@@ -552,7 +580,7 @@ class LookaheadFn(torch.autograd.Function):
         lo, hi = ctx.clamp if ctx.clamp is not None else (0.0, 0.0)
         dy = dy.contiguous()
         dx = torch.empty_like(x) if ctx.needs_input_grad[0] else None
-        dw = torch.empty_like(w) if ctx.needs_input_grad[1] else None
+        dw = grad_like(w) if ctx.needs_input_grad[1] else None
         ws = _ws(_lib.size("ds2_lookahead_bwd_workspace_size", t, n, h, context), x.device)
         _lib.call("ds2_lookahead_bwd", dy.data_ptr(), _p(y), lo, hi, x.data_ptr(), t, n, h,
                   w.data_ptr(), context, _p(dx), _p(dw), ws.data_ptr(), ws.numel(), _stream())

@@ -21,7 +21,7 @@ import torch
 import torch.distributed as dist
 
 from . import _lib
-from .ops import _stream, _p
+from .ops import _stream, _p, register_grad_slot
 
 
 class FlatParams:
@@ -45,9 +45,33 @@ class FlatParams:
             self.flat[o:o + n].copy_(p.data.reshape(-1))
             p.data = self.flat[o:o + n].view_as(p)
             p.grad = self.grad[o:o + n].view_as(p)
+            register_grad_slot(p, self.grad, o)
 
     def zero_grad(self):
-        self.grad.zero_()
+        """set_to_none semantics (torch's default): the next backward writes every
+        parameter gradient straight into its slice (ops.grad_like) and autograd adopts
+        the view, so no memset and no accumulate kernels.  finalize_grads() zeroes the
+        slices of parameters that received no gradient."""
+        for p in self.params:
+            p.grad = None
+
+    def adopt(self, p, o):
+        """Make p.grad the view of its slice: zero it when no gradient arrived, copy a
+        gradient that some other op (not ops.grad_like) produced elsewhere."""
+        n = p.numel()
+        slot = self.grad[o:o + n]
+        g = p.grad
+        if g is None:
+            slot.zero_()
+        elif g.data_ptr() != slot.data_ptr():
+            slot.copy_(g.reshape(-1))
+        else:
+            return
+        p.grad = slot.view_as(p)
+
+    def finalize_grads(self):
+        for p, o in zip(self.params, self.offsets):
+            self.adopt(p, o)
 
     def slices(self):
         for p, o in zip(self.params, self.offsets):
@@ -77,11 +101,13 @@ class FusedSGD:
 
     def grad_norm(self) -> torch.Tensor:
         """Global L2 norm of the gradients, on the device (no host sync)."""
+        self.flat.finalize_grads()
         _lib.call("ds2_grad_norm", self.flat.grad.data_ptr(), self.flat.numel, self.norm.data_ptr(),
                   self.ws.data_ptr(), self.ws.numel(), _stream())
         return self.norm
 
     def step(self, skip_flag: Optional[torch.Tensor] = None):
+        self.flat.finalize_grads()
         norm_ptr = None
         if self.max_norm > 0:
             self.grad_norm()
@@ -121,6 +147,7 @@ class GradAllReducer:
         self.param_bucket = {}
         start, members = 0, []
         plist = list(flat.slices())
+        self.param_offset = {id(p): o for p, o, _ in plist}
         for i, (p, o, n) in enumerate(plist):
             members.append(p)
             nxt = plist[i + 1][1] if i + 1 < len(plist) else flat.numel
@@ -147,6 +174,7 @@ class GradAllReducer:
         self.handles = [None] * len(self.buckets)
 
     def _on_ready(self, p):
+        self.flat.adopt(p, self.param_offset[id(p)])
         b = self.param_bucket[id(p)]
         self.pending[b] -= 1
         if self.pending[b] == 0:
@@ -157,6 +185,7 @@ class GradAllReducer:
     def finish(self):
         if not self._hooks:
             return
+        self.flat.finalize_grads()   # zero the slices no gradient was written to
         for b, h in enumerate(self.handles):
             if h is None:     # a bucket whose params received no gradient this step
                 s, e, _ = self.buckets[b]

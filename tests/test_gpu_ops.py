@@ -394,12 +394,16 @@ def test_lookahead(dev, t, n, h, context, fused):
 
 
 # ---------------------------------------------------------------------------- CTC
-def test_ctc_vs_torch(dev):
+@pytest.mark.parametrize("t,act,lab", [
+    (60, [60, 55, 40, 12, 30, 5], [20, 1, 0, 5, 14, 2]),
+    # several 32-step log-prob chunks of the scan; lengths on and next to chunk edges
+    (160, [160, 128, 97, 64, 33, 32], [70, 40, 30, 20, 10, 31])])
+def test_ctc_vs_torch(dev, t, act, lab):
     g = torch.Generator().manual_seed(9)
-    t, n, c = 60, 6, 30
+    n, c = 6, 30
     acts = torch.randn(t, n, c, generator=g) * 3
-    act_lens = torch.tensor([60, 55, 40, 12, 30, 5], dtype=torch.int32)
-    label_lens = torch.tensor([20, 1, 0, 5, 14, 2], dtype=torch.int32)
+    act_lens = torch.tensor(act, dtype=torch.int32)
+    label_lens = torch.tensor(lab, dtype=torch.int32)
     labels = torch.randint(1, c, (int(label_lens.sum()),), generator=g, dtype=torch.int32)
     labels[3:6] = 7                       # repeats inside sample 0
     loss_ref, grad_ref = orc.ctc_loss(acts.double(), labels, act_lens, label_lens)
@@ -408,8 +412,9 @@ def test_ctc_vs_torch(dev):
                                     label_lens.to(dev), int(label_lens.max()))
     _close(costs, costs_ref, 1e-5, "ctc costs")
     # alpha/beta live in fp32 log space (warp-ctc's arithmetic class): |alpha| ~ nll ~ 1e2
-    # carries ~1e-5 absolute rounding into exp(alpha + beta + nll); grads are O(1).
-    _close(grads, grad_ref, 2e-4, "ctc grads")
+    # (~5e2 for the 160-step case) carries ~1e-5 (~5e-5) absolute rounding into
+    # exp(alpha + beta + nll); grads are O(1).
+    _close(grads, grad_ref, 2e-4 if t <= 64 else 5e-4, "ctc grads")
 
 
 def test_ctc_infeasible_and_module(dev):
@@ -515,8 +520,9 @@ def test_fused_sgd_matches_torch(dev):
         torch.nn.utils.clip_grad_norm_(ref, 1.0)
         opt.step()
         fopt.zero_grad()
+        assert all(p.grad is None for p in mine)      # set_to_none, like torch
         for p, gr in zip(mine, grads):
-            p.grad.copy_(gr.to(dev))
+            p.grad = gr.to(dev)                       # adopted into the flat buffer by step()
         fopt.step()
         for p, r in zip(mine, ref):
             _close(p, r, 1e-6, f"sgd step {step}")
