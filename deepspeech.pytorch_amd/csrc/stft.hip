@@ -17,6 +17,7 @@ namespace ds2 {
 
 constexpr int SF = 8;          // frames per workgroup
 constexpr int SMAXN = 1024;    // max n_fft
+constexpr int kMaskInts = 9;   // per utterance: f_lo0 f_hi0 f_lo1 f_hi1 t_lo0 t_hi0 t_lo1 t_hi1 f_cut
 
 __device__ __forceinline__ int reflect_idx(int i, int n) {
   // numpy 'reflect' (edge sample not repeated); assumes n > 1
@@ -40,7 +41,8 @@ __global__ __launch_bounds__(256) void stft_kernel(const float* __restrict__ pcm
                                                    int max_samples, int n_fft, int hop,
                                                    const double* __restrict__ window,
                                                    int normalize, float* __restrict__ out,
-                                                   int max_frames, float* __restrict__ frame_mean) {
+                                                   int max_frames, float* __restrict__ frame_mean,
+                                                   const int* __restrict__ masks) {
   __shared__ double cs[SMAXN], sn[SMAXN];
   __shared__ double fr[SF][SMAXN];
   __shared__ double red[SF][4];
@@ -67,6 +69,20 @@ __global__ __launch_bounds__(256) void stft_kernel(const float* __restrict__ pcm
   }
   __syncthreads();
   const int k = threadIdx.x;
+  // spectrogram augmentation masks of this utterance (kMaskInts per utterance, see the
+  // entry point): frequency bands, time bands and the 8 kHz cut, applied to |D| before
+  // the log like data_loader_aug.py:236-248 does
+  int fm[4] = {0, 0, 0, 0}, tm[4] = {0, 0, 0, 0}, fcut = F;
+  if (masks != nullptr) {
+    const int* mk = masks + b * kMaskInts;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      fm[i] = mk[i];
+      tm[i] = mk[4 + i];
+    }
+    fcut = mk[8];
+  }
+  const bool fmasked = (k >= fm[0] && k < fm[1]) || (k >= fm[2] && k < fm[3]) || k >= fcut;
   double lsum[SF];
 #pragma unroll
   for (int f = 0; f < SF; ++f) lsum[f] = 0.0;
@@ -92,7 +108,10 @@ __global__ __launch_bounds__(256) void stft_kernel(const float* __restrict__ pcm
       if (t >= max_frames) continue;
       float val = 0.f;
       if (t < T) {
-        const float mag = hypotf(static_cast<float>(re[f]), static_cast<float>(im[f]));
+        const bool masked =
+            fmasked || (t >= tm[0] && t < tm[1]) || (t >= tm[2] && t < tm[3]);
+        const float mag =
+            masked ? 0.f : hypotf(static_cast<float>(re[f]), static_cast<float>(im[f]));
         val = normalize ? log1pf(mag * 1048576.0f) : log1pf(mag);
         lsum[f] = val;
       }
@@ -163,10 +182,11 @@ size_t ds2_stft_workspace_size(int batch, int max_frames) {
   return (size_t)batch * max_frames * sizeof(float) + (size_t)batch * sizeof(float) + 512;
 }
 
-ds2_status_t ds2_stft_logmag(const float* pcm, const int* n_samples, int batch, int max_samples,
-                             int n_fft, int hop, const double* window, int normalize,
-                             const float* gauss_taps, int gauss_radius, float* out,
-                             int max_frames, void* ws, size_t ws_bytes, ds2_stream_t stream) {
+ds2_status_t ds2_stft_logmag_masked(const float* pcm, const int* n_samples, int batch,
+                                    int max_samples, int n_fft, int hop, const double* window,
+                                    int normalize, const float* gauss_taps, int gauss_radius,
+                                    const int* masks, float* out, int max_frames, void* ws,
+                                    size_t ws_bytes, ds2_stream_t stream) {
   if (batch < 0 || n_fft < 2 || n_fft > SMAXN || hop < 1 || max_frames < 1) return DS2_INVALID_VALUE;
   if (n_fft / 2 + 1 > 256) return DS2_UNSUPPORTED_SHAPE;
   if (normalize == 1 && (gauss_taps == nullptr || gauss_radius < 0)) return DS2_INVALID_VALUE;
@@ -179,7 +199,7 @@ ds2_status_t ds2_stft_logmag(const float* pcm, const int* n_samples, int batch, 
   const int F = n_fft / 2 + 1;
   hipLaunchKernelGGL(stft_kernel, dim3(cdiv(max_frames, SF), batch), dim3(256), 0, st, pcm,
                      n_samples, max_samples, n_fft, hop, window, normalize, out, max_frames,
-                     frame_mean);
+                     frame_mean, masks);
   if (normalize == 1) {
     hipLaunchKernelGGL(maxframe_offset_kernel, dim3(batch), dim3(256), 0, st, n_samples, hop,
                        max_frames, frame_mean, gauss_taps, gauss_radius, offset);
@@ -189,6 +209,15 @@ ds2_status_t ds2_stft_logmag(const float* pcm, const int* n_samples, int batch, 
                        max_frames, offset, out);
   }
   return launch_status("ds2_stft_logmag");
+}
+
+ds2_status_t ds2_stft_logmag(const float* pcm, const int* n_samples, int batch, int max_samples,
+                             int n_fft, int hop, const double* window, int normalize,
+                             const float* gauss_taps, int gauss_radius, float* out,
+                             int max_frames, void* ws, size_t ws_bytes, ds2_stream_t stream) {
+  return ds2_stft_logmag_masked(pcm, n_samples, batch, max_samples, n_fft, hop, window,
+                                normalize, gauss_taps, gauss_radius, nullptr, out, max_frames, ws,
+                                ws_bytes, stream);
 }
 
 }  // extern "C"

@@ -28,6 +28,8 @@ _PROTOS = {
     "ds2_stft_workspace_size": (_sz, [_c_int, _c_int]),
     "ds2_stft_logmag": (_c_int, [_vp, _vp, _c_int, _c_int, _c_int, _c_int, _vp, _c_int, _vp,
                                  _c_int, _vp, _c_int, _vp, _sz, _vp]),
+    "ds2_stft_logmag_masked": (_c_int, [_vp, _vp, _c_int, _c_int, _c_int, _c_int, _vp, _c_int,
+                                        _vp, _c_int, _vp, _vp, _c_int, _vp, _sz, _vp]),
     "ds2_sgemm": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _c_f, _vp, _c_i64, _c_i64,
                            _vp, _c_i64, _c_i64, _c_f, _vp, _c_i64, _c_i64, _c_int, _vp, _vp]),
     "ds2_sgemm_workspace_size": (_sz, [_c_int, _c_int, _c_int, _c_int]),

@@ -21,6 +21,7 @@ from torch.utils.data import DataLoader
 from torch.utils.data.sampler import Sampler
 
 from . import ops
+from .spect_aug import SpectAugmenter
 
 
 def hamming(n: int) -> np.ndarray:
@@ -81,6 +82,9 @@ class SpectrogramParser(object):
         self.cache_path = cache_path
         self.device = torch.device(device) if device is not None else torch.device('cuda')
         self._cache = {}
+        # spectrogram augmentations (data_loader_aug.py:241-248), drawn on the host and
+        # applied inside the STFT kernel; inactive unless audio_conf enables them
+        self.spect_aug = SpectAugmenter(audio_conf)
 
     def _consts(self, sample_rate):
         key = sample_rate
@@ -112,7 +116,9 @@ class SpectrogramParser(object):
         pcm_d = torch.from_numpy(pcm).to(self.device)
         ns_d = torch.tensor(lens, dtype=torch.int32).to(self.device)
         frames = [1 + n // hop for n in lens]
-        out = ops.stft_logmag(pcm_d, ns_d, n_fft, hop, win, self._mode(), taps, max(frames))
+        masks = self.spect_aug.masks(n_fft // 2 + 1, frames, self.device)
+        out = ops.stft_logmag(pcm_d, ns_d, n_fft, hop, win, self._mode(), taps, max(frames),
+                              masks=masks)
         if self.augment and self.normalize == 'max_frame':
             # one U(-0.5, 0.5) offset per utterance on its valid frames (data_loader_aug.py:213-214)
             off = (torch.rand(len(signals)) - 0.5).to(self.device)

@@ -283,7 +283,8 @@ def ctc_beam_decode_raw(probs: torch.Tensor, sizes: Optional[torch.Tensor], beam
 
 def stft_logmag(pcm: torch.Tensor, n_samples: torch.Tensor, n_fft: int, hop: int,
                 window: torch.Tensor, normalize: int, gauss_taps: Optional[torch.Tensor],
-                max_frames: int) -> torch.Tensor:
+                max_frames: int, masks: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """masks: None or int32 [batch, 9] spectrogram-augmentation bands (ds2hip.h)."""
     pcm = _need(pcm, "stft.pcm")
     n_samples = _need(n_samples, "stft.n_samples", _I32)
     window = _need(window, "stft.window", torch.float64)
@@ -292,9 +293,13 @@ def stft_logmag(pcm: torch.Tensor, n_samples: torch.Tensor, n_fft: int, hop: int
     out = torch.empty(b, f, max_frames, device=pcm.device, dtype=_F32)
     ws = _ws(_lib.size("ds2_stft_workspace_size", b, max_frames), pcm.device)
     radius = 0 if gauss_taps is None else (gauss_taps.numel() - 1) // 2
-    _lib.call("ds2_stft_logmag", pcm.data_ptr(), n_samples.data_ptr(), b, max_samples, n_fft, hop,
-              window.data_ptr(), int(normalize), _p(gauss_taps), radius, out.data_ptr(),
-              max_frames, ws.data_ptr(), ws.numel(), _stream())
+    if masks is not None:
+        masks = _need(masks, "stft.masks", _I32)
+        if tuple(masks.shape) != (b, 9):
+            raise _lib.Ds2Error(f"stft masks must be [batch, 9], got {tuple(masks.shape)}")
+    _lib.call("ds2_stft_logmag_masked", pcm.data_ptr(), n_samples.data_ptr(), b, max_samples,
+              n_fft, hop, window.data_ptr(), int(normalize), _p(gauss_taps), radius, _p(masks),
+              out.data_ptr(), max_frames, ws.data_ptr(), ws.numel(), _stream())
     return out
 
 

@@ -54,9 +54,21 @@ ds2_status_t ds2_stft_logmag(const float* pcm, const int* n_samples, int batch, 
                              const float* gauss_taps, int gauss_radius,
                              float* out, int max_frames, void* ws, size_t ws_bytes,
                              ds2_stream_t stream);
+/* The same with the spectrogram augmentations of data/data_loader_aug.py:236-248
+ * (FrequencyMask / TimeMask via SOneOf, data/spectrogram_aug.py:64-117, and the
+ * aug_prob_8khz cut) applied to |X| before the log, as the reference does.  masks: NULL
+ * or [batch][9] int32 = {f_lo0, f_hi0, f_lo1, f_hi1, t_lo0, t_hi0, t_lo1, t_hi1, f_cut}:
+ * bins in [f_lo, f_hi), frames in [t_lo, t_hi) and bins >= f_cut are zeroed (empty when
+ * lo >= hi; f_cut = n_fft/2+1 for none).  The random draws stay on the host
+ * (ds2amd/spect_aug.py) so they follow the reference's `random` call sequence. */
+ds2_status_t ds2_stft_logmag_masked(const float* pcm, const int* n_samples, int batch,
+                                    int max_samples, int n_fft, int hop, const double* window,
+                                    int normalize, const float* gauss_taps, int gauss_radius,
+                                    const int* masks, float* out, int max_frames, void* ws,
+                                    size_t ws_bytes, ds2_stream_t stream);
 
 /* ------------------------------------------------------------------------ */
-/* Dense fp32 GEMM on MFMA (v_mfma_f32_32x32x2_f32), strided-batched, row-major.
+/* Dense fp32 GEMM on MFMA (v_mfma_f32_16x16x4_f32 / 32x32x2_f32), strided-batched, row-major.
  * C[b] = alpha * op(A[b]) @ op(B[b]) + beta * C[b] (+ bias[n] if bias != NULL)
  * trans_a = 0: A is [m][lda];  1: A is stored [k][lda] (A^T)
  * trans_b = 0: B is [k][ldb];  1: B is stored [n][ldb] (B^T)

@@ -502,6 +502,31 @@ def test_stft_vs_oracle(dev, golden_dir):
                                atol=2e-4, rtol=0)
 
 
+def test_stft_spect_aug_masks_vs_oracle(dev):
+    """Frequency / time bands and the 8 kHz cut zero |X| before the log and the
+    'max_frame' normalisation (data_loader_aug.py:236-248): device kernel vs the oracle
+    spectrogram with the same bands applied to its magnitude."""
+    import random
+    from ds2amd.data_loader import SpectrogramParser
+    from ds2amd.spect_aug import apply_masks_np
+    conf = dict(sample_rate=16000, window_size=0.02, window_stride=0.01, window='hamming',
+                noise_prob=1.0, aug_prob_spect=1.0, aug_prob_8khz=0.5)
+    parser = SpectrogramParser(conf, normalize='max_frame', device=dev)
+    parser.spect_aug.rng = random.Random(3)
+    rng = np.random.default_rng(1)
+    wavs = [(rng.standard_normal(n) * 0.3).astype(np.float32) for n in (23456, 16000, 8000, 31999)]
+    replay = SpectrogramParser(conf, normalize='max_frame', device=dev).spect_aug
+    replay.rng = random.Random(3)
+    out, frames = parser.parse_batch(wavs)
+    for i, y in enumerate(wavs):
+        row = replay.draw_one(161, int(frames[i]))
+        mag = orc.stft_magnitude(y)
+        ref = orc.normalize_max_frame(apply_masks_np(mag, row))
+        got = out[i, 0, :, :ref.shape[1]].cpu()
+        err = (got - ref).abs().max().item()
+        assert err < 2e-4, f"wav {i} row {row}: max abs err {err}"
+
+
 # ---------------------------------------------------------------------------- optimizer
 def test_fused_sgd_matches_torch(dev):
     from ds2amd.optim import FlatParams, FusedSGD

@@ -242,3 +242,45 @@ def test_reference_package_round_trip(golden_dir, tmp_path):
     torch.save(ours, out)
     m2 = dsm.DeepSpeech.load_model(str(out))
     assert all(torch.equal(m2.state_dict()[n], v) for n, v in m.state_dict().items())
+
+
+# ------------------------------------------------------------------ spectrogram augmentations
+def test_spect_aug_draws_follow_reference_semantics():
+    """ds2amd.spect_aug draws bands exactly as data/spectrogram_aug.py would zero them,
+    call for call on a seeded random.Random (restated; the reference module needs cv2,
+    absent here, so the draw order is pinned by the code it restates, not by a run)."""
+    import random
+    from ds2amd.spect_aug import SpectAugmenter, apply_masks_np
+    conf = dict(noise_prob=1.0, aug_prob_spect=0.5, aug_prob_8khz=0.5)
+    a = SpectAugmenter(conf, rng=random.Random(7))
+    # hand replay of the same sequence on a second generator
+    r = random.Random(7)
+    rows = [a.draw_one(161, 300) for _ in range(6)]
+    probs = {"freq": 0.5, "time": 0.5}
+    for row in rows:
+        assert r.random() < 1.0                       # SOneOf(prob = noise_prob = 1)
+        kind = r.choice(["freq", "time"])
+        probs[kind] = 1.0                             # reference side effect: t.prob = 1
+        exp = [0, 0, 0, 0, 0, 0, 0, 0, 161]
+        bands = []
+        for _ in range(2):
+            if r.random() < probs[kind]:
+                if kind == "freq":
+                    w = r.randint(0, 20)
+                    c = r.randint(0, 161)
+                    bands.append((max(0, int(c - w // 2)), min(int(c + w // 2), 161)))
+                else:
+                    w = min(r.randint(0, 50), int(.15 * 300))
+                    c = r.randint(0, 300)
+                    bands.append((max(0, int(c - w // 2)), min(int(c + w // 2), 300)))
+        base = 0 if kind == "freq" else 4
+        for i, (lo, hi) in enumerate(bands):
+            exp[base + 2 * i], exp[base + 2 * i + 1] = lo, hi
+        if r.random() < 0.5:
+            exp[8] = 81
+        assert row == exp
+    # numpy application = the reference's slicing
+    s = np.ones((161, 300), np.float32)
+    apply_masks_np(s, [10, 20, 150, 140, 5, 7, 0, 0, 81])
+    assert s[10:20].sum() == 0 and s[81:].sum() == 0 and s[:, 5:7].sum() == 0
+    assert s[0:10, 7:].min() == 1 and s[20:81, 7:].min() == 1      # reversed band is empty
