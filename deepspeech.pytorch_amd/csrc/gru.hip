@@ -417,7 +417,11 @@ __global__ __launch_bounds__(GT) void gru_fwd_persist_kernel(
 // the workgroup with a barrier (MI355X_MICROARCH.md "Valid forms" row 1).  A slot is
 // rewritten two steps later, after every consumer of the group has published the step
 // in between, i.e. after all its loads of the slot have returned.
-template <int NBW>
+//
+// SENT = true: sentinel-ring hand-off (rnn_common.h, kRingSlots slots, no flags): every
+// wave spins on its own producers' tiles, so the wait, the poll round trip and the
+// producer's drain-before-flag all leave the critical path.
+template <int NBW, bool SENT>
 __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void gru_fwd_dop_kernel(
     int T, int N, int H, int D, int UB, int BT, const float* __restrict__ xproj,
     const float* __restrict__ w_f, const float* __restrict__ w_r, const float* __restrict__ b_f,
@@ -438,9 +442,15 @@ __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   const unsigned* gflags = counters + (D * BT + 1) + (d * BT + bt) * UB;
   unsigned* myflag = counters + (D * BT + 1) + (d * BT + bt) * UB + ub;
   const int slot_floats = D * BT * UB * 256;
+  constexpr int NSLOT = SENT ? kRingSlots : 2;
   const __amdgpu_buffer_rsrc_t x_rs =
-      __builtin_amdgcn_make_buffer_rsrc(hx, (short)0, 2 * slot_floats * 4, 0x00020000);
+      __builtin_amdgcn_make_buffer_rsrc(hx, (short)0, NSLOT * slot_floats * 4, 0x00020000);
   const int grp_off = (d * BT + bt) * UB * 256;            // this group's tiles in a slot
+  __shared__ int failed;
+  if (SENT) {
+    if (threadIdx.x == 0) failed = 0;
+    __syncthreads();
+  }
   const bool tracing = stamps != nullptr && threadIdx.x == 0;
   auto trace_at = [&](int s, int p) {
     if (tracing && s >= kTraceS0 && s < kTraceS0 + kTraceSteps)
@@ -493,12 +503,12 @@ __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     for (int g = 0; g < 3; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
     trace_at(s, 0);
     if (s > 0) {
-      if (!flags_wait(gflags, UB, (unsigned)s, err, &flag)) {
+      if (!SENT && !flags_wait(gflags, UB, (unsigned)s, err, &flag)) {
         poison_rest(h_all, s, T, d != 0, N, D, n, d, H, j, H, 1, owner);
         return;
       }
       trace_at(s, 1);
-      const int base = (((s - 1) & 1) * slot_floats + grp_off + b0 * 256 + lane * 4) * 4;
+      const int base = (((s - 1) % NSLOT) * slot_floats + grp_off + b0 * 256 + lane * 4) * 4;
       f32x4 hv[NBW];
 #pragma unroll
       for (int i = 0; i < NBW; ++i) {
@@ -509,13 +519,16 @@ __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
       // interleave them with the MFMAs and expose one load latency per block)
       asm volatile("" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
+      // SENT: MFMAs start on the first tile; a wave spins on one tile at a time (spin_tile)
 #pragma unroll
-      for (int i = 0; i < NBW; ++i)
+      for (int i = 0; i < NBW; ++i) {
+        if (SENT && i < nb && !spin_tile(hv[i], x_rs, base + i * 1024, err)) failed = 1;
 #pragma unroll
         for (int c = 0; c < 4; ++c)
 #pragma unroll
           for (int g = 0; g < 3; ++g)
             acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(hv[i][c], w[g][i][c], acc[g], 0, 0, 0);
+      }
       trace_at(s, 2);
     }
 #pragma unroll
@@ -524,6 +537,10 @@ __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
       for (int r = 0; r < 4; ++r)
         red[(wave * GB + (lane >> 4) * 4 + r) * RP + g * GU + (lane & 15)] = acc[g][r];
     __syncthreads();
+    if (SENT && failed) {
+      poison_rest(h_all, s, T, d != 0, N, D, n, d, H, j, H, 1, owner);
+      return;
+    }
     trace_at(s, 3);
     if (threadIdx.x < GB * GU) {
       float hout = 0.f;
@@ -556,12 +573,21 @@ __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     __syncthreads();
     // publish: wave 0 stores the tile (one 16-B sc1 store per lane), drains, flags
     if (wave == 0) {
-      const u32x4 v = *reinterpret_cast<const u32x4*>(tile + lane * 4);
-      __builtin_amdgcn_raw_buffer_store_b128(v, x_rs, ((s & 1) * slot_floats + grp_off +
-                                                       ub * 256 + lane * 4) * 4, 0, kSc1);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (lane == 0)
-        __hip_atomic_store(myflag, (unsigned)s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int toff = (grp_off + ub * 256 + lane * 4) * 4;
+      if (SENT) {
+        const u32x4 v = desentinel(*reinterpret_cast<const u32x4*>(tile + lane * 4));
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // last step's sentinel store first
+        __builtin_amdgcn_raw_buffer_store_b128(v, x_rs, (s % NSLOT) * slot_floats * 4 + toff, 0, kSc1);
+        const u32x4 sv = u32x4{kSentinel, kSentinel, kSentinel, kSentinel};
+        __builtin_amdgcn_raw_buffer_store_b128(sv, x_rs, ((s + 2) % NSLOT) * slot_floats * 4 + toff,
+                                               0, kSc1);
+      } else {
+        const u32x4 v = *reinterpret_cast<const u32x4*>(tile + lane * 4);
+        __builtin_amdgcn_raw_buffer_store_b128(v, x_rs, (s & 1) * slot_floats * 4 + toff, 0, kSc1);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0)
+          __hip_atomic_store(myflag, (unsigned)s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
     trace_at(s, 4);
     // outputs consumed only by later kernels, off the critical path
@@ -722,7 +748,8 @@ __global__ __launch_bounds__(GT) void gru_bwd_persist_kernel(
 //   gx[slot][d][bt][3 UB blocks][q][r][c],
 // whose block order is the k order of dgh; wave w owns blocks [b0, b0 + nb) of the 3 UB.
 // dgh (for the weight-gradient GEMM) and dgx are stored after the flag.
-template <int NBW>
+// SENT selects the sentinel-ring hand-off as in gru_fwd_dop_kernel.
+template <int NBW, bool SENT>
 __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void gru_bwd_dop_kernel(
     int T, int N, int H, int D, int UB, int BT, const float* __restrict__ dy, int dyd,
     const float* __restrict__ w_f, const float* __restrict__ w_r,
@@ -746,9 +773,15 @@ __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   const unsigned* gflags = counters + (D * BT + 1) + (d * BT + bt) * UB;
   unsigned* myflag = counters + (D * BT + 1) + (d * BT + bt) * UB + ub;
   const int slot_floats = D * BT * NB3 * 256;
+  constexpr int NSLOT = SENT ? kRingSlots : 2;
   const __amdgpu_buffer_rsrc_t x_rs =
-      __builtin_amdgcn_make_buffer_rsrc(gx, (short)0, 2 * slot_floats * 4, 0x00020000);
+      __builtin_amdgcn_make_buffer_rsrc(gx, (short)0, NSLOT * slot_floats * 4, 0x00020000);
   const int grp_off = (d * BT + bt) * NB3 * 256;
+  __shared__ int failed;
+  if (SENT) {
+    if (threadIdx.x == 0) failed = 0;
+    __syncthreads();
+  }
   const bool tracing = stamps != nullptr && threadIdx.x == 0;
   auto trace_at = [&](int s, int p) {
     if (tracing && s >= kTraceS0 && s < kTraceS0 + kTraceSteps)
@@ -794,12 +827,12 @@ __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
       if (tp >= 0 && tp < T) hp = h_all[(((int64_t)tp * N + n) * D + d) * H + j];
     }
     if (s > 0) {
-      if (!flags_wait(gflags, UB, (unsigned)s, err, &flag)) {
+      if (!SENT && !flags_wait(gflags, UB, (unsigned)s, err, &flag)) {
         poison_rest(dgx, s, T, d == 0, N, D, n, d, H, j, H3, 3, owner);
         return;
       }
       trace_at(s, 1);
-      const int base = (((s - 1) & 1) * slot_floats + grp_off + b0 * 256 + lane * 4) * 4;
+      const int base = (((s - 1) % NSLOT) * slot_floats + grp_off + b0 * 256 + lane * 4) * 4;
       f32x4 gv[NBW];
 #pragma unroll
       for (int i = 0; i < NBW; ++i) {
@@ -810,6 +843,7 @@ __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int i = 0; i < NBW; ++i) {
+        if (SENT && i < nb && !spin_tile(gv[i], x_rs, base + i * 1024, err)) failed = 1;
         acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(gv[i][0], w[i][0], acc0, 0, 0, 0);
         acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(gv[i][1], w[i][1], acc1, 0, 0, 0);
         acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(gv[i][2], w[i][2], acc0, 0, 0, 0);
@@ -821,6 +855,10 @@ __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     for (int r = 0; r < 4; ++r)
       red[(wave * GB + (lane >> 4) * 4 + r) * RP + (lane & 15)] = acc0[r] + acc1[r];
     __syncthreads();
+    if (SENT && failed) {
+      poison_rest(dgx, s, T, d == 0, N, D, n, d, H, j, H3, 3, owner);
+      return;
+    }
     trace_at(s, 3);
     if (threadIdx.x < GB * GU) {
       float dar = 0.f, daz = 0.f, dan = 0.f, dghn = 0.f;
@@ -851,15 +889,33 @@ __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     }
     __syncthreads();
     if (wave == 0) {
-      const int so = ((s & 1) * slot_floats + grp_off + ub * 256 + lane * 4) * 4;
+      const int toff = (grp_off + ub * 256 + lane * 4) * 4;
+      if (SENT) {
+        u32x4 v[3];
 #pragma unroll
-      for (int g = 0; g < 3; ++g) {
-        const u32x4 v = *reinterpret_cast<const u32x4*>(tile + g * GB * GU + lane * 4);
-        __builtin_amdgcn_raw_buffer_store_b128(v, x_rs, so + g * UB * 1024, 0, kSc1);
+        for (int g = 0; g < 3; ++g)
+          v[g] = desentinel(*reinterpret_cast<const u32x4*>(tile + g * GB * GU + lane * 4));
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // last step's sentinel stores first
+        const int so = (s % NSLOT) * slot_floats * 4 + toff;
+#pragma unroll
+        for (int g = 0; g < 3; ++g)
+          __builtin_amdgcn_raw_buffer_store_b128(v[g], x_rs, so + g * UB * 1024, 0, kSc1);
+        const u32x4 sv = u32x4{kSentinel, kSentinel, kSentinel, kSentinel};
+        const int sn = ((s + 2) % NSLOT) * slot_floats * 4 + toff;
+#pragma unroll
+        for (int g = 0; g < 3; ++g)
+          __builtin_amdgcn_raw_buffer_store_b128(sv, x_rs, sn + g * UB * 1024, 0, kSc1);
+      } else {
+        const int so = (s & 1) * slot_floats * 4 + toff;
+#pragma unroll
+        for (int g = 0; g < 3; ++g) {
+          const u32x4 v = *reinterpret_cast<const u32x4*>(tile + g * GB * GU + lane * 4);
+          __builtin_amdgcn_raw_buffer_store_b128(v, x_rs, so + g * UB * 1024, 0, kSc1);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0)
+          __hip_atomic_store(myflag, (unsigned)s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (lane == 0)
-        __hip_atomic_store(myflag, (unsigned)s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     trace_at(s, 4);
     if (owner) {
@@ -898,9 +954,21 @@ static inline int dop_enabled() {
 }
 constexpr unsigned kDopPadLds = 80 * 1024;
 // smallest instantiated blocks-per-wave >= need (extra blocks are predicated off)
+// hand-off form of the direct-operand kernels: sentinel ring or per-producer flags.
+// DS2_RNN_HANDOFF_FWD / _BWD (or DS2_RNN_HANDOFF for both) = "sentinel" | "flags";
+// defaults: sentinel forward, flags backward (the measured faster forms)
+static inline bool sentinel_mode(bool fwd) {
+  const char* e = getenv(fwd ? "DS2_RNN_HANDOFF_FWD" : "DS2_RNN_HANDOFF_BWD");
+  if (e == nullptr || e[0] == 0) e = getenv("DS2_RNN_HANDOFF");
+  if (e == nullptr || e[0] == 0) return fwd;
+  return e[0] == 's';
+}
 static const void* bwd_dop_fn(int need) {
-#define DS2_BDOP(K) \
-  if (need <= K) return reinterpret_cast<const void*>(gru_bwd_dop_kernel<K>);
+  const bool sent = sentinel_mode(false);
+#define DS2_BDOP(K)                                                                      \
+  if (need <= K)                                                                         \
+    return sent ? reinterpret_cast<const void*>(gru_bwd_dop_kernel<K, true>)             \
+                : reinterpret_cast<const void*>(gru_bwd_dop_kernel<K, false>);
   DS2_BDOP(1) DS2_BDOP(2) DS2_BDOP(3) DS2_BDOP(4) DS2_BDOP(6) DS2_BDOP(8) DS2_BDOP(10)
   DS2_BDOP(13) DS2_BDOP(16) DS2_BDOP(19) DS2_BDOP(22) DS2_BDOP(24)
 #undef DS2_BDOP
@@ -920,11 +988,16 @@ static inline unsigned long long* stamp_slots(unsigned* ctrs, int n, int num_dir
                                                align256(ctr_words(n, num_dirs) * sizeof(unsigned)));
 }
 
-// two-slot ring of 1-KB hand-off tiles for the direct-operand kernels (gates tiles per
-// unit block: 1 forward, 3 backward)
+// ring of 1-KB hand-off tiles for the direct-operand kernels (gates tiles per unit block:
+// 1 forward, 3 backward): 2 slots for the flag hand-off, kRingSlots for the sentinel one
 static inline size_t ring_bytes(int n, int h, int num_dirs, int tiles) {
   const size_t UB = (h + GU - 1) / GU, BT = (n + GB - 1) / GB;
-  return align256(2 * (size_t)num_dirs * BT * UB * tiles * 256 * sizeof(float));
+  return align256(kRingSlots * (size_t)num_dirs * BT * UB * tiles * 256 * sizeof(float));
+}
+// every ring word starts as the sentinel (slots 0 and 1 must; the rest for simplicity)
+static inline hipError_t ring_reset(float* ring, int n, int h, int num_dirs, int tiles,
+                                    hipStream_t st) {
+  return hipMemsetAsync(ring, 0xFF, ring_bytes(n, h, num_dirs, tiles), st);
 }
 
 size_t ds2_gru_fwd_workspace_size(int n, int h, int num_dirs) {
@@ -981,18 +1054,21 @@ ds2_status_t ds2_gru_fwd(int t_max, int n, int h, int num_dirs, const float* xpr
                                            align256(counter_bytes(n, num_dirs)));
     void* args[] = {&T_, &N_, &H_, &D_, &UB_, &BT_, &xproj, &w_hh_f, &w_hh_r, &b_hh_f,
                     &b_hh_r, &lens, &h_all, &gates, &ring, &ctrs, &err, &stamps};
+    const bool sent = sentinel_mode(true);
+    if (sent && ring_reset(ring, n, h, num_dirs, 1, st) != hipSuccess)
+      return launch_status("ds2_gru ring");
     const void* fn = nullptr;
+#define DS2_FDOP(K)                                                                  \
+  case K:                                                                            \
+    fn = sent ? reinterpret_cast<const void*>(gru_fwd_dop_kernel<K, true>)           \
+              : reinterpret_cast<const void*>(gru_fwd_dop_kernel<K, false>);         \
+    break;
     switch ((UB + GW - 1) / GW) {
-      case 1: fn = reinterpret_cast<const void*>(gru_fwd_dop_kernel<1>); break;
-      case 2: fn = reinterpret_cast<const void*>(gru_fwd_dop_kernel<2>); break;
-      case 3: fn = reinterpret_cast<const void*>(gru_fwd_dop_kernel<3>); break;
-      case 4: fn = reinterpret_cast<const void*>(gru_fwd_dop_kernel<4>); break;
-      case 5: fn = reinterpret_cast<const void*>(gru_fwd_dop_kernel<5>); break;
-      case 6: fn = reinterpret_cast<const void*>(gru_fwd_dop_kernel<6>); break;
-      case 7: fn = reinterpret_cast<const void*>(gru_fwd_dop_kernel<7>); break;
-      case 8: fn = reinterpret_cast<const void*>(gru_fwd_dop_kernel<8>); break;
+      DS2_FDOP(1) DS2_FDOP(2) DS2_FDOP(3) DS2_FDOP(4) DS2_FDOP(5) DS2_FDOP(6) DS2_FDOP(7)
+      DS2_FDOP(8)
       default: break;
     }
+#undef DS2_FDOP
     // the dynamic LDS keeps one workgroup per CU (every workgroup gets a whole CU's SIMDs)
     if (fn != nullptr &&
         hipLaunchCooperativeKernel(fn, dim3(grid), dim3(GT), args, kDopPadLds, st) == hipSuccess)
@@ -1087,6 +1163,8 @@ ds2_status_t ds2_gru_bwd(int t_max, int n, int h, int num_dirs, const float* dy,
                                            align256(counter_bytes(n, num_dirs)));
     void* args[] = {&T_, &N_, &H_, &D_, &UB_, &BT_, &dy, &DYD_, &w_hh_f, &w_hh_r, &h_all,
                     &gates, &lens, &dgates_x, &dgates_h, &ring, &ctrs, &err, &stamps};
+    if (sentinel_mode(false) && ring_reset(ring, n, h, num_dirs, 3, st) != hipSuccess)
+      return launch_status("ds2_gru ring");
     const void* fn = bwd_dop_fn((3 * UB + GW - 1) / GW);
     if (fn != nullptr &&
         hipLaunchCooperativeKernel(fn, dim3(grid), dim3(GT), args, kDopPadLds, st) == hipSuccess)

@@ -218,6 +218,51 @@ __device__ __forceinline__ void group_arrive(unsigned* ctr) {
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 constexpr int kSc1 = 16;   // buffer-op aux bit: sc1 (write-through store / L1-bypassing load)
 
+// Sentinel-ring hand-off of the direct-operand kernels (the data is the flag; the R2 idea
+// of cdna_hip_programming.md G16 without widening the payload).  Each producer tile lives
+// in a ring of kRingSlots slots; a slot that will next hold step s + 2 is refilled with the
+// sentinel word at step s (once the producer has consumed every producer's step s - 1
+// tile, so every consumer has finished reading the slot's old step s - 2 contents).  The
+// producer drains vmcnt before each data store, so the sentinel of a slot is performed
+// before the tile a consumer must observe before it reads that slot again.  Consumers
+// spin with sc1 loads until none of their words is the sentinel.  Every word is written
+// whole by one 16-B sc1 store (R2: untorn).  A payload word equal to the sentinel (one
+// NaN bit pattern) is published as the canonical quiet NaN instead.
+constexpr unsigned kSentinel = 0xFFFFFFFFu;
+constexpr int kRingSlots = 4;
+
+__device__ __forceinline__ bool tile_ready(f32x4 v) {
+  const u32x4 b = __builtin_bit_cast(u32x4, v);
+  return (b.x != kSentinel) & (b.y != kSentinel) & (b.z != kSentinel) & (b.w != kSentinel);
+}
+
+__device__ __forceinline__ u32x4 desentinel(u32x4 v) {
+  const unsigned qnan = 0x7FC00000u;
+  return u32x4{v.x == kSentinel ? qnan : v.x, v.y == kSentinel ? qnan : v.y,
+               v.z == kSentinel ? qnan : v.z, v.w == kSentinel ? qnan : v.w};
+}
+
+// wave-uniform "every lane's tile words are ready"
+__device__ __forceinline__ bool wave_ready(f32x4 v) { return __ballot(!tile_ready(v)) == 0ull; }
+
+// Spin until the wave's ring tile at byte offset off (already loaded into v once) holds no
+// sentinel word, re-loading it alone; false (and the error word set) after kSpinLimit polls.
+// The wave's later tiles stay in flight meanwhile.
+__device__ __forceinline__ bool spin_tile(f32x4& v, __amdgpu_buffer_rsrc_t rs, int off,
+                                          unsigned* err) {
+  for (unsigned spins = 0; !wave_ready(v); ++spins) {
+    if (spins > kSpinLimit) {
+      if ((threadIdx.x & 63) == 0)
+        __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+    asm volatile("" ::: "memory");   // the re-load is not loop-invariant (no LICM)
+    v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, kSc1));
+  }
+  return true;
+}
+
 // Stage rows [n0, n0+16) x [0, cols) of a row-major slab (row stride ld floats, N
 // valid rows, `width` valid columns) into hs[m][pitch] with 16-byte sc1 buffer loads.
 // Rows >= N and columns >= width read as zero (out-of-range buffer offsets return

@@ -1,6 +1,7 @@
 """A/B timing of the GRU recurrence variants at the bench shape (T=501, N=32, H=800,
-bidirectional): LDS-staged vs direct-operand kernels and their polling forms, selected
-through the environment switches the library reads at every call."""
+bidirectional): direct-operand kernels with the flag or the sentinel-ring hand-off (and,
+with `all`, the LDS-staged kernels), selected through the environment switches the
+library reads at every call."""
 import os
 import sys
 
@@ -50,7 +51,12 @@ def timed(fn, reps=5):
     return e0.elapsed_time(e1) / reps
 
 
-variants = {"staged": {"DS2_GRU_DOP": "0"}, "direct-operand": {"DS2_GRU_DOP": "1"}}
+variants = {"dop-flags": {"DS2_GRU_DOP": "1", "DS2_RNN_HANDOFF": "flags"},
+            "dop-sentinel": {"DS2_GRU_DOP": "1", "DS2_RNN_HANDOFF": "sentinel"}}
+if len(sys.argv) > 1 and sys.argv[1] == "all":
+    variants = {"staged": {"DS2_GRU_DOP": "0"}, **variants}
+rounds = int(os.environ.get("AB_ROUNDS", "3"))
+variants = {f"{k}#{r}": v for r in range(rounds) for k, v in variants.items()}
 ref = None
 for name, env in variants.items():
     os.environ.update(env)

@@ -286,6 +286,35 @@ def test_gru_direct_operand_equals_staged(dev, n, h, bidir, monkeypatch):
         _close(a, b, 2e-5, "direct-operand vs staged")
 
 
+@pytest.mark.parametrize("n,h,bidir", [(32, 64, True), (20, 800, True), (7, 48, False)])
+def test_gru_sentinel_handoff_equals_flag_handoff(dev, n, h, bidir, monkeypatch):
+    """The sentinel-ring and the per-producer-flag hand-offs of the direct-operand
+    recurrences synchronise differently but sum in the same order: bit-identical outputs
+    and gradients (ragged lengths, so producers finish their sequences unevenly)."""
+    t, inp = 37, 40
+    nd = 2 if bidir else 1
+    g = torch.Generator().manual_seed(h + 3 * n)
+    weights = [torch.rand(s, generator=g) * 0.4 - 0.2 for s in
+               [(3 * h, inp), (3 * h, h), (3 * h,), (3 * h,)] * nd]
+    lens = torch.tensor(sorted([t - (i % 7) * 5 for i in range(n)], reverse=True),
+                        dtype=torch.int32)
+    x = torch.randn(t, n, inp, generator=g)
+    dy = torch.randn(t, n, h, generator=g)
+    outs = []
+    monkeypatch.setenv("DS2_GRU_DOP", "1")
+    for mode in ("flags", "sentinel"):
+        monkeypatch.setenv("DS2_RNN_HANDOFF", mode)
+        ws = [w.to(dev).requires_grad_(True) for w in weights]
+        xd = x.to(dev).requires_grad_(True)
+        y = ops.GRULayerFn.apply(xd, lens.to(dev), True, h, *ws)
+        y.backward(dy.to(dev))
+        torch.cuda.synchronize()
+        outs.append([y.detach().cpu(), xd.grad.cpu()] + [w.grad.cpu() for w in ws])
+    for a, b in zip(*outs):
+        assert torch.isfinite(a).all()
+        assert torch.equal(a, b)
+
+
 def test_gru_per_direction_output(dev):
     n, t, inp, h = 4, 11, 8, 16
     g = torch.Generator().manual_seed(5)
