@@ -53,11 +53,12 @@ def synthetic_batch(rank: int):
 
 
 class KernelProbe:
-    """Brackets every launch of one C-ABI entry point with HIP events on the stream the
-    kernel runs on (torch's current stream), to time it live inside the bench."""
+    """Brackets every launch of the named C-ABI entry points with HIP events on the stream
+    the kernel runs on (torch's current stream), to time them live inside the bench."""
 
-    def __init__(self, name, flop_fn):
-        self.name = name
+    def __init__(self, names, flop_fn):
+        self.names = (names,) if isinstance(names, str) else tuple(names)
+        self.name = "/".join(self.names)
         self.flop_fn = flop_fn
         self.events = []
         self.flops = []
@@ -69,7 +70,7 @@ class KernelProbe:
         probe = self
 
         def call(name, *args):
-            if probe.active and name == probe.name:
+            if probe.active and name in probe.names:
                 s = torch.cuda.Event(enable_timing=True)
                 e = torch.cuda.Event(enable_timing=True)
                 s.record()
@@ -122,6 +123,13 @@ def pmc_traffic_per_launch(prefix="sgemm", extra=("splitk_reduce_kernel",)):
 def sgemm_flops(args):
     m, n, k = args[2], args[3], args[4]
     return 2.0 * m * n * k
+
+
+def gru_recurrence_flops(args):
+    """ds2_gru_fwd / ds2_gru_bwd (t_max, n, h, num_dirs, ...): the W_hh contraction of
+    every step, 2 * T * N * D * 3H * H (backward: the same product with W_hh^T)."""
+    t, n, h, d = args[0], args[1], args[2], args[3]
+    return 2.0 * t * n * d * 3 * h * h
 
 
 def cpu_baseline(seconds_budget: float = 20.0):
@@ -198,6 +206,8 @@ def main():
 
     probe = KernelProbe(args.probe, sgemm_flops)
     probe.install()
+    rprobe = KernelProbe(("ds2_gru_fwd", "ds2_gru_bwd"), gru_recurrence_flops)
+    rprobe.install()
 
     def step():
         inp = x if featurize is None else featurize()
@@ -209,7 +219,7 @@ def main():
     if distributed:
         dist.barrier()
     torch.cuda.synchronize()
-    probe.active = True
+    probe.active = rprobe.active = True
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = step()
@@ -218,13 +228,14 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    probe.active = False
+    probe.active = rprobe.active = False
     if distributed:
         tt = torch.tensor([dt], device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
     final_loss = float(loss.item())
     pk = probe.summary()
+    rk = rprobe.summary()
 
     if rank == 0:
         audio = world * BATCH * SECONDS * args.steps
@@ -242,6 +253,17 @@ def main():
                     "traffic": None if traffic is None else round(traffic),
                     "traffic_unit": "bytes/launch (HBM, PMC)", "traffic_source": traffic_src,
                     "step_achieved_tflops": round(TRAIN_FLOP_PER_STEP / (ms_per_step * 1e-3) / 1e12, 3)}
+        rec = None
+        if rk is not None:
+            # the recurrences are latency-bound (T' dependent steps, one cross-CU hand-off
+            # each); their MFMA floor is the per-CU share of the step's W_hh product
+            avg_ms, flop, count = rk
+            achieved = flop / (avg_ms * 1e-3) / 1e12
+            rec = {"bound": "latency", "kernel": rprobe.name, "launches": count,
+                   "avg_launch_ms": round(avg_ms, 5),
+                   "us_per_step": round(avg_ms * 1e3 / ((T_FRAMES - 1) // 2 + 1), 3),
+                   "achieved": round(achieved, 3), "peak": PEAK_F32_MFMA_TFLOPS,
+                   "unit": "TFLOP/s", "frac": round(achieved / PEAK_F32_MFMA_TFLOPS, 4)}
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline()
@@ -260,6 +282,7 @@ def main():
                        "parallelism": f"dp{world}"},
             "loss": round(final_loss, 4),
             "roofline": roof,
+            "recurrence": rec,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

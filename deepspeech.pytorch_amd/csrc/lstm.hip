@@ -253,14 +253,14 @@ __global__ __launch_bounds__(GT) void lstm_fwd_persist_kernel(
     const float* __restrict__ wp, const float* __restrict__ b_f, const float* __restrict__ b_r,
     const int* __restrict__ lens, float* __restrict__ h_all, float* __restrict__ c_all,
     float* __restrict__ gates, unsigned* __restrict__ counters, unsigned* __restrict__ err,
-    int use_flags) {
+    int use_flags, int n_base) {
   constexpr int PITCH = LKC_FWD + 4;
   __shared__ __attribute__((aligned(16))) float hs[GB * PITCH];
   __shared__ float red[GW * GB * LRP];
   __shared__ int flag;
   int ub, d, bt;
   if (!map_work(UB * D, BT, UB, ub, d, bt)) return;
-  const int n0 = bt * GB;
+  const int n0 = n_base + bt * GB;     // samples [n_base, ...) of a batch chunk
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int KS = H / 4;                    // host guarantees H % 4 == 0, GW * KSW >= KS
@@ -376,7 +376,7 @@ __global__ __launch_bounds__(GT) void lstm_bwd_persist_kernel(
     int T, int N, int H, int D, int UB, int BT, const float* __restrict__ dy, int dyd,
     const float* __restrict__ wpt, const float* __restrict__ c_all,
     const float* __restrict__ gates, const int* __restrict__ lens, float* __restrict__ dg,
-    unsigned* __restrict__ counters, unsigned* __restrict__ err, int use_flags) {
+    unsigned* __restrict__ counters, unsigned* __restrict__ err, int use_flags, int n_base) {
   constexpr int CW = 4 * GW * KSWC;         // gate columns per chunk (<= LKC_BWD)
   constexpr int PITCH = CW + 4;
   __shared__ __attribute__((aligned(16))) float hs[GB * PITCH];
@@ -384,7 +384,7 @@ __global__ __launch_bounds__(GT) void lstm_bwd_persist_kernel(
   __shared__ int flag;
   int ub, d, bt;
   if (!map_work(UB * D, BT, UB, ub, d, bt)) return;
-  const int n0 = bt * GB;
+  const int n0 = n_base + bt * GB;     // samples [n_base, ...) of a batch chunk
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int H4 = 4 * H;
@@ -516,6 +516,16 @@ static inline int lstm_flags_mode() {
   return !(e != nullptr && e[0] == '0');
 }
 
+// Batch chunking of the persistent launches: the largest number of 16-sample tiles per
+// launch whose grid fits the chip (one workgroup per CU); a batch with more tiles runs as
+// consecutive launches over sample ranges [n_base, n_base + 16 * chunk) -- the samples'
+// recurrences are independent (cfg4: 7 x BiLSTM-1024 at batch 64 = two launches of 256).
+static inline int lstm_chunk_tiles(int UB, int D, int BT) {
+  int c = BT;
+  while (c > 1 && mapped_grid(UB * D, c) > num_cus()) --c;
+  return c;
+}
+
 size_t ds2_lstm_fwd_workspace_size(int n, int h, int num_dirs) {
   const int64_t UB = (h + GU - 1) / GU;
   const int64_t KS = (h + 3) / 4;
@@ -559,15 +569,9 @@ ds2_status_t ds2_lstm_fwd(int t_max, int n, int h, int num_dirs, const float* xp
                      dim3(256), 0, st, w_hh_f, w_hh_r, h, num_dirs, UB, KS, wp);
   const int grid = mapped_grid(UB * num_dirs, BT);
   const int kp = persist_ksw((KS + GW - 1) / GW, LKC_FWD);
-  if (persistent_enabled() && (h % 4) == 0 && grid <= num_cus() && kp > 0 && kp <= 32 &&
-      (int64_t)t_max * n * num_dirs * h * 4 < (1ll << 31)) {
-    unsigned* err = ctrs + num_dirs * BT;
-    if (hipMemsetAsync(ctrs, 0, lstm_counter_bytes(n, num_dirs), st) != hipSuccess)
-      return launch_status("ds2_lstm counters");
-    int T_ = t_max, N_ = n, H_ = h, D_ = num_dirs, UB_ = UB, BT_ = BT;
-    int flags_ = lstm_flags_mode();
-    void* args[] = {&T_, &N_, &H_, &D_, &UB_, &BT_, &xproj, &wp, &b_hh_f, &b_hh_r, &lens,
-                    &h_all, &c_all, &gates, &ctrs, &err, &flags_};
+  const int ct = lstm_chunk_tiles(UB, num_dirs, BT);
+  if (persistent_enabled() && (h % 4) == 0 && mapped_grid(UB * num_dirs, ct) <= num_cus() &&
+      kp > 0 && kp <= 32 && (int64_t)t_max * n * num_dirs * h * 4 < (1ll << 31)) {
     const void* fn = nullptr;
     switch (kp) {
       case 8: fn = reinterpret_cast<const void*>(lstm_fwd_persist_kernel<8>); break;
@@ -576,9 +580,20 @@ ds2_status_t ds2_lstm_fwd(int t_max, int n, int h, int num_dirs, const float* xp
       case 32: fn = reinterpret_cast<const void*>(lstm_fwd_persist_kernel<32>); break;
       default: break;
     }
-    if (fn != nullptr &&
-        hipLaunchCooperativeKernel(fn, dim3(grid), dim3(GT), args, 0, st) == hipSuccess)
-      return launch_status("ds2_lstm_fwd");
+    bool ok = fn != nullptr;
+    for (int b0 = 0; ok && b0 < BT; b0 += ct) {
+      int T_ = t_max, N_ = n, H_ = h, D_ = num_dirs, UB_ = UB, BT_ = std::min(ct, BT - b0);
+      int flags_ = lstm_flags_mode(), NB_ = b0 * GB;
+      unsigned* err = ctrs + num_dirs * BT_;
+      if (hipMemsetAsync(ctrs, 0, lstm_counter_bytes(n, num_dirs), st) != hipSuccess)
+        return launch_status("ds2_lstm counters");
+      void* args[] = {&T_, &N_, &H_, &D_, &UB_, &BT_, &xproj, &wp, &b_hh_f, &b_hh_r, &lens,
+                      &h_all, &c_all, &gates, &ctrs, &err, &flags_, &NB_};
+      ok = hipLaunchCooperativeKernel(fn, dim3(mapped_grid(UB * num_dirs, BT_)), dim3(GT), args,
+                                      0, st) == hipSuccess;
+      if (!ok && b0 > 0) return launch_status("ds2_lstm_fwd chunk");
+    }
+    if (ok) return launch_status("ds2_lstm_fwd");
     (void)hipGetLastError();   // fall back to one launch per step
   }
   for (int s = 0; s < t_max; ++s) {
@@ -629,7 +644,7 @@ ds2_status_t ds2_lstm_bwd(int t_max, int n, int h, int num_dirs, const float* dy
   hipLaunchKernelGGL(pack_bwd_kernel<4>, dim3(grid_cap((int64_t)num_dirs * UB * KS * 64)),
                      dim3(256), 0, st, w_hh_f, w_hh_r, h, num_dirs, UB, KS, wpt);
   const int grid = mapped_grid(UB * num_dirs, BT);
-  if (persistent_enabled() && (h % 4) == 0 && grid <= num_cus() &&
+  if (persistent_enabled() && (h % 4) == 0 &&
       (int64_t)t_max * n * num_dirs * 4 * h * 4 < (1ll << 31)) {
     // smallest (k-steps per wave per chunk, chunks) covering 4H gate columns
     const int opts[] = {8, 16, 25, 32, 48, 64};
@@ -648,18 +663,22 @@ ds2_status_t ds2_lstm_bwd(int t_max, int n, int h, int num_dirs, const float* dy
     DS2_LBP(8, 1) DS2_LBP(16, 1) DS2_LBP(25, 1) DS2_LBP(32, 1) DS2_LBP(48, 1) DS2_LBP(64, 1)
     DS2_LBP(48, 2) DS2_LBP(64, 2)
 #undef DS2_LBP
-    if (fn != nullptr) {
-      unsigned* err = ctrs + num_dirs * BT;
+    const int ct = lstm_chunk_tiles(UB, num_dirs, BT);
+    bool ok = fn != nullptr && mapped_grid(UB * num_dirs, ct) <= num_cus();
+    for (int b0 = 0; ok && b0 < BT; b0 += ct) {
+      int T_ = t_max, N_ = n, H_ = h, D_ = num_dirs, UB_ = UB, BT_ = std::min(ct, BT - b0);
+      int DYD_ = dy_dirs, flags_ = lstm_flags_mode(), NB_ = b0 * GB;
+      unsigned* err = ctrs + num_dirs * BT_;
       if (hipMemsetAsync(ctrs, 0, lstm_counter_bytes(n, num_dirs), st) != hipSuccess)
         return launch_status("ds2_lstm counters");
-      int T_ = t_max, N_ = n, H_ = h, D_ = num_dirs, UB_ = UB, BT_ = BT, DYD_ = dy_dirs;
-      int flags_ = lstm_flags_mode();
       void* args[] = {&T_, &N_, &H_, &D_, &UB_, &BT_, &dy, &DYD_, &wpt, &c_all, &gates, &lens,
-                      &dgates, &ctrs, &err, &flags_};
-      if (hipLaunchCooperativeKernel(fn, dim3(grid), dim3(GT), args, 0, st) == hipSuccess)
-        return launch_status("ds2_lstm_bwd");
-      (void)hipGetLastError();
+                      &dgates, &ctrs, &err, &flags_, &NB_};
+      ok = hipLaunchCooperativeKernel(fn, dim3(mapped_grid(UB * num_dirs, BT_)), dim3(GT), args,
+                                      0, st) == hipSuccess;
+      if (!ok && b0 > 0) return launch_status("ds2_lstm_bwd chunk");
     }
+    if (ok) return launch_status("ds2_lstm_bwd");
+    (void)hipGetLastError();
   }
   for (int s = 0; s < t_max; ++s) {
     switch (ksw) {

@@ -351,7 +351,7 @@ def _lstm_case(n, t, inp, h, bidir, seed):
 
 @pytest.mark.parametrize("n,t,inp,h,bidir", [(5, 23, 40, 24, True), (19, 9, 33, 400, True),
                                              (3, 17, 20, 16, False),
-                                             (64, 5, 64, 1024, True),     # cfg4 shape: per-step path
+                                             (64, 5, 64, 1024, True),     # cfg4 shape: 2 batch chunks
                                              (32, 6, 48, 1024, False)])   # persistent, 2 bwd chunks
 def test_lstm_layer(dev, n, t, inp, h, bidir):
     """ds2amd LSTM layer == pack -> nn.LSTM -> pad (-> direction sum), fwd and bwd."""
@@ -373,9 +373,11 @@ def test_lstm_layer(dev, n, t, inp, h, bidir):
         _close(wd.grad, p.grad, 1e-4, "lstm " + name)
 
 
-@pytest.mark.parametrize("h", [24, 800])
-def test_lstm_persistent_equals_per_step(dev, h, monkeypatch):
-    n, t, inp = 21, 19, 40
+@pytest.mark.parametrize("h,n", [(24, 21), (800, 21), (1024, 40)])
+def test_lstm_persistent_equals_per_step(dev, h, n, monkeypatch):
+    """Persistent launches (for h = 1024, n = 40: 3 batch tiles run as a 2-tile chunk and a
+    1-tile chunk, bidirectional) equal the one-launch-per-step kernels."""
+    t, inp = 19, 40
     lstm, lens, x, g = _lstm_case(n, t, inp, h, True, h)
     weights = [p.detach().float() for p in lstm.parameters()]
     x = x.float()
