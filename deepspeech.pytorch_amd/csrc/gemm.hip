@@ -467,6 +467,165 @@ __global__ __launch_bounds__(256, 2) void sgemm64_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// bf16-operand variant (BASELINE cfg4 "bf16 MFMA RNN GEMMs", opt-in): fp32 operands in
+// memory are rounded to bf16 (round-to-nearest-even, v_cvt_pk_bf16_f32) while they are
+// staged, multiplied with v_mfma_f32_16x16x32_bf16 and accumulated in fp32; C, bias, the
+// split-K plan and the epilogue are those of sgemm64_kernel (tile 128 x 128, 4 waves of
+// 4 x 4 16x16 tiles).  Each operand is staged k-contiguous in LDS whatever its global
+// layout: rows of 64 bf16 (128 B) in 16-B slots (8 k each) swizzled by (row >> 1) & 7, so a
+// lane's A or B fragment (8 consecutive k of one row) is one conflict-free ds_read_b128.
+//   k-contiguous source: a thread unit = (row, slot): 2 float4 loads -> 1 ds_write_b128;
+//   row-contiguous source: a unit = (4 rows, slot): 8 float4 loads (one per k) -> 4 writes.
+constexpr int KB16 = 64;   // k per stage
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ int bslot(int row, int s) { return row * KB16 + 8 * (s ^ ((row >> 1) & 7)); }
+
+template <bool KC>
+__device__ __forceinline__ void bload_stage(__amdgpu_buffer_rsrc_t rs, int ld, int rows, int kend,
+                                            int r0, int k0, f32x4 (&v)[8]) {
+  constexpr int kOob = 0x7ffffff0;
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    int r, k;
+    if (KC) {                        // units t + 256 i (i = q / 2): row u / 8, slot u % 8
+      const int u = t + 256 * (q >> 1);
+      r = r0 + (u >> 3);
+      k = k0 + 8 * (u & 7) + 4 * (q & 1);
+    } else {                         // 4-row group t % 32, slot t / 32, k row q of the slot
+      r = r0 + 4 * (t & 31);
+      k = k0 + 8 * (t >> 5) + q;
+    }
+    const int off = (r < rows && k < kend) ? (KC ? r * ld + k : k * ld + r) * 4 : kOob;
+    v[q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+  }
+}
+
+template <bool KC>
+__device__ __forceinline__ void bstore_stage(unsigned short* __restrict__ s, const f32x4 (&v)[8]) {
+  const int t = threadIdx.x;
+  if (KC) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int u = t + 256 * i;
+      const f32x4 a = v[2 * i], b = v[2 * i + 1];
+      const bf16x8 p{(__bf16)a.x, (__bf16)a.y, (__bf16)a.z, (__bf16)a.w,
+                     (__bf16)b.x, (__bf16)b.y, (__bf16)b.z, (__bf16)b.w};
+      *reinterpret_cast<bf16x8*>(s + bslot(u >> 3, u & 7)) = p;
+    }
+  } else {
+    const int g = t & 31, sl = t >> 5;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const bf16x8 p{(__bf16)v[0][c], (__bf16)v[1][c], (__bf16)v[2][c], (__bf16)v[3][c],
+                     (__bf16)v[4][c], (__bf16)v[5][c], (__bf16)v[6][c], (__bf16)v[7][c]};
+      *reinterpret_cast<bf16x8*>(s + bslot(4 * g + c, sl)) = p;
+    }
+  }
+}
+
+template <int TA, int TB>
+__global__ __launch_bounds__(256, 2) void sbgemm_kernel(
+    int M, int N, int K, float alpha, const float* __restrict__ A, int64_t lda, int64_t sA,
+    const float* __restrict__ B, int64_t ldb, int64_t sB, float beta, float* __restrict__ C,
+    int64_t ldc, int64_t sC, const float* __restrict__ bias, int main_wgs, int tail_tile0,
+    int tail_tiles, int nsplit, int kchunk, float* __restrict__ partial) {
+  constexpr bool AK = (TA == 0);
+  constexpr bool BKc = (TB == 1);
+  constexpr int TBN = 128;
+  __shared__ __attribute__((aligned(16))) unsigned short As[BM * KB16];
+  __shared__ __attribute__((aligned(16))) unsigned short Bs[TBN * KB16];
+
+  int m0, n0, kbeg, kend, bz;
+  float* part;
+  decode_work(M, N, K, main_wgs, tail_tile0, tail_tiles, nsplit, kchunk, partial, m0, n0, kbeg,
+              kend, bz, part, TBN);
+  A += bz * sA;
+  B += bz * sB;
+  C += bz * sC;
+  const int a_rows = AK ? M : K, b_rows = BKc ? N : K;
+  const __amdgpu_buffer_rsrc_t a_rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(A), (short)0, static_cast<int>(a_rows * lda * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t b_rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(B), (short)0, static_cast<int>(b_rows * ldb * 4), 0x00020000);
+  const int ilda = static_cast<int>(lda), ildb = static_cast<int>(ldb);
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int wm = (wave >> 1) * 64;
+  const int wn = (wave & 1) * 64;
+  const int fr = lane & 15, fq = lane >> 4;
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  f32x4 ra[8], rb[8];
+  const int ktiles = (kend - kbeg + KB16 - 1) / KB16;
+  bload_stage<AK>(a_rs, ilda, M, kend, m0, kbeg, ra);
+  bload_stage<BKc>(b_rs, ildb, N, kend, n0, kbeg, rb);
+  for (int kt = 0; kt < ktiles; ++kt) {
+    bstore_stage<AK>(As, ra);
+    bstore_stage<BKc>(Bs, rb);
+    __syncthreads();
+    if (kt + 1 < ktiles) {   // next stage's global loads fly during this stage's MFMAs
+      bload_stage<AK>(a_rs, ilda, M, kend, m0, kbeg + (kt + 1) * KB16, ra);
+      bload_stage<BKc>(b_rs, ildb, N, kend, n0, kbeg + (kt + 1) * KB16, rb);
+    }
+    // k-steps past kend hold zeros: skip them
+    const int ns = min(KB16 / 32, (kend - kbeg - kt * KB16 + 31) / 32);
+#pragma unroll
+    for (int s = 0; s < KB16 / 32; ++s) {
+      if (s >= ns) break;
+      bf16x8 a[4], b[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        a[i] = *reinterpret_cast<const bf16x8*>(As + bslot(wm + 16 * i + fr, 4 * s + fq));
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        b[j] = *reinterpret_cast<const bf16x8*>(Bs + bslot(wn + 16 * j + fr, 4 * s + fq));
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+
+  // epilogue (16x16 C/D map: col = lane & 15, row = 4 * (lane >> 4) + r), as sgemm64_kernel
+  const int lc = lane & 15;
+  const int lr = 4 * (lane >> 4);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int cl = wn + 16 * j + lc;
+      if (part != nullptr) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) part[(wm + 16 * i + lr + r) * TBN + cl] = acc[i][j][r];
+        continue;
+      }
+      const int col = n0 + cl;
+      if (col >= N) continue;
+      const float bv = bias != nullptr ? bias[col] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wm + 16 * i + lr + r;
+        if (row < M) {
+          float* cp = C + (int64_t)row * ldc + col;
+          float v = alpha * acc[i][j][r] + bv;
+          if (beta != 0.f) v += beta * *cp;
+          *cp = v;
+        }
+      }
+    }
+  }
+}
+
 // Tail tiles: C[b] = alpha * sum_s partial[b][s][tile] + beta * C[b] + bias (fixed order)
 __global__ void splitk_reduce_kernel(const float* __restrict__ partial, int M, int N, int nsplit,
                                      int batch, int tail_tile0, int tail_tiles, float alpha,
@@ -699,6 +858,61 @@ extern "C" ds2_status_t ds2_sgemm_ws(int trans_a, int trans_b, int m, int n, int
                        p.bn);
   }
   return launch_status("ds2_sgemm");
+}
+
+// bf16-operand GEMM (sbgemm_kernel): same contract as ds2_sgemm_ws; every operand must be
+// float4-staged (16-B aligned, ld and the contiguous extent multiples of 4) and span
+// < 2^31 bytes, else DS2_UNSUPPORTED_SHAPE (no silent fp32 fallback).
+extern "C" size_t ds2_sgemm_bf16_workspace_size(int m, int n, int k, int batch) {
+  if (m <= 0 || n <= 0 || k <= 0 || batch <= 0) return 0;
+  return plan_ws(plan_bn(m, n, k, batch, 128, 2 * device_cus(), KB16, 1.0).p, batch);
+}
+
+extern "C" ds2_status_t ds2_sgemm_bf16_ws(int trans_a, int trans_b, int m, int n, int k,
+                                          float alpha, const float* a, int64_t lda,
+                                          int64_t stride_a, const float* b, int64_t ldb,
+                                          int64_t stride_b, float beta, float* c, int64_t ldc,
+                                          int64_t stride_c, int batch, const float* bias,
+                                          void* ws, size_t ws_bytes, ds2_stream_t stream) {
+  if (m < 0 || n < 0 || k < 0 || batch < 0) return DS2_INVALID_VALUE;
+  if (m == 0 || n == 0 || batch == 0) return DS2_OK;
+  if (ldc < n) return DS2_INVALID_VALUE;
+  if (trans_a ? lda < m : lda < k) return DS2_INVALID_VALUE;
+  if (trans_b ? ldb < k : ldb < n) return DS2_INVALID_VALUE;
+  const bool va = aligned16(a) && (lda % 4 == 0) && (stride_a % 4 == 0) &&
+                  (trans_a ? (m % 4 == 0) : (k % 4 == 0));
+  const bool vb = aligned16(b) && (ldb % 4 == 0) && (stride_b % 4 == 0) &&
+                  (trans_b ? (k % 4 == 0) : (n % 4 == 0));
+  if (!va || !vb || !fits_rsrc(trans_a ? k : m, lda) || !fits_rsrc(trans_b ? n : k, ldb))
+    return DS2_UNSUPPORTED_SHAPE;
+  GemmPlan p = plan_bn(m, n, k, batch, 128, 2 * device_cus(), KB16, 1.0).p;
+  if (p.nsplit > 1 && (ws == nullptr || ws_bytes < plan_ws(p, batch))) {
+    p.nsplit = 1;
+    p.kchunk = std::max(k, 1);
+  }
+  float* partial = p.nsplit > 1 ? static_cast<float*>(ws) : nullptr;
+  const int64_t nwg = p.main_wgs + (int64_t)p.tail_tiles * batch * p.nsplit;
+  if (nwg > 0x7fffffff) return DS2_UNSUPPORTED_SHAPE;
+  dim3 grid(static_cast<unsigned>(nwg));
+  hipStream_t st = as_stream(stream);
+#define DS2_B(TA_, TB_)                                                                        \
+  hipLaunchKernelGGL((sbgemm_kernel<TA_, TB_>), grid, dim3(256), 0, st, m, n, k, alpha, a, lda, \
+                     stride_a, b, ldb, stride_b, beta, c, ldc, stride_c, bias, p.main_wgs,      \
+                     p.tail_tile0, p.tail_tiles, p.nsplit, p.kchunk, partial)
+  if (!trans_a && !trans_b) DS2_B(0, 0);
+  else if (!trans_a && trans_b) DS2_B(0, 1);
+  else if (trans_a && !trans_b) DS2_B(1, 0);
+  else DS2_B(1, 1);
+#undef DS2_B
+  if (p.nsplit > 1) {
+    const int64_t total = (int64_t)batch * p.tail_tiles * BM * p.bn;
+    int g = cdiv(total, 256);
+    if (g > 4096) g = 4096;
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(g), dim3(256), 0, st, partial, m, n, p.nsplit,
+                       batch, p.tail_tile0, p.tail_tiles, alpha, beta, c, ldc, stride_c, bias,
+                       p.bn);
+  }
+  return launch_status("ds2_sgemm_bf16");
 }
 
 extern "C" ds2_status_t ds2_sgemm(int trans_a, int trans_b, int m, int n, int k, float alpha,

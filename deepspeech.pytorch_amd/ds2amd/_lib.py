@@ -36,6 +36,10 @@ _PROTOS = {
     "ds2_sgemm_ws": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _c_f, _vp, _c_i64, _c_i64,
                               _vp, _c_i64, _c_i64, _c_f, _vp, _c_i64, _c_i64, _c_int, _vp, _vp,
                               _sz, _vp]),
+    "ds2_sgemm_bf16_workspace_size": (_sz, [_c_int, _c_int, _c_int, _c_int]),
+    "ds2_sgemm_bf16_ws": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _c_f, _vp, _c_i64,
+                                   _c_i64, _vp, _c_i64, _c_i64, _c_f, _vp, _c_i64, _c_i64, _c_int,
+                                   _vp, _vp, _sz, _vp]),
     "ds2_conv2d_workspace_size": (_sz, [_c_int] * 11),
     "ds2_conv2d_fwd": (_c_int, [_vp, _vp, _vp, _vp] + [_c_int] * 11 + [_vp, _vp, _sz, _vp]),
     "ds2_conv2d_dgrad": (_c_int, [_vp, _vp, _vp] + [_c_int] * 11 + [_vp, _sz, _vp]),

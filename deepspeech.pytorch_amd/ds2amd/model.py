@@ -34,6 +34,10 @@ class _HipRNN(nn.Module):
     """
     GATES = 0
     FN = None
+    # precision of this layer's GEMMs: 'fp32' (reference parity) or 'bf16' (BASELINE cfg4's
+    # opt-in bf16 MFMA RNN GEMMs; the recurrence itself stays fp32).  Not a parameter or
+    # buffer: state_dicts are unchanged.
+    gemm_precision = 'fp32'
 
     def __init__(self, input_size, hidden_size, bidirectional=False, bias=True, num_layers=1):
         super().__init__()
@@ -68,7 +72,8 @@ class _HipRNN(nn.Module):
         return ws
 
     def run(self, x, lens_dev, sum_dirs=False):
-        return self.FN.apply(x, lens_dev, sum_dirs, self.hidden_size, *self._weights())
+        with ops.rnn_gemm_precision(self.gemm_precision):
+            return self.FN.apply(x, lens_dev, sum_dirs, self.hidden_size, *self._weights())
 
     def forward(self, x, lengths=None):
         if isinstance(x, PackedSequence):
@@ -247,7 +252,10 @@ class DeepSpeech(nn.Module):
 
     def __init__(self, rnn_type='gru', labels="abc", rnn_hidden_size=768, nb_layers=6,
                  audio_conf=None, bidirectional=True, context=20, bnm=0.1, dropout=0,
-                 cnn_width=256):
+                 cnn_width=256, rnn_gemm_precision='fp32'):
+        """The reference's constructor (model.py:184-186) plus ``rnn_gemm_precision``:
+        'fp32' (default, the reference's arithmetic) or 'bf16' (the recurrent layers'
+        GEMMs on the bf16 MFMA with fp32 accumulation, BASELINE cfg4)."""
         super().__init__()
         if audio_conf is None:
             audio_conf = {}
@@ -293,6 +301,7 @@ class DeepSpeech(nn.Module):
                                                   hidden_size=rnn_hidden_size, rnn_type=rnn_cls,
                                                   bidirectional=bidirectional, bnm=bnm)))
         self.rnns = nn.Sequential(OrderedDict(rnns))
+        self.set_rnn_gemm_precision(rnn_gemm_precision)
         self.lookahead = nn.Sequential(
             Lookahead(rnn_hidden_size, context=context),
             Hardtanh(0, 20, inplace=True)
@@ -302,6 +311,14 @@ class DeepSpeech(nn.Module):
             Linear(rnn_hidden_size, num_classes, bias=False)
         )
         self.fc = nn.Sequential(SequenceWise(fully_connected))
+
+    def set_rnn_gemm_precision(self, precision: str):
+        """'fp32' | 'bf16' for every recurrent layer's GEMMs (see __init__)."""
+        ops.rnn_gemm_precision(precision)          # validates
+        self._rnn_gemm_precision = precision
+        for m in self.rnns:
+            m.rnn.gemm_precision = precision
+        return self
 
     def forward(self, x, lengths):
         """x [N,1,161,T] on the GPU, lengths [N] ints (host or device).

@@ -46,15 +46,18 @@ def _ws(nbytes: int, device) -> torch.Tensor:
 def sgemm(a: torch.Tensor, b: torch.Tensor, c: torch.Tensor, *, m: int, n: int, k: int,
           trans_a: bool = False, trans_b: bool = False, lda: int, ldb: int, ldc: int,
           alpha: float = 1.0, beta: float = 0.0, bias: Optional[torch.Tensor] = None,
-          a_off: int = 0, b_off: int = 0, c_off: int = 0) -> torch.Tensor:
+          a_off: int = 0, b_off: int = 0, c_off: int = 0, bf16: bool = False) -> torch.Tensor:
     """C = alpha*op(A)@op(B) + beta*C (+bias) on raw row-major storage.
 
-    ``*_off`` are element offsets into the (contiguous) storage of a/b/c.
+    ``*_off`` are element offsets into the (contiguous) storage of a/b/c.  ``bf16``: the
+    operands are rounded to bf16 and multiplied on the bf16 MFMA (fp32 accumulation,
+    ds2_sgemm_bf16_ws) -- the opt-in precision of BASELINE cfg4's RNN GEMMs.
     """
     es = 4
-    nbytes = _lib.size("ds2_sgemm_workspace_size", m, n, k, 1)
+    fn = "ds2_sgemm_bf16" if bf16 else "ds2_sgemm"
+    nbytes = _lib.size(fn + "_workspace_size", m, n, k, 1)
     ws = _ws(nbytes, c.device) if nbytes > 0 else None
-    _lib.call("ds2_sgemm_ws", int(trans_a), int(trans_b), m, n, k, float(alpha),
+    _lib.call(fn + "_ws", int(trans_a), int(trans_b), m, n, k, float(alpha),
               a.data_ptr() + es * a_off, lda, 0, b.data_ptr() + es * b_off, ldb, 0,
               float(beta), c.data_ptr() + es * c_off, ldc, 0, 1, _p(bias), _p(ws),
               0 if ws is None else ws.numel(), _stream())
@@ -397,7 +400,32 @@ class LinearFn(torch.autograd.Function):
         return dx, dw
 
 
-def _rnn_input_proj(x, weights, nd, g):
+# Precision of the recurrent layers' GEMMs (input projection, dX, dW_ih, dW_hh): fp32 by
+# default (parity with the reference's fp32 path); bf16 operands on the bf16 MFMA with fp32
+# accumulation as BASELINE cfg4's opt-in ("bf16 MFMA RNN GEMMs").  Set around one layer
+# call by rnn_gemm_precision(); the autograd Functions record it for their backward.
+_RNN_GEMM_BF16 = [False]
+
+
+class rnn_gemm_precision:
+    """Context manager: ``with rnn_gemm_precision('bf16'): y = GRULayerFn.apply(...)``."""
+
+    def __init__(self, precision: str):
+        if precision not in ('fp32', 'bf16'):
+            raise ValueError(f"rnn GEMM precision must be 'fp32' or 'bf16', got {precision!r}")
+        self.bf16 = precision == 'bf16'
+
+    def __enter__(self):
+        self.prev = _RNN_GEMM_BF16[0]
+        _RNN_GEMM_BF16[0] = self.bf16
+        return self
+
+    def __exit__(self, *exc):
+        _RNN_GEMM_BF16[0] = self.prev
+        return False
+
+
+def _rnn_input_proj(x, weights, nd, g, bf16=False):
     """xproj[T, N, D, g] = x @ W_ih^T + b_ih for every direction (one GEMM each)."""
     t, n, inp = x.shape
     x2d = x.view(t * n, inp)
@@ -405,7 +433,7 @@ def _rnn_input_proj(x, weights, nd, g):
     for d in range(nd):
         w_ih, _, b_ih, _ = weights[4 * d: 4 * d + 4]
         sgemm(x2d, w_ih, xproj, m=t * n, n=g, k=inp, trans_b=True, lda=inp, ldb=inp,
-              ldc=nd * g, bias=b_ih, c_off=d * g)
+              ldc=nd * g, bias=b_ih, c_off=d * g, bf16=bf16)
     return xproj
 
 
@@ -418,7 +446,7 @@ def _rnn_output(h_all, sum_dirs, nd):
     return h_all.view(t, n, nd * h)
 
 
-def _rnn_param_grads(x, h_all, dgx, dgh, weights, nd, g, need_dx):
+def _rnn_param_grads(x, h_all, dgx, dgh, weights, nd, g, need_dx, bf16=False):
     """Weight/bias/input gradients of one recurrent layer from the gate gradients.
 
     dgx = d/d(x W_ih^T + b_ih), dgh = d/d(h W_hh^T + b_hh), both [T, N, D, g]
@@ -436,7 +464,7 @@ def _rnn_param_grads(x, h_all, dgx, dgh, weights, nd, g, need_dx):
         w_ih, w_hh, b_ih, b_hh = weights[4 * d: 4 * d + 4]
         dw_ih = grad_like(w_ih)
         sgemm(dgx, x2d, dw_ih, m=g, n=inp, k=tn, trans_a=True, lda=ld, ldb=inp, ldc=inp,
-              a_off=d * g)
+              a_off=d * g, bf16=bf16)
         db_ih = grad_like(b_ih)
         colsum(dgx, tn, g, ld, db_ih, off=d * g)
         dw_hh = grad_like(w_hh)
@@ -445,7 +473,7 @@ def _rnn_param_grads(x, h_all, dgx, dgh, weights, nd, g, need_dx):
             a_off = (n * ld if d == 0 else 0) + d * g
             b_off = (0 if d == 0 else n * nd * h) + d * h
             sgemm(dgh, h_all, dw_hh, m=g, n=h, k=(t - 1) * n, trans_a=True, lda=ld,
-                  ldb=nd * h, ldc=h, a_off=a_off, b_off=b_off)
+                  ldb=nd * h, ldc=h, a_off=a_off, b_off=b_off, bf16=bf16)
         else:
             dw_hh.zero_()
         db_hh = grad_like(b_hh)
@@ -455,7 +483,7 @@ def _rnn_param_grads(x, h_all, dgx, dgh, weights, nd, g, need_dx):
             colsum(dgh, tn, g, ld, db_hh, off=d * g)
         if dx is not None:
             sgemm(dgx, w_ih, dx, m=tn, n=inp, k=g, lda=ld, ldb=inp, ldc=inp,
-                  beta=0.0 if d == 0 else 1.0, a_off=d * g)
+                  beta=0.0 if d == 0 else 1.0, a_off=d * g, bf16=bf16)
         grads += [dw_ih, dw_hh, db_ih, db_hh]
     return dx, grads
 
@@ -474,7 +502,8 @@ class GRULayerFn(torch.autograd.Function):
         h = hidden
         nd = len(weights) // 4
         dev = x.device
-        xproj = _rnn_input_proj(x, weights, nd, 3 * h)
+        bf16 = _RNN_GEMM_BF16[0]
+        xproj = _rnn_input_proj(x, weights, nd, 3 * h, bf16)
         h_all = torch.empty(t, n, nd, h, device=dev, dtype=_F32)
         need_grad = any(ctx.needs_input_grad)   # forward() itself runs under no_grad
         gates = torch.empty(t, n, nd, 4 * h, device=dev, dtype=_F32) if need_grad else None
@@ -486,13 +515,13 @@ class GRULayerFn(torch.autograd.Function):
                   b_hh_f.data_ptr(), _p(b_hh_r), lens.data_ptr(), h_all.data_ptr(), _p(gates),
                   ws.data_ptr(), ws.numel(), _stream())
         ctx.save_for_backward(x, lens, h_all, gates, *weights)
-        ctx.cfg = (sum_dirs, h, nd)
+        ctx.cfg = (sum_dirs, h, nd, bf16)
         return _rnn_output(h_all, sum_dirs, nd)
 
     @staticmethod
     def backward(ctx, dy):
         x, lens, h_all, gates, *weights = ctx.saved_tensors
-        sum_dirs, h, nd = ctx.cfg
+        sum_dirs, h, nd, bf16 = ctx.cfg
         t, n, _ = x.shape
         dev = x.device
         h3 = 3 * h
@@ -507,7 +536,7 @@ class GRULayerFn(torch.autograd.Function):
                   _p(w_hh_r), h_all.data_ptr(), gates.data_ptr(), lens.data_ptr(), dgx.data_ptr(),
                   dgh.data_ptr(), ws.data_ptr(), ws.numel(), _stream())
         dx, grads = _rnn_param_grads(x, h_all, dgx, dgh, weights, nd, h3,
-                                     ctx.needs_input_grad[0])
+                                     ctx.needs_input_grad[0], bf16)
         return (dx, None, None, None, *grads)
 
 
@@ -523,7 +552,8 @@ class LSTMLayerFn(torch.autograd.Function):
         h = hidden
         nd = len(weights) // 4
         dev = x.device
-        xproj = _rnn_input_proj(x, weights, nd, 4 * h)
+        bf16 = _RNN_GEMM_BF16[0]
+        xproj = _rnn_input_proj(x, weights, nd, 4 * h, bf16)
         h_all = torch.empty(t, n, nd, h, device=dev, dtype=_F32)
         need_grad = any(ctx.needs_input_grad)
         c_all = torch.empty(t, n, nd, h, device=dev, dtype=_F32) if need_grad else None
@@ -536,13 +566,13 @@ class LSTMLayerFn(torch.autograd.Function):
                   b_hh_f.data_ptr(), _p(b_hh_r), lens.data_ptr(), h_all.data_ptr(), _p(c_all),
                   _p(gates), ws.data_ptr(), ws.numel(), _stream())
         ctx.save_for_backward(x, lens, h_all, c_all, gates, *weights)
-        ctx.cfg = (sum_dirs, h, nd)
+        ctx.cfg = (sum_dirs, h, nd, bf16)
         return _rnn_output(h_all, sum_dirs, nd)
 
     @staticmethod
     def backward(ctx, dy):
         x, lens, h_all, c_all, gates, *weights = ctx.saved_tensors
-        sum_dirs, h, nd = ctx.cfg
+        sum_dirs, h, nd, bf16 = ctx.cfg
         t, n, _ = x.shape
         dev = x.device
         dy = dy.contiguous()
@@ -555,7 +585,7 @@ class LSTMLayerFn(torch.autograd.Function):
                   _p(w_hh_r), c_all.data_ptr(), gates.data_ptr(), lens.data_ptr(), dg.data_ptr(),
                   ws.data_ptr(), ws.numel(), _stream())
         dx, grads = _rnn_param_grads(x, h_all, dg, dg, weights, nd, 4 * h,
-                                     ctx.needs_input_grad[0])
+                                     ctx.needs_input_grad[0], bf16)
         return (dx, None, None, None, *grads)
 
 

@@ -88,6 +88,17 @@ ds2_status_t ds2_sgemm_ws(int trans_a, int trans_b, int m, int n, int k, float a
                           const float* b, int64_t ldb, int64_t stride_b, float beta,
                           float* c, int64_t ldc, int64_t stride_c, int batch,
                           const float* bias, void* ws, size_t ws_bytes, ds2_stream_t stream);
+/* bf16-operand variant (BASELINE cfg4 "bf16 MFMA RNN GEMMs", opt-in): same contract, A and
+ * B rounded to bf16 (nearest even) as they are staged, v_mfma_f32_16x16x32_bf16, fp32
+ * accumulation and fp32 C.  Needs float4-aligned operands (16-B aligned pointers, ld and
+ * the contiguous extent multiples of 4): DS2_UNSUPPORTED_SHAPE otherwise. */
+size_t ds2_sgemm_bf16_workspace_size(int m, int n, int k, int batch);
+ds2_status_t ds2_sgemm_bf16_ws(int trans_a, int trans_b, int m, int n, int k, float alpha,
+                               const float* a, int64_t lda, int64_t stride_a,
+                               const float* b, int64_t ldb, int64_t stride_b, float beta,
+                               float* c, int64_t ldc, int64_t stride_c, int batch,
+                               const float* bias, void* ws, size_t ws_bytes,
+                               ds2_stream_t stream);
 
 /* ------------------------------------------------------------------------ */
 /* Conv2d, NCHW fp32, on MFMA. ref model.py:209,212 (nn.Conv2d via cuDNN), masked

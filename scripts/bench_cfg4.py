@@ -3,7 +3,8 @@ batch 64, 10 s synthetic spectrograms, one full training step (forward, CTC, bac
 clip + SGD) per timed iteration on one GPU.  Unidirectional models carry the Lookahead
 (context 20) + Hardtanh head of model.py:329-333.
 
-usage: python scripts/bench_cfg4.py [--bidir 0|1] [--steps K] [--warmup W] [--batch N]
+usage: python scripts/bench_cfg4.py [--bidir 0|1] [--rnn-gemm fp32|bf16] [--steps K]
+                                   [--warmup W] [--batch N]
 """
 import argparse
 import json
@@ -27,6 +28,8 @@ def main():
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--hidden", type=int, default=1024)
     ap.add_argument("--layers", type=int, default=7)
+    ap.add_argument("--rnn-gemm", choices=["fp32", "bf16"], default="fp32",
+                    help="precision of the recurrent layers' GEMMs (cfg4 names bf16)")
     args = ap.parse_args()
     from ds2amd import model as dsm
     from ds2amd.trainer import Trainer
@@ -34,7 +37,7 @@ def main():
     torch.manual_seed(123456)
     m = dsm.DeepSpeech(rnn_type='lstm', labels=bench.LABELS, rnn_hidden_size=args.hidden,
                        nb_layers=args.layers, audio_conf=bench.CONF,
-                       bidirectional=bool(args.bidir))
+                       bidirectional=bool(args.bidir), rnn_gemm_precision=args.rnn_gemm)
     tr = Trainer(m, bench.LABELS, lr=3e-4, momentum=0.9, max_norm=100.0, device=dev)
     bench.BATCH = args.batch
     x, tg, pct, ts = bench.synthetic_batch(0)
@@ -53,7 +56,8 @@ def main():
     dt = time.perf_counter() - t0
     print(json.dumps({
         "config": f"cfg4: {args.layers}x{'Bi' if args.bidir else ''}LSTM-{args.hidden}"
-                  f"{'' if args.bidir else ' + lookahead(20)'}, batch {args.batch}, 10 s, fp32",
+                  f"{'' if args.bidir else ' + lookahead(20)'}, batch {args.batch}, 10 s, "
+                  f"RNN GEMMs {args.rnn_gemm}, recurrence + rest fp32",
         "audio_seconds_per_sec": round(args.batch * bench.SECONDS * args.steps / dt, 2),
         "ms_per_step": round(dt * 1e3 / args.steps, 2), "loss": round(float(loss), 4),
         "steps": args.steps}), flush=True)

@@ -154,6 +154,48 @@ def test_lstm_1024_forward_matches_oracle(dev, bidir):
     assert _rel(probs, rp) < REL
 
 
+@pytest.mark.parametrize("rnn_type,bidir", [('lstm', True), ('lstm', False), ('gru', True)])
+def test_bf16_rnn_gemms_track_the_fp32_oracle(dev, rnn_type, bidir):
+    """BASELINE cfg4's opt-in precision: the recurrent layers' GEMMs (input projection,
+    dX, dW_ih, dW_hh) on bf16 operands with fp32 accumulation.  Same weights, same batch:
+    logits within 2e-2 (relative to max |logit|) of the fp32 oracle, loss within 1 %,
+    recurrent-layer weight gradients within 1e-1 (bf16 activations and gate gradients
+    compound over the 3 layers; a layout error would be O(1)); the fp32 model is bit-for-bit unaffected by the switch
+    being available (rnn_gemm_precision defaults to 'fp32')."""
+    from ds2amd.ctc import CTCLoss
+    m = build(91, 256, 3, rnn_type=rnn_type, bidirectional=bidir).to(dev).train()
+    m16 = build(91, 256, 3, rnn_type=rnn_type, bidirectional=bidir).to(dev).train()
+    m16.set_rnn_gemm_precision('bf16')
+    assert m16.rnns[1].rnn.gemm_precision == 'bf16' and m.rnns[1].rnn.gemm_precision == 'fp32'
+    o = orc.OracleDS2({k: v.detach().cpu() for k, v in m.state_dict().items()}, 3, 256,
+                      bidirectional=bidir, rnn_type=rnn_type)
+    g = torch.Generator().manual_seed(4)
+    t_list = [161, 150, 120, 97]
+    x = torch.zeros(4, 1, 161, 161)
+    for i, t in enumerate(t_list):
+        x[i, 0, :, :t] = torch.randn(161, t, generator=g)
+    sizes = torch.IntTensor(t_list)
+    tg = torch.randint(1, 29, (4 * 20,), generator=g, dtype=torch.int32)
+    tl = torch.full((4,), 20, dtype=torch.int32)
+    with torch.no_grad():
+        rl, _, ro, _ = o.forward(x, sizes, training=True)
+    losses, grads = [], []
+    for mm in (m, m16):
+        logits, _, out_lens = mm(x.to(dev), sizes)
+        if mm is m:
+            assert _rel(logits, rl) < REL                        # fp32 path unchanged
+        else:
+            assert _rel(logits, rl) < 2e-2
+        loss = CTCLoss()(logits.transpose(0, 1), tg, out_lens, tl)
+        loss.backward()
+        losses.append(float(loss))
+        grads.append({k: p.grad.detach().cpu().clone() for k, p in mm.named_parameters()})
+    assert abs(losses[1] - losses[0]) <= 1e-2 * abs(losses[0])
+    for k, g32 in grads[0].items():
+        if k.startswith('rnns.'):
+            assert _rel(grads[1][k], g32) < 1e-1, k
+
+
 def test_cfg2_shape_step_properties(dev):
     """Full benchmark shape (bs32, 10 s): a train step is finite, deterministic and
     decodes identically to the oracle decoder on the same probs."""

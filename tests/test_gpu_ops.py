@@ -66,6 +66,43 @@ def test_sgemm_full_rounds_plus_split_tail(dev, ta, tb, mode, monkeypatch):
     _close(cd, ref, 1e-5, "sgemm main+tail")
 
 
+@pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
+@pytest.mark.parametrize("m,n,k", [(4, 4, 4), (36, 52, 28), (128, 128, 64), (300, 256, 516),
+                                   (516, 2400, 132), (256, 300, 5000),      # split-K tail
+                                   (128 * 29, 128 * 27 + 52, 2080)])       # rounds + tail
+def test_sgemm_bf16(dev, ta, tb, m, n, k):
+    """bf16-operand GEMM (BASELINE cfg4): operands rounded to bf16 (nearest even) on the
+    way in, exact products, fp32 accumulation.  Reference: the same bf16 roundings done by
+    torch on the host, multiplied in fp64 -- so only the fp32 summation differs (1e-5)."""
+    g = torch.Generator().manual_seed(m * 7 + n * 3 + k + 1)
+    a = torch.randn(k, m, generator=g) if ta else torch.randn(m, k, generator=g)
+    b = torch.randn(n, k, generator=g) if tb else torch.randn(k, n, generator=g)
+    c0 = torch.randn(m, n, generator=g)
+    bias = torch.randn(n, generator=g)
+    rb = lambda t: t.to(torch.bfloat16).double()
+    ref = 0.5 * ((rb(a).t() if ta else rb(a)) @ (rb(b).t() if tb else rb(b))) \
+        + 0.25 * c0.double() + bias.double()
+    ad, bd, cd = a.to(dev), b.to(dev), c0.to(dev).clone()
+    ops.sgemm(ad, bd, cd, m=m, n=n, k=k, trans_a=bool(ta), trans_b=bool(tb),
+              lda=ad.shape[1], ldb=bd.shape[1], ldc=n, alpha=0.5, beta=0.25, bias=bias.to(dev),
+              bf16=True)
+    torch.cuda.synchronize()
+    _close(cd, ref, 1e-5, "sgemm bf16")
+    # and it is a bf16 product: far from the fp32 one at this scale
+    full = 0.5 * ((a.t() if ta else a).double() @ (b.t() if tb else b).double()) \
+        + 0.25 * c0.double() + bias.double()
+    if k >= 28:
+        assert (cd.double().cpu() - full).abs().max() > 1e-4 * full.abs().max()
+
+
+def test_sgemm_bf16_rejects_unaligned(dev):
+    a = torch.randn(8, 6, device=dev)
+    b = torch.randn(6, 8, device=dev)
+    c = torch.empty(8, 8, device=dev)
+    with pytest.raises(_lib.Ds2Error):
+        ops.sgemm(a, b, c, m=8, n=8, k=6, lda=6, ldb=8, ldc=8, bf16=True)
+
+
 # ---------------------------------------------------------------------------- conv
 CONVS = [  # (n, ci, h, w, co, kh, kw, sh, sw, ph, pw)
     (2, 1, 161, 37, 32, 41, 11, 2, 2, 20, 5),
