@@ -302,6 +302,10 @@ __global__ __launch_bounds__(GT) void gru_fwd_persist_kernel(
     bias_n = bh[2 * H + j];
     len = lens[n];
   }
+  settle(bias_r);
+  settle(bias_z);
+  settle(bias_n);
+  settle(len);
   constexpr int RP = 3 * GU + 1;
   __shared__ float red[GW * GB * RP];
   float g_r = 0.f, g_z = 0.f, g_n = 0.f, g_hn = 0.f;   // gate cache of the previous step
@@ -484,6 +488,10 @@ __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     bias_n = bh[2 * H + j];
     len = lens[n];
   }
+  settle(bias_r);
+  settle(bias_z);
+  settle(bias_n);
+  settle(len);
   // this thread's slot in the transposed tile: (q = u >> 2, r = m, c = u & 3)
   const int tpos = ((u >> 2) * GB + m) * 4 + (u & 3);
   float g_r = 0.f, g_z = 0.f, g_n = 0.f, g_hn = 0.f, h_own = 0.f;
@@ -536,6 +544,11 @@ __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
 #pragma unroll
       for (int r = 0; r < 4; ++r)
         red[(wave * GB + (lane >> 4) * 4 + r) * RP + g * GU + (lane & 15)] = acc[g][r];
+    // the step's xproj loads are consumed on every path here (not at the next step's
+    // re-initialisation, where the waitcnt pass would wait for the hand-off stores too)
+    settle(xr);
+    settle(xz);
+    settle(xn);
     __syncthreads();
     if (SENT && failed) {
       poison_rest(h_all, s, T, d != 0, N, D, n, d, H, j, H, 1, owner);
@@ -643,7 +656,8 @@ __global__ __launch_bounds__(GT) void gru_bwd_persist_kernel(
   const int n = n0 + m;
   const int j = ub * GU + u;
   const bool owner = threadIdx.x < GB * GU && n < N && j < H;
-  const int len = owner ? lens[n] : 0;
+  int len = owner ? lens[n] : 0;
+  settle(len);
   constexpr int RP = GU + 1;
   float dh_prev = 0.f, z_prev = 0.f;        // this thread's unit, carried in registers
   // trace mode (DS2_GRU_STAMPS=2, as in the forward kernel)
@@ -798,13 +812,18 @@ __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     for (int i = 0; i < NBW; ++i)
 #pragma unroll
       for (int c = 0; c < 4; ++c) w[i][c] = i < nb ? wc[(int64_t)(16 * i + c) * H] : 0.f;
+    // pending at loop entry, these loads made the in-loop zero-initialisations of the
+    // step's prefetch registers wait for the previous step's hand-off stores (settle)
+#pragma unroll
+    for (int i = 0; i < NBW; ++i) settle(w[i]);
   }
   const int m = threadIdx.x >> 4;
   const int u = threadIdx.x & 15;
   const int n = n0 + m;
   const int j = ub * GU + u;
   const bool owner = threadIdx.x < GB * GU && n < N;
-  const int len = owner ? lens[n] : 0;
+  int len = owner ? lens[n] : 0;
+  settle(len);
   const int tpos = ((u >> 2) * GB + m) * 4 + (u & 3);
   float dh_prev = 0.f, z_prev = 0.f;
   float px_dar = 0.f, px_daz = 0.f, px_dan = 0.f, px_dghn = 0.f;
@@ -854,6 +873,12 @@ __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
 #pragma unroll
     for (int r = 0; r < 4; ++r)
       red[(wave * GB + (lane >> 4) * 4 + r) * RP + (lane & 15)] = acc0[r] + acc1[r];
+    settle(dyv);                      // consumed here on every path (see the forward)
+    settle(g_r);
+    settle(g_z);
+    settle(g_n);
+    settle(g_hn);
+    settle(hp);
     __syncthreads();
     if (SENT && failed) {
       poison_rest(dgx, s, T, d == 0, N, D, n, d, H, j, H3, 3, owner);

@@ -294,6 +294,9 @@ __global__ __launch_bounds__(GT) void lstm_fwd_persist_kernel(
     for (int g = 0; g < 4; ++g) bias[g] = bh[g * H + j];
     len = lens[n];
   }
+#pragma unroll
+  for (int g = 0; g < 4; ++g) settle(bias[g]);
+  settle(len);
   float c = 0.f;
   LstmFwdOut prev{0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   int64_t prev_row = -1;
@@ -410,7 +413,8 @@ __global__ __launch_bounds__(GT) void lstm_bwd_persist_kernel(
   const int n = n0 + m;
   const int j = ub * GU + u;
   const bool owner = threadIdx.x < GB * GU && n < N && j < H;
-  const int len = owner ? lens[n] : 0;
+  int len = owner ? lens[n] : 0;
+  settle(len);
   constexpr int RP = GU + 1;
   float carry = 0.f;
 

@@ -218,6 +218,13 @@ __device__ __forceinline__ void group_arrive(unsigned* ctr) {
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 constexpr int kSc1 = 16;   // buffer-op aux bit: sc1 (write-through store / L1-bypassing load)
 
+// Wait for a loaded value HERE, once: a loop-invariant load first used inside the step loop
+// makes the waitcnt pass put a conservative vmcnt(0) at that use on EVERY iteration, which
+// then also waits for the previous step's write-through hand-off stores (gru_fwd_dop_kernel:
+// 1.16 us of a 5.5 us step).  "+v" forces the value into a VGPR and redefines it.
+template <typename T>
+__device__ __forceinline__ void settle(T& v) { asm volatile("" : "+v"(v)); }
+
 // Sentinel-ring hand-off of the direct-operand kernels (the data is the flag; the R2 idea
 // of cdna_hip_programming.md G16 without widening the payload).  Each producer tile lives
 // in a ring of kRingSlots slots; a slot that will next hold step s + 2 is refilled with the
