@@ -422,10 +422,12 @@ __global__ __launch_bounds__(GT) void gru_fwd_persist_kernel(
 // rewritten two steps later, after every consumer of the group has published the step
 // in between, i.e. after all its loads of the slot have returned.
 //
-// SENT = true: sentinel-ring hand-off (rnn_common.h, kRingSlots slots, no flags): every
-// wave spins on its own producers' tiles, so the wait, the poll round trip and the
-// producer's drain-before-flag all leave the critical path.
-template <int NBW, bool SENT>
+// HM (hand-off mode): 0 = per-producer flags (above); 1 = sentinel ring (rnn_common.h,
+// kRingSlots slots, no flags): every wave spins on its own producers' tiles, so the wait,
+// the poll round trip and the producer's drain-before-flag all leave the critical path;
+// 2 = hybrid: the flag poll of mode 0 tells a consumer when to load, the sentinel ring of
+// mode 1 validates what it loads, so the producer stores its flag without draining first.
+template <int NBW, int HM>
 __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void gru_fwd_dop_kernel(
     int T, int N, int H, int D, int UB, int BT, const float* __restrict__ xproj,
     const float* __restrict__ w_f, const float* __restrict__ w_r, const float* __restrict__ b_f,
@@ -446,6 +448,8 @@ __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   const unsigned* gflags = counters + (D * BT + 1) + (d * BT + bt) * UB;
   unsigned* myflag = counters + (D * BT + 1) + (d * BT + bt) * UB + ub;
   const int slot_floats = D * BT * UB * 256;
+  constexpr bool SENT = HM != 0;     // sentinel ring: tiles validate themselves
+  constexpr bool FLAG = HM != 1;     // per-producer flags polled before loading
   constexpr int NSLOT = SENT ? kRingSlots : 2;
   const __amdgpu_buffer_rsrc_t x_rs =
       __builtin_amdgcn_make_buffer_rsrc(hx, (short)0, NSLOT * slot_floats * 4, 0x00020000);
@@ -511,7 +515,7 @@ __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     for (int g = 0; g < 3; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
     trace_at(s, 0);
     if (s > 0) {
-      if (!SENT && !flags_wait(gflags, UB, (unsigned)s, err, &flag)) {
+      if (FLAG && !flags_wait(gflags, UB, (unsigned)s, err, &flag)) {
         poison_rest(h_all, s, T, d != 0, N, D, n, d, H, j, H, 1, owner);
         return;
       }
@@ -594,6 +598,8 @@ __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
         const u32x4 sv = u32x4{kSentinel, kSentinel, kSentinel, kSentinel};
         __builtin_amdgcn_raw_buffer_store_b128(sv, x_rs, ((s + 2) % NSLOT) * slot_floats * 4 + toff,
                                                0, kSc1);
+        if (FLAG && lane == 0)      // hybrid: no drain, the consumer validates the tile
+          __hip_atomic_store(myflag, (unsigned)s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       } else {
         const u32x4 v = *reinterpret_cast<const u32x4*>(tile + lane * 4);
         __builtin_amdgcn_raw_buffer_store_b128(v, x_rs, (s & 1) * slot_floats * 4 + toff, 0, kSc1);
@@ -762,8 +768,8 @@ __global__ __launch_bounds__(GT) void gru_bwd_persist_kernel(
 //   gx[slot][d][bt][3 UB blocks][q][r][c],
 // whose block order is the k order of dgh; wave w owns blocks [b0, b0 + nb) of the 3 UB.
 // dgh (for the weight-gradient GEMM) and dgx are stored after the flag.
-// SENT selects the sentinel-ring hand-off as in gru_fwd_dop_kernel.
-template <int NBW, bool SENT>
+// HM selects the hand-off form as in gru_fwd_dop_kernel.
+template <int NBW, int HM>
 __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void gru_bwd_dop_kernel(
     int T, int N, int H, int D, int UB, int BT, const float* __restrict__ dy, int dyd,
     const float* __restrict__ w_f, const float* __restrict__ w_r,
@@ -787,6 +793,8 @@ __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   const unsigned* gflags = counters + (D * BT + 1) + (d * BT + bt) * UB;
   unsigned* myflag = counters + (D * BT + 1) + (d * BT + bt) * UB + ub;
   const int slot_floats = D * BT * NB3 * 256;
+  constexpr bool SENT = HM != 0;     // sentinel ring: tiles validate themselves
+  constexpr bool FLAG = HM != 1;     // per-producer flags polled before loading
   constexpr int NSLOT = SENT ? kRingSlots : 2;
   const __amdgpu_buffer_rsrc_t x_rs =
       __builtin_amdgcn_make_buffer_rsrc(gx, (short)0, NSLOT * slot_floats * 4, 0x00020000);
@@ -846,7 +854,7 @@ __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
       if (tp >= 0 && tp < T) hp = h_all[(((int64_t)tp * N + n) * D + d) * H + j];
     }
     if (s > 0) {
-      if (!SENT && !flags_wait(gflags, UB, (unsigned)s, err, &flag)) {
+      if (FLAG && !flags_wait(gflags, UB, (unsigned)s, err, &flag)) {
         poison_rest(dgx, s, T, d == 0, N, D, n, d, H, j, H3, 3, owner);
         return;
       }
@@ -930,6 +938,8 @@ __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
 #pragma unroll
         for (int g = 0; g < 3; ++g)
           __builtin_amdgcn_raw_buffer_store_b128(sv, x_rs, sn + g * UB * 1024, 0, kSc1);
+        if (FLAG && lane == 0)      // hybrid: no drain, the consumer validates the tiles
+          __hip_atomic_store(myflag, (unsigned)s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       } else {
         const int so = (s & 1) * slot_floats * 4 + toff;
 #pragma unroll
@@ -979,21 +989,22 @@ static inline int dop_enabled() {
 }
 constexpr unsigned kDopPadLds = 80 * 1024;
 // smallest instantiated blocks-per-wave >= need (extra blocks are predicated off)
-// hand-off form of the direct-operand kernels: sentinel ring or per-producer flags.
-// DS2_RNN_HANDOFF_FWD / _BWD (or DS2_RNN_HANDOFF for both) = "sentinel" | "flags";
-// defaults: sentinel forward, flags backward (the measured faster forms)
-static inline bool sentinel_mode(bool fwd) {
+// hand-off form of the direct-operand kernels (template HM): per-producer flags (0),
+// sentinel ring (1) or hybrid (2).  DS2_RNN_HANDOFF_FWD / _BWD (or DS2_RNN_HANDOFF for
+// both) = "flags" | "sentinel" | "hybrid"; defaults: the measured faster forms.
+static inline int handoff_mode(bool fwd) {
   const char* e = getenv(fwd ? "DS2_RNN_HANDOFF_FWD" : "DS2_RNN_HANDOFF_BWD");
   if (e == nullptr || e[0] == 0) e = getenv("DS2_RNN_HANDOFF");
-  if (e == nullptr || e[0] == 0) return fwd;
-  return e[0] == 's';
+  if (e == nullptr || e[0] == 0) return fwd ? 1 : 0;
+  return e[0] == 's' ? 1 : (e[0] == 'h' ? 2 : 0);
 }
 static const void* bwd_dop_fn(int need) {
-  const bool sent = sentinel_mode(false);
+  const int hm = handoff_mode(false);
 #define DS2_BDOP(K)                                                                      \
   if (need <= K)                                                                         \
-    return sent ? reinterpret_cast<const void*>(gru_bwd_dop_kernel<K, true>)             \
-                : reinterpret_cast<const void*>(gru_bwd_dop_kernel<K, false>);
+    return hm == 1 ? reinterpret_cast<const void*>(gru_bwd_dop_kernel<K, 1>)             \
+         : hm == 2 ? reinterpret_cast<const void*>(gru_bwd_dop_kernel<K, 2>)             \
+                   : reinterpret_cast<const void*>(gru_bwd_dop_kernel<K, 0>);
   DS2_BDOP(1) DS2_BDOP(2) DS2_BDOP(3) DS2_BDOP(4) DS2_BDOP(6) DS2_BDOP(8) DS2_BDOP(10)
   DS2_BDOP(13) DS2_BDOP(16) DS2_BDOP(19) DS2_BDOP(22) DS2_BDOP(24)
 #undef DS2_BDOP
@@ -1079,14 +1090,15 @@ ds2_status_t ds2_gru_fwd(int t_max, int n, int h, int num_dirs, const float* xpr
                                            align256(counter_bytes(n, num_dirs)));
     void* args[] = {&T_, &N_, &H_, &D_, &UB_, &BT_, &xproj, &w_hh_f, &w_hh_r, &b_hh_f,
                     &b_hh_r, &lens, &h_all, &gates, &ring, &ctrs, &err, &stamps};
-    const bool sent = sentinel_mode(true);
-    if (sent && ring_reset(ring, n, h, num_dirs, 1, st) != hipSuccess)
+    const int hm = handoff_mode(true);
+    if (hm != 0 && ring_reset(ring, n, h, num_dirs, 1, st) != hipSuccess)
       return launch_status("ds2_gru ring");
     const void* fn = nullptr;
 #define DS2_FDOP(K)                                                                  \
   case K:                                                                            \
-    fn = sent ? reinterpret_cast<const void*>(gru_fwd_dop_kernel<K, true>)           \
-              : reinterpret_cast<const void*>(gru_fwd_dop_kernel<K, false>);         \
+    fn = hm == 1 ? reinterpret_cast<const void*>(gru_fwd_dop_kernel<K, 1>)           \
+       : hm == 2 ? reinterpret_cast<const void*>(gru_fwd_dop_kernel<K, 2>)           \
+                 : reinterpret_cast<const void*>(gru_fwd_dop_kernel<K, 0>);          \
     break;
     switch ((UB + GW - 1) / GW) {
       DS2_FDOP(1) DS2_FDOP(2) DS2_FDOP(3) DS2_FDOP(4) DS2_FDOP(5) DS2_FDOP(6) DS2_FDOP(7)
@@ -1188,7 +1200,7 @@ ds2_status_t ds2_gru_bwd(int t_max, int n, int h, int num_dirs, const float* dy,
                                            align256(counter_bytes(n, num_dirs)));
     void* args[] = {&T_, &N_, &H_, &D_, &UB_, &BT_, &dy, &DYD_, &w_hh_f, &w_hh_r, &h_all,
                     &gates, &lens, &dgates_x, &dgates_h, &ring, &ctrs, &err, &stamps};
-    if (sentinel_mode(false) && ring_reset(ring, n, h, num_dirs, 3, st) != hipSuccess)
+    if (handoff_mode(false) != 0 && ring_reset(ring, n, h, num_dirs, 3, st) != hipSuccess)
       return launch_status("ds2_gru ring");
     const void* fn = bwd_dop_fn((3 * UB + GW - 1) / GW);
     if (fn != nullptr &&

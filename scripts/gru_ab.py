@@ -52,7 +52,8 @@ def timed(fn, reps=5):
 
 
 variants = {"dop-flags": {"DS2_GRU_DOP": "1", "DS2_RNN_HANDOFF": "flags"},
-            "dop-sentinel": {"DS2_GRU_DOP": "1", "DS2_RNN_HANDOFF": "sentinel"}}
+            "dop-sentinel": {"DS2_GRU_DOP": "1", "DS2_RNN_HANDOFF": "sentinel"},
+            "dop-hybrid": {"DS2_GRU_DOP": "1", "DS2_RNN_HANDOFF": "hybrid"}}
 if len(sys.argv) > 1 and sys.argv[1] == "all":
     variants = {"staged": {"DS2_GRU_DOP": "0"}, **variants}
 rounds = int(os.environ.get("AB_ROUNDS", "3"))

@@ -324,10 +324,11 @@ def test_gru_direct_operand_equals_staged(dev, n, h, bidir, monkeypatch):
 
 
 @pytest.mark.parametrize("n,h,bidir", [(32, 64, True), (20, 800, True), (7, 48, False)])
-def test_gru_sentinel_handoff_equals_flag_handoff(dev, n, h, bidir, monkeypatch):
-    """The sentinel-ring and the per-producer-flag hand-offs of the direct-operand
-    recurrences synchronise differently but sum in the same order: bit-identical outputs
-    and gradients (ragged lengths, so producers finish their sequences unevenly)."""
+def test_gru_handoff_forms_agree(dev, n, h, bidir, monkeypatch):
+    """The per-producer-flag, sentinel-ring and hybrid (flag poll + sentinel-validated
+    tiles, no drain before the flag) hand-offs of the direct-operand recurrences
+    synchronise differently but sum in the same order: bit-identical outputs and
+    gradients (ragged lengths, so producers finish their sequences unevenly)."""
     t, inp = 37, 40
     nd = 2 if bidir else 1
     g = torch.Generator().manual_seed(h + 3 * n)
@@ -339,7 +340,7 @@ def test_gru_sentinel_handoff_equals_flag_handoff(dev, n, h, bidir, monkeypatch)
     dy = torch.randn(t, n, h, generator=g)
     outs = []
     monkeypatch.setenv("DS2_GRU_DOP", "1")
-    for mode in ("flags", "sentinel"):
+    for mode in ("flags", "sentinel", "hybrid"):
         monkeypatch.setenv("DS2_RNN_HANDOFF", mode)
         ws = [w.to(dev).requires_grad_(True) for w in weights]
         xd = x.to(dev).requires_grad_(True)
@@ -347,9 +348,9 @@ def test_gru_sentinel_handoff_equals_flag_handoff(dev, n, h, bidir, monkeypatch)
         y.backward(dy.to(dev))
         torch.cuda.synchronize()
         outs.append([y.detach().cpu(), xd.grad.cpu()] + [w.grad.cpu() for w in ws])
-    for a, b in zip(*outs):
+    for a, b, c in zip(*outs):
         assert torch.isfinite(a).all()
-        assert torch.equal(a, b)
+        assert torch.equal(a, b) and torch.equal(a, c)
 
 
 def test_gru_per_direction_output(dev):
