@@ -307,6 +307,11 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
   __shared__ int order[BEAM_CMAX];
   __shared__ int b_node[2][BEAM_MAX], b_last[2][BEAM_MAX];
   __shared__ float b_pb[2][BEAM_MAX], b_pnb[2][BEAM_MAX];
+  // per-entry copies of the entry's trie node's parent and best last-char log-prob, so
+  // the per-frame chain has no global-memory reads (the trie is written, never read,
+  // until the final back-tracking)
+  __shared__ int b_par[2][BEAM_MAX];
+  __shared__ float b_lpc[2][BEAM_MAX];
   __shared__ float score[BEAM_MAX];
   __shared__ int pidx[BEAM_MAX];
   __shared__ signed char child_of[BEAM_MAX * BEAM_CMAX];
@@ -327,20 +332,23 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
 
   if (lane == 0) {
     b_node[0][0] = 0; b_last[0][0] = -1; b_pb[0][0] = 0.f; b_pnb[0][0] = -INFINITY;
+    b_par[0][0] = -1; b_lpc[0][0] = -INFINITY;
     par[0] = -1; chr[0] = -1; tst[0] = -1; lpcv[0] = -INFINITY;
     s_nb = 1;
     s_nodes = 1;
   }
   __syncthreads();
   int cur = 0;
+  float pv_next = (lane < C && size > 0) ? pn[lane] : 0.f;   // frame t + 1 loads during frame t
   for (int t = 0; t < size; ++t) {
     const int nb = s_nb;
     if (nb == 0) break;
     // ---- vocabulary pruning and log probs
     float pv = 0.f;
     if (lane < C) {
-      pv = pn[(int64_t)t * stride_t + lane];
+      pv = pv_next;
       lp[lane] = logf(pv + 1.17549435e-38f);
+      if (t + 1 < size) pv_next = pn[(int64_t)(t + 1) * stride_t + lane];
     }
     if (prune) {
       int rank = 0;
@@ -366,7 +374,7 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
     if (lane < nb) {
       score[lane] = beam_lse(b_pb[cur][lane], b_pnb[cur][lane]);
       const int nd = b_node[cur][lane];
-      const int pnode = nd > 0 ? par[nd] : -1;
+      const int pnode = nd > 0 ? b_par[cur][lane] : -1;
       int j = -1;
       for (int i = 0; i < nb; ++i)
         if (pnode >= 0 && b_node[cur][i] == pnode) j = i;
@@ -393,7 +401,8 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
                               : lp[last_i] + score[j];
           pnb = beam_lse(pnb, e);
           const int nd = b_node[cur][i];
-          if (lp[last_i] > lpcv[nd]) {
+          if (lp[last_i] > b_lpc[cur][i]) {   // one blank candidate per entry: no race
+            b_lpc[cur][i] = lp[last_i];
             lpcv[nd] = lp[last_i];
             tst[nd] = t;
           }
@@ -454,6 +463,8 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
         if (c == blank) {
           b_node[nxt][r] = b_node[cur][i];
           b_last[nxt][r] = b_last[cur][i];
+          b_par[nxt][r] = b_par[cur][i];
+          b_lpc[nxt][r] = b_lpc[cur][i];
         } else {
           par[nodes] = b_node[cur][i];
           chr[nodes] = c;
@@ -461,6 +472,8 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
           lpcv[nodes] = lp[c];
           b_node[nxt][r] = nodes;
           b_last[nxt][r] = c;
+          b_par[nxt][r] = b_node[cur][i];
+          b_lpc[nxt][r] = lp[c];
           ++nodes;
         }
         b_pb[nxt][r] = cpb[k];

@@ -9,6 +9,7 @@ frame equal to the previous *frame* is dropped, the space label maps to ' ' and
 """
 from __future__ import annotations
 
+import numpy as np
 import torch
 
 from . import ops
@@ -84,13 +85,16 @@ class BeamCTCDecoder(Decoder):
 
     def decode(self, probs, sizes=None):
         ids, offs, lens, _ = self.decode_raw(probs, sizes)
-        ids, offs, lens = ids.cpu(), offs.cpu(), lens.cpu()
+        # one device->host copy, then vectorised id->char lookups (a per-element tensor
+        # loop here cost more than the beam search itself on 30 s utterances)
+        ids, offs, lens = ids.cpu().numpy(), offs.cpu(), lens.cpu().numpy()
+        lut = np.array([self.int_to_char[i] for i in range(len(self.labels))])
         strings, offsets = [], []
         for b in range(ids.shape[0]):
             sb, ob = [], []
             for p in range(ids.shape[1]):
                 k = int(lens[b, p])
-                sb.append(''.join(self.int_to_char[int(x)] for x in ids[b, p, :k]))
+                sb.append(''.join(lut[ids[b, p, :k]].tolist()))
                 ob.append(offs[b, p, :k].clone() if k > 0 else torch.tensor([], dtype=torch.int))
             strings.append(sb)
             offsets.append(ob)
