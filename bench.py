@@ -293,9 +293,3 @@ def main():
 
 if __name__ == "__main__":
     main()
-    # leave without running the interpreter's teardown: under rocprofv3 the profiler's
-    # exit-time handlers and the HIP runtime's static destructors have crashed at exit
-    # (SIGSEGV after all output was written)
-    sys.stdout.flush()
-    sys.stderr.flush()
-    os._exit(0)
