@@ -62,6 +62,16 @@ __device__ __forceinline__ float log_add(float a, float b) {
   return m + log1pf(expf(-fabsf(a - b)));
 }
 
+// log(exp(a) + exp(b)) on the hardware v_exp_f32 / v_log_f32 (about 1 ulp each): the CTC
+// alpha/beta recursions are a dependent chain of these, and log1pf/expf cost ~10x the
+// instructions.  log(1 + x) for x = exp(-|a - b|) <= 1 loses only terms below ulp(m).
+__device__ __forceinline__ float log_add_fast(float a, float b) {
+  if (a == -INFINITY) return b;
+  if (b == -INFINITY) return a;
+  const float m = fmaxf(a, b);
+  return m + __logf(1.0f + __expf(-fabsf(a - b)));
+}
+
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
 
 }  // namespace ds2
