@@ -74,4 +74,13 @@ __device__ __forceinline__ float log_add_fast(float a, float b) {
 
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
 
+// Gate nonlinearities on v_exp_f32 / v_rcp_f32 (absolute error ~1e-7) for the recurrences'
+// per-step critical path; tanh(x) = 1 - 2 / (1 + e^{2x}) saturates correctly at +-inf.
+__device__ __forceinline__ float sigmoid_fast(float x) {
+  return __builtin_amdgcn_rcpf(1.0f + __expf(-x));
+}
+__device__ __forceinline__ float tanh_fast(float x) {
+  return 1.0f - 2.0f * __builtin_amdgcn_rcpf(1.0f + __expf(2.0f * x));
+}
+
 }  // namespace ds2

@@ -575,9 +575,9 @@ __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
         float ghn = gh[2] + bias_n;
         float r = 0.f, z = 0.f, nn = 0.f;
         if (t < len) {
-          r = sigmoidf_(ghr + xr);
-          z = sigmoidf_(ghz + xz);
-          nn = tanhf(xn + r * ghn);
+          r = sigmoid_fast(ghr + xr);
+          z = sigmoid_fast(ghz + xz);
+          nn = tanh_fast(xn + r * ghn);
           hout = (h_own - nn) * z + nn;
         } else {
           ghn = 0.f;

@@ -35,12 +35,12 @@ struct LstmFwdOut {
 
 __device__ __forceinline__ LstmFwdOut lstm_cell(float ai, float af, float ag, float ao, float cp) {
   LstmFwdOut r;
-  r.i = sigmoidf_(ai);
-  r.f = sigmoidf_(af);
-  r.g = tanhf(ag);
-  r.o = sigmoidf_(ao);
+  r.i = sigmoid_fast(ai);
+  r.f = sigmoid_fast(af);
+  r.g = tanh_fast(ag);
+  r.o = sigmoid_fast(ao);
   r.c = r.f * cp + r.i * r.g;
-  r.h = r.o * tanhf(r.c);
+  r.h = r.o * tanh_fast(r.c);
   return r;
 }
 
@@ -49,7 +49,7 @@ __device__ __forceinline__ LstmFwdOut lstm_cell(float ai, float af, float ag, fl
 __device__ __forceinline__ float lstm_cell_bwd(float dh, float dc_carry, float gi, float gf,
                                                float gg, float go, float c, float cp,
                                                float& dai, float& daf, float& dag, float& dao) {
-  const float tc = tanhf(c);
+  const float tc = tanh_fast(c);
   const float dc = dc_carry + dh * go * (1.f - tc * tc);
   dao = dh * tc * go * (1.f - go);
   dai = dc * gg * gi * (1.f - gi);
