@@ -217,11 +217,15 @@ __device__ __forceinline__ bool sum_pairs(const double* __restrict__ partial, in
   const int grp = threadIdx.x >> 6;
   c = blockIdx.x * 64 + lane;
   double a = 0.0, b = 0.0;
-  if (c < C)
+  // unrolled so that 8 partials' loads are in flight at once (the sums keep their order):
+  // one dependent load per iteration made these finals latency-bound (~18 us each)
+  if (c < C) {
+#pragma unroll 8
     for (int p = grp; p < nparts; p += 4) {
       a += partial[((int64_t)p * C + c) * 2 + 0];
       b += partial[((int64_t)p * C + c) * 2 + 1];
     }
+  }
   red[0][grp][lane] = a;
   red[1][grp][lane] = b;
   __syncthreads();

@@ -343,7 +343,8 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ partial, int N, in
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < per;
        i += (int64_t)gridDim.x * blockDim.x) {
     float s = 0.f;
-    for (int n = 0; n < N; ++n) s += partial[(int64_t)n * per + i];
+#pragma unroll 8
+    for (int n = 0; n < N; ++n) s += partial[(int64_t)n * per + i];   // loads in flight, order kept
     dw[i] = s;
   }
 }

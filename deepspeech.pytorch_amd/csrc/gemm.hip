@@ -645,7 +645,8 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ partial, int M, i
     const int col = (tile % tn) * bn + e % bn;
     if (row >= M || col >= N) continue;
     float acc = 0.f;
-    for (int sp = 0; sp < nsplit; ++sp)
+#pragma unroll 8
+    for (int sp = 0; sp < nsplit; ++sp)   // loads in flight, summation order kept
       acc += partial[(((int64_t)b * nsplit + sp) * tail_tiles + lt) * TE + e];
     float* cp = C + b * sC + (int64_t)row * ldc + col;
     float v = alpha * acc + (bias != nullptr ? bias[col] : 0.f);

@@ -111,8 +111,10 @@ __global__ __launch_bounds__(256) void colsum_final_kernel(const double* __restr
   const int grp = threadIdx.x >> 6;
   const int col = blockIdx.x * 64 + lane;
   double s = 0.0;
-  if (col < cols)
-    for (int c = grp; c < chunks; c += 4) s += partial[(int64_t)c * cols + col];
+  if (col < cols) {
+#pragma unroll 8
+    for (int c = grp; c < chunks; c += 4) s += partial[(int64_t)c * cols + col];   // order kept
+  }
   part[grp][lane] = s;
   __syncthreads();
   if (grp == 0 && col < cols) {
@@ -192,6 +194,7 @@ __global__ void sqnorm_partial_kernel(const float* __restrict__ g, int64_t numel
 __global__ void sqnorm_final_kernel(const double* __restrict__ partial, int nparts,
                                     float* __restrict__ out_norm) {
   double acc = 0.0;
+#pragma unroll 8
   for (int i = threadIdx.x; i < nparts; i += blockDim.x) acc += partial[i];
   __shared__ double red[4];
   acc = wave_sum_d(acc);
