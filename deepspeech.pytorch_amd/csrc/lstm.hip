@@ -246,8 +246,13 @@ __global__ __launch_bounds__(GT) void lstm_bwd_step_kernel(
 // ---------------------------------------------------------------------------
 // persistent forward: W_hh fragments (4 gates x KSW k-steps) in registers, cell
 // state in a register of the owning thread, h hand-off through sc1 stores +
-// per-(direction, batch tile) arrival counters.
-template <int KSW>
+// per-(direction, batch tile) arrival counters.  BTS = 16-sample tiles per workgroup:
+// with BTS = 2 every wave runs its W_hh fragments over two tiles of A operands, so a
+// batch whose 16-sample tiles would not fit the chip as one workgroup each (cfg4: 7 x
+// BiLSTM-1024 at batch 64 = 512 workgroups) runs as ONE launch of 32-sample workgroups
+// instead of two consecutive launches (the dependent steps, not the MFMAs, set the pace);
+// the reduction tile then aliases the staged rows.
+template <int KSW, int BTS>
 __global__ __launch_bounds__(GT) void lstm_fwd_persist_kernel(
     int T, int N, int H, int D, int UB, int BT, const float* __restrict__ xproj,
     const float* __restrict__ wp, const float* __restrict__ b_f, const float* __restrict__ b_r,
@@ -255,12 +260,15 @@ __global__ __launch_bounds__(GT) void lstm_fwd_persist_kernel(
     float* __restrict__ gates, unsigned* __restrict__ counters, unsigned* __restrict__ err,
     int use_flags, int n_base) {
   constexpr int PITCH = LKC_FWD + 4;
-  __shared__ __attribute__((aligned(16))) float hs[GB * PITCH];
-  __shared__ float red[GW * GB * LRP];
+  constexpr int RB = GB * BTS;         // samples per workgroup
+  constexpr int HSF = RB * PITCH, REDF = GW * RB * LRP;
+  __shared__ __attribute__((aligned(16))) float hs[BTS == 1 || HSF >= REDF ? HSF : REDF];
+  __shared__ float red_own[BTS == 1 ? REDF : 1];
+  float* red = BTS == 1 ? red_own : hs;
   __shared__ int flag;
   int ub, d, bt;
   if (!map_work(UB * D, BT, UB, ub, d, bt)) return;
-  const int n0 = n_base + bt * GB;     // samples [n_base, ...) of a batch chunk
+  const int n0 = n_base + bt * RB;     // samples [n_base, ...) of a batch chunk
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int KS = H / 4;                    // host guarantees H % 4 == 0, GW * KSW >= KS
@@ -286,7 +294,7 @@ __global__ __launch_bounds__(GT) void lstm_fwd_persist_kernel(
   const int u = threadIdx.x & 15;
   const int n = n0 + m;
   const int j = ub * GU + u;
-  const bool owner = threadIdx.x < GB * GU && n < N && j < H;
+  const bool owner = threadIdx.x < RB * GU && n < N && j < H;
   float bias[4] = {0.f, 0.f, 0.f, 0.f};
   int len = 0;
   if (owner) {
@@ -310,32 +318,40 @@ __global__ __launch_bounds__(GT) void lstm_fwd_persist_kernel(
 #pragma unroll
       for (int g = 0; g < 4; ++g) xg[g] = xp[g * H + j];
     }
-    f32x4 acc[4];
+    f32x4 acc[BTS][4];
 #pragma unroll
-    for (int g = 0; g < 4; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int b = 0; b < BTS; ++b)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) acc[b][g] = f32x4{0.f, 0.f, 0.f, 0.f};
     if (s > 0) {
       if (!(use_flags ? flags_wait(gflags, UB, (unsigned)s, err, &flag)
                       : group_wait(ctr, (unsigned)s * UB, err, &flag))) {
         poison_rest(h_all, s, T, d != 0, N, D, n, d, H, j, H, 1, owner);
         return;
       }
-      stage_rows_sc1<(GB * LKC_FWD / 4 + GT - 1) / GT>(h_all + ((int64_t)tp * N * D + d) * H,
-                                                        D * H, N, n0, H, 4 * GW * KSW, hs, PITCH);
+      stage_rows_sc1<(RB * LKC_FWD / 4 + GT - 1) / GT, RB>(
+          h_all + ((int64_t)tp * N * D + d) * H, D * H, N, n0, H, 4 * GW * KSW, hs, PITCH);
       __syncthreads();
-      const float* hrow = hs + (lane & 15) * PITCH + (lane >> 4) + 4 * a_ks;
 #pragma unroll
-      for (int i = 0; i < KSW; ++i) {
-        const float a = hrow[4 * i];
+      for (int b = 0; b < BTS; ++b) {
+        const float* hrow = hs + (b * GB + (lane & 15)) * PITCH + (lane >> 4) + 4 * a_ks;
 #pragma unroll
-        for (int g = 0; g < 4; ++g)
-          acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, w[g][i], acc[g], 0, 0, 0);
+        for (int i = 0; i < KSW; ++i) {
+          const float a = hrow[4 * i];
+#pragma unroll
+          for (int g = 0; g < 4; ++g)
+            acc[b][g] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, w[g][i], acc[b][g], 0, 0, 0);
+        }
       }
+      if (BTS > 1) __syncthreads();   // every wave's reads of hs done before red overwrites it
     }
 #pragma unroll
-    for (int g = 0; g < 4; ++g)
+    for (int b = 0; b < BTS; ++b)
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        red[(wave * GB + (lane >> 4) * 4 + r) * LRP + g * GU + (lane & 15)] = acc[g][r];
+      for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          red[(wave * RB + b * GB + (lane >> 4) * 4 + r) * LRP + g * GU + (lane & 15)] = acc[b][g][r];
     __syncthreads();
     if (owner) {
       LstmFwdOut o{0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -345,7 +361,7 @@ __global__ __launch_bounds__(GT) void lstm_fwd_persist_kernel(
         for (int g = 0; g < 4; ++g) {
           float v = 0.f;
 #pragma unroll
-          for (int w8 = 0; w8 < GW; ++w8) v += red[(w8 * GB + m) * LRP + g * GU + u];
+          for (int w8 = 0; w8 < GW; ++w8) v += red[(w8 * RB + m) * LRP + g * GU + u];
           gh[g] = v + bias[g] + xg[g];
         }
         o = lstm_cell(gh[0], gh[1], gh[2], gh[3], c);
@@ -374,7 +390,8 @@ __global__ __launch_bounds__(GT) void lstm_fwd_persist_kernel(
 
 // persistent backward: W_hh^T fragments for NCH chunks of 4*GW*KSWC gate columns in
 // registers; dc carried in a register; gate gradients handed off through sc1 stores.
-template <int KSWC, int NCH>
+// BTS as in the forward (BTS = 2 stages 32 rows per chunk: KSWC = 32 keeps them in LDS).
+template <int KSWC, int NCH, int BTS>
 __global__ __launch_bounds__(GT) void lstm_bwd_persist_kernel(
     int T, int N, int H, int D, int UB, int BT, const float* __restrict__ dy, int dyd,
     const float* __restrict__ wpt, const float* __restrict__ c_all,
@@ -382,12 +399,13 @@ __global__ __launch_bounds__(GT) void lstm_bwd_persist_kernel(
     unsigned* __restrict__ counters, unsigned* __restrict__ err, int use_flags, int n_base) {
   constexpr int CW = 4 * GW * KSWC;         // gate columns per chunk (<= LKC_BWD)
   constexpr int PITCH = CW + 4;
-  __shared__ __attribute__((aligned(16))) float hs[GB * PITCH];
+  constexpr int RB = GB * BTS;              // samples per workgroup
+  __shared__ __attribute__((aligned(16))) float hs[RB * PITCH];
   float* red = hs;                          // reduction buffer aliases the staged rows
   __shared__ int flag;
   int ub, d, bt;
   if (!map_work(UB * D, BT, UB, ub, d, bt)) return;
-  const int n0 = n_base + bt * GB;     // samples [n_base, ...) of a batch chunk
+  const int n0 = n_base + bt * RB;     // samples [n_base, ...) of a batch chunk
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int H4 = 4 * H;
@@ -412,7 +430,7 @@ __global__ __launch_bounds__(GT) void lstm_bwd_persist_kernel(
   const int u = threadIdx.x & 15;
   const int n = n0 + m;
   const int j = ub * GU + u;
-  const bool owner = threadIdx.x < GB * GU && n < N && j < H;
+  const bool owner = threadIdx.x < RB * GU && n < N && j < H;
   int len = owner ? lens[n] : 0;
   settle(len);
   constexpr int RP = GU + 1;
@@ -434,8 +452,12 @@ __global__ __launch_bounds__(GT) void lstm_bwd_persist_kernel(
       const int tp = d == 0 ? t - 1 : t + 1;
       if (tp >= 0 && tp < T) cp = c_all[(((int64_t)tp * N + n) * D + d) * H + j];
     }
-    f32x4 acc0 = f32x4{0.f, 0.f, 0.f, 0.f};
-    f32x4 acc1 = f32x4{0.f, 0.f, 0.f, 0.f};
+    f32x4 acc0[BTS], acc1[BTS];
+#pragma unroll
+    for (int b = 0; b < BTS; ++b) {
+      acc0[b] = f32x4{0.f, 0.f, 0.f, 0.f};
+      acc1[b] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
     if (s > 0) {
       const int tq = d == 0 ? t + 1 : t - 1;
       if (!(use_flags ? flags_wait(gflags, UB, (unsigned)s, err, &flag)
@@ -448,36 +470,43 @@ __global__ __launch_bounds__(GT) void lstm_bwd_persist_kernel(
       for (int c = 0; c < NCH; ++c) {
         if (c > 0) __syncthreads();
         const int c0 = c * CW;
-        // two half-chunk stagings keep the in-flight load registers bounded
+        // 16 rows: two half-chunk stagings keep the in-flight load registers bounded;
+        // 32 rows (CW <= 1024): one staging, every load of the chunk in flight at once
+        constexpr int NH = BTS == 1 ? 2 : 1;
 #pragma unroll
-        for (int hh = 0; hh < 2; ++hh) {
-          const int off = c0 + hh * (CW / 2);
-          stage_rows_sc1<(GB * CW / 8 + GT - 1) / GT>(dgq + off, D * H4, N, n0,
-                                                      max(0, min(H4 - off, CW / 2)), CW / 2,
-                                                      hs + hh * (CW / 2), PITCH);
+        for (int hh = 0; hh < NH; ++hh) {
+          const int off = c0 + hh * (CW / NH);
+          stage_rows_sc1<(RB * CW / 4 / NH + GT - 1) / GT, RB>(dgq + off, D * H4, N, n0,
+                                                               max(0, min(H4 - off, CW / NH)),
+                                                               CW / NH, hs + hh * (CW / NH), PITCH);
         }
         __syncthreads();
-        const float* hrow = hs + (lane & 15) * PITCH + (lane >> 4) + 4 * wave * KSWC;
 #pragma unroll
-        for (int i = 0; i < KSWC; i += 2) {
-          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(hrow[4 * i], w[c][i], acc0, 0, 0, 0);
-          if (i + 1 < KSWC)
-            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(hrow[4 * i + 4], w[c][i + 1], acc1, 0, 0,
-                                                        0);
+        for (int b = 0; b < BTS; ++b) {
+          const float* hrow = hs + (b * GB + (lane & 15)) * PITCH + (lane >> 4) + 4 * wave * KSWC;
+#pragma unroll
+          for (int i = 0; i < KSWC; i += 2) {
+            acc0[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(hrow[4 * i], w[c][i], acc0[b], 0, 0, 0);
+            if (i + 1 < KSWC)
+              acc1[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(hrow[4 * i + 4], w[c][i + 1], acc1[b],
+                                                             0, 0, 0);
+          }
         }
       }
       __syncthreads();                      // all reads of hs done before red overwrites it
     }
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
-      red[(wave * GB + (lane >> 4) * 4 + r) * RP + (lane & 15)] = acc0[r] + acc1[r];
+    for (int b = 0; b < BTS; ++b)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        red[(wave * RB + b * GB + (lane >> 4) * 4 + r) * RP + (lane & 15)] = acc0[b][r] + acc1[b][r];
     __syncthreads();
     if (owner) {
       float dai = 0.f, daf = 0.f, dag = 0.f, dao = 0.f;
       if (t < len) {
         float rec = 0.f;
 #pragma unroll
-        for (int w8 = 0; w8 < GW; ++w8) rec += red[(w8 * GB + m) * RP + u];
+        for (int w8 = 0; w8 < GW; ++w8) rec += red[(w8 * RB + m) * RP + u];
         carry = lstm_cell_bwd(dyv + rec, carry, gi, gf, gg, go, cc, cp, dai, daf, dag, dao);
       } else {
         carry = 0.f;
@@ -530,6 +559,18 @@ static inline int lstm_chunk_tiles(int UB, int D, int BT) {
   return c;
 }
 
+// 16-sample tiles per workgroup of the persistent kernels (template BTS): 2 when the
+// batch's 16-sample tiles would not fit the chip one workgroup each but its 32-sample
+// tiles do -- one launch per layer instead of consecutive batch chunks.  DS2_LSTM_BTS=1|2
+// forces the choice (2 wherever 32-sample workgroups fit; used by the tests).
+static inline int lstm_bts(int UB, int D, int BT) {
+  const bool fits2 = mapped_grid(UB * D, (BT + 1) / 2) <= num_cus();
+  const char* e = getenv("DS2_LSTM_BTS");
+  if (e != nullptr && e[0] == '1') return 1;
+  if (e != nullptr && e[0] == '2') return fits2 ? 2 : 1;
+  return mapped_grid(UB * D, BT) > num_cus() && fits2 ? 2 : 1;
+}
+
 size_t ds2_lstm_fwd_workspace_size(int n, int h, int num_dirs) {
   const int64_t UB = (h + GU - 1) / GU;
   const int64_t KS = (h + 3) / 4;
@@ -573,21 +614,26 @@ ds2_status_t ds2_lstm_fwd(int t_max, int n, int h, int num_dirs, const float* xp
                      dim3(256), 0, st, w_hh_f, w_hh_r, h, num_dirs, UB, KS, wp);
   const int grid = mapped_grid(UB * num_dirs, BT);
   const int kp = persist_ksw((KS + GW - 1) / GW, LKC_FWD);
-  const int ct = lstm_chunk_tiles(UB, num_dirs, BT);
+  const int bts = lstm_bts(UB, num_dirs, BT);
+  const int BTW = (BT + bts - 1) / bts;                   // workgroup batch tiles
+  const int ct = lstm_chunk_tiles(UB, num_dirs, BTW);
   if (persistent_enabled() && (h % 4) == 0 && mapped_grid(UB * num_dirs, ct) <= num_cus() &&
       kp > 0 && kp <= 32 && (int64_t)t_max * n * num_dirs * h * 4 < (1ll << 31)) {
     const void* fn = nullptr;
+#define DS2_LFP(K)                                                                        \
+  case K:                                                                                 \
+    fn = bts == 2 ? reinterpret_cast<const void*>(lstm_fwd_persist_kernel<K, 2>)          \
+                  : reinterpret_cast<const void*>(lstm_fwd_persist_kernel<K, 1>);         \
+    break;
     switch (kp) {
-      case 8: fn = reinterpret_cast<const void*>(lstm_fwd_persist_kernel<8>); break;
-      case 16: fn = reinterpret_cast<const void*>(lstm_fwd_persist_kernel<16>); break;
-      case 25: fn = reinterpret_cast<const void*>(lstm_fwd_persist_kernel<25>); break;
-      case 32: fn = reinterpret_cast<const void*>(lstm_fwd_persist_kernel<32>); break;
+      DS2_LFP(8) DS2_LFP(16) DS2_LFP(25) DS2_LFP(32)
       default: break;
     }
+#undef DS2_LFP
     bool ok = fn != nullptr;
-    for (int b0 = 0; ok && b0 < BT; b0 += ct) {
-      int T_ = t_max, N_ = n, H_ = h, D_ = num_dirs, UB_ = UB, BT_ = std::min(ct, BT - b0);
-      int flags_ = lstm_flags_mode(), NB_ = b0 * GB;
+    for (int b0 = 0; ok && b0 < BTW; b0 += ct) {
+      int T_ = t_max, N_ = n, H_ = h, D_ = num_dirs, UB_ = UB, BT_ = std::min(ct, BTW - b0);
+      int flags_ = lstm_flags_mode(), NB_ = b0 * GB * bts;
       unsigned* err = ctrs + num_dirs * BT_;
       if (hipMemsetAsync(ctrs, 0, lstm_counter_bytes(n, num_dirs), st) != hipSuccess)
         return launch_status("ds2_lstm counters");
@@ -660,18 +706,29 @@ ds2_status_t ds2_lstm_bwd(int t_max, int n, int h, int num_dirs, const float* dy
           nch = c;
           break;
         }
+    // 32-sample workgroups stage chunks of at most 1024 gate columns (32 rows in LDS);
+    // past two chunks (H > 512) the W_hh^T fragments and a chunk's in-flight loads exceed
+    // the 256 VGPRs, so the batch runs in 16-sample chunks instead
+    int bts = lstm_bts(UB, num_dirs, BT);
+    if (bts == 2 && 4 * h > 2 * 4 * GW * 32) bts = 1;
+    if (bts == 2) {
+      kswc = 32;
+      nch = (4 * h + 4 * GW * 32 - 1) / (4 * GW * 32);
+    }
     const void* fn = nullptr;
-#define DS2_LBP(K, C)                                                      \
-  if (kswc == K && nch == C)                                               \
-    fn = reinterpret_cast<const void*>(lstm_bwd_persist_kernel<K, C>);
-    DS2_LBP(8, 1) DS2_LBP(16, 1) DS2_LBP(25, 1) DS2_LBP(32, 1) DS2_LBP(48, 1) DS2_LBP(64, 1)
-    DS2_LBP(48, 2) DS2_LBP(64, 2)
+#define DS2_LBP(K, C, B)                                                   \
+  if (kswc == K && nch == C && bts == B)                                   \
+    fn = reinterpret_cast<const void*>(lstm_bwd_persist_kernel<K, C, B>);
+    DS2_LBP(8, 1, 1) DS2_LBP(16, 1, 1) DS2_LBP(25, 1, 1) DS2_LBP(32, 1, 1) DS2_LBP(48, 1, 1)
+    DS2_LBP(64, 1, 1) DS2_LBP(48, 2, 1) DS2_LBP(64, 2, 1)
+    DS2_LBP(32, 1, 2) DS2_LBP(32, 2, 2)
 #undef DS2_LBP
-    const int ct = lstm_chunk_tiles(UB, num_dirs, BT);
+    const int BTW = (BT + bts - 1) / bts;
+    const int ct = lstm_chunk_tiles(UB, num_dirs, BTW);
     bool ok = fn != nullptr && mapped_grid(UB * num_dirs, ct) <= num_cus();
-    for (int b0 = 0; ok && b0 < BT; b0 += ct) {
-      int T_ = t_max, N_ = n, H_ = h, D_ = num_dirs, UB_ = UB, BT_ = std::min(ct, BT - b0);
-      int DYD_ = dy_dirs, flags_ = lstm_flags_mode(), NB_ = b0 * GB;
+    for (int b0 = 0; ok && b0 < BTW; b0 += ct) {
+      int T_ = t_max, N_ = n, H_ = h, D_ = num_dirs, UB_ = UB, BT_ = std::min(ct, BTW - b0);
+      int DYD_ = dy_dirs, flags_ = lstm_flags_mode(), NB_ = b0 * GB * bts;
       unsigned* err = ctrs + num_dirs * BT_;
       if (hipMemsetAsync(ctrs, 0, lstm_counter_bytes(n, num_dirs), st) != hipSuccess)
         return launch_status("ds2_lstm counters");

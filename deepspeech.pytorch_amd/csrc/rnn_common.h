@@ -270,19 +270,19 @@ __device__ __forceinline__ bool spin_tile(f32x4& v, __amdgpu_buffer_rsrc_t rs, i
   return true;
 }
 
-// Stage rows [n0, n0+16) x [0, cols) of a row-major slab (row stride ld floats, N
+// Stage rows [n0, n0+ROWS) x [0, cols) of a row-major slab (row stride ld floats, N
 // valid rows, `width` valid columns) into hs[m][pitch] with 16-byte sc1 buffer loads.
 // Rows >= N and columns >= width read as zero (out-of-range buffer offsets return
 // 0), so the MFMA loop needs no bounds checks.  All MAXI loads of a thread are
 // issued before the first LDS store.  width, cols and ld are multiples of 4.
-template <int MAXI>
+template <int MAXI, int ROWS = GB>
 __device__ __forceinline__ void stage_rows_sc1(const float* src, int ld, int N, int n0,
                                                int width, int cols, float* __restrict__ hs,
                                                int pitch) {
   const __amdgpu_buffer_rsrc_t rs =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(src), (short)0, N * ld * 4, 0x00020000);
   const int q = cols >> 2;
-  const int total = GB * q;
+  const int total = ROWS * q;
   u32x4 v[MAXI];
 #pragma unroll
   for (int r = 0; r < MAXI; ++r) {

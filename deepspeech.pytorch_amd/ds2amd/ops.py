@@ -479,6 +479,11 @@ def _rnn_param_grads(x, h_all, dgx, dgh, weights, nd, g, need_dx, bf16=False):
         db_hh = grad_like(b_hh)
         if dgh is dgx:
             db_hh.copy_(db_ih)
+        elif g == 3 * h:
+            # GRU: the r and z columns of dgh are dgx's (the kernels store the same values),
+            # so only the n third needs its own column sum
+            db_hh[:2 * h].copy_(db_ih[:2 * h])
+            colsum(dgh, tn, h, ld, db_hh[2 * h:], off=d * g + 2 * h)
         else:
             colsum(dgh, tn, g, ld, db_hh, off=d * g)
         if dx is not None:

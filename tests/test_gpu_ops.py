@@ -433,6 +433,30 @@ def test_lstm_persistent_equals_per_step(dev, h, n, monkeypatch):
         _close(a, b, 1e-5, "lstm persistent vs per-step")
 
 
+@pytest.mark.parametrize("h,n", [(24, 37), (400, 40), (1024, 40)])
+def test_lstm_two_tile_workgroups(dev, h, n, monkeypatch):
+    """32-sample persistent workgroups (DS2_LSTM_BTS=2; cfg4's forward at batch 64) equal
+    16-sample ones: the forward bit for bit (same k split and reduction order per sample),
+    the backward to fp32 rounding (its gate-column chunking differs)."""
+    t, inp = 13, 40
+    lstm, lens, x, g = _lstm_case(n, t, inp, h, True, h + 7)
+    weights = [p.detach().float() for p in lstm.parameters()]
+    x = x.float()
+    dy = torch.randn(t, n, h, generator=g)
+    outs = []
+    for bts in ("1", "2"):
+        monkeypatch.setenv("DS2_LSTM_BTS", bts)
+        ws = [w.to(dev).requires_grad_(True) for w in weights]
+        xd = x.to(dev).requires_grad_(True)
+        y = ops.LSTMLayerFn.apply(xd, lens.to(dev), True, h, *ws)
+        y.backward(dy.to(dev))
+        torch.cuda.synchronize()
+        outs.append([y.detach().cpu(), xd.grad.cpu()] + [w.grad.cpu() for w in ws])
+    assert torch.equal(outs[0][0], outs[1][0]), "lstm forward: 32- vs 16-sample workgroups"
+    for a, b in zip(outs[0][1:], outs[1][1:]):
+        _close(a, b, 1e-5, "lstm 32- vs 16-sample workgroups")
+
+
 # ---------------------------------------------------------------------------- Lookahead
 @pytest.mark.parametrize("t,n,h,context", [(37, 3, 20, 20), (7, 2, 33, 20), (50, 5, 130, 3),
                                            (1, 1, 1, 1)])
