@@ -525,6 +525,212 @@ __global__ __launch_bounds__(GT) void lstm_bwd_persist_kernel(
   }
 }
 
+// Direct-operand persistent forward (H % 16 == 0): gru_fwd_dop_kernel's hand-off with
+// the LSTM cell.  Each producer publishes its 16 units x 16 samples of h_t per batch tile
+// as one 1-KB transposed tile,
+//   hx[slot][d][workgroup batch tile][b < BTS][unit block][q][r][c]  (unit 4 q + c, sample r),
+// stored by wave 0 with one 16-B sc1 store per lane; every consumer wave loads the tiles of
+// its own producers straight into its A operands (lane (r, q): the k values 16 blk + 4 q +
+// 0..3 of sample r), so no LDS staging of h and no barrier stands between the loads and
+// the MFMAs.  HM as in gru.hip (0 flags, 1 sentinel ring, 2 hybrid); BTS as in
+// lstm_fwd_persist_kernel.  h_all, c_all and the gate cache are written after the publish.
+template <int NBW, int HM, int BTS>
+__global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void lstm_fwd_dop_kernel(
+    int T, int N, int H, int D, int UB, int BT, const float* __restrict__ xproj,
+    const float* __restrict__ w_f, const float* __restrict__ w_r, const float* __restrict__ b_f,
+    const float* __restrict__ b_r, const int* __restrict__ lens, float* __restrict__ h_all,
+    float* __restrict__ c_all, float* __restrict__ gates, float* __restrict__ hx,
+    unsigned* __restrict__ counters, unsigned* __restrict__ err, int n_base) {
+  constexpr int RB = GB * BTS;
+  __shared__ float red[GW * RB * LRP];
+  __shared__ __attribute__((aligned(16))) float tile[RB * GU];
+  __shared__ int flag;
+  __shared__ int failed;
+  int ub, d, bt;
+  if (!map_work(UB * D, BT, UB, ub, d, bt)) return;
+  const int n0 = n_base + bt * RB;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int b0, nb;
+  simd_split(UB, wave, b0, nb);                 // host guarantees nb <= NBW
+  const unsigned* gflags = counters + (D * BT + 1) + (d * BT + bt) * UB;
+  unsigned* myflag = counters + (D * BT + 1) + (d * BT + bt) * UB + ub;
+  const int slot_floats = D * BT * BTS * UB * 256;
+  constexpr bool SENT = HM != 0;
+  constexpr bool FLAG = HM != 1;
+  constexpr int NSLOT = SENT ? kRingSlots : 2;
+  const __amdgpu_buffer_rsrc_t x_rs =
+      __builtin_amdgcn_make_buffer_rsrc(hx, (short)0, NSLOT * slot_floats * 4, 0x00020000);
+  const int grp_off = (d * BT + bt) * BTS * UB * 256;      // this group's tiles in a slot
+  if (SENT) {
+    if (threadIdx.x == 0) failed = 0;
+    __syncthreads();
+  }
+
+  // W_hh fragments: w[g][i][c] = W_hh[g H + ub 16 + (lane & 15)][16 (b0 + i) + 4 (lane >> 4) + c]
+  f32x4 w[4][NBW];
+  {
+    const float* W = d == 0 ? w_f : w_r;
+    const float* wr = W + (int64_t)(ub * GU + (lane & 15)) * H + 16 * b0 + 4 * (lane >> 4);
+#pragma unroll
+    for (int i = 0; i < NBW; ++i)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        w[g][i] = i < nb ? *reinterpret_cast<const f32x4*>(wr + (int64_t)g * H * H + 16 * i)
+                         : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < NBW; ++i)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) settle(w[g][i]);
+  }
+  const float* bh = d == 0 ? b_f : b_r;
+  const int m = threadIdx.x >> 4;               // sample within the workgroup (< RB)
+  const int u = threadIdx.x & 15;
+  const int n = n0 + m;
+  const int j = ub * GU + u;
+  const bool owner = threadIdx.x < RB * GU && n < N;
+  float bias[4] = {0.f, 0.f, 0.f, 0.f};
+  int len = 0;
+  if (owner) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) bias[g] = bh[g * H + j];
+    len = lens[n];
+  }
+#pragma unroll
+  for (int g = 0; g < 4; ++g) settle(bias[g]);
+  settle(len);
+  // this thread's slot in its batch tile's transposed tile: (q = u >> 2, r = m % 16, c = u & 3)
+  const int tpos = (m >> 4) * GB * GU + ((u >> 2) * GB + (m & 15)) * 4 + (u & 3);
+  float c = 0.f;
+  LstmFwdOut prev{0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  int64_t prev_row = -1;
+  for (int s = 0; s < T; ++s) {
+    const int t = d == 0 ? s : T - 1 - s;
+    const int64_t row = ((int64_t)t * N + n) * D + d;
+    float xg[4] = {0.f, 0.f, 0.f, 0.f};
+    if (owner && t < len) {
+      const float* xp = xproj + row * 4 * H;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) xg[g] = xp[g * H + j];
+    }
+    f32x4 acc[BTS][4];
+#pragma unroll
+    for (int b = 0; b < BTS; ++b)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) acc[b][g] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (s > 0) {
+      if (FLAG && !flags_wait(gflags, UB, (unsigned)s, err, &flag)) {
+        poison_rest(h_all, s, T, d != 0, N, D, n, d, H, j, H, 1, owner);
+        return;
+      }
+      const int base = (((s - 1) % NSLOT) * slot_floats + grp_off + b0 * 256 + lane * 4) * 4;
+      f32x4 hv[BTS][NBW];
+#pragma unroll
+      for (int b = 0; b < BTS; ++b)
+#pragma unroll
+        for (int i = 0; i < NBW; ++i) {
+          const int off = i < nb ? base + (b * UB + i) * 1024 : 0x7ffffff0;
+          hv[b][i] = __builtin_bit_cast(f32x4,
+                                        __builtin_amdgcn_raw_buffer_load_b128(x_rs, off, 0, kSc1));
+        }
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int b = 0; b < BTS; ++b)
+#pragma unroll
+        for (int i = 0; i < NBW; ++i) {
+          if (SENT && i < nb && !spin_tile(hv[b][i], x_rs, base + (b * UB + i) * 1024, err))
+            failed = 1;
+#pragma unroll
+          for (int cc = 0; cc < 4; ++cc)
+#pragma unroll
+            for (int g = 0; g < 4; ++g)
+              acc[b][g] = __builtin_amdgcn_mfma_f32_16x16x4f32(hv[b][i][cc], w[g][i][cc],
+                                                               acc[b][g], 0, 0, 0);
+        }
+    }
+#pragma unroll
+    for (int b = 0; b < BTS; ++b)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          red[(wave * RB + b * GB + (lane >> 4) * 4 + r) * LRP + g * GU + (lane & 15)] = acc[b][g][r];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) settle(xg[g]);
+    __syncthreads();
+    if (SENT && failed) {
+      poison_rest(h_all, s, T, d != 0, N, D, n, d, H, j, H, 1, owner);
+      return;
+    }
+    if (threadIdx.x < RB * GU) {
+      float hout = 0.f;
+      if (owner) {
+        LstmFwdOut o{0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        if (t < len) {
+          float gh[4];
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            float v = 0.f;
+#pragma unroll
+            for (int w8 = 0; w8 < GW; ++w8) v += red[(w8 * RB + m) * LRP + g * GU + u];
+            gh[g] = v + bias[g] + xg[g];
+          }
+          o = lstm_cell(gh[0], gh[1], gh[2], gh[3], c);
+        }
+        c = o.c;
+        hout = o.h;
+        prev = o;
+        prev_row = row;
+      }
+      tile[tpos] = hout;
+    }
+    __syncthreads();
+    if (wave == 0) {
+#pragma unroll
+      for (int b = 0; b < BTS; ++b) {
+        const int toff = (grp_off + (b * UB + ub) * 256 + lane * 4) * 4;
+        if (SENT) {
+          const u32x4 v = desentinel(*reinterpret_cast<const u32x4*>(tile + b * GB * GU + lane * 4));
+          if (b == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // last step's sentinels
+          __builtin_amdgcn_raw_buffer_store_b128(v, x_rs, (s % NSLOT) * slot_floats * 4 + toff, 0,
+                                                 kSc1);
+        } else {
+          const u32x4 v = *reinterpret_cast<const u32x4*>(tile + b * GB * GU + lane * 4);
+          __builtin_amdgcn_raw_buffer_store_b128(v, x_rs, (s & 1) * slot_floats * 4 + toff, 0, kSc1);
+        }
+      }
+      if (SENT) {
+        const u32x4 sv = u32x4{kSentinel, kSentinel, kSentinel, kSentinel};
+#pragma unroll
+        for (int b = 0; b < BTS; ++b) {
+          const int toff = (grp_off + (b * UB + ub) * 256 + lane * 4) * 4;
+          __builtin_amdgcn_raw_buffer_store_b128(sv, x_rs, ((s + 2) % NSLOT) * slot_floats * 4 + toff,
+                                                 0, kSc1);
+        }
+        if (FLAG && lane == 0)
+          __hip_atomic_store(myflag, (unsigned)s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0)
+          __hip_atomic_store(myflag, (unsigned)s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    // outputs consumed only by later kernels, off the critical path
+    if (owner) {
+      h_all[row * H + j] = prev.h;
+      if (c_all != nullptr) c_all[prev_row * H + j] = prev.c;
+      if (gates != nullptr) {
+        float* gp = gates + prev_row * 4 * H;
+        gp[j] = prev.i;
+        gp[H + j] = prev.f;
+        gp[2 * H + j] = prev.g;
+        gp[3 * H + j] = prev.o;
+      }
+    }
+  }
+}
+
 // per-step kernels: forward needs <= 32 (H <= 1024), backward <= 64 (2048-column chunks)
 static int lstm_pick_ksw(int per) {
   const int opts[] = {8, 16, 32, 64};
@@ -571,12 +777,32 @@ static inline int lstm_bts(int UB, int D, int BT) {
   return mapped_grid(UB * D, BT) > num_cus() && fits2 ? 2 : 1;
 }
 
+// ring of 1-KB hand-off tiles of the direct-operand forward: kRingSlots slots of
+// (direction, 16-sample tile rounded up to a 32-sample workgroup, unit block)
+static inline size_t lstm_ring_bytes(int n, int h, int num_dirs) {
+  const size_t UB = (h + GU - 1) / GU, BT2 = 2 * (((size_t)n + 2 * GB - 1) / (2 * GB));
+  return align256(kRingSlots * (size_t)num_dirs * BT2 * UB * 256 * sizeof(float));
+}
+constexpr unsigned kLstmDopPadLds = 80 * 1024;   // dynamic LDS: one workgroup per CU
+static bool lstm_dop_enabled() {
+  const char* e = getenv("DS2_LSTM_DOP");
+  return !(e != nullptr && e[0] == '0');
+}
+// hand-off form of the direct-operand forward (the variables of gru.hip's handoff_mode):
+// 0 flags, 1 sentinel ring (default), 2 hybrid
+static int lstm_handoff_mode() {
+  const char* e = getenv("DS2_RNN_HANDOFF_FWD");
+  if (e == nullptr || e[0] == 0) e = getenv("DS2_RNN_HANDOFF");
+  if (e == nullptr || e[0] == 0) return 1;
+  return e[0] == 's' ? 1 : (e[0] == 'h' ? 2 : 0);
+}
+
 size_t ds2_lstm_fwd_workspace_size(int n, int h, int num_dirs) {
   const int64_t UB = (h + GU - 1) / GU;
   const int64_t KS = (h + 3) / 4;
   return align256((size_t)(num_dirs * UB * KS * 4 * 64) * sizeof(float)) +
          align256((size_t)2 * n * num_dirs * h * sizeof(float)) + lstm_counter_bytes(n, num_dirs) +
-         256;
+         lstm_ring_bytes(n, h, num_dirs) + 256;
 }
 
 #define DS2_LFWD_CASE(K)                                                                    \
@@ -610,6 +836,61 @@ ds2_status_t ds2_lstm_fwd(int t_max, int n, int h, int num_dirs, const float* xp
   float* cs = reinterpret_cast<float*>(static_cast<char*>(ws) + off);
   off += align256((size_t)2 * n * num_dirs * h * sizeof(float));
   unsigned* ctrs = reinterpret_cast<unsigned*>(static_cast<char*>(ws) + off);
+  float* ring = reinterpret_cast<float*>(static_cast<char*>(ws) + off +
+                                         lstm_counter_bytes(n, num_dirs));
+  // direct-operand persistent kernels (W_hh read unpacked; no LDS staging of h)
+  if (lstm_dop_enabled() && persistent_enabled() && (h % GU) == 0 && UB <= 8 * GW &&
+      (int64_t)t_max * n * num_dirs * h * 4 < (1ll << 31)) {
+    int hm = lstm_handoff_mode();
+    const int bts = lstm_bts(UB, num_dirs, BT);
+    const int BTW = (BT + bts - 1) / bts;
+    const int ct = lstm_chunk_tiles(UB, num_dirs, BTW);
+    // NBW = blocks per wave, rounded up to an instantiated 1, 2, 4 or 8 (extra blocks are
+    // predicated off)
+    const int need = (UB + GW - 1) / GW;
+    const int nbw = need <= 1 ? 1 : need <= 2 ? 2 : need <= 4 ? 4 : 8;
+    // 8 blocks per wave (H > 512): W_hh's 128 fragment registers leave no room for the
+    // sentinel spin's live state (it spills), so those run the flag hand-off
+    if (nbw == 8) hm = 0;
+    const void* fn = nullptr;
+#define DS2_LDOP(K)                                                                          \
+  case K:                                                                                    \
+    fn = bts == 2 ? (hm == 1 ? reinterpret_cast<const void*>(lstm_fwd_dop_kernel<K, 1, 2>)   \
+                  : hm == 2 ? reinterpret_cast<const void*>(lstm_fwd_dop_kernel<K, 2, 2>)   \
+                            : reinterpret_cast<const void*>(lstm_fwd_dop_kernel<K, 0, 2>))  \
+                  : (hm == 1 ? reinterpret_cast<const void*>(lstm_fwd_dop_kernel<K, 1, 1>)   \
+                  : hm == 2 ? reinterpret_cast<const void*>(lstm_fwd_dop_kernel<K, 2, 1>)   \
+                            : reinterpret_cast<const void*>(lstm_fwd_dop_kernel<K, 0, 1>)); \
+    break;
+    switch (nbw) {
+      DS2_LDOP(1) DS2_LDOP(2) DS2_LDOP(4)
+      case 8:
+        fn = bts == 2 ? reinterpret_cast<const void*>(lstm_fwd_dop_kernel<8, 0, 2>)
+                      : reinterpret_cast<const void*>(lstm_fwd_dop_kernel<8, 0, 1>);
+        break;
+      default: break;
+    }
+#undef DS2_LDOP
+    bool ok = fn != nullptr && mapped_grid(UB * num_dirs, ct) <= num_cus();
+    bool launched = false;
+    for (int b0 = 0; ok && b0 < BTW; b0 += ct) {
+      int T_ = t_max, N_ = n, H_ = h, D_ = num_dirs, UB_ = UB, BT_ = std::min(ct, BTW - b0);
+      int NB_ = b0 * GB * bts;
+      unsigned* err = ctrs + num_dirs * BT_;
+      if (hipMemsetAsync(ctrs, 0, lstm_counter_bytes(n, num_dirs), st) != hipSuccess)
+        return launch_status("ds2_lstm counters");
+      if (hm != 0 && hipMemsetAsync(ring, 0xFF, lstm_ring_bytes(n, h, num_dirs), st) != hipSuccess)
+        return launch_status("ds2_lstm ring");
+      void* args[] = {&T_, &N_, &H_, &D_, &UB_, &BT_, &xproj, &w_hh_f, &w_hh_r, &b_hh_f,
+                      &b_hh_r, &lens, &h_all, &c_all, &gates, &ring, &ctrs, &err, &NB_};
+      ok = hipLaunchCooperativeKernel(fn, dim3(mapped_grid(UB * num_dirs, BT_)), dim3(GT), args,
+                                      kLstmDopPadLds, st) == hipSuccess;
+      if (!ok && launched) return launch_status("ds2_lstm_fwd chunk");
+      launched = launched || ok;
+    }
+    if (ok) return launch_status("ds2_lstm_fwd");
+    (void)hipGetLastError();
+  }
   hipLaunchKernelGGL(pack_fwd_kernel<4>, dim3(grid_cap((int64_t)num_dirs * UB * KS * 256)),
                      dim3(256), 0, st, w_hh_f, w_hh_r, h, num_dirs, UB, KS, wp);
   const int grid = mapped_grid(UB * num_dirs, BT);

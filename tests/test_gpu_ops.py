@@ -457,6 +457,33 @@ def test_lstm_two_tile_workgroups(dev, h, n, monkeypatch):
         _close(a, b, 1e-5, "lstm 32- vs 16-sample workgroups")
 
 
+@pytest.mark.parametrize("h,n,handoff", [(32, 21, "sentinel"), (32, 21, "flags"),
+                                         (400, 37, "sentinel"), (400, 37, "hybrid"),
+                                         (1024, 40, "flags")])
+def test_lstm_direct_operand_forward(dev, h, n, handoff, monkeypatch):
+    """The direct-operand forward (h tiles loaded straight into MFMA operands; sentinel ring,
+    flags or hybrid hand-off) equals the LDS-staged persistent forward to fp32 rounding
+    (their K splits over the waves differ) and gives the same gradients downstream."""
+    t, inp = 11, 24
+    lstm, lens, x, g = _lstm_case(n, t, inp, h, True, h + 3)
+    weights = [p.detach().float() for p in lstm.parameters()]
+    x = x.float()
+    dy = torch.randn(t, n, h, generator=g)
+    monkeypatch.setenv("DS2_RNN_HANDOFF_FWD", handoff)
+    outs = []
+    for dop in ("1", "0"):
+        monkeypatch.setenv("DS2_LSTM_DOP", dop)
+        ws = [w.to(dev).requires_grad_(True) for w in weights]
+        xd = x.to(dev).requires_grad_(True)
+        y = ops.LSTMLayerFn.apply(xd, lens.to(dev), True, h, *ws)
+        y.backward(dy.to(dev))
+        torch.cuda.synchronize()
+        assert torch.isfinite(y).all()
+        outs.append([y.detach().cpu(), xd.grad.cpu()] + [w.grad.cpu() for w in ws])
+    for a, b in zip(*outs):
+        _close(a, b, 1e-5, "lstm direct-operand vs staged forward")
+
+
 # ---------------------------------------------------------------------------- Lookahead
 @pytest.mark.parametrize("t,n,h,context", [(37, 3, 20, 20), (7, 2, 33, 20), (50, 5, 130, 3),
                                            (1, 1, 1, 1)])
