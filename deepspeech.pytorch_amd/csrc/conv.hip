@@ -543,7 +543,7 @@ __global__ __launch_bounds__(256) void conv_patch_kernel(const float* __restrict
   const PatchGeom p = patch_geom<DGRAD>(g, by, c0);
   const int tid = threadIdx.x;
   const int lane = tid & 63;
-  const int wave = tid >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int B = g.kw;
   const int plane = in_h * in_w;
   const float* inn = in + (int64_t)n * L * plane;
@@ -638,7 +638,10 @@ __global__ __launch_bounds__(256) void conv_patch_kernel(const float* __restrict
     };
     float aA, aB, vA[4], vB[4];
     read(0, aA, vA);
-    for (int s = 0; s < steps; s += 2) {
+    // a wave whose output row lies past the plane (the last row tile of 41 / 81 rows)
+    // skips its MFMAs: its SIMD time goes to the other workgroups' waves on the CU
+    const int nsteps = p.r_first + wave * p.r_step < out_h ? steps : 0;
+    for (int s = 0; s < nsteps; s += 2) {
       advance();
       read(s + 1, aB, vB);
       __builtin_amdgcn_sched_barrier(0);
