@@ -462,14 +462,15 @@ def test_lstm_two_tile_workgroups(dev, h, n, monkeypatch):
                                          (1024, 40, "flags")])
 def test_lstm_direct_operand_forward(dev, h, n, handoff, monkeypatch):
     """The direct-operand forward (h tiles loaded straight into MFMA operands; sentinel ring,
-    flags or hybrid hand-off) equals the LDS-staged persistent forward to fp32 rounding
-    (their K splits over the waves differ) and gives the same gradients downstream."""
+    flags or hybrid hand-off) and the opt-in direct-operand backward equal the LDS-staged
+    persistent kernels to fp32 rounding (their K splits over the waves differ)."""
     t, inp = 11, 24
     lstm, lens, x, g = _lstm_case(n, t, inp, h, True, h + 3)
     weights = [p.detach().float() for p in lstm.parameters()]
     x = x.float()
     dy = torch.randn(t, n, h, generator=g)
     monkeypatch.setenv("DS2_RNN_HANDOFF_FWD", handoff)
+    monkeypatch.setenv("DS2_LSTM_DOP_BWD", "1")     # the opt-in direct-operand backward too
     outs = []
     for dop in ("1", "0"):
         monkeypatch.setenv("DS2_LSTM_DOP", dop)
