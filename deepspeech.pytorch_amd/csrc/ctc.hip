@@ -356,9 +356,13 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
       if (t + 1 < size) pv_next = pn[(int64_t)(t + 1) * stride_t + lane];
     }
     if (prune) {
+      // rank of this lane's probability: C uniform lane reads (v_readlane), no LDS
       int rank = 0;
-      for (int k = 0; k < C; ++k) {
-        const float q = __shfl(pv, k, 64);
+#pragma unroll
+      for (int k = 0; k < BEAM_CMAX; ++k) {
+        if (k >= C) break;
+        const float q = __builtin_bit_cast(
+            float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, pv), k));
         rank += (q > pv || (q == pv && k < lane)) ? 1 : 0;
       }
       if (lane < C) order[rank] = lane;
@@ -422,21 +426,37 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
       cpnb[k] = pnb;
     }
     __syncthreads();
-    // ---- keep the best `beam` candidates
+    // ---- keep the best `beam` candidates: each lane holds its candidates (k = lane + 64 j)
+    // and their keys in registers, so a selection round is a register scan + a wave
+    // reduction, with no LDS traffic and no barrier
+    constexpr int SJ = BEAM_MAX * BEAM_CMAX / 64;
+    const int jn = (nb * C + 63) / 64;                   // wave-uniform
+    float rs[SJ];
+    int rk[SJ];
+#pragma unroll
+    for (int jj = 0; jj < SJ; ++jj) {
+      rs[jj] = -INFINITY;
+      rk[jj] = 0x7fffffff;
+      if (jj >= jn) continue;
+      const int k = lane + 64 * jj;
+      if (k < nb * C) {
+        const int i = k / C;
+        const int c = k - i * C;
+        const int ch = c == blank ? b_last[cur][i] : c;
+        rs[jj] = cs[k];
+        rk[jj] = (ch + 1) * 4096 + k;
+      }
+    }
     int nsel = 0;
     for (int r = 0; r < beam; ++r) {
       float bs = -INFINITY;
       int bkey = 0x7fffffff;
-      for (int k = lane; k < nb * C; k += 64) {
-        const float sk = cs[k];
-        if (sk == -INFINITY) continue;
-        const int i = k / C;
-        const int c = k - i * C;
-        const int ch = c == blank ? b_last[cur][i] : c;
-        const int key = (ch + 1) * 4096 + k;
-        if (beam_better(sk, key, bs, bkey)) {
-          bs = sk;
-          bkey = key;
+#pragma unroll
+      for (int jj = 0; jj < SJ; ++jj) {
+        if (jj >= jn) break;
+        if (rs[jj] != -INFINITY && beam_better(rs[jj], rk[jj], bs, bkey)) {
+          bs = rs[jj];
+          bkey = rk[jj];
         }
       }
 #pragma unroll
@@ -450,42 +470,53 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
       }
       if (bs == -INFINITY) break;
       const int k = bkey & 4095;
-      if (lane == 0) {
-        sel_k[r] = k;
-        cs[k] = -INFINITY;
-      }
-      __syncthreads();
+#pragma unroll
+      for (int jj = 0; jj < SJ; ++jj)
+        if (lane + 64 * jj == k) rs[jj] = -INFINITY;
+      if (lane == 0) sel_k[r] = k;
       ++nsel;
     }
-    // ---- new beam (new prefixes get trie nodes in rank order)
+    __syncthreads();
+    // ---- new beam: lane r builds entry r; new prefixes get trie nodes in rank order
+    // (node = first free + the number of extensions ranked before it)
     const int nxt = cur ^ 1;
-    if (lane == 0) {
-      int nodes = s_nodes;
-      for (int r = 0; r < nsel; ++r) {
-        const int k = sel_k[r];
-        const int i = k / C;
-        const int c = k - i * C;
-        if (c == blank) {
-          b_node[nxt][r] = b_node[cur][i];
-          b_last[nxt][r] = b_last[cur][i];
-          b_par[nxt][r] = b_par[cur][i];
-          b_lpc[nxt][r] = b_lpc[cur][i];
-        } else {
-          par[nodes] = b_node[cur][i];
-          chr[nodes] = c;
-          tst[nodes] = t;
-          lpcv[nodes] = lp[c];
-          b_node[nxt][r] = nodes;
-          b_last[nxt][r] = c;
-          b_par[nxt][r] = b_node[cur][i];
-          b_lpc[nxt][r] = lp[c];
-          ++nodes;
-        }
-        b_pb[nxt][r] = cpb[k];
-        b_pnb[nxt][r] = cpnb[k];
+    {
+      int k = 0, i = 0, c = blank;
+      if (lane < nsel) {
+        k = sel_k[lane];
+        i = k / C;
+        c = k - i * C;
       }
-      s_nodes = nodes;
-      s_nb = nsel;
+      const bool ext = lane < nsel && c != blank;
+      const unsigned long long em = __ballot(ext);
+      const int before = __builtin_amdgcn_mbcnt_hi(static_cast<unsigned>(em >> 32),
+                                                   __builtin_amdgcn_mbcnt_lo(static_cast<unsigned>(em), 0));
+      const int nodes0 = s_nodes;
+      if (lane < nsel) {
+        if (!ext) {
+          b_node[nxt][lane] = b_node[cur][i];
+          b_last[nxt][lane] = b_last[cur][i];
+          b_par[nxt][lane] = b_par[cur][i];
+          b_lpc[nxt][lane] = b_lpc[cur][i];
+        } else {
+          const int nd = nodes0 + before;
+          par[nd] = b_node[cur][i];
+          chr[nd] = c;
+          tst[nd] = t;
+          lpcv[nd] = lp[c];
+          b_node[nxt][lane] = nd;
+          b_last[nxt][lane] = c;
+          b_par[nxt][lane] = b_node[cur][i];
+          b_lpc[nxt][lane] = lp[c];
+        }
+        b_pb[nxt][lane] = cpb[k];
+        b_pnb[nxt][lane] = cpnb[k];
+      }
+      __syncthreads();
+      if (lane == 0) {
+        s_nodes = nodes0 + __popcll(em);
+        s_nb = nsel;
+      }
     }
     __syncthreads();
     cur = nxt;

@@ -70,5 +70,3 @@ def main():
 
 if __name__ == "__main__":
     main()
-    sys.stdout.flush()
-    os._exit(0)
