@@ -287,6 +287,9 @@ __global__ void greedy_kernel(const float* __restrict__ probs, int n, int t_max,
 // same algorithm (parity with ctcdecode itself is unpinned: it is not available).
 constexpr int BEAM_MAX = 32;
 constexpr int BEAM_CMAX = 64;
+// frames of probabilities staged in LDS at a time: a global load consumed inside the frame
+// loop would make the waitcnt pass wait (vmcnt(0)) for the previous frame's trie stores
+constexpr int BEAM_TCH = 128;
 
 __device__ __forceinline__ float beam_lse(float a, float b) {
   if (a == -INFINITY) return b;
@@ -323,6 +326,7 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
   __shared__ float cs[BEAM_MAX * BEAM_CMAX], cpb[BEAM_MAX * BEAM_CMAX], cpnb[BEAM_MAX * BEAM_CMAX];
   __shared__ int sel_k[BEAM_MAX];
   __shared__ int s_nb, s_nodes;
+  __shared__ float pch[BEAM_TCH * BEAM_CMAX];
 
   const int n = blockIdx.x;
   const int lane = threadIdx.x;
@@ -344,16 +348,26 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
   }
   __syncthreads();
   int cur = 0;
-  float pv_next = (lane < C && size > 0) ? pn[lane] : 0.f;   // frame t + 1 loads during frame t
   for (int t = 0; t < size; ++t) {
     const int nb = s_nb;
     if (nb == 0) break;
+    const int tc = t % BEAM_TCH;
+    if (tc == 0) {   // stage the next BEAM_TCH frames (all loads of a lane in flight at once)
+      const int nf = min(BEAM_TCH, size - t);
+#pragma unroll 8
+      for (int e = lane; e < BEAM_TCH * C; e += 64) {
+        const int f = e / C;
+        const int c = e - f * C;
+        pch[f * BEAM_CMAX + c] = f < nf ? pn[(int64_t)(t + f) * stride_t + c] : 0.f;
+      }
+      __syncthreads();
+    }
+    const float* pf = pch + tc * BEAM_CMAX;
     // ---- vocabulary pruning and log probs
     float pv = 0.f;
     if (lane < C) {
-      pv = pv_next;
+      pv = pf[lane];
       lp[lane] = logf(pv + 1.17549435e-38f);
-      if (t + 1 < size) pv_next = pn[(int64_t)(t + 1) * stride_t + lane];
     }
     if (prune) {
       // rank of this lane's probability: C uniform lane reads (v_readlane), no LDS
@@ -371,7 +385,7 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
         int ok = rank < cutoff_top_n;
         if (ok && cutoff_prob < 1.0) {
           double cum = 0.0;
-          for (int r = 0; r < rank; ++r) cum += (double)pn[(int64_t)t * stride_t + order[r]];
+          for (int r = 0; r < rank; ++r) cum += (double)pf[order[r]];
           ok = cum < cutoff_prob;
         }
         allowed[lane] = ok;
