@@ -303,6 +303,41 @@ __device__ __forceinline__ bool beam_better(float s1, int key1, float s2, int ke
   return s1 > s2 || (s1 == s2 && key1 < key2);
 }
 
+// one step of a wave arg-best over (score, key) through a DPP lane pattern (no LDS)
+template <int CTRL>
+__device__ __forceinline__ void beam_dpp_step(float& bs, int& bk) {
+  const float os = __builtin_bit_cast(
+      float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, bs), CTRL, 0xF, 0xF, false));
+  const int ok = __builtin_amdgcn_update_dpp(0, bk, CTRL, 0xF, 0xF, false);
+  if (beam_better(os, ok, bs, bk)) {
+    bs = os;
+    bk = ok;
+  }
+}
+
+// the wave's best (score, key) -- a strict order (keys are unique), so any reduction tree
+// gives the same winner: xor 1 and xor 2 within quads, half-row and row mirrors (best of
+// each 16-lane row), then the four row winners through v_readlane
+__device__ __forceinline__ void beam_wave_best(float& bs, int& bk) {
+  beam_dpp_step<0xB1>(bs, bk);    // quad_perm [1,0,3,2]
+  beam_dpp_step<0x4E>(bs, bk);    // quad_perm [2,3,0,1]
+  beam_dpp_step<0x141>(bs, bk);   // row_half_mirror
+  beam_dpp_step<0x140>(bs, bk);   // row_mirror
+  float best = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, bs), 0));
+  int key = __builtin_amdgcn_readlane(bk, 0);
+#pragma unroll
+  for (int r = 16; r < 64; r += 16) {
+    const float s2 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, bs), r));
+    const int k2 = __builtin_amdgcn_readlane(bk, r);
+    if (beam_better(s2, k2, best, key)) {
+      best = s2;
+      key = k2;
+    }
+  }
+  bs = best;
+  bk = key;
+}
+
 __global__ __launch_bounds__(64) void ctc_beam_kernel(
     const float* __restrict__ probs, int t_max, int C, int64_t stride_n, int64_t stride_t,
     const int* __restrict__ sizes, int blank, int beam, int cutoff_top_n, double cutoff_prob,
@@ -473,15 +508,7 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
           bkey = rk[jj];
         }
       }
-#pragma unroll
-      for (int off = 32; off > 0; off >>= 1) {
-        const float os = __shfl_xor(bs, off, 64);
-        const int ok = __shfl_xor(bkey, off, 64);
-        if (beam_better(os, ok, bs, bkey)) {
-          bs = os;
-          bkey = ok;
-        }
-      }
+      beam_wave_best(bs, bkey);
       if (bs == -INFINITY) break;
       const int k = bkey & 4095;
 #pragma unroll
