@@ -358,7 +358,7 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
   __shared__ float score[BEAM_MAX];
   __shared__ int pidx[BEAM_MAX];
   __shared__ signed char child_of[BEAM_MAX * BEAM_CMAX];
-  __shared__ float cs[BEAM_MAX * BEAM_CMAX], cpb[BEAM_MAX * BEAM_CMAX], cpnb[BEAM_MAX * BEAM_CMAX];
+  __shared__ float cpb[BEAM_MAX * BEAM_CMAX], cpnb[BEAM_MAX * BEAM_CMAX];
   __shared__ int sel_k[BEAM_MAX];
   __shared__ int s_nb, s_nodes;
   __shared__ float pch[BEAM_TCH * BEAM_CMAX];
@@ -442,60 +442,64 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
     __syncthreads();
     if (lane < nb && pidx[lane] >= 0) child_of[pidx[lane] * C + b_last[cur][lane]] = lane;
     __syncthreads();
-    // ---- candidates
-    for (int k = lane; k < nb * C; k += 64) {
-      const int i = k / C;
-      const int c = k - i * C;
-      const int last_i = b_last[cur][i];
-      const float pb_i = b_pb[cur][i];
-      float sc = -INFINITY, pb = -INFINITY, pnb = -INFINITY;
-      if (c == blank) {
-        pb = allowed[blank] ? lp[blank] + score[i] : -INFINITY;
-        pnb = (last_i >= 0 && allowed[last_i]) ? lp[last_i] + b_pnb[cur][i] : -INFINITY;
-        const int j = pidx[i];
-        if (j >= 0 && allowed[last_i]) {
-          const float e = (last_i == b_last[cur][j])
-                              ? (b_pb[cur][j] != -INFINITY ? lp[last_i] + b_pb[cur][j] : -INFINITY)
-                              : lp[last_i] + score[j];
-          pnb = beam_lse(pnb, e);
-          const int nd = b_node[cur][i];
-          if (lp[last_i] > b_lpc[cur][i]) {   // one blank candidate per entry: no race
-            b_lpc[cur][i] = lp[last_i];
-            lpcv[nd] = lp[last_i];
-            tst[nd] = t;
-          }
-        }
-        sc = beam_lse(pb, pnb);
-      } else if (allowed[c] && child_of[k] < 0) {
-        pnb = (c == last_i) ? (pb_i != -INFINITY ? lp[c] + pb_i : -INFINITY) : lp[c] + score[i];
-        sc = pnb;
-      }
-      cs[k] = sc;
-      cpb[k] = pb;
-      cpnb[k] = pnb;
-    }
-    __syncthreads();
-    // ---- keep the best `beam` candidates: each lane holds its candidates (k = lane + 64 j)
-    // and their keys in registers, so a selection round is a register scan + a wave
-    // reduction, with no LDS traffic and no barrier
+    // ---- candidates, scored straight into registers: lane holds k = lane + 64 jj (the
+    // selection below scans them there); the unrolled loop lets the LDS reads of several
+    // candidates overlap.  (i, c) = divmod(k, C) advanced incrementally.
     constexpr int SJ = BEAM_MAX * BEAM_CMAX / 64;
     const int jn = (nb * C + 63) / 64;                   // wave-uniform
     float rs[SJ];
     int rk[SJ];
+    {
+      int i = lane / C;
+      int c = lane - i * C;
+      const int di = 64 / C, dc = 64 - (64 / C) * C;
 #pragma unroll
-    for (int jj = 0; jj < SJ; ++jj) {
-      rs[jj] = -INFINITY;
-      rk[jj] = 0x7fffffff;
-      if (jj >= jn) continue;
-      const int k = lane + 64 * jj;
-      if (k < nb * C) {
-        const int i = k / C;
-        const int c = k - i * C;
-        const int ch = c == blank ? b_last[cur][i] : c;
-        rs[jj] = cs[k];
-        rk[jj] = (ch + 1) * 4096 + k;
+      for (int jj = 0; jj < SJ; ++jj) {
+        rs[jj] = -INFINITY;
+        rk[jj] = 0x7fffffff;
+        if (jj >= jn) continue;
+        const int k = lane + 64 * jj;
+        if (k < nb * C) {
+          const int last_i = b_last[cur][i];
+          const float pb_i = b_pb[cur][i];
+          float sc = -INFINITY, pb = -INFINITY, pnb = -INFINITY;
+          if (c == blank) {
+            pb = allowed[blank] ? lp[blank] + score[i] : -INFINITY;
+            pnb = (last_i >= 0 && allowed[last_i]) ? lp[last_i] + b_pnb[cur][i] : -INFINITY;
+            const int jp = pidx[i];
+            if (jp >= 0 && allowed[last_i]) {
+              const float e = (last_i == b_last[cur][jp])
+                                  ? (b_pb[cur][jp] != -INFINITY ? lp[last_i] + b_pb[cur][jp] : -INFINITY)
+                                  : lp[last_i] + score[jp];
+              pnb = beam_lse(pnb, e);
+              const int nd = b_node[cur][i];
+              if (lp[last_i] > b_lpc[cur][i]) {   // one blank candidate per entry: no race
+                b_lpc[cur][i] = lp[last_i];
+                lpcv[nd] = lp[last_i];
+                tst[nd] = t;
+              }
+            }
+            sc = beam_lse(pb, pnb);
+          } else if (allowed[c] && child_of[k] < 0) {
+            pnb = (c == last_i) ? (pb_i != -INFINITY ? lp[c] + pb_i : -INFINITY) : lp[c] + score[i];
+            sc = pnb;
+          }
+          cpb[k] = pb;
+          cpnb[k] = pnb;
+          rs[jj] = sc;
+          rk[jj] = ((c == blank ? last_i : c) + 1) * 4096 + k;
+        }
+        i += di;
+        c += dc;
+        if (c >= C) {
+          c -= C;
+          ++i;
+        }
       }
     }
+    __syncthreads();
+    // ---- keep the best `beam` candidates: a selection round is a register scan + a wave
+    // arg-best, with no LDS traffic and no barrier
     int nsel = 0;
     for (int r = 0; r < beam; ++r) {
       float bs = -INFINITY;
