@@ -733,7 +733,9 @@ static bool fits_rsrc(int64_t rows, int64_t ld) { return rows * ld * 4 < (1ll <<
 // cost k each, the tail ceil(pieces / slots) * kchunk; a split adds its partial-slab
 // write + read (8 B per element at ~4 TB/s) and the reduce launch.  `eff` is the tile's
 // relative MFMA efficiency (160-wide tiles: 5 B fragments per 4 A, measured ~7 % faster
-// per unit of work than 128-wide).
+// per unit of work than 128-wide in isolation; 1.15 in the plan, where it also stands in
+// for the 160-wide tile's smaller tail: a whole training step measured 1.0 < 1.07 < 1.15
+// ~ 1.25 ~ 1.4, the last three within noise).
 struct PlanChoice {
   GemmPlan p;
   double t;   // seconds (model)
@@ -784,8 +786,13 @@ static GemmPlan gemm_plan(int m, int n, int k, int batch, bool k64) {
   if (!k64) return plan_bn(m, n, k, batch, BN, 3 * cus, BK, 1.0).p;
   const char* e = getenv("DS2_GEMM_BN");
   if (e != nullptr) return plan_bn(m, n, k, batch, e[1] == '6' ? 160 : 128, 2 * cus, K64, 1.0).p;
+  // DS2_GEMM_EFF160: the 160-wide tile's relative efficiency in the time model (tuning)
+  static const double eff160 = [] {
+    const char* v = getenv("DS2_GEMM_EFF160");
+    return v != nullptr ? atof(v) : 1.15;
+  }();
   const PlanChoice a = plan_bn(m, n, k, batch, 128, 2 * cus, K64, 1.0);
-  const PlanChoice b = plan_bn(m, n, k, batch, 160, 2 * cus, K64, 1.07);
+  const PlanChoice b = plan_bn(m, n, k, batch, 160, 2 * cus, K64, eff160);
   return b.t < a.t ? b.p : a.p;
 }
 
