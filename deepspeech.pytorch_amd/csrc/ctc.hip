@@ -434,8 +434,11 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
       const int nd = b_node[cur][lane];
       const int pnode = nd > 0 ? b_par[cur][lane] : -1;
       int j = -1;
-      for (int i = 0; i < nb; ++i)
+#pragma unroll
+      for (int i = 0; i < BEAM_MAX; ++i) {   // unrolled: the nb LDS reads overlap
+        if (i >= nb) break;
         if (pnode >= 0 && b_node[cur][i] == pnode) j = i;
+      }
       pidx[lane] = j;
     }
     for (int e = lane; e < nb * C; e += 64) child_of[e] = -1;
