@@ -5,11 +5,13 @@ python bench.py [--gpus N --steps K --warmup W]          (N=1: plain process)
 python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
 
 One step = the reference's train_batch (train.py:555-632) on the HIP path:
-forward (conv/BN/5 BiGRU/FC/softmax), greedy decode, CTC (+grad), backward,
+forward (conv/BN/5 BiGRU/FC/softmax), greedy decode + per-batch CER/WER, CTC (+grad), backward,
 bucketed RCCL gradient all-reduce overlapped with backward (N > 1), clip 100 +
 SGD-Nesterov.  Synthetic 10 s spectrograms [32, 1, 161, 1001] resident in HBM,
 random-init weights (seed 123456), 150-label targets.  Weak scaling: 32
-utterances per GPU.  Rank 0 prints one JSON line.
+utterances per GPU.  Rank 0 prints one JSON line: ``value`` from the wall clock around
+exactly K steps (the contract; max over ranks), plus the median per-step time from HIP
+events (5 warm-up, median of 20).
 """
 from __future__ import annotations
 
@@ -132,36 +134,97 @@ def gru_recurrence_flops(args):
     return 2.0 * t * n * d * 3 * h * h
 
 
-def cpu_baseline(seconds_budget: float = 20.0):
-    """The oracle (stock torch CPU ops, the reference's op set) on the host cores: one
-    bounded train step of the same architecture on 2 x 10 s utterances."""
+def _cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
+def _cpu_threads() -> int:
+    """The host cores this process may use: the box's share (OMP_NUM_THREADS, set to 16 per
+    GPU on the pool; os.cpu_count() there counts the whole machine), else the affinity set."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        return int(env)
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
+def _progress(msg):
+    print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
+def cpu_baseline(train_steps: int = 3, fwd_steps: int = 2, budget_s: float = 150.0):
+    """BASELINE.md §4 / SURVEY §8(d): the oracle (the reference's stock torch CPU op set:
+    conv2d / batch_norm / packed nn.GRU / ctc_loss / SGD) on the SAME cfg2 batch the GPU
+    trains on (32 x 10 s, 5 x BiGRU-800, seed 123456), all usable host threads, 1 warm-up +
+    ``train_steps`` timed training steps, plus a train-mode forward-only figure (1 warm-up +
+    ``fwd_steps`` timed).  Medians reported.  Timed training steps stop (never below one) once
+    another would exceed ``budget_s``, so the default bench run stays within a few minutes;
+    the sample string says what ran."""
     from oracle import ds2_oracle as orc
     from ds2amd import model as dsm
-    threads = min(16, os.cpu_count() or 1)
+    threads = _cpu_threads()
     torch.set_num_threads(threads)
     torch.manual_seed(123456)
     m = dsm.DeepSpeech(rnn_type='gru', labels=LABELS, rnn_hidden_size=HIDDEN, nb_layers=LAYERS,
                        audio_conf=CONF, bidirectional=True)
     o = orc.OracleDS2({k: v.detach() for k, v in m.state_dict().items()}, LAYERS, HIDDEN)
-    nb = 4
     x, tg, pct, ts = synthetic_batch(0)
-    x, pct, ts = x[:nb], pct[:nb], ts[:nb]
-    tg = tg[:nb * LABEL_LEN]
+    sizes = orc.input_sizes_quirk(pct, x.shape[3])
+    train_t, fwd_t = [], []
+    # warm-up: one train step on 2 of the utterances (allocator, thread pool, kernels); a
+    # full-batch warm-up step would double the baseline's cost (≈2 min per bs32 step on 16
+    # cores: the packed-GRU backward dominates) for a sub-percent effect
     t0 = time.perf_counter()
-    orc.train_step(o, x, pct.clone(), tg, ts)
-    dt = time.perf_counter() - t0
-    return {"value": round(nb * SECONDS / dt, 4), "unit": "audio-seconds/sec",
-            "cores": threads, "kind": "port",
-            "sample": f"1 oracle train step (fwd+CTC+bwd+clip+SGD), 5xBiGRU-800, {nb} x 10 s "
-                      f"utterances, torch CPU fp32, {dt:.1f} s"}
+    orc.train_step(o, x[:2], pct[:2].clone(), tg[:2 * LABEL_LEN], ts[:2])
+    _progress(f"cpu baseline: warm-up step (2 utterances) {time.perf_counter() - t0:.1f} s "
+              f"on {threads} threads")
+    t_start = time.perf_counter()
+    for i in range(train_steps):
+        t0 = time.perf_counter()
+        orc.train_step(o, x, pct.clone(), tg, ts)
+        train_t.append(time.perf_counter() - t0)
+        _progress(f"cpu baseline: train step {i + 1}/{train_steps} {train_t[-1]:.1f} s")
+        if time.perf_counter() - t_start + train_t[-1] > budget_s:
+            break
+    with torch.no_grad():
+        for i in range(1 + fwd_steps):
+            t0 = time.perf_counter()
+            o.forward(x, sizes, training=True)
+            if i > 0:
+                fwd_t.append(time.perf_counter() - t0)
+            _progress(f"cpu baseline: forward {i}/{fwd_steps} {time.perf_counter() - t0:.1f} s")
+    med = lambda v: sorted(v)[len(v) // 2]
+    tr, fw = med(train_t), med(fwd_t)
+    return {"value": round(BATCH * SECONDS / tr, 4), "unit": "audio-seconds/sec",
+            "cores": threads, "kind": "port", "cpu_model": _cpu_model(),
+            "forward_only_value": round(BATCH * SECONDS / fw, 4),
+            "train_step_s": [round(v, 3) for v in train_t],
+            "forward_s": [round(v, 3) for v in fwd_t],
+            "sample": f"oracle train step (fwd+CTC+bwd+clip+SGD) on the cfg2 batch, "
+                      f"{BATCH} x 10 s, 5xBiGRU-800, torch CPU fp32 on {threads} threads: "
+                      f"1 warm-up step on 2 utterances + {len(train_t)} timed full-batch "
+                      f"step(s) (at most {train_steps}, {budget_s:.0f} s budget; median "
+                      f"{tr:.1f} s); forward-only "
+                      f"(train mode, no grad): 1 warm-up + {fwd_steps} timed (median {fw:.1f} s)"}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-steps", type=int, default=3,
+                    help="timed oracle training steps of the CPU baseline (after 1 warm-up)")
     ap.add_argument("--probe", default="ds2_sgemm_ws")
     ap.add_argument("--input", choices=["spect", "pcm"], default="spect",
                     help="spect: 10 s spectrograms resident in HBM (the headline metric); "
@@ -174,19 +237,19 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # DS2_FORCE_DIST=1 under torchrun exercises the RCCL path even at world size 1
     distributed = world > 1 or os.environ.get("DS2_FORCE_DIST") == "1"
-    if distributed:
-        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
-
     from ds2amd import model as dsm
-    from ds2amd.trainer import Trainer
+    from ds2amd.trainer import Trainer, init_distributed
+    if distributed:
+        init_distributed("nccl", local)            # RCCL over xGMI, channel cap
+    dev = torch.device("cuda", local)
 
     torch.manual_seed(123456)
     m = dsm.DeepSpeech(rnn_type='gru', labels=LABELS, rnn_hidden_size=HIDDEN, nb_layers=LAYERS,
                        audio_conf=CONF, bidirectional=True)
-    tr = Trainer(m, LABELS, lr=3e-4, momentum=0.9, max_norm=100.0, device=dev)
+    # score=True: the reference computes CER/WER of the greedy decode every batch
+    # (train.py:575-591); here on the device (ds2_edit_distance), inside the timed step
+    tr = Trainer(m, LABELS, lr=3e-4, momentum=0.9, max_norm=100.0, device=dev, score=True,
+                 verbose=False)
     x, tg, pct, ts = synthetic_batch(rank)
     x = x.to(dev)                                      # inputs resident in HBM
     featurize = None
@@ -220,15 +283,21 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     probe.active = rprobe.active = True
+    marks = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    marks[0].record()
+    for i in range(args.steps):
         loss = step()
+        marks[i + 1].record()
     torch.cuda.synchronize()
     if distributed:
         dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     probe.active = rprobe.active = False
+    tr.poll_status(block=True)      # raises Ds2Error if a recurrence hand-off failed
+    step_ms = sorted(marks[i].elapsed_time(marks[i + 1]) for i in range(args.steps))
+    median_ms = step_ms[len(step_ms) // 2]
     if distributed:
         tt = torch.tensor([dt], device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -266,11 +335,13 @@ def main():
                    "unit": "TFLOP/s", "frac": round(achieved / PEAK_F32_MFMA_TFLOPS, 4)}
         cpu = None
         if not args.no_cpu_baseline and world == 1:
-            cpu = cpu_baseline()
+            cpu = cpu_baseline(args.cpu_steps)
         out = {
             "metric": "audio-seconds/sec training, DS2 5x BiGRU-800 bs32, at 1/2/4/8 MI355X",
             "value": round(value, 2), "unit": "audio-seconds/sec", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
+            "ms_per_step_median": round(median_ms, 3),
+            "value_at_median": round(world * BATCH * SECONDS / (median_ms * 1e-3), 2),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": ("synthetic 10 s spectrograms [32,1,161,1001] + 150-label targets, random init"
                      if featurize is None else

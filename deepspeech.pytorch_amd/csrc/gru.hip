@@ -554,7 +554,7 @@ __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
           }
         }
         if (pend == 0u) break;
-        if (spins > kSpinLimit) {
+        if (spins > g_spin_limit) {
           if (lane == 0) __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           failed = 1;
           break;
@@ -1091,7 +1091,7 @@ static int pick_ksw(int per) {
 ds2_status_t ds2_gru_fwd(int t_max, int n, int h, int num_dirs, const float* xproj,
                          const float* w_hh_f, const float* w_hh_r, const float* b_hh_f,
                          const float* b_hh_r, const int* lens, float* h_all, float* gates,
-                         void* ws, size_t ws_bytes, ds2_stream_t stream) {
+                         unsigned* err_out, void* ws, size_t ws_bytes, ds2_stream_t stream) {
   if (t_max < 0 || n < 0 || h < 1 || (num_dirs != 1 && num_dirs != 2)) return DS2_INVALID_VALUE;
   if (h > KC_FWD) return DS2_UNSUPPORTED_SHAPE;
   if (t_max == 0 || n == 0) return DS2_OK;
@@ -1102,6 +1102,7 @@ ds2_status_t ds2_gru_fwd(int t_max, int n, int h, int num_dirs, const float* xpr
     b_hh_r = b_hh_f;
   }
   hipStream_t st = as_stream(stream);
+  apply_spin_limit_env();
   const int UB = (h + GU - 1) / GU;
   const int KS = (h + 3) / 4;
   const int BT = (n + GB - 1) / GB;
@@ -1140,8 +1141,10 @@ ds2_status_t ds2_gru_fwd(int t_max, int n, int h, int num_dirs, const float* xpr
 #undef DS2_FDOP
     // the dynamic LDS keeps one workgroup per CU (every workgroup gets a whole CU's SIMDs)
     if (fn != nullptr &&
-        hipLaunchCooperativeKernel(fn, dim3(grid), dim3(GT), args, kDopPadLds, st) == hipSuccess)
+        hipLaunchCooperativeKernel(fn, dim3(grid), dim3(GT), args, kDopPadLds, st) == hipSuccess) {
+      fold_err(err, err_out, st);
       return launch_status("ds2_gru_fwd");
+    }
     (void)hipGetLastError();
   }
   hipLaunchKernelGGL(pack_fwd_kernel<3>, dim3(grid_cap((int64_t)num_dirs * UB * KS * 192)),
@@ -1169,8 +1172,10 @@ ds2_status_t ds2_gru_fwd(int t_max, int n, int h, int num_dirs, const float* xpr
       default: break;
     }
     if (fn != nullptr &&
-        hipLaunchCooperativeKernel(fn, dim3(grid), dim3(GT), args, 0, st) == hipSuccess)
+        hipLaunchCooperativeKernel(fn, dim3(grid), dim3(GT), args, 0, st) == hipSuccess) {
+      fold_err(err, err_out, st);
       return launch_status("ds2_gru_fwd");
+    }
     (void)hipGetLastError();   // fall back to one launch per step
   }
   for (int s = 0; s < t_max; ++s) {
@@ -1200,7 +1205,7 @@ size_t ds2_gru_bwd_workspace_size(int n, int h, int num_dirs) {
 ds2_status_t ds2_gru_bwd(int t_max, int n, int h, int num_dirs, const float* dy, int dy_dirs,
                          const float* w_hh_f, const float* w_hh_r, const float* h_all,
                          const float* gates, const int* lens, float* dgates_x, float* dgates_h,
-                         void* ws, size_t ws_bytes, ds2_stream_t stream) {
+                         unsigned* err_out, void* ws, size_t ws_bytes, ds2_stream_t stream) {
   if (t_max < 0 || n < 0 || h < 1 || (num_dirs != 1 && num_dirs != 2)) return DS2_INVALID_VALUE;
   if (t_max == 0 || n == 0) return DS2_OK;
   if (gates == nullptr) return DS2_INVALID_VALUE;
@@ -1209,6 +1214,7 @@ ds2_status_t ds2_gru_bwd(int t_max, int n, int h, int num_dirs, const float* dy,
     return DS2_WORKSPACE_TOO_SMALL;
   if (num_dirs == 1) w_hh_r = w_hh_f;
   hipStream_t st = as_stream(stream);
+  apply_spin_limit_env();
   const int UB = (h + GU - 1) / GU;
   const int KS = (3 * h + 3) / 4;
   const int BT = (n + GB - 1) / GB;
@@ -1236,8 +1242,10 @@ ds2_status_t ds2_gru_bwd(int t_max, int n, int h, int num_dirs, const float* dy,
       return launch_status("ds2_gru ring");
     const void* fn = bwd_dop_fn((3 * UB + GW - 1) / GW);
     if (fn != nullptr &&
-        hipLaunchCooperativeKernel(fn, dim3(grid), dim3(GT), args, kDopPadLds, st) == hipSuccess)
+        hipLaunchCooperativeKernel(fn, dim3(grid), dim3(GT), args, kDopPadLds, st) == hipSuccess) {
+      fold_err(err, err_out, st);
       return launch_status("ds2_gru_bwd");
+    }
     (void)hipGetLastError();
   }
   hipLaunchKernelGGL(pack_bwd_kernel<3>, dim3(grid_cap((int64_t)num_dirs * UB * KS * 64)),
@@ -1267,8 +1275,10 @@ ds2_status_t ds2_gru_bwd(int t_max, int n, int h, int num_dirs, const float* dy,
       default: break;
     }
     if (fn != nullptr &&
-        hipLaunchCooperativeKernel(fn, dim3(grid), dim3(GT), args, 0, st) == hipSuccess)
+        hipLaunchCooperativeKernel(fn, dim3(grid), dim3(GT), args, 0, st) == hipSuccess) {
+      fold_err(err, err_out, st);
       return launch_status("ds2_gru_bwd");
+    }
     (void)hipGetLastError();
   }
   for (int s = 0; s < t_max; ++s) {

@@ -973,7 +973,8 @@ size_t ds2_lstm_fwd_workspace_size(int n, int h, int num_dirs) {
 ds2_status_t ds2_lstm_fwd(int t_max, int n, int h, int num_dirs, const float* xproj,
                           const float* w_hh_f, const float* w_hh_r, const float* b_hh_f,
                           const float* b_hh_r, const int* lens, float* h_all, float* c_all,
-                          float* gates, void* ws, size_t ws_bytes, ds2_stream_t stream) {
+                          float* gates, unsigned* err_out, void* ws, size_t ws_bytes,
+                          ds2_stream_t stream) {
   if (t_max < 0 || n < 0 || h < 1 || (num_dirs != 1 && num_dirs != 2)) return DS2_INVALID_VALUE;
   if (h > LKC_FWD) return DS2_UNSUPPORTED_SHAPE;
   if (t_max == 0 || n == 0) return DS2_OK;
@@ -984,6 +985,7 @@ ds2_status_t ds2_lstm_fwd(int t_max, int n, int h, int num_dirs, const float* xp
     b_hh_r = b_hh_f;
   }
   hipStream_t st = as_stream(stream);
+  apply_spin_limit_env();
   const int UB = (h + GU - 1) / GU;
   const int KS = (h + 3) / 4;
   const int BT = (n + GB - 1) / GB;
@@ -1043,6 +1045,7 @@ ds2_status_t ds2_lstm_fwd(int t_max, int n, int h, int num_dirs, const float* xp
                       &b_hh_r, &lens, &h_all, &c_all, &gates, &ring, &ctrs, &err, &NB_};
       ok = hipLaunchCooperativeKernel(fn, dim3(mapped_grid(UB * num_dirs, BT_)), dim3(GT), args,
                                       kLstmDopPadLds, st) == hipSuccess;
+      if (ok) fold_err(err, err_out, st);
       if (!ok && launched) return launch_status("ds2_lstm_fwd chunk");
       launched = launched || ok;
     }
@@ -1080,6 +1083,7 @@ ds2_status_t ds2_lstm_fwd(int t_max, int n, int h, int num_dirs, const float* xp
                       &h_all, &c_all, &gates, &ctrs, &err, &flags_, &NB_};
       ok = hipLaunchCooperativeKernel(fn, dim3(mapped_grid(UB * num_dirs, BT_)), dim3(GT), args,
                                       0, st) == hipSuccess;
+      if (ok) fold_err(err, err_out, st);
       if (!ok && b0 > 0) return launch_status("ds2_lstm_fwd chunk");
     }
     if (ok) return launch_status("ds2_lstm_fwd");
@@ -1116,8 +1120,8 @@ size_t ds2_lstm_bwd_workspace_size(int n, int h, int num_dirs) {
 
 ds2_status_t ds2_lstm_bwd(int t_max, int n, int h, int num_dirs, const float* dy, int dy_dirs,
                           const float* w_hh_f, const float* w_hh_r, const float* c_all,
-                          const float* gates, const int* lens, float* dgates, void* ws,
-                          size_t ws_bytes, ds2_stream_t stream) {
+                          const float* gates, const int* lens, float* dgates, unsigned* err_out,
+                          void* ws, size_t ws_bytes, ds2_stream_t stream) {
   if (t_max < 0 || n < 0 || h < 1 || (num_dirs != 1 && num_dirs != 2)) return DS2_INVALID_VALUE;
   if (t_max == 0 || n == 0) return DS2_OK;
   if (gates == nullptr || c_all == nullptr) return DS2_INVALID_VALUE;
@@ -1126,6 +1130,7 @@ ds2_status_t ds2_lstm_bwd(int t_max, int n, int h, int num_dirs, const float* dy
     return DS2_WORKSPACE_TOO_SMALL;
   if (num_dirs == 1) w_hh_r = w_hh_f;
   hipStream_t st = as_stream(stream);
+  apply_spin_limit_env();
   const int UB = (h + GU - 1) / GU;
   const int KS = h;
   const int BT = (n + GB - 1) / GB;
@@ -1166,6 +1171,7 @@ ds2_status_t ds2_lstm_bwd(int t_max, int n, int h, int num_dirs, const float* dy
                       &gates, &lens, &dgates, &ring, &ctrs, &err, &NB_};
       ok = hipLaunchCooperativeKernel(fn, dim3(mapped_grid(UB * num_dirs, BT_)), dim3(GT), args,
                                       kLstmDopPadLds, st) == hipSuccess;
+      if (ok) fold_err(err, err_out, st);
       if (!ok && launched) return launch_status("ds2_lstm_bwd chunk");
       launched = launched || ok;
     }
@@ -1217,6 +1223,7 @@ ds2_status_t ds2_lstm_bwd(int t_max, int n, int h, int num_dirs, const float* dy
                       &dgates, &ctrs, &err, &flags_, &NB_};
       ok = hipLaunchCooperativeKernel(fn, dim3(mapped_grid(UB * num_dirs, BT_)), dim3(GT), args,
                                       0, st) == hipSuccess;
+      if (ok) fold_err(err, err_out, st);
       if (!ok && b0 > 0) return launch_status("ds2_lstm_bwd chunk");
     }
     if (ok) return launch_status("ds2_lstm_bwd");

@@ -245,17 +245,30 @@ __global__ void clip_sgd_nesterov_kernel(float* __restrict__ p, const float* __r
 }
 
 __global__ void nan_guard_kernel(float* __restrict__ x, int64_t numel, int zero_nans,
-                                 int* __restrict__ flag) {
+                                 int* __restrict__ flag, unsigned char* __restrict__ mask) {
   int found = 0;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < numel;
        i += (int64_t)gridDim.x * blockDim.x) {
     float v = x[i];
-    if (v != v) {
+    const bool nan = v != v;
+    if (nan) {
       found = 1;
       if (zero_nans) x[i] = 0.0f;
     }
+    if (mask != nullptr) mask[i] = nan ? 1 : 0;
   }
   if (__any(found) && (threadIdx.x & 63) == 0) atomicOr(flag, 1);
+}
+
+// Backward of the in-place NaN zeroing (train.py:598 `logits[isnan(logits)] = 0`): autograd's
+// index_put gives the zeroed positions a zero gradient.  Nothing to do unless *flag says a NaN
+// was seen (the common case reads one word and leaves).
+__global__ void zero_masked_kernel(float* __restrict__ x, const unsigned char* __restrict__ mask,
+                                   int64_t numel, const int* __restrict__ flag) {
+  if (flag != nullptr && *flag == 0) return;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < numel;
+       i += (int64_t)gridDim.x * blockDim.x)
+    if (mask[i]) x[i] = 0.0f;
 }
 
 __global__ void scale_kernel(float* __restrict__ x, int64_t numel, const float* __restrict__ s) {
@@ -377,12 +390,21 @@ ds2_status_t ds2_clip_sgd_nesterov(float* params, const float* grads, float* mom
 }
 
 ds2_status_t ds2_nan_guard(float* x, int64_t numel, int zero_nans, int* flag,
-                           ds2_stream_t stream) {
+                           unsigned char* mask, ds2_stream_t stream) {
   if (numel < 0 || flag == nullptr) return DS2_INVALID_VALUE;
   if (numel == 0) return DS2_OK;
   hipLaunchKernelGGL(nan_guard_kernel, dim3(grid_for(numel, 256)), dim3(256), 0,
-                     as_stream(stream), x, numel, zero_nans, flag);
+                     as_stream(stream), x, numel, zero_nans, flag, mask);
   return launch_status("ds2_nan_guard");
+}
+
+ds2_status_t ds2_zero_masked(float* x, const unsigned char* mask, int64_t numel, const int* flag,
+                             ds2_stream_t stream) {
+  if (numel < 0 || (numel > 0 && mask == nullptr)) return DS2_INVALID_VALUE;
+  if (numel == 0) return DS2_OK;
+  hipLaunchKernelGGL(zero_masked_kernel, dim3(grid_for(numel, 256)), dim3(256), 0,
+                     as_stream(stream), x, mask, numel, flag);
+  return launch_status("ds2_zero_masked");
 }
 
 ds2_status_t ds2_scale_by_device_scalar(float* x, int64_t numel, const float* scalar,

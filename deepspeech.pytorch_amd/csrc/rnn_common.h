@@ -110,6 +110,35 @@ static inline int mapped_grid(int P, int BT) { return 8 * ((P + 7) / 8) * BT; }
 // error word and the workgroup leaves (no hang, results invalid).
 constexpr unsigned kSpinLimit = 1u << 21;
 
+// The bound the kernels use: kSpinLimit unless DS2_RNN_SPIN_LIMIT is set in the environment
+// (checked at every recurrence entry point) -- a test lowers it to force the timeout path and
+// check that the failure surfaces through err_out instead of going silent.
+static __constant__ unsigned g_spin_limit = kSpinLimit;
+
+static void apply_spin_limit_env() {
+  static unsigned applied = kSpinLimit;
+  const char* e = getenv("DS2_RNN_SPIN_LIMIT");
+  const unsigned v = (e == nullptr || e[0] == 0) ? kSpinLimit
+                                                 : static_cast<unsigned>(strtoul(e, nullptr, 10));
+  if (v == applied) return;
+  // synchronous symbol write: only ever taken when a test changes the variable
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_spin_limit), &v, sizeof(v)) == hipSuccess) applied = v;
+}
+
+// err_out (C ABI, nullable): the caller's device status word.  After a persistent launch the
+// launch's own error word (in the workspace, reset before every launch) is OR-ed into it, so
+// a hand-off timeout stays visible to the host after the workspace is recycled.
+static __global__ void err_fold_kernel(const unsigned* __restrict__ err, unsigned* __restrict__ out) {
+  if (threadIdx.x == 0) {
+    const unsigned v = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (v != 0u) __hip_atomic_fetch_or(out, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+static inline void fold_err(const unsigned* err, unsigned* err_out, hipStream_t st) {
+  if (err_out != nullptr) hipLaunchKernelGGL(err_fold_kernel, dim3(1), dim3(64), 0, st, err, err_out);
+}
+
 __device__ __forceinline__ void st_sc1(float* p, float v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -131,7 +160,7 @@ __device__ __forceinline__ bool group_wait(unsigned* ctr, unsigned target, unsig
     int ok = 1;
     while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
       __builtin_amdgcn_s_sleep(2);
-      if (++spins > kSpinLimit || __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+      if (++spins > g_spin_limit || __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
         __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         ok = 0;
         break;
@@ -160,7 +189,7 @@ __device__ __forceinline__ bool flags_wait(const unsigned* flags, int count, uns
                                       : target;
       if (__ballot(v < target) == 0ull) break;
       __builtin_amdgcn_s_sleep(1);
-      if (++spins > kSpinLimit) {
+      if (++spins > g_spin_limit) {
         if (lane == 0) __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         ok = 0;
         break;
@@ -253,12 +282,12 @@ __device__ __forceinline__ u32x4 desentinel(u32x4 v) {
 __device__ __forceinline__ bool wave_ready(f32x4 v) { return __ballot(!tile_ready(v)) == 0ull; }
 
 // Spin until the wave's ring tile at byte offset off (already loaded into v once) holds no
-// sentinel word, re-loading it alone; false (and the error word set) after kSpinLimit polls.
+// sentinel word, re-loading it alone; false (and the error word set) after g_spin_limit polls.
 // The wave's later tiles stay in flight meanwhile.
 __device__ __forceinline__ bool spin_tile(f32x4& v, __amdgpu_buffer_rsrc_t rs, int off,
                                           unsigned* err) {
   for (unsigned spins = 0; !wave_ready(v); ++spins) {
-    if (spins > kSpinLimit) {
+    if (spins > g_spin_limit) {
       if ((threadIdx.x & 63) == 0)
         __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       return false;

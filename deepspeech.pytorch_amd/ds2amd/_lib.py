@@ -57,16 +57,16 @@ _PROTOS = {
                                  _vp]),
     "ds2_gru_fwd_workspace_size": (_sz, [_c_int, _c_int, _c_int]),
     "ds2_gru_fwd": (_c_int, [_c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
-                             _vp, _vp, _sz, _vp]),
+                             _vp, _vp, _vp, _sz, _vp]),
     "ds2_gru_bwd_workspace_size": (_sz, [_c_int, _c_int, _c_int]),
     "ds2_gru_bwd": (_c_int, [_c_int, _c_int, _c_int, _c_int, _vp, _c_int, _vp, _vp, _vp, _vp,
-                             _vp, _vp, _vp, _vp, _sz, _vp]),
+                             _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
     "ds2_lstm_fwd_workspace_size": (_sz, [_c_int, _c_int, _c_int]),
     "ds2_lstm_fwd": (_c_int, [_c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
-                              _vp, _vp, _vp, _sz, _vp]),
+                              _vp, _vp, _vp, _vp, _sz, _vp]),
     "ds2_lstm_bwd_workspace_size": (_sz, [_c_int, _c_int, _c_int]),
     "ds2_lstm_bwd": (_c_int, [_c_int, _c_int, _c_int, _c_int, _vp, _c_int, _vp, _vp, _vp, _vp,
-                              _vp, _vp, _vp, _sz, _vp]),
+                              _vp, _vp, _vp, _vp, _sz, _vp]),
     "ds2_lookahead_fwd": (_c_int, [_vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_f,
                                    _c_f, _vp, _vp]),
     "ds2_lookahead_bwd_workspace_size": (_sz, [_c_int, _c_int, _c_int, _c_int]),
@@ -91,7 +91,8 @@ _PROTOS = {
     "ds2_optim_workspace_size": (_sz, [_c_i64]),
     "ds2_grad_norm": (_c_int, [_vp, _c_i64, _vp, _vp, _sz, _vp]),
     "ds2_clip_sgd_nesterov": (_c_int, [_vp, _vp, _vp, _c_i64, _c_f, _c_f, _c_f, _vp, _vp, _vp]),
-    "ds2_nan_guard": (_c_int, [_vp, _c_i64, _c_int, _vp, _vp]),
+    "ds2_nan_guard": (_c_int, [_vp, _c_i64, _c_int, _vp, _vp, _vp]),
+    "ds2_zero_masked": (_c_int, [_vp, _vp, _c_i64, _vp, _vp]),
     "ds2_scale_by_device_scalar": (_c_int, [_vp, _c_i64, _vp, _vp]),
 }
 

@@ -41,6 +41,49 @@ def _ws(nbytes: int, device) -> torch.Tensor:
     return torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=device)
 
 
+# Hand-off status of the persistent recurrence kernels (ds2hip.h err_out): one device word per
+# device, OR-ed by every ds2_gru_* / ds2_lstm_* launch and never cleared by the library.  It is
+# read only where the host synchronises anyway (Trainer.poll_status / check_rnn_status), so a
+# hand-off timeout raises Ds2Error instead of turning into a silently NaN-zeroed step.
+RNN_ERR_HANDOFF_TIMEOUT = 1
+_RNN_STATUS = {}
+
+
+def rnn_status_word(device) -> torch.Tensor:
+    device = torch.device(device)
+    if device.index is None:
+        device = torch.device(device.type, torch.cuda.current_device())
+    w = _RNN_STATUS.get(device)
+    if w is None:
+        w = torch.zeros(1, dtype=_I32, device=device)
+        _RNN_STATUS[device] = w
+    return w
+
+
+def rnn_status_error(value: int) -> Optional[str]:
+    if value == 0:
+        return None
+    what = []
+    if value & RNN_ERR_HANDOFF_TIMEOUT:
+        what.append("hand-off timeout (a workgroup of a persistent GRU/LSTM kernel waited past "
+                    "its spin bound; outputs from that step on are NaN)")
+    if value & ~RNN_ERR_HANDOFF_TIMEOUT:
+        what.append(f"unknown status bits 0x{value & ~RNN_ERR_HANDOFF_TIMEOUT:x}")
+    return "recurrence kernel failure: " + "; ".join(what)
+
+
+def check_rnn_status(device=None, reset: bool = True) -> None:
+    """Synchronising read of the device status word; raises Ds2Error if any recurrence launch
+    since the last reset reported a failure."""
+    w = rnn_status_word(device if device is not None else torch.device("cuda"))
+    v = int(w.item())
+    if reset and v:
+        w.zero_()
+    msg = rnn_status_error(v)
+    if msg is not None:
+        raise _lib.Ds2Error(msg)
+
+
 # ----------------------------------------------------------------------------
 # raw ops
 def sgemm(a: torch.Tensor, b: torch.Tensor, c: torch.Tensor, *, m: int, n: int, k: int,
@@ -493,6 +536,30 @@ def _rnn_param_grads(x, h_all, dgx, dgh, weights, nd, g, need_dx, bf16=False):
     return dx, grads
 
 
+# Cooperative-launch guard (optim.GradAllReducer.guard_cooperative): called with the persistent
+# recurrence's workgroup count before each backward launch, while gradient all-reduces of the
+# same step may be in flight on RCCL's stream.
+_COOP_GUARD = [None]
+
+
+def set_cooperative_guard(fn) -> None:
+    _COOP_GUARD[0] = fn
+
+
+def persistent_grid_estimate(n: int, h: int, nd: int) -> int:
+    """Upper bound of the persistent recurrence's grid (rnn_common.h mapped_grid: 16 units x
+    16 samples per workgroup, unit-block pairs padded to multiples of 8); the LSTM's 32-sample
+    workgroups and batch chunks only make it smaller (never above the chip's CU count)."""
+    ub = (h + 15) // 16
+    return 8 * ((ub * nd + 7) // 8) * ((n + 15) // 16)
+
+
+def _guard_cooperative(n, h, nd):
+    g = _COOP_GUARD[0]
+    if g is not None:
+        g(persistent_grid_estimate(n, h, nd))
+
+
 class GRULayerFn(torch.autograd.Function):
     """One (bi)directional GRU layer over padded [T, N, In] input with lengths.
 
@@ -518,7 +585,7 @@ class GRULayerFn(torch.autograd.Function):
         ws = _ws(_lib.size("ds2_gru_fwd_workspace_size", n, h, nd), dev)
         _lib.call("ds2_gru_fwd", t, n, h, nd, xproj.data_ptr(), w_hh_f.data_ptr(), _p(w_hh_r),
                   b_hh_f.data_ptr(), _p(b_hh_r), lens.data_ptr(), h_all.data_ptr(), _p(gates),
-                  ws.data_ptr(), ws.numel(), _stream())
+                  rnn_status_word(dev).data_ptr(), ws.data_ptr(), ws.numel(), _stream())
         ctx.save_for_backward(x, lens, h_all, gates, *weights)
         ctx.cfg = (sum_dirs, h, nd, bf16)
         return _rnn_output(h_all, sum_dirs, nd)
@@ -537,9 +604,11 @@ class GRULayerFn(torch.autograd.Function):
         w_hh_f = weights[1]
         w_hh_r = weights[5] if nd == 2 else None
         ws = _ws(_lib.size("ds2_gru_bwd_workspace_size", n, h, nd), dev)
+        _guard_cooperative(n, h, nd)
         _lib.call("ds2_gru_bwd", t, n, h, nd, dy.data_ptr(), dy_dirs, w_hh_f.data_ptr(),
                   _p(w_hh_r), h_all.data_ptr(), gates.data_ptr(), lens.data_ptr(), dgx.data_ptr(),
-                  dgh.data_ptr(), ws.data_ptr(), ws.numel(), _stream())
+                  dgh.data_ptr(), rnn_status_word(dev).data_ptr(), ws.data_ptr(), ws.numel(),
+                  _stream())
         dx, grads = _rnn_param_grads(x, h_all, dgx, dgh, weights, nd, h3,
                                      ctx.needs_input_grad[0], bf16)
         return (dx, None, None, None, *grads)
@@ -569,7 +638,7 @@ class LSTMLayerFn(torch.autograd.Function):
         ws = _ws(_lib.size("ds2_lstm_fwd_workspace_size", n, h, nd), dev)
         _lib.call("ds2_lstm_fwd", t, n, h, nd, xproj.data_ptr(), w_hh_f.data_ptr(), _p(w_hh_r),
                   b_hh_f.data_ptr(), _p(b_hh_r), lens.data_ptr(), h_all.data_ptr(), _p(c_all),
-                  _p(gates), ws.data_ptr(), ws.numel(), _stream())
+                  _p(gates), rnn_status_word(dev).data_ptr(), ws.data_ptr(), ws.numel(), _stream())
         ctx.save_for_backward(x, lens, h_all, c_all, gates, *weights)
         ctx.cfg = (sum_dirs, h, nd, bf16)
         return _rnn_output(h_all, sum_dirs, nd)
@@ -586,9 +655,10 @@ class LSTMLayerFn(torch.autograd.Function):
         w_hh_f = weights[1]
         w_hh_r = weights[5] if nd == 2 else None
         ws = _ws(_lib.size("ds2_lstm_bwd_workspace_size", n, h, nd), dev)
+        _guard_cooperative(n, h, nd)
         _lib.call("ds2_lstm_bwd", t, n, h, nd, dy.data_ptr(), dy_dirs, w_hh_f.data_ptr(),
                   _p(w_hh_r), c_all.data_ptr(), gates.data_ptr(), lens.data_ptr(), dg.data_ptr(),
-                  ws.data_ptr(), ws.numel(), _stream())
+                  rnn_status_word(dev).data_ptr(), ws.data_ptr(), ws.numel(), _stream())
         dx, grads = _rnn_param_grads(x, h_all, dg, dg, weights, nd, 4 * h,
                                      ctx.needs_input_grad[0], bf16)
         return (dx, None, None, None, *grads)

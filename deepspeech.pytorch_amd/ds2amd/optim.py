@@ -15,6 +15,7 @@ front to back while backward is still running.
 """
 from __future__ import annotations
 
+import os
 from typing import List, Optional
 
 import torch
@@ -95,6 +96,7 @@ class FusedSGD:
         self.skip = torch.zeros(1, dtype=torch.int32, device=dev)
         self.ws = torch.empty(max(16, _lib.size("ds2_optim_workspace_size", flat.numel)),
                               dtype=torch.uint8, device=dev)
+        self.steps = 0
 
     def zero_grad(self):
         self.flat.zero_grad()
@@ -115,17 +117,128 @@ class FusedSGD:
         _lib.call("ds2_clip_sgd_nesterov", self.flat.flat.data_ptr(), self.flat.grad.data_ptr(),
                   self.buf.data_ptr(), self.flat.numel, float(self.lr), float(self.momentum),
                   float(self.max_norm), norm_ptr, _p(skip_flag), _stream())
+        self.steps += 1
+
+    # ---- torch.optim.SGD's state_dict format (model.py:446 optim_dict; train.py:843) ----
+    def _model_order(self):
+        """(param, flat offset) in the reference optimizer's order: model.parameters()
+        (build_optimizer(args, model.parameters()), train.py:139-152, 939)."""
+        return list(zip(reversed(self.flat.params), reversed(self.flat.offsets)))
+
+    def _group_defaults(self):
+        # the installed torch's own SGD param_group keys, so the dict loads into
+        # torch.optim.SGD of this torch version unchanged
+        probe = torch.optim.SGD([torch.zeros(1, requires_grad=True)], lr=self.lr,
+                                momentum=self.momentum, nesterov=True)
+        g = dict(probe.param_groups[0])
+        g.pop('params')
+        return g
 
     def state_dict(self):
-        return {"lr": self.lr, "momentum": self.momentum, "max_norm": self.max_norm,
-                "momentum_buffer": self.buf.detach().cpu()}
+        """torch.optim.SGD(model.parameters(), lr, momentum, nesterov=True).state_dict():
+        per-parameter ``momentum_buffer`` (after the first step) in model.parameters()
+        order and one param_group.  ``max_norm`` is train.py's --max-norm argument, not
+        optimizer state, so it is not stored (as in the reference)."""
+        order = self._model_order()
+        state = {}
+        if self.steps > 0:
+            for i, (p, o) in enumerate(order):
+                state[i] = {'momentum_buffer': self.buf[o:o + p.numel()].detach().view_as(p)
+                            .cpu().clone()}
+        group = self._group_defaults()
+        group['params'] = list(range(len(order)))
+        return {'state': state, 'param_groups': [group]}
 
     def load_state_dict(self, sd):
-        self.lr = sd.get("lr", self.lr)
-        self.momentum = sd.get("momentum", self.momentum)
-        self.max_norm = sd.get("max_norm", self.max_norm)
-        if "momentum_buffer" in sd:
-            self.buf.copy_(sd["momentum_buffer"].to(self.buf.device))
+        """Accepts torch.optim.SGD's format (a reference ``package['optim_dict']``).  Raises
+        on anything else instead of silently restarting the momentum."""
+        if not isinstance(sd, dict) or set(sd) != {'state', 'param_groups'}:
+            raise ValueError("FusedSGD.load_state_dict expects a torch.optim.SGD state_dict "
+                             f"({{'state', 'param_groups'}}), got keys {sorted(sd) if isinstance(sd, dict) else type(sd)}")
+        groups = sd['param_groups']
+        order = self._model_order()
+        if len(groups) != 1:
+            raise ValueError(f"expected one param_group (model.parameters()), got {len(groups)}")
+        g = groups[0]
+        if len(g['params']) != len(order):
+            raise ValueError(f"param_group holds {len(g['params'])} parameters, the model has "
+                             f"{len(order)}")
+        if not g.get('nesterov', False) or g.get('dampening', 0) != 0 or \
+                g.get('weight_decay', 0) != 0 or g.get('maximize', False):
+            raise ValueError("FusedSGD implements SGD(momentum, nesterov=True, dampening=0, "
+                             "weight_decay=0) (train.py:146-149); the state_dict has "
+                             f"nesterov={g.get('nesterov')}, dampening={g.get('dampening')}, "
+                             f"weight_decay={g.get('weight_decay')}")
+        self.lr = float(g['lr'])
+        self.momentum = float(g['momentum'])
+        self.buf.zero_()
+        state = sd['state']
+        for slot, idx in enumerate(g['params']):
+            st = state.get(idx)
+            if not st:
+                continue
+            unknown = set(st) - {'momentum_buffer'}
+            if unknown:
+                raise ValueError(f"unrecognised SGD state keys {sorted(unknown)} for param {idx}")
+            mb = st.get('momentum_buffer')
+            if mb is None:
+                continue
+            p, o = order[slot]
+            if tuple(mb.shape) != tuple(p.shape):
+                raise ValueError(f"momentum_buffer {idx}: shape {tuple(mb.shape)} != parameter "
+                                 f"{tuple(p.shape)}")
+            self.buf[o:o + p.numel()].copy_(mb.reshape(-1).to(self.buf.device, torch.float32))
+        self.steps = max(self.steps, 1 if state else 0)
+
+
+class ParamBroadcaster:
+    """DistributedDataParallel's replica consistency (train.py:947-951): rank 0's parameters
+    and buffers are broadcast once at construction, and (broadcast_buffers=True, DDP's
+    default) rank 0's BatchNorm running statistics before every forward.
+
+    The float buffers (running_mean / running_var, 32.5 KB at cfg2) are re-pointed into one
+    flat tensor so the per-forward sync is ONE broadcast; num_batches_tracked (int64,
+    identical on every rank: one increment per forward) is broadcast once at construction.
+    """
+
+    def __init__(self, model, flat: FlatParams, group=None, broadcast_buffers: bool = True):
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.src = dist.get_global_rank(group, 0) if (group is not None and self.world > 1) else 0
+        self.broadcast_buffers = broadcast_buffers
+        bufs = [b for b in model.buffers() if b.is_floating_point()]
+        self.others = [b for b in model.buffers() if not b.is_floating_point()]
+        total = sum(b.numel() for b in bufs)
+        dev = flat.flat.device
+        self.flat_buffers = torch.zeros(total, dtype=torch.float32, device=dev)
+        o = 0
+        for b in bufs:
+            n = b.numel()
+            self.flat_buffers[o:o + n].copy_(b.data.reshape(-1))
+            b.data = self.flat_buffers[o:o + n].view_as(b)
+            o += n
+        self.flat = flat
+        self.broadcasts = 0
+        if self.world > 1:
+            dist.broadcast(flat.flat, self.src, group=group)
+            dist.broadcast(self.flat_buffers, self.src, group=group)
+            for b in self.others:
+                dist.broadcast(b.data, self.src, group=group)
+            self.broadcasts += 1
+
+    def before_forward(self):
+        if self.world > 1 and self.broadcast_buffers and self.flat_buffers.numel():
+            dist.broadcast(self.flat_buffers, self.src, group=self.group)
+            self.broadcasts += 1
+
+
+def rccl_channel_cap() -> int:
+    """The CTA budget RCCL may hold while a persistent recurrence runs:
+    NCCL_MAX_NCHANNELS, which init_distributed() defaults to 32."""
+    try:
+        return int(os.environ.get("NCCL_MAX_NCHANNELS", "64"))
+    except ValueError:
+        return 64
 
 
 class GradAllReducer:
@@ -135,7 +248,14 @@ class GradAllReducer:
     first).  A post-accumulate hook counts ready parameters per bucket; the
     moment a bucket is complete its all_reduce is issued asynchronously (RCCL
     over xGMI with backend 'nccl', gloo on CPU test rigs) while autograd keeps
-    producing earlier layers' gradients.  ``finish()`` waits and applies 1/world.
+    producing earlier layers' gradients.  ``finish()`` waits and applies 1/world
+    (exact for power-of-two worlds, so it equals DDP's divide-then-sum bit for bit).
+
+    CU budget: the recurrences' backward is ONE cooperative launch that needs all its
+    workgroups resident at once (208 of 256 CUs at cfg2).  ``guard_cooperative(grid)`` is
+    called before each such launch; when the grid plus RCCL's CTA cap would not fit the
+    chip, the compute stream first waits for the all-reduces already in flight (a stream
+    wait, no host sync), so a collective never holds CUs a spinning recurrence needs.
     """
 
     def __init__(self, flat: FlatParams, bucket_mb: float = 40.0, group=None):
@@ -156,6 +276,12 @@ class GradAllReducer:
                 start, members = nxt, []
         self.pending = [0] * len(self.buckets)
         self.handles = [None] * len(self.buckets)
+        self.issued_from_hooks = 0
+        self.guard_waits = 0
+        self.cus = 0
+        if flat.flat.is_cuda:
+            self.cus = torch.cuda.get_device_properties(flat.flat.device).multi_processor_count
+        self.rccl_ctas = rccl_channel_cap()
         self._hooks = []
         # hooks whenever a process group exists (world 1 included: that exercises the
         # RCCL path on a single-GPU box; the all-reduce is then a no-op copy)
@@ -172,6 +298,7 @@ class GradAllReducer:
     def begin(self):
         self.pending = [b[2] for b in self.buckets]
         self.handles = [None] * len(self.buckets)
+        self.issued_from_hooks = 0
 
     def _on_ready(self, p):
         self.flat.adopt(p, self.param_offset[id(p)])
@@ -181,6 +308,17 @@ class GradAllReducer:
             s, e, _ = self.buckets[b]
             self.handles[b] = dist.all_reduce(self.flat.grad[s:e], group=self.group,
                                               async_op=True)
+            self.issued_from_hooks += 1
+
+    def guard_cooperative(self, grid: int):
+        if self.world <= 1 or self.cus <= 0:
+            return
+        if min(grid, self.cus) + self.rccl_ctas <= self.cus:
+            return
+        for h in self.handles:
+            if h is not None:
+                h.wait()
+                self.guard_waits += 1
 
     def finish(self):
         if not self._hooks:

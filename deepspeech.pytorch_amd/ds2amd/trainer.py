@@ -2,13 +2,23 @@
 on the HIP path, with the reference's data-parallel semantics (train.py:804-809,
 947-951; data/utils.py:40-44).
 
-Per batch: input-size quirk (pct * T -> int, float32), forward, greedy decode,
-NaN guard, CTC / N, zero_grad, backward with the bucketed gradient all-reduce
-overlapped, clip_grad_norm_(max_norm) and SGD-Nesterov — the last two as one
-device-resident pass with the NaN-skip decided on the device.
+Per batch: input-size quirk (pct * T -> int, float32), forward, greedy decode (+ the
+per-batch CER/WER of train.py:575-587 on the device), the NaN work-around of
+train.py:595-598 (NaN logits zeroed in place, their gradient zero, the step always
+taken -- the reference's skip check at :625 can never fire after :598), CTC / N,
+zero_grad, backward with the bucketed gradient all-reduce overlapped,
+clip_grad_norm_(max_norm) and SGD-Nesterov as one device-resident pass.
+
+No host synchronisation per step: the reference's two warnings (NaN logits, inf loss)
+and the persistent recurrences' hand-off status (ds2hip.h err_out) travel to the host
+in a small pinned ring and are read once the GPU has finished that step -- at the next
+``train_batch``, in ``poll_status(block=True)``, or when ``return_item=True`` asks for
+the loss value anyway.  A hand-off failure raises ``Ds2Error``.
 """
 from __future__ import annotations
 
+import os
+from collections import deque
 from typing import Optional
 
 import torch
@@ -18,7 +28,7 @@ from . import _lib, ops
 from .ctc import CTCLoss
 from .decoder import GreedyDecoder
 from .ops import _stream
-from .optim import FlatParams, FusedSGD, GradAllReducer
+from .optim import FlatParams, FusedSGD, GradAllReducer, ParamBroadcaster
 
 
 def reduce_tensor(tensor, world_size):
@@ -42,11 +52,53 @@ def get_cer_wer(decoder, transcript, reference):
     return wer, cer, wer_ref, cer_ref
 
 
+def init_distributed(backend: str = "nccl", device_id: Optional[int] = None):
+    """One process per GPU (torch.distributed.run env).  Before the communicator exists,
+    cap RCCL's channels (= CTAs it may hold) at 32 unless the user chose otherwise, so an
+    all-reduce overlapping the backward always leaves the persistent recurrence its 208
+    co-resident workgroups."""
+    os.environ.setdefault("NCCL_MAX_NCHANNELS", "32")
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    local = int(os.environ.get("LOCAL_RANK", "0")) if device_id is None else device_id
+    if backend == "nccl":
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        dist.init_process_group(backend)
+    return local
+
+
+class _ZeroNaN(torch.autograd.Function):
+    """train.py:595-598 ``logits[torch.isnan(logits)] = 0`` as an in-place op: NaNs become 0
+    (ds2_nan_guard, which also sets the step's flag and records a byte mask) and, as for
+    autograd's index_put, the zeroed positions pass no gradient (ds2_zero_masked, a no-op
+    unless the flag is set)."""
+
+    @staticmethod
+    def forward(ctx, x, flag, mask):
+        _lib.call("ds2_nan_guard", x.data_ptr(), x.numel(), 1, flag.data_ptr(), mask.data_ptr(),
+                  _stream())
+        ctx.mark_dirty(x)
+        ctx.save_for_backward(flag, mask)
+        return x
+
+    @staticmethod
+    def backward(ctx, g):
+        flag, mask = ctx.saved_tensors
+        g = g.contiguous().clone()
+        _lib.call("ds2_zero_masked", g.data_ptr(), mask.data_ptr(), g.numel(), flag.data_ptr(),
+                  _stream())
+        return g, None, None
+
+
 class Trainer:
     """Owns the model's flat buffers, the fused optimizer and the gradient reducer."""
 
+    STATUS_RING = 4
+
     def __init__(self, model, labels, lr=3e-4, momentum=0.9, max_norm=100.0, device=None,
-                 bucket_mb=40.0, decode=True, score=False, group=None):
+                 bucket_mb=40.0, decode=True, score=False, group=None, broadcast_buffers=True,
+                 verbose=True):
         self.device = torch.device(device) if device is not None else torch.device('cuda')
         self.model = model.to(self.device)
         self.model.train()
@@ -54,13 +106,29 @@ class Trainer:
         self.optimizer = FusedSGD(self.flat, lr=lr, momentum=momentum, max_norm=max_norm)
         self.reducer = GradAllReducer(self.flat, bucket_mb=bucket_mb, group=group)
         self.world = self.reducer.world
+        # DDP: rank 0's parameters and buffers everywhere (construction), rank 0's BN running
+        # statistics before every forward (broadcast_buffers, train.py:950-951)
+        self.sync = ParamBroadcaster(self.model, self.flat, group=group,
+                                     broadcast_buffers=broadcast_buffers)
+        if dist.is_initialized():
+            ops.set_cooperative_guard(self.reducer.guard_cooperative)
         self.criterion = CTCLoss()
         self.decoder = GreedyDecoder(labels)
         self.decode = decode
         self.score = score
+        self.verbose = verbose
         self.nan_flag = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self._nan_mask = None
         # device accumulators of (wer, cer, words, chars): no host sync per batch
         self._score_acc = torch.zeros(4, dtype=torch.float64, device=self.device)
+        self._rnn_word = ops.rnn_status_word(self.device)
+        # pinned ring of (nan flag, rnn status, loss bits) per in-flight step
+        self._ring = [torch.zeros(3, dtype=torch.int32).pin_memory()
+                      for _ in range(self.STATUS_RING)]
+        self._ring_next = 0
+        self._inflight = deque()
+        self._status = torch.zeros(3, dtype=torch.int32, device=self.device)
+        self.warnings = {"nan": 0, "inf_loss": 0}
 
     # train.py:584-587 running sums, read lazily (one device->host copy)
     @property
@@ -79,10 +147,57 @@ class Trainer:
     def num_chars(self):
         return float(self._score_acc[3])
 
+    # ---- deferred status --------------------------------------------------------------
+    def _record_status(self, loss):
+        """Stage (nan flag, recurrence status, loss bits) of this step for the host."""
+        st = self._status
+        st[0:1].copy_(self.nan_flag)
+        st[1:2].copy_(self._rnn_word)
+        st[2:3].copy_(loss.detach().reshape(1).view(torch.int32))
+        if len(self._inflight) == self.STATUS_RING:
+            self._drain_one(block=True)
+        buf = self._ring[self._ring_next]
+        self._ring_next = (self._ring_next + 1) % self.STATUS_RING
+        buf.copy_(st, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self._inflight.append((ev, buf))
+
+    def _drain_one(self, block: bool) -> bool:
+        ev, buf = self._inflight[0]
+        if not block and not ev.query():
+            return False
+        ev.synchronize()
+        self._inflight.popleft()
+        nan, err, loss_bits = (int(v) for v in buf.tolist())
+        loss = torch.tensor([loss_bits], dtype=torch.int32).view(torch.float32).item()
+        msg = ops.rnn_status_error(err)
+        if msg is not None:
+            self._rnn_word.zero_()
+            raise _lib.Ds2Error(msg)
+        if nan:
+            self.warnings["nan"] += 1
+            if self.verbose:
+                print("WARNING: Working around NaNs in data")          # train.py:597
+        if loss in (float('inf'), float('-inf')):
+            self.warnings["inf_loss"] += 1
+            if self.verbose:
+                print("WARNING: received an inf loss, setting loss value to 1000")   # :608
+        return True
+
+    def poll_status(self, block: bool = False) -> None:
+        """Read the status of finished steps (all in-flight steps with block=True); raises
+        Ds2Error if a recurrence kernel reported a hand-off failure."""
+        while self._inflight and self._drain_one(block):
+            pass
+
+    # ---- the step ---------------------------------------------------------------------
     def train_batch(self, data, return_item: bool = False):
+        self.poll_status(block=False)
         inputs, targets, filenames, input_percentages, target_sizes = data
         input_sizes = input_percentages.mul_(int(inputs.size(3))).int()   # train.py:557 quirk
         inputs = inputs.to(self.device, non_blocking=True)
+        self.sync.before_forward()
         logits, probs, output_sizes = self.model(inputs, input_sizes)
 
         if self.decode:
@@ -92,8 +207,9 @@ class Trainer:
 
         logits = logits.transpose(0, 1)                                   # T x N x C
         self.nan_flag.zero_()
-        _lib.call("ds2_nan_guard", logits.data_ptr(), logits.numel(), 1,
-                  self.nan_flag.data_ptr(), _stream())                    # train.py:595-598
+        if self._nan_mask is None or self._nan_mask.numel() < logits.numel():
+            self._nan_mask = torch.empty(logits.numel(), dtype=torch.uint8, device=self.device)
+        logits = _ZeroNaN.apply(logits, self.nan_flag, self._nan_mask)    # train.py:595-598
         loss = self.criterion(logits, targets, output_sizes, target_sizes)
         loss = loss / inputs.size(0)
 
@@ -101,10 +217,12 @@ class Trainer:
         self.reducer.begin()
         loss.backward()
         self.reducer.finish()
-        self.optimizer.step(skip_flag=self.nan_flag)                       # clip + SGD, NaN skip
+        self.optimizer.step()               # clip + SGD; always taken (see module docstring)
         if self.world > 1:
             loss = reduce_tensor(loss.detach(), self.world)
+        self._record_status(loss)
         if return_item:
+            self.poll_status(block=True)
             v = float(loss.item())
             if v in (float('inf'), float('-inf')):
                 v = 1000.0

@@ -172,12 +172,20 @@ ds2_status_t ds2_bn_backward(const float* dy, int dy_layout, const float* x, int
  *   xproj : [T][N][D][3H]  x @ W_ih^T + b_ih for each direction
  *   h_all : [T][N][D][H]   per-direction hidden states (output)
  *   gates : [T][N][D][4H]  (r, z, n, W_hn h + b_hn) cache for backward, or NULL
- * num_dirs = 1 or 2; w_hh_r / b_hh_r ignored when num_dirs == 1.              */
+ * num_dirs = 1 or 2; w_hh_r / b_hh_r ignored when num_dirs == 1.
+ * err_out: NULL, or a caller-owned device status word; the persistent
+ * (one-launch-per-layer) kernels OR their hand-off status into it after the
+ * launch (DS2_RNN_ERR_HANDOFF_TIMEOUT: a workgroup waited past the spin bound,
+ * its outputs from that step on are NaN).  The word is never cleared by the
+ * library, so one word can collect a whole training step; the caller reads
+ * it whenever it synchronises anyway (same convention for ds2_gru_bwd and
+ * ds2_lstm_fwd / ds2_lstm_bwd).                                               */
+#define DS2_RNN_ERR_HANDOFF_TIMEOUT 1u
 size_t ds2_gru_fwd_workspace_size(int n, int h, int num_dirs);
 ds2_status_t ds2_gru_fwd(int t_max, int n, int h, int num_dirs, const float* xproj,
                          const float* w_hh_f, const float* w_hh_r, const float* b_hh_f,
                          const float* b_hh_r, const int* lens, float* h_all, float* gates,
-                         void* ws, size_t ws_bytes, ds2_stream_t stream);
+                         unsigned* err_out, void* ws, size_t ws_bytes, ds2_stream_t stream);
 size_t ds2_gru_bwd_workspace_size(int n, int h, int num_dirs);
 /* dy: [T][N][dy_dirs][H]; dy_dirs = 1: gradient of the direction-summed output
  * (model.py:107), dy_dirs = num_dirs: per-direction output gradient.
@@ -186,7 +194,7 @@ size_t ds2_gru_bwd_workspace_size(int n, int h, int num_dirs);
 ds2_status_t ds2_gru_bwd(int t_max, int n, int h, int num_dirs, const float* dy, int dy_dirs,
                          const float* w_hh_f, const float* w_hh_r, const float* h_all,
                          const float* gates, const int* lens, float* dgates_x, float* dgates_h,
-                         void* ws, size_t ws_bytes, ds2_stream_t stream);
+                         unsigned* err_out, void* ws, size_t ws_bytes, ds2_stream_t stream);
 
 /* ------------------------------------------------------------------------ */
 /* (Bi)directional LSTM recurrence (torch gate order i, f, g, o), same packed-
@@ -200,14 +208,15 @@ size_t ds2_lstm_fwd_workspace_size(int n, int h, int num_dirs);
 ds2_status_t ds2_lstm_fwd(int t_max, int n, int h, int num_dirs, const float* xproj,
                           const float* w_hh_f, const float* w_hh_r, const float* b_hh_f,
                           const float* b_hh_r, const int* lens, float* h_all, float* c_all,
-                          float* gates, void* ws, size_t ws_bytes, ds2_stream_t stream);
+                          float* gates, unsigned* err_out, void* ws, size_t ws_bytes,
+                          ds2_stream_t stream);
 size_t ds2_lstm_bwd_workspace_size(int n, int h, int num_dirs);
 /* dy as for ds2_gru_bwd.  dgates: [T][N][D][4H] gradient wrt the gate
  * pre-activations (= wrt xproj and wrt W_hh h + b_hh).                       */
 ds2_status_t ds2_lstm_bwd(int t_max, int n, int h, int num_dirs, const float* dy, int dy_dirs,
                           const float* w_hh_f, const float* w_hh_r, const float* c_all,
-                          const float* gates, const int* lens, float* dgates, void* ws,
-                          size_t ws_bytes, ds2_stream_t stream);
+                          const float* gates, const int* lens, float* dgates, unsigned* err_out,
+                          void* ws, size_t ws_bytes, ds2_stream_t stream);
 
 /* ------------------------------------------------------------------------ */
 /* Lookahead convolution, ref model.py:140-177 (Lookahead.forward), optionally
@@ -303,9 +312,14 @@ ds2_status_t ds2_clip_sgd_nesterov(float* params, const float* grads, float* mom
                                    const float* norm, const int* skip_flag,
                                    ds2_stream_t stream);
 /* *flag = 1 if any x is NaN (flag must be zeroed by the caller first);
- * if zero_nans, NaNs are replaced by 0 in place (train.py:595-598).           */
+ * if zero_nans, NaNs are replaced by 0 in place (train.py:595-598); mask
+ * (nullable, one byte per element) records where the NaNs were.              */
 ds2_status_t ds2_nan_guard(float* x, int64_t numel, int zero_nans, int* flag,
-                           ds2_stream_t stream);
+                           unsigned char* mask, ds2_stream_t stream);
+/* Gradient of that in-place zeroing (autograd's index_put, train.py:598):
+ * x[i] = 0 where mask[i]; a no-op when flag is non-NULL and *flag == 0.      */
+ds2_status_t ds2_zero_masked(float* x, const unsigned char* mask, int64_t numel, const int* flag,
+                             ds2_stream_t stream);
 /* x[i] *= *scalar (device scalar, e.g. autograd's grad_output). */
 ds2_status_t ds2_scale_by_device_scalar(float* x, int64_t numel, const float* scalar,
                                         ds2_stream_t stream);

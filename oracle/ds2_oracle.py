@@ -248,12 +248,24 @@ def greedy_decode(probs: torch.Tensor, sizes: Optional[Sequence[int]], labels: s
 # ----------------------------------------------------------------------------
 # training step: train.py:555-632 (+ build_optimizer train.py:139-152)
 def train_step(model: OracleDS2, x, input_percentages, targets, target_sizes, lr=3e-4,
-               momentum=0.9, max_norm=100.0, momentum_buffers: Optional[dict] = None):
-    """One reference training step on CPU.  Returns (loss, new_params, buffers, grads)."""
+               momentum=0.9, max_norm=100.0, momentum_buffers: Optional[dict] = None,
+               plant_nan: Optional[torch.Tensor] = None):
+    """One reference training step on CPU.  Returns (loss, new_params, buffers, grads, norm).
+
+    plant_nan: optional bool mask over the logits [N, T', C] set to NaN right after the
+    forward (a test hook standing in for bad data); the step then follows train.py:595-598
+    (NaN logits zeroed in place, zero gradient there) and, as the reference does once
+    they are zeroed, always steps (the skip at :625 cannot fire).
+    """
     input_sizes = input_sizes_quirk(input_percentages, x.shape[3])
     params = {k: v.detach().clone().requires_grad_(True) for k, v in model.parameters().items()}
     logits, probs, out_lens, _ = model.forward(x, input_sizes, training=True, params=params)
+    if plant_nan is not None:
+        logits = logits.masked_fill(plant_nan, float('nan'))
     acts = logits.transpose(0, 1)
+    if torch.isnan(acts).any():                   # train.py:595-598
+        acts = acts.clone()
+        acts[torch.isnan(acts)] = 0
     lp = F.log_softmax(acts, dim=2)
     loss = F.ctc_loss(lp, targets.long(), out_lens.long(), target_sizes.long(), blank=0,
                       reduction='sum') / x.shape[0]
@@ -272,3 +284,15 @@ def train_step(model: OracleDS2, x, input_percentages, targets, target_sizes, lr
         d = g + momentum * b                      # nesterov
         new[k] = params[k].detach() - lr * d
     return loss.detach(), new, bufs, grads, total.detach()
+
+
+def momentum_from_optim_dict(param_names: Sequence[str], optim_dict: dict) -> dict:
+    """torch.optim.SGD state_dict (model.py:446 package['optim_dict']) -> {name: momentum
+    buffer}; the SGD's params are model.parameters() in registration order (train.py:939)."""
+    group = optim_dict['param_groups'][0]
+    out = {}
+    for name, idx in zip(param_names, group['params']):
+        st = optim_dict['state'].get(idx)
+        if st and st.get('momentum_buffer') is not None:
+            out[name] = st['momentum_buffer'].detach().clone().float()
+    return out

@@ -29,13 +29,13 @@ wsb = torch.zeros(_lib.size("ds2_gru_bwd_workspace_size", N, H, D), dtype=torch.
 def fwd():
     _lib.call("ds2_gru_fwd", T, N, H, D, xproj.data_ptr(), w[0].data_ptr(), w[1].data_ptr(),
               b[0].data_ptr(), b[1].data_ptr(), lens.data_ptr(), h_all.data_ptr(),
-              gates.data_ptr(), wsf.data_ptr(), wsf.numel(), ops._stream())
+              gates.data_ptr(), None, wsf.data_ptr(), wsf.numel(), ops._stream())
 
 
 def bwd():
     _lib.call("ds2_gru_bwd", T, N, H, D, dy.data_ptr(), 1, w[0].data_ptr(), w[1].data_ptr(),
               h_all.data_ptr(), gates.data_ptr(), lens.data_ptr(), dgx.data_ptr(),
-              dgh.data_ptr(), wsb.data_ptr(), wsb.numel(), ops._stream())
+              dgh.data_ptr(), None, wsb.data_ptr(), wsb.numel(), ops._stream())
 
 
 def timed(fn, reps=5):

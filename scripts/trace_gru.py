@@ -33,7 +33,7 @@ grid = 8 * ((P + 7) // 8) * BT
 for it in range(3):
     _lib.call("ds2_gru_fwd", T, N, H, D, xproj.data_ptr(), w[0].data_ptr(), w[1].data_ptr(),
               b[0].data_ptr(), b[1].data_ptr(), lens.data_ptr(), h_all.data_ptr(),
-              gates.data_ptr(), ws.data_ptr(), ws.numel(), ops._stream())
+              gates.data_ptr(), None, ws.data_ptr(), ws.numel(), ops._stream())
     torch.cuda.synchronize()
 
 
@@ -93,7 +93,7 @@ wsb = torch.zeros(_lib.size("ds2_gru_bwd_workspace_size", N, H, D), dtype=torch.
 for it in range(3):
     _lib.call("ds2_gru_bwd", T, N, H, D, dy.data_ptr(), 1, w[0].data_ptr(), w[1].data_ptr(),
               h_all.data_ptr(), gates.data_ptr(), lens.data_ptr(), dgx.data_ptr(), dgh.data_ptr(),
-              wsb.data_ptr(), wsb.numel(), ops._stream())
+              None, wsb.data_ptr(), wsb.numel(), ops._stream())
     torch.cuda.synchronize()
 KS3 = (3 * H + 3) // 4
 offb = al(D * UB * KS3 * 64 * 4) + al(2 * N * D * H * 4) + al((D * BT + 1 + D * BT * 64) * 4)

@@ -248,6 +248,45 @@ def golden_package(path, seed=1234):
     print('wrote', path, sorted(pkg))
 
 
+def golden_resume(pkg_path, npz_path, seed=1234):
+    """Optimizer-state compatibility (model.py:446 package['optim_dict'] =
+    optimizer.state_dict(); train.py:838-844 resume): the tiny model after ONE reference
+    train step with torch.optim.SGD(nesterov), serialized by the reference's own serialize
+    (weights, BN buffers and the SGD state dict), plus the parameters after a SECOND step on
+    the same batch -- what a resumed run must reproduce."""
+    g0 = np.load(os.path.join(HERE, 'tiny_ds2.npz'))
+    m = make_ref(seed, 16, 2)
+    m.train()
+    opt = torch.optim.SGD(m.parameters(), lr=3e-4, momentum=0.9, nesterov=True)
+    x = torch.from_numpy(g0['x'])
+    tg = torch.from_numpy(g0['targets']).long()
+    tl = torch.from_numpy(g0['target_sizes']).long()
+    input_sizes = torch.from_numpy(g0['pct']).clone().mul_(x.shape[3]).int()
+
+    def step():
+        lg, _, ol = ref_forward(m, x, input_sizes)
+        acts = lg.transpose(0, 1)
+        loss = F.ctc_loss(F.log_softmax(acts, 2), tg, ol.long(), tl, reduction='sum') / x.shape[0]
+        opt.zero_grad()
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(m.parameters(), 100.0)
+        opt.step()
+        return float(loss)
+
+    loss1 = step()
+    pkg = ref_model.DeepSpeech.serialize(m, optimizer=opt, epoch=0, iteration=0)
+    torch.save(pkg, pkg_path)
+    loss2 = step()
+    out = dict(loss1=np.float32(loss1), loss2=np.float32(loss2))
+    for k, v in m.state_dict().items():
+        if v.is_floating_point():
+            out['after_step2/' + k] = v.numpy()
+    for i, st in opt.state_dict()['state'].items():
+        out[f'momentum2/{i}'] = st['momentum_buffer'].numpy()
+    np.savez_compressed(npz_path, **out)
+    print('wrote', pkg_path, npz_path, 'losses', loss1, loss2)
+
+
 if __name__ == '__main__':
     torch.set_num_threads(8)
     golden_tiny(os.path.join(HERE, 'tiny_ds2.npz'))
@@ -260,3 +299,4 @@ if __name__ == '__main__':
     golden_decoder(os.path.join(HERE, 'greedy_decoder.npz'))
     golden_seq_lens(os.path.join(HERE, 'seq_lens.npz'))
     golden_package(os.path.join(HERE, 'tiny_ref_package.pth'))
+    golden_resume(os.path.join(HERE, 'tiny_ref_resume.pth'), os.path.join(HERE, 'tiny_resume.npz'))

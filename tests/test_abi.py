@@ -59,3 +59,22 @@ def test_invalid_args_rejected_without_launch():
                             None) == 1
     with pytest.raises(_lib.Ds2Error):
         _lib.call("ds2_dirsum", None, -1, 2, 4, None, None)
+
+
+def declared_arities():
+    """{symbol: number of parameters} from the prototypes in ds2hip.h."""
+    text = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    out = {}
+    for m in re.finditer(r"\b(ds2_[a-z0-9_]+)\s*\(([^;{]*?)\)\s*;", text):
+        args = m.group(2).strip()
+        out[m.group(1)] = 0 if args in ("", "void") else args.count(",") + 1
+    return out
+
+
+def test_ctypes_prototypes_match_header_arity():
+    """Every ctypes prototype has exactly as many arguments as the C declaration (a changed
+    signature, e.g. the err_out word of the recurrences, cannot drift silently)."""
+    ar = declared_arities()
+    for name, (_, argtypes) in _lib._PROTOS.items():
+        assert name in ar, name
+        assert len(argtypes) == ar[name], f"{name}: ctypes {len(argtypes)} vs header {ar[name]}"

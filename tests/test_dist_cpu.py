@@ -104,3 +104,57 @@ def test_distributed_bucketing_sampler_matches_reference_semantics():
     s0.shuffle(5)
     s1.shuffle(5)
     assert list(s0) == list(s1)              # epoch-seeded, identical on every rank
+
+
+class _BNNet(torch.nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.lin = torch.nn.Linear(4, 6)
+        self.bn = torch.nn.BatchNorm1d(6)
+
+    def forward(self, x):
+        return self.bn(self.lin(x))
+
+
+def _bcast_worker(rank, world, port, out_q):
+    from ds2amd.optim import ParamBroadcaster
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(100 + rank)                 # deliberately different replicas
+    m = _BNNet()
+    m.bn.running_mean.fill_(float(rank + 1))
+    flat = FlatParams(list(m.parameters()), "cpu")
+    sync = ParamBroadcaster(m, flat)
+    after_init = [p.detach().numpy().copy() for p in m.parameters()]
+    rm0 = m.bn.running_mean.numpy().copy()
+    m.train()
+    g = torch.Generator().manual_seed(rank)       # different data per rank
+    m(torch.randn(8, 4, generator=g))             # local BN stats diverge here
+    sync.before_forward()                         # DDP: rank 0's buffers win before a forward
+    out_q.put((rank, after_init, rm0, m.bn.running_mean.numpy().copy(),
+               m.bn.running_var.numpy().copy(), int(m.bn.num_batches_tracked)))
+    dist.destroy_process_group()
+
+
+def test_param_broadcaster_matches_ddp_semantics():
+    """DistributedDataParallel (train.py:947-951): rank 0's parameters and buffers are
+    broadcast at construction; rank 0's BN running stats before every forward
+    (broadcast_buffers=True)."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bcast_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (_, p0, rm0_0, rm_0, rv_0, nb0), (_, p1, rm0_1, rm_1, rv_1, nb1) = res
+    for a, b in zip(p0, p1):
+        assert (a == b).all()
+    assert (rm0_0 == 1.0).all() and (rm0_1 == 1.0).all()     # rank 0's buffer everywhere
+    assert (rm_0 == rm_1).all() and (rv_0 == rv_1).all()
+    assert nb0 == nb1 == 1

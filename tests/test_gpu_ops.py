@@ -674,17 +674,26 @@ def test_fused_sgd_matches_torch(dev):
             _close(p, r, 1e-6, f"sgd step {step}")
 
 
-def test_nan_guard_and_skip(dev):
+def test_nan_guard_mask_and_skip(dev):
     from ds2amd.optim import FlatParams, FusedSGD
-    x = torch.tensor([1.0, float('nan'), 3.0], device=dev)
+    x = torch.tensor([1.0, float('nan'), 3.0, float('nan')], device=dev)
     flag = torch.zeros(1, dtype=torch.int32, device=dev)
-    _lib.call("ds2_nan_guard", x.data_ptr(), 3, 1, flag.data_ptr(), ops._stream())
-    assert flag.item() == 1 and x.tolist() == [1.0, 0.0, 3.0]
+    mask = torch.full((4,), 7, dtype=torch.uint8, device=dev)
+    _lib.call("ds2_nan_guard", x.data_ptr(), 4, 1, flag.data_ptr(), mask.data_ptr(), ops._stream())
+    assert flag.item() == 1 and x.tolist() == [1.0, 0.0, 3.0, 0.0]
+    assert mask.tolist() == [0, 1, 0, 1]
+    g = torch.tensor([5.0, 6.0, 7.0, 8.0], device=dev)
+    _lib.call("ds2_zero_masked", g.data_ptr(), mask.data_ptr(), 4, flag.data_ptr(), ops._stream())
+    assert g.tolist() == [5.0, 0.0, 7.0, 0.0]
+    clean = torch.zeros(1, dtype=torch.int32, device=dev)       # flag 0: no-op
+    g2 = torch.tensor([5.0, 6.0, 7.0, 8.0], device=dev)
+    _lib.call("ds2_zero_masked", g2.data_ptr(), mask.data_ptr(), 4, clean.data_ptr(), ops._stream())
+    assert g2.tolist() == [5.0, 6.0, 7.0, 8.0]
     p = torch.nn.Parameter(torch.ones(8, device=dev))
     flat = FlatParams([p], dev)
     opt = FusedSGD(flat, lr=1.0, momentum=0.9)
     p.grad.fill_(1.0)
-    opt.step(skip_flag=flag)
+    opt.step(skip_flag=flag)          # the C ABI's optional skip word still works
     assert torch.all(p == 1).item()
 
 

@@ -1,0 +1,311 @@
+"""GPU: the training step (ds2amd.trainer.Trainer = train.py:555-632) at the benchmark's own
+shape, its failure semantics, optimizer-state resume and the data-parallel hook path, each
+against the CPU oracle (itself pinned by the reference goldens, tests/test_oracle_golden.py).
+
+Tolerances (north_star / DESIGN.md §2): loss and logits within 1e-4 relative
+(max |diff| / max |ref|); every parameter gradient within 5e-4 relative (BPTT over 501 steps in
+fp32 with a different summation order than MIOpen/ATen); lengths, argmax and decoded strings
+bit-exact.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from ds2amd import _lib, ops
+from ds2amd import model as dsm
+from ds2amd.trainer import Trainer
+from oracle import ds2_oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+LABELS = orc.LABELS
+CONF = dict(sample_rate=16000, window_size=0.02, window_stride=0.01, window='hamming')
+
+
+def _rel(got, ref):
+    got = got.detach().double().cpu()
+    ref = ref.detach().double().cpu() if torch.is_tensor(ref) else torch.from_numpy(ref).double()
+    return (got - ref).abs().max().item() / max(ref.abs().max().item(), 1e-30)
+
+
+def _build(seed, hidden, layers, rnn_type='gru', bidirectional=True):
+    torch.manual_seed(seed)
+    return dsm.DeepSpeech(rnn_type=rnn_type, labels=LABELS, rnn_hidden_size=hidden,
+                          nb_layers=layers, audio_conf=CONF, bidirectional=bidirectional)
+
+
+def _threads():
+    torch.set_num_threads(max(1, min(16, int(os.environ.get("OMP_NUM_THREADS") or 16))))
+
+
+def _targets(g, lens):
+    tg = []
+    for L in lens:
+        prev = -1
+        for _ in range(L):
+            v = int(torch.randint(1, 29, (1,), generator=g))
+            while v == prev:
+                v = int(torch.randint(1, 29, (1,), generator=g))
+            tg.append(v)
+            prev = v
+    return torch.tensor(tg, dtype=torch.int32), torch.tensor(lens, dtype=torch.int32)
+
+
+def _spect_batch(g, t_list, t_max):
+    x = torch.zeros(len(t_list), 1, 161, t_max)
+    for i, t in enumerate(t_list):
+        x[i, 0, :, :t] = torch.randn(161, t, generator=g)
+    return x
+
+
+# --------------------------------------------------------------------------- benchmark shape
+def test_benchmark_train_step_matches_oracle(dev):
+    """5 x BiGRU-800 at T = 1001 (10 s), bs 4, variable lengths through input_percentages
+    with the float32 quirk lengths of T_max = 1001 (508 -> 507, 254 -> 253; train.py:557):
+    the full Trainer.train_batch (forward, decode, CTC, BPTT over 501 steps through both
+    batch tiles of the persistent kernels, clip, SGD-Nesterov) vs oracle.train_step."""
+    _threads()
+    t_list = [1001, 877, 508, 254]
+    g = torch.Generator().manual_seed(11)
+    x = _spect_batch(g, t_list, 1001)
+    pct = torch.tensor([t / 1001.0 for t in t_list], dtype=torch.float32)
+    tg, tl = _targets(g, [150, 120, 80, 40])
+    m = _build(123456, 800, 5)
+    o = orc.OracleDS2({k: v.detach().clone() for k, v in m.state_dict().items()}, 5, 800)
+    before = {k: v.detach().clone() for k, v in m.named_parameters()}
+    tr = Trainer(m, LABELS, lr=3e-4, momentum=0.9, max_norm=100.0, device=dev)
+    loss = tr.train_batch((x, tg, None, pct.clone(), tl), return_item=True)
+    rloss, rnew, _, rgrads, rnorm = orc.train_step(o, x, pct.clone(), tg, tl)
+    assert abs(loss - float(rloss)) <= 1e-4 * abs(float(rloss))
+    assert abs(float(tr.optimizer.norm.item()) - float(rnorm)) <= 1e-4 * float(rnorm)
+    worst = {}
+    for name, p in m.named_parameters():
+        worst[name] = _rel(p.grad, rgrads[name])
+        assert worst[name] <= 5e-4, (name, worst[name])
+        # the update itself (p_new - p_old), not just p_new (dominated by p_old); both
+        # differences carry the float32 rounding of p_new (half an ulp of |p| each)
+        d = p.detach().cpu() - before[name]
+        rd = rnew[name] - before[name]
+        ulp = torch.finfo(torch.float32).eps * before[name].abs().max().item()
+        assert (d - rd).abs().max().item() <= 5e-4 * rd.abs().max().item() + ulp, (name, 'update')
+    for k, v in m.state_dict().items():
+        if 'running' in k:
+            assert _rel(v, o.sd[k]) <= 1e-5, k
+
+
+def test_benchmark_bs32_forward_matches_oracle(dev):
+    """The benchmark batch itself (bs 32, 10 s, equal lengths), train-mode forward without
+    grad: logits and probs within 1e-4, output lengths exact, BN running stats 1e-5."""
+    _threads()
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(32, 1, 161, 1001, generator=g)
+    sizes = torch.full((32,), 1001, dtype=torch.int32)
+    m = _build(123456, 800, 5).to(dev).train()
+    o = orc.OracleDS2({k: v.detach().cpu().clone() for k, v in m.state_dict().items()}, 5, 800)
+    with torch.no_grad():
+        logits, probs, out_lens = m(x.to(dev), sizes)
+        rl, rp, ro, _ = o.forward(x, sizes, training=True)
+    np.testing.assert_array_equal(out_lens.cpu().numpy(), ro.numpy())
+    assert _rel(logits, rl) < 1e-4
+    assert _rel(probs, rp) < 1e-4
+    for k, v in m.state_dict().items():
+        if 'running' in k:
+            assert _rel(v, o.sd[k]) <= 1e-5, k
+
+
+# --------------------------------------------------------------------------- failure semantics
+def test_nan_logits_zeroed_and_step_taken_like_reference(dev, golden_dir):
+    """train.py:595-598,625: NaN logits are zeroed in place (zero gradient there) and the
+    SGD step is taken -- post-step parameters equal the oracle's with the same planted NaNs;
+    the reference's warning is counted (printed lazily, no per-step host sync)."""
+    g = np.load(os.path.join(golden_dir, 'tiny_ds2.npz'))
+    m = _build(int(g['seed']), int(g['hidden']), int(g['layers']))
+    o = orc.OracleDS2({k: v.detach().clone() for k, v in m.state_dict().items()}, 2, 16)
+    x = torch.from_numpy(g['x'])
+    n, t = x.shape[0], int(g['out_lens'].max())
+    plant = torch.zeros(n, t, len(LABELS), dtype=torch.bool)
+    plant[0, 3, 5] = plant[1, 10, 0] = plant[2, 7, 29] = plant[0, 20, 11] = True
+
+    def hook(mod, inp, out):          # the FC output [T', N, C] of the HIP model
+        out = out.clone()
+        out[plant.transpose(0, 1).to(out.device)] = float('nan')
+        return out
+
+    m.fc.register_forward_hook(hook)
+    tr = Trainer(m, LABELS, lr=3e-4, momentum=0.9, max_norm=100.0, device=dev, verbose=False)
+    data = (x, torch.from_numpy(g['targets']), None, torch.from_numpy(g['pct']).clone(),
+            torch.from_numpy(g['target_sizes']))
+    loss = tr.train_batch(data, return_item=True)
+    rloss, rnew, _, _, _ = orc.train_step(o, x, torch.from_numpy(g['pct']).clone(),
+                                          torch.from_numpy(g['targets']),
+                                          torch.from_numpy(g['target_sizes']), plant_nan=plant)
+    assert np.isfinite(loss)
+    assert abs(loss - float(rloss)) <= 1e-4 * abs(float(rloss))
+    assert tr.warnings['nan'] == 1
+    for name, p in m.named_parameters():
+        ref = rnew[name]
+        assert torch.isfinite(p).all().item(), name
+        assert (p.detach().cpu() - ref).abs().max().item() <= 1e-6 + 1e-5 * ref.abs().max().item(), name
+
+
+def test_rnn_handoff_timeout_raises(dev, monkeypatch):
+    """A persistent recurrence whose hand-off times out (spin bound forced to 0 through
+    DS2_RNN_SPIN_LIMIT) must raise Ds2Error from the Trainer, not turn into a silently
+    NaN-zeroed step; with the bound restored the same step runs clean."""
+    g = torch.Generator().manual_seed(2)
+    x = torch.randn(32, 1, 161, 301, generator=g)
+    tg, tl = _targets(g, [20] * 32)
+    pct = torch.ones(32)
+    ops.rnn_status_word(dev).zero_()
+    monkeypatch.setenv("DS2_RNN_SPIN_LIMIT", "0")
+    tr = Trainer(_build(3, 256, 2), LABELS, device=dev, verbose=False)
+    with pytest.raises(_lib.Ds2Error, match="hand-off"):
+        tr.train_batch((x, tg, None, pct.clone(), tl), return_item=True)
+    # the op-level query sees it too
+    lens = torch.full((32,), 151, dtype=torch.int32, device=dev)
+    xs = torch.randn(151, 32, 256, device=dev)
+    layer = dsm.GRU(256, 256, bidirectional=True).to(dev)
+    with torch.no_grad():
+        layer.run(xs, lens)
+    with pytest.raises(_lib.Ds2Error, match="hand-off"):
+        ops.check_rnn_status(dev)
+    monkeypatch.delenv("DS2_RNN_SPIN_LIMIT")
+    tr2 = Trainer(_build(3, 256, 2), LABELS, device=dev, verbose=False)
+    v = tr2.train_batch((x, tg, None, pct.clone(), tl), return_item=True)
+    assert np.isfinite(v)
+    ops.check_rnn_status(dev)          # clean
+
+
+# --------------------------------------------------------------------------- resume
+def test_resume_from_reference_package(dev, golden_dir):
+    """train.py:827-844: a package written by the reference's serialize after one SGD step
+    (weights, BN buffers, torch.optim.SGD state) resumes here; the second step matches the
+    reference's second step (loss, every parameter) and the momentum it leaves behind."""
+    pkg = torch.load(os.path.join(golden_dir, 'tiny_ref_resume.pth'), map_location='cpu',
+                     weights_only=True)
+    g0 = np.load(os.path.join(golden_dir, 'tiny_ds2.npz'))
+    g2 = np.load(os.path.join(golden_dir, 'tiny_resume.npz'))
+    m = dsm.DeepSpeech.load_model_package(pkg)
+    tr = Trainer(m, LABELS, lr=1.0, momentum=0.5, max_norm=100.0, device=dev)
+    tr.optimizer.load_state_dict(pkg['optim_dict'])
+    data = (torch.from_numpy(g0['x']), torch.from_numpy(g0['targets']), None,
+            torch.from_numpy(g0['pct']).clone(), torch.from_numpy(g0['target_sizes']))
+    loss = tr.train_batch(data, return_item=True)
+    assert abs(loss - float(g2['loss2'])) <= 1e-4 * abs(float(g2['loss2']))
+    sd = m.state_dict()
+    for k in g2.files:
+        if k.startswith('after_step2/'):
+            name = k[len('after_step2/'):]
+            ref = torch.from_numpy(g2[k])
+            assert (sd[name].cpu() - ref).abs().max().item() <= 1e-6 + 1e-5 * ref.abs().max().item(), name
+    st = tr.optimizer.state_dict()['state']
+    for i in range(len(st)):
+        assert _rel(st[i]['momentum_buffer'], g2[f'momentum2/{i}']) <= 1e-4, i
+
+
+# --------------------------------------------------------------------------- data parallel
+def test_world1_nccl_trainer_hooks_and_bit_identity(dev, golden_dir, tmp_path):
+    """The DS2 Trainer under a world-1 RCCL ('nccl') process group: every gradient bucket's
+    all-reduce is issued from the post-accumulate hooks during backward, the reduced
+    gradients (HIP gradient slots in the flat buffer) are bit-identical to the
+    no-process-group Trainer's, and the step is the same."""
+    import torch.distributed as dist
+    g = np.load(os.path.join(golden_dir, 'tiny_ds2.npz'))
+
+    def data():
+        return (torch.from_numpy(g['x']), torch.from_numpy(g['targets']), None,
+                torch.from_numpy(g['pct']).clone(), torch.from_numpy(g['target_sizes']))
+
+    ref = Trainer(_build(int(g['seed']), 16, 2), LABELS, device=dev, bucket_mb=0.05)
+    ref.train_batch(data(), return_item=True)
+    ref_grad = ref.flat.grad.clone()
+    ref_params = ref.flat.flat.clone()
+    store = dist.FileStore(str(tmp_path / "store"), 1)
+    dist.init_process_group("nccl", store=store, rank=0, world_size=1, device_id=dev)
+    try:
+        tr = Trainer(_build(int(g['seed']), 16, 2), LABELS, device=dev, bucket_mb=0.05)
+        assert len(tr.reducer.buckets) > 1 and tr.reducer._hooks
+        tr.train_batch(data(), return_item=True)
+        assert tr.reducer.issued_from_hooks == len(tr.reducer.buckets)
+        assert torch.equal(tr.flat.grad, ref_grad)
+        assert torch.equal(tr.flat.flat, ref_params)
+    finally:
+        ops.set_cooperative_guard(None)
+        dist.destroy_process_group()
+
+
+# --------------------------------------------------------------------------- cfg4 / cfg5 shapes
+def test_cfg5_30s_eval_forward_and_beam10(dev):
+    """cfg5's defining shape: 30 s utterances (T = 3001, T' = 1501) through 5 x BiGRU-800 in
+    eval mode, bs 2, against the oracle; then the beam-10 prefix search on those probs
+    against the oracle/ctc_beam.py restatement (ids and offsets of every path)."""
+    _threads()
+    from ds2amd.decoder import BeamCTCDecoder
+    from oracle import ctc_beam
+    g = torch.Generator().manual_seed(30)
+    t_list = [3001, 2400]
+    x = _spect_batch(g, t_list, 3001)
+    sizes = torch.tensor(t_list, dtype=torch.int32)
+    m = _build(123456, 800, 5).to(dev).eval()
+    o = orc.OracleDS2({k: v.detach().cpu().clone() for k, v in m.state_dict().items()}, 5, 800)
+    with torch.no_grad():
+        logits, probs, out_lens = m(x.to(dev), sizes)
+        rl, rp, ro, _ = o.forward(x, sizes, training=False)
+    np.testing.assert_array_equal(out_lens.cpu().numpy(), ro.numpy())
+    assert out_lens.tolist() == [1501, 1200]
+    assert _rel(logits, rl) < 1e-4
+    beam = BeamCTCDecoder(LABELS, beam_width=10, cutoff_top_n=40)
+    strings, offsets = beam.decode(probs, out_lens)
+    ref = ctc_beam.beam_decode(probs.cpu().numpy(), out_lens.cpu().tolist(), 10)
+    for i, paths in enumerate(ref):
+        for p, (_, ids, ts) in enumerate(paths):
+            assert strings[i][p] == ''.join(LABELS[k] for k in ids)
+            assert offsets[i][p].tolist() == ts
+
+
+def test_cfg4_lstm1024_bf16_gemms_and_batch64_chunks(dev):
+    """cfg4's layer (BiLSTM-1024): (a) batch 64 in fp32 -- the persistent kernels' 32-sample
+    workgroups / two-chunk backward -- forward + input gradient vs the oracle; (b) the opt-in
+    bf16 RNN GEMMs at H = 1024 over a 3-layer stack track the fp32 oracle (logits 2e-2,
+    loss 1 %)."""
+    _threads()
+    from ds2amd.ctc import CTCLoss
+    g = torch.Generator().manual_seed(64)
+    t_list = [161] * 40 + [140] * 24
+    x = _spect_batch(g, t_list, 161)
+    sizes = torch.tensor(t_list, dtype=torch.int32)
+    m = _build(77, 1024, 2, rnn_type='lstm').to(dev).train()
+    o = orc.OracleDS2({k: v.detach().cpu().clone() for k, v in m.state_dict().items()}, 2, 1024,
+                      rnn_type='lstm')
+    tg, tl = _targets(g, [20] * 64)
+    logits, _, out_lens = m(x.to(dev), sizes)
+    loss = CTCLoss()(logits.transpose(0, 1), tg, out_lens, tl) / 64
+    loss.backward()
+    params = {k: v.detach().clone().requires_grad_(True) for k, v in o.parameters().items()}
+    rl, _, ro, _ = o.forward(x, sizes, training=True, params=params)
+    rloss = torch.nn.functional.ctc_loss(rl.transpose(0, 1).log_softmax(2), tg.long(), ro.long(),
+                                         tl.long(), reduction='sum') / 64
+    rloss.backward()
+    assert _rel(logits, rl) < 1e-4
+    assert abs(float(loss) - float(rloss)) <= 1e-4 * abs(float(rloss))
+    for name, p in m.named_parameters():
+        if name.startswith('rnns.'):
+            assert _rel(p.grad, params[name].grad) <= 5e-4, name
+    # (b) bf16 RNN GEMMs, 3 layers at H = 1024
+    m32 = _build(78, 1024, 3, rnn_type='lstm').to(dev).train()
+    m16 = _build(78, 1024, 3, rnn_type='lstm').to(dev).train()
+    m16.set_rnn_gemm_precision('bf16')
+    o3 = orc.OracleDS2({k: v.detach().cpu().clone() for k, v in m32.state_dict().items()}, 3,
+                       1024, rnn_type='lstm')
+    xb, sb = x[:4], sizes[:4]
+    with torch.no_grad():
+        l32, _, ol = m32(xb.to(dev), sb)
+        l16, _, _ = m16(xb.to(dev), sb)
+        rl3, _, _, _ = o3.forward(xb, sb, training=True)
+    assert _rel(l32, rl3) < 1e-4
+    assert _rel(l16, rl3) < 2e-2
+    c32 = CTCLoss()(l32.transpose(0, 1).contiguous(), tg[:80], ol, tl[:4])
+    c16 = CTCLoss()(l16.transpose(0, 1).contiguous(), tg[:80], ol, tl[:4])
+    assert abs(float(c16) - float(c32)) <= 1e-2 * abs(float(c32))

@@ -284,3 +284,68 @@ def test_spect_aug_draws_follow_reference_semantics():
     apply_masks_np(s, [10, 20, 150, 140, 5, 7, 0, 0, 81])
     assert s[10:20].sum() == 0 and s[81:].sum() == 0 and s[:, 5:7].sum() == 0
     assert s[0:10, 7:].min() == 1 and s[20:81, 7:].min() == 1      # reversed band is empty
+
+
+# ------------------------------------------------------------------ optimizer-state compatibility
+def _resume_inputs(golden_dir):
+    pkg = torch.load(os.path.join(golden_dir, 'tiny_ref_resume.pth'), map_location='cpu',
+                     weights_only=True)
+    g0 = _load(golden_dir, 'tiny_ds2.npz')
+    g2 = _load(golden_dir, 'tiny_resume.npz')
+    return pkg, g0, g2
+
+
+def test_oracle_resume_matches_reference(golden_dir):
+    """The oracle resumed from a reference package (weights + BN buffers + the SGD state
+    dict, model.py:426-468 / train.py:838-844) reproduces the reference's second step."""
+    pkg, g0, g2 = _resume_inputs(golden_dir)
+    m = dsm.DeepSpeech.load_model_package(pkg)
+    names = [n for n, _ in m.named_parameters()]
+    o = orc.OracleDS2(pkg['state_dict'], nb_layers=2, hidden=16)
+    bufs = orc.momentum_from_optim_dict(names, pkg['optim_dict'])
+    assert len(bufs) == len(names)
+    loss, new, nb, _, _ = orc.train_step(
+        o, torch.from_numpy(g0['x']), torch.from_numpy(g0['pct']).clone(),
+        torch.from_numpy(g0['targets']), torch.from_numpy(g0['target_sizes']),
+        momentum_buffers=bufs)
+    np.testing.assert_allclose(float(loss), float(g2['loss2']), rtol=1e-5)
+    for k, v in new.items():
+        np.testing.assert_allclose(v.numpy(), g2['after_step2/' + k], rtol=1e-6, atol=1e-7, err_msg=k)
+    for i, n in enumerate(names):
+        np.testing.assert_allclose(nb[n].numpy(), g2[f'momentum2/{i}'], rtol=1e-5, atol=1e-8,
+                                   err_msg=n)
+
+
+def test_fused_sgd_state_dict_is_torch_sgd_format(golden_dir):
+    """FusedSGD (flat buffers, reverse layer order inside) loads a reference optim_dict and
+    writes back exactly torch.optim.SGD's format in model.parameters() order; torch's own
+    SGD accepts what it writes; anything else is refused (no silent momentum restart)."""
+    from ds2amd.optim import FlatParams, FusedSGD
+    pkg, _, _ = _resume_inputs(golden_dir)
+    m = dsm.DeepSpeech.load_model_package(pkg)
+    flat = FlatParams(list(m.parameters()), 'cpu')
+    opt = FusedSGD(flat, lr=1.0, momentum=0.5, max_norm=100.0)
+    ref = pkg['optim_dict']
+    opt.load_state_dict(ref)
+    assert (opt.lr, opt.momentum) == (ref['param_groups'][0]['lr'], ref['param_groups'][0]['momentum'])
+    ours = opt.state_dict()
+    assert sorted(ours) == ['param_groups', 'state']
+    assert ours['param_groups'][0]['params'] == ref['param_groups'][0]['params']
+    for k in ('lr', 'momentum', 'nesterov', 'dampening', 'weight_decay'):
+        assert ours['param_groups'][0][k] == ref['param_groups'][0][k], k
+    assert sorted(ours['state']) == sorted(ref['state'])
+    for i, st in ref['state'].items():
+        assert torch.equal(ours['state'][i]['momentum_buffer'], st['momentum_buffer']), i
+    sgd = torch.optim.SGD(m.parameters(), lr=0.1, momentum=0.9, nesterov=True)
+    sgd.load_state_dict(ours)
+    # set_lr (train.py:322-326) round trip
+    sd = opt.state_dict()
+    sd['param_groups'][0]['lr'] = 1e-5
+    opt.load_state_dict(sd)
+    assert opt.lr == 1e-5
+    with pytest.raises(ValueError):
+        opt.load_state_dict({'lr': 1.0, 'momentum': 0.9, 'momentum_buffer': torch.zeros(3)})
+    bad = opt.state_dict()
+    bad['param_groups'][0]['nesterov'] = False
+    with pytest.raises(ValueError):
+        opt.load_state_dict(bad)
