@@ -521,6 +521,7 @@ __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
       }
       trace_at(s, 1);
       const int base = (((s - 1) % NSLOT) * slot_floats + grp_off + b0 * 256 + lane * 4) * 4;
+      if (HM == 1) sleep_units(g_rnn_tune[1]);
       f32x4 hv[NBW];
 #pragma unroll
       for (int i = 0; i < NBW; ++i) {
@@ -559,7 +560,7 @@ __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
           failed = 1;
           break;
         }
-        __builtin_amdgcn_s_sleep(1);
+        sleep_units(g_rnn_tune[0]);
         asm volatile("" ::: "memory");   // the re-loads are not loop-invariant (no LICM)
 #pragma unroll
         for (int i = 0; i < NBW; ++i)
@@ -1000,6 +1001,21 @@ __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
 
 }  // namespace ds2
 
+namespace ds2 {
+// gru_split.hip: the same direct-operand recurrences with the W_hh contraction on the bf16
+// matrix cores at fp32 accuracy (default; DS2_GRU_X6=0 selects the fp32-MFMA kernels below)
+bool launch_gru_fwd_x6(int hm, int t_max, int n, int h, int num_dirs, const float* xproj,
+                       const float* w_hh_f, const float* w_hh_r, const float* b_hh_f,
+                       const float* b_hh_r, const int* lens, float* h_all, float* gates,
+                       float* ring, unsigned* ctrs, unsigned* err, unsigned long long* stamps,
+                       size_t lds_pad, hipStream_t st);
+bool launch_gru_bwd_x6(int hm, int t_max, int n, int h, int num_dirs, const float* dy, int dy_dirs,
+                       const float* w_hh_f, const float* w_hh_r, const float* h_all,
+                       const float* gates, const int* lens, float* dgates_x, float* dgates_h,
+                       float* ring, unsigned* ctrs, unsigned* err, unsigned long long* stamps,
+                       size_t lds_pad, hipStream_t st);
+}  // namespace ds2
+
 using namespace ds2;
 
 extern "C" {
@@ -1103,6 +1119,7 @@ ds2_status_t ds2_gru_fwd(int t_max, int n, int h, int num_dirs, const float* xpr
   }
   hipStream_t st = as_stream(stream);
   apply_spin_limit_env();
+  apply_rnn_tune_env();
   const int UB = (h + GU - 1) / GU;
   const int KS = (h + 3) / 4;
   const int BT = (n + GB - 1) / GB;
@@ -1126,6 +1143,12 @@ ds2_status_t ds2_gru_fwd(int t_max, int n, int h, int num_dirs, const float* xpr
     const int hm = handoff_mode(true);
     if (hm != 0 && ring_reset(ring, n, h, num_dirs, 1, st) != hipSuccess)
       return launch_status("ds2_gru ring");
+    if (launch_gru_fwd_x6(hm, t_max, n, h, num_dirs, xproj, w_hh_f, w_hh_r, b_hh_f, b_hh_r, lens,
+                          h_all, gates, ring, ctrs, err, stamps, kDopPadLds, st)) {
+      fold_err(err, err_out, st);
+      return launch_status("ds2_gru_fwd");
+    }
+    (void)hipGetLastError();
     const void* fn = nullptr;
 #define DS2_FDOP(K)                                                                  \
   case K:                                                                            \
@@ -1215,6 +1238,7 @@ ds2_status_t ds2_gru_bwd(int t_max, int n, int h, int num_dirs, const float* dy,
   if (num_dirs == 1) w_hh_r = w_hh_f;
   hipStream_t st = as_stream(stream);
   apply_spin_limit_env();
+  apply_rnn_tune_env();
   const int UB = (h + GU - 1) / GU;
   const int KS = (3 * h + 3) / 4;
   const int BT = (n + GB - 1) / GB;
@@ -1238,8 +1262,15 @@ ds2_status_t ds2_gru_bwd(int t_max, int n, int h, int num_dirs, const float* dy,
                                            align256(counter_bytes(n, num_dirs)));
     void* args[] = {&T_, &N_, &H_, &D_, &UB_, &BT_, &dy, &DYD_, &w_hh_f, &w_hh_r, &h_all,
                     &gates, &lens, &dgates_x, &dgates_h, &ring, &ctrs, &err, &stamps};
-    if (handoff_mode(false) != 0 && ring_reset(ring, n, h, num_dirs, 3, st) != hipSuccess)
+    const int hmb = handoff_mode(false);
+    if (hmb != 0 && ring_reset(ring, n, h, num_dirs, 3, st) != hipSuccess)
       return launch_status("ds2_gru ring");
+    if (launch_gru_bwd_x6(hmb, t_max, n, h, num_dirs, dy, dy_dirs, w_hh_f, w_hh_r, h_all, gates,
+                          lens, dgates_x, dgates_h, ring, ctrs, err, stamps, kDopPadLds, st)) {
+      fold_err(err, err_out, st);
+      return launch_status("ds2_gru_bwd");
+    }
+    (void)hipGetLastError();
     const void* fn = bwd_dop_fn((3 * UB + GW - 1) / GW);
     if (fn != nullptr &&
         hipLaunchCooperativeKernel(fn, dim3(grid), dim3(GT), args, kDopPadLds, st) == hipSuccess) {

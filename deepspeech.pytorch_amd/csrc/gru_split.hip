@@ -1,0 +1,575 @@
+// GRU recurrences with the W_hh contraction on the bf16 matrix cores at fp32 accuracy.
+//
+// The fp32 MFMA (v_mfma_f32_16x16x4_f32) runs at 1/16 of the bf16 rate, and at cfg2 (H 800,
+// one workgroup per (16 units, direction, 16 samples)) it was ~2.2 us of every 5.6 us
+// recurrence step.  Here every fp32 operand x is split into three bf16 terms,
+//   hi = bf16(x), mid = bf16(x - hi), lo = bf16(x - hi - mid)     (x = hi + mid + lo exactly
+//   up to the last bit of lo: 8 + 8 + 8 significant bits),
+// and a product a.b is formed from the six terms that carry fp32 weight:
+//   hi.hi + hi.mid + mid.hi + hi.lo + lo.hi + mid.mid
+// (dropped: mid.lo, lo.mid, lo.lo, all below 2^-24 relative).  Each bf16 product is exact in
+// the fp32 accumulator, so the result has fp32 accuracy (a 501-step GRU at H 800 drifts
+// 1.9e-7 from fp64, plain fp32 2.2e-7); six v_mfma_f32_16x16x32_bf16 (16 cycles each) per 32
+// k replace eight v_mfma_f32_16x16x4_f32 (32 cycles each): 2.7x fewer matrix cycles.
+//
+// W_hh is split once at kernel start and stays in registers for all T steps (3 terms x 8 bf16
+// per 32 k); the handed-off h (forward) / gate gradients (backward) are split by the
+// consumer after their loads.  Workgroups of 256 threads: 4 waves, ONE per SIMD with the
+// whole 512-entry register file (the split W needs 1.5x the fp32 fragment registers), each
+// wave owning a contiguous range of 32-k pairs of the hand-off tiles; the MFMA k slot j of
+// lane (r, q) holds tile 2p + (j >> 2), k = 4q + (j & 3) -- exactly the 16 bytes that lane
+// loads from each 1-KB tile, so the hand-off tiles, ring layout and protocols are those of
+// gru_fwd_dop_kernel / gru_bwd_dop_kernel (gru.hip) unchanged.
+#include "rnn_common.h"
+
+namespace ds2 {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+constexpr int XW = 4;            // waves per workgroup, one per SIMD
+constexpr int kXTraceS0 = 100, kXTraceSteps = 16;   // = gru.hip's DS2_GRU_STAMPS=2 window
+constexpr int XT = XW * 64;      // 256 threads = 16 samples x 16 units
+
+struct Tri {
+  bf16x8 hi, mid, lo;
+};
+
+// 8 fp32 values (k slots 0..3 from a, 4..7 from b) -> three bf16 terms (RNE splits; each
+// residual is exact in fp32)
+__device__ __forceinline__ Tri split3(const f32x4 a, const f32x4 b) {
+  Tri t;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float v = j < 4 ? a[j] : b[j - 4];
+    const __bf16 h = (__bf16)v;
+    const float r1 = v - (float)h;
+    const __bf16 m = (__bf16)r1;
+    const float r2 = r1 - (float)m;
+    t.hi[j] = h;
+    t.mid[j] = m;
+    t.lo[j] = (__bf16)r2;
+  }
+  return t;
+}
+
+// c += a.b to fp32 accuracy (small terms first)
+__device__ __forceinline__ f32x4 mma6(const Tri& a, const Tri& b, f32x4 c) {
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.mid, b.mid, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.lo, b.hi, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.hi, b.lo, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.mid, b.hi, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.hi, b.mid, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.hi, b.hi, c, 0, 0, 0);
+  return c;
+}
+
+// wave's contiguous share [p0, p0 + np) of `pairs` 32-k pairs
+__device__ __forceinline__ void pair_split(int pairs, int wave, int& p0, int& np) {
+  p0 = (pairs * wave) / XW;
+  np = (pairs * (wave + 1)) / XW - p0;
+}
+
+// ---------------------------------------------------------------------------------------
+// forward: gh[16 samples x 48] = h_{t-1}[16 x H] . W_hh[r, z, n rows of 16 units]^T.
+// HM = hand-off form as in gru_fwd_dop_kernel: 0 per-producer flags, 1 sentinel ring.
+template <int NP, int HM>
+__global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(1, 1))) void gru_fwd_x6_kernel(
+    int T, int N, int H, int D, int UB, int BT, const float* __restrict__ xproj,
+    const float* __restrict__ w_f, const float* __restrict__ w_r, const float* __restrict__ b_f,
+    const float* __restrict__ b_r, const int* __restrict__ lens, float* __restrict__ h_all,
+    float* __restrict__ gates, float* __restrict__ hx, unsigned* __restrict__ counters,
+    unsigned* __restrict__ err, unsigned long long* __restrict__ stamps) {
+  constexpr int RP = 3 * GU + 1;
+  constexpr bool SENT = HM == 1;
+  constexpr int NSLOT = SENT ? kRingSlots : 2;
+  __shared__ float red[XW * GB * RP];
+  __shared__ __attribute__((aligned(16))) float tile[GB * GU];
+  __shared__ int flag;
+  __shared__ int failed;
+  int ub, d, bt;
+  if (!map_work(UB * D, BT, UB, ub, d, bt)) return;
+  const int n0 = bt * GB;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int p0, np;
+  pair_split((UB + 1) >> 1, wave, p0, np);          // host guarantees np <= NP
+  const int t_first = 2 * p0;                       // first hand-off tile of this wave
+  const unsigned* gflags = counters + (D * BT + 1) + (d * BT + bt) * UB;
+  unsigned* myflag = counters + (D * BT + 1) + (d * BT + bt) * UB + ub;
+  const int slot_floats = D * BT * UB * 256;
+  const __amdgpu_buffer_rsrc_t x_rs =
+      __builtin_amdgcn_make_buffer_rsrc(hx, (short)0, NSLOT * slot_floats * 4, 0x00020000);
+  const int grp_off = (d * BT + bt) * UB * 256;
+  if (threadIdx.x == 0) failed = 0;
+  __syncthreads();
+  // diagnostic timeline (DS2_GRU_STAMPS=2, scripts/trace_gru.py): s_memrealtime at step
+  // start / wait done / products done / reduction done / published, for kXTraceSteps steps
+  const bool tracing = stamps != nullptr && threadIdx.x == 0;
+  auto trace_at = [&](int s, int p) {
+    if (tracing && s >= kXTraceS0 && s < kXTraceS0 + kXTraceSteps)
+      stamps[((int64_t)(s - kXTraceS0) * gridDim.x + blockIdx.x) * 5 + p] =
+          __builtin_amdgcn_s_memrealtime();
+  };
+
+  // W_hh split fragments: pair p, gate g, k slot j -> W[g H + 16 ub + (lane & 15)]
+  //   [16 (t_first + 2p + (j >> 2)) + 4 (lane >> 4) + (j & 3)]
+  Tri w[3][NP];
+  {
+    const float* W = d == 0 ? w_f : w_r;
+    const float* wr = W + (int64_t)(ub * GU + (lane & 15)) * H + 4 * (lane >> 4);
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      const int ta = t_first + 2 * p, tb = ta + 1;
+#pragma unroll
+      for (int g = 0; g < 3; ++g) {
+        const float* wg = wr + (int64_t)g * H * H;
+        const f32x4 z4 = f32x4{0.f, 0.f, 0.f, 0.f};
+        const f32x4 a = (p < np && ta < UB) ? *reinterpret_cast<const f32x4*>(wg + 16 * ta) : z4;
+        const f32x4 b = (p < np && tb < UB) ? *reinterpret_cast<const f32x4*>(wg + 16 * tb) : z4;
+        w[g][p] = split3(a, b);
+      }
+    }
+  }
+  const float* bh = d == 0 ? b_f : b_r;
+  const int m = threadIdx.x >> 4;
+  const int u = threadIdx.x & 15;
+  const int n = n0 + m;
+  const int j = ub * GU + u;
+  const bool owner = n < N;
+  float bias_r = 0.f, bias_z = 0.f, bias_n = 0.f;
+  int len = 0;
+  if (owner) {
+    bias_r = bh[j];
+    bias_z = bh[H + j];
+    bias_n = bh[2 * H + j];
+    len = lens[n];
+  }
+  settle(bias_r);
+  settle(bias_z);
+  settle(bias_n);
+  settle(len);
+  const int tpos = ((u >> 2) * GB + m) * 4 + (u & 3);
+  float g_r = 0.f, g_z = 0.f, g_n = 0.f, g_hn = 0.f, h_own = 0.f;
+  int64_t g_row = -1;
+  for (int s = 0; s < T; ++s) {
+    const int t = d == 0 ? s : T - 1 - s;
+    const int64_t row = ((int64_t)t * N + n) * D + d;
+    float xr = 0.f, xz = 0.f, xn = 0.f;
+    if (owner && t < len) {
+      const float* xp = xproj + row * 3 * H;
+      xr = xp[j];
+      xz = xp[H + j];
+      xn = xp[2 * H + j];
+    }
+    f32x4 acc[3];
+#pragma unroll
+    for (int g = 0; g < 3; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+    trace_at(s, 0);
+    if (s > 0) {
+      if (!SENT && !flags_wait(gflags, UB, (unsigned)s, err, &flag)) {
+        poison_rest(h_all, s, T, d != 0, N, D, n, d, H, j, H, 1, owner);
+        return;
+      }
+      trace_at(s, 1);
+      const int base = (((s - 1) % NSLOT) * slot_floats + grp_off + t_first * 256 + lane * 4) * 4;
+      if (SENT) sleep_units(g_rnn_tune[1]);
+      f32x4 hv[2 * NP];
+#pragma unroll
+      for (int i = 0; i < 2 * NP; ++i) {
+        const int off = (i < 2 * np && t_first + i < UB) ? base + i * 1024 : 0x7ffffff0;
+        hv[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(x_rs, off, 0, kSc1));
+      }
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      // per-pair partials summed in a fixed order afterwards: pairs are multiplied in
+      // arrival order (one re-load round trip per pass), the result is deterministic
+      f32x4 pacc[NP][3];
+#pragma unroll
+      for (int p = 0; p < NP; ++p)
+#pragma unroll
+        for (int g = 0; g < 3; ++g) pacc[p][g] = f32x4{0.f, 0.f, 0.f, 0.f};
+      unsigned pend = (1u << np) - 1u;
+      for (unsigned spins = 0;; ++spins) {
+#pragma unroll
+        for (int p = 0; p < NP; ++p) {
+          if (((pend >> p) & 1u) && (!SENT || (wave_ready(hv[2 * p]) && wave_ready(hv[2 * p + 1])))) {
+            const Tri a = split3(hv[2 * p], hv[2 * p + 1]);
+#pragma unroll
+            for (int g = 0; g < 3; ++g) pacc[p][g] = mma6(a, w[g][p], pacc[p][g]);
+            pend &= ~(1u << p);
+          }
+        }
+        if (pend == 0u) break;
+        if (spins > g_spin_limit) {
+          if (lane == 0) __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          failed = 1;
+          break;
+        }
+        sleep_units(g_rnn_tune[0]);
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int i = 0; i < 2 * NP; ++i)
+          if (((pend >> (i >> 1)) & 1u) && t_first + i < UB)
+            hv[i] = __builtin_bit_cast(
+                f32x4, __builtin_amdgcn_raw_buffer_load_b128(x_rs, base + i * 1024, 0, kSc1));
+      }
+#pragma unroll
+      for (int g = 0; g < 3; ++g) {
+        acc[g] = pacc[0][g];
+#pragma unroll
+        for (int p = 1; p < NP; ++p) acc[g] += pacc[p][g];
+      }
+      trace_at(s, 2);
+    }
+#pragma unroll
+    for (int g = 0; g < 3; ++g)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        red[(wave * GB + (lane >> 4) * 4 + r) * RP + g * GU + (lane & 15)] = acc[g][r];
+    settle(xr);
+    settle(xz);
+    settle(xn);
+    __syncthreads();
+    if (failed) {
+      poison_rest(h_all, s, T, d != 0, N, D, n, d, H, j, H, 1, owner);
+      return;
+    }
+    trace_at(s, 3);
+    float hout = 0.f;
+    if (owner) {
+      float gh[3];
+#pragma unroll
+      for (int g = 0; g < 3; ++g) {
+        float v = 0.f;
+#pragma unroll
+        for (int w8 = 0; w8 < XW; ++w8) v += red[(w8 * GB + m) * RP + g * GU + u];
+        gh[g] = v;
+      }
+      const float ghr = gh[0] + bias_r;
+      const float ghz = gh[1] + bias_z;
+      float ghn = gh[2] + bias_n;
+      float r = 0.f, z = 0.f, nn = 0.f;
+      if (t < len) {
+        r = sigmoid_fast(ghr + xr);
+        z = sigmoid_fast(ghz + xz);
+        nn = tanh_fast(xn + r * ghn);
+        hout = (h_own - nn) * z + nn;
+      } else {
+        ghn = 0.f;
+      }
+      h_own = hout;
+      g_r = r; g_z = z; g_n = nn; g_hn = ghn; g_row = row;
+    }
+    tile[tpos] = hout;
+    __syncthreads();
+    if (wave == 0) {
+      const int toff = (grp_off + ub * 256 + lane * 4) * 4;
+      if (SENT) {
+        const u32x4 v = desentinel(*reinterpret_cast<const u32x4*>(tile + lane * 4));
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // last step's sentinel store first
+        __builtin_amdgcn_raw_buffer_store_b128(v, x_rs, (s % NSLOT) * slot_floats * 4 + toff, 0, kSc1);
+        const u32x4 sv = u32x4{kSentinel, kSentinel, kSentinel, kSentinel};
+        __builtin_amdgcn_raw_buffer_store_b128(sv, x_rs, ((s + 2) % NSLOT) * slot_floats * 4 + toff,
+                                               0, kSc1);
+      } else {
+        const u32x4 v = *reinterpret_cast<const u32x4*>(tile + lane * 4);
+        __builtin_amdgcn_raw_buffer_store_b128(v, x_rs, (s & 1) * slot_floats * 4 + toff, 0, kSc1);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0)
+          __hip_atomic_store(myflag, (unsigned)s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    trace_at(s, 4);
+    if (owner) {
+      h_all[row * H + j] = h_own;
+      if (gates != nullptr) {
+        float* gp = gates + g_row * 4 * H;
+        gp[j] = g_r;
+        gp[H + j] = g_z;
+        gp[2 * H + j] = g_n;
+        gp[3 * H + j] = g_hn;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// backward: rec[16 samples x 16 units] = dG[16 x 3H] . W_hh[3H rows, 16 units], dG = the
+// (dar, daz, dghn) gate gradients of the step after (tiles g UB + ub of the ring, as in
+// gru_bwd_dop_kernel).  HM: 0 per-producer flags, 1 sentinel ring (pairs in order).
+template <int NP, int HM>
+__global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(1, 1))) void gru_bwd_x6_kernel(
+    int T, int N, int H, int D, int UB, int BT, const float* __restrict__ dy, int dyd,
+    const float* __restrict__ w_f, const float* __restrict__ w_r,
+    const float* __restrict__ h_all, const float* __restrict__ gates,
+    const int* __restrict__ lens, float* __restrict__ dgx, float* __restrict__ dgh,
+    float* __restrict__ gx, unsigned* __restrict__ counters, unsigned* __restrict__ err,
+    unsigned long long* __restrict__ stamps) {
+  constexpr int RP = GU + 1;
+  constexpr bool SENT = HM == 1;
+  constexpr int NSLOT = SENT ? kRingSlots : 2;
+  __shared__ float red[XW * GB * RP];
+  __shared__ __attribute__((aligned(16))) float tile[3 * GB * GU];
+  __shared__ int flag;
+  __shared__ int failed;
+  int ub, d, bt;
+  if (!map_work(UB * D, BT, UB, ub, d, bt)) return;
+  const int n0 = bt * GB;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int H3 = 3 * H;
+  const int NB3 = 3 * UB;
+  int p0, np;
+  pair_split((NB3 + 1) >> 1, wave, p0, np);
+  const int t_first = 2 * p0;
+  const unsigned* gflags = counters + (D * BT + 1) + (d * BT + bt) * UB;
+  unsigned* myflag = counters + (D * BT + 1) + (d * BT + bt) * UB + ub;
+  const int slot_floats = D * BT * NB3 * 256;
+  const __amdgpu_buffer_rsrc_t x_rs =
+      __builtin_amdgcn_make_buffer_rsrc(gx, (short)0, NSLOT * slot_floats * 4, 0x00020000);
+  const int grp_off = (d * BT + bt) * NB3 * 256;
+  if (threadIdx.x == 0) failed = 0;
+  __syncthreads();
+  // diagnostic timeline (DS2_GRU_STAMPS=2, scripts/trace_gru.py): s_memrealtime at step
+  // start / wait done / products done / reduction done / published, for kXTraceSteps steps
+  const bool tracing = stamps != nullptr && threadIdx.x == 0;
+  auto trace_at = [&](int s, int p) {
+    if (tracing && s >= kXTraceS0 && s < kXTraceS0 + kXTraceSteps)
+      stamps[((int64_t)(s - kXTraceS0) * gridDim.x + blockIdx.x) * 5 + p] =
+          __builtin_amdgcn_s_memrealtime();
+  };
+
+  // W_hh^T split fragments: pair p, k slot j -> W_hh[16 (t_first + 2p + (j >> 2)) +
+  //   4 (lane >> 4) + (j & 3)][16 ub + (lane & 15)]
+  Tri w[NP];
+  {
+    const float* W = d == 0 ? w_f : w_r;
+    const float* wc = W + (int64_t)(4 * (lane >> 4)) * H + ub * GU + (lane & 15);
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      const int ta = t_first + 2 * p, tb = ta + 1;
+      f32x4 a = f32x4{0.f, 0.f, 0.f, 0.f}, b = a;
+      if (p < np && ta < NB3)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) a[c] = wc[(int64_t)(16 * ta + c) * H];
+      if (p < np && tb < NB3)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) b[c] = wc[(int64_t)(16 * tb + c) * H];
+      w[p] = split3(a, b);
+    }
+  }
+  const int m = threadIdx.x >> 4;
+  const int u = threadIdx.x & 15;
+  const int n = n0 + m;
+  const int j = ub * GU + u;
+  const bool owner = n < N;
+  int len = owner ? lens[n] : 0;
+  settle(len);
+  const int tpos = ((u >> 2) * GB + m) * 4 + (u & 3);
+  float dh_prev = 0.f, z_prev = 0.f;
+  float px_dar = 0.f, px_daz = 0.f, px_dan = 0.f, px_dghn = 0.f;
+  int64_t px_row = -1;
+  for (int s = 0; s < T; ++s) {
+    const int t = d == 0 ? T - 1 - s : s;
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+    float dyv = 0.f, g_r = 0.f, g_z = 0.f, g_n = 0.f, g_hn = 0.f, hp = 0.f;
+    const int64_t row = ((int64_t)t * N + n) * D + d;
+    if (owner && t < len) {
+      dyv = dy[(((int64_t)t * N + n) * dyd + (dyd > 1 ? d : 0)) * H + j];
+      const float* gp = gates + row * 4 * H;
+      g_r = gp[j];
+      g_z = gp[H + j];
+      g_n = gp[2 * H + j];
+      g_hn = gp[3 * H + j];
+      const int tp = d == 0 ? t - 1 : t + 1;
+      if (tp >= 0 && tp < T) hp = h_all[(((int64_t)tp * N + n) * D + d) * H + j];
+    }
+    trace_at(s, 0);
+    if (s > 0) {
+      if (!SENT && !flags_wait(gflags, UB, (unsigned)s, err, &flag)) {
+        poison_rest(dgx, s, T, d == 0, N, D, n, d, H, j, H3, 3, owner);
+        return;
+      }
+      trace_at(s, 1);
+      const int base = (((s - 1) % NSLOT) * slot_floats + grp_off + t_first * 256 + lane * 4) * 4;
+      f32x4 gv[2 * NP];
+#pragma unroll
+      for (int i = 0; i < 2 * NP; ++i) {
+        const int off = (i < 2 * np && t_first + i < NB3) ? base + i * 1024 : 0x7ffffff0;
+        gv[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(x_rs, off, 0, kSc1));
+      }
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int p = 0; p < NP; ++p) {
+        if (SENT && p < np) {
+          if (!spin_tile(gv[2 * p], x_rs, base + 2 * p * 1024, err)) failed = 1;
+          if (t_first + 2 * p + 1 < NB3 &&
+              !spin_tile(gv[2 * p + 1], x_rs, base + (2 * p + 1) * 1024, err))
+            failed = 1;
+        }
+        acc = mma6(split3(gv[2 * p], gv[2 * p + 1]), w[p], acc);
+      }
+      trace_at(s, 2);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      red[(wave * GB + (lane >> 4) * 4 + r) * RP + (lane & 15)] = acc[r];
+    settle(dyv);
+    settle(g_r);
+    settle(g_z);
+    settle(g_n);
+    settle(g_hn);
+    settle(hp);
+    __syncthreads();
+    if (failed) {
+      poison_rest(dgx, s, T, d == 0, N, D, n, d, H, j, H3, 3, owner);
+      return;
+    }
+    trace_at(s, 3);
+    float dar = 0.f, daz = 0.f, dan = 0.f, dghn = 0.f;
+    if (owner) {
+      float dh = 0.f, zc = 0.f;
+      if (t < len) {
+        float carry = 0.f;
+        if (s > 0) {
+          float rec = 0.f;
+#pragma unroll
+          for (int w8 = 0; w8 < XW; ++w8) rec += red[(w8 * GB + m) * RP + u];
+          carry = dh_prev * z_prev + rec;
+        }
+        dh = dyv + carry;
+        zc = g_z;
+        dan = dh * (1.f - zc) * (1.f - g_n * g_n);
+        daz = dh * (hp - g_n) * zc * (1.f - zc);
+        dar = dan * g_hn * g_r * (1.f - g_r);
+        dghn = dan * g_r;
+      }
+      dh_prev = dh;
+      z_prev = zc;
+      px_dar = dar; px_daz = daz; px_dan = dan; px_dghn = dghn; px_row = row;
+    }
+    tile[tpos] = dar;
+    tile[GB * GU + tpos] = daz;
+    tile[2 * GB * GU + tpos] = dghn;
+    __syncthreads();
+    if (wave == 0) {
+      const int toff = (grp_off + ub * 256 + lane * 4) * 4;
+      if (SENT) {
+        u32x4 v[3];
+#pragma unroll
+        for (int g = 0; g < 3; ++g)
+          v[g] = desentinel(*reinterpret_cast<const u32x4*>(tile + g * GB * GU + lane * 4));
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int so = (s % NSLOT) * slot_floats * 4 + toff;
+#pragma unroll
+        for (int g = 0; g < 3; ++g)
+          __builtin_amdgcn_raw_buffer_store_b128(v[g], x_rs, so + g * UB * 1024, 0, kSc1);
+        const u32x4 sv = u32x4{kSentinel, kSentinel, kSentinel, kSentinel};
+        const int sn = ((s + 2) % NSLOT) * slot_floats * 4 + toff;
+#pragma unroll
+        for (int g = 0; g < 3; ++g)
+          __builtin_amdgcn_raw_buffer_store_b128(sv, x_rs, sn + g * UB * 1024, 0, kSc1);
+      } else {
+        const int so = (s & 1) * slot_floats * 4 + toff;
+#pragma unroll
+        for (int g = 0; g < 3; ++g) {
+          const u32x4 v = *reinterpret_cast<const u32x4*>(tile + g * GB * GU + lane * 4);
+          __builtin_amdgcn_raw_buffer_store_b128(v, x_rs, so + g * UB * 1024, 0, kSc1);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0)
+          __hip_atomic_store(myflag, (unsigned)s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    trace_at(s, 4);
+    if (owner) {
+      float* gxr = dgx + px_row * H3;
+      gxr[j] = px_dar;
+      gxr[H + j] = px_daz;
+      gxr[2 * H + j] = px_dan;
+      float* ghr = dgh + px_row * H3;
+      ghr[j] = px_dar;
+      ghr[H + j] = px_daz;
+      ghr[2 * H + j] = px_dghn;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// host launchers (called by ds2_gru_fwd / ds2_gru_bwd in gru.hip with their workspace
+// carve-up); false = shape not covered (caller falls back to the fp32-MFMA kernels)
+
+// forward: on by default (DS2_GRU_X6=0 selects the fp32-MFMA kernel).  backward: opt-in
+// (DS2_GRU_X6_BWD=1): its consumer-side splits of 3H-wide gate gradients make it VALU-bound
+// after the flag wait (6.5 vs 6.2 us per step for the fp32-MFMA kernel at cfg2).
+static inline bool x6_enabled() {
+  const char* e = getenv("DS2_GRU_X6");
+  return !(e != nullptr && e[0] == '0');
+}
+
+static inline bool x6_bwd_enabled() {
+  const char* e = getenv("DS2_GRU_X6_BWD");
+  return x6_enabled() && e != nullptr && e[0] == '1';
+}
+
+static const void* fwd_x6_fn(int need, int hm) {
+#define DS2_FX6(K) \
+  if (need <= K)   \
+    return hm == 1 ? reinterpret_cast<const void*>(gru_fwd_x6_kernel<K, 1>)  \
+                   : reinterpret_cast<const void*>(gru_fwd_x6_kernel<K, 0>);
+  DS2_FX6(1) DS2_FX6(2) DS2_FX6(3) DS2_FX6(4) DS2_FX6(5) DS2_FX6(6) DS2_FX6(7)
+#undef DS2_FX6
+  return nullptr;
+}
+
+static const void* bwd_x6_fn(int need, int hm) {
+#define DS2_BX6(K) \
+  if (need <= K)   \
+    return hm == 1 ? reinterpret_cast<const void*>(gru_bwd_x6_kernel<K, 1>)  \
+                   : reinterpret_cast<const void*>(gru_bwd_x6_kernel<K, 0>);
+  DS2_BX6(1) DS2_BX6(2) DS2_BX6(3) DS2_BX6(4) DS2_BX6(6) DS2_BX6(8) DS2_BX6(10)
+  DS2_BX6(13) DS2_BX6(16) DS2_BX6(19)
+#undef DS2_BX6
+  return nullptr;
+}
+
+bool launch_gru_fwd_x6(int hm, int t_max, int n, int h, int num_dirs, const float* xproj,
+                       const float* w_hh_f, const float* w_hh_r, const float* b_hh_f,
+                       const float* b_hh_r, const int* lens, float* h_all, float* gates,
+                       float* ring, unsigned* ctrs, unsigned* err, unsigned long long* stamps,
+                       size_t lds_pad, hipStream_t st) {
+  if (!x6_enabled() || (h % GU) != 0) return false;
+  apply_spin_limit_env();     // this translation unit's copies of the device knobs
+  apply_rnn_tune_env();
+  const int UB = h / GU, BT = (n + GB - 1) / GB;
+  const int need = ((UB + 1) / 2 + XW - 1) / XW;
+  const void* fn = fwd_x6_fn(need, hm == 1 ? 1 : 0);
+  if (fn == nullptr) return false;
+  int T_ = t_max, N_ = n, H_ = h, D_ = num_dirs, UB_ = UB, BT_ = BT;
+  void* args[] = {&T_, &N_, &H_, &D_, &UB_, &BT_, &xproj, &w_hh_f, &w_hh_r, &b_hh_f,
+                  &b_hh_r, &lens, &h_all, &gates, &ring, &ctrs, &err, &stamps};
+  return hipLaunchCooperativeKernel(fn, dim3(mapped_grid(UB * num_dirs, BT)), dim3(XT), args,
+                                    lds_pad, st) == hipSuccess;
+}
+
+bool launch_gru_bwd_x6(int hm, int t_max, int n, int h, int num_dirs, const float* dy, int dy_dirs,
+                       const float* w_hh_f, const float* w_hh_r, const float* h_all,
+                       const float* gates, const int* lens, float* dgates_x, float* dgates_h,
+                       float* ring, unsigned* ctrs, unsigned* err, unsigned long long* stamps,
+                       size_t lds_pad, hipStream_t st) {
+  if (!x6_bwd_enabled() || (h % GU) != 0) return false;
+  apply_spin_limit_env();
+  apply_rnn_tune_env();
+  const int UB = h / GU, BT = (n + GB - 1) / GB;
+  const int need = ((3 * UB + 1) / 2 + XW - 1) / XW;
+  const void* fn = bwd_x6_fn(need, hm == 1 ? 1 : 0);
+  if (fn == nullptr) return false;
+  int T_ = t_max, N_ = n, H_ = h, D_ = num_dirs, UB_ = UB, BT_ = BT, DYD_ = dy_dirs;
+  void* args[] = {&T_, &N_, &H_, &D_, &UB_, &BT_, &dy, &DYD_, &w_hh_f, &w_hh_r, &h_all,
+                  &gates, &lens, &dgates_x, &dgates_h, &ring, &ctrs, &err, &stamps};
+  return hipLaunchCooperativeKernel(fn, dim3(mapped_grid(UB * num_dirs, BT)), dim3(XT), args,
+                                    lds_pad, st) == hipSuccess;
+}
+
+}  // namespace ds2

@@ -125,6 +125,34 @@ static void apply_spin_limit_env() {
   if (hipMemcpyToSymbol(HIP_SYMBOL(g_spin_limit), &v, sizeof(v)) == hipSuccess) applied = v;
 }
 
+// Polling knobs of the sentinel hand-off: [0] s_sleep(1) units between re-load passes, [1]
+// units before a step's first load pass (a consumer that loads right after publishing mostly
+// gets sentinels back, and those full-tile polls from every workgroup crowd the fabric that
+// carries the real tiles).  Defaults from scripts/gru_ab.py sweeps; DS2_RNN_TUNE="a,b"
+// overrides them (diagnostic; checked at every recurrence entry point).
+constexpr unsigned kRepollSleep = 1u, kFirstPollDelay = 14u;
+static __constant__ unsigned g_rnn_tune[2] = {kRepollSleep, kFirstPollDelay};
+
+static void apply_rnn_tune_env() {
+  static unsigned applied[2] = {kRepollSleep, kFirstPollDelay};
+  unsigned v[2] = {kRepollSleep, kFirstPollDelay};
+  const char* e = getenv("DS2_RNN_TUNE");
+  if (e != nullptr && e[0] != 0) {
+    char* end = nullptr;
+    v[0] = static_cast<unsigned>(strtoul(e, &end, 10));
+    if (end != nullptr && *end == ',') v[1] = static_cast<unsigned>(strtoul(end + 1, nullptr, 10));
+  }
+  if (v[0] == applied[0] && v[1] == applied[1]) return;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_rnn_tune), v, sizeof(v)) == hipSuccess) {
+    applied[0] = v[0];
+    applied[1] = v[1];
+  }
+}
+
+__device__ __forceinline__ void sleep_units(unsigned k) {
+  for (unsigned i = 0; i < k; ++i) __builtin_amdgcn_s_sleep(1);
+}
+
 // err_out (C ABI, nullable): the caller's device status word.  After a persistent launch the
 // launch's own error word (in the workspace, reset before every launch) is OR-ed into it, so
 // a hand-off timeout stays visible to the host after the workspace is recycled.

@@ -51,11 +51,21 @@ def timed(fn, reps=5):
     return e0.elapsed_time(e1) / reps
 
 
-variants = {"dop-flags": {"DS2_GRU_DOP": "1", "DS2_RNN_HANDOFF": "flags"},
-            "dop-sentinel": {"DS2_GRU_DOP": "1", "DS2_RNN_HANDOFF": "sentinel"},
-            "dop-hybrid": {"DS2_GRU_DOP": "1", "DS2_RNN_HANDOFF": "hybrid"}}
+variants = {"x6-default": {"DS2_GRU_DOP": "1", "DS2_GRU_X6": "1", "DS2_RNN_HANDOFF": ""},
+            "x6-flags": {"DS2_GRU_DOP": "1", "DS2_GRU_X6": "1", "DS2_RNN_HANDOFF": "flags"},
+            "x6-sentinel": {"DS2_GRU_DOP": "1", "DS2_GRU_X6": "1", "DS2_RNN_HANDOFF": "sentinel"},
+            "f32-default": {"DS2_GRU_DOP": "1", "DS2_GRU_X6": "0", "DS2_RNN_HANDOFF": ""}}
 if len(sys.argv) > 1 and sys.argv[1] == "all":
-    variants = {"staged": {"DS2_GRU_DOP": "0"}, **variants}
+    variants = {"staged": {"DS2_GRU_DOP": "0"}, **variants,
+                "f32-flags": {"DS2_GRU_DOP": "1", "DS2_GRU_X6": "0", "DS2_RNN_HANDOFF": "flags"},
+                "f32-sentinel": {"DS2_GRU_DOP": "1", "DS2_GRU_X6": "0",
+                                 "DS2_RNN_HANDOFF": "sentinel"}}
+if len(sys.argv) > 1 and sys.argv[1] == "tune":
+    variants = {}
+    for x6 in ("1", "0"):
+        for t in ("1,0", "1,10", "1,14", "1,18", "2,14", "1,22"):
+            variants[f"{'x6' if x6 == '1' else 'f32'}-tune-{t}"] = {
+                "DS2_GRU_X6": x6, "DS2_RNN_HANDOFF": "", "DS2_RNN_TUNE": t}
 rounds = int(os.environ.get("AB_ROUNDS", "3"))
 variants = {f"{k}#{r}": v for r in range(rounds) for k, v in variants.items()}
 ref = None

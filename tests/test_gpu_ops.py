@@ -353,6 +353,41 @@ def test_gru_handoff_forms_agree(dev, n, h, bidir, monkeypatch):
         assert torch.equal(a, b) and torch.equal(a, c)
 
 
+@pytest.mark.parametrize("n,h,bidir", [(32, 800, True), (20, 64, True), (7, 48, False),
+                                       (17, 784, True)])
+def test_gru_bf16x6_matches_fp32_mfma(dev, n, h, bidir, monkeypatch):
+    """gru_split.hip (W_hh contraction as six bf16 products of three-term splits, fp32
+    accumulation) against the fp32-MFMA direct-operand kernels: equal within fp32 rounding
+    (different summation order); its flag and sentinel hand-offs bit-identical (odd UB = 49
+    included: the last 32-k pair is half empty)."""
+    t, inp = 41, 40
+    nd = 2 if bidir else 1
+    g = torch.Generator().manual_seed(h + 7 * n)
+    a = 0.2 if h <= 64 else h ** -0.5
+    weights = [torch.rand(s, generator=g) * 2 * a - a for s in
+               [(3 * h, inp), (3 * h, h), (3 * h,), (3 * h,)] * nd]
+    lens = torch.tensor(sorted([t - (i % 6) * 5 for i in range(n)], reverse=True),
+                        dtype=torch.int32)
+    x = torch.randn(t, n, inp, generator=g)
+    dy = torch.randn(t, n, h, generator=g)
+    outs = []
+    monkeypatch.setenv("DS2_GRU_DOP", "1")
+    for x6, mode in (("0", ""), ("1", "flags"), ("1", "sentinel")):
+        monkeypatch.setenv("DS2_GRU_X6", x6)
+        monkeypatch.setenv("DS2_GRU_X6_BWD", x6)      # the opt-in bf16x6 backward too
+        monkeypatch.setenv("DS2_RNN_HANDOFF", mode)
+        ws = [w.to(dev).requires_grad_(True) for w in weights]
+        xd = x.to(dev).requires_grad_(True)
+        y = ops.GRULayerFn.apply(xd, lens.to(dev), True, h, *ws)
+        y.backward(dy.to(dev))
+        torch.cuda.synchronize()
+        outs.append([y.detach().cpu(), xd.grad.cpu()] + [w.grad.cpu() for w in ws])
+    for f32, flags, sent in zip(*outs):
+        assert torch.isfinite(flags).all()
+        _close(flags, f32, 2e-5, "bf16x6 vs fp32 MFMA")
+        assert torch.equal(flags, sent)
+
+
 def test_gru_per_direction_output(dev):
     n, t, inp, h = 4, 11, 8, 16
     g = torch.Generator().manual_seed(5)

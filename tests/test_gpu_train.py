@@ -160,6 +160,7 @@ def test_rnn_handoff_timeout_raises(dev, monkeypatch):
     pct = torch.ones(32)
     ops.rnn_status_word(dev).zero_()
     monkeypatch.setenv("DS2_RNN_SPIN_LIMIT", "0")
+    monkeypatch.setenv("DS2_RNN_TUNE", "1,0")   # poll at once: early polls must find stale tiles
     tr = Trainer(_build(3, 256, 2), LABELS, device=dev, verbose=False)
     with pytest.raises(_lib.Ds2Error, match="hand-off"):
         tr.train_batch((x, tg, None, pct.clone(), tl), return_item=True)
@@ -172,6 +173,7 @@ def test_rnn_handoff_timeout_raises(dev, monkeypatch):
     with pytest.raises(_lib.Ds2Error, match="hand-off"):
         ops.check_rnn_status(dev)
     monkeypatch.delenv("DS2_RNN_SPIN_LIMIT")
+    monkeypatch.delenv("DS2_RNN_TUNE")
     tr2 = Trainer(_build(3, 256, 2), LABELS, device=dev, verbose=False)
     v = tr2.train_batch((x, tg, None, pct.clone(), tl), return_item=True)
     assert np.isfinite(v)
