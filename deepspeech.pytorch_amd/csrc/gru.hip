@@ -893,6 +893,7 @@ __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
       }
       trace_at(s, 1);
       const int base = (((s - 1) % NSLOT) * slot_floats + grp_off + b0 * 256 + lane * 4) * 4;
+      if (HM == 1) sleep_units(g_rnn_tune[2]);
       f32x4 gv[NBW];
 #pragma unroll
       for (int i = 0; i < NBW; ++i) {
@@ -901,13 +902,51 @@ __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
       }
       asm volatile("" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
+      if (SENT) {
+        // sentinel ring (and hybrid, HM 2: flag-polled, sentinel-validated): passes over the
+        // wave's tiles; each pass marks the ready ones,
+        // multiplies the ready PREFIX in tile order (one accumulation order for every
+        // hand-off form: bit-identical results) and re-loads only the stale tiles, so a
+        // pass costs one round trip however many tiles are stale
+        unsigned rdy = 0u;
+        int next = 0;
+        for (unsigned spins = 0;; ++spins) {
 #pragma unroll
-      for (int i = 0; i < NBW; ++i) {
-        if (SENT && i < nb && !spin_tile(gv[i], x_rs, base + i * 1024, err)) failed = 1;
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(gv[i][0], w[i][0], acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(gv[i][1], w[i][1], acc1, 0, 0, 0);
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(gv[i][2], w[i][2], acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(gv[i][3], w[i][3], acc1, 0, 0, 0);
+          for (int i = 0; i < NBW; ++i)
+            if (i >= next && i < nb && !((rdy >> i) & 1u) && wave_ready(gv[i])) rdy |= 1u << i;
+#pragma unroll
+          for (int i = 0; i < NBW; ++i) {
+            if (i == next && i < nb && ((rdy >> i) & 1u)) {
+              acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(gv[i][0], w[i][0], acc0, 0, 0, 0);
+              acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(gv[i][1], w[i][1], acc1, 0, 0, 0);
+              acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(gv[i][2], w[i][2], acc0, 0, 0, 0);
+              acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(gv[i][3], w[i][3], acc1, 0, 0, 0);
+              ++next;
+            }
+          }
+          if (next >= nb) break;
+          if (spins > g_spin_limit) {
+            if (lane == 0) __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            failed = 1;
+            break;
+          }
+          sleep_units(g_rnn_tune[0]);
+          asm volatile("" ::: "memory");
+#pragma unroll
+          for (int i = 0; i < NBW; ++i)
+            if (i >= next && i < nb && !((rdy >> i) & 1u))
+              gv[i] = __builtin_bit_cast(
+                  f32x4, __builtin_amdgcn_raw_buffer_load_b128(x_rs, base + i * 1024, 0, kSc1));
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < NBW; ++i) {
+          if (SENT && i < nb && !spin_tile(gv[i], x_rs, base + i * 1024, err)) failed = 1;
+          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(gv[i][0], w[i][0], acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(gv[i][1], w[i][1], acc1, 0, 0, 0);
+          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(gv[i][2], w[i][2], acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(gv[i][3], w[i][3], acc1, 0, 0, 0);
+        }
       }
       trace_at(s, 2);
     }

@@ -297,8 +297,12 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
 // backward: rec[16 samples x 16 units] = dG[16 x 3H] . W_hh[3H rows, 16 units], dG = the
 // (dar, daz, dghn) gate gradients of the step after (tiles g UB + ub of the ring, as in
 // gru_bwd_dop_kernel).  HM: 0 per-producer flags, 1 sentinel ring (pairs in order).
-template <int NP, int HM>
-__global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(1, 1))) void gru_bwd_x6_kernel(
+// NW waves per workgroup: 4 (one per SIMD, all NP pairs' tiles loaded at once) or 8 (two
+// per SIMD: the consumer-side splits are VALU work, and a lone wave issues VALU at half the
+// rate of two co-resident ones; 256 registers each, so the tiles stream through a window of
+// LW pairs in flight).
+template <int NP, int HM, int NW>
+__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW / 4, NW / 4))) void gru_bwd_x6_kernel(
     int T, int N, int H, int D, int UB, int BT, const float* __restrict__ dy, int dyd,
     const float* __restrict__ w_f, const float* __restrict__ w_r,
     const float* __restrict__ h_all, const float* __restrict__ gates,
@@ -308,7 +312,8 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   constexpr int RP = GU + 1;
   constexpr bool SENT = HM == 1;
   constexpr int NSLOT = SENT ? kRingSlots : 2;
-  __shared__ float red[XW * GB * RP];
+  constexpr int LW = NW == 4 ? NP : 3;          // pairs whose loads are in flight
+  __shared__ float red[NW * GB * RP];
   __shared__ __attribute__((aligned(16))) float tile[3 * GB * GU];
   __shared__ int flag;
   __shared__ int failed;
@@ -319,8 +324,9 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int H3 = 3 * H;
   const int NB3 = 3 * UB;
-  int p0, np;
-  pair_split((NB3 + 1) >> 1, wave, p0, np);
+  const int pairs = (NB3 + 1) >> 1;
+  const int p0 = (pairs * wave) / NW;
+  const int np = (pairs * (wave + 1)) / NW - p0;   // host guarantees np <= NP
   const int t_first = 2 * p0;
   const unsigned* gflags = counters + (D * BT + 1) + (d * BT + bt) * UB;
   unsigned* myflag = counters + (D * BT + 1) + (d * BT + bt) * UB + ub;
@@ -358,11 +364,12 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
       w[p] = split3(a, b);
     }
   }
-  const int m = threadIdx.x >> 4;
+  const int m = (threadIdx.x >> 4) & 15;
   const int u = threadIdx.x & 15;
   const int n = n0 + m;
   const int j = ub * GU + u;
-  const bool owner = n < N;
+  const bool gate_thread = threadIdx.x < GB * GU;
+  const bool owner = gate_thread && n < N;
   int len = owner ? lens[n] : 0;
   settle(len);
   const int tpos = ((u >> 2) * GB + m) * 4 + (u & 3);
@@ -393,15 +400,20 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
       trace_at(s, 1);
       const int base = (((s - 1) % NSLOT) * slot_floats + grp_off + t_first * 256 + lane * 4) * 4;
       f32x4 gv[2 * NP];
-#pragma unroll
-      for (int i = 0; i < 2 * NP; ++i) {
+      auto load_tile = [&](int i) {
         const int off = (i < 2 * np && t_first + i < NB3) ? base + i * 1024 : 0x7ffffff0;
         gv[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(x_rs, off, 0, kSc1));
-      }
+      };
+#pragma unroll
+      for (int i = 0; i < 2 * LW; ++i) load_tile(i);
       asm volatile("" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int p = 0; p < NP; ++p) {
+        if (p + LW < NP) {
+          load_tile(2 * (p + LW));
+          load_tile(2 * (p + LW) + 1);
+        }
         if (SENT && p < np) {
           if (!spin_tile(gv[2 * p], x_rs, base + 2 * p * 1024, err)) failed = 1;
           if (t_first + 2 * p + 1 < NB3 &&
@@ -435,7 +447,7 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
         if (s > 0) {
           float rec = 0.f;
 #pragma unroll
-          for (int w8 = 0; w8 < XW; ++w8) rec += red[(w8 * GB + m) * RP + u];
+          for (int w8 = 0; w8 < NW; ++w8) rec += red[(w8 * GB + m) * RP + u];
           carry = dh_prev * z_prev + rec;
         }
         dh = dyv + carry;
@@ -449,9 +461,11 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
       z_prev = zc;
       px_dar = dar; px_daz = daz; px_dan = dan; px_dghn = dghn; px_row = row;
     }
-    tile[tpos] = dar;
-    tile[GB * GU + tpos] = daz;
-    tile[2 * GB * GU + tpos] = dghn;
+    if (gate_thread) {
+      tile[tpos] = dar;
+      tile[GB * GU + tpos] = daz;
+      tile[2 * GB * GU + tpos] = dghn;
+    }
     __syncthreads();
     if (wave == 0) {
       const int toff = (grp_off + ub * 256 + lane * 4) * 4;
@@ -523,13 +537,24 @@ static const void* fwd_x6_fn(int need, int hm) {
   return nullptr;
 }
 
-static const void* bwd_x6_fn(int need, int hm) {
-#define DS2_BX6(K) \
-  if (need <= K)   \
-    return hm == 1 ? reinterpret_cast<const void*>(gru_bwd_x6_kernel<K, 1>)  \
-                   : reinterpret_cast<const void*>(gru_bwd_x6_kernel<K, 0>);
-  DS2_BX6(1) DS2_BX6(2) DS2_BX6(3) DS2_BX6(4) DS2_BX6(6) DS2_BX6(8) DS2_BX6(10)
-  DS2_BX6(13) DS2_BX6(16) DS2_BX6(19)
+static int x6_bwd_waves() {
+  const char* e = getenv("DS2_GRU_X6_BWD_WAVES");
+  return (e != nullptr && e[0] == '4') ? 4 : 8;
+}
+
+static const void* bwd_x6_fn(int pairs, int hm, int nw) {
+  const int need = (pairs + nw - 1) / nw;
+#define DS2_BX6(K, W)                                                                      \
+  if (need <= K)                                                                           \
+    return hm == 1 ? reinterpret_cast<const void*>(gru_bwd_x6_kernel<K, 1, W>)            \
+                   : reinterpret_cast<const void*>(gru_bwd_x6_kernel<K, 0, W>);
+  if (nw == 4) {
+    DS2_BX6(1, 4) DS2_BX6(2, 4) DS2_BX6(3, 4) DS2_BX6(4, 4) DS2_BX6(6, 4) DS2_BX6(8, 4)
+    DS2_BX6(10, 4) DS2_BX6(13, 4) DS2_BX6(16, 4) DS2_BX6(19, 4)
+  } else {
+    DS2_BX6(1, 8) DS2_BX6(2, 8) DS2_BX6(3, 8) DS2_BX6(4, 8) DS2_BX6(5, 8) DS2_BX6(6, 8)
+    DS2_BX6(8, 8) DS2_BX6(10, 8) DS2_BX6(12, 8)
+  }
 #undef DS2_BX6
   return nullptr;
 }
@@ -562,13 +587,13 @@ bool launch_gru_bwd_x6(int hm, int t_max, int n, int h, int num_dirs, const floa
   apply_spin_limit_env();
   apply_rnn_tune_env();
   const int UB = h / GU, BT = (n + GB - 1) / GB;
-  const int need = ((3 * UB + 1) / 2 + XW - 1) / XW;
-  const void* fn = bwd_x6_fn(need, hm == 1 ? 1 : 0);
+  const int nw = x6_bwd_waves();
+  const void* fn = bwd_x6_fn((3 * UB + 1) / 2, hm == 1 ? 1 : 0, nw);
   if (fn == nullptr) return false;
   int T_ = t_max, N_ = n, H_ = h, D_ = num_dirs, UB_ = UB, BT_ = BT, DYD_ = dy_dirs;
   void* args[] = {&T_, &N_, &H_, &D_, &UB_, &BT_, &dy, &DYD_, &w_hh_f, &w_hh_r, &h_all,
                   &gates, &lens, &dgates_x, &dgates_h, &ring, &ctrs, &err, &stamps};
-  return hipLaunchCooperativeKernel(fn, dim3(mapped_grid(UB * num_dirs, BT)), dim3(XT), args,
+  return hipLaunchCooperativeKernel(fn, dim3(mapped_grid(UB * num_dirs, BT)), dim3(nw * 64), args,
                                     lds_pad, st) == hipSuccess;
 }
 

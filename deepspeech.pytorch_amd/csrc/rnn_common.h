@@ -126,27 +126,26 @@ static void apply_spin_limit_env() {
 }
 
 // Polling knobs of the sentinel hand-off: [0] s_sleep(1) units between re-load passes, [1]
-// units before a step's first load pass (a consumer that loads right after publishing mostly
-// gets sentinels back, and those full-tile polls from every workgroup crowd the fabric that
-// carries the real tiles).  Defaults from scripts/gru_ab.py sweeps; DS2_RNN_TUNE="a,b"
-// overrides them (diagnostic; checked at every recurrence entry point).
-constexpr unsigned kRepollSleep = 1u, kFirstPollDelay = 14u;
-static __constant__ unsigned g_rnn_tune[2] = {kRepollSleep, kFirstPollDelay};
+// units before a forward step's first load pass, [2] the same for the backward (a consumer
+// that loads right after publishing mostly gets sentinels back, and those full-tile polls
+// from every workgroup crowd the fabric that carries the real tiles).  Defaults from
+// scripts/gru_ab.py sweeps; DS2_RNN_TUNE="a,b,c" overrides them (diagnostic; checked at every
+// recurrence entry point).
+constexpr unsigned kRepollSleep = 1u, kFirstPollDelay = 14u, kFirstPollDelayBwd = 14u;
+static __constant__ unsigned g_rnn_tune[3] = {kRepollSleep, kFirstPollDelay, kFirstPollDelayBwd};
 
 static void apply_rnn_tune_env() {
-  static unsigned applied[2] = {kRepollSleep, kFirstPollDelay};
-  unsigned v[2] = {kRepollSleep, kFirstPollDelay};
+  static unsigned applied[3] = {kRepollSleep, kFirstPollDelay, kFirstPollDelayBwd};
+  unsigned v[3] = {kRepollSleep, kFirstPollDelay, kFirstPollDelayBwd};
   const char* e = getenv("DS2_RNN_TUNE");
-  if (e != nullptr && e[0] != 0) {
+  for (int i = 0; e != nullptr && e[0] != 0 && i < 3; ++i) {
     char* end = nullptr;
-    v[0] = static_cast<unsigned>(strtoul(e, &end, 10));
-    if (end != nullptr && *end == ',') v[1] = static_cast<unsigned>(strtoul(end + 1, nullptr, 10));
+    v[i] = static_cast<unsigned>(strtoul(e, &end, 10));
+    e = (end != nullptr && *end == ',') ? end + 1 : nullptr;
   }
-  if (v[0] == applied[0] && v[1] == applied[1]) return;
-  if (hipMemcpyToSymbol(HIP_SYMBOL(g_rnn_tune), v, sizeof(v)) == hipSuccess) {
-    applied[0] = v[0];
-    applied[1] = v[1];
-  }
+  if (v[0] == applied[0] && v[1] == applied[1] && v[2] == applied[2]) return;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_rnn_tune), v, sizeof(v)) == hipSuccess)
+    for (int i = 0; i < 3; ++i) applied[i] = v[i];
 }
 
 __device__ __forceinline__ void sleep_units(unsigned k) {

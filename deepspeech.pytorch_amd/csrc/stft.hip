@@ -17,6 +17,7 @@ namespace ds2 {
 
 constexpr int SF = 8;          // frames per workgroup
 constexpr int SMAXN = 1024;    // max n_fft
+constexpr int kRows = 161;     // rows of the returned spectrogram (data_loader_aug.py:234-249)
 constexpr int kMaskInts = 9;   // per utterance: f_lo0 f_hi0 f_lo1 f_hi1 t_lo0 t_hi0 t_lo1 t_hi1 f_cut
 
 __device__ __forceinline__ int reflect_idx(int i, int n) {
@@ -42,7 +43,8 @@ __global__ __launch_bounds__(256) void stft_kernel(const float* __restrict__ pcm
                                                    const double* __restrict__ window,
                                                    int normalize, float* __restrict__ out,
                                                    int max_frames, float* __restrict__ frame_mean,
-                                                   const int* __restrict__ masks) {
+                                                   const int* __restrict__ masks,
+                                                   float* __restrict__ raw) {
   __shared__ double cs[SMAXN], sn[SMAXN];
   __shared__ double fr[SF][SMAXN];
   __shared__ double red[SF][4];
@@ -51,6 +53,9 @@ __global__ __launch_bounds__(256) void stft_kernel(const float* __restrict__ pcm
   const int nb = n_samples[b];
   const int T = 1 + nb / hop;
   const int F = n_fft / 2 + 1;
+  // bins computed: the 161 returned rows when F >= 161 (spect[:161], :249); all F bins in
+  // the raw mode (F < 161: the mirror-fill layout is built from them by remap_kernel)
+  const int R = raw != nullptr ? F : (F < kRows ? F : kRows);
   const int pad = n_fft / 2;
   const float* y = pcm + (int64_t)b * max_samples;
   for (int m = threadIdx.x; m < n_fft; m += blockDim.x) {
@@ -86,7 +91,7 @@ __global__ __launch_bounds__(256) void stft_kernel(const float* __restrict__ pcm
   double lsum[SF];
 #pragma unroll
   for (int f = 0; f < SF; ++f) lsum[f] = 0.0;
-  if (k < F) {
+  if (k < R) {
     double re[SF], im[SF];
 #pragma unroll
     for (int f = 0; f < SF; ++f) { re[f] = 0.0; im[f] = 0.0; }
@@ -102,6 +107,16 @@ __global__ __launch_bounds__(256) void stft_kernel(const float* __restrict__ pcm
       idx += k;
       if (idx >= n_fft) idx -= n_fft;
     }
+    if (raw != nullptr) {     // |D| frame-major, the memory order of librosa's stft matrix
+#pragma unroll
+      for (int f = 0; f < SF; ++f) {
+        const int t = t0 + f;
+        if (t < T && t < max_frames)
+          raw[((int64_t)b * max_frames + t) * F + k] =
+              hypotf(static_cast<float>(re[f]), static_cast<float>(im[f]));
+      }
+      return;
+    }
 #pragma unroll
     for (int f = 0; f < SF; ++f) {
       const int t = t0 + f;
@@ -115,9 +130,10 @@ __global__ __launch_bounds__(256) void stft_kernel(const float* __restrict__ pcm
         val = normalize ? log1pf(mag * 1048576.0f) : log1pf(mag);
         lsum[f] = val;
       }
-      out[((int64_t)b * F + k) * max_frames + t] = val;
+      out[((int64_t)b * R + k) * max_frames + t] = val;
     }
   }
+  if (raw != nullptr) return;
   // mean over the F bins of every frame (torch spect.mean(dim=0))
 #pragma unroll
   for (int f = 0; f < SF; ++f) {
@@ -130,9 +146,58 @@ __global__ __launch_bounds__(256) void stft_kernel(const float* __restrict__ pcm
     const int t = t0 + f;
     if (t < T && t < max_frames) {
       const double s = red[f][0] + red[f][1] + red[f][2] + red[f][3];
-      frame_mean[(int64_t)b * max_frames + t] = static_cast<float>(s / F);
+      frame_mean[(int64_t)b * max_frames + t] = static_cast<float>(s / R);
     }
   }
+}
+
+// F < 161 bins (sample rates below 16 kHz): data_loader_aug.py:234-238
+//   spect.resize((161, T)); spect[81:] = spect[80:0:-1]
+// on librosa's stft matrix, which is Fortran-ordered (frame-major memory), so ndarray.resize
+// keeps the first 161 T values of that memory in column-major order and zero-fills the rest:
+// row r <= 80 of column t holds flat value 161 t + r (bin (161 t + r) % F of frame
+// (161 t + r) / F), rows 81..160 mirror rows 80..1.  Then the spectrogram masks, the 8 kHz
+// cut, log1p and the per-column mean, as in the fused kernel.  One wave per column.
+__global__ __launch_bounds__(256) void remap_kernel(const float* __restrict__ raw,
+                                                    const int* __restrict__ n_samples, int hop,
+                                                    int F, int normalize, int max_frames,
+                                                    const int* __restrict__ masks,
+                                                    float* __restrict__ out,
+                                                    float* __restrict__ frame_mean) {
+  const int b = blockIdx.y;
+  const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (t >= max_frames) return;
+  const int T = 1 + n_samples[b] / hop;
+  int fm[4] = {0, 0, 0, 0}, tm[4] = {0, 0, 0, 0}, fcut = kRows;
+  if (masks != nullptr) {
+    const int* mk = masks + b * kMaskInts;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      fm[i] = mk[i];
+      tm[i] = mk[4 + i];
+    }
+    fcut = mk[8];
+  }
+  const bool tmasked = (t >= tm[0] && t < tm[1]) || (t >= tm[2] && t < tm[3]);
+  const float* rb = raw + (int64_t)b * max_frames * F;
+  const int64_t valid = (int64_t)F * (T < max_frames ? T : max_frames);
+  double lsum = 0.0;
+  for (int r = lane; r < kRows; r += 64) {
+    float val = 0.f;
+    if (t < T) {
+      const int rs = r <= 80 ? r : kRows - r;
+      const int64_t kf = (int64_t)kRows * t + rs;
+      const bool masked = tmasked || (r >= fm[0] && r < fm[1]) || (r >= fm[2] && r < fm[3]) ||
+                          r >= fcut;
+      const float mag = (masked || kf >= valid) ? 0.f : rb[kf];
+      val = normalize ? log1pf(mag * 1048576.0f) : log1pf(mag);
+      lsum += val;
+    }
+    out[((int64_t)b * kRows + r) * max_frames + t] = val;
+  }
+  lsum = wave_sum_d(lsum);
+  if (lane == 0 && t < T) frame_mean[(int64_t)b * max_frames + t] = static_cast<float>(lsum / kRows);
 }
 
 // One block per utterance: max_mean = mean_t(gaussian_filter1d(frame_mean, sigma)).
@@ -178,8 +243,15 @@ using namespace ds2;
 
 extern "C" {
 
-size_t ds2_stft_workspace_size(int batch, int max_frames) {
+static size_t stft_base_ws(int batch, int max_frames) {
   return (size_t)batch * max_frames * sizeof(float) + (size_t)batch * sizeof(float) + 512;
+}
+
+size_t ds2_stft_workspace_size(int batch, int max_frames, int n_fft) {
+  const int F = n_fft / 2 + 1;
+  size_t bytes = stft_base_ws(batch, max_frames);
+  if (F < kRows) bytes += (size_t)batch * max_frames * F * sizeof(float) + 256;
+  return bytes;
 }
 
 ds2_status_t ds2_stft_logmag_masked(const float* pcm, const int* n_samples, int batch,
@@ -191,22 +263,32 @@ ds2_status_t ds2_stft_logmag_masked(const float* pcm, const int* n_samples, int 
   if (n_fft / 2 + 1 > 256) return DS2_UNSUPPORTED_SHAPE;
   if (normalize == 1 && (gauss_taps == nullptr || gauss_radius < 0)) return DS2_INVALID_VALUE;
   if (batch == 0) return DS2_OK;
-  if (ws == nullptr || ws_bytes < ds2_stft_workspace_size(batch, max_frames))
+  if (ws == nullptr || ws_bytes < ds2_stft_workspace_size(batch, max_frames, n_fft))
     return DS2_WORKSPACE_TOO_SMALL;
   hipStream_t st = as_stream(stream);
   float* frame_mean = static_cast<float*>(ws);
   float* offset = frame_mean + (size_t)batch * max_frames;
   const int F = n_fft / 2 + 1;
-  hipLaunchKernelGGL(stft_kernel, dim3(cdiv(max_frames, SF), batch), dim3(256), 0, st, pcm,
-                     n_samples, max_samples, n_fft, hop, window, normalize, out, max_frames,
-                     frame_mean, masks);
+  if (F < kRows) {
+    float* raw = reinterpret_cast<float*>(
+        static_cast<char*>(ws) + ((stft_base_ws(batch, max_frames) + 255) & ~(size_t)255));
+    hipLaunchKernelGGL(stft_kernel, dim3(cdiv(max_frames, SF), batch), dim3(256), 0, st, pcm,
+                       n_samples, max_samples, n_fft, hop, window, normalize, out, max_frames,
+                       frame_mean, masks, raw);
+    hipLaunchKernelGGL(remap_kernel, dim3(cdiv(max_frames, 4), batch), dim3(256), 0, st, raw,
+                       n_samples, hop, F, normalize, max_frames, masks, out, frame_mean);
+  } else {
+    hipLaunchKernelGGL(stft_kernel, dim3(cdiv(max_frames, SF), batch), dim3(256), 0, st, pcm,
+                       n_samples, max_samples, n_fft, hop, window, normalize, out, max_frames,
+                       frame_mean, masks, nullptr);
+  }
   if (normalize == 1) {
     hipLaunchKernelGGL(maxframe_offset_kernel, dim3(batch), dim3(256), 0, st, n_samples, hop,
                        max_frames, frame_mean, gauss_taps, gauss_radius, offset);
-    int g = cdiv((int64_t)F * max_frames, 256);
+    int g = cdiv((int64_t)kRows * max_frames, 256);
     if (g > 512) g = 512;
-    hipLaunchKernelGGL(subtract_offset_kernel, dim3(g, batch), dim3(256), 0, st, n_samples, hop, F,
-                       max_frames, offset, out);
+    hipLaunchKernelGGL(subtract_offset_kernel, dim3(g, batch), dim3(256), 0, st, n_samples, hop,
+                       kRows, max_frames, offset, out);
   }
   return launch_status("ds2_stft_logmag");
 }

@@ -25,7 +25,7 @@ _PROTOS = {
     "ds2_status_string": (ctypes.c_char_p, [_c_int]),
     "ds2_last_error": (ctypes.c_char_p, []),
     "ds2_version": (ctypes.c_char_p, []),
-    "ds2_stft_workspace_size": (_sz, [_c_int, _c_int]),
+    "ds2_stft_workspace_size": (_sz, [_c_int, _c_int, _c_int]),
     "ds2_stft_logmag": (_c_int, [_vp, _vp, _c_int, _c_int, _c_int, _c_int, _vp, _c_int, _vp,
                                  _c_int, _vp, _c_int, _vp, _sz, _vp]),
     "ds2_stft_logmag_masked": (_c_int, [_vp, _vp, _c_int, _c_int, _c_int, _c_int, _vp, _c_int,

@@ -116,7 +116,7 @@ class SpectrogramParser(object):
         pcm_d = torch.from_numpy(pcm).to(self.device)
         ns_d = torch.tensor(lens, dtype=torch.int32).to(self.device)
         frames = [1 + n // hop for n in lens]
-        masks = self.spect_aug.masks(n_fft // 2 + 1, frames, self.device)
+        masks = self.spect_aug.masks(ops.SPECT_ROWS, frames, self.device)
         out = ops.stft_logmag(pcm_d, ns_d, n_fft, hop, win, self._mode(), taps, max(frames),
                               masks=masks)
         if self.augment and self.normalize == 'max_frame':

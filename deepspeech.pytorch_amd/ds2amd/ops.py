@@ -327,17 +327,21 @@ def ctc_beam_decode_raw(probs: torch.Tensor, sizes: Optional[torch.Tensor], beam
     return ids, offs, lens, scores
 
 
+SPECT_ROWS = 161   # rows of every spectrogram the reference returns (data_loader_aug.py:234-249)
+
+
 def stft_logmag(pcm: torch.Tensor, n_samples: torch.Tensor, n_fft: int, hop: int,
                 window: torch.Tensor, normalize: int, gauss_taps: Optional[torch.Tensor],
                 max_frames: int, masks: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """masks: None or int32 [batch, 9] spectrogram-augmentation bands (ds2hip.h)."""
+    """-> [batch, 161, max_frames]: the first 161 bins, or the reference's mirror-fill when
+    n_fft/2+1 < 161 (8 kHz audio; ds2hip.h).  masks: None or int32 [batch, 9]
+    spectrogram-augmentation bands (ds2hip.h), rows of the 161-row output."""
     pcm = _need(pcm, "stft.pcm")
     n_samples = _need(n_samples, "stft.n_samples", _I32)
     window = _need(window, "stft.window", torch.float64)
     b, max_samples = pcm.shape
-    f = n_fft // 2 + 1
-    out = torch.empty(b, f, max_frames, device=pcm.device, dtype=_F32)
-    ws = _ws(_lib.size("ds2_stft_workspace_size", b, max_frames), pcm.device)
+    out = torch.empty(b, SPECT_ROWS, max_frames, device=pcm.device, dtype=_F32)
+    ws = _ws(_lib.size("ds2_stft_workspace_size", b, max_frames, n_fft), pcm.device)
     radius = 0 if gauss_taps is None else (gauss_taps.numel() - 1) // 2
     if masks is not None:
         masks = _need(masks, "stft.masks", _I32)

@@ -45,10 +45,13 @@ const char* ds2_version(void);
 /* Features: SpectrogramParser.audio_to_stft + normalize_audio('max_frame') */
 /* ref data/data_loader.py:201-220,276-284; data/data_loader_aug.py:220-249,297-307 */
 /* pcm:  [batch][max_samples] float32, utterance b has n_samples[b] valid samples   */
-/* out:  [batch][n_fft/2+1][max_frames], frames t >= 1 + n_samples[b]/hop are zero  */
+/* out:  [batch][161][max_frames], frames t >= 1 + n_samples[b]/hop are zero: the     */
+/*       reference always returns 161 rows (data_loader_aug.py:234-249): the first   */
+/*       161 bins when n_fft/2+1 >= 161, else its mirror-fill of ndarray.resize on    */
+/*       librosa's (Fortran-ordered) stft matrix -- see stft.hip remap_kernel.         */
 /* window: n_fft doubles (symmetric Hamming in the reference).                     */
 /* normalize: 0 = log1p(|X|), 1 = 'max_frame' (log1p(|X|*2^20) - mean(gauss20(mean_f))) */
-size_t ds2_stft_workspace_size(int batch, int max_frames);
+size_t ds2_stft_workspace_size(int batch, int max_frames, int n_fft);
 ds2_status_t ds2_stft_logmag(const float* pcm, const int* n_samples, int batch, int max_samples,
                              int n_fft, int hop, const double* window, int normalize,
                              const float* gauss_taps, int gauss_radius,
@@ -59,7 +62,7 @@ ds2_status_t ds2_stft_logmag(const float* pcm, const int* n_samples, int batch, 
  * aug_prob_8khz cut) applied to |X| before the log, as the reference does.  masks: NULL
  * or [batch][9] int32 = {f_lo0, f_hi0, f_lo1, f_hi1, t_lo0, t_hi0, t_lo1, t_hi1, f_cut}:
  * bins in [f_lo, f_hi), frames in [t_lo, t_hi) and bins >= f_cut are zeroed (empty when
- * lo >= hi; f_cut = n_fft/2+1 for none).  The random draws stay on the host
+ * lo >= hi; f_cut = 161 for none), rows of the 161-row output.  The random draws stay on the host
  * (ds2amd/spect_aug.py) so they follow the reference's `random` call sequence. */
 ds2_status_t ds2_stft_logmag_masked(const float* pcm, const int* n_samples, int batch,
                                     int max_samples, int n_fft, int hop, const double* window,

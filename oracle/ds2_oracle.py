@@ -52,6 +52,22 @@ def stft_magnitude(y: np.ndarray, sample_rate=16000, window_size=0.02, window_st
     return np.abs(spec)
 
 
+def rows161(spect: np.ndarray) -> np.ndarray:
+    """data_loader_aug.py:233-238,249 on the magnitude: fewer than 161 bins (sample rates
+    below 16 kHz) -> ``spect.resize((161, T)); spect[81:] = spect[80:0:-1]``; then
+    ``spect[:161]``.  librosa < 0.10 allocates the stft matrix Fortran-ordered and np.abs
+    keeps that order (so does stft_magnitude above), and ndarray.resize works on the memory
+    order: row r <= 80 of column t receives flat value 161 t + r of the frame-major data
+    (zeros past its end), not row r of frame t.  Restated literally; parity with librosa
+    itself is unpinned (absent here)."""
+    shape = spect.shape
+    if shape[0] < 161:
+        spect = spect.copy(order='K')
+        spect.resize((161, *shape[1:]), refcheck=False)
+        spect[81:] = spect[80:0:-1]
+    return spect[:161]
+
+
 def gaussian_filter1d_reflect(x: np.ndarray, sigma: float, truncate: float = 4.0):
     """scipy.ndimage.gaussian_filter1d(x, sigma) for 1-D float32 x (mode 'reflect')."""
     from scipy.ndimage import gaussian_filter1d
@@ -71,7 +87,7 @@ def normalize_max_frame(spect: np.ndarray) -> torch.Tensor:
 
 def spectrogram(y, sample_rate=16000, window_size=0.02, window_stride=0.01,
                 normalize='max_frame') -> torch.Tensor:
-    mag = stft_magnitude(y, sample_rate, window_size, window_stride)
+    mag = rows161(stft_magnitude(y, sample_rate, window_size, window_stride))
     if normalize == 'max_frame':
         return normalize_max_frame(mag)
     return torch.FloatTensor(np.log1p(mag))

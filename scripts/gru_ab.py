@@ -66,6 +66,13 @@ if len(sys.argv) > 1 and sys.argv[1] == "tune":
         for t in ("1,0", "1,10", "1,14", "1,18", "2,14", "1,22"):
             variants[f"{'x6' if x6 == '1' else 'f32'}-tune-{t}"] = {
                 "DS2_GRU_X6": x6, "DS2_RNN_HANDOFF": "", "DS2_RNN_TUNE": t}
+if len(sys.argv) > 1 and sys.argv[1] == "btune":
+    variants = {"bwd-f32-flags": {"DS2_GRU_X6": "1", "DS2_GRU_X6_BWD": "0",
+                                  "DS2_RNN_HANDOFF_BWD": "flags"},
+                "bwd-x6w8-flags": {"DS2_GRU_X6": "1", "DS2_GRU_X6_BWD": "1",
+                                   "DS2_GRU_X6_BWD_WAVES": "8", "DS2_RNN_HANDOFF_BWD": "flags"},
+                "bwd-x6w4-flags": {"DS2_GRU_X6": "1", "DS2_GRU_X6_BWD": "1",
+                                   "DS2_GRU_X6_BWD_WAVES": "4", "DS2_RNN_HANDOFF_BWD": "flags"}}
 rounds = int(os.environ.get("AB_ROUNDS", "3"))
 variants = {f"{k}#{r}": v for r in range(rounds) for k, v in variants.items()}
 ref = None

@@ -47,7 +47,9 @@ def test_host_queries():
     assert _lib.size("ds2_gru_bwd_workspace_size", 32, 800, 2) >= 2 * 800 * 2400 * 4
     assert _lib.size("ds2_conv2d_wgrad_workspace_size", 32, 32, 81, 501, 32, 21, 11, 2, 1, 10,
                      5) >= 32 * 32 * 7392 * 4
-    assert _lib.size("ds2_stft_workspace_size", 32, 1001) >= 32 * 1001 * 4
+    assert _lib.size("ds2_stft_workspace_size", 32, 1001, 320) >= 32 * 1001 * 4
+    # 8 kHz (81 bins): room for the frame-major magnitudes of the mirror-fill
+    assert _lib.size("ds2_stft_workspace_size", 2, 101, 160) >= 2 * 101 * 81 * 4
 
 
 def test_invalid_args_rejected_without_launch():

@@ -683,6 +683,39 @@ def test_stft_spect_aug_masks_vs_oracle(dev):
         assert err < 2e-4, f"wav {i} row {row}: max abs err {err}"
 
 
+@pytest.mark.parametrize("sr", [8000, 11025, 22050])
+@pytest.mark.parametrize("masked", [False, True])
+def test_stft_other_sample_rates_vs_oracle(dev, sr, masked):
+    """Sample rates other than 16 kHz (data_loader_aug.py:221-249): fewer than 161 bins
+    (8 kHz: 81, 11.025 kHz: 111) take the reference's resize + mirror-fill layout, more
+    (22.05 kHz: 221) are cut to 161 rows; spectrogram masks then act on the 161 rows."""
+    import random
+    from ds2amd.data_loader import SpectrogramParser
+    from ds2amd.spect_aug import apply_masks_np
+    conf = dict(sample_rate=sr, window_size=0.02, window_stride=0.01, window='hamming')
+    if masked:
+        conf.update(noise_prob=1.0, aug_prob_spect=1.0, aug_prob_8khz=0.5)
+    parser = SpectrogramParser(conf, normalize='max_frame', device=dev)
+    parser.spect_aug.rng = random.Random(5)
+    replay = SpectrogramParser(conf, normalize='max_frame', device=dev).spect_aug
+    replay.rng = random.Random(5)
+    rng = np.random.default_rng(sr)
+    wavs = [(rng.standard_normal(n) * 0.3).astype(np.float32)
+            for n in (sr * 2 + 17, sr, sr // 2 + 3)]
+    out, frames = parser.parse_batch(wavs, sr)
+    assert out.shape[2] == 161
+    for i, y in enumerate(wavs):
+        mag = orc.rows161(orc.stft_magnitude(y, sr))
+        if masked:
+            mag = apply_masks_np(mag, replay.draw_one(161, int(frames[i])))
+        ref = orc.normalize_max_frame(mag)
+        assert int(frames[i]) == ref.shape[1]
+        got = out[i, 0, :, :ref.shape[1]].cpu()
+        err = (got - ref).abs().max().item()
+        assert err < 2e-4, f"sr {sr} wav {i}: max abs err {err}"
+        assert out[i, 0, :, ref.shape[1]:].abs().sum().item() == 0
+
+
 # ---------------------------------------------------------------------------- optimizer
 def test_fused_sgd_matches_torch(dev):
     from ds2amd.optim import FlatParams, FusedSGD

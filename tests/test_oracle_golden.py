@@ -349,3 +349,25 @@ def test_fused_sgd_state_dict_is_torch_sgd_format(golden_dir):
     bad['param_groups'][0]['nesterov'] = False
     with pytest.raises(ValueError):
         opt.load_state_dict(bad)
+
+
+def test_rows161_resize_mirror_semantics():
+    """data_loader_aug.py:233-238,249: a Fortran-ordered magnitude with < 161 bins (librosa's
+    layout) resized in memory order then mirrored; >= 161 bins cut to 161; 161 untouched."""
+    F, T = 81, 7
+    m = np.asfortranarray(np.arange(F * T, dtype=np.float32).reshape(T, F).T + 1)  # [F, T]
+    r = orc.rows161(m)
+    flat = m.T.reshape(-1)                       # frame-major memory order
+    exp = np.zeros((161, T), np.float32)
+    for t in range(T):
+        for row in range(81):
+            k = 161 * t + row
+            exp[row, t] = flat[k] if k < F * T else 0
+    exp[81:] = exp[80:0:-1]
+    np.testing.assert_array_equal(r, exp)
+    assert np.array_equal(m, np.asfortranarray(np.arange(F * T, dtype=np.float32)
+                                               .reshape(T, F).T + 1))   # input untouched
+    big = np.ones((221, 5), np.float32)
+    assert orc.rows161(big).shape == (161, 5)
+    y = np.random.default_rng(0).standard_normal(8000).astype(np.float32)
+    assert orc.spectrogram(y, sample_rate=8000).shape == (161, 101)
