@@ -278,15 +278,18 @@ __global__ void greedy_kernel(const float* __restrict__ probs, int n, int t_max,
 // ---------------------------------------------------------------------------
 // CTC prefix beam search without a language model (BeamCTCDecoder, decoder.py:90-143,
 // wrapping ctcdecode's ctc_beam_search_decoder with lm_path=None).  One 64-lane
-// workgroup per utterance; the beam (<= BEAM_MAX prefixes) lives in LDS, the prefix
+// workgroup per utterance; the beam (<= 128 prefixes) lives in LDS, the prefix
 // trie (parent, char, timestep, best char log-prob) in the workspace.  Per frame:
 // prune the vocabulary (cutoff_top_n / cutoff_prob), score every candidate
 // (prefix x char: blank / repeat "stay" terms, extensions, extensions that land on a
 // prefix already in the beam are merged into it), then keep the beam_width best by
 // (score desc, last char asc, candidate index asc).  oracle/ctc_beam.py restates the
 // same algorithm (parity with ctcdecode itself is unpinned: it is not available).
-constexpr int BEAM_MAX = 32;
-constexpr int BEAM_CMAX = 64;
+// two instantiations: beams <= 32 over vocabularies <= 64, and beams <= 128 (the
+// reference's default beam_width is 100, decoder.py:89) over vocabularies <= 32 -- both
+// keep every candidate (k = entry * C + char < 4096) in the wave's registers
+constexpr int BEAM_SMALL = 32, BEAM_SMALL_C = 64;
+constexpr int BEAM_LARGE = 128, BEAM_LARGE_C = 32;
 // frames of probabilities staged in LDS at a time: a global load consumed inside the frame
 // loop would make the waitcnt pass wait (vmcnt(0)) for the previous frame's trie stores
 constexpr int BEAM_TCH = 128;
@@ -338,6 +341,7 @@ __device__ __forceinline__ void beam_wave_best(float& bs, int& bk) {
   bk = key;
 }
 
+template <int BM, int CM>
 __global__ __launch_bounds__(64) void ctc_beam_kernel(
     const float* __restrict__ probs, int t_max, int C, int64_t stride_n, int64_t stride_t,
     const int* __restrict__ sizes, int blank, int beam, int cutoff_top_n, double cutoff_prob,
@@ -345,23 +349,24 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
     int* __restrict__ node_ts, float* __restrict__ node_lpc, int64_t node_cap,
     int* __restrict__ out_ids, int* __restrict__ out_ts, int* __restrict__ out_lens,
     float* __restrict__ out_scores) {
-  __shared__ float lp[BEAM_CMAX];
-  __shared__ int allowed[BEAM_CMAX];
-  __shared__ int order[BEAM_CMAX];
-  __shared__ int b_node[2][BEAM_MAX], b_last[2][BEAM_MAX];
-  __shared__ float b_pb[2][BEAM_MAX], b_pnb[2][BEAM_MAX];
+  constexpr int EPL = (BM + 63) / 64;   // beam entries per lane
+  __shared__ float lp[CM];
+  __shared__ int allowed[CM];
+  __shared__ int order[CM];
+  __shared__ int b_node[2][BM], b_last[2][BM];
+  __shared__ float b_pb[2][BM], b_pnb[2][BM];
   // per-entry copies of the entry's trie node's parent and best last-char log-prob, so
   // the per-frame chain has no global-memory reads (the trie is written, never read,
   // until the final back-tracking)
-  __shared__ int b_par[2][BEAM_MAX];
-  __shared__ float b_lpc[2][BEAM_MAX];
-  __shared__ float score[BEAM_MAX];
-  __shared__ int pidx[BEAM_MAX];
-  __shared__ signed char child_of[BEAM_MAX * BEAM_CMAX];
-  __shared__ float cpb[BEAM_MAX * BEAM_CMAX], cpnb[BEAM_MAX * BEAM_CMAX];
-  __shared__ int sel_k[BEAM_MAX];
+  __shared__ int b_par[2][BM];
+  __shared__ float b_lpc[2][BM];
+  __shared__ float score[BM];
+  __shared__ int pidx[BM];
+  __shared__ signed char child_of[BM * CM];
+  __shared__ float cpb[BM * CM], cpnb[BM * CM];
+  __shared__ int sel_k[BM];
   __shared__ int s_nb, s_nodes;
-  __shared__ float pch[BEAM_TCH * BEAM_CMAX];
+  __shared__ float pch[BEAM_TCH * CM];
 
   const int n = blockIdx.x;
   const int lane = threadIdx.x;
@@ -393,11 +398,11 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
       for (int e = lane; e < BEAM_TCH * C; e += 64) {
         const int f = e / C;
         const int c = e - f * C;
-        pch[f * BEAM_CMAX + c] = f < nf ? pn[(int64_t)(t + f) * stride_t + c] : 0.f;
+        pch[f * CM + c] = f < nf ? pn[(int64_t)(t + f) * stride_t + c] : 0.f;
       }
       __syncthreads();
     }
-    const float* pf = pch + tc * BEAM_CMAX;
+    const float* pf = pch + tc * CM;
     // ---- vocabulary pruning and log probs
     float pv = 0.f;
     if (lane < C) {
@@ -408,11 +413,11 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
       // rank of this lane's probability: C uniform lane reads (v_readlane), no LDS
       int rank = 0;
 #pragma unroll
-      for (int k = 0; k < BEAM_CMAX; ++k) {
-        if (k >= C) break;
+      for (int k = 0; k < CM; ++k) {
+        if (CM > 32 && k >= C) break;
         const float q = __builtin_bit_cast(
             float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, pv), k));
-        rank += (q > pv || (q == pv && k < lane)) ? 1 : 0;
+        rank += (k < C && (q > pv || (q == pv && k < lane))) ? 1 : 0;
       }
       if (lane < C) order[rank] = lane;
       __syncthreads();
@@ -429,26 +434,34 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
       allowed[lane] = 1;
     }
     // ---- beam bookkeeping: scores, parent index in the beam, child map
-    if (lane < nb) {
-      score[lane] = beam_lse(b_pb[cur][lane], b_pnb[cur][lane]);
-      const int nd = b_node[cur][lane];
-      const int pnode = nd > 0 ? b_par[cur][lane] : -1;
-      int j = -1;
 #pragma unroll
-      for (int i = 0; i < BEAM_MAX; ++i) {   // unrolled: the nb LDS reads overlap
-        if (i >= nb) break;
-        if (pnode >= 0 && b_node[cur][i] == pnode) j = i;
+    for (int q = 0; q < EPL; ++q) {
+      const int e = lane + 64 * q;
+      if (e < nb) {
+        score[e] = beam_lse(b_pb[cur][e], b_pnb[cur][e]);
+        const int nd = b_node[cur][e];
+        const int pnode = nd > 0 ? b_par[cur][e] : -1;
+        int j = -1;
+#pragma unroll
+        for (int i = 0; i < BM; ++i) {   // unrolled: the nb LDS reads overlap
+          if (i >= nb) break;
+          if (pnode >= 0 && b_node[cur][i] == pnode) j = i;
+        }
+        pidx[e] = j;
       }
-      pidx[lane] = j;
     }
     for (int e = lane; e < nb * C; e += 64) child_of[e] = -1;
     __syncthreads();
-    if (lane < nb && pidx[lane] >= 0) child_of[pidx[lane] * C + b_last[cur][lane]] = lane;
+#pragma unroll
+    for (int q = 0; q < EPL; ++q) {
+      const int e = lane + 64 * q;
+      if (e < nb && pidx[e] >= 0) child_of[pidx[e] * C + b_last[cur][e]] = static_cast<signed char>(e);
+    }
     __syncthreads();
     // ---- candidates, scored straight into registers: lane holds k = lane + 64 jj (the
     // selection below scans them there); the unrolled loop lets the LDS reads of several
     // candidates overlap.  (i, c) = divmod(k, C) advanced incrementally.
-    constexpr int SJ = BEAM_MAX * BEAM_CMAX / 64;
+    constexpr int SJ = BM * CM / 64;
     const int jn = (nb * C + 63) / 64;                   // wave-uniform
     float rs[SJ];
     int rk[SJ];
@@ -509,7 +522,8 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
       int bkey = 0x7fffffff;
 #pragma unroll
       for (int jj = 0; jj < SJ; ++jj) {
-        if (jj >= jn) break;
+        // slots past jn hold -inf; the early exit only where the unroller accepts it
+        if (SJ <= 32 && jj >= jn) break;
         if (rs[jj] != -INFINITY && beam_better(rs[jj], rk[jj], bs, bkey)) {
           bs = rs[jj];
           bkey = rk[jj];
@@ -525,44 +539,50 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
       ++nsel;
     }
     __syncthreads();
-    // ---- new beam: lane r builds entry r; new prefixes get trie nodes in rank order
-    // (node = first free + the number of extensions ranked before it)
+    // ---- new beam: lane r builds entries r, r + 64, ...; new prefixes get trie nodes in
+    // rank order (node = first free + the number of extensions ranked before it)
     const int nxt = cur ^ 1;
     {
-      int k = 0, i = 0, c = blank;
-      if (lane < nsel) {
-        k = sel_k[lane];
-        i = k / C;
-        c = k - i * C;
-      }
-      const bool ext = lane < nsel && c != blank;
-      const unsigned long long em = __ballot(ext);
-      const int before = __builtin_amdgcn_mbcnt_hi(static_cast<unsigned>(em >> 32),
-                                                   __builtin_amdgcn_mbcnt_lo(static_cast<unsigned>(em), 0));
       const int nodes0 = s_nodes;
-      if (lane < nsel) {
-        if (!ext) {
-          b_node[nxt][lane] = b_node[cur][i];
-          b_last[nxt][lane] = b_last[cur][i];
-          b_par[nxt][lane] = b_par[cur][i];
-          b_lpc[nxt][lane] = b_lpc[cur][i];
-        } else {
-          const int nd = nodes0 + before;
-          par[nd] = b_node[cur][i];
-          chr[nd] = c;
-          tst[nd] = t;
-          lpcv[nd] = lp[c];
-          b_node[nxt][lane] = nd;
-          b_last[nxt][lane] = c;
-          b_par[nxt][lane] = b_node[cur][i];
-          b_lpc[nxt][lane] = lp[c];
+      int run = 0;
+#pragma unroll
+      for (int q = 0; q < EPL; ++q) {
+        const int e = lane + 64 * q;
+        int k = 0, i = 0, c = blank;
+        if (e < nsel) {
+          k = sel_k[e];
+          i = k / C;
+          c = k - i * C;
         }
-        b_pb[nxt][lane] = cpb[k];
-        b_pnb[nxt][lane] = cpnb[k];
+        const bool ext = e < nsel && c != blank;
+        const unsigned long long em = __ballot(ext);
+        const int before = __builtin_amdgcn_mbcnt_hi(static_cast<unsigned>(em >> 32),
+                                                     __builtin_amdgcn_mbcnt_lo(static_cast<unsigned>(em), 0));
+        if (e < nsel) {
+          if (!ext) {
+            b_node[nxt][e] = b_node[cur][i];
+            b_last[nxt][e] = b_last[cur][i];
+            b_par[nxt][e] = b_par[cur][i];
+            b_lpc[nxt][e] = b_lpc[cur][i];
+          } else {
+            const int nd = nodes0 + run + before;
+            par[nd] = b_node[cur][i];
+            chr[nd] = c;
+            tst[nd] = t;
+            lpcv[nd] = lp[c];
+            b_node[nxt][e] = nd;
+            b_last[nxt][e] = c;
+            b_par[nxt][e] = b_node[cur][i];
+            b_lpc[nxt][e] = lp[c];
+          }
+          b_pb[nxt][e] = cpb[k];
+          b_pnb[nxt][e] = cpnb[k];
+        }
+        run += __popcll(em);
       }
       __syncthreads();
       if (lane == 0) {
-        s_nodes = nodes0 + __popcll(em);
+        s_nodes = nodes0 + run;
         s_nb = nsel;
       }
     }
@@ -571,21 +591,23 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
   }
   // ---- final ranking and back-tracking (one lane per returned path)
   const int nb = s_nb;
-  if (lane < nb) score[lane] = beam_lse(b_pb[cur][lane], b_pnb[cur][lane]);
+#pragma unroll
+  for (int q = 0; q < EPL; ++q)
+    if (lane + 64 * q < nb) score[lane + 64 * q] = beam_lse(b_pb[cur][lane + 64 * q], b_pnb[cur][lane + 64 * q]);
   __syncthreads();
-  if (lane < nb) {
+  for (int e = lane; e < nb; e += 64) {
     int rank = 0;
-    const float s0 = score[lane];
-    const int key0 = (b_last[cur][lane] + 1) * 4096 + lane;
+    const float s0 = score[e];
+    const int key0 = (b_last[cur][e] + 1) * 4096 + e;
     for (int i = 0; i < nb; ++i)
-      if (i != lane && beam_better(score[i], (b_last[cur][i] + 1) * 4096 + i, s0, key0)) ++rank;
+      if (i != e && beam_better(score[i], (b_last[cur][i] + 1) * 4096 + i, s0, key0)) ++rank;
     if (rank < top_paths) {
       int len = 0;
-      for (int nd = b_node[cur][lane]; nd > 0; nd = par[nd]) ++len;
+      for (int nd = b_node[cur][e]; nd > 0; nd = par[nd]) ++len;
       int* ids = out_ids + ((int64_t)n * top_paths + rank) * t_max;
       int* tsp = out_ts + ((int64_t)n * top_paths + rank) * t_max;
       int pos = len;
-      for (int nd = b_node[cur][lane]; nd > 0; nd = par[nd]) {
+      for (int nd = b_node[cur][e]; nd > 0; nd = par[nd]) {
         --pos;
         ids[pos] = chr[nd];
         tsp[pos] = tst[nd];
@@ -818,8 +840,8 @@ ds2_status_t ds2_ctc_beam_decode(const float* probs, int n, int t_max, int c, in
   if (n < 0 || t_max < 0 || c < 1 || blank < 0 || blank >= c || beam_width < 1 ||
       top_paths < 1 || top_paths > beam_width || cutoff_top_n < 1)
     return DS2_INVALID_VALUE;
-  if (c > BEAM_CMAX || beam_width > BEAM_MAX || (int64_t)beam_width * c > 4096)
-    return DS2_UNSUPPORTED_SHAPE;
+  const bool small = c <= BEAM_SMALL_C && beam_width <= BEAM_SMALL;
+  if (!small && (c > BEAM_LARGE_C || beam_width > BEAM_LARGE)) return DS2_UNSUPPORTED_SHAPE;
   if (n == 0) return DS2_OK;
   if (ws == nullptr || ws_bytes < ds2_ctc_beam_workspace_size(n, t_max, beam_width))
     return DS2_WORKSPACE_TOO_SMALL;
@@ -830,7 +852,8 @@ ds2_status_t ds2_ctc_beam_decode(const float* probs, int n, int t_max, int c, in
   int* chr = reinterpret_cast<int*>(w + plane);
   int* tst = reinterpret_cast<int*>(w + 2 * plane);
   float* lpc = reinterpret_cast<float*>(w + 3 * plane);
-  hipLaunchKernelGGL(ctc_beam_kernel, dim3(n), dim3(64), 0, as_stream(stream), probs, t_max, c,
+  auto kern = small ? ctc_beam_kernel<BEAM_SMALL, BEAM_SMALL_C> : ctc_beam_kernel<BEAM_LARGE, BEAM_LARGE_C>;
+  hipLaunchKernelGGL(kern, dim3(n), dim3(64), 0, as_stream(stream), probs, t_max, c,
                      stride_n, stride_t, sizes, blank, beam_width, cutoff_top_n, cutoff_prob,
                      top_paths, par, chr, tst, lpc, cap, out_ids, out_offsets, out_lens,
                      out_scores);

@@ -30,6 +30,9 @@ _PROTOS = {
                                  _c_int, _vp, _c_int, _vp, _sz, _vp]),
     "ds2_stft_logmag_masked": (_c_int, [_vp, _vp, _c_int, _c_int, _c_int, _c_int, _vp, _c_int,
                                         _vp, _c_int, _vp, _vp, _c_int, _vp, _sz, _vp]),
+    "ds2_wave_aug_workspace_size": (_sz, [_c_int, _c_i64]),
+    "ds2_wave_aug": (_c_int, [_vp, _c_i64, _vp, _c_int, _vp, _vp, _c_int, _vp, _c_i64, _vp,
+                              _c_i64, _vp, _c_i64, _vp, _vp, _sz, _vp]),
     "ds2_sgemm": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _c_f, _vp, _c_i64, _c_i64,
                            _vp, _c_i64, _c_i64, _c_f, _vp, _c_i64, _c_i64, _c_int, _vp, _vp]),
     "ds2_sgemm_workspace_size": (_sz, [_c_int, _c_int, _c_int, _c_int]),

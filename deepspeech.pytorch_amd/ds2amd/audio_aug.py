@@ -1,0 +1,256 @@
+"""Waveform augmentations — drop-in for the reference ``data/audio_aug.py`` on the
+device front-end.
+
+The transforms keep the reference's class names, constructor arguments, call
+signature (``t(wav=..., sr=...) -> {'wav': ..., 'sr': ...}``) and — the part that
+decides which augmentation an utterance gets — its exact sequence of ``random`` /
+``np.random`` draws.  What they do not do is touch the samples: each one appends a
+record to the :class:`Wave` it is handed, and :func:`apply_waves` replays the
+records of a whole batch in one HIP launch (``ds2_wave_aug``) straight into the
+device PCM buffer the STFT kernel reads.
+
+* ``Shift`` (audio_aug.py:26-44), ``AudioDistort`` (:47-60, ``clip`` :177-178),
+  ``AddNoise`` (:78-107, incl. ``get_stacked_noise`` :110-134): built.
+* ``ChangeAudioSpeed`` (:7-23) and ``PitchShift`` (:63-75) wrap librosa's phase
+  vocoder / resampler, which are absent here: their draws are made in the reference
+  order, and applying them raises ``NotImplementedError``.
+* ``Compose`` / ``OneOf`` / ``OneOrOther`` (:137-174): same semantics, including
+  ``OneOf`` setting the chosen transform's ``prob`` to 1 for good (:160).
+"""
+from __future__ import annotations
+
+import random
+from typing import List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import ops
+
+SHIFT, DISTORT, NOISE = 1, 2, 3
+MAX_DURATION_AUG = 10          # seconds (data_loader_aug.py:49)
+
+
+class Wave(object):
+    """An utterance on its way through the transforms: the loaded fp32 samples plus
+    the records of what the transforms decided.  ``shape`` follows the length the
+    reference's array would have, so the transforms' length checks read the same."""
+
+    def __init__(self, samples):
+        self.samples = np.ascontiguousarray(np.asarray(samples, dtype=np.float32).reshape(-1))
+        self.length = int(self.samples.shape[0])
+        self.records = []      # (kind, a, b, alpha, noise float64 slice or None)
+
+    @property
+    def shape(self):
+        return (self.length,)
+
+    def record(self, kind, a=0, b=0, alpha=0.0, noise=None):
+        self.records.append((kind, int(a), int(b), float(alpha), noise))
+
+
+def _as_wave(wav) -> Wave:
+    return wav if isinstance(wav, Wave) else Wave(wav)
+
+
+class ChangeAudioSpeed:
+    def __init__(self, limit=0.15, prob=0.5, max_duration=10, sr=16000):
+        self.limit = limit
+        self.prob = prob
+        self.max_duration = max_duration * sr
+
+    def __call__(self, wav=None, sr=None):
+        wav = _as_wave(wav)
+        assert len(wav.shape) == 1
+        if random.random() < self.prob:
+            alpha = 1.0 + self.limit * random.uniform(-1, 1)
+            raise NotImplementedError(
+                f"ChangeAudioSpeed (librosa.effects.time_stretch, rate {alpha:.4f}) is not "
+                "available on the ds2amd device front-end (librosa is absent)")
+        return {'wav': wav, 'sr': sr}
+
+
+class Shift:
+    def __init__(self, limit=512, prob=0.5, max_duration=10, sr=16000):
+        self.limit = int(limit)
+        self.prob = prob
+        self.max_duration = max_duration * sr
+
+    def __call__(self, wav=None, sr=None):
+        wav = _as_wave(wav)
+        assert len(wav.shape) == 1
+        if random.random() < self.prob:
+            limit = self.limit
+            shift = round(random.uniform(0, limit))
+            if wav.length + limit < self.max_duration:
+                wav.record(SHIFT, shift, limit)
+                wav.length += limit
+        return {'wav': wav, 'sr': sr}
+
+
+class AudioDistort:
+    def __init__(self, limit=0.3, prob=0.5):
+        self.limit = limit
+        self.prob = prob
+
+    def __call__(self, wav=None, sr=None):
+        wav = _as_wave(wav)
+        if random.random() < self.prob:
+            alpha = 1.0 + self.limit * random.uniform(-1, 1)
+            # float32 numpy math in the reference: f32(alpha) * wav, clipped to [0, max(wav)]
+            wav.record(DISTORT, alpha=float(np.float32(alpha)))
+        return {'wav': wav, 'sr': sr}
+
+
+class PitchShift:
+    def __init__(self, limit=5, prob=0.5):
+        self.limit = abs(limit)
+        self.prob = prob
+
+    def __call__(self, wav=None, sr=22050):
+        wav = _as_wave(wav)
+        assert len(wav.shape) == 1
+        if random.random() < self.prob:
+            alpha = self.limit * random.uniform(-1, 1)
+            raise NotImplementedError(
+                f"PitchShift (librosa.effects.pitch_shift, {alpha:.3f} half-steps) is not "
+                "available on the ds2amd device front-end (librosa is absent)")
+        return {'wav': wav, 'sr': sr}
+
+
+def get_stacked_noise(noise_path=None, wav=None, sr=16000):
+    """audio_aug.py:110-134.  The reference reads one noise file; when it is shorter than
+    the utterance its next iteration np.stack-s two 1-D arrays and fails its own
+    ``assert len(noise.shape)==1`` — restated as that AssertionError."""
+    from .data_loader import load_audio_norm
+    noise, sample_rate = load_audio_norm(noise_path)
+    assert len(noise.shape) == 1
+    if sample_rate != sr:
+        raise NotImplementedError("get_stacked_noise: resampling noise needs librosa (absent)")
+    if noise.shape[0] > wav.shape[0]:
+        return noise
+    assert False, "get_stacked_noise: noise shorter than the utterance (reference :123-128)"
+
+
+class AddNoise:
+    def __init__(self, limit=0.2, prob=0.5, noise_samples=[]):
+        self.limit = abs(limit)
+        self.prob = prob
+        self.noise_samples = noise_samples
+
+    def __call__(self, wav=None, sr=None):
+        wav = _as_wave(wav)
+        assert len(wav.shape) == 1
+        for i in range(0, 2):
+            if random.random() < self.prob:
+                if i == 0:
+                    _noise = get_stacked_noise(noise_path=random.sample(self.noise_samples, k=1)[0],
+                                               wav=wav, sr=sr)
+                    if _noise.shape[0] < wav.shape[0]:
+                        return {'wav': wav, 'sr': sr}
+                else:
+                    _noise = np.random.normal(0, 1, wav.shape[0] * 2)
+                alpha = self.limit * random.uniform(0, 1)
+                pos = random.randint(0, _noise.shape[0] - wav.shape[0])
+                seg = np.ascontiguousarray(_noise[pos:pos + wav.shape[0]], dtype=np.float64)
+                wav.record(NOISE, alpha=alpha, noise=seg)
+        return {'wav': wav, 'sr': sr}
+
+
+class Compose(object):
+    def __init__(self, transforms, p=1.):
+        self.transforms = [t for t in transforms if t is not None]
+        self.p = p
+
+    def __call__(self, **data):
+        if np.random.random() < self.p:
+            for t in self.transforms:
+                data = t(**data)
+        return data
+
+
+class OneOf(object):
+    def __init__(self, transforms, prob=.5):
+        self.transforms = transforms
+        self.p = prob
+        transforms_ps = [t.prob for t in transforms]
+        s = sum(transforms_ps)
+        self.transforms_ps = [t / s for t in transforms_ps]
+
+    def __call__(self, **data):
+        if np.random.random() < self.p:
+            t = np.random.choice(self.transforms, p=self.transforms_ps)
+            t.prob = 1.
+            data = t(**data)
+        return data
+
+
+class OneOrOther(object):
+    def __init__(self, first, second, prob=.5):
+        self.first = first
+        first.prob = 1.
+        self.second = second
+        second.pprob = 1.     # sic (audio_aug.py:170): the second transform keeps its prob
+        self.p = prob
+
+    def __call__(self, **data):
+        return self.first(**data) if np.random.random() < self.p else self.second(**data)
+
+
+def build_audio_augs(audio_conf, noise_samples: Sequence[str] = (), max_duration=None):
+    """The aug_type 0 pipeline of SpectrogramDataset (data_loader_aug.py:355-418):
+    OneOf([AddNoise, ChangeAudioSpeed, AudioDistort, Shift, PitchShift]) at
+    ``noise_prob``; None when noise_prob <= 0."""
+    aug_prob = audio_conf.get('noise_prob') or 0
+    if aug_prob <= 0:
+        return None
+    sr = audio_conf.get('sample_rate')
+    md = max_duration if max_duration is not None else MAX_DURATION_AUG
+    return OneOf([
+        AddNoise(limit=0.2, prob=aug_prob, noise_samples=list(noise_samples)),
+        ChangeAudioSpeed(limit=0.15, prob=aug_prob, sr=sr, max_duration=md),
+        AudioDistort(limit=0.05, prob=aug_prob),
+        Shift(limit=sr * 0.5, prob=aug_prob, sr=sr, max_duration=md),
+        PitchShift(limit=2, prob=aug_prob),
+    ], prob=aug_prob)
+
+
+def apply_waves(waves: Sequence[Wave], device) -> tuple:
+    """Replay the records of a batch on the device: -> (pcm [N, S_max] fp32 device,
+    lengths list).  One ds2_wave_aug launch; the input is uploaded once."""
+    waves = [_as_wave(w) for w in waves]
+    n = len(waves)
+    s_in = max(w.samples.shape[0] for w in waves)
+    k = max(1, max(len(w.records) for w in waves))
+    pcm = np.zeros((n, max(s_in, 1)), dtype=np.float32)
+    op_i = np.zeros((n, k, 4), dtype=np.int32)
+    op_f = np.zeros((n, k), dtype=np.float64)
+    rows: List[np.ndarray] = []
+    cap = 1
+    for b, w in enumerate(waves):
+        pcm[b, :w.samples.shape[0]] = w.samples
+        ln = w.samples.shape[0]
+        cap = max(cap, ln)
+        for j, (kind, a, bb, alpha, nz) in enumerate(w.records):
+            if kind == SHIFT:
+                ln += bb
+            elif kind == NOISE:
+                a = len(rows)
+                rows.append(nz)
+            op_i[b, j] = (kind, a, bb, 0)
+            op_f[b, j] = alpha
+            cap = max(cap, ln)
+        assert ln == w.length
+    lens = [w.length for w in waves]
+    noise = None
+    if rows:
+        nl = max(r.shape[0] for r in rows)
+        nz = np.zeros((len(rows), nl), dtype=np.float64)
+        for r, seg in enumerate(rows):
+            nz[r, :seg.shape[0]] = seg
+        noise = torch.from_numpy(nz).to(device)
+    out = ops.wave_aug(torch.from_numpy(pcm).to(device),
+                       torch.tensor([w.samples.shape[0] for w in waves], dtype=torch.int32).to(device),
+                       torch.from_numpy(op_i).to(device), torch.from_numpy(op_f).to(device), noise,
+                       lens, max(lens), cap)
+    return out, lens

@@ -13,6 +13,8 @@ reference ``data/data_loader.py`` / ``data/data_loader_aug.py``.
 from __future__ import annotations
 
 import math
+import random
+from glob import glob
 from typing import List, Sequence
 
 import numpy as np
@@ -21,7 +23,16 @@ from torch.utils.data import DataLoader
 from torch.utils.data.sampler import Sampler
 
 from . import ops
+from .audio_aug import Wave, apply_waves, build_audio_augs
 from .spect_aug import SpectAugmenter
+
+# tempo classes of the reference's legacy sox path (data_loader_aug.py:108-112); only the
+# draws they cause are kept (the sox branch itself is dead code there, :690-697)
+TEMPOS = {
+    0: ('1.0', (1.0, 1.0)),
+    1: ('0.9', (0.85, 0.95)),
+    2: ('1.1', (1.05, 1.15))
+}
 
 
 def hamming(n: int) -> np.ndarray:
@@ -69,6 +80,23 @@ def load_audio_norm(path, channel=-1):
     return sound, sample_rate
 
 
+def load_randomly_augmented_audio(path, sample_rate=16000, tempo_range=(0.85, 1.15),
+                                  gain_range=(-10, 10), channel=-1, transforms=None):
+    """data_loader_aug.py:679-699 (+ augment_audio_with_augs :660-676): the tempo and gain
+    draws the reference makes (and no longer uses), the normalised wav, then the
+    transforms' records.  -> (audio_aug.Wave, sample_rate)."""
+    np.random.uniform(low=tempo_range[0], high=tempo_range[1])
+    np.random.uniform(low=gain_range[0], high=gain_range[1])
+    y, sr = load_audio_norm(path, channel=channel)
+    if sr != sample_rate:
+        raise NotImplementedError(f"{path}: {sr} Hz audio needs librosa.resample to {sample_rate} "
+                                  "Hz (librosa is absent)")
+    wav = Wave(y)
+    if transforms is not None:
+        wav = transforms(**{'wav': wav, 'sr': sample_rate})['wav']
+    return wav, sample_rate
+
+
 class SpectrogramParser(object):
     def __init__(self, audio_conf, cache_path=None, normalize=False, augment=False, channel=-1,
                  device=None):
@@ -85,6 +113,10 @@ class SpectrogramParser(object):
         # spectrogram augmentations (data_loader_aug.py:241-248), drawn on the host and
         # applied inside the STFT kernel; inactive unless audio_conf enables them
         self.spect_aug = SpectAugmenter(audio_conf)
+        # waveform augmentations (data_loader_aug.py:361-418, aug_type 0), drawn on the
+        # host and replayed on the device (ds2_wave_aug); None unless noise_prob > 0
+        noise_dir = audio_conf.get('noise_dir')
+        self.augs = build_audio_augs(audio_conf, sorted(glob(noise_dir)) if noise_dir else ())
 
     def _consts(self, sample_rate):
         key = sample_rate
@@ -104,16 +136,20 @@ class SpectrogramParser(object):
         raise NotImplementedError(f"normalize={self.normalize!r} is not on the ds2amd hot path "
                                   "(reference default is 'max_frame', train.py:75)")
 
-    def parse_batch(self, signals: Sequence[np.ndarray], sample_rate=None):
-        """Raw PCM list -> (spect [N,1,F,T_max] on device, frames int32 [N])."""
+    def parse_batch(self, signals: Sequence, sample_rate=None):
+        """Raw PCM list (numpy arrays, or audio_aug.Wave records of augmented utterances)
+        -> (spect [N,1,F,T_max] on device, frames int32 [N])."""
         sr = sample_rate or self.sample_rate
         n_fft, hop, win, taps = self._consts(sr)
-        lens = [len(s) for s in signals]
-        max_s = max(lens)
-        pcm = np.zeros((len(signals), max_s), dtype=np.float32)
-        for i, s in enumerate(signals):
-            pcm[i, :len(s)] = s
-        pcm_d = torch.from_numpy(pcm).to(self.device)
+        if any(isinstance(s, Wave) for s in signals):
+            pcm_d, lens = apply_waves(signals, self.device)
+        else:
+            lens = [len(s) for s in signals]
+            max_s = max(lens)
+            pcm = np.zeros((len(signals), max_s), dtype=np.float32)
+            for i, s in enumerate(signals):
+                pcm[i, :len(s)] = s
+            pcm_d = torch.from_numpy(pcm).to(self.device)
         ns_d = torch.tensor(lens, dtype=torch.int32).to(self.device)
         frames = [1 + n // hop for n in lens]
         masks = self.spect_aug.masks(ops.SPECT_ROWS, frames, self.device)
@@ -128,12 +164,20 @@ class SpectrogramParser(object):
         return out.unsqueeze(1), torch.tensor(frames, dtype=torch.int32)
 
     def audio_to_stft(self, y, sample_rate):
-        """Single utterance -> normalised spectrogram [F, T] (device tensor)."""
-        spect, _ = self.parse_batch([np.asarray(y, dtype=np.float32)], sample_rate)
+        """Single utterance (PCM or audio_aug.Wave) -> normalised spectrogram [F, T]
+        (device tensor)."""
+        if not isinstance(y, Wave):
+            y = np.asarray(y, dtype=np.float32)
+        spect, _ = self.parse_batch([y], sample_rate)
         return spect[0, 0]
 
     def parse_audio(self, audio_path):
-        y, sr = load_audio_norm(audio_path, channel=self.channel)
+        """data_loader_aug.py:163-215 with the reference's draws: tempo class (augment
+        only), the two unused sox draws, then the waveform augs (self.augs)."""
+        tempo_id = random.randrange(3) if self.augment else 0
+        y, sr = load_randomly_augmented_audio(audio_path, self.sample_rate, channel=self.channel,
+                                              tempo_range=TEMPOS[tempo_id][1],
+                                              transforms=self.augs)
         return self.audio_to_stft(y, sr)
 
     def parse_audio_for_transcription(self, audio_path):

@@ -71,8 +71,12 @@ class BeamCTCDecoder(Decoder):
         if lm_path is not None:
             raise NotImplementedError("ds2amd.BeamCTCDecoder: KenLM language-model scoring is "
                                       "not supported (lm_path must be None)")
-        if beam_width > 32:
-            raise ValueError("ds2amd.BeamCTCDecoder: beam_width <= 32")
+        # the device search keeps every candidate in one wave's registers:
+        # beam_width <= 128 over <= 32 labels (the reference default 100 over 29), or
+        # beam_width <= 32 over <= 64 labels
+        if beam_width > (128 if len(labels) <= 32 else 32) or len(labels) > 64:
+            raise ValueError("ds2amd.BeamCTCDecoder: beam_width <= 128 with <= 32 labels, "
+                             "or beam_width <= 32 with <= 64 labels")
         self.beam_width = int(beam_width)
         self.cutoff_top_n = int(cutoff_top_n)
         self.cutoff_prob = float(cutoff_prob)

@@ -327,6 +327,32 @@ def ctc_beam_decode_raw(probs: torch.Tensor, sizes: Optional[torch.Tensor], beam
     return ids, offs, lens, scores
 
 
+def wave_aug(pcm: torch.Tensor, in_lens: torch.Tensor, op_i: torch.Tensor, op_f: torch.Tensor,
+             noise: Optional[torch.Tensor], out_lens, out_stride: int, cap: int) -> torch.Tensor:
+    """Replay host-drawn waveform-augmentation records on the device (ds2_wave_aug).
+    pcm [N, S] fp32, in_lens int32 [N], op_i int32 [N, K, 4], op_f float64 [N, K],
+    noise float64 [R, L] or None -> [N, out_stride] fp32 zero padded."""
+    pcm = _need(pcm, "wave_aug.pcm")
+    in_lens = _need(in_lens, "wave_aug.in_lens", _I32)
+    op_i = _need(op_i, "wave_aug.op_i", _I32)
+    op_f = _need(op_f, "wave_aug.op_f", torch.float64)
+    n, k = op_i.shape[0], op_i.shape[1]
+    dev = pcm.device
+    if noise is not None:
+        noise = _need(noise, "wave_aug.noise", torch.float64)
+    out_lens = _need(torch.as_tensor(out_lens, dtype=_I32).to(dev), "wave_aug.out_lens", _I32)
+    out = torch.empty(n, out_stride, device=dev, dtype=_F32)
+    err = torch.zeros(1, device=dev, dtype=_I32)
+    ws = _ws(_lib.size("ds2_wave_aug_workspace_size", n, cap), dev)
+    _lib.call("ds2_wave_aug", pcm.data_ptr(), pcm.stride(0), in_lens.data_ptr(), n, op_i.data_ptr(),
+              op_f.data_ptr(), k, _p(noise), 0 if noise is None else noise.stride(0),
+              out.data_ptr(), out_stride, out_lens.data_ptr(), cap, err.data_ptr(), ws.data_ptr(),
+              ws.numel(), _stream())
+    if int(err.item()) != 0:
+        raise _lib.Ds2Error(f"ds2_wave_aug: inconsistent op records (err {int(err.item())})")
+    return out
+
+
 SPECT_ROWS = 161   # rows of every spectrogram the reference returns (data_loader_aug.py:234-249)
 
 

@@ -70,6 +70,22 @@ ds2_status_t ds2_stft_logmag_masked(const float* pcm, const int* n_samples, int 
                                     const int* masks, float* out, int max_frames, void* ws,
                                     size_t ws_bytes, ds2_stream_t stream);
 
+/* Waveform augmentations before the STFT: replays per-utterance op records drawn on the
+ * host by ds2amd/audio_aug.py in the reference's `random` / `np.random` order —
+ * Shift (data/audio_aug.py:26-44), AudioDistort (:47-60,177-178), AddNoise (:78-107).
+ * in: [n][in_stride] fp32 PCM with in_lens; op_i [n][max_ops][4] = {kind, a, b, 0}
+ * (kind 0 end, 1 shift (a = shift, b = limit), 2 distort, 3 noise (a = noise row)),
+ * op_f [n][max_ops] = alpha; noise [rows][noise_stride] float64 slices; out:
+ * [n][out_stride] zero padded, out_lens = the lengths the host expects (mismatch, a bad
+ * record or cap too small sets *err).  cap = the longest intermediate length.  Replaces
+ * the numpy arithmetic of load_randomly_augmented_audio (data_loader_aug.py:660-699). */
+size_t ds2_wave_aug_workspace_size(int n, int64_t cap);
+ds2_status_t ds2_wave_aug(const float* in, int64_t in_stride, const int* in_lens, int n,
+                          const int* op_i, const double* op_f, int max_ops, const double* noise,
+                          int64_t noise_stride, float* out, int64_t out_stride,
+                          const int* out_lens, int64_t cap, int* err, void* ws, size_t ws_bytes,
+                          ds2_stream_t stream);
+
 /* ------------------------------------------------------------------------ */
 /* Dense fp32 GEMM on MFMA (v_mfma_f32_16x16x4_f32 / 32x32x2_f32), strided-batched, row-major.
  * C[b] = alpha * op(A[b]) @ op(B[b]) + beta * C[b] (+ bias[n] if bias != NULL)
@@ -283,7 +299,8 @@ ds2_status_t ds2_greedy_decode(const float* probs, int n, int t_max, int c, int6
  * prefixes (best first): out_ids / out_offsets [n][top_paths][t_max] (char ids and
  * the frame of each char), out_lens [n][top_paths], out_scores [n][top_paths]
  * (log prob).  cutoff_top_n / cutoff_prob prune the vocabulary per frame as
- * ctcdecode does.  beam_width <= 32, c <= 64.                                  */
+ * ctcdecode does.  beam_width <= 32 with c <= 64, or beam_width <= 128 with
+ * c <= 32 (the reference default beam_width = 100 over its 29 labels).        */
 /* Batched CER / WER edit distances (data/utils.py:47-57 get_cer_wer, decoder.py
  * Decoder.cer / .wer) over id sequences: a = decoded ids [n][a_stride] with a_lens,
  * b = reference ids flat with b_offsets / b_lens.  out[4*i .. 4*i+3] = {word

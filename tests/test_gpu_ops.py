@@ -785,13 +785,16 @@ def _beam_check(dev, probs, sizes, beam, top_n=40, cutoff=1.0):
             assert abs(float(scores[n, p]) - s) <= 1e-5 * max(1.0, abs(s)), (n, p)
 
 
-@pytest.mark.parametrize("beam,top_n,cutoff", [(8, 40, 1.0), (4, 5, 1.0), (6, 40, 0.95),
-                                               (1, 40, 1.0)])
-def test_ctc_beam_vs_oracle(dev, beam, top_n, cutoff):
+@pytest.mark.parametrize("beam,top_n,cutoff,c", [(8, 40, 1.0, 30), (4, 5, 1.0, 30),
+                                                 (6, 40, 0.95, 30), (1, 40, 1.0, 30),
+                                                 (100, 40, 1.0, 29), (128, 40, 1.0, 32),
+                                                 (100, 10, 0.99, 29), (33, 40, 1.0, 29)])
+def test_ctc_beam_vs_oracle(dev, beam, top_n, cutoff, c):
     """ds2_ctc_beam_decode == oracle/ctc_beam.py (prefix beam search, no LM): ids, char
-    frames and lengths bit-exact for every returned beam, scores to 1e-5 rel."""
+    frames and lengths bit-exact for every returned beam, scores to 1e-5 rel.  Beams
+    above 32 (the reference default is 100, decoder.py:89) take the 128-entry kernel."""
     g = np.random.default_rng(beam * 10 + top_n)
-    n, t, c = 5, 37, 30
+    n, t = 5, 37
     logits = g.standard_normal((n, t, c)).astype(np.float32) * 3
     logits[:, :, 0] += 1.5                                  # blank-heavy, like a trained model
     probs = np.exp(logits - logits.max(-1, keepdims=True))
@@ -807,6 +810,21 @@ def test_ctc_beam_hand_case_and_decoder(dev):
     strings, offsets = dec.decode(torch.from_numpy(probs).to(dev), torch.IntTensor([2]))
     assert strings == [["a", ""]]
     assert offsets[0][0].tolist() == [0]
+    # the reference's constructor defaults (beam_width=100) over its own 29 labels
+    dec = BeamCTCDecoder(orc.LABELS)
+    assert dec.beam_width == 100
+    g = np.random.default_rng(5)
+    logits = g.standard_normal((2, 25, len(orc.LABELS))).astype(np.float32) * 3
+    logits[:, :, 0] += 1.5
+    p = np.exp(logits - logits.max(-1, keepdims=True))
+    p = (p / p.sum(-1, keepdims=True)).astype(np.float32)
+    strings, _ = dec.decode(torch.from_numpy(p).to(dev), torch.IntTensor([25, 17]))
+    from oracle import ctc_beam
+    ref = ctc_beam.beam_decode(p, [25, 17], 100, cutoff_top_n=40, cutoff_prob=1.0)
+    for n, paths in enumerate(ref):
+        assert len(strings[n]) == 100
+        for q, (_, rid, _) in enumerate(paths):
+            assert strings[n][q] == ''.join(orc.LABELS[i] for i in rid), (n, q)
 
 
 # ---------------------------------------------------------------------------- CER / WER
