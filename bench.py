@@ -34,6 +34,18 @@ BATCH, T_FRAMES, SECONDS, HIDDEN, LAYERS, LABEL_LEN = 32, 1001, 10.0, 800, 5, 15
 # fp32 algorithmic work per training step at this shape (BASELINE.md §3 / SURVEY §8d)
 TRAIN_FLOP_PER_STEP = 4.940e12
 PEAK_F32_MFMA_TFLOPS = 157.3     # MI355X dense fp32 (MI355X_MICROARCH.md)
+# fp32 GEMMs run as bf16x6 split products on the bf16 matrix cores (gemm.hip sxgemm2_kernel,
+# fp32-accurate): their peak is the dense bf16 MFMA peak (16 x fp32) / 6 products
+PEAK_BF16_MFMA_TFLOPS = 16 * PEAK_F32_MFMA_TFLOPS
+PEAK_X6_TFLOPS = PEAK_BF16_MFMA_TFLOPS / 6
+
+
+def gemm_peak():
+    """(peak TFLOP/s, arithmetic) of ds2_sgemm_ws as configured (DS2_GEMM_X6=0: fp32 MFMA)."""
+    if os.environ.get("DS2_GEMM_X6", "1")[:1] == "0":
+        return PEAK_F32_MFMA_TFLOPS, "fp32 MFMA (v_mfma_f32_16x16x4_f32)"
+    return PEAK_X6_TFLOPS, ("fp32 operands split into 3 bf16 terms, 6 products on "
+                            "v_mfma_f32_32x32x16_bf16, fp32 accumulation (bf16 dense peak / 6)")
 
 
 def synthetic_batch(rank: int):
@@ -92,7 +104,7 @@ class KernelProbe:
         return sum(ms) / len(ms), sum(self.flops) / len(self.flops), len(ms)
 
 
-def pmc_traffic_per_launch(prefix="sgemm", extra=("splitk_reduce_kernel",)):
+def pmc_traffic_per_launch(prefix="gemm", extra=("splitk_reduce_kernel",)):
     """HBM bytes per ds2_sgemm_ws launch from the newest committed PMC summary
     (profiles/r*_pmc_traffic.csv, made by scripts/pmc_traffic.sh + pmc_summary.py:
     FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE, one pass per counter)."""
@@ -315,10 +327,11 @@ def main():
         if pk is not None:
             avg_ms, flop, count = pk
             achieved = flop / (avg_ms * 1e-3) / 1e12
+            peak, arith = gemm_peak()
             roof = {"bound": "mfma", "kernel": args.probe, "launches": count,
                     "avg_launch_ms": round(avg_ms, 5), "achieved": round(achieved, 3),
-                    "peak": PEAK_F32_MFMA_TFLOPS, "unit": "TFLOP/s",
-                    "frac": round(achieved / PEAK_F32_MFMA_TFLOPS, 4),
+                    "peak": round(peak, 1), "unit": "TFLOP/s", "arith": arith,
+                    "frac": round(achieved / peak, 4),
                     "traffic": None if traffic is None else round(traffic),
                     "traffic_unit": "bytes/launch (HBM, PMC)", "traffic_source": traffic_src,
                     "step_achieved_tflops": round(TRAIN_FLOP_PER_STEP / (ms_per_step * 1e-3) / 1e12, 3)}

@@ -100,7 +100,8 @@ __device__ __forceinline__ void store_tile(float* __restrict__ s, const float (&
 __device__ __forceinline__ void decode_work(int M, int N, int K, int main_wgs, int tail_tile0,
                                             int tail_tiles, int nsplit, int kchunk,
                                             float* partial, int& m0, int& n0, int& kbeg,
-                                            int& kend, int& bz, float*& part, int bn = BN) {
+                                            int& kend, int& bz, float*& part, int bn = BN,
+                                            int bm = BM) {
   const int tn = (N + bn - 1) / bn;
   const int orig = blockIdx.x;
   int tile, z = 0;
@@ -118,7 +119,7 @@ __device__ __forceinline__ void decode_work(int M, int N, int K, int main_wgs, i
     z = pidx / tail_tiles;
     const int lt = pidx - z * tail_tiles;
     tile = tail_tile0 + lt;
-    if (nsplit > 1) part = partial + ((int64_t)z * tail_tiles + lt) * (BM * bn);
+    if (nsplit > 1) part = partial + ((int64_t)z * tail_tiles + lt) * (bm * bn);
   }
   const int tile_m = tile / tn;
   const int tile_n = tile - tile_m * tn;
@@ -127,7 +128,7 @@ __device__ __forceinline__ void decode_work(int M, int N, int K, int main_wgs, i
   const int sp = z - bz * nsplit;
   kbeg = orig < main_wgs ? 0 : sp * kchunk;
   kend = orig < main_wgs ? K : min(K, kbeg + kchunk);
-  m0 = tile_m * BM;
+  m0 = tile_m * bm;
   n0 = tile_n * bn;
 }
 
@@ -626,12 +627,480 @@ __global__ __launch_bounds__(256, 2) void sbgemm_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// fp32 GEMM on the bf16 matrix cores at fp32 accuracy (default for float4-staged operands;
+// DS2_GEMM_X6=0 selects sgemm64_kernel).  Every fp32 operand value x is split while it is
+// staged into three bf16 terms, hi = bf16(x), mid = bf16(x - hi), lo = bf16(x - hi - mid)
+// (round to nearest even; x = hi + mid + lo to 2^-26 |x|), and a product a.b is formed on
+// v_mfma_f32_16x16x32_bf16 from the six terms that carry fp32 weight,
+//   mid.mid + lo.hi + hi.lo + mid.hi + hi.mid + hi.hi       (small terms first)
+// (dropped: mid.lo, lo.mid, lo.lo, each below 2^-25 |a b|).  Each bf16 product is exact
+// in the fp32 accumulator, so the result carries fp32 rounding only: six 16-cycle bf16
+// MFMAs per 32 k replace eight 32-cycle fp32 MFMAs (2.7x fewer matrix cycles; the fp32-
+// equivalent peak is the dense bf16 peak / 6 = 419 TF).  The same split and products
+// run the GRU recurrences (gru_split.hip).
+//   tile 128 x 128, stages of 32 k, 4 waves of 4 x 4 16x16 tiles, two workgroups per CU;
+//   LDS: per operand three bf16 planes [128 rows][32 k] (64-B rows, 16-B slot s of row r
+//   at s ^ ((r >> 2) & 3): conflict-free ds_read_b128 fragments and stores);
+//   k-contiguous source: a thread unit = (row, 8-k slot), two float4 loads;
+//   row-contiguous source: a thread = one row x 16 k, 16 dword loads (consecutive threads
+//   read consecutive rows), so the transposed stores need no register shuffles.
+constexpr int XS = 32;                  // k per stage
+constexpr int XPLANE = BM * XS;         // bf16 per plane (BM = 128 rows)
+
+__device__ __forceinline__ int xslot(int row, int s) { return row * XS + 8 * (s ^ ((row >> 2) & 3)); }
+
+template <bool KC>
+__device__ __forceinline__ void xload_stage(__amdgpu_buffer_rsrc_t rs, int ld, int rows, int kend,
+                                            int r0, int k0, float (&v)[16]) {
+  constexpr int kOob = 0x7ffffff0;
+  const int t = threadIdx.x;
+  if (KC) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int u = t + 256 * (q >> 1);
+      const int r = r0 + (u >> 2);
+      const int k = k0 + 8 * (u & 3) + 4 * (q & 1);
+      const int off = (r < rows && k < kend) ? (r * ld + k) * 4 : kOob;
+      const f32x4 x = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+#pragma unroll
+      for (int c = 0; c < 4; ++c) v[4 * q + c] = x[c];
+    }
+  } else {
+    const int r = r0 + (t & (BM - 1));
+    const int kb = k0 + 16 * (t >> 7);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int k = kb + j;
+      const int off = (r < rows && k < kend) ? (k * ld + r) * 4 : kOob;
+      v[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0));
+    }
+  }
+}
+
+// 8 fp32 -> hi / mid / lo bf16x8, stored into the three planes at one slot
+__device__ __forceinline__ void xsplit_store(unsigned short* __restrict__ s, int at, const float* v) {
+  bf16x8 h, m, l;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const __bf16 a = (__bf16)v[j];
+    const float r1 = v[j] - (float)a;
+    const __bf16 b = (__bf16)r1;
+    h[j] = a;
+    m[j] = b;
+    l[j] = (__bf16)(r1 - (float)b);
+  }
+  *reinterpret_cast<bf16x8*>(s + at) = h;
+  *reinterpret_cast<bf16x8*>(s + XPLANE + at) = m;
+  *reinterpret_cast<bf16x8*>(s + 2 * XPLANE + at) = l;
+}
+
+template <bool KC>
+__device__ __forceinline__ void xstore_stage(unsigned short* __restrict__ s, const float (&v)[16]) {
+  const int t = threadIdx.x;
+  if (KC) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int u = t + 256 * i;
+      xsplit_store(s, xslot(u >> 2, u & 3), v + 8 * i);
+    }
+  } else {
+    const int r = t & (BM - 1);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) xsplit_store(s, xslot(r, 2 * (t >> 7) + i), v + 8 * i);
+  }
+}
+
+template <int TA, int TB>
+__global__ __launch_bounds__(256, 2) void sxgemm_kernel(
+    int M, int N, int K, float alpha, const float* __restrict__ A, int64_t lda, int64_t sA,
+    const float* __restrict__ B, int64_t ldb, int64_t sB, float beta, float* __restrict__ C,
+    int64_t ldc, int64_t sC, const float* __restrict__ bias, int main_wgs, int tail_tile0,
+    int tail_tiles, int nsplit, int kchunk, float* __restrict__ partial) {
+  constexpr bool AK = (TA == 0);
+  constexpr bool BKc = (TB == 1);
+  constexpr int TBN = 128;
+  __shared__ __attribute__((aligned(16))) unsigned short As[3 * XPLANE];
+  __shared__ __attribute__((aligned(16))) unsigned short Bs[3 * XPLANE];
+
+  int m0, n0, kbeg, kend, bz;
+  float* part;
+  decode_work(M, N, K, main_wgs, tail_tile0, tail_tiles, nsplit, kchunk, partial, m0, n0, kbeg,
+              kend, bz, part, TBN);
+  A += bz * sA;
+  B += bz * sB;
+  C += bz * sC;
+  const int a_rows = AK ? M : K, b_rows = BKc ? N : K;
+  const __amdgpu_buffer_rsrc_t a_rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(A), (short)0, static_cast<int>(a_rows * lda * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t b_rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(B), (short)0, static_cast<int>(b_rows * ldb * 4), 0x00020000);
+  const int ilda = static_cast<int>(lda), ildb = static_cast<int>(ldb);
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int wm = (wave >> 1) * 64;
+  const int wn = (wave & 1) * 64;
+  const int fr = lane & 15, fq = lane >> 4;
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  float ra[16], rb[16];
+  const int ktiles = (kend - kbeg + XS - 1) / XS;
+  xload_stage<AK>(a_rs, ilda, M, kend, m0, kbeg, ra);
+  xload_stage<BKc>(b_rs, ildb, N, kend, n0, kbeg, rb);
+  for (int kt = 0; kt < ktiles; ++kt) {
+    xstore_stage<AK>(As, ra);
+    xstore_stage<BKc>(Bs, rb);
+    __syncthreads();
+    if (kt + 1 < ktiles) {   // next stage's global loads fly during this stage's MFMAs
+      xload_stage<AK>(a_rs, ilda, M, kend, m0, kbeg + (kt + 1) * XS, ra);
+      xload_stage<BKc>(b_rs, ildb, N, kend, n0, kbeg + (kt + 1) * XS, rb);
+    }
+    bf16x8 ah[4], am[4], al[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int at = xslot(wm + 16 * i + fr, fq);
+      ah[i] = *reinterpret_cast<const bf16x8*>(As + at);
+      am[i] = *reinterpret_cast<const bf16x8*>(As + XPLANE + at);
+      al[i] = *reinterpret_cast<const bf16x8*>(As + 2 * XPLANE + at);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int bt = xslot(wn + 16 * j + fr, fq);
+      const bf16x8 bh = *reinterpret_cast<const bf16x8*>(Bs + bt);
+      const bf16x8 bm = *reinterpret_cast<const bf16x8*>(Bs + XPLANE + bt);
+      const bf16x8 bl = *reinterpret_cast<const bf16x8*>(Bs + 2 * XPLANE + bt);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        f32x4 c = acc[i][j];
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am[i], bm, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], bh, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bl, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am[i], bh, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bm, c, 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bh, c, 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+
+  // epilogue (16x16 C/D map: col = lane & 15, row = 4 * (lane >> 4) + r), as sgemm64_kernel
+  const int lc = lane & 15;
+  const int lr = 4 * (lane >> 4);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int cl = wn + 16 * j + lc;
+      if (part != nullptr) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) part[(wm + 16 * i + lr + r) * TBN + cl] = acc[i][j][r];
+        continue;
+      }
+      const int col = n0 + cl;
+      if (col >= N) continue;
+      const float bv = bias != nullptr ? bias[col] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wm + 16 * i + lr + r;
+        if (row < M) {
+          float* cp = C + (int64_t)row * ldc + col;
+          float v = alpha * acc[i][j][r] + bv;
+          if (beta != 0.f) v += beta * *cp;
+          *cp = v;
+        }
+      }
+    }
+  }
+}
+
+// The default bf16x6 kernel: tile 256 x 128, eight waves (two per SIMD) of 2 x 2 32x32
+// tiles on v_mfma_f32_32x32x16_bf16 (which holds the SIMD's vector issue for 8 of its 32
+// cycles, half the share of the 16x16x32 form), ONE workgroup per CU with two LDS stages
+// (2 x 72 KB).  Stage kt + 1 is split and stored into the other buffer in the same basic
+// block as stage kt's MFMAs, and sched_group_barrier interleaves the split's VALU work with
+// the MFMAs (three VALU per MFMA), so it issues in the MFMAs' shadow instead of in a phase
+// of its own; one barrier per stage; stage kt + 2's global loads are issued behind it.
+// Per-thread staging as sxgemm_kernel: k-contiguous units of (row, 8-k slot), or one row x
+// (8 or 16) k of a row-contiguous operand (consecutive threads on consecutive rows).
+constexpr int X2M = 256;                 // tile rows
+constexpr int X2T = 512;                 // threads
+constexpr int X2_AP = X2M * XS;          // bf16 per A plane
+constexpr int X2_BP = 128 * XS;          // bf16 per B plane
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
+
+template <bool KC, int ROWS>
+struct X2Op {
+  static constexpr int F = ROWS * XS / X2T;   // floats per thread per stage (16 or 8)
+  static constexpr int SL = F / 8;            // 8-k slots per thread
+  static constexpr int P = ROWS * XS;         // bf16 per plane
+};
+
+// One stage of an operand into registers.  The lane-dependent part of every offset is
+// loop-invariant (voff: the lane's row, kOob for a row past the operand) and the
+// k-dependent part is wave-uniform (the scalar offset), so a load costs no VALU work.
+// KCHK: some stage may end inside [k0, k0 + 32) (K or the split chunk not a multiple of 32):
+// values at k >= kend are zeroed.  Loads past the operand's end read as zero (buffer range).
+template <bool KC, int ROWS, bool KCHK>
+__device__ __forceinline__ void x2_load(__amdgpu_buffer_rsrc_t rs, int ld, int voff, int kend,
+                                        int k0, float (&v)[X2Op<KC, ROWS>::F]) {
+  using O = X2Op<KC, ROWS>;
+  const int t = threadIdx.x;
+  if (KC) {
+    // voff = (row * ld + 8 (t & 3)) * 4; units t + 512 u lie 128 rows apart
+#pragma unroll
+    for (int u = 0; u < O::SL; ++u) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int so = (k0 + 4 * h + u * (X2T / 4) * ld) * 4;
+        const f32x4 x = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, so, 0));
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const bool ok = !KCHK || k0 + 8 * (t & 3) + 4 * h + c < kend;
+          v[8 * u + 4 * h + c] = ok ? x[c] : 0.f;
+        }
+      }
+    }
+  } else {
+    // voff = row * 4; this wave's k run starts at k0 + F (t / ROWS) (wave-uniform)
+    const int kb = k0 + O::F * __builtin_amdgcn_readfirstlane(t / ROWS);
+#pragma unroll
+    for (int j = 0; j < O::F; ++j) {
+      const float x = __builtin_bit_cast(
+          float, __builtin_amdgcn_raw_buffer_load_b32(rs, voff, (kb + j) * ld * 4, 0));
+      v[j] = (!KCHK || kb + j < kend) ? x : 0.f;
+    }
+  }
+}
+
+// two fp32 -> (hi, mid, lo) bf16 pairs: v_cvt_pk_bf16_f32 (RNE), exact residuals
+__device__ __forceinline__ void x2_split2(float x0, float x1, unsigned& h, unsigned& m,
+                                          unsigned& l) {
+  h = __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2{x0, x1}, bf16x2));
+  const float r0 = x0 - __builtin_bit_cast(float, h << 16);
+  const float r1 = x1 - __builtin_bit_cast(float, h & 0xffff0000u);
+  m = __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2{r0, r1}, bf16x2));
+  const float l0 = r0 - __builtin_bit_cast(float, m << 16);
+  const float l1 = r1 - __builtin_bit_cast(float, m & 0xffff0000u);
+  l = __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2{l0, l1}, bf16x2));
+}
+
+__device__ __forceinline__ void x2_split_store(unsigned short* __restrict__ s, int plane, int at,
+                                               const float* v) {
+  u32x4v h, m, l;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    unsigned a, b, c;
+    x2_split2(v[2 * j], v[2 * j + 1], a, b, c);
+    h[j] = a;
+    m[j] = b;
+    l[j] = c;
+  }
+  *reinterpret_cast<u32x4v*>(s + at) = h;
+  *reinterpret_cast<u32x4v*>(s + plane + at) = m;
+  *reinterpret_cast<u32x4v*>(s + 2 * plane + at) = l;
+}
+
+template <bool KC, int ROWS>
+__device__ __forceinline__ void x2_store(unsigned short* __restrict__ s,
+                                         const float (&v)[X2Op<KC, ROWS>::F]) {
+  using O = X2Op<KC, ROWS>;
+  const int t = threadIdx.x;
+  if (KC) {
+#pragma unroll
+    for (int u = 0; u < O::SL; ++u) {
+      const int unit = t + X2T * u;
+      x2_split_store(s, O::P, xslot(unit >> 2, unit & 3), v + 8 * u);
+    }
+  } else {
+    const int r = t % ROWS;
+#pragma unroll
+    for (int u = 0; u < O::SL; ++u) x2_split_store(s, O::P, xslot(r, O::SL * (t / ROWS) + u), v + 8 * u);
+  }
+}
+
+// c += a.b to fp32 accuracy on the 32x32x16 form (small terms first)
+__device__ __forceinline__ void x2_mma6(const bf16x8 (&a)[3], const bf16x8 (&b)[3], f32x16& c) {
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[1], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[0], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[2], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[0], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[1], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], c, 0, 0, 0);
+}
+
+template <int TA, int TB, bool KCHK>
+__global__ __launch_bounds__(X2T, 1) void sxgemm2_kernel(
+    int M, int N, int K, float alpha, const float* __restrict__ A, int64_t lda, int64_t sA,
+    const float* __restrict__ B, int64_t ldb, int64_t sB, float beta, float* __restrict__ C,
+    int64_t ldc, int64_t sC, const float* __restrict__ bias, int main_wgs, int tail_tile0,
+    int tail_tiles, int nsplit, int kchunk, float* __restrict__ partial) {
+  constexpr bool AK = (TA == 0);
+  constexpr bool BKc = (TB == 1);
+  constexpr int TBN = 128;
+  using OA = X2Op<AK, X2M>;
+  using OB = X2Op<BKc, TBN>;
+  __shared__ __attribute__((aligned(16))) unsigned short As[2][3 * X2_AP];
+  __shared__ __attribute__((aligned(16))) unsigned short Bs[2][3 * X2_BP];
+
+  int m0, n0, kbeg, kend, bz;
+  float* part;
+  decode_work(M, N, K, main_wgs, tail_tile0, tail_tiles, nsplit, kchunk, partial, m0, n0, kbeg,
+              kend, bz, part, TBN, X2M);
+  A += bz * sA;
+  B += bz * sB;
+  C += bz * sC;
+  const int a_rows = AK ? M : K, b_rows = BKc ? N : K;
+  const __amdgpu_buffer_rsrc_t a_rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(A), (short)0, static_cast<int>(a_rows * lda * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t b_rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(B), (short)0, static_cast<int>(b_rows * ldb * 4), 0x00020000);
+  const int ilda = static_cast<int>(lda), ildb = static_cast<int>(ldb);
+  const int t = threadIdx.x;
+  const int lane = t & 63;
+  const int wave = t >> 6;
+  const int wm = (wave >> 1) * 64;
+  const int wn = (wave & 1) * 64;
+  const int fr = lane & 31, fk = lane >> 5;
+  // loop-invariant lane offsets of the staging loads (kOob: a row past the operand); a
+  // k-contiguous A unit 1 lies 128 rows below unit 0 and is checked on its own
+  constexpr int kOob = 0x7ffffff0;
+  int a_voff, b_voff;
+  bool a_ok1 = true;
+  if (AK) {
+    const int r = m0 + (t >> 2);
+    a_voff = r < M ? (r * ilda + 8 * (t & 3)) * 4 : kOob;
+    a_ok1 = r + X2T / 4 < M;
+  } else {
+    const int r = m0 + (t % X2M);
+    a_voff = r < M ? r * 4 : kOob;
+  }
+  if (BKc) {
+    const int r = n0 + (t >> 2);
+    b_voff = r < N ? (r * ildb + 8 * (t & 3)) * 4 : kOob;
+  } else {
+    const int r = n0 + (t % TBN);
+    b_voff = r < N ? r * 4 : kOob;
+  }
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  // two register sets: stage kt + 2's loads are issued at the top of stage kt (a whole
+  // stage of latency) while the split of stage kt + 1 reads the other set
+  float ra0[OA::F], rb0[OB::F], ra1[OA::F], rb1[OB::F];
+  auto load = [&](int k0, float (&va)[OA::F], float (&vb)[OB::F]) {
+    x2_load<AK, X2M, KCHK>(a_rs, ilda, a_voff, kend, k0, va);
+    if (AK && !a_ok1) {   // unit 1 (rows + 128) past M
+#pragma unroll
+      for (int c = 8; c < 16; ++c) va[c] = 0.f;
+    }
+    x2_load<BKc, TBN, KCHK>(b_rs, ildb, b_voff, kend, k0, vb);
+  };
+  auto body = [&](int kt, int cur, float (&la)[OA::F], float (&lb)[OB::F],
+                  const float (&sa)[OA::F], const float (&sb)[OB::F]) {
+    // stage kt visible; every wave is done reading the other buffer (stage kt - 1)
+    __syncthreads();
+    load(kbeg + (kt + 2) * XS, la, lb);          // stages past kend load as zeros
+    const unsigned short* as = As[cur];
+    const unsigned short* bs = Bs[cur];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 af[2][3], bfr[2][3];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int at = xslot(wm + 32 * i + fr, 2 * ks + fk);
+#pragma unroll
+        for (int p = 0; p < 3; ++p) af[i][p] = *reinterpret_cast<const bf16x8*>(as + p * X2_AP + at);
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int bt = xslot(wn + 32 * j + fr, 2 * ks + fk);
+#pragma unroll
+        for (int p = 0; p < 3; ++p) bfr[j][p] = *reinterpret_cast<const bf16x8*>(bs + p * X2_BP + bt);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) x2_mma6(af[i], bfr[j], acc[i][j]);
+    }
+    // stage kt + 1 -> the other buffer (a stage past the end writes zeros nobody reads)
+    x2_store<AK, X2M>(As[cur ^ 1], sa);
+    x2_store<BKc, TBN>(Bs[cur ^ 1], sb);
+    // schedule: the loads, the first k-step's fragments, then each MFMA followed by up to
+    // three VALU (the split of the next stage), the second k-step's fragments early, the
+    // LDS stores of the split spread over the second half
+    __builtin_amdgcn_sched_group_barrier(0x020, 24, 0);
+    __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);
+#pragma unroll
+    for (int q = 0; q < 24; ++q) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+      if (q == 8) __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);
+    }
+#pragma unroll
+    for (int q = 0; q < 24; ++q) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+      if (q % 3 == 2) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+    }
+  };
+  const int ktiles = (kend - kbeg + XS - 1) / XS;
+  load(kbeg, ra0, rb0);
+  x2_store<AK, X2M>(As[0], ra0);
+  x2_store<BKc, TBN>(Bs[0], rb0);
+  load(kbeg + XS, ra1, rb1);
+  for (int kt = 0; kt < ktiles; kt += 2) {
+    body(kt, 0, ra0, rb0, ra1, rb1);
+    if (kt + 1 < ktiles) body(kt + 1, 1, ra1, rb1, ra0, rb0);
+  }
+
+  // epilogue (32x32 C/D map: col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5))
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int cl = wn + 32 * j + (lane & 31);
+      if (part != nullptr) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          part[(wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * fk) * TBN + cl] = acc[i][j][r];
+        continue;
+      }
+      const int col = n0 + cl;
+      if (col >= N) continue;
+      const float bv = bias != nullptr ? bias[col] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * fk;
+        if (row < M) {
+          float* cp = C + (int64_t)row * ldc + col;
+          float v = alpha * acc[i][j][r] + bv;
+          if (beta != 0.f) v += beta * *cp;
+          *cp = v;
+        }
+      }
+    }
+  }
+}
+
 // Tail tiles: C[b] = alpha * sum_s partial[b][s][tile] + beta * C[b] + bias (fixed order)
 __global__ void splitk_reduce_kernel(const float* __restrict__ partial, int M, int N, int nsplit,
                                      int batch, int tail_tile0, int tail_tiles, float alpha,
                                      float beta, float* __restrict__ C, int64_t ldc, int64_t sC,
-                                     const float* __restrict__ bias, int bn) {
-  const int TE = BM * bn;
+                                     const float* __restrict__ bias, int bn, int bm) {
+  const int TE = bm * bn;
   const int tn = (N + bn - 1) / bn;
   const int64_t total = (int64_t)batch * tail_tiles * TE;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
@@ -641,7 +1110,7 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ partial, int M, i
     const int lt = static_cast<int>(bt % tail_tiles);
     const int b = static_cast<int>(bt / tail_tiles);
     const int tile = tail_tile0 + lt;
-    const int row = (tile / tn) * BM + e / bn;
+    const int row = (tile / tn) * bm + e / bn;
     const int col = (tile % tn) * bn + e % bn;
     if (row >= M || col >= N) continue;
     float acc = 0.f;
@@ -715,11 +1184,19 @@ static int device_cus() {
 // 768 + 90 tail tiles x 8 splits; the weight gradient 2400 x 800 (133 tiles, K = 16032)
 // becomes 133 tiles x 5 splits.  Split partials are reduced in a fixed order.
 struct GemmPlan {
-  int main_wgs, tail_tile0, tail_tiles, nsplit, kchunk, bn;
+  int main_wgs, tail_tile0, tail_tiles, nsplit, kchunk, bn, bm;
 };
 
 // the deep-K kernel (sgemm64_kernel) runs 2 workgroups per CU and BK = 64, the
 // original one 3 per CU and BK = 16
+// 0: fp32-MFMA kernels; 1 (default): bf16x6 256 x 128 kernel; 2: bf16x6 128 x 128 kernel
+static int x6_mode(bool va, bool vb) {
+  if (!va || !vb) return 0;
+  const char* e = getenv("DS2_GEMM_X6");
+  if (e == nullptr || e[0] == 0) return 1;
+  return e[0] == '0' ? 0 : (e[0] == '2' ? 2 : 1);
+}
+
 static bool use_k64(bool va, bool vb) {
   const char* e = getenv("DS2_GEMM64");
   return va && vb && !(e != nullptr && e[0] == '0');
@@ -742,9 +1219,9 @@ struct PlanChoice {
 };
 
 static PlanChoice plan_bn(int m, int n, int k, int batch, int bn, int slots, int bk,
-                          double eff) {
-  const int tiles = cdiv(m, BM) * cdiv(n, bn);
-  GemmPlan p{0, 0, tiles, 1, std::max(k, 1), bn};
+                          double eff, int bm = BM) {
+  const int tiles = cdiv(m, bm) * cdiv(n, bn);
+  GemmPlan p{0, 0, tiles, 1, std::max(k, 1), bn, bm};
   if (batch == 1) {
     p.main_wgs = (tiles / slots) * slots;
     p.tail_tile0 = p.main_wgs;
@@ -756,7 +1233,7 @@ static PlanChoice plan_bn(int m, int n, int k, int batch, int bn, int slots, int
     }
   }
   // seconds per unit (one k step of one BM x bn tile on one slot)
-  const double unit = 2.0 * BM * bn / (157.3e12 * eff / slots);
+  const double unit = 2.0 * bm * bn / (157.3e12 * eff / slots);
   const double main_t = (double)(p.main_wgs / slots) * k * unit;
   const int64_t tail = (int64_t)p.tail_tiles * batch;
   const int smax = std::max(1, std::min(32, k / 256));
@@ -768,7 +1245,7 @@ static PlanChoice plan_bn(int m, int n, int k, int batch, int bn, int slots, int
     if (s > 1 && ns != s) continue;
     const int64_t pieces = tail * ns;
     double t = (double)((pieces + slots - 1) / slots) * kc * unit;
-    if (ns > 1) t += (double)pieces * BM * bn * 8.0 / 4e12 + 6e-6;
+    if (ns > 1) t += (double)pieces * bm * bn * 8.0 / 4e12 + 6e-6;
     if (t < best - 1e-12) {
       best = t;
       bs = ns;
@@ -797,15 +1274,24 @@ static GemmPlan gemm_plan(int m, int n, int k, int batch, bool k64) {
 }
 
 static size_t plan_ws(const GemmPlan& p, int batch) {
-  return p.nsplit > 1 ? (size_t)p.nsplit * batch * p.tail_tiles * BM * p.bn * sizeof(float) + 256
+  return p.nsplit > 1 ? (size_t)p.nsplit * batch * p.tail_tiles * p.bm * p.bn * sizeof(float) + 256
                       : 0;
 }
 
-// large enough for either kernel's plan (the choice depends on operand alignment)
+// the bf16x6 kernels: 128-wide tiles, split-K in 32-k chunks; 256-row tiles one workgroup
+// per CU (mode 1) or 128-row tiles two per CU (mode 2)
+static GemmPlan x6_plan(int m, int n, int k, int batch, int mode) {
+  if (mode == 2) return plan_bn(m, n, k, batch, 128, 2 * device_cus(), XS, 1.0).p;
+  return plan_bn(m, n, k, batch, 128, device_cus(), XS, 1.0, X2M).p;
+}
+
+// large enough for any kernel's plan (the choice depends on operand alignment)
 extern "C" size_t ds2_sgemm_workspace_size(int m, int n, int k, int batch) {
   if (m <= 0 || n <= 0 || k <= 0 || batch <= 0) return 0;
-  return std::max(plan_ws(gemm_plan(m, n, k, batch, false), batch),
-                  plan_ws(gemm_plan(m, n, k, batch, true), batch));
+  return std::max(std::max(plan_ws(gemm_plan(m, n, k, batch, false), batch),
+                           plan_ws(gemm_plan(m, n, k, batch, true), batch)),
+                  std::max(plan_ws(x6_plan(m, n, k, batch, 1), batch),
+                           plan_ws(x6_plan(m, n, k, batch, 2), batch)));
 }
 
 extern "C" ds2_status_t ds2_sgemm_ws(int trans_a, int trans_b, int m, int n, int k, float alpha,
@@ -824,11 +1310,12 @@ extern "C" ds2_status_t ds2_sgemm_ws(int trans_a, int trans_b, int m, int n, int
                   (trans_a ? (m % 4 == 0) : (k % 4 == 0));
   const bool vb = aligned16(b) && (ldb % 4 == 0) && (stride_b % 4 == 0) &&
                   (trans_b ? (k % 4 == 0) : (n % 4 == 0));
-  const bool k64 = use_k64(va, vb) && fits_rsrc(trans_a ? k : m, lda) &&
-                   fits_rsrc(trans_b ? n : k, ldb);
+  const bool fits = fits_rsrc(trans_a ? k : m, lda) && fits_rsrc(trans_b ? n : k, ldb);
+  const int x6 = fits ? x6_mode(va, vb) : 0;
+  const bool k64 = x6 == 0 && use_k64(va, vb) && fits;
   const char* dbe = getenv("DS2_GEMM_DB");
   const bool db = dbe != nullptr && dbe[0] == '1';
-  GemmPlan p = gemm_plan(m, n, k, batch, k64);
+  GemmPlan p = x6 ? x6_plan(m, n, k, batch, x6) : gemm_plan(m, n, k, batch, k64);
   if (p.nsplit > 1 && (ws == nullptr || ws_bytes < plan_ws(p, batch))) {
     p.nsplit = 1;                       // no workspace: whole-K pieces
     p.kchunk = std::max(k, 1);
@@ -838,8 +1325,22 @@ extern "C" ds2_status_t ds2_sgemm_ws(int trans_a, int trans_b, int m, int n, int
   if (nwg > 0x7fffffff) return DS2_UNSUPPORTED_SHAPE;
   dim3 grid(static_cast<unsigned>(nwg));
   hipStream_t st = as_stream(stream);
+  // every stage of every piece lies wholly inside [0, K): no per-element k check
+  const bool kalign = k % XS == 0 && (p.nsplit == 1 || p.kchunk % XS == 0);
 #define DS2_G(TA_, TB_)                                                                       \
-  if (k64)                                                                                    \
+  if (x6 == 1 && kalign)                                                                      \
+    hipLaunchKernelGGL((sxgemm2_kernel<TA_, TB_, false>), grid, dim3(X2T), 0, st, m, n, k, alpha, \
+                       a, lda, stride_a, b, ldb, stride_b, beta, c, ldc, stride_c, bias,        \
+                       p.main_wgs, p.tail_tile0, p.tail_tiles, p.nsplit, p.kchunk, partial);   \
+  else if (x6 == 1)                                                                           \
+    hipLaunchKernelGGL((sxgemm2_kernel<TA_, TB_, true>), grid, dim3(X2T), 0, st, m, n, k, alpha,  \
+                       a, lda, stride_a, b, ldb, stride_b, beta, c, ldc, stride_c, bias,        \
+                       p.main_wgs, p.tail_tile0, p.tail_tiles, p.nsplit, p.kchunk, partial);   \
+  else if (x6 == 2)                                                                           \
+    hipLaunchKernelGGL((sxgemm_kernel<TA_, TB_>), grid, dim3(256), 0, st, m, n, k, alpha, a, lda, \
+                       stride_a, b, ldb, stride_b, beta, c, ldc, stride_c, bias, p.main_wgs,    \
+                       p.tail_tile0, p.tail_tiles, p.nsplit, p.kchunk, partial);               \
+  else if (k64)                                                                               \
     launch_k64<TA_, TB_>(p.bn, db, grid, st, m, n, k, alpha, a, lda, stride_a, b, ldb, stride_b, \
                          beta, c, ldc, stride_c, bias, p.main_wgs, p.tail_tile0, p.tail_tiles,  \
                          p.nsplit, p.kchunk, partial);                                         \
@@ -858,12 +1359,12 @@ extern "C" ds2_status_t ds2_sgemm_ws(int trans_a, int trans_b, int m, int n, int
   }
 #undef DS2_G
   if (p.nsplit > 1) {
-    const int64_t total = (int64_t)batch * p.tail_tiles * BM * p.bn;
+    const int64_t total = (int64_t)batch * p.tail_tiles * p.bm * p.bn;
     int g = cdiv(total, 256);
     if (g > 4096) g = 4096;
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3(g), dim3(256), 0, st, partial, m, n, p.nsplit,
                        batch, p.tail_tile0, p.tail_tiles, alpha, beta, c, ldc, stride_c, bias,
-                       p.bn);
+                       p.bn, p.bm);
   }
   return launch_status("ds2_sgemm");
 }
@@ -913,12 +1414,12 @@ extern "C" ds2_status_t ds2_sgemm_bf16_ws(int trans_a, int trans_b, int m, int n
   else DS2_B(1, 1);
 #undef DS2_B
   if (p.nsplit > 1) {
-    const int64_t total = (int64_t)batch * p.tail_tiles * BM * p.bn;
+    const int64_t total = (int64_t)batch * p.tail_tiles * p.bm * p.bn;
     int g = cdiv(total, 256);
     if (g > 4096) g = 4096;
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3(g), dim3(256), 0, st, partial, m, n, p.nsplit,
                        batch, p.tail_tile0, p.tail_tiles, alpha, beta, c, ldc, stride_c, bias,
-                       p.bn);
+                       p.bn, p.bm);
   }
   return launch_status("ds2_sgemm_bf16");
 }

@@ -23,10 +23,15 @@ def _close(got, ref, rel=1e-5, name=""):
 
 
 # ---------------------------------------------------------------------------- GEMM
+@pytest.mark.parametrize("x6", ["1", "0"])
 @pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
 @pytest.mark.parametrize("m,n,k", [(1, 1, 1), (37, 53, 29), (128, 128, 16), (300, 257, 513),
-                                   (515, 2400, 132), (257, 300, 5000)])   # last: split-K path
-def test_sgemm(dev, ta, tb, m, n, k):
+                                   (515, 2400, 132), (257, 300, 5000),   # split-K path
+                                   (300, 256, 516), (260, 132, 1000)])   # float4 staging, K % 32 != 0
+def test_sgemm(dev, ta, tb, m, n, k, x6, monkeypatch):
+    """ds2_sgemm_ws vs fp64 at 1e-5: the bf16x6 kernel (default for float4-staged operands)
+    and the fp32-MFMA kernels (DS2_GEMM_X6=0)."""
+    monkeypatch.setenv("DS2_GEMM_X6", x6)
     g = torch.Generator().manual_seed(m * 7 + n * 3 + k)
     a = torch.randn(k, m, generator=g) if ta else torch.randn(m, k, generator=g)
     b = torch.randn(n, k, generator=g) if tb else torch.randn(k, n, generator=g)
@@ -41,14 +46,16 @@ def test_sgemm(dev, ta, tb, m, n, k):
     _close(cd, ref, 1e-5, "sgemm")
 
 
-@pytest.mark.parametrize("mode", ["bk16", "128", "160", "db128", "db160"])
-@pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0)])
+@pytest.mark.parametrize("mode", ["bk16", "128", "160", "db128", "db160", "x6", "x6-128"])
+@pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
 def test_sgemm_full_rounds_plus_split_tail(dev, ta, tb, mode, monkeypatch):
     """Whole rounds of resident workgroups + a tail whose K range is split (one launch) and
-    reduced in a fixed order; alpha/beta/bias applied once.  Both kernels: BK = 16 /
-    32x32x2 (DS2_GEMM64=0) and BK = 64 / 16x16x4 with 128- and 160-wide tiles."""
+    reduced in a fixed order; alpha/beta/bias applied once.  fp32 kernels: BK = 16 /
+    32x32x2 (DS2_GEMM64=0) and BK = 64 / 16x16x4 with 128- and 160-wide tiles; bf16x6
+    kernels: 256 x 128 (default) and 128 x 128 (DS2_GEMM_X6=2)."""
+    monkeypatch.setenv("DS2_GEMM_X6", {"x6": "1", "x6-128": "2"}.get(mode, "0"))
     monkeypatch.setenv("DS2_GEMM64", "0" if mode == "bk16" else "1")
-    if mode != "bk16":
+    if mode in ("128", "160", "db128", "db160"):
         monkeypatch.setenv("DS2_GEMM_BN", mode[-3:])
         monkeypatch.setenv("DS2_GEMM_DB", "1" if mode.startswith("db") else "0")
     m, n, k = 128 * 29, 128 * 27 + 52, 2080
@@ -64,6 +71,27 @@ def test_sgemm_full_rounds_plus_split_tail(dev, ta, tb, mode, monkeypatch):
               lda=ad.shape[1], ldb=bd.shape[1], ldc=n, alpha=0.5, beta=0.25, bias=bias.to(dev))
     torch.cuda.synchronize()
     _close(cd, ref, 1e-5, "sgemm main+tail")
+
+
+@pytest.mark.parametrize("ta,tb,m,n,k", [(0, 1, 2048, 2400, 800), (0, 0, 2048, 800, 2400),
+                                         (1, 0, 2400, 800, 4096), (1, 0, 2400, 1312, 4096)])
+def test_sgemm_x6_is_fp32_accurate(dev, ta, tb, m, n, k, monkeypatch):
+    """The bf16x6 kernel's error against fp64 is no larger than the fp32-MFMA kernel's on the
+    step's GEMM shapes (rows cut to keep the test short): it is an fp32 GEMM, not a
+    reduced-precision one."""
+    g = torch.Generator().manual_seed(m + n + k)
+    a = (torch.randn(k, m, generator=g) if ta else torch.randn(m, k, generator=g)).to(dev)
+    b = (torch.randn(n, k, generator=g) if tb else torch.randn(k, n, generator=g)).to(dev)
+    ref = (a.t() if ta else a).double() @ (b.t() if tb else b).double()
+    scale = ref.abs().max().item()
+    errs = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("DS2_GEMM_X6", mode)
+        c = torch.empty(m, n, device=dev)
+        ops.sgemm(a, b, c, m=m, n=n, k=k, trans_a=bool(ta), trans_b=bool(tb), lda=a.shape[1],
+                  ldb=b.shape[1], ldc=n)
+        errs[mode] = (c.double() - ref).abs().max().item() / scale
+    assert errs["1"] <= 1.5 * errs["0"] and errs["1"] < 5e-6, errs
 
 
 @pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
