@@ -836,6 +836,312 @@ __global__ __launch_bounds__(256) void conv_wgrad_patch_kernel(const float* __re
   }
 }
 
+// ---------------------------------------------------------------------------
+// bf16x6 direct convolution (width stride 1), forward and dgrad, on the bf16 matrix cores at
+// fp32 accuracy: every fp32 operand value is split into hi / mid / lo bf16 terms and a
+// product is formed from the six terms that carry fp32 weight (gemm.hip sxgemm_kernel), on
+// v_mfma_f32_32x32x16_bf16: M = 32 output channels, N = 32 output columns, K = 16 taps.
+//
+// K order: tap rows a in runs of 8 (a-group g) x kernel columns b in pairs (p): lane half
+// h of the MFMA takes b = 2p + h and a = 8g .. 8g + 7, so its 8 k values are 8 consecutive
+// input ROWS of one input column -- contiguous in a column-major LDS patch (16-B aligned,
+// one ds_read_b128 per plane), and 8 consecutive a of one (m, b) in the weight image.
+// Taps past the kernel (a >= rows of taps, b >= kw) have zero weight.
+//   fwd  : out y[n][co][ho][wo], loop channels ci, input row ho*sh - ph + a, col wo - pw + b
+//   dgrad: out dx[n][ci][hi][wi] for hi of stride class q, loop channels co, taps of the
+//          class reversed (dy row (hi + ph - q)/sh - (A_q - 1) + a, col wi + pw - kw + 1 + b)
+// Workgroup: one output row x 256 columns x 32 output channels; 8 waves = 4 column
+// quarters (64 columns, 2 MFMA tiles) x 2 halves of the k-steps, whose partial sums meet in
+// LDS once at the end.  Per loop channel the input patch (KA rows x 256 + 2 NBP - 1
+// columns) is split and stored column-major (pitch P = 8 x odd bf16: conflict-free
+// fragment reads) and the channel's pre-split weight image [3][32][COP] is copied in; the
+// next channel's global loads fly during the MFMAs.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef cu32x4 u32x4;
+constexpr int CX_T = 512;
+constexpr int CX_COLS = 256;
+constexpr int CX_PATCH = 3 * 267 * 40;   // bf16: 3 planes x columns x pitch (max)
+constexpr int CX_WIMG = 3 * 32 * 296;    // bf16: 3 planes x 32 channels x COP (max)
+constexpr int CX_PU = 2;                 // patch staging units per thread
+constexpr int CX_WQ = 7;                 // 16-B weight-image chunks per thread
+
+struct CxGeom {
+  int KA;     // tap rows padded to 8
+  int NBP;    // kernel-column pairs
+  int P;      // patch column pitch (bf16)
+  int COP;    // weight-image channel pitch (bf16)
+  int PCOL;   // patch columns
+};
+
+__host__ __device__ inline int cx_pitch8odd(int v) {   // smallest 8 * odd >= v
+  int k = (v + 7) / 8;
+  if ((k & 1) == 0) ++k;
+  return 8 * k;
+}
+
+__host__ __device__ inline CxGeom cx_geom(const ConvDims& g, bool dgrad) {
+  CxGeom c;
+  const int a = dgrad ? class_taps(g, 0) : g.kh;
+  c.KA = (a + 7) / 8 * 8;
+  c.NBP = (g.kw + 1) / 2;
+  c.P = cx_pitch8odd(c.KA + 1);
+  c.COP = cx_pitch8odd(2 * c.NBP * c.KA + 1);
+  c.PCOL = CX_COLS + 2 * c.NBP - 1;
+  return c;
+}
+
+// split-weight image: [class][mb][loop channel][plane][32][COP] bf16
+template <bool DGRAD>
+__global__ void conv_x6_wimg_kernel(const float* __restrict__ w, ConvDims g, CxGeom c,
+                                    unsigned short* __restrict__ img) {
+  const int M = DGRAD ? g.ci : g.co;
+  const int L = DGRAD ? g.co : g.ci;
+  const int mbn = (M + 31) / 32;
+  const int classes = DGRAD ? g.sh : 1;
+  const int64_t per = (int64_t)32 * c.COP;             // one plane of one (class, mb, l)
+  const int64_t total = (int64_t)classes * mbn * L * per;
+  const int KHW = g.kh * g.kw;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t r = i;
+    const int e = static_cast<int>(r % per); r /= per;
+    const int l = static_cast<int>(r % L); r /= L;
+    const int mb = static_cast<int>(r % mbn); r /= mbn;
+    const int q = static_cast<int>(r);
+    const int mm = e / c.COP, rem = e - mm * c.COP;
+    const int b = rem / c.KA, a = rem - b * c.KA;
+    const int m = mb * 32 + mm;
+    float v = 0.f;
+    if (rem < 2 * c.NBP * c.KA && m < M && b < g.kw) {
+      if (!DGRAD) {
+        if (a < g.kh) v = w[((int64_t)m * g.ci + l) * KHW + a * g.kw + b];
+      } else {
+        const int aq = class_taps(g, q);
+        if (a < aq) v = w[((int64_t)l * g.ci + m) * KHW + (q + g.sh * (aq - 1 - a)) * g.kw + (g.kw - 1 - b)];
+      }
+    }
+    const __bf16 hb = (__bf16)v;
+    const float r1 = v - (float)hb;
+    const __bf16 mbf = (__bf16)r1;
+    const __bf16 lb = (__bf16)(r1 - (float)mbf);
+    const int64_t base = ((((int64_t)q * mbn + mb) * L + l) * 3) * per + e;
+    img[base] = __builtin_bit_cast(unsigned short, hb);
+    img[base + per] = __builtin_bit_cast(unsigned short, mbf);
+    img[base + 2 * per] = __builtin_bit_cast(unsigned short, lb);
+  }
+}
+
+// NGA, NBP > 0: compile-time a-groups / column pairs (fully unrolled k loop for the model's
+// conv2: fwd 3 x 6, dgrad 2 x 6); 0: read from c at run time
+template <bool DGRAD, int NGA, int NBP_>
+__global__ __launch_bounds__(CX_T, 1) void conv_x6_kernel(const float* __restrict__ in,
+                                                          const unsigned short* __restrict__ img,
+                                                          const float* __restrict__ bias,
+                                                          float* __restrict__ out, ConvDims g,
+                                                          const int* __restrict__ out_lens,
+                                                          CxGeom c, int gx, int gy) {
+  __shared__ __attribute__((aligned(16))) unsigned short ps[CX_PATCH];
+  __shared__ __attribute__((aligned(16))) unsigned short ws[CX_WIMG];
+  const int M = DGRAD ? g.ci : g.co;
+  const int L = DGRAD ? g.co : g.ci;
+  const int in_h = DGRAD ? g.ho : g.hi;
+  const int in_w = DGRAD ? g.wo : g.wi;
+  const int out_h = DGRAD ? g.hi : g.ho;
+  const int out_w = DGRAD ? g.wi : g.wo;
+  const int mbn = (M + 31) / 32;
+  int bx, by, bz;
+  xcd_tile(gx, gy, bx, by, bz);
+  const int n = bz / mbn;
+  const int mb = bz - n * mbn;
+  const int m0 = mb * 32;
+  const int c0 = bx * CX_COLS;
+  // output row and the first input row of its taps
+  int orow, prow0, q = 0, A;
+  if (!DGRAD) {
+    orow = by;
+    prow0 = orow * g.sh - g.ph;
+    A = g.kh;
+  } else {
+    int t = by, hq = 0;
+    for (q = 0; q < g.sh; ++q) {
+      hq = ((q - g.ph) % g.sh + g.sh) % g.sh;
+      const int cnt = hq < g.hi ? (g.hi - 1 - hq) / g.sh + 1 : 0;
+      if (t < cnt) break;
+      t -= cnt;
+    }
+    A = class_taps(g, q);
+    orow = hq + g.sh * t;
+    prow0 = (orow + g.ph - q) / g.sh - (A - 1);
+  }
+  const int pcol0 = DGRAD ? c0 + g.pw - g.kw + 1 : c0 - g.pw;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int cw = wave & 3, kk = wave >> 2;
+  const int plane_in = in_h * in_w;
+  const float* inn = in + (int64_t)n * L * plane_in;
+  const int PPL = c.PCOL * c.P;                // bf16 per patch plane
+  const int WPL = 32 * c.COP;                  // bf16 per weight plane
+  const int64_t wstride = (int64_t)3 * WPL;    // one loop channel's image
+  const unsigned short* wimg = img + ((int64_t)q * mbn + mb) * L * wstride;
+  const int ngr = NGA > 0 ? NGA : c.KA / 8;
+  const int nbp = NBP_ > 0 ? NBP_ : c.NBP;
+  const int units = c.PCOL * ngr;
+  const int wchunks = (int)(wstride / 8);
+
+  float rp[CX_PU][8];
+  u32x4 rw[CX_WQ];
+  auto load = [&](int l) {
+    const __amdgpu_buffer_rsrc_t rs = conv_rsrc(inn + (int64_t)l * plane_in, plane_in);
+#pragma unroll
+    for (int u = 0; u < CX_PU; ++u) {
+      const int unit = tid + CX_T * u;
+      const int j = unit / ngr, rg = unit - (unit / ngr) * ngr;
+      const int ic = pcol0 + j;
+      const bool cok = unit < units && ic >= 0 && ic < in_w;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int a = 8 * rg + i, ir = prow0 + a;
+        const bool ok = cok && a < A && ir >= 0 && ir < in_h;
+        rp[u][i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                 rs, ok ? (ir * in_w + ic) * 4 : 0x7ffffff0, 0, 0));
+      }
+    }
+    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<unsigned short*>(wimg + (int64_t)l * wstride), (short)0,
+        static_cast<int>(wstride * 2), 0x00020000);
+#pragma unroll
+    for (int r = 0; r < CX_WQ; ++r) {
+      const int i = tid + CX_T * r;
+      rw[r] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                            wr, i < wchunks ? i * 16 : 0x7ffffff0, 0, 0));
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int u = 0; u < CX_PU; ++u) {
+      const int unit = tid + CX_T * u;
+      if (unit < units) {
+        const int j = unit / ngr, rg = unit - (unit / ngr) * ngr;
+        u32x4 h, m, lo;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float x0 = rp[u][2 * e], x1 = rp[u][2 * e + 1];
+          const __bf16 h0 = (__bf16)x0, h1 = (__bf16)x1;
+          const float r0 = x0 - (float)h0, r1 = x1 - (float)h1;
+          const __bf16 m0_ = (__bf16)r0, m1_ = (__bf16)r1;
+          const __bf16 l0 = (__bf16)(r0 - (float)m0_), l1 = (__bf16)(r1 - (float)m1_);
+          h[e] = (unsigned)__builtin_bit_cast(unsigned short, h0) |
+                 ((unsigned)__builtin_bit_cast(unsigned short, h1) << 16);
+          m[e] = (unsigned)__builtin_bit_cast(unsigned short, m0_) |
+                 ((unsigned)__builtin_bit_cast(unsigned short, m1_) << 16);
+          lo[e] = (unsigned)__builtin_bit_cast(unsigned short, l0) |
+                  ((unsigned)__builtin_bit_cast(unsigned short, l1) << 16);
+        }
+        const int at = j * c.P + 8 * rg;
+        *reinterpret_cast<u32x4*>(ps + at) = h;
+        *reinterpret_cast<u32x4*>(ps + PPL + at) = m;
+        *reinterpret_cast<u32x4*>(ps + 2 * PPL + at) = lo;
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < CX_WQ; ++r) {
+      const int i = tid + CX_T * r;
+      if (i < wchunks) *reinterpret_cast<u32x4*>(ws + 8 * i) = rw[r];
+    }
+  };
+
+  f32x16 acc[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+  const int nks = ngr * nbp;
+  const int s_beg = kk == 0 ? 0 : (nks + 1) / 2;
+  const int s_end = kk == 0 ? (nks + 1) / 2 : nks;
+  const int fr = lane & 31, fh = lane >> 5;
+  const bool active = orow < out_h && c0 + 64 * cw < out_w;
+
+  load(0);
+  store();
+  __syncthreads();
+  for (int l = 0; l < L; ++l) {
+    if (l + 1 < L) load(l + 1);
+    if (active) {
+      auto kstep = [&](int st) {
+        const int ga = st / nbp, p = st - (st / nbp) * nbp;
+        const int b = 2 * p + fh;
+        bf16x8 af[3], bfr[2][3];
+        const int aw = fr * c.COP + b * c.KA + 8 * ga;
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) af[pl] = *reinterpret_cast<const bf16x8*>(ws + pl * WPL + aw);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int ap = (64 * cw + 32 * j + fr + b) * c.P + 8 * ga;
+#pragma unroll
+          for (int pl = 0; pl < 3; ++pl)
+            bfr[j][pl] = *reinterpret_cast<const bf16x8*>(ps + pl * PPL + ap);
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          f32x16 cc = acc[j];
+          cc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1], bfr[j][1], cc, 0, 0, 0);
+          cc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[2], bfr[j][0], cc, 0, 0, 0);
+          cc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bfr[j][2], cc, 0, 0, 0);
+          cc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1], bfr[j][0], cc, 0, 0, 0);
+          cc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bfr[j][1], cc, 0, 0, 0);
+          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bfr[j][0], cc, 0, 0, 0);
+        }
+      };
+      if (NGA > 0 && NBP_ > 0) {
+        constexpr int NK = NGA * NBP_, H0 = (NK + 1) / 2;
+        if (kk == 0) {
+#pragma unroll
+          for (int st = 0; st < H0; ++st) kstep(st);
+        } else {
+#pragma unroll
+          for (int st = H0; st < NK; ++st) kstep(st);
+        }
+      } else {
+        for (int st = s_beg; st < s_end; ++st) kstep(st);
+      }
+    }
+    __syncthreads();
+    if (l + 1 < L) {
+      store();
+      __syncthreads();
+    }
+  }
+  // the two k halves meet in LDS (the patch area): half 1 writes, half 0 adds (fixed order)
+  float* red = reinterpret_cast<float*>(ps);
+  if (kk == 1) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) red[((cw * 2 + j) * 16 + r) * 64 + lane] = acc[j][r];
+  }
+  __syncthreads();
+  if (kk == 1 || !active) return;
+  const int len = (!DGRAD && out_lens != nullptr) ? out_lens[n] : out_w;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int col = c0 + 64 * cw + 32 * j + fr;
+    if (col >= out_w) continue;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int m = m0 + (r & 3) + 8 * (r >> 2) + 4 * fh;
+      if (m < M) {
+        float v = acc[j][r] + red[((cw * 2 + j) * 16 + r) * 64 + lane];
+        if (!DGRAD) {
+          if (bias != nullptr) v += bias[m];
+          if (col >= len) v = 0.f;
+        }
+        out[(((int64_t)n * M + m) * out_h + orow) * out_w + col] = v;
+      }
+    }
+  }
+}
+
 static inline bool make_dims(ConvDims& g, int n, int c_in, int h_in, int w_in, int c_out, int kh,
                              int kw, int sh, int sw, int ph, int pw) {
   if (n < 0 || c_in < 1 || h_in < 1 || w_in < 1 || c_out < 1 || kh < 1 || kw < 1 || sh < 1 ||
@@ -864,6 +1170,55 @@ static size_t patch_ws_bytes(const ConvDims& g, bool dgrad) {
   const int L = dgrad ? g.co : g.ci;
   const int classes = dgrad ? g.sh : 1;
   return (size_t)classes * ((M + 31) / 32) * L * wimg_tile(wimg_tstride(g, dgrad)) * sizeof(float);
+}
+
+// the bf16x6 kernel covers width stride 1 with <= 24 tap rows, <= 12 kernel columns and
+// planes that fit 32-bit buffer offsets (DS2_CONV_X6=0 selects the fp32 patch kernel)
+static inline bool x6_ok(const ConvDims& g, bool dgrad) {
+  const char* e = getenv("DS2_CONV_X6");
+  if (e != nullptr && e[0] == '0') return false;
+  if (g.sw != 1 || g.kw < 1 || g.kw > 12) return false;
+  const CxGeom c = cx_geom(g, dgrad);
+  if (c.KA > 24 || 3 * c.PCOL * c.P > CX_PATCH || 3 * 32 * c.COP > CX_WIMG) return false;
+  if (c.PCOL * (c.KA / 8) > CX_PU * CX_T || 3 * 32 * c.COP / 8 > CX_WQ * CX_T) return false;
+  const int64_t plane = dgrad ? (int64_t)g.ho * g.wo : (int64_t)g.hi * g.wi;
+  return plane * 4 < (1ll << 31) - 64;
+}
+
+static size_t x6_ws_bytes(const ConvDims& g, bool dgrad) {
+  if (!x6_ok(g, dgrad)) return 0;
+  const CxGeom c = cx_geom(g, dgrad);
+  const int M = dgrad ? g.ci : g.co;
+  const int L = dgrad ? g.co : g.ci;
+  const int classes = dgrad ? g.sh : 1;
+  return (size_t)classes * ((M + 31) / 32) * L * 3 * 32 * c.COP * sizeof(unsigned short);
+}
+
+template <bool DGRAD>
+static ds2_status_t launch_x6(const float* in, const float* w, const float* bias, float* out,
+                              const ConvDims& g, const int* out_lens, void* ws, hipStream_t st) {
+  const CxGeom c = cx_geom(g, DGRAD);
+  unsigned short* img = static_cast<unsigned short*>(ws);
+  const int64_t total = (int64_t)x6_ws_bytes(g, DGRAD) / 6;   // elements of one plane set
+  hipLaunchKernelGGL(conv_x6_wimg_kernel<DGRAD>, dim3(cdiv(total, 256) > 2048 ? 2048 : cdiv(total, 256)),
+                     dim3(256), 0, st, w, g, c, img);
+  const int M = DGRAD ? g.ci : g.co;
+  const int gy = DGRAD ? g.hi : g.ho;
+  const int gx = cdiv(DGRAD ? g.wi : g.wo, CX_COLS);
+  const int64_t nwg = (int64_t)gx * gy * g.n * cdiv(M, 32);
+  if (nwg > 0x7fffffff) return DS2_UNSUPPORTED_SHAPE;
+  const dim3 grid(static_cast<unsigned>(nwg));
+  const int nga = c.KA / 8;
+  if (!DGRAD && nga == 3 && c.NBP == 6)
+    hipLaunchKernelGGL((conv_x6_kernel<DGRAD, 3, 6>), grid, dim3(CX_T), 0, st, in, img, bias, out, g,
+                       out_lens, c, gx, gy);
+  else if (DGRAD && nga == 2 && c.NBP == 6)
+    hipLaunchKernelGGL((conv_x6_kernel<DGRAD, 2, 6>), grid, dim3(CX_T), 0, st, in, img, bias, out, g,
+                       out_lens, c, gx, gy);
+  else
+    hipLaunchKernelGGL((conv_x6_kernel<DGRAD, 0, 0>), grid, dim3(CX_T), 0, st, in, img, bias, out, g,
+                       out_lens, c, gx, gy);
+  return launch_status(DGRAD ? "ds2_conv2d_dgrad" : "ds2_conv2d_fwd");
 }
 
 template <bool DGRAD>
@@ -937,7 +1292,9 @@ size_t ds2_conv2d_workspace_size(int n, int c_in, int h_in, int w_in, int c_out,
                                  int sh, int sw, int ph, int pw) {
   ConvDims g;
   if (!make_dims(g, n, c_in, h_in, w_in, c_out, kh, kw, sh, sw, ph, pw)) return 0;
-  const size_t a = patch_ws_bytes(g, false), b = patch_ws_bytes(g, true);
+  size_t a = patch_ws_bytes(g, false), b = patch_ws_bytes(g, true);
+  a = a > x6_ws_bytes(g, false) ? a : x6_ws_bytes(g, false);
+  b = b > x6_ws_bytes(g, true) ? b : x6_ws_bytes(g, true);
   return (a > b ? a : b) + 256;
 }
 
@@ -949,6 +1306,10 @@ ds2_status_t ds2_conv2d_fwd(const float* x, const float* w, const float* bias, f
   if (!make_dims(g, n, c_in, h_in, w_in, c_out, kh, kw, sh, sw, ph, pw)) return DS2_INVALID_VALUE;
   if (n == 0) return DS2_OK;
   if (g.ho > 65535) return DS2_UNSUPPORTED_SHAPE;
+  if (x6_ok(g, false)) {
+    if (ws == nullptr || ws_bytes < x6_ws_bytes(g, false)) return DS2_WORKSPACE_TOO_SMALL;
+    return launch_x6<false>(x, w, bias, y, g, out_lens, ws, as_stream(stream));
+  }
   if (patch_ok(g, false)) {
     if (ws == nullptr || ws_bytes < patch_ws_bytes(g, false)) return DS2_WORKSPACE_TOO_SMALL;
     return launch_patch<false>(x, w, bias, y, g, out_lens, ws, as_stream(stream));
@@ -965,6 +1326,10 @@ ds2_status_t ds2_conv2d_dgrad(const float* dy, const float* w, float* dx, int n,
   ConvDims g;
   if (!make_dims(g, n, c_in, h_in, w_in, c_out, kh, kw, sh, sw, ph, pw)) return DS2_INVALID_VALUE;
   if (n == 0) return DS2_OK;
+  if (x6_ok(g, true)) {
+    if (ws == nullptr || ws_bytes < x6_ws_bytes(g, true)) return DS2_WORKSPACE_TOO_SMALL;
+    return launch_x6<true>(dy, w, nullptr, dx, g, nullptr, ws, as_stream(stream));
+  }
   if (patch_ok(g, true)) {
     if (ws == nullptr || ws_bytes < patch_ws_bytes(g, true)) return DS2_WORKSPACE_TOO_SMALL;
     return launch_patch<true>(dy, w, nullptr, dx, g, nullptr, ws, as_stream(stream));

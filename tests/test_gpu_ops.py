@@ -145,8 +145,13 @@ CONVS = [  # (n, ci, h, w, co, kh, kw, sh, sw, ph, pw)
 ]
 
 
+@pytest.mark.parametrize("x6", ["1", "0"])
 @pytest.mark.parametrize("cfg", CONVS)
-def test_conv_fwd_bwd(dev, cfg):
+def test_conv_fwd_bwd(dev, cfg, x6, monkeypatch):
+    """conv fwd / dgrad / wgrad vs fp64 torch at 1e-5: the bf16x6 direct kernels (default
+    where they fit: width stride 1, <= 24 tap rows, <= 12 kernel columns) and the fp32
+    LDS-patch / implicit-GEMM kernels (DS2_CONV_X6=0)."""
+    monkeypatch.setenv("DS2_CONV_X6", x6)
     n, ci, h, w, co, kh, kw, sh, sw, ph, pw = cfg
     g = torch.Generator().manual_seed(sum(cfg))
     x = torch.randn(n, ci, h, w, generator=g, dtype=torch.float64)
@@ -172,6 +177,26 @@ def test_conv_fwd_bwd(dev, cfg):
     _close(dx, x.grad, 1e-5, "conv dgrad")
     _close(dw, wt.grad, 1e-5, "conv wgrad")
     _close(db, dy.sum((0, 2, 3)), 1e-5, "conv dbias")
+
+
+def test_conv_x6_is_fp32_accurate(dev, monkeypatch):
+    """On the model's conv2 (32 -> 32 channels, 21 x 11 taps, stride (2, 1)) the bf16x6
+    kernels' error against fp64 is no larger than the fp32 kernels' (fwd and dgrad)."""
+    n, ci, h, w, co, kh, kw, sh, sw, ph, pw = 2, 32, 81, 300, 32, 21, 11, 2, 1, 10, 5
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(n, ci, h, w, generator=g, dtype=torch.float64)
+    wt = torch.randn(co, ci, kh, kw, generator=g, dtype=torch.float64) * 0.1
+    y = F.conv2d(x, wt, None, stride=(sh, sw), padding=(ph, pw))
+    dy = torch.randn(y.shape, generator=g, dtype=torch.float64)
+    dxr = torch.nn.grad.conv2d_input(x.shape, wt, dy, stride=(sh, sw), padding=(ph, pw))
+    errs = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("DS2_CONV_X6", mode)
+        yd = ops.conv2d_fwd(x.float().to(dev), wt.float().to(dev), None, (sh, sw), (ph, pw))
+        dx = ops.conv2d_dgrad(dy.float().to(dev), wt.float().to(dev), x.shape, (sh, sw), (ph, pw))
+        errs[mode] = ((yd.double().cpu() - y).abs().max().item() / y.abs().max().item(),
+                      (dx.double().cpu() - dxr).abs().max().item() / dxr.abs().max().item())
+    assert errs["1"][0] <= 1.5 * errs["0"][0] and errs["1"][1] <= 1.5 * errs["0"][1], errs
 
 
 # ---------------------------------------------------------------------------- BN
