@@ -844,37 +844,45 @@ struct X2Op {
 
 // One stage of an operand into registers.  The lane-dependent part of every offset is
 // loop-invariant (voff: the lane's row, kOob for a row past the operand) and the
-// k-dependent part is wave-uniform (the scalar offset), so a load costs no VALU work.
-// KCHK: some stage may end inside [k0, k0 + 32) (K or the split chunk not a multiple of 32):
-// values at k >= kend are zeroed.  Loads past the operand's end read as zero (buffer range).
+// k-dependent part is wave-uniform (the scalar offset), so a load costs no VALU work.  The
+// buffer range check covers the vector offset only, never the scalar one, so a k past the
+// operand (the prefetch of a stage beyond the end) must not reach the address: such a scalar
+// offset is clamped to 0 (a real, unused element), and in KCHK mode a lane whose own k lies
+// past K gets kOob.  KCHK: some stage may end inside [k0, k0 + 32) (K or the split chunk not
+// a multiple of 32): values at k >= kend are zeroed.
 template <bool KC, int ROWS, bool KCHK>
-__device__ __forceinline__ void x2_load(__amdgpu_buffer_rsrc_t rs, int ld, int voff, int kend,
-                                        int k0, float (&v)[X2Op<KC, ROWS>::F]) {
+__device__ __forceinline__ void x2_load(__amdgpu_buffer_rsrc_t rs, int ld, const int (&voff)[2],
+                                        int K, int kend, int k0, float (&v)[X2Op<KC, ROWS>::F]) {
   using O = X2Op<KC, ROWS>;
+  constexpr int kOob = 0x7ffffff0;
   const int t = threadIdx.x;
   if (KC) {
-    // voff = (row * ld + 8 (t & 3)) * 4; units t + 512 u lie 128 rows apart
+    // voff[u] = (row_u * ld + 8 (t & 3)) * 4 of unit t + 512 u (rows 128 apart)
 #pragma unroll
     for (int u = 0; u < O::SL; ++u) {
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        const int so = (k0 + 4 * h + u * (X2T / 4) * ld) * 4;
-        const f32x4 x = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, so, 0));
+        const int kw = k0 + 4 * h;                       // wave-uniform part of k
+        const int so = kw < K ? kw * 4 : 0;
+        const int kl = kw + 8 * (t & 3);                 // this lane's first k
+        const int vo = (KCHK && kl >= K) ? kOob : voff[u];
+        const f32x4 x = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, vo, so, 0));
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
-          const bool ok = !KCHK || k0 + 8 * (t & 3) + 4 * h + c < kend;
+          const bool ok = !KCHK || kl + c < kend;
           v[8 * u + 4 * h + c] = ok ? x[c] : 0.f;
         }
       }
     }
   } else {
-    // voff = row * 4; this wave's k run starts at k0 + F (t / ROWS) (wave-uniform)
+    // voff[0] = row * 4; this wave's k run starts at k0 + F (t / ROWS) (wave-uniform)
     const int kb = k0 + O::F * __builtin_amdgcn_readfirstlane(t / ROWS);
 #pragma unroll
     for (int j = 0; j < O::F; ++j) {
+      const int k = kb + j;
       const float x = __builtin_bit_cast(
-          float, __builtin_amdgcn_raw_buffer_load_b32(rs, voff, (kb + j) * ld * 4, 0));
-      v[j] = (!KCHK || kb + j < kend) ? x : 0.f;
+          float, __builtin_amdgcn_raw_buffer_load_b32(rs, voff[0], k < K ? k * ld * 4 : 0, 0));
+      v[j] = (!KCHK || k < kend) ? x : 0.f;
     }
   }
 }
@@ -969,24 +977,25 @@ __global__ __launch_bounds__(X2T, 1) void sxgemm2_kernel(
   const int wn = (wave & 1) * 64;
   const int fr = lane & 31, fk = lane >> 5;
   // loop-invariant lane offsets of the staging loads (kOob: a row past the operand); a
-  // k-contiguous A unit 1 lies 128 rows below unit 0 and is checked on its own
+  // k-contiguous A unit 1 lies 128 rows below unit 0
   constexpr int kOob = 0x7ffffff0;
-  int a_voff, b_voff;
-  bool a_ok1 = true;
+  int a_voff[2] = {kOob, kOob}, b_voff[2] = {kOob, kOob};
   if (AK) {
-    const int r = m0 + (t >> 2);
-    a_voff = r < M ? (r * ilda + 8 * (t & 3)) * 4 : kOob;
-    a_ok1 = r + X2T / 4 < M;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int r = m0 + (t >> 2) + u * (X2T / 4);
+      if (r < M) a_voff[u] = (r * ilda + 8 * (t & 3)) * 4;
+    }
   } else {
     const int r = m0 + (t % X2M);
-    a_voff = r < M ? r * 4 : kOob;
+    if (r < M) a_voff[0] = r * 4;
   }
   if (BKc) {
     const int r = n0 + (t >> 2);
-    b_voff = r < N ? (r * ildb + 8 * (t & 3)) * 4 : kOob;
+    if (r < N) b_voff[0] = (r * ildb + 8 * (t & 3)) * 4;
   } else {
     const int r = n0 + (t % TBN);
-    b_voff = r < N ? r * 4 : kOob;
+    if (r < N) b_voff[0] = r * 4;
   }
 
   f32x16 acc[2][2];
@@ -1001,12 +1010,8 @@ __global__ __launch_bounds__(X2T, 1) void sxgemm2_kernel(
   // stage of latency) while the split of stage kt + 1 reads the other set
   float ra0[OA::F], rb0[OB::F], ra1[OA::F], rb1[OB::F];
   auto load = [&](int k0, float (&va)[OA::F], float (&vb)[OB::F]) {
-    x2_load<AK, X2M, KCHK>(a_rs, ilda, a_voff, kend, k0, va);
-    if (AK && !a_ok1) {   // unit 1 (rows + 128) past M
-#pragma unroll
-      for (int c = 8; c < 16; ++c) va[c] = 0.f;
-    }
-    x2_load<BKc, TBN, KCHK>(b_rs, ildb, b_voff, kend, k0, vb);
+    x2_load<AK, X2M, KCHK>(a_rs, ilda, a_voff, K, kend, k0, va);
+    x2_load<BKc, TBN, KCHK>(b_rs, ildb, b_voff, K, kend, k0, vb);
   };
   auto body = [&](int kt, int cur, float (&la)[OA::F], float (&lb)[OB::F],
                   const float (&sa)[OA::F], const float (&sb)[OB::F]) {

@@ -554,8 +554,8 @@ __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
             pend &= ~(1u << i);
           }
         }
-        if (pend == 0u) break;
-        if (spins > g_spin_limit) {
+        if (pend == 0u && g_spin_limit != 0) break;
+        if (spins > g_spin_limit || g_spin_limit == 0) {
           if (lane == 0) __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           failed = 1;
           break;
@@ -924,8 +924,8 @@ __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
               ++next;
             }
           }
-          if (next >= nb) break;
-          if (spins > g_spin_limit) {
+          if (next >= nb && g_spin_limit != 0) break;
+          if (spins > g_spin_limit || g_spin_limit == 0) {
             if (lane == 0) __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             failed = 1;
             break;

@@ -111,8 +111,9 @@ static inline int mapped_grid(int P, int BT) { return 8 * ((P + 7) / 8) * BT; }
 constexpr unsigned kSpinLimit = 1u << 21;
 
 // The bound the kernels use: kSpinLimit unless DS2_RNN_SPIN_LIMIT is set in the environment
-// (checked at every recurrence entry point) -- a test lowers it to force the timeout path and
-// check that the failure surfaces through err_out instead of going silent.
+// (checked at every recurrence entry point).  0 is fault injection: every hand-off wait fails
+// as a timeout would, whether or not its data has arrived -- the test that checks the failure
+// surfaces through err_out (and as Ds2Error in the Trainer) instead of going silent uses it.
 static __constant__ unsigned g_spin_limit = kSpinLimit;
 
 static void apply_spin_limit_env() {
@@ -185,7 +186,11 @@ __device__ __forceinline__ bool group_wait(unsigned* ctr, unsigned target, unsig
   if (threadIdx.x == 0) {
     unsigned spins = 0;
     int ok = 1;
-    while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+    if (g_spin_limit == 0) {   // fault injection
+      __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      ok = 0;
+    }
+    while (ok && __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
       __builtin_amdgcn_s_sleep(2);
       if (++spins > g_spin_limit || __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
         __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -210,7 +215,11 @@ __device__ __forceinline__ bool flags_wait(const unsigned* flags, int count, uns
     const int lane = threadIdx.x;
     unsigned spins = 0;
     int ok = 1;
-    for (;;) {
+    if (g_spin_limit == 0) {   // fault injection
+      if (lane == 0) __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      ok = 0;
+    }
+    for (; ok;) {
       const unsigned v = lane < count ? __hip_atomic_load(flags + lane, __ATOMIC_RELAXED,
                                                           __HIP_MEMORY_SCOPE_AGENT)
                                       : target;
@@ -313,8 +322,8 @@ __device__ __forceinline__ bool wave_ready(f32x4 v) { return __ballot(!tile_read
 // The wave's later tiles stay in flight meanwhile.
 __device__ __forceinline__ bool spin_tile(f32x4& v, __amdgpu_buffer_rsrc_t rs, int off,
                                           unsigned* err) {
-  for (unsigned spins = 0; !wave_ready(v); ++spins) {
-    if (spins > g_spin_limit) {
+  for (unsigned spins = 0; g_spin_limit == 0 || !wave_ready(v); ++spins) {
+    if (spins > g_spin_limit || g_spin_limit == 0) {
       if ((threadIdx.x & 63) == 0)
         __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       return false;
