@@ -943,7 +943,65 @@ __device__ __forceinline__ void x2_mma6(const bf16x8 (&a)[3], const bf16x8 (&b)[
   c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], c, 0, 0, 0);
 }
 
-template <int TA, int TB, bool KCHK>
+// B stages of 160 rows (N = 800 / 2400 without a partial tile column): 640 (row, 8-k slot)
+// units, units t and t + 512 (t < 128) per thread.  k-contiguous: as x2_load (wave-uniform
+// scalar k offset); row-contiguous: rows 0..127 with the 128-row mapping (wave-uniform k),
+// rows 128..159 (threads < 128, four slots per wave) with the whole offset in the vector
+// register (range-checked).
+template <bool KC, bool KCHK>
+__device__ __forceinline__ void x2_load160(__amdgpu_buffer_rsrc_t rs, int ld, const int (&voff)[2],
+                                           int rows_ok1, int K, int kend, int k0, float (&v)[16]) {
+  constexpr int kOob = 0x7ffffff0;
+  const int t = threadIdx.x;
+  if (KC) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int kw = k0 + 4 * h;
+        const int so = kw < K ? kw * 4 : 0;
+        const int kl = kw + 8 * (t & 3);
+        const int vo = (KCHK && kl >= K) ? kOob : voff[u];
+        const f32x4 x = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, vo, so, 0));
+#pragma unroll
+        for (int c = 0; c < 4; ++c) v[8 * u + 4 * h + c] = (!KCHK || kl + c < kend) ? x[c] : 0.f;
+      }
+    }
+  } else {
+    const int kb = k0 + 8 * __builtin_amdgcn_readfirstlane(t >> 7);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = kb + j;
+      const float x = __builtin_bit_cast(
+          float, __builtin_amdgcn_raw_buffer_load_b32(rs, voff[0], k < K ? k * ld * 4 : 0, 0));
+      v[j] = (!KCHK || k < kend) ? x : 0.f;
+    }
+    // rows 128..159: voff[1] = that row * 4 (kOob past N or for threads >= 128)
+    const int k1 = k0 + 8 * ((t >> 5) & 3);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = k1 + j;
+      const int vo = (rows_ok1 && k < K) ? voff[1] + k * ld * 4 : kOob;
+      const float x = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, vo, 0, 0));
+      v[8 + j] = (!KCHK || k < kend) ? x : 0.f;
+    }
+  }
+}
+
+template <bool KC>
+__device__ __forceinline__ void x2_store160(unsigned short* __restrict__ s, const float (&v)[16]) {
+  constexpr int P = 160 * XS;
+  const int t = threadIdx.x;
+  if (KC) {
+    x2_split_store(s, P, xslot(t >> 2, t & 3), v);
+    if (t < 128) x2_split_store(s, P, xslot((t + X2T) >> 2, (t + X2T) & 3), v + 8);
+  } else {
+    x2_split_store(s, P, xslot(t & 127, t >> 7), v);
+    if (t < 128) x2_split_store(s, P, xslot(128 + (t & 31), (t >> 5) & 3), v + 8);
+  }
+}
+
+template <int TA, int TB, bool KCHK, int TBN>
 __global__ __launch_bounds__(X2T, 1) void sxgemm2_kernel(
     int M, int N, int K, float alpha, const float* __restrict__ A, int64_t lda, int64_t sA,
     const float* __restrict__ B, int64_t ldb, int64_t sB, float beta, float* __restrict__ C,
@@ -951,11 +1009,14 @@ __global__ __launch_bounds__(X2T, 1) void sxgemm2_kernel(
     int tail_tiles, int nsplit, int kchunk, float* __restrict__ partial) {
   constexpr bool AK = (TA == 0);
   constexpr bool BKc = (TB == 1);
-  constexpr int TBN = 128;
+  static_assert(TBN == 128 || TBN == 160, "tile width");
+  // waves: 4 (M) x 2 (N) of 2 x 2 32x32 tiles (TBN 128) or 8 (M) x 1 (N) of 1 x 5 (TBN 160)
+  constexpr int WMT = TBN == 128 ? 2 : 1, WNT = TBN == 128 ? 2 : 5;
+  constexpr int BP = TBN * XS;             // bf16 per B plane
+  constexpr int BF = TBN == 128 ? 8 : 16;  // B floats per thread per stage
   using OA = X2Op<AK, X2M>;
-  using OB = X2Op<BKc, TBN>;
   __shared__ __attribute__((aligned(16))) unsigned short As[2][3 * X2_AP];
-  __shared__ __attribute__((aligned(16))) unsigned short Bs[2][3 * X2_BP];
+  __shared__ __attribute__((aligned(16))) unsigned short Bs[2][3 * BP];
 
   int m0, n0, kbeg, kend, bz;
   float* part;
@@ -973,8 +1034,8 @@ __global__ __launch_bounds__(X2T, 1) void sxgemm2_kernel(
   const int t = threadIdx.x;
   const int lane = t & 63;
   const int wave = t >> 6;
-  const int wm = (wave >> 1) * 64;
-  const int wn = (wave & 1) * 64;
+  const int wm = TBN == 128 ? (wave >> 1) * 64 : wave * 32;
+  const int wn = TBN == 128 ? (wave & 1) * 64 : 0;
   const int fr = lane & 31, fk = lane >> 5;
   // loop-invariant lane offsets of the staging loads (kOob: a row past the operand); a
   // k-contiguous A unit 1 lies 128 rows below unit 0
@@ -990,72 +1051,100 @@ __global__ __launch_bounds__(X2T, 1) void sxgemm2_kernel(
     const int r = m0 + (t % X2M);
     if (r < M) a_voff[0] = r * 4;
   }
-  if (BKc) {
-    const int r = n0 + (t >> 2);
-    if (r < N) b_voff[0] = (r * ildb + 8 * (t & 3)) * 4;
+  int b_ok1 = 0;
+  if (TBN == 128) {
+    if (BKc) {
+      const int r = n0 + (t >> 2);
+      if (r < N) b_voff[0] = (r * ildb + 8 * (t & 3)) * 4;
+    } else {
+      const int r = n0 + (t % TBN);
+      if (r < N) b_voff[0] = r * 4;
+    }
   } else {
-    const int r = n0 + (t % TBN);
-    if (r < N) b_voff[0] = r * 4;
+    if (BKc) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int unit = t + X2T * u;
+        const int r = n0 + (unit >> 2);
+        if (unit < 640 && r < N) b_voff[u] = (r * ildb + 8 * (t & 3)) * 4;
+      }
+    } else {
+      const int r0 = n0 + (t & 127), r1 = n0 + 128 + (t & 31);
+      if (r0 < N) b_voff[0] = r0 * 4;
+      b_voff[1] = r1 * 4;
+      b_ok1 = t < 128 && r1 < N;
+    }
   }
 
-  f32x16 acc[2][2];
+  f32x16 acc[WMT][WNT];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < WMT; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < WNT; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   // two register sets: stage kt + 2's loads are issued at the top of stage kt (a whole
   // stage of latency) while the split of stage kt + 1 reads the other set
-  float ra0[OA::F], rb0[OB::F], ra1[OA::F], rb1[OB::F];
-  auto load = [&](int k0, float (&va)[OA::F], float (&vb)[OB::F]) {
+  float ra0[OA::F], rb0[BF], ra1[OA::F], rb1[BF];
+  auto load = [&](int k0, float (&va)[OA::F], float (&vb)[BF]) {
     x2_load<AK, X2M, KCHK>(a_rs, ilda, a_voff, K, kend, k0, va);
-    x2_load<BKc, TBN, KCHK>(b_rs, ildb, b_voff, K, kend, k0, vb);
+    if constexpr (TBN == 128)
+      x2_load<BKc, TBN, KCHK>(b_rs, ildb, b_voff, K, kend, k0, vb);
+    else
+      x2_load160<BKc, KCHK>(b_rs, ildb, b_voff, b_ok1, K, kend, k0, vb);
   };
-  auto body = [&](int kt, int cur, float (&la)[OA::F], float (&lb)[OB::F],
-                  const float (&sa)[OA::F], const float (&sb)[OB::F]) {
+  auto bstore = [&](unsigned short* dst, const float (&vb)[BF]) {
+    if constexpr (TBN == 128)
+      x2_store<BKc, TBN>(dst, vb);
+    else
+      x2_store160<BKc>(dst, vb);
+  };
+  auto body = [&](int kt, int cur, float (&la)[OA::F], float (&lb)[BF],
+                  const float (&sa)[OA::F], const float (&sb)[BF]) {
     // stage kt visible; every wave is done reading the other buffer (stage kt - 1)
     __syncthreads();
     load(kbeg + (kt + 2) * XS, la, lb);          // stages past kend load as zeros
     const unsigned short* as = As[cur];
     const unsigned short* bs = Bs[cur];
+    constexpr int NMF = WMT * WNT * 6;         // MFMAs per k-step
+    constexpr int NRD = (WMT + WNT) * 3;       // fragment reads per k-step
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 af[2][3], bfr[2][3];
+      bf16x8 af[WMT][3], bfr[WNT][3];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
+      for (int i = 0; i < WMT; ++i) {
         const int at = xslot(wm + 32 * i + fr, 2 * ks + fk);
 #pragma unroll
         for (int p = 0; p < 3; ++p) af[i][p] = *reinterpret_cast<const bf16x8*>(as + p * X2_AP + at);
       }
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
+      for (int j = 0; j < WNT; ++j) {
         const int bt = xslot(wn + 32 * j + fr, 2 * ks + fk);
 #pragma unroll
-        for (int p = 0; p < 3; ++p) bfr[j][p] = *reinterpret_cast<const bf16x8*>(bs + p * X2_BP + bt);
+        for (int p = 0; p < 3; ++p) bfr[j][p] = *reinterpret_cast<const bf16x8*>(bs + p * BP + bt);
       }
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < WMT; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) x2_mma6(af[i], bfr[j], acc[i][j]);
+        for (int j = 0; j < WNT; ++j) x2_mma6(af[i], bfr[j], acc[i][j]);
     }
     // stage kt + 1 -> the other buffer (a stage past the end writes zeros nobody reads)
     x2_store<AK, X2M>(As[cur ^ 1], sa);
-    x2_store<BKc, TBN>(Bs[cur ^ 1], sb);
+    bstore(Bs[cur ^ 1], sb);
     // schedule: the loads, the first k-step's fragments, then each MFMA followed by up to
     // three VALU (the split of the next stage), the second k-step's fragments early, the
     // LDS stores of the split spread over the second half
-    __builtin_amdgcn_sched_group_barrier(0x020, 24, 0);
-    __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);
+    __builtin_amdgcn_sched_group_barrier(0x020, 32, 0);
+    __builtin_amdgcn_sched_group_barrier(0x100, NRD, 0);
 #pragma unroll
-    for (int q = 0; q < 24; ++q) {
+    for (int q = 0; q < NMF; ++q) {
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
       __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
-      if (q == 8) __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);
+      if (q == NMF / 3) __builtin_amdgcn_sched_group_barrier(0x100, NRD, 0);
     }
 #pragma unroll
-    for (int q = 0; q < 24; ++q) {
+    for (int q = 0; q < NMF; ++q) {
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
       __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
       if (q % 3 == 2) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
@@ -1064,7 +1153,7 @@ __global__ __launch_bounds__(X2T, 1) void sxgemm2_kernel(
   const int ktiles = (kend - kbeg + XS - 1) / XS;
   load(kbeg, ra0, rb0);
   x2_store<AK, X2M>(As[0], ra0);
-  x2_store<BKc, TBN>(Bs[0], rb0);
+  bstore(Bs[0], rb0);
   load(kbeg + XS, ra1, rb1);
   for (int kt = 0; kt < ktiles; kt += 2) {
     body(kt, 0, ra0, rb0, ra1, rb1);
@@ -1073,9 +1162,9 @@ __global__ __launch_bounds__(X2T, 1) void sxgemm2_kernel(
 
   // epilogue (32x32 C/D map: col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5))
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < WMT; ++i) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
+    for (int j = 0; j < WNT; ++j) {
       const int cl = wn + 32 * j + (lane & 31);
       if (part != nullptr) {
 #pragma unroll
@@ -1287,7 +1376,12 @@ static size_t plan_ws(const GemmPlan& p, int batch) {
 // per CU (mode 1) or 128-row tiles two per CU (mode 2)
 static GemmPlan x6_plan(int m, int n, int k, int batch, int mode) {
   if (mode == 2) return plan_bn(m, n, k, batch, 128, 2 * device_cus(), XS, 1.0).p;
-  return plan_bn(m, n, k, batch, 128, device_cus(), XS, 1.0, X2M).p;
+  const char* e = getenv("DS2_GEMM_X6_BN");
+  if (e != nullptr && e[0] != 0)
+    return plan_bn(m, n, k, batch, e[1] == '6' ? 160 : 128, device_cus(), XS, 1.0, X2M).p;
+  // 160-wide tiles measured faster on every step shape with N >= 800 (scripts/bench_gemm_x6.py:
+  // 180-201 vs 159-194 TF), 128-wide on narrow N (the FC's 32 columns)
+  return plan_bn(m, n, k, batch, n >= 256 ? 160 : 128, device_cus(), XS, 1.0, X2M).p;
 }
 
 // large enough for any kernel's plan (the choice depends on operand alignment)
@@ -1295,7 +1389,8 @@ extern "C" size_t ds2_sgemm_workspace_size(int m, int n, int k, int batch) {
   if (m <= 0 || n <= 0 || k <= 0 || batch <= 0) return 0;
   return std::max(std::max(plan_ws(gemm_plan(m, n, k, batch, false), batch),
                            plan_ws(gemm_plan(m, n, k, batch, true), batch)),
-                  std::max(plan_ws(x6_plan(m, n, k, batch, 1), batch),
+                  std::max(std::max(plan_ws(plan_bn(m, n, k, batch, 128, device_cus(), XS, 1.0, X2M).p, batch),
+                                    plan_ws(plan_bn(m, n, k, batch, 160, device_cus(), XS, 1.0, X2M).p, batch)),
                            plan_ws(x6_plan(m, n, k, batch, 2), batch)));
 }
 
@@ -1333,13 +1428,21 @@ extern "C" ds2_status_t ds2_sgemm_ws(int trans_a, int trans_b, int m, int n, int
   // every stage of every piece lies wholly inside [0, K): no per-element k check
   const bool kalign = k % XS == 0 && (p.nsplit == 1 || p.kchunk % XS == 0);
 #define DS2_G(TA_, TB_)                                                                       \
-  if (x6 == 1 && kalign)                                                                      \
-    hipLaunchKernelGGL((sxgemm2_kernel<TA_, TB_, false>), grid, dim3(X2T), 0, st, m, n, k, alpha, \
-                       a, lda, stride_a, b, ldb, stride_b, beta, c, ldc, stride_c, bias,        \
+  if (x6 == 1 && kalign && p.bn == 160)                                                       \
+    hipLaunchKernelGGL((sxgemm2_kernel<TA_, TB_, false, 160>), grid, dim3(X2T), 0, st, m, n, k,   \
+                       alpha, a, lda, stride_a, b, ldb, stride_b, beta, c, ldc, stride_c, bias, \
+                       p.main_wgs, p.tail_tile0, p.tail_tiles, p.nsplit, p.kchunk, partial);   \
+  else if (x6 == 1 && p.bn == 160)                                                            \
+    hipLaunchKernelGGL((sxgemm2_kernel<TA_, TB_, true, 160>), grid, dim3(X2T), 0, st, m, n, k,    \
+                       alpha, a, lda, stride_a, b, ldb, stride_b, beta, c, ldc, stride_c, bias, \
+                       p.main_wgs, p.tail_tile0, p.tail_tiles, p.nsplit, p.kchunk, partial);   \
+  else if (x6 == 1 && kalign)                                                                 \
+    hipLaunchKernelGGL((sxgemm2_kernel<TA_, TB_, false, 128>), grid, dim3(X2T), 0, st, m, n, k,   \
+                       alpha, a, lda, stride_a, b, ldb, stride_b, beta, c, ldc, stride_c, bias, \
                        p.main_wgs, p.tail_tile0, p.tail_tiles, p.nsplit, p.kchunk, partial);   \
   else if (x6 == 1)                                                                           \
-    hipLaunchKernelGGL((sxgemm2_kernel<TA_, TB_, true>), grid, dim3(X2T), 0, st, m, n, k, alpha,  \
-                       a, lda, stride_a, b, ldb, stride_b, beta, c, ldc, stride_c, bias,        \
+    hipLaunchKernelGGL((sxgemm2_kernel<TA_, TB_, true, 128>), grid, dim3(X2T), 0, st, m, n, k,    \
+                       alpha, a, lda, stride_a, b, ldb, stride_b, beta, c, ldc, stride_c, bias, \
                        p.main_wgs, p.tail_tile0, p.tail_tiles, p.nsplit, p.kchunk, partial);   \
   else if (x6 == 2)                                                                           \
     hipLaunchKernelGGL((sxgemm_kernel<TA_, TB_>), grid, dim3(256), 0, st, m, n, k, alpha, a, lda, \

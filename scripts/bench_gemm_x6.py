@@ -54,8 +54,10 @@ def main():
         ref = torch.mm(at.double(), bt.double())
         scale = ref.abs().max().item()
         line = f"{name:12s} {m:6d}x{n:5d}x{k:6d} |"
-        for tag, env, peak in (("x6", "1", PEAKX6), ("x6-128", "2", PEAKX6), ("fp32", "0", PEAK32)):
-            os.environ["DS2_GEMM_X6"] = env
+        for tag, env, peak in (("x6", "1", PEAKX6), ("x6-bn128", "1/128", PEAKX6),
+                               ("x6-bn160", "1/160", PEAKX6), ("fp32", "0", PEAK32)):
+            os.environ["DS2_GEMM_X6"] = env.split("/")[0]
+            os.environ["DS2_GEMM_X6_BN"] = env.split("/")[1] if "/" in env else ""
             t = timeit(lambda: ops.sgemm(a, b, c, **kw))
             err = (c.double() - ref).abs().max().item() / scale
             tf = fl / t / 1e9

@@ -23,15 +23,16 @@ def _close(got, ref, rel=1e-5, name=""):
 
 
 # ---------------------------------------------------------------------------- GEMM
-@pytest.mark.parametrize("x6", ["1", "0"])
+@pytest.mark.parametrize("x6", ["1", "0", "160"])
 @pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
 @pytest.mark.parametrize("m,n,k", [(1, 1, 1), (37, 53, 29), (128, 128, 16), (300, 257, 513),
                                    (515, 2400, 132), (257, 300, 5000),   # split-K path
                                    (300, 256, 516), (260, 132, 1000)])   # float4 staging, K % 32 != 0
 def test_sgemm(dev, ta, tb, m, n, k, x6, monkeypatch):
     """ds2_sgemm_ws vs fp64 at 1e-5: the bf16x6 kernel (default for float4-staged operands)
-    and the fp32-MFMA kernels (DS2_GEMM_X6=0)."""
-    monkeypatch.setenv("DS2_GEMM_X6", x6)
+    and the fp32-MFMA kernels (DS2_GEMM_X6=0); "160" forces the 256 x 160 bf16x6 tile."""
+    monkeypatch.setenv("DS2_GEMM_X6", "1" if x6 == "160" else x6)
+    monkeypatch.setenv("DS2_GEMM_X6_BN", "160" if x6 == "160" else "")
     g = torch.Generator().manual_seed(m * 7 + n * 3 + k)
     a = torch.randn(k, m, generator=g) if ta else torch.randn(m, k, generator=g)
     b = torch.randn(n, k, generator=g) if tb else torch.randn(k, n, generator=g)
@@ -46,14 +47,17 @@ def test_sgemm(dev, ta, tb, m, n, k, x6, monkeypatch):
     _close(cd, ref, 1e-5, "sgemm")
 
 
-@pytest.mark.parametrize("mode", ["bk16", "128", "160", "db128", "db160", "x6", "x6-128"])
+@pytest.mark.parametrize("mode", ["bk16", "128", "160", "db128", "db160", "x6", "x6-128",
+                                  "x6-bn128", "x6-bn160"])
 @pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
 def test_sgemm_full_rounds_plus_split_tail(dev, ta, tb, mode, monkeypatch):
     """Whole rounds of resident workgroups + a tail whose K range is split (one launch) and
     reduced in a fixed order; alpha/beta/bias applied once.  fp32 kernels: BK = 16 /
     32x32x2 (DS2_GEMM64=0) and BK = 64 / 16x16x4 with 128- and 160-wide tiles; bf16x6
     kernels: 256 x 128 (default) and 128 x 128 (DS2_GEMM_X6=2)."""
-    monkeypatch.setenv("DS2_GEMM_X6", {"x6": "1", "x6-128": "2"}.get(mode, "0"))
+    monkeypatch.setenv("DS2_GEMM_X6", {"x6": "1", "x6-128": "2", "x6-bn128": "1",
+                                       "x6-bn160": "1"}.get(mode, "0"))
+    monkeypatch.setenv("DS2_GEMM_X6_BN", mode[-3:] if mode.startswith("x6-bn") else "")
     monkeypatch.setenv("DS2_GEMM64", "0" if mode == "bk16" else "1")
     if mode in ("128", "160", "db128", "db160"):
         monkeypatch.setenv("DS2_GEMM_BN", mode[-3:])
