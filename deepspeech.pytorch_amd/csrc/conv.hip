@@ -1142,6 +1142,176 @@ __global__ __launch_bounds__(CX_T, 1) void conv_x6_kernel(const float* __restric
   }
 }
 
+// ---------------------------------------------------------------------------
+// bf16x6 weight gradient (width stride 1, <= 32 input and output channels; instantiated for
+// the model's conv2 columns: kw = 11, pw = 5) on v_mfma_f32_32x32x16_bf16 at fp32 accuracy:
+//   dW[co][ci][a][b] = sum over (n, ho, wo) of dy[n][co][ho][wo] x[n][ci][ho sh - ph + a][wo - pw + b]
+// For ONE tap (a, b) this is a 32 x 32 (co x ci) product over positions: M = co, N = ci,
+// K = 16 consecutive output columns.  Wave w of a workgroup owns tap row a = 4 gi + w and all
+// kw kernel columns (kw accumulators).  Its A fragment (dy: 8 consecutive columns of one co,
+// one ds_read_b128 per plane) serves all kw taps; the B fragments of the kw taps are windows
+// at offsets b + 8 - pw into 24 consecutive x columns of one ci (three aligned ds_read_b128
+// per plane), cut out by register selection (even offsets) or v_alignbit (odd).
+// Workgroup = (tap-row group gi, split s): it runs over the (n, ho) rows of split s in
+// 64-column stages -- dy[32 co][64] and x[4 rows][32 ci][80 columns] split into hi/mid/lo
+// bf16 planes in LDS (81 KB, so two workgroups share a CU and cover each other's staging) --
+// and writes its kw x 32 x 32 sums into slab s; wgrad_reduce_kernel adds the slabs in a fixed
+// order (deterministic).
+constexpr int CW_T = 256;
+constexpr int CW_COLS = 64;
+constexpr int CW_XP = 88;                  // x row pitch (bf16): 80 columns, 8 x odd
+constexpr int CW_DP = 72;                  // dy row pitch (bf16): 64 columns, 8 x odd
+constexpr int CW_XPL = 4 * 32 * CW_XP;     // bf16 per x plane
+constexpr int CW_DPL = 32 * CW_DP;         // bf16 per dy plane
+constexpr int CW_SLOTS = 512;              // workgroups per launch (two per CU)
+
+// 8 fp32 -> hi / mid / lo bf16 rows of 16 B (RNE casts, exact residuals)
+__device__ __forceinline__ void cw_split_store(unsigned short* __restrict__ s, int plane, int at,
+                                               const float (&v)[8]) {
+  u32x4 h, m, l;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const float x0 = v[2 * e], x1 = v[2 * e + 1];
+    const __bf16 h0 = (__bf16)x0, h1 = (__bf16)x1;
+    const float q0 = x0 - (float)h0, q1 = x1 - (float)h1;
+    const __bf16 m0 = (__bf16)q0, m1 = (__bf16)q1;
+    const __bf16 l0 = (__bf16)(q0 - (float)m0), l1 = (__bf16)(q1 - (float)m1);
+    h[e] = (unsigned)__builtin_bit_cast(unsigned short, h0) |
+           ((unsigned)__builtin_bit_cast(unsigned short, h1) << 16);
+    m[e] = (unsigned)__builtin_bit_cast(unsigned short, m0) |
+           ((unsigned)__builtin_bit_cast(unsigned short, m1) << 16);
+    l[e] = (unsigned)__builtin_bit_cast(unsigned short, l0) |
+           ((unsigned)__builtin_bit_cast(unsigned short, l1) << 16);
+  }
+  *reinterpret_cast<u32x4*>(s + at) = h;
+  *reinterpret_cast<u32x4*>(s + plane + at) = m;
+  *reinterpret_cast<u32x4*>(s + 2 * plane + at) = l;
+}
+
+template <int KW, int OFF0>
+__global__ __launch_bounds__(CW_T, 2) void conv_x6_wgrad_kernel(const float* __restrict__ dy,
+                                                                 const float* __restrict__ x,
+                                                                 float* __restrict__ partial,
+                                                                 ConvDims g, int S) {
+  __shared__ __attribute__((aligned(16))) unsigned short xs[3 * CW_XPL];
+  __shared__ __attribute__((aligned(16))) unsigned short ds[3 * CW_DPL];
+  constexpr int kOob = 0x7ffffff0;
+  const int G = (g.kh + 3) / 4;
+  const int gi = blockIdx.x % G, s = blockIdx.x / G;
+  const int R = g.n * g.ho;
+  const int r0 = static_cast<int>((int64_t)s * R / S);
+  const int r1 = static_cast<int>((int64_t)(s + 1) * R / S);
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int a = 4 * gi + wave;
+  const bool active = a < g.kh;
+  const int fr = lane & 31, fh = lane >> 5;
+  const int nch = (g.wo + CW_COLS - 1) / CW_COLS;
+  const int dplane = g.ho * g.wo, xplane = g.hi * g.wi;   // host: channel stacks < 2^31 B
+  const int dco = tid >> 3, dseg = tid & 7;                 // dy staging: co, 8-column segment
+
+  f32x16 acc[KW];
+#pragma unroll
+  for (int b = 0; b < KW; ++b)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[b][r] = 0.f;
+
+  for (int row = r0; row < r1; ++row) {
+    const int n = row / g.ho, ho = row - (row / g.ho) * g.ho;
+    const __amdgpu_buffer_rsrc_t drs = conv_rsrc(dy + (int64_t)n * g.co * dplane, (int64_t)g.co * dplane);
+    const __amdgpu_buffer_rsrc_t xrs = conv_rsrc(x + (int64_t)n * g.ci * xplane, (int64_t)g.ci * xplane);
+    const int xr0 = ho * g.sh - g.ph + 4 * gi;
+    for (int ch = 0; ch < nch; ++ch) {
+      const int c0 = ch * CW_COLS;
+      // one base offset per 8-column run; a column past either edge of its row (or a row
+      // outside the input) loads from the out-of-range offset, i.e. zero
+      float dv[8], xv[5][8];
+      {
+        const int cb = c0 + 8 * dseg;
+        const int vo = dco < g.co ? (dco * dplane + ho * g.wo + cb) * 4 : kOob;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          dv[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                drs, cb + i < g.wo ? vo + 4 * i : kOob, 0, 0));
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 5; ++u) {
+        const int id = tid + CW_T * u;
+        const int j = id % 10, ci = (id / 10) & 31, w = id / 320;
+        const int xr = xr0 + w;
+        const bool ok = ci < g.ci && xr >= 0 && xr < g.hi && 4 * gi + w < g.kh;
+        const int cb = c0 - 8 + 8 * j;
+        const int vo = ok ? (ci * xplane + xr * g.wi + cb) * 4 : kOob;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const bool cok = cb + i >= 0 && cb + i < g.wi;
+          xv[u][i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                   xrs, cok ? vo + 4 * i : kOob, 0, 0));
+        }
+      }
+      __syncthreads();   // every wave is done with the previous stage's fragments
+      cw_split_store(ds, CW_DPL, dco * CW_DP + 8 * dseg, dv);
+#pragma unroll
+      for (int u = 0; u < 5; ++u) {
+        const int id = tid + CW_T * u;
+        const int j = id % 10, ci = (id / 10) & 31, w = id / 320;
+        cw_split_store(xs, CW_XPL, (w * 32 + ci) * CW_XP + 8 * j, xv[u]);
+      }
+      __syncthreads();
+      if (active) {
+#pragma unroll 1
+        for (int kst = 0; kst < CW_COLS / 16; ++kst) {
+          bf16x8 af[3];
+#pragma unroll
+          for (int pl = 0; pl < 3; ++pl)
+            af[pl] = *reinterpret_cast<const bf16x8*>(ds + pl * CW_DPL + fr * CW_DP + 16 * kst + 8 * fh);
+          // one plane of x at a time (12 window registers): products with the lo, then
+          // the mid, then the hi terms of x, each over the kw taps
+#pragma unroll
+          for (int pi = 0; pi < 3; ++pi) {
+            const int pl = 2 - pi;
+            unsigned wv[12];
+#pragma unroll
+            for (int jj = 0; jj < 3; ++jj) {
+              const u32x4 q = *reinterpret_cast<const u32x4*>(
+                  xs + pl * CW_XPL + (wave * 32 + fr) * CW_XP + 8 * (2 * kst + fh + jj));
+#pragma unroll
+              for (int e = 0; e < 4; ++e) wv[4 * jj + e] = q[e];
+            }
+#pragma unroll
+            for (int b = 0; b < KW; ++b) {
+              const int o = b + OFF0;   // window offset of tap column b (compile time)
+              u32x4 q;
+#pragma unroll
+              for (int e = 0; e < 4; ++e)
+                q[e] = (o & 1) ? __builtin_amdgcn_alignbit(wv[(o + 1) / 2 + e], wv[(o - 1) / 2 + e], 16)
+                               : wv[o / 2 + e];
+              const bf16x8 bx = __builtin_bit_cast(bf16x8, q);
+              // x term pl (0 hi, 1 mid, 2 lo) pairs with the dy terms i <= 2 - pl (the
+              // products that carry fp32 weight), smaller terms first
+#pragma unroll
+              for (int i = 2 - pl; i >= 0; --i)
+                acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bx, acc[b], 0, 0, 0);
+            }
+          }
+        }
+      }
+    }
+  }
+  if (!active || fr >= g.ci) return;
+  const int Kc = g.ci * g.kh * KW;
+  float* slab = partial + (int64_t)s * g.co * Kc;
+#pragma unroll
+  for (int b = 0; b < KW; ++b)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int co = (r & 3) + 8 * (r >> 2) + 4 * fh;
+      if (co < g.co) slab[(int64_t)co * Kc + (fr * g.kh + a) * KW + b] = acc[b][r];
+    }
+}
+
 static inline bool make_dims(ConvDims& g, int n, int c_in, int h_in, int w_in, int c_out, int kh,
                              int kw, int sh, int sw, int ph, int pw) {
   if (n < 0 || c_in < 1 || h_in < 1 || w_in < 1 || c_out < 1 || kh < 1 || kw < 1 || sh < 1 ||
@@ -1282,6 +1452,24 @@ static inline WgradPlan wgrad_plan(const ConvDims& g) {
   return pl;
 }
 
+// the bf16x6 weight-gradient kernel: width stride 1, the instantiated kernel columns (kw 11,
+// pw 5), <= 32 channels each side, channel stacks that fit 32-bit buffer offsets
+static inline bool x6w_ok(const ConvDims& g) {
+  const char* e = getenv("DS2_CONV_X6");
+  if (e != nullptr && e[0] == '0') return false;
+  if (g.sw != 1 || g.kw != 11 || g.pw != 5 || g.ci > 32 || g.co > 32) return false;
+  const int64_t lim = (1ll << 31) - 64;
+  return (int64_t)g.co * g.ho * g.wo * 4 < lim && (int64_t)g.ci * g.hi * g.wi * 4 < lim;
+}
+
+static inline int x6w_splits(const ConvDims& g) {
+  const int G = (g.kh + 3) / 4;
+  const int64_t R = (int64_t)g.n * g.ho;
+  int64_t S = CW_SLOTS / G;
+  if (S < 1) S = 1;
+  return static_cast<int>(S > R ? R : S);
+}
+
 }  // namespace ds2
 
 using namespace ds2;
@@ -1343,8 +1531,10 @@ size_t ds2_conv2d_wgrad_workspace_size(int n, int c_in, int h_in, int w_in, int 
                                        int kw, int sh, int sw, int ph, int pw) {
   ConvDims g;
   if (!make_dims(g, n, c_in, h_in, w_in, c_out, kh, kw, sh, sw, ph, pw)) return 0;
+  const size_t per = (size_t)c_out * c_in * kh * kw * sizeof(float);
+  if (x6w_ok(g)) return (size_t)x6w_splits(g) * per + 256;
   const WgradPlan pl = wgrad_plan(g);
-  return (size_t)n * (pl.nt > 0 ? pl.bands : 1) * c_out * c_in * kh * kw * sizeof(float) + 256;
+  return (size_t)n * (pl.nt > 0 ? pl.bands : 1) * per + 256;
 }
 
 ds2_status_t ds2_conv2d_wgrad(const float* dy, const float* x, float* dw, float* dbias, int n,
@@ -1362,7 +1552,12 @@ ds2_status_t ds2_conv2d_wgrad(const float* dy, const float* x, float* dw, float*
   float* partial = static_cast<float*>(ws);
   const WgradPlan pl = wgrad_plan(g);
   int slabs = n;
-  if (pl.nt > 0) {
+  if (x6w_ok(g)) {
+    slabs = x6w_splits(g);
+    const int G = (kh + 3) / 4;
+    hipLaunchKernelGGL((conv_x6_wgrad_kernel<11, 3>), dim3(G * slabs), dim3(CW_T), 0, st, dy, x,
+                       partial, g, slabs);
+  } else if (pl.nt > 0) {
     dim3 grid(static_cast<unsigned>((int64_t)pl.bands * c_in * n * cdiv(c_out, 32)));
     if (pl.nt == 2)
       hipLaunchKernelGGL((conv_wgrad_patch_kernel<2, WG_XS_SMALL>), grid, dim3(256), 0, st, dy, x,

@@ -1,5 +1,5 @@
 """conv2 of the headline model (32 x [32, 81, 501] -> 32 channels, 21 x 11 taps, stride
-(2, 1)) forward and dgrad: the bf16x6 direct kernels (default) vs the fp32 LDS-patch
+(2, 1)) forward, dgrad and wgrad: the bf16x6 kernels (default) vs the fp32 LDS-patch
 kernels (DS2_CONV_X6=0); TFLOP/s of the algorithmic 2 * taps * in_ch * outputs.
 usage: python scripts/bench_conv_x6.py"""
 import os
@@ -35,5 +35,6 @@ for mode in ("1", "0"):
     os.environ["DS2_CONV_X6"] = mode
     tf = timeit(lambda: ops.conv2d_fwd(x, wt, None, (sh, sw), (ph, pw)))
     td = timeit(lambda: ops.conv2d_dgrad(dy, wt, x.shape, (sh, sw), (ph, pw)))
+    tw = timeit(lambda: ops.conv2d_wgrad(dy, x, tuple(wt.shape), (sh, sw), (ph, pw), with_bias=False))
     print(f"x6={mode}: fwd {tf:.3f} ms ({flop / tf / 1e9:.1f} TF)  dgrad {td:.3f} ms "
-          f"({flop / td / 1e9:.1f} TF)", flush=True)
+          f"({flop / td / 1e9:.1f} TF)  wgrad {tw:.3f} ms ({flop / tw / 1e9:.1f} TF)", flush=True)

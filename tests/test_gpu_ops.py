@@ -144,6 +144,9 @@ CONVS = [  # (n, ci, h, w, co, kh, kw, sh, sw, ph, pw)
     # width stride 1 -> LDS-patch direct kernels (several column tiles, two output-channel
     # blocks, 3 stride classes in dgrad, odd tap counts, edge rows / columns)
     (2, 32, 81, 200, 32, 21, 11, 2, 1, 10, 5),
+    # conv2's kernel columns with fewer channels and tap rows (bf16x6 wgrad: partial
+    # channel blocks, idle tap-row waves, one output row per split)
+    (3, 5, 30, 70, 20, 7, 11, 1, 1, 3, 5),
     (3, 5, 19, 140, 40, 3, 3, 1, 1, 1, 1),
     (2, 4, 30, 50, 8, 7, 5, 3, 1, 3, 2),
     (1, 2, 9, 7, 3, 4, 2, 2, 1, 3, 0),
@@ -186,7 +189,7 @@ def test_conv_fwd_bwd(dev, cfg, x6, monkeypatch):
 
 def test_conv_x6_is_fp32_accurate(dev, monkeypatch):
     """On the model's conv2 (32 -> 32 channels, 21 x 11 taps, stride (2, 1)) the bf16x6
-    kernels' error against fp64 is of the fp32 kernels' order (fwd and dgrad)."""
+    kernels' error against fp64 is of the fp32 kernels' order (fwd, dgrad and wgrad)."""
     n, ci, h, w, co, kh, kw, sh, sw, ph, pw = 2, 32, 81, 300, 32, 21, 11, 2, 1, 10, 5
     g = torch.Generator().manual_seed(11)
     x = torch.randn(n, ci, h, w, generator=g, dtype=torch.float64)
@@ -194,14 +197,17 @@ def test_conv_x6_is_fp32_accurate(dev, monkeypatch):
     y = F.conv2d(x, wt, None, stride=(sh, sw), padding=(ph, pw))
     dy = torch.randn(y.shape, generator=g, dtype=torch.float64)
     dxr = torch.nn.grad.conv2d_input(x.shape, wt, dy, stride=(sh, sw), padding=(ph, pw))
+    dwr = torch.nn.grad.conv2d_weight(x, wt.shape, dy, stride=(sh, sw), padding=(ph, pw))
     errs = {}
     for mode in ("1", "0"):
         monkeypatch.setenv("DS2_CONV_X6", mode)
         yd = ops.conv2d_fwd(x.float().to(dev), wt.float().to(dev), None, (sh, sw), (ph, pw))
         dx = ops.conv2d_dgrad(dy.float().to(dev), wt.float().to(dev), x.shape, (sh, sw), (ph, pw))
-        errs[mode] = ((yd.double().cpu() - y).abs().max().item() / y.abs().max().item(),
-                      (dx.double().cpu() - dxr).abs().max().item() / dxr.abs().max().item())
-    assert errs["1"][0] <= 2.5 * errs["0"][0] and errs["1"][1] <= 2.5 * errs["0"][1], errs
+        dw, _ = ops.conv2d_wgrad(dy.float().to(dev), x.float().to(dev), tuple(wt.shape), (sh, sw),
+                                 (ph, pw), with_bias=False)
+        errs[mode] = tuple((a.double().cpu() - r).abs().max().item() / r.abs().max().item()
+                           for a, r in ((yd, y), (dx, dxr), (dw, dwr)))
+    assert all(e1 <= 2.5 * e0 for e1, e0 in zip(errs["1"], errs["0"])), errs
     assert max(errs["1"]) < 5e-6, errs
 
 
