@@ -140,7 +140,7 @@ def sgemm_flops(args):
 
 
 def gru_recurrence_flops(args):
-    """ds2_gru_fwd / ds2_gru_bwd (t_max, n, h, num_dirs, ...): the W_hh contraction of
+    """ds2_gru_fwd / ds2_gru_bwd[_bias] (t_max, n, h, num_dirs, ...): the W_hh contraction of
     every step, 2 * T * N * D * 3H * H (backward: the same product with W_hh^T)."""
     t, n, h, d = args[0], args[1], args[2], args[3]
     return 2.0 * t * n * d * 3 * h * h
@@ -281,7 +281,7 @@ def main():
 
     probe = KernelProbe(args.probe, sgemm_flops)
     probe.install()
-    rprobe = KernelProbe(("ds2_gru_fwd", "ds2_gru_bwd"), gru_recurrence_flops)
+    rprobe = KernelProbe(("ds2_gru_fwd", "ds2_gru_bwd", "ds2_gru_bwd_bias"), gru_recurrence_flops)
     rprobe.install()
 
     def step():

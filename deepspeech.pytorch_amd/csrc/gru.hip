@@ -809,9 +809,9 @@ __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     const float* __restrict__ h_all, const float* __restrict__ gates,
     const int* __restrict__ lens, float* __restrict__ dgx, float* __restrict__ dgh,
     float* __restrict__ gx, unsigned* __restrict__ counters, unsigned* __restrict__ err,
-    unsigned long long* __restrict__ stamps) {
+    unsigned long long* __restrict__ stamps, double* __restrict__ dbp) {
   constexpr int RP = GU + 1;
-  __shared__ float red[GW * GB * RP];
+  __shared__ __attribute__((aligned(8))) float red[GW * GB * RP];
   __shared__ __attribute__((aligned(16))) float tile[3 * GB * GU];
   __shared__ int flag;
   int ub, d, bt;
@@ -869,6 +869,9 @@ __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   float dh_prev = 0.f, z_prev = 0.f;
   float px_dar = 0.f, px_daz = 0.f, px_dan = 0.f, px_dghn = 0.f;
   int64_t px_row = -1;
+  // bias-gradient sums over this thread's (sample, unit) rows in step order (dbp != null):
+  // db_ih = column sums of dgx (r, z, n), db_hh's n third = column sums of dgh's n third
+  double sb_r = 0.0, sb_z = 0.0, sb_n = 0.0, sb_hn = 0.0;
   for (int s = 0; s < T; ++s) {
     const int t = d == 0 ? T - 1 - s : s;
     f32x4 acc0 = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -987,6 +990,7 @@ __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
         dh_prev = dh;
         z_prev = zc;
         px_dar = dar; px_daz = daz; px_dan = dan; px_dghn = dghn; px_row = row;
+        sb_r += dar; sb_z += daz; sb_n += dan; sb_hn += dghn;
       }
       tile[tpos] = dar;
       tile[GB * GU + tpos] = daz;
@@ -1035,6 +1039,65 @@ __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
       ghr[H + j] = px_daz;
       ghr[2 * H + j] = px_dghn;
     }
+  }
+  if (dbp == nullptr) return;
+  // the workgroup's 16 samples summed per unit in sample order -> dbp[bt][d][4][H]
+  double* rd = reinterpret_cast<double*>(red);   // 1024 doubles fit in red
+  __syncthreads();
+  if (threadIdx.x < GB * GU) {
+    const bool mine = owner;
+    rd[(0 * GB + m) * GU + u] = mine ? sb_r : 0.0;
+    rd[(1 * GB + m) * GU + u] = mine ? sb_z : 0.0;
+    rd[(2 * GB + m) * GU + u] = mine ? sb_n : 0.0;
+    rd[(3 * GB + m) * GU + u] = mine ? sb_hn : 0.0;
+  }
+  __syncthreads();
+  if (threadIdx.x < 4 * GU) {
+    const int g = threadIdx.x / GU, uu = threadIdx.x - (threadIdx.x / GU) * GU;
+    double acc = 0.0;
+#pragma unroll
+    for (int mm = 0; mm < GB; ++mm) acc += rd[(g * GB + mm) * GU + uu];
+    dbp[(((int64_t)bt * D + d) * 4 + g) * H + ub * GU + uu] = acc;
+  }
+}
+
+// Bias gradients from dgx / dgh when the recurrence kernel did not sum them (every path
+// but the direct-operand backward): one block per (direction, gate column), fixed order.
+__global__ void gru_db_cols_kernel(const float* __restrict__ dgx, const float* __restrict__ dgh,
+                                   int rows, int D, int H, double* __restrict__ dbp) {
+  const int c = blockIdx.x;                    // (d, g, j): dbp[0][d][g][j]
+  const int d = c / (4 * H), k = c - d * 4 * H;
+  const int g = k / H, j = k - g * H;
+  const float* src = g < 3 ? dgx + d * 3 * H + g * H + j : dgh + d * 3 * H + 2 * H + j;
+  const int64_t stride = (int64_t)D * 3 * H;
+  double acc = 0.0;
+  for (int r = threadIdx.x; r < rows; r += blockDim.x) acc += src[r * stride];
+  __shared__ double sh[256];
+  sh[threadIdx.x] = acc;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) sh[threadIdx.x] += sh[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) dbp[c] = sh[0];
+}
+
+// db_ih[d] = sum over batch tiles of dbp[.][d][0..2], db_hh[d][:2H] = the same r, z sums
+// (dgh's r, z columns are dgx's), db_hh[d][2H:] = the n sums of dgh
+__global__ void gru_db_final_kernel(const double* __restrict__ dbp, int BT, int D, int H,
+                                    float* __restrict__ dbi_f, float* __restrict__ dbh_f,
+                                    float* __restrict__ dbi_r, float* __restrict__ dbh_r) {
+  const int total = D * 4 * H;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int d = i / (4 * H), k = i - d * 4 * H;
+    double acc = 0.0;
+    for (int b = 0; b < BT; ++b) acc += dbp[(int64_t)b * total + i];
+    const float v = static_cast<float>(acc);
+    float* dbi = d == 0 ? dbi_f : dbi_r;
+    float* dbh = d == 0 ? dbh_f : dbh_r;
+    if (k < 3 * H) dbi[k] = v;
+    if (k < 2 * H) dbh[k] = v;
+    if (k >= 3 * H) dbh[k - H] = v;
   }
 }
 
@@ -1249,12 +1312,23 @@ ds2_status_t ds2_gru_fwd(int t_max, int n, int h, int num_dirs, const float* xpr
   return launch_status("ds2_gru_fwd");
 }
 
-size_t ds2_gru_bwd_workspace_size(int n, int h, int num_dirs) {
+static size_t gru_bwd_ws_base(int n, int h, int num_dirs) {
   const int64_t UB = (h + GU - 1) / GU;
   const int64_t KS = (3 * h + 3) / 4;
   return align256((size_t)(num_dirs * UB * KS * 64) * sizeof(float)) +
          align256((size_t)2 * n * num_dirs * h * sizeof(float)) +
          align256(counter_bytes(n, num_dirs)) + ring_bytes(n, h, num_dirs, 3) + 512;
+}
+
+// bias-gradient partial sums [batch tile][direction][4][H] fp64, at the end of the workspace
+static size_t gru_db_bytes(int n, int h, int num_dirs) {
+  return align256((size_t)((n + GB - 1) / GB) * num_dirs * 4 * h * sizeof(double));
+}
+
+size_t ds2_gru_bwd_workspace_size(int n, int h, int num_dirs) {
+  const int64_t UB = (h + GU - 1) / GU;
+  const int64_t KS = (3 * h + 3) / 4;
+  return gru_bwd_ws_base(n, h, num_dirs) + gru_db_bytes(n, h, num_dirs);
 }
 
 #define DS2_BWD_CASE(K)                                                                     \
@@ -1268,14 +1342,66 @@ ds2_status_t ds2_gru_bwd(int t_max, int n, int h, int num_dirs, const float* dy,
                          const float* w_hh_f, const float* w_hh_r, const float* h_all,
                          const float* gates, const int* lens, float* dgates_x, float* dgates_h,
                          unsigned* err_out, void* ws, size_t ws_bytes, ds2_stream_t stream) {
+  return ds2_gru_bwd_bias(t_max, n, h, num_dirs, dy, dy_dirs, w_hh_f, w_hh_r, h_all, gates, lens,
+                          dgates_x, dgates_h, nullptr, nullptr, nullptr, nullptr, err_out, ws,
+                          ws_bytes, stream);
+}
+
+// the recurrence; then, with db_ih_f non-null, the bias gradients (summed by the
+// direct-operand kernel itself, else from dgates_x / dgates_h)
+static ds2_status_t gru_bwd_run(int t_max, int n, int h, int num_dirs, const float* dy, int dy_dirs,
+                                const float* w_hh_f, const float* w_hh_r, const float* h_all,
+                                const float* gates, const int* lens, float* dgates_x,
+                                float* dgates_h, unsigned* err_out, void* ws, hipStream_t st,
+                                double* dbp, bool& summed);
+
+ds2_status_t ds2_gru_bwd_bias(int t_max, int n, int h, int num_dirs, const float* dy, int dy_dirs,
+                              const float* w_hh_f, const float* w_hh_r, const float* h_all,
+                              const float* gates, const int* lens, float* dgates_x,
+                              float* dgates_h, float* db_ih_f, float* db_hh_f, float* db_ih_r,
+                              float* db_hh_r, unsigned* err_out, void* ws, size_t ws_bytes,
+                              ds2_stream_t stream) {
   if (t_max < 0 || n < 0 || h < 1 || (num_dirs != 1 && num_dirs != 2)) return DS2_INVALID_VALUE;
-  if (t_max == 0 || n == 0) return DS2_OK;
   if (gates == nullptr) return DS2_INVALID_VALUE;
   if (dy_dirs != 1 && dy_dirs != num_dirs) return DS2_INVALID_VALUE;
+  const bool want_db = db_ih_f != nullptr;
+  if (want_db && (db_hh_f == nullptr || (num_dirs == 2 && (db_ih_r == nullptr || db_hh_r == nullptr))))
+    return DS2_INVALID_VALUE;
   if (ws == nullptr || ws_bytes < ds2_gru_bwd_workspace_size(n, h, num_dirs))
     return DS2_WORKSPACE_TOO_SMALL;
-  if (num_dirs == 1) w_hh_r = w_hh_f;
   hipStream_t st = as_stream(stream);
+  double* dbp = reinterpret_cast<double*>(static_cast<char*>(ws) + gru_bwd_ws_base(n, h, num_dirs));
+  if (t_max == 0 || n == 0) {
+    if (!want_db) return DS2_OK;
+    // no rows: zero bias gradients
+    if (hipMemsetAsync(dbp, 0, gru_db_bytes(n > 0 ? n : 1, h, num_dirs), st) != hipSuccess)
+      return launch_status("ds2_gru_bwd_bias");
+    hipLaunchKernelGGL(gru_db_final_kernel, dim3(cdiv(num_dirs * 4 * h, 256)), dim3(256), 0, st,
+                       dbp, 1, num_dirs, h, db_ih_f, db_hh_f, db_ih_r, db_hh_r);
+    return launch_status("ds2_gru_bwd_bias");
+  }
+  bool summed = false;
+  const ds2_status_t rc = gru_bwd_run(t_max, n, h, num_dirs, dy, dy_dirs, w_hh_f, w_hh_r, h_all,
+                                      gates, lens, dgates_x, dgates_h, err_out, ws, st,
+                                      want_db ? dbp : nullptr, summed);
+  if (rc != DS2_OK || !want_db) return rc;
+  int bt = (n + GB - 1) / GB;
+  if (!summed) {
+    hipLaunchKernelGGL(gru_db_cols_kernel, dim3(num_dirs * 4 * h), dim3(256), 0, st, dgates_x,
+                       dgates_h, t_max * n, num_dirs, h, dbp);
+    bt = 1;
+  }
+  hipLaunchKernelGGL(gru_db_final_kernel, dim3(cdiv(num_dirs * 4 * h, 256)), dim3(256), 0, st, dbp,
+                     bt, num_dirs, h, db_ih_f, db_hh_f, db_ih_r, db_hh_r);
+  return launch_status("ds2_gru_bwd_bias");
+}
+
+static ds2_status_t gru_bwd_run(int t_max, int n, int h, int num_dirs, const float* dy, int dy_dirs,
+                                const float* w_hh_f, const float* w_hh_r, const float* h_all,
+                                const float* gates, const int* lens, float* dgates_x,
+                                float* dgates_h, unsigned* err_out, void* ws, hipStream_t st,
+                                double* dbp, bool& summed) {
+  if (num_dirs == 1) w_hh_r = w_hh_f;
   apply_spin_limit_env();
   apply_rnn_tune_env();
   const int UB = (h + GU - 1) / GU;
@@ -1300,7 +1426,7 @@ ds2_status_t ds2_gru_bwd(int t_max, int n, int h, int num_dirs, const float* dy,
     float* ring = reinterpret_cast<float*>(reinterpret_cast<char*>(ctrs) +
                                            align256(counter_bytes(n, num_dirs)));
     void* args[] = {&T_, &N_, &H_, &D_, &UB_, &BT_, &dy, &DYD_, &w_hh_f, &w_hh_r, &h_all,
-                    &gates, &lens, &dgates_x, &dgates_h, &ring, &ctrs, &err, &stamps};
+                    &gates, &lens, &dgates_x, &dgates_h, &ring, &ctrs, &err, &stamps, &dbp};
     const int hmb = handoff_mode(false);
     if (hmb != 0 && ring_reset(ring, n, h, num_dirs, 3, st) != hipSuccess)
       return launch_status("ds2_gru ring");
@@ -1314,6 +1440,7 @@ ds2_status_t ds2_gru_bwd(int t_max, int n, int h, int num_dirs, const float* dy,
     if (fn != nullptr &&
         hipLaunchCooperativeKernel(fn, dim3(grid), dim3(GT), args, kDopPadLds, st) == hipSuccess) {
       fold_err(err, err_out, st);
+      summed = dbp != nullptr;
       return launch_status("ds2_gru_bwd");
     }
     (void)hipGetLastError();

@@ -64,6 +64,8 @@ _PROTOS = {
     "ds2_gru_bwd_workspace_size": (_sz, [_c_int, _c_int, _c_int]),
     "ds2_gru_bwd": (_c_int, [_c_int, _c_int, _c_int, _c_int, _vp, _c_int, _vp, _vp, _vp, _vp,
                              _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
+    "ds2_gru_bwd_bias": (_c_int, [_c_int, _c_int, _c_int, _c_int, _vp, _c_int, _vp, _vp, _vp,
+                                  _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
     "ds2_lstm_fwd_workspace_size": (_sz, [_c_int, _c_int, _c_int]),
     "ds2_lstm_fwd": (_c_int, [_c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                               _vp, _vp, _vp, _vp, _sz, _vp]),

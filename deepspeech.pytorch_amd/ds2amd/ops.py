@@ -519,11 +519,12 @@ def _rnn_output(h_all, sum_dirs, nd):
     return h_all.view(t, n, nd * h)
 
 
-def _rnn_param_grads(x, h_all, dgx, dgh, weights, nd, g, need_dx, bf16=False):
+def _rnn_param_grads(x, h_all, dgx, dgh, weights, nd, g, need_dx, bf16=False, dbias=None):
     """Weight/bias/input gradients of one recurrent layer from the gate gradients.
 
     dgx = d/d(x W_ih^T + b_ih), dgh = d/d(h W_hh^T + b_hh), both [T, N, D, g]
-    (the same tensor for LSTM).  All plain GEMMs + column sums.
+    (the same tensor for LSTM).  All plain GEMMs + column sums; dbias = [db_ih, db_hh] per
+    direction already summed (the GRU backward kernel's own sums) skips the column sums.
     """
     t, n, inp = x.shape
     h = h_all.shape[-1]
@@ -538,8 +539,11 @@ def _rnn_param_grads(x, h_all, dgx, dgh, weights, nd, g, need_dx, bf16=False):
         dw_ih = grad_like(w_ih)
         sgemm(dgx, x2d, dw_ih, m=g, n=inp, k=tn, trans_a=True, lda=ld, ldb=inp, ldc=inp,
               a_off=d * g, bf16=bf16)
-        db_ih = grad_like(b_ih)
-        colsum(dgx, tn, g, ld, db_ih, off=d * g)
+        if dbias is not None:
+            db_ih, db_hh = dbias[2 * d], dbias[2 * d + 1]
+        else:
+            db_ih = grad_like(b_ih)
+            colsum(dgx, tn, g, ld, db_ih, off=d * g)
         dw_hh = grad_like(w_hh)
         if t > 1:
             # sum_t dgh_t^T h_{t-1} (fwd) / h_{t+1} (rev); h_prev = 0 at the start
@@ -549,16 +553,17 @@ def _rnn_param_grads(x, h_all, dgx, dgh, weights, nd, g, need_dx, bf16=False):
                   ldb=nd * h, ldc=h, a_off=a_off, b_off=b_off, bf16=bf16)
         else:
             dw_hh.zero_()
-        db_hh = grad_like(b_hh)
-        if dgh is dgx:
-            db_hh.copy_(db_ih)
-        elif g == 3 * h:
-            # GRU: the r and z columns of dgh are dgx's (the kernels store the same values),
-            # so only the n third needs its own column sum
-            db_hh[:2 * h].copy_(db_ih[:2 * h])
-            colsum(dgh, tn, h, ld, db_hh[2 * h:], off=d * g + 2 * h)
-        else:
-            colsum(dgh, tn, g, ld, db_hh, off=d * g)
+        if dbias is None:
+            db_hh = grad_like(b_hh)
+            if dgh is dgx:
+                db_hh.copy_(db_ih)
+            elif g == 3 * h:
+                # GRU: the r and z columns of dgh are dgx's (the kernels store the same
+                # values), so only the n third needs its own column sum
+                db_hh[:2 * h].copy_(db_ih[:2 * h])
+                colsum(dgh, tn, h, ld, db_hh[2 * h:], off=d * g + 2 * h)
+            else:
+                colsum(dgh, tn, g, ld, db_hh, off=d * g)
         if dx is not None:
             sgemm(dgx, w_ih, dx, m=tn, n=inp, k=g, lda=ld, ldb=inp, ldc=inp,
                   beta=0.0 if d == 0 else 1.0, a_off=d * g, bf16=bf16)
@@ -635,12 +640,15 @@ class GRULayerFn(torch.autograd.Function):
         w_hh_r = weights[5] if nd == 2 else None
         ws = _ws(_lib.size("ds2_gru_bwd_workspace_size", n, h, nd), dev)
         _guard_cooperative(n, h, nd)
-        _lib.call("ds2_gru_bwd", t, n, h, nd, dy.data_ptr(), dy_dirs, w_hh_f.data_ptr(),
+        # bias gradients straight into their slots, summed by the recurrence kernel
+        dbias = [grad_like(weights[4 * d + k]) for d in range(nd) for k in (2, 3)]
+        _lib.call("ds2_gru_bwd_bias", t, n, h, nd, dy.data_ptr(), dy_dirs, w_hh_f.data_ptr(),
                   _p(w_hh_r), h_all.data_ptr(), gates.data_ptr(), lens.data_ptr(), dgx.data_ptr(),
-                  dgh.data_ptr(), rnn_status_word(dev).data_ptr(), ws.data_ptr(), ws.numel(),
-                  _stream())
+                  dgh.data_ptr(), dbias[0].data_ptr(), dbias[1].data_ptr(),
+                  _p(dbias[2] if nd == 2 else None), _p(dbias[3] if nd == 2 else None),
+                  rnn_status_word(dev).data_ptr(), ws.data_ptr(), ws.numel(), _stream())
         dx, grads = _rnn_param_grads(x, h_all, dgx, dgh, weights, nd, h3,
-                                     ctx.needs_input_grad[0], bf16)
+                                     ctx.needs_input_grad[0], bf16, dbias=dbias)
         return (dx, None, None, None, *grads)
 
 

@@ -214,6 +214,18 @@ ds2_status_t ds2_gru_bwd(int t_max, int n, int h, int num_dirs, const float* dy,
                          const float* w_hh_f, const float* w_hh_r, const float* h_all,
                          const float* gates, const int* lens, float* dgates_x, float* dgates_h,
                          unsigned* err_out, void* ws, size_t ws_bytes, ds2_stream_t stream);
+/* ds2_gru_bwd plus the bias gradients of the layer (replaces the column sums of the
+ * reference's autograd over bias_ih_l* / bias_hh_l*, nn.GRU via model.py:97-109):
+ * db_ih_{f,r} [3H] = sum over rows of dgates_x, db_hh_{f,r} [3H] = sum over rows of
+ * dgates_h.  The direct-operand backward sums them while it runs (fp64, fixed order);
+ * other recurrence paths sum dgates_x / dgates_h afterwards.  db_ih_f == NULL: same as
+ * ds2_gru_bwd; with num_dirs == 1 the _r pointers may be NULL.                 */
+ds2_status_t ds2_gru_bwd_bias(int t_max, int n, int h, int num_dirs, const float* dy, int dy_dirs,
+                              const float* w_hh_f, const float* w_hh_r, const float* h_all,
+                              const float* gates, const int* lens, float* dgates_x,
+                              float* dgates_h, float* db_ih_f, float* db_hh_f, float* db_ih_r,
+                              float* db_hh_r, unsigned* err_out, void* ws, size_t ws_bytes,
+                              ds2_stream_t stream);
 
 /* ------------------------------------------------------------------------ */
 /* (Bi)directional LSTM recurrence (torch gate order i, f, g, o), same packed-
