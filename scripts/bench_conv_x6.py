@@ -31,8 +31,17 @@ def timeit(fn, iters=10):
     return a.elapsed_time(b) / iters
 
 
-for mode in ("1", "0"):
+# conv1: 32 x [1, 161, 1001] -> 32 channels, 41 x 11 taps, stride (2, 2)
+x1 = torch.randn(n, 1, 161, 1001, device=dev)
+w1 = torch.randn(co, 1, 41, 11, device=dev) * 0.1
+flop1 = 2.0 * 41 * 11 * co * n * 81 * 501
+
+for mode in ("2", "1", "0"):   # 2: + conv1 on the bf16x6 kernel (opt-in)
     os.environ["DS2_CONV_X6"] = mode
+    t1 = timeit(lambda: ops.conv2d_fwd(x1, w1, None, (2, 2), (20, 5)))
+    print(f"x6={mode}: conv1 fwd {t1:.3f} ms ({flop1 / t1 / 1e9:.1f} TF)", flush=True)
+    if mode == "2":
+        continue
     tf = timeit(lambda: ops.conv2d_fwd(x, wt, None, (sh, sw), (ph, pw)))
     td = timeit(lambda: ops.conv2d_dgrad(dy, wt, x.shape, (sh, sw), (ph, pw)))
     tw = timeit(lambda: ops.conv2d_wgrad(dy, x, tuple(wt.shape), (sh, sw), (ph, pw), with_bias=False))

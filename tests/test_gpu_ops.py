@@ -153,12 +153,13 @@ CONVS = [  # (n, ci, h, w, co, kh, kw, sh, sw, ph, pw)
 ]
 
 
-@pytest.mark.parametrize("x6", ["1", "0"])
+@pytest.mark.parametrize("x6", ["1", "2", "0"])
 @pytest.mark.parametrize("cfg", CONVS)
 def test_conv_fwd_bwd(dev, cfg, x6, monkeypatch):
     """conv fwd / dgrad / wgrad vs fp64 torch at 1e-5: the bf16x6 direct kernels (default
-    where they fit: width stride 1, <= 24 tap rows, <= 12 kernel columns) and the fp32
-    LDS-patch / implicit-GEMM kernels (DS2_CONV_X6=0)."""
+    where they fit: width stride 1, <= 24 tap rows, <= 12 kernel columns; DS2_CONV_X6=2 adds
+    the forward's width stride 2 and tap-row chunks) and the fp32 LDS-patch / implicit-GEMM
+    kernels (DS2_CONV_X6=0)."""
     monkeypatch.setenv("DS2_CONV_X6", x6)
     n, ci, h, w, co, kh, kw, sh, sw, ph, pw = cfg
     g = torch.Generator().manual_seed(sum(cfg))
@@ -209,6 +210,23 @@ def test_conv_x6_is_fp32_accurate(dev, monkeypatch):
                            for a, r in ((yd, y), (dx, dxr), (dw, dwr)))
     assert all(e1 <= 2.5 * e0 for e1, e0 in zip(errs["1"], errs["0"])), errs
     assert max(errs["1"]) < 5e-6, errs
+
+
+def test_conv1_x6_is_fp32_accurate(dev, monkeypatch):
+    """The model's conv1 (1 -> 32 channels, 41 x 11 taps, stride (2, 2): three 16-row tap
+    chunks, stride-2 patch columns) on the opt-in bf16x6 kernel (DS2_CONV_X6=2): error
+    against fp64 of the fp32 kernel's order."""
+    n, ci, h, w, co, kh, kw, sh, sw, ph, pw = 2, 1, 161, 300, 32, 41, 11, 2, 2, 20, 5
+    g = torch.Generator().manual_seed(12)
+    x = torch.randn(n, ci, h, w, generator=g, dtype=torch.float64)
+    wt = torch.randn(co, ci, kh, kw, generator=g, dtype=torch.float64) * 0.1
+    y = F.conv2d(x, wt, None, stride=(sh, sw), padding=(ph, pw))
+    errs = {}
+    for mode in ("2", "0"):
+        monkeypatch.setenv("DS2_CONV_X6", mode)
+        yd = ops.conv2d_fwd(x.float().to(dev), wt.float().to(dev), None, (sh, sw), (ph, pw))
+        errs[mode] = (yd.double().cpu() - y).abs().max().item() / y.abs().max().item()
+    assert errs["2"] <= 2.5 * errs["0"] and errs["2"] < 5e-6, errs
 
 
 # ---------------------------------------------------------------------------- BN
