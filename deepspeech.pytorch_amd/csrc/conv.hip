@@ -1211,7 +1211,16 @@ __global__ __launch_bounds__(CW_T, 2) void conv_x6_wgrad_kernel(const float* __r
   __shared__ __attribute__((aligned(16))) unsigned short ds[3 * CW_DPL];
   constexpr int kOob = 0x7ffffff0;
   const int G = (g.kh + 3) / 4;
-  const int gi = blockIdx.x % G, s = blockIdx.x / G;
+  // XCD-aware: the G tap-row groups of one split (the same x rows) get consecutive ids of
+  // one XCD's run (blocks are dealt to the XCDs round-robin), so they share its L2
+  int gi, s;
+  {
+    const int nwg = gridDim.x, o = blockIdx.x;
+    const int q = nwg >> 3, r = nwg & 7, xcd = o & 7;
+    const int id = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (o >> 3);
+    gi = id % G;
+    s = id / G;
+  }
   const int R = g.n * g.ho;
   const int r0 = static_cast<int>((int64_t)s * R / S);
   const int r1 = static_cast<int>((int64_t)(s + 1) * R / S);
