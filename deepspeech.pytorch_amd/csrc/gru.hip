@@ -1061,6 +1061,190 @@ __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Reduce-scatter backward (DS2_GRU_BWD_RS=1): each workgroup multiplies its OWN gate
+// gradients dG[16 samples][3 x 16 units] (K = 48) by the 48 rows of W_hh they belong to,
+// [48][H], into a partial dh for ALL H units, and publishes it as UB 1-KB tiles (one per
+// consuming unit block); a consumer sums the UB partial tiles of its 16 units in producer
+// order (deterministic).  Per step a workgroup reads UB KB (gru_bwd_dop_kernel: 3 UB KB, every
+// producer's three gate tiles) and writes UB KB.  Hand-off: per-producer flags (flags_wait;
+// the flag after every storing wave drained), 2-slot ring [slot][d][bt][consumer][producer]
+// [256].  Tiles are [unit][sample]: the 16x16x4 MFMA's D layout (lane l: unit l & 15,
+// samples 4 (l >> 4) .. + 3), so each lane publishes one 16-B store per consumer block.
+template <int NBK>
+__global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void gru_bwd_rs_kernel(
+    int T, int N, int H, int D, int UB, int BT, const float* __restrict__ dy, int dyd,
+    const float* __restrict__ w_f, const float* __restrict__ w_r,
+    const float* __restrict__ h_all, const float* __restrict__ gates,
+    const int* __restrict__ lens, float* __restrict__ dgx, float* __restrict__ dgh,
+    float* __restrict__ ring, unsigned* __restrict__ counters, unsigned* __restrict__ err,
+    double* __restrict__ dbp) {
+  constexpr int GP = GU + 1;                   // dG tile pitch (conflict-free A reads)
+  __shared__ __attribute__((aligned(16))) float red[GW * 256];   // [wave][unit][sample]
+  __shared__ float gt[3 * GB * GP];            // this step's dG [gate][sample][unit]
+  __shared__ int flag;
+  int ub, d, bt;
+  if (!map_work(UB * D, BT, UB, ub, d, bt)) return;
+  const int n0 = bt * GB;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int H3 = 3 * H;
+  int c0, nc;
+  simd_split(UB, wave, c0, nc);                // consumer blocks this wave produces for and
+                                               // producers whose tiles it sums (host: <= NBK)
+  const unsigned* gflags = counters + (D * BT + 1) + (d * BT + bt) * UB;
+  unsigned* myflag = counters + (D * BT + 1) + (d * BT + bt) * UB + ub;
+  const int slot_floats = D * BT * UB * UB * 256;
+  const int grp = (d * BT + bt) * UB;          // consumer index base within a slot
+  const __amdgpu_buffer_rsrc_t r_rs =
+      __builtin_amdgcn_make_buffer_rsrc(ring, (short)0, 2 * slot_floats * 4, 0x00020000);
+
+  // B operand: w[c][kk] = W_hh[(k >> 4) H + 16 ub + (k & 15)][16 (c0 + c) + (lane & 15)],
+  // k = 4 kk + (lane >> 4)
+  float w[NBK][12];
+  {
+    const float* W = d == 0 ? w_f : w_r;
+#pragma unroll
+    for (int c = 0; c < NBK; ++c)
+#pragma unroll
+      for (int kk = 0; kk < 12; ++kk) {
+        const int k = 4 * kk + (lane >> 4);
+        const int64_t row = (int64_t)(k >> 4) * H + ub * GU + (k & 15);
+        w[c][kk] = c < nc ? W[row * H + GU * (c0 + c) + (lane & 15)] : 0.f;
+      }
+#pragma unroll
+    for (int c = 0; c < NBK; ++c)
+#pragma unroll
+      for (int kk = 0; kk < 12; ++kk) settle(w[c][kk]);
+  }
+  const int m = threadIdx.x >> 4;
+  const int u = threadIdx.x & 15;
+  const int n = n0 + m;
+  const int j = ub * GU + u;
+  const bool owner = threadIdx.x < GB * GU && n < N;
+  int len = owner ? lens[n] : 0;
+  settle(len);
+  float dh_prev = 0.f, z_prev = 0.f;
+  float px_dar = 0.f, px_daz = 0.f, px_dan = 0.f, px_dghn = 0.f;
+  int64_t px_row = -1;
+  double sb_r = 0.0, sb_z = 0.0, sb_n = 0.0, sb_hn = 0.0;
+  for (int s = 0; s < T; ++s) {
+    const int t = d == 0 ? T - 1 - s : s;
+    float dyv = 0.f, g_r = 0.f, g_z = 0.f, g_n = 0.f, g_hn = 0.f, hp = 0.f;
+    const int64_t row = ((int64_t)t * N + n) * D + d;
+    if (owner && t < len) {
+      dyv = dy[(((int64_t)t * N + n) * dyd + (dyd > 1 ? d : 0)) * H + j];
+      const float* gp = gates + row * 4 * H;
+      g_r = gp[j];
+      g_z = gp[H + j];
+      g_n = gp[2 * H + j];
+      g_hn = gp[3 * H + j];
+      const int tp = d == 0 ? t - 1 : t + 1;
+      if (tp >= 0 && tp < T) hp = h_all[(((int64_t)tp * N + n) * D + d) * H + j];
+    }
+    if (s > 0) {
+      if (!flags_wait(gflags, UB, (unsigned)s, err, &flag)) {
+        poison_rest(dgx, s, T, d == 0, N, D, n, d, H, j, H3, 3, owner);
+        return;
+      }
+      // the partial tiles of producers [c0, c0 + nc) for this workgroup's units
+      const int base = (((s - 1) & 1) * slot_floats + (grp + ub) * UB * 256 + c0 * 256) * 4 + lane * 16;
+      f32x4 pv[NBK];
+#pragma unroll
+      for (int c = 0; c < NBK; ++c)
+        pv[c] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                              r_rs, c < nc ? base + c * 1024 : 0x7ffffff0, 0, kSc1));
+      f32x4 sacc = pv[0];
+#pragma unroll
+      for (int c = 1; c < NBK; ++c) sacc += pv[c];
+      *reinterpret_cast<f32x4*>(red + wave * 256 + lane * 4) = sacc;
+    }
+    settle(dyv);
+    settle(g_r);
+    settle(g_z);
+    settle(g_n);
+    settle(g_hn);
+    settle(hp);
+    __syncthreads();
+    if (threadIdx.x < GB * GU) {
+      float dar = 0.f, daz = 0.f, dghn = 0.f;
+      if (owner) {
+        float dh = 0.f, zc = 0.f, dan = 0.f;
+        if (t < len) {
+          float carry = 0.f;
+          if (s > 0) {
+            float rec = 0.f;
+#pragma unroll
+            for (int w8 = 0; w8 < GW; ++w8) rec += red[w8 * 256 + u * 16 + m];
+            carry = dh_prev * z_prev + rec;
+          }
+          dh = dyv + carry;
+          zc = g_z;
+          dan = dh * (1.f - zc) * (1.f - g_n * g_n);
+          daz = dh * (hp - g_n) * zc * (1.f - zc);
+          dar = dan * g_hn * g_r * (1.f - g_r);
+          dghn = dan * g_r;
+        }
+        dh_prev = dh;
+        z_prev = zc;
+        px_dar = dar; px_daz = daz; px_dan = dan; px_dghn = dghn; px_row = row;
+        sb_r += dar; sb_z += daz; sb_n += dan; sb_hn += dghn;
+      }
+      gt[(0 * GB + m) * GP + u] = dar;
+      gt[(1 * GB + m) * GP + u] = daz;
+      gt[(2 * GB + m) * GP + u] = dghn;
+    }
+    __syncthreads();
+    // partial dh of every unit block c: [16 samples] x [K = 48] . [48] x [16 units]
+    float a[12];
+#pragma unroll
+    for (int kk = 0; kk < 12; ++kk) {
+      const int k = 4 * kk + (lane >> 4);
+      a[kk] = gt[((k >> 4) * GB + (lane & 15)) * GP + (k & 15)];
+    }
+    const int so = ((s & 1) * slot_floats + grp * UB * 256 + ub * 256) * 4 +
+                   ((lane & 15) * 16 + 4 * (lane >> 4)) * 4;
+#pragma unroll
+    for (int c = 0; c < NBK; ++c) {
+      if (c < nc) {
+        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kk = 0; kk < 12; ++kk) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[kk], w[c][kk], acc, 0, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc), r_rs,
+                                               so + (c0 + c) * UB * 1024, 0, kSc1);
+      }
+    }
+    flags_arrive(myflag, (unsigned)s + 1);
+    if (owner) {
+      float* gxr = dgx + px_row * H3;
+      gxr[j] = px_dar;
+      gxr[H + j] = px_daz;
+      gxr[2 * H + j] = px_dan;
+      float* ghr = dgh + px_row * H3;
+      ghr[j] = px_dar;
+      ghr[H + j] = px_daz;
+      ghr[2 * H + j] = px_dghn;
+    }
+  }
+  if (dbp == nullptr) return;
+  double* rd = reinterpret_cast<double*>(red);   // 1024 doubles fit in red
+  __syncthreads();
+  if (threadIdx.x < GB * GU) {
+    rd[(0 * GB + m) * GU + u] = owner ? sb_r : 0.0;
+    rd[(1 * GB + m) * GU + u] = owner ? sb_z : 0.0;
+    rd[(2 * GB + m) * GU + u] = owner ? sb_n : 0.0;
+    rd[(3 * GB + m) * GU + u] = owner ? sb_hn : 0.0;
+  }
+  __syncthreads();
+  if (threadIdx.x < 4 * GU) {
+    const int g = threadIdx.x / GU, uu = threadIdx.x - (threadIdx.x / GU) * GU;
+    double acc = 0.0;
+#pragma unroll
+    for (int mm = 0; mm < GB; ++mm) acc += rd[(g * GB + mm) * GU + uu];
+    dbp[(((int64_t)bt * D + d) * 4 + g) * H + ub * GU + uu] = acc;
+  }
+}
+
 // Bias gradients from dgx / dgh when the recurrence kernel did not sum them (every path
 // but the direct-operand backward): one block per (direction, gate column), fixed order.
 __global__ void gru_db_cols_kernel(const float* __restrict__ dgx, const float* __restrict__ dgh,
@@ -1325,10 +1509,29 @@ static size_t gru_db_bytes(int n, int h, int num_dirs) {
   return align256((size_t)((n + GB - 1) / GB) * num_dirs * 4 * h * sizeof(double));
 }
 
+// reduce-scatter backward's ring: 2 slots x D x BT x UB consumers x UB producers x 1 KB
+static size_t gru_rs_ring_bytes(int n, int h, int num_dirs) {
+  const size_t UB = (h + GU - 1) / GU, BT = (n + GB - 1) / GB;
+  return align256(2 * (size_t)num_dirs * BT * UB * UB * 256 * sizeof(float));
+}
+
 size_t ds2_gru_bwd_workspace_size(int n, int h, int num_dirs) {
-  const int64_t UB = (h + GU - 1) / GU;
-  const int64_t KS = (3 * h + 3) / 4;
-  return gru_bwd_ws_base(n, h, num_dirs) + gru_db_bytes(n, h, num_dirs);
+  return gru_bwd_ws_base(n, h, num_dirs) + gru_db_bytes(n, h, num_dirs) +
+         gru_rs_ring_bytes(n, h, num_dirs);
+}
+
+// reduce-scatter backward (gru_bwd_rs_kernel): DS2_GRU_BWD_RS=1 selects it
+static inline bool rs_enabled() {
+  const char* e = getenv("DS2_GRU_BWD_RS");
+  return e != nullptr && e[0] == '1';
+}
+
+static const void* bwd_rs_fn(int need) {
+#define DS2_BRS(K) \
+  if (need <= K) return reinterpret_cast<const void*>(gru_bwd_rs_kernel<K>);
+  DS2_BRS(1) DS2_BRS(2) DS2_BRS(3) DS2_BRS(4) DS2_BRS(5) DS2_BRS(6) DS2_BRS(7) DS2_BRS(8)
+#undef DS2_BRS
+  return nullptr;
 }
 
 #define DS2_BWD_CASE(K)                                                                     \
@@ -1427,6 +1630,20 @@ static ds2_status_t gru_bwd_run(int t_max, int n, int h, int num_dirs, const flo
                                            align256(counter_bytes(n, num_dirs)));
     void* args[] = {&T_, &N_, &H_, &D_, &UB_, &BT_, &dy, &DYD_, &w_hh_f, &w_hh_r, &h_all,
                     &gates, &lens, &dgates_x, &dgates_h, &ring, &ctrs, &err, &stamps, &dbp};
+    if (rs_enabled() && dbp != nullptr) {
+      // blocks per wave of simd_split(UB): ceil(ceil(UB / 4) / 2) at most
+      const void* rfn = bwd_rs_fn(((UB + 3) / 4 + 1) / 2);
+      float* rring = reinterpret_cast<float*>(reinterpret_cast<char*>(dbp) + gru_db_bytes(n, h, num_dirs));
+      void* rargs[] = {&T_, &N_, &H_, &D_, &UB_, &BT_, &dy, &DYD_, &w_hh_f, &w_hh_r, &h_all,
+                       &gates, &lens, &dgates_x, &dgates_h, &rring, &ctrs, &err, &dbp};
+      if (rfn != nullptr &&
+          hipLaunchCooperativeKernel(rfn, dim3(grid), dim3(GT), rargs, kDopPadLds, st) == hipSuccess) {
+        fold_err(err, err_out, st);
+        summed = true;
+        return launch_status("ds2_gru_bwd");
+      }
+      (void)hipGetLastError();
+    }
     const int hmb = handoff_mode(false);
     if (hmb != 0 && ring_reset(ring, n, h, num_dirs, 3, st) != hipSuccess)
       return launch_status("ds2_gru ring");

@@ -406,6 +406,37 @@ def test_gru_direct_operand_equals_staged(dev, n, h, bidir, monkeypatch):
         _close(a, b, 2e-5, "direct-operand vs staged")
 
 
+@pytest.mark.parametrize("n,h,bidir", [(32, 64, True), (20, 800, True), (7, 48, False),
+                                       (17, 784, True)])
+def test_gru_reduce_scatter_backward(dev, n, h, bidir, monkeypatch):
+    """The reduce-scatter backward (each workgroup multiplies its own gate gradients into
+    partial dh tiles for every unit block; consumers sum them) against the direct-operand
+    backward: the same gradients within fp32 rounding (the K sum is split differently),
+    finite, bias gradients included."""
+    t, inp = 33, 40
+    nd = 2 if bidir else 1
+    g = torch.Generator().manual_seed(h + 5 * n)
+    a = 0.2 if h <= 64 else h ** -0.5
+    weights = [torch.rand(s, generator=g) * 2 * a - a for s in
+               [(3 * h, inp), (3 * h, h), (3 * h,), (3 * h,)] * nd]
+    lens = torch.tensor(sorted([t - (i % 6) * 5 for i in range(n)], reverse=True),
+                        dtype=torch.int32)
+    x = torch.randn(t, n, inp, generator=g)
+    dy = torch.randn(t, n, h, generator=g)
+    outs = []
+    for rs in ("0", "1"):
+        monkeypatch.setenv("DS2_GRU_BWD_RS", rs)
+        ws = [w.to(dev).requires_grad_(True) for w in weights]
+        xd = x.to(dev).requires_grad_(True)
+        y = ops.GRULayerFn.apply(xd, lens.to(dev), True, h, *ws)
+        y.backward(dy.to(dev))
+        torch.cuda.synchronize()
+        outs.append([xd.grad.cpu()] + [w.grad.cpu() for w in ws])
+    for a_, b_ in zip(*outs):
+        assert torch.isfinite(b_).all()
+        _close(b_, a_, 2e-5, "reduce-scatter vs direct-operand backward")
+
+
 @pytest.mark.parametrize("n,h,bidir", [(32, 64, True), (20, 800, True), (7, 48, False)])
 def test_gru_handoff_forms_agree(dev, n, h, bidir, monkeypatch):
     """The per-producer-flag, sentinel-ring and hybrid (flag poll + sentinel-validated
