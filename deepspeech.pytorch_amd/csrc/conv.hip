@@ -1335,6 +1335,222 @@ __global__ __launch_bounds__(CW_T, 2) void conv_x6_wgrad_kernel(const float* __r
     }
 }
 
+// ---------------------------------------------------------------------------
+// bf16x6 dgrad with 4-row x 2-column fragments (default for <= 12 class tap rows and <= 12
+// kernel columns: conv2's 11 x 11 class taps take 3 x 3 k-steps of 16 taps -- 144 tap slots
+// for 121 -- instead of the 8-row fragments' 2 x 6 -- 192).  K order of k-step (row quad rq,
+// column quad cq): lane half h takes tap rows 4 rq .. + 3 x tap columns 4 cq + 2 h, + 1
+// (element 2 r + c).  The patch is stored as column PAIRS, [pair][row][2], twice -- pairs
+// starting at even columns (E) and at odd columns (O) -- so a lane's 8 values are one 16-B run
+// whatever the parity of its first column.  Pair pitch 24 bf16 (3 x 16 B) and the O copy 128 B
+// off the E copy's bank phase: the 8 E and 8 O lanes of a b128 lane group hit 16 distinct
+// 16-B bank slots.  Workgroup, waves, weight staging and epilogue as conv_x6_kernel's dgrad.
+constexpr int CQ_ROWS = 12;                          // class tap rows, padded to 4
+constexpr int CQ_PP = 2 * CQ_ROWS;                   // bf16 per column pair
+constexpr int CQ_PAIRS = (CX_COLS + 11 + 1) / 2;     // pairs per copy (<= 12 kernel columns)
+constexpr int CQ_OFFO = 3264;                        // O copy (bf16): 6528 B = 128 mod 256
+constexpr int CQ_PPL = 6656;                         // bf16 per plane: 13312 B = 0 mod 256
+constexpr int CQ_NK = 9;                             // 3 row quads x 3 column quads
+constexpr int CQ_COP = 152;                          // weight-image ci pitch: 8 x odd >= 144
+constexpr int CQ_UNITS = 2 * CQ_PAIRS * 3;           // staging units (copy, pair, row quad)
+static_assert(CQ_OFFO >= CQ_PAIRS * CQ_PP && CQ_OFFO + CQ_PAIRS * CQ_PP <= CQ_PPL, "patch plane");
+static_assert(CQ_UNITS <= 2 * CX_T, "two staging units per thread");
+
+// pre-split weight image [class][mb][co][plane][32 ci][CQ_COP]: k-step st, half h, element e
+__global__ void conv_x6q_wimg_kernel(const float* __restrict__ w, ConvDims g,
+                                     unsigned short* __restrict__ img) {
+  const int M = g.ci, L = g.co;
+  const int mbn = (M + 31) / 32;
+  const int64_t per = (int64_t)32 * CQ_COP;
+  const int64_t total = (int64_t)g.sh * mbn * L * per;
+  const int KHW = g.kh * g.kw;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t r = i;
+    const int e = static_cast<int>(r % per); r /= per;
+    const int l = static_cast<int>(r % L); r /= L;
+    const int mb = static_cast<int>(r % mbn); r /= mbn;
+    const int q = static_cast<int>(r);
+    const int mm = e / CQ_COP, slot = e - mm * CQ_COP;
+    const int m = mb * 32 + mm;
+    float v = 0.f;
+    if (slot < CQ_NK * 16 && m < M) {
+      const int st = slot >> 4, h = (slot >> 3) & 1, x = slot & 7;
+      const int a = 4 * (st / 3) + (x >> 1), b = 4 * (st % 3) + 2 * h + (x & 1);
+      const int aq = class_taps(g, q);
+      if (a < aq && b < g.kw)
+        v = w[((int64_t)l * g.ci + m) * KHW + (q + g.sh * (aq - 1 - a)) * g.kw + (g.kw - 1 - b)];
+    }
+    const __bf16 hb = (__bf16)v;
+    const float r1 = v - (float)hb;
+    const __bf16 mbf = (__bf16)r1;
+    const __bf16 lb = (__bf16)(r1 - (float)mbf);
+    const int64_t base = ((((int64_t)q * mbn + mb) * L + l) * 3) * per + e;
+    img[base] = __builtin_bit_cast(unsigned short, hb);
+    img[base + per] = __builtin_bit_cast(unsigned short, mbf);
+    img[base + 2 * per] = __builtin_bit_cast(unsigned short, lb);
+  }
+}
+
+__global__ __launch_bounds__(CX_T, 1) void conv_x6q_dgrad_kernel(const float* __restrict__ dy,
+                                                                 const unsigned short* __restrict__ img,
+                                                                 float* __restrict__ dx, ConvDims g,
+                                                                 int gx, int gy) {
+  __shared__ __attribute__((aligned(16))) unsigned short ps[3 * CQ_PPL];
+  __shared__ __attribute__((aligned(16))) unsigned short ws[3 * 32 * CQ_COP];
+  const int M = g.ci, L = g.co;
+  const int in_h = g.ho, in_w = g.wo, out_h = g.hi, out_w = g.wi;
+  const int mbn = (M + 31) / 32;
+  int bx, by, bz;
+  xcd_tile(gx, gy, bx, by, bz);
+  const int n = bz / mbn;
+  const int mb = bz - n * mbn;
+  const int m0 = mb * 32;
+  const int c0 = bx * CX_COLS;
+  int t = by, hq = 0, q;
+  for (q = 0; q < g.sh; ++q) {
+    hq = ((q - g.ph) % g.sh + g.sh) % g.sh;
+    const int cnt = hq < g.hi ? (g.hi - 1 - hq) / g.sh + 1 : 0;
+    if (t < cnt) break;
+    t -= cnt;
+  }
+  const int A = class_taps(g, q);
+  const int orow = hq + g.sh * t;
+  const int prow0 = (orow + g.ph - q) / g.sh - (A - 1);
+  const int pcol0 = c0 + g.pw - g.kw + 1;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int cw = wave & 3, kk = wave >> 2;
+  const int plane_in = in_h * in_w;
+  const float* inn = dy + (int64_t)n * L * plane_in;
+  constexpr int WPL = 32 * CQ_COP;
+  constexpr int wstride = 3 * WPL;
+  const unsigned short* wimg = img + ((int64_t)q * mbn + mb) * L * wstride;
+  constexpr int wchunks = wstride / 8;
+
+  float rp[2][8];
+  u32x4 rw[(wchunks + CX_T - 1) / CX_T];
+  auto load = [&](int l) {
+    const __amdgpu_buffer_rsrc_t rs = conv_rsrc(inn + (int64_t)l * plane_in, plane_in);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int unit = tid + CX_T * u;
+      const int cp = unit / (CQ_PAIRS * 3), rem = unit - cp * (CQ_PAIRS * 3);
+      const int j = rem / 3, rq = rem - (rem / 3) * 3;
+      const int col = pcol0 + 2 * j + cp;          // the pair's first column
+#pragma unroll
+      for (int x = 0; x < 8; ++x) {
+        const int a = 4 * rq + (x >> 1), ir = prow0 + a, ic = col + (x & 1);
+        const bool ok = unit < CQ_UNITS && a < A && ir >= 0 && ir < in_h && ic >= 0 && ic < in_w;
+        rp[u][x] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                 rs, ok ? (ir * in_w + ic) * 4 : 0x7ffffff0, 0, 0));
+      }
+    }
+    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<unsigned short*>(wimg + (int64_t)l * wstride), (short)0, wstride * 2, 0x00020000);
+#pragma unroll
+    for (int r = 0; r < (wchunks + CX_T - 1) / CX_T; ++r) {
+      const int i = tid + CX_T * r;
+      rw[r] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                            wr, i < wchunks ? i * 16 : 0x7ffffff0, 0, 0));
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int unit = tid + CX_T * u;
+      if (unit < CQ_UNITS) {
+        const int cp = unit / (CQ_PAIRS * 3), rem = unit - cp * (CQ_PAIRS * 3);
+        const int j = rem / 3, rq = rem - (rem / 3) * 3;
+        cw_split_store(ps, CQ_PPL, cp * CQ_OFFO + j * CQ_PP + 8 * rq, rp[u]);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < (wchunks + CX_T - 1) / CX_T; ++r) {
+      const int i = tid + CX_T * r;
+      if (i < wchunks) *reinterpret_cast<u32x4*>(ws + 8 * i) = rw[r];
+    }
+  };
+
+  f32x16 acc[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+  const int fr = lane & 31, fh = lane >> 5;
+  const bool active = orow < out_h && c0 + 64 * cw < out_w;
+  constexpr int H0 = (CQ_NK + 1) / 2;
+
+  load(0);
+  store();
+  __syncthreads();
+  for (int l = 0; l < L; ++l) {
+    if (l + 1 < L) load(l + 1);
+    if (active) {
+      auto kstep = [&](int st) {
+        const int rq = st / 3, cq = st - (st / 3) * 3;
+        bf16x8 af[3], bfr[2][3];
+        const int aw = fr * CQ_COP + (st * 2 + fh) * 8;
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) af[pl] = *reinterpret_cast<const bf16x8*>(ws + pl * WPL + aw);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int sc = 64 * cw + 32 * j + fr + 4 * cq + 2 * fh;   // first patch column
+          const int ap = (sc & 1) * CQ_OFFO + (sc >> 1) * CQ_PP + 8 * rq;
+#pragma unroll
+          for (int pl = 0; pl < 3; ++pl)
+            bfr[j][pl] = *reinterpret_cast<const bf16x8*>(ps + pl * CQ_PPL + ap);
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          f32x16 cc = acc[j];
+          cc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1], bfr[j][1], cc, 0, 0, 0);
+          cc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[2], bfr[j][0], cc, 0, 0, 0);
+          cc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bfr[j][2], cc, 0, 0, 0);
+          cc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1], bfr[j][0], cc, 0, 0, 0);
+          cc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bfr[j][1], cc, 0, 0, 0);
+          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bfr[j][0], cc, 0, 0, 0);
+        }
+      };
+      if (kk == 0) {
+#pragma unroll
+        for (int st = 0; st < H0; ++st) kstep(st);
+      } else {
+#pragma unroll
+        for (int st = H0; st < CQ_NK; ++st) kstep(st);
+      }
+    }
+    __syncthreads();
+    if (l + 1 < L) {
+      store();
+      __syncthreads();
+    }
+  }
+  // the two k halves meet in LDS (the patch area): half 1 writes, half 0 adds (fixed order)
+  float* red = reinterpret_cast<float*>(ps);
+  if (kk == 1) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) red[((cw * 2 + j) * 16 + r) * 64 + lane] = acc[j][r];
+  }
+  __syncthreads();
+  if (kk == 1 || !active) return;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int col = c0 + 64 * cw + 32 * j + fr;
+    if (col >= out_w) continue;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int m = m0 + (r & 3) + 8 * (r >> 2) + 4 * fh;
+      if (m < M)
+        dx[(((int64_t)n * M + m) * out_h + orow) * out_w + col] =
+            acc[j][r] + red[((cw * 2 + j) * 16 + r) * 64 + lane];
+    }
+  }
+}
+
 static inline bool make_dims(ConvDims& g, int n, int c_in, int h_in, int w_in, int c_out, int kh,
                              int kw, int sh, int sw, int ph, int pw) {
   if (n < 0 || c_in < 1 || h_in < 1 || w_in < 1 || c_out < 1 || kh < 1 || kw < 1 || sh < 1 ||
@@ -1380,6 +1596,38 @@ static inline bool x6_ok(const ConvDims& g, bool dgrad) {
   if (c.PCOL * (c.KA / 8) > CX_PU * CX_T || 3 * 32 * c.COP / 8 > CX_WQ * CX_T) return false;
   const int64_t plane = dgrad ? (int64_t)g.ho * g.wo : (int64_t)g.hi * g.wi;
   return plane * 4 < (1ll << 31) - 64;
+}
+
+// the 4 x 2-fragment dgrad (conv_x6q_dgrad_kernel): width stride 1, <= 12 class tap rows and
+// <= 12 kernel columns (DS2_CONV_X6Q=0 or DS2_CONV_X6=0 selects the other kernels)
+static inline bool x6q_ok(const ConvDims& g) {
+  const char* e = getenv("DS2_CONV_X6");
+  if (e != nullptr && e[0] == '0') return false;
+  const char* f = getenv("DS2_CONV_X6Q");
+  if (f != nullptr && f[0] == '0') return false;
+  if (g.sw != 1 || g.kw < 1 || g.kw > 12 || class_taps(g, 0) > CQ_ROWS) return false;
+  const int64_t plane = (int64_t)g.ho * g.wo;
+  const int64_t wimg = (int64_t)g.co * 3 * 32 * CQ_COP * 2;
+  return plane * 4 < (1ll << 31) - 64 && wimg < (1ll << 31) - 64;
+}
+
+static size_t x6q_ws_bytes(const ConvDims& g) {
+  if (!x6q_ok(g)) return 0;
+  return (size_t)g.sh * ((g.ci + 31) / 32) * g.co * 3 * 32 * CQ_COP * sizeof(unsigned short);
+}
+
+static ds2_status_t launch_x6q(const float* dy, const float* w, float* dx, const ConvDims& g,
+                               void* ws, hipStream_t st) {
+  unsigned short* img = static_cast<unsigned short*>(ws);
+  const int64_t total = (int64_t)x6q_ws_bytes(g) / 6;
+  hipLaunchKernelGGL(conv_x6q_wimg_kernel, dim3(cdiv(total, 256) > 2048 ? 2048 : cdiv(total, 256)),
+                     dim3(256), 0, st, w, g, img);
+  const int gx = cdiv(g.wi, CX_COLS);
+  const int64_t nwg = (int64_t)gx * g.hi * g.n * cdiv(g.ci, 32);
+  if (nwg > 0x7fffffff) return DS2_UNSUPPORTED_SHAPE;
+  hipLaunchKernelGGL(conv_x6q_dgrad_kernel, dim3(static_cast<unsigned>(nwg)), dim3(CX_T), 0, st, dy,
+                     img, dx, g, gx, g.hi);
+  return launch_status("ds2_conv2d_dgrad");
 }
 
 static size_t x6_ws_bytes(const ConvDims& g, bool dgrad) {
@@ -1514,6 +1762,7 @@ size_t ds2_conv2d_workspace_size(int n, int c_in, int h_in, int w_in, int c_out,
   size_t a = patch_ws_bytes(g, false), b = patch_ws_bytes(g, true);
   a = a > x6_ws_bytes(g, false) ? a : x6_ws_bytes(g, false);
   b = b > x6_ws_bytes(g, true) ? b : x6_ws_bytes(g, true);
+  b = b > x6q_ws_bytes(g) ? b : x6q_ws_bytes(g);
   return (a > b ? a : b) + 256;
 }
 
@@ -1545,6 +1794,10 @@ ds2_status_t ds2_conv2d_dgrad(const float* dy, const float* w, float* dx, int n,
   ConvDims g;
   if (!make_dims(g, n, c_in, h_in, w_in, c_out, kh, kw, sh, sw, ph, pw)) return DS2_INVALID_VALUE;
   if (n == 0) return DS2_OK;
+  if (x6q_ok(g)) {
+    if (ws == nullptr || ws_bytes < x6q_ws_bytes(g)) return DS2_WORKSPACE_TOO_SMALL;
+    return launch_x6q(dy, w, dx, g, ws, as_stream(stream));
+  }
   if (x6_ok(g, true)) {
     if (ws == nullptr || ws_bytes < x6_ws_bytes(g, true)) return DS2_WORKSPACE_TOO_SMALL;
     return launch_x6<true>(dy, w, nullptr, dx, g, nullptr, ws, as_stream(stream));
