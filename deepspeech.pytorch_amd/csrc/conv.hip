@@ -349,20 +349,35 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ partial, int N, in
   }
 }
 
-// dbias[co] = sum over (n, ho, wo) of dy; one block per channel.
-__global__ void bias_grad_kernel(const float* __restrict__ dy, int N, int C, int64_t plane,
-                                 float* __restrict__ db) {
+// dbias[co] = sum over (n, ho, wo) of dy; one 1024-thread block per channel, eight loads
+// in flight per thread (a channel is N planes: 5.2 MB for conv1), fp64 sums in a fixed order.
+constexpr int BG_T = 1024;
+__global__ __launch_bounds__(BG_T) void bias_grad_kernel(const float* __restrict__ dy, int N, int C,
+                                                         int64_t plane, float* __restrict__ db) {
   const int c = blockIdx.x;
   double acc = 0.0;
   for (int n = 0; n < N; ++n) {
     const float* p = dy + ((int64_t)n * C + c) * plane;
-    for (int64_t i = threadIdx.x; i < plane; i += blockDim.x) acc += p[i];
+    int64_t i = threadIdx.x;
+    for (; i + 7 * BG_T < plane; i += 8 * BG_T) {
+      float v[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = p[i + k * BG_T];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc += v[k];
+    }
+    for (; i < plane; i += BG_T) acc += p[i];
   }
-  __shared__ double red[4];
+  __shared__ double red[BG_T / 64];
   acc = wave_sum_d(acc);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
   __syncthreads();
-  if (threadIdx.x == 0) db[c] = static_cast<float>(red[0] + red[1] + red[2] + red[3]);
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+#pragma unroll
+    for (int w = 0; w < BG_T / 64; ++w) t += red[w];
+    db[c] = static_cast<float>(t);
+  }
 }
 
 // XCD-aware decode of a 3-D grid launched as gx*gy*gz 1-D blocks: the blocks one XCD
@@ -721,12 +736,14 @@ __global__ __launch_bounds__(256) void conv_wgrad_patch_kernel(const float* __re
   const int prow = (WG_RW - 1) * g.sh + g.kh;          // patch rows
   const int pcol = (WG_CW - 1) * g.sw + g.kw;          // patch columns
   const int pe = prow * pcol;
+  // band = an equal share of the sample's (row chunk, column tile) list, so every
+  // workgroup of a launch carries the same MFMA work (whole row-chunk bands left a third of
+  // conv1's workgroups idle or in a half-empty second round)
   const int rchunks = (g.ho + WG_RW - 1) / WG_RW;
-  const int per_band = (rchunks + bands - 1) / bands;
-  const int rc0 = band * per_band;
-  const int rc1 = min(rchunks, rc0 + per_band);
   const int ctiles = (g.wo + WG_CW - 1) / WG_CW;
-  const int nchunks = (rc1 - rc0) * ctiles;
+  const int nck = rchunks * ctiles;
+  const int kc0 = static_cast<int>((int64_t)band * nck / bands);
+  const int nchunks = static_cast<int>((int64_t)(band + 1) * nck / bands) - kc0;
   const int dplane = g.ho * g.wo;
   const int xplane = g.hi * g.wi;
   const __amdgpu_buffer_rsrc_t drs =
@@ -743,9 +760,10 @@ __global__ __launch_bounds__(256) void conv_wgrad_patch_kernel(const float* __re
 
   float rd[DYREG], rx[XREG];
   auto load = [&](int k) {
-    const int rc = rc0 + k / ctiles;
+    const int kk = kc0 + k;
+    const int rc = kk / ctiles;
     const int ho0 = rc * WG_RW;
-    const int wo0 = (k - (k / ctiles) * ctiles) * WG_CW;
+    const int wo0 = (kk - rc * ctiles) * WG_CW;
 #pragma unroll
     for (int r = 0; r < DYREG; ++r) {
       const int idx = tid + 256 * r;                  // (co, row, col), col fastest
@@ -1723,11 +1741,12 @@ static inline WgradPlan wgrad_plan(const ConvDims& g) {
     return pl;
   }
   pl.xpitch = pitch;
-  // enough workgroups to fill the chip about three times over
+  // one round of equal workgroups: 2 per CU (80 KB of LDS each at NT 4) x 256 CUs; the
+  // bands split each sample's chunk list evenly (conv1: 32 x 16 bands of 10-11 chunks)
   const int64_t wgs = (int64_t)g.n * g.ci * ((g.co + 31) / 32);
-  const int rchunks = (g.ho + WG_RW - 1) / WG_RW;
-  int bands = static_cast<int>((768 + wgs - 1) / wgs);
-  pl.bands = bands < 1 ? 1 : (bands > rchunks ? rchunks : bands);
+  const int nck = ((g.ho + WG_RW - 1) / WG_RW) * ((g.wo + WG_CW - 1) / WG_CW);
+  int bands = static_cast<int>((512 + wgs / 2) / wgs);
+  pl.bands = bands < 1 ? 1 : (bands > nck ? nck : bands);
   return pl;
 }
 
@@ -1859,7 +1878,7 @@ ds2_status_t ds2_conv2d_wgrad(const float* dy, const float* x, float* dw, float*
   if (rg > 2048) rg = 2048;
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(rg), dim3(256), 0, st, partial, slabs, per, dw);
   if (dbias != nullptr)
-    hipLaunchKernelGGL(bias_grad_kernel, dim3(c_out), dim3(256), 0, st, dy, n, c_out,
+    hipLaunchKernelGGL(bias_grad_kernel, dim3(c_out), dim3(BG_T), 0, st, dy, n, c_out,
                        (int64_t)g.ho * g.wo, dbias);
   return launch_status("ds2_conv2d_wgrad");
 }

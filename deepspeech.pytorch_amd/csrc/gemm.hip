@@ -95,8 +95,25 @@ __device__ __forceinline__ void store_tile(float* __restrict__ s, const float (&
 //                       on, K range split nsplit ways; dispatched last, they fill the
 //                       slots the whole tiles leave in the final round.
 // XCD-aware (bijective) remap of both ranges: the blocks the dispatcher deals to one XCD
-// (ids congruent mod 8) get a contiguous run of tiles (pieces), n-tile fastest, so
-// workgroups sharing an operand panel share that XCD's L2.
+// (ids congruent mod 8) get a contiguous run of tiles (pieces) in the grouped order below,
+// so workgroups sharing an operand panel share that XCD's L2.
+// Grouped tile order: tile ids run over groups of g_tile_group m-rows, inside a group column
+// by column (m fastest), so the ~32 tiles one XCD runs at once span 4 m-rows x 8 n-columns
+// (A: 4 panels, B: 8) instead of ~2 m-rows x every n-column (the input projection's 15 B
+// panels, 7.7 MB, overflow the XCD's 4-MB L2 and were fetched again for every m-row).
+// g_tile_group 1 is the plain n-fastest order (DS2_GEMM_GROUP, diagnostic).
+constexpr int kTileGroup = 4;
+static __constant__ int g_tile_group = kTileGroup;
+
+__device__ __forceinline__ void tile_coords(int tile, int tn, int tm, int& tile_m, int& tile_n) {
+  const int G = g_tile_group;
+  const int g = tile / (G * tn);
+  const int rem = tile - g * G * tn;
+  const int rows = min(G, tm - g * G);
+  tile_n = rem / rows;
+  tile_m = g * G + (rem - tile_n * rows);
+}
+
 __device__ __forceinline__ void decode_work(int M, int N, int K, int main_wgs, int tail_tile0,
                                             int tail_tiles, int nsplit, int kchunk,
                                             float* partial, int& m0, int& n0, int& kbeg,
@@ -121,8 +138,8 @@ __device__ __forceinline__ void decode_work(int M, int N, int K, int main_wgs, i
     tile = tail_tile0 + lt;
     if (nsplit > 1) part = partial + ((int64_t)z * tail_tiles + lt) * (bm * bn);
   }
-  const int tile_m = tile / tn;
-  const int tile_n = tile - tile_m * tn;
+  int tile_m, tile_n;
+  tile_coords(tile, tn, (M + bm - 1) / bm, tile_m, tile_n);
   // z = batch * nsplit + split
   bz = z / nsplit;
   const int sp = z - bz * nsplit;
@@ -1204,8 +1221,10 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ partial, int M, i
     const int lt = static_cast<int>(bt % tail_tiles);
     const int b = static_cast<int>(bt / tail_tiles);
     const int tile = tail_tile0 + lt;
-    const int row = (tile / tn) * bm + e / bn;
-    const int col = (tile % tn) * bn + e % bn;
+    int tile_m, tile_n;
+    tile_coords(tile, tn, (M + bm - 1) / bm, tile_m, tile_n);
+    const int row = tile_m * bm + e / bn;
+    const int col = tile_n * bn + e % bn;
     if (row >= M || col >= N) continue;
     float acc = 0.f;
 #pragma unroll 8
@@ -1258,6 +1277,17 @@ static inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t
 }  // namespace ds2
 
 using namespace ds2;
+
+// DS2_GEMM_GROUP overrides the grouped tile order's group height (1: n-fastest order);
+// checked at every GEMM entry point, the symbol written only when the value changes
+static void apply_tile_group_env() {
+  static int applied = kTileGroup;
+  const char* e = getenv("DS2_GEMM_GROUP");
+  int v = (e == nullptr || e[0] == 0) ? kTileGroup : atoi(e);
+  if (v < 1) v = 1;
+  if (v == applied) return;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_tile_group), &v, sizeof(v)) == hipSuccess) applied = v;
+}
 
 static int g_cus = -1;
 static int device_cus() {
@@ -1400,6 +1430,7 @@ extern "C" ds2_status_t ds2_sgemm_ws(int trans_a, int trans_b, int m, int n, int
                                      float* c, int64_t ldc, int64_t stride_c, int batch,
                                      const float* bias, void* ws, size_t ws_bytes,
                                      ds2_stream_t stream) {
+  apply_tile_group_env();
   if (m < 0 || n < 0 || k < 0 || batch < 0) return DS2_INVALID_VALUE;
   if (m == 0 || n == 0 || batch == 0) return DS2_OK;
   if (ldc < n) return DS2_INVALID_VALUE;
@@ -1491,6 +1522,7 @@ extern "C" ds2_status_t ds2_sgemm_bf16_ws(int trans_a, int trans_b, int m, int n
                                           int64_t stride_b, float beta, float* c, int64_t ldc,
                                           int64_t stride_c, int batch, const float* bias,
                                           void* ws, size_t ws_bytes, ds2_stream_t stream) {
+  apply_tile_group_env();
   if (m < 0 || n < 0 || k < 0 || batch < 0) return DS2_INVALID_VALUE;
   if (m == 0 || n == 0 || batch == 0) return DS2_OK;
   if (ldc < n) return DS2_INVALID_VALUE;

@@ -532,47 +532,85 @@ __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
       // interleave them with the MFMAs and expose one load latency per block)
       asm volatile("" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
-      // Per-tile partial products summed in a fixed order afterwards, so the tiles can be
-      // multiplied in arrival order (SENT: a pass multiplies every ready pending tile, then
-      // re-loads the still-pending ones together: one round trip per pass, not per tile).
-      f32x4 pacc[NBW][3];
-#pragma unroll
-      for (int i = 0; i < NBW; ++i)
-#pragma unroll
-        for (int g = 0; g < 3; ++g) pacc[i][g] = f32x4{0.f, 0.f, 0.f, 0.f};
-      unsigned pend = (1u << nb) - 1u;                 // wave-uniform (nb <= NBW <= 8)
-      for (unsigned spins = 0;; ++spins) {
-#pragma unroll
-        for (int i = 0; i < NBW; ++i) {
-          if (((pend >> i) & 1u) && (!SENT || wave_ready(hv[i]))) {
-#pragma unroll
-            for (int c = 0; c < 4; ++c)
-#pragma unroll
-              for (int g = 0; g < 3; ++g)
-                pacc[i][g] = __builtin_amdgcn_mfma_f32_16x16x4f32(hv[i][c], w[g][i][c], pacc[i][g],
-                                                                  0, 0, 0);
-            pend &= ~(1u << i);
-          }
-        }
-        if (pend == 0u && g_spin_limit != 0) break;
-        if (spins > g_spin_limit || g_spin_limit == 0) {
-          if (lane == 0) __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          failed = 1;
-          break;
-        }
-        sleep_units(g_rnn_tune[0]);
-        asm volatile("" ::: "memory");   // the re-loads are not loop-invariant (no LICM)
-#pragma unroll
+      if constexpr (NBW <= 7) {
+        // Per-tile partial products summed in a fixed order afterwards, so the tiles can be
+        // multiplied in arrival order (SENT: a pass multiplies every ready pending tile, then
+        // re-loads the still-pending ones together: one round trip per pass, not per tile).
+        f32x4 pacc[NBW][3];
+  #pragma unroll
         for (int i = 0; i < NBW; ++i)
-          if ((pend >> i) & 1u)
-            hv[i] = __builtin_bit_cast(
-                f32x4, __builtin_amdgcn_raw_buffer_load_b128(x_rs, base + i * 1024, 0, kSc1));
-      }
+  #pragma unroll
+          for (int g = 0; g < 3; ++g) pacc[i][g] = f32x4{0.f, 0.f, 0.f, 0.f};
+        unsigned pend = (1u << nb) - 1u;                 // wave-uniform (nb <= NBW <= 8)
+        for (unsigned spins = 0;; ++spins) {
+  #pragma unroll
+          for (int i = 0; i < NBW; ++i) {
+            if (((pend >> i) & 1u) && (!SENT || wave_ready(hv[i]))) {
+  #pragma unroll
+              for (int c = 0; c < 4; ++c)
+  #pragma unroll
+                for (int g = 0; g < 3; ++g)
+                  pacc[i][g] = __builtin_amdgcn_mfma_f32_16x16x4f32(hv[i][c], w[g][i][c], pacc[i][g],
+                                                                    0, 0, 0);
+              pend &= ~(1u << i);
+            }
+          }
+          if (pend == 0u && g_spin_limit != 0) break;
+          if (spins > g_spin_limit || g_spin_limit == 0) {
+            if (lane == 0) __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            failed = 1;
+            break;
+          }
+          sleep_units(g_rnn_tune[0]);
+          asm volatile("" ::: "memory");   // the re-loads are not loop-invariant (no LICM)
+  #pragma unroll
+          for (int i = 0; i < NBW; ++i)
+            if ((pend >> i) & 1u)
+              hv[i] = __builtin_bit_cast(
+                  f32x4, __builtin_amdgcn_raw_buffer_load_b128(x_rs, base + i * 1024, 0, kSc1));
+        }
+  #pragma unroll
+        for (int g = 0; g < 3; ++g) {
+          acc[g] = pacc[0][g];
+  #pragma unroll
+          for (int i = 1; i < NBW; ++i) acc[g] += pacc[i][g];
+        }
+      } else {
+        // 8 tiles per wave (H > 896): the per-tile partials would spill (96 more VGPRs), so
+        // the ready PREFIX is multiplied in tile order straight into acc (as in the backward:
+        // one accumulation order for every hand-off form) and only stale tiles are re-loaded
+        unsigned rdy = 0u;
+        int next = 0;
+        for (unsigned spins = 0;; ++spins) {
 #pragma unroll
-      for (int g = 0; g < 3; ++g) {
-        acc[g] = pacc[0][g];
+          for (int i = 0; i < NBW; ++i)
+            if (i >= next && i < nb && !((rdy >> i) & 1u) && (!SENT || wave_ready(hv[i])))
+              rdy |= 1u << i;
 #pragma unroll
-        for (int i = 1; i < NBW; ++i) acc[g] += pacc[i][g];
+          for (int i = 0; i < NBW; ++i) {
+            if (i == next && i < nb && ((rdy >> i) & 1u)) {
+#pragma unroll
+              for (int c = 0; c < 4; ++c)
+#pragma unroll
+                for (int g = 0; g < 3; ++g)
+                  acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(hv[i][c], w[g][i][c], acc[g], 0, 0, 0);
+              ++next;
+            }
+          }
+          if (next >= nb && g_spin_limit != 0) break;
+          if (spins > g_spin_limit || g_spin_limit == 0) {
+            if (lane == 0) __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            failed = 1;
+            break;
+          }
+          sleep_units(g_rnn_tune[0]);
+          asm volatile("" ::: "memory");
+#pragma unroll
+          for (int i = 0; i < NBW; ++i)
+            if (i >= next && i < nb && !((rdy >> i) & 1u))
+              hv[i] = __builtin_bit_cast(
+                  f32x4, __builtin_amdgcn_raw_buffer_load_b128(x_rs, base + i * 1024, 0, kSc1));
+        }
       }
       trace_at(s, 2);
     }

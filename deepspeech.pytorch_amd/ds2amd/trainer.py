@@ -121,6 +121,10 @@ class Trainer:
         self._nan_mask = None
         # device accumulators of (wer, cer, words, chars): no host sync per batch
         self._score_acc = torch.zeros(4, dtype=torch.float64, device=self.device)
+        # greedy decode + CER/WER depend on the forward alone: they run on a side stream
+        # beside the CTC / backward (the recurrences leave CUs idle) and are joined before
+        # the step ends
+        self._side = torch.cuda.Stream(device=self.device) if self.device.type == 'cuda' else None
         self._rnn_word = ops.rnn_status_word(self.device)
         # pinned ring of (nan flag, rnn status, loss bits) per in-flight step
         self._ring = [torch.zeros(3, dtype=torch.int32).pin_memory()
@@ -197,13 +201,24 @@ class Trainer:
         inputs, targets, filenames, input_percentages, target_sizes = data
         input_sizes = input_percentages.mul_(int(inputs.size(3))).int()   # train.py:557 quirk
         inputs = inputs.to(self.device, non_blocking=True)
+        side = self._side if self.decode else None
+        if side is not None and self.score:
+            with torch.cuda.stream(side):      # idle stream: the host copies do not wait
+                tg_d = targets.to(self.device, torch.int32, non_blocking=True)
+                ts_d = target_sizes.to(self.device, torch.int32, non_blocking=True)
         self.sync.before_forward()
         logits, probs, output_sizes = self.model(inputs, input_sizes)
 
-        if self.decode:
-            ids, offs, counts = self.decoder.decode_ids(probs, output_sizes)
-            if self.score:
-                self._score(ids, counts, targets, target_sizes)
+        if side is not None:
+            main = torch.cuda.current_stream(self.device)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                ids, offs, counts = self.decoder.decode_ids(probs, output_sizes)
+                if self.score:
+                    self._score(ids, counts, tg_d, ts_d)
+            for t in (probs, output_sizes):
+                if torch.is_tensor(t) and t.is_cuda:
+                    t.record_stream(side)
 
         logits = logits.transpose(0, 1)                                   # T x N x C
         self.nan_flag.zero_()
@@ -218,6 +233,8 @@ class Trainer:
         loss.backward()
         self.reducer.finish()
         self.optimizer.step()               # clip + SGD; always taken (see module docstring)
+        if side is not None:
+            torch.cuda.current_stream(self.device).wait_stream(side)
         if self.world > 1:
             loss = reduce_tensor(loss.detach(), self.world)
         self._record_status(loss)

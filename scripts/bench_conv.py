@@ -38,6 +38,7 @@ for name, n, ci, h, w, co, kh, kw, sh, sw, ph, pw in CONVS:
     if ci > 1:
         td = timeit(lambda: ops.conv2d_dgrad(dy, wt, x.shape, (sh, sw), (ph, pw)))
         out.append(f"dgrad {td * 1e3:7.1f} us {fl / td / 1e9:6.1f} TF")
-    tw = timeit(lambda: ops.conv2d_wgrad(dy, x, wt.shape, (sh, sw), (ph, pw), True))
+    # no bias gradient: the training step takes the conv bias gradient from the BN backward
+    tw = timeit(lambda: ops.conv2d_wgrad(dy, x, wt.shape, (sh, sw), (ph, pw), False))
     out.append(f"wgrad {tw * 1e3:7.1f} us {fl / tw / 1e9:6.1f} TF")
     print(f"{name}: " + " | ".join(out), flush=True)

@@ -294,7 +294,8 @@ def test_conv_block_fwd_bwd(dev, layout):
 
 # ---------------------------------------------------------------------------- GRU
 @pytest.mark.parametrize("n,t,inp,h,bidir", [(5, 23, 40, 24, True), (19, 9, 33, 400, True),
-                                             (3, 17, 20, 16, False), (20, 30, 64, 800, True)])
+                                             (3, 17, 20, 16, False), (20, 30, 64, 800, True),
+                                             (6, 12, 32, 1024, True)])
 def test_gru_layer(dev, n, t, inp, h, bidir):
     g = torch.Generator().manual_seed(n * 100 + h)
     gru = torch.nn.GRU(inp, h, bidirectional=bidir).double()
@@ -437,7 +438,8 @@ def test_gru_reduce_scatter_backward(dev, n, h, bidir, monkeypatch):
         _close(b_, a_, 2e-5, "reduce-scatter vs direct-operand backward")
 
 
-@pytest.mark.parametrize("n,h,bidir", [(32, 64, True), (20, 800, True), (7, 48, False)])
+@pytest.mark.parametrize("n,h,bidir", [(32, 64, True), (20, 800, True), (7, 48, False),
+                                       (16, 1024, True)])
 def test_gru_handoff_forms_agree(dev, n, h, bidir, monkeypatch):
     """The per-producer-flag, sentinel-ring and hybrid (flag poll + sentinel-validated
     tiles, no drain before the flag) hand-offs of the direct-operand recurrences
