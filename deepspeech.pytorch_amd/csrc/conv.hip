@@ -855,6 +855,143 @@ __global__ __launch_bounds__(256) void conv_wgrad_patch_kernel(const float* __re
 }
 
 // ---------------------------------------------------------------------------
+// Single-input-channel forward from an LDS patch (conv1: 1 -> 32 channels, 41 x 11 taps,
+// stride 2 x 2) on v_mfma_f32_32x32x2_f32: M = 32 output channels, N = 32 output columns,
+// K = taps.  A workgroup owns one sample's C1_RW output rows x C1_WC output columns; the
+// input patch those outputs read (47 x 265 floats for conv1) and the whole filter bank as
+// [tap][co] (452 x 32 floats) are staged in LDS once, then every k-pair is one A read (32
+// consecutive channels), two B reads (patch offset of the lane's tap + its column * stride;
+// consecutive taps differ by an odd offset, so the two half-waves hit disjoint banks) and two
+// MFMAs.  The implicit-GEMM conv_fwd_kernel gathered every tap of every position from global
+// memory instead (16 scattered loads + index arithmetic per thread per 16 taps).
+// Wave w: output row w >> 1, columns (w & 1) * 64 + [0, 64) as two 32-column tiles.
+constexpr int C1_RW = 4;
+constexpr int C1_WC = 128;
+constexpr int C1_T = 512;
+constexpr int C1_PATCH = 12560;      // floats: ((C1_RW - 1) sh + kh) x ((C1_WC - 1) sw + kw)
+constexpr int C1_KMAX = 452;         // taps, padded to a multiple of 4
+constexpr int C1_WP = 33;            // filter-bank row pitch (odd: conflict-free stores)
+constexpr int C1_PREG = (C1_PATCH + C1_T - 1) / C1_T;
+constexpr int C1_WREG = (32 * (C1_KMAX - 1) + C1_T - 1) / C1_T;
+
+__global__ __launch_bounds__(C1_T, 1) void conv1_patch_fwd_kernel(
+    const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
+    float* __restrict__ y, ConvDims g, const int* __restrict__ out_lens, int gx, int gy) {
+  __shared__ float ps[C1_PATCH];
+  __shared__ float wsm[C1_KMAX * C1_WP];
+  int bx, by, bz;
+  xcd_tile(gx, gy, bx, by, bz);
+  const int n = bz;
+  const int ho0 = by * C1_RW, wo0 = bx * C1_WC;
+  const int T = g.kh * g.kw;
+  const int T4 = (T + 3) & ~3;
+  const int PR = (C1_RW - 1) * g.sh + g.kh;
+  const int PC = (C1_WC - 1) * g.sw + g.kw;
+  const int ir0 = ho0 * g.sh - g.ph, ic0 = wo0 * g.sw - g.pw;
+  const float* xn = x + (int64_t)n * g.hi * g.wi;
+  {
+    // every load of the patch and of the filter bank issued before the first LDS store
+    // (indices stepped, no per-element division); the bank is read in its own [co][tap]
+    // order (coalesced) and stored as [tap][co] with an odd pitch (conflict-free both ways)
+    const int pe = PR * PC;
+    float rp[C1_PREG], rw[C1_WREG];
+    int r = threadIdx.x / PC, c = threadIdx.x - (threadIdx.x / PC) * PC;
+    const int dr = C1_T / PC, dc = C1_T - (C1_T / PC) * PC;
+#pragma unroll
+    for (int u = 0; u < C1_PREG; ++u) {
+      const int ir = ir0 + r, ic = ic0 + c;
+      const bool ok = threadIdx.x + u * C1_T < pe && ir >= 0 && ir < g.hi && ic >= 0 && ic < g.wi;
+      rp[u] = ok ? xn[(int64_t)ir * g.wi + ic] : 0.f;
+      r += dr;
+      c += dc;
+      if (c >= PC) {
+        c -= PC;
+        ++r;
+      }
+    }
+    const int nw = 32 * T;
+    int co = threadIdx.x / T, k = threadIdx.x - (threadIdx.x / T) * T;
+    const int dco = C1_T / T, dk = C1_T - (C1_T / T) * T;
+    int wk[C1_WREG];
+#pragma unroll
+    for (int u = 0; u < C1_WREG; ++u) {
+      const int i = threadIdx.x + u * C1_T;
+      rw[u] = (i < nw && co < g.co) ? w[i] : 0.f;
+      wk[u] = i < nw ? k * C1_WP + co : -1;
+      co += dco;
+      k += dk;
+      if (k >= T) {
+        k -= T;
+        ++co;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < C1_PREG; ++u)
+      if (threadIdx.x + u * C1_T < pe) ps[threadIdx.x + u * C1_T] = rp[u];
+#pragma unroll
+    for (int u = 0; u < C1_WREG; ++u)
+      if (wk[u] >= 0) wsm[wk[u]] = rw[u];
+    if (threadIdx.x < 32 * (T4 - T))                                       // padded taps
+      wsm[(T + (threadIdx.x >> 5)) * C1_WP + (threadIdx.x & 31)] = 0.f;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int lr = lane & 31, lk = lane >> 5;
+  const int orow = wave >> 1;
+  const int ocol = (wave & 1) * 64;
+  const float* pb0 = ps + orow * g.sh * PC + (ocol + lr) * g.sw;
+  const float* pb1 = pb0 + 32 * g.sw;
+  const float* wa = wsm + lk * C1_WP + lr;
+  f32x16 acc0, acc1;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    acc0[r] = 0.f;
+    acc1[r] = 0.f;
+  }
+  // tap (row, column) of k = k0 + lk and of k0 + 2 + lk, stepped by 4 taps per iteration
+  int ta = lk / g.kw, tb = lk - (lk / g.kw) * g.kw;
+  int ua = (lk + 2) / g.kw, ub = (lk + 2) - ((lk + 2) / g.kw) * g.kw;
+  for (int k0 = 0; k0 < T4; k0 += 4) {
+    const int t0 = k0 + lk < T ? ta * PC + tb : 0;       // padded taps: zero weight
+    const int t1 = k0 + 2 + lk < T ? ua * PC + ub : 0;
+    const float a0 = wa[k0 * C1_WP], a1 = wa[(k0 + 2) * C1_WP];
+    const float b00 = pb0[t0], b01 = pb1[t0], b10 = pb0[t1], b11 = pb1[t1];
+    acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b00, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b01, acc1, 0, 0, 0);
+    acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b10, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b11, acc1, 0, 0, 0);
+    tb += 4;                   // kw >= 4 (host check): at most one wrap per step
+    if (tb >= g.kw) {
+      tb -= g.kw;
+      ++ta;
+    }
+    ub += 4;
+    if (ub >= g.kw) {
+      ub -= g.kw;
+      ++ua;
+    }
+  }
+  const int ho = ho0 + orow;
+  if (ho >= g.ho) return;
+  const int len = out_lens != nullptr ? out_lens[n] : g.wo;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int col = wo0 + ocol + 32 * j + lr;
+    if (col >= g.wo) continue;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int c = (r & 3) + 8 * (r >> 2) + 4 * lk;
+      if (c < g.co) {
+        float v = (j == 0 ? acc0[r] : acc1[r]) + (bias != nullptr ? bias[c] : 0.f);
+        if (col >= len) v = 0.f;
+        y[(((int64_t)n * g.co + c) * g.ho + ho) * g.wo + col] = v;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // bf16x6 direct convolution, forward (width stride 1 or 2) and dgrad (width stride 1), on the
 // bf16 matrix cores at
 // fp32 accuracy: every fp32 operand value is split into hi / mid / lo bf16 terms and a
@@ -1591,6 +1728,17 @@ static inline bool patch_ok(const ConvDims& g, bool dgrad) {
   return rows <= PT_PROWS && taps <= PT_TMAX && plane * 4 < (1ll << 31) - 64;
 }
 
+// the single-channel patch forward (conv1_patch_fwd_kernel): one input channel, <= 32 output
+// channels, kw >= 4, a patch and filter bank that fit its LDS, input planes within 32-bit
+// offsets (DS2_CONV_PATCH=0 selects the implicit-GEMM kernel)
+static inline bool c1_ok(const ConvDims& g) {
+  if (getenv("DS2_CONV_PATCH") != nullptr && getenv("DS2_CONV_PATCH")[0] == '0') return false;
+  if (g.ci != 1 || g.co > 32 || g.kw < 4) return false;
+  const int64_t pe = (int64_t)((C1_RW - 1) * g.sh + g.kh) * ((C1_WC - 1) * g.sw + g.kw);
+  return pe <= C1_PATCH && 32 * g.kh * g.kw <= C1_WREG * C1_T &&
+         ((g.kh * g.kw + 3) & ~3) <= C1_KMAX;
+}
+
 static size_t patch_ws_bytes(const ConvDims& g, bool dgrad) {
   if (!patch_ok(g, dgrad)) return 0;
   const int M = dgrad ? g.ci : g.co;
@@ -1800,6 +1948,14 @@ ds2_status_t ds2_conv2d_fwd(const float* x, const float* w, const float* bias, f
   if (patch_ok(g, false)) {
     if (ws == nullptr || ws_bytes < patch_ws_bytes(g, false)) return DS2_WORKSPACE_TOO_SMALL;
     return launch_patch<false>(x, w, bias, y, g, out_lens, ws, as_stream(stream));
+  }
+  if (c1_ok(g)) {
+    const int gx = cdiv(g.wo, C1_WC), gy = cdiv(g.ho, C1_RW);
+    const int64_t nwg = (int64_t)gx * gy * n;
+    if (nwg > 0x7fffffff) return DS2_UNSUPPORTED_SHAPE;
+    hipLaunchKernelGGL(conv1_patch_fwd_kernel, dim3(static_cast<unsigned>(nwg)), dim3(C1_T), 0,
+                       as_stream(stream), x, w, bias, y, g, out_lens, gx, gy);
+    return launch_status("ds2_conv2d_fwd");
   }
   dim3 grid(cdiv(g.wo, CBN), g.ho, n * cdiv(c_out, 32));
   hipLaunchKernelGGL(conv_fwd_kernel, grid, dim3(256), 0, as_stream(stream), x, w, bias, y, g,
