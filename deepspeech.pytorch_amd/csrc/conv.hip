@@ -824,6 +824,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_patch_kernel(const float* __re
   for (int k = 0; k < nchunks; ++k) {
     if (k + 1 < nchunks) load(k + 1);
     const float* arow = dys + lk * WG_DYP + lr;
+    // (software-pipelining these reads a position pair ahead measured slower: 0.58 -> 0.66 ms)
 #pragma unroll 4
     for (int s2 = 0; s2 < WG_RW * WG_CW / 2; ++s2) {
       const int pos = 2 * s2;                        // + lk (folded into arow / boff)
@@ -876,27 +877,38 @@ constexpr int C1_WREG = (32 * (C1_KMAX - 1) + C1_T - 1) / C1_T;
 
 __global__ __launch_bounds__(C1_T, 1) void conv1_patch_fwd_kernel(
     const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
-    float* __restrict__ y, ConvDims g, const int* __restrict__ out_lens, int gx, int gy) {
-  __shared__ float ps[C1_PATCH];
+    float* __restrict__ y, ConvDims g, const int* __restrict__ out_lens, int gx, int gy,
+    int tiles) {
+  // persistent: the filter bank is staged once per workgroup; the patch is double-buffered,
+  // the next tile's loads in flight during this tile's MFMAs (one barrier per tile)
+  __shared__ float ps[2][C1_PATCH];
   __shared__ float wsm[C1_KMAX * C1_WP];
-  int bx, by, bz;
-  xcd_tile(gx, gy, bx, by, bz);
-  const int n = bz;
-  const int ho0 = by * C1_RW, wo0 = bx * C1_WC;
   const int T = g.kh * g.kw;
   const int T4 = (T + 3) & ~3;
   const int PR = (C1_RW - 1) * g.sh + g.kh;
   const int PC = (C1_WC - 1) * g.sw + g.kw;
-  const int ir0 = ho0 * g.sh - g.ph, ic0 = wo0 * g.sw - g.pw;
-  const float* xn = x + (int64_t)n * g.hi * g.wi;
-  {
-    // every load of the patch and of the filter bank issued before the first LDS store
-    // (indices stepped, no per-element division); the bank is read in its own [co][tap]
-    // order (coalesced) and stored as [tap][co] with an odd pitch (conflict-free both ways)
-    const int pe = PR * PC;
-    float rp[C1_PREG], rw[C1_WREG];
-    int r = threadIdx.x / PC, c = threadIdx.x - (threadIdx.x / PC) * PC;
-    const int dr = C1_T / PC, dc = C1_T - (C1_T / PC) * PC;
+  const int pe = PR * PC;
+  // XCD-aware: the workgroups one XCD is dealt (ids congruent mod 8) take consecutive tiles
+  // of every round (neighbouring row tiles share 31 of their 47 patch rows in that L2)
+  const int G = gridDim.x;
+  const int q8 = G >> 3, r8 = G & 7, xcd = blockIdx.x & 7;
+  const int slot = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (blockIdx.x >> 3);
+  float rp[C1_PREG];
+  const int r00 = threadIdx.x / PC, c00 = threadIdx.x - (threadIdx.x / PC) * PC;
+  const int dr = C1_T / PC, dc = C1_T - (C1_T / PC) * PC;
+  auto tile_of = [&](int t, int& n, int& ho0, int& wo0) {
+    const int bx = t % gx, rest = t / gx;
+    wo0 = bx * C1_WC;
+    ho0 = (rest % gy) * C1_RW;
+    n = rest / gy;
+  };
+  // every load of a patch issued before its LDS stores (indices stepped, no division)
+  auto load_patch = [&](int t) {
+    int n, ho0, wo0;
+    tile_of(t, n, ho0, wo0);
+    const int ir0 = ho0 * g.sh - g.ph, ic0 = wo0 * g.sw - g.pw;
+    const float* xn = x + (int64_t)n * g.hi * g.wi;
+    int r = r00, c = c00;
 #pragma unroll
     for (int u = 0; u < C1_PREG; ++u) {
       const int ir = ir0 + r, ic = ic0 + c;
@@ -909,10 +921,23 @@ __global__ __launch_bounds__(C1_T, 1) void conv1_patch_fwd_kernel(
         ++r;
       }
     }
+  };
+  auto store_patch = [&](float* dst) {
+#pragma unroll
+    for (int u = 0; u < C1_PREG; ++u)
+      if (threadIdx.x + u * C1_T < pe) dst[threadIdx.x + u * C1_T] = rp[u];
+  };
+  int t = slot;
+  if (t >= tiles) return;
+  load_patch(t);
+  {
+    // the bank read in its own [co][tap] order (coalesced), stored as [tap][co] with an odd
+    // pitch (conflict-free both ways)
+    float rw[C1_WREG];
+    int wk[C1_WREG];
     const int nw = 32 * T;
     int co = threadIdx.x / T, k = threadIdx.x - (threadIdx.x / T) * T;
     const int dco = C1_T / T, dk = C1_T - (C1_T / T) * T;
-    int wk[C1_WREG];
 #pragma unroll
     for (int u = 0; u < C1_WREG; ++u) {
       const int i = threadIdx.x + u * C1_T;
@@ -925,9 +950,7 @@ __global__ __launch_bounds__(C1_T, 1) void conv1_patch_fwd_kernel(
         ++co;
       }
     }
-#pragma unroll
-    for (int u = 0; u < C1_PREG; ++u)
-      if (threadIdx.x + u * C1_T < pe) ps[threadIdx.x + u * C1_T] = rp[u];
+    store_patch(ps[0]);
 #pragma unroll
     for (int u = 0; u < C1_WREG; ++u)
       if (wk[u] >= 0) wsm[wk[u]] = rw[u];
@@ -940,54 +963,68 @@ __global__ __launch_bounds__(C1_T, 1) void conv1_patch_fwd_kernel(
   const int lr = lane & 31, lk = lane >> 5;
   const int orow = wave >> 1;
   const int ocol = (wave & 1) * 64;
-  const float* pb0 = ps + orow * g.sh * PC + (ocol + lr) * g.sw;
-  const float* pb1 = pb0 + 32 * g.sw;
+  const int poff = orow * g.sh * PC + (ocol + lr) * g.sw;
   const float* wa = wsm + lk * C1_WP + lr;
-  f32x16 acc0, acc1;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    acc0[r] = 0.f;
-    acc1[r] = 0.f;
-  }
-  // tap (row, column) of k = k0 + lk and of k0 + 2 + lk, stepped by 4 taps per iteration
-  int ta = lk / g.kw, tb = lk - (lk / g.kw) * g.kw;
-  int ua = (lk + 2) / g.kw, ub = (lk + 2) - ((lk + 2) / g.kw) * g.kw;
-  for (int k0 = 0; k0 < T4; k0 += 4) {
-    const int t0 = k0 + lk < T ? ta * PC + tb : 0;       // padded taps: zero weight
-    const int t1 = k0 + 2 + lk < T ? ua * PC + ub : 0;
-    const float a0 = wa[k0 * C1_WP], a1 = wa[(k0 + 2) * C1_WP];
-    const float b00 = pb0[t0], b01 = pb1[t0], b10 = pb0[t1], b11 = pb1[t1];
-    acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b00, acc0, 0, 0, 0);
-    acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b01, acc1, 0, 0, 0);
-    acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b10, acc0, 0, 0, 0);
-    acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b11, acc1, 0, 0, 0);
-    tb += 4;                   // kw >= 4 (host check): at most one wrap per step
-    if (tb >= g.kw) {
-      tb -= g.kw;
-      ++ta;
-    }
-    ub += 4;
-    if (ub >= g.kw) {
-      ub -= g.kw;
-      ++ua;
-    }
-  }
-  const int ho = ho0 + orow;
-  if (ho >= g.ho) return;
-  const int len = out_lens != nullptr ? out_lens[n] : g.wo;
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int col = wo0 + ocol + 32 * j + lr;
-    if (col >= g.wo) continue;
+  const int ta0 = lk / g.kw, tb0 = lk - (lk / g.kw) * g.kw;
+  const int ua0 = (lk + 2) / g.kw, ub0 = (lk + 2) - ((lk + 2) / g.kw) * g.kw;
+  for (int cur = 0; t < tiles; t += G, cur ^= 1) {
+    const bool more = t + G < tiles;
+    if (more) load_patch(t + G);
+    const float* pb0 = ps[cur] + poff;
+    const float* pb1 = pb0 + 32 * g.sw;
+    f32x16 acc0, acc1;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int c = (r & 3) + 8 * (r >> 2) + 4 * lk;
-      if (c < g.co) {
-        float v = (j == 0 ? acc0[r] : acc1[r]) + (bias != nullptr ? bias[c] : 0.f);
-        if (col >= len) v = 0.f;
-        y[(((int64_t)n * g.co + c) * g.ho + ho) * g.wo + col] = v;
+      acc0[r] = 0.f;
+      acc1[r] = 0.f;
+    }
+    // tap (row, column) of k = k0 + lk and of k0 + 2 + lk, stepped by 4 taps per iteration
+    // (software-pipelining the LDS reads a step ahead measured slower: 570 -> 620 us)
+    int ta = ta0, tb = tb0, ua = ua0, ub = ub0;
+    for (int k0 = 0; k0 < T4; k0 += 4) {
+      const int t0 = k0 + lk < T ? ta * PC + tb : 0;       // padded taps: zero weight
+      const int t1 = k0 + 2 + lk < T ? ua * PC + ub : 0;
+      const float a0 = wa[k0 * C1_WP], a1 = wa[(k0 + 2) * C1_WP];
+      const float b00 = pb0[t0], b01 = pb1[t0], b10 = pb0[t1], b11 = pb1[t1];
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b00, acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b01, acc1, 0, 0, 0);
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b10, acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b11, acc1, 0, 0, 0);
+      tb += 4;                 // kw >= 4 (host check): at most one wrap per step
+      if (tb >= g.kw) {
+        tb -= g.kw;
+        ++ta;
+      }
+      ub += 4;
+      if (ub >= g.kw) {
+        ub -= g.kw;
+        ++ua;
       }
     }
+    // nobody reads the other buffer this round (the last barrier followed every wave's
+    // previous round of reads): fill it, then one barrier before it is read
+    if (more) store_patch(ps[cur ^ 1]);
+    int n, ho0, wo0;
+    tile_of(t, n, ho0, wo0);
+    const int ho = ho0 + orow;
+    if (ho < g.ho) {
+      const int len = out_lens != nullptr ? out_lens[n] : g.wo;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int col = wo0 + ocol + 32 * j + lr;
+        if (col >= g.wo) continue;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int c = (r & 3) + 8 * (r >> 2) + 4 * lk;
+          if (c < g.co) {
+            float v = (j == 0 ? acc0[r] : acc1[r]) + (bias != nullptr ? bias[c] : 0.f);
+            if (col >= len) v = 0.f;
+            y[(((int64_t)n * g.co + c) * g.ho + ho) * g.wo + col] = v;
+          }
+        }
+      }
+    }
+    __syncthreads();
   }
 }
 
@@ -1728,6 +1765,18 @@ static inline bool patch_ok(const ConvDims& g, bool dgrad) {
   return rows <= PT_PROWS && taps <= PT_TMAX && plane * 4 < (1ll << 31) - 64;
 }
 
+static int conv_cus() {
+  static int cus = -1;
+  if (cus < 0) {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
+      v = 256;
+    cus = v;
+  }
+  return cus;
+}
+
 // the single-channel patch forward (conv1_patch_fwd_kernel): one input channel, <= 32 output
 // channels, kw >= 4, a patch and filter bank that fit its LDS, input planes within 32-bit
 // offsets (DS2_CONV_PATCH=0 selects the implicit-GEMM kernel)
@@ -1951,10 +2000,11 @@ ds2_status_t ds2_conv2d_fwd(const float* x, const float* w, const float* bias, f
   }
   if (c1_ok(g)) {
     const int gx = cdiv(g.wo, C1_WC), gy = cdiv(g.ho, C1_RW);
-    const int64_t nwg = (int64_t)gx * gy * n;
-    if (nwg > 0x7fffffff) return DS2_UNSUPPORTED_SHAPE;
-    hipLaunchKernelGGL(conv1_patch_fwd_kernel, dim3(static_cast<unsigned>(nwg)), dim3(C1_T), 0,
-                       as_stream(stream), x, w, bias, y, g, out_lens, gx, gy);
+    const int64_t tiles = (int64_t)gx * gy * n;
+    if (tiles > 0x7fffffff) return DS2_UNSUPPORTED_SHAPE;
+    const int grid = static_cast<int>(std::min<int64_t>(tiles, conv_cus()));   // one per CU
+    hipLaunchKernelGGL(conv1_patch_fwd_kernel, dim3(grid), dim3(C1_T), 0, as_stream(stream), x, w,
+                       bias, y, g, out_lens, gx, gy, static_cast<int>(tiles));
     return launch_status("ds2_conv2d_fwd");
   }
   dim3 grid(cdiv(g.wo, CBN), g.ho, n * cdiv(c_out, 32));
