@@ -143,6 +143,7 @@ CONVS = [  # (n, ci, h, w, co, kh, kw, sh, sw, ph, pw)
     # output channels, other strides / taps
     (2, 1, 161, 300, 32, 41, 11, 2, 2, 20, 5),
     (2, 1, 33, 260, 20, 7, 5, 3, 2, 3, 2),
+    (2, 1, 20, 150, 16, 5, 4, 1, 1, 2, 1),
     (2, 32, 81, 23, 32, 21, 11, 2, 1, 10, 5),
     (3, 3, 17, 300, 40, 5, 3, 1, 2, 2, 1),
     # width stride 1 -> LDS-patch direct kernels (several column tiles, two output-channel
