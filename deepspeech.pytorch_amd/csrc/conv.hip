@@ -869,24 +869,29 @@ __global__ __launch_bounds__(256) void conv_wgrad_patch_kernel(const float* __re
 constexpr int C1_RW = 4;
 constexpr int C1_WC = 128;
 constexpr int C1_T = 512;
-constexpr int C1_PATCH = 12560;      // floats: ((C1_RW - 1) sh + kh) x ((C1_WC - 1) sw + kw)
-constexpr int C1_KMAX = 452;         // taps, padded to a multiple of 4
-constexpr int C1_WP = 33;            // filter-bank row pitch (odd: conflict-free stores)
+constexpr int C1_PATCH = 12560;      // floats: ((C1_RW - 1) sh + kh) x ((C1_WC - 1) sw + kw2)
+constexpr int C1_KROWS = 492;        // filter-bank rows kh x kw2 (conv1: 41 x 12)
 constexpr int C1_PREG = (C1_PATCH + C1_T - 1) / C1_T;
-constexpr int C1_WREG = (32 * (C1_KMAX - 1) + C1_T - 1) / C1_T;
+constexpr int C1_WREG = (32 * C1_KROWS + C1_T - 1) / C1_T;
+static_assert(2 * C1_PATCH * 4 + C1_KROWS * 32 * 4 <= 160 * 1024, "conv1 patch kernel LDS");
 
+// KWH = kernel columns padded to even, halved (conv1: 11 -> 12 -> 6): a k-pair is two
+// adjacent columns of one tap row, so every LDS read of the inner loop is a fixed offset
+// from a per-row base (no per-tap index arithmetic: the stepped-tap form spent ~10 VALU per
+// MFMA, SQ_INSTS_VALU / SQ_INSTS_MFMA); the padded column has zero weight (+9 % MFMAs)
+template <int KWH>
 __global__ __launch_bounds__(C1_T, 1) void conv1_patch_fwd_kernel(
     const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
     float* __restrict__ y, ConvDims g, const int* __restrict__ out_lens, int gx, int gy,
     int tiles) {
   // persistent: the filter bank is staged once per workgroup; the patch is double-buffered,
   // the next tile's loads in flight during this tile's MFMAs (one barrier per tile)
+  constexpr int KW2 = 2 * KWH;
   __shared__ float ps[2][C1_PATCH];
-  __shared__ float wsm[C1_KMAX * C1_WP];
+  __shared__ float wsm[C1_KROWS * 32];
   const int T = g.kh * g.kw;
-  const int T4 = (T + 3) & ~3;
   const int PR = (C1_RW - 1) * g.sh + g.kh;
-  const int PC = (C1_WC - 1) * g.sw + g.kw;
+  const int PC = (C1_WC - 1) * g.sw + KW2;
   const int pe = PR * PC;
   // XCD-aware: the workgroups one XCD is dealt (ids congruent mod 8) take consecutive tiles
   // of every round (neighbouring row tiles share 31 of their 47 patch rows in that L2)
@@ -931,18 +936,18 @@ __global__ __launch_bounds__(C1_T, 1) void conv1_patch_fwd_kernel(
   if (t >= tiles) return;
   load_patch(t);
   {
-    // the bank read in its own [co][tap] order (coalesced), stored as [tap][co] with an odd
-    // pitch (conflict-free both ways)
+    // the bank read in its own [co][tap] order (coalesced), stored as [tap row x kw2][co];
+    // the padded column's rows are zero
     float rw[C1_WREG];
     int wk[C1_WREG];
-    const int nw = 32 * T;
     int co = threadIdx.x / T, k = threadIdx.x - (threadIdx.x / T) * T;
     const int dco = C1_T / T, dk = C1_T - (C1_T / T) * T;
 #pragma unroll
     for (int u = 0; u < C1_WREG; ++u) {
-      const int i = threadIdx.x + u * C1_T;
-      rw[u] = (i < nw && co < g.co) ? w[i] : 0.f;
-      wk[u] = i < nw ? k * C1_WP + co : -1;
+      const bool in = co < 32;
+      rw[u] = (in && co < g.co) ? w[(int64_t)co * T + k] : 0.f;
+      const int a = k / g.kw;
+      wk[u] = in ? ((a * KW2 + (k - a * g.kw)) << 5) + co : -1;
       co += dco;
       k += dk;
       if (k >= T) {
@@ -954,8 +959,10 @@ __global__ __launch_bounds__(C1_T, 1) void conv1_patch_fwd_kernel(
 #pragma unroll
     for (int u = 0; u < C1_WREG; ++u)
       if (wk[u] >= 0) wsm[wk[u]] = rw[u];
-    if (threadIdx.x < 32 * (T4 - T))                                       // padded taps
-      wsm[(T + (threadIdx.x >> 5)) * C1_WP + (threadIdx.x & 31)] = 0.f;
+    for (int j = threadIdx.x; j < g.kh * (KW2 - g.kw) * 32; j += C1_T) {
+      const int a = (j >> 5) / (KW2 - g.kw), b = g.kw + (j >> 5) - a * (KW2 - g.kw);
+      wsm[((a * KW2 + b) << 5) + (j & 31)] = 0.f;
+    }
   }
   __syncthreads();
   const int lane = threadIdx.x & 63;
@@ -963,10 +970,9 @@ __global__ __launch_bounds__(C1_T, 1) void conv1_patch_fwd_kernel(
   const int lr = lane & 31, lk = lane >> 5;
   const int orow = wave >> 1;
   const int ocol = (wave & 1) * 64;
-  const int poff = orow * g.sh * PC + (ocol + lr) * g.sw;
-  const float* wa = wsm + lk * C1_WP + lr;
-  const int ta0 = lk / g.kw, tb0 = lk - (lk / g.kw) * g.kw;
-  const int ua0 = (lk + 2) / g.kw, ub0 = (lk + 2) - ((lk + 2) / g.kw) * g.kw;
+  // lane half lk takes kernel column 2p + lk of the pair
+  const int poff = orow * g.sh * PC + (ocol + lr) * g.sw + lk;
+  const float* wa = wsm + lk * 32 + lr;
   for (int cur = 0; t < tiles; t += G, cur ^= 1) {
     const bool more = t + G < tiles;
     if (more) load_patch(t + G);
@@ -978,27 +984,15 @@ __global__ __launch_bounds__(C1_T, 1) void conv1_patch_fwd_kernel(
       acc0[r] = 0.f;
       acc1[r] = 0.f;
     }
-    // tap (row, column) of k = k0 + lk and of k0 + 2 + lk, stepped by 4 taps per iteration
-    // (software-pipelining the LDS reads a step ahead measured slower: 570 -> 620 us)
-    int ta = ta0, tb = tb0, ua = ua0, ub = ub0;
-    for (int k0 = 0; k0 < T4; k0 += 4) {
-      const int t0 = k0 + lk < T ? ta * PC + tb : 0;       // padded taps: zero weight
-      const int t1 = k0 + 2 + lk < T ? ua * PC + ub : 0;
-      const float a0 = wa[k0 * C1_WP], a1 = wa[(k0 + 2) * C1_WP];
-      const float b00 = pb0[t0], b01 = pb1[t0], b10 = pb0[t1], b11 = pb1[t1];
-      acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b00, acc0, 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b01, acc1, 0, 0, 0);
-      acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b10, acc0, 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b11, acc1, 0, 0, 0);
-      tb += 4;                 // kw >= 4 (host check): at most one wrap per step
-      if (tb >= g.kw) {
-        tb -= g.kw;
-        ++ta;
-      }
-      ub += 4;
-      if (ub >= g.kw) {
-        ub -= g.kw;
-        ++ua;
+    for (int a = 0; a < g.kh; ++a) {
+      const float* r0 = pb0 + a * PC;
+      const float* r1 = pb1 + a * PC;
+      const float* wr = wa + a * KW2 * 32;
+#pragma unroll
+      for (int p = 0; p < KWH; ++p) {
+        const float av = wr[2 * p * 32];
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(av, r0[2 * p], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(av, r1[2 * p], acc1, 0, 0, 0);
       }
     }
     // nobody reads the other buffer this round (the last barrier followed every wave's
@@ -1778,14 +1772,14 @@ static int conv_cus() {
 }
 
 // the single-channel patch forward (conv1_patch_fwd_kernel): one input channel, <= 32 output
-// channels, kw >= 4, a patch and filter bank that fit its LDS, input planes within 32-bit
+// channels, 3 <= kw <= 12, a patch and filter bank that fit its LDS, input planes within 32-bit
 // offsets (DS2_CONV_PATCH=0 selects the implicit-GEMM kernel)
 static inline bool c1_ok(const ConvDims& g) {
   if (getenv("DS2_CONV_PATCH") != nullptr && getenv("DS2_CONV_PATCH")[0] == '0') return false;
-  if (g.ci != 1 || g.co > 32 || g.kw < 4) return false;
-  const int64_t pe = (int64_t)((C1_RW - 1) * g.sh + g.kh) * ((C1_WC - 1) * g.sw + g.kw);
-  return pe <= C1_PATCH && 32 * g.kh * g.kw <= C1_WREG * C1_T &&
-         ((g.kh * g.kw + 3) & ~3) <= C1_KMAX;
+  if (g.ci != 1 || g.co > 32 || g.kw < 3 || g.kw > 12) return false;
+  const int kw2 = (g.kw + 1) & ~1;
+  const int64_t pe = (int64_t)((C1_RW - 1) * g.sh + g.kh) * ((C1_WC - 1) * g.sw + kw2);
+  return pe <= C1_PATCH && g.kh * kw2 <= C1_KROWS;
 }
 
 static size_t patch_ws_bytes(const ConvDims& g, bool dgrad) {
@@ -2003,8 +1997,18 @@ ds2_status_t ds2_conv2d_fwd(const float* x, const float* w, const float* bias, f
     const int64_t tiles = (int64_t)gx * gy * n;
     if (tiles > 0x7fffffff) return DS2_UNSUPPORTED_SHAPE;
     const int grid = static_cast<int>(std::min<int64_t>(tiles, conv_cus()));   // one per CU
-    hipLaunchKernelGGL(conv1_patch_fwd_kernel, dim3(grid), dim3(C1_T), 0, as_stream(stream), x, w,
-                       bias, y, g, out_lens, gx, gy, static_cast<int>(tiles));
+    const int tl = static_cast<int>(tiles);
+#define DS2_C1(KWH)                                                                          \
+  hipLaunchKernelGGL(conv1_patch_fwd_kernel<KWH>, dim3(grid), dim3(C1_T), 0, as_stream(stream), \
+                     x, w, bias, y, g, out_lens, gx, gy, tl)
+    switch ((g.kw + 1) / 2) {
+      case 6: DS2_C1(6); break;
+      case 5: DS2_C1(5); break;
+      case 4: DS2_C1(4); break;
+      case 3: DS2_C1(3); break;
+      default: DS2_C1(2); break;
+    }
+#undef DS2_C1
     return launch_status("ds2_conv2d_fwd");
   }
   dim3 grid(cdiv(g.wo, CBN), g.ho, n * cdiv(c_out, 32));
