@@ -711,7 +711,7 @@ constexpr int WG_RW = 2;            // output rows per chunk
 constexpr int WG_CW = 128;          // output columns per chunk
 constexpr int WG_DYP = 33;          // dy tile row pitch
 
-template <int NT, int XS>
+template <int NT, int XS, int SW>
 __global__ __launch_bounds__(256) void conv_wgrad_patch_kernel(const float* __restrict__ dy,
                                                                const float* __restrict__ x,
                                                                float* __restrict__ partial,
@@ -824,17 +824,22 @@ __global__ __launch_bounds__(256) void conv_wgrad_patch_kernel(const float* __re
   for (int k = 0; k < nchunks; ++k) {
     if (k + 1 < nchunks) load(k + 1);
     const float* arow = dys + lk * WG_DYP + lr;
+    // per output row of the chunk one base per tap tile; the position pairs of the row are then
+    // fixed offsets (width stride SW a template parameter): no per-position index arithmetic
     // (software-pipelining these reads a position pair ahead measured slower: 0.58 -> 0.66 ms)
-#pragma unroll 4
-    for (int s2 = 0; s2 < WG_RW * WG_CW / 2; ++s2) {
-      const int pos = 2 * s2;                        // + lk (folded into arow / boff)
-      const int rr = pos / WG_CW;
-      const int cc = pos - rr * WG_CW + lk;
-      const float av = arow[pos * WG_DYP];
-      const int boff = rr * rstep + cc * g.sw;
 #pragma unroll
-      for (int j = 0; j < NT; ++j)
-        acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, xs[tb[j] + boff], acc[j], 0, 0, 0);
+    for (int rr = 0; rr < WG_RW; ++rr) {
+      const float* ar = arow + rr * WG_CW * WG_DYP;
+      const float* xb[NT];
+#pragma unroll
+      for (int j = 0; j < NT; ++j) xb[j] = xs + tb[j] + rr * rstep + lk * SW;
+#pragma unroll 8
+      for (int s = 0; s < WG_CW / 2; ++s) {
+        const float av = ar[2 * s * WG_DYP];
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+          acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, xb[j][2 * s * SW], acc[j], 0, 0, 0);
+      }
     }
     __syncthreads();
     if (k + 1 < nchunks) {
@@ -1918,6 +1923,7 @@ struct WgradPlan {
 static inline WgradPlan wgrad_plan(const ConvDims& g) {
   WgradPlan pl{0, 1, 0};
   if (getenv("DS2_CONV_PATCH") != nullptr && getenv("DS2_CONV_PATCH")[0] == '0') return pl;
+  if (g.sw > 2) return pl;                 // kernels instantiated for width stride 1 and 2
   const int T = g.kh * g.kw;
   const int prow = (WG_RW - 1) * g.sh + g.kh;
   const int pcol = (WG_CW - 1) * g.sw + g.kw;
@@ -2072,12 +2078,15 @@ ds2_status_t ds2_conv2d_wgrad(const float* dy, const float* x, float* dw, float*
                        partial, g, slabs);
   } else if (pl.nt > 0) {
     dim3 grid(static_cast<unsigned>((int64_t)pl.bands * c_in * n * cdiv(c_out, 32)));
-    if (pl.nt == 2)
-      hipLaunchKernelGGL((conv_wgrad_patch_kernel<2, WG_XS_SMALL>), grid, dim3(256), 0, st, dy, x,
-                         partial, g, pl.bands, pl.xpitch);
-    else
-      hipLaunchKernelGGL((conv_wgrad_patch_kernel<4, WG_XS_LARGE>), grid, dim3(256), 0, st, dy, x,
-                         partial, g, pl.bands, pl.xpitch);
+#define DS2_WGP(NT_, XS_, SW_)                                                               \
+  hipLaunchKernelGGL((conv_wgrad_patch_kernel<NT_, XS_, SW_>), grid, dim3(256), 0, st, dy, x, \
+                     partial, g, pl.bands, pl.xpitch)
+    if (pl.nt == 2) {
+      if (g.sw == 2) DS2_WGP(2, WG_XS_SMALL, 2); else DS2_WGP(2, WG_XS_SMALL, 1);
+    } else {
+      if (g.sw == 2) DS2_WGP(4, WG_XS_LARGE, 2); else DS2_WGP(4, WG_XS_LARGE, 1);
+    }
+#undef DS2_WGP
     slabs = n * pl.bands;
   } else {
     dim3 grid(cdiv(Kc, CBNW), n, cdiv(c_out, 32));
