@@ -243,6 +243,13 @@ def main():
                          "pcm: raw 16 kHz PCM resident in HBM, the device STFT + max_frame "
                          "normalisation inside every timed step (SURVEY 8d secondary variant)")
     args = ap.parse_args()
+    maps_out = os.environ.get("DS2_DUMP_MAPS")
+    if maps_out:
+        # exit-time fault forensics: the loaded objects' address ranges, written from an
+        # atexit hook (Python's atexit runs before the C-level exit handlers)
+        import atexit
+        import shutil
+        atexit.register(lambda: shutil.copyfile("/proc/self/maps", maps_out))
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -365,6 +372,14 @@ def main():
                        "global_batch": BATCH * world, "seq_len": T_FRAMES,
                        "parallelism": f"dp{world}"},
             "loss": round(final_loss, 4),
+            "dp": {"process_group": distributed, "world": world,
+                   "buckets": len(tr.reducer.buckets),
+                   "bucket_mb": [round((e - s) * 4 / 2**20, 2) for s, e, _ in tr.reducer.buckets],
+                   "issued_from_hooks": tr.reducer.issued_from_hooks,
+                   "guard_waits": tr.reducer.guard_waits,
+                   "rccl_cta_cap": tr.reducer.rccl_ctas,
+                   "broadcasts": tr.sync.broadcasts,
+                   "status_clean": True},
             "roofline": roof,
             "recurrence": rec,
             "cpu_baseline": cpu,

@@ -6,6 +6,11 @@
 // used in data/audio_aug.py:20,74): center=True with reflect padding of n_fft/2,
 // frames of n_fft every hop, window = the caller's n_fft taps (scipy hamming,
 // symmetric), real FFT evaluated in float64, stored complex64, |.| in float32.
+// normalize_audio modes (data_loader_aug.py:274-313): 0 'none' log1p(S); 1 'max_frame'
+// log1p(S*2^20) - mean_t(gauss20(mean_f)); 2 'mean' log1p(S) - mean; 3 'norm' (log1p(S) -
+// mean) / mean_t(std_f, unbiased); 4 'frame' log1p(S) - mean_t(gauss50(mean_f)).  The stft
+// kernel writes every frame's mean (and, for 'norm', its std) over the 161 rows; one block
+// per utterance turns them into an offset (and scale) that a last pass applies.
 // The DFT is evaluated directly in fp64 (161 bins x 320 taps per frame,
 // twiddles from an LDS table indexed by (k*m) mod n_fft): ~13 GFLOP of fp64 for
 // a 32 x 10 s batch, far below the fp64 roof, and bit-for-bit free of the
@@ -43,11 +48,12 @@ __global__ __launch_bounds__(256) void stft_kernel(const float* __restrict__ pcm
                                                    const double* __restrict__ window,
                                                    int normalize, float* __restrict__ out,
                                                    int max_frames, float* __restrict__ frame_mean,
+                                                   float* __restrict__ frame_std,
                                                    const int* __restrict__ masks,
                                                    float* __restrict__ raw) {
   __shared__ double cs[SMAXN], sn[SMAXN];
   __shared__ double fr[SF][SMAXN];
-  __shared__ double red[SF][4];
+  __shared__ double red[SF][4], red2[SF][4];
   const int b = blockIdx.y;
   const int t0 = blockIdx.x * SF;
   const int nb = n_samples[b];
@@ -91,6 +97,7 @@ __global__ __launch_bounds__(256) void stft_kernel(const float* __restrict__ pcm
   double lsum[SF];
 #pragma unroll
   for (int f = 0; f < SF; ++f) lsum[f] = 0.0;
+  const float gain = normalize == 1 ? 1048576.0f : 1.0f;
   if (k < R) {
     double re[SF], im[SF];
 #pragma unroll
@@ -127,18 +134,26 @@ __global__ __launch_bounds__(256) void stft_kernel(const float* __restrict__ pcm
             fmasked || (t >= tm[0] && t < tm[1]) || (t >= tm[2] && t < tm[3]);
         const float mag =
             masked ? 0.f : hypotf(static_cast<float>(re[f]), static_cast<float>(im[f]));
-        val = normalize ? log1pf(mag * 1048576.0f) : log1pf(mag);
+        val = log1pf(mag * gain);
         lsum[f] = val;
       }
       out[((int64_t)b * R + k) * max_frames + t] = val;
     }
   }
   if (raw != nullptr) return;
-  // mean over the F bins of every frame (torch spect.mean(dim=0))
+  // mean over the F bins of every frame (torch spect.mean(dim=0)); 'norm' also the sum of
+  // squares for the frame's unbiased std (spect.std(dim=0))
 #pragma unroll
   for (int f = 0; f < SF; ++f) {
     double v = wave_sum_d(lsum[f]);
     if ((threadIdx.x & 63) == 0) red[f][threadIdx.x >> 6] = v;
+  }
+  if (frame_std != nullptr) {
+#pragma unroll
+    for (int f = 0; f < SF; ++f) {
+      double v = wave_sum_d(lsum[f] * lsum[f]);
+      if ((threadIdx.x & 63) == 0) red2[f][threadIdx.x >> 6] = v;
+    }
   }
   __syncthreads();
   if (threadIdx.x < SF) {
@@ -147,6 +162,11 @@ __global__ __launch_bounds__(256) void stft_kernel(const float* __restrict__ pcm
     if (t < T && t < max_frames) {
       const double s = red[f][0] + red[f][1] + red[f][2] + red[f][3];
       frame_mean[(int64_t)b * max_frames + t] = static_cast<float>(s / R);
+      if (frame_std != nullptr) {
+        const double q = red2[f][0] + red2[f][1] + red2[f][2] + red2[f][3];
+        const double var = (q - s * s / R) / (R - 1);
+        frame_std[(int64_t)b * max_frames + t] = static_cast<float>(sqrt(var > 0.0 ? var : 0.0));
+      }
     }
   }
 }
@@ -163,7 +183,8 @@ __global__ __launch_bounds__(256) void remap_kernel(const float* __restrict__ ra
                                                     int F, int normalize, int max_frames,
                                                     const int* __restrict__ masks,
                                                     float* __restrict__ out,
-                                                    float* __restrict__ frame_mean) {
+                                                    float* __restrict__ frame_mean,
+                                                    float* __restrict__ frame_std) {
   const int b = blockIdx.y;
   const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
@@ -182,7 +203,8 @@ __global__ __launch_bounds__(256) void remap_kernel(const float* __restrict__ ra
   const bool tmasked = (t >= tm[0] && t < tm[1]) || (t >= tm[2] && t < tm[3]);
   const float* rb = raw + (int64_t)b * max_frames * F;
   const int64_t valid = (int64_t)F * (T < max_frames ? T : max_frames);
-  double lsum = 0.0;
+  double lsum = 0.0, lsq = 0.0;
+  const float gain = normalize == 1 ? 1048576.0f : 1.0f;
   for (int r = lane; r < kRows; r += 64) {
     float val = 0.f;
     if (t < T) {
@@ -191,49 +213,77 @@ __global__ __launch_bounds__(256) void remap_kernel(const float* __restrict__ ra
       const bool masked = tmasked || (r >= fm[0] && r < fm[1]) || (r >= fm[2] && r < fm[3]) ||
                           r >= fcut;
       const float mag = (masked || kf >= valid) ? 0.f : rb[kf];
-      val = normalize ? log1pf(mag * 1048576.0f) : log1pf(mag);
+      val = log1pf(mag * gain);
       lsum += val;
+      lsq += (double)val * val;
     }
     out[((int64_t)b * kRows + r) * max_frames + t] = val;
   }
   lsum = wave_sum_d(lsum);
-  if (lane == 0 && t < T) frame_mean[(int64_t)b * max_frames + t] = static_cast<float>(lsum / kRows);
+  lsq = wave_sum_d(lsq);
+  if (lane == 0 && t < T) {
+    frame_mean[(int64_t)b * max_frames + t] = static_cast<float>(lsum / kRows);
+    if (frame_std != nullptr) {
+      const double var = (lsq - lsum * lsum / kRows) / (kRows - 1);
+      frame_std[(int64_t)b * max_frames + t] = static_cast<float>(sqrt(var > 0.0 ? var : 0.0));
+    }
+  }
 }
 
-// One block per utterance: max_mean = mean_t(gaussian_filter1d(frame_mean, sigma)).
+// One block per utterance.  taps != nullptr ('max_frame', 'frame'): offset =
+// mean_t(gaussian_filter1d(frame_mean, sigma)); else ('mean', 'norm') offset = the mean over
+// all 161 x T values = mean_t(frame_mean), and with frame_std ('norm') scale = mean_t(std).
 __global__ void maxframe_offset_kernel(const int* __restrict__ n_samples, int hop,
                                        int max_frames, const float* __restrict__ frame_mean,
+                                       const float* __restrict__ frame_std,
                                        const float* __restrict__ taps, int radius,
-                                       float* __restrict__ offset) {
+                                       float* __restrict__ offset, float* __restrict__ scale) {
   const int b = blockIdx.x;
   int T = 1 + n_samples[b] / hop;
   if (T > max_frames) T = max_frames;
   const float* m = frame_mean + (int64_t)b * max_frames;
-  double acc = 0.0;
+  double acc = 0.0, acc2 = 0.0;
   for (int t = threadIdx.x; t < T; t += blockDim.x) {
-    double s = 0.0;
-    for (int j = -radius; j <= radius; ++j) s += (double)taps[j + radius] * m[scipy_reflect(t + j, T)];
-    acc += (double)static_cast<float>(s);   // scipy writes the float32 filtered signal
+    if (taps != nullptr) {
+      double s = 0.0;
+      for (int j = -radius; j <= radius; ++j) s += (double)taps[j + radius] * m[scipy_reflect(t + j, T)];
+      acc += (double)static_cast<float>(s);   // scipy writes the float32 filtered signal
+    } else {
+      acc += (double)m[t];
+      if (frame_std != nullptr) acc2 += (double)frame_std[(int64_t)b * max_frames + t];
+    }
   }
-  __shared__ double red[4];
+  __shared__ double red[4], red2[4];
   acc = wave_sum_d(acc);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  acc2 = wave_sum_d(acc2);
+  if ((threadIdx.x & 63) == 0) {
+    red[threadIdx.x >> 6] = acc;
+    red2[threadIdx.x >> 6] = acc2;
+  }
   __syncthreads();
-  if (threadIdx.x == 0) offset[b] = static_cast<float>((red[0] + red[1] + red[2] + red[3]) / T);
+  if (threadIdx.x == 0) {
+    offset[b] = static_cast<float>((red[0] + red[1] + red[2] + red[3]) / T);
+    if (scale != nullptr) scale[b] = static_cast<float>((red2[0] + red2[1] + red2[2] + red2[3]) / T);
+  }
 }
 
 __global__ void subtract_offset_kernel(const int* __restrict__ n_samples, int hop, int F,
                                        int max_frames, const float* __restrict__ offset,
+                                       const float* __restrict__ scale,
                                        float* __restrict__ out) {
   const int b = blockIdx.y;
   int T = 1 + n_samples[b] / hop;
   if (T > max_frames) T = max_frames;
   const float o = offset[b];
+  const float sc = scale != nullptr ? scale[b] : 1.0f;
   const int64_t total = (int64_t)F * max_frames;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * blockDim.x) {
     const int t = static_cast<int>(i % max_frames);
-    if (t < T) out[(int64_t)b * total + i] -= o;
+    if (t < T) {
+      const float v = out[(int64_t)b * total + i] - o;     // spect.add_(-mean)
+      out[(int64_t)b * total + i] = scale != nullptr ? v / sc : v;   // spect.div_(std.mean())
+    }
   }
 }
 
@@ -243,8 +293,9 @@ using namespace ds2;
 
 extern "C" {
 
+// frame_mean, frame_std [batch][max_frames]; offset, scale [batch]
 static size_t stft_base_ws(int batch, int max_frames) {
-  return (size_t)batch * max_frames * sizeof(float) + (size_t)batch * sizeof(float) + 512;
+  return 2 * (size_t)batch * max_frames * sizeof(float) + 2 * (size_t)batch * sizeof(float) + 512;
 }
 
 size_t ds2_stft_workspace_size(int batch, int max_frames, int n_fft) {
@@ -261,34 +312,40 @@ ds2_status_t ds2_stft_logmag_masked(const float* pcm, const int* n_samples, int 
                                     size_t ws_bytes, ds2_stream_t stream) {
   if (batch < 0 || n_fft < 2 || n_fft > SMAXN || hop < 1 || max_frames < 1) return DS2_INVALID_VALUE;
   if (n_fft / 2 + 1 > 256) return DS2_UNSUPPORTED_SHAPE;
-  if (normalize == 1 && (gauss_taps == nullptr || gauss_radius < 0)) return DS2_INVALID_VALUE;
+  if (normalize < 0 || normalize > 4) return DS2_INVALID_VALUE;
+  const bool smooth = normalize == 1 || normalize == 4;
+  if (smooth && (gauss_taps == nullptr || gauss_radius < 0)) return DS2_INVALID_VALUE;
   if (batch == 0) return DS2_OK;
   if (ws == nullptr || ws_bytes < ds2_stft_workspace_size(batch, max_frames, n_fft))
     return DS2_WORKSPACE_TOO_SMALL;
   hipStream_t st = as_stream(stream);
   float* frame_mean = static_cast<float*>(ws);
-  float* offset = frame_mean + (size_t)batch * max_frames;
+  float* frame_std = frame_mean + (size_t)batch * max_frames;
+  float* offset = frame_std + (size_t)batch * max_frames;
+  float* scale = offset + batch;
+  float* fstd = normalize == 3 ? frame_std : nullptr;
   const int F = n_fft / 2 + 1;
   if (F < kRows) {
     float* raw = reinterpret_cast<float*>(
         static_cast<char*>(ws) + ((stft_base_ws(batch, max_frames) + 255) & ~(size_t)255));
     hipLaunchKernelGGL(stft_kernel, dim3(cdiv(max_frames, SF), batch), dim3(256), 0, st, pcm,
                        n_samples, max_samples, n_fft, hop, window, normalize, out, max_frames,
-                       frame_mean, masks, raw);
+                       frame_mean, nullptr, masks, raw);
     hipLaunchKernelGGL(remap_kernel, dim3(cdiv(max_frames, 4), batch), dim3(256), 0, st, raw,
-                       n_samples, hop, F, normalize, max_frames, masks, out, frame_mean);
+                       n_samples, hop, F, normalize, max_frames, masks, out, frame_mean, fstd);
   } else {
     hipLaunchKernelGGL(stft_kernel, dim3(cdiv(max_frames, SF), batch), dim3(256), 0, st, pcm,
                        n_samples, max_samples, n_fft, hop, window, normalize, out, max_frames,
-                       frame_mean, masks, nullptr);
+                       frame_mean, fstd, masks, nullptr);
   }
-  if (normalize == 1) {
+  if (normalize != 0) {
     hipLaunchKernelGGL(maxframe_offset_kernel, dim3(batch), dim3(256), 0, st, n_samples, hop,
-                       max_frames, frame_mean, gauss_taps, gauss_radius, offset);
+                       max_frames, frame_mean, fstd, smooth ? gauss_taps : nullptr, gauss_radius,
+                       offset, normalize == 3 ? scale : nullptr);
     int g = cdiv((int64_t)kRows * max_frames, 256);
     if (g > 512) g = 512;
     hipLaunchKernelGGL(subtract_offset_kernel, dim3(g, batch), dim3(256), 0, st, n_samples, hop,
-                       kRows, max_frames, offset, out);
+                       kRows, max_frames, offset, normalize == 3 ? scale : nullptr, out);
   }
   return launch_status("ds2_stft_logmag");
 }

@@ -116,7 +116,9 @@ class SpectrogramParser(object):
         # waveform augmentations (data_loader_aug.py:361-418, aug_type 0), drawn on the
         # host and replayed on the device (ds2_wave_aug); None unless noise_prob > 0
         noise_dir = audio_conf.get('noise_dir')
-        self.augs = build_audio_augs(audio_conf, sorted(glob(noise_dir)) if noise_dir else ())
+        # glob order unsorted, as the reference's (data_loader_aug.py:363): AddNoise picks a
+        # file by index, so the same draws mix in the same file on the same filesystem
+        self.augs = build_audio_augs(audio_conf, glob(noise_dir) if noise_dir else ())
 
     def _consts(self, sample_rate):
         key = sample_rate
@@ -124,26 +126,35 @@ class SpectrogramParser(object):
             n_fft = int(sample_rate * (self.window_size + 1e-8))
             hop = int(sample_rate * (self.window_stride + 1e-8))
             win = torch.tensor(self.window(n_fft), dtype=torch.float64, device=self.device)
-            taps = torch.tensor(gaussian_taps(20), dtype=torch.float32, device=self.device)
+            # the gaussian_filter1d of 'max_frame' (sigma 20) / 'frame' (sigma 50)
+            sigma = {1: 20, 4: 50}.get(self._mode())
+            taps = None if sigma is None else torch.tensor(gaussian_taps(sigma),
+                                                            dtype=torch.float32, device=self.device)
             self._cache[key] = (n_fft, hop, win, taps)
         return self._cache[key]
 
+    # normalize_audio (data_loader_aug.py:274-313; --norm, train.py:75) -> ds2_stft_logmag mode
+    NORM_MODES = {'none': 0, 'max_frame': 1, 'mean': 2, 'norm': 3, 'frame': 4}
+
     def _mode(self):
-        if self.normalize == 'max_frame':
-            return 1
-        if not self.normalize or self.normalize == 'none':
+        if not self.normalize:
             return 0
-        raise NotImplementedError(f"normalize={self.normalize!r} is not on the ds2amd hot path "
-                                  "(reference default is 'max_frame', train.py:75)")
+        try:
+            return self.NORM_MODES[self.normalize]
+        except KeyError:
+            raise ValueError(f"normalize={self.normalize!r}: the reference's modes are "
+                             f"{sorted(self.NORM_MODES)} (data_loader_aug.py:274-313)") from None
 
     def parse_batch(self, signals: Sequence, sample_rate=None):
         """Raw PCM list (numpy arrays, or audio_aug.Wave records of augmented utterances)
         -> (spect [N,1,F,T_max] on device, frames int32 [N])."""
         sr = sample_rate or self.sample_rate
         n_fft, hop, win, taps = self._consts(sr)
-        if any(isinstance(s, Wave) for s in signals):
+        if any(isinstance(s, Wave) and s.records for s in signals):
             pcm_d, lens = apply_waves(signals, self.device)
         else:
+            # no transform applied anything: the plain PCM upload, no ds2_wave_aug launch
+            signals = [s.samples if isinstance(s, Wave) else s for s in signals]
             lens = [len(s) for s in signals]
             max_s = max(lens)
             pcm = np.zeros((len(signals), max_s), dtype=np.float32)

@@ -328,10 +328,13 @@ def ctc_beam_decode_raw(probs: torch.Tensor, sizes: Optional[torch.Tensor], beam
 
 
 def wave_aug(pcm: torch.Tensor, in_lens: torch.Tensor, op_i: torch.Tensor, op_f: torch.Tensor,
-             noise: Optional[torch.Tensor], out_lens, out_stride: int, cap: int) -> torch.Tensor:
+             noise: Optional[torch.Tensor], out_lens, out_stride: int, cap: int,
+             check: bool = True) -> torch.Tensor:
     """Replay host-drawn waveform-augmentation records on the device (ds2_wave_aug).
     pcm [N, S] fp32, in_lens int32 [N], op_i int32 [N, K, 4], op_f float64 [N, K],
-    noise float64 [R, L] or None -> [N, out_stride] fp32 zero padded."""
+    noise float64 [R, L] or None -> [N, out_stride] fp32 zero padded.  check=False skips the
+    blocking read of the kernel's consistency word, for callers that validated the records
+    on the host (audio_aug.apply_waves)."""
     pcm = _need(pcm, "wave_aug.pcm")
     in_lens = _need(in_lens, "wave_aug.in_lens", _I32)
     op_i = _need(op_i, "wave_aug.op_i", _I32)
@@ -348,7 +351,7 @@ def wave_aug(pcm: torch.Tensor, in_lens: torch.Tensor, op_i: torch.Tensor, op_f:
               op_f.data_ptr(), k, _p(noise), 0 if noise is None else noise.stride(0),
               out.data_ptr(), out_stride, out_lens.data_ptr(), cap, err.data_ptr(), ws.data_ptr(),
               ws.numel(), _stream())
-    if int(err.item()) != 0:
+    if check and int(err.item()) != 0:
         raise _lib.Ds2Error(f"ds2_wave_aug: inconsistent op records (err {int(err.item())})")
     return out
 

@@ -234,11 +234,12 @@ class ParamBroadcaster:
 
 def rccl_channel_cap() -> int:
     """The CTA budget RCCL may hold while a persistent recurrence runs:
-    NCCL_MAX_NCHANNELS, which init_distributed() defaults to 32."""
+    NCCL_MAX_NCHANNELS, which init_distributed() defaults to 32 (the same default applies
+    when the process group was created elsewhere)."""
     try:
-        return int(os.environ.get("NCCL_MAX_NCHANNELS", "64"))
+        return int(os.environ.get("NCCL_MAX_NCHANNELS", "32"))
     except ValueError:
-        return 64
+        return 32
 
 
 class GradAllReducer:

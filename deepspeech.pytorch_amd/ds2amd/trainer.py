@@ -232,7 +232,11 @@ class Trainer:
         self.reducer.begin()
         loss.backward()
         self.reducer.finish()
-        self.optimizer.step()               # clip + SGD; always taken (see module docstring)
+        # clip + SGD; always taken for NaN data (see module docstring).  Skipped on the device
+        # when a persistent recurrence reported a hand-off failure this step: its outputs are
+        # NaN and the update would write NaN into every parameter and momentum slot before the
+        # host sees the error (the word is 0 in a normal step; no host sync)
+        self.optimizer.step(skip_flag=self._rnn_word)
         if side is not None:
             torch.cuda.current_stream(self.device).wait_stream(side)
         if self.world > 1:

@@ -50,7 +50,10 @@ const char* ds2_version(void);
 /*       161 bins when n_fft/2+1 >= 161, else its mirror-fill of ndarray.resize on    */
 /*       librosa's (Fortran-ordered) stft matrix -- see stft.hip remap_kernel.         */
 /* window: n_fft doubles (symmetric Hamming in the reference).                     */
-/* normalize: 0 = log1p(|X|), 1 = 'max_frame' (log1p(|X|*2^20) - mean(gauss20(mean_f))) */
+/* normalize (normalize_audio, data_loader_aug.py:274-313): 0 = 'none' log1p(|X|),        */
+/*   1 = 'max_frame' log1p(|X|*2^20) - mean_t(gauss20(mean_f)), 2 = 'mean' log1p(|X|) - mean, */
+/*   3 = 'norm' (log1p(|X|) - mean) / mean_t(std_f), 4 = 'frame' log1p(|X|) -               */
+/*   mean_t(gauss50(mean_f)); gauss_taps (2 radius + 1 scipy correlation weights) for 1, 4.  */
 size_t ds2_stft_workspace_size(int batch, int max_frames, int n_fft);
 ds2_status_t ds2_stft_logmag(const float* pcm, const int* n_samples, int batch, int max_samples,
                              int n_fft, int hop, const double* window, int normalize,

@@ -85,12 +85,36 @@ def normalize_max_frame(spect: np.ndarray) -> torch.Tensor:
     return s
 
 
+def normalize_audio(spect: np.ndarray, normalize) -> torch.Tensor:
+    """normalize_audio (data_loader_aug.py:274-313), every mode, same op order and dtypes:
+    numpy log1p on the float32 magnitude, then float32 torch reductions."""
+    if normalize == 'mean':                                   # :276-280
+        s = torch.FloatTensor(np.log1p(spect))
+        s.add_(-s.mean())
+        return s
+    if normalize == 'norm':                                   # :281-287
+        s = torch.FloatTensor(np.log1p(spect))
+        s.add_(-s.mean())
+        std = s.std(dim=0, keepdim=True)
+        s.div_(std.mean())
+        return s
+    if normalize == 'frame':                                  # :288-296
+        s = torch.FloatTensor(np.log1p(spect))
+        mean = s.mean(dim=0, keepdim=True)
+        mean = torch.FloatTensor(gaussian_filter1d_reflect(mean.numpy(), 50))
+        s.add_(-mean.mean())
+        return s
+    if normalize == 'max_frame':                              # :297-307
+        return normalize_max_frame(spect)
+    if not normalize or normalize == 'none':                  # :308-310
+        return torch.FloatTensor(np.log1p(spect))
+    raise Exception("No such normalization")                  # :311-312
+
+
 def spectrogram(y, sample_rate=16000, window_size=0.02, window_stride=0.01,
                 normalize='max_frame') -> torch.Tensor:
     mag = rows161(stft_magnitude(y, sample_rate, window_size, window_stride))
-    if normalize == 'max_frame':
-        return normalize_max_frame(mag)
-    return torch.FloatTensor(np.log1p(mag))
+    return normalize_audio(mag, normalize)
 
 
 # ----------------------------------------------------------------------------

@@ -158,3 +158,103 @@ def test_param_broadcaster_matches_ddp_semantics():
     assert (rm0_0 == 1.0).all() and (rm0_1 == 1.0).all()     # rank 0's buffer everywhere
     assert (rm_0 == rm_1).all() and (rv_0 == rv_1).all()
     assert nb0 == nb1 == 1
+
+
+# ---------------------------------------------------------------- the real DS2 layout
+LABELS = "_'ABCDEFGHIJKLMNOPQRSTUVWXYZ2 "
+CONF = dict(sample_rate=16000, window_size=0.02, window_stride=0.01, window='hamming')
+
+
+def _ds2_params():
+    from ds2amd import model as dsm
+    torch.manual_seed(123456)
+    m = dsm.DeepSpeech(rnn_type='gru', labels=LABELS, rnn_hidden_size=800, nb_layers=5,
+                       audio_conf=CONF, bidirectional=True)
+    return m
+
+
+def _rank_grads(params, rank):
+    g = torch.Generator().manual_seed(1000 + rank)
+    return [torch.randn(p.shape, generator=g) for p in params]
+
+
+def _ds2_worker(rank, world, port, out_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.set_num_threads(2)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    m = _ds2_params()
+    params = [p for p in m.parameters() if p.requires_grad]
+    flat = FlatParams(params, "cpu")
+    red = GradAllReducer(flat, bucket_mb=40.0)
+    grads = _rank_grads(params, rank)
+    flat.zero_grad()
+    red.begin()
+    # injected per-rank gradients through autograd, so every parameter's post-accumulate
+    # hook fires as in the real backward (the HIP ops write into the flat slots instead)
+    loss = sum((p * g).sum() for p, g in zip(params, grads))
+    loss.backward()
+    issued = red.issued_from_hooks
+    in_flight = sum(h is not None for h in red.handles)
+    # CU budget: the 208-workgroup cooperative backward plus RCCL's
+    # 32-CTA default fits 256 CUs -> no wait; a 64-channel cap would not -> the compute
+    # stream waits for every all-reduce in flight
+    red.cus = 256
+    red.guard_cooperative(208)
+    waits_fit = red.guard_waits
+    red.rccl_ctas = 64
+    red.guard_cooperative(208)
+    waits_over = red.guard_waits
+    red.finish()
+    out_q.put((rank, red.buckets, flat.offsets, [p.numel() for p in flat.params], flat.numel,
+               issued, in_flight, waits_fit, waits_over, flat.grad.numpy().copy()))
+    dist.destroy_process_group()
+
+
+def test_grad_allreduce_real_ds2_layout():
+    """GradAllReducer over the real DeepSpeech(5 x BiGRU-800) parameter list (41.2 M
+    parameters, 164.8 MB flat, reverse layer order) with the bench's 40 MB buckets, gloo
+    world 2: bucket boundaries fall on the first parameter boundary at or past 40 MB, every
+    bucket is issued from the backward hooks, the result is the 1/W average of the ranks'
+    gradients (train.py:947-951, data/utils.py:40-44), and the CU-budget guard waits only
+    when the cooperative grid plus RCCL's CTA cap exceeds the chip."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ds2_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    m = _ds2_params()
+    params = [p for p in m.parameters() if p.requires_grad]
+    assert sum(p.numel() for p in params) > 41_000_000
+    cap = 40 * 1024 * 1024 // 4
+    expect = None
+    for rank, buckets, offs, sizes, numel, issued, in_flight, waits_fit, waits_over, g in res:
+        # boundaries: contiguous, cover the flat buffer, close at the first parameter
+        # boundary at or past the cap
+        assert buckets[0][0] == 0 and buckets[-1][1] == numel
+        bounds = offs[1:] + [numel]
+        for i, (s_, e, n) in enumerate(buckets):
+            assert e in bounds and n >= 1
+            if i + 1 < len(buckets):
+                assert buckets[i + 1][0] == e
+                assert e - s_ >= cap
+                prev = [b for b in bounds if s_ < b < e]
+                assert all(b - s_ < cap for b in prev)
+        assert len(buckets) == 4, [(b[1] - b[0]) * 4 / 2**20 for b in buckets]
+        assert sum(b[2] for b in buckets) == len(sizes)
+        assert issued == len(buckets) and in_flight == len(buckets)
+        assert waits_fit == 0 and waits_over == len(buckets)
+        if expect is None:
+            # (g0 + g1) / 2 in the flat layout (reverse registration order)
+            g0 = _rank_grads(params, 0)
+            g1 = _rank_grads(params, 1)
+            expect = torch.zeros(numel)
+            for p_, a, b, o in zip(reversed(params), reversed(g0), reversed(g1), offs):
+                expect[o:o + p_.numel()] = ((a + b) * 0.5).reshape(-1)
+        assert torch.equal(torch.from_numpy(g), expect)

@@ -837,6 +837,39 @@ def test_stft_other_sample_rates_vs_oracle(dev, sr, masked):
         assert out[i, 0, :, ref.shape[1]:].abs().sum().item() == 0
 
 
+@pytest.mark.parametrize("norm", ["none", "mean", "norm", "frame", "max_frame"])
+@pytest.mark.parametrize("sr", [16000, 8000])
+def test_stft_norm_modes_vs_oracle(dev, norm, sr):
+    """Every normalize_audio mode (data_loader_aug.py:274-313; --norm, train.py:75) on the
+    device against the oracle's restatement, on the 161-bin path (16 kHz) and the 8 kHz
+    mirror-fill path; utterance lengths include 'frame''s sigma-50 filter (radius 200)
+    reflecting over fewer frames than its radius."""
+    from ds2amd.data_loader import SpectrogramParser
+    conf = dict(sample_rate=sr, window_size=0.02, window_stride=0.01, window='hamming')
+    parser = SpectrogramParser(conf, normalize=norm, device=dev)
+    rng = np.random.default_rng(11)
+    wavs = [(rng.standard_normal(n) * 0.3).astype(np.float32)
+            for n in (sr * 3 + 5, sr // 2 + 7, sr // 10)]
+    wavs.append(np.sin(np.arange(sr) * 0.05).astype(np.float32) * 0.5)
+    out, frames = parser.parse_batch(wavs, sr)
+    for i, y in enumerate(wavs):
+        ref = orc.spectrogram(y, sr, normalize=norm)
+        assert int(frames[i]) == ref.shape[1]
+        got = out[i, 0, :, :ref.shape[1]].cpu()
+        scale = max(1.0, ref.abs().max().item())
+        err = (got - ref).abs().max().item()
+        assert err < 2e-5 * scale + 1e-5, f"{norm} sr {sr} wav {i}: max abs err {err}"
+        assert out[i, 0, :, ref.shape[1]:].abs().sum().item() == 0
+
+
+def test_stft_unknown_norm_raises():
+    from ds2amd.data_loader import SpectrogramParser
+    p = SpectrogramParser(dict(sample_rate=16000, window_size=0.02, window_stride=0.01),
+                          normalize='bogus', device='cpu')
+    with pytest.raises(ValueError, match="normalize"):
+        p._mode()
+
+
 # ---------------------------------------------------------------------------- optimizer
 def test_fused_sgd_matches_torch(dev):
     from ds2amd.optim import FlatParams, FusedSGD

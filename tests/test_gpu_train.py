@@ -64,14 +64,30 @@ def _spect_batch(g, t_list, t_max):
 def test_benchmark_train_step_matches_oracle(dev):
     """5 x BiGRU-800 at T = 1001 (10 s), bs 4, variable lengths through input_percentages
     with the float32 quirk lengths of T_max = 1001 (508 -> 507, 254 -> 253; train.py:557):
-    the full Trainer.train_batch (forward, decode, CTC, BPTT over 501 steps through both
-    batch tiles of the persistent kernels, clip, SGD-Nesterov) vs oracle.train_step."""
+    the full Trainer.train_batch (forward, decode, CTC, BPTT over 501 steps in ONE
+    16-sample batch tile of the persistent kernels, clip, SGD-Nesterov) vs oracle.train_step.
+    Two batch tiles at this shape: test_benchmark_train_step_two_batch_tiles."""
+    _check_train_step(dev, [1001, 877, 508, 254], [150, 120, 80, 40], seed=11)
+
+
+@pytest.mark.timeout(600)
+def test_benchmark_train_step_two_batch_tiles(dev):
+    """As above at bs 20: the persistent recurrences run TWO batch tiles (samples 0-15 and
+    16-19, the second one partly empty) per direction, so the hand-off groups of both tiles,
+    the per-tile length masks and the bias-gradient partials of both tiles are checked over
+    the full 501-step BPTT against the oracle, with the same bounds."""
+    t_list = [1001, 1001, 990, 950, 901, 877, 820, 760, 700, 640, 600, 508, 470, 400, 333,
+              300, 254, 200, 150, 101]
+    lab = [max(10, t // 7) for t in t_list]
+    _check_train_step(dev, t_list, lab, seed=12)
+
+
+def _check_train_step(dev, t_list, label_lens, seed):
     _threads()
-    t_list = [1001, 877, 508, 254]
-    g = torch.Generator().manual_seed(11)
+    g = torch.Generator().manual_seed(seed)
     x = _spect_batch(g, t_list, 1001)
     pct = torch.tensor([t / 1001.0 for t in t_list], dtype=torch.float32)
-    tg, tl = _targets(g, [150, 120, 80, 40])
+    tg, tl = _targets(g, label_lens)
     m = _build(123456, 800, 5)
     o = orc.OracleDS2({k: v.detach().clone() for k, v in m.state_dict().items()}, 5, 800)
     before = {k: v.detach().clone() for k, v in m.named_parameters()}
@@ -162,8 +178,12 @@ def test_rnn_handoff_timeout_raises(dev, monkeypatch):
     monkeypatch.setenv("DS2_RNN_SPIN_LIMIT", "0")
     monkeypatch.setenv("DS2_RNN_TUNE", "1,0")   # poll at once: early polls must find stale tiles
     tr = Trainer(_build(3, 256, 2), LABELS, device=dev, verbose=False)
+    p0, m0 = tr.flat.flat.clone(), tr.optimizer.buf.clone()
     with pytest.raises(_lib.Ds2Error, match="hand-off"):
         tr.train_batch((x, tg, None, pct.clone(), tl), return_item=True)
+    # the failed step's update was skipped on the device: parameters and momentum intact
+    assert torch.isfinite(tr.flat.flat).all() and torch.isfinite(tr.optimizer.buf).all()
+    assert torch.equal(tr.flat.flat, p0) and torch.equal(tr.optimizer.buf, m0)
     # the op-level query sees it too
     lens = torch.full((32,), 151, dtype=torch.int32, device=dev)
     xs = torch.randn(151, 32, 256, device=dev)
