@@ -388,6 +388,15 @@ def main():
     if distributed:
         dist.barrier()
         dist.destroy_process_group()
+    if os.environ.get("DS2_CLEAN_EXIT") == "1":
+        # release every device object of the run before the interpreter's exit handlers
+        # (exit-time teardown diagnostics, scripts/prof_exit_probe2.sh)
+        import gc
+        torch.cuda.synchronize()
+        del tr, m, x, probe, rprobe
+        gc.collect()
+        torch.cuda.empty_cache()
+        torch.cuda.synchronize()
 
 
 if __name__ == "__main__":

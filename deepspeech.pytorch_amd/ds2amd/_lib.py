@@ -33,6 +33,12 @@ _PROTOS = {
     "ds2_wave_aug_workspace_size": (_sz, [_c_int, _c_i64]),
     "ds2_wave_aug": (_c_int, [_vp, _c_i64, _vp, _c_int, _vp, _vp, _c_int, _vp, _c_i64, _vp,
                               _c_i64, _vp, _c_i64, _vp, _vp, _sz, _vp]),
+    "ds2_time_stretch_workspace_size": (_sz, [_c_int, _c_int, _c_int]),
+    "ds2_time_stretch": (_c_int, [_vp, _c_i64, _vp, _c_int, _vp, _vp, _vp, _vp, _vp, _vp, _c_i64,
+                                  _c_int, _c_int, _vp, _sz, _vp]),
+    "ds2_resample_workspace_size": (_sz, [_c_int, _c_i64]),
+    "ds2_resample": (_c_int, [_vp, _c_i64, _vp, _c_int, _vp, _vp, _vp, _c_int, _c_int, _vp,
+                              _c_i64, _vp, _sz, _vp]),
     "ds2_sgemm": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _c_f, _vp, _c_i64, _c_i64,
                            _vp, _c_i64, _c_i64, _c_f, _vp, _c_i64, _c_i64, _c_int, _vp, _vp]),
     "ds2_sgemm_workspace_size": (_sz, [_c_int, _c_int, _c_int, _c_int]),

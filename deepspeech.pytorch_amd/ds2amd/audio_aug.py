@@ -11,9 +11,12 @@ device PCM buffer the STFT kernel reads.
 
 * ``Shift`` (audio_aug.py:26-44), ``AudioDistort`` (:47-60, ``clip`` :177-178),
   ``AddNoise`` (:78-107, incl. ``get_stacked_noise`` :110-134): built.
-* ``ChangeAudioSpeed`` (:7-23) and ``PitchShift`` (:63-75) wrap librosa's phase
-  vocoder / resampler, which are absent here: their draws are made in the reference
-  order, and applying them raises ``NotImplementedError``.
+* ``ChangeAudioSpeed`` (:7-23, librosa.effects.time_stretch) and ``PitchShift``
+  (:63-75, librosa.effects.pitch_shift = time stretch + resampy resampling): their draws
+  are made in the reference order and replayed on the device by ``ds2_time_stretch`` /
+  ``ds2_resample`` (csrc/effects.hip, restated from librosa 0.8 / resampy 0.2; parity with
+  librosa itself unpinned, it is absent here — oracle/librosa_effects.py is the checker).
+  A file at another sample rate is resampled the same way (data_loader_aug.py:668).
 * ``Compose`` / ``OneOf`` / ``OneOrOther`` (:137-174): same semantics, including
   ``OneOf`` setting the chosen transform's ``prob`` to 1 for good (:160).
 """
@@ -27,7 +30,9 @@ import torch
 
 from . import ops
 
-SHIFT, DISTORT, NOISE = 1, 2, 3
+SHIFT, DISTORT, NOISE = 1, 2, 3          # replayed by ds2_wave_aug
+STRETCH, PITCH, RESAMPLE = 4, 5, 6       # ds2_time_stretch / ds2_resample (before the above)
+HEAVY = (STRETCH, PITCH, RESAMPLE)
 MAX_DURATION_AUG = 10          # seconds (data_loader_aug.py:49)
 
 
@@ -64,9 +69,10 @@ class ChangeAudioSpeed:
         assert len(wav.shape) == 1
         if random.random() < self.prob:
             alpha = 1.0 + self.limit * random.uniform(-1, 1)
-            raise NotImplementedError(
-                f"ChangeAudioSpeed (librosa.effects.time_stretch, rate {alpha:.4f}) is not "
-                "available on the ds2amd device front-end (librosa is absent)")
+            new_len = ops.stretch_plan(wav.length, alpha)[0]     # len(time_stretch(wav, alpha))
+            if new_len < self.max_duration:
+                wav.record(STRETCH, alpha=alpha)
+                wav.length = new_len
         return {'wav': wav, 'sr': sr}
 
 
@@ -112,9 +118,7 @@ class PitchShift:
         assert len(wav.shape) == 1
         if random.random() < self.prob:
             alpha = self.limit * random.uniform(-1, 1)
-            raise NotImplementedError(
-                f"PitchShift (librosa.effects.pitch_shift, {alpha:.3f} half-steps) is not "
-                "available on the ds2amd device front-end (librosa is absent)")
+            wav.record(PITCH, a=int(sr), alpha=alpha)     # length unchanged (fix_length)
         return {'wav': wav, 'sr': sr}
 
 
@@ -126,7 +130,9 @@ def get_stacked_noise(noise_path=None, wav=None, sr=16000):
     noise, sample_rate = load_audio_norm(noise_path)
     assert len(noise.shape) == 1
     if sample_rate != sr:
-        raise NotImplementedError("get_stacked_noise: resampling noise needs librosa (absent)")
+        # the reference's branch resamples an undefined `y` (audio_aug.py:117-118)
+        raise NameError("get_stacked_noise: name 'y' is not defined (reference "
+                        "data/audio_aug.py:118 resamples an undefined variable)")
     if noise.shape[0] > wav.shape[0]:
         return noise
     assert False, "get_stacked_noise: noise shorter than the utterance (reference :123-128)"
@@ -215,23 +221,82 @@ def build_audio_augs(audio_conf, noise_samples: Sequence[str] = (), max_duration
     ], prob=aug_prob)
 
 
+def _heavy(kind, a, b, alpha, lens, pcm):
+    """One device effect over the selected rows: -> (out [k, S'], new lengths)."""
+    if kind == STRETCH:
+        return ops.time_stretch(pcm, lens, alpha)
+    if kind == RESAMPLE:
+        ratios = [float(bb) / aa for aa, bb in zip(a, b)]                # sr_new / sr_orig
+        out_lens = [int(np.ceil(l * r)) for l, r in zip(lens, ratios)]   # librosa fix_length
+        return ops.resample(pcm, lens, ratios, out_lens)
+    # PITCH: time_stretch by rate = 2 ** (-n / 12), resample sr / rate -> sr, fix_length(len)
+    rates = [2.0 ** (-float(n) / 12) for n in alpha]
+    y, ylens = ops.time_stretch(pcm, lens, rates)
+    ratios = [float(sr) / (float(sr) / r) for sr, r in zip(a, rates)]
+    return ops.resample(y, ylens, ratios, [int(l) for l in lens])
+
+
+def heavy_length(kind, a, b, alpha, length):
+    if kind == STRETCH:
+        return ops.stretch_plan(length, alpha)[0]
+    if kind == RESAMPLE:
+        return int(np.ceil(length * (float(b) / a)))
+    return length
+
+
 def apply_waves(waves: Sequence[Wave], device) -> tuple:
     """Replay the records of a batch on the device: -> (pcm [N, S_max] fp32 device,
-    lengths list).  One ds2_wave_aug launch; the input is uploaded once."""
+    lengths list).  The librosa effects (resample, time stretch, pitch shift) lead an
+    utterance's records (a file's resampling at load, then OneOf's one transform); each
+    round of them is one ds2_resample / ds2_time_stretch launch over the utterances that
+    have one; the remaining records are one ds2_wave_aug launch.  Uploaded once."""
     waves = [_as_wave(w) for w in waves]
     n = len(waves)
+    heavy, light = [], []
+    for b, w in enumerate(waves):
+        k = 0
+        while k < len(w.records) and w.records[k][0] in HEAVY:
+            k += 1
+        if any(r[0] in HEAVY for r in w.records[k:]):
+            raise NotImplementedError(f"utterance {b}: a librosa effect after a replayed "
+                                      "transform (the reference's pipelines never do this)")
+        heavy.append(w.records[:k])
+        light.append(w.records[k:])
     s_in = max(w.samples.shape[0] for w in waves)
-    k = max(1, max(len(w.records) for w in waves))
     pcm = np.zeros((n, max(s_in, 1)), dtype=np.float32)
+    for b, w in enumerate(waves):
+        pcm[b, :w.samples.shape[0]] = w.samples
+    pcm_d = torch.from_numpy(pcm).to(device)
+    base = [w.samples.shape[0] for w in waves]
+    for h in range(max((len(r) for r in heavy), default=0)):
+        outs = {}
+        for kind in HEAVY:
+            rows = [b for b in range(n) if len(heavy[b]) > h and heavy[b][h][0] == kind]
+            if not rows:
+                continue
+            recs = [heavy[b][h] for b in rows]
+            y, ylens = _heavy(kind, [r[1] for r in recs], [r[2] for r in recs],
+                              [r[3] for r in recs], [base[b] for b in rows],
+                              pcm_d[torch.tensor(rows, device=device)])
+            for i, b in enumerate(rows):
+                outs[b] = (y[i], ylens[i])
+        new_base = [outs[b][1] if b in outs else base[b] for b in range(n)]
+        nxt = torch.zeros(n, max(1, max(new_base)), device=device, dtype=torch.float32)
+        for b in range(n):
+            if b in outs:
+                nxt[b, :new_base[b]] = outs[b][0][:new_base[b]]
+            else:
+                nxt[b, :base[b]] = pcm_d[b, :base[b]]
+        pcm_d, base = nxt, new_base
+    k = max(1, max(len(r) for r in light))
     op_i = np.zeros((n, k, 4), dtype=np.int32)
     op_f = np.zeros((n, k), dtype=np.float64)
     rows: List[np.ndarray] = []
     cap = 1
     for b, w in enumerate(waves):
-        pcm[b, :w.samples.shape[0]] = w.samples
-        ln = w.samples.shape[0]
+        ln = base[b]
         cap = max(cap, ln)
-        for j, (kind, a, bb, alpha, nz) in enumerate(w.records):
+        for j, (kind, a, bb, alpha, nz) in enumerate(light[b]):
             if kind == SHIFT:
                 ln += bb
             elif kind == NOISE:
@@ -243,6 +308,8 @@ def apply_waves(waves: Sequence[Wave], device) -> tuple:
         if ln != w.length:
             raise ValueError(f"utterance {b}: records give {ln} samples, the transforms {w.length}")
     lens = [w.length for w in waves]
+    if not any(light):
+        return pcm_d, lens
     # the records were validated above (every length and the buffer cap follow from them,
     # as the kernel recomputes), so the kernel's consistency word is not read back: no
     # device sync per batch
@@ -253,8 +320,7 @@ def apply_waves(waves: Sequence[Wave], device) -> tuple:
         for r, seg in enumerate(rows):
             nz[r, :seg.shape[0]] = seg
         noise = torch.from_numpy(nz).to(device)
-    out = ops.wave_aug(torch.from_numpy(pcm).to(device),
-                       torch.tensor([w.samples.shape[0] for w in waves], dtype=torch.int32).to(device),
+    out = ops.wave_aug(pcm_d, torch.tensor(base, dtype=torch.int32).to(device),
                        torch.from_numpy(op_i).to(device), torch.from_numpy(op_f).to(device), noise,
                        lens, max(lens), cap, check=False)
     return out, lens

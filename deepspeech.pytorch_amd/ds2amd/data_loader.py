@@ -23,7 +23,7 @@ from torch.utils.data import DataLoader
 from torch.utils.data.sampler import Sampler
 
 from . import ops
-from .audio_aug import Wave, apply_waves, build_audio_augs
+from .audio_aug import RESAMPLE, Wave, apply_waves, build_audio_augs, heavy_length
 from .spect_aug import SpectAugmenter
 
 # tempo classes of the reference's legacy sox path (data_loader_aug.py:108-112); only the
@@ -88,10 +88,11 @@ def load_randomly_augmented_audio(path, sample_rate=16000, tempo_range=(0.85, 1.
     np.random.uniform(low=tempo_range[0], high=tempo_range[1])
     np.random.uniform(low=gain_range[0], high=gain_range[1])
     y, sr = load_audio_norm(path, channel=channel)
-    if sr != sample_rate:
-        raise NotImplementedError(f"{path}: {sr} Hz audio needs librosa.resample to {sample_rate} "
-                                  "Hz (librosa is absent)")
     wav = Wave(y)
+    if sr != sample_rate:
+        # librosa.resample(y, sr, sample_rate) (data_loader_aug.py:667-668), on the device
+        wav.record(RESAMPLE, a=sr, b=sample_rate)
+        wav.length = heavy_length(RESAMPLE, sr, sample_rate, 0.0, wav.length)
     if transforms is not None:
         wav = transforms(**{'wav': wav, 'sr': sample_rate})['wav']
     return wav, sample_rate

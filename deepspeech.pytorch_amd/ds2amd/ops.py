@@ -10,6 +10,7 @@ from __future__ import annotations
 
 from typing import Optional, Tuple
 
+import numpy as np
 import torch
 
 from . import _lib
@@ -354,6 +355,109 @@ def wave_aug(pcm: torch.Tensor, in_lens: torch.Tensor, op_i: torch.Tensor, op_f:
     if check and int(err.item()) != 0:
         raise _lib.Ds2Error(f"ds2_wave_aug: inconsistent op records (err {int(err.item())})")
     return out
+
+
+# librosa / resampy effects (csrc/effects.hip): ChangeAudioSpeed, PitchShift, resampling
+FX_N_FFT, FX_HOP = 2048, 512
+
+
+def hann_periodic(n: int) -> np.ndarray:
+    """scipy.signal.get_window('hann', n, fftbins=True): general_cosine over n + 1 points,
+    last one dropped (same float64 operations as scipy)."""
+    fac = np.linspace(-np.pi, np.pi, n + 1)
+    w = np.zeros(n + 1)
+    w += 0.5 * np.cos(0 * fac)
+    w += 0.5 * np.cos(fac)
+    return w[:-1]
+
+
+_FX_CONST = {}
+
+
+def _fx_window(dev):
+    key = ('hann', dev)
+    if key not in _FX_CONST:
+        _FX_CONST[key] = torch.from_numpy(hann_periodic(FX_N_FFT)).to(dev)
+    return _FX_CONST[key]
+
+
+def kaiser_best_filter() -> tuple:
+    """resampy 'kaiser_best': sinc_window(num_zeros=64, precision=9,
+    window=kaiser(beta=14.769656459379492), rolloff=0.9475937167399596) -> (right wing
+    float64 [64 * 512 + 1], 512 samples per zero crossing)."""
+    from scipy.signal.windows import kaiser
+    num_zeros, num_bits, beta, rolloff = 64, 2 ** 9, 14.769656459379492, 0.9475937167399596
+    n = num_bits * num_zeros
+    sinc_win = rolloff * np.sinc(rolloff * np.linspace(0, num_zeros, num=n + 1, endpoint=True))
+    taper = kaiser(2 * n + 1, beta)[n:]
+    return taper * sinc_win, num_bits
+
+
+def _fx_filter(dev):
+    key = ('kaiser_best', dev)
+    if key not in _FX_CONST:
+        win, nb = kaiser_best_filter()
+        _FX_CONST[key] = (torch.from_numpy(np.ascontiguousarray(win)).to(dev), nb)
+    return _FX_CONST[key]
+
+
+def stretch_plan(in_len: int, rate: float) -> tuple:
+    """(out_len, out_frames, used_frames) of librosa.effects.time_stretch(y, rate) for a
+    len-in_len y: round(len / rate) (Python round), ceil(frames / rate) (np.arange length),
+    min(that, ceil((out_len + n_fft) / hop)) (istft's length-limited frame count)."""
+    import math
+    frames = 1 + in_len // FX_HOP
+    out_len = int(round(in_len / rate))
+    out_frames = int(math.ceil((frames - 0) / rate))
+    used = min(out_frames, int(math.ceil((out_len + FX_N_FFT) / FX_HOP)))
+    return out_len, out_frames, used
+
+
+def time_stretch(pcm: torch.Tensor, lens, rates) -> tuple:
+    """Per-utterance librosa.effects.time_stretch on the device (ds2_time_stretch).
+    pcm [N, S] fp32 device, lens / rates host sequences -> (out [N, max out_len], out_lens)."""
+    pcm = _need(pcm, "time_stretch.pcm")
+    n = pcm.shape[0]
+    dev = pcm.device
+    plans = [stretch_plan(int(l), float(r)) for l, r in zip(lens, rates)]
+    out_lens = [p[0] for p in plans]
+    stride = max(1, max(out_lens) if out_lens else 1)
+    max_in = max([1 + int(l) // FX_HOP for l in lens] or [1])
+    max_out = max([p[1] for p in plans] or [1])
+    i32 = lambda v: torch.tensor(v, dtype=_I32).to(dev)
+    out = torch.empty(n, stride, device=dev, dtype=_F32)
+    ws = _ws(_lib.size("ds2_time_stretch_workspace_size", n, max_in, max_out), dev)
+    lens_d, rate_d = i32([int(l) for l in lens]), torch.tensor([float(r) for r in rates],
+                                                               dtype=torch.float64).to(dev)
+    of_d, uf_d, ol_d = i32([p[1] for p in plans]), i32([p[2] for p in plans]), i32(out_lens)
+    _lib.call("ds2_time_stretch", pcm.data_ptr(), pcm.stride(0), lens_d.data_ptr(), n,
+              rate_d.data_ptr(), of_d.data_ptr(), uf_d.data_ptr(), ol_d.data_ptr(),
+              _fx_window(dev).data_ptr(), out.data_ptr(), stride, max_in, max_out, ws.data_ptr(),
+              ws.numel(), _stream())
+    return out, out_lens
+
+
+def resample(pcm: torch.Tensor, lens, ratios, out_lens=None) -> tuple:
+    """Per-utterance resampy 'kaiser_best' resampling on the device (ds2_resample).
+    ratios = sr_new / sr_orig (float64 as numpy forms it); each utterance yields
+    int(len * ratio) samples, zero-padded to out_lens (default: that count)."""
+    pcm = _need(pcm, "resample.pcm")
+    n = pcm.shape[0]
+    dev = pcm.device
+    valid = [int(int(l) * float(r)) for l, r in zip(lens, ratios)]
+    if out_lens is None:
+        out_lens = valid
+    stride = max(1, max(out_lens) if len(out_lens) else 1)
+    out = torch.empty(n, stride, device=dev, dtype=_F32)
+    win, nb = _fx_filter(dev)
+    ws = _ws(_lib.size("ds2_resample_workspace_size", n, stride), dev)
+    lens_d = torch.tensor([int(l) for l in lens], dtype=_I32).to(dev)
+    valid_d = torch.tensor([min(v, o) for v, o in zip(valid, out_lens)], dtype=_I32).to(dev)
+    ratio_d = torch.tensor([float(r) for r in ratios], dtype=torch.float64).to(dev)
+    _lib.call("ds2_resample", pcm.data_ptr(), pcm.stride(0), lens_d.data_ptr(), n,
+              ratio_d.data_ptr(), valid_d.data_ptr(), win.data_ptr(), win.numel(), nb,
+              out.data_ptr(), stride, ws.data_ptr(), ws.numel(), _stream())
+    return out, list(out_lens)
 
 
 SPECT_ROWS = 161   # rows of every spectrogram the reference returns (data_loader_aug.py:234-249)

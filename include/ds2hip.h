@@ -89,6 +89,29 @@ ds2_status_t ds2_wave_aug(const float* in, int64_t in_stride, const int* in_lens
                           const int* out_lens, int64_t cap, int* err, void* ws, size_t ws_bytes,
                           ds2_stream_t stream);
 
+/* librosa.effects.time_stretch(y, rate[b]) per utterance (ChangeAudioSpeed, data/audio_aug.py:7-23;
+ * the stretch half of PitchShift, :63-75): STFT (n_fft 2048, hop 512, periodic Hann `window`
+ * [2048] doubles, reflect pad) -> phase vocoder -> ISTFT, librosa 0.8 semantics (csrc/effects.hip,
+ * oracle/librosa_effects.py).  x: [n][x_stride] fp32 with in_lens; per utterance, host-computed:
+ * out_frames = ceil((1 + in_len / 512) / rate) (np.arange), used_frames = min(out_frames,
+ * ceil((out_len + 2048) / 512)) (istft's `length`), out_lens = round(in_len / rate).  out:
+ * [n][out_stride], zero past out_lens.  max_*_frames bound the per-utterance counts. */
+size_t ds2_time_stretch_workspace_size(int n, int max_in_frames, int max_out_frames);
+ds2_status_t ds2_time_stretch(const float* x, int64_t x_stride, const int* in_lens, int n,
+                              const double* rate, const int* out_frames, const int* used_frames,
+                              const int* out_lens, const double* window, float* out,
+                              int64_t out_stride, int max_in_frames, int max_out_frames, void* ws,
+                              size_t ws_bytes, ds2_stream_t stream);
+/* resampy.resample(x, sr_orig, sr_new, filter='kaiser_best') per utterance (librosa.resample,
+ * data_loader_aug.py:668; the resample half of PitchShift): ratio[b] = sr_new / sr_orig,
+ * n_valid[b] = int(in_len * ratio) output samples, zero up to out_stride (librosa's fix_length).
+ * win: the filter's right wing (nwin doubles, num_table samples per zero crossing). */
+size_t ds2_resample_workspace_size(int n, int64_t max_out);
+ds2_status_t ds2_resample(const float* x, int64_t x_stride, const int* in_lens, int n,
+                          const double* ratio, const int* n_valid, const double* win, int nwin,
+                          int num_table, float* out, int64_t out_stride, void* ws,
+                          size_t ws_bytes, ds2_stream_t stream);
+
 /* ------------------------------------------------------------------------ */
 /* Dense fp32 GEMM on MFMA (v_mfma_f32_16x16x4_f32 / 32x32x2_f32), strided-batched, row-major.
  * C[b] = alpha * op(A[b]) @ op(B[b]) + beta * C[b] (+ bias[n] if bias != NULL)

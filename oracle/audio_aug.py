@@ -1,7 +1,8 @@
 """CPU restatement of the reference waveform augmentations — TEST INFRASTRUCTURE.
 
 Restates data/audio_aug.py's Shift (:26-44), AudioDistort (:47-60, clip :177-178),
-AddNoise (:78-107, get_stacked_noise :110-134) and OneOf (:149-162) on numpy arrays,
+AddNoise (:78-107, get_stacked_noise :110-134), ChangeAudioSpeed (:7-23) and PitchShift
+(:63-75) (on oracle/librosa_effects.py's librosa restatement) and OneOf (:149-162) on numpy arrays,
 with the reference's `random` / `np.random` calls in the reference's order and its
 numpy dtypes (float32 in, float64 after Shift's np.zeros or AddNoise's float64 mix,
 float32 math in AudioDistort).  Transforms are plain dicts here ({'kind', 'prob', ...});
@@ -64,7 +65,28 @@ def _add_noise(t, wav, sr):
     return wav
 
 
-APPLY = {'shift': _shift, 'distort': _distort, 'noise': _add_noise}
+def _stretch(t, wav, sr):
+    """ChangeAudioSpeed (audio_aug.py:7-23) on the librosa restatement."""
+    from oracle import librosa_effects as le
+    if random.random() < t['prob']:
+        a = 1.0 + t['limit'] * random.uniform(-1, 1)
+        y = le.time_stretch(wav, a)
+        if y.shape[0] < t['max_duration'] * t['sr']:
+            wav = y
+    return wav
+
+
+def _pitch(t, wav, sr):
+    """PitchShift (audio_aug.py:63-75) on the librosa restatement."""
+    from oracle import librosa_effects as le
+    if random.random() < t['prob']:
+        a = t['limit'] * random.uniform(-1, 1)
+        wav = le.pitch_shift(wav, sr, n_steps=a)
+    return wav
+
+
+APPLY = {'shift': _shift, 'distort': _distort, 'noise': _add_noise, 'stretch': _stretch,
+         'pitch': _pitch}
 
 
 def make_one_of(transforms, p):

@@ -94,12 +94,18 @@ def test_distort_hand_case():
     assert _replay(w).tolist() == [0.0, 0.25, 1.0]
 
 
-def test_librosa_transforms_raise_only_when_drawn():
+def test_librosa_transforms_record_when_drawn():
+    """ChangeAudioSpeed / PitchShift record their effect (replayed by ds2_time_stretch /
+    ds2_resample, tests/test_librosa_effects.py) only when their draw fires."""
     random.seed(0)
     t = aa.ChangeAudioSpeed(prob=0.0)
-    assert t(wav=np.zeros(10, np.float32))['wav'].length == 10
-    with pytest.raises(NotImplementedError):
-        aa.PitchShift(prob=1.0)(wav=np.zeros(10, np.float32))
+    w = t(wav=np.zeros(1000, np.float32))['wav']
+    assert w.length == 1000 and not w.records
+    w = aa.ChangeAudioSpeed(limit=0.15, prob=1.0, sr=SR, max_duration=10)(
+        wav=np.zeros(1000, np.float32))['wav']
+    assert w.records[0][0] == aa.STRETCH and w.length == int(round(1000 / w.records[0][3]))
+    w = aa.PitchShift(prob=1.0)(wav=np.zeros(1000, np.float32), sr=SR)['wav']
+    assert w.records[0][0] == aa.PITCH and w.length == 1000 and w.records[0][1] == SR
 
 
 @pytest.mark.gpu
