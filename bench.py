@@ -288,8 +288,11 @@ def main():
 
     probe = KernelProbe(args.probe, sgemm_flops)
     probe.install()
-    rprobe = KernelProbe(("ds2_gru_fwd", "ds2_gru_bwd", "ds2_gru_bwd_bias"), gru_recurrence_flops)
-    rprobe.install()
+    fprobe = KernelProbe(("ds2_gru_fwd",), gru_recurrence_flops)
+    fprobe.install()
+    bprobe = KernelProbe(("ds2_gru_bwd", "ds2_gru_bwd_bias"), gru_recurrence_flops)
+    bprobe.install()
+    probes = (probe, fprobe, bprobe)
 
     def step():
         inp = x if featurize is None else featurize()
@@ -301,7 +304,8 @@ def main():
     if distributed:
         dist.barrier()
     torch.cuda.synchronize()
-    probe.active = rprobe.active = True
+    for p_ in probes:
+        p_.active = True
     marks = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     t0 = time.perf_counter()
     marks[0].record()
@@ -313,7 +317,8 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    probe.active = rprobe.active = False
+    for p_ in probes:
+        p_.active = False
     tr.poll_status(block=True)      # raises Ds2Error if a recurrence hand-off failed
     step_ms = sorted(marks[i].elapsed_time(marks[i + 1]) for i in range(args.steps))
     median_ms = step_ms[len(step_ms) // 2]
@@ -322,37 +327,45 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
     final_loss = float(loss.item())
-    pk = probe.summary()
-    rk = rprobe.summary()
+    pk, fk, bk = (p_.summary() for p_ in probes)
 
     if rank == 0:
         audio = world * BATCH * SECONDS * args.steps
         value = audio / dt
         ms_per_step = dt * 1000.0 / args.steps
-        roof = None
-        traffic, traffic_src = pmc_traffic_per_launch()
-        if pk is not None:
-            avg_ms, flop, count = pk
+        step_tf = round(TRAIN_FLOP_PER_STEP / (ms_per_step * 1e-3) / 1e12, 3)
+        kernels = {}
+
+        def entry(name, summ, peak, arith, bound, pmc):
+            if summ is None:
+                return
+            avg_ms, flop, count = summ
             achieved = flop / (avg_ms * 1e-3) / 1e12
-            peak, arith = gemm_peak()
-            roof = {"bound": "mfma", "kernel": args.probe, "launches": count,
-                    "avg_launch_ms": round(avg_ms, 5), "achieved": round(achieved, 3),
-                    "peak": round(peak, 1), "unit": "TFLOP/s", "arith": arith,
-                    "frac": round(achieved / peak, 4),
-                    "traffic": None if traffic is None else round(traffic),
-                    "traffic_unit": "bytes/launch (HBM, PMC)", "traffic_source": traffic_src,
-                    "step_achieved_tflops": round(TRAIN_FLOP_PER_STEP / (ms_per_step * 1e-3) / 1e12, 3)}
-        rec = None
-        if rk is not None:
-            # the recurrences are latency-bound (T' dependent steps, one cross-CU hand-off
-            # each); their MFMA floor is the per-CU share of the step's W_hh product
-            avg_ms, flop, count = rk
-            achieved = flop / (avg_ms * 1e-3) / 1e12
-            rec = {"bound": "latency", "kernel": rprobe.name, "launches": count,
-                   "avg_launch_ms": round(avg_ms, 5),
-                   "us_per_step": round(avg_ms * 1e3 / ((T_FRAMES - 1) // 2 + 1), 3),
-                   "achieved": round(achieved, 3), "peak": PEAK_F32_MFMA_TFLOPS,
-                   "unit": "TFLOP/s", "frac": round(achieved / PEAK_F32_MFMA_TFLOPS, 4)}
+            traffic, src = pmc_traffic_per_launch(*pmc)
+            e = {"bound": bound, "kernel": name, "launches": count,
+                 "launches_per_step": round(count / args.steps, 2),
+                 "avg_launch_ms": round(avg_ms, 5),
+                 "ms_per_step": round(avg_ms * count / args.steps, 3),
+                 "achieved": round(achieved, 3), "peak": round(peak, 1), "unit": "TFLOP/s",
+                 "arith": arith, "frac": round(achieved / peak, 4),
+                 "traffic": None if traffic is None else round(traffic),
+                 "traffic_unit": "bytes/launch (HBM, PMC)", "traffic_source": src,
+                 "step_achieved_tflops": step_tf}
+            if name.startswith("ds2_gru"):
+                # latency-bound: T' dependent steps, one cross-CU hand-off each
+                e["us_per_step"] = round(avg_ms * 1e3 / ((T_FRAMES - 1) // 2 + 1), 3)
+            kernels[name] = e
+
+        gpeak, garith = gemm_peak()
+        entry(args.probe, pk, gpeak, garith, "mfma", ("gemm", ("splitk_reduce_kernel",)))
+        x6f = os.environ.get("DS2_GRU_X6", "1")[:1] != "0"
+        entry("ds2_gru_fwd", fk, PEAK_X6_TFLOPS if x6f else PEAK_F32_MFMA_TFLOPS,
+              "W_hh contraction, bf16x6 (fp32-accurate) on v_mfma_f32_16x16x32_bf16" if x6f
+              else "W_hh contraction, fp32 MFMA", "mfma", ("gru_fwd_x6_kernel" if x6f else "gru_fwd_dop_kernel", ()))
+        entry("ds2_gru_bwd", bk, PEAK_F32_MFMA_TFLOPS,
+              "W_hh^T contraction, fp32 MFMA (v_mfma_f32_16x16x4_f32)", "mfma", ("gru_bwd_dh_kernel", ()))
+        # the roofline object is the dominant kernel family of the step (most ms per step)
+        roof = max(kernels.values(), key=lambda e: e["ms_per_step"]) if kernels else None
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(args.cpu_steps)
@@ -381,7 +394,7 @@ def main():
                    "broadcasts": tr.sync.broadcasts,
                    "status_clean": True},
             "roofline": roof,
-            "recurrence": rec,
+            "kernels": kernels,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
@@ -393,7 +406,7 @@ def main():
         # (exit-time teardown diagnostics, scripts/prof_exit_probe2.sh)
         import gc
         torch.cuda.synchronize()
-        del tr, m, x, probe, rprobe
+        del tr, m, x, probe, fprobe, bprobe, probes
         gc.collect()
         torch.cuda.empty_cache()
         torch.cuda.synchronize()

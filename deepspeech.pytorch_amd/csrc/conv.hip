@@ -1052,6 +1052,38 @@ __global__ __launch_bounds__(C1_T, 1) void conv1_patch_fwd_kernel(
 // next channel's global loads fly during the MFMAs.
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef cu32x4 u32x4;
+typedef __bf16 cbf16x2 __attribute__((ext_vector_type(2)));
+typedef float cf32x2 __attribute__((ext_vector_type(2)));
+
+// two fp32 -> (hi, mid, lo) bf16 pairs: one v_cvt_pk_bf16_f32 (RNE) per term pair, the
+// residuals exact in fp32 (bit-identical to per-element casts, half the instructions)
+__device__ __forceinline__ void cx_split2(float x0, float x1, unsigned& h, unsigned& m,
+                                          unsigned& l) {
+  h = __builtin_bit_cast(unsigned, __builtin_convertvector(cf32x2{x0, x1}, cbf16x2));
+  const float r0 = x0 - __builtin_bit_cast(float, h << 16);
+  const float r1 = x1 - __builtin_bit_cast(float, h & 0xffff0000u);
+  m = __builtin_bit_cast(unsigned, __builtin_convertvector(cf32x2{r0, r1}, cbf16x2));
+  const float q0 = r0 - __builtin_bit_cast(float, m << 16);
+  const float q1 = r1 - __builtin_bit_cast(float, m & 0xffff0000u);
+  l = __builtin_bit_cast(unsigned, __builtin_convertvector(cf32x2{q0, q1}, cbf16x2));
+}
+
+// 8 fp32 -> hi / mid / lo rows of 16 B at s + at, + plane, + 2 plane
+__device__ __forceinline__ void cx_split_store8(unsigned short* __restrict__ s, int plane, int at,
+                                                const float* v) {
+  u32x4 h, m, l;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    unsigned a, b, c;
+    cx_split2(v[2 * e], v[2 * e + 1], a, b, c);
+    h[e] = a;
+    m[e] = b;
+    l[e] = c;
+  }
+  *reinterpret_cast<u32x4*>(s + at) = h;
+  *reinterpret_cast<u32x4*>(s + plane + at) = m;
+  *reinterpret_cast<u32x4*>(s + 2 * plane + at) = l;
+}
 constexpr int CX_T = 512;
 constexpr int CX_COLS = 256;
 constexpr int CX_PATCH = 3 * 522 * 24;   // bf16: 3 planes x columns x pitch (max)
@@ -1228,25 +1260,7 @@ __global__ __launch_bounds__(CX_T, 1) void conv_x6_kernel(const float* __restric
       const int unit = tid + CX_T * u;
       if (unit < units) {
         const int j = unit / ngr, rg = unit - (unit / ngr) * ngr;
-        u32x4 h, m, lo;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float x0 = rp[u][2 * e], x1 = rp[u][2 * e + 1];
-          const __bf16 h0 = (__bf16)x0, h1 = (__bf16)x1;
-          const float r0 = x0 - (float)h0, r1 = x1 - (float)h1;
-          const __bf16 m0_ = (__bf16)r0, m1_ = (__bf16)r1;
-          const __bf16 l0 = (__bf16)(r0 - (float)m0_), l1 = (__bf16)(r1 - (float)m1_);
-          h[e] = (unsigned)__builtin_bit_cast(unsigned short, h0) |
-                 ((unsigned)__builtin_bit_cast(unsigned short, h1) << 16);
-          m[e] = (unsigned)__builtin_bit_cast(unsigned short, m0_) |
-                 ((unsigned)__builtin_bit_cast(unsigned short, m1_) << 16);
-          lo[e] = (unsigned)__builtin_bit_cast(unsigned short, l0) |
-                  ((unsigned)__builtin_bit_cast(unsigned short, l1) << 16);
-        }
-        const int at = j * c.P + 8 * rg;
-        *reinterpret_cast<u32x4*>(ps + at) = h;
-        *reinterpret_cast<u32x4*>(ps + PPL + at) = m;
-        *reinterpret_cast<u32x4*>(ps + 2 * PPL + at) = lo;
+        cx_split_store8(ps, PPL, j * c.P + 8 * rg, rp[u]);
       }
     }
 #pragma unroll
@@ -1373,24 +1387,7 @@ constexpr int CW_SLOTS = 512;              // workgroups per launch (two per CU)
 // 8 fp32 -> hi / mid / lo bf16 rows of 16 B (RNE casts, exact residuals)
 __device__ __forceinline__ void cw_split_store(unsigned short* __restrict__ s, int plane, int at,
                                                const float (&v)[8]) {
-  u32x4 h, m, l;
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const float x0 = v[2 * e], x1 = v[2 * e + 1];
-    const __bf16 h0 = (__bf16)x0, h1 = (__bf16)x1;
-    const float q0 = x0 - (float)h0, q1 = x1 - (float)h1;
-    const __bf16 m0 = (__bf16)q0, m1 = (__bf16)q1;
-    const __bf16 l0 = (__bf16)(q0 - (float)m0), l1 = (__bf16)(q1 - (float)m1);
-    h[e] = (unsigned)__builtin_bit_cast(unsigned short, h0) |
-           ((unsigned)__builtin_bit_cast(unsigned short, h1) << 16);
-    m[e] = (unsigned)__builtin_bit_cast(unsigned short, m0) |
-           ((unsigned)__builtin_bit_cast(unsigned short, m1) << 16);
-    l[e] = (unsigned)__builtin_bit_cast(unsigned short, l0) |
-           ((unsigned)__builtin_bit_cast(unsigned short, l1) << 16);
-  }
-  *reinterpret_cast<u32x4*>(s + at) = h;
-  *reinterpret_cast<u32x4*>(s + plane + at) = m;
-  *reinterpret_cast<u32x4*>(s + 2 * plane + at) = l;
+  cx_split_store8(s, plane, at, v);
 }
 
 template <int KW, int OFF0>

@@ -1331,13 +1331,21 @@ namespace ds2 {
 bool launch_gru_fwd_x6(int hm, int t_max, int n, int h, int num_dirs, const float* xproj,
                        const float* w_hh_f, const float* w_hh_r, const float* b_hh_f,
                        const float* b_hh_r, const int* lens, float* h_all, float* gates,
-                       float* ring, unsigned* ctrs, unsigned* err, unsigned long long* stamps,
-                       size_t lds_pad, hipStream_t st);
+                       float* coef, float* ring, unsigned* ctrs, unsigned* err,
+                       unsigned long long* stamps, size_t lds_pad, hipStream_t st);
 bool launch_gru_bwd_x6(int hm, int t_max, int n, int h, int num_dirs, const float* dy, int dy_dirs,
                        const float* w_hh_f, const float* w_hh_r, const float* h_all,
                        const float* gates, const int* lens, float* dgates_x, float* dgates_h,
                        float* ring, unsigned* ctrs, unsigned* err, unsigned long long* stamps,
                        size_t lds_pad, hipStream_t st);
+// gru_bwd_dh.hip: the dh-exchange backward (default) and the coefficient tiles it reads
+bool launch_gru_bwd_dh(int t_max, int n, int h, int num_dirs, const float* dy, int dy_dirs,
+                       const float* w_hh_f, const float* w_hh_r, const float* gates,
+                       const float* coef, const int* lens, float* dgates_x, float* dgates_h,
+                       float* ring, unsigned* ctrs, unsigned* err, unsigned long long* stamps,
+                       double* dbp, size_t lds_pad, hipStream_t st);
+void launch_gru_coef(const float* gates, const float* h_all, const int* lens, int t_max, int n,
+                     int h, int num_dirs, float* coef, hipStream_t st);
 }  // namespace ds2
 
 using namespace ds2;
@@ -1408,6 +1416,27 @@ static inline hipError_t ring_reset(float* ring, int n, int h, int num_dirs, int
   return hipMemsetAsync(ring, 0xFF, ring_bytes(n, h, num_dirs, tiles), st);
 }
 
+// the gate cache: [T][N][D][4H] (r, z, n, W_hn h + b_hn), then the backward's coefficient
+// tiles (rnn_common.h, gru_bwd_dh.hip)
+static inline float* coef_part(const float* gates, int t_max, int n, int h, int num_dirs) {
+  return gates == nullptr ? nullptr
+                          : const_cast<float*>(gates) + (size_t)t_max * n * num_dirs * 4 * h;
+}
+
+size_t ds2_gru_cache_floats(int t_max, int n, int h, int num_dirs) {
+  if (t_max <= 0 || n <= 0 || h <= 0 || num_dirs <= 0) return 0;
+  return (size_t)t_max * n * num_dirs * 4 * h + gru_coef_floats(t_max, n, h, num_dirs);
+}
+
+// every forward path but the bf16x6 one (which writes them itself): coefficient tiles after it
+static ds2_status_t fwd_coef(const float* gates, const float* h_all, const int* lens, int t_max,
+                             int n, int h, int num_dirs, hipStream_t st) {
+  if (gates != nullptr)
+    launch_gru_coef(gates, h_all, lens, t_max, n, h, num_dirs,
+                    coef_part(gates, t_max, n, h, num_dirs), st);
+  return launch_status("ds2_gru_fwd");
+}
+
 size_t ds2_gru_fwd_workspace_size(int n, int h, int num_dirs) {
   const int64_t UB = (h + GU - 1) / GU;
   const int64_t KS = (h + 3) / 4;
@@ -1468,7 +1497,8 @@ ds2_status_t ds2_gru_fwd(int t_max, int n, int h, int num_dirs, const float* xpr
     if (hm != 0 && ring_reset(ring, n, h, num_dirs, 1, st) != hipSuccess)
       return launch_status("ds2_gru ring");
     if (launch_gru_fwd_x6(hm, t_max, n, h, num_dirs, xproj, w_hh_f, w_hh_r, b_hh_f, b_hh_r, lens,
-                          h_all, gates, ring, ctrs, err, stamps, kDopPadLds, st)) {
+                          h_all, gates, coef_part(gates, t_max, n, h, num_dirs), ring, ctrs, err,
+                          stamps, kDopPadLds, st)) {
       fold_err(err, err_out, st);
       return launch_status("ds2_gru_fwd");
     }
@@ -1490,7 +1520,7 @@ ds2_status_t ds2_gru_fwd(int t_max, int n, int h, int num_dirs, const float* xpr
     if (fn != nullptr &&
         hipLaunchCooperativeKernel(fn, dim3(grid), dim3(GT), args, kDopPadLds, st) == hipSuccess) {
       fold_err(err, err_out, st);
-      return launch_status("ds2_gru_fwd");
+      return fwd_coef(gates, h_all, lens, t_max, n, h, num_dirs, st);
     }
     (void)hipGetLastError();
   }
@@ -1521,7 +1551,7 @@ ds2_status_t ds2_gru_fwd(int t_max, int n, int h, int num_dirs, const float* xpr
     if (fn != nullptr &&
         hipLaunchCooperativeKernel(fn, dim3(grid), dim3(GT), args, 0, st) == hipSuccess) {
       fold_err(err, err_out, st);
-      return launch_status("ds2_gru_fwd");
+      return fwd_coef(gates, h_all, lens, t_max, n, h, num_dirs, st);
     }
     (void)hipGetLastError();   // fall back to one launch per step
   }
@@ -1531,7 +1561,7 @@ ds2_status_t ds2_gru_fwd(int t_max, int n, int h, int num_dirs, const float* xpr
       DS2_FWD_CASE(80) DS2_FWD_CASE(96)
     }
   }
-  return launch_status("ds2_gru_fwd");
+  return fwd_coef(gates, h_all, lens, t_max, n, h, num_dirs, st);
 }
 
 static size_t gru_bwd_ws_base(int n, int h, int num_dirs) {
@@ -1682,6 +1712,14 @@ static ds2_status_t gru_bwd_run(int t_max, int n, int h, int num_dirs, const flo
       }
       (void)hipGetLastError();
     }
+    if (launch_gru_bwd_dh(t_max, n, h, num_dirs, dy, dy_dirs, w_hh_f, w_hh_r, gates,
+                          coef_part(gates, t_max, n, h, num_dirs), lens, dgates_x, dgates_h, ring,
+                          ctrs, err, stamps, dbp, kDopPadLds, st)) {
+      fold_err(err, err_out, st);
+      summed = dbp != nullptr;
+      return launch_status("ds2_gru_bwd");
+    }
+    (void)hipGetLastError();
     const int hmb = handoff_mode(false);
     if (hmb != 0 && ring_reset(ring, n, h, num_dirs, 3, st) != hipSuccess)
       return launch_status("ds2_gru ring");

@@ -77,8 +77,9 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     int T, int N, int H, int D, int UB, int BT, const float* __restrict__ xproj,
     const float* __restrict__ w_f, const float* __restrict__ w_r, const float* __restrict__ b_f,
     const float* __restrict__ b_r, const int* __restrict__ lens, float* __restrict__ h_all,
-    float* __restrict__ gates, float* __restrict__ hx, unsigned* __restrict__ counters,
-    unsigned* __restrict__ err, unsigned long long* __restrict__ stamps) {
+    float* __restrict__ gates, float* __restrict__ coef, float* __restrict__ hx,
+    unsigned* __restrict__ counters, unsigned* __restrict__ err,
+    unsigned long long* __restrict__ stamps) {
   constexpr int RP = 3 * GU + 1;
   constexpr bool SENT = HM == 1;
   constexpr int NSLOT = SENT ? kRingSlots : 2;
@@ -150,7 +151,9 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   settle(len);
   const int tpos = ((u >> 2) * GB + m) * 4 + (u & 3);
   float g_r = 0.f, g_z = 0.f, g_n = 0.f, g_hn = 0.f, h_own = 0.f;
+  float c_r = 0.f, c_z = 0.f, c_hn = 0.f;
   int64_t g_row = -1;
+  int g_t = 0;
   for (int s = 0; s < T; ++s) {
     const int t = d == 0 ? s : T - 1 - s;
     const int64_t row = ((int64_t)t * N + n) * D + d;
@@ -254,11 +257,13 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
         z = sigmoid_fast(ghz + xz);
         nn = tanh_fast(xn + r * ghn);
         hout = (h_own - nn) * z + nn;
+        gru_coefs(r, z, nn, ghn, h_own, c_r, c_z, c_hn);
       } else {
         ghn = 0.f;
+        c_r = c_z = c_hn = 0.f;
       }
       h_own = hout;
-      g_r = r; g_z = z; g_n = nn; g_hn = ghn; g_row = row;
+      g_r = r; g_z = z; g_n = nn; g_hn = ghn; g_row = row; g_t = t;
     }
     tile[tpos] = hout;
     __syncthreads();
@@ -289,6 +294,12 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
         gp[2 * H + j] = g_n;
         gp[3 * H + j] = g_hn;
       }
+    }
+    if (coef != nullptr) {     // every tile slot written (zeros for samples past N)
+      float* cp = coef + coef_tile(owner ? g_t : t, d, bt, 0, ub, D, BT, UB) * 256 + tpos;
+      cp[0] = owner ? c_r : 0.f;
+      cp[(int64_t)UB * 256] = owner ? c_z : 0.f;
+      cp[(int64_t)2 * UB * 256] = owner ? c_hn : 0.f;
     }
   }
 }
@@ -562,8 +573,8 @@ static const void* bwd_x6_fn(int pairs, int hm, int nw) {
 bool launch_gru_fwd_x6(int hm, int t_max, int n, int h, int num_dirs, const float* xproj,
                        const float* w_hh_f, const float* w_hh_r, const float* b_hh_f,
                        const float* b_hh_r, const int* lens, float* h_all, float* gates,
-                       float* ring, unsigned* ctrs, unsigned* err, unsigned long long* stamps,
-                       size_t lds_pad, hipStream_t st) {
+                       float* coef, float* ring, unsigned* ctrs, unsigned* err,
+                       unsigned long long* stamps, size_t lds_pad, hipStream_t st) {
   if (!x6_enabled() || (h % GU) != 0) return false;
   apply_spin_limit_env();     // this translation unit's copies of the device knobs
   apply_rnn_tune_env();
@@ -573,7 +584,7 @@ bool launch_gru_fwd_x6(int hm, int t_max, int n, int h, int num_dirs, const floa
   if (fn == nullptr) return false;
   int T_ = t_max, N_ = n, H_ = h, D_ = num_dirs, UB_ = UB, BT_ = BT;
   void* args[] = {&T_, &N_, &H_, &D_, &UB_, &BT_, &xproj, &w_hh_f, &w_hh_r, &b_hh_f,
-                  &b_hh_r, &lens, &h_all, &gates, &ring, &ctrs, &err, &stamps};
+                  &b_hh_r, &lens, &h_all, &gates, &coef, &ring, &ctrs, &err, &stamps};
   return hipLaunchCooperativeKernel(fn, dim3(mapped_grid(UB * num_dirs, BT)), dim3(XT), args,
                                     lds_pad, st) == hipSuccess;
 }

@@ -406,5 +406,36 @@ static inline int grid_cap(int64_t work) {
 
 static inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
+// ---------------------------------------------------------------------------------------
+// GRU backward coefficient tiles (the part of the gate cache after the [T][N][D][4H] gates,
+// ds2_gru_cache_floats).  The backward's gate gradients are the step's dh times per-element
+// coefficients that the forward already knows:
+//   dan  = dh * c_n,  c_n  = (1 - z)(1 - n^2)          dar  = dh * c_r,  c_r  = c_n hn r (1 - r)
+//   daz  = dh * c_z,  c_z  = (h_prev - n) z (1 - z)    dghn = dh * c_hn, c_hn = c_n r
+// so the recurrence can exchange dh (H per sample) instead of (dar, daz, dghn) (3H) and every
+// consumer forms its MFMA A operands as dh x c.  Tiles of 16 units x 16 samples in the hand-off
+// tile order (tpos), one per (t, direction, batch tile, g in {c_r, c_z, c_hn}, unit block):
+//   coef[t][d][bt][g][ub][256]
+constexpr int kCoefPlanes = 3;
+
+__device__ __forceinline__ int64_t coef_tile(int t, int d, int bt, int g, int ub, int D, int BT,
+                                             int UB) {
+  return ((((int64_t)t * D + d) * BT + bt) * kCoefPlanes + g) * UB + ub;
+}
+
+// c_r, c_z, c_hn of one element (0 past the sequence end: t >= len)
+__device__ __forceinline__ void gru_coefs(float r, float z, float n, float hn, float hp,
+                                          float& cr, float& cz, float& chn) {
+  const float cn = (1.f - z) * (1.f - n * n);
+  cr = cn * hn * r * (1.f - r);
+  cz = (hp - n) * z * (1.f - z);
+  chn = cn * r;
+}
+
+static inline size_t gru_coef_floats(int t, int n, int h, int d) {
+  const size_t BT = (n + GB - 1) / GB, UB = (h + GU - 1) / GU;
+  return (size_t)t * d * BT * kCoefPlanes * UB * 256;
+}
+
 
 }  // namespace ds2

@@ -65,6 +65,7 @@ _PROTOS = {
                                  _vp, _c_int, _vp, _c_f, _c_f, _vp, _vp, _vp, _vp, _vp, _sz,
                                  _vp]),
     "ds2_gru_fwd_workspace_size": (_sz, [_c_int, _c_int, _c_int]),
+    "ds2_gru_cache_floats": (_sz, [_c_int, _c_int, _c_int, _c_int]),
     "ds2_gru_fwd": (_c_int, [_c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                              _vp, _vp, _vp, _sz, _vp]),
     "ds2_gru_bwd_workspace_size": (_sz, [_c_int, _c_int, _c_int]),

@@ -720,7 +720,9 @@ class GRULayerFn(torch.autograd.Function):
         xproj = _rnn_input_proj(x, weights, nd, 3 * h, bf16)
         h_all = torch.empty(t, n, nd, h, device=dev, dtype=_F32)
         need_grad = any(ctx.needs_input_grad)   # forward() itself runs under no_grad
-        gates = torch.empty(t, n, nd, 4 * h, device=dev, dtype=_F32) if need_grad else None
+        # backward cache: [T][N][D][4H] gates + the dh-exchange backward's coefficient tiles
+        gates = (torch.empty(_lib.size("ds2_gru_cache_floats", t, n, h, nd), device=dev,
+                             dtype=_F32) if need_grad else None)
         w_hh_f, b_hh_f = weights[1], weights[3]
         w_hh_r = weights[5] if nd == 2 else None
         b_hh_r = weights[7] if nd == 2 else None

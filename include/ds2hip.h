@@ -216,7 +216,10 @@ ds2_status_t ds2_bn_backward(const float* dy, int dy_layout, const float* x, int
  * pack -> nn.GRU -> pad), model.py:16 (supported_rnns['gru']).
  *   xproj : [T][N][D][3H]  x @ W_ih^T + b_ih for each direction
  *   h_all : [T][N][D][H]   per-direction hidden states (output)
- *   gates : [T][N][D][4H]  (r, z, n, W_hn h + b_hn) cache for backward, or NULL
+ *   gates : the backward cache, or NULL: ds2_gru_cache_floats(T, N, H, D) floats =
+ *           [T][N][D][4H] (r, z, n, W_hn h + b_hn), then the backward's coefficient tiles
+ *           (c_r, c_z, c_hn in hand-off tile order, csrc/rnn_common.h) that let the backward
+ *           recurrence exchange dh instead of the 3H gate gradients (csrc/gru_bwd_dh.hip)
  * num_dirs = 1 or 2; w_hh_r / b_hh_r ignored when num_dirs == 1.
  * err_out: NULL, or a caller-owned device status word; the persistent
  * (one-launch-per-layer) kernels OR their hand-off status into it after the
@@ -226,6 +229,7 @@ ds2_status_t ds2_bn_backward(const float* dy, int dy_layout, const float* x, int
  * it whenever it synchronises anyway (same convention for ds2_gru_bwd and
  * ds2_lstm_fwd / ds2_lstm_bwd).                                               */
 #define DS2_RNN_ERR_HANDOFF_TIMEOUT 1u
+size_t ds2_gru_cache_floats(int t_max, int n, int h, int num_dirs);
 size_t ds2_gru_fwd_workspace_size(int n, int h, int num_dirs);
 ds2_status_t ds2_gru_fwd(int t_max, int n, int h, int num_dirs, const float* xproj,
                          const float* w_hh_f, const float* w_hh_r, const float* b_hh_f,

@@ -509,6 +509,88 @@ def test_gru_bf16x6_matches_fp32_mfma(dev, n, h, bidir, monkeypatch):
         assert torch.equal(flags, sent)
 
 
+def _gru_run(dev, n, t, inp, h, nd, seed, env, monkeypatch, amp=None):
+    g = torch.Generator().manual_seed(seed)
+    a = amp if amp is not None else (0.2 if h <= 64 else h ** -0.5)
+    weights = [torch.rand(s, generator=g) * 2 * a - a for s in
+               [(3 * h, inp), (3 * h, h), (3 * h,), (3 * h,)] * nd]
+    lens = torch.tensor(sorted([t - (i % 6) * 5 for i in range(n)], reverse=True),
+                        dtype=torch.int32)
+    x = torch.randn(t, n, inp, generator=g)
+    dy = torch.randn(t, n, h, generator=g)
+    outs = []
+    for e in env:
+        for k, v in e.items():
+            monkeypatch.setenv(k, v)
+        ws = [w.to(dev).requires_grad_(True) for w in weights]
+        xd = x.to(dev).requires_grad_(True)
+        y = ops.GRULayerFn.apply(xd, lens.to(dev), True, h, *ws)
+        y.backward(dy.to(dev))
+        torch.cuda.synchronize()
+        ops.check_rnn_status(dev)
+        outs.append([y.detach().cpu(), xd.grad.cpu()] + [w.grad.cpu() for w in ws])
+    return outs
+
+
+@pytest.mark.parametrize("n,h,bidir", [(32, 800, True), (20, 800, True), (7, 48, False),
+                                       (17, 784, True), (33, 256, True), (5, 512, False)])
+def test_gru_dh_backward_matches_gate_exchange(dev, n, h, bidir, monkeypatch):
+    """The dh-exchange backward (gru_bwd_dh.hip: producers publish dh, consumers form
+    dG = dh x the forward's coefficient tiles) against the gate-exchange backward
+    (DS2_GRU_BWD=dg): equal within fp32 rounding (the gate gradients are dh x c instead of
+    ((dh x a) x b) ...); flag and sentinel hand-offs bit-identical; the 8-wave form (H <= 512)
+    within rounding; with the fp32-MFMA forward the coefficient tiles come from the
+    conversion kernel (gru_coef_kernel) and the same holds."""
+    nd = 2 if bidir else 1
+    base = {"DS2_GRU_DOP": "1", "DS2_GRU_X6_BWD": "0", "DS2_GRU_BWD_WAVES": "4"}
+    env = [dict(base, DS2_GRU_BWD="dg", DS2_RNN_HANDOFF=""),
+           dict(base, DS2_GRU_BWD="dh", DS2_RNN_HANDOFF="flags"),
+           dict(base, DS2_GRU_BWD="dh", DS2_RNN_HANDOFF="sentinel"),
+           dict(base, DS2_GRU_BWD="dh", DS2_RNN_HANDOFF="", DS2_GRU_BWD_WAVES="8")]
+    outs = _gru_run(dev, n, 37, 40, h, nd, h + 11 * n, env, monkeypatch)
+    ref, flags, sent, w8 = outs
+    for r, f, s_, e in zip(ref, flags, sent, w8):
+        assert torch.isfinite(f).all()
+        _close(f, r, 2e-5, "dh vs gate-exchange backward")
+        assert torch.equal(f, s_)
+        _close(e, f, 2e-5, "dh backward 8 vs 4 waves")
+    env32 = [dict(base, DS2_GRU_X6="0", DS2_GRU_BWD="dg", DS2_RNN_HANDOFF=""),
+             dict(base, DS2_GRU_X6="0", DS2_GRU_BWD="dh", DS2_RNN_HANDOFF="")]
+    r32, d32 = _gru_run(dev, n, 37, 40, h, nd, h + 11 * n, env32, monkeypatch)
+    for r, f in zip(r32, d32):
+        _close(f, r, 2e-5, "dh backward after the fp32-MFMA forward (converted coefficients)")
+
+
+def test_gru_dh_backward_full_length_vs_torch(dev):
+    """The cfg2 recurrence shape (bs 32, H 800, both directions) over 201 steps with ragged
+    lengths, dh-exchange backward against torch's nn.GRU in fp64."""
+    n, t, inp, h = 32, 201, 64, 800
+    g = torch.Generator().manual_seed(3)
+    gru = torch.nn.GRU(inp, h, bidirectional=True).double()
+    with torch.no_grad():
+        for p in gru.parameters():
+            p.copy_((torch.rand(p.shape, generator=g, dtype=torch.float64) * 2 - 1) * h ** -0.5)
+    lens = torch.tensor(sorted([t - 6 * i for i in range(n)], reverse=True), dtype=torch.int32)
+    x = torch.randn(t, n, inp, generator=g, dtype=torch.float64)
+    for i in range(n):
+        x[int(lens[i]):, i] = 0
+    xr = x.clone().requires_grad_(True)
+    out, _ = gru(torch.nn.utils.rnn.pack_padded_sequence(xr, lens.numpy()))
+    out, _ = torch.nn.utils.rnn.pad_packed_sequence(out, total_length=t)
+    summed = out.view(t, n, 2, h).sum(2)
+    dy = torch.randn(summed.shape, generator=g, dtype=torch.float64)
+    summed.backward(dy)
+    weights = [p.detach().float().to(dev).requires_grad_(True) for p in gru.parameters()]
+    xd = x.float().to(dev).requires_grad_(True)
+    yd = ops.GRULayerFn.apply(xd, lens.to(dev), True, h, *weights)
+    yd.backward(dy.float().to(dev))
+    ops.check_rnn_status(dev)
+    _close(yd, summed, 1e-5, "gru y")
+    _close(xd.grad, xr.grad, 1e-4, "gru dx")
+    for (name, p), wd in zip(gru.named_parameters(), weights):
+        _close(wd.grad, p.grad, 1e-4, "gru " + name)
+
+
 def test_gru_per_direction_output(dev):
     n, t, inp, h = 4, 11, 8, 16
     g = torch.Generator().manual_seed(5)
