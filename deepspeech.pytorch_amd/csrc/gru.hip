@@ -1419,19 +1419,21 @@ static inline hipError_t ring_reset(float* ring, int n, int h, int num_dirs, int
 // the gate cache: [T][N][D][4H] (r, z, n, W_hn h + b_hn), then the backward's coefficient
 // tiles (rnn_common.h, gru_bwd_dh.hip)
 static inline float* coef_part(const float* gates, int t_max, int n, int h, int num_dirs) {
-  return gates == nullptr ? nullptr
-                          : const_cast<float*>(gates) + (size_t)t_max * n * num_dirs * 4 * h;
+  return (gates == nullptr || !gru_dh_bwd_opted_in())
+             ? nullptr
+             : const_cast<float*>(gates) + (size_t)t_max * n * num_dirs * 4 * h;
 }
 
 size_t ds2_gru_cache_floats(int t_max, int n, int h, int num_dirs) {
   if (t_max <= 0 || n <= 0 || h <= 0 || num_dirs <= 0) return 0;
-  return (size_t)t_max * n * num_dirs * 4 * h + gru_coef_floats(t_max, n, h, num_dirs);
+  return (size_t)t_max * n * num_dirs * 4 * h +
+         (gru_dh_bwd_opted_in() ? gru_coef_floats(t_max, n, h, num_dirs) : 0);
 }
 
 // every forward path but the bf16x6 one (which writes them itself): coefficient tiles after it
 static ds2_status_t fwd_coef(const float* gates, const float* h_all, const int* lens, int t_max,
                              int n, int h, int num_dirs, hipStream_t st) {
-  if (gates != nullptr)
+  if (coef_part(gates, t_max, n, h, num_dirs) != nullptr)
     launch_gru_coef(gates, h_all, lens, t_max, n, h, num_dirs,
                     coef_part(gates, t_max, n, h, num_dirs), st);
   return launch_status("ds2_gru_fwd");
@@ -1518,7 +1520,7 @@ ds2_status_t ds2_gru_fwd(int t_max, int n, int h, int num_dirs, const float* xpr
 #undef DS2_FDOP
     // the dynamic LDS keeps one workgroup per CU (every workgroup gets a whole CU's SIMDs)
     if (fn != nullptr &&
-        hipLaunchCooperativeKernel(fn, dim3(grid), dim3(GT), args, kDopPadLds, st) == hipSuccess) {
+        rnn_launch(fn, dim3(grid), dim3(GT), args, kDopPadLds, st) == hipSuccess) {
       fold_err(err, err_out, st);
       return fwd_coef(gates, h_all, lens, t_max, n, h, num_dirs, st);
     }
@@ -1549,7 +1551,7 @@ ds2_status_t ds2_gru_fwd(int t_max, int n, int h, int num_dirs, const float* xpr
       default: break;
     }
     if (fn != nullptr &&
-        hipLaunchCooperativeKernel(fn, dim3(grid), dim3(GT), args, 0, st) == hipSuccess) {
+        rnn_launch(fn, dim3(grid), dim3(GT), args, 0, st) == hipSuccess) {
       fold_err(err, err_out, st);
       return fwd_coef(gates, h_all, lens, t_max, n, h, num_dirs, st);
     }
@@ -1705,7 +1707,7 @@ static ds2_status_t gru_bwd_run(int t_max, int n, int h, int num_dirs, const flo
       void* rargs[] = {&T_, &N_, &H_, &D_, &UB_, &BT_, &dy, &DYD_, &w_hh_f, &w_hh_r, &h_all,
                        &gates, &lens, &dgates_x, &dgates_h, &rring, &ctrs, &err, &dbp};
       if (rfn != nullptr &&
-          hipLaunchCooperativeKernel(rfn, dim3(grid), dim3(GT), rargs, kDopPadLds, st) == hipSuccess) {
+          rnn_launch(rfn, dim3(grid), dim3(GT), rargs, kDopPadLds, st) == hipSuccess) {
         fold_err(err, err_out, st);
         summed = true;
         return launch_status("ds2_gru_bwd");
@@ -1731,7 +1733,7 @@ static ds2_status_t gru_bwd_run(int t_max, int n, int h, int num_dirs, const flo
     (void)hipGetLastError();
     const void* fn = bwd_dop_fn((3 * UB + GW - 1) / GW);
     if (fn != nullptr &&
-        hipLaunchCooperativeKernel(fn, dim3(grid), dim3(GT), args, kDopPadLds, st) == hipSuccess) {
+        rnn_launch(fn, dim3(grid), dim3(GT), args, kDopPadLds, st) == hipSuccess) {
       fold_err(err, err_out, st);
       summed = dbp != nullptr;
       return launch_status("ds2_gru_bwd");
@@ -1765,7 +1767,7 @@ static ds2_status_t gru_bwd_run(int t_max, int n, int h, int num_dirs, const flo
       default: break;
     }
     if (fn != nullptr &&
-        hipLaunchCooperativeKernel(fn, dim3(grid), dim3(GT), args, 0, st) == hipSuccess) {
+        rnn_launch(fn, dim3(grid), dim3(GT), args, 0, st) == hipSuccess) {
       fold_err(err, err_out, st);
       return launch_status("ds2_gru_bwd");
     }

@@ -1,4 +1,5 @@
-// GRU backward recurrence that exchanges dh instead of the gate gradients (default).
+// GRU backward recurrence that exchanges dh instead of the gate gradients (opt-in,
+// DS2_GRU_BWD=dh; measured slower than the gate exchange, see the end of this comment).
 //
 // The backward step of one direction is (model.py:97-109 nn.GRU BPTT, gates r, z, n):
 //   dh_t   = dy_t + z_{t+1} dh_{t+1} + sum_k dG_{t+1}[k] W_hh[k][u]        (k over the 3H gate rows)
@@ -18,11 +19,59 @@
 // (dh x coefficients, the same products the consumers form), sum the bias gradients, and
 // publish the dh tile.  HM: 0 per-producer flags (ring of 2 slots), 1 sentinel ring (the data
 // is the flag), as the direct-operand forward.
+//
+// Measured (cfg2, same box, alternating with the gate exchange at 6.31-6.39 us per step):
+// 7.05-7.09 us with the coefficient loads issued before the flag poll, 7.53-7.55 issued after
+// the MFMAs (a __syncthreads drains them at the next barrier), 8.57 with raw LDS barriers so
+// they stay in flight across the reduction, publish and poll.  The coefficients are 150 KB per
+// workgroup per step -- the bytes the gate exchange hands off -- and the longer they stream
+// beside the hand-off, the more they slow it: the per-CU memory queue, not the freshness of
+// the bytes, prices the step (MI355X_MICROARCH.md handoff-1to1 under streaming waves).
 #include "rnn_common.h"
 
 namespace ds2 {
 
 constexpr int kDhTraceS0 = 100, kDhTraceSteps = 16;   // = gru.hip's DS2_GRU_STAMPS=2 window
+
+// Workgroup barrier for LDS data only: waits for this wave's LDS operations, not its vector
+// memory ones.  __syncthreads() carries a workgroup fence, before which hipcc drains vmcnt --
+// that would stall every wave on the coefficient prefetch below at each of the step's barriers.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// flags_wait (rnn_common.h) with the raw barrier: wave 0 polls the UB producer flags (one
+// sc1 load + ballot per round); the other waves load after the barrier it joins (the valid
+// form's consumer rule), with their prefetches still in flight
+__device__ __forceinline__ bool dh_flags_wait(const unsigned* flags, int count, unsigned target,
+                                              unsigned* err, int* lds_flag) {
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    unsigned spins = 0;
+    int ok = 1;
+    if (g_spin_limit == 0) {   // fault injection
+      if (lane == 0) __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      ok = 0;
+    }
+    for (; ok;) {
+      const unsigned v = lane < count ? __hip_atomic_load(flags + lane, __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT)
+                                      : target;
+      if (__ballot(v < target) == 0ull) break;
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > g_spin_limit) {
+        if (lane == 0) __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ok = 0;
+        break;
+      }
+    }
+    if (lane == 0) *lds_flag = ok;
+  }
+  lds_barrier();
+  return *lds_flag != 0;
+}
 
 template <int NVB, int HM, int NW>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW / 4, NW / 4))) void gru_bwd_dh_kernel(
@@ -125,7 +174,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW / 4,
       c_hn = cp[(int64_t)2 * UB * 256];
     }
     if (s > 0) {
-      if (!SENT && !flags_wait(gflags, UB, (unsigned)s, err, &flag)) {
+      if (!SENT && !dh_flags_wait(gflags, UB, (unsigned)s, err, &flag)) {
         poison_rest(dgx, s, T, d == 0, N, D, n, d, H, j, H3, 3, owner);
         return;
       }
@@ -186,17 +235,21 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW / 4,
       }
       trace_at(s, 2);
     }
-    // the coefficients step s + 1 multiplies (time t), issued a whole reduction + publish +
-    // hand-off wait ahead of their use
-    if (s + 1 < T) {
+    // the coefficients step s + 1 multiplies (time t), in flight across the step's barriers
+    // (lds_barrier): waves 1.. issue them now, wave 0 -- which drains vmcnt to publish and
+    // then polls -- right after its flag store
+    auto prefetch = [&]() {
+      if (s + 1 < T) {
 #pragma unroll
-      for (int g = 0; g < 3; ++g)
+        for (int g = 0; g < 3; ++g)
 #pragma unroll
-        for (int i = 0; i < NVB; ++i)
-          cf[g][i] = __builtin_bit_cast(
-              f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                         c_rs, i < nb ? coef_off(t, g, b0 + i) : 0x7ffffff0, 0, 0));
-    }
+          for (int i = 0; i < NVB; ++i)
+            cf[g][i] = __builtin_bit_cast(
+                f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                           c_rs, i < nb ? coef_off(t, g, b0 + i) : 0x7ffffff0, 0, 0));
+      }
+    };
+    if (wave != 0) prefetch();
 #pragma unroll
     for (int r = 0; r < 4; ++r)
       red[(wave * GB + (lane >> 4) * 4 + r) * RP + (lane & 15)] = acc0[r] + acc1[r];
@@ -206,7 +259,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW / 4,
     settle(c_r);
     settle(c_z);
     settle(c_hn);
-    __syncthreads();
+    lds_barrier();
     if (SENT && failed) {
       poison_rest(dgx, s, T, d == 0, N, D, n, d, H, j, H3, 3, owner);
       return;
@@ -237,7 +290,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW / 4,
       sb_r += dar; sb_z += daz; sb_n += dan; sb_hn += dghn;
     }
     if (gate_thread) tile[tpos] = dh;
-    __syncthreads();
+    lds_barrier();
     if (wave == 0) {
       const int toff = (grp_off + ub * 256 + lane * 4) * 4;
       if (SENT) {
@@ -254,6 +307,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW / 4,
         if (lane == 0)
           __hip_atomic_store(myflag, (unsigned)s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
+      prefetch();
     }
     trace_at(s, 4);
     if (owner) {
@@ -318,10 +372,7 @@ __global__ void gru_coef_kernel(const float* __restrict__ gates, const float* __
   }
 }
 
-static inline bool dh_bwd_enabled() {
-  const char* e = getenv("DS2_GRU_BWD");      // "dg" or "0": the gate-exchange kernels
-  return !(e != nullptr && ((e[0] == 'd' && e[1] == 'g') || e[0] == '0'));
-}
+static inline bool dh_bwd_enabled() { return gru_dh_bwd_opted_in(); }
 
 static inline int dh_handoff_mode() {
   const char* e = getenv("DS2_RNN_HANDOFF_BWD");
@@ -387,7 +438,7 @@ bool launch_gru_bwd_dh(int t_max, int n, int h, int num_dirs, const float* dy, i
   int T_ = t_max, N_ = n, H_ = h, D_ = num_dirs, UB_ = UB, BT_ = BT, DYD_ = dy_dirs;
   void* args[] = {&T_, &N_, &H_, &D_, &UB_, &BT_, &dy, &DYD_, &w_hh_f, &w_hh_r, &gates,
                   &coef, &lens, &dgates_x, &dgates_h, &ring, &ctrs, &err, &stamps, &dbp};
-  return hipLaunchCooperativeKernel(fn, dim3(mapped_grid(UB * num_dirs, BT)), dim3(nw * 64), args,
+  return rnn_launch(fn, dim3(mapped_grid(UB * num_dirs, BT)), dim3(nw * 64), args,
                                     lds_pad, st) == hipSuccess;
 }
 

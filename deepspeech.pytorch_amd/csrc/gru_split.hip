@@ -585,7 +585,7 @@ bool launch_gru_fwd_x6(int hm, int t_max, int n, int h, int num_dirs, const floa
   int T_ = t_max, N_ = n, H_ = h, D_ = num_dirs, UB_ = UB, BT_ = BT;
   void* args[] = {&T_, &N_, &H_, &D_, &UB_, &BT_, &xproj, &w_hh_f, &w_hh_r, &b_hh_f,
                   &b_hh_r, &lens, &h_all, &gates, &coef, &ring, &ctrs, &err, &stamps};
-  return hipLaunchCooperativeKernel(fn, dim3(mapped_grid(UB * num_dirs, BT)), dim3(XT), args,
+  return rnn_launch(fn, dim3(mapped_grid(UB * num_dirs, BT)), dim3(XT), args,
                                     lds_pad, st) == hipSuccess;
 }
 
@@ -604,7 +604,7 @@ bool launch_gru_bwd_x6(int hm, int t_max, int n, int h, int num_dirs, const floa
   int T_ = t_max, N_ = n, H_ = h, D_ = num_dirs, UB_ = UB, BT_ = BT, DYD_ = dy_dirs;
   void* args[] = {&T_, &N_, &H_, &D_, &UB_, &BT_, &dy, &DYD_, &w_hh_f, &w_hh_r, &h_all,
                   &gates, &lens, &dgates_x, &dgates_h, &ring, &ctrs, &err, &stamps};
-  return hipLaunchCooperativeKernel(fn, dim3(mapped_grid(UB * num_dirs, BT)), dim3(nw * 64), args,
+  return rnn_launch(fn, dim3(mapped_grid(UB * num_dirs, BT)), dim3(nw * 64), args,
                                     lds_pad, st) == hipSuccess;
 }
 

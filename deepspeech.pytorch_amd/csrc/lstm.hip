@@ -1043,7 +1043,7 @@ ds2_status_t ds2_lstm_fwd(int t_max, int n, int h, int num_dirs, const float* xp
         return launch_status("ds2_lstm ring");
       void* args[] = {&T_, &N_, &H_, &D_, &UB_, &BT_, &xproj, &w_hh_f, &w_hh_r, &b_hh_f,
                       &b_hh_r, &lens, &h_all, &c_all, &gates, &ring, &ctrs, &err, &NB_};
-      ok = hipLaunchCooperativeKernel(fn, dim3(mapped_grid(UB * num_dirs, BT_)), dim3(GT), args,
+      ok = rnn_launch(fn, dim3(mapped_grid(UB * num_dirs, BT_)), dim3(GT), args,
                                       kLstmDopPadLds, st) == hipSuccess;
       if (ok) fold_err(err, err_out, st);
       if (!ok && launched) return launch_status("ds2_lstm_fwd chunk");
@@ -1081,7 +1081,7 @@ ds2_status_t ds2_lstm_fwd(int t_max, int n, int h, int num_dirs, const float* xp
         return launch_status("ds2_lstm counters");
       void* args[] = {&T_, &N_, &H_, &D_, &UB_, &BT_, &xproj, &wp, &b_hh_f, &b_hh_r, &lens,
                       &h_all, &c_all, &gates, &ctrs, &err, &flags_, &NB_};
-      ok = hipLaunchCooperativeKernel(fn, dim3(mapped_grid(UB * num_dirs, BT_)), dim3(GT), args,
+      ok = rnn_launch(fn, dim3(mapped_grid(UB * num_dirs, BT_)), dim3(GT), args,
                                       0, st) == hipSuccess;
       if (ok) fold_err(err, err_out, st);
       if (!ok && b0 > 0) return launch_status("ds2_lstm_fwd chunk");
@@ -1169,7 +1169,7 @@ ds2_status_t ds2_lstm_bwd(int t_max, int n, int h, int num_dirs, const float* dy
         return launch_status("ds2_lstm counters");
       void* args[] = {&T_, &N_, &H_, &D_, &UB_, &BT_, &dy, &DYD_, &w_hh_f, &w_hh_r, &c_all,
                       &gates, &lens, &dgates, &ring, &ctrs, &err, &NB_};
-      ok = hipLaunchCooperativeKernel(fn, dim3(mapped_grid(UB * num_dirs, BT_)), dim3(GT), args,
+      ok = rnn_launch(fn, dim3(mapped_grid(UB * num_dirs, BT_)), dim3(GT), args,
                                       kLstmDopPadLds, st) == hipSuccess;
       if (ok) fold_err(err, err_out, st);
       if (!ok && launched) return launch_status("ds2_lstm_bwd chunk");
@@ -1221,7 +1221,7 @@ ds2_status_t ds2_lstm_bwd(int t_max, int n, int h, int num_dirs, const float* dy
         return launch_status("ds2_lstm counters");
       void* args[] = {&T_, &N_, &H_, &D_, &UB_, &BT_, &dy, &DYD_, &wpt, &c_all, &gates, &lens,
                       &dgates, &ctrs, &err, &flags_, &NB_};
-      ok = hipLaunchCooperativeKernel(fn, dim3(mapped_grid(UB * num_dirs, BT_)), dim3(GT), args,
+      ok = rnn_launch(fn, dim3(mapped_grid(UB * num_dirs, BT_)), dim3(GT), args,
                                       0, st) == hipSuccess;
       if (ok) fold_err(err, err_out, st);
       if (!ok && b0 > 0) return launch_status("ds2_lstm_bwd chunk");

@@ -399,6 +399,21 @@ static bool persistent_enabled() {
   return !(e != nullptr && e[0] == '0');
 }
 
+// Launch of a persistent recurrence kernel.  The host has already sized the grid to the
+// chip (grid <= CUs, one workgroup per CU through its LDS footprint), so a cooperative launch
+// adds only the runtime's occupancy check (and 15-20 us of host time per launch; residency is
+// the same for plain and cooperative launches, MI355X_MICROARCH.md "Residency and
+// cooperative launch").  DS2_RNN_COOP=0 selects plain launches.
+static inline hipError_t rnn_launch(const void* fn, dim3 grid, dim3 block, void** args,
+                                    size_t lds, hipStream_t st) {
+  static const int coop = [] {
+    const char* e = getenv("DS2_RNN_COOP");
+    return (e != nullptr && e[0] == '0') ? 0 : 1;
+  }();
+  return coop ? hipLaunchCooperativeKernel(fn, grid, block, args, lds, st)
+              : hipLaunchKernel(fn, grid, block, args, lds, st);
+}
+
 static inline int grid_cap(int64_t work) {
   int64_t g = (work + 255) / 256;
   return static_cast<int>(g > 2048 ? 2048 : (g < 1 ? 1 : g));
@@ -430,6 +445,14 @@ __device__ __forceinline__ void gru_coefs(float r, float z, float n, float hn, f
   cr = cn * hn * r * (1.f - r);
   cz = (hp - n) * z * (1.f - z);
   chn = cn * r;
+}
+
+// the dh-exchange backward is opt-in (DS2_GRU_BWD=dh): measured slower than the gate
+// exchange (gru_bwd_dh.hip header), so by default the forward writes no coefficient tiles and
+// the gate cache is the classic [T][N][D][4H]
+static inline bool gru_dh_bwd_opted_in() {
+  const char* e = getenv("DS2_GRU_BWD");
+  return e != nullptr && e[0] == 'd' && e[1] == 'h';
 }
 
 static inline size_t gru_coef_floats(int t, int n, int h, int d) {

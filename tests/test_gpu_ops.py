@@ -535,9 +535,9 @@ def _gru_run(dev, n, t, inp, h, nd, seed, env, monkeypatch, amp=None):
 @pytest.mark.parametrize("n,h,bidir", [(32, 800, True), (20, 800, True), (7, 48, False),
                                        (17, 784, True), (33, 256, True), (5, 512, False)])
 def test_gru_dh_backward_matches_gate_exchange(dev, n, h, bidir, monkeypatch):
-    """The dh-exchange backward (gru_bwd_dh.hip: producers publish dh, consumers form
-    dG = dh x the forward's coefficient tiles) against the gate-exchange backward
-    (DS2_GRU_BWD=dg): equal within fp32 rounding (the gate gradients are dh x c instead of
+    """The opt-in dh-exchange backward (DS2_GRU_BWD=dh, gru_bwd_dh.hip: producers publish dh,
+    consumers form dG = dh x the forward's coefficient tiles) against the default gate-exchange
+    backward: equal within fp32 rounding (the gate gradients are dh x c instead of
     ((dh x a) x b) ...); flag and sentinel hand-offs bit-identical; the 8-wave form (H <= 512)
     within rounding; with the fp32-MFMA forward the coefficient tiles come from the
     conversion kernel (gru_coef_kernel) and the same holds."""
@@ -561,9 +561,12 @@ def test_gru_dh_backward_matches_gate_exchange(dev, n, h, bidir, monkeypatch):
         _close(f, r, 2e-5, "dh backward after the fp32-MFMA forward (converted coefficients)")
 
 
-def test_gru_dh_backward_full_length_vs_torch(dev):
+@pytest.mark.parametrize("bwd", ["dg", "dh"])
+def test_gru_backward_full_length_vs_torch(dev, bwd, monkeypatch):
     """The cfg2 recurrence shape (bs 32, H 800, both directions) over 201 steps with ragged
-    lengths, dh-exchange backward against torch's nn.GRU in fp64."""
+    lengths: the default gate-exchange and the opt-in dh-exchange backward against torch's
+    nn.GRU in fp64."""
+    monkeypatch.setenv("DS2_GRU_BWD", bwd)
     n, t, inp, h = 32, 201, 64, 800
     g = torch.Generator().manual_seed(3)
     gru = torch.nn.GRU(inp, h, bidirectional=True).double()
