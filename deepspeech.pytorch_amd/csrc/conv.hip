@@ -1088,6 +1088,7 @@ constexpr int CX_T = 512;
 constexpr int CX_COLS = 256;
 constexpr int CX_PATCH = 3 * 522 * 24;   // bf16: 3 planes x columns x pitch (max)
 constexpr int CX_PATCH1 = 3 * 267 * 40;  // the same for width stride 1 without row chunks
+constexpr int CX_PATCH_DB = 2 * 3 * 267 * 24;   // double-buffered (conv2 fwd: pitch 24)
 constexpr int CX_WIMG = 3 * 32 * 296;    // bf16: 3 planes x 32 channels x COP (max)
 constexpr int CX_PU = 3;                 // patch staging units per thread (max; template PU)
 constexpr int CX_WQ = 7;                 // 16-B weight-image chunks per thread
@@ -1113,7 +1114,7 @@ __host__ __device__ inline CxGeom cx_geom(const ConvDims& g, bool dgrad) {
   c.KA = a <= 24 ? (a + 7) / 8 * 8 : 16;
   c.RC = (a + c.KA - 1) / c.KA;
   c.NBP = (g.kw + 1) / 2;
-  c.P = cx_pitch8odd(c.KA + 1);
+  c.P = cx_pitch8odd(c.KA);        // 8 x odd bf16: conflict-free 16-B fragment reads
   c.COP = cx_pitch8odd(2 * c.NBP * c.KA + 1);
   c.PCOL = (CX_COLS - 1) * (dgrad ? 1 : g.sw) + 2 * c.NBP;
   return c;
@@ -1166,14 +1167,18 @@ __global__ void conv_x6_wimg_kernel(const float* __restrict__ w, ConvDims g, CxG
 // staging units per thread (2, or 3 for conv1's 522-column stride-2 patch).  SW: width stride
 // (0: run time); RCH: tap-row chunks (c.RC) possible.  The width-stride-1 unchunked form
 // (conv2) keeps its smaller LDS patch and compile-time addressing.
-template <bool DGRAD, int NGA, int NBP_, int PU, int SW, bool RCH>
+// DB: the input patch double-buffered (conv2 fwd): the next channel's patch is split and
+// stored into the other buffer in the middle of this channel's k-steps (its loads were issued
+// at the channel's start), so only the weight image copy stays between the two barriers.
+template <bool DGRAD, int NGA, int NBP_, int PU, int SW, bool RCH, bool DB = false>
 __global__ __launch_bounds__(CX_T, 1) void conv_x6_kernel(const float* __restrict__ in,
                                                           const unsigned short* __restrict__ img,
                                                           const float* __restrict__ bias,
                                                           float* __restrict__ out, ConvDims g,
                                                           const int* __restrict__ out_lens,
                                                           CxGeom c, int gx, int gy) {
-  __shared__ __attribute__((aligned(16))) unsigned short ps[(SW == 1 && !RCH) ? CX_PATCH1 : CX_PATCH];
+  __shared__ __attribute__((aligned(16))) unsigned short
+      ps[DB ? CX_PATCH_DB : ((SW == 1 && !RCH) ? CX_PATCH1 : CX_PATCH)];
   __shared__ __attribute__((aligned(16))) unsigned short ws[CX_WIMG];
   const int M = DGRAD ? g.ci : g.co;
   const int L = DGRAD ? g.co : g.ci;
@@ -1227,6 +1232,17 @@ __global__ __launch_bounds__(CX_T, 1) void conv_x6_kernel(const float* __restric
 
   float rp[PU][8];
   u32x4 rw[CX_WQ];
+  auto load_w = [&](int l) {
+    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<unsigned short*>(wimg + (int64_t)l * wstride), (short)0,
+        static_cast<int>(wstride * 2), 0x00020000);
+#pragma unroll
+    for (int r = 0; r < CX_WQ; ++r) {
+      const int i = tid + CX_T * r;
+      rw[r] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                            wr, i < wchunks ? i * 16 : 0x7ffffff0, 0, 0));
+    }
+  };
   auto load = [&](int l) {
     const int ch = RCH ? l / RC : l, ar0 = RCH ? (l - ch * RC) * c.KA : 0;   // chunk's first tap row
     const __amdgpu_buffer_rsrc_t rs = conv_rsrc(inn + (int64_t)ch * plane_in, plane_in);
@@ -1244,30 +1260,28 @@ __global__ __launch_bounds__(CX_T, 1) void conv_x6_kernel(const float* __restric
                                                  rs, ok ? (ir * in_w + ic) * 4 : 0x7ffffff0, 0, 0));
       }
     }
-    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<unsigned short*>(wimg + (int64_t)l * wstride), (short)0,
-        static_cast<int>(wstride * 2), 0x00020000);
-#pragma unroll
-    for (int r = 0; r < CX_WQ; ++r) {
-      const int i = tid + CX_T * r;
-      rw[r] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                            wr, i < wchunks ? i * 16 : 0x7ffffff0, 0, 0));
-    }
+    if (!DB) load_w(l);
   };
-  auto store = [&]() {
+  auto store_patch = [&](unsigned short* dst) {
 #pragma unroll
     for (int u = 0; u < PU; ++u) {
       const int unit = tid + CX_T * u;
       if (unit < units) {
         const int j = unit / ngr, rg = unit - (unit / ngr) * ngr;
-        cx_split_store8(ps, PPL, j * c.P + 8 * rg, rp[u]);
+        cx_split_store8(dst, PPL, j * c.P + 8 * rg, rp[u]);
       }
     }
+  };
+  auto store_w = [&]() {
 #pragma unroll
     for (int r = 0; r < CX_WQ; ++r) {
       const int i = tid + CX_T * r;
       if (i < wchunks) *reinterpret_cast<u32x4*>(ws + 8 * i) = rw[r];
     }
+  };
+  auto store = [&]() {
+    store_patch(ps);
+    store_w();
   };
 
   f32x16 acc[2];
@@ -1282,10 +1296,14 @@ __global__ __launch_bounds__(CX_T, 1) void conv_x6_kernel(const float* __restric
   const bool active = orow < out_h && c0 + 64 * cw < out_w;
 
   load(0);
+  if (DB) load_w(0);
   store();
   __syncthreads();
   for (int l = 0; l < LL; ++l) {
     if (l + 1 < LL) load(l + 1);
+    const unsigned short* pcur = DB ? ps + (l & 1) * 3 * PPL : ps;
+    unsigned short* pnext = ps + ((l + 1) & 1) * 3 * PPL;
+    bool staged = false;
     if (active) {
       auto kstep = [&](int st) {
         const int ga = st / nbp, p = st - (st / nbp) * nbp;
@@ -1299,7 +1317,7 @@ __global__ __launch_bounds__(CX_T, 1) void conv_x6_kernel(const float* __restric
           const int ap = ((64 * cw + 32 * j + fr) * sw + b) * c.P + 8 * ga;
 #pragma unroll
           for (int pl = 0; pl < 3; ++pl)
-            bfr[j][pl] = *reinterpret_cast<const bf16x8*>(ps + pl * PPL + ap);
+            bfr[j][pl] = *reinterpret_cast<const bf16x8*>(pcur + pl * PPL + ap);
         }
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
@@ -1314,20 +1332,45 @@ __global__ __launch_bounds__(CX_T, 1) void conv_x6_kernel(const float* __restric
       };
       if (NGA > 0 && NBP_ > 0) {
         constexpr int NK = NGA * NBP_, H0 = (NK + 1) / 2;
+        constexpr int MID = H0 / 2 + 1;     // DB: stage the next patch after these k-steps
         if (kk == 0) {
 #pragma unroll
-          for (int st = 0; st < H0; ++st) kstep(st);
+          for (int st = 0; st < H0; ++st) {
+            if (DB && st == MID && l + 1 < LL) {
+              store_patch(pnext);
+              load_w(l + 1);        // issued once rp is free: rp and rw never live together
+              staged = true;
+            }
+            kstep(st);
+            if (DB) __builtin_amdgcn_sched_barrier(0);   // bound the fragment-read hoisting
+          }
         } else {
 #pragma unroll
-          for (int st = H0; st < NK; ++st) kstep(st);
+          for (int st = H0; st < NK; ++st) {
+            if (DB && st == H0 + MID && l + 1 < LL) {
+              store_patch(pnext);
+              load_w(l + 1);
+              staged = true;
+            }
+            kstep(st);
+            if (DB) __builtin_amdgcn_sched_barrier(0);
+          }
         }
       } else {
         for (int st = s_beg; st < s_end; ++st) kstep(st);
       }
     }
+    if (DB && !staged && l + 1 < LL) {
+      store_patch(pnext);
+      load_w(l + 1);
+    }
     __syncthreads();
     if (l + 1 < LL) {
-      store();
+      if (DB) {
+        store_w();
+      } else {
+        store();
+      }
       __syncthreads();
     }
   }
@@ -1841,6 +1884,12 @@ static ds2_status_t launch_x6q(const float* dy, const float* w, float* dx, const
   return launch_status("ds2_conv2d_dgrad");
 }
 
+// DS2_CONV_X6_DB=0: the single-buffered conv2 forward (diagnostic)
+static inline bool cx_db_enabled() {
+  const char* e = getenv("DS2_CONV_X6_DB");
+  return !(e != nullptr && e[0] == '0');
+}
+
 static size_t x6_ws_bytes(const ConvDims& g, bool dgrad) {
   if (!x6_ok(g, dgrad)) return 0;
   const CxGeom c = cx_geom(g, dgrad);
@@ -1869,7 +1918,11 @@ static ds2_status_t launch_x6(const float* in, const float* w, const float* bias
 #define DS2_CX(NG, NB, PU, SW, RCH)                                                          \
   hipLaunchKernelGGL((conv_x6_kernel<DGRAD, NG, NB, PU, SW, RCH>), grid, dim3(CX_T), 0, st, in, \
                      img, bias, out, g, out_lens, c, gx, gy)
-  if (small && !DGRAD && nga == 3 && c.NBP == 6)
+  const bool db = small && 2 * 3 * c.PCOL * c.P <= CX_PATCH_DB && cx_db_enabled();
+  if (small && !DGRAD && nga == 3 && c.NBP == 6 && db)
+    hipLaunchKernelGGL((conv_x6_kernel<DGRAD, 3, 6, 2, 1, false, true>), grid, dim3(CX_T), 0, st,
+                       in, img, bias, out, g, out_lens, c, gx, gy);   // conv2 fwd, double-buffered
+  else if (small && !DGRAD && nga == 3 && c.NBP == 6)
     DS2_CX(3, 6, 2, 1, false);                           // conv2 fwd
   else if (small && DGRAD && nga == 2 && c.NBP == 6)
     DS2_CX(2, 6, 2, 1, false);                           // conv2 dgrad

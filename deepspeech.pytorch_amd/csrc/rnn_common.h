@@ -401,14 +401,19 @@ static bool persistent_enabled() {
 
 // Launch of a persistent recurrence kernel.  The host has already sized the grid to the
 // chip (grid <= CUs, one workgroup per CU through its LDS footprint), so a cooperative launch
-// adds only the runtime's occupancy check (and 15-20 us of host time per launch; residency is
-// the same for plain and cooperative launches, MI355X_MICROARCH.md "Residency and
-// cooperative launch").  DS2_RNN_COOP=0 selects plain launches.
+// would add only the runtime's occupancy check (and 15-20 us of host time per launch;
+// residency is the same for plain and cooperative launches, MI355X_MICROARCH.md "Residency
+// and cooperative launch").  Plain launches are the default: a process that had made one
+// hipLaunchCooperativeKernel died with SIGSEGV at exit under rocprofv3 (inside
+// libhsa-runtime64, called from the HIP runtime's exit handler, on a /dev/dri doorbell
+// mapping; scripts/prof_exit_probe2.sh: one cooperative GRU launch reproduces it, the same
+// launch made plainly exits 0), and the step time is unchanged (profiles/r3g_coop_ab.txt).
+// DS2_RNN_COOP=1 selects cooperative launches.
 static inline hipError_t rnn_launch(const void* fn, dim3 grid, dim3 block, void** args,
                                     size_t lds, hipStream_t st) {
   static const int coop = [] {
     const char* e = getenv("DS2_RNN_COOP");
-    return (e != nullptr && e[0] == '0') ? 0 : 1;
+    return (e != nullptr && e[0] == '1') ? 1 : 0;
   }();
   return coop ? hipLaunchCooperativeKernel(fn, grid, block, args, lds, st)
               : hipLaunchKernel(fn, grid, block, args, lds, st);

@@ -13,7 +13,7 @@ for G in 1 4; do
       -d "$GRAFT_REPO_ROOT/gpurun_out/gab.pmc$G" -o run --output-format csv -- \
       python "$GRAFT_REPO_ROOT/scripts/gemm_one.py" 0 1 16032 2400 800 5 > "$GRAFT_REPO_ROOT/gpurun_out/gab.pmc$G.log" 2>&1 )
   rc=$?; echo "PMC $G EXIT $rc"
-  if [ $rc -ne 0 ] && [ $rc -ne 139 ]; then exit $rc; fi
+  if [ $rc -ne 0 ]; then exit $rc; fi
 done
 for R in 1 2; do
   for G in 1 4; do

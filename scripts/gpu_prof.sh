@@ -8,6 +8,5 @@ cd /tmp && export TMPDIR=/tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/$TAG.prof" -o run --output-format csv -- python "$GRAFT_REPO_ROOT/bench.py" --steps 5 --warmup 2 --no-cpu-baseline > "$GRAFT_REPO_ROOT/gpurun_out/$TAG.prof.log" 2>&1
 rc=$?
 echo "PROF EXIT $rc"
-# 139: the profiler's exit-time crash after the summaries were written
-if [ $rc -ne 0 ] && [ $rc -ne 139 ]; then exit $rc; fi
+if [ $rc -ne 0 ]; then exit $rc; fi
 cd "$GRAFT_REPO_ROOT" && bash scripts/pmc_traffic.sh $TAG.pmc

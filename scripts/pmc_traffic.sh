@@ -11,5 +11,5 @@ for C in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 900 rocprofv3 --pmc $C --kernel-trace -d "$GRAFT_REPO_ROOT/gpurun_out/$TAG.$C" -o run --output-format csv -- python "$GRAFT_REPO_ROOT/bench.py" --steps 1 --warmup 0 --no-cpu-baseline > "$GRAFT_REPO_ROOT/gpurun_out/$TAG.$C.log" 2>&1
   rc=$?
   echo "$C EXIT $rc"
-  if [ $rc -ne 0 ] && [ $rc -ne 139 ]; then exit $rc; fi
+  if [ $rc -ne 0 ]; then exit $rc; fi
 done
