@@ -1102,11 +1102,21 @@ struct CxGeom {
   int RC;     // tap-row chunks per loop channel
 };
 
-__host__ __device__ inline int cx_pitch8odd(int v) {   // smallest 8 * odd >= v
-  int k = (v + 7) / 8;
-  if ((k & 1) == 0) ++k;
-  return 8 * k;
+__host__ __device__ constexpr int cx_pitch8odd(int v) {   // smallest 8 * odd >= v
+  return 8 * (((v + 7) / 8) % 2 == 0 ? (v + 7) / 8 + 1 : (v + 7) / 8);
 }
+
+// The geometry cx_geom gives an instantiation with compile-time a-groups / column pairs and
+// width stride 1 without row chunks (conv2 fwd / dgrad): with it a compile-time constant,
+// every fragment read is one per-lane base + an immediate offset (no address registers or
+// VALU per k-step).
+template <int NGA, int NBP>
+struct CxConst {
+  static constexpr int KA = 8 * NGA;
+  static constexpr int P = cx_pitch8odd(KA);
+  static constexpr int COP = cx_pitch8odd(2 * NBP * KA + 1);
+  static constexpr int PCOL = (256 - 1) + 2 * NBP;
+};
 
 __host__ __device__ inline CxGeom cx_geom(const ConvDims& g, bool dgrad) {
   CxGeom c;
@@ -1221,13 +1231,19 @@ __global__ __launch_bounds__(CX_T, 1) void conv_x6_kernel(const float* __restric
   const int cw = wave & 3, kk = wave >> 2;
   const int plane_in = in_h * in_w;
   const float* inn = in + (int64_t)n * L * plane_in;
-  const int PPL = c.PCOL * c.P;                // bf16 per patch plane
-  const int WPL = 32 * c.COP;                  // bf16 per weight plane
+  constexpr bool CG = NGA > 0 && NBP_ > 0 && SW == 1 && !RCH;   // compile-time geometry
+  using CC = CxConst<(NGA > 0 ? NGA : 1), (NBP_ > 0 ? NBP_ : 1)>;
+  const int cP = CG ? CC::P : c.P;
+  const int cCOP = CG ? CC::COP : c.COP;
+  const int cKA = CG ? CC::KA : c.KA;
+  const int cPCOL = CG ? CC::PCOL : c.PCOL;
+  const int PPL = cPCOL * cP;                  // bf16 per patch plane
+  const int WPL = 32 * cCOP;                   // bf16 per weight plane
   const int64_t wstride = (int64_t)3 * WPL;    // one loop channel's image
   const unsigned short* wimg = img + ((int64_t)q * mbn + mb) * L * RC * wstride;
-  const int ngr = NGA > 0 ? NGA : c.KA / 8;
+  const int ngr = NGA > 0 ? NGA : cKA / 8;
   const int nbp = NBP_ > 0 ? NBP_ : c.NBP;
-  const int units = c.PCOL * ngr;
+  const int units = cPCOL * ngr;
   const int wchunks = (int)(wstride / 8);
 
   float rp[PU][8];
@@ -1244,7 +1260,7 @@ __global__ __launch_bounds__(CX_T, 1) void conv_x6_kernel(const float* __restric
     }
   };
   auto load = [&](int l) {
-    const int ch = RCH ? l / RC : l, ar0 = RCH ? (l - ch * RC) * c.KA : 0;   // chunk's first tap row
+    const int ch = RCH ? l / RC : l, ar0 = RCH ? (l - ch * RC) * cKA : 0;   // chunk's first tap row
     const __amdgpu_buffer_rsrc_t rs = conv_rsrc(inn + (int64_t)ch * plane_in, plane_in);
 #pragma unroll
     for (int u = 0; u < PU; ++u) {
@@ -1268,7 +1284,7 @@ __global__ __launch_bounds__(CX_T, 1) void conv_x6_kernel(const float* __restric
       const int unit = tid + CX_T * u;
       if (unit < units) {
         const int j = unit / ngr, rg = unit - (unit / ngr) * ngr;
-        cx_split_store8(dst, PPL, j * c.P + 8 * rg, rp[u]);
+        cx_split_store8(dst, PPL, j * cP + 8 * rg, rp[u]);
       }
     }
   };
@@ -1309,12 +1325,12 @@ __global__ __launch_bounds__(CX_T, 1) void conv_x6_kernel(const float* __restric
         const int ga = st / nbp, p = st - (st / nbp) * nbp;
         const int b = 2 * p + fh;
         bf16x8 af[3], bfr[2][3];
-        const int aw = fr * c.COP + b * c.KA + 8 * ga;
+        const int aw = fr * cCOP + b * cKA + 8 * ga;
 #pragma unroll
         for (int pl = 0; pl < 3; ++pl) af[pl] = *reinterpret_cast<const bf16x8*>(ws + pl * WPL + aw);
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
-          const int ap = ((64 * cw + 32 * j + fr) * sw + b) * c.P + 8 * ga;
+          const int ap = ((64 * cw + 32 * j + fr) * sw + b) * cP + 8 * ga;
 #pragma unroll
           for (int pl = 0; pl < 3; ++pl)
             bfr[j][pl] = *reinterpret_cast<const bf16x8*>(pcur + pl * PPL + ap);
@@ -1567,6 +1583,186 @@ __global__ __launch_bounds__(CW_T, 2) void conv_x6_wgrad_kernel(const float* __r
 }
 
 // ---------------------------------------------------------------------------
+// Sliding-window form of the bf16x6 weight gradient (default where conv_x6_wgrad_kernel
+// applies and the height stride is <= 2).  Same workgroups (tap-row group gi of 4 rows, split
+// s; 4 waves, one tap row each, kw accumulators) and the same per-tap MFMA step, but a split
+// walks the (n, 32-column chunk, ho) rows with ho fastest: output row ho + 1's four x rows are
+// row ho's moved down by sh, so each row stages only sh NEW x rows (plus its dy row) into a
+// 6-slot ring (4 window rows + 2 incoming) -- 1.5 instead of 5 staging units of 8 values per
+// thread -- while the MFMAs of row ho run on the other slots; one barrier per row.  Each x row
+// is staged once per (group, chunk) instead of kh / sh times, and the G groups of a split run on
+// one XCD (consecutive workgroup ids), so they share its L2 for x and dy.
+constexpr int SW_T = 256;
+constexpr int SW_COLS = 32;                 // output columns per row stage (two 16-column k-steps)
+constexpr int SW_XP = 48;                   // x slot row pitch (bf16): columns c0 - 8 .. c0 + 39
+constexpr int SW_DP = 40;                   // dy row pitch (bf16): 32 columns, 5 x 16 B
+constexpr int SW_RING = 6;                  // x slots: 4 window rows + 2 incoming
+constexpr int SW_XSL = 32 * SW_XP;          // bf16 per x slot (32 input channels)
+constexpr int SW_XPL = SW_RING * SW_XSL;    // bf16 per x plane
+constexpr int SW_DPL = 32 * SW_DP;          // bf16 per dy plane
+
+template <int KW, int OFF0>
+__global__ __launch_bounds__(SW_T, 2) void conv_x6_wgrad_sw_kernel(const float* __restrict__ dy,
+                                                                   const float* __restrict__ x,
+                                                                   float* __restrict__ partial,
+                                                                   ConvDims g, int S) {
+  __shared__ __attribute__((aligned(16))) unsigned short xs[3 * SW_XPL];
+  __shared__ __attribute__((aligned(16))) unsigned short ds[2][3 * SW_DPL];
+  constexpr int kOob = 0x7ffffff0;
+  const int G = (g.kh + 3) / 4;
+  int gi, s;
+  {
+    const int nwg = gridDim.x, o = blockIdx.x;
+    const int q = nwg >> 3, r = nwg & 7, xcd = o & 7;
+    const int id = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (o >> 3);
+    gi = id % G;
+    s = id / G;
+  }
+  const int nch = (g.wo + SW_COLS - 1) / SW_COLS;
+  const int R = g.n * nch * g.ho;                           // host: < 2^31
+  const int r0 = static_cast<int>((int64_t)s * R / S);
+  const int r1 = static_cast<int>((int64_t)(s + 1) * R / S);
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int a = 4 * gi + wave;
+  const bool active = a < g.kh;
+  const int fr = lane & 31, fh = lane >> 5;
+  const int dplane = g.ho * g.wo, xplane = g.hi * g.wi;   // host: channel stacks < 2^31 B
+  const int wtop = 4 * gi - g.ph;                           // window row 0 of output row 0
+  // staging units (8 values each): 384 x units (incoming row r, channel, 8-column run j) and
+  // 128 dy units (channel, run j); thread t takes units t and t + 256
+  // (unit kinds are wave-uniform: waves 0-2 unit a row 0, wave 3 row 1; waves 0-1 unit b x
+  // row 1, waves 2-3 dy -- so the buffer resources stay scalar)
+  const int u1 = tid + SW_T;
+  const int xr_a = wave == 3 ? 1 : 0, xc_a = (tid / 6) & 31, xj_a = tid % 6;
+  const bool b_is_x = wave < 2;
+  const int xc_b = (u1 / 6) & 31, xj_b = u1 % 6;             // x unit: incoming row 1
+  const int dc_b = (u1 - 384) >> 2, dj_b = (u1 - 384) & 3;   // dy unit
+
+  f32x16 acc[KW];
+#pragma unroll
+  for (int b = 0; b < KW; ++b)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[b][r] = 0.f;
+
+  float va[8], vb[8];
+  auto slot_of = [](int xr) { return ((xr % SW_RING) + SW_RING) % SW_RING; };
+
+  int row = r0;
+  while (row < r1) {
+    const int ho0 = row % g.ho, q = row / g.ho;
+    const int ch = q % nch, n = q / nch;
+    const int nrow = min(r1 - row, g.ho - ho0);              // rows of this (n, chunk) segment
+    const int c0 = ch * SW_COLS;
+    const __amdgpu_buffer_rsrc_t drs = conv_rsrc(dy + (int64_t)n * g.co * dplane, (int64_t)g.co * dplane);
+    const __amdgpu_buffer_rsrc_t xrs = conv_rsrc(x + (int64_t)n * g.ci * xplane, (int64_t)g.ci * xplane);
+    // loads of x rows xr0 + r (r < nr; r = 0 unit a, r = 1 unit b) and, when hd >= 0, dy row hd
+    auto load = [&](int xr0, int nr, int hd) {
+      {
+        const int xr = xr0 + xr_a, cb = c0 - 8 + 8 * xj_a;
+        const bool ok = xr_a < nr && xc_a < g.ci && xr >= 0 && xr < g.hi;
+        const int vo = ok ? (xc_a * xplane + xr * g.wi + cb) * 4 : kOob;
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          va[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                xrs, (cb + i >= 0 && cb + i < g.wi) ? vo + 4 * i : kOob, 0, 0));
+      }
+      if (b_is_x) {
+        const int xr = xr0 + 1, cb = c0 - 8 + 8 * xj_b;
+        const bool ok = nr > 1 && xc_b < g.ci && xr >= 0 && xr < g.hi;
+        const int vo = ok ? (xc_b * xplane + xr * g.wi + cb) * 4 : kOob;
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          vb[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                xrs, (cb + i >= 0 && cb + i < g.wi) ? vo + 4 * i : kOob, 0, 0));
+      } else {
+        const int cb = c0 + 8 * dj_b;
+        const int vo = (hd >= 0 && dc_b < g.co) ? (dc_b * dplane + hd * g.wo + cb) * 4 : kOob;
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          vb[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                drs, cb + i < g.wo ? vo + 4 * i : kOob, 0, 0));
+      }
+    };
+    auto store = [&](int xr0, int nr, int db) {
+      if (xr_a < nr) cw_split_store(xs, SW_XPL, slot_of(xr0 + xr_a) * SW_XSL + xc_a * SW_XP + 8 * xj_a, va);
+      if (b_is_x) {
+        if (nr > 1) cw_split_store(xs, SW_XPL, slot_of(xr0 + 1) * SW_XSL + xc_b * SW_XP + 8 * xj_b, vb);
+      } else if (db >= 0) {
+        cw_split_store(ds[db], SW_DPL, dc_b * SW_DP + 8 * dj_b, vb);
+      }
+    };
+    // segment start: every slot and dy buffer is free once all waves pass this barrier; the
+    // four window rows of ho0 go in two passes (the first with ho0's dy row)
+    const int xb0 = ho0 * g.sh + wtop;
+    __syncthreads();
+    load(xb0, 2, ho0);
+    store(xb0, 2, ho0 & 1);
+    load(xb0 + 2, 2, -1);
+    store(xb0 + 2, 2, -1);
+    __syncthreads();
+    for (int k = 0; k < nrow; ++k) {
+      const int ho = ho0 + k;
+      const bool more = k + 1 < nrow;
+      const int xb = ho * g.sh + wtop;                      // window row 0 of this output row
+      const int xin = xb + 4;                               // row ho + 1's incoming rows
+      if (more) load(xin, g.sh, ho + 1);
+      if (active) {
+        const unsigned short* dsb = ds[ho & 1];
+        const unsigned short* xsl = xs + slot_of(xb + wave) * SW_XSL + fr * SW_XP;
+#pragma unroll
+        for (int kst = 0; kst < SW_COLS / 16; ++kst) {
+          bf16x8 af[3];
+#pragma unroll
+          for (int pl = 0; pl < 3; ++pl)
+            af[pl] = *reinterpret_cast<const bf16x8*>(dsb + pl * SW_DPL + fr * SW_DP + 16 * kst + 8 * fh);
+#pragma unroll
+          for (int pi = 0; pi < 3; ++pi) {
+            const int pl = 2 - pi;
+            unsigned wv[12];
+#pragma unroll
+            for (int jj = 0; jj < 3; ++jj) {
+              const u32x4 qv = *reinterpret_cast<const u32x4*>(xsl + pl * SW_XPL + 8 * (2 * kst + fh + jj));
+#pragma unroll
+              for (int e = 0; e < 4; ++e) wv[4 * jj + e] = qv[e];
+            }
+#pragma unroll
+            for (int b = 0; b < KW; ++b) {
+              const int o = b + OFF0;
+              u32x4 qb;
+#pragma unroll
+              for (int e = 0; e < 4; ++e)
+                qb[e] = (o & 1) ? __builtin_amdgcn_alignbit(wv[(o + 1) / 2 + e], wv[(o - 1) / 2 + e], 16)
+                                : wv[o / 2 + e];
+              const bf16x8 bx = __builtin_bit_cast(bf16x8, qb);
+#pragma unroll
+              for (int i = 2 - pl; i >= 0; --i)
+                acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bx, acc[b], 0, 0, 0);
+            }
+          }
+        }
+      }
+      // the incoming slots held rows xb - 2, xb - 1 (read by row ho - 1, before the last
+      // barrier); the other dy buffer likewise
+      if (more) store(xin, g.sh, (ho + 1) & 1);
+      __syncthreads();
+    }
+    row += nrow;
+  }
+  if (!active || fr >= g.ci) return;
+  const int Kc = g.ci * g.kh * KW;
+  float* slab = partial + (int64_t)s * g.co * Kc;
+#pragma unroll
+  for (int b = 0; b < KW; ++b)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int co = (r & 3) + 8 * (r >> 2) + 4 * fh;
+      if (co < g.co) slab[(int64_t)co * Kc + (fr * g.kh + a) * KW + b] = acc[b][r];
+    }
+}
+
+// ---------------------------------------------------------------------------
 // bf16x6 dgrad with 4-row x 2-column fragments (default for <= 12 class tap rows and <= 12
 // kernel columns: conv2's 11 x 11 class taps take 3 x 3 k-steps of 16 taps -- 144 tap slots
 // for 121 -- instead of the 8-row fragments' 2 x 6 -- 192).  K order of k-step (row quad rq,
@@ -1623,12 +1819,19 @@ __global__ void conv_x6q_wimg_kernel(const float* __restrict__ w, ConvDims g,
   }
 }
 
+// DB: double-buffered patch and weight chunk (2 x 69 KB of LDS) -- channel l + 1 is staged
+// into the other buffer right after the k-steps of channel l, one barrier per channel.  The
+// patch gather offsets (and their bounds) are the same for every channel and are hoisted.
+template <bool DB>
 __global__ __launch_bounds__(CX_T, 1) void conv_x6q_dgrad_kernel(const float* __restrict__ dy,
                                                                  const unsigned short* __restrict__ img,
                                                                  float* __restrict__ dx, ConvDims g,
                                                                  int gx, int gy) {
-  __shared__ __attribute__((aligned(16))) unsigned short ps[3 * CQ_PPL];
-  __shared__ __attribute__((aligned(16))) unsigned short ws[3 * 32 * CQ_COP];
+  constexpr int NB = DB ? 2 : 1;
+  constexpr int WPL = 32 * CQ_COP;
+  constexpr int wstride = 3 * WPL;
+  __shared__ __attribute__((aligned(16))) unsigned short ps[NB * 3 * CQ_PPL];
+  __shared__ __attribute__((aligned(16))) unsigned short ws[NB * wstride];
   const int M = g.ci, L = g.co;
   const int in_h = g.ho, in_w = g.wo, out_h = g.hi, out_w = g.wi;
   const int mbn = (M + 31) / 32;
@@ -1655,52 +1858,56 @@ __global__ __launch_bounds__(CX_T, 1) void conv_x6q_dgrad_kernel(const float* __
   const int cw = wave & 3, kk = wave >> 2;
   const int plane_in = in_h * in_w;
   const float* inn = dy + (int64_t)n * L * plane_in;
-  constexpr int WPL = 32 * CQ_COP;
-  constexpr int wstride = 3 * WPL;
   const unsigned short* wimg = img + ((int64_t)q * mbn + mb) * L * wstride;
   constexpr int wchunks = wstride / 8;
+  constexpr int WR = (wchunks + CX_T - 1) / CX_T;
+
+  // per-thread gather offsets (bytes; out-of-range elements read the buffer's zero tail)
+  int goff[2][8];
+  int soff[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int unit = tid + CX_T * u;
+    const int cp = unit / (CQ_PAIRS * 3), rem = unit - cp * (CQ_PAIRS * 3);
+    const int j = rem / 3, rq = rem - (rem / 3) * 3;
+    const int col = pcol0 + 2 * j + cp;            // the pair's first column
+    soff[u] = unit < CQ_UNITS ? cp * CQ_OFFO + j * CQ_PP + 8 * rq : -1;
+#pragma unroll
+    for (int x = 0; x < 8; ++x) {
+      const int a = 4 * rq + (x >> 1), ir = prow0 + a, ic = col + (x & 1);
+      const bool ok = unit < CQ_UNITS && a < A && ir >= 0 && ir < in_h && ic >= 0 && ic < in_w;
+      goff[u][x] = ok ? (ir * in_w + ic) * 4 : 0x7ffffff0;
+    }
+  }
 
   float rp[2][8];
-  u32x4 rw[(wchunks + CX_T - 1) / CX_T];
+  u32x4 rw[WR];
   auto load = [&](int l) {
     const __amdgpu_buffer_rsrc_t rs = conv_rsrc(inn + (int64_t)l * plane_in, plane_in);
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int unit = tid + CX_T * u;
-      const int cp = unit / (CQ_PAIRS * 3), rem = unit - cp * (CQ_PAIRS * 3);
-      const int j = rem / 3, rq = rem - (rem / 3) * 3;
-      const int col = pcol0 + 2 * j + cp;          // the pair's first column
+    for (int u = 0; u < 2; ++u)
 #pragma unroll
-      for (int x = 0; x < 8; ++x) {
-        const int a = 4 * rq + (x >> 1), ir = prow0 + a, ic = col + (x & 1);
-        const bool ok = unit < CQ_UNITS && a < A && ir >= 0 && ir < in_h && ic >= 0 && ic < in_w;
-        rp[u][x] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                                 rs, ok ? (ir * in_w + ic) * 4 : 0x7ffffff0, 0, 0));
-      }
-    }
+      for (int x = 0; x < 8; ++x)
+        rp[u][x] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, goff[u][x], 0, 0));
     const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<unsigned short*>(wimg + (int64_t)l * wstride), (short)0, wstride * 2, 0x00020000);
 #pragma unroll
-    for (int r = 0; r < (wchunks + CX_T - 1) / CX_T; ++r) {
+    for (int r = 0; r < WR; ++r) {
       const int i = tid + CX_T * r;
       rw[r] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
                                             wr, i < wchunks ? i * 16 : 0x7ffffff0, 0, 0));
     }
   };
-  auto store = [&]() {
+  auto store = [&](int b) {
+    unsigned short* pb = ps + b * (3 * CQ_PPL);
+    unsigned short* wb = ws + b * wstride;
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int unit = tid + CX_T * u;
-      if (unit < CQ_UNITS) {
-        const int cp = unit / (CQ_PAIRS * 3), rem = unit - cp * (CQ_PAIRS * 3);
-        const int j = rem / 3, rq = rem - (rem / 3) * 3;
-        cw_split_store(ps, CQ_PPL, cp * CQ_OFFO + j * CQ_PP + 8 * rq, rp[u]);
-      }
-    }
+    for (int u = 0; u < 2; ++u)
+      if (soff[u] >= 0) cw_split_store(pb, CQ_PPL, soff[u], rp[u]);
 #pragma unroll
-    for (int r = 0; r < (wchunks + CX_T - 1) / CX_T; ++r) {
+    for (int r = 0; r < WR; ++r) {
       const int i = tid + CX_T * r;
-      if (i < wchunks) *reinterpret_cast<u32x4*>(ws + 8 * i) = rw[r];
+      if (i < wchunks) *reinterpret_cast<u32x4*>(wb + 8 * i) = rw[r];
     }
   };
 
@@ -1714,24 +1921,27 @@ __global__ __launch_bounds__(CX_T, 1) void conv_x6q_dgrad_kernel(const float* __
   constexpr int H0 = (CQ_NK + 1) / 2;
 
   load(0);
-  store();
+  store(0);
   __syncthreads();
   for (int l = 0; l < L; ++l) {
+    const int cur = DB ? (l & 1) : 0;
     if (l + 1 < L) load(l + 1);
     if (active) {
+      const unsigned short* pc = ps + cur * (3 * CQ_PPL);
+      const unsigned short* wc = ws + cur * wstride;
       auto kstep = [&](int st) {
         const int rq = st / 3, cq = st - (st / 3) * 3;
         bf16x8 af[3], bfr[2][3];
         const int aw = fr * CQ_COP + (st * 2 + fh) * 8;
 #pragma unroll
-        for (int pl = 0; pl < 3; ++pl) af[pl] = *reinterpret_cast<const bf16x8*>(ws + pl * WPL + aw);
+        for (int pl = 0; pl < 3; ++pl) af[pl] = *reinterpret_cast<const bf16x8*>(wc + pl * WPL + aw);
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
           const int sc = 64 * cw + 32 * j + fr + 4 * cq + 2 * fh;   // first patch column
           const int ap = (sc & 1) * CQ_OFFO + (sc >> 1) * CQ_PP + 8 * rq;
 #pragma unroll
           for (int pl = 0; pl < 3; ++pl)
-            bfr[j][pl] = *reinterpret_cast<const bf16x8*>(ps + pl * CQ_PPL + ap);
+            bfr[j][pl] = *reinterpret_cast<const bf16x8*>(pc + pl * CQ_PPL + ap);
         }
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
@@ -1752,10 +1962,16 @@ __global__ __launch_bounds__(CX_T, 1) void conv_x6q_dgrad_kernel(const float* __
         for (int st = H0; st < CQ_NK; ++st) kstep(st);
       }
     }
-    __syncthreads();
-    if (l + 1 < L) {
-      store();
+    if (DB) {
+      // the other buffer was last read in channel l - 1, before the previous barrier
+      if (l + 1 < L) store(cur ^ 1);
       __syncthreads();
+    } else {
+      __syncthreads();
+      if (l + 1 < L) {
+        store(0);
+        __syncthreads();
+      }
     }
   }
   // the two k halves meet in LDS (the patch area): half 1 writes, half 0 adds (fixed order)
@@ -1870,6 +2086,12 @@ static size_t x6q_ws_bytes(const ConvDims& g) {
   return (size_t)g.sh * ((g.ci + 31) / 32) * g.co * 3 * 32 * CQ_COP * sizeof(unsigned short);
 }
 
+// DS2_CONV_X6_DB=0: the single-buffered conv2 forward and x6q dgrad (diagnostic)
+static inline bool cx_db_enabled() {
+  const char* e = getenv("DS2_CONV_X6_DB");
+  return !(e != nullptr && e[0] == '0');
+}
+
 static ds2_status_t launch_x6q(const float* dy, const float* w, float* dx, const ConvDims& g,
                                void* ws, hipStream_t st) {
   unsigned short* img = static_cast<unsigned short*>(ws);
@@ -1879,15 +2101,13 @@ static ds2_status_t launch_x6q(const float* dy, const float* w, float* dx, const
   const int gx = cdiv(g.wi, CX_COLS);
   const int64_t nwg = (int64_t)gx * g.hi * g.n * cdiv(g.ci, 32);
   if (nwg > 0x7fffffff) return DS2_UNSUPPORTED_SHAPE;
-  hipLaunchKernelGGL(conv_x6q_dgrad_kernel, dim3(static_cast<unsigned>(nwg)), dim3(CX_T), 0, st, dy,
-                     img, dx, g, gx, g.hi);
+  if (cx_db_enabled())
+    hipLaunchKernelGGL(conv_x6q_dgrad_kernel<true>, dim3(static_cast<unsigned>(nwg)), dim3(CX_T), 0, st,
+                       dy, img, dx, g, gx, g.hi);
+  else
+    hipLaunchKernelGGL(conv_x6q_dgrad_kernel<false>, dim3(static_cast<unsigned>(nwg)), dim3(CX_T), 0,
+                       st, dy, img, dx, g, gx, g.hi);
   return launch_status("ds2_conv2d_dgrad");
-}
-
-// DS2_CONV_X6_DB=0: the single-buffered conv2 forward (diagnostic)
-static inline bool cx_db_enabled() {
-  const char* e = getenv("DS2_CONV_X6_DB");
-  return !(e != nullptr && e[0] == '0');
 }
 
 static size_t x6_ws_bytes(const ConvDims& g, bool dgrad) {
@@ -1914,10 +2134,16 @@ static ds2_status_t launch_x6(const float* in, const float* w, const float* bias
   if (nwg > 0x7fffffff) return DS2_UNSUPPORTED_SHAPE;
   const dim3 grid(static_cast<unsigned>(nwg));
   const int nga = c.KA / 8;
-  const bool small = g.sw == 1 && c.RC == 1 && 3 * c.PCOL * c.P <= CX_PATCH1 && c.PCOL * nga <= 2 * CX_T;
+  bool small = g.sw == 1 && c.RC == 1 && 3 * c.PCOL * c.P <= CX_PATCH1 && c.PCOL * nga <= 2 * CX_T;
 #define DS2_CX(NG, NB, PU, SW, RCH)                                                          \
   hipLaunchKernelGGL((conv_x6_kernel<DGRAD, NG, NB, PU, SW, RCH>), grid, dim3(CX_T), 0, st, in, \
                      img, bias, out, g, out_lens, c, gx, gy)
+  // the compile-time-geometry instantiations must see the geometry cx_geom computed
+  const bool c36 = c.KA == CxConst<3, 6>::KA && c.P == CxConst<3, 6>::P &&
+                   c.COP == CxConst<3, 6>::COP && c.PCOL == CxConst<3, 6>::PCOL && c.NBP == 6;
+  const bool c26 = c.KA == CxConst<2, 6>::KA && c.P == CxConst<2, 6>::P &&
+                   c.COP == CxConst<2, 6>::COP && c.PCOL == CxConst<2, 6>::PCOL && c.NBP == 6;
+  small = small && (DGRAD ? c26 : c36);
   const bool db = small && 2 * 3 * c.PCOL * c.P <= CX_PATCH_DB && cx_db_enabled();
   if (small && !DGRAD && nga == 3 && c.NBP == 6 && db)
     hipLaunchKernelGGL((conv_x6_kernel<DGRAD, 3, 6, 2, 1, false, true>), grid, dim3(CX_T), 0, st,
@@ -2007,9 +2233,18 @@ static inline bool x6w_ok(const ConvDims& g) {
   return (int64_t)g.co * g.ho * g.wo * 4 < lim && (int64_t)g.ci * g.hi * g.wi * 4 < lim;
 }
 
+// DS2_CONV_X6W_SW=0: the per-row-restaging form (conv_x6_wgrad_kernel) for every shape
+static inline bool x6w_sw(const ConvDims& g) {
+  const char* e = getenv("DS2_CONV_X6W_SW");
+  if (e != nullptr && e[0] == '0') return false;
+  const int64_t R = (int64_t)g.n * ((g.wo + SW_COLS - 1) / SW_COLS) * g.ho;
+  return g.sh <= 2 && R < (1ll << 31) - 1;
+}
+
 static inline int x6w_splits(const ConvDims& g) {
   const int G = (g.kh + 3) / 4;
-  const int64_t R = (int64_t)g.n * g.ho;
+  const int64_t R = x6w_sw(g) ? (int64_t)g.n * ((g.wo + SW_COLS - 1) / SW_COLS) * g.ho
+                              : (int64_t)g.n * g.ho;
   int64_t S = CW_SLOTS / G;
   if (S < 1) S = 1;
   return static_cast<int>(S > R ? R : S);
@@ -2124,8 +2359,12 @@ ds2_status_t ds2_conv2d_wgrad(const float* dy, const float* x, float* dw, float*
   if (x6w_ok(g)) {
     slabs = x6w_splits(g);
     const int G = (kh + 3) / 4;
-    hipLaunchKernelGGL((conv_x6_wgrad_kernel<11, 3>), dim3(G * slabs), dim3(CW_T), 0, st, dy, x,
-                       partial, g, slabs);
+    if (x6w_sw(g))
+      hipLaunchKernelGGL((conv_x6_wgrad_sw_kernel<11, 3>), dim3(G * slabs), dim3(SW_T), 0, st, dy,
+                         x, partial, g, slabs);
+    else
+      hipLaunchKernelGGL((conv_x6_wgrad_kernel<11, 3>), dim3(G * slabs), dim3(CW_T), 0, st, dy, x,
+                         partial, g, slabs);
   } else if (pl.nt > 0) {
     dim3 grid(static_cast<unsigned>((int64_t)pl.bands * c_in * n * cdiv(c_out, 32)));
 #define DS2_WGP(NT_, XS_, SW_)                                                               \

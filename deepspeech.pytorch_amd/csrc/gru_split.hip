@@ -63,6 +63,37 @@ __device__ __forceinline__ f32x4 mma6(const Tri& a, const Tri& b, f32x4 c) {
   return c;
 }
 
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+
+// 4 fp32 -> their (hi, mid) bf16 terms packed as one 16-B run {hi01, hi23, mid01, mid23} and
+// their lo terms as one 8-B run (v_cvt_pk_bf16_f32, RNE: the terms split3 forms)
+__device__ __forceinline__ void split_pk4(const f32x4 v, u32x4& hm, u32x2& lo) {
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const float x0 = v[2 * q], x1 = v[2 * q + 1];
+    const unsigned h = __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2{x0, x1}, bf16x2v));
+    const float r0 = x0 - __builtin_bit_cast(float, h << 16);
+    const float r1 = x1 - __builtin_bit_cast(float, h & 0xffff0000u);
+    const unsigned m = __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2{r0, r1}, bf16x2v));
+    const float l0 = r0 - __builtin_bit_cast(float, m << 16);
+    const float l1 = r1 - __builtin_bit_cast(float, m & 0xffff0000u);
+    hm[q] = h;
+    hm[2 + q] = m;
+    lo[q] = __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2{l0, l1}, bf16x2v));
+  }
+}
+
+// the Tri of a 32-k pair from two pre-split tiles' runs (slots 0..3 tile a, 4..7 tile b)
+__device__ __forceinline__ Tri tri_of(const u32x4 ha, const u32x2 la, const u32x4 hb, const u32x2 lb) {
+  Tri t;
+  t.hi = __builtin_bit_cast(bf16x8, u32x4{ha[0], ha[1], hb[0], hb[1]});
+  t.mid = __builtin_bit_cast(bf16x8, u32x4{ha[2], ha[3], hb[2], hb[3]});
+  t.lo = __builtin_bit_cast(bf16x8, u32x4{la[0], la[1], lb[0], lb[1]});
+  return t;
+}
+
 // wave's contiguous share [p0, p0 + np) of `pairs` 32-k pairs
 __device__ __forceinline__ void pair_split(int pairs, int wave, int& p0, int& np) {
   p0 = (pairs * wave) / XW;
@@ -312,19 +343,27 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
 // per SIMD: the consumer-side splits are VALU work, and a lone wave issues VALU at half the
 // rate of two co-resident ones; 256 registers each, so the tiles stream through a window of
 // LW pairs in flight).
-template <int NP, int HM, int NW>
+// PRE: the producers publish their gate-gradient tiles pre-split (per lane a 16-B {hi, mid}
+// run and an 8-B lo run: 1.5 KB per tile instead of 1 KB of fp32), so the consumer loads
+// ready MFMA operands and does no split VALU (flag hand-off only).
+// dbp (nullable): per-unit bias-gradient partials as gru_bwd_dop_kernel's.
+template <int NP, int HM, int NW, bool PRE>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW / 4, NW / 4))) void gru_bwd_x6_kernel(
     int T, int N, int H, int D, int UB, int BT, const float* __restrict__ dy, int dyd,
     const float* __restrict__ w_f, const float* __restrict__ w_r,
     const float* __restrict__ h_all, const float* __restrict__ gates,
     const int* __restrict__ lens, float* __restrict__ dgx, float* __restrict__ dgh,
     float* __restrict__ gx, unsigned* __restrict__ counters, unsigned* __restrict__ err,
-    unsigned long long* __restrict__ stamps) {
+    unsigned long long* __restrict__ stamps, double* __restrict__ dbp) {
+  static_assert(!PRE || HM == 0, "pre-split tiles use the flag hand-off");
   constexpr int RP = GU + 1;
   constexpr bool SENT = HM == 1;
   constexpr int NSLOT = SENT ? kRingSlots : 2;
   constexpr int LW = NW == 4 ? NP : 3;          // pairs whose loads are in flight
-  __shared__ float red[NW * GB * RP];
+  constexpr int TF = PRE ? 384 : 256;           // ring floats per tile
+  constexpr int LWP = NW == 4 ? (NP < 12 ? NP : 12) : (NP < 5 ? NP : 5);   // PRE window
+  constexpr int RED = NW * GB * RP > 8 * GB * GU ? NW * GB * RP : 8 * GB * GU;
+  __shared__ __attribute__((aligned(8))) float red[RED];
   __shared__ __attribute__((aligned(16))) float tile[3 * GB * GU];
   __shared__ int flag;
   __shared__ int failed;
@@ -341,10 +380,10 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW / 4,
   const int t_first = 2 * p0;
   const unsigned* gflags = counters + (D * BT + 1) + (d * BT + bt) * UB;
   unsigned* myflag = counters + (D * BT + 1) + (d * BT + bt) * UB + ub;
-  const int slot_floats = D * BT * NB3 * 256;
+  const int slot_floats = D * BT * NB3 * TF;
   const __amdgpu_buffer_rsrc_t x_rs =
       __builtin_amdgcn_make_buffer_rsrc(gx, (short)0, NSLOT * slot_floats * 4, 0x00020000);
-  const int grp_off = (d * BT + bt) * NB3 * 256;
+  const int grp_off = (d * BT + bt) * NB3 * TF;
   if (threadIdx.x == 0) failed = 0;
   __syncthreads();
   // diagnostic timeline (DS2_GRU_STAMPS=2, scripts/trace_gru.py): s_memrealtime at step
@@ -387,6 +426,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW / 4,
   float dh_prev = 0.f, z_prev = 0.f;
   float px_dar = 0.f, px_daz = 0.f, px_dan = 0.f, px_dghn = 0.f;
   int64_t px_row = -1;
+  double sb_r = 0.0, sb_z = 0.0, sb_n = 0.0, sb_hn = 0.0;
   for (int s = 0; s < T; ++s) {
     const int t = d == 0 ? T - 1 - s : s;
     f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -409,6 +449,33 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW / 4,
         return;
       }
       trace_at(s, 1);
+      if constexpr (PRE) {
+        // LWP pairs' runs in flight, the next pair's issued as each pair is multiplied
+        const int tb0 = (((s - 1) & 1) * slot_floats + grp_off + t_first * TF) * 4;
+        u32x4 hm[2 * NP];
+        u32x2 lo[2 * NP];
+        auto load_run = [&](int i) {
+          const bool ok = i < 2 * np && t_first + i < NB3;
+          const int to = tb0 + i * TF * 4;
+          hm[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                x_rs, ok ? to + lane * 16 : 0x7ffffff0, 0, kSc1));
+          lo[i] = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(
+                                                x_rs, ok ? to + 1024 + lane * 8 : 0x7ffffff0, 0, kSc1));
+        };
+#pragma unroll
+        for (int i = 0; i < 2 * LWP; ++i) load_run(i);
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int p = 0; p < NP; ++p) {
+          if (p + LWP < NP) {
+            load_run(2 * (p + LWP));
+            load_run(2 * (p + LWP) + 1);
+          }
+          acc = mma6(tri_of(hm[2 * p], lo[2 * p], hm[2 * p + 1], lo[2 * p + 1]), w[p], acc);
+        }
+        trace_at(s, 2);
+      } else {
       const int base = (((s - 1) % NSLOT) * slot_floats + grp_off + t_first * 256 + lane * 4) * 4;
       f32x4 gv[2 * NP];
       auto load_tile = [&](int i) {
@@ -434,6 +501,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW / 4,
         acc = mma6(split3(gv[2 * p], gv[2 * p + 1]), w[p], acc);
       }
       trace_at(s, 2);
+      }
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r)
@@ -471,6 +539,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW / 4,
       dh_prev = dh;
       z_prev = zc;
       px_dar = dar; px_daz = daz; px_dan = dan; px_dghn = dghn; px_row = row;
+      sb_r += dar; sb_z += daz; sb_n += dan; sb_hn += dghn;
     }
     if (gate_thread) {
       tile[tpos] = dar;
@@ -495,6 +564,20 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW / 4,
 #pragma unroll
         for (int g = 0; g < 3; ++g)
           __builtin_amdgcn_raw_buffer_store_b128(sv, x_rs, sn + g * UB * 1024, 0, kSc1);
+      } else if constexpr (PRE) {
+        const int so = ((s & 1) * slot_floats + grp_off + ub * TF) * 4;
+#pragma unroll
+        for (int g = 0; g < 3; ++g) {
+          u32x4 hmv;
+          u32x2 lov;
+          split_pk4(*reinterpret_cast<const f32x4*>(tile + g * GB * GU + lane * 4), hmv, lov);
+          const int go = so + g * UB * TF * 4;
+          __builtin_amdgcn_raw_buffer_store_b128(hmv, x_rs, go + lane * 16, 0, kSc1);
+          __builtin_amdgcn_raw_buffer_store_b64(lov, x_rs, go + 1024 + lane * 8, 0, kSc1);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0)
+          __hip_atomic_store(myflag, (unsigned)s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       } else {
         const int so = (s & 1) * slot_floats * 4 + toff;
 #pragma unroll
@@ -519,6 +602,24 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW / 4,
       ghr[2 * H + j] = px_dghn;
     }
   }
+  if (dbp == nullptr) return;
+  // the workgroup's 16 samples summed per unit in sample order -> dbp[bt][d][4][H]
+  double* rd = reinterpret_cast<double*>(red);
+  __syncthreads();
+  if (gate_thread) {
+    rd[(0 * GB + m) * GU + u] = owner ? sb_r : 0.0;
+    rd[(1 * GB + m) * GU + u] = owner ? sb_z : 0.0;
+    rd[(2 * GB + m) * GU + u] = owner ? sb_n : 0.0;
+    rd[(3 * GB + m) * GU + u] = owner ? sb_hn : 0.0;
+  }
+  __syncthreads();
+  if (threadIdx.x < 4 * GU) {
+    const int g = threadIdx.x / GU, uu = threadIdx.x - (threadIdx.x / GU) * GU;
+    double a = 0.0;
+#pragma unroll
+    for (int mm = 0; mm < GB; ++mm) a += rd[(g * GB + mm) * GU + uu];
+    dbp[(((int64_t)bt * D + d) * 4 + g) * H + ub * GU + uu] = a;
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -533,9 +634,12 @@ static inline bool x6_enabled() {
   return !(e != nullptr && e[0] == '0');
 }
 
-static inline bool x6_bwd_enabled() {
+// DS2_GRU_X6_BWD: 1 = consumer-side splits, 2 = pre-split tiles (flag hand-off);
+// DS2_GRU_X6_BWD_WAVES=4: one wave per SIMD instead of two
+static inline int x6_bwd_mode() {
   const char* e = getenv("DS2_GRU_X6_BWD");
-  return x6_enabled() && e != nullptr && e[0] == '1';
+  if (!x6_enabled() || e == nullptr) return 0;
+  return e[0] == '1' ? 1 : (e[0] == '2' ? 2 : 0);
 }
 
 static const void* fwd_x6_fn(int need, int hm) {
@@ -553,12 +657,25 @@ static int x6_bwd_waves() {
   return (e != nullptr && e[0] == '4') ? 4 : 8;
 }
 
-static const void* bwd_x6_fn(int pairs, int hm, int nw) {
+static const void* bwd_x6_fn(int pairs, int hm, int nw, bool pre) {
   const int need = (pairs + nw - 1) / nw;
+  if (pre) {
+#define DS2_BP6(K, W) \
+    if (need <= K) return reinterpret_cast<const void*>(gru_bwd_x6_kernel<K, 0, W, true>);
+    if (nw == 4) {
+      DS2_BP6(1, 4) DS2_BP6(2, 4) DS2_BP6(4, 4) DS2_BP6(6, 4) DS2_BP6(8, 4) DS2_BP6(10, 4)
+      DS2_BP6(13, 4) DS2_BP6(16, 4) DS2_BP6(19, 4)
+    } else {
+      DS2_BP6(1, 8) DS2_BP6(2, 8) DS2_BP6(3, 8) DS2_BP6(4, 8) DS2_BP6(6, 8) DS2_BP6(8, 8)
+      DS2_BP6(10, 8) DS2_BP6(12, 8)
+    }
+#undef DS2_BP6
+    return nullptr;
+  }
 #define DS2_BX6(K, W)                                                                      \
   if (need <= K)                                                                           \
-    return hm == 1 ? reinterpret_cast<const void*>(gru_bwd_x6_kernel<K, 1, W>)            \
-                   : reinterpret_cast<const void*>(gru_bwd_x6_kernel<K, 0, W>);
+    return hm == 1 ? reinterpret_cast<const void*>(gru_bwd_x6_kernel<K, 1, W, false>)     \
+                   : reinterpret_cast<const void*>(gru_bwd_x6_kernel<K, 0, W, false>);
   if (nw == 4) {
     DS2_BX6(1, 4) DS2_BX6(2, 4) DS2_BX6(3, 4) DS2_BX6(4, 4) DS2_BX6(6, 4) DS2_BX6(8, 4)
     DS2_BX6(10, 4) DS2_BX6(13, 4) DS2_BX6(16, 4) DS2_BX6(19, 4)
@@ -593,17 +710,20 @@ bool launch_gru_bwd_x6(int hm, int t_max, int n, int h, int num_dirs, const floa
                        const float* w_hh_f, const float* w_hh_r, const float* h_all,
                        const float* gates, const int* lens, float* dgates_x, float* dgates_h,
                        float* ring, unsigned* ctrs, unsigned* err, unsigned long long* stamps,
-                       size_t lds_pad, hipStream_t st) {
-  if (!x6_bwd_enabled() || (h % GU) != 0) return false;
+                       double* dbp, size_t lds_pad, hipStream_t st) {
+  const int mode = x6_bwd_mode();
+  if (mode == 0 || (h % GU) != 0) return false;
+  const bool pre = mode == 2;
+  if (pre && hm != 0) return false;          // pre-split tiles: flag hand-off only
   apply_spin_limit_env();
   apply_rnn_tune_env();
   const int UB = h / GU, BT = (n + GB - 1) / GB;
   const int nw = x6_bwd_waves();
-  const void* fn = bwd_x6_fn((3 * UB + 1) / 2, hm == 1 ? 1 : 0, nw);
+  const void* fn = bwd_x6_fn((3 * UB + 1) / 2, hm == 1 ? 1 : 0, nw, pre);
   if (fn == nullptr) return false;
   int T_ = t_max, N_ = n, H_ = h, D_ = num_dirs, UB_ = UB, BT_ = BT, DYD_ = dy_dirs;
   void* args[] = {&T_, &N_, &H_, &D_, &UB_, &BT_, &dy, &DYD_, &w_hh_f, &w_hh_r, &h_all,
-                  &gates, &lens, &dgates_x, &dgates_h, &ring, &ctrs, &err, &stamps};
+                  &gates, &lens, &dgates_x, &dgates_h, &ring, &ctrs, &err, &stamps, &dbp};
   return rnn_launch(fn, dim3(mapped_grid(UB * num_dirs, BT)), dim3(nw * 64), args,
                                     lds_pad, st) == hipSuccess;
 }

@@ -217,6 +217,27 @@ def test_conv_x6_is_fp32_accurate(dev, monkeypatch):
     assert max(errs["1"]) < 5e-6, errs
 
 
+@pytest.mark.parametrize("cfg", [(2, 32, 81, 200, 32, 21, 11, 2, 1, 10, 5),
+                                 (3, 5, 30, 70, 20, 7, 11, 1, 1, 3, 5),
+                                 (4, 32, 81, 70, 32, 21, 11, 2, 1, 10, 5)])
+def test_conv_x6_wgrad_forms(dev, cfg, monkeypatch):
+    """The sliding-window bf16x6 weight gradient (default: sh new x rows per output row into a
+    6-slot ring) and the per-row-restaging form (DS2_CONV_X6W_SW=0) against fp64 torch: splits
+    that start mid-segment and segments of one row (4 x 70 columns = 3 chunks per row)."""
+    n, ci, h, w, co, kh, kw, sh, sw, ph, pw = cfg
+    g = torch.Generator().manual_seed(sum(cfg) + 1)
+    x = torch.randn(n, ci, h, w, generator=g, dtype=torch.float64)
+    wt = torch.randn(co, ci, kh, kw, generator=g, dtype=torch.float64) * 0.1
+    y = F.conv2d(x, wt, None, stride=(sh, sw), padding=(ph, pw))
+    dy = torch.randn(y.shape, generator=g, dtype=torch.float64)
+    dwr = torch.nn.grad.conv2d_weight(x, wt.shape, dy, stride=(sh, sw), padding=(ph, pw))
+    for form in ("1", "0"):
+        monkeypatch.setenv("DS2_CONV_X6W_SW", form)
+        dw, _ = ops.conv2d_wgrad(dy.float().to(dev), x.float().to(dev), tuple(wt.shape), (sh, sw),
+                                 (ph, pw), with_bias=False)
+        _close(dw, dwr, 1e-5, "conv wgrad form " + form)
+
+
 def test_conv1_x6_is_fp32_accurate(dev, monkeypatch):
     """The model's conv1 (1 -> 32 channels, 41 x 11 taps, stride (2, 2): three 16-row tap
     chunks, stride-2 patch columns) on the opt-in bf16x6 kernel (DS2_CONV_X6=2): error
@@ -561,11 +582,70 @@ def test_gru_dh_backward_matches_gate_exchange(dev, n, h, bidir, monkeypatch):
         _close(f, r, 2e-5, "dh backward after the fp32-MFMA forward (converted coefficients)")
 
 
-@pytest.mark.parametrize("bwd", ["dg", "dh"])
+@pytest.mark.parametrize("n,h,bidir", [(32, 800, True), (7, 48, False), (17, 784, True),
+                                       (33, 256, True)])
+def test_gru_presplit_backward(dev, n, h, bidir, monkeypatch):
+    """DS2_GRU_X6_BWD=2 (producers publish their gate-gradient tiles as pre-split bf16 runs,
+    consumers load ready MFMA operands) against the consumer-split bf16x6 backward: the same
+    terms in the same MFMA order, so bit-identical at either wave count; and against the
+    default fp32-MFMA backward within fp32 rounding."""
+    nd = 2 if bidir else 1
+    base = {"DS2_GRU_DOP": "1", "DS2_GRU_BWD": "dg", "DS2_RNN_HANDOFF": "flags"}
+    env = [dict(base, DS2_GRU_X6_BWD="0", DS2_GRU_X6_BWD_WAVES="8"),
+           dict(base, DS2_GRU_X6_BWD="1", DS2_GRU_X6_BWD_WAVES="8"),
+           dict(base, DS2_GRU_X6_BWD="2", DS2_GRU_X6_BWD_WAVES="8"),
+           dict(base, DS2_GRU_X6_BWD="1", DS2_GRU_X6_BWD_WAVES="4"),
+           dict(base, DS2_GRU_X6_BWD="2", DS2_GRU_X6_BWD_WAVES="4")]
+    ref, c8, p8, c4, p4 = _gru_run(dev, n, 37, 40, h, nd, h + 13 * n, env, monkeypatch)
+    for r, a8, b8, a4, b4 in zip(ref, c8, p8, c4, p4):
+        assert torch.isfinite(b8).all() and torch.isfinite(b4).all()
+        assert torch.equal(a8, b8) and torch.equal(a4, b4)
+        _close(b8, r, 2e-5, "pre-split x6 vs fp32-MFMA backward")
+        _close(b4, r, 2e-5, "pre-split x6 (4 waves) vs fp32-MFMA backward")
+
+
+@pytest.mark.parametrize("n,h,bidir", [(32, 800, True), (7, 48, False), (17, 784, True)])
+def test_gru_progressive_backward(dev, n, h, bidir, monkeypatch):
+    """DS2_RNN_HANDOFF_BWD=progressive (every wave polls the group's flags itself and loads a
+    producer's tiles as soon as that producer has published) against the default flag hand-off:
+    the same tiles multiplied in the same order, so bit-identical; a forced hand-off timeout in
+    the backward alone surfaces as a hand-off error."""
+    nd = 2 if bidir else 1
+    base = {"DS2_GRU_DOP": "1", "DS2_GRU_BWD": "dg", "DS2_GRU_X6_BWD": "0", "DS2_RNN_HANDOFF": ""}
+    env = [dict(base, DS2_RNN_HANDOFF_BWD="flags"), dict(base, DS2_RNN_HANDOFF_BWD="progressive")]
+    ref, prog = _gru_run(dev, n, 37, 40, h, nd, h + 17 * n, env, monkeypatch)
+    for r, p_ in zip(ref, prog):
+        assert torch.isfinite(p_).all()
+        assert torch.equal(r, p_)
+    # timeout in the progressive wait: forward with the normal bound, backward with bound 0
+    g = torch.Generator().manual_seed(5)
+    t = 23
+    weights = [torch.rand(sz, generator=g) * 0.2 - 0.1 for sz in
+               [(3 * h, 40), (3 * h, h), (3 * h,), (3 * h,)] * nd]
+    lens = torch.full((n,), t, dtype=torch.int32, device=dev)
+    ws = [w.to(dev).requires_grad_(True) for w in weights]
+    xd = torch.randn(t, n, 40, generator=g).to(dev).requires_grad_(True)
+    ops.rnn_status_word(dev).zero_()
+    y = ops.GRULayerFn.apply(xd, lens, True, h, *ws)
+    torch.cuda.synchronize()
+    ops.check_rnn_status(dev)
+    monkeypatch.setenv("DS2_RNN_SPIN_LIMIT", "0")
+    y.backward(torch.ones_like(y))
+    torch.cuda.synchronize()
+    with pytest.raises(_lib.Ds2Error, match="hand-off"):
+        ops.check_rnn_status(dev)
+    monkeypatch.delenv("DS2_RNN_SPIN_LIMIT")
+    ops.rnn_status_word(dev).zero_()
+
+
+@pytest.mark.parametrize("bwd", ["dg", "dh", "x6p"])
 def test_gru_backward_full_length_vs_torch(dev, bwd, monkeypatch):
     """The cfg2 recurrence shape (bs 32, H 800, both directions) over 201 steps with ragged
-    lengths: the default gate-exchange and the opt-in dh-exchange backward against torch's
-    nn.GRU in fp64."""
+    lengths: the default gate-exchange, the opt-in dh-exchange and the pre-split bf16x6
+    backward against torch's nn.GRU in fp64."""
+    if bwd == "x6p":
+        monkeypatch.setenv("DS2_GRU_X6_BWD", "2")
+        bwd = "dg"
     monkeypatch.setenv("DS2_GRU_BWD", bwd)
     n, t, inp, h = 32, 201, 64, 800
     g = torch.Generator().manual_seed(3)
