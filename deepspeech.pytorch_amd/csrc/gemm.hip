@@ -847,7 +847,6 @@ __global__ __launch_bounds__(256, 2) void sxgemm_kernel(
 constexpr int X2M = 256;                 // tile rows
 constexpr int X2T = 512;                 // threads
 constexpr int X2_AP = X2M * XS;          // bf16 per A plane
-constexpr int X2_BP = 128 * XS;          // bf16 per B plane
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
@@ -916,23 +915,33 @@ __device__ __forceinline__ void x2_split2(float x0, float x1, unsigned& h, unsig
   l = __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2{l0, l1}, bf16x2));
 }
 
+// NPL 3: the hi / mid / lo planes; NPL 1: the bf16 (RNE) rounding alone (the bf16-operand GEMM)
+template <int NPL = 3>
 __device__ __forceinline__ void x2_split_store(unsigned short* __restrict__ s, int plane, int at,
                                                const float* v) {
-  u32x4v h, m, l;
+  if constexpr (NPL == 1) {
+    u32x4v h;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    unsigned a, b, c;
-    x2_split2(v[2 * j], v[2 * j + 1], a, b, c);
-    h[j] = a;
-    m[j] = b;
-    l[j] = c;
+    for (int j = 0; j < 4; ++j)
+      h[j] = __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2{v[2 * j], v[2 * j + 1]}, bf16x2));
+    *reinterpret_cast<u32x4v*>(s + at) = h;
+  } else {
+    u32x4v h, m, l;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      unsigned a, b, c;
+      x2_split2(v[2 * j], v[2 * j + 1], a, b, c);
+      h[j] = a;
+      m[j] = b;
+      l[j] = c;
+    }
+    *reinterpret_cast<u32x4v*>(s + at) = h;
+    *reinterpret_cast<u32x4v*>(s + plane + at) = m;
+    *reinterpret_cast<u32x4v*>(s + 2 * plane + at) = l;
   }
-  *reinterpret_cast<u32x4v*>(s + at) = h;
-  *reinterpret_cast<u32x4v*>(s + plane + at) = m;
-  *reinterpret_cast<u32x4v*>(s + 2 * plane + at) = l;
 }
 
-template <bool KC, int ROWS>
+template <bool KC, int ROWS, int NPL = 3>
 __device__ __forceinline__ void x2_store(unsigned short* __restrict__ s,
                                          const float (&v)[X2Op<KC, ROWS>::F]) {
   using O = X2Op<KC, ROWS>;
@@ -941,12 +950,13 @@ __device__ __forceinline__ void x2_store(unsigned short* __restrict__ s,
 #pragma unroll
     for (int u = 0; u < O::SL; ++u) {
       const int unit = t + X2T * u;
-      x2_split_store(s, O::P, xslot(unit >> 2, unit & 3), v + 8 * u);
+      x2_split_store<NPL>(s, O::P, xslot(unit >> 2, unit & 3), v + 8 * u);
     }
   } else {
     const int r = t % ROWS;
 #pragma unroll
-    for (int u = 0; u < O::SL; ++u) x2_split_store(s, O::P, xslot(r, O::SL * (t / ROWS) + u), v + 8 * u);
+    for (int u = 0; u < O::SL; ++u)
+      x2_split_store<NPL>(s, O::P, xslot(r, O::SL * (t / ROWS) + u), v + 8 * u);
   }
 }
 
@@ -1005,20 +1015,23 @@ __device__ __forceinline__ void x2_load160(__amdgpu_buffer_rsrc_t rs, int ld, co
   }
 }
 
-template <bool KC>
+template <bool KC, int NPL = 3>
 __device__ __forceinline__ void x2_store160(unsigned short* __restrict__ s, const float (&v)[16]) {
   constexpr int P = 160 * XS;
   const int t = threadIdx.x;
   if (KC) {
-    x2_split_store(s, P, xslot(t >> 2, t & 3), v);
-    if (t < 128) x2_split_store(s, P, xslot((t + X2T) >> 2, (t + X2T) & 3), v + 8);
+    x2_split_store<NPL>(s, P, xslot(t >> 2, t & 3), v);
+    if (t < 128) x2_split_store<NPL>(s, P, xslot((t + X2T) >> 2, (t + X2T) & 3), v + 8);
   } else {
-    x2_split_store(s, P, xslot(t & 127, t >> 7), v);
-    if (t < 128) x2_split_store(s, P, xslot(128 + (t & 31), (t >> 5) & 3), v + 8);
+    x2_split_store<NPL>(s, P, xslot(t & 127, t >> 7), v);
+    if (t < 128) x2_split_store<NPL>(s, P, xslot(128 + (t & 31), (t >> 5) & 3), v + 8);
   }
 }
 
-template <int TA, int TB, bool KCHK, int TBN>
+// NPL 3: the bf16x6 fp32-accurate GEMM; NPL 1: the bf16-operand GEMM (operands rounded to
+// bf16 while staged, one product per fragment pair, fp32 accumulation -- cfg4's opt-in
+// precision), one LDS plane per operand
+template <int TA, int TB, bool KCHK, int TBN, int NPL = 3>
 __global__ __launch_bounds__(X2T, 1) void sxgemm2_kernel(
     int M, int N, int K, float alpha, const float* __restrict__ A, int64_t lda, int64_t sA,
     const float* __restrict__ B, int64_t ldb, int64_t sB, float beta, float* __restrict__ C,
@@ -1032,8 +1045,9 @@ __global__ __launch_bounds__(X2T, 1) void sxgemm2_kernel(
   constexpr int BP = TBN * XS;             // bf16 per B plane
   constexpr int BF = TBN == 128 ? 8 : 16;  // B floats per thread per stage
   using OA = X2Op<AK, X2M>;
-  __shared__ __attribute__((aligned(16))) unsigned short As[2][3 * X2_AP];
-  __shared__ __attribute__((aligned(16))) unsigned short Bs[2][3 * BP];
+  static_assert(NPL == 1 || NPL == 3, "planes");
+  __shared__ __attribute__((aligned(16))) unsigned short As[2][NPL * X2_AP];
+  __shared__ __attribute__((aligned(16))) unsigned short Bs[2][NPL * BP];
 
   int m0, n0, kbeg, kend, bz;
   float* part;
@@ -1113,9 +1127,9 @@ __global__ __launch_bounds__(X2T, 1) void sxgemm2_kernel(
   };
   auto bstore = [&](unsigned short* dst, const float (&vb)[BF]) {
     if constexpr (TBN == 128)
-      x2_store<BKc, TBN>(dst, vb);
+      x2_store<BKc, TBN, NPL>(dst, vb);
     else
-      x2_store160<BKc>(dst, vb);
+      x2_store160<BKc, NPL>(dst, vb);
   };
   auto body = [&](int kt, int cur, float (&la)[OA::F], float (&lb)[BF],
                   const float (&sa)[OA::F], const float (&sb)[BF]) {
@@ -1124,8 +1138,8 @@ __global__ __launch_bounds__(X2T, 1) void sxgemm2_kernel(
     load(kbeg + (kt + 2) * XS, la, lb);          // stages past kend load as zeros
     const unsigned short* as = As[cur];
     const unsigned short* bs = Bs[cur];
-    constexpr int NMF = WMT * WNT * 6;         // MFMAs per k-step
-    constexpr int NRD = (WMT + WNT) * 3;       // fragment reads per k-step
+    constexpr int NMF = WMT * WNT * (NPL == 3 ? 6 : 1);   // MFMAs per k-step
+    constexpr int NRD = (WMT + WNT) * NPL;                 // fragment reads per k-step
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       bf16x8 af[WMT][3], bfr[WNT][3];
@@ -1133,21 +1147,26 @@ __global__ __launch_bounds__(X2T, 1) void sxgemm2_kernel(
       for (int i = 0; i < WMT; ++i) {
         const int at = xslot(wm + 32 * i + fr, 2 * ks + fk);
 #pragma unroll
-        for (int p = 0; p < 3; ++p) af[i][p] = *reinterpret_cast<const bf16x8*>(as + p * X2_AP + at);
+        for (int p = 0; p < NPL; ++p) af[i][p] = *reinterpret_cast<const bf16x8*>(as + p * X2_AP + at);
       }
 #pragma unroll
       for (int j = 0; j < WNT; ++j) {
         const int bt = xslot(wn + 32 * j + fr, 2 * ks + fk);
 #pragma unroll
-        for (int p = 0; p < 3; ++p) bfr[j][p] = *reinterpret_cast<const bf16x8*>(bs + p * BP + bt);
+        for (int p = 0; p < NPL; ++p) bfr[j][p] = *reinterpret_cast<const bf16x8*>(bs + p * BP + bt);
       }
 #pragma unroll
       for (int i = 0; i < WMT; ++i)
 #pragma unroll
-        for (int j = 0; j < WNT; ++j) x2_mma6(af[i], bfr[j], acc[i][j]);
+        for (int j = 0; j < WNT; ++j) {
+          if constexpr (NPL == 3)
+            x2_mma6(af[i], bfr[j], acc[i][j]);
+          else
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][0], bfr[j][0], acc[i][j], 0, 0, 0);
+        }
     }
     // stage kt + 1 -> the other buffer (a stage past the end writes zeros nobody reads)
-    x2_store<AK, X2M>(As[cur ^ 1], sa);
+    x2_store<AK, X2M, NPL>(As[cur ^ 1], sa);
     bstore(Bs[cur ^ 1], sb);
     // schedule: the loads, the first k-step's fragments, then each MFMA followed by up to
     // three VALU (the split of the next stage), the second k-step's fragments early, the
@@ -1169,7 +1188,7 @@ __global__ __launch_bounds__(X2T, 1) void sxgemm2_kernel(
   };
   const int ktiles = (kend - kbeg + XS - 1) / XS;
   load(kbeg, ra0, rb0);
-  x2_store<AK, X2M>(As[0], ra0);
+  x2_store<AK, X2M, NPL>(As[0], ra0);
   bstore(Bs[0], rb0);
   load(kbeg + XS, ra1, rb1);
   for (int kt = 0; kt < ktiles; kt += 2) {
@@ -1511,9 +1530,18 @@ extern "C" ds2_status_t ds2_sgemm_ws(int trans_a, int trans_b, int m, int n, int
 // bf16-operand GEMM (sbgemm_kernel): same contract as ds2_sgemm_ws; every operand must be
 // float4-staged (16-B aligned, ld and the contiguous extent multiples of 4) and span
 // < 2^31 bytes, else DS2_UNSUPPORTED_SHAPE (no silent fp32 fallback).
+// The bf16-operand GEMM runs on sxgemm2_kernel with one plane (NPL 1: 256-row tiles, one
+// workgroup per CU, 32x32x16 MFMAs from one LDS image per operand); DS2_GEMM_BF16_X2=0
+// selects the older sbgemm_kernel (128 x 128, 16x16x32).
+static bool bf16_x2_enabled() {
+  const char* e = getenv("DS2_GEMM_BF16_X2");
+  return !(e != nullptr && e[0] == '0');
+}
+
 extern "C" size_t ds2_sgemm_bf16_workspace_size(int m, int n, int k, int batch) {
   if (m <= 0 || n <= 0 || k <= 0 || batch <= 0) return 0;
-  return plan_ws(plan_bn(m, n, k, batch, 128, 2 * device_cus(), KB16, 1.0).p, batch);
+  return std::max(plan_ws(plan_bn(m, n, k, batch, 128, 2 * device_cus(), KB16, 1.0).p, batch),
+                  plan_ws(x6_plan(m, n, k, batch, 1), batch));
 }
 
 extern "C" ds2_status_t ds2_sgemm_bf16_ws(int trans_a, int trans_b, int m, int n, int k,
@@ -1534,7 +1562,9 @@ extern "C" ds2_status_t ds2_sgemm_bf16_ws(int trans_a, int trans_b, int m, int n
                   (trans_b ? (k % 4 == 0) : (n % 4 == 0));
   if (!va || !vb || !fits_rsrc(trans_a ? k : m, lda) || !fits_rsrc(trans_b ? n : k, ldb))
     return DS2_UNSUPPORTED_SHAPE;
-  GemmPlan p = plan_bn(m, n, k, batch, 128, 2 * device_cus(), KB16, 1.0).p;
+  const bool x2 = bf16_x2_enabled();
+  GemmPlan p = x2 ? x6_plan(m, n, k, batch, 1)
+                  : plan_bn(m, n, k, batch, 128, 2 * device_cus(), KB16, 1.0).p;
   if (p.nsplit > 1 && (ws == nullptr || ws_bytes < plan_ws(p, batch))) {
     p.nsplit = 1;
     p.kchunk = std::max(k, 1);
@@ -1544,10 +1574,28 @@ extern "C" ds2_status_t ds2_sgemm_bf16_ws(int trans_a, int trans_b, int m, int n
   if (nwg > 0x7fffffff) return DS2_UNSUPPORTED_SHAPE;
   dim3 grid(static_cast<unsigned>(nwg));
   hipStream_t st = as_stream(stream);
+  const bool kalign = k % XS == 0 && (p.nsplit == 1 || p.kchunk % XS == 0);
 #define DS2_B(TA_, TB_)                                                                        \
-  hipLaunchKernelGGL((sbgemm_kernel<TA_, TB_>), grid, dim3(256), 0, st, m, n, k, alpha, a, lda, \
-                     stride_a, b, ldb, stride_b, beta, c, ldc, stride_c, bias, p.main_wgs,      \
-                     p.tail_tile0, p.tail_tiles, p.nsplit, p.kchunk, partial)
+  if (x2 && kalign && p.bn == 160)                                                             \
+    hipLaunchKernelGGL((sxgemm2_kernel<TA_, TB_, false, 160, 1>), grid, dim3(X2T), 0, st, m, n, \
+                       k, alpha, a, lda, stride_a, b, ldb, stride_b, beta, c, ldc, stride_c, bias, \
+                       p.main_wgs, p.tail_tile0, p.tail_tiles, p.nsplit, p.kchunk, partial);    \
+  else if (x2 && p.bn == 160)                                                                  \
+    hipLaunchKernelGGL((sxgemm2_kernel<TA_, TB_, true, 160, 1>), grid, dim3(X2T), 0, st, m, n,  \
+                       k, alpha, a, lda, stride_a, b, ldb, stride_b, beta, c, ldc, stride_c, bias, \
+                       p.main_wgs, p.tail_tile0, p.tail_tiles, p.nsplit, p.kchunk, partial);    \
+  else if (x2 && kalign)                                                                       \
+    hipLaunchKernelGGL((sxgemm2_kernel<TA_, TB_, false, 128, 1>), grid, dim3(X2T), 0, st, m, n, \
+                       k, alpha, a, lda, stride_a, b, ldb, stride_b, beta, c, ldc, stride_c, bias, \
+                       p.main_wgs, p.tail_tile0, p.tail_tiles, p.nsplit, p.kchunk, partial);    \
+  else if (x2)                                                                                 \
+    hipLaunchKernelGGL((sxgemm2_kernel<TA_, TB_, true, 128, 1>), grid, dim3(X2T), 0, st, m, n,  \
+                       k, alpha, a, lda, stride_a, b, ldb, stride_b, beta, c, ldc, stride_c, bias, \
+                       p.main_wgs, p.tail_tile0, p.tail_tiles, p.nsplit, p.kchunk, partial);    \
+  else                                                                                         \
+    hipLaunchKernelGGL((sbgemm_kernel<TA_, TB_>), grid, dim3(256), 0, st, m, n, k, alpha, a, lda, \
+                       stride_a, b, ldb, stride_b, beta, c, ldc, stride_c, bias, p.main_wgs,    \
+                       p.tail_tile0, p.tail_tiles, p.nsplit, p.kchunk, partial)
   if (!trans_a && !trans_b) DS2_B(0, 0);
   else if (!trans_a && trans_b) DS2_B(0, 1);
   else if (trans_a && !trans_b) DS2_B(1, 0);

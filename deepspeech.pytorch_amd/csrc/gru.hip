@@ -866,13 +866,12 @@ __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   const int slot_floats = D * BT * NB3 * 256;
   constexpr bool SENT = HM == 1 || HM == 2;   // sentinel ring: tiles validate themselves
   constexpr bool FLAG = HM == 0 || HM == 2;   // per-producer flags polled before loading
-  constexpr bool PROG = HM == 3;              // per-tile flag waits (progressive)
   constexpr int NSLOT = SENT ? kRingSlots : 2;
   const __amdgpu_buffer_rsrc_t x_rs =
       __builtin_amdgcn_make_buffer_rsrc(gx, (short)0, NSLOT * slot_floats * 4, 0x00020000);
   const int grp_off = (d * BT + bt) * NB3 * 256;
   __shared__ int failed;
-  if (SENT || PROG) {
+  if (SENT) {
     if (threadIdx.x == 0) failed = 0;
     __syncthreads();
   }
@@ -937,47 +936,10 @@ __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
       const int base = (((s - 1) % NSLOT) * slot_floats + grp_off + b0 * 256 + lane * 4) * 4;
       if (HM == 1) sleep_units(g_rnn_tune[2]);
       f32x4 gv[NBW];
-      if constexpr (PROG) {
-        // every wave polls the group's flags itself and issues each tile's load as soon as ITS
-        // producer has published (tile b of the 3 UB comes from unit block b mod UB), so the
-        // loads of early producers' tiles overlap the wait for late ones; the products still
-        // run in tile order.  Each load follows this wave's own matching poll (row 1 of the
-        // valid hand-off forms).
-        unsigned long long rdy = 0ull;
-        bool ok = g_spin_limit != 0;
-        unsigned spins = 0;
-        auto poll = [&]() {
-          const unsigned v = lane < UB ? __hip_atomic_load(gflags + lane, __ATOMIC_RELAXED,
-                                                           __HIP_MEMORY_SCOPE_AGENT)
-                                       : (unsigned)s;
-          rdy = __ballot(v >= (unsigned)s);
-        };
-        if (ok) poll();
-#pragma unroll
-        for (int i = 0; i < NBW; ++i) {
-          if (i < nb) {
-            int prod = b0 + i;
-            prod -= prod >= UB ? UB : 0;
-            prod -= prod >= UB ? UB : 0;
-            while (ok && ((rdy >> prod) & 1ull) == 0ull) {
-              __builtin_amdgcn_s_sleep(1);
-              if (++spins > g_spin_limit) ok = false;
-              else poll();
-            }
-          }
-          const int off = (ok && i < nb) ? base + i * 1024 : 0x7ffffff0;
-          gv[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(x_rs, off, 0, kSc1));
-        }
-        if (!ok && lane == 0) {
-          __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          failed = 1;
-        }
-      } else {
 #pragma unroll
       for (int i = 0; i < NBW; ++i) {
         const int off = i < nb ? base + i * 1024 : 0x7ffffff0;
         gv[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(x_rs, off, 0, kSc1));
-      }
       }
       asm volatile("" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
@@ -1039,7 +1001,7 @@ __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     settle(g_hn);
     settle(hp);
     __syncthreads();
-    if ((SENT || PROG) && failed) {
+    if (SENT && failed) {
       poison_rest(dgx, s, T, d == 0, N, D, n, d, H, j, H3, 3, owner);
       return;
     }
@@ -1415,7 +1377,7 @@ static inline int handoff_mode(bool fwd) {
   const char* e = getenv(fwd ? "DS2_RNN_HANDOFF_FWD" : "DS2_RNN_HANDOFF_BWD");
   if (e == nullptr || e[0] == 0) e = getenv("DS2_RNN_HANDOFF");
   if (e == nullptr || e[0] == 0) return fwd ? 1 : 0;
-  return e[0] == 's' ? 1 : (e[0] == 'h' ? 2 : (e[0] == 'p' && !fwd ? 3 : 0));
+  return e[0] == 's' ? 1 : (e[0] == 'h' ? 2 : 0);
 }
 static const void* bwd_dop_fn(int need) {
   const int hm = handoff_mode(false);
@@ -1423,7 +1385,6 @@ static const void* bwd_dop_fn(int need) {
   if (need <= K)                                                                         \
     return hm == 1 ? reinterpret_cast<const void*>(gru_bwd_dop_kernel<K, 1>)             \
          : hm == 2 ? reinterpret_cast<const void*>(gru_bwd_dop_kernel<K, 2>)             \
-         : hm == 3 ? reinterpret_cast<const void*>(gru_bwd_dop_kernel<K, 3>)             \
                    : reinterpret_cast<const void*>(gru_bwd_dop_kernel<K, 0>);
   DS2_BDOP(1) DS2_BDOP(2) DS2_BDOP(3) DS2_BDOP(4) DS2_BDOP(6) DS2_BDOP(8) DS2_BDOP(10)
   DS2_BDOP(13) DS2_BDOP(16) DS2_BDOP(19) DS2_BDOP(22) DS2_BDOP(24)

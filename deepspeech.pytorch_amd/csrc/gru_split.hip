@@ -626,19 +626,23 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW / 4,
 // host launchers (called by ds2_gru_fwd / ds2_gru_bwd in gru.hip with their workspace
 // carve-up); false = shape not covered (caller falls back to the fp32-MFMA kernels)
 
-// forward: on by default (DS2_GRU_X6=0 selects the fp32-MFMA kernel).  backward: opt-in
-// (DS2_GRU_X6_BWD=1): its consumer-side splits of 3H-wide gate gradients make it VALU-bound
-// after the flag wait (6.5 vs 6.2 us per step for the fp32-MFMA kernel at cfg2).
+// forward: on by default (DS2_GRU_X6=0 selects the fp32-MFMA kernel).  backward: the
+// pre-split form by default (cfg2: 6.13 / 6.22 vs 6.29 / 6.27 us per step for the fp32-MFMA
+// kernel, alternating runs on one box); the consumer-side splits of 3H-wide gate gradients
+// made the first x6 backward VALU-bound after the flag wait (6.5 vs 6.2), and one wave per
+// SIMD with every pre-split run in flight measured 7.1.
 static inline bool x6_enabled() {
   const char* e = getenv("DS2_GRU_X6");
   return !(e != nullptr && e[0] == '0');
 }
 
-// DS2_GRU_X6_BWD: 1 = consumer-side splits, 2 = pre-split tiles (flag hand-off);
+// DS2_GRU_X6_BWD: 2 (default) = pre-split tiles (flag hand-off; the sentinel forms keep the
+// fp32-MFMA kernel), 1 = consumer-side splits, 0 = the fp32-MFMA kernel (gru.hip);
 // DS2_GRU_X6_BWD_WAVES=4: one wave per SIMD instead of two
 static inline int x6_bwd_mode() {
   const char* e = getenv("DS2_GRU_X6_BWD");
-  if (!x6_enabled() || e == nullptr) return 0;
+  if (!x6_enabled()) return 0;
+  if (e == nullptr || e[0] == 0) return 2;
   return e[0] == '1' ? 1 : (e[0] == '2' ? 2 : 0);
 }
 

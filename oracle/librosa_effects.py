@@ -44,21 +44,41 @@ def stft(y: np.ndarray, n_fft: int = N_FFT, hop: int = HOP) -> np.ndarray:
     return np.fft.fft(frames, axis=0)[:1 + n_fft // 2].astype(np.complex64)
 
 
+# numpy's float32 np.abs / np.angle / np.exp(1j * x) of a complex64 are platform-dependent in
+# their last bits (libm hypotf / atan2f / sincosf, or SVML-based SIMD loops on AVX-512 hosts),
+# and the vocoder's float32 phase accumulator (which grows to ~1e4 rad in the high bins) turns a
+# one-ulp difference of an angle into a visibly different rounding.  The restatement fixes them
+# to their correctly rounded values (evaluated in float64, rounded once to float32).
+def _absf(c: np.ndarray) -> np.ndarray:
+    re, im = c.real.astype(np.float64), c.imag.astype(np.float64)
+    return np.sqrt(re * re + im * im).astype(np.float32)
+
+
+def _anglef(c: np.ndarray) -> np.ndarray:
+    return np.arctan2(c.imag.astype(np.float64), c.real.astype(np.float64)).astype(np.float32)
+
+
+def _expjf(x: np.ndarray) -> np.ndarray:
+    xd = x.astype(np.float64)
+    return (np.cos(xd).astype(np.float32) + 1j * np.sin(xd).astype(np.float32)).astype(np.complex64)
+
+
 def phase_vocoder(D: np.ndarray, rate: float, hop: int = HOP) -> np.ndarray:
     """librosa.phase_vocoder(D, rate) (0.8)."""
     time_steps = np.arange(0, D.shape[1], rate, dtype=np.float64)
     out = np.zeros((D.shape[0], len(time_steps)), D.dtype, order='F')
     phi_advance = np.linspace(0, np.pi * hop, D.shape[0])
-    phase_acc = np.angle(D[:, 0])                      # float32 for complex64 D
+    phase_acc = _anglef(D[:, 0])                       # float32 for complex64 D
     D = np.pad(D, [(0, 0), (0, 2)], mode='constant')
     for t, step in enumerate(time_steps):
         cols = D[:, int(step):int(step + 2)]
         alpha = np.mod(step, 1.0)
         # numpy 1.x (the reference's era) value-based casting: the float64 scalars (1 - alpha),
         # alpha meet the float32 magnitudes in float32; stated explicitly so numpy 2 agrees
-        mag = np.float32(1.0 - alpha) * np.abs(cols[:, 0]) + np.float32(alpha) * np.abs(cols[:, 1])
-        out[:, t] = mag * np.exp(1.j * phase_acc)
-        dphase = np.angle(cols[:, 1]) - np.angle(cols[:, 0]) - phi_advance
+        mag = np.float32(1.0 - alpha) * _absf(cols[:, 0]) + np.float32(alpha) * _absf(cols[:, 1])
+        e = _expjf(phase_acc)                          # complex64 (cos, sin) of the float32 phase
+        out[:, t] = (mag * e.real).astype(np.float32) + 1j * (mag * e.imag).astype(np.float32)
+        dphase = (_anglef(cols[:, 1]) - _anglef(cols[:, 0])) - phi_advance
         dphase = dphase - 2.0 * np.pi * np.round(dphase / (2.0 * np.pi))
         phase_acc += phi_advance + dphase
     return out

@@ -451,6 +451,7 @@ def test_gru_reduce_scatter_backward(dev, n, h, bidir, monkeypatch):
     x = torch.randn(t, n, inp, generator=g)
     dy = torch.randn(t, n, h, generator=g)
     outs = []
+    monkeypatch.setenv("DS2_GRU_X6_BWD", "0")
     for rs in ("0", "1"):
         monkeypatch.setenv("DS2_GRU_BWD_RS", rs)
         ws = [w.to(dev).requires_grad_(True) for w in weights]
@@ -482,6 +483,7 @@ def test_gru_handoff_forms_agree(dev, n, h, bidir, monkeypatch):
     dy = torch.randn(t, n, h, generator=g)
     outs = []
     monkeypatch.setenv("DS2_GRU_DOP", "1")
+    monkeypatch.setenv("DS2_GRU_X6_BWD", "0")   # the fp32-MFMA backward has all three forms
     for mode in ("flags", "sentinel", "hybrid"):
         monkeypatch.setenv("DS2_RNN_HANDOFF", mode)
         ws = [w.to(dev).requires_grad_(True) for w in weights]
@@ -604,47 +606,13 @@ def test_gru_presplit_backward(dev, n, h, bidir, monkeypatch):
         _close(b4, r, 2e-5, "pre-split x6 (4 waves) vs fp32-MFMA backward")
 
 
-@pytest.mark.parametrize("n,h,bidir", [(32, 800, True), (7, 48, False), (17, 784, True)])
-def test_gru_progressive_backward(dev, n, h, bidir, monkeypatch):
-    """DS2_RNN_HANDOFF_BWD=progressive (every wave polls the group's flags itself and loads a
-    producer's tiles as soon as that producer has published) against the default flag hand-off:
-    the same tiles multiplied in the same order, so bit-identical; a forced hand-off timeout in
-    the backward alone surfaces as a hand-off error."""
-    nd = 2 if bidir else 1
-    base = {"DS2_GRU_DOP": "1", "DS2_GRU_BWD": "dg", "DS2_GRU_X6_BWD": "0", "DS2_RNN_HANDOFF": ""}
-    env = [dict(base, DS2_RNN_HANDOFF_BWD="flags"), dict(base, DS2_RNN_HANDOFF_BWD="progressive")]
-    ref, prog = _gru_run(dev, n, 37, 40, h, nd, h + 17 * n, env, monkeypatch)
-    for r, p_ in zip(ref, prog):
-        assert torch.isfinite(p_).all()
-        assert torch.equal(r, p_)
-    # timeout in the progressive wait: forward with the normal bound, backward with bound 0
-    g = torch.Generator().manual_seed(5)
-    t = 23
-    weights = [torch.rand(sz, generator=g) * 0.2 - 0.1 for sz in
-               [(3 * h, 40), (3 * h, h), (3 * h,), (3 * h,)] * nd]
-    lens = torch.full((n,), t, dtype=torch.int32, device=dev)
-    ws = [w.to(dev).requires_grad_(True) for w in weights]
-    xd = torch.randn(t, n, 40, generator=g).to(dev).requires_grad_(True)
-    ops.rnn_status_word(dev).zero_()
-    y = ops.GRULayerFn.apply(xd, lens, True, h, *ws)
-    torch.cuda.synchronize()
-    ops.check_rnn_status(dev)
-    monkeypatch.setenv("DS2_RNN_SPIN_LIMIT", "0")
-    y.backward(torch.ones_like(y))
-    torch.cuda.synchronize()
-    with pytest.raises(_lib.Ds2Error, match="hand-off"):
-        ops.check_rnn_status(dev)
-    monkeypatch.delenv("DS2_RNN_SPIN_LIMIT")
-    ops.rnn_status_word(dev).zero_()
-
-
-@pytest.mark.parametrize("bwd", ["dg", "dh", "x6p"])
+@pytest.mark.parametrize("bwd", ["dg", "dh", "dg32"])
 def test_gru_backward_full_length_vs_torch(dev, bwd, monkeypatch):
     """The cfg2 recurrence shape (bs 32, H 800, both directions) over 201 steps with ragged
-    lengths: the default gate-exchange, the opt-in dh-exchange and the pre-split bf16x6
-    backward against torch's nn.GRU in fp64."""
-    if bwd == "x6p":
-        monkeypatch.setenv("DS2_GRU_X6_BWD", "2")
+    lengths: the default gate-exchange backward (pre-split bf16x6 tiles), its fp32-MFMA form
+    (DS2_GRU_X6_BWD=0) and the opt-in dh-exchange backward against torch's nn.GRU in fp64."""
+    if bwd == "dg32":
+        monkeypatch.setenv("DS2_GRU_X6_BWD", "0")
         bwd = "dg"
     monkeypatch.setenv("DS2_GRU_BWD", bwd)
     n, t, inp, h = 32, 201, 64, 800
