@@ -48,6 +48,22 @@ def gemm_peak():
                             "v_mfma_f32_32x32x16_bf16, fp32 accumulation (bf16 dense peak / 6)")
 
 
+def gru_bwd_kernel(x6f: bool):
+    """(peak, arithmetic, kernel name) of the GRU backward recurrence as configured: the
+    pre-split bf16x6 kernel by default (gru_split.hip), DS2_GRU_X6_BWD=1 its consumer-split
+    form, =0 (or DS2_GRU_X6=0, or a sentinel backward hand-off) the fp32-MFMA kernel, and
+    DS2_GRU_BWD=dh the dh-exchange kernel."""
+    if os.environ.get("DS2_GRU_BWD", "")[:2] == "dh":
+        return PEAK_F32_MFMA_TFLOPS, "W_hh^T contraction, fp32 MFMA (dh exchange)", "gru_bwd_dh_kernel"
+    mode = os.environ.get("DS2_GRU_X6_BWD", "2")[:1] or "2"
+    hand = (os.environ.get("DS2_RNN_HANDOFF_BWD") or os.environ.get("DS2_RNN_HANDOFF") or "f")[:1]
+    if x6f and mode in ("1", "2") and (mode == "1" or hand not in ("s", "h")):
+        form = "pre-split tiles" if mode == "2" else "consumer-side splits"
+        return (PEAK_X6_TFLOPS, "W_hh^T contraction, bf16x6 (fp32-accurate, " + form +
+                ") on v_mfma_f32_16x16x32_bf16", "gru_bwd_x6_kernel")
+    return PEAK_F32_MFMA_TFLOPS, "W_hh^T contraction, fp32 MFMA (v_mfma_f32_16x16x4_f32)", "gru_bwd_dop_kernel"
+
+
 def synthetic_batch(rank: int):
     g = torch.Generator().manual_seed(1234 + rank)
     x = torch.randn(BATCH, 1, 161, T_FRAMES, generator=g)
@@ -362,8 +378,8 @@ def main():
         entry("ds2_gru_fwd", fk, PEAK_X6_TFLOPS if x6f else PEAK_F32_MFMA_TFLOPS,
               "W_hh contraction, bf16x6 (fp32-accurate) on v_mfma_f32_16x16x32_bf16" if x6f
               else "W_hh contraction, fp32 MFMA", "mfma", ("gru_fwd_x6_kernel" if x6f else "gru_fwd_dop_kernel", ()))
-        entry("ds2_gru_bwd", bk, PEAK_F32_MFMA_TFLOPS,
-              "W_hh^T contraction, fp32 MFMA (v_mfma_f32_16x16x4_f32)", "mfma", ("gru_bwd_dh_kernel", ()))
+        bpeak, barith, bkern = gru_bwd_kernel(x6f)
+        entry("ds2_gru_bwd", bk, bpeak, barith, "mfma", (bkern, ()))
         # the roofline object is the dominant kernel family of the step (most ms per step)
         roof = max(kernels.values(), key=lambda e: e["ms_per_step"]) if kernels else None
         cpu = None

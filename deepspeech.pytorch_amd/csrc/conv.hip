@@ -1449,6 +1449,49 @@ __device__ __forceinline__ void cw_split_store(unsigned short* __restrict__ s, i
   cx_split_store8(s, plane, at, v);
 }
 
+// Partial sums of the bf16x6 weight-gradient kernels: one contiguous block per workgroup,
+// partial[s][gi][co 32][w 4][b KW][ci 32] (tap row a = 4 gi + w) -- lane fr = ci, so every
+// store instruction writes two whole 128-B runs; wgrad_reduce_x6_kernel sums the splits in
+// order and scatters into dW[co][ci][a][b].  (The [co][ci][a][b] slab layout had each lane
+// store to its own line: 2.6x the partial bytes in write traffic.)
+constexpr int X6W_BLOCK = 32 * 4 * 32;     // floats per (co, w, ci) plane of one kernel column
+template <int KW>
+__device__ __forceinline__ void x6w_store_block(float* __restrict__ partial, int s, int G, int gi,
+                                                int wave, bool active, int fr, int fh,
+                                                const f32x16 (&acc)[KW]) {
+  if (!active) return;   // rows a >= kh: never read by the reduce
+  float* blk = partial + ((int64_t)s * G + gi) * X6W_BLOCK * KW;
+#pragma unroll
+  for (int b = 0; b < KW; ++b)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int co = (r & 3) + 8 * (r >> 2) + 4 * fh;
+      blk[((co * 4 + wave) * KW + b) * 32 + fr] = acc[b][r];
+    }
+}
+
+// dW[co][ci][a][b] = sum over the S splits (in order) of the blocks above; thread = one
+// (gi, co, w, b, ci) element in block order (coalesced loads)
+__global__ void wgrad_reduce_x6_kernel(const float* __restrict__ partial, int S, int G, int KW,
+                                       ConvDims g, float* __restrict__ dw) {
+  const int64_t per = (int64_t)G * X6W_BLOCK * KW;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < per;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t r = i;
+    const int ci = static_cast<int>(r % 32); r /= 32;
+    const int b = static_cast<int>(r % KW); r /= KW;
+    const int w = static_cast<int>(r % 4); r /= 4;
+    const int co = static_cast<int>(r % 32);
+    const int gi = static_cast<int>(r / 32);
+    const int a = 4 * gi + w;
+    if (a >= g.kh || co >= g.co || ci >= g.ci) continue;
+    float acc = 0.f;
+#pragma unroll 8
+    for (int s = 0; s < S; ++s) acc += partial[(int64_t)s * per + i];   // order kept
+    dw[((int64_t)co * g.ci + ci) * g.kh * KW + a * KW + b] = acc;
+  }
+}
+
 template <int KW, int OFF0>
 __global__ __launch_bounds__(CW_T, 2) void conv_x6_wgrad_kernel(const float* __restrict__ dy,
                                                                  const float* __restrict__ x,
@@ -1570,16 +1613,7 @@ __global__ __launch_bounds__(CW_T, 2) void conv_x6_wgrad_kernel(const float* __r
       }
     }
   }
-  if (!active || fr >= g.ci) return;
-  const int Kc = g.ci * g.kh * KW;
-  float* slab = partial + (int64_t)s * g.co * Kc;
-#pragma unroll
-  for (int b = 0; b < KW; ++b)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int co = (r & 3) + 8 * (r >> 2) + 4 * fh;
-      if (co < g.co) slab[(int64_t)co * Kc + (fr * g.kh + a) * KW + b] = acc[b][r];
-    }
+  x6w_store_block<KW>(partial, s, G, gi, wave, active, fr, fh, acc);
 }
 
 // ---------------------------------------------------------------------------
@@ -1750,16 +1784,7 @@ __global__ __launch_bounds__(SW_T, 2) void conv_x6_wgrad_sw_kernel(const float* 
     }
     row += nrow;
   }
-  if (!active || fr >= g.ci) return;
-  const int Kc = g.ci * g.kh * KW;
-  float* slab = partial + (int64_t)s * g.co * Kc;
-#pragma unroll
-  for (int b = 0; b < KW; ++b)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int co = (r & 3) + 8 * (r >> 2) + 4 * fh;
-      if (co < g.co) slab[(int64_t)co * Kc + (fr * g.kh + a) * KW + b] = acc[b][r];
-    }
+  x6w_store_block<KW>(partial, s, G, gi, wave, active, fr, fh, acc);
 }
 
 // ---------------------------------------------------------------------------
@@ -2336,7 +2361,8 @@ size_t ds2_conv2d_wgrad_workspace_size(int n, int c_in, int h_in, int w_in, int 
   ConvDims g;
   if (!make_dims(g, n, c_in, h_in, w_in, c_out, kh, kw, sh, sw, ph, pw)) return 0;
   const size_t per = (size_t)c_out * c_in * kh * kw * sizeof(float);
-  if (x6w_ok(g)) return (size_t)x6w_splits(g) * per + 256;
+  if (x6w_ok(g))
+    return (size_t)x6w_splits(g) * ((kh + 3) / 4) * X6W_BLOCK * kw * sizeof(float) + 256;
   const WgradPlan pl = wgrad_plan(g);
   return (size_t)n * (pl.nt > 0 ? pl.bands : 1) * per + 256;
 }
@@ -2384,7 +2410,15 @@ ds2_status_t ds2_conv2d_wgrad(const float* dy, const float* x, float* dw, float*
   const int64_t per = (int64_t)c_out * Kc;
   int rg = cdiv(per, 256);
   if (rg > 2048) rg = 2048;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(rg), dim3(256), 0, st, partial, slabs, per, dw);
+  if (x6w_ok(g)) {
+    const int G = (kh + 3) / 4;
+    const int64_t blk = (int64_t)G * X6W_BLOCK * kw;
+    const int xg = static_cast<int>(std::min<int64_t>(cdiv(blk, 256), 2048));
+    hipLaunchKernelGGL(wgrad_reduce_x6_kernel, dim3(xg), dim3(256), 0, st, partial, slabs, G, kw,
+                       g, dw);
+  } else {
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(rg), dim3(256), 0, st, partial, slabs, per, dw);
+  }
   if (dbias != nullptr)
     hipLaunchKernelGGL(bias_grad_kernel, dim3(c_out), dim3(BG_T), 0, st, dy, n, c_out,
                        (int64_t)g.ho * g.wo, dbias);

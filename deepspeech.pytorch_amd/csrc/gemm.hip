@@ -1530,12 +1530,14 @@ extern "C" ds2_status_t ds2_sgemm_ws(int trans_a, int trans_b, int m, int n, int
 // bf16-operand GEMM (sbgemm_kernel): same contract as ds2_sgemm_ws; every operand must be
 // float4-staged (16-B aligned, ld and the contiguous extent multiples of 4) and span
 // < 2^31 bytes, else DS2_UNSUPPORTED_SHAPE (no silent fp32 fallback).
-// The bf16-operand GEMM runs on sxgemm2_kernel with one plane (NPL 1: 256-row tiles, one
-// workgroup per CU, 32x32x16 MFMAs from one LDS image per operand); DS2_GEMM_BF16_X2=0
-// selects the older sbgemm_kernel (128 x 128, 16x16x32).
+// DS2_GEMM_BF16_X2=1: the bf16-operand GEMM on sxgemm2_kernel with one plane (NPL 1: 256-row
+// tiles, one workgroup per CU, 32x32x16 MFMAs from one LDS image per operand) instead of
+// sbgemm_kernel (128 x 128, two workgroups per CU).  Opt-in: cfg4 7xBiLSTM-1024 bf16 3998 vs
+// 4063 audio-s/s on one box -- with one product per fragment pair the fp32 operand staging,
+// not the MFMAs, bounds both, and the two-workgroup kernel hides it better.
 static bool bf16_x2_enabled() {
   const char* e = getenv("DS2_GEMM_BF16_X2");
-  return !(e != nullptr && e[0] == '0');
+  return e != nullptr && e[0] == '1';
 }
 
 extern "C" size_t ds2_sgemm_bf16_workspace_size(int m, int n, int k, int batch) {

@@ -5,9 +5,8 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out
 TAG=${1:-r3k}
-timeout -k 10 900 python -u -m pytest tests/test_gpu_ops.py tests/test_librosa_effects.py tests/test_audio_aug.py \
-  -x -v --timeout 300 --timeout-method thread -m gpu -k "gru or sgemm or effects or stretch or resample or pitch or aug" \
-  > gpurun_out/$TAG.tests.log 2>&1 || exit $?
+timeout -k 10 900 python -u -m pytest tests/test_gpu_ops.py -x -v --timeout 300 --timeout-method thread \
+  -m gpu -k "gru or sgemm" > gpurun_out/$TAG.tests.log 2>&1 || exit $?
 tail -1 gpurun_out/$TAG.tests.log
 for x2 in 1 0; do
   DS2_GEMM_BF16_X2=$x2 timeout -k 10 400 python -u scripts/bench_cfg4.py --rnn-gemm bf16 --steps 3 \
@@ -16,4 +15,7 @@ for x2 in 1 0; do
 done
 timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/$TAG.bench.log 2>&1 || exit $?
 grep -o '"value": [0-9.]*\|"us_per_step": [0-9.]*' gpurun_out/$TAG.bench.log | tr '\n' ' '; echo
-bash scripts/gpu_prof.sh $TAG
+bash scripts/gpu_prof.sh $TAG || exit $?
+timeout -k 10 600 python -u -m pytest tests/test_librosa_effects.py tests/test_audio_aug.py -x -v \
+  --timeout 300 --timeout-method thread -m gpu > gpurun_out/$TAG.effects.log 2>&1 || exit $?
+tail -1 gpurun_out/$TAG.effects.log

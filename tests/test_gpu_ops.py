@@ -103,10 +103,13 @@ def test_sgemm_x6_is_fp32_accurate(dev, ta, tb, m, n, k, monkeypatch):
 @pytest.mark.parametrize("m,n,k", [(4, 4, 4), (36, 52, 28), (128, 128, 64), (300, 256, 516),
                                    (516, 2400, 132), (256, 300, 5000),      # split-K tail
                                    (128 * 29, 128 * 27 + 52, 2080)])       # rounds + tail
-def test_sgemm_bf16(dev, ta, tb, m, n, k):
+@pytest.mark.parametrize("x2", ["0", "1"])
+def test_sgemm_bf16(dev, ta, tb, m, n, k, x2, monkeypatch):
     """bf16-operand GEMM (BASELINE cfg4): operands rounded to bf16 (nearest even) on the
     way in, exact products, fp32 accumulation.  Reference: the same bf16 roundings done by
-    torch on the host, multiplied in fp64 -- so only the fp32 summation differs (1e-5)."""
+    torch on the host, multiplied in fp64 -- so only the fp32 summation differs (1e-5).
+    x2 "1": the one-plane sxgemm2 form (DS2_GEMM_BF16_X2=1)."""
+    monkeypatch.setenv("DS2_GEMM_BF16_X2", x2)
     g = torch.Generator().manual_seed(m * 7 + n * 3 + k + 1)
     a = torch.randn(k, m, generator=g) if ta else torch.randn(m, k, generator=g)
     b = torch.randn(n, k, generator=g) if tb else torch.randn(k, n, generator=g)

@@ -117,10 +117,16 @@ def _cmp(got, exp, tol):
 
 @pytest.mark.gpu
 def test_time_stretch_device_matches_oracle(dev):
-    """Ragged batch, rates over ChangeAudioSpeed's range: device vs restatement.  Bound
-    1e-5 of the peak: the phase vocoder's float32 accumulator is reproduced bit for bit
-    (libm-style hypot / atan2 / sin / cos: evaluated in double, rounded once), the FFTs
-    differ from numpy's pocketfft only in the last bits of fp64."""
+    """Ragged batch, rates over ChangeAudioSpeed's range: device vs restatement.  librosa's
+    chain carries float32 phase noise: the vocoder's float32 accumulator reaches ~1e4-1e5 rad
+    in the high bins (an ulp of 1e-3-1e-2 rad), so the restatement itself sits 1e-5 (513
+    samples) to 2e-2 (10 s) of the peak away from the same chain in float64
+    (le.time_stretch_f64), and any last-bit difference upstream decorrelates those roundings
+    (two windows 2.2e-16 apart move the restatement by 7e-5 of the peak on 1 s;
+    scripts/diag_stretch.py).  The device's fp64 radix-2 FFTs differ from pocketfft in those
+    last bits, so the bound is relative to that noise: the device is closer to the
+    restatement than 3/4 of the restatement's own distance from float64, and no farther from
+    float64 than 1.5x the restatement."""
     lens = [16000, 9001, 23456, 4096, 513, 160000]
     rates = [0.85, 1.15, 0.93, 1.0, 1.07, 0.891]
     wavs = [_speech_like(n, i) for i, n in enumerate(lens)]
@@ -131,9 +137,13 @@ def test_time_stretch_device_matches_oracle(dev):
     out = out.cpu().numpy()
     for i, (y, r) in enumerate(zip(wavs, rates)):
         e = le.time_stretch(y, r)
+        f = le.time_stretch_f64(y, r)
         assert olens[i] == len(e)
-        err = _cmp(out[i, :len(e)], e, 1e-5)
-        assert err < 1e-5, (i, r, err)
+        noise = _cmp(e, f, 0)
+        err = _cmp(out[i, :len(e)], e, 0)
+        err64 = _cmp(out[i, :len(e)], f, 0)
+        assert err <= 0.75 * noise + 2e-6, (i, r, err, noise)
+        assert err64 <= 1.5 * noise + 2e-6, (i, r, err64, noise)
         assert not out[i, len(e):].any()
 
 
@@ -188,7 +198,10 @@ def test_pitch_shift_and_file_resample_through_apply_waves(dev):
     out = out.cpu().numpy()
     for i, e in enumerate(exp):
         assert lens[i] == len(e)
-        assert _cmp(out[i, :len(e)], e, 1e-5) < 1e-5, i
+        # the phase-vocoder bound of test_time_stretch_device_matches_oracle (pitch shift is
+        # a stretch plus a resample; the float32 phase noise of these <= 1 s signals is
+        # 1e-5-1e-3 of the peak)
+        assert _cmp(out[i, :len(e)], e, 0) < 5e-4, i
         assert not out[i, len(e):].any()
 
 
@@ -229,6 +242,19 @@ def test_parse_audio_full_aug_type0_pipeline(dev, tmp_path):
         y = oaa.one_of(ref, y, SR)
         exp = orc.spectrogram(y)
         assert got.shape == exp.shape
-        assert (got - exp).abs().max().item() < 2e-3
+        # the noise scale of librosa's float32 phase vocoder on this utterance: the same draws
+        # through the float64 chain (test_time_stretch_device_matches_oracle)
+        random.seed(100 + i)
+        np.random.seed(100 + i)
+        np.random.uniform(0.85, 1.15)
+        np.random.uniform(-10, 10)
+        ts = le.time_stretch
+        le.time_stretch = lambda w, r: le.time_stretch_f64(w, r).astype(np.float32)
+        try:
+            y64 = oaa.one_of(ref, oaa._read_norm(p)[0], SR)
+        finally:
+            le.time_stretch = ts
+        noise = (exp - orc.spectrogram(y64)).abs().max().item()
+        assert (got - exp).abs().max().item() <= 0.75 * noise + 2e-3, (i, noise)
         seen.update(t['kind'] for t in ref['transforms'] if t['prob'] == 1.0)
     assert {'stretch', 'pitch'} <= seen
