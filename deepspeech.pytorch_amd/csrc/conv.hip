@@ -1628,7 +1628,10 @@ __global__ __launch_bounds__(CW_T, 2) void conv_x6_wgrad_kernel(const float* __r
 // one XCD (consecutive workgroup ids), so they share its L2 for x and dy.
 constexpr int SW_T = 256;
 constexpr int SW_COLS = 32;                 // output columns per row stage (two 16-column k-steps)
-constexpr int SW_XP = 48;                   // x slot row pitch (bf16): columns c0 - 8 .. c0 + 39
+constexpr int SW_XP = 56;                   // x slot row pitch (bf16): columns c0 - 8 .. c0 + 39;
+                                            // 7 x 16 B (odd): ds_read_b128's 16-lane groups
+                                            // hit 16 distinct 16-B bank slots (48 had 2-way
+                                            // conflicts: 34 % of LDS cycles in SQ counters)
 constexpr int SW_DP = 40;                   // dy row pitch (bf16): 32 columns, 5 x 16 B
 constexpr int SW_RING = 6;                  // x slots: 4 window rows + 2 incoming
 constexpr int SW_XSL = 32 * SW_XP;          // bf16 per x slot (32 input channels)

@@ -658,14 +658,20 @@ __global__ __launch_bounds__(256, 2) void sbgemm_kernel(
 // run the GRU recurrences (gru_split.hip).
 //   tile 128 x 128, stages of 32 k, 4 waves of 4 x 4 16x16 tiles, two workgroups per CU;
 //   LDS: per operand three bf16 planes [128 rows][32 k] (64-B rows, 16-B slot s of row r
-//   at s ^ ((r >> 2) & 3): conflict-free ds_read_b128 fragments and stores);
+//   at s ^ xswz(r), below: conflict-free ds_read_b128 fragments and stores);
 //   k-contiguous source: a thread unit = (row, 8-k slot), two float4 loads;
 //   row-contiguous source: a thread = one row x 16 k, 16 dword loads (consecutive threads
 //   read consecutive rows), so the transposed stores need no register shuffles.
 constexpr int XS = 32;                  // k per stage
 constexpr int XPLANE = BM * XS;         // bf16 per plane (BM = 128 rows)
 
-__device__ __forceinline__ int xslot(int row, int s) { return row * XS + 8 * (s ^ ((row >> 2) & 3)); }
+// 16-B slot s of a 64-B row, XOR-swizzled by q(row) = bit 2 | (bit 1 ^ bit 3) << 1: with it
+// the fragment reads (ds_read_b128 serves lanes in four 16-lane groups, rows {0-3, 12-15,
+// 20-27} and the rest of 32) and both staging stores (ds_write_b128 in 8-lane groups: 8
+// consecutive rows of one slot, or 2 rows x 4 slots) hit distinct banks.  The earlier
+// (row >> 2) & 3 left the row-contiguous stores 4-way conflicted (12 % of LDS cycles).
+__device__ __forceinline__ int xswz(int row) { return ((row >> 2) & 1) | ((((row >> 1) ^ (row >> 3)) & 1) << 1); }
+__device__ __forceinline__ int xslot(int row, int s) { return row * XS + 8 * (s ^ xswz(row)); }
 
 template <bool KC>
 __device__ __forceinline__ void xload_stage(__amdgpu_buffer_rsrc_t rs, int ld, int rows, int kend,

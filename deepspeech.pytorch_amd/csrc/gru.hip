@@ -1405,11 +1405,13 @@ static inline unsigned long long* stamp_slots(unsigned* ctrs, int n, int num_dir
                                                align256(ctr_words(n, num_dirs) * sizeof(unsigned)));
 }
 
-// ring of 1-KB hand-off tiles for the direct-operand kernels (gates tiles per unit block:
-// 1 forward, 3 backward): 2 slots for the flag hand-off, kRingSlots for the sentinel one
+// ring of hand-off tiles for the direct-operand kernels (gates tiles per unit block: 1
+// forward, 3 backward): 2 slots for the flag hand-off, kRingSlots for the sentinel one; the
+// backward's tiles are sized for the pre-split form (1.5 KB, gru_split.hip)
 static inline size_t ring_bytes(int n, int h, int num_dirs, int tiles) {
   const size_t UB = (h + GU - 1) / GU, BT = (n + GB - 1) / GB;
-  return align256(kRingSlots * (size_t)num_dirs * BT * UB * tiles * 256 * sizeof(float));
+  const size_t tile_floats = tiles == 3 ? 384 : 256;
+  return align256(kRingSlots * (size_t)num_dirs * BT * UB * tiles * tile_floats * sizeof(float));
 }
 // every ring word starts as the sentinel (slots 0 and 1 must; the rest for simplicity)
 static inline hipError_t ring_reset(float* ring, int n, int h, int num_dirs, int tiles,

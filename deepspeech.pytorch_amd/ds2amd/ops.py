@@ -605,11 +605,32 @@ class rnn_gemm_precision:
         return False
 
 
+def _stacked_rows(a: torch.Tensor, b: torch.Tensor):
+    """[a; b] as one row-major matrix when b starts where a ends in the same storage (the
+    layout optim.FlatParams gives a bidirectional layer's W_ih pair and its gradient
+    slots), else None."""
+    if a.dim() != 2 or tuple(b.shape) != tuple(a.shape) or not (a.is_contiguous() and
+                                                                   b.is_contiguous()):
+        return None
+    if a.untyped_storage().data_ptr() != b.untyped_storage().data_ptr():
+        return None
+    if b.data_ptr() != a.data_ptr() + a.numel() * a.element_size():
+        return None
+    return a.as_strided((2 * a.shape[0], a.shape[1]), (a.shape[1], 1))
+
+
 def _rnn_input_proj(x, weights, nd, g, bf16=False):
-    """xproj[T, N, D, g] = x @ W_ih^T + b_ih for every direction (one GEMM each)."""
+    """xproj[T, N, D, g] = x @ W_ih^T + b_ih for every direction: one GEMM over both
+    directions when their W_ih lie back to back (N = 2g), else one GEMM each."""
     t, n, inp = x.shape
     x2d = x.view(t * n, inp)
     xproj = torch.empty(t, n, nd, g, device=x.device, dtype=_F32)
+    ws = _stacked_rows(weights[0], weights[4]) if nd == 2 else None
+    if ws is not None:
+        bias = torch.cat([weights[2], weights[6]])
+        sgemm(x2d, ws, xproj, m=t * n, n=2 * g, k=inp, trans_b=True, lda=inp, ldb=inp,
+              ldc=2 * g, bias=bias, bf16=bf16)
+        return xproj
     for d in range(nd):
         w_ih, _, b_ih, _ = weights[4 * d: 4 * d + 4]
         sgemm(x2d, w_ih, xproj, m=t * n, n=g, k=inp, trans_b=True, lda=inp, ldb=inp,
@@ -641,11 +662,21 @@ def _rnn_param_grads(x, h_all, dgx, dgh, weights, nd, g, need_dx, bf16=False, db
     ld = nd * g
     grads = []
     dx = torch.empty(t, n, inp, device=dev, dtype=_F32) if need_dx else None
+    # both directions in one GEMM where W_ih (dX) and its gradient slots (dW_ih) are stacked
+    w_st = _stacked_rows(weights[0], weights[4]) if nd == 2 else None
+    dw_ih_all = [grad_like(weights[4 * d]) for d in range(nd)]
+    dw_st = _stacked_rows(dw_ih_all[0], dw_ih_all[1]) if w_st is not None else None
+    if dw_st is not None:
+        sgemm(dgx, x2d, dw_st, m=2 * g, n=inp, k=tn, trans_a=True, lda=ld, ldb=inp, ldc=inp,
+              bf16=bf16)
+    if dx is not None and w_st is not None:
+        sgemm(dgx, w_st, dx, m=tn, n=inp, k=2 * g, lda=ld, ldb=inp, ldc=inp, bf16=bf16)
     for d in range(nd):
         w_ih, w_hh, b_ih, b_hh = weights[4 * d: 4 * d + 4]
-        dw_ih = grad_like(w_ih)
-        sgemm(dgx, x2d, dw_ih, m=g, n=inp, k=tn, trans_a=True, lda=ld, ldb=inp, ldc=inp,
-              a_off=d * g, bf16=bf16)
+        dw_ih = dw_ih_all[d]
+        if dw_st is None:
+            sgemm(dgx, x2d, dw_ih, m=g, n=inp, k=tn, trans_a=True, lda=ld, ldb=inp, ldc=inp,
+                  a_off=d * g, bf16=bf16)
         if dbias is not None:
             db_ih, db_hh = dbias[2 * d], dbias[2 * d + 1]
         else:
@@ -671,7 +702,7 @@ def _rnn_param_grads(x, h_all, dgx, dgh, weights, nd, g, need_dx, bf16=False, db
                 colsum(dgh, tn, h, ld, db_hh[2 * h:], off=d * g + 2 * h)
             else:
                 colsum(dgh, tn, g, ld, db_hh, off=d * g)
-        if dx is not None:
+        if dx is not None and w_st is None:
             sgemm(dgx, w_ih, dx, m=tn, n=inp, k=g, lda=ld, ldb=inp, ldc=inp,
                   beta=0.0 if d == 0 else 1.0, a_off=d * g, bf16=bf16)
         grads += [dw_ih, dw_hh, db_ih, db_hh]

@@ -30,15 +30,38 @@ class FlatParams:
 
     ALIGN = 64  # elements; keeps every view 256-byte aligned
 
-    def __init__(self, params: List[torch.nn.Parameter], device):
+    def __init__(self, params: List[torch.nn.Parameter], device, adjacent=()):
+        """adjacent: (first, second) parameter pairs laid out back to back (first, then
+        second, no padding between when first fills whole 64-element blocks) -- a
+        bidirectional recurrent layer's W_ih of both directions, so its input projection,
+        dX and dW_ih GEMMs run as one GEMM over both directions (ops._stacked_rows)."""
         params = [p for p in params if p.requires_grad]
-        self.params = list(reversed(params))       # backward-completion order
+        self.model_params = params                 # model.parameters() order
+        order = list(reversed(params))             # backward-completion order
+        second_of = {id(a): b for a, b in adjacent}
+        seconds = {id(b) for _, b in adjacent}
+        first_of = {id(b): a for a, b in adjacent}
+        self.params = []
+        placed = set()
+        for p in order:
+            if id(p) in placed:
+                continue
+            if id(p) in second_of or id(p) in seconds:
+                a = p if id(p) in second_of else first_of[id(p)]
+                b = second_of[id(a)]
+                for q in (a, b):
+                    self.params.append(q)
+                    placed.add(id(q))
+            else:
+                self.params.append(p)
+                placed.add(id(p))
         offs, total = [], 0
         for p in self.params:
             offs.append(total)
             total += (p.numel() + self.ALIGN - 1) // self.ALIGN * self.ALIGN
         self.numel = total
         self.offsets = offs
+        self.offset_of = {id(p): o for p, o in zip(self.params, offs)}
         self.flat = torch.zeros(total, dtype=torch.float32, device=device)
         self.grad = torch.zeros(total, dtype=torch.float32, device=device)
         for p, o in zip(self.params, offs):
@@ -123,7 +146,7 @@ class FusedSGD:
     def _model_order(self):
         """(param, flat offset) in the reference optimizer's order: model.parameters()
         (build_optimizer(args, model.parameters()), train.py:139-152, 939)."""
-        return list(zip(reversed(self.flat.params), reversed(self.flat.offsets)))
+        return [(p, self.flat.offset_of[id(p)]) for p in self.flat.model_params]
 
     def _group_defaults(self):
         # the installed torch's own SGD param_group keys, so the dict loads into

@@ -173,6 +173,12 @@ def _ds2_params():
     return m
 
 
+def _ds2_pairs(m):
+    """The Trainer's adjacent pairs: both directions' W_ih of every bidirectional layer."""
+    return [(mm.weight_ih_l0, mm.weight_ih_l0_reverse) for mm in m.modules()
+            if hasattr(mm, 'weight_ih_l0_reverse')]
+
+
 def _rank_grads(params, rank):
     g = torch.Generator().manual_seed(1000 + rank)
     return [torch.randn(p.shape, generator=g) for p in params]
@@ -185,7 +191,7 @@ def _ds2_worker(rank, world, port, out_q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     m = _ds2_params()
     params = [p for p in m.parameters() if p.requires_grad]
-    flat = FlatParams(params, "cpu")
+    flat = FlatParams(params, "cpu", adjacent=_ds2_pairs(m))
     red = GradAllReducer(flat, bucket_mb=40.0)
     grads = _rank_grads(params, rank)
     flat.zero_grad()
@@ -232,6 +238,7 @@ def test_grad_allreduce_real_ds2_layout():
     m = _ds2_params()
     params = [p for p in m.parameters() if p.requires_grad]
     assert sum(p.numel() for p in params) > 41_000_000
+    layout = FlatParams(params, "cpu", adjacent=_ds2_pairs(m))
     cap = 40 * 1024 * 1024 // 4
     expect = None
     for rank, buckets, offs, sizes, numel, issued, in_flight, waits_fit, waits_over, g in res:
@@ -251,10 +258,49 @@ def test_grad_allreduce_real_ds2_layout():
         assert issued == len(buckets) and in_flight == len(buckets)
         assert waits_fit == 0 and waits_over == len(buckets)
         if expect is None:
-            # (g0 + g1) / 2 in the flat layout (reverse registration order)
+            # (g0 + g1) / 2 in the flat layout (reverse registration order, W_ih pairs
+            # back to back)
+            assert offs == layout.offsets
             g0 = _rank_grads(params, 0)
             g1 = _rank_grads(params, 1)
             expect = torch.zeros(numel)
-            for p_, a, b, o in zip(reversed(params), reversed(g0), reversed(g1), offs):
+            for p_, a, b in zip(params, g0, g1):
+                o = layout.offset_of[id(p_)]
                 expect[o:o + p_.numel()] = ((a + b) * 0.5).reshape(-1)
         assert torch.equal(torch.from_numpy(g), expect)
+
+
+def test_flat_params_stacks_w_ih_pairs():
+    """FlatParams with the Trainer's pairs: each bidirectional layer's W_ih (and its gradient
+    slot) lies back to back, so ops._stacked_rows sees [W_ih_f; W_ih_r] as one matrix; every
+    other parameter keeps the reverse registration order, and the optimizer's state order is
+    still model.parameters() (torch.optim.SGD's)."""
+    from ds2amd import ops
+    from ds2amd.optim import FusedSGD
+    torch.manual_seed(3)
+    from ds2amd import model as dsm
+    m = dsm.DeepSpeech(rnn_type="gru", labels=LABELS, rnn_hidden_size=64, nb_layers=3,
+                       audio_conf=CONF, bidirectional=True)
+    pairs = _ds2_pairs(m)
+    assert len(pairs) == 3
+    before = [p.detach().clone() for p in m.parameters()]
+    params = list(m.parameters())
+    flat = FlatParams(params, "cpu", adjacent=pairs)
+    for p, b in zip(m.parameters(), before):
+        assert torch.equal(p.detach(), b)
+    flat.zero_grad()                   # as the Trainer before each backward
+    for a, b in pairs:
+        st = ops._stacked_rows(a, b)
+        assert st is not None and torch.equal(st, torch.cat([a, b]))
+        ga, gb = ops.grad_like(a), ops.grad_like(b)
+        gs = ops._stacked_rows(ga, gb)
+        assert gs is not None
+        gs.fill_(1.5)
+        assert (flat.grad[flat.offset_of[id(a)]:flat.offset_of[id(b)] + b.numel()] == 1.5).all()
+    rest = [p for p in reversed(params) if all(p is not a and p is not b for a, b in pairs)]
+    order = [p for p in flat.params if all(p is not a and p is not b for a, b in pairs)]
+    assert [id(p) for p in order] == [id(p) for p in rest]
+    opt = FusedSGD(flat, lr=0.1)
+    assert [id(p) for p, _ in opt._model_order()] == [id(p) for p in params]
+    # unpaired tensors are not stacked
+    assert ops._stacked_rows(params[0], params[1]) is None
