@@ -85,16 +85,6 @@ __device__ __forceinline__ void split_pk4(const f32x4 v, u32x4& hm, u32x2& lo) {
   }
 }
 
-// sentinel ring over pre-split runs: a run is ready when no lane holds the sentinel word in
-// it (a split of finite values never packs two 0xFFFF bf16 NaNs into one word; a published
-// word that would is replaced by two quiet NaNs)
-__device__ __forceinline__ bool runs_ready(const u32x4 h, const u32x2 l) {
-  const bool ok = (h.x != kSentinel) & (h.y != kSentinel) & (h.z != kSentinel) &
-                  (h.w != kSentinel) & (l.x != kSentinel) & (l.y != kSentinel);
-  return __ballot(!ok) == 0ull;
-}
-__device__ __forceinline__ unsigned desent_bf2(unsigned v) { return v == kSentinel ? 0x7FC07FC0u : v; }
-
 // the Tri of a 32-k pair from two pre-split tiles' runs (slots 0..3 tile a, 4..7 tile b)
 __device__ __forceinline__ Tri tri_of(const u32x4 ha, const u32x2 la, const u32x4 hb, const u32x2 lb) {
   Tri t;
@@ -355,9 +345,9 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
 // LW pairs in flight).
 // PRE: the producers publish their gate-gradient tiles pre-split (per lane a 16-B {hi, mid}
 // run and an 8-B lo run: 1.5 KB per tile instead of 1 KB of fp32), so the consumer loads
-// ready MFMA operands and does no split VALU.  With the flag hand-off (HM 0) the runs stream
-// through a window of LWP pairs; with the sentinel ring (HM 1: no drain, no flag -- the data
-// is the flag) through the same window, each stale pass re-issuing the window (below).
+// ready MFMA operands and does no split VALU (flag hand-off; the runs stream through a window
+// of LWP pairs).  A sentinel ring over the runs (no drain, no flag: the data is the flag; each
+// stale pass re-issuing the window) measured 9.2 vs 6.3 us per step and was removed.
 // dbp (nullable): per-unit bias-gradient partials as gru_bwd_dop_kernel's.
 template <int NP, int HM, int NW, bool PRE>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW / 4, NW / 4))) void gru_bwd_x6_kernel(
@@ -367,12 +357,9 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW / 4,
     const int* __restrict__ lens, float* __restrict__ dgx, float* __restrict__ dgh,
     float* __restrict__ gx, unsigned* __restrict__ counters, unsigned* __restrict__ err,
     unsigned long long* __restrict__ stamps, double* __restrict__ dbp) {
-  static_assert(!PRE || HM == 0 || HM == 1, "pre-split tiles: flag or sentinel hand-off");
+  static_assert(!PRE || HM == 0, "pre-split tiles use the flag hand-off");
   constexpr int RP = GU + 1;
   constexpr bool SENT = HM == 1;
-  constexpr bool PSENT = PRE && SENT;
-  constexpr int WLO = PSENT ? NW * NP * 64 : 1;   // PSENT: W_hh^T lo terms in LDS (registers
-  __shared__ u32x4 wlo_s[WLO];                    // go to the spin state)
   constexpr int NSLOT = SENT ? kRingSlots : 2;
   constexpr int LW = NW == 4 ? NP : 3;          // pairs whose loads are in flight
   constexpr int TF = PRE ? 384 : 256;           // ring floats per tile
@@ -427,7 +414,6 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW / 4,
 #pragma unroll
         for (int c = 0; c < 4; ++c) b[c] = wc[(int64_t)(16 * tb + c) * H];
       w[p] = split3(a, b);
-      if constexpr (PSENT) wlo_s[(wave * NP + p) * 64 + lane] = __builtin_bit_cast(u32x4, w[p].lo);
     }
   }
   const int m = (threadIdx.x >> 4) & 15;
@@ -465,58 +451,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW / 4,
         return;
       }
       trace_at(s, 1);
-      if constexpr (PSENT) {
-        // LWP pairs' runs in flight as in the flag form; pair p is multiplied once both its
-        // runs hold no sentinel, and while it waits each pass re-issues its runs AND the later
-        // in-flight pairs' (issued as early, so as stale): one round trip per pass, not one
-        // per stale tile
-        const int tb0 = (((s - 1) % NSLOT) * slot_floats + grp_off + t_first * TF) * 4;
-        sleep_units(g_rnn_tune[2]);
-        u32x4 hm[2 * NP];
-        u32x2 lo[2 * NP];
-        auto load_run = [&](int i) {
-          const bool ok = i < 2 * np && t_first + i < NB3;
-          const int to = tb0 + i * TF * 4;
-          hm[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                x_rs, ok ? to + lane * 16 : 0x7ffffff0, 0, kSc1));
-          lo[i] = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(
-                                                x_rs, ok ? to + 1024 + lane * 8 : 0x7ffffff0, 0, kSc1));
-        };
-#pragma unroll
-        for (int i = 0; i < 2 * LWP; ++i) load_run(i);
-#pragma unroll
-        for (int p = 0; p < NP; ++p) {
-          if (p + LWP < NP) {
-            load_run(2 * (p + LWP));
-            load_run(2 * (p + LWP) + 1);
-          }
-          if (p < np) {
-            for (unsigned spins = 0;; ++spins) {
-              // a run past NB3 or past the wave's tiles reads zeros: ready
-              if (g_spin_limit != 0 && runs_ready(hm[2 * p], lo[2 * p]) &&
-                  runs_ready(hm[2 * p + 1], lo[2 * p + 1]))
-                break;
-              if (spins > g_spin_limit || g_spin_limit == 0) {
-                if (lane == 0) __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                failed = 1;
-                break;
-              }
-              sleep_units(g_rnn_tune[0]);
-              asm volatile("" ::: "memory");
-#pragma unroll
-              for (int q = p; q < NP && q < p + LWP; ++q) {
-                load_run(2 * q);
-                load_run(2 * q + 1);
-              }
-            }
-            if (failed) break;
-            Tri wb = w[p];
-            wb.lo = __builtin_bit_cast(bf16x8, wlo_s[(wave * NP + p) * 64 + lane]);
-            acc = mma6(tri_of(hm[2 * p], lo[2 * p], hm[2 * p + 1], lo[2 * p + 1]), wb, acc);
-          }
-        }
-        trace_at(s, 2);
-      } else if constexpr (PRE) {
+      if constexpr (PRE) {
         // LWP pairs' runs in flight, the next pair's issued as each pair is multiplied
         const int tb0 = (((s - 1) & 1) * slot_floats + grp_off + t_first * TF) * 4;
         u32x4 hm[2 * NP];
@@ -616,35 +551,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW / 4,
     __syncthreads();
     if (wave == 0) {
       const int toff = (grp_off + ub * 256 + lane * 4) * 4;
-      if constexpr (PSENT) {
-        u32x4 hmv[3];
-        u32x2 lov[3];
-#pragma unroll
-        for (int g = 0; g < 3; ++g) {
-          split_pk4(*reinterpret_cast<const f32x4*>(tile + g * GB * GU + lane * 4), hmv[g], lov[g]);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) hmv[g][e] = desent_bf2(hmv[g][e]);
-#pragma unroll
-          for (int e = 0; e < 2; ++e) lov[g][e] = desent_bf2(lov[g][e]);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // last step's sentinel stores first
-        const int so = ((s % NSLOT) * slot_floats + grp_off + ub * TF) * 4;
-        const int sn = (((s + 2) % NSLOT) * slot_floats + grp_off + ub * TF) * 4;
-        const u32x4 sv4 = u32x4{kSentinel, kSentinel, kSentinel, kSentinel};
-        const u32x2 sv2 = u32x2{kSentinel, kSentinel};
-#pragma unroll
-        for (int g = 0; g < 3; ++g) {
-          const int go = so + g * UB * TF * 4;
-          __builtin_amdgcn_raw_buffer_store_b128(hmv[g], x_rs, go + lane * 16, 0, kSc1);
-          __builtin_amdgcn_raw_buffer_store_b64(lov[g], x_rs, go + 1024 + lane * 8, 0, kSc1);
-        }
-#pragma unroll
-        for (int g = 0; g < 3; ++g) {
-          const int gn = sn + g * UB * TF * 4;
-          __builtin_amdgcn_raw_buffer_store_b128(sv4, x_rs, gn + lane * 16, 0, kSc1);
-          __builtin_amdgcn_raw_buffer_store_b64(sv2, x_rs, gn + 1024 + lane * 8, 0, kSc1);
-        }
-      } else if (SENT) {
+      if (SENT) {
         u32x4 v[3];
 #pragma unroll
         for (int g = 0; g < 3; ++g)
@@ -759,10 +666,8 @@ static int x6_bwd_waves() {
 static const void* bwd_x6_fn(int pairs, int hm, int nw, bool pre) {
   const int need = (pairs + nw - 1) / nw;
   if (pre) {
-#define DS2_BP6(K, W)                                                                    \
-    if (need <= K)                                                                       \
-      return hm == 1 ? reinterpret_cast<const void*>(gru_bwd_x6_kernel<K, 1, W, true>)   \
-                     : reinterpret_cast<const void*>(gru_bwd_x6_kernel<K, 0, W, true>);
+#define DS2_BP6(K, W) \
+    if (need <= K) return reinterpret_cast<const void*>(gru_bwd_x6_kernel<K, 0, W, true>);
     if (nw == 4) {
       DS2_BP6(1, 4) DS2_BP6(2, 4) DS2_BP6(4, 4) DS2_BP6(6, 4) DS2_BP6(8, 4) DS2_BP6(10, 4)
       DS2_BP6(13, 4) DS2_BP6(16, 4) DS2_BP6(19, 4)
@@ -815,7 +720,7 @@ bool launch_gru_bwd_x6(int hm, int t_max, int n, int h, int num_dirs, const floa
   const int mode = x6_bwd_mode();
   if (mode == 0 || (h % GU) != 0) return false;
   const bool pre = mode == 2;
-  if (pre && hm == 2) return false;          // pre-split tiles: flag or sentinel hand-off
+  if (pre && hm != 0) return false;          // pre-split tiles: flag hand-off only
   apply_spin_limit_env();
   apply_rnn_tune_env();
   const int UB = h / GU, BT = (n + GB - 1) / GB;

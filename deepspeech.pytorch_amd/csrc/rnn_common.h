@@ -409,12 +409,22 @@ static bool persistent_enabled() {
 // mapping; scripts/prof_exit_probe2.sh: one cooperative GRU launch reproduces it, the same
 // launch made plainly exits 0), and the step time is unchanged (profiles/r3g_coop_ab.txt).
 // DS2_RNN_COOP=1 selects cooperative launches.
+// `lds` is a dynamic-LDS pad that keeps one workgroup per CU; a kernel whose static LDS
+// already takes more than half the CU's LDS gets less pad, so static + pad never exceeds the
+// per-workgroup limit (a dispatch over it faulted: the pre-split sentinel backward's 94 KB of
+// static LDS + the 80 KB pad).
 static inline hipError_t rnn_launch(const void* fn, dim3 grid, dim3 block, void** args,
                                     size_t lds, hipStream_t st) {
   static const int coop = [] {
     const char* e = getenv("DS2_RNN_COOP");
     return (e != nullptr && e[0] == '1') ? 1 : 0;
   }();
+  constexpr size_t max_lds = 160 * 1024;   // gfx950: LDS per CU = per workgroup maximum
+  hipFuncAttributes fa;
+  if (hipFuncGetAttributes(&fa, fn) != hipSuccess) return hipErrorInvalidDeviceFunction;
+  const size_t stat = fa.sharedSizeBytes;
+  if (stat > max_lds) return hipErrorInvalidValue;
+  if (stat + lds > max_lds) lds = max_lds - stat;
   return coop ? hipLaunchCooperativeKernel(fn, grid, block, args, lds, st)
               : hipLaunchKernel(fn, grid, block, args, lds, st);
 }

@@ -600,15 +600,11 @@ def test_gru_presplit_backward(dev, n, h, bidir, monkeypatch):
            dict(base, DS2_GRU_X6_BWD="1", DS2_GRU_X6_BWD_WAVES="8"),
            dict(base, DS2_GRU_X6_BWD="2", DS2_GRU_X6_BWD_WAVES="8"),
            dict(base, DS2_GRU_X6_BWD="1", DS2_GRU_X6_BWD_WAVES="4"),
-           dict(base, DS2_GRU_X6_BWD="2", DS2_GRU_X6_BWD_WAVES="4"),
-           # the sentinel ring over pre-split runs (no drain, no flag)
-           dict(base, DS2_GRU_X6_BWD="2", DS2_GRU_X6_BWD_WAVES="8", DS2_RNN_HANDOFF_BWD="sentinel"),
-           dict(base, DS2_GRU_X6_BWD="2", DS2_GRU_X6_BWD_WAVES="4", DS2_RNN_HANDOFF_BWD="sentinel")]
-    ref, c8, p8, c4, p4, s8, s4 = _gru_run(dev, n, 37, 40, h, nd, h + 13 * n, env, monkeypatch)
-    for r, a8, b8, a4, b4, e8, e4 in zip(ref, c8, p8, c4, p4, s8, s4):
+           dict(base, DS2_GRU_X6_BWD="2", DS2_GRU_X6_BWD_WAVES="4")]
+    ref, c8, p8, c4, p4 = _gru_run(dev, n, 37, 40, h, nd, h + 13 * n, env, monkeypatch)
+    for r, a8, b8, a4, b4 in zip(ref, c8, p8, c4, p4):
         assert torch.isfinite(b8).all() and torch.isfinite(b4).all()
         assert torch.equal(a8, b8) and torch.equal(a4, b4)
-        assert torch.equal(b8, e8) and torch.equal(b4, e4)
         _close(b8, r, 2e-5, "pre-split x6 vs fp32-MFMA backward")
         _close(b4, r, 2e-5, "pre-split x6 (4 waves) vs fp32-MFMA backward")
 
