@@ -73,6 +73,11 @@ if len(sys.argv) > 1 and sys.argv[1] == "btune":
                                    "DS2_GRU_X6_BWD_WAVES": "8", "DS2_RNN_HANDOFF_BWD": "flags"},
                 "bwd-x6w4-flags": {"DS2_GRU_X6": "1", "DS2_GRU_X6_BWD": "1",
                                    "DS2_GRU_X6_BWD_WAVES": "4", "DS2_RNN_HANDOFF_BWD": "flags"}}
+if len(sys.argv) > 1 and sys.argv[1] == "pre":
+    variants = {"bwd-f32-flags": {"DS2_GRU_X6": "1", "DS2_GRU_X6_BWD": "0",
+                                  "DS2_RNN_HANDOFF_BWD": "flags"},
+                "bwd-x6pre-w8": {"DS2_GRU_X6": "1", "DS2_GRU_X6_BWD": "2",
+                                 "DS2_GRU_X6_BWD_WAVES": "8", "DS2_RNN_HANDOFF_BWD": "flags"}}
 rounds = int(os.environ.get("AB_ROUNDS", "3"))
 variants = {f"{k}#{r}": v for r in range(rounds) for k, v in variants.items()}
 ref = None
