@@ -402,6 +402,8 @@ def main():
                        "parallelism": f"dp{world}"},
             "loss": round(final_loss, 4),
             "dp": {"process_group": distributed, "world": world,
+                   "allreduce": "ds2_allreduce_bucket" if tr.reducer.comm is not None
+                                else "torch.distributed",
                    "buckets": len(tr.reducer.buckets),
                    "bucket_mb": [round((e - s) * 4 / 2**20, 2) for s, e, _ in tr.reducer.buckets],
                    "issued_from_hooks": tr.reducer.issued_from_hooks,

@@ -24,6 +24,7 @@ inline hipStream_t as_stream(ds2_stream_t s) { return reinterpret_cast<hipStream
 
 // Records the last HIP error string for ds2_last_error().
 void set_last_error(const char* where, hipError_t e);
+void set_last_error_text(const char* where, const char* what);
 
 inline ds2_status_t launch_status(const char* where) {
   hipError_t e = hipGetLastError();

@@ -341,15 +341,115 @@ __device__ __forceinline__ void beam_wave_best(float& bs, int& bk) {
   bk = key;
 }
 
-template <int BM, int CM>
+// Word n-gram LM of the beam search (ctcdecode's KenLM Scorer, decoder.py:90-99 with
+// lm_path; tables built by ds2amd/lm.py from an ARPA file, oracle/ctc_beam_lm.py restates
+// the semantics).  n-gram hash table: 32-byte records {w0..w5, log10 prob, log10 backoff}
+// (ids -1 padded, w0 = -1 = empty slot), FNV-1a + avalanche, linear probing; vocabulary
+// trie: dnext [S][C] arcs, dmask [S] the arcs as a char bit mask, dword [S] the word a
+// state spells (-1 none); state 0 = start, fstate = after a word's space (no arcs).
+struct BeamLm {
+  const int* dnext;
+  const unsigned long long* dmask;
+  const int* dword;
+  const int4* tab;
+  unsigned tmask;
+  int fstate, order, start, space;
+  double alpha, beta;
+};
+
+constexpr int LM_MAX_ORDER = 6;
+
+__device__ __forceinline__ unsigned lm_hash(const int* k) {
+  unsigned h = 2166136261u;
+#pragma unroll
+  for (int i = 0; i < LM_MAX_ORDER; ++i) h = (h ^ static_cast<unsigned>(k[i])) * 16777619u;
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
+  return h;
+}
+
+__device__ __noinline__ bool lm_find(const BeamLm& L, const int* k, float& prob, float& bo) {
+  unsigned s = lm_hash(k) & L.tmask;
+  for (unsigned p = 0; p <= L.tmask; ++p) {
+    const int4 a = L.tab[2 * s], b = L.tab[2 * s + 1];
+    if (a.x == -1) return false;
+    if (a.x == k[0] && a.y == k[1] && a.z == k[2] && a.w == k[3] && b.x == k[4] && b.y == k[5]) {
+      prob = __int_as_float(b.z);
+      bo = __int_as_float(b.w);
+      return true;
+    }
+    s = (s + 1) & L.tmask;
+  }
+  return false;
+}
+
+// float(alpha * ln p(w | hist)) -- get_log_cond_prob(make_ngram(prefix)) * alpha; hist holds
+// the order-1 preceding words, oldest first ("<s>" padded).  KenLM back-off: the longest
+// n-gram ending in w gives the log10 prob, then the backoffs of every longer context
+// suffix in the model are added (float32, shorter context first); an unknown word (w < 0:
+// the partial word spells no vocabulary word) is OOV_SCORE = -1000.
+__device__ __noinline__ float lm_term(const BeamLm& L, const int* hist, int w) {
+  const int n1 = L.order - 1;
+  double lnp = -1000.0;
+  if (w >= 0) {
+    int key[LM_MAX_ORDER];
+    float p = 0.f, bo = 0.f;
+    int m = L.order;
+    bool found = false;
+    for (; m >= 1; --m) {
+#pragma unroll
+      for (int i = 0; i < LM_MAX_ORDER; ++i)
+        key[i] = i < m - 1 ? hist[n1 - (m - 1) + i] : (i == m - 1 ? w : -1);
+      if (lm_find(L, key, p, bo)) {
+        found = true;
+        break;
+      }
+    }
+    if (found) {
+      for (int ln = m; ln <= n1; ++ln) {
+#pragma unroll
+        for (int i = 0; i < LM_MAX_ORDER; ++i) key[i] = i < ln ? hist[n1 - ln + i] : -1;
+        float pp, b;
+        if (lm_find(L, key, pp, b)) p += b;
+      }
+      lnp = static_cast<double>(p) / static_cast<double>(0.4342944819f);   // NUM_FLT_LOGE
+    }
+  }
+  return static_cast<float>(lnp * L.alpha);
+}
+
+// log_p += score; log_p += beta (float, then a double add rounded to float)
+__device__ __forceinline__ float lm_add(float v, float term, double beta) {
+  return static_cast<float>(static_cast<double>(v + term) + beta);
+}
+
+// wave minimum (every lane gets it)
+__device__ __forceinline__ float wave_min(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = fminf(v, __shfl_xor(v, o));
+  return v;
+}
+
+template <int BM, int CM, bool LM>
 __global__ __launch_bounds__(64) void ctc_beam_kernel(
     const float* __restrict__ probs, int t_max, int C, int64_t stride_n, int64_t stride_t,
     const int* __restrict__ sizes, int blank, int beam, int cutoff_top_n, double cutoff_prob,
     int top_paths, int* __restrict__ node_parent, int* __restrict__ node_ch,
     int* __restrict__ node_ts, float* __restrict__ node_lpc, int64_t node_cap,
     int* __restrict__ out_ids, int* __restrict__ out_ts, int* __restrict__ out_lens,
-    float* __restrict__ out_scores) {
+    float* __restrict__ out_scores, BeamLm L) {
   constexpr int EPL = (BM + 63) / 64;   // beam entries per lane
+  // LM state per beam entry: trie state, the order-1 preceding words, the cached
+  // alpha-scaled LM score of the entry's current word (used by a space extension and by
+  // the final scoring); per frame the char an entry's dictionary reset consumes and its
+  // valid-extension mask
+  constexpr int LB = LM ? BM : 1;
+  __shared__ int b_dst[2][LB];
+  __shared__ int b_hist[2][LB][LM_MAX_ORDER - 1];
+  __shared__ float b_lms[2][LB];
+  __shared__ int cstar[LB];
+  __shared__ unsigned long long vmask[LB];
   __shared__ float lp[CM];
   __shared__ int allowed[CM];
   __shared__ int order[CM];
@@ -385,6 +485,11 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
     par[0] = -1; chr[0] = -1; tst[0] = -1; lpcv[0] = -INFINITY;
     s_nb = 1;
     s_nodes = 1;
+    if constexpr (LM) {
+      b_dst[0][0] = 0;
+      for (int h = 0; h < LM_MAX_ORDER - 1; ++h) b_hist[0][0][h] = L.start;
+      b_lms[0][0] = 0.f;
+    }
   }
   __syncthreads();
   int cur = 0;
@@ -457,6 +562,46 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
       const int e = lane + 64 * q;
       if (e < nb && pidx[e] >= 0) child_of[pidx[e] * C + b_last[cur][e]] = static_cast<signed char>(e);
     }
+    // ---- LM: the scorer's pruning bound (min_cutoff = worst beam score + log p_blank -
+    // max(0, beta), applied once the beam is full), the dictionary reset of post-space
+    // entries (their first attempted non-blank char is rejected and the trie state goes
+    // back to the start) and each entry's valid-extension mask
+    float mincut = -INFINITY;
+    bool full = false;
+    if constexpr (LM) {
+      float wv = INFINITY;
+      for (int e = lane; e < nb; e += 64) wv = fminf(wv, score[e]);
+      wv = wave_min(wv);
+      const double pbl = static_cast<double>(pf[blank]);
+      mincut = static_cast<float>(static_cast<double>(wv) + (pbl > 0.0 ? log(pbl) : -INFINITY) -
+                                  fmax(0.0, L.beta));
+      full = nb == beam;
+#pragma unroll
+      for (int q = 0; q < EPL; ++q) {
+        const int e = lane + 64 * q;
+        if (e < nb) {
+          const int s = b_dst[cur][e];
+          int cs = -1;
+          unsigned long long vm;
+          if (s == L.fstate) {
+            const float se = score[e];
+            for (int r = 0; r < C; ++r) {
+              const int cc = prune ? order[r] : r;
+              if (cc == blank || !allowed[cc]) continue;
+              if (!(full && lp[cc] + se < mincut)) {
+                cs = cc;
+                break;
+              }
+            }
+            vm = L.dmask[0] & ~(cs >= 0 ? (1ull << cs) : 0ull);
+          } else {
+            vm = L.dmask[s];
+          }
+          cstar[e] = cs;
+          vmask[e] = vm;
+        }
+      }
+    }
     __syncthreads();
     // ---- candidates, scored straight into registers: lane holds k = lane + 64 jj (the
     // selection below scans them there); the unrolled loop lets the LDS reads of several
@@ -479,14 +624,18 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
           const int last_i = b_last[cur][i];
           const float pb_i = b_pb[cur][i];
           float sc = -INFINITY, pb = -INFINITY, pnb = -INFINITY;
+          // with an LM a (prefix, char) pair below the pruning bound is skipped entirely
+          const float sc_i = score[i];
           if (c == blank) {
-            pb = allowed[blank] ? lp[blank] + score[i] : -INFINITY;
-            pnb = (last_i >= 0 && allowed[last_i]) ? lp[last_i] + b_pnb[cur][i] : -INFINITY;
+            pb = (allowed[blank] && !(full && lp[blank] + sc_i < mincut)) ? lp[blank] + sc_i : -INFINITY;
+            pnb = (last_i >= 0 && allowed[last_i] && !(full && lp[last_i] + sc_i < mincut))
+                      ? lp[last_i] + b_pnb[cur][i] : -INFINITY;
             const int jp = pidx[i];
-            if (jp >= 0 && allowed[last_i]) {
-              const float e = (last_i == b_last[cur][jp])
-                                  ? (b_pb[cur][jp] != -INFINITY ? lp[last_i] + b_pb[cur][jp] : -INFINITY)
-                                  : lp[last_i] + score[jp];
+            if (jp >= 0 && allowed[last_i] && !(full && lp[last_i] + score[jp] < mincut)) {
+              float e = (last_i == b_last[cur][jp])
+                            ? (b_pb[cur][jp] != -INFINITY ? lp[last_i] + b_pb[cur][jp] : -INFINITY)
+                            : lp[last_i] + score[jp];
+              if (LM && last_i == L.space) e = lm_add(e, b_lms[cur][jp], L.beta);
               pnb = beam_lse(pnb, e);
               const int nd = b_node[cur][i];
               if (lp[last_i] > b_lpc[cur][i]) {   // one blank candidate per entry: no race
@@ -496,8 +645,10 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
               }
             }
             sc = beam_lse(pb, pnb);
-          } else if (allowed[c] && child_of[k] < 0) {
-            pnb = (c == last_i) ? (pb_i != -INFINITY ? lp[c] + pb_i : -INFINITY) : lp[c] + score[i];
+          } else if (allowed[c] && child_of[k] < 0 &&
+                     (!LM || (!(full && lp[c] + sc_i < mincut) && ((vmask[i] >> c) & 1ull)))) {
+            pnb = (c == last_i) ? (pb_i != -INFINITY ? lp[c] + pb_i : -INFINITY) : lp[c] + sc_i;
+            if (LM && c == L.space) pnb = lm_add(pnb, b_lms[cur][i], L.beta);
             sc = pnb;
           }
           cpb[k] = pb;
@@ -559,6 +710,29 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
         const int before = __builtin_amdgcn_mbcnt_hi(static_cast<unsigned>(em >> 32),
                                                      __builtin_amdgcn_mbcnt_lo(static_cast<unsigned>(em), 0));
         if (e < nsel) {
+          if constexpr (LM) {
+            const int n1 = L.order - 1;
+            int si = b_dst[cur][i];
+            if (!ext) {
+              // the dictionary reset sticks to the node
+              b_dst[nxt][e] = (si == L.fstate && cstar[i] >= 0) ? 0 : si;
+              for (int h = 0; h < n1; ++h) b_hist[nxt][e][h] = b_hist[cur][i][h];
+              b_lms[nxt][e] = b_lms[cur][i];
+            } else {
+              if (si == L.fstate) si = 0;
+              if (c == L.space) {   // the space completes the word of state si
+                b_dst[nxt][e] = L.fstate;
+                for (int h = 0; h + 1 < n1; ++h) b_hist[nxt][e][h] = b_hist[cur][i][h + 1];
+                if (n1 > 0) b_hist[nxt][e][n1 - 1] = L.dword[si];
+                b_lms[nxt][e] = 0.f;
+              } else {
+                const int ns = L.dnext[(int64_t)si * C + c];
+                b_dst[nxt][e] = ns;
+                for (int h = 0; h < n1; ++h) b_hist[nxt][e][h] = b_hist[cur][i][h];
+                b_lms[nxt][e] = lm_term(L, &b_hist[cur][i][0], L.dword[ns]);
+              }
+            }
+          }
           if (!ext) {
             b_node[nxt][e] = b_node[cur][i];
             b_last[nxt][e] = b_last[cur][i];
@@ -592,8 +766,16 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
   // ---- final ranking and back-tracking (one lane per returned path)
   const int nb = s_nb;
 #pragma unroll
-  for (int q = 0; q < EPL; ++q)
-    if (lane + 64 * q < nb) score[lane + 64 * q] = beam_lse(b_pb[cur][lane + 64 * q], b_pnb[cur][lane + 64 * q]);
+  for (int q = 0; q < EPL; ++q) {
+    const int e = lane + 64 * q;
+    if (e < nb) {
+      float s = beam_lse(b_pb[cur][e], b_pnb[cur][e]);
+      // LM: the last word of every non-empty prefix not ending in a space is scored too
+      if (LM && b_node[cur][e] != 0 && b_last[cur][e] != L.space)
+        s = s + static_cast<float>(static_cast<double>(b_lms[cur][e]) + L.beta);
+      score[e] = s;
+    }
+  }
   __syncthreads();
   for (int e = lane; e < nb; e += 64) {
     int rank = 0;
@@ -831,12 +1013,12 @@ size_t ds2_ctc_beam_workspace_size(int n, int t_max, int beam) {
   return 4 * al256((size_t)n * cap * 4) + 256;
 }
 
-ds2_status_t ds2_ctc_beam_decode(const float* probs, int n, int t_max, int c, int64_t stride_n,
-                                 int64_t stride_t, const int* sizes, int blank, int beam_width,
-                                 int cutoff_top_n, double cutoff_prob, int top_paths,
-                                 int* out_ids, int* out_offsets, int* out_lens,
-                                 float* out_scores, void* ws, size_t ws_bytes,
-                                 ds2_stream_t stream) {
+static ds2_status_t beam_decode(const float* probs, int n, int t_max, int c, int64_t stride_n,
+                                int64_t stride_t, const int* sizes, int blank, int beam_width,
+                                int cutoff_top_n, double cutoff_prob, int top_paths,
+                                int* out_ids, int* out_offsets, int* out_lens,
+                                float* out_scores, void* ws, size_t ws_bytes,
+                                const BeamLm* lm, ds2_stream_t stream, const char* what) {
   if (n < 0 || t_max < 0 || c < 1 || blank < 0 || blank >= c || beam_width < 1 ||
       top_paths < 1 || top_paths > beam_width || cutoff_top_n < 1)
     return DS2_INVALID_VALUE;
@@ -852,12 +1034,60 @@ ds2_status_t ds2_ctc_beam_decode(const float* probs, int n, int t_max, int c, in
   int* chr = reinterpret_cast<int*>(w + plane);
   int* tst = reinterpret_cast<int*>(w + 2 * plane);
   float* lpc = reinterpret_cast<float*>(w + 3 * plane);
-  auto kern = small ? ctc_beam_kernel<BEAM_SMALL, BEAM_SMALL_C> : ctc_beam_kernel<BEAM_LARGE, BEAM_LARGE_C>;
+  BeamLm L{};
+  if (lm != nullptr) L = *lm;
+  auto kern = lm != nullptr
+                  ? (small ? ctc_beam_kernel<BEAM_SMALL, BEAM_SMALL_C, true>
+                           : ctc_beam_kernel<BEAM_LARGE, BEAM_LARGE_C, true>)
+                  : (small ? ctc_beam_kernel<BEAM_SMALL, BEAM_SMALL_C, false>
+                           : ctc_beam_kernel<BEAM_LARGE, BEAM_LARGE_C, false>);
   hipLaunchKernelGGL(kern, dim3(n), dim3(64), 0, as_stream(stream), probs, t_max, c,
                      stride_n, stride_t, sizes, blank, beam_width, cutoff_top_n, cutoff_prob,
                      top_paths, par, chr, tst, lpc, cap, out_ids, out_offsets, out_lens,
-                     out_scores);
-  return launch_status("ds2_ctc_beam_decode");
+                     out_scores, L);
+  return launch_status(what);
+}
+
+ds2_status_t ds2_ctc_beam_decode(const float* probs, int n, int t_max, int c, int64_t stride_n,
+                                 int64_t stride_t, const int* sizes, int blank, int beam_width,
+                                 int cutoff_top_n, double cutoff_prob, int top_paths,
+                                 int* out_ids, int* out_offsets, int* out_lens,
+                                 float* out_scores, void* ws, size_t ws_bytes,
+                                 ds2_stream_t stream) {
+  return beam_decode(probs, n, t_max, c, stride_n, stride_t, sizes, blank, beam_width,
+                     cutoff_top_n, cutoff_prob, top_paths, out_ids, out_offsets, out_lens,
+                     out_scores, ws, ws_bytes, nullptr, stream, "ds2_ctc_beam_decode");
+}
+
+ds2_status_t ds2_ctc_beam_decode_lm(const float* probs, int n, int t_max, int c, int64_t stride_n,
+                                    int64_t stride_t, const int* sizes, int blank, int beam_width,
+                                    int cutoff_top_n, double cutoff_prob, int top_paths,
+                                    int space_id, int lm_order, int start_id, double alpha,
+                                    double beta, const int* dict_next, const void* dict_mask,
+                                    const int* dict_word, int dict_states, const int* lm_table,
+                                    int64_t lm_slots, int* out_ids, int* out_offsets,
+                                    int* out_lens, float* out_scores, void* ws, size_t ws_bytes,
+                                    ds2_stream_t stream) {
+  if (space_id < 0 || space_id >= c || space_id == blank || lm_order < 1 ||
+      lm_order > LM_MAX_ORDER || start_id < 0 || dict_states < 2 || dict_next == nullptr ||
+      dict_mask == nullptr || dict_word == nullptr || lm_table == nullptr || lm_slots < 1 ||
+      (lm_slots & (lm_slots - 1)) != 0 || lm_slots > (int64_t(1) << 31) || c > 64)
+    return DS2_INVALID_VALUE;
+  BeamLm L;
+  L.dnext = dict_next;
+  L.dmask = static_cast<const unsigned long long*>(dict_mask);
+  L.dword = dict_word;
+  L.tab = reinterpret_cast<const int4*>(lm_table);
+  L.tmask = static_cast<unsigned>(lm_slots - 1);
+  L.fstate = dict_states - 1;
+  L.order = lm_order;
+  L.start = start_id;
+  L.space = space_id;
+  L.alpha = alpha;
+  L.beta = beta;
+  return beam_decode(probs, n, t_max, c, stride_n, stride_t, sizes, blank, beam_width,
+                     cutoff_top_n, cutoff_prob, top_paths, out_ids, out_offsets, out_lens,
+                     out_scores, ws, ws_bytes, &L, stream, "ds2_ctc_beam_decode_lm");
 }
 
 ds2_status_t ds2_edit_distance(const int* a_ids, int64_t a_stride, const int* a_lens,

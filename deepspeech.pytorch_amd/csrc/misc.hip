@@ -13,6 +13,10 @@ void set_last_error(const char* where, hipError_t e) {
   snprintf(g_last_error, sizeof(g_last_error), "%s: %s", where, hipGetErrorString(e));
 }
 
+void set_last_error_text(const char* where, const char* what) {
+  snprintf(g_last_error, sizeof(g_last_error), "%s: %s", where, what);
+}
+
 static inline int grid_for(int64_t work, int block) {
   int64_t g = (work + block - 1) / block;
   if (g > 2048) g = 2048;

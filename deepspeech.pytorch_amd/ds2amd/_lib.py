@@ -100,6 +100,15 @@ _PROTOS = {
     "ds2_ctc_beam_decode": (_c_int, [_vp, _c_int, _c_int, _c_int, _c_i64, _c_i64, _vp, _c_int,
                                      _c_int, _c_int, ctypes.c_double, _c_int, _vp, _vp, _vp, _vp,
                                      _vp, _sz, _vp]),
+    "ds2_ctc_beam_decode_lm": (_c_int, [_vp, _c_int, _c_int, _c_int, _c_i64, _c_i64, _vp, _c_int,
+                                        _c_int, _c_int, ctypes.c_double, _c_int, _c_int, _c_int,
+                                        _c_int, ctypes.c_double, ctypes.c_double, _vp, _vp, _vp,
+                                        _c_int, _vp, _c_i64, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
+    "ds2_comm_id_bytes": (_sz, []),
+    "ds2_comm_get_unique_id": (_c_int, [_vp]),
+    "ds2_comm_init": (_c_int, [_vp, _vp, _c_int, _c_int, _c_int]),
+    "ds2_allreduce_bucket": (_c_int, [_vp, _vp, _c_i64, _vp]),
+    "ds2_comm_destroy": (_c_int, [_vp]),
     "ds2_optim_workspace_size": (_sz, [_c_i64]),
     "ds2_grad_norm": (_c_int, [_vp, _c_i64, _vp, _vp, _sz, _vp]),
     "ds2_clip_sgd_nesterov": (_c_int, [_vp, _vp, _vp, _c_i64, _c_f, _c_f, _c_f, _vp, _vp, _vp]),

@@ -56,21 +56,25 @@ class Decoder(object):
 
 
 class BeamCTCDecoder(Decoder):
-    """CTC prefix beam search on the GPU (ds2_ctc_beam_decode), drop-in for ref
-    decoder.py:90-143 without a language model.
+    """CTC prefix beam search on the GPU (ds2_ctc_beam_decode[_lm]), drop-in for ref
+    decoder.py:90-143.
 
     Same constructor and ``decode(probs, sizes) -> (strings, offsets)`` as the
     reference, whose ctcdecode backend returns every beam: strings[n][p] /
-    offsets[n][p] for p < beam_width, best first.  KenLM scoring (lm_path, alpha,
-    beta) is not available; without an LM ctcdecode ignores alpha/beta too.
+    offsets[n][p] for p < beam_width, best first.  With ``lm_path`` (an ARPA file --
+    KenLM's text format; its binary format is not read) the search scores words with
+    the n-gram model like ctcdecode's KenLM Scorer (alpha: LM weight, beta: word bonus;
+    ds2amd/lm.py builds the device tables once); without an LM ctcdecode ignores
+    alpha/beta and so does this.
     """
 
     def __init__(self, labels, lm_path=None, alpha=0, beta=0, cutoff_top_n=40, cutoff_prob=1.0,
                  beam_width=100, num_processes=4, blank_index=0):
         super().__init__(labels, blank_index=blank_index)
+        self.scorer = None
         if lm_path is not None:
-            raise NotImplementedError("ds2amd.BeamCTCDecoder: KenLM language-model scoring is "
-                                      "not supported (lm_path must be None)")
+            from .lm import ArpaScorer
+            self.scorer = ArpaScorer(lm_path, labels, alpha, beta)
         # the device search keeps every candidate in one wave's registers:
         # beam_width <= 128 over <= 32 labels (the reference default 100 over 29), or
         # beam_width <= 32 over <= 64 labels
@@ -83,6 +87,11 @@ class BeamCTCDecoder(Decoder):
 
     def decode_raw(self, probs, sizes=None):
         """Device tensors (ids [N,P,T], offsets [N,P,T], lens [N,P], scores [N,P])."""
+        if self.scorer is not None:
+            return ops.ctc_beam_decode_lm_raw(probs, sizes, self.beam_width, self.beam_width,
+                                              self.scorer, blank=self.blank_index,
+                                              cutoff_top_n=self.cutoff_top_n,
+                                              cutoff_prob=self.cutoff_prob)
         return ops.ctc_beam_decode_raw(probs, sizes, self.beam_width, self.beam_width,
                                        blank=self.blank_index, cutoff_top_n=self.cutoff_top_n,
                                        cutoff_prob=self.cutoff_prob)

@@ -328,6 +328,38 @@ def ctc_beam_decode_raw(probs: torch.Tensor, sizes: Optional[torch.Tensor], beam
     return ids, offs, lens, scores
 
 
+def ctc_beam_decode_lm_raw(probs: torch.Tensor, sizes: Optional[torch.Tensor], beam_width: int,
+                           top_paths: int, scorer, blank: int = 0, cutoff_top_n: int = 40,
+                           cutoff_prob: float = 1.0):
+    """ctc_beam_decode_raw with a word n-gram LM (scorer: ds2amd.lm.ArpaScorer, its tables
+    on the same device).  Same outputs; scores include the LM terms."""
+    if not probs.is_cuda or probs.dtype != _F32:
+        raise _lib.Ds2Error("ctc_beam_decode_lm: expected a float32 device tensor")
+    n, t, c = probs.shape
+    if probs.stride(2) != 1:
+        probs = probs.contiguous()
+    dev = probs.device
+    if scorer.table.device != dev:
+        raise _lib.Ds2Error("ctc_beam_decode_lm: the LM tables live on another device")
+    if scorer.dict_next.shape[1] != c:
+        raise _lib.Ds2Error("ctc_beam_decode_lm: the LM was built for another label set")
+    ids = torch.empty(n, top_paths, t, device=dev, dtype=_I32)
+    offs = torch.empty(n, top_paths, t, device=dev, dtype=_I32)
+    lens = torch.empty(n, top_paths, device=dev, dtype=_I32)
+    scores = torch.empty(n, top_paths, device=dev, dtype=_F32)
+    if sizes is not None:
+        sizes = sizes.to(device=dev, dtype=_I32).contiguous()
+    ws = _ws(_lib.size("ds2_ctc_beam_workspace_size", n, t, beam_width), dev)
+    _lib.call("ds2_ctc_beam_decode_lm", probs.data_ptr(), n, t, c, probs.stride(0),
+              probs.stride(1), _p(sizes), int(blank), int(beam_width), int(cutoff_top_n),
+              float(cutoff_prob), int(top_paths), scorer.space, scorer.order, scorer.start_id,
+              scorer.alpha, scorer.beta, scorer.dict_next.data_ptr(), scorer.dict_mask.data_ptr(),
+              scorer.dict_word.data_ptr(), scorer.n_states, scorer.table.data_ptr(),
+              scorer.table_mask + 1, ids.data_ptr(), offs.data_ptr(), lens.data_ptr(),
+              scores.data_ptr(), ws.data_ptr(), ws.numel(), _stream())
+    return ids, offs, lens, scores
+
+
 def wave_aug(pcm: torch.Tensor, in_lens: torch.Tensor, op_i: torch.Tensor, op_f: torch.Tensor,
              noise: Optional[torch.Tensor], out_lens, out_stride: int, cap: int,
              check: bool = True) -> torch.Tensor:

@@ -15,6 +15,7 @@ front to back while backward is still running.
 """
 from __future__ import annotations
 
+import ctypes
 import os
 from typing import List, Optional
 
@@ -265,6 +266,62 @@ def rccl_channel_cap() -> int:
         return 32
 
 
+class _StreamDone:
+    """Completion of a collective enqueued on a side stream: ``wait()`` makes the current
+    stream wait for it (no host sync), like an async torch.distributed work handle."""
+
+    def __init__(self, event: torch.cuda.Event):
+        self.event = event
+
+    def wait(self):
+        torch.cuda.current_stream().wait_event(self.event)
+
+
+class RcclComm:
+    """``ds2_comm_t``: this rank's RCCL communicator created through the C ABI
+    (ds2_comm_get_unique_id on rank 0, the id carried to every rank by
+    torch.distributed, ds2_comm_init), and ``all_reduce_async`` = ds2_allreduce_bucket
+    on a dedicated communication stream ordered after the current stream's work so far
+    (SURVEY §8b allreduce_bucket; replaces DDP's NCCL all-reduce, train.py:947-951)."""
+
+    def __init__(self, group=None, device=None):
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        dev = torch.device("cuda") if device is None else torch.device(device)
+        if dev.index is None:
+            dev = torch.device("cuda", torch.cuda.current_device())
+        nbytes = _lib.size("ds2_comm_id_bytes")
+        uid = torch.zeros(nbytes, dtype=torch.uint8)
+        if self.rank == 0:
+            buf = ctypes.create_string_buffer(nbytes)
+            _lib.call("ds2_comm_get_unique_id", ctypes.addressof(buf))
+            uid = torch.frombuffer(bytearray(buf.raw), dtype=torch.uint8).clone()
+        t = uid.to(dev) if dist.get_backend(group) == "nccl" else uid
+        src = dist.get_global_rank(group, 0) if group is not None else 0
+        dist.broadcast(t, src, group=group)
+        idbuf = ctypes.create_string_buffer(t.cpu().numpy().tobytes(), nbytes)
+        self.handle = ctypes.c_void_p()
+        _lib.call("ds2_comm_init", ctypes.addressof(self.handle), ctypes.addressof(idbuf),
+                  self.world, self.rank, dev.index)
+        self.stream = torch.cuda.Stream(dev)
+
+    def all_reduce_async(self, bucket: torch.Tensor) -> _StreamDone:
+        """In-place SUM of one contiguous fp32 bucket across the ranks."""
+        ready = torch.cuda.Event()
+        ready.record()
+        self.stream.wait_event(ready)
+        _lib.call("ds2_allreduce_bucket", self.handle.value, bucket.data_ptr(), bucket.numel(),
+                  self.stream.cuda_stream)
+        done = torch.cuda.Event()
+        done.record(self.stream)
+        return _StreamDone(done)
+
+    def close(self):
+        if self.handle.value:
+            _lib.call("ds2_comm_destroy", self.handle.value)
+            self.handle = ctypes.c_void_p()
+
+
 class GradAllReducer:
     """Bucketed gradient all-reduce (SUM, then /world) overlapped with backward.
 
@@ -282,9 +339,11 @@ class GradAllReducer:
     wait, no host sync), so a collective never holds CUs a spinning recurrence needs.
     """
 
-    def __init__(self, flat: FlatParams, bucket_mb: float = 40.0, group=None):
+    def __init__(self, flat: FlatParams, bucket_mb: float = 40.0, group=None,
+                 comm: Optional[RcclComm] = None):
         self.flat = flat
         self.group = group
+        self.comm = comm     # None: torch.distributed; else ds2_allreduce_bucket
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         cap = int(bucket_mb * 1024 * 1024 / 4)
         self.buckets = []          # (start, end, n_params) element ranges
@@ -330,9 +389,13 @@ class GradAllReducer:
         self.pending[b] -= 1
         if self.pending[b] == 0:
             s, e, _ = self.buckets[b]
-            self.handles[b] = dist.all_reduce(self.flat.grad[s:e], group=self.group,
-                                              async_op=True)
+            self.handles[b] = self._all_reduce(self.flat.grad[s:e])
             self.issued_from_hooks += 1
+
+    def _all_reduce(self, bucket):
+        if self.comm is not None:
+            return self.comm.all_reduce_async(bucket)
+        return dist.all_reduce(bucket, group=self.group, async_op=True)
 
     def guard_cooperative(self, grid: int):
         if self.world <= 1 or self.cus <= 0:
@@ -351,7 +414,7 @@ class GradAllReducer:
         for b, h in enumerate(self.handles):
             if h is None:     # a bucket whose params received no gradient this step
                 s, e, _ = self.buckets[b]
-                h = dist.all_reduce(self.flat.grad[s:e], group=self.group, async_op=True)
+                h = self._all_reduce(self.flat.grad[s:e])
             h.wait()
         if self.world > 1:
             self.flat.grad.mul_(1.0 / self.world)

@@ -28,7 +28,7 @@ from . import _lib, ops
 from .ctc import CTCLoss
 from .decoder import GreedyDecoder
 from .ops import _stream
-from .optim import FlatParams, FusedSGD, GradAllReducer, ParamBroadcaster
+from .optim import FlatParams, FusedSGD, GradAllReducer, ParamBroadcaster, RcclComm
 
 
 def reduce_tensor(tensor, world_size):
@@ -110,7 +110,13 @@ class Trainer:
             if hasattr(m, 'weight_ih_l0_reverse')]
         self.flat = FlatParams(list(self.model.parameters()), self.device, adjacent=pairs)
         self.optimizer = FusedSGD(self.flat, lr=lr, momentum=momentum, max_norm=max_norm)
-        self.reducer = GradAllReducer(self.flat, bucket_mb=bucket_mb, group=group)
+        # DS2_ALLREDUCE=ds2: the buckets go through the library's own RCCL communicator
+        # (ds2_comm_init / ds2_allreduce_bucket) instead of torch.distributed's
+        comm = None
+        if (dist.is_initialized() and self.device.type == "cuda"
+                and os.environ.get("DS2_ALLREDUCE", "torch") == "ds2"):
+            comm = RcclComm(group, self.device)
+        self.reducer = GradAllReducer(self.flat, bucket_mb=bucket_mb, group=group, comm=comm)
         self.world = self.reducer.world
         # DDP: rank 0's parameters and buffers everywhere (construction), rank 0's BN running
         # statistics before every forward (broadcast_buffers, train.py:950-951)

@@ -361,6 +361,47 @@ ds2_status_t ds2_ctc_beam_decode(const float* probs, int n, int t_max, int c, in
                                  float* out_scores, void* ws, size_t ws_bytes,
                                  ds2_stream_t stream);
 
+/* The same search with a word n-gram language model: BeamCTCDecoder(labels, lm_path,
+ * alpha, beta, ...) (decoder.py:90-99 -> ctcdecode's KenLM Scorer; opts.py:6-10
+ * --lm-path / --alpha / --beta).  A space extension adds float(alpha * ln p(word |
+ * preceding order-1 words, "<s>" padded)) and beta; extensions follow the vocabulary
+ * trie; once the beam is full a (prefix, char) below worst + log p_blank - max(0, beta)
+ * is skipped; the last partial word is scored after the final frame
+ * (oracle/ctc_beam_lm.py restates it).  Tables (device memory, ds2amd/lm.py builds them
+ * from an ARPA file): dict_next int32 [dict_states][c] trie arcs (-1 none; state 0 =
+ * start, dict_states-1 = after a word's space), dict_mask uint64 [dict_states] the arcs
+ * as char bits, dict_word int32 [dict_states] the word id a state spells (-1 none);
+ * lm_table int32 [lm_slots][8] {w0..w5 (-1 padded), log10 prob bits, log10 backoff
+ * bits}, w0 = -1 marks an empty slot, FNV-1a over w0..w5 + avalanche, linear probing,
+ * lm_slots a power of two.  lm_order <= 6; start_id = the id of "<s>"; c <= 64.
+ * Same outputs and workspace as ds2_ctc_beam_decode (scores include the LM terms). */
+ds2_status_t ds2_ctc_beam_decode_lm(const float* probs, int n, int t_max, int c, int64_t stride_n,
+                                    int64_t stride_t, const int* sizes, int blank, int beam_width,
+                                    int cutoff_top_n, double cutoff_prob, int top_paths,
+                                    int space_id, int lm_order, int start_id, double alpha,
+                                    double beta, const int* dict_next, const void* dict_mask,
+                                    const int* dict_word, int dict_states, const int* lm_table,
+                                    int64_t lm_slots, int* out_ids, int* out_offsets,
+                                    int* out_lens, float* out_scores, void* ws, size_t ws_bytes,
+                                    ds2_stream_t stream);
+
+/* ------------------------------------------------------------------------ */
+/* Data-parallel gradient exchange over RCCL (SURVEY §8b allreduce_bucket /
+ * ds2_comm_t; replaces DistributedDataParallel's bucketed all-reduce, train.py:947-951).
+ * Rank 0 makes an id (ds2_comm_id_bytes() bytes), the caller carries it to every
+ * rank (torch.distributed or a file), each rank creates its communicator on its GPU;
+ * ds2_allreduce_bucket sums one contiguous fp32 bucket in place across the ranks,
+ * enqueued on `stream` (no averaging: the caller scales once after the last bucket).
+ * RCCL is loaded at run time (librccl.so.1); DS2_RCCL_ERROR with ds2_last_error()
+ * when it is missing or a collective fails.                                      */
+typedef struct ds2_comm* ds2_comm_t;
+size_t ds2_comm_id_bytes(void);
+ds2_status_t ds2_comm_get_unique_id(void* id_out);
+ds2_status_t ds2_comm_init(ds2_comm_t* comm, const void* id, int nranks, int rank, int device);
+ds2_status_t ds2_allreduce_bucket(ds2_comm_t comm, float* bucket, int64_t count,
+                                  ds2_stream_t stream);
+ds2_status_t ds2_comm_destroy(ds2_comm_t comm);
+
 /* ------------------------------------------------------------------------ */
 /* Training-step tail (ref train.py:595-632): clip_grad_norm_(max_norm) then
  * SGD(momentum, nesterov) on flat fp32 buffers.  The global L2 norm is reduced

@@ -3,6 +3,8 @@
 Tolerances (fp32 kernels): relative to the magnitude of the result, 1e-5..1e-4;
 integer/index outputs (greedy decode, lengths) bit-exact.
 """
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -97,6 +99,37 @@ def test_sgemm_x6_is_fp32_accurate(dev, ta, tb, m, n, k, monkeypatch):
                   ldb=b.shape[1], ldc=n)
         errs[mode] = (c.double() - ref).abs().max().item() / scale
     assert errs["1"] <= 2.5 * errs["0"] and errs["1"] < 5e-6, errs
+
+
+@pytest.mark.parametrize("ta,tb", [(0, 1), (1, 0)])
+def test_sgemm_x6_nonfinite_operands(dev, ta, tb, monkeypatch):
+    """Bad-data semantics of the bf16x6 split: an inf operand splits into
+    hi = inf and NaN residual terms, so its products are NaN where fp32 gives +-inf (or
+    NaN).  Pinned here: the set of non-finite outputs equals the fp32-MFMA kernel's
+    (DS2_GEMM_X6=0) and every finite output still matches it -- the NaN guard of the step
+    sees the same rows either way.  (Finite values within 0.4 % of FLT_MAX round to a
+    bf16 inf and are the one case where a finite fp32 result turns non-finite.)"""
+    m, n, k = 256, 160, 96
+    g = torch.Generator().manual_seed(11)
+    a = torch.randn(k, m, generator=g) if ta else torch.randn(m, k, generator=g)
+    b = torch.randn(n, k, generator=g) if tb else torch.randn(k, n, generator=g)
+    if ta:
+        a[5, 7] = float('inf'); a[9, 100] = float('-inf'); a[3, 40] = float('nan')
+    else:
+        a[7, 5] = float('inf'); a[100, 9] = float('-inf'); a[40, 3] = float('nan')
+    b[2, 3] = float('inf')
+    a, b = a.to(dev), b.to(dev)
+    out = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("DS2_GEMM_X6", mode)
+        c = torch.empty(m, n, device=dev)
+        ops.sgemm(a, b, c, m=m, n=n, k=k, trans_a=bool(ta), trans_b=bool(tb), lda=a.shape[1],
+                  ldb=b.shape[1], ldc=n)
+        out[mode] = c.cpu()
+    bad1, bad0 = ~torch.isfinite(out["1"]), ~torch.isfinite(out["0"])
+    assert bad0.any() and torch.equal(bad1, bad0)
+    fin = ~bad0
+    assert (out["1"][fin] - out["0"][fin]).abs().max().item() <= 1e-4 * out["0"][fin].abs().max().item()
 
 
 @pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
@@ -1115,6 +1148,71 @@ def test_ctc_beam_hand_case_and_decoder(dev):
         assert len(strings[n]) == 100
         for q, (_, rid, _) in enumerate(paths):
             assert strings[n][q] == ''.join(orc.LABELS[i] for i in rid), (n, q)
+
+
+def _spelled(text, g, noise, peak=5.0, blank_bias=1.0):
+    labels = orc.LABELS
+    frames, prev = [], None
+    for ch in text:
+        if ch == prev:
+            frames.append(0)
+        frames += [labels.index(ch), 0]
+        prev = ch
+    logits = g.standard_normal((len(frames), len(labels))).astype(np.float32) * noise
+    logits[:, 0] += blank_bias
+    logits[np.arange(len(frames)), frames] += peak
+    p = np.exp(logits - logits.max(-1, keepdims=True))
+    return (p / p.sum(-1, keepdims=True)).astype(np.float32)
+
+
+@pytest.mark.parametrize("beam,top_n,cutoff,alpha,beta,noise",
+                         [(8, 40, 1.0, 0.8, 1.0, 1.5), (4, 40, 1.0, 2.0, -0.5, 2.0),
+                          (16, 10, 0.99, 0.8, 1.0, 2.0), (32, 40, 1.0, 0.3, 2.0, 2.5),
+                          (100, 40, 1.0, 0.8, 1.0, 2.0), (33, 8, 1.0, 1.2, 0.5, 3.0)])
+def test_ctc_beam_lm_vs_oracle(dev, beam, top_n, cutoff, alpha, beta, noise):
+    """ds2_ctc_beam_decode_lm (BeamCTCDecoder with lm_path) == oracle/ctc_beam_lm.py
+    (ctcdecode's KenLM Scorer semantics restated; ctcdecode itself is absent, parity with
+    it unpinned) on the committed 3-gram tests/golden/tiny_lm.arpa: ids, char frames and
+    lengths of every returned beam bit-exact, scores to 1e-5 rel.  Noisy spelled
+    sentences (word boundaries, back-off chains, words outside the vocabulary), sizes 0
+    and 1, both kernel sizes (beams <= 32 and the 128-entry kernel)."""
+    from oracle import ctc_beam_lm as obl
+    from ds2amd.lm import ArpaScorer
+    path = os.path.join(os.path.dirname(__file__), "golden", "tiny_lm.arpa")
+    labels = orc.LABELS
+    g = np.random.default_rng(beam * 7 + top_n)
+    texts = ["THE CAT SAT ", "I DON'T NO ", "AND THEY SAT ON A HAT", "CATS IN THEN"]
+    ps = [_spelled(s, g, noise) for s in texts]
+    t = max(p.shape[0] for p in ps)
+    probs = np.full((len(ps) + 2, t, len(labels)), 1.0 / len(labels), np.float32)
+    for i, p in enumerate(ps):
+        probs[i, :p.shape[0]] = p
+    sizes = [p.shape[0] for p in ps] + [0, 1]
+    scorer = ArpaScorer(path, labels, alpha, beta, device=dev)
+    ids, offs, lens, scores = ops.ctc_beam_decode_lm_raw(
+        torch.from_numpy(probs).to(dev), torch.tensor(sizes, dtype=torch.int32).to(dev), beam,
+        beam, scorer, cutoff_top_n=top_n, cutoff_prob=cutoff)
+    ids, offs, lens, scores = ids.cpu(), offs.cpu(), lens.cpu(), scores.cpu()
+    lm = obl.ArpaLM(path)
+    ref = obl.beam_decode_lm(probs, sizes, beam, lm, labels, alpha, beta, cutoff_top_n=top_n,
+                             cutoff_prob=cutoff)
+    for n, paths in enumerate(ref):
+        for p in range(beam):
+            if p >= len(paths):
+                assert int(lens[n, p]) == 0
+                continue
+            s, rid, rts = paths[p]
+            k = int(lens[n, p])
+            assert ids[n, p, :k].tolist() == rid, (n, p, ids[n, p, :k].tolist(), rid)
+            assert offs[n, p, :k].tolist() == rts, (n, p)
+            assert abs(float(scores[n, p]) - s) <= 1e-5 * max(1.0, abs(s)), (n, p)
+    # the decoder front end: lm_path -> the same best strings
+    from ds2amd.decoder import BeamCTCDecoder
+    dec = BeamCTCDecoder(labels, lm_path=path, alpha=alpha, beta=beta, cutoff_top_n=top_n,
+                         cutoff_prob=cutoff, beam_width=beam)
+    strings, _ = dec.decode(torch.from_numpy(probs).to(dev), torch.tensor(sizes, dtype=torch.int32))
+    for n, paths in enumerate(ref):
+        assert strings[n][0] == ''.join(labels[i] for i in paths[0][1])
 
 
 # ---------------------------------------------------------------------------- CER / WER

@@ -228,12 +228,17 @@ def test_resume_from_reference_package(dev, golden_dir):
 
 
 # --------------------------------------------------------------------------- data parallel
-def test_world1_nccl_trainer_hooks_and_bit_identity(dev, golden_dir, tmp_path):
+@pytest.mark.parametrize("allreduce", ["torch", "ds2"])
+def test_world1_nccl_trainer_hooks_and_bit_identity(dev, golden_dir, tmp_path, monkeypatch,
+                                                    allreduce):
     """The DS2 Trainer under a world-1 RCCL ('nccl') process group: every gradient bucket's
     all-reduce is issued from the post-accumulate hooks during backward, the reduced
     gradients (HIP gradient slots in the flat buffer) are bit-identical to the
-    no-process-group Trainer's, and the step is the same."""
+    no-process-group Trainer's, and the step is the same.  allreduce='ds2': the buckets go
+    through the C ABI's own RCCL communicator (ds2_comm_init / ds2_allreduce_bucket on a
+    side stream) instead of torch.distributed."""
     import torch.distributed as dist
+    monkeypatch.setenv("DS2_ALLREDUCE", allreduce)
     g = np.load(os.path.join(golden_dir, 'tiny_ds2.npz'))
 
     def data():
@@ -249,10 +254,14 @@ def test_world1_nccl_trainer_hooks_and_bit_identity(dev, golden_dir, tmp_path):
     try:
         tr = Trainer(_build(int(g['seed']), 16, 2), LABELS, device=dev, bucket_mb=0.05)
         assert len(tr.reducer.buckets) > 1 and tr.reducer._hooks
+        assert (tr.reducer.comm is not None) == (allreduce == "ds2")
         tr.train_batch(data(), return_item=True)
         assert tr.reducer.issued_from_hooks == len(tr.reducer.buckets)
         assert torch.equal(tr.flat.grad, ref_grad)
         assert torch.equal(tr.flat.flat, ref_params)
+        if tr.reducer.comm is not None:
+            torch.cuda.synchronize()
+            tr.reducer.comm.close()
     finally:
         ops.set_cooperative_guard(None)
         dist.destroy_process_group()

@@ -1,0 +1,190 @@
+"""CPU tests of the LM beam-search pieces: the KenLM back-off restatement on hand-made
+ARPA models (known answers), the device tables ds2amd/lm.py builds (hash table and
+vocabulary trie, queried here exactly as the kernel queries them) against the oracle,
+and the oracle's LM beam search on spelled inputs."""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import ctc_beam_lm as obl
+from oracle.ds2_oracle import LABELS
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+TINY_LM = os.path.join(HERE, "golden", "tiny_lm.arpa")
+
+HAND_ARPA = """
+\\data\\
+ngram 1=5
+ngram 2=2
+ngram 3=1
+
+\\1-grams:
+-99\t<s>\t-0.5
+-1.0\tA\t-0.3
+-1.2\tB\t-0.2
+-1.5\t</s>
+-2.0\t<unk>
+
+\\2-grams:
+-0.4\t<s> A\t-0.1
+-0.3\tA B\t-0.05
+
+\\3-grams:
+-0.2\t<s> A B
+
+\\end\\
+"""
+
+
+@pytest.fixture()
+def hand_lm(tmp_path):
+    p = tmp_path / "hand.arpa"
+    p.write_text(HAND_ARPA)
+    return str(p)
+
+
+def test_arpa_backoff_known_answers(hand_lm):
+    """KenLM BaseScore semantics (ARPA back-off), by hand:
+    p(B | <s> A) = trigram -0.2; p(A | A B) = p(A) + bo(B) + bo(A B) = -1.0 - 0.2 - 0.05;
+    p(B | B A) = p(B | A) = -0.3 (the context 'B A' is not in the model: no backoff);
+    p(A | <s> <s>) = p(A | <s>) = -0.4; an OOV word anywhere -> None (OOV_SCORE)."""
+    lm = obl.ArpaLM(hand_lm)
+    assert lm.order == 3
+    f = np.float32
+    assert lm.cond_log10(("<s>", "A", "B")) == f(-0.2)
+    assert lm.cond_log10(("A", "B", "A")) == f(f(f(-1.0) + f(-0.2)) + f(-0.05))
+    assert lm.cond_log10(("B", "A", "B")) == f(-0.3)
+    assert lm.cond_log10(("<s>", "<s>", "A")) == f(-0.4)
+    assert lm.cond_log10(("<s>", "<s>", "B")) == f(f(-1.2) + f(-0.5))
+    assert lm.cond_log10(("<s>", "C", "A")) is None
+    t = obl.lm_term(lm, ("<s>", "A"), "B", 0.8)
+    assert t == np.float32(-0.2 / float(np.float32(0.4342944819)) * 0.8)
+    assert obl.lm_term(lm, ("<s>", "A"), None, 0.8) == np.float32(-800.0)
+
+
+def _table_lookup(tab, key):
+    """The kernel's lm_find: FNV-1a + avalanche, linear probing, w0 = -1 empty."""
+    from ds2amd.lm import _hash
+    mask = tab.shape[0] - 1
+    s = int(_hash(np.asarray([key], np.int32))[0]) & mask
+    while True:
+        row = tab[s]
+        if row[0] == -1:
+            return None
+        if list(row[:6]) == list(key):
+            return row[6:8].view(np.float32)
+        s = (s + 1) & mask
+
+
+def _device_cond(tab, order, hist, w):
+    """The kernel's lm_term before the ln / alpha scaling (log10, float32)."""
+    n1 = order - 1
+    for m in range(order, 0, -1):
+        key = [hist[n1 - (m - 1) + i] if i < m - 1 else (w if i == m - 1 else -1) for i in range(6)]
+        r = _table_lookup(tab, key)
+        if r is not None:
+            p = np.float32(r[0])
+            break
+    else:
+        return None
+    for ln in range(m, n1 + 1):
+        key = [hist[n1 - ln + i] if i < ln else -1 for i in range(6)]
+        r = _table_lookup(tab, key)
+        if r is not None:
+            p = np.float32(p + np.float32(r[1]))
+    return p
+
+
+@pytest.mark.parametrize("which", ["hand", "tiny"])
+def test_device_tables_match_oracle(which, hand_lm):
+    """ds2amd/lm.py's hash table, queried the kernel's way, gives the oracle's KenLM
+    score for every (two-word history, word) over the vocabulary."""
+    from ds2amd import lm as dlm
+    path = hand_lm if which == "hand" else TINY_LM
+    vocab, order, keys, prob, bo = dlm.read_arpa(path)
+    tab = dlm.build_table(keys, prob, bo)
+    assert tab.shape[0] >= 4 * keys.shape[0] and (tab[:, 0] >= 0).sum() == keys.shape[0]
+    olm = obl.ArpaLM(path)
+    assert olm.vocab == vocab and olm.order == order == 3
+    ctx = ["<s>"] + [w for w in vocab if w not in ("<s>", "</s>", "<unk>")]
+    n = 0
+    for a in ctx:
+        for b in ctx:
+            for w in vocab:
+                if w == "<s>":
+                    continue
+                ref = olm.cond_log10((a, b, w))
+                got = _device_cond(tab, order, [vocab.index(a), vocab.index(b)], vocab.index(w))
+                assert ref == got, (a, b, w, ref, got)
+                n += 1
+    assert n >= 36
+
+
+def test_dictionary_tables():
+    """The vocabulary trie: words spelled over the labels only, the space arc after
+    every complete word, nothing after the space; the mask mirrors the arcs."""
+    from ds2amd import lm as dlm
+    vocab, *_ = dlm.read_arpa(TINY_LM)
+    space = LABELS.index(" ")
+    nxt, mask, word = dlm.build_dictionary(vocab, LABELS, space)
+    wd = obl.WordDict(vocab, LABELS, space)
+    assert nxt.shape == (len(wd.next), len(LABELS))
+    m64 = mask[:, 0].astype(np.uint64) | (mask[:, 1].astype(np.uint64) << np.uint64(32))
+
+    def spell(w):
+        s = 0
+        for ch in w:
+            s = int(nxt[s, LABELS.index(ch)])
+            if s < 0:
+                return None
+        return s
+
+    for w in vocab:
+        s = spell(w) if all(ch in LABELS for ch in w) else None
+        if w in ("<s>", "</s>", "<unk>", "café"):
+            assert s is None
+            continue
+        assert word[s] == vocab.index(w)
+        f = nxt[s, space]
+        assert f == nxt.shape[0] - 1 and (nxt[f] < 0).all()
+    assert int(nxt[0, space]) < 0 and spell("CA") is not None and word[spell("CA")] == -1
+    for s in range(nxt.shape[0]):
+        bits = sum(1 << c for c in range(len(LABELS)) if nxt[s, c] >= 0)
+        assert int(m64[s]) == bits
+
+
+def spelled_probs(text, g, noise=1.0, peak=5.0, blank_bias=1.0):
+    """[T, C] probs that spell `text` (one frame per char, blanks between repeats and
+    around words) plus Gaussian logit noise."""
+    frames = []
+    prev = None
+    for ch in text:
+        if ch == prev:
+            frames.append(0)
+        frames.append(LABELS.index(ch))
+        frames.append(0)
+        prev = ch
+    t = len(frames)
+    logits = g.standard_normal((t, len(LABELS))).astype(np.float32) * noise
+    logits[:, 0] += blank_bias
+    logits[np.arange(t), frames] += peak
+    p = np.exp(logits - logits.max(-1, keepdims=True))
+    return (p / p.sum(-1, keepdims=True)).astype(np.float32)
+
+
+def test_lm_beam_oracle_spelled_sentence():
+    """With clean spelled inputs the LM search returns the sentence; with a misspelled
+    word the dictionary keeps every returned prefix inside the vocabulary."""
+    lm = obl.ArpaLM(TINY_LM)
+    g = np.random.default_rng(3)
+    p = spelled_probs("THE CAT SAT ", g, noise=0.5)
+    res = obl.beam_decode_lm_one(p, p.shape[0], 8, lm, LABELS, alpha=0.8, beta=1.0)
+    assert "".join(LABELS[i] for i in res[0][1]) == "THE CAT SAT "
+    p = spelled_probs("THE CQT ", g, noise=0.5)
+    res = obl.beam_decode_lm_one(p, p.shape[0], 8, lm, LABELS, alpha=0.8, beta=1.0)
+    words = set(w for w in lm.vocab)
+    for _, ids, _ in res:
+        s = "".join(LABELS[i] for i in ids)
+        for w in s.split(" ")[:-1]:
+            assert w in words, s
