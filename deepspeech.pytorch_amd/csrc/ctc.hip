@@ -276,8 +276,8 @@ __global__ void greedy_kernel(const float* __restrict__ probs, int n, int t_max,
 
 
 // ---------------------------------------------------------------------------
-// CTC prefix beam search without a language model (BeamCTCDecoder, decoder.py:90-143,
-// wrapping ctcdecode's ctc_beam_search_decoder with lm_path=None).  One 64-lane
+// CTC prefix beam search (BeamCTCDecoder, decoder.py:90-143, wrapping ctcdecode's
+// ctc_beam_search_decoder; LM = true adds its KenLM Scorer, see BeamLm below).  One 64-lane
 // workgroup per utterance; the beam (<= 128 prefixes) lives in LDS, the prefix
 // trie (parent, char, timestep, best char log-prob) in the workspace.  Per frame:
 // prune the vocabulary (cutoff_top_n / cutoff_prob), score every candidate
@@ -369,7 +369,7 @@ __device__ __forceinline__ unsigned lm_hash(const int* k) {
   return h;
 }
 
-__device__ __noinline__ bool lm_find(const BeamLm& L, const int* k, float& prob, float& bo) {
+__device__ __forceinline__ bool lm_find(const BeamLm& L, const int* k, float& prob, float& bo) {
   unsigned s = lm_hash(k) & L.tmask;
   for (unsigned p = 0; p <= L.tmask; ++p) {
     const int4 a = L.tab[2 * s], b = L.tab[2 * s + 1];
@@ -389,7 +389,7 @@ __device__ __noinline__ bool lm_find(const BeamLm& L, const int* k, float& prob,
 // n-gram ending in w gives the log10 prob, then the backoffs of every longer context
 // suffix in the model are added (float32, shorter context first); an unknown word (w < 0:
 // the partial word spells no vocabulary word) is OOV_SCORE = -1000.
-__device__ __noinline__ float lm_term(const BeamLm& L, const int* hist, int w) {
+__device__ __forceinline__ float lm_term(const BeamLm& L, const int* hist, int w) {
   const int n1 = L.order - 1;
   double lnp = -1000.0;
   if (w >= 0) {
@@ -512,7 +512,8 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
     float pv = 0.f;
     if (lane < C) {
       pv = pf[lane];
-      lp[lane] = logf(pv + 1.17549435e-38f);
+      // ctcdecode's get_pruned_log_probs: log of the double prob + FLT_MIN, stored as float
+      lp[lane] = static_cast<float>(log(static_cast<double>(pv) + 1.1754943508222875e-38));
     }
     if (prune) {
       // rank of this lane's probability: C uniform lane reads (v_readlane), no LDS
@@ -566,16 +567,17 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
     // max(0, beta), applied once the beam is full), the dictionary reset of post-space
     // entries (their first attempted non-blank char is rejected and the trie state goes
     // back to the start) and each entry's valid-extension mask
-    float mincut = -INFINITY;
-    bool full = false;
+    // cut = min_cutoff once the beam is full, else -inf (nothing is below it); wave-uniform
+    float cut = -INFINITY;
     if constexpr (LM) {
       float wv = INFINITY;
       for (int e = lane; e < nb; e += 64) wv = fminf(wv, score[e]);
       wv = wave_min(wv);
       const double pbl = static_cast<double>(pf[blank]);
-      mincut = static_cast<float>(static_cast<double>(wv) + (pbl > 0.0 ? log(pbl) : -INFINITY) -
-                                  fmax(0.0, L.beta));
-      full = nb == beam;
+      const float mincut = static_cast<float>(
+          static_cast<double>(wv) + (pbl > 0.0 ? log(pbl) : -INFINITY) - fmax(0.0, L.beta));
+      cut = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(
+                                          int, nb == beam ? mincut : -INFINITY)));
 #pragma unroll
       for (int q = 0; q < EPL; ++q) {
         const int e = lane + 64 * q;
@@ -588,7 +590,7 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
             for (int r = 0; r < C; ++r) {
               const int cc = prune ? order[r] : r;
               if (cc == blank || !allowed[cc]) continue;
-              if (!(full && lp[cc] + se < mincut)) {
+              if (!(lp[cc] + se < cut)) {
                 cs = cc;
                 break;
               }
@@ -627,11 +629,11 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
           // with an LM a (prefix, char) pair below the pruning bound is skipped entirely
           const float sc_i = score[i];
           if (c == blank) {
-            pb = (allowed[blank] && !(full && lp[blank] + sc_i < mincut)) ? lp[blank] + sc_i : -INFINITY;
-            pnb = (last_i >= 0 && allowed[last_i] && !(full && lp[last_i] + sc_i < mincut))
+            pb = (allowed[blank] && !(lp[blank] + sc_i < cut)) ? lp[blank] + sc_i : -INFINITY;
+            pnb = (last_i >= 0 && allowed[last_i] && !(lp[last_i] + sc_i < cut))
                       ? lp[last_i] + b_pnb[cur][i] : -INFINITY;
             const int jp = pidx[i];
-            if (jp >= 0 && allowed[last_i] && !(full && lp[last_i] + score[jp] < mincut)) {
+            if (jp >= 0 && allowed[last_i] && !(lp[last_i] + score[jp] < cut)) {
               float e = (last_i == b_last[cur][jp])
                             ? (b_pb[cur][jp] != -INFINITY ? lp[last_i] + b_pb[cur][jp] : -INFINITY)
                             : lp[last_i] + score[jp];
@@ -646,7 +648,7 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
             }
             sc = beam_lse(pb, pnb);
           } else if (allowed[c] && child_of[k] < 0 &&
-                     (!LM || (!(full && lp[c] + sc_i < mincut) && ((vmask[i] >> c) & 1ull)))) {
+                     (!LM || (!(lp[c] + sc_i < cut) && ((vmask[i] >> c) & 1ull)))) {
             pnb = (c == last_i) ? (pb_i != -INFINITY ? lp[c] + pb_i : -INFINITY) : lp[c] + sc_i;
             if (LM && c == L.space) pnb = lm_add(pnb, b_lms[cur][i], L.beta);
             sc = pnb;

@@ -13,7 +13,8 @@ the library leaves to container iteration order:
   * vocabulary pruning per frame (get_pruned_log_probs): sort (char, prob) by prob
     descending (ties: lower index first), keep the first cutoff_top_n, and when
     cutoff_prob < 1 stop once the double cumulative prob reaches cutoff_prob;
-    log prob = float32 log(prob + FLT_MIN);
+    log prob = float(log(double(prob) + FLT_MIN)) (get_pruned_log_probs: the probs are
+    doubles there, the log is taken in double and stored as float);
   * per frame, for every beam prefix i (score_i = lse(pb_i, pnb_i)):
       blank:            pb'  = lp[blank] + score_i
       repeat last char: pnb' = lp[last] + pnb_i
@@ -38,6 +39,7 @@ import numpy as np
 F32 = np.float32
 NEG = F32(-np.inf)
 FLT_MIN = F32(np.finfo(np.float32).tiny)
+FLT_MIN_D = float(FLT_MIN)
 
 
 def lse(a: np.float32, b: np.float32) -> np.float32:
@@ -68,7 +70,7 @@ def pruned_log_probs(p: np.ndarray, cutoff_top_n: int, cutoff_prob: float):
             keep = order[:cutoff_top_n]
         allowed[:] = False
         allowed[keep] = True
-    lp = np.log((p.astype(np.float32) + FLT_MIN).astype(np.float32)).astype(np.float32)
+    lp = np.array([F32(math.log(float(x) + FLT_MIN_D)) for x in p.astype(np.float32)], np.float32)
     return allowed, lp
 
 
