@@ -364,6 +364,9 @@ def main():
                  "ms_per_step": round(avg_ms * count / args.steps, 3),
                  "achieved": round(achieved, 3), "peak": round(peak, 1), "unit": "TFLOP/s",
                  "arith": arith, "frac": round(achieved / peak, 4),
+                 # the same work against the dense fp32 MFMA peak (the dtype's own peak; the
+                 # bf16x6 kernels run their fp32 products on the bf16 engine, `frac` above)
+                 "frac_fp32_mfma_peak": round(achieved / PEAK_F32_MFMA_TFLOPS, 4),
                  "traffic": None if traffic is None else round(traffic),
                  "traffic_unit": "bytes/launch (HBM, PMC)", "traffic_source": src,
                  "step_achieved_tflops": step_tf}

@@ -1391,9 +1391,11 @@ static const void* bwd_dop_fn(int need) {
 #undef DS2_BDOP
   return nullptr;
 }
+// group counters, the error word, 64 per-producer flags per group, then 64 per-producer XCC
+// ids per group (DS2_GRU_XCD)
 static inline size_t ctr_words(int n, int num_dirs) {
   const int groups = num_dirs * ((n + GB - 1) / GB);
-  return (size_t)groups + 1 + (size_t)groups * 64;
+  return (size_t)groups + 1 + (size_t)groups * 128;
 }
 static inline size_t counter_bytes(int n, int num_dirs) {
   const size_t trace = stamp_mode() == 2 ? (size_t)kTraceSteps * 1024 * 5 : 16;

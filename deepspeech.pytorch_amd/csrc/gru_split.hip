@@ -356,7 +356,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW / 4,
     const float* __restrict__ h_all, const float* __restrict__ gates,
     const int* __restrict__ lens, float* __restrict__ dgx, float* __restrict__ dgh,
     float* __restrict__ gx, unsigned* __restrict__ counters, unsigned* __restrict__ err,
-    unsigned long long* __restrict__ stamps, double* __restrict__ dbp) {
+    unsigned long long* __restrict__ stamps, double* __restrict__ dbp, int xmode) {
   static_assert(!PRE || HM == 0, "pre-split tiles use the flag hand-off");
   constexpr int RP = GU + 1;
   constexpr bool SENT = HM == 1;
@@ -370,12 +370,21 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW / 4,
   __shared__ int flag;
   __shared__ int failed;
   int ub, d, bt;
-  if (!map_work(UB * D, BT, UB, ub, d, bt)) return;
+  // xmode (PRE only): same-XCD groups -- every tile is also stored plainly into ring slots
+  // 2-3 (kept in the producer's L2) and a consumer loads the tiles of the producers that
+  // share its XCD from there
+  const bool xg = PRE && xmode != 0;
+  if (xg ? !map_work_xgrp(UB, BT, D, ub, d, bt) : !map_work(UB * D, BT, UB, ub, d, bt)) return;
   const int n0 = bt * GB;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int H3 = 3 * H;
   const int NB3 = 3 * UB;
+  unsigned* xtab = counters + (D * BT + 1) + D * BT * 64 + (d * BT + bt) * 64;
+  const unsigned my_xcc = xcc_id() + 1u;
+  if (xg && threadIdx.x == 0)   // published by the step-0 flag (wave 0 drains before it)
+    __hip_atomic_store(xtab + ub, my_xcc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  unsigned tsame = 0;           // bit i: this wave's tile t_first + i comes from this XCD
   const int pairs = (NB3 + 1) >> 1;
   const int p0 = (pairs * wave) / NW;
   const int np = (pairs * (wave + 1)) / NW - p0;   // host guarantees np <= NP
@@ -383,9 +392,10 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW / 4,
   const unsigned* gflags = counters + (D * BT + 1) + (d * BT + bt) * UB;
   unsigned* myflag = counters + (D * BT + 1) + (d * BT + bt) * UB + ub;
   const int slot_floats = D * BT * NB3 * TF;
-  const __amdgpu_buffer_rsrc_t x_rs =
-      __builtin_amdgcn_make_buffer_rsrc(gx, (short)0, NSLOT * slot_floats * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t x_rs = __builtin_amdgcn_make_buffer_rsrc(
+      gx, (short)0, (xg ? 4 : NSLOT) * slot_floats * 4, 0x00020000);
   const int grp_off = (d * BT + bt) * NB3 * TF;
+  const int aoff = 2 * slot_floats * 4;   // the plain-store copies (xmode)
   if (threadIdx.x == 0) failed = 0;
   __syncthreads();
   // diagnostic timeline (DS2_GRU_STAMPS=2, scripts/trace_gru.py): s_memrealtime at step
@@ -452,13 +462,21 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW / 4,
       }
       trace_at(s, 1);
       if constexpr (PRE) {
+        if (xg && s == 1) {   // which producers share this XCD (their ids came with step 0)
+          const unsigned v = lane < UB ? __hip_atomic_load(xtab + lane, __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_AGENT) : 0u;
+          const unsigned long long same = __ballot(v == my_xcc);
+#pragma unroll
+          for (int i = 0; i < 2 * NP; ++i)
+            if ((same >> ((t_first + i) % UB)) & 1ull) tsame |= 1u << i;
+        }
         // LWP pairs' runs in flight, the next pair's issued as each pair is multiplied
         const int tb0 = (((s - 1) & 1) * slot_floats + grp_off + t_first * TF) * 4;
         u32x4 hm[2 * NP];
         u32x2 lo[2 * NP];
         auto load_run = [&](int i) {
           const bool ok = i < 2 * np && t_first + i < NB3;
-          const int to = tb0 + i * TF * 4;
+          const int to = tb0 + i * TF * 4 + (((tsame >> i) & 1u) ? aoff : 0);
           hm[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
                                                 x_rs, ok ? to + lane * 16 : 0x7ffffff0, 0, kSc1));
           lo[i] = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(
@@ -576,6 +594,10 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW / 4,
           const int go = so + g * UB * TF * 4;
           __builtin_amdgcn_raw_buffer_store_b128(hmv, x_rs, go + lane * 16, 0, kSc1);
           __builtin_amdgcn_raw_buffer_store_b64(lov, x_rs, go + 1024 + lane * 8, 0, kSc1);
+          if (xg) {   // plain copies: stay in this XCD's L2 for the same-XCD consumers
+            __builtin_amdgcn_raw_buffer_store_b128(hmv, x_rs, aoff + go + lane * 16, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b64(lov, x_rs, aoff + go + 1024 + lane * 8, 0, 0);
+          }
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (lane == 0)
@@ -727,11 +749,17 @@ bool launch_gru_bwd_x6(int hm, int t_max, int n, int h, int num_dirs, const floa
   const int nw = x6_bwd_waves();
   const void* fn = bwd_x6_fn((3 * UB + 1) / 2, hm == 1 ? 1 : 0, nw, pre);
   if (fn == nullptr) return false;
+  // DS2_GRU_XCD=1: same-XCD hand-off groups (pre-split tiles only; rnn_common.h map_work_xgrp)
+  static const bool xcd_on = [] {
+    const char* e = getenv("DS2_GRU_XCD");
+    return e != nullptr && e[0] == '1';
+  }();
+  int XM_ = (pre && xcd_on && xgrp_fits(UB, BT, num_dirs)) ? 1 : 0;
+  const int grid = XM_ ? xgrp_grid(UB, BT, num_dirs) : mapped_grid(UB * num_dirs, BT);
   int T_ = t_max, N_ = n, H_ = h, D_ = num_dirs, UB_ = UB, BT_ = BT, DYD_ = dy_dirs;
   void* args[] = {&T_, &N_, &H_, &D_, &UB_, &BT_, &dy, &DYD_, &w_hh_f, &w_hh_r, &h_all,
-                  &gates, &lens, &dgates_x, &dgates_h, &ring, &ctrs, &err, &stamps, &dbp};
-  return rnn_launch(fn, dim3(mapped_grid(UB * num_dirs, BT)), dim3(nw * 64), args,
-                                    lds_pad, st) == hipSuccess;
+                  &gates, &lens, &dgates_x, &dgates_h, &ring, &ctrs, &err, &stamps, &dbp, &XM_};
+  return rnn_launch(fn, dim3(grid), dim3(nw * 64), args, lds_pad, st) == hipSuccess;
 }
 
 }  // namespace ds2

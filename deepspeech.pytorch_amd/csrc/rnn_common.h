@@ -95,6 +95,32 @@ __device__ __forceinline__ bool map_work(int P, int BT, int UB, int& ub, int& d,
 
 static inline int mapped_grid(int P, int BT) { return 8 * ((P + 7) / 8) * BT; }
 
+// Same-XCD groups (DS2_GRU_XCD, the pre-split GRU backward): each of the G = D * BT hand-off
+// groups on its own 8 / G XCDs, UB / (8 / G) unit blocks per XCD (cfg2: 4 groups x 2 XCDs x
+// 25), so half of a consumer's producers share its XCD and the consumer reads their tiles
+// from copies the producers also store plainly (kept in that XCD's L2: MI355X_MICROARCH
+// "handoff-payload", 104-122 vs 66-73 GB/s per block).  Which producer shares the XCD is read
+// at run time (xcc_id(), published per producer), never assumed from the placement.
+static inline bool xgrp_fits(int UB, int BT, int D) {
+  const int G = D * BT;
+  return G >= 1 && G <= 8 && 8 % G == 0 && UB % (8 / G) == 0;
+}
+static inline int xgrp_grid(int UB, int BT, int D) { return 8 * (UB / (8 / (D * BT))); }
+__device__ __forceinline__ bool map_work_xgrp(int UB, int BT, int D, int& ub, int& d, int& bt) {
+  const int wg = blockIdx.x;
+  const int xcd = wg & 7, slot = wg >> 3;
+  const int G = D * BT, xpg = 8 / G, per = UB / xpg;
+  const int q = xcd / xpg, part = xcd - q * xpg;
+  if (slot >= per || q >= G) return false;
+  ub = part * per + slot;
+  d = q / BT;
+  bt = q - d * BT;
+  return true;
+}
+__device__ __forceinline__ unsigned xcc_id() {
+  return __builtin_amdgcn_s_getreg(20 | (0 << 6) | ((4 - 1) << 11)) & 15u;   // HW_REG_XCC_ID
+}
+
 
 // ===========================================================================
 // Persistent variants: one launch per layer and direction pair.  Each workgroup

@@ -78,6 +78,11 @@ if len(sys.argv) > 1 and sys.argv[1] == "pre":
                                   "DS2_RNN_HANDOFF_BWD": "flags"},
                 "bwd-x6pre-w8": {"DS2_GRU_X6": "1", "DS2_GRU_X6_BWD": "2",
                                  "DS2_GRU_X6_BWD_WAVES": "8", "DS2_RNN_HANDOFF_BWD": "flags"}}
+if len(sys.argv) > 1 and sys.argv[1] == "xcd":
+    # the same-XCD groups are chosen once per process (DS2_GRU_XCD read at first launch):
+    # run this script once per setting and compare the lines
+    variants = {f"bwd-x6pre-xcd{os.environ.get('DS2_GRU_XCD', '0')}": {
+        "DS2_GRU_X6": "1", "DS2_GRU_X6_BWD": "2", "DS2_RNN_HANDOFF_BWD": "flags"}}
 rounds = int(os.environ.get("AB_ROUNDS", "3"))
 variants = {f"{k}#{r}": v for r in range(rounds) for k, v in variants.items()}
 ref = None
