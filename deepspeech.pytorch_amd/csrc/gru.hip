@@ -1410,10 +1410,13 @@ static inline unsigned long long* stamp_slots(unsigned* ctrs, int n, int num_dir
 // ring of hand-off tiles for the direct-operand kernels (gates tiles per unit block: 1
 // forward, 3 backward): 2 slots for the flag hand-off, kRingSlots for the sentinel one; the
 // backward's tiles are sized for the pre-split form (1.5 KB, gru_split.hip)
+// (the forward's ring is doubled: the same-XCD groups keep a plainly stored copy of the
+// sentinel ring; the backward's pre-split flag form uses slots 2-3 for its copies)
 static inline size_t ring_bytes(int n, int h, int num_dirs, int tiles) {
   const size_t UB = (h + GU - 1) / GU, BT = (n + GB - 1) / GB;
   const size_t tile_floats = tiles == 3 ? 384 : 256;
-  return align256(kRingSlots * (size_t)num_dirs * BT * UB * tiles * tile_floats * sizeof(float));
+  const size_t slots = tiles == 3 ? kRingSlots : 2 * kRingSlots;
+  return align256(slots * (size_t)num_dirs * BT * UB * tiles * tile_floats * sizeof(float));
 }
 // every ring word starts as the sentinel (slots 0 and 1 must; the rest for simplicity)
 static inline hipError_t ring_reset(float* ring, int n, int h, int num_dirs, int tiles,

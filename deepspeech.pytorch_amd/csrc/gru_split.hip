@@ -110,7 +110,7 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     const float* __restrict__ b_r, const int* __restrict__ lens, float* __restrict__ h_all,
     float* __restrict__ gates, float* __restrict__ coef, float* __restrict__ hx,
     unsigned* __restrict__ counters, unsigned* __restrict__ err,
-    unsigned long long* __restrict__ stamps) {
+    unsigned long long* __restrict__ stamps, int xmode) {
   constexpr int RP = 3 * GU + 1;
   constexpr bool SENT = HM == 1;
   constexpr int NSLOT = SENT ? kRingSlots : 2;
@@ -119,7 +119,16 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   __shared__ int flag;
   __shared__ int failed;
   int ub, d, bt;
-  if (!map_work(UB * D, BT, UB, ub, d, bt)) return;
+  // xmode (sentinel ring only): same-XCD groups as in the backward -- every tile and its
+  // sentinel refill also stored plainly into a second ring (slots NSLOT..2 NSLOT-1), from
+  // which the consumers on the producer's XCD read it
+  const bool xg = SENT && xmode != 0;
+  if (xg ? !map_work_xgrp(UB, BT, D, ub, d, bt) : !map_work(UB * D, BT, UB, ub, d, bt)) return;
+  unsigned* xtab = counters + (D * BT + 1) + D * BT * 64 + (d * BT + bt) * 64;
+  const unsigned my_xcc = xcc_id() + 1u;
+  if (xg && threadIdx.x == 0)
+    __hip_atomic_store(xtab + ub, my_xcc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  unsigned tsame = 0;           // bit i: this wave's tile t_first + i comes from this XCD
   const int n0 = bt * GB;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -129,9 +138,10 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   const unsigned* gflags = counters + (D * BT + 1) + (d * BT + bt) * UB;
   unsigned* myflag = counters + (D * BT + 1) + (d * BT + bt) * UB + ub;
   const int slot_floats = D * BT * UB * 256;
-  const __amdgpu_buffer_rsrc_t x_rs =
-      __builtin_amdgcn_make_buffer_rsrc(hx, (short)0, NSLOT * slot_floats * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t x_rs = __builtin_amdgcn_make_buffer_rsrc(
+      hx, (short)0, (xg ? 2 * NSLOT : NSLOT) * slot_floats * 4, 0x00020000);
   const int grp_off = (d * BT + bt) * UB * 256;
+  const int aoff = NSLOT * slot_floats * 4;   // the plain-store ring (xmode)
   if (threadIdx.x == 0) failed = 0;
   __syncthreads();
   // diagnostic timeline (DS2_GRU_STAMPS=2, scripts/trace_gru.py): s_memrealtime at step
@@ -205,12 +215,26 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
         return;
       }
       trace_at(s, 1);
+      if (xg && s == 1) {   // which producers share this XCD (ids published at their start)
+        unsigned v = 0;
+        for (unsigned spins = 0;; ++spins) {
+          v = lane < UB ? __hip_atomic_load(xtab + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                        : 1u;
+          if (__ballot(v == 0u) == 0ull || spins > g_spin_limit) break;
+          __builtin_amdgcn_s_sleep(1);
+        }
+        const unsigned long long same = __ballot(v == my_xcc);   // an id never seen: no bit
+#pragma unroll
+        for (int i = 0; i < 2 * NP; ++i)
+          if (t_first + i < UB && ((same >> (t_first + i)) & 1ull)) tsame |= 1u << i;
+      }
       const int base = (((s - 1) % NSLOT) * slot_floats + grp_off + t_first * 256 + lane * 4) * 4;
       if (SENT) sleep_units(g_rnn_tune[1]);
       f32x4 hv[2 * NP];
 #pragma unroll
       for (int i = 0; i < 2 * NP; ++i) {
-        const int off = (i < 2 * np && t_first + i < UB) ? base + i * 1024 : 0x7ffffff0;
+        const int off = (i < 2 * np && t_first + i < UB)
+                            ? base + i * 1024 + (((tsame >> i) & 1u) ? aoff : 0) : 0x7ffffff0;
         hv[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(x_rs, off, 0, kSc1));
       }
       asm volatile("" ::: "memory");
@@ -245,7 +269,8 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
         for (int i = 0; i < 2 * NP; ++i)
           if (((pend >> (i >> 1)) & 1u) && t_first + i < UB)
             hv[i] = __builtin_bit_cast(
-                f32x4, __builtin_amdgcn_raw_buffer_load_b128(x_rs, base + i * 1024, 0, kSc1));
+                f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                           x_rs, base + i * 1024 + (((tsame >> i) & 1u) ? aoff : 0), 0, kSc1));
       }
 #pragma unroll
       for (int g = 0; g < 3; ++g) {
@@ -307,6 +332,12 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
         const u32x4 sv = u32x4{kSentinel, kSentinel, kSentinel, kSentinel};
         __builtin_amdgcn_raw_buffer_store_b128(sv, x_rs, ((s + 2) % NSLOT) * slot_floats * 4 + toff,
                                                0, kSc1);
+        if (xg) {   // plain copies for the same-XCD consumers (kept in this XCD's L2)
+          __builtin_amdgcn_raw_buffer_store_b128(v, x_rs, aoff + (s % NSLOT) * slot_floats * 4 + toff,
+                                                 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b128(
+              sv, x_rs, aoff + ((s + 2) % NSLOT) * slot_floats * 4 + toff, 0, 0);
+        }
       } else {
         const u32x4 v = *reinterpret_cast<const u32x4*>(tile + lane * 4);
         __builtin_amdgcn_raw_buffer_store_b128(v, x_rs, (s & 1) * slot_floats * 4 + toff, 0, kSc1);
@@ -727,11 +758,14 @@ bool launch_gru_fwd_x6(int hm, int t_max, int n, int h, int num_dirs, const floa
   const int need = ((UB + 1) / 2 + XW - 1) / XW;
   const void* fn = fwd_x6_fn(need, hm == 1 ? 1 : 0);
   if (fn == nullptr) return false;
+  // same-XCD groups for the sentinel ring (as the backward; DS2_GRU_XCD=0 turns them off)
+  const char* xe = getenv("DS2_GRU_XCD");
+  int XM_ = (hm == 1 && !(xe != nullptr && xe[0] == '0') && xgrp_fits(UB, BT, num_dirs)) ? 1 : 0;
+  const int grid = XM_ ? xgrp_grid(UB, BT, num_dirs) : mapped_grid(UB * num_dirs, BT);
   int T_ = t_max, N_ = n, H_ = h, D_ = num_dirs, UB_ = UB, BT_ = BT;
   void* args[] = {&T_, &N_, &H_, &D_, &UB_, &BT_, &xproj, &w_hh_f, &w_hh_r, &b_hh_f,
-                  &b_hh_r, &lens, &h_all, &gates, &coef, &ring, &ctrs, &err, &stamps};
-  return rnn_launch(fn, dim3(mapped_grid(UB * num_dirs, BT)), dim3(XT), args,
-                                    lds_pad, st) == hipSuccess;
+                  &b_hh_r, &lens, &h_all, &gates, &coef, &ring, &ctrs, &err, &stamps, &XM_};
+  return rnn_launch(fn, dim3(grid), dim3(XT), args, lds_pad, st) == hipSuccess;
 }
 
 bool launch_gru_bwd_x6(int hm, int t_max, int n, int h, int num_dirs, const float* dy, int dy_dirs,
@@ -749,11 +783,11 @@ bool launch_gru_bwd_x6(int hm, int t_max, int n, int h, int num_dirs, const floa
   const int nw = x6_bwd_waves();
   const void* fn = bwd_x6_fn((3 * UB + 1) / 2, hm == 1 ? 1 : 0, nw, pre);
   if (fn == nullptr) return false;
-  // DS2_GRU_XCD=1: same-XCD hand-off groups (pre-split tiles only; rnn_common.h map_work_xgrp)
-  static const bool xcd_on = [] {
-    const char* e = getenv("DS2_GRU_XCD");
-    return e != nullptr && e[0] == '1';
-  }();
+  // same-XCD hand-off groups (pre-split tiles only; rnn_common.h map_work_xgrp), default on:
+  // cfg2 backward 5.82 -> 5.43 us per step in isolation, 6.14 -> 5.69 in the training step
+  // (scripts/gpu_r3s.sh, alternating runs on one box); DS2_GRU_XCD=0 keeps map_work's layout
+  const char* xe = getenv("DS2_GRU_XCD");
+  const bool xcd_on = !(xe != nullptr && xe[0] == '0');
   int XM_ = (pre && xcd_on && xgrp_fits(UB, BT, num_dirs)) ? 1 : 0;
   const int grid = XM_ ? xgrp_grid(UB, BT, num_dirs) : mapped_grid(UB * num_dirs, BT);
   int T_ = t_max, N_ = n, H_ = h, D_ = num_dirs, UB_ = UB, BT_ = BT, DYD_ = dy_dirs;

@@ -1,10 +1,10 @@
 #!/bin/bash
-# same-XCD hand-off groups for the pre-split GRU backward (DS2_GRU_XCD=1): parity of the
+# same-XCD hand-off groups (GRU pre-split backward, sentinel forward; default, DS2_GRU_XCD=0 off): parity
 # pre-split forms with it on, then alternating recurrence timings and bench lines
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out
 TAG=${1:-r3s}
-DS2_GRU_XCD=1 timeout -k 10 600 python -u -m pytest tests/test_gpu_ops.py -x -v --timeout 300 --timeout-method thread \
+timeout -k 10 600 python -u -m pytest tests/test_gpu_ops.py tests/test_gpu_train.py -x -v --timeout 300 --timeout-method thread \
   -m gpu -k "presplit or full_length or bf16x6_matches or handoff_forms or two_batch" > gpurun_out/$TAG.tests.log 2>&1 || { tail -30 gpurun_out/$TAG.tests.log; exit 1; }
 tail -1 gpurun_out/$TAG.tests.log
 for x in 0 1 0 1; do

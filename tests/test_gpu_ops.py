@@ -621,7 +621,7 @@ def test_gru_dh_backward_matches_gate_exchange(dev, n, h, bidir, monkeypatch):
 
 
 @pytest.mark.parametrize("n,h,bidir", [(32, 800, True), (7, 48, False), (17, 784, True),
-                                       (33, 256, True)])
+                                       (33, 256, True), (16, 1024, True), (64, 256, False)])
 def test_gru_presplit_backward(dev, n, h, bidir, monkeypatch):
     """DS2_GRU_X6_BWD=2 (producers publish their gate-gradient tiles as pre-split bf16 runs,
     consumers load ready MFMA operands) against the consumer-split bf16x6 backward: the same
@@ -633,11 +633,14 @@ def test_gru_presplit_backward(dev, n, h, bidir, monkeypatch):
            dict(base, DS2_GRU_X6_BWD="1", DS2_GRU_X6_BWD_WAVES="8"),
            dict(base, DS2_GRU_X6_BWD="2", DS2_GRU_X6_BWD_WAVES="8"),
            dict(base, DS2_GRU_X6_BWD="1", DS2_GRU_X6_BWD_WAVES="4"),
-           dict(base, DS2_GRU_X6_BWD="2", DS2_GRU_X6_BWD_WAVES="4")]
-    ref, c8, p8, c4, p4 = _gru_run(dev, n, 37, 40, h, nd, h + 13 * n, env, monkeypatch)
-    for r, a8, b8, a4, b4 in zip(ref, c8, p8, c4, p4):
+           dict(base, DS2_GRU_X6_BWD="2", DS2_GRU_X6_BWD_WAVES="4"),
+           dict(base, DS2_GRU_X6_BWD="2", DS2_GRU_X6_BWD_WAVES="8", DS2_GRU_XCD="0")]
+    ref, c8, p8, c4, p4, q8 = _gru_run(dev, n, 37, 40, h, nd, h + 13 * n, env, monkeypatch)
+    for r, a8, b8, a4, b4, x8 in zip(ref, c8, p8, c4, p4, q8):
         assert torch.isfinite(b8).all() and torch.isfinite(b4).all()
-        assert torch.equal(a8, b8) and torch.equal(a4, b4)
+        # the same-XCD groups (default where the groups tile the XCDs: 32 x 800 and 16 x 1024
+        # bidirectional) read the same bytes from plainly stored copies: bit-identical
+        assert torch.equal(a8, b8) and torch.equal(a4, b4) and torch.equal(b8, x8)
         _close(b8, r, 2e-5, "pre-split x6 vs fp32-MFMA backward")
         _close(b4, r, 2e-5, "pre-split x6 (4 waves) vs fp32-MFMA backward")
 
