@@ -27,7 +27,7 @@ gates = torch.empty(T, N, D, 4 * H, device=dev)
 ws = torch.zeros(_lib.size("ds2_gru_fwd_workspace_size", N, H, D), dtype=torch.uint8, device=dev)
 UB, KS, BT = (H + 15) // 16, (H + 3) // 4, (N + 15) // 16
 al = lambda x: (x + 255) & ~255
-off = al(D * UB * KS * 3 * 64 * 4) + al((D * BT + 1 + D * BT * 64) * 4)
+off = al(D * UB * KS * 3 * 64 * 4) + al((D * BT + 1 + D * BT * 128) * 4)
 P = UB * D
 grid = 8 * ((P + 7) // 8) * BT
 for it in range(3):
@@ -96,5 +96,5 @@ for it in range(3):
               None, wsb.data_ptr(), wsb.numel(), ops._stream())
     torch.cuda.synchronize()
 KS3 = (3 * H + 3) // 4
-offb = al(D * UB * KS3 * 64 * 4) + al(2 * N * D * H * 4) + al((D * BT + 1 + D * BT * 64) * 4)
+offb = al(D * UB * KS3 * 64 * 4) + al(2 * N * D * H * 4) + al((D * BT + 1 + D * BT * 128) * 4)
 analyse(wsb[offb:offb + NS * grid * 5 * 8].view(torch.int64).cpu().numpy().reshape(NS, grid, 5), "backward")
