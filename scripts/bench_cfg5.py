@@ -27,6 +27,9 @@ def main():
     ap.add_argument("--seconds", type=float, default=30.0)
     ap.add_argument("--beam", type=int, default=10)
     ap.add_argument("--iters", type=int, default=3)
+    ap.add_argument("--lm", default=os.path.join(os.path.dirname(os.path.abspath(__file__)), "..",
+                                                 "tests", "golden", "tiny_lm.arpa"),
+                    help="ARPA model for the beam_lm line (default: the committed 3-gram fixture)")
     args = ap.parse_args()
     from ds2amd import model as dsm, ops
     from ds2amd.data_loader import SpectrogramParser
@@ -43,6 +46,8 @@ def main():
     ns = torch.full((args.batch,), n_samp, dtype=torch.int32, device=dev)
     frames = 1 + n_samp // hop
     beam = BeamCTCDecoder(bench.LABELS, beam_width=args.beam, cutoff_top_n=40)
+    beam_lm = BeamCTCDecoder(bench.LABELS, lm_path=args.lm, alpha=0.8, beta=1.0,
+                             beam_width=args.beam, cutoff_top_n=40)
     greedy = GreedyDecoder(bench.LABELS)
 
     def run(decoder):
@@ -53,7 +58,7 @@ def main():
 
     out = {"config": f"cfg5: batched inference, DS2 5xBiGRU-800, {args.batch} x {args.seconds:g} s "
                      f"PCM -> STFT -> forward -> decode, fp32", "batch": args.batch}
-    for name, dec in (("beam", beam), ("greedy", greedy)):
+    for name, dec in (("beam", beam), ("beam_lm", beam_lm), ("greedy", greedy)):
         run(dec)
         torch.cuda.synchronize()
         t0 = time.perf_counter()

@@ -29,7 +29,10 @@ UB, KS, BT = (H + 15) // 16, (H + 3) // 4, (N + 15) // 16
 al = lambda x: (x + 255) & ~255
 off = al(D * UB * KS * 3 * 64 * 4) + al((D * BT + 1 + D * BT * 128) * 4)
 P = UB * D
-grid = 8 * ((P + 7) // 8) * BT
+G = D * BT
+# same-XCD groups (the default where they tile the XCDs; DS2_GRU_XCD=0 the interleaved layout)
+XG = os.environ.get("DS2_GRU_XCD", "1")[:1] != "0" and 8 % G == 0 and UB % (8 // G) == 0
+grid = 8 * (UB // (8 // G)) if XG else 8 * ((P + 7) // 8) * BT
 for it in range(3):
     _lib.call("ds2_gru_fwd", T, N, H, D, xproj.data_ptr(), w[0].data_ptr(), w[1].data_ptr(),
               b[0].data_ptr(), b[1].data_ptr(), lens.data_ptr(), h_all.data_ptr(),
@@ -42,6 +45,10 @@ def analyse(tr, label):
     groups = {}
     for wg in range(grid):
         xcd, slot = wg & 7, wg >> 3
+        if XG:
+            q = xcd // (8 // G)
+            groups.setdefault((q // BT, q % BT), []).append(wg)
+            continue
         pair = xcd + 8 * (slot // BT)
         bt = slot % BT
         if pair >= P:
