@@ -294,6 +294,19 @@ def test_cfg5_30s_eval_forward_and_beam10(dev):
         for p, (_, ids, ts) in enumerate(paths):
             assert strings[i][p] == ''.join(LABELS[k] for k in ids)
             assert offsets[i][p].tolist() == ts
+    # the same search with the committed word 3-gram LM (ctcdecode's KenLM scorer restated,
+    # oracle/ctc_beam_lm.py) over the 1501 frames: every path and its frames
+    from oracle import ctc_beam_lm
+    lm_path = os.path.join(os.path.dirname(__file__), "golden", "tiny_lm.arpa")
+    beam = BeamCTCDecoder(LABELS, lm_path=lm_path, alpha=0.8, beta=1.0, beam_width=10,
+                          cutoff_top_n=40)
+    strings, offsets = beam.decode(probs, out_lens)
+    ref = ctc_beam_lm.beam_decode_lm(probs.cpu().numpy(), out_lens.cpu().tolist(), 10,
+                                     ctc_beam_lm.ArpaLM(lm_path), LABELS, 0.8, 1.0)
+    for i, paths in enumerate(ref):
+        for p, (_, ids, ts) in enumerate(paths):
+            assert strings[i][p] == ''.join(LABELS[k] for k in ids), (i, p)
+            assert offsets[i][p].tolist() == ts
 
 
 def test_cfg4_lstm1024_bf16_gemms_and_batch64_chunks(dev):
