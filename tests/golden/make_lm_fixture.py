@@ -22,47 +22,46 @@ WORDS = ["A", "AN", "AND", "ANT", "THE", "THEY", "THEN", "CAT", "CATS", "CAR", "
          "I", "IT", "IS", "IN", "ON", "NO", "NOT", "TO", "TOO", "SAT", "HAT", "café"]
 
 
-def build(seed: int = 7):
+def build(seed: int = 7, order: int = 3, top: int = 40):
+    """A back-off model of `order` (1..6): `top` random top-order n-grams, every prefix and
+    suffix of each added (lower orders padded with random extra n-grams), backoffs on every
+    n-gram that is the context of a longer one.  build() = the committed tiny_lm.arpa."""
     g = np.random.default_rng(seed)
     vocab = ["<s>", "</s>", "<unk>"] + WORDS
-    tri = set()
-    while len(tri) < 40:
-        a = ["<s>"] + WORDS
-        w1 = a[g.integers(len(a))]
-        w2 = WORDS[g.integers(len(WORDS))]
-        w3 = WORDS[g.integers(len(WORDS))] if g.random() < 0.9 else "</s>"
-        tri.add((w1, w2, w3))
-    bi = set()
-    for t in tri:
-        bi.add(t[:2])
-        bi.add(t[1:])
-    while len(bi) < 90:
-        a = ["<s>"] + WORDS
-        bi.add((a[g.integers(len(a))], (WORDS + ["</s>"])[g.integers(len(WORDS) + 1)]))
-    uni = [(w,) for w in vocab]
-    ctx_bi = {t[:2] for t in tri}
-    ctx_uni = {b[:1] for b in bi}
+    grams = {n: set() for n in range(1, order + 1)}
+    if order > 1:
+        while len(grams[order]) < top:
+            a = ["<s>"] + WORDS
+            ng = [a[g.integers(len(a))]] + [WORDS[g.integers(len(WORDS))] for _ in range(order - 2)]
+            ng.append(WORDS[g.integers(len(WORDS))] if g.random() < 0.9 else "</s>")
+            grams[order].add(tuple(ng))
+        for n in range(order - 1, 1, -1):
+            for t in grams[n + 1]:
+                grams[n].add(t[:-1])
+                grams[n].add(t[1:])
+        while len(grams[2]) < 90 and order == 3:
+            a = ["<s>"] + WORDS
+            grams[2].add((a[g.integers(len(a))], (WORDS + ["</s>"])[g.integers(len(WORDS) + 1)]))
+    grams[1] = {(w,) for w in vocab}
+    ctx = {n: {t[:-1] for t in grams[n + 1]} if n < order else set() for n in range(1, order + 1)}
 
     def p10(lo, hi):
         return float(np.round(g.uniform(lo, hi), 4))
 
-    lines = ["", "\\data\\", f"ngram 1={len(uni)}", f"ngram 2={len(bi)}", f"ngram 3={len(tri)}",
-             "", "\\1-grams:"]
-    for (w,) in uni:
-        prob = -99.0 if w == "<s>" else p10(-3.2, -0.8)
-        if (w,) in ctx_uni:
-            lines.append(f"{prob:.4f}\t{w}\t{p10(-1.2, -0.05):.4f}")
-        else:
-            lines.append(f"{prob:.4f}\t{w}")
-    lines += ["", "\\2-grams:"]
-    for b in sorted(bi):
-        if b in ctx_bi:
-            lines.append(f"{p10(-2.0, -0.2):.4f}\t{' '.join(b)}\t{p10(-0.9, -0.02):.4f}")
-        else:
-            lines.append(f"{p10(-2.0, -0.2):.4f}\t{' '.join(b)}")
-    lines += ["", "\\3-grams:"]
-    for t in sorted(tri):
-        lines.append(f"{p10(-1.5, -0.1):.4f}\t{' '.join(t)}")
+    lines = ["", "\\data\\"] + [f"ngram {n}={len(grams[n])}" for n in range(1, order + 1)]
+    for n in range(1, order + 1):
+        lines += ["", f"\\{n}-grams:"]
+        items = [(w,) for w in vocab] if n == 1 else sorted(grams[n])
+        for t in items:
+            if n == 1:
+                prob = -99.0 if t[0] == "<s>" else p10(-3.2, -0.8)
+            else:
+                prob = p10(-2.0, -0.2) if n == 2 else p10(-1.5, -0.1)
+            if t in ctx[n]:
+                bo = p10(-1.2, -0.05) if n == 1 else p10(-0.9, -0.02)
+                lines.append(f"{prob:.4f}\t{' '.join(t)}\t{bo:.4f}")
+            else:
+                lines.append(f"{prob:.4f}\t{' '.join(t)}")
     lines += ["", "\\end\\", ""]
     return "\n".join(lines)
 

@@ -1218,6 +1218,49 @@ def test_ctc_beam_lm_vs_oracle(dev, beam, top_n, cutoff, alpha, beta, noise):
         assert strings[n][0] == (''.join(labels[i] for i in paths[0][1]) if paths else '')
 
 
+@pytest.mark.parametrize("order,beam", [(1, 16), (2, 8), (5, 16), (6, 100)])
+def test_ctc_beam_lm_orders_vs_oracle(dev, order, beam, tmp_path):
+    """The LM search with models of every order the kernel takes (1..6: no history, the
+    <s>-padded histories up to five words, back-off chains up to six lookups), generated by
+    tests/golden/make_lm_fixture.build(order=...), against oracle/ctc_beam_lm.py."""
+    import importlib.util
+    from oracle import ctc_beam_lm as obl
+    from ds2amd.lm import ArpaScorer
+    spec = importlib.util.spec_from_file_location(
+        "make_lm_fixture", os.path.join(os.path.dirname(__file__), "golden", "make_lm_fixture.py"))
+    mk = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mk)
+    path = str(tmp_path / f"lm{order}.arpa")
+    with open(path, "w", encoding="utf-8") as f:
+        f.write(mk.build(seed=order, order=order, top=60))
+    labels = orc.LABELS
+    g = np.random.default_rng(order)
+    texts = ["THE CAT SAT ON A HAT", "I DON'T NO THEN ", "CATS AND DOG TOO"]
+    ps = [_spelled(s, g, 2.0) for s in texts]
+    t = max(p.shape[0] for p in ps)
+    probs = np.full((len(ps), t, len(labels)), 1.0 / len(labels), np.float32)
+    for i, p in enumerate(ps):
+        probs[i, :p.shape[0]] = p
+    sizes = [p.shape[0] for p in ps]
+    scorer = ArpaScorer(path, labels, 1.1, 0.7, device=dev)
+    assert scorer.order == order
+    ids, offs, lens, scores = ops.ctc_beam_decode_lm_raw(
+        torch.from_numpy(probs).to(dev), torch.tensor(sizes, dtype=torch.int32).to(dev), beam,
+        beam, scorer)
+    ids, offs, lens, scores = ids.cpu(), offs.cpu(), lens.cpu(), scores.cpu()
+    ref = obl.beam_decode_lm(probs, sizes, beam, obl.ArpaLM(path), labels, 1.1, 0.7)
+    for n, paths in enumerate(ref):
+        for p in range(beam):
+            if p >= len(paths):
+                assert int(lens[n, p]) == 0
+                continue
+            s_, rid, rts = paths[p]
+            k = int(lens[n, p])
+            assert ids[n, p, :k].tolist() == rid, (n, p)
+            assert offs[n, p, :k].tolist() == rts, (n, p)
+            assert abs(float(scores[n, p]) - s_) <= 1e-5 * max(1.0, abs(s_)), (n, p)
+
+
 # ---------------------------------------------------------------------------- CER / WER
 def test_edit_distance_vs_reference_semantics(dev):
     """ds2_edit_distance == get_cer_wer (data/utils.py:47-57) with Decoder.wer/.cer's

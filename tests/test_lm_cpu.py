@@ -188,3 +188,51 @@ def test_lm_beam_oracle_spelled_sentence():
         s = "".join(LABELS[i] for i in ids)
         for w in s.split(" ")[:-1]:
             assert w in words, s
+
+
+@pytest.mark.parametrize("order", [1, 2, 4, 5, 6])
+def test_device_tables_match_oracle_any_order(order, tmp_path):
+    """The hash table queried the kernel's way equals the oracle's KenLM score for models of
+    every order the kernel accepts (histories <s>-padded to order - 1 words)."""
+    import importlib.util
+    from ds2amd import lm as dlm
+    spec = importlib.util.spec_from_file_location(
+        "make_lm_fixture", os.path.join(HERE, "golden", "make_lm_fixture.py"))
+    mk = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mk)
+    path = str(tmp_path / "m.arpa")
+    with open(path, "w", encoding="utf-8") as f:
+        f.write(mk.build(seed=order, order=order, top=60))
+    vocab, o, keys, prob, bo = dlm.read_arpa(path)
+    assert o == order
+    tab = dlm.build_table(keys, prob, bo)
+    olm = obl.ArpaLM(path)
+    g = np.random.default_rng(order)
+    words = [w for w in vocab if w not in ("<s>", "</s>", "<unk>")]
+    ngrams = [k for k in olm.ngrams if len(k) == order]
+    for trial in range(400):
+        if trial < len(ngrams) and order > 1:     # every top-order n-gram, then random ones
+            ng = list(ngrams[trial])
+        else:
+            ng = (["<s>"] * g.integers(0, order)) + [words[g.integers(len(words))] for _ in range(order)]
+            ng = ng[-order:]
+        hist, w = ng[:-1], ng[-1]
+        if w == "<s>":
+            continue
+        ref = olm.cond_log10(tuple(ng))
+        got = _device_cond(tab, order, [vocab.index(x) for x in hist], vocab.index(w))
+        assert ref == got, (ng, ref, got)
+
+
+def test_scorer_rejects_char_lms_and_binary_files(tmp_path):
+    """Character-based LMs (ctcdecode's other scorer mode) and non-ARPA files raise."""
+    from ds2amd.lm import ArpaScorer
+    p = tmp_path / "char.arpa"
+    p.write_text("\\data\\\nngram 1=5\n\n\\1-grams:\n-99\t<s>\n-1\t</s>\n-1\t<unk>\n"
+                 "-0.5\tA\n-0.6\tB\n\n\\end\\\n")
+    with pytest.raises(NotImplementedError):
+        ArpaScorer(str(p), LABELS, 0.8, 1.0, device="cpu")
+    b = tmp_path / "lm.binary"
+    b.write_bytes(b"mmap lm http://kheafield.com/code format version 5\n\0\0\0")
+    with pytest.raises(ValueError):
+        ArpaScorer(str(b), LABELS, 0.8, 1.0, device="cpu")
