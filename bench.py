@@ -419,6 +419,7 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
+    tr.close()
     if distributed:
         dist.barrier()
         dist.destroy_process_group()

@@ -207,6 +207,14 @@ class Trainer:
         while self._inflight and self._drain_one(block):
             pass
 
+    def close(self) -> None:
+        """Finish pending work and release the library's own RCCL communicator (DS2_ALLREDUCE=ds2;
+        a no-op otherwise).  Call before destroying the process group."""
+        if self.reducer.comm is not None:
+            torch.cuda.synchronize(self.device)
+            self.reducer.comm.close()
+            self.reducer.comm = None
+
     # ---- the step ---------------------------------------------------------------------
     def train_batch(self, data, return_item: bool = False):
         self.poll_status(block=False)

@@ -259,9 +259,8 @@ def test_world1_nccl_trainer_hooks_and_bit_identity(dev, golden_dir, tmp_path, m
         assert tr.reducer.issued_from_hooks == len(tr.reducer.buckets)
         assert torch.equal(tr.flat.grad, ref_grad)
         assert torch.equal(tr.flat.flat, ref_params)
-        if tr.reducer.comm is not None:
-            torch.cuda.synchronize()
-            tr.reducer.comm.close()
+        tr.close()
+        assert tr.reducer.comm is None
     finally:
         ops.set_cooperative_guard(None)
         dist.destroy_process_group()
