@@ -156,9 +156,11 @@ static void apply_spin_limit_env() {
 // units before a forward step's first load pass, [2] the same for the backward (a consumer
 // that loads right after publishing mostly gets sentinels back, and those full-tile polls
 // from every workgroup crowd the fabric that carries the real tiles).  Defaults from
-// scripts/gru_ab.py sweeps; DS2_RNN_TUNE="a,b,c" overrides them (diagnostic; checked at every
-// recurrence entry point).
-constexpr unsigned kRepollSleep = 1u, kFirstPollDelay = 14u, kFirstPollDelayBwd = 14u;
+// scripts/gru_ab.py sweeps (the forward's first-poll delay 14 -> 10 with the same-XCD groups,
+// whose same-XCD tiles arrive sooner: 4.32-4.40 -> 4.26 us per step, `ftune`,
+// profiles/r3fa_fwd_tune.txt); DS2_RNN_TUNE="a,b,c" overrides them (diagnostic; checked at
+// every recurrence entry point).
+constexpr unsigned kRepollSleep = 1u, kFirstPollDelay = 10u, kFirstPollDelayBwd = 14u;
 static __constant__ unsigned g_rnn_tune[3] = {kRepollSleep, kFirstPollDelay, kFirstPollDelayBwd};
 
 static void apply_rnn_tune_env() {
