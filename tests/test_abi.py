@@ -80,3 +80,23 @@ def test_ctypes_prototypes_match_header_arity():
     for name, (_, argtypes) in _lib._PROTOS.items():
         assert name in ar, name
         assert len(argtypes) == ar[name], f"{name}: ctypes {len(argtypes)} vs header {ar[name]}"
+
+
+def test_comm_and_lm_decode_argument_checks():
+    """Host-side argument validation of the RCCL and LM-decode entry points (returns before
+    any RCCL or HIP call): a NULL communicator, a negative count, a bad LM order or table size
+    are DS2_INVALID_VALUE; destroying NULL is a no-op; the id is NCCL_UNIQUE_ID_BYTES."""
+    lib = _lib.load()
+    assert lib.ds2_comm_id_bytes() == 128
+    assert lib.ds2_allreduce_bucket(None, None, 16, None) == 1
+    assert lib.ds2_comm_destroy(None) == 0
+    assert lib.ds2_comm_init(None, None, 1, 0, 0) == 1
+    assert lib.ds2_comm_get_unique_id(None) == 1
+    # probs, n, t, c, strides, sizes, blank, beam, top_n, cutoff, top_paths, space, order, start,
+    # alpha, beta, dict_next, dict_mask, dict_word, states, table, slots, outs..., ws, ws_bytes, stream
+    base = [1, 1, 1, 30, 30, 30, None, 0, 4, 40, 1.0, 4, 29, 3, 0, 0.8, 1.0, 1, 1, 1, 5, 1, 8,
+            1, 1, 1, 1, 1, 1 << 20, None]
+    for i, bad in [(13, 7), (13, 0), (22, 12), (11, 0), (12, 30), (12, 0), (20, 1)]:
+        args = list(base)
+        args[i] = bad
+        assert lib.ds2_ctc_beam_decode_lm(*args) == 1, (i, bad)
