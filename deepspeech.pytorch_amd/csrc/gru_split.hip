@@ -394,7 +394,9 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW / 4,
   constexpr int NSLOT = SENT ? kRingSlots : 2;
   constexpr int LW = NW == 4 ? NP : 3;          // pairs whose loads are in flight
   constexpr int TF = PRE ? 384 : 256;           // ring floats per tile
-  constexpr int LWP = NW == 4 ? (NP < 12 ? NP : 12) : (NP < 5 ? NP : 5);   // PRE window
+  // PRE window: pairs of runs in flight per wave; with the same-XCD groups 4 (or 3) beat 5
+  // (5.41 -> 5.34 us per step, 6: 5.47; profiles/r3lw_bwd_window.txt)
+  constexpr int LWP = NW == 4 ? (NP < 12 ? NP : 12) : (NP < 4 ? NP : 4);
   constexpr int RED = NW * GB * RP > 8 * GB * GU ? NW * GB * RP : 8 * GB * GU;
   __shared__ __attribute__((aligned(8))) float red[RED];
   __shared__ __attribute__((aligned(16))) float tile[3 * GB * GU];
