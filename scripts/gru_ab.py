@@ -88,6 +88,10 @@ if len(sys.argv) > 1 and sys.argv[1] == "ftune":
     # same-XCD groups on
     variants = {f"fwd-tune-{t}": {"DS2_GRU_X6": "1", "DS2_RNN_HANDOFF": "", "DS2_RNN_TUNE": t}
                 for t in ("1,14,14", "1,6,14", "1,10,14", "1,18,14", "0,10,14", "2,10,14")}
+if len(sys.argv) > 1 and sys.argv[1] == "prewaves":
+    variants = {f"bwd-x6pre-w{w}": {"DS2_GRU_X6": "1", "DS2_GRU_X6_BWD": "2",
+                                    "DS2_GRU_X6_BWD_WAVES": w, "DS2_RNN_HANDOFF_BWD": "flags"}
+                for w in ("8", "4")}
 rounds = int(os.environ.get("AB_ROUNDS", "3"))
 variants = {f"{k}#{r}": v for r in range(rounds) for k, v in variants.items()}
 ref = None
