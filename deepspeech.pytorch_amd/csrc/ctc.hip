@@ -285,6 +285,12 @@ __global__ void greedy_kernel(const float* __restrict__ probs, int n, int t_max,
 // prefix already in the beam are merged into it), then keep the beam_width best by
 // (score desc, last char asc, candidate index asc).  oracle/ctc_beam.py restates the
 // same algorithm (parity with ctcdecode itself is unpinned: it is not available).
+// Trie-node revival (path_trie.cpp get_path_trie / remove): a node pruned from the beam
+// stays in the trie while a descendant is in the beam, and an extension onto it revives
+// it.  Per node: cnt = (in the beam) + (children alive), km = the chars of its alive
+// children, a child list (fc first child, ns next sibling); a pruned node whose cnt drops
+// to 0 is dead and takes its bit out of its parent's km (and its count, recursively).
+// km is loaded per frame, so the list walk runs only where a revival is attempted.
 // two instantiations: beams <= 32 over vocabularies <= 64, and beams <= 128 (the
 // reference's default beam_width is 100, decoder.py:89) over vocabularies <= 32 -- both
 // keep every candidate (k = entry * C + char < 4096) in the wave's registers
@@ -425,6 +431,18 @@ __device__ __forceinline__ float lm_add(float v, float term, double beta) {
 }
 
 // wave minimum (every lane gets it)
+// alive child of trie node p with char c, or -1 (the lists only grow; dead nodes stay)
+__device__ int trie_alive_child(const int* fc, const int* ns, const int* chr, const int* cnt,
+                                int p, int c, int64_t cap) {
+  int x = __hip_atomic_load(fc + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (int64_t g = 0; x > 0 && g < cap; ++g) {
+    if (chr[x] == c && __hip_atomic_load(cnt + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > 0)
+      return x;
+    x = ns[x];
+  }
+  return -1;
+}
+
 __device__ __forceinline__ float wave_min(float v) {
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) v = fminf(v, __shfl_xor(v, o));
@@ -436,8 +454,9 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
     const float* __restrict__ probs, int t_max, int C, int64_t stride_n, int64_t stride_t,
     const int* __restrict__ sizes, int blank, int beam, int cutoff_top_n, double cutoff_prob,
     int top_paths, int* __restrict__ node_parent, int* __restrict__ node_ch,
-    int* __restrict__ node_ts, float* __restrict__ node_lpc, int64_t node_cap,
-    int* __restrict__ out_ids, int* __restrict__ out_ts, int* __restrict__ out_lens,
+    int* __restrict__ node_ts, float* __restrict__ node_lpc, int* __restrict__ node_cnt,
+    int* __restrict__ node_fc, int* __restrict__ node_ns, unsigned long long* __restrict__ node_km,
+    int64_t node_cap, int* __restrict__ out_ids, int* __restrict__ out_ts, int* __restrict__ out_lens,
     float* __restrict__ out_scores, BeamLm L) {
   constexpr int EPL = (BM + 63) / 64;   // beam entries per lane
   // LM state per beam entry: trie state, the order-1 preceding words, the cached
@@ -465,7 +484,13 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
   __shared__ signed char child_of[BM * CM];
   __shared__ float cpb[BM * CM], cpnb[BM * CM];
   __shared__ int sel_k[BM];
-  __shared__ int s_nb, s_nodes;
+  __shared__ int s_nb, s_nodes, s_nr;
+  // trie revival: per entry its node's alive-children chars; the attempted extensions onto
+  // pruned-but-alive children (their char frames are updated after the scoring loop); the
+  // entries of the old beam that stay
+  __shared__ unsigned long long b_km[BM];
+  __shared__ int rlist[BM * CM];
+  __shared__ int kept[BM];
   __shared__ float pch[BEAM_TCH * CM];
 
   const int n = blockIdx.x;
@@ -477,12 +502,17 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
   int* chr = node_ch + (int64_t)n * node_cap;
   int* tst = node_ts + (int64_t)n * node_cap;
   float* lpcv = node_lpc + (int64_t)n * node_cap;
+  int* cnt = node_cnt + (int64_t)n * node_cap;
+  int* fc = node_fc + (int64_t)n * node_cap;
+  int* ns = node_ns + (int64_t)n * node_cap;
+  unsigned long long* km = node_km + (int64_t)n * node_cap;
   const bool prune = cutoff_prob < 1.0 || cutoff_top_n < C;
 
   if (lane == 0) {
     b_node[0][0] = 0; b_last[0][0] = -1; b_pb[0][0] = 0.f; b_pnb[0][0] = -INFINITY;
     b_par[0][0] = -1; b_lpc[0][0] = -INFINITY;
     par[0] = -1; chr[0] = -1; tst[0] = -1; lpcv[0] = -INFINITY;
+    cnt[0] = 1; fc[0] = -1; ns[0] = -1; km[0] = 0ull;
     s_nb = 1;
     s_nodes = 1;
     if constexpr (LM) {
@@ -546,6 +576,8 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
       if (e < nb) {
         score[e] = beam_lse(b_pb[cur][e], b_pnb[cur][e]);
         const int nd = b_node[cur][e];
+        b_km[e] = __hip_atomic_load(km + nd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        kept[e] = 0;
         const int pnode = nd > 0 ? b_par[cur][e] : -1;
         int j = -1;
 #pragma unroll
@@ -557,6 +589,7 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
       }
     }
     for (int e = lane; e < nb * C; e += 64) child_of[e] = -1;
+    if (lane == 0) s_nr = 0;
     __syncthreads();
 #pragma unroll
     for (int q = 0; q < EPL; ++q) {
@@ -652,6 +685,7 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
             pnb = (c == last_i) ? (pb_i != -INFINITY ? lp[c] + pb_i : -INFINITY) : lp[c] + sc_i;
             if (LM && c == L.space) pnb = lm_add(pnb, b_lms[cur][i], L.beta);
             sc = pnb;
+            if ((b_km[i] >> c) & 1ull) rlist[atomicAdd(&s_nr, 1)] = k;   // revival attempt
           }
           cpb[k] = pb;
           cpnb[k] = pnb;
@@ -667,6 +701,17 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
       }
     }
     __syncthreads();
+    // ---- attempted extensions onto pruned-but-alive trie nodes take the log_prob_c rule
+    // (get_path_trie updates a found child whether or not it is kept)
+    for (int r = lane; r < s_nr; r += 64) {
+      const int k = rlist[r];
+      const int i = k / C, c = k - (k / C) * C;
+      const int x = trie_alive_child(fc, ns, chr, cnt, b_node[cur][i], c, node_cap);
+      if (x > 0 && lp[c] > lpcv[x]) {
+        lpcv[x] = lp[c];
+        tst[x] = t;
+      }
+    }
     // ---- keep the best `beam` candidates: a selection round is a register scan + a wave
     // arg-best, with no LDS traffic and no barrier
     int nsel = 0;
@@ -698,6 +743,19 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
     {
       const int nodes0 = s_nodes;
       int run = 0;
+      // revived nodes first: every lookup reads only the trie as the previous frame left it
+      int rv[EPL];
+#pragma unroll
+      for (int q = 0; q < EPL; ++q) {
+        const int e = lane + 64 * q;
+        rv[q] = -1;
+        if (e < nsel) {
+          const int k = sel_k[e];
+          const int i = k / C, c = k - (k / C) * C;
+          if (c != blank && ((b_km[i] >> c) & 1ull))
+            rv[q] = trie_alive_child(fc, ns, chr, cnt, b_node[cur][i], c, node_cap);
+        }
+      }
 #pragma unroll
       for (int q = 0; q < EPL; ++q) {
         const int e = lane + 64 * q;
@@ -708,7 +766,8 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
           c = k - i * C;
         }
         const bool ext = e < nsel && c != blank;
-        const unsigned long long em = __ballot(ext);
+        const bool revived = ext && rv[q] > 0;
+        const unsigned long long em = __ballot(ext && !revived);
         const int before = __builtin_amdgcn_mbcnt_hi(static_cast<unsigned>(em >> 32),
                                                      __builtin_amdgcn_mbcnt_lo(static_cast<unsigned>(em), 0));
         if (e < nsel) {
@@ -723,7 +782,8 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
             } else {
               if (si == L.fstate) si = 0;
               if (c == L.space) {   // the space completes the word of state si
-                b_dst[nxt][e] = L.fstate;
+                // (a revived post-space node has a child: its reset has happened)
+                b_dst[nxt][e] = revived ? 0 : L.fstate;
                 for (int h = 0; h + 1 < n1; ++h) b_hist[nxt][e][h] = b_hist[cur][i][h + 1];
                 if (n1 > 0) b_hist[nxt][e][n1 - 1] = L.dword[si];
                 b_lms[nxt][e] = 0.f;
@@ -740,12 +800,27 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
             b_last[nxt][e] = b_last[cur][i];
             b_par[nxt][e] = b_par[cur][i];
             b_lpc[nxt][e] = b_lpc[cur][i];
+            kept[i] = 1;
+          } else if (revived) {
+            const int x = rv[q];
+            atomicAdd(cnt + x, 1);
+            b_node[nxt][e] = x;
+            b_last[nxt][e] = c;
+            b_par[nxt][e] = b_node[cur][i];
+            b_lpc[nxt][e] = lpcv[x];
           } else {
             const int nd = nodes0 + run + before;
-            par[nd] = b_node[cur][i];
+            const int p = b_node[cur][i];
+            par[nd] = p;
             chr[nd] = c;
             tst[nd] = t;
             lpcv[nd] = lp[c];
+            cnt[nd] = 1;
+            fc[nd] = -1;
+            km[nd] = 0ull;
+            ns[nd] = atomicExch(fc + p, nd);
+            atomicAdd(cnt + p, 1);
+            atomicOr(km + p, 1ull << c);
             b_node[nxt][e] = nd;
             b_last[nxt][e] = c;
             b_par[nxt][e] = b_node[cur][i];
@@ -757,6 +832,21 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
         run += __popcll(em);
       }
       __syncthreads();
+      // pruned entries leave the beam; a node with no alive child left dies and takes its
+      // bit and count out of its parent (recursively; the root never dies)
+#pragma unroll
+      for (int q = 0; q < EPL; ++q) {
+        const int e = lane + 64 * q;
+        if (e < nb && !kept[e]) {
+          int x = b_node[cur][e];
+          for (int64_t g = 0; x > 0 && g < node_cap; ++g) {
+            if (atomicSub(cnt + x, 1) != 1) break;
+            const int p = par[x];
+            atomicAnd(km + p, ~(1ull << chr[x]));
+            x = p;
+          }
+        }
+      }
       if (lane == 0) {
         s_nodes = nodes0 + run;
         s_nb = nsel;
@@ -1010,9 +1100,11 @@ ds2_status_t ds2_greedy_decode(const float* probs, int n, int t_max, int c, int6
   return launch_status("ds2_greedy_decode");
 }
 
+// per node: parent, char, timestep, best char log-prob, cnt, first child, next sibling
+// (4 bytes each) and the alive-children char mask (8 bytes)
 size_t ds2_ctc_beam_workspace_size(int n, int t_max, int beam) {
   const size_t cap = (size_t)t_max * (beam > 0 ? beam : 1) + 1;
-  return 4 * al256((size_t)n * cap * 4) + 256;
+  return 7 * al256((size_t)n * cap * 4) + al256((size_t)n * cap * 8) + 256;
 }
 
 static ds2_status_t beam_decode(const float* probs, int n, int t_max, int c, int64_t stride_n,
@@ -1036,6 +1128,10 @@ static ds2_status_t beam_decode(const float* probs, int n, int t_max, int c, int
   int* chr = reinterpret_cast<int*>(w + plane);
   int* tst = reinterpret_cast<int*>(w + 2 * plane);
   float* lpc = reinterpret_cast<float*>(w + 3 * plane);
+  int* ncnt = reinterpret_cast<int*>(w + 4 * plane);
+  int* nfc = reinterpret_cast<int*>(w + 5 * plane);
+  int* nns = reinterpret_cast<int*>(w + 6 * plane);
+  auto* nkm = reinterpret_cast<unsigned long long*>(w + 7 * plane);
   BeamLm L{};
   if (lm != nullptr) L = *lm;
   auto kern = lm != nullptr
@@ -1045,7 +1141,7 @@ static ds2_status_t beam_decode(const float* probs, int n, int t_max, int c, int
                            : ctc_beam_kernel<BEAM_LARGE, BEAM_LARGE_C, false>);
   hipLaunchKernelGGL(kern, dim3(n), dim3(64), 0, as_stream(stream), probs, t_max, c,
                      stride_n, stride_t, sizes, blank, beam_width, cutoff_top_n, cutoff_prob,
-                     top_paths, par, chr, tst, lpc, cap, out_ids, out_offsets, out_lens,
+                     top_paths, par, chr, tst, lpc, ncnt, nfc, nns, nkm, cap, out_ids, out_offsets, out_lens,
                      out_scores, L);
   return launch_status(what);
 }

@@ -25,7 +25,13 @@ the library leaves to container iteration order:
   * the beam keeps the beam_width best candidates by (score desc, last char asc,
     candidate index asc); candidates with score -inf are dropped;
   * a prefix's char timestep (the `offsets`) is the frame of its best-scoring
-    extension event (ctcdecode's PathTrie log_prob_c rule).
+    extension event (ctcdecode's PathTrie log_prob_c rule);
+  * trie-node revival (path_trie.cpp get_path_trie / remove): a prefix pruned from the
+    beam stays in the trie while one of its descendants is still in the beam; an
+    extension (i, c) that lands on such a node revives it instead of creating a new one,
+    so the node keeps its identity (later extensions of it merge into the kept
+    descendant) and its char frame, and every attempted extension onto it takes the
+    log_prob_c rule above, whether or not it is selected.
 
 Pure Python loops: small inputs only.
 """
@@ -40,6 +46,7 @@ F32 = np.float32
 NEG = F32(-np.inf)
 FLT_MIN = F32(np.finfo(np.float32).tiny)
 FLT_MIN_D = float(FLT_MIN)
+STATS = {"revived": 0}      # revivals selected into a beam (tests check they are exercised)
 
 
 def lse(a: np.float32, b: np.float32) -> np.float32:
@@ -50,6 +57,21 @@ def lse(a: np.float32, b: np.float32) -> np.float32:
         return a
     m = a if a > b else b
     return F32(np.log(F32(np.exp(F32(a - m)) + np.exp(F32(b - m)))) + m)
+
+
+def alive_children(bm, parent, ch):
+    """{(parent node, char): node} over the trie nodes still alive at the start of a frame:
+    the beam's nodes and all their ancestors (PathTrie::remove deletes a pruned node only
+    once it has no children left)."""
+    alive = {}
+    seen = set()
+    for e in bm:
+        nd = e[0]
+        while nd > 0 and nd not in seen:
+            seen.add(nd)
+            alive[(parent[nd], ch[nd])] = nd
+            nd = parent[nd]
+    return alive
 
 
 def pruned_log_probs(p: np.ndarray, cutoff_top_n: int, cutoff_prob: float):
@@ -88,6 +110,7 @@ def beam_decode_one(probs: np.ndarray, size: int, beam: int, blank: int = 0,
         node_to_idx = {e[0]: i for i, e in enumerate(bm)}
         pidx = [node_to_idx.get(parent[e[0]], -1) if e[0] != 0 else -1 for e in bm]
         child_of = {(pidx[q], bm[q][1]): q for q in range(nb) if pidx[q] >= 0}
+        alive = alive_children(bm, parent, ch)
 
         def ext_val(i, cc):
             if cc == bm[i][1]:
@@ -114,6 +137,9 @@ def beam_decode_one(probs: np.ndarray, size: int, beam: int, blank: int = 0,
                 else:
                     if not allowed[cc] or (i, cc) in child_of:
                         continue
+                    x = alive.get((bm[i][0], cc))      # a pruned node still in the trie
+                    if x is not None and lp[cc] > lpc[x]:
+                        ts_upd[x] = (t, lp[cc])
                     e = ext_val(i, cc)
                     if e != NEG:
                         cands.append((e, cc, k, 'ext', i, NEG, e))
@@ -125,6 +151,9 @@ def beam_decode_one(probs: np.ndarray, size: int, beam: int, blank: int = 0,
         for s, last, k, kind, i, pb, pnb in cands[:beam]:
             if kind == 'stay':
                 new.append([bm[i][0], last, pb, pnb])
+            elif (bm[i][0], last) in alive:           # revived
+                STATS["revived"] += 1
+                new.append([alive[(bm[i][0], last)], last, pb, pnb])
             else:
                 parent.append(bm[i][0])
                 ch.append(last)

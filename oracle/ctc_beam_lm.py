@@ -34,9 +34,10 @@ top of oracle/ctc_beam.py's no-LM restatement (same candidate form, same tie rul
       char for this and every lower prefix (blank / repeat / extension alike);
     * after the last frame every non-empty prefix not ending in a space gets
       float(float(alpha * lnp(ngram)) + beta) added before the final ranking.
-  Not restated: character-based LMs (every vocabulary word one character); nodes dropped
-  from the beam but kept alive by a descendant are re-created rather than revived (as in
-  oracle/ctc_beam.py); the returned score is the LM-inclusive one (ctcdecode returns an
+    * trie-node revival as in oracle/ctc_beam.py; a revived node keeps its dictionary
+      state (a revived post-space node was necessarily reset: it has a child), and the
+      found-child branch of get_path_trie skips the dictionary check.
+  Not restated: character-based LMs (every vocabulary word one character); the returned score is the LM-inclusive one (ctcdecode returns an
   "approx_ctc" score the reference discards, decoder.py:136).
 
 Pure Python loops: small inputs only.
@@ -49,7 +50,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 
-from .ctc_beam import F32, NEG, lse, pruned_log_probs
+from .ctc_beam import F32, NEG, STATS, alive_children, lse, pruned_log_probs
 
 OOV_SCORE = -1000.0
 NUM_FLT_LOGE = float(np.float32(0.4342944819))   # decoder_utils.h: a float constant
@@ -211,6 +212,7 @@ def beam_decode_lm_one(probs: np.ndarray, size: int, beam: int, lm: ArpaLM, labe
         node_to_idx = {e[0]: i for i, e in enumerate(bm)}
         pidx = [node_to_idx.get(parent[e[0]], -1) if e[0] != 0 else -1 for e in bm]
         child_of = {(pidx[q], bm[q][1]): q for q in range(nb) if pidx[q] >= 0}
+        alive = alive_children(bm, parent, ch)
         cands = []
         ts_upd = {}
         for i in range(nb):
@@ -232,9 +234,14 @@ def beam_decode_lm_one(probs: np.ndarray, size: int, beam: int, lm: ArpaLM, labe
                 else:
                     if not allowed[cc] or (i, cc) in child_of or not att(i, cc):
                         continue
-                    st = eff_state(i, cc)
-                    if st is None or cc not in wd.next[st]:
-                        continue
+                    x = alive.get((bm[i][0], cc))      # a pruned node still in the trie
+                    if x is not None:
+                        if lp[cc] > lpc[x]:
+                            ts_upd[x] = (t, lp[cc])
+                    else:
+                        st = eff_state(i, cc)
+                        if st is None or cc not in wd.next[st]:
+                            continue
                     e = ext_val(i, cc)
                     if e != NEG:
                         cands.append((e, cc, k, 'ext', i, NEG, e))
@@ -247,6 +254,12 @@ def beam_decode_lm_one(probs: np.ndarray, size: int, beam: int, lm: ArpaLM, labe
             nd_i = bm[i][0]
             if kind == 'stay':
                 new.append([nd_i, last, pb, pnb])
+                continue
+            if (nd_i, last) in alive:                  # revived: keeps its LM state
+                x = alive[(nd_i, last)]
+                assert ch[x] != space or dst[x] == 0
+                STATS["revived"] += 1
+                new.append([x, last, pb, pnb])
                 continue
             st = eff_state(i, last)
             ns = wd.next[st][last]

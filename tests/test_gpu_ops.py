@@ -1261,6 +1261,45 @@ def test_ctc_beam_lm_orders_vs_oracle(dev, order, beam, tmp_path):
             assert abs(float(scores[n, p]) - s_) <= 1e-5 * max(1.0, abs(s_)), (n, p)
 
 
+@pytest.mark.parametrize("noise,beam", [(2.0, 100), (3.0, 100), (3.0, 32)])
+def test_ctc_beam_trie_revival_vs_oracle(dev, noise, beam):
+    """Trie-node revival (ctcdecode path_trie.cpp get_path_trie / remove): a pruned prefix
+    kept in the trie by a descendant in the beam is revived by an extension onto it (its
+    node, char frame and dictionary state kept) rather than created again.  Noisy spelled
+    sentences where the oracle revives prefixes (counted), with and without the LM: the
+    device search equals oracle/ctc_beam.py / ctc_beam_lm.py bit-exactly (ids, frames) and
+    every returned beam holds distinct strings."""
+    from oracle import ctc_beam, ctc_beam_lm as obl
+    from ds2amd.lm import ArpaScorer
+    labels = orc.LABELS
+    g = np.random.default_rng(11)
+    ps = [_spelled(s, g, noise) for s in ["THE CAT SAT ON A HAT", "I DON'T NO THEN ",
+                                          "AND THEY SAT ON A CAT", "CATS IN THEN TOO"]]
+    t = max(p.shape[0] for p in ps)
+    probs = np.full((len(ps), t, len(labels)), 1.0 / len(labels), np.float32)
+    for i, p in enumerate(ps):
+        probs[i, :p.shape[0]] = p
+    sizes = [p.shape[0] for p in ps]
+    ctc_beam.STATS["revived"] = 0
+    _beam_check(dev, probs, sizes, beam)
+    path = os.path.join(os.path.dirname(__file__), "golden", "tiny_lm.arpa")
+    scorer = ArpaScorer(path, labels, 0.8, 1.0, device=dev)
+    ids, offs, lens, scores = ops.ctc_beam_decode_lm_raw(
+        torch.from_numpy(probs).to(dev), torch.tensor(sizes, dtype=torch.int32).to(dev), beam,
+        beam, scorer)
+    ids, offs, lens = ids.cpu(), offs.cpu(), lens.cpu()
+    ref = obl.beam_decode_lm(probs, sizes, beam, obl.ArpaLM(path), labels, 0.8, 1.0)
+    assert ctc_beam.STATS["revived"] > 0
+    for n, paths in enumerate(ref):
+        got = []
+        for p in range(len(paths)):
+            k = int(lens[n, p])
+            got.append(tuple(ids[n, p, :k].tolist()))
+            assert list(got[-1]) == paths[p][1], (n, p)
+            assert offs[n, p, :k].tolist() == paths[p][2], (n, p)
+        assert len(set(got)) == len(got)
+
+
 # ---------------------------------------------------------------------------- CER / WER
 def test_edit_distance_vs_reference_semantics(dev):
     """ds2_edit_distance == get_cer_wer (data/utils.py:47-57) with Decoder.wer/.cer's

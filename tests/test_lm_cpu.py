@@ -236,3 +236,37 @@ def test_scorer_rejects_char_lms_and_binary_files(tmp_path):
     b.write_bytes(b"mmap lm http://kheafield.com/code format version 5\n\0\0\0")
     with pytest.raises(ValueError):
         ArpaScorer(str(b), LABELS, 0.8, 1.0, device="cpu")
+
+
+def _spelled_cpu(text, g, noise, peak=5.0, blank_bias=1.0):
+    frames, prev = [], None
+    for ch in text:
+        if ch == prev:
+            frames.append(0)
+        frames += [LABELS.index(ch), 0]
+        prev = ch
+    logits = g.standard_normal((len(frames), len(LABELS))).astype(np.float32) * noise
+    logits[:, 0] += blank_bias
+    logits[np.arange(len(frames)), frames] += peak
+    p = np.exp(logits - logits.max(-1, keepdims=True))
+    return (p / p.sum(-1, keepdims=True)).astype(np.float32)
+
+
+def test_beam_trie_revival_keeps_prefixes_unique():
+    """ctcdecode's PathTrie revives a pruned prefix that a kept descendant holds in the
+    trie (path_trie.cpp get_path_trie / remove) instead of creating a second node for it,
+    so every prefix is one node and a beam never holds the same string twice.  The noisy
+    spelled sentences at beam 100 revive prefixes in both searches; every returned beam
+    must hold distinct strings."""
+    from oracle import ctc_beam
+    g = np.random.default_rng(11)
+    ps = [_spelled_cpu(s, g, 2.0) for s in ["THE CAT SAT ON A HAT", "I DON'T NO THEN "]]
+    lm = obl.ArpaLM(os.path.join(HERE, "golden", "tiny_lm.arpa"))
+    for use_lm in (False, True):
+        ctc_beam.STATS["revived"] = 0
+        for p in ps:
+            out = (obl.beam_decode_lm_one(p, p.shape[0], 100, lm, LABELS, 0.8, 1.0) if use_lm
+                   else ctc_beam.beam_decode_one(p, p.shape[0], 100))
+            strings = [tuple(ids) for _, ids, _ in out]
+            assert len(set(strings)) == len(strings)
+        assert ctc_beam.STATS["revived"] > 0, use_lm
