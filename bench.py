@@ -120,13 +120,19 @@ class KernelProbe:
         return sum(ms) / len(ms), sum(self.flops) / len(self.flops), len(ms)
 
 
+PMC_SUMMARY = "r3end_pmc_traffic.csv"   # profiles/: PMC passes on the round-3 final kernels
+
+
 def pmc_traffic_per_launch(prefix="gemm", extra=("splitk_reduce_kernel",)):
     """HBM bytes per ds2_sgemm_ws launch from the newest committed PMC summary
     (profiles/r*_pmc_traffic.csv, made by scripts/pmc_traffic.sh + pmc_summary.py:
     FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE, one pass per counter)."""
     import csv
     import glob
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_traffic.csv")))
+    # the summary measured on the current kernels; else the last one by name
+    cur = os.path.join(REPO, "profiles", PMC_SUMMARY)
+    files = ([cur] if os.path.exists(cur) else
+             sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_traffic.csv"))))
     if not files:
         return None, None
     launches, total = 0, 0.0
