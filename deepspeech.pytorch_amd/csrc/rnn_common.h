@@ -158,23 +158,25 @@ static void apply_spin_limit_env() {
 // from every workgroup crowd the fabric that carries the real tiles).  Defaults from
 // scripts/gru_ab.py sweeps (the forward's first-poll delay 14 -> 10 with the same-XCD groups,
 // whose same-XCD tiles arrive sooner: 4.32-4.40 -> 4.26 us per step, `ftune`,
-// profiles/r3fa_fwd_tune.txt); DS2_RNN_TUNE="a,b,c" overrides them (diagnostic; checked at
-// every recurrence entry point).
-constexpr unsigned kRepollSleep = 1u, kFirstPollDelay = 10u, kFirstPollDelayBwd = 14u;
-static __constant__ unsigned g_rnn_tune[3] = {kRepollSleep, kFirstPollDelay, kFirstPollDelayBwd};
+// profiles/r3fa_fwd_tune.txt); [3] s_sleep(1) units between the flag hand-off's polls.
+// DS2_RNN_TUNE="a,b,c,d" overrides them (diagnostic; checked at every recurrence entry point).
+constexpr unsigned kRepollSleep = 1u, kFirstPollDelay = 10u, kFirstPollDelayBwd = 14u,
+                   kFlagPollSleep = 1u;
+static __constant__ unsigned g_rnn_tune[4] = {kRepollSleep, kFirstPollDelay, kFirstPollDelayBwd,
+                                              kFlagPollSleep};
 
 static void apply_rnn_tune_env() {
-  static unsigned applied[3] = {kRepollSleep, kFirstPollDelay, kFirstPollDelayBwd};
-  unsigned v[3] = {kRepollSleep, kFirstPollDelay, kFirstPollDelayBwd};
+  static unsigned applied[4] = {kRepollSleep, kFirstPollDelay, kFirstPollDelayBwd, kFlagPollSleep};
+  unsigned v[4] = {kRepollSleep, kFirstPollDelay, kFirstPollDelayBwd, kFlagPollSleep};
   const char* e = getenv("DS2_RNN_TUNE");
-  for (int i = 0; e != nullptr && e[0] != 0 && i < 3; ++i) {
+  for (int i = 0; e != nullptr && e[0] != 0 && i < 4; ++i) {
     char* end = nullptr;
     v[i] = static_cast<unsigned>(strtoul(e, &end, 10));
     e = (end != nullptr && *end == ',') ? end + 1 : nullptr;
   }
-  if (v[0] == applied[0] && v[1] == applied[1] && v[2] == applied[2]) return;
+  if (v[0] == applied[0] && v[1] == applied[1] && v[2] == applied[2] && v[3] == applied[3]) return;
   if (hipMemcpyToSymbol(HIP_SYMBOL(g_rnn_tune), v, sizeof(v)) == hipSuccess)
-    for (int i = 0; i < 3; ++i) applied[i] = v[i];
+    for (int i = 0; i < 4; ++i) applied[i] = v[i];
 }
 
 __device__ __forceinline__ void sleep_units(unsigned k) {
@@ -252,7 +254,7 @@ __device__ __forceinline__ bool flags_wait(const unsigned* flags, int count, uns
                                                           __HIP_MEMORY_SCOPE_AGENT)
                                       : target;
       if (__ballot(v < target) == 0ull) break;
-      __builtin_amdgcn_s_sleep(1);
+      sleep_units(g_rnn_tune[3]);
       if (++spins > g_spin_limit) {
         if (lane == 0) __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         ok = 0;

@@ -92,6 +92,10 @@ if len(sys.argv) > 1 and sys.argv[1] == "prewaves":
     variants = {f"bwd-x6pre-w{w}": {"DS2_GRU_X6": "1", "DS2_GRU_X6_BWD": "2",
                                     "DS2_GRU_X6_BWD_WAVES": w, "DS2_RNN_HANDOFF_BWD": "flags"}
                 for w in ("8", "4")}
+if len(sys.argv) > 1 and sys.argv[1] == "flagpoll":
+    # s_sleep(1) units between the flag hand-off's polls (the pre-split backward's wait)
+    variants = {f"bwd-poll-{t}": {"DS2_GRU_X6": "1", "DS2_RNN_HANDOFF": "", "DS2_RNN_TUNE": t}
+                for t in ("1,10,14,1", "1,10,14,0", "1,10,14,2", "1,10,14,4")}
 rounds = int(os.environ.get("AB_ROUNDS", "3"))
 variants = {f"{k}#{r}": v for r in range(rounds) for k, v in variants.items()}
 ref = None
