@@ -354,6 +354,7 @@ __device__ __forceinline__ void beam_wave_best(float& bs, int& bk) {
 // trie: dnext [S][C] arcs, dmask [S] the arcs as a char bit mask, dword [S] the word a
 // state spells (-1 none); state 0 = start, fstate = after a word's space (no arcs).
 struct BeamLm {
+  int nstates;   // dict_states: an arc outside [0, nstates) reads as no arc (-1)
   const int* dnext;
   const unsigned long long* dmask;
   const int* dword;
@@ -788,7 +789,8 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
                 if (n1 > 0) b_hist[nxt][e][n1 - 1] = L.dword[si];
                 b_lms[nxt][e] = 0.f;
               } else {
-                const int ns = L.dnext[(int64_t)si * C + c];
+                int ns = L.dnext[(int64_t)si * C + c];
+                if ((unsigned)ns >= (unsigned)L.nstates) ns = L.fstate;   // a malformed arc
                 b_dst[nxt][e] = ns;
                 for (int h = 0; h < n1; ++h) b_hist[nxt][e][h] = b_hist[cur][i][h];
                 b_lms[nxt][e] = lm_term(L, &b_hist[cur][i][0], L.dword[ns]);
@@ -1160,14 +1162,16 @@ ds2_status_t ds2_ctc_beam_decode(const float* probs, int n, int t_max, int c, in
 ds2_status_t ds2_ctc_beam_decode_lm(const float* probs, int n, int t_max, int c, int64_t stride_n,
                                     int64_t stride_t, const int* sizes, int blank, int beam_width,
                                     int cutoff_top_n, double cutoff_prob, int top_paths,
-                                    int space_id, int lm_order, int start_id, double alpha,
-                                    double beta, const int* dict_next, const void* dict_mask,
-                                    const int* dict_word, int dict_states, const int* lm_table,
-                                    int64_t lm_slots, int* out_ids, int* out_offsets,
-                                    int* out_lens, float* out_scores, void* ws, size_t ws_bytes,
+                                    int space_id, int lm_order, int start_id, int lm_vocab,
+                                    double alpha, double beta, const int* dict_next,
+                                    const void* dict_mask, const int* dict_word, int dict_states,
+                                    int dict_cols, const int* lm_table, int64_t lm_slots,
+                                    int* out_ids, int* out_offsets, int* out_lens,
+                                    float* out_scores, void* ws, size_t ws_bytes,
                                     ds2_stream_t stream) {
   if (space_id < 0 || space_id >= c || space_id == blank || lm_order < 1 ||
-      lm_order > LM_MAX_ORDER || start_id < 0 || dict_states < 2 || dict_next == nullptr ||
+      lm_order > LM_MAX_ORDER || start_id < 0 || start_id >= lm_vocab || dict_states < 2 ||
+      dict_cols != c || dict_next == nullptr ||
       dict_mask == nullptr || dict_word == nullptr || lm_table == nullptr || lm_slots < 1 ||
       (lm_slots & (lm_slots - 1)) != 0 || lm_slots > (int64_t(1) << 31) || c > 64)
     return DS2_INVALID_VALUE;
@@ -1178,6 +1182,7 @@ ds2_status_t ds2_ctc_beam_decode_lm(const float* probs, int n, int t_max, int c,
   L.tab = reinterpret_cast<const int4*>(lm_table);
   L.tmask = static_cast<unsigned>(lm_slots - 1);
   L.fstate = dict_states - 1;
+  L.nstates = dict_states;
   L.order = lm_order;
   L.start = start_id;
   L.space = space_id;

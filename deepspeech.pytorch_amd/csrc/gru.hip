@@ -1345,6 +1345,7 @@ bool launch_gru_bwd_dh(int t_max, int n, int h, int num_dirs, const float* dy, i
                        const float* coef, const int* lens, float* dgates_x, float* dgates_h,
                        float* ring, unsigned* ctrs, unsigned* err, unsigned long long* stamps,
                        double* dbp, size_t lds_pad, hipStream_t st);
+int gru_bwd_x6_grid(int n, int h, int num_dirs);
 void launch_gru_coef(const float* gates, const float* h_all, const int* lens, int t_max, int n,
                      int h, int num_dirs, float* coef, hipStream_t st);
 }  // namespace ds2
@@ -1618,6 +1619,24 @@ static const void* bwd_rs_fn(int need) {
                        num_dirs, UB, BT, dy, dy_dirs, wpt, h_all, gates, lens, dgates_x,     \
                        dgates_h, dhs);                                                       \
     break;
+
+static inline bool rs_enabled();
+// workgroups the persistent backward launch holds at once (gru_bwd_run's choice), 0 for the
+// per-step kernels
+int ds2_gru_bwd_grid(int n, int h, int num_dirs) {
+  if (n < 1 || h < 1 || (num_dirs != 1 && num_dirs != 2)) return 0;
+  const int UB = (h + GU - 1) / GU, BT = (n + GB - 1) / GB;
+  const int grid = mapped_grid(UB * num_dirs, BT);
+  if (grid > num_cus()) return 0;
+  if (dop_enabled() && flags_mode() && (h % GU) == 0 && UB <= 8 * GW) {
+    if (!rs_enabled() && !gru_dh_bwd_opted_in()) {
+      const int g = gru_bwd_x6_grid(n, h, num_dirs);
+      if (g > 0) return g;
+    }
+    return grid;
+  }
+  return (persistent_enabled() && 3 * h <= KC_BWD && (h % 4) == 0) ? grid : 0;
+}
 
 ds2_status_t ds2_gru_bwd(int t_max, int n, int h, int num_dirs, const float* dy, int dy_dirs,
                          const float* w_hh_f, const float* w_hh_r, const float* h_all,

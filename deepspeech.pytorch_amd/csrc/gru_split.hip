@@ -111,6 +111,7 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     float* __restrict__ gates, float* __restrict__ coef, float* __restrict__ hx,
     unsigned* __restrict__ counters, unsigned* __restrict__ err,
     unsigned long long* __restrict__ stamps, int xmode) {
+  static_assert(2 * NP <= 64, "tsame holds a wave's tiles");
   constexpr int RP = 3 * GU + 1;
   constexpr bool SENT = HM == 1;
   constexpr int NSLOT = SENT ? kRingSlots : 2;
@@ -128,7 +129,7 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   const unsigned my_xcc = xcc_id() + 1u;
   if (xg && threadIdx.x == 0)
     __hip_atomic_store(xtab + ub, my_xcc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  unsigned tsame = 0;           // bit i: this wave's tile t_first + i comes from this XCD
+  uint64_t tsame = 0;           // bit i: this wave's tile t_first + i comes from this XCD
   const int n0 = bt * GB;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -226,7 +227,7 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
         const unsigned long long same = __ballot(v == my_xcc);   // an id never seen: no bit
 #pragma unroll
         for (int i = 0; i < 2 * NP; ++i)
-          if (t_first + i < UB && ((same >> (t_first + i)) & 1ull)) tsame |= 1u << i;
+          if (t_first + i < UB && ((same >> (t_first + i)) & 1ull)) tsame |= 1ull << i;
       }
       const int base = (((s - 1) % NSLOT) * slot_floats + grp_off + t_first * 256 + lane * 4) * 4;
       if (SENT) sleep_units(g_rnn_tune[1]);
@@ -234,7 +235,7 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
 #pragma unroll
       for (int i = 0; i < 2 * NP; ++i) {
         const int off = (i < 2 * np && t_first + i < UB)
-                            ? base + i * 1024 + (((tsame >> i) & 1u) ? aoff : 0) : 0x7ffffff0;
+                            ? base + i * 1024 + (((tsame >> i) & 1ull) ? aoff : 0) : 0x7ffffff0;
         hv[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(x_rs, off, 0, kSc1));
       }
       asm volatile("" ::: "memory");
@@ -270,7 +271,7 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
           if (((pend >> (i >> 1)) & 1u) && t_first + i < UB)
             hv[i] = __builtin_bit_cast(
                 f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                           x_rs, base + i * 1024 + (((tsame >> i) & 1u) ? aoff : 0), 0, kSc1));
+                           x_rs, base + i * 1024 + (((tsame >> i) & 1ull) ? aoff : 0), 0, kSc1));
       }
 #pragma unroll
       for (int g = 0; g < 3; ++g) {
@@ -389,6 +390,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW / 4,
     float* __restrict__ gx, unsigned* __restrict__ counters, unsigned* __restrict__ err,
     unsigned long long* __restrict__ stamps, double* __restrict__ dbp, int xmode) {
   static_assert(!PRE || HM == 0, "pre-split tiles use the flag hand-off");
+  static_assert(2 * NP <= 64, "tsame holds a wave's tiles");
   constexpr int RP = GU + 1;
   constexpr bool SENT = HM == 1;
   constexpr int NSLOT = SENT ? kRingSlots : 2;
@@ -417,7 +419,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW / 4,
   const unsigned my_xcc = xcc_id() + 1u;
   if (xg && threadIdx.x == 0)   // published by the step-0 flag (wave 0 drains before it)
     __hip_atomic_store(xtab + ub, my_xcc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  unsigned tsame = 0;           // bit i: this wave's tile t_first + i comes from this XCD
+  uint64_t tsame = 0;           // bit i: this wave's tile t_first + i comes from this XCD
   const int pairs = (NB3 + 1) >> 1;
   const int p0 = (pairs * wave) / NW;
   const int np = (pairs * (wave + 1)) / NW - p0;   // host guarantees np <= NP
@@ -501,7 +503,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW / 4,
           const unsigned long long same = __ballot(v == my_xcc);
 #pragma unroll
           for (int i = 0; i < 2 * NP; ++i)
-            if ((same >> ((t_first + i) % UB)) & 1ull) tsame |= 1u << i;
+            if ((same >> ((t_first + i) % UB)) & 1ull) tsame |= 1ull << i;
         }
         // LWP pairs' runs in flight, the next pair's issued as each pair is multiplied
         const int tb0 = (((s - 1) & 1) * slot_floats + grp_off + t_first * TF) * 4;
@@ -509,7 +511,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW / 4,
         u32x2 lo[2 * NP];
         auto load_run = [&](int i) {
           const bool ok = i < 2 * np && t_first + i < NB3;
-          const int to = tb0 + i * TF * 4 + (((tsame >> i) & 1u) ? aoff : 0);
+          const int to = tb0 + i * TF * 4 + (((tsame >> i) & 1ull) ? aoff : 0);
           hm[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
                                                 x_rs, ok ? to + lane * 16 : 0x7ffffff0, 0, kSc1));
           lo[i] = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(
@@ -768,6 +770,18 @@ bool launch_gru_fwd_x6(int hm, int t_max, int n, int h, int num_dirs, const floa
   void* args[] = {&T_, &N_, &H_, &D_, &UB_, &BT_, &xproj, &w_hh_f, &w_hh_r, &b_hh_f,
                   &b_hh_r, &lens, &h_all, &gates, &coef, &ring, &ctrs, &err, &stamps, &XM_};
   return rnn_launch(fn, dim3(grid), dim3(XT), args, lds_pad, st) == hipSuccess;
+}
+
+// grid of the x6 backward launch_gru_bwd_x6 would make (flag hand-off), -1 if it declines
+int gru_bwd_x6_grid(int n, int h, int num_dirs) {
+  const int mode = x6_bwd_mode();
+  if (mode == 0 || (h % GU) != 0) return -1;
+  const int UB = h / GU, BT = (n + GB - 1) / GB;
+  if (bwd_x6_fn((3 * UB + 1) / 2, 0, x6_bwd_waves(), mode == 2) == nullptr) return -1;
+  const char* xe = getenv("DS2_GRU_XCD");
+  const bool xcd_on = !(xe != nullptr && xe[0] == '0');
+  return (mode == 2 && xcd_on && xgrp_fits(UB, BT, num_dirs)) ? xgrp_grid(UB, BT, num_dirs)
+                                                                : mapped_grid(UB * num_dirs, BT);
 }
 
 bool launch_gru_bwd_x6(int hm, int t_max, int n, int h, int num_dirs, const float* dy, int dy_dirs,

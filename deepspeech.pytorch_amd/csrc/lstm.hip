@@ -1118,6 +1118,19 @@ size_t ds2_lstm_bwd_workspace_size(int n, int h, int num_dirs) {
                        num_dirs, UB, BT, dy, dy_dirs, wpt, c_all, gates, lens, dgates, dcs);  \
     break;
 
+// workgroups one persistent backward launch holds at once (a batch larger than the chip
+// runs as consecutive launches of at most this many), 0 for the per-step kernels
+int ds2_lstm_bwd_grid(int n, int h, int num_dirs) {
+  if (n < 1 || h < 1 || (num_dirs != 1 && num_dirs != 2)) return 0;
+  if (!persistent_enabled() || (h % 4) != 0) return 0;
+  const int UB = (h + GU - 1) / GU, BT = (n + GB - 1) / GB;
+  int bts = lstm_bts(UB, num_dirs, BT);
+  if (bts == 2 && 4 * h > 2 * 4 * GW * 32) bts = 1;
+  const int BTW = (BT + bts - 1) / bts;
+  const int g = mapped_grid(UB * num_dirs, lstm_chunk_tiles(UB, num_dirs, BTW));
+  return g <= num_cus() ? g : 0;
+}
+
 ds2_status_t ds2_lstm_bwd(int t_max, int n, int h, int num_dirs, const float* dy, int dy_dirs,
                           const float* w_hh_f, const float* w_hh_r, const float* c_all,
                           const float* gates, const int* lens, float* dgates, unsigned* err_out,

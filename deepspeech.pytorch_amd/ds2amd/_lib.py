@@ -69,6 +69,11 @@ _PROTOS = {
     "ds2_gru_fwd": (_c_int, [_c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                              _vp, _vp, _vp, _sz, _vp]),
     "ds2_gru_bwd_workspace_size": (_sz, [_c_int, _c_int, _c_int]),
+    "ds2_gru_bwd_grid": (_c_int, [_c_int, _c_int, _c_int]),
+    "ds2_lstm_bwd_grid": (_c_int, [_c_int, _c_int, _c_int]),
+    "ds2_test_occupy": (_c_int, [_c_int, _c_int, _c_int, _vp, _vp]),
+    "ds2_test_rnn_launch_lds": (_c_int, [_c_int, _c_int, _vp, _vp]),
+    "ds2_test_timestamp": (_c_int, [_vp, _vp]),
     "ds2_gru_bwd": (_c_int, [_c_int, _c_int, _c_int, _c_int, _vp, _c_int, _vp, _vp, _vp, _vp,
                              _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
     "ds2_gru_bwd_bias": (_c_int, [_c_int, _c_int, _c_int, _c_int, _vp, _c_int, _vp, _vp, _vp,
@@ -102,8 +107,9 @@ _PROTOS = {
                                      _vp, _sz, _vp]),
     "ds2_ctc_beam_decode_lm": (_c_int, [_vp, _c_int, _c_int, _c_int, _c_i64, _c_i64, _vp, _c_int,
                                         _c_int, _c_int, ctypes.c_double, _c_int, _c_int, _c_int,
-                                        _c_int, ctypes.c_double, ctypes.c_double, _vp, _vp, _vp,
-                                        _c_int, _vp, _c_i64, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
+                                        _c_int, _c_int, ctypes.c_double, ctypes.c_double, _vp, _vp,
+                                        _vp, _c_int, _c_int, _vp, _c_i64, _vp, _vp, _vp, _vp, _vp,
+                                        _sz, _vp]),
     "ds2_comm_id_bytes": (_sz, []),
     "ds2_comm_get_unique_id": (_c_int, [_vp]),
     "ds2_comm_init": (_c_int, [_vp, _vp, _c_int, _c_int, _c_int]),

@@ -353,8 +353,9 @@ def ctc_beam_decode_lm_raw(probs: torch.Tensor, sizes: Optional[torch.Tensor], b
     _lib.call("ds2_ctc_beam_decode_lm", probs.data_ptr(), n, t, c, probs.stride(0),
               probs.stride(1), _p(sizes), int(blank), int(beam_width), int(cutoff_top_n),
               float(cutoff_prob), int(top_paths), scorer.space, scorer.order, scorer.start_id,
-              scorer.alpha, scorer.beta, scorer.dict_next.data_ptr(), scorer.dict_mask.data_ptr(),
-              scorer.dict_word.data_ptr(), scorer.n_states, scorer.table.data_ptr(),
+              len(scorer.vocab), scorer.alpha, scorer.beta, scorer.dict_next.data_ptr(),
+              scorer.dict_mask.data_ptr(), scorer.dict_word.data_ptr(), scorer.n_states,
+              int(scorer.dict_next.shape[1]), scorer.table.data_ptr(),
               scorer.table_mask + 1, ids.data_ptr(), offs.data_ptr(), lens.data_ptr(),
               scores.data_ptr(), ws.data_ptr(), ws.numel(), _stream())
     return ids, offs, lens, scores
@@ -751,18 +752,19 @@ def set_cooperative_guard(fn) -> None:
     _COOP_GUARD[0] = fn
 
 
-def persistent_grid_estimate(n: int, h: int, nd: int) -> int:
-    """Upper bound of the persistent recurrence's grid (rnn_common.h mapped_grid: 16 units x
-    16 samples per workgroup, unit-block pairs padded to multiples of 8); the LSTM's 32-sample
-    workgroups and batch chunks only make it smaller (never above the chip's CU count)."""
-    ub = (h + 15) // 16
-    return 8 * ((ub * nd + 7) // 8) * ((n + 15) // 16)
+def persistent_bwd_grid(cell: str, n: int, h: int, nd: int) -> int:
+    """Workgroups the persistent backward recurrence of this shape holds at once, as the
+    library will launch it (ds2_gru_bwd_grid / ds2_lstm_bwd_grid; 0 for the per-step
+    kernels, which need no co-residency)."""
+    return _lib.size("ds2_gru_bwd_grid" if cell == "gru" else "ds2_lstm_bwd_grid", n, h, nd)
 
 
-def _guard_cooperative(n, h, nd):
+def _guard_cooperative(cell, n, h, nd):
     g = _COOP_GUARD[0]
     if g is not None:
-        g(persistent_grid_estimate(n, h, nd))
+        grid = persistent_bwd_grid(cell, n, h, nd)
+        if grid > 0:
+            g(grid)
 
 
 class GRULayerFn(torch.autograd.Function):
@@ -811,7 +813,7 @@ class GRULayerFn(torch.autograd.Function):
         w_hh_f = weights[1]
         w_hh_r = weights[5] if nd == 2 else None
         ws = _ws(_lib.size("ds2_gru_bwd_workspace_size", n, h, nd), dev)
-        _guard_cooperative(n, h, nd)
+        _guard_cooperative("gru", n, h, nd)
         # bias gradients straight into their slots, summed by the recurrence kernel
         dbias = [grad_like(weights[4 * d + k]) for d in range(nd) for k in (2, 3)]
         _lib.call("ds2_gru_bwd_bias", t, n, h, nd, dy.data_ptr(), dy_dirs, w_hh_f.data_ptr(),
@@ -865,7 +867,7 @@ class LSTMLayerFn(torch.autograd.Function):
         w_hh_f = weights[1]
         w_hh_r = weights[5] if nd == 2 else None
         ws = _ws(_lib.size("ds2_lstm_bwd_workspace_size", n, h, nd), dev)
-        _guard_cooperative(n, h, nd)
+        _guard_cooperative("lstm", n, h, nd)
         _lib.call("ds2_lstm_bwd", t, n, h, nd, dy.data_ptr(), dy_dirs, w_hh_f.data_ptr(),
                   _p(w_hh_r), c_all.data_ptr(), gates.data_ptr(), lens.data_ptr(), dg.data_ptr(),
                   rnn_status_word(dev).data_ptr(), ws.data_ptr(), ws.numel(), _stream())

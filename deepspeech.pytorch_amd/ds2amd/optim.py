@@ -258,12 +258,25 @@ class ParamBroadcaster:
 
 def rccl_channel_cap() -> int:
     """The CTA budget RCCL may hold while a persistent recurrence runs:
-    NCCL_MAX_NCHANNELS, which init_distributed() defaults to 32 (the same default applies
-    when the process group was created elsewhere)."""
+    NCCL_MAX_NCHANNELS, which init_distributed() sets to 32 before the communicator exists.
+    Unset (a process group created elsewhere: RCCL then picks its own channel count) the
+    budget is the conservative 64, so the guard waits rather than trusting a count nobody
+    capped."""
     try:
-        return int(os.environ.get("NCCL_MAX_NCHANNELS", "32"))
-    except ValueError:
-        return 32
+        return int(os.environ["NCCL_MAX_NCHANNELS"])
+    except (KeyError, ValueError):
+        return 64
+
+
+def global_status_word(word: torch.Tensor, group=None) -> torch.Tensor:
+    """Make a per-rank status word global, in place: MAX over the ranks (any rank's non-zero
+    word becomes every rank's).  The step's skip decision must be one decision: a rank whose
+    recurrence failed has already summed its NaN gradients into every rank's buckets, so
+    every rank skips the update and every rank raises at the same step (no rank is left
+    waiting in the next collective).  A no-op without a process group or at world 1."""
+    if dist.is_initialized() and dist.get_world_size(group) > 1:
+        dist.all_reduce(word, op=dist.ReduceOp.MAX, group=group)
+    return word
 
 
 class _StreamDone:
@@ -332,15 +345,20 @@ class GradAllReducer:
     producing earlier layers' gradients.  ``finish()`` waits and applies 1/world
     (exact for power-of-two worlds, so it equals DDP's divide-then-sum bit for bit).
 
-    CU budget: the recurrences' backward is ONE cooperative launch that needs all its
-    workgroups resident at once (208 of 256 CUs at cfg2).  ``guard_cooperative(grid)`` is
-    called before each such launch; when the grid plus RCCL's CTA cap would not fit the
-    chip, the compute stream first waits for the all-reduces already in flight (a stream
-    wait, no host sync), so a collective never holds CUs a spinning recurrence needs.
+    CU budget: each recurrence's backward is ONE persistent launch (a plain launch sized to
+    one workgroup per CU: 200 of 256 CUs at cfg2) whose workgroups spin on each other's
+    hand-offs, so all of them must be resident at once; the hardware gives no such guarantee
+    beside a collective that holds CUs.  ``guard_cooperative(grid)`` is called before each
+    such launch; when the grid plus the CTAs the collectives in flight may hold
+    (``collective_ctas``: RCCL's channel cap at world > 1) would not fit the chip, the compute
+    stream first waits for the all-reduces already in flight (a stream wait, no host sync),
+    so a collective never holds CUs a spinning recurrence needs.  ``collective_ctas`` can be
+    given explicitly (the one-GPU residency test drives the guard at world 1 with an
+    occupying kernel registered through ``track``).
     """
 
     def __init__(self, flat: FlatParams, bucket_mb: float = 40.0, group=None,
-                 comm: Optional[RcclComm] = None):
+                 comm: Optional[RcclComm] = None, collective_ctas: Optional[int] = None):
         self.flat = flat
         self.group = group
         self.comm = comm     # None: torch.distributed; else ds2_allreduce_bucket
@@ -364,7 +382,10 @@ class GradAllReducer:
         self.cus = 0
         if flat.flat.is_cuda:
             self.cus = torch.cuda.get_device_properties(flat.flat.device).multi_processor_count
-        self.rccl_ctas = rccl_channel_cap()
+        if collective_ctas is None:
+            collective_ctas = rccl_channel_cap() if self.world > 1 else 0
+        self.rccl_ctas = int(collective_ctas)
+        self.extra = []            # in-flight work registered by track()
         self._hooks = []
         # hooks whenever a process group exists (world 1 included: that exercises the
         # RCCL path on a single-GPU box; the all-reduce is then a no-op copy)
@@ -382,6 +403,12 @@ class GradAllReducer:
         self.pending = [b[2] for b in self.buckets]
         self.handles = [None] * len(self.buckets)
         self.issued_from_hooks = 0
+        self.extra = []
+
+    def track(self, handle):
+        """Register other in-flight work that may hold CUs (an object with ``wait()`` that
+        makes the current stream wait for it): the guard waits for it like a bucket."""
+        self.extra.append(handle)
 
     def _on_ready(self, p):
         self.flat.adopt(p, self.param_offset[id(p)])
@@ -398,11 +425,11 @@ class GradAllReducer:
         return dist.all_reduce(bucket, group=self.group, async_op=True)
 
     def guard_cooperative(self, grid: int):
-        if self.world <= 1 or self.cus <= 0:
+        if self.cus <= 0 or self.rccl_ctas <= 0:
             return
         if min(grid, self.cus) + self.rccl_ctas <= self.cus:
             return
-        for h in self.handles:
+        for h in list(self.handles) + self.extra:
             if h is not None:
                 h.wait()
                 self.guard_waits += 1

@@ -28,7 +28,8 @@ from . import _lib, ops
 from .ctc import CTCLoss
 from .decoder import GreedyDecoder
 from .ops import _stream
-from .optim import FlatParams, FusedSGD, GradAllReducer, ParamBroadcaster, RcclComm
+from .optim import (FlatParams, FusedSGD, GradAllReducer, ParamBroadcaster, RcclComm,
+                    global_status_word)
 
 
 def reduce_tensor(tensor, world_size):
@@ -255,7 +256,11 @@ class Trainer:
         # clip + SGD; always taken for NaN data (see module docstring).  Skipped on the device
         # when a persistent recurrence reported a hand-off failure this step: its outputs are
         # NaN and the update would write NaN into every parameter and momentum slot before the
-        # host sees the error (the word is 0 in a normal step; no host sync)
+        # host sees the error (the word is 0 in a normal step; no host sync).  With several
+        # ranks the word is first made global (MAX over the ranks): the failing rank's NaN
+        # gradients are already in every rank's buckets, so all ranks skip and all raise.
+        if self.world > 1:
+            global_status_word(self._rnn_word, self.reducer.group)
         self.optimizer.step(skip_flag=self._rnn_word)
         if side is not None:
             torch.cuda.current_stream(self.device).wait_stream(side)

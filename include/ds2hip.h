@@ -240,6 +240,12 @@ size_t ds2_gru_bwd_workspace_size(int n, int h, int num_dirs);
  * (model.py:107), dy_dirs = num_dirs: per-direction output gradient.
  * dgates_x: [T][N][D][3H] grad wrt xproj;  dgates_h: [T][N][D][3H] grad wrt
  * W_hh h + b_hh.  Weight gradients are then plain GEMMs (see ds2amd/ops.py). */
+/* Workgroups the persistent backward recurrence holds at once for this shape (one per
+ * CU, all resident together: they spin on each other's hand-offs), 0 when the shape runs
+ * the per-step kernels.  What a concurrent collective must leave free (DESIGN.md §6;
+ * optim.GradAllReducer.guard_cooperative).                                     */
+int ds2_gru_bwd_grid(int n, int h, int num_dirs);
+int ds2_lstm_bwd_grid(int n, int h, int num_dirs);
 ds2_status_t ds2_gru_bwd(int t_max, int n, int h, int num_dirs, const float* dy, int dy_dirs,
                          const float* w_hh_f, const float* w_hh_r, const float* h_all,
                          const float* gates, const int* lens, float* dgates_x, float* dgates_h,
@@ -373,17 +379,34 @@ ds2_status_t ds2_ctc_beam_decode(const float* probs, int n, int t_max, int c, in
  * as char bits, dict_word int32 [dict_states] the word id a state spells (-1 none);
  * lm_table int32 [lm_slots][8] {w0..w5 (-1 padded), log10 prob bits, log10 backoff
  * bits}, w0 = -1 marks an empty slot, FNV-1a over w0..w5 + avalanche, linear probing,
- * lm_slots a power of two.  lm_order <= 6; start_id = the id of "<s>"; c <= 64.
+ * lm_slots a power of two.  lm_order <= 6; start_id = the id of "<s>" (< lm_vocab, the
+ * LM's word count); dict_cols = the label count dict_next was built for (must equal c);
+ * an arc past dict_states is treated as leading to the post-space state; c <= 64.
  * Same outputs and workspace as ds2_ctc_beam_decode (scores include the LM terms). */
 ds2_status_t ds2_ctc_beam_decode_lm(const float* probs, int n, int t_max, int c, int64_t stride_n,
                                     int64_t stride_t, const int* sizes, int blank, int beam_width,
                                     int cutoff_top_n, double cutoff_prob, int top_paths,
-                                    int space_id, int lm_order, int start_id, double alpha,
-                                    double beta, const int* dict_next, const void* dict_mask,
-                                    const int* dict_word, int dict_states, const int* lm_table,
-                                    int64_t lm_slots, int* out_ids, int* out_offsets,
-                                    int* out_lens, float* out_scores, void* ws, size_t ws_bytes,
+                                    int space_id, int lm_order, int start_id, int lm_vocab,
+                                    double alpha, double beta, const int* dict_next,
+                                    const void* dict_mask, const int* dict_word, int dict_states,
+                                    int dict_cols, const int* lm_table, int64_t lm_slots,
+                                    int* out_ids, int* out_offsets, int* out_lens,
+                                    float* out_scores, void* ws, size_t ws_bytes,
                                     ds2_stream_t stream);
+
+/* ------------------------------------------------------------------------ */
+/* Residency test hooks (csrc/residency.hip; not on the training path).  ds2_test_occupy:
+ * `ctas` one-wave workgroups with lds_kb KB of dynamic LDS each (> 80: alone on their CU,
+ * no recurrence workgroup fits beside), each spinning for max_us microseconds on the
+ * device clock, recording rec[4*i..4*i+3] = {start, end (s_memrealtime, 100 MHz),
+ * XCC id, HW_ID}.  ds2_test_rnn_launch_lds: the same with 94 KB of static LDS launched
+ * through the recurrences' launcher and its 80 KB pad (the pad must be clamped to fit).
+ * ds2_test_timestamp: *out = s_memrealtime when the stream reaches it.         */
+ds2_status_t ds2_test_occupy(int ctas, int lds_kb, int max_us, unsigned long long* rec,
+                             ds2_stream_t stream);
+ds2_status_t ds2_test_rnn_launch_lds(int ctas, int max_us, unsigned long long* rec,
+                                     ds2_stream_t stream);
+ds2_status_t ds2_test_timestamp(unsigned long long* out, ds2_stream_t stream);
 
 /* ------------------------------------------------------------------------ */
 /* Data-parallel gradient exchange over RCCL (SURVEY §8b allreduce_bucket /

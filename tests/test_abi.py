@@ -93,10 +93,14 @@ def test_comm_and_lm_decode_argument_checks():
     assert lib.ds2_comm_init(None, None, 1, 0, 0) == 1
     assert lib.ds2_comm_get_unique_id(None) == 1
     # probs, n, t, c, strides, sizes, blank, beam, top_n, cutoff, top_paths, space, order, start,
-    # alpha, beta, dict_next, dict_mask, dict_word, states, table, slots, outs..., ws, ws_bytes, stream
-    base = [1, 1, 1, 30, 30, 30, None, 0, 4, 40, 1.0, 4, 29, 3, 0, 0.8, 1.0, 1, 1, 1, 5, 1, 8,
-            1, 1, 1, 1, 1, 1 << 20, None]
-    for i, bad in [(13, 7), (13, 0), (22, 12), (11, 0), (12, 30), (12, 0), (20, 1)]:
+    # vocab, alpha, beta, dict_next, dict_mask, dict_word, states, cols, table, slots, outs...,
+    # ws, ws_bytes, stream
+    base = [1, 1, 1, 30, 30, 30, None, 0, 4, 40, 1.0, 4, 29, 3, 0, 9, 0.8, 1.0, 1, 1, 1, 5, 30, 1,
+            8, 1, 1, 1, 1, 1, 1 << 20, None]
+    # order 7 / 0, slots 12 (not a power of two), top_paths 0, space = c / = blank, states 1,
+    # start >= vocab, a dictionary built for 29 labels on 30-label probs
+    for i, bad in [(13, 7), (13, 0), (24, 12), (11, 0), (12, 30), (12, 0), (21, 1), (15, 0),
+                   (22, 29)]:
         args = list(base)
         args[i] = bad
         assert lib.ds2_ctc_beam_decode_lm(*args) == 1, (i, bad)

@@ -202,14 +202,18 @@ def _ds2_worker(rank, world, port, out_q):
     loss.backward()
     issued = red.issued_from_hooks
     in_flight = sum(h is not None for h in red.handles)
-    # CU budget: the 208-workgroup cooperative backward plus RCCL's
-    # 32-CTA default fits 256 CUs -> no wait; a 64-channel cap would not -> the compute
-    # stream waits for every all-reduce in flight
+    # CU budget: the 200-workgroup persistent backward plus the
+    # 32-CTA cap init_distributed sets fits 256 CUs -> no wait; with no cap set the budget
+    # is RCCL's 64 (rccl_channel_cap) and 200 + 64 does not fit -> the compute stream waits
+    # for every all-reduce in flight
+    from ds2amd.optim import rccl_channel_cap
+    assert red.rccl_ctas == rccl_channel_cap()
     red.cus = 256
-    red.guard_cooperative(208)
+    red.rccl_ctas = 32
+    red.guard_cooperative(200)
     waits_fit = red.guard_waits
     red.rccl_ctas = 64
-    red.guard_cooperative(208)
+    red.guard_cooperative(200)
     waits_over = red.guard_waits
     red.finish()
     out_q.put((rank, red.buckets, flat.offsets, [p.numel() for p in flat.params], flat.numel,
@@ -304,3 +308,47 @@ def test_flat_params_stacks_w_ih_pairs():
     assert [id(p) for p, _ in opt._model_order()] == [id(p) for p in params]
     # unpaired tensors are not stacked
     assert ops._stacked_rows(params[0], params[1]) is None
+
+
+def _status_worker(rank, world, port, out_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from ds2amd.optim import global_status_word
+    w = torch.zeros(1, dtype=torch.int32)
+    if rank == 1:
+        w.fill_(1)                 # this rank's recurrence timed out (RNN_ERR_HANDOFF_TIMEOUT)
+    global_status_word(w)
+    out_q.put((rank, int(w.item())))
+    dist.destroy_process_group()
+
+
+def test_skip_decision_is_global():
+    """a hand-off failure on ONE rank must skip the SGD step on EVERY rank (its
+    NaN gradients were already all-reduced into every rank's buckets) and make every rank
+    raise: the Trainer makes its status word global (MAX over the ranks) before the step.
+    gloo world 2, the word set on rank 1 only -> both ranks see it."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_status_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(world)])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res == [(0, 1), (1, 1)]
+
+
+def test_rccl_cap_defaults(monkeypatch):
+    """The guard's CTA budget: NCCL_MAX_NCHANNELS when set (init_distributed sets 32 before the
+    communicator exists), the conservative 64 when nobody capped RCCL."""
+    from ds2amd.optim import rccl_channel_cap
+    monkeypatch.delenv("NCCL_MAX_NCHANNELS", raising=False)
+    assert rccl_channel_cap() == 64
+    monkeypatch.setenv("NCCL_MAX_NCHANNELS", "32")
+    assert rccl_channel_cap() == 32
+    monkeypatch.setenv("NCCL_MAX_NCHANNELS", "junk")
+    assert rccl_channel_cap() == 64

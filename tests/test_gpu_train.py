@@ -82,6 +82,16 @@ def test_benchmark_train_step_two_batch_tiles(dev):
     _check_train_step(dev, t_list, lab, seed=12)
 
 
+@pytest.mark.timeout(900)
+def test_benchmark_batch_train_step_matches_oracle(dev):
+    """The bench's own batch (bench.py / BASELINE cfg2): bs 32, all 32 utterances 10 s
+    (T = 1001 -> T' = 501), 150-label targets -- the full Trainer.train_batch (both batch tiles
+    of the persistent recurrences full, the same-XCD hand-off groups, the stacked W_ih GEMMs,
+    clip, SGD-Nesterov) vs oracle.train_step with the same bounds.  One oracle step at this
+    shape is ~150 s on 16 host threads."""
+    _check_train_step(dev, [1001] * 32, [150] * 32, seed=13)
+
+
 def _check_train_step(dev, t_list, label_lens, seed):
     _threads()
     g = torch.Generator().manual_seed(seed)
