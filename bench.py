@@ -50,17 +50,11 @@ def gemm_peak():
 
 def gru_bwd_kernel(x6f: bool):
     """(peak, arithmetic, kernel name) of the GRU backward recurrence as configured: the
-    pre-split bf16x6 kernel by default (gru_split.hip), DS2_GRU_X6_BWD=1 its consumer-split
-    form, =0 (or DS2_GRU_X6=0, or a sentinel backward hand-off) the fp32-MFMA kernel, and
-    DS2_GRU_BWD=dh the dh-exchange kernel."""
-    if os.environ.get("DS2_GRU_BWD", "")[:2] == "dh":
-        return PEAK_F32_MFMA_TFLOPS, "W_hh^T contraction, fp32 MFMA (dh exchange)", "gru_bwd_dh_kernel"
-    mode = os.environ.get("DS2_GRU_X6_BWD", "2")[:1] or "2"
-    hand = (os.environ.get("DS2_RNN_HANDOFF_BWD") or os.environ.get("DS2_RNN_HANDOFF") or "f")[:1]
-    if x6f and mode in ("1", "2") and (mode == "1" or hand not in ("s", "h")):
-        form = "pre-split tiles" if mode == "2" else "consumer-side splits"
-        return (PEAK_X6_TFLOPS, "W_hh^T contraction, bf16x6 (fp32-accurate, " + form +
-                ") on v_mfma_f32_16x16x32_bf16", "gru_bwd_x6_kernel")
+    pre-split bf16x6 kernel by default (gru_split.hip), the fp32-MFMA kernel with
+    DS2_GRU_X6=0."""
+    if x6f:
+        return (PEAK_X6_TFLOPS, "W_hh^T contraction, bf16x6 (fp32-accurate, pre-split tiles) "
+                "on v_mfma_f32_16x16x32_bf16", "gru_bwd_x6_kernel")
     return PEAK_F32_MFMA_TFLOPS, "W_hh^T contraction, fp32 MFMA (v_mfma_f32_16x16x4_f32)", "gru_bwd_dop_kernel"
 
 
@@ -265,13 +259,6 @@ def main():
                          "pcm: raw 16 kHz PCM resident in HBM, the device STFT + max_frame "
                          "normalisation inside every timed step (SURVEY 8d secondary variant)")
     args = ap.parse_args()
-    maps_out = os.environ.get("DS2_DUMP_MAPS")
-    if maps_out:
-        # exit-time fault forensics: the loaded objects' address ranges, written from an
-        # atexit hook (Python's atexit runs before the C-level exit handlers)
-        import atexit
-        import shutil
-        atexit.register(lambda: shutil.copyfile("/proc/self/maps", maps_out))
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

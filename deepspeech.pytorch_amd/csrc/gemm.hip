@@ -101,12 +101,10 @@ __device__ __forceinline__ void store_tile(float* __restrict__ s, const float (&
 // by column (m fastest), so the ~32 tiles one XCD runs at once span 4 m-rows x 8 n-columns
 // (A: 4 panels, B: 8) instead of ~2 m-rows x every n-column (the input projection's 15 B
 // panels, 7.7 MB, overflow the XCD's 4-MB L2 and were fetched again for every m-row).
-// g_tile_group 1 is the plain n-fastest order (DS2_GEMM_GROUP, diagnostic).
 constexpr int kTileGroup = 4;
-static __constant__ int g_tile_group = kTileGroup;
 
 __device__ __forceinline__ void tile_coords(int tile, int tn, int tm, int& tile_m, int& tile_n) {
-  const int G = g_tile_group;
+  constexpr int G = kTileGroup;
   const int g = tile / (G * tn);
   const int rem = tile - g * G * tn;
   const int rows = min(G, tm - g * G);
@@ -648,22 +646,16 @@ __global__ __launch_bounds__(256, 2) void sbgemm_kernel(
 // fp32 GEMM on the bf16 matrix cores at fp32 accuracy (default for float4-staged operands;
 // DS2_GEMM_X6=0 selects sgemm64_kernel).  Every fp32 operand value x is split while it is
 // staged into three bf16 terms, hi = bf16(x), mid = bf16(x - hi), lo = bf16(x - hi - mid)
-// (round to nearest even; x = hi + mid + lo to 2^-26 |x|), and a product a.b is formed on
-// v_mfma_f32_16x16x32_bf16 from the six terms that carry fp32 weight,
+// (round to nearest even; x = hi + mid + lo to 2^-26 |x|), and a product a.b is formed from
+// the six terms that carry fp32 weight,
 //   mid.mid + lo.hi + hi.lo + mid.hi + hi.mid + hi.hi       (small terms first)
 // (dropped: mid.lo, lo.mid, lo.lo, each below 2^-25 |a b|).  Each bf16 product is exact
-// in the fp32 accumulator, so the result carries fp32 rounding only: six 16-cycle bf16
-// MFMAs per 32 k replace eight 32-cycle fp32 MFMAs (2.7x fewer matrix cycles; the fp32-
-// equivalent peak is the dense bf16 peak / 6 = 419 TF).  The same split and products
-// run the GRU recurrences (gru_split.hip).
-//   tile 128 x 128, stages of 32 k, 4 waves of 4 x 4 16x16 tiles, two workgroups per CU;
-//   LDS: per operand three bf16 planes [128 rows][32 k] (64-B rows, 16-B slot s of row r
-//   at s ^ xswz(r), below: conflict-free ds_read_b128 fragments and stores);
-//   k-contiguous source: a thread unit = (row, 8-k slot), two float4 loads;
-//   row-contiguous source: a thread = one row x 16 k, 16 dword loads (consecutive threads
-//   read consecutive rows), so the transposed stores need no register shuffles.
+// in the fp32 accumulator, so the result carries fp32 rounding only (the fp32-equivalent
+// peak is the dense bf16 peak / 6 = 419 TF).  The same split and products run the GRU
+// recurrences (gru_split.hip).  LDS: per operand three bf16 planes [rows][32 k] (64-B rows,
+// 16-B slot s of row r at s ^ xswz(r), below: conflict-free ds_read_b128 fragments and
+// stores).
 constexpr int XS = 32;                  // k per stage
-constexpr int XPLANE = BM * XS;         // bf16 per plane (BM = 128 rows)
 
 // 16-B slot s of a 64-B row, XOR-swizzled by q(row) = bit 2 | (bit 1 ^ bit 3) << 1: with it
 // the fragment reads (ds_read_b128 serves lanes in four 16-lane groups, rows {0-3, 12-15,
@@ -672,174 +664,6 @@ constexpr int XPLANE = BM * XS;         // bf16 per plane (BM = 128 rows)
 // (row >> 2) & 3 left the row-contiguous stores 4-way conflicted (12 % of LDS cycles).
 __device__ __forceinline__ int xswz(int row) { return ((row >> 2) & 1) | ((((row >> 1) ^ (row >> 3)) & 1) << 1); }
 __device__ __forceinline__ int xslot(int row, int s) { return row * XS + 8 * (s ^ xswz(row)); }
-
-template <bool KC>
-__device__ __forceinline__ void xload_stage(__amdgpu_buffer_rsrc_t rs, int ld, int rows, int kend,
-                                            int r0, int k0, float (&v)[16]) {
-  constexpr int kOob = 0x7ffffff0;
-  const int t = threadIdx.x;
-  if (KC) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int u = t + 256 * (q >> 1);
-      const int r = r0 + (u >> 2);
-      const int k = k0 + 8 * (u & 3) + 4 * (q & 1);
-      const int off = (r < rows && k < kend) ? (r * ld + k) * 4 : kOob;
-      const f32x4 x = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
-#pragma unroll
-      for (int c = 0; c < 4; ++c) v[4 * q + c] = x[c];
-    }
-  } else {
-    const int r = r0 + (t & (BM - 1));
-    const int kb = k0 + 16 * (t >> 7);
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const int k = kb + j;
-      const int off = (r < rows && k < kend) ? (k * ld + r) * 4 : kOob;
-      v[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0));
-    }
-  }
-}
-
-// 8 fp32 -> hi / mid / lo bf16x8, stored into the three planes at one slot
-__device__ __forceinline__ void xsplit_store(unsigned short* __restrict__ s, int at, const float* v) {
-  bf16x8 h, m, l;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const __bf16 a = (__bf16)v[j];
-    const float r1 = v[j] - (float)a;
-    const __bf16 b = (__bf16)r1;
-    h[j] = a;
-    m[j] = b;
-    l[j] = (__bf16)(r1 - (float)b);
-  }
-  *reinterpret_cast<bf16x8*>(s + at) = h;
-  *reinterpret_cast<bf16x8*>(s + XPLANE + at) = m;
-  *reinterpret_cast<bf16x8*>(s + 2 * XPLANE + at) = l;
-}
-
-template <bool KC>
-__device__ __forceinline__ void xstore_stage(unsigned short* __restrict__ s, const float (&v)[16]) {
-  const int t = threadIdx.x;
-  if (KC) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int u = t + 256 * i;
-      xsplit_store(s, xslot(u >> 2, u & 3), v + 8 * i);
-    }
-  } else {
-    const int r = t & (BM - 1);
-#pragma unroll
-    for (int i = 0; i < 2; ++i) xsplit_store(s, xslot(r, 2 * (t >> 7) + i), v + 8 * i);
-  }
-}
-
-template <int TA, int TB>
-__global__ __launch_bounds__(256, 2) void sxgemm_kernel(
-    int M, int N, int K, float alpha, const float* __restrict__ A, int64_t lda, int64_t sA,
-    const float* __restrict__ B, int64_t ldb, int64_t sB, float beta, float* __restrict__ C,
-    int64_t ldc, int64_t sC, const float* __restrict__ bias, int main_wgs, int tail_tile0,
-    int tail_tiles, int nsplit, int kchunk, float* __restrict__ partial) {
-  constexpr bool AK = (TA == 0);
-  constexpr bool BKc = (TB == 1);
-  constexpr int TBN = 128;
-  __shared__ __attribute__((aligned(16))) unsigned short As[3 * XPLANE];
-  __shared__ __attribute__((aligned(16))) unsigned short Bs[3 * XPLANE];
-
-  int m0, n0, kbeg, kend, bz;
-  float* part;
-  decode_work(M, N, K, main_wgs, tail_tile0, tail_tiles, nsplit, kchunk, partial, m0, n0, kbeg,
-              kend, bz, part, TBN);
-  A += bz * sA;
-  B += bz * sB;
-  C += bz * sC;
-  const int a_rows = AK ? M : K, b_rows = BKc ? N : K;
-  const __amdgpu_buffer_rsrc_t a_rs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float*>(A), (short)0, static_cast<int>(a_rows * lda * 4), 0x00020000);
-  const __amdgpu_buffer_rsrc_t b_rs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float*>(B), (short)0, static_cast<int>(b_rows * ldb * 4), 0x00020000);
-  const int ilda = static_cast<int>(lda), ildb = static_cast<int>(ldb);
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int wm = (wave >> 1) * 64;
-  const int wn = (wave & 1) * 64;
-  const int fr = lane & 15, fq = lane >> 4;
-
-  f32x4 acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  float ra[16], rb[16];
-  const int ktiles = (kend - kbeg + XS - 1) / XS;
-  xload_stage<AK>(a_rs, ilda, M, kend, m0, kbeg, ra);
-  xload_stage<BKc>(b_rs, ildb, N, kend, n0, kbeg, rb);
-  for (int kt = 0; kt < ktiles; ++kt) {
-    xstore_stage<AK>(As, ra);
-    xstore_stage<BKc>(Bs, rb);
-    __syncthreads();
-    if (kt + 1 < ktiles) {   // next stage's global loads fly during this stage's MFMAs
-      xload_stage<AK>(a_rs, ilda, M, kend, m0, kbeg + (kt + 1) * XS, ra);
-      xload_stage<BKc>(b_rs, ildb, N, kend, n0, kbeg + (kt + 1) * XS, rb);
-    }
-    bf16x8 ah[4], am[4], al[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int at = xslot(wm + 16 * i + fr, fq);
-      ah[i] = *reinterpret_cast<const bf16x8*>(As + at);
-      am[i] = *reinterpret_cast<const bf16x8*>(As + XPLANE + at);
-      al[i] = *reinterpret_cast<const bf16x8*>(As + 2 * XPLANE + at);
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int bt = xslot(wn + 16 * j + fr, fq);
-      const bf16x8 bh = *reinterpret_cast<const bf16x8*>(Bs + bt);
-      const bf16x8 bm = *reinterpret_cast<const bf16x8*>(Bs + XPLANE + bt);
-      const bf16x8 bl = *reinterpret_cast<const bf16x8*>(Bs + 2 * XPLANE + bt);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        f32x4 c = acc[i][j];
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am[i], bm, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], bh, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bl, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am[i], bh, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bm, c, 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bh, c, 0, 0, 0);
-      }
-    }
-    __syncthreads();
-  }
-
-  // epilogue (16x16 C/D map: col = lane & 15, row = 4 * (lane >> 4) + r), as sgemm64_kernel
-  const int lc = lane & 15;
-  const int lr = 4 * (lane >> 4);
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int cl = wn + 16 * j + lc;
-      if (part != nullptr) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) part[(wm + 16 * i + lr + r) * TBN + cl] = acc[i][j][r];
-        continue;
-      }
-      const int col = n0 + cl;
-      if (col >= N) continue;
-      const float bv = bias != nullptr ? bias[col] : 0.f;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = m0 + wm + 16 * i + lr + r;
-        if (row < M) {
-          float* cp = C + (int64_t)row * ldc + col;
-          float v = alpha * acc[i][j][r] + bv;
-          if (beta != 0.f) v += beta * *cp;
-          *cp = v;
-        }
-      }
-    }
-  }
-}
 
 // The default bf16x6 kernel: tile 256 x 128, eight waves (two per SIMD) of 2 x 2 32x32
 // tiles on v_mfma_f32_32x32x16_bf16 (which holds the SIMD's vector issue for 8 of its 32
@@ -1280,20 +1104,17 @@ static void launch_sgemm_t(bool va, bool vb, dim3 grid, hipStream_t st, int M, i
 }
 
 template <int TA, int TB>
-static void launch_k64(int bn, bool db, dim3 grid, hipStream_t st, int M, int N, int K,
+static void launch_k64(int bn, dim3 grid, hipStream_t st, int M, int N, int K,
                        float alpha, const float* A, int64_t lda, int64_t sA, const float* B,
                        int64_t ldb, int64_t sB, float beta, float* C, int64_t ldc, int64_t sC,
                        const float* bias, int main_wgs, int tail_tile0, int tail_tiles,
                        int nsplit, int kchunk, float* partial) {
-#define DS2_K(WN, KS, NB)                                                                   \
-  hipLaunchKernelGGL((sgemm64_kernel<TA, TB, WN, KS, NB>), grid, dim3(256), 0, st, M, N, K,    \
+#define DS2_K(WN)                                                                           \
+  hipLaunchKernelGGL((sgemm64_kernel<TA, TB, WN, 64, 1>), grid, dim3(256), 0, st, M, N, K,     \
                      alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC, bias, main_wgs,          \
                      tail_tile0, tail_tiles, nsplit, kchunk, partial)
-  if (bn == 160) {
-    if (db) DS2_K(5, 32, 2); else DS2_K(5, 64, 1);
-  } else {
-    if (db) DS2_K(4, 32, 2); else DS2_K(4, 64, 1);
-  }
+  if (bn == 160) DS2_K(5);
+  else DS2_K(4);
 #undef DS2_K
 }
 
@@ -1302,17 +1123,6 @@ static inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t
 }  // namespace ds2
 
 using namespace ds2;
-
-// DS2_GEMM_GROUP overrides the grouped tile order's group height (1: n-fastest order);
-// checked at every GEMM entry point, the symbol written only when the value changes
-static void apply_tile_group_env() {
-  static int applied = kTileGroup;
-  const char* e = getenv("DS2_GEMM_GROUP");
-  int v = (e == nullptr || e[0] == 0) ? kTileGroup : atoi(e);
-  if (v < 1) v = 1;
-  if (v == applied) return;
-  if (hipMemcpyToSymbol(HIP_SYMBOL(g_tile_group), &v, sizeof(v)) == hipSuccess) applied = v;
-}
 
 static int g_cus = -1;
 static int device_cus() {
@@ -1336,19 +1146,14 @@ struct GemmPlan {
   int main_wgs, tail_tile0, tail_tiles, nsplit, kchunk, bn, bm;
 };
 
-// the deep-K kernel (sgemm64_kernel) runs 2 workgroups per CU and BK = 64, the
-// original one 3 per CU and BK = 16
-// 0: fp32-MFMA kernels; 1 (default): bf16x6 256 x 128 kernel; 2: bf16x6 128 x 128 kernel
-static int x6_mode(bool va, bool vb) {
-  if (!va || !vb) return 0;
+// DS2_GEMM_X6=0 selects the fp32-MFMA kernels (the accuracy cross-check of the tests); the
+// bf16x6 kernel needs float4-staged operands (the fp32 kernels take any alignment; the
+// deep-K sgemm64_kernel runs 2 workgroups per CU and BK = 64, the original one 3 per CU and
+// BK = 16, for operands that are not float4-aligned)
+static bool x6_enabled(bool va, bool vb) {
+  if (!va || !vb) return false;
   const char* e = getenv("DS2_GEMM_X6");
-  if (e == nullptr || e[0] == 0) return 1;
-  return e[0] == '0' ? 0 : (e[0] == '2' ? 2 : 1);
-}
-
-static bool use_k64(bool va, bool vb) {
-  const char* e = getenv("DS2_GEMM64");
-  return va && vb && !(e != nullptr && e[0] == '0');
+  return !(e != nullptr && e[0] == '0');
 }
 
 // 32-bit buffer offsets: each operand (one batch entry) must span < 2^31 bytes
@@ -1407,18 +1212,17 @@ static PlanChoice plan_bn(int m, int n, int k, int batch, int bn, int slots, int
   return {p, main_t + best};
 }
 
+// 160-wide tiles are ~7 % faster per unit of work than 128-wide in isolation (5 B fragments
+// per 4 A); 1.15 in the time model, where it also stands in for the 160-wide tile's smaller
+// tail (a whole training step measured 1.0 < 1.07 < 1.15 ~ 1.25 ~ 1.4, the last three
+// within noise)
+constexpr double kEff160 = 1.15;
+
 static GemmPlan gemm_plan(int m, int n, int k, int batch, bool k64) {
   const int cus = device_cus();
   if (!k64) return plan_bn(m, n, k, batch, BN, 3 * cus, BK, 1.0).p;
-  const char* e = getenv("DS2_GEMM_BN");
-  if (e != nullptr) return plan_bn(m, n, k, batch, e[1] == '6' ? 160 : 128, 2 * cus, K64, 1.0).p;
-  // DS2_GEMM_EFF160: the 160-wide tile's relative efficiency in the time model (tuning)
-  static const double eff160 = [] {
-    const char* v = getenv("DS2_GEMM_EFF160");
-    return v != nullptr ? atof(v) : 1.15;
-  }();
   const PlanChoice a = plan_bn(m, n, k, batch, 128, 2 * cus, K64, 1.0);
-  const PlanChoice b = plan_bn(m, n, k, batch, 160, 2 * cus, K64, eff160);
+  const PlanChoice b = plan_bn(m, n, k, batch, 160, 2 * cus, K64, kEff160);
   return b.t < a.t ? b.p : a.p;
 }
 
@@ -1427,15 +1231,10 @@ static size_t plan_ws(const GemmPlan& p, int batch) {
                       : 0;
 }
 
-// the bf16x6 kernels: 128-wide tiles, split-K in 32-k chunks; 256-row tiles one workgroup
-// per CU (mode 1) or 128-row tiles two per CU (mode 2)
-static GemmPlan x6_plan(int m, int n, int k, int batch, int mode) {
-  if (mode == 2) return plan_bn(m, n, k, batch, 128, 2 * device_cus(), XS, 1.0).p;
-  const char* e = getenv("DS2_GEMM_X6_BN");
-  if (e != nullptr && e[0] != 0)
-    return plan_bn(m, n, k, batch, e[1] == '6' ? 160 : 128, device_cus(), XS, 1.0, X2M).p;
-  // 160-wide tiles measured faster on every step shape with N >= 800 (scripts/bench_gemm_x6.py:
-  // 180-201 vs 159-194 TF), 128-wide on narrow N (the FC's 32 columns)
+// the bf16x6 kernel: 256-row tiles, one workgroup per CU, split-K in 32-k chunks; 160-wide
+// tiles measured faster on every step shape with N >= 800 (scripts/bench_gemm_x6.py: 180-201
+// vs 159-194 TF), 128-wide on narrow N (the FC's 29 columns)
+static GemmPlan x6_plan(int m, int n, int k, int batch) {
   return plan_bn(m, n, k, batch, n >= 256 ? 160 : 128, device_cus(), XS, 1.0, X2M).p;
 }
 
@@ -1444,9 +1243,7 @@ extern "C" size_t ds2_sgemm_workspace_size(int m, int n, int k, int batch) {
   if (m <= 0 || n <= 0 || k <= 0 || batch <= 0) return 0;
   return std::max(std::max(plan_ws(gemm_plan(m, n, k, batch, false), batch),
                            plan_ws(gemm_plan(m, n, k, batch, true), batch)),
-                  std::max(std::max(plan_ws(plan_bn(m, n, k, batch, 128, device_cus(), XS, 1.0, X2M).p, batch),
-                                    plan_ws(plan_bn(m, n, k, batch, 160, device_cus(), XS, 1.0, X2M).p, batch)),
-                           plan_ws(x6_plan(m, n, k, batch, 2), batch)));
+                  plan_ws(x6_plan(m, n, k, batch), batch));
 }
 
 extern "C" ds2_status_t ds2_sgemm_ws(int trans_a, int trans_b, int m, int n, int k, float alpha,
@@ -1455,7 +1252,6 @@ extern "C" ds2_status_t ds2_sgemm_ws(int trans_a, int trans_b, int m, int n, int
                                      float* c, int64_t ldc, int64_t stride_c, int batch,
                                      const float* bias, void* ws, size_t ws_bytes,
                                      ds2_stream_t stream) {
-  apply_tile_group_env();
   if (m < 0 || n < 0 || k < 0 || batch < 0) return DS2_INVALID_VALUE;
   if (m == 0 || n == 0 || batch == 0) return DS2_OK;
   if (ldc < n) return DS2_INVALID_VALUE;
@@ -1467,11 +1263,9 @@ extern "C" ds2_status_t ds2_sgemm_ws(int trans_a, int trans_b, int m, int n, int
   const bool vb = aligned16(b) && (ldb % 4 == 0) && (stride_b % 4 == 0) &&
                   (trans_b ? (k % 4 == 0) : (n % 4 == 0));
   const bool fits = fits_rsrc(trans_a ? k : m, lda) && fits_rsrc(trans_b ? n : k, ldb);
-  const int x6 = fits ? x6_mode(va, vb) : 0;
-  const bool k64 = x6 == 0 && use_k64(va, vb) && fits;
-  const char* dbe = getenv("DS2_GEMM_DB");
-  const bool db = dbe != nullptr && dbe[0] == '1';
-  GemmPlan p = x6 ? x6_plan(m, n, k, batch, x6) : gemm_plan(m, n, k, batch, k64);
+  const bool x6 = fits && x6_enabled(va, vb);
+  const bool k64 = !x6 && va && vb && fits;
+  GemmPlan p = x6 ? x6_plan(m, n, k, batch) : gemm_plan(m, n, k, batch, k64);
   if (p.nsplit > 1 && (ws == nullptr || ws_bytes < plan_ws(p, batch))) {
     p.nsplit = 1;                       // no workspace: whole-K pieces
     p.kchunk = std::max(k, 1);
@@ -1483,29 +1277,17 @@ extern "C" ds2_status_t ds2_sgemm_ws(int trans_a, int trans_b, int m, int n, int
   hipStream_t st = as_stream(stream);
   // every stage of every piece lies wholly inside [0, K): no per-element k check
   const bool kalign = k % XS == 0 && (p.nsplit == 1 || p.kchunk % XS == 0);
+#define DS2_X6(TA_, TB_, KCHK_, BN_)                                                          \
+  hipLaunchKernelGGL((sxgemm2_kernel<TA_, TB_, KCHK_, BN_>), grid, dim3(X2T), 0, st, m, n, k,   \
+                     alpha, a, lda, stride_a, b, ldb, stride_b, beta, c, ldc, stride_c, bias,   \
+                     p.main_wgs, p.tail_tile0, p.tail_tiles, p.nsplit, p.kchunk, partial)
 #define DS2_G(TA_, TB_)                                                                       \
-  if (x6 == 1 && kalign && p.bn == 160)                                                       \
-    hipLaunchKernelGGL((sxgemm2_kernel<TA_, TB_, false, 160>), grid, dim3(X2T), 0, st, m, n, k,   \
-                       alpha, a, lda, stride_a, b, ldb, stride_b, beta, c, ldc, stride_c, bias, \
-                       p.main_wgs, p.tail_tile0, p.tail_tiles, p.nsplit, p.kchunk, partial);   \
-  else if (x6 == 1 && p.bn == 160)                                                            \
-    hipLaunchKernelGGL((sxgemm2_kernel<TA_, TB_, true, 160>), grid, dim3(X2T), 0, st, m, n, k,    \
-                       alpha, a, lda, stride_a, b, ldb, stride_b, beta, c, ldc, stride_c, bias, \
-                       p.main_wgs, p.tail_tile0, p.tail_tiles, p.nsplit, p.kchunk, partial);   \
-  else if (x6 == 1 && kalign)                                                                 \
-    hipLaunchKernelGGL((sxgemm2_kernel<TA_, TB_, false, 128>), grid, dim3(X2T), 0, st, m, n, k,   \
-                       alpha, a, lda, stride_a, b, ldb, stride_b, beta, c, ldc, stride_c, bias, \
-                       p.main_wgs, p.tail_tile0, p.tail_tiles, p.nsplit, p.kchunk, partial);   \
-  else if (x6 == 1)                                                                           \
-    hipLaunchKernelGGL((sxgemm2_kernel<TA_, TB_, true, 128>), grid, dim3(X2T), 0, st, m, n, k,    \
-                       alpha, a, lda, stride_a, b, ldb, stride_b, beta, c, ldc, stride_c, bias, \
-                       p.main_wgs, p.tail_tile0, p.tail_tiles, p.nsplit, p.kchunk, partial);   \
-  else if (x6 == 2)                                                                           \
-    hipLaunchKernelGGL((sxgemm_kernel<TA_, TB_>), grid, dim3(256), 0, st, m, n, k, alpha, a, lda, \
-                       stride_a, b, ldb, stride_b, beta, c, ldc, stride_c, bias, p.main_wgs,    \
-                       p.tail_tile0, p.tail_tiles, p.nsplit, p.kchunk, partial);               \
+  if (x6 && kalign && p.bn == 160) DS2_X6(TA_, TB_, false, 160);                             \
+  else if (x6 && p.bn == 160) DS2_X6(TA_, TB_, true, 160);                                   \
+  else if (x6 && kalign) DS2_X6(TA_, TB_, false, 128);                                       \
+  else if (x6) DS2_X6(TA_, TB_, true, 128);                                                  \
   else if (k64)                                                                               \
-    launch_k64<TA_, TB_>(p.bn, db, grid, st, m, n, k, alpha, a, lda, stride_a, b, ldb, stride_b, \
+    launch_k64<TA_, TB_>(p.bn, grid, st, m, n, k, alpha, a, lda, stride_a, b, ldb, stride_b,   \
                          beta, c, ldc, stride_c, bias, p.main_wgs, p.tail_tile0, p.tail_tiles,  \
                          p.nsplit, p.kchunk, partial);                                         \
   else                                                                                        \
@@ -1522,6 +1304,7 @@ extern "C" ds2_status_t ds2_sgemm_ws(int trans_a, int trans_b, int m, int n, int
     DS2_G(1, 1);
   }
 #undef DS2_G
+#undef DS2_X6
   if (p.nsplit > 1) {
     const int64_t total = (int64_t)batch * p.tail_tiles * p.bm * p.bn;
     int g = cdiv(total, 256);
@@ -1536,20 +1319,9 @@ extern "C" ds2_status_t ds2_sgemm_ws(int trans_a, int trans_b, int m, int n, int
 // bf16-operand GEMM (sbgemm_kernel): same contract as ds2_sgemm_ws; every operand must be
 // float4-staged (16-B aligned, ld and the contiguous extent multiples of 4) and span
 // < 2^31 bytes, else DS2_UNSUPPORTED_SHAPE (no silent fp32 fallback).
-// DS2_GEMM_BF16_X2=1: the bf16-operand GEMM on sxgemm2_kernel with one plane (NPL 1: 256-row
-// tiles, one workgroup per CU, 32x32x16 MFMAs from one LDS image per operand) instead of
-// sbgemm_kernel (128 x 128, two workgroups per CU).  Opt-in: cfg4 7xBiLSTM-1024 bf16 3998 vs
-// 4063 audio-s/s on one box -- with one product per fragment pair the fp32 operand staging,
-// not the MFMAs, bounds both, and the two-workgroup kernel hides it better.
-static bool bf16_x2_enabled() {
-  const char* e = getenv("DS2_GEMM_BF16_X2");
-  return e != nullptr && e[0] == '1';
-}
-
 extern "C" size_t ds2_sgemm_bf16_workspace_size(int m, int n, int k, int batch) {
   if (m <= 0 || n <= 0 || k <= 0 || batch <= 0) return 0;
-  return std::max(plan_ws(plan_bn(m, n, k, batch, 128, 2 * device_cus(), KB16, 1.0).p, batch),
-                  plan_ws(x6_plan(m, n, k, batch, 1), batch));
+  return plan_ws(plan_bn(m, n, k, batch, 128, 2 * device_cus(), KB16, 1.0).p, batch);
 }
 
 extern "C" ds2_status_t ds2_sgemm_bf16_ws(int trans_a, int trans_b, int m, int n, int k,
@@ -1558,7 +1330,6 @@ extern "C" ds2_status_t ds2_sgemm_bf16_ws(int trans_a, int trans_b, int m, int n
                                           int64_t stride_b, float beta, float* c, int64_t ldc,
                                           int64_t stride_c, int batch, const float* bias,
                                           void* ws, size_t ws_bytes, ds2_stream_t stream) {
-  apply_tile_group_env();
   if (m < 0 || n < 0 || k < 0 || batch < 0) return DS2_INVALID_VALUE;
   if (m == 0 || n == 0 || batch == 0) return DS2_OK;
   if (ldc < n) return DS2_INVALID_VALUE;
@@ -1570,9 +1341,7 @@ extern "C" ds2_status_t ds2_sgemm_bf16_ws(int trans_a, int trans_b, int m, int n
                   (trans_b ? (k % 4 == 0) : (n % 4 == 0));
   if (!va || !vb || !fits_rsrc(trans_a ? k : m, lda) || !fits_rsrc(trans_b ? n : k, ldb))
     return DS2_UNSUPPORTED_SHAPE;
-  const bool x2 = bf16_x2_enabled();
-  GemmPlan p = x2 ? x6_plan(m, n, k, batch, 1)
-                  : plan_bn(m, n, k, batch, 128, 2 * device_cus(), KB16, 1.0).p;
+  GemmPlan p = plan_bn(m, n, k, batch, 128, 2 * device_cus(), KB16, 1.0).p;
   if (p.nsplit > 1 && (ws == nullptr || ws_bytes < plan_ws(p, batch))) {
     p.nsplit = 1;
     p.kchunk = std::max(k, 1);
@@ -1582,28 +1351,10 @@ extern "C" ds2_status_t ds2_sgemm_bf16_ws(int trans_a, int trans_b, int m, int n
   if (nwg > 0x7fffffff) return DS2_UNSUPPORTED_SHAPE;
   dim3 grid(static_cast<unsigned>(nwg));
   hipStream_t st = as_stream(stream);
-  const bool kalign = k % XS == 0 && (p.nsplit == 1 || p.kchunk % XS == 0);
 #define DS2_B(TA_, TB_)                                                                        \
-  if (x2 && kalign && p.bn == 160)                                                             \
-    hipLaunchKernelGGL((sxgemm2_kernel<TA_, TB_, false, 160, 1>), grid, dim3(X2T), 0, st, m, n, \
-                       k, alpha, a, lda, stride_a, b, ldb, stride_b, beta, c, ldc, stride_c, bias, \
-                       p.main_wgs, p.tail_tile0, p.tail_tiles, p.nsplit, p.kchunk, partial);    \
-  else if (x2 && p.bn == 160)                                                                  \
-    hipLaunchKernelGGL((sxgemm2_kernel<TA_, TB_, true, 160, 1>), grid, dim3(X2T), 0, st, m, n,  \
-                       k, alpha, a, lda, stride_a, b, ldb, stride_b, beta, c, ldc, stride_c, bias, \
-                       p.main_wgs, p.tail_tile0, p.tail_tiles, p.nsplit, p.kchunk, partial);    \
-  else if (x2 && kalign)                                                                       \
-    hipLaunchKernelGGL((sxgemm2_kernel<TA_, TB_, false, 128, 1>), grid, dim3(X2T), 0, st, m, n, \
-                       k, alpha, a, lda, stride_a, b, ldb, stride_b, beta, c, ldc, stride_c, bias, \
-                       p.main_wgs, p.tail_tile0, p.tail_tiles, p.nsplit, p.kchunk, partial);    \
-  else if (x2)                                                                                 \
-    hipLaunchKernelGGL((sxgemm2_kernel<TA_, TB_, true, 128, 1>), grid, dim3(X2T), 0, st, m, n,  \
-                       k, alpha, a, lda, stride_a, b, ldb, stride_b, beta, c, ldc, stride_c, bias, \
-                       p.main_wgs, p.tail_tile0, p.tail_tiles, p.nsplit, p.kchunk, partial);    \
-  else                                                                                         \
-    hipLaunchKernelGGL((sbgemm_kernel<TA_, TB_>), grid, dim3(256), 0, st, m, n, k, alpha, a, lda, \
-                       stride_a, b, ldb, stride_b, beta, c, ldc, stride_c, bias, p.main_wgs,    \
-                       p.tail_tile0, p.tail_tiles, p.nsplit, p.kchunk, partial)
+  hipLaunchKernelGGL((sbgemm_kernel<TA_, TB_>), grid, dim3(256), 0, st, m, n, k, alpha, a, lda, \
+                     stride_a, b, ldb, stride_b, beta, c, ldc, stride_c, bias, p.main_wgs,      \
+                     p.tail_tile0, p.tail_tiles, p.nsplit, p.kchunk, partial)
   if (!trans_a && !trans_b) DS2_B(0, 0);
   else if (!trans_a && trans_b) DS2_B(0, 1);
   else if (trans_a && !trans_b) DS2_B(1, 0);

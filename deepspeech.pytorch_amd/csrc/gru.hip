@@ -248,7 +248,7 @@ __global__ __launch_bounds__(GT) void gru_fwd_persist_kernel(
     const float* __restrict__ wp, const float* __restrict__ b_f, const float* __restrict__ b_r,
     const int* __restrict__ lens, float* __restrict__ h_all, float* __restrict__ gates,
     unsigned* __restrict__ counters, unsigned* __restrict__ err,
-    unsigned long long* __restrict__ stamps, int trace, int use_flags) {
+    unsigned long long* __restrict__ stamps, int trace) {
   constexpr int PITCH = KC_FWD + 4;
   __shared__ __attribute__((aligned(16))) float hs[GB * PITCH];
   __shared__ int flag;
@@ -260,8 +260,7 @@ __global__ __launch_bounds__(GT) void gru_fwd_persist_kernel(
   const int KS = (H + 3) / 4;
   const int a_ks = wave * KSW;           // host guarantees GW * KSW >= KS
   const int b_ks = min(KS, a_ks + KSW);
-  unsigned* ctr = counters + d * BT + bt;
-  unsigned* gflags = counters + (D * BT + 1) + (d * BT + bt) * UB;   // flag variant
+  unsigned* gflags = counters + (D * BT + 1) + (d * BT + bt) * UB;
   const __amdgpu_buffer_rsrc_t h_rs = __builtin_amdgcn_make_buffer_rsrc(
       h_all, (short)0, T * N * D * H * 4, 0x00020000);
   const bool stamping = stamps != nullptr && !trace && blockIdx.x == 0 && threadIdx.x == 0;
@@ -329,8 +328,7 @@ __global__ __launch_bounds__(GT) void gru_fwd_persist_kernel(
     if (stamping) t0 = stamp_now();
     trace_at(s, 0);
     if (s > 0) {
-      if (!(use_flags ? flags_wait(gflags, UB, (unsigned)s, err, &flag)
-                      : group_wait(ctr, (unsigned)s * UB, err, &flag))) {
+      if (!flags_wait(gflags, UB, (unsigned)s, err, &flag)) {
         poison_rest(h_all, s, T, d != 0, N, D, n, d, H, j, H, 1, owner);
         return;
       }
@@ -388,8 +386,7 @@ __global__ __launch_bounds__(GT) void gru_fwd_persist_kernel(
       g_r = r; g_z = z; g_n = nn; g_hn = ghn; g_row = row;
     }
     if (stamping) { t1 = stamp_now(); acc_t[3] += t1 - t0; t0 = t1; }
-    if (use_flags) flags_arrive(gflags + ub, (unsigned)s + 1);
-    else group_arrive(ctr);
+    flags_arrive(gflags + ub, (unsigned)s + 1);
     trace_at(s, 4);
     if (stamping) { t1 = stamp_now(); acc_t[4] += t1 - t0; t0 = t1; }
     // the gate cache is consumed only by the backward kernel: store it off the
@@ -422,12 +419,12 @@ __global__ __launch_bounds__(GT) void gru_fwd_persist_kernel(
 // rewritten two steps later, after every consumer of the group has published the step
 // in between, i.e. after all its loads of the slot have returned.
 //
-// HM (hand-off mode): 0 = per-producer flags (above); 1 = sentinel ring (rnn_common.h,
-// kRingSlots slots, no flags): every wave spins on its own producers' tiles, so the wait,
-// the poll round trip and the producer's drain-before-flag all leave the critical path;
-// 2 = hybrid: the flag poll of mode 0 tells a consumer when to load, the sentinel ring of
-// mode 1 validates what it loads, so the producer stores its flag without draining first.
-template <int NBW, int HM>
+// Hand-off: the sentinel ring (rnn_common.h, kRingSlots slots, no flags; the form above with
+// the data as the flag): every wave spins on its own producers' tiles, so the wait, the poll
+// round trip and the producer's drain-before-flag all leave the critical path (5.93 -> 5.51
+// us per step).  The per-producer flag form and a hybrid (flag-polled, sentinel-validated)
+// were measured slower and removed in round 4's pruning; the backward keeps the flags.
+template <int NBW>
 __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void gru_fwd_dop_kernel(
     int T, int N, int H, int D, int UB, int BT, const float* __restrict__ xproj,
     const float* __restrict__ w_f, const float* __restrict__ w_r, const float* __restrict__ b_f,
@@ -437,7 +434,6 @@ __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   constexpr int RP = 3 * GU + 1;
   __shared__ float red[GW * GB * RP];
   __shared__ __attribute__((aligned(16))) float tile[GB * GU];
-  __shared__ int flag;
   int ub, d, bt;
   if (!map_work(UB * D, BT, UB, ub, d, bt)) return;
   const int n0 = bt * GB;
@@ -445,20 +441,15 @@ __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   int b0, nb;
   simd_split(UB, wave, b0, nb);                 // host guarantees nb <= NBW
-  const unsigned* gflags = counters + (D * BT + 1) + (d * BT + bt) * UB;
-  unsigned* myflag = counters + (D * BT + 1) + (d * BT + bt) * UB + ub;
   const int slot_floats = D * BT * UB * 256;
-  constexpr bool SENT = HM != 0;     // sentinel ring: tiles validate themselves
-  constexpr bool FLAG = HM != 1;     // per-producer flags polled before loading
-  constexpr int NSLOT = SENT ? kRingSlots : 2;
+  constexpr bool SENT = true;        // sentinel ring: tiles validate themselves
+  constexpr int NSLOT = kRingSlots;
   const __amdgpu_buffer_rsrc_t x_rs =
       __builtin_amdgcn_make_buffer_rsrc(hx, (short)0, NSLOT * slot_floats * 4, 0x00020000);
   const int grp_off = (d * BT + bt) * UB * 256;            // this group's tiles in a slot
   __shared__ int failed;
-  if (SENT) {
-    if (threadIdx.x == 0) failed = 0;
-    __syncthreads();
-  }
+  if (threadIdx.x == 0) failed = 0;
+  __syncthreads();
   const bool tracing = stamps != nullptr && threadIdx.x == 0;
   auto trace_at = [&](int s, int p) {
     if (tracing && s >= kTraceS0 && s < kTraceS0 + kTraceSteps)
@@ -515,13 +506,9 @@ __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     for (int g = 0; g < 3; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
     trace_at(s, 0);
     if (s > 0) {
-      if (FLAG && !flags_wait(gflags, UB, (unsigned)s, err, &flag)) {
-        poison_rest(h_all, s, T, d != 0, N, D, n, d, H, j, H, 1, owner);
-        return;
-      }
       trace_at(s, 1);
       const int base = (((s - 1) % NSLOT) * slot_floats + grp_off + b0 * 256 + lane * 4) * 4;
-      if (HM == 1) sleep_units(g_rnn_tune[1]);
+      sleep_units(g_rnn_tune[1]);
       f32x4 hv[NBW];
 #pragma unroll
       for (int i = 0; i < NBW; ++i) {
@@ -625,7 +612,7 @@ __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     settle(xz);
     settle(xn);
     __syncthreads();
-    if (SENT && failed) {
+    if (failed) {
       poison_rest(h_all, s, T, d != 0, N, D, n, d, H, j, H, 1, owner);
       return;
     }
@@ -662,22 +649,12 @@ __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     // publish: wave 0 stores the tile (one 16-B sc1 store per lane), drains, flags
     if (wave == 0) {
       const int toff = (grp_off + ub * 256 + lane * 4) * 4;
-      if (SENT) {
-        const u32x4 v = desentinel(*reinterpret_cast<const u32x4*>(tile + lane * 4));
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // last step's sentinel store first
-        __builtin_amdgcn_raw_buffer_store_b128(v, x_rs, (s % NSLOT) * slot_floats * 4 + toff, 0, kSc1);
-        const u32x4 sv = u32x4{kSentinel, kSentinel, kSentinel, kSentinel};
-        __builtin_amdgcn_raw_buffer_store_b128(sv, x_rs, ((s + 2) % NSLOT) * slot_floats * 4 + toff,
-                                               0, kSc1);
-        if (FLAG && lane == 0)      // hybrid: no drain, the consumer validates the tile
-          __hip_atomic_store(myflag, (unsigned)s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      } else {
-        const u32x4 v = *reinterpret_cast<const u32x4*>(tile + lane * 4);
-        __builtin_amdgcn_raw_buffer_store_b128(v, x_rs, (s & 1) * slot_floats * 4 + toff, 0, kSc1);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (lane == 0)
-          __hip_atomic_store(myflag, (unsigned)s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
+      const u32x4 v = desentinel(*reinterpret_cast<const u32x4*>(tile + lane * 4));
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // last step's sentinel store first
+      __builtin_amdgcn_raw_buffer_store_b128(v, x_rs, (s % NSLOT) * slot_floats * 4 + toff, 0, kSc1);
+      const u32x4 sv = u32x4{kSentinel, kSentinel, kSentinel, kSentinel};
+      __builtin_amdgcn_raw_buffer_store_b128(sv, x_rs, ((s + 2) % NSLOT) * slot_floats * 4 + toff,
+                                             0, kSc1);
     }
     trace_at(s, 4);
     // outputs consumed only by later kernels, off the critical path
@@ -700,7 +677,7 @@ __global__ __launch_bounds__(GT) void gru_bwd_persist_kernel(
     const float* __restrict__ wpt, const float* __restrict__ h_all,
     const float* __restrict__ gates, const int* __restrict__ lens, float* __restrict__ dgx,
     float* __restrict__ dgh, unsigned* __restrict__ counters, unsigned* __restrict__ err,
-    int use_flags, unsigned long long* __restrict__ stamps) {
+    unsigned long long* __restrict__ stamps) {
   constexpr int PITCH = KC_BWD + 4;
   __shared__ __attribute__((aligned(16))) float hs[GB * PITCH];
   float* red = hs;                          // reduction buffer aliases the staged rows
@@ -714,8 +691,7 @@ __global__ __launch_bounds__(GT) void gru_bwd_persist_kernel(
   const int KS = (H3 + 3) / 4;             // single chunk: 32 * KSW <= KC_BWD (host-checked)
   const int a_ks = wave * KSW;
   const int b_ks = min(KS, a_ks + KSW);
-  unsigned* ctr = counters + d * BT + bt;
-  unsigned* gflags = counters + (D * BT + 1) + (d * BT + bt) * UB;   // flag variant
+  unsigned* gflags = counters + (D * BT + 1) + (d * BT + bt) * UB;
   const __amdgpu_buffer_rsrc_t g_rs = __builtin_amdgcn_make_buffer_rsrc(
       dgh, (short)0, T * N * D * H3 * 4, 0x00020000);
 
@@ -767,8 +743,7 @@ __global__ __launch_bounds__(GT) void gru_bwd_persist_kernel(
     }
     if (s > 0) {
       const int tq = d == 0 ? t + 1 : t - 1;
-      if (!(use_flags ? flags_wait(gflags, UB, (unsigned)s, err, &flag)
-                      : group_wait(ctr, (unsigned)s * UB, err, &flag))) {
+      if (!flags_wait(gflags, UB, (unsigned)s, err, &flag)) {
         poison_rest(dgx, s, T, d == 0, N, D, n, d, H, j, H3, 3, owner);
         return;
       }
@@ -820,8 +795,7 @@ __global__ __launch_bounds__(GT) void gru_bwd_persist_kernel(
       z_prev = zc;
       px_dar = dar; px_daz = daz; px_dan = dan; px_row = row;
     }
-    if (use_flags) flags_arrive(gflags + ub, (unsigned)s + 1);
-    else group_arrive(ctr);
+    flags_arrive(gflags + ub, (unsigned)s + 1);
     trace_at(s, 4);
     // dgx is consumed only by later kernels: store it after the hand-off is signalled
     if (owner) {
@@ -838,9 +812,10 @@ __global__ __launch_bounds__(GT) void gru_bwd_persist_kernel(
 // (dar, daz, dghn) as three 1-KB tiles, tile g * UB + ub of the ring
 //   gx[slot][d][bt][3 UB blocks][q][r][c],
 // whose block order is the k order of dgh; wave w owns blocks [b0, b0 + nb) of the 3 UB.
-// dgh (for the weight-gradient GEMM) and dgx are stored after the flag.
-// HM selects the hand-off form as in gru_fwd_dop_kernel.
-template <int NBW, int HM>
+// dgh (for the weight-gradient GEMM) and dgx are stored after the flag.  (A sentinel ring
+// measured slower here: 19 tiles per wave, and an early consumer pays one serial round trip
+// per stale tile, 7.55 vs 6.3 us per step; removed with the hybrid form in round 4.)
+template <int NBW>
 __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void gru_bwd_dop_kernel(
     int T, int N, int H, int D, int UB, int BT, const float* __restrict__ dy, int dyd,
     const float* __restrict__ w_f, const float* __restrict__ w_r,
@@ -864,17 +839,9 @@ __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   const unsigned* gflags = counters + (D * BT + 1) + (d * BT + bt) * UB;
   unsigned* myflag = counters + (D * BT + 1) + (d * BT + bt) * UB + ub;
   const int slot_floats = D * BT * NB3 * 256;
-  constexpr bool SENT = HM == 1 || HM == 2;   // sentinel ring: tiles validate themselves
-  constexpr bool FLAG = HM == 0 || HM == 2;   // per-producer flags polled before loading
-  constexpr int NSLOT = SENT ? kRingSlots : 2;
   const __amdgpu_buffer_rsrc_t x_rs =
-      __builtin_amdgcn_make_buffer_rsrc(gx, (short)0, NSLOT * slot_floats * 4, 0x00020000);
+      __builtin_amdgcn_make_buffer_rsrc(gx, (short)0, 2 * slot_floats * 4, 0x00020000);
   const int grp_off = (d * BT + bt) * NB3 * 256;
-  __shared__ int failed;
-  if (SENT) {
-    if (threadIdx.x == 0) failed = 0;
-    __syncthreads();
-  }
   const bool tracing = stamps != nullptr && threadIdx.x == 0;
   auto trace_at = [&](int s, int p) {
     if (tracing && s >= kTraceS0 && s < kTraceS0 + kTraceSteps)
@@ -928,13 +895,12 @@ __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
       if (tp >= 0 && tp < T) hp = h_all[(((int64_t)tp * N + n) * D + d) * H + j];
     }
     if (s > 0) {
-      if (FLAG && !flags_wait(gflags, UB, (unsigned)s, err, &flag)) {
+      if (!flags_wait(gflags, UB, (unsigned)s, err, &flag)) {
         poison_rest(dgx, s, T, d == 0, N, D, n, d, H, j, H3, 3, owner);
         return;
       }
       trace_at(s, 1);
-      const int base = (((s - 1) % NSLOT) * slot_floats + grp_off + b0 * 256 + lane * 4) * 4;
-      if (HM == 1) sleep_units(g_rnn_tune[2]);
+      const int base = (((s - 1) & 1) * slot_floats + grp_off + b0 * 256 + lane * 4) * 4;
       f32x4 gv[NBW];
 #pragma unroll
       for (int i = 0; i < NBW; ++i) {
@@ -943,51 +909,12 @@ __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
       }
       asm volatile("" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
-      if (SENT) {
-        // sentinel ring (and hybrid, HM 2: flag-polled, sentinel-validated): passes over the
-        // wave's tiles; each pass marks the ready ones,
-        // multiplies the ready PREFIX in tile order (one accumulation order for every
-        // hand-off form: bit-identical results) and re-loads only the stale tiles, so a
-        // pass costs one round trip however many tiles are stale
-        unsigned rdy = 0u;
-        int next = 0;
-        for (unsigned spins = 0;; ++spins) {
 #pragma unroll
-          for (int i = 0; i < NBW; ++i)
-            if (i >= next && i < nb && !((rdy >> i) & 1u) && wave_ready(gv[i])) rdy |= 1u << i;
-#pragma unroll
-          for (int i = 0; i < NBW; ++i) {
-            if (i == next && i < nb && ((rdy >> i) & 1u)) {
-              acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(gv[i][0], w[i][0], acc0, 0, 0, 0);
-              acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(gv[i][1], w[i][1], acc1, 0, 0, 0);
-              acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(gv[i][2], w[i][2], acc0, 0, 0, 0);
-              acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(gv[i][3], w[i][3], acc1, 0, 0, 0);
-              ++next;
-            }
-          }
-          if (next >= nb && g_spin_limit != 0) break;
-          if (spins > g_spin_limit || g_spin_limit == 0) {
-            if (lane == 0) __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            failed = 1;
-            break;
-          }
-          sleep_units(g_rnn_tune[0]);
-          asm volatile("" ::: "memory");
-#pragma unroll
-          for (int i = 0; i < NBW; ++i)
-            if (i >= next && i < nb && !((rdy >> i) & 1u))
-              gv[i] = __builtin_bit_cast(
-                  f32x4, __builtin_amdgcn_raw_buffer_load_b128(x_rs, base + i * 1024, 0, kSc1));
-        }
-      } else {
-#pragma unroll
-        for (int i = 0; i < NBW; ++i) {
-          if (SENT && i < nb && !spin_tile(gv[i], x_rs, base + i * 1024, err)) failed = 1;
-          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(gv[i][0], w[i][0], acc0, 0, 0, 0);
-          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(gv[i][1], w[i][1], acc1, 0, 0, 0);
-          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(gv[i][2], w[i][2], acc0, 0, 0, 0);
-          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(gv[i][3], w[i][3], acc1, 0, 0, 0);
-        }
+      for (int i = 0; i < NBW; ++i) {
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(gv[i][0], w[i][0], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(gv[i][1], w[i][1], acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(gv[i][2], w[i][2], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(gv[i][3], w[i][3], acc1, 0, 0, 0);
       }
       trace_at(s, 2);
     }
@@ -1001,10 +928,6 @@ __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     settle(g_hn);
     settle(hp);
     __syncthreads();
-    if (SENT && failed) {
-      poison_rest(dgx, s, T, d == 0, N, D, n, d, H, j, H3, 3, owner);
-      return;
-    }
     trace_at(s, 3);
     if (threadIdx.x < GB * GU) {
       float dar = 0.f, daz = 0.f, dan = 0.f, dghn = 0.f;
@@ -1037,34 +960,15 @@ __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     __syncthreads();
     if (wave == 0) {
       const int toff = (grp_off + ub * 256 + lane * 4) * 4;
-      if (SENT) {
-        u32x4 v[3];
+      const int so = (s & 1) * slot_floats * 4 + toff;
 #pragma unroll
-        for (int g = 0; g < 3; ++g)
-          v[g] = desentinel(*reinterpret_cast<const u32x4*>(tile + g * GB * GU + lane * 4));
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // last step's sentinel stores first
-        const int so = (s % NSLOT) * slot_floats * 4 + toff;
-#pragma unroll
-        for (int g = 0; g < 3; ++g)
-          __builtin_amdgcn_raw_buffer_store_b128(v[g], x_rs, so + g * UB * 1024, 0, kSc1);
-        const u32x4 sv = u32x4{kSentinel, kSentinel, kSentinel, kSentinel};
-        const int sn = ((s + 2) % NSLOT) * slot_floats * 4 + toff;
-#pragma unroll
-        for (int g = 0; g < 3; ++g)
-          __builtin_amdgcn_raw_buffer_store_b128(sv, x_rs, sn + g * UB * 1024, 0, kSc1);
-        if (FLAG && lane == 0)      // hybrid: no drain, the consumer validates the tiles
-          __hip_atomic_store(myflag, (unsigned)s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      } else {
-        const int so = (s & 1) * slot_floats * 4 + toff;
-#pragma unroll
-        for (int g = 0; g < 3; ++g) {
-          const u32x4 v = *reinterpret_cast<const u32x4*>(tile + g * GB * GU + lane * 4);
-          __builtin_amdgcn_raw_buffer_store_b128(v, x_rs, so + g * UB * 1024, 0, kSc1);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (lane == 0)
-          __hip_atomic_store(myflag, (unsigned)s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (int g = 0; g < 3; ++g) {
+        const u32x4 v = *reinterpret_cast<const u32x4*>(tile + g * GB * GU + lane * 4);
+        __builtin_amdgcn_raw_buffer_store_b128(v, x_rs, so + g * UB * 1024, 0, kSc1);
       }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0)
+        __hip_atomic_store(myflag, (unsigned)s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     trace_at(s, 4);
     if (owner) {
@@ -1088,190 +992,6 @@ __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     rd[(1 * GB + m) * GU + u] = mine ? sb_z : 0.0;
     rd[(2 * GB + m) * GU + u] = mine ? sb_n : 0.0;
     rd[(3 * GB + m) * GU + u] = mine ? sb_hn : 0.0;
-  }
-  __syncthreads();
-  if (threadIdx.x < 4 * GU) {
-    const int g = threadIdx.x / GU, uu = threadIdx.x - (threadIdx.x / GU) * GU;
-    double acc = 0.0;
-#pragma unroll
-    for (int mm = 0; mm < GB; ++mm) acc += rd[(g * GB + mm) * GU + uu];
-    dbp[(((int64_t)bt * D + d) * 4 + g) * H + ub * GU + uu] = acc;
-  }
-}
-
-// ---------------------------------------------------------------------------------------
-// Reduce-scatter backward (DS2_GRU_BWD_RS=1): each workgroup multiplies its OWN gate
-// gradients dG[16 samples][3 x 16 units] (K = 48) by the 48 rows of W_hh they belong to,
-// [48][H], into a partial dh for ALL H units, and publishes it as UB 1-KB tiles (one per
-// consuming unit block); a consumer sums the UB partial tiles of its 16 units in producer
-// order (deterministic).  Per step a workgroup reads UB KB (gru_bwd_dop_kernel: 3 UB KB, every
-// producer's three gate tiles) and writes UB KB.  Hand-off: per-producer flags (flags_wait;
-// the flag after every storing wave drained), 2-slot ring [slot][d][bt][consumer][producer]
-// [256].  Tiles are [unit][sample]: the 16x16x4 MFMA's D layout (lane l: unit l & 15,
-// samples 4 (l >> 4) .. + 3), so each lane publishes one 16-B store per consumer block.
-template <int NBK>
-__global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void gru_bwd_rs_kernel(
-    int T, int N, int H, int D, int UB, int BT, const float* __restrict__ dy, int dyd,
-    const float* __restrict__ w_f, const float* __restrict__ w_r,
-    const float* __restrict__ h_all, const float* __restrict__ gates,
-    const int* __restrict__ lens, float* __restrict__ dgx, float* __restrict__ dgh,
-    float* __restrict__ ring, unsigned* __restrict__ counters, unsigned* __restrict__ err,
-    double* __restrict__ dbp) {
-  constexpr int GP = GU + 1;                   // dG tile pitch (conflict-free A reads)
-  __shared__ __attribute__((aligned(16))) float red[GW * 256];   // [wave][unit][sample]
-  __shared__ float gt[3 * GB * GP];            // this step's dG [gate][sample][unit]
-  __shared__ int flag;
-  int ub, d, bt;
-  if (!map_work(UB * D, BT, UB, ub, d, bt)) return;
-  const int n0 = bt * GB;
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int H3 = 3 * H;
-  int c0, nc;
-  simd_split(UB, wave, c0, nc);                // consumer blocks this wave produces for and
-                                               // producers whose tiles it sums (host: <= NBK)
-  const unsigned* gflags = counters + (D * BT + 1) + (d * BT + bt) * UB;
-  unsigned* myflag = counters + (D * BT + 1) + (d * BT + bt) * UB + ub;
-  const int slot_floats = D * BT * UB * UB * 256;
-  const int grp = (d * BT + bt) * UB;          // consumer index base within a slot
-  const __amdgpu_buffer_rsrc_t r_rs =
-      __builtin_amdgcn_make_buffer_rsrc(ring, (short)0, 2 * slot_floats * 4, 0x00020000);
-
-  // B operand: w[c][kk] = W_hh[(k >> 4) H + 16 ub + (k & 15)][16 (c0 + c) + (lane & 15)],
-  // k = 4 kk + (lane >> 4)
-  float w[NBK][12];
-  {
-    const float* W = d == 0 ? w_f : w_r;
-#pragma unroll
-    for (int c = 0; c < NBK; ++c)
-#pragma unroll
-      for (int kk = 0; kk < 12; ++kk) {
-        const int k = 4 * kk + (lane >> 4);
-        const int64_t row = (int64_t)(k >> 4) * H + ub * GU + (k & 15);
-        w[c][kk] = c < nc ? W[row * H + GU * (c0 + c) + (lane & 15)] : 0.f;
-      }
-#pragma unroll
-    for (int c = 0; c < NBK; ++c)
-#pragma unroll
-      for (int kk = 0; kk < 12; ++kk) settle(w[c][kk]);
-  }
-  const int m = threadIdx.x >> 4;
-  const int u = threadIdx.x & 15;
-  const int n = n0 + m;
-  const int j = ub * GU + u;
-  const bool owner = threadIdx.x < GB * GU && n < N;
-  int len = owner ? lens[n] : 0;
-  settle(len);
-  float dh_prev = 0.f, z_prev = 0.f;
-  float px_dar = 0.f, px_daz = 0.f, px_dan = 0.f, px_dghn = 0.f;
-  int64_t px_row = -1;
-  double sb_r = 0.0, sb_z = 0.0, sb_n = 0.0, sb_hn = 0.0;
-  for (int s = 0; s < T; ++s) {
-    const int t = d == 0 ? T - 1 - s : s;
-    float dyv = 0.f, g_r = 0.f, g_z = 0.f, g_n = 0.f, g_hn = 0.f, hp = 0.f;
-    const int64_t row = ((int64_t)t * N + n) * D + d;
-    if (owner && t < len) {
-      dyv = dy[(((int64_t)t * N + n) * dyd + (dyd > 1 ? d : 0)) * H + j];
-      const float* gp = gates + row * 4 * H;
-      g_r = gp[j];
-      g_z = gp[H + j];
-      g_n = gp[2 * H + j];
-      g_hn = gp[3 * H + j];
-      const int tp = d == 0 ? t - 1 : t + 1;
-      if (tp >= 0 && tp < T) hp = h_all[(((int64_t)tp * N + n) * D + d) * H + j];
-    }
-    if (s > 0) {
-      if (!flags_wait(gflags, UB, (unsigned)s, err, &flag)) {
-        poison_rest(dgx, s, T, d == 0, N, D, n, d, H, j, H3, 3, owner);
-        return;
-      }
-      // the partial tiles of producers [c0, c0 + nc) for this workgroup's units
-      const int base = (((s - 1) & 1) * slot_floats + (grp + ub) * UB * 256 + c0 * 256) * 4 + lane * 16;
-      f32x4 pv[NBK];
-#pragma unroll
-      for (int c = 0; c < NBK; ++c)
-        pv[c] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                              r_rs, c < nc ? base + c * 1024 : 0x7ffffff0, 0, kSc1));
-      f32x4 sacc = pv[0];
-#pragma unroll
-      for (int c = 1; c < NBK; ++c) sacc += pv[c];
-      *reinterpret_cast<f32x4*>(red + wave * 256 + lane * 4) = sacc;
-    }
-    settle(dyv);
-    settle(g_r);
-    settle(g_z);
-    settle(g_n);
-    settle(g_hn);
-    settle(hp);
-    __syncthreads();
-    if (threadIdx.x < GB * GU) {
-      float dar = 0.f, daz = 0.f, dghn = 0.f;
-      if (owner) {
-        float dh = 0.f, zc = 0.f, dan = 0.f;
-        if (t < len) {
-          float carry = 0.f;
-          if (s > 0) {
-            float rec = 0.f;
-#pragma unroll
-            for (int w8 = 0; w8 < GW; ++w8) rec += red[w8 * 256 + u * 16 + m];
-            carry = dh_prev * z_prev + rec;
-          }
-          dh = dyv + carry;
-          zc = g_z;
-          dan = dh * (1.f - zc) * (1.f - g_n * g_n);
-          daz = dh * (hp - g_n) * zc * (1.f - zc);
-          dar = dan * g_hn * g_r * (1.f - g_r);
-          dghn = dan * g_r;
-        }
-        dh_prev = dh;
-        z_prev = zc;
-        px_dar = dar; px_daz = daz; px_dan = dan; px_dghn = dghn; px_row = row;
-        sb_r += dar; sb_z += daz; sb_n += dan; sb_hn += dghn;
-      }
-      gt[(0 * GB + m) * GP + u] = dar;
-      gt[(1 * GB + m) * GP + u] = daz;
-      gt[(2 * GB + m) * GP + u] = dghn;
-    }
-    __syncthreads();
-    // partial dh of every unit block c: [16 samples] x [K = 48] . [48] x [16 units]
-    float a[12];
-#pragma unroll
-    for (int kk = 0; kk < 12; ++kk) {
-      const int k = 4 * kk + (lane >> 4);
-      a[kk] = gt[((k >> 4) * GB + (lane & 15)) * GP + (k & 15)];
-    }
-    const int so = ((s & 1) * slot_floats + grp * UB * 256 + ub * 256) * 4 +
-                   ((lane & 15) * 16 + 4 * (lane >> 4)) * 4;
-#pragma unroll
-    for (int c = 0; c < NBK; ++c) {
-      if (c < nc) {
-        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int kk = 0; kk < 12; ++kk) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[kk], w[c][kk], acc, 0, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc), r_rs,
-                                               so + (c0 + c) * UB * 1024, 0, kSc1);
-      }
-    }
-    flags_arrive(myflag, (unsigned)s + 1);
-    if (owner) {
-      float* gxr = dgx + px_row * H3;
-      gxr[j] = px_dar;
-      gxr[H + j] = px_daz;
-      gxr[2 * H + j] = px_dan;
-      float* ghr = dgh + px_row * H3;
-      ghr[j] = px_dar;
-      ghr[H + j] = px_daz;
-      ghr[2 * H + j] = px_dghn;
-    }
-  }
-  if (dbp == nullptr) return;
-  double* rd = reinterpret_cast<double*>(red);   // 1024 doubles fit in red
-  __syncthreads();
-  if (threadIdx.x < GB * GU) {
-    rd[(0 * GB + m) * GU + u] = owner ? sb_r : 0.0;
-    rd[(1 * GB + m) * GU + u] = owner ? sb_z : 0.0;
-    rd[(2 * GB + m) * GU + u] = owner ? sb_n : 0.0;
-    rd[(3 * GB + m) * GU + u] = owner ? sb_hn : 0.0;
   }
   __syncthreads();
   if (threadIdx.x < 4 * GU) {
@@ -1327,27 +1047,18 @@ __global__ void gru_db_final_kernel(const double* __restrict__ dbp, int BT, int 
 
 namespace ds2 {
 // gru_split.hip: the same direct-operand recurrences with the W_hh contraction on the bf16
-// matrix cores at fp32 accuracy (default; DS2_GRU_X6=0 selects the fp32-MFMA kernels below)
-bool launch_gru_fwd_x6(int hm, int t_max, int n, int h, int num_dirs, const float* xproj,
+// matrix cores at fp32 accuracy (default; DS2_GRU_X6=0 selects the fp32-MFMA kernels above)
+bool launch_gru_fwd_x6(int t_max, int n, int h, int num_dirs, const float* xproj,
                        const float* w_hh_f, const float* w_hh_r, const float* b_hh_f,
                        const float* b_hh_r, const int* lens, float* h_all, float* gates,
-                       float* coef, float* ring, unsigned* ctrs, unsigned* err,
-                       unsigned long long* stamps, size_t lds_pad, hipStream_t st);
-bool launch_gru_bwd_x6(int hm, int t_max, int n, int h, int num_dirs, const float* dy, int dy_dirs,
+                       float* ring, unsigned* ctrs, unsigned* err, unsigned long long* stamps,
+                       size_t lds_pad, hipStream_t st);
+bool launch_gru_bwd_x6(int t_max, int n, int h, int num_dirs, const float* dy, int dy_dirs,
                        const float* w_hh_f, const float* w_hh_r, const float* h_all,
                        const float* gates, const int* lens, float* dgates_x, float* dgates_h,
                        float* ring, unsigned* ctrs, unsigned* err, unsigned long long* stamps,
-                       double* dbp,
-                       size_t lds_pad, hipStream_t st);
-// gru_bwd_dh.hip: the dh-exchange backward (opt-in) and the coefficient tiles it reads
-bool launch_gru_bwd_dh(int t_max, int n, int h, int num_dirs, const float* dy, int dy_dirs,
-                       const float* w_hh_f, const float* w_hh_r, const float* gates,
-                       const float* coef, const int* lens, float* dgates_x, float* dgates_h,
-                       float* ring, unsigned* ctrs, unsigned* err, unsigned long long* stamps,
                        double* dbp, size_t lds_pad, hipStream_t st);
 int gru_bwd_x6_grid(int n, int h, int num_dirs);
-void launch_gru_coef(const float* gates, const float* h_all, const int* lens, int t_max, int n,
-                     int h, int num_dirs, float* coef, hipStream_t st);
 }  // namespace ds2
 
 using namespace ds2;
@@ -1358,42 +1069,19 @@ static inline int stamp_mode() {
   const char* e = getenv("DS2_GRU_STAMPS");
   return e == nullptr ? 0 : (e[0] == '1' ? 1 : (e[0] == '2' ? 2 : 0));
 }
-// per-producer flags (default) or one arrival counter per group (DS2_RNN_FLAGS=0)
-static inline int flags_mode() {
-  const char* e = getenv("DS2_RNN_FLAGS");
-  return !(e != nullptr && e[0] == '0');
-}
-// counters (one per group) + error word + per-producer flags (64 per group), then stamps
-// direct-operand recurrence kernels (default; DS2_GRU_DOP=0 selects the LDS-staged ones)
-static inline int dop_enabled() {
-  const char* e = getenv("DS2_GRU_DOP");
-  return !(e != nullptr && e[0] == '0');
-}
+// the dynamic LDS of the direct-operand kernels: one workgroup per CU
 constexpr unsigned kDopPadLds = 80 * 1024;
 // smallest instantiated blocks-per-wave >= need (extra blocks are predicated off)
-// hand-off form of the direct-operand kernels (template HM): per-producer flags (0),
-// sentinel ring (1) or hybrid (2).  DS2_RNN_HANDOFF_FWD / _BWD (or DS2_RNN_HANDOFF for
-// both) = "flags" | "sentinel" | "hybrid"; defaults: the measured faster forms.
-static inline int handoff_mode(bool fwd) {
-  const char* e = getenv(fwd ? "DS2_RNN_HANDOFF_FWD" : "DS2_RNN_HANDOFF_BWD");
-  if (e == nullptr || e[0] == 0) e = getenv("DS2_RNN_HANDOFF");
-  if (e == nullptr || e[0] == 0) return fwd ? 1 : 0;
-  return e[0] == 's' ? 1 : (e[0] == 'h' ? 2 : 0);
-}
 static const void* bwd_dop_fn(int need) {
-  const int hm = handoff_mode(false);
-#define DS2_BDOP(K)                                                                      \
-  if (need <= K)                                                                         \
-    return hm == 1 ? reinterpret_cast<const void*>(gru_bwd_dop_kernel<K, 1>)             \
-         : hm == 2 ? reinterpret_cast<const void*>(gru_bwd_dop_kernel<K, 2>)             \
-                   : reinterpret_cast<const void*>(gru_bwd_dop_kernel<K, 0>);
+#define DS2_BDOP(K) \
+  if (need <= K) return reinterpret_cast<const void*>(gru_bwd_dop_kernel<K>);
   DS2_BDOP(1) DS2_BDOP(2) DS2_BDOP(3) DS2_BDOP(4) DS2_BDOP(6) DS2_BDOP(8) DS2_BDOP(10)
   DS2_BDOP(13) DS2_BDOP(16) DS2_BDOP(19) DS2_BDOP(22) DS2_BDOP(24)
 #undef DS2_BDOP
   return nullptr;
 }
 // group counters, the error word, 64 per-producer flags per group, then 64 per-producer XCC
-// ids per group (DS2_GRU_XCD)
+// ids per group (the same-XCD groups of gru_split.hip)
 static inline size_t ctr_words(int n, int num_dirs) {
   const int groups = num_dirs * ((n + GB - 1) / GB);
   return (size_t)groups + 1 + (size_t)groups * 128;
@@ -1409,43 +1097,24 @@ static inline unsigned long long* stamp_slots(unsigned* ctrs, int n, int num_dir
 }
 
 // ring of hand-off tiles for the direct-operand kernels (gates tiles per unit block: 1
-// forward, 3 backward): 2 slots for the flag hand-off, kRingSlots for the sentinel one; the
-// backward's tiles are sized for the pre-split form (1.5 KB, gru_split.hip)
-// (the forward's ring is doubled: the same-XCD groups keep a plainly stored copy of the
-// sentinel ring; the backward's pre-split flag form uses slots 2-3 for its copies)
+// forward, 3 backward).  Forward: kRingSlots slots of the sentinel ring, doubled for the
+// plainly stored copy the same-XCD groups read.  Backward: 2 slots of the flag hand-off plus
+// the 2 slots of plain copies, tiles sized for the pre-split form (1.5 KB, gru_split.hip).
 static inline size_t ring_bytes(int n, int h, int num_dirs, int tiles) {
   const size_t UB = (h + GU - 1) / GU, BT = (n + GB - 1) / GB;
   const size_t tile_floats = tiles == 3 ? 384 : 256;
-  const size_t slots = tiles == 3 ? kRingSlots : 2 * kRingSlots;
+  const size_t slots = tiles == 3 ? 4 : 2 * kRingSlots;
   return align256(slots * (size_t)num_dirs * BT * UB * tiles * tile_floats * sizeof(float));
 }
-// every ring word starts as the sentinel (slots 0 and 1 must; the rest for simplicity)
-static inline hipError_t ring_reset(float* ring, int n, int h, int num_dirs, int tiles,
-                                    hipStream_t st) {
-  return hipMemsetAsync(ring, 0xFF, ring_bytes(n, h, num_dirs, tiles), st);
+// every word of the forward's sentinel ring starts as the sentinel
+static inline hipError_t ring_reset(float* ring, int n, int h, int num_dirs, hipStream_t st) {
+  return hipMemsetAsync(ring, 0xFF, ring_bytes(n, h, num_dirs, 1), st);
 }
 
-// the gate cache: [T][N][D][4H] (r, z, n, W_hn h + b_hn), then the backward's coefficient
-// tiles (rnn_common.h, gru_bwd_dh.hip)
-static inline float* coef_part(const float* gates, int t_max, int n, int h, int num_dirs) {
-  return (gates == nullptr || !gru_dh_bwd_opted_in())
-             ? nullptr
-             : const_cast<float*>(gates) + (size_t)t_max * n * num_dirs * 4 * h;
-}
-
+// the gate cache: [T][N][D][4H] (r, z, n, W_hn h + b_hn)
 size_t ds2_gru_cache_floats(int t_max, int n, int h, int num_dirs) {
   if (t_max <= 0 || n <= 0 || h <= 0 || num_dirs <= 0) return 0;
-  return (size_t)t_max * n * num_dirs * 4 * h +
-         (gru_dh_bwd_opted_in() ? gru_coef_floats(t_max, n, h, num_dirs) : 0);
-}
-
-// every forward path but the bf16x6 one (which writes them itself): coefficient tiles after it
-static ds2_status_t fwd_coef(const float* gates, const float* h_all, const int* lens, int t_max,
-                             int n, int h, int num_dirs, hipStream_t st) {
-  if (coef_part(gates, t_max, n, h, num_dirs) != nullptr)
-    launch_gru_coef(gates, h_all, lens, t_max, n, h, num_dirs,
-                    coef_part(gates, t_max, n, h, num_dirs), st);
-  return launch_status("ds2_gru_fwd");
+  return (size_t)t_max * n * num_dirs * 4 * h;
 }
 
 size_t ds2_gru_fwd_workspace_size(int n, int h, int num_dirs) {
@@ -1468,6 +1137,10 @@ static int pick_ksw(int per) {
   return -1;
 }
 
+// Kernel choice (forward and backward alike): the direct-operand persistent kernels where
+// H % 16 == 0 and the grid fits the chip -- bf16x6 (gru_split.hip) by default, the fp32-MFMA
+// forms with DS2_GRU_X6=0 --, else the LDS-staged persistent kernels (H % 4 == 0), else one
+// launch per step (also DS2_RNN_PERSISTENT=0).
 ds2_status_t ds2_gru_fwd(int t_max, int n, int h, int num_dirs, const float* xproj,
                          const float* w_hh_f, const float* w_hh_r, const float* b_hh_f,
                          const float* b_hh_r, const int* lens, float* h_all, float* gates,
@@ -1491,11 +1164,12 @@ ds2_status_t ds2_gru_fwd(int t_max, int n, int h, int num_dirs, const float* xpr
   if (ksw < 0) return DS2_UNSUPPORTED_SHAPE;
   float* wp = static_cast<float*>(ws);
   const int grid = mapped_grid(UB * num_dirs, BT);
-  if (dop_enabled() && flags_mode() && (h % GU) == 0 && UB <= 8 * GW && grid <= num_cus() &&
-      (int64_t)t_max * n * num_dirs * h * 4 < (1ll << 31)) {
-    unsigned* ctrs = reinterpret_cast<unsigned*>(
-        static_cast<char*>(ws) + align256((size_t)num_dirs * UB * KS * 3 * 64 * sizeof(float)));
-    unsigned* err = ctrs + num_dirs * BT;
+  const bool persistent = persistent_enabled() && grid <= num_cus() &&
+                          (int64_t)t_max * n * num_dirs * h * 4 < (1ll << 31);
+  unsigned* ctrs = reinterpret_cast<unsigned*>(
+      static_cast<char*>(ws) + align256((size_t)num_dirs * UB * KS * 3 * 64 * sizeof(float)));
+  unsigned* err = ctrs + num_dirs * BT;
+  if (persistent && (h % GU) == 0 && UB <= 8 * GW) {
     if (hipMemsetAsync(ctrs, 0, counter_bytes(n, num_dirs), st) != hipSuccess)
       return launch_status("ds2_gru counters");
     int T_ = t_max, N_ = n, H_ = h, D_ = num_dirs, UB_ = UB, BT_ = BT;
@@ -1504,23 +1178,16 @@ ds2_status_t ds2_gru_fwd(int t_max, int n, int h, int num_dirs, const float* xpr
                                            align256(counter_bytes(n, num_dirs)));
     void* args[] = {&T_, &N_, &H_, &D_, &UB_, &BT_, &xproj, &w_hh_f, &w_hh_r, &b_hh_f,
                     &b_hh_r, &lens, &h_all, &gates, &ring, &ctrs, &err, &stamps};
-    const int hm = handoff_mode(true);
-    if (hm != 0 && ring_reset(ring, n, h, num_dirs, 1, st) != hipSuccess)
-      return launch_status("ds2_gru ring");
-    if (launch_gru_fwd_x6(hm, t_max, n, h, num_dirs, xproj, w_hh_f, w_hh_r, b_hh_f, b_hh_r, lens,
-                          h_all, gates, coef_part(gates, t_max, n, h, num_dirs), ring, ctrs, err,
-                          stamps, kDopPadLds, st)) {
+    if (ring_reset(ring, n, h, num_dirs, st) != hipSuccess) return launch_status("ds2_gru ring");
+    if (launch_gru_fwd_x6(t_max, n, h, num_dirs, xproj, w_hh_f, w_hh_r, b_hh_f, b_hh_r, lens,
+                          h_all, gates, ring, ctrs, err, stamps, kDopPadLds, st)) {
       fold_err(err, err_out, st);
       return launch_status("ds2_gru_fwd");
     }
     (void)hipGetLastError();
     const void* fn = nullptr;
-#define DS2_FDOP(K)                                                                  \
-  case K:                                                                            \
-    fn = hm == 1 ? reinterpret_cast<const void*>(gru_fwd_dop_kernel<K, 1>)           \
-       : hm == 2 ? reinterpret_cast<const void*>(gru_fwd_dop_kernel<K, 2>)           \
-                 : reinterpret_cast<const void*>(gru_fwd_dop_kernel<K, 0>);          \
-    break;
+#define DS2_FDOP(K) \
+  case K: fn = reinterpret_cast<const void*>(gru_fwd_dop_kernel<K>); break;
     switch ((UB + GW - 1) / GW) {
       DS2_FDOP(1) DS2_FDOP(2) DS2_FDOP(3) DS2_FDOP(4) DS2_FDOP(5) DS2_FDOP(6) DS2_FDOP(7)
       DS2_FDOP(8)
@@ -1531,25 +1198,20 @@ ds2_status_t ds2_gru_fwd(int t_max, int n, int h, int num_dirs, const float* xpr
     if (fn != nullptr &&
         rnn_launch(fn, dim3(grid), dim3(GT), args, kDopPadLds, st) == hipSuccess) {
       fold_err(err, err_out, st);
-      return fwd_coef(gates, h_all, lens, t_max, n, h, num_dirs, st);
+      return launch_status("ds2_gru_fwd");
     }
     (void)hipGetLastError();
   }
   hipLaunchKernelGGL(pack_fwd_kernel<3>, dim3(grid_cap((int64_t)num_dirs * UB * KS * 192)),
                      dim3(256), 0, st, w_hh_f, w_hh_r, h, num_dirs, UB, KS, wp);
-  if (persistent_enabled() && (h % 4) == 0 && grid <= num_cus() &&
-      (int64_t)t_max * n * num_dirs * h * 4 < (1ll << 31)) {
-    unsigned* ctrs = reinterpret_cast<unsigned*>(
-        static_cast<char*>(ws) + align256((size_t)num_dirs * UB * KS * 3 * 64 * sizeof(float)));
-    unsigned* err = ctrs + num_dirs * BT;
+  if (persistent && (h % 4) == 0) {
     if (hipMemsetAsync(ctrs, 0, counter_bytes(n, num_dirs), st) != hipSuccess)
       return launch_status("ds2_gru counters");
     int T_ = t_max, N_ = n, H_ = h, D_ = num_dirs, UB_ = UB, BT_ = BT;
     unsigned long long* stamps = stamp_slots(ctrs, n, num_dirs);
     int trace_ = stamp_mode() == 2 ? 1 : 0;
-    int flags_ = flags_mode();
     void* args[] = {&T_, &N_, &H_, &D_, &UB_, &BT_, &xproj, &wp, &b_hh_f, &b_hh_r, &lens,
-                    &h_all, &gates, &ctrs, &err, &stamps, &trace_, &flags_};
+                    &h_all, &gates, &ctrs, &err, &stamps, &trace_};
     const void* fn = nullptr;
     const int kp = persist_ksw((KS + GW - 1) / GW, KC_FWD);
     switch (kp) {
@@ -1562,7 +1224,7 @@ ds2_status_t ds2_gru_fwd(int t_max, int n, int h, int num_dirs, const float* xpr
     if (fn != nullptr &&
         rnn_launch(fn, dim3(grid), dim3(GT), args, 0, st) == hipSuccess) {
       fold_err(err, err_out, st);
-      return fwd_coef(gates, h_all, lens, t_max, n, h, num_dirs, st);
+      return launch_status("ds2_gru_fwd");
     }
     (void)hipGetLastError();   // fall back to one launch per step
   }
@@ -1572,7 +1234,7 @@ ds2_status_t ds2_gru_fwd(int t_max, int n, int h, int num_dirs, const float* xpr
       DS2_FWD_CASE(80) DS2_FWD_CASE(96)
     }
   }
-  return fwd_coef(gates, h_all, lens, t_max, n, h, num_dirs, st);
+  return launch_status("ds2_gru_fwd");
 }
 
 static size_t gru_bwd_ws_base(int n, int h, int num_dirs) {
@@ -1588,29 +1250,8 @@ static size_t gru_db_bytes(int n, int h, int num_dirs) {
   return align256((size_t)((n + GB - 1) / GB) * num_dirs * 4 * h * sizeof(double));
 }
 
-// reduce-scatter backward's ring: 2 slots x D x BT x UB consumers x UB producers x 1 KB
-static size_t gru_rs_ring_bytes(int n, int h, int num_dirs) {
-  const size_t UB = (h + GU - 1) / GU, BT = (n + GB - 1) / GB;
-  return align256(2 * (size_t)num_dirs * BT * UB * UB * 256 * sizeof(float));
-}
-
 size_t ds2_gru_bwd_workspace_size(int n, int h, int num_dirs) {
-  return gru_bwd_ws_base(n, h, num_dirs) + gru_db_bytes(n, h, num_dirs) +
-         gru_rs_ring_bytes(n, h, num_dirs);
-}
-
-// reduce-scatter backward (gru_bwd_rs_kernel): DS2_GRU_BWD_RS=1 selects it
-static inline bool rs_enabled() {
-  const char* e = getenv("DS2_GRU_BWD_RS");
-  return e != nullptr && e[0] == '1';
-}
-
-static const void* bwd_rs_fn(int need) {
-#define DS2_BRS(K) \
-  if (need <= K) return reinterpret_cast<const void*>(gru_bwd_rs_kernel<K>);
-  DS2_BRS(1) DS2_BRS(2) DS2_BRS(3) DS2_BRS(4) DS2_BRS(5) DS2_BRS(6) DS2_BRS(7) DS2_BRS(8)
-#undef DS2_BRS
-  return nullptr;
+  return gru_bwd_ws_base(n, h, num_dirs) + gru_db_bytes(n, h, num_dirs);
 }
 
 #define DS2_BWD_CASE(K)                                                                     \
@@ -1620,22 +1261,18 @@ static const void* bwd_rs_fn(int need) {
                        dgates_h, dhs);                                                       \
     break;
 
-static inline bool rs_enabled();
 // workgroups the persistent backward launch holds at once (gru_bwd_run's choice), 0 for the
 // per-step kernels
 int ds2_gru_bwd_grid(int n, int h, int num_dirs) {
   if (n < 1 || h < 1 || (num_dirs != 1 && num_dirs != 2)) return 0;
   const int UB = (h + GU - 1) / GU, BT = (n + GB - 1) / GB;
   const int grid = mapped_grid(UB * num_dirs, BT);
-  if (grid > num_cus()) return 0;
-  if (dop_enabled() && flags_mode() && (h % GU) == 0 && UB <= 8 * GW) {
-    if (!rs_enabled() && !gru_dh_bwd_opted_in()) {
-      const int g = gru_bwd_x6_grid(n, h, num_dirs);
-      if (g > 0) return g;
-    }
-    return grid;
+  if (!persistent_enabled() || grid > num_cus()) return 0;
+  if ((h % GU) == 0 && UB <= 8 * GW) {
+    const int g = gru_bwd_x6_grid(n, h, num_dirs);
+    return g > 0 ? g : grid;
   }
-  return (persistent_enabled() && 3 * h <= KC_BWD && (h % 4) == 0) ? grid : 0;
+  return (3 * h <= KC_BWD && (h % 4) == 0) ? grid : 0;
 }
 
 ds2_status_t ds2_gru_bwd(int t_max, int n, int h, int num_dirs, const float* dy, int dy_dirs,
@@ -1714,11 +1351,12 @@ static ds2_status_t gru_bwd_run(int t_max, int n, int h, int num_dirs, const flo
   size_t off = align256((size_t)num_dirs * UB * KS * 64 * sizeof(float));
   float* dhs = reinterpret_cast<float*>(static_cast<char*>(ws) + off);
   const int grid = mapped_grid(UB * num_dirs, BT);
-  if (dop_enabled() && flags_mode() && (h % GU) == 0 && UB <= 8 * GW && grid <= num_cus() &&
-      (int64_t)t_max * n * num_dirs * 3 * h * 4 < (1ll << 31)) {
-    unsigned* ctrs = reinterpret_cast<unsigned*>(
-        reinterpret_cast<char*>(dhs) + align256((size_t)2 * n * num_dirs * h * sizeof(float)));
-    unsigned* err = ctrs + num_dirs * BT;
+  const bool persistent = persistent_enabled() && grid <= num_cus() &&
+                          (int64_t)t_max * n * num_dirs * 3 * h * 4 < (1ll << 31);
+  unsigned* ctrs = reinterpret_cast<unsigned*>(
+      reinterpret_cast<char*>(dhs) + align256((size_t)2 * n * num_dirs * h * sizeof(float)));
+  unsigned* err = ctrs + num_dirs * BT;
+  if (persistent && (h % GU) == 0 && UB <= 8 * GW) {
     if (hipMemsetAsync(ctrs, 0, counter_bytes(n, num_dirs), st) != hipSuccess)
       return launch_status("ds2_gru counters");
     int T_ = t_max, N_ = n, H_ = h, D_ = num_dirs, UB_ = UB, BT_ = BT, DYD_ = dy_dirs;
@@ -1727,32 +1365,7 @@ static ds2_status_t gru_bwd_run(int t_max, int n, int h, int num_dirs, const flo
                                            align256(counter_bytes(n, num_dirs)));
     void* args[] = {&T_, &N_, &H_, &D_, &UB_, &BT_, &dy, &DYD_, &w_hh_f, &w_hh_r, &h_all,
                     &gates, &lens, &dgates_x, &dgates_h, &ring, &ctrs, &err, &stamps, &dbp};
-    if (rs_enabled() && dbp != nullptr) {
-      // blocks per wave of simd_split(UB): ceil(ceil(UB / 4) / 2) at most
-      const void* rfn = bwd_rs_fn(((UB + 3) / 4 + 1) / 2);
-      float* rring = reinterpret_cast<float*>(reinterpret_cast<char*>(dbp) + gru_db_bytes(n, h, num_dirs));
-      void* rargs[] = {&T_, &N_, &H_, &D_, &UB_, &BT_, &dy, &DYD_, &w_hh_f, &w_hh_r, &h_all,
-                       &gates, &lens, &dgates_x, &dgates_h, &rring, &ctrs, &err, &dbp};
-      if (rfn != nullptr &&
-          rnn_launch(rfn, dim3(grid), dim3(GT), rargs, kDopPadLds, st) == hipSuccess) {
-        fold_err(err, err_out, st);
-        summed = true;
-        return launch_status("ds2_gru_bwd");
-      }
-      (void)hipGetLastError();
-    }
-    if (launch_gru_bwd_dh(t_max, n, h, num_dirs, dy, dy_dirs, w_hh_f, w_hh_r, gates,
-                          coef_part(gates, t_max, n, h, num_dirs), lens, dgates_x, dgates_h, ring,
-                          ctrs, err, stamps, dbp, kDopPadLds, st)) {
-      fold_err(err, err_out, st);
-      summed = dbp != nullptr;
-      return launch_status("ds2_gru_bwd");
-    }
-    (void)hipGetLastError();
-    const int hmb = handoff_mode(false);
-    if ((hmb == 1 || hmb == 2) && ring_reset(ring, n, h, num_dirs, 3, st) != hipSuccess)
-      return launch_status("ds2_gru ring");
-    if (launch_gru_bwd_x6(hmb, t_max, n, h, num_dirs, dy, dy_dirs, w_hh_f, w_hh_r, h_all, gates,
+    if (launch_gru_bwd_x6(t_max, n, h, num_dirs, dy, dy_dirs, w_hh_f, w_hh_r, h_all, gates,
                           lens, dgates_x, dgates_h, ring, ctrs, err, stamps, dbp, kDopPadLds, st)) {
       fold_err(err, err_out, st);
       summed = dbp != nullptr;
@@ -1770,18 +1383,13 @@ static ds2_status_t gru_bwd_run(int t_max, int n, int h, int num_dirs, const flo
   }
   hipLaunchKernelGGL(pack_bwd_kernel<3>, dim3(grid_cap((int64_t)num_dirs * UB * KS * 64)),
                      dim3(256), 0, st, w_hh_f, w_hh_r, h, num_dirs, UB, KS, wpt);
-  if (persistent_enabled() && 3 * h <= KC_BWD && (h % 4) == 0 && grid <= num_cus() &&
-      (int64_t)t_max * n * num_dirs * 3 * h * 4 < (1ll << 31)) {
-    unsigned* ctrs = reinterpret_cast<unsigned*>(
-        reinterpret_cast<char*>(dhs) + align256((size_t)2 * n * num_dirs * h * sizeof(float)));
-    unsigned* err = ctrs + num_dirs * BT;
+  if (persistent && 3 * h <= KC_BWD && (h % 4) == 0) {
     if (hipMemsetAsync(ctrs, 0, counter_bytes(n, num_dirs), st) != hipSuccess)
       return launch_status("ds2_gru counters");
     int T_ = t_max, N_ = n, H_ = h, D_ = num_dirs, UB_ = UB, BT_ = BT, DYD_ = dy_dirs;
-    int flags_ = flags_mode();
     unsigned long long* stamps = stamp_mode() == 2 ? stamp_slots(ctrs, n, num_dirs) : nullptr;
     void* args[] = {&T_, &N_, &H_, &D_, &UB_, &BT_, &dy, &DYD_, &wpt, &h_all, &gates, &lens,
-                    &dgates_x, &dgates_h, &ctrs, &err, &flags_, &stamps};
+                    &dgates_x, &dgates_h, &ctrs, &err, &stamps};
     const void* fn = nullptr;
     const int kp = persist_ksw((KS + GW - 1) / GW, KC_BWD);
     switch (kp) {

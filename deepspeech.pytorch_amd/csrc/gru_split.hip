@@ -101,29 +101,26 @@ __device__ __forceinline__ void pair_split(int pairs, int wave, int& p0, int& np
 }
 
 // ---------------------------------------------------------------------------------------
-// forward: gh[16 samples x 48] = h_{t-1}[16 x H] . W_hh[r, z, n rows of 16 units]^T.
-// HM = hand-off form as in gru_fwd_dop_kernel: 0 per-producer flags, 1 sentinel ring.
-template <int NP, int HM>
+// forward: gh[16 samples x 48] = h_{t-1}[16 x H] . W_hh[r, z, n rows of 16 units]^T, with
+// the sentinel-ring hand-off of gru_fwd_dop_kernel (the data is the flag).
+template <int NP>
 __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(1, 1))) void gru_fwd_x6_kernel(
     int T, int N, int H, int D, int UB, int BT, const float* __restrict__ xproj,
     const float* __restrict__ w_f, const float* __restrict__ w_r, const float* __restrict__ b_f,
     const float* __restrict__ b_r, const int* __restrict__ lens, float* __restrict__ h_all,
-    float* __restrict__ gates, float* __restrict__ coef, float* __restrict__ hx,
-    unsigned* __restrict__ counters, unsigned* __restrict__ err,
-    unsigned long long* __restrict__ stamps, int xmode) {
+    float* __restrict__ gates, float* __restrict__ hx, unsigned* __restrict__ counters,
+    unsigned* __restrict__ err, unsigned long long* __restrict__ stamps, int xmode) {
   static_assert(2 * NP <= 64, "tsame holds a wave's tiles");
   constexpr int RP = 3 * GU + 1;
-  constexpr bool SENT = HM == 1;
-  constexpr int NSLOT = SENT ? kRingSlots : 2;
+  constexpr int NSLOT = kRingSlots;
   __shared__ float red[XW * GB * RP];
   __shared__ __attribute__((aligned(16))) float tile[GB * GU];
-  __shared__ int flag;
   __shared__ int failed;
   int ub, d, bt;
-  // xmode (sentinel ring only): same-XCD groups as in the backward -- every tile and its
-  // sentinel refill also stored plainly into a second ring (slots NSLOT..2 NSLOT-1), from
-  // which the consumers on the producer's XCD read it
-  const bool xg = SENT && xmode != 0;
+  // xmode: same-XCD groups as in the backward -- every tile and its sentinel refill also
+  // stored plainly into a second ring (slots NSLOT..2 NSLOT-1), from which the consumers on
+  // the producer's XCD read it
+  const bool xg = xmode != 0;
   if (xg ? !map_work_xgrp(UB, BT, D, ub, d, bt) : !map_work(UB * D, BT, UB, ub, d, bt)) return;
   unsigned* xtab = counters + (D * BT + 1) + D * BT * 64 + (d * BT + bt) * 64;
   const unsigned my_xcc = xcc_id() + 1u;
@@ -136,8 +133,6 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   int p0, np;
   pair_split((UB + 1) >> 1, wave, p0, np);          // host guarantees np <= NP
   const int t_first = 2 * p0;                       // first hand-off tile of this wave
-  const unsigned* gflags = counters + (D * BT + 1) + (d * BT + bt) * UB;
-  unsigned* myflag = counters + (D * BT + 1) + (d * BT + bt) * UB + ub;
   const int slot_floats = D * BT * UB * 256;
   const __amdgpu_buffer_rsrc_t x_rs = __builtin_amdgcn_make_buffer_rsrc(
       hx, (short)0, (xg ? 2 * NSLOT : NSLOT) * slot_floats * 4, 0x00020000);
@@ -193,9 +188,7 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   settle(len);
   const int tpos = ((u >> 2) * GB + m) * 4 + (u & 3);
   float g_r = 0.f, g_z = 0.f, g_n = 0.f, g_hn = 0.f, h_own = 0.f;
-  float c_r = 0.f, c_z = 0.f, c_hn = 0.f;
   int64_t g_row = -1;
-  int g_t = 0;
   for (int s = 0; s < T; ++s) {
     const int t = d == 0 ? s : T - 1 - s;
     const int64_t row = ((int64_t)t * N + n) * D + d;
@@ -211,10 +204,6 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     for (int g = 0; g < 3; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
     trace_at(s, 0);
     if (s > 0) {
-      if (!SENT && !flags_wait(gflags, UB, (unsigned)s, err, &flag)) {
-        poison_rest(h_all, s, T, d != 0, N, D, n, d, H, j, H, 1, owner);
-        return;
-      }
       trace_at(s, 1);
       if (xg && s == 1) {   // which producers share this XCD (ids published at their start)
         unsigned v = 0;
@@ -230,7 +219,7 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
           if (t_first + i < UB && ((same >> (t_first + i)) & 1ull)) tsame |= 1ull << i;
       }
       const int base = (((s - 1) % NSLOT) * slot_floats + grp_off + t_first * 256 + lane * 4) * 4;
-      if (SENT) sleep_units(g_rnn_tune[1]);
+      sleep_units(g_rnn_tune[1]);
       f32x4 hv[2 * NP];
 #pragma unroll
       for (int i = 0; i < 2 * NP; ++i) {
@@ -251,7 +240,7 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
       for (unsigned spins = 0;; ++spins) {
 #pragma unroll
         for (int p = 0; p < NP; ++p) {
-          if (((pend >> p) & 1u) && (!SENT || (wave_ready(hv[2 * p]) && wave_ready(hv[2 * p + 1])))) {
+          if (((pend >> p) & 1u) && wave_ready(hv[2 * p]) && wave_ready(hv[2 * p + 1])) {
             const Tri a = split3(hv[2 * p], hv[2 * p + 1]);
 #pragma unroll
             for (int g = 0; g < 3; ++g) pacc[p][g] = mma6(a, w[g][p], pacc[p][g]);
@@ -314,37 +303,27 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
         z = sigmoid_fast(ghz + xz);
         nn = tanh_fast(xn + r * ghn);
         hout = (h_own - nn) * z + nn;
-        gru_coefs(r, z, nn, ghn, h_own, c_r, c_z, c_hn);
       } else {
         ghn = 0.f;
-        c_r = c_z = c_hn = 0.f;
       }
       h_own = hout;
-      g_r = r; g_z = z; g_n = nn; g_hn = ghn; g_row = row; g_t = t;
+      g_r = r; g_z = z; g_n = nn; g_hn = ghn; g_row = row;
     }
     tile[tpos] = hout;
     __syncthreads();
     if (wave == 0) {
       const int toff = (grp_off + ub * 256 + lane * 4) * 4;
-      if (SENT) {
-        const u32x4 v = desentinel(*reinterpret_cast<const u32x4*>(tile + lane * 4));
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // last step's sentinel store first
-        __builtin_amdgcn_raw_buffer_store_b128(v, x_rs, (s % NSLOT) * slot_floats * 4 + toff, 0, kSc1);
-        const u32x4 sv = u32x4{kSentinel, kSentinel, kSentinel, kSentinel};
-        __builtin_amdgcn_raw_buffer_store_b128(sv, x_rs, ((s + 2) % NSLOT) * slot_floats * 4 + toff,
-                                               0, kSc1);
-        if (xg) {   // plain copies for the same-XCD consumers (kept in this XCD's L2)
-          __builtin_amdgcn_raw_buffer_store_b128(v, x_rs, aoff + (s % NSLOT) * slot_floats * 4 + toff,
-                                                 0, 0);
-          __builtin_amdgcn_raw_buffer_store_b128(
-              sv, x_rs, aoff + ((s + 2) % NSLOT) * slot_floats * 4 + toff, 0, 0);
-        }
-      } else {
-        const u32x4 v = *reinterpret_cast<const u32x4*>(tile + lane * 4);
-        __builtin_amdgcn_raw_buffer_store_b128(v, x_rs, (s & 1) * slot_floats * 4 + toff, 0, kSc1);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (lane == 0)
-          __hip_atomic_store(myflag, (unsigned)s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const u32x4 v = desentinel(*reinterpret_cast<const u32x4*>(tile + lane * 4));
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // last step's sentinel store first
+      __builtin_amdgcn_raw_buffer_store_b128(v, x_rs, (s % NSLOT) * slot_floats * 4 + toff, 0, kSc1);
+      const u32x4 sv = u32x4{kSentinel, kSentinel, kSentinel, kSentinel};
+      __builtin_amdgcn_raw_buffer_store_b128(sv, x_rs, ((s + 2) % NSLOT) * slot_floats * 4 + toff,
+                                             0, kSc1);
+      if (xg) {   // plain copies for the same-XCD consumers (kept in this XCD's L2)
+        __builtin_amdgcn_raw_buffer_store_b128(v, x_rs, aoff + (s % NSLOT) * slot_floats * 4 + toff,
+                                               0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(
+            sv, x_rs, aoff + ((s + 2) % NSLOT) * slot_floats * 4 + toff, 0, 0);
       }
     }
     trace_at(s, 4);
@@ -358,57 +337,45 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
         gp[3 * H + j] = g_hn;
       }
     }
-    if (coef != nullptr) {     // every tile slot written (zeros for samples past N)
-      float* cp = coef + coef_tile(owner ? g_t : t, d, bt, 0, ub, D, BT, UB) * 256 + tpos;
-      cp[0] = owner ? c_r : 0.f;
-      cp[(int64_t)UB * 256] = owner ? c_z : 0.f;
-      cp[(int64_t)2 * UB * 256] = owner ? c_hn : 0.f;
-    }
   }
 }
 
 // ---------------------------------------------------------------------------------------
 // backward: rec[16 samples x 16 units] = dG[16 x 3H] . W_hh[3H rows, 16 units], dG = the
 // (dar, daz, dghn) gate gradients of the step after (tiles g UB + ub of the ring, as in
-// gru_bwd_dop_kernel).  HM: 0 per-producer flags, 1 sentinel ring (pairs in order).
-// NW waves per workgroup: 4 (one per SIMD, all NP pairs' tiles loaded at once) or 8 (two
-// per SIMD: the consumer-side splits are VALU work, and a lone wave issues VALU at half the
-// rate of two co-resident ones; 256 registers each, so the tiles stream through a window of
-// LW pairs in flight).
-// PRE: the producers publish their gate-gradient tiles pre-split (per lane a 16-B {hi, mid}
-// run and an 8-B lo run: 1.5 KB per tile instead of 1 KB of fp32), so the consumer loads
-// ready MFMA operands and does no split VALU (flag hand-off; the runs stream through a window
-// of LWP pairs).  A sentinel ring over the runs (no drain, no flag: the data is the flag; each
-// stale pass re-issuing the window) measured 9.2 vs 6.3 us per step and was removed.
-// dbp (nullable): per-unit bias-gradient partials as gru_bwd_dop_kernel's.
-template <int NP, int HM, int NW, bool PRE>
-__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW / 4, NW / 4))) void gru_bwd_x6_kernel(
+// gru_bwd_dop_kernel).  8 waves per workgroup, two per SIMD (256 registers each).  The
+// producers publish their gate-gradient tiles PRE-SPLIT (per lane a 16-B {hi, mid} run and an
+// 8-B lo run: 1.5 KB per tile instead of 1 KB of fp32), so the consumer loads ready MFMA
+// operands and does no split VALU; the runs stream through a window of LWP pairs per wave;
+// per-producer flag hand-off (MI355X_MICROARCH "Valid forms" row 1).  Measured and removed in
+// round 4's pruning: consumer-side splits of fp32 tiles (6.5 vs 6.2 us per step), one wave
+// per SIMD with every run in flight (7.1), a sentinel ring over the runs (9.2: each stale pass
+// re-issues the window).  dbp (nullable): per-unit bias-gradient partials as
+// gru_bwd_dop_kernel's.
+constexpr int BW = 8;            // waves per backward workgroup
+template <int NP>
+__global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(2, 2))) void gru_bwd_x6_kernel(
     int T, int N, int H, int D, int UB, int BT, const float* __restrict__ dy, int dyd,
     const float* __restrict__ w_f, const float* __restrict__ w_r,
     const float* __restrict__ h_all, const float* __restrict__ gates,
     const int* __restrict__ lens, float* __restrict__ dgx, float* __restrict__ dgh,
     float* __restrict__ gx, unsigned* __restrict__ counters, unsigned* __restrict__ err,
     unsigned long long* __restrict__ stamps, double* __restrict__ dbp, int xmode) {
-  static_assert(!PRE || HM == 0, "pre-split tiles use the flag hand-off");
   static_assert(2 * NP <= 64, "tsame holds a wave's tiles");
   constexpr int RP = GU + 1;
-  constexpr bool SENT = HM == 1;
-  constexpr int NSLOT = SENT ? kRingSlots : 2;
-  constexpr int LW = NW == 4 ? NP : 3;          // pairs whose loads are in flight
-  constexpr int TF = PRE ? 384 : 256;           // ring floats per tile
-  // PRE window: pairs of runs in flight per wave; with the same-XCD groups 4 (or 3) beat 5
-  // (5.41 -> 5.34 us per step, 6: 5.47; profiles/r3lw_bwd_window.txt)
-  constexpr int LWP = NW == 4 ? (NP < 12 ? NP : 12) : (NP < 4 ? NP : 4);
-  constexpr int RED = NW * GB * RP > 8 * GB * GU ? NW * GB * RP : 8 * GB * GU;
+  constexpr int TF = 384;                       // ring floats per pre-split tile
+  // pairs of runs in flight per wave: with the same-XCD groups 4 (or 3) beat 5 (5.41 -> 5.34
+  // us per step, 6: 5.47; profiles/r3lw_bwd_window.txt)
+  constexpr int LWP = NP < 4 ? NP : 4;
+  constexpr int RED = BW * GB * RP > 8 * GB * GU ? BW * GB * RP : 8 * GB * GU;
   __shared__ __attribute__((aligned(8))) float red[RED];
   __shared__ __attribute__((aligned(16))) float tile[3 * GB * GU];
   __shared__ int flag;
-  __shared__ int failed;
   int ub, d, bt;
-  // xmode (PRE only): same-XCD groups -- every tile is also stored plainly into ring slots
-  // 2-3 (kept in the producer's L2) and a consumer loads the tiles of the producers that
-  // share its XCD from there
-  const bool xg = PRE && xmode != 0;
+  // xmode: same-XCD groups -- every tile is also stored plainly into ring slots 2-3 (kept in
+  // the producer's L2) and a consumer loads the tiles of the producers that share its XCD
+  // from there
+  const bool xg = xmode != 0;
   if (xg ? !map_work_xgrp(UB, BT, D, ub, d, bt) : !map_work(UB * D, BT, UB, ub, d, bt)) return;
   const int n0 = bt * GB;
   const int lane = threadIdx.x & 63;
@@ -421,18 +388,16 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW / 4,
     __hip_atomic_store(xtab + ub, my_xcc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   uint64_t tsame = 0;           // bit i: this wave's tile t_first + i comes from this XCD
   const int pairs = (NB3 + 1) >> 1;
-  const int p0 = (pairs * wave) / NW;
-  const int np = (pairs * (wave + 1)) / NW - p0;   // host guarantees np <= NP
+  const int p0 = (pairs * wave) / BW;
+  const int np = (pairs * (wave + 1)) / BW - p0;   // host guarantees np <= NP
   const int t_first = 2 * p0;
   const unsigned* gflags = counters + (D * BT + 1) + (d * BT + bt) * UB;
   unsigned* myflag = counters + (D * BT + 1) + (d * BT + bt) * UB + ub;
   const int slot_floats = D * BT * NB3 * TF;
   const __amdgpu_buffer_rsrc_t x_rs = __builtin_amdgcn_make_buffer_rsrc(
-      gx, (short)0, (xg ? 4 : NSLOT) * slot_floats * 4, 0x00020000);
+      gx, (short)0, (xg ? 4 : 2) * slot_floats * 4, 0x00020000);
   const int grp_off = (d * BT + bt) * NB3 * TF;
   const int aoff = 2 * slot_floats * 4;   // the plain-store copies (xmode)
-  if (threadIdx.x == 0) failed = 0;
-  __syncthreads();
   // diagnostic timeline (DS2_GRU_STAMPS=2, scripts/trace_gru.py): s_memrealtime at step
   // start / wait done / products done / reduction done / published, for kXTraceSteps steps
   const bool tracing = stamps != nullptr && threadIdx.x == 0;
@@ -491,72 +456,44 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW / 4,
     }
     trace_at(s, 0);
     if (s > 0) {
-      if (!SENT && !flags_wait(gflags, UB, (unsigned)s, err, &flag)) {
+      if (!flags_wait(gflags, UB, (unsigned)s, err, &flag)) {
         poison_rest(dgx, s, T, d == 0, N, D, n, d, H, j, H3, 3, owner);
         return;
       }
       trace_at(s, 1);
-      if constexpr (PRE) {
-        if (xg && s == 1) {   // which producers share this XCD (their ids came with step 0)
-          const unsigned v = lane < UB ? __hip_atomic_load(xtab + lane, __ATOMIC_RELAXED,
-                                                           __HIP_MEMORY_SCOPE_AGENT) : 0u;
-          const unsigned long long same = __ballot(v == my_xcc);
+      if (xg && s == 1) {   // which producers share this XCD (their ids came with step 0)
+        const unsigned v = lane < UB ? __hip_atomic_load(xtab + lane, __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT) : 0u;
+        const unsigned long long same = __ballot(v == my_xcc);
 #pragma unroll
-          for (int i = 0; i < 2 * NP; ++i)
-            if ((same >> ((t_first + i) % UB)) & 1ull) tsame |= 1ull << i;
-        }
-        // LWP pairs' runs in flight, the next pair's issued as each pair is multiplied
-        const int tb0 = (((s - 1) & 1) * slot_floats + grp_off + t_first * TF) * 4;
-        u32x4 hm[2 * NP];
-        u32x2 lo[2 * NP];
-        auto load_run = [&](int i) {
-          const bool ok = i < 2 * np && t_first + i < NB3;
-          const int to = tb0 + i * TF * 4 + (((tsame >> i) & 1ull) ? aoff : 0);
-          hm[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                x_rs, ok ? to + lane * 16 : 0x7ffffff0, 0, kSc1));
-          lo[i] = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(
-                                                x_rs, ok ? to + 1024 + lane * 8 : 0x7ffffff0, 0, kSc1));
-        };
-#pragma unroll
-        for (int i = 0; i < 2 * LWP; ++i) load_run(i);
-        asm volatile("" ::: "memory");
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int p = 0; p < NP; ++p) {
-          if (p + LWP < NP) {
-            load_run(2 * (p + LWP));
-            load_run(2 * (p + LWP) + 1);
-          }
-          acc = mma6(tri_of(hm[2 * p], lo[2 * p], hm[2 * p + 1], lo[2 * p + 1]), w[p], acc);
-        }
-        trace_at(s, 2);
-      } else {
-      const int base = (((s - 1) % NSLOT) * slot_floats + grp_off + t_first * 256 + lane * 4) * 4;
-      f32x4 gv[2 * NP];
-      auto load_tile = [&](int i) {
-        const int off = (i < 2 * np && t_first + i < NB3) ? base + i * 1024 : 0x7ffffff0;
-        gv[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(x_rs, off, 0, kSc1));
+        for (int i = 0; i < 2 * NP; ++i)
+          if ((same >> ((t_first + i) % UB)) & 1ull) tsame |= 1ull << i;
+      }
+      // LWP pairs' runs in flight, the next pair's issued as each pair is multiplied
+      const int tb0 = (((s - 1) & 1) * slot_floats + grp_off + t_first * TF) * 4;
+      u32x4 hm[2 * NP];
+      u32x2 lo[2 * NP];
+      auto load_run = [&](int i) {
+        const bool ok = i < 2 * np && t_first + i < NB3;
+        const int to = tb0 + i * TF * 4 + (((tsame >> i) & 1ull) ? aoff : 0);
+        hm[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                              x_rs, ok ? to + lane * 16 : 0x7ffffff0, 0, kSc1));
+        lo[i] = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(
+                                              x_rs, ok ? to + 1024 + lane * 8 : 0x7ffffff0, 0, kSc1));
       };
 #pragma unroll
-      for (int i = 0; i < 2 * LW; ++i) load_tile(i);
+      for (int i = 0; i < 2 * LWP; ++i) load_run(i);
       asm volatile("" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int p = 0; p < NP; ++p) {
-        if (p + LW < NP) {
-          load_tile(2 * (p + LW));
-          load_tile(2 * (p + LW) + 1);
+        if (p + LWP < NP) {
+          load_run(2 * (p + LWP));
+          load_run(2 * (p + LWP) + 1);
         }
-        if (SENT && p < np) {
-          if (!spin_tile(gv[2 * p], x_rs, base + 2 * p * 1024, err)) failed = 1;
-          if (t_first + 2 * p + 1 < NB3 &&
-              !spin_tile(gv[2 * p + 1], x_rs, base + (2 * p + 1) * 1024, err))
-            failed = 1;
-        }
-        acc = mma6(split3(gv[2 * p], gv[2 * p + 1]), w[p], acc);
+        acc = mma6(tri_of(hm[2 * p], lo[2 * p], hm[2 * p + 1], lo[2 * p + 1]), w[p], acc);
       }
       trace_at(s, 2);
-      }
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r)
@@ -568,10 +505,6 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW / 4,
     settle(g_hn);
     settle(hp);
     __syncthreads();
-    if (failed) {
-      poison_rest(dgx, s, T, d == 0, N, D, n, d, H, j, H3, 3, owner);
-      return;
-    }
     trace_at(s, 3);
     float dar = 0.f, daz = 0.f, dan = 0.f, dghn = 0.f;
     if (owner) {
@@ -581,7 +514,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW / 4,
         if (s > 0) {
           float rec = 0.f;
 #pragma unroll
-          for (int w8 = 0; w8 < NW; ++w8) rec += red[(w8 * GB + m) * RP + u];
+          for (int w8 = 0; w8 < BW; ++w8) rec += red[(w8 * GB + m) * RP + u];
           carry = dh_prev * z_prev + rec;
         }
         dh = dyv + carry;
@@ -603,51 +536,23 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW / 4,
     }
     __syncthreads();
     if (wave == 0) {
-      const int toff = (grp_off + ub * 256 + lane * 4) * 4;
-      if (SENT) {
-        u32x4 v[3];
+      const int so = ((s & 1) * slot_floats + grp_off + ub * TF) * 4;
 #pragma unroll
-        for (int g = 0; g < 3; ++g)
-          v[g] = desentinel(*reinterpret_cast<const u32x4*>(tile + g * GB * GU + lane * 4));
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const int so = (s % NSLOT) * slot_floats * 4 + toff;
-#pragma unroll
-        for (int g = 0; g < 3; ++g)
-          __builtin_amdgcn_raw_buffer_store_b128(v[g], x_rs, so + g * UB * 1024, 0, kSc1);
-        const u32x4 sv = u32x4{kSentinel, kSentinel, kSentinel, kSentinel};
-        const int sn = ((s + 2) % NSLOT) * slot_floats * 4 + toff;
-#pragma unroll
-        for (int g = 0; g < 3; ++g)
-          __builtin_amdgcn_raw_buffer_store_b128(sv, x_rs, sn + g * UB * 1024, 0, kSc1);
-      } else if constexpr (PRE) {
-        const int so = ((s & 1) * slot_floats + grp_off + ub * TF) * 4;
-#pragma unroll
-        for (int g = 0; g < 3; ++g) {
-          u32x4 hmv;
-          u32x2 lov;
-          split_pk4(*reinterpret_cast<const f32x4*>(tile + g * GB * GU + lane * 4), hmv, lov);
-          const int go = so + g * UB * TF * 4;
-          __builtin_amdgcn_raw_buffer_store_b128(hmv, x_rs, go + lane * 16, 0, kSc1);
-          __builtin_amdgcn_raw_buffer_store_b64(lov, x_rs, go + 1024 + lane * 8, 0, kSc1);
-          if (xg) {   // plain copies: stay in this XCD's L2 for the same-XCD consumers
-            __builtin_amdgcn_raw_buffer_store_b128(hmv, x_rs, aoff + go + lane * 16, 0, 0);
-            __builtin_amdgcn_raw_buffer_store_b64(lov, x_rs, aoff + go + 1024 + lane * 8, 0, 0);
-          }
+      for (int g = 0; g < 3; ++g) {
+        u32x4 hmv;
+        u32x2 lov;
+        split_pk4(*reinterpret_cast<const f32x4*>(tile + g * GB * GU + lane * 4), hmv, lov);
+        const int go = so + g * UB * TF * 4;
+        __builtin_amdgcn_raw_buffer_store_b128(hmv, x_rs, go + lane * 16, 0, kSc1);
+        __builtin_amdgcn_raw_buffer_store_b64(lov, x_rs, go + 1024 + lane * 8, 0, kSc1);
+        if (xg) {   // plain copies: stay in this XCD's L2 for the same-XCD consumers
+          __builtin_amdgcn_raw_buffer_store_b128(hmv, x_rs, aoff + go + lane * 16, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b64(lov, x_rs, aoff + go + 1024 + lane * 8, 0, 0);
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (lane == 0)
-          __hip_atomic_store(myflag, (unsigned)s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      } else {
-        const int so = (s & 1) * slot_floats * 4 + toff;
-#pragma unroll
-        for (int g = 0; g < 3; ++g) {
-          const u32x4 v = *reinterpret_cast<const u32x4*>(tile + g * GB * GU + lane * 4);
-          __builtin_amdgcn_raw_buffer_store_b128(v, x_rs, so + g * UB * 1024, 0, kSc1);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (lane == 0)
-          __hip_atomic_store(myflag, (unsigned)s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0)
+        __hip_atomic_store(myflag, (unsigned)s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     trace_at(s, 4);
     if (owner) {
@@ -685,131 +590,84 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW / 4,
 // host launchers (called by ds2_gru_fwd / ds2_gru_bwd in gru.hip with their workspace
 // carve-up); false = shape not covered (caller falls back to the fp32-MFMA kernels)
 
-// forward: on by default (DS2_GRU_X6=0 selects the fp32-MFMA kernel).  backward: the
-// pre-split form by default (cfg2: 6.13 / 6.22 vs 6.29 / 6.27 us per step for the fp32-MFMA
-// kernel, alternating runs on one box); the consumer-side splits of 3H-wide gate gradients
-// made the first x6 backward VALU-bound after the flag wait (6.5 vs 6.2), and one wave per
-// SIMD with every pre-split run in flight measured 7.1.
+// on by default; DS2_GRU_X6=0 selects the fp32-MFMA kernels (gru.hip: the accuracy
+// cross-check of the tests)
 static inline bool x6_enabled() {
   const char* e = getenv("DS2_GRU_X6");
   return !(e != nullptr && e[0] == '0');
 }
 
-// DS2_GRU_X6_BWD: 2 (default) = pre-split tiles (flag hand-off; the sentinel forms keep the
-// fp32-MFMA kernel), 1 = consumer-side splits, 0 = the fp32-MFMA kernel (gru.hip);
-// DS2_GRU_X6_BWD_WAVES=4: one wave per SIMD instead of two
-static inline int x6_bwd_mode() {
-  const char* e = getenv("DS2_GRU_X6_BWD");
-  if (!x6_enabled()) return 0;
-  if (e == nullptr || e[0] == 0) return 2;
-  return e[0] == '1' ? 1 : (e[0] == '2' ? 2 : 0);
-}
-
-static const void* fwd_x6_fn(int need, int hm) {
+static const void* fwd_x6_fn(int need) {
 #define DS2_FX6(K) \
-  if (need <= K)   \
-    return hm == 1 ? reinterpret_cast<const void*>(gru_fwd_x6_kernel<K, 1>)  \
-                   : reinterpret_cast<const void*>(gru_fwd_x6_kernel<K, 0>);
+  if (need <= K) return reinterpret_cast<const void*>(gru_fwd_x6_kernel<K>);
   DS2_FX6(1) DS2_FX6(2) DS2_FX6(3) DS2_FX6(4) DS2_FX6(5) DS2_FX6(6) DS2_FX6(7)
 #undef DS2_FX6
   return nullptr;
 }
 
-static int x6_bwd_waves() {
-  const char* e = getenv("DS2_GRU_X6_BWD_WAVES");
-  return (e != nullptr && e[0] == '4') ? 4 : 8;
-}
-
-static const void* bwd_x6_fn(int pairs, int hm, int nw, bool pre) {
-  const int need = (pairs + nw - 1) / nw;
-  if (pre) {
-#define DS2_BP6(K, W) \
-    if (need <= K) return reinterpret_cast<const void*>(gru_bwd_x6_kernel<K, 0, W, true>);
-    if (nw == 4) {
-      DS2_BP6(1, 4) DS2_BP6(2, 4) DS2_BP6(4, 4) DS2_BP6(6, 4) DS2_BP6(8, 4) DS2_BP6(10, 4)
-      DS2_BP6(13, 4) DS2_BP6(16, 4) DS2_BP6(19, 4)
-    } else {
-      DS2_BP6(1, 8) DS2_BP6(2, 8) DS2_BP6(3, 8) DS2_BP6(4, 8) DS2_BP6(6, 8) DS2_BP6(8, 8)
-      DS2_BP6(10, 8) DS2_BP6(12, 8)
-    }
+static const void* bwd_x6_fn(int pairs) {
+  const int need = (pairs + BW - 1) / BW;
+#define DS2_BP6(K) \
+  if (need <= K) return reinterpret_cast<const void*>(gru_bwd_x6_kernel<K>);
+  DS2_BP6(1) DS2_BP6(2) DS2_BP6(3) DS2_BP6(4) DS2_BP6(6) DS2_BP6(8) DS2_BP6(10) DS2_BP6(12)
 #undef DS2_BP6
-    return nullptr;
-  }
-#define DS2_BX6(K, W)                                                                      \
-  if (need <= K)                                                                           \
-    return hm == 1 ? reinterpret_cast<const void*>(gru_bwd_x6_kernel<K, 1, W, false>)     \
-                   : reinterpret_cast<const void*>(gru_bwd_x6_kernel<K, 0, W, false>);
-  if (nw == 4) {
-    DS2_BX6(1, 4) DS2_BX6(2, 4) DS2_BX6(3, 4) DS2_BX6(4, 4) DS2_BX6(6, 4) DS2_BX6(8, 4)
-    DS2_BX6(10, 4) DS2_BX6(13, 4) DS2_BX6(16, 4) DS2_BX6(19, 4)
-  } else {
-    DS2_BX6(1, 8) DS2_BX6(2, 8) DS2_BX6(3, 8) DS2_BX6(4, 8) DS2_BX6(5, 8) DS2_BX6(6, 8)
-    DS2_BX6(8, 8) DS2_BX6(10, 8) DS2_BX6(12, 8)
-  }
-#undef DS2_BX6
   return nullptr;
 }
 
-bool launch_gru_fwd_x6(int hm, int t_max, int n, int h, int num_dirs, const float* xproj,
+// same-XCD hand-off groups (rnn_common.h map_work_xgrp), default on where the groups tile the
+// 8 XCDs: cfg2 backward 5.82 -> 5.43 us per step in isolation, 6.14 -> 5.69 in the training
+// step; DS2_GRU_XCD=0 keeps map_work's interleaved layout (bit-identical results)
+static inline bool xcd_groups(int UB, int BT, int num_dirs) {
+  const char* xe = getenv("DS2_GRU_XCD");
+  return !(xe != nullptr && xe[0] == '0') && xgrp_fits(UB, BT, num_dirs);
+}
+
+bool launch_gru_fwd_x6(int t_max, int n, int h, int num_dirs, const float* xproj,
                        const float* w_hh_f, const float* w_hh_r, const float* b_hh_f,
                        const float* b_hh_r, const int* lens, float* h_all, float* gates,
-                       float* coef, float* ring, unsigned* ctrs, unsigned* err,
-                       unsigned long long* stamps, size_t lds_pad, hipStream_t st) {
+                       float* ring, unsigned* ctrs, unsigned* err, unsigned long long* stamps,
+                       size_t lds_pad, hipStream_t st) {
   if (!x6_enabled() || (h % GU) != 0) return false;
   apply_spin_limit_env();     // this translation unit's copies of the device knobs
   apply_rnn_tune_env();
   const int UB = h / GU, BT = (n + GB - 1) / GB;
   const int need = ((UB + 1) / 2 + XW - 1) / XW;
-  const void* fn = fwd_x6_fn(need, hm == 1 ? 1 : 0);
+  const void* fn = fwd_x6_fn(need);
   if (fn == nullptr) return false;
-  // same-XCD groups for the sentinel ring (as the backward; DS2_GRU_XCD=0 turns them off)
-  const char* xe = getenv("DS2_GRU_XCD");
-  int XM_ = (hm == 1 && !(xe != nullptr && xe[0] == '0') && xgrp_fits(UB, BT, num_dirs)) ? 1 : 0;
+  int XM_ = xcd_groups(UB, BT, num_dirs) ? 1 : 0;
   const int grid = XM_ ? xgrp_grid(UB, BT, num_dirs) : mapped_grid(UB * num_dirs, BT);
   int T_ = t_max, N_ = n, H_ = h, D_ = num_dirs, UB_ = UB, BT_ = BT;
   void* args[] = {&T_, &N_, &H_, &D_, &UB_, &BT_, &xproj, &w_hh_f, &w_hh_r, &b_hh_f,
-                  &b_hh_r, &lens, &h_all, &gates, &coef, &ring, &ctrs, &err, &stamps, &XM_};
+                  &b_hh_r, &lens, &h_all, &gates, &ring, &ctrs, &err, &stamps, &XM_};
   return rnn_launch(fn, dim3(grid), dim3(XT), args, lds_pad, st) == hipSuccess;
 }
 
-// grid of the x6 backward launch_gru_bwd_x6 would make (flag hand-off), -1 if it declines
+// grid of the x6 backward launch_gru_bwd_x6 would make, -1 if it declines the shape
 int gru_bwd_x6_grid(int n, int h, int num_dirs) {
-  const int mode = x6_bwd_mode();
-  if (mode == 0 || (h % GU) != 0) return -1;
+  if (!x6_enabled() || (h % GU) != 0) return -1;
   const int UB = h / GU, BT = (n + GB - 1) / GB;
-  if (bwd_x6_fn((3 * UB + 1) / 2, 0, x6_bwd_waves(), mode == 2) == nullptr) return -1;
-  const char* xe = getenv("DS2_GRU_XCD");
-  const bool xcd_on = !(xe != nullptr && xe[0] == '0');
-  return (mode == 2 && xcd_on && xgrp_fits(UB, BT, num_dirs)) ? xgrp_grid(UB, BT, num_dirs)
-                                                                : mapped_grid(UB * num_dirs, BT);
+  if (bwd_x6_fn((3 * UB + 1) / 2) == nullptr) return -1;
+  return xcd_groups(UB, BT, num_dirs) ? xgrp_grid(UB, BT, num_dirs)
+                                      : mapped_grid(UB * num_dirs, BT);
 }
 
-bool launch_gru_bwd_x6(int hm, int t_max, int n, int h, int num_dirs, const float* dy, int dy_dirs,
+bool launch_gru_bwd_x6(int t_max, int n, int h, int num_dirs, const float* dy, int dy_dirs,
                        const float* w_hh_f, const float* w_hh_r, const float* h_all,
                        const float* gates, const int* lens, float* dgates_x, float* dgates_h,
                        float* ring, unsigned* ctrs, unsigned* err, unsigned long long* stamps,
                        double* dbp, size_t lds_pad, hipStream_t st) {
-  const int mode = x6_bwd_mode();
-  if (mode == 0 || (h % GU) != 0) return false;
-  const bool pre = mode == 2;
-  if (pre && hm != 0) return false;          // pre-split tiles: flag hand-off only
+  if (!x6_enabled() || (h % GU) != 0) return false;
   apply_spin_limit_env();
   apply_rnn_tune_env();
   const int UB = h / GU, BT = (n + GB - 1) / GB;
-  const int nw = x6_bwd_waves();
-  const void* fn = bwd_x6_fn((3 * UB + 1) / 2, hm == 1 ? 1 : 0, nw, pre);
+  const void* fn = bwd_x6_fn((3 * UB + 1) / 2);
   if (fn == nullptr) return false;
-  // same-XCD hand-off groups (pre-split tiles only; rnn_common.h map_work_xgrp), default on:
-  // cfg2 backward 5.82 -> 5.43 us per step in isolation, 6.14 -> 5.69 in the training step
-  // (scripts/gpu_r3s.sh, alternating runs on one box); DS2_GRU_XCD=0 keeps map_work's layout
-  const char* xe = getenv("DS2_GRU_XCD");
-  const bool xcd_on = !(xe != nullptr && xe[0] == '0');
-  int XM_ = (pre && xcd_on && xgrp_fits(UB, BT, num_dirs)) ? 1 : 0;
+  int XM_ = xcd_groups(UB, BT, num_dirs) ? 1 : 0;
   const int grid = XM_ ? xgrp_grid(UB, BT, num_dirs) : mapped_grid(UB * num_dirs, BT);
   int T_ = t_max, N_ = n, H_ = h, D_ = num_dirs, UB_ = UB, BT_ = BT, DYD_ = dy_dirs;
   void* args[] = {&T_, &N_, &H_, &D_, &UB_, &BT_, &dy, &DYD_, &w_hh_f, &w_hh_r, &h_all,
                   &gates, &lens, &dgates_x, &dgates_h, &ring, &ctrs, &err, &stamps, &dbp, &XM_};
-  return rnn_launch(fn, dim3(grid), dim3(nw * 64), args, lds_pad, st) == hipSuccess;
+  return rnn_launch(fn, dim3(grid), dim3(BW * 64), args, lds_pad, st) == hipSuccess;
 }
 
 }  // namespace ds2

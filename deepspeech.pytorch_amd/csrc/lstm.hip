@@ -258,7 +258,7 @@ __global__ __launch_bounds__(GT) void lstm_fwd_persist_kernel(
     const float* __restrict__ wp, const float* __restrict__ b_f, const float* __restrict__ b_r,
     const int* __restrict__ lens, float* __restrict__ h_all, float* __restrict__ c_all,
     float* __restrict__ gates, unsigned* __restrict__ counters, unsigned* __restrict__ err,
-    int use_flags, int n_base) {
+    int n_base) {
   constexpr int PITCH = LKC_FWD + 4;
   constexpr int RB = GB * BTS;         // samples per workgroup
   constexpr int HSF = RB * PITCH, REDF = GW * RB * LRP;
@@ -274,7 +274,6 @@ __global__ __launch_bounds__(GT) void lstm_fwd_persist_kernel(
   const int KS = H / 4;                    // host guarantees H % 4 == 0, GW * KSW >= KS
   const int a_ks = wave * KSW;
   const int b_ks = min(KS, a_ks + KSW);
-  unsigned* ctr = counters + d * BT + bt;
   unsigned* gflags = counters + (D * BT + 1) + (d * BT + bt) * UB;   // flag variant
   const __amdgpu_buffer_rsrc_t h_rs = __builtin_amdgcn_make_buffer_rsrc(
       h_all, (short)0, T * N * D * H * 4, 0x00020000);
@@ -324,8 +323,7 @@ __global__ __launch_bounds__(GT) void lstm_fwd_persist_kernel(
 #pragma unroll
       for (int g = 0; g < 4; ++g) acc[b][g] = f32x4{0.f, 0.f, 0.f, 0.f};
     if (s > 0) {
-      if (!(use_flags ? flags_wait(gflags, UB, (unsigned)s, err, &flag)
-                      : group_wait(ctr, (unsigned)s * UB, err, &flag))) {
+      if (!flags_wait(gflags, UB, (unsigned)s, err, &flag)) {
         poison_rest(h_all, s, T, d != 0, N, D, n, d, H, j, H, 1, owner);
         return;
       }
@@ -372,8 +370,7 @@ __global__ __launch_bounds__(GT) void lstm_fwd_persist_kernel(
       prev = o;
       prev_row = row;
     }
-    if (use_flags) flags_arrive(gflags + ub, (unsigned)s + 1);
-    else group_arrive(ctr);
+    flags_arrive(gflags + ub, (unsigned)s + 1);
     // backward-only caches, off the critical path
     if (owner) {
       if (c_all != nullptr) c_all[prev_row * H + j] = prev.c;
@@ -396,7 +393,7 @@ __global__ __launch_bounds__(GT) void lstm_bwd_persist_kernel(
     int T, int N, int H, int D, int UB, int BT, const float* __restrict__ dy, int dyd,
     const float* __restrict__ wpt, const float* __restrict__ c_all,
     const float* __restrict__ gates, const int* __restrict__ lens, float* __restrict__ dg,
-    unsigned* __restrict__ counters, unsigned* __restrict__ err, int use_flags, int n_base) {
+    unsigned* __restrict__ counters, unsigned* __restrict__ err, int n_base) {
   constexpr int CW = 4 * GW * KSWC;         // gate columns per chunk (<= LKC_BWD)
   constexpr int PITCH = CW + 4;
   constexpr int RB = GB * BTS;              // samples per workgroup
@@ -410,7 +407,6 @@ __global__ __launch_bounds__(GT) void lstm_bwd_persist_kernel(
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int H4 = 4 * H;
   const int KS = H;
-  unsigned* ctr = counters + d * BT + bt;
   unsigned* gflags = counters + (D * BT + 1) + (d * BT + bt) * UB;   // flag variant
   const __amdgpu_buffer_rsrc_t g_rs = __builtin_amdgcn_make_buffer_rsrc(
       dg, (short)0, T * N * D * H4 * 4, 0x00020000);
@@ -460,8 +456,7 @@ __global__ __launch_bounds__(GT) void lstm_bwd_persist_kernel(
     }
     if (s > 0) {
       const int tq = d == 0 ? t + 1 : t - 1;
-      if (!(use_flags ? flags_wait(gflags, UB, (unsigned)s, err, &flag)
-                      : group_wait(ctr, (unsigned)s * UB, err, &flag))) {
+      if (!flags_wait(gflags, UB, (unsigned)s, err, &flag)) {
         poison_rest(dg, s, T, d == 0, N, D, n, d, H, j, H4, 4, owner);
         return;
       }
@@ -520,8 +515,7 @@ __global__ __launch_bounds__(GT) void lstm_bwd_persist_kernel(
       __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, dao), g_rs, o + 12 * H, 0,
                                             kSc1);
     }
-    if (use_flags) flags_arrive(gflags + ub, (unsigned)s + 1);
-    else group_arrive(ctr);
+    flags_arrive(gflags + ub, (unsigned)s + 1);
   }
 }
 
@@ -532,8 +526,9 @@ __global__ __launch_bounds__(GT) void lstm_bwd_persist_kernel(
 // stored by wave 0 with one 16-B sc1 store per lane; every consumer wave loads the tiles of
 // its own producers straight into its A operands (lane (r, q): the k values 16 blk + 4 q +
 // 0..3 of sample r), so no LDS staging of h and no barrier stands between the loads and
-// the MFMAs.  HM as in gru.hip (0 flags, 1 sentinel ring, 2 hybrid); BTS as in
-// lstm_fwd_persist_kernel.  h_all, c_all and the gate cache are written after the publish.
+// the MFMAs.  HM: 1 the sentinel ring of gru_fwd_dop_kernel, 0 per-producer flags (the 8-tile
+// shapes, H > 512: W_hh's 128 fragment registers leave no room for the sentinel spin's live
+// state); BTS as in lstm_fwd_persist_kernel.  h_all, c_all and the gate cache are written after the publish.
 template <int NBW, int HM, int BTS>
 __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void lstm_fwd_dop_kernel(
     int T, int N, int H, int D, int UB, int BT, const float* __restrict__ xproj,
@@ -556,8 +551,9 @@ __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   const unsigned* gflags = counters + (D * BT + 1) + (d * BT + bt) * UB;
   unsigned* myflag = counters + (D * BT + 1) + (d * BT + bt) * UB + ub;
   const int slot_floats = D * BT * BTS * UB * 256;
-  constexpr bool SENT = HM != 0;
-  constexpr bool FLAG = HM != 1;
+  static_assert(HM == 0 || HM == 1, "hand-off form");
+  constexpr bool SENT = HM == 1;
+  constexpr bool FLAG = HM == 0;
   constexpr int NSLOT = SENT ? kRingSlots : 2;
   const __amdgpu_buffer_rsrc_t x_rs =
       __builtin_amdgcn_make_buffer_rsrc(hx, (short)0, NSLOT * slot_floats * 4, 0x00020000);
@@ -708,8 +704,6 @@ __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
           __builtin_amdgcn_raw_buffer_store_b128(sv, x_rs, ((s + 2) % NSLOT) * slot_floats * 4 + toff,
                                                  0, kSc1);
         }
-        if (FLAG && lane == 0)
-          __hip_atomic_store(myflag, (unsigned)s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (lane == 0)
@@ -727,164 +721,6 @@ __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
         gp[2 * H + j] = prev.g;
         gp[3 * H + j] = prev.o;
       }
-    }
-  }
-}
-
-// Direct-operand persistent backward (H % 16 == 0, per-producer flags): the form of
-// gru_bwd_dop_kernel over K = 4H.  Each producer publishes its gate gradients (dai, daf,
-// dag, dao) as four 1-KB transposed tiles, tile g * UB + ub of the two-slot ring
-//   gx[slot][d][bt][4 UB blocks][q][r][c],
-// whose block order is the k order of dgates; wave w owns blocks [b0, b0 + nb) of the 4 UB
-// and loads them in groups of 8 tiles straight into its A operands, two groups in flight
-// (W_hh^T's fragments already hold 128 registers at H = 1024).  dgates is stored after the
-// flag.
-template <int NBW>
-__global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void lstm_bwd_dop_kernel(
-    int T, int N, int H, int D, int UB, int BT, const float* __restrict__ dy, int dyd,
-    const float* __restrict__ w_f, const float* __restrict__ w_r, const float* __restrict__ c_all,
-    const float* __restrict__ gates, const int* __restrict__ lens, float* __restrict__ dg,
-    float* __restrict__ gx, unsigned* __restrict__ counters, unsigned* __restrict__ err,
-    int n_base) {
-  constexpr int RP = GU + 1;
-  constexpr int GRP = 8;                         // tiles per load group
-  constexpr int NG = NBW / GRP;                  // NBW is a multiple of GRP
-  __shared__ float red[GW * GB * RP];
-  __shared__ __attribute__((aligned(16))) float tile[4 * GB * GU];
-  __shared__ int flag;
-  int ub, d, bt;
-  if (!map_work(UB * D, BT, UB, ub, d, bt)) return;
-  const int n0 = n_base + bt * GB;
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int H4 = 4 * H;
-  const int NB4 = 4 * UB;
-  int b0, nb;
-  simd_split(NB4, wave, b0, nb);                 // host guarantees nb <= NBW
-  const unsigned* gflags = counters + (D * BT + 1) + (d * BT + bt) * UB;
-  unsigned* myflag = counters + (D * BT + 1) + (d * BT + bt) * UB + ub;
-  const int slot_floats = D * BT * NB4 * 256;
-  const __amdgpu_buffer_rsrc_t x_rs =
-      __builtin_amdgcn_make_buffer_rsrc(gx, (short)0, 2 * slot_floats * 4, 0x00020000);
-  const int grp_off = (d * BT + bt) * NB4 * 256;
-
-  // W_hh^T fragments: w[i][c] = W_hh[16 (b0 + i) + 4 (lane >> 4) + c][ub 16 + (lane & 15)]
-  f32x4 w[NBW];
-  {
-    const float* W = d == 0 ? w_f : w_r;
-    const float* wc = W + (int64_t)(16 * b0 + 4 * (lane >> 4)) * H + ub * GU + (lane & 15);
-#pragma unroll
-    for (int i = 0; i < NBW; ++i)
-#pragma unroll
-      for (int c = 0; c < 4; ++c) w[i][c] = i < nb ? wc[(int64_t)(16 * i + c) * H] : 0.f;
-#pragma unroll
-    for (int i = 0; i < NBW; ++i) settle(w[i]);
-  }
-  const int m = threadIdx.x >> 4;
-  const int u = threadIdx.x & 15;
-  const int n = n0 + m;
-  const int j = ub * GU + u;
-  const bool owner = threadIdx.x < GB * GU && n < N;
-  int len = owner ? lens[n] : 0;
-  settle(len);
-  const int tpos = ((u >> 2) * GB + m) * 4 + (u & 3);
-  float carry = 0.f;
-  for (int s = 0; s < T; ++s) {
-    const int t = d == 0 ? T - 1 - s : s;
-    const int64_t row = ((int64_t)t * N + n) * D + d;
-    // inputs of this step that do not depend on other workgroups: issue first
-    float dyv = 0.f, gi = 0.f, gf = 0.f, gg = 0.f, go = 0.f, cc = 0.f, cp = 0.f;
-    if (owner && t < len) {
-      dyv = dy[(((int64_t)t * N + n) * dyd + (dyd > 1 ? d : 0)) * H + j];
-      const float* gp = gates + row * 4 * H;
-      gi = gp[j];
-      gf = gp[H + j];
-      gg = gp[2 * H + j];
-      go = gp[3 * H + j];
-      cc = c_all[row * H + j];
-      const int tp = d == 0 ? t - 1 : t + 1;
-      if (tp >= 0 && tp < T) cp = c_all[(((int64_t)tp * N + n) * D + d) * H + j];
-    }
-    f32x4 acc0 = f32x4{0.f, 0.f, 0.f, 0.f};
-    f32x4 acc1 = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (s > 0) {
-      if (!flags_wait(gflags, UB, (unsigned)s, err, &flag)) {
-        poison_rest(dg, s, T, d == 0, N, D, n, d, H, j, H4, 4, owner);
-        return;
-      }
-      const int base = ((((s - 1) & 1) * slot_floats + grp_off + b0 * 256 + lane * 4) * 4);
-      f32x4 ga[GRP], gb[GRP];
-      auto load_group = [&](f32x4 (&dst)[GRP], int g) {
-#pragma unroll
-        for (int k = 0; k < GRP; ++k) {
-          const int i = g * GRP + k;
-          const int off = i < nb ? base + i * 1024 : 0x7ffffff0;
-          dst[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(x_rs, off, 0, kSc1));
-        }
-      };
-      load_group(ga, 0);
-      if (NG > 1) load_group(gb, 1);
-#pragma unroll
-      for (int g = 0; g < NG; ++g) {
-        f32x4 (&cur)[GRP] = (g & 1) ? gb : ga;
-#pragma unroll
-        for (int k = 0; k < GRP; ++k) {
-          const int i = g * GRP + k;
-          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(cur[k][0], w[i][0], acc0, 0, 0, 0);
-          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(cur[k][1], w[i][1], acc1, 0, 0, 0);
-          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(cur[k][2], w[i][2], acc0, 0, 0, 0);
-          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(cur[k][3], w[i][3], acc1, 0, 0, 0);
-        }
-        if (g + 2 < NG) load_group(cur, g + 2);
-      }
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-      red[(wave * GB + (lane >> 4) * 4 + r) * RP + (lane & 15)] = acc0[r] + acc1[r];
-    settle(dyv);
-    settle(gi);
-    settle(gf);
-    settle(gg);
-    settle(go);
-    settle(cc);
-    settle(cp);
-    __syncthreads();
-    float dai = 0.f, daf = 0.f, dag = 0.f, dao = 0.f;
-    if (owner) {
-      if (t < len) {
-        float rec = 0.f;
-#pragma unroll
-        for (int w8 = 0; w8 < GW; ++w8) rec += red[(w8 * GB + m) * RP + u];
-        carry = lstm_cell_bwd(dyv + rec, carry, gi, gf, gg, go, cc, cp, dai, daf, dag, dao);
-      } else {
-        carry = 0.f;
-      }
-    }
-    if (threadIdx.x < GB * GU) {
-      tile[tpos] = dai;
-      tile[GB * GU + tpos] = daf;
-      tile[2 * GB * GU + tpos] = dag;
-      tile[3 * GB * GU + tpos] = dao;
-    }
-    __syncthreads();
-    if (wave == 0) {
-      const int so = ((s & 1) * slot_floats + grp_off + ub * 256 + lane * 4) * 4;
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const u32x4 v = *reinterpret_cast<const u32x4*>(tile + g * GB * GU + lane * 4);
-        __builtin_amdgcn_raw_buffer_store_b128(v, x_rs, so + g * UB * 1024, 0, kSc1);
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (lane == 0)
-        __hip_atomic_store(myflag, (unsigned)s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    // dgates feeds only later kernels: stored after the flag
-    if (owner) {
-      float* o = dg + row * H4 + j;
-      o[0] = dai;
-      o[H] = daf;
-      o[2 * H] = dag;
-      o[3 * H] = dao;
     }
   }
 }
@@ -908,10 +744,6 @@ static inline size_t lstm_counter_bytes(int n, int num_dirs) {
   const size_t groups = (size_t)num_dirs * ((n + GB - 1) / GB);
   return align256((groups + 1 + groups * 64) * sizeof(unsigned));
 }
-static inline int lstm_flags_mode() {
-  const char* e = getenv("DS2_RNN_FLAGS");
-  return !(e != nullptr && e[0] == '0');
-}
 
 // Batch chunking of the persistent launches: the largest number of 16-sample tiles per
 // launch whose grid fits the chip (one workgroup per CU); a batch with more tiles runs as
@@ -925,13 +757,9 @@ static inline int lstm_chunk_tiles(int UB, int D, int BT) {
 
 // 16-sample tiles per workgroup of the persistent kernels (template BTS): 2 when the
 // batch's 16-sample tiles would not fit the chip one workgroup each but its 32-sample
-// tiles do -- one launch per layer instead of consecutive batch chunks.  DS2_LSTM_BTS=1|2
-// forces the choice (2 wherever 32-sample workgroups fit; used by the tests).
+// tiles do -- one launch per layer instead of consecutive batch chunks.
 static inline int lstm_bts(int UB, int D, int BT) {
   const bool fits2 = mapped_grid(UB * D, (BT + 1) / 2) <= num_cus();
-  const char* e = getenv("DS2_LSTM_BTS");
-  if (e != nullptr && e[0] == '1') return 1;
-  if (e != nullptr && e[0] == '2') return fits2 ? 2 : 1;
   return mapped_grid(UB * D, BT) > num_cus() && fits2 ? 2 : 1;
 }
 
@@ -942,18 +770,6 @@ static inline size_t lstm_ring_bytes(int n, int h, int num_dirs) {
   return align256(kRingSlots * (size_t)num_dirs * BT2 * UB * 256 * sizeof(float));
 }
 constexpr unsigned kLstmDopPadLds = 80 * 1024;   // dynamic LDS: one workgroup per CU
-static bool lstm_dop_enabled() {
-  const char* e = getenv("DS2_LSTM_DOP");
-  return !(e != nullptr && e[0] == '0');
-}
-// hand-off form of the direct-operand forward (the variables of gru.hip's handoff_mode):
-// 0 flags, 1 sentinel ring (default), 2 hybrid
-static int lstm_handoff_mode() {
-  const char* e = getenv("DS2_RNN_HANDOFF_FWD");
-  if (e == nullptr || e[0] == 0) e = getenv("DS2_RNN_HANDOFF");
-  if (e == nullptr || e[0] == 0) return 1;
-  return e[0] == 's' ? 1 : (e[0] == 'h' ? 2 : 0);
-}
 
 size_t ds2_lstm_fwd_workspace_size(int n, int h, int num_dirs) {
   const int64_t UB = (h + GU - 1) / GU;
@@ -999,9 +815,9 @@ ds2_status_t ds2_lstm_fwd(int t_max, int n, int h, int num_dirs, const float* xp
   float* ring = reinterpret_cast<float*>(static_cast<char*>(ws) + off +
                                          lstm_counter_bytes(n, num_dirs));
   // direct-operand persistent kernels (W_hh read unpacked; no LDS staging of h)
-  if (lstm_dop_enabled() && persistent_enabled() && (h % GU) == 0 && UB <= 8 * GW &&
+  if (persistent_enabled() && (h % GU) == 0 && UB <= 8 * GW &&
       (int64_t)t_max * n * num_dirs * h * 4 < (1ll << 31)) {
-    int hm = lstm_handoff_mode();
+    int hm = 1;   // the sentinel ring
     const int bts = lstm_bts(UB, num_dirs, BT);
     const int BTW = (BT + bts - 1) / bts;
     const int ct = lstm_chunk_tiles(UB, num_dirs, BTW);
@@ -1015,12 +831,8 @@ ds2_status_t ds2_lstm_fwd(int t_max, int n, int h, int num_dirs, const float* xp
     const void* fn = nullptr;
 #define DS2_LDOP(K)                                                                          \
   case K:                                                                                    \
-    fn = bts == 2 ? (hm == 1 ? reinterpret_cast<const void*>(lstm_fwd_dop_kernel<K, 1, 2>)   \
-                  : hm == 2 ? reinterpret_cast<const void*>(lstm_fwd_dop_kernel<K, 2, 2>)   \
-                            : reinterpret_cast<const void*>(lstm_fwd_dop_kernel<K, 0, 2>))  \
-                  : (hm == 1 ? reinterpret_cast<const void*>(lstm_fwd_dop_kernel<K, 1, 1>)   \
-                  : hm == 2 ? reinterpret_cast<const void*>(lstm_fwd_dop_kernel<K, 2, 1>)   \
-                            : reinterpret_cast<const void*>(lstm_fwd_dop_kernel<K, 0, 1>)); \
+    fn = bts == 2 ? reinterpret_cast<const void*>(lstm_fwd_dop_kernel<K, 1, 2>)              \
+                  : reinterpret_cast<const void*>(lstm_fwd_dop_kernel<K, 1, 1>);             \
     break;
     switch (nbw) {
       DS2_LDOP(1) DS2_LDOP(2) DS2_LDOP(4)
@@ -1075,12 +887,12 @@ ds2_status_t ds2_lstm_fwd(int t_max, int n, int h, int num_dirs, const float* xp
     bool ok = fn != nullptr;
     for (int b0 = 0; ok && b0 < BTW; b0 += ct) {
       int T_ = t_max, N_ = n, H_ = h, D_ = num_dirs, UB_ = UB, BT_ = std::min(ct, BTW - b0);
-      int flags_ = lstm_flags_mode(), NB_ = b0 * GB * bts;
+      int NB_ = b0 * GB * bts;
       unsigned* err = ctrs + num_dirs * BT_;
       if (hipMemsetAsync(ctrs, 0, lstm_counter_bytes(n, num_dirs), st) != hipSuccess)
         return launch_status("ds2_lstm counters");
       void* args[] = {&T_, &N_, &H_, &D_, &UB_, &BT_, &xproj, &wp, &b_hh_f, &b_hh_r, &lens,
-                      &h_all, &c_all, &gates, &ctrs, &err, &flags_, &NB_};
+                      &h_all, &c_all, &gates, &ctrs, &err, &NB_};
       ok = rnn_launch(fn, dim3(mapped_grid(UB * num_dirs, BT_)), dim3(GT), args,
                                       0, st) == hipSuccess;
       if (ok) fold_err(err, err_out, st);
@@ -1097,19 +909,12 @@ ds2_status_t ds2_lstm_fwd(int t_max, int n, int h, int num_dirs, const float* xp
   return launch_status("ds2_lstm_fwd");
 }
 
-// two-slot ring of the direct-operand backward: 4 gate tiles per (direction, batch tile,
-// unit block)
-static inline size_t lstm_bwd_ring_bytes(int n, int h, int num_dirs) {
-  const size_t UB = (h + GU - 1) / GU, BT = ((size_t)n + GB - 1) / GB;
-  return align256(2 * (size_t)num_dirs * BT * 4 * UB * 256 * sizeof(float));
-}
-
 size_t ds2_lstm_bwd_workspace_size(int n, int h, int num_dirs) {
   const int64_t UB = (h + GU - 1) / GU;
   const int64_t KS = h;
   return align256((size_t)(num_dirs * UB * KS * 64) * sizeof(float)) +
          align256((size_t)2 * n * num_dirs * h * sizeof(float)) + lstm_counter_bytes(n, num_dirs) +
-         lstm_bwd_ring_bytes(n, h, num_dirs) + 256;
+         256;
 }
 
 #define DS2_LBWD_CASE(K)                                                                    \
@@ -1155,42 +960,6 @@ ds2_status_t ds2_lstm_bwd(int t_max, int n, int h, int num_dirs, const float* dy
   float* dcs = reinterpret_cast<float*>(static_cast<char*>(ws) + off);
   off += align256((size_t)2 * n * num_dirs * h * sizeof(float));
   unsigned* ctrs = reinterpret_cast<unsigned*>(static_cast<char*>(ws) + off);
-  // direct-operand persistent backward (W_hh read unpacked; no LDS staging of dgates):
-  // opt-in (DS2_LSTM_DOP_BWD=1) -- at cfg4's H = 1024 each workgroup loads 256 KB of 1-KB
-  // tiles per step, and with two 8-tile groups in flight it measured slower than the
-  // LDS-staged kernel (cfg4 step 276 vs 263 ms)
-  const char* dop_bwd = getenv("DS2_LSTM_DOP_BWD");
-  if (dop_bwd != nullptr && dop_bwd[0] == '1' && lstm_dop_enabled() && persistent_enabled() &&
-      (h % GU) == 0 &&
-      (int64_t)t_max * n * num_dirs * 4 * h * 4 < (1ll << 31)) {
-    float* ring = reinterpret_cast<float*>(reinterpret_cast<char*>(ctrs) +
-                                           lstm_counter_bytes(n, num_dirs));
-    const int need = (4 * UB + GW - 1) / GW;       // blocks per wave (simd_split bound)
-    const void* fn = nullptr;
-    if (need <= 8) fn = reinterpret_cast<const void*>(lstm_bwd_dop_kernel<8>);
-    else if (need <= 16) fn = reinterpret_cast<const void*>(lstm_bwd_dop_kernel<16>);
-    else if (need <= 24) fn = reinterpret_cast<const void*>(lstm_bwd_dop_kernel<24>);
-    else if (need <= 32) fn = reinterpret_cast<const void*>(lstm_bwd_dop_kernel<32>);
-    const int ct = lstm_chunk_tiles(UB, num_dirs, BT);
-    bool ok = fn != nullptr && mapped_grid(UB * num_dirs, ct) <= num_cus();
-    bool launched = false;
-    for (int b0 = 0; ok && b0 < BT; b0 += ct) {
-      int T_ = t_max, N_ = n, H_ = h, D_ = num_dirs, UB_ = UB, BT_ = std::min(ct, BT - b0);
-      int DYD_ = dy_dirs, NB_ = b0 * GB;
-      unsigned* err = ctrs + num_dirs * BT_;
-      if (hipMemsetAsync(ctrs, 0, lstm_counter_bytes(n, num_dirs), st) != hipSuccess)
-        return launch_status("ds2_lstm counters");
-      void* args[] = {&T_, &N_, &H_, &D_, &UB_, &BT_, &dy, &DYD_, &w_hh_f, &w_hh_r, &c_all,
-                      &gates, &lens, &dgates, &ring, &ctrs, &err, &NB_};
-      ok = rnn_launch(fn, dim3(mapped_grid(UB * num_dirs, BT_)), dim3(GT), args,
-                                      kLstmDopPadLds, st) == hipSuccess;
-      if (ok) fold_err(err, err_out, st);
-      if (!ok && launched) return launch_status("ds2_lstm_bwd chunk");
-      launched = launched || ok;
-    }
-    if (ok) return launch_status("ds2_lstm_bwd");
-    (void)hipGetLastError();
-  }
   hipLaunchKernelGGL(pack_bwd_kernel<4>, dim3(grid_cap((int64_t)num_dirs * UB * KS * 64)),
                      dim3(256), 0, st, w_hh_f, w_hh_r, h, num_dirs, UB, KS, wpt);
   const int grid = mapped_grid(UB * num_dirs, BT);
@@ -1228,12 +997,12 @@ ds2_status_t ds2_lstm_bwd(int t_max, int n, int h, int num_dirs, const float* dy
     bool ok = fn != nullptr && mapped_grid(UB * num_dirs, ct) <= num_cus();
     for (int b0 = 0; ok && b0 < BTW; b0 += ct) {
       int T_ = t_max, N_ = n, H_ = h, D_ = num_dirs, UB_ = UB, BT_ = std::min(ct, BTW - b0);
-      int DYD_ = dy_dirs, flags_ = lstm_flags_mode(), NB_ = b0 * GB * bts;
+      int DYD_ = dy_dirs, NB_ = b0 * GB * bts;
       unsigned* err = ctrs + num_dirs * BT_;
       if (hipMemsetAsync(ctrs, 0, lstm_counter_bytes(n, num_dirs), st) != hipSuccess)
         return launch_status("ds2_lstm counters");
       void* args[] = {&T_, &N_, &H_, &D_, &UB_, &BT_, &dy, &DYD_, &wpt, &c_all, &gates, &lens,
-                      &dgates, &ctrs, &err, &flags_, &NB_};
+                      &dgates, &ctrs, &err, &NB_};
       ok = rnn_launch(fn, dim3(mapped_grid(UB * num_dirs, BT_)), dim3(GT), args,
                                       0, st) == hipSuccess;
       if (ok) fold_err(err, err_out, st);

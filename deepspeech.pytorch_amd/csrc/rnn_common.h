@@ -129,11 +129,11 @@ __device__ __forceinline__ unsigned xcc_id() {
 // workgroups of a (direction, batch tile) group follows the write-through form
 // of MI355X_MICROARCH.md "Valid forms" row 1: payload stored sc1 (agent-scope
 // relaxed atomic stores), every storing wave drains vmcnt, workgroup barrier,
-// one lane adds to the group's arrival counter (agent atomic); consumers poll
-// that counter relaxed (one lane, s_sleep, bounded), barrier, then load the
-// payload with sc1 (agent-scope relaxed atomic) loads.  Counters are zeroed by
-// a hipMemsetAsync before every launch; a spin that exceeds its bound sets the
-// error word and the workgroup leaves (no hang, results invalid).
+// one lane stores the producer's step count to its flag (sc1); consumers poll
+// the group's flags relaxed (one wave, s_sleep, bounded), barrier, then load the
+// payload with sc1 loads -- or the sentinel ring below, where the data is the flag.
+// Flags are zeroed by a hipMemsetAsync before every launch; a spin that exceeds its
+// bound sets the error word and the workgroup leaves (no hang, results invalid).
 constexpr unsigned kSpinLimit = 1u << 21;
 
 // The bound the kernels use: kSpinLimit unless DS2_RNN_SPIN_LIMIT is set in the environment
@@ -210,30 +210,6 @@ __device__ __forceinline__ float ld_sc1(const float* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// thread 0 waits until *ctr >= target; returns false (for the whole workgroup) on timeout
-__device__ __forceinline__ bool group_wait(unsigned* ctr, unsigned target, unsigned* err,
-                                           int* lds_flag) {
-  if (threadIdx.x == 0) {
-    unsigned spins = 0;
-    int ok = 1;
-    if (g_spin_limit == 0) {   // fault injection
-      __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      ok = 0;
-    }
-    while (ok && __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-      __builtin_amdgcn_s_sleep(2);
-      if (++spins > g_spin_limit || __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-        __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        ok = 0;
-        break;
-      }
-    }
-    *lds_flag = ok;
-  }
-  __syncthreads();
-  return *lds_flag != 0;
-}
-
 // Per-producer flag variant of the hand-off (same valid form, row 1: one lane of each
 // storing workgroup publishes with an sc1 store; the consumer polls every shard).  The
 // group's UB flags sit in one or two cache lines; wave 0 polls them with one vector sc1
@@ -302,12 +278,6 @@ __device__ __forceinline__ void flags_arrive(unsigned* flag, unsigned value) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains first
   __syncthreads();
   if (threadIdx.x == 0) __hip_atomic_store(flag, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-__device__ __forceinline__ void group_arrive(unsigned* ctr) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains first
-  __syncthreads();
-  if (threadIdx.x == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -429,34 +399,27 @@ static bool persistent_enabled() {
   return !(e != nullptr && e[0] == '0');
 }
 
-// Launch of a persistent recurrence kernel.  The host has already sized the grid to the
-// chip (grid <= CUs, one workgroup per CU through its LDS footprint), so a cooperative launch
-// would add only the runtime's occupancy check (and 15-20 us of host time per launch;
-// residency is the same for plain and cooperative launches, MI355X_MICROARCH.md "Residency
-// and cooperative launch").  Plain launches are the default: a process that had made one
-// hipLaunchCooperativeKernel died with SIGSEGV at exit under rocprofv3 (inside
-// libhsa-runtime64, called from the HIP runtime's exit handler, on a /dev/dri doorbell
-// mapping; scripts/prof_exit_probe2.sh: one cooperative GRU launch reproduces it, the same
-// launch made plainly exits 0), and the step time is unchanged (profiles/r3g_coop_ab.txt).
-// DS2_RNN_COOP=1 selects cooperative launches.
+// Launch of a persistent recurrence kernel: a plain launch.  The host has already sized the
+// grid to the chip (grid <= CUs, one workgroup per CU through its LDS footprint), so a
+// cooperative launch would add only the runtime's occupancy check (and 15-20 us of host time
+// per launch; residency is the same for plain and cooperative launches, MI355X_MICROARCH.md
+// "Residency and cooperative launch").  Cooperative launches were also the cause of round 2's
+// rocprofv3 exit SIGSEGV (scripts/prof_exit_probe2.sh) and were removed.  What a concurrent
+// collective may take is budgeted by optim.GradAllReducer.guard_cooperative
+// (tests/test_gpu_residency.py).
 // `lds` is a dynamic-LDS pad that keeps one workgroup per CU; a kernel whose static LDS
 // already takes more than half the CU's LDS gets less pad, so static + pad never exceeds the
 // per-workgroup limit (a dispatch over it faulted: the pre-split sentinel backward's 94 KB of
-// static LDS + the 80 KB pad).
+// static LDS + the 80 KB pad; pinned by ds2_test_rnn_launch_lds).
 static inline hipError_t rnn_launch(const void* fn, dim3 grid, dim3 block, void** args,
                                     size_t lds, hipStream_t st) {
-  static const int coop = [] {
-    const char* e = getenv("DS2_RNN_COOP");
-    return (e != nullptr && e[0] == '1') ? 1 : 0;
-  }();
   constexpr size_t max_lds = 160 * 1024;   // gfx950: LDS per CU = per workgroup maximum
   hipFuncAttributes fa;
   if (hipFuncGetAttributes(&fa, fn) != hipSuccess) return hipErrorInvalidDeviceFunction;
   const size_t stat = fa.sharedSizeBytes;
   if (stat > max_lds) return hipErrorInvalidValue;
   if (stat + lds > max_lds) lds = max_lds - stat;
-  return coop ? hipLaunchCooperativeKernel(fn, grid, block, args, lds, st)
-              : hipLaunchKernel(fn, grid, block, args, lds, st);
+  return hipLaunchKernel(fn, grid, block, args, lds, st);
 }
 
 static inline int grid_cap(int64_t work) {
@@ -465,45 +428,5 @@ static inline int grid_cap(int64_t work) {
 }
 
 static inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
-
-// ---------------------------------------------------------------------------------------
-// GRU backward coefficient tiles (the part of the gate cache after the [T][N][D][4H] gates,
-// ds2_gru_cache_floats).  The backward's gate gradients are the step's dh times per-element
-// coefficients that the forward already knows:
-//   dan  = dh * c_n,  c_n  = (1 - z)(1 - n^2)          dar  = dh * c_r,  c_r  = c_n hn r (1 - r)
-//   daz  = dh * c_z,  c_z  = (h_prev - n) z (1 - z)    dghn = dh * c_hn, c_hn = c_n r
-// so the recurrence can exchange dh (H per sample) instead of (dar, daz, dghn) (3H) and every
-// consumer forms its MFMA A operands as dh x c.  Tiles of 16 units x 16 samples in the hand-off
-// tile order (tpos), one per (t, direction, batch tile, g in {c_r, c_z, c_hn}, unit block):
-//   coef[t][d][bt][g][ub][256]
-constexpr int kCoefPlanes = 3;
-
-__device__ __forceinline__ int64_t coef_tile(int t, int d, int bt, int g, int ub, int D, int BT,
-                                             int UB) {
-  return ((((int64_t)t * D + d) * BT + bt) * kCoefPlanes + g) * UB + ub;
-}
-
-// c_r, c_z, c_hn of one element (0 past the sequence end: t >= len)
-__device__ __forceinline__ void gru_coefs(float r, float z, float n, float hn, float hp,
-                                          float& cr, float& cz, float& chn) {
-  const float cn = (1.f - z) * (1.f - n * n);
-  cr = cn * hn * r * (1.f - r);
-  cz = (hp - n) * z * (1.f - z);
-  chn = cn * r;
-}
-
-// the dh-exchange backward is opt-in (DS2_GRU_BWD=dh): measured slower than the gate
-// exchange (gru_bwd_dh.hip header), so by default the forward writes no coefficient tiles and
-// the gate cache is the classic [T][N][D][4H]
-static inline bool gru_dh_bwd_opted_in() {
-  const char* e = getenv("DS2_GRU_BWD");
-  return e != nullptr && e[0] == 'd' && e[1] == 'h';
-}
-
-static inline size_t gru_coef_floats(int t, int n, int h, int d) {
-  const size_t BT = (n + GB - 1) / GB, UB = (h + GU - 1) / GU;
-  return (size_t)t * d * BT * kCoefPlanes * UB * 256;
-}
-
 
 }  // namespace ds2

@@ -104,11 +104,9 @@ class Trainer:
         self.model = model.to(self.device)
         self.model.train()
         # both directions' W_ih of a bidirectional recurrent layer back to back: one GEMM
-        # per layer for the input projection, dX and dW_ih (ops._stacked_rows);
-        # DS2_RNN_STACK=0 keeps the per-direction GEMMs (diagnostic)
-        pairs = [] if os.environ.get("DS2_RNN_STACK", "1")[:1] == "0" else [
-            (m.weight_ih_l0, m.weight_ih_l0_reverse) for m in self.model.modules()
-            if hasattr(m, 'weight_ih_l0_reverse')]
+        # per layer for the input projection, dX and dW_ih (ops._stacked_rows)
+        pairs = [(m.weight_ih_l0, m.weight_ih_l0_reverse) for m in self.model.modules()
+                 if hasattr(m, 'weight_ih_l0_reverse')]
         self.flat = FlatParams(list(self.model.parameters()), self.device, adjacent=pairs)
         self.optimizer = FusedSGD(self.flat, lr=lr, momentum=momentum, max_norm=max_norm)
         # DS2_ALLREDUCE=ds2: the buckets go through the library's own RCCL communicator

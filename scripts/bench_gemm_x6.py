@@ -4,7 +4,7 @@ T' = 501: TN = 16032 rows).  Error = max |C - C_fp64| / max |C_fp64| for both ke
 the fp64 product computed by torch on the device.  Prints TFLOP/s and the fraction of the
 fp32-equivalent peak each kernel runs against (fp32 MFMA 157.3 TF; bf16x6 2516.6 / 6 TF).
 
-usage: python scripts/bench_gemm_x6.py   (DS2_GEMM_X6: 1 = 256 x 128 kernel, 2 = 128 x 128, 0 = fp32)
+usage: python scripts/bench_gemm_x6.py
 """
 import os
 import sys
@@ -54,10 +54,8 @@ def main():
         ref = torch.mm(at.double(), bt.double())
         scale = ref.abs().max().item()
         line = f"{name:12s} {m:6d}x{n:5d}x{k:6d} |"
-        for tag, env, peak in (("x6", "1", PEAKX6), ("x6-bn128", "1/128", PEAKX6),
-                               ("x6-bn160", "1/160", PEAKX6), ("fp32", "0", PEAK32)):
-            os.environ["DS2_GEMM_X6"] = env.split("/")[0]
-            os.environ["DS2_GEMM_X6_BN"] = env.split("/")[1] if "/" in env else ""
+        for tag, env, peak in (("x6", "1", PEAKX6), ("fp32", "0", PEAK32)):
+            os.environ["DS2_GEMM_X6"] = env
             t = timeit(lambda: ops.sgemm(a, b, c, **kw))
             err = (c.double() - ref).abs().max().item() / scale
             tf = fl / t / 1e9

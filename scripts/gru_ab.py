@@ -1,7 +1,7 @@
 """A/B timing of the GRU recurrence variants at the bench shape (T=501, N=32, H=800,
-bidirectional): direct-operand kernels with the flag or the sentinel-ring hand-off (and,
-with `all`, the LDS-staged kernels), selected through the environment switches the
-library reads at every call."""
+bidirectional), alternating in one process: the bf16x6 kernels vs the fp32-MFMA ones, the
+same-XCD groups vs the interleaved layout, and poll-knob sweeps (DS2_RNN_TUNE) -- selected
+through the environment switches the library reads at every call."""
 import os
 import sys
 
@@ -51,50 +51,18 @@ def timed(fn, reps=5):
     return e0.elapsed_time(e1) / reps
 
 
-variants = {"x6-default": {"DS2_GRU_DOP": "1", "DS2_GRU_X6": "1", "DS2_RNN_HANDOFF": ""},
-            "x6-flags": {"DS2_GRU_DOP": "1", "DS2_GRU_X6": "1", "DS2_RNN_HANDOFF": "flags"},
-            "x6-sentinel": {"DS2_GRU_DOP": "1", "DS2_GRU_X6": "1", "DS2_RNN_HANDOFF": "sentinel"},
-            "f32-default": {"DS2_GRU_DOP": "1", "DS2_GRU_X6": "0", "DS2_RNN_HANDOFF": ""}}
-if len(sys.argv) > 1 and sys.argv[1] == "all":
-    variants = {"staged": {"DS2_GRU_DOP": "0"}, **variants,
-                "f32-flags": {"DS2_GRU_DOP": "1", "DS2_GRU_X6": "0", "DS2_RNN_HANDOFF": "flags"},
-                "f32-sentinel": {"DS2_GRU_DOP": "1", "DS2_GRU_X6": "0",
-                                 "DS2_RNN_HANDOFF": "sentinel"}}
-if len(sys.argv) > 1 and sys.argv[1] == "tune":
-    variants = {}
-    for x6 in ("1", "0"):
-        for t in ("1,0", "1,10", "1,14", "1,18", "2,14", "1,22"):
-            variants[f"{'x6' if x6 == '1' else 'f32'}-tune-{t}"] = {
-                "DS2_GRU_X6": x6, "DS2_RNN_HANDOFF": "", "DS2_RNN_TUNE": t}
-if len(sys.argv) > 1 and sys.argv[1] == "btune":
-    variants = {"bwd-f32-flags": {"DS2_GRU_X6": "1", "DS2_GRU_X6_BWD": "0",
-                                  "DS2_RNN_HANDOFF_BWD": "flags"},
-                "bwd-x6w8-flags": {"DS2_GRU_X6": "1", "DS2_GRU_X6_BWD": "1",
-                                   "DS2_GRU_X6_BWD_WAVES": "8", "DS2_RNN_HANDOFF_BWD": "flags"},
-                "bwd-x6w4-flags": {"DS2_GRU_X6": "1", "DS2_GRU_X6_BWD": "1",
-                                   "DS2_GRU_X6_BWD_WAVES": "4", "DS2_RNN_HANDOFF_BWD": "flags"}}
-if len(sys.argv) > 1 and sys.argv[1] == "pre":
-    variants = {"bwd-f32-flags": {"DS2_GRU_X6": "1", "DS2_GRU_X6_BWD": "0",
-                                  "DS2_RNN_HANDOFF_BWD": "flags"},
-                "bwd-x6pre-w8": {"DS2_GRU_X6": "1", "DS2_GRU_X6_BWD": "2",
-                                 "DS2_GRU_X6_BWD_WAVES": "8", "DS2_RNN_HANDOFF_BWD": "flags"}}
+variants = {"x6": {"DS2_GRU_X6": "1", "DS2_RNN_TUNE": ""},
+            "f32": {"DS2_GRU_X6": "0", "DS2_RNN_TUNE": ""}}
 if len(sys.argv) > 1 and sys.argv[1] == "xcd":
-    # the same-XCD groups are chosen once per process (DS2_GRU_XCD read at first launch):
-    # run this script once per setting and compare the lines
-    variants = {f"bwd-x6pre-xcd{os.environ.get('DS2_GRU_XCD', '0')}": {
-        "DS2_GRU_X6": "1", "DS2_GRU_X6_BWD": "2", "DS2_RNN_HANDOFF_BWD": "flags"}}
+    # the same-XCD groups vs the interleaved layout (DS2_GRU_XCD, read at every call)
+    variants = {f"xcd{v}": {"DS2_GRU_X6": "1", "DS2_GRU_XCD": v} for v in ("1", "0")}
 if len(sys.argv) > 1 and sys.argv[1] == "ftune":
-    # the sentinel forward's first-poll delay / re-poll sleep (s_sleep units) with the
-    # same-XCD groups on
-    variants = {f"fwd-tune-{t}": {"DS2_GRU_X6": "1", "DS2_RNN_HANDOFF": "", "DS2_RNN_TUNE": t}
+    # the sentinel forward's first-poll delay / re-poll sleep (s_sleep units)
+    variants = {f"fwd-tune-{t}": {"DS2_GRU_X6": "1", "DS2_RNN_TUNE": t}
                 for t in ("1,14,14", "1,6,14", "1,10,14", "1,18,14", "0,10,14", "2,10,14")}
-if len(sys.argv) > 1 and sys.argv[1] == "prewaves":
-    variants = {f"bwd-x6pre-w{w}": {"DS2_GRU_X6": "1", "DS2_GRU_X6_BWD": "2",
-                                    "DS2_GRU_X6_BWD_WAVES": w, "DS2_RNN_HANDOFF_BWD": "flags"}
-                for w in ("8", "4")}
 if len(sys.argv) > 1 and sys.argv[1] == "flagpoll":
     # s_sleep(1) units between the flag hand-off's polls (the pre-split backward's wait)
-    variants = {f"bwd-poll-{t}": {"DS2_GRU_X6": "1", "DS2_RNN_HANDOFF": "", "DS2_RNN_TUNE": t}
+    variants = {f"bwd-poll-{t}": {"DS2_GRU_X6": "1", "DS2_RNN_TUNE": t}
                 for t in ("1,10,14,1", "1,10,14,0", "1,10,14,2", "1,10,14,4")}
 rounds = int(os.environ.get("AB_ROUNDS", "3"))
 variants = {f"{k}#{r}": v for r in range(rounds) for k, v in variants.items()}

@@ -25,16 +25,16 @@ def _close(got, ref, rel=1e-5, name=""):
 
 
 # ---------------------------------------------------------------------------- GEMM
-@pytest.mark.parametrize("x6", ["1", "0", "160"])
+@pytest.mark.parametrize("x6", ["1", "0"])
 @pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
 @pytest.mark.parametrize("m,n,k", [(1, 1, 1), (37, 53, 29), (128, 128, 16), (300, 257, 513),
                                    (515, 2400, 132), (257, 300, 5000),   # split-K path
                                    (300, 256, 516), (260, 132, 1000)])   # float4 staging, K % 32 != 0
 def test_sgemm(dev, ta, tb, m, n, k, x6, monkeypatch):
-    """ds2_sgemm_ws vs fp64 at 1e-5: the bf16x6 kernel (default for float4-staged operands)
-    and the fp32-MFMA kernels (DS2_GEMM_X6=0); "160" forces the 256 x 160 bf16x6 tile."""
-    monkeypatch.setenv("DS2_GEMM_X6", "1" if x6 == "160" else x6)
-    monkeypatch.setenv("DS2_GEMM_X6_BN", "160" if x6 == "160" else "")
+    """ds2_sgemm_ws vs fp64 at 1e-5: the bf16x6 kernel (default for float4-staged operands;
+    256 x 160 tiles for N >= 256, 256 x 128 below) and the fp32-MFMA kernels
+    (DS2_GEMM_X6=0)."""
+    monkeypatch.setenv("DS2_GEMM_X6", x6)
     g = torch.Generator().manual_seed(m * 7 + n * 3 + k)
     a = torch.randn(k, m, generator=g) if ta else torch.randn(m, k, generator=g)
     b = torch.randn(n, k, generator=g) if tb else torch.randn(k, n, generator=g)
@@ -49,22 +49,17 @@ def test_sgemm(dev, ta, tb, m, n, k, x6, monkeypatch):
     _close(cd, ref, 1e-5, "sgemm")
 
 
-@pytest.mark.parametrize("mode", ["bk16", "128", "160", "db128", "db160", "x6", "x6-128",
-                                  "x6-bn128", "x6-bn160"])
+@pytest.mark.parametrize("mode", ["x6", "x6-narrow", "fp32", "fp32-narrow", "unaligned"])
 @pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
 def test_sgemm_full_rounds_plus_split_tail(dev, ta, tb, mode, monkeypatch):
     """Whole rounds of resident workgroups + a tail whose K range is split (one launch) and
-    reduced in a fixed order; alpha/beta/bias applied once.  fp32 kernels: BK = 16 /
-    32x32x2 (DS2_GEMM64=0) and BK = 64 / 16x16x4 with 128- and 160-wide tiles; bf16x6
-    kernels: 256 x 128 (default) and 128 x 128 (DS2_GEMM_X6=2)."""
-    monkeypatch.setenv("DS2_GEMM_X6", {"x6": "1", "x6-128": "2", "x6-bn128": "1",
-                                       "x6-bn160": "1"}.get(mode, "0"))
-    monkeypatch.setenv("DS2_GEMM_X6_BN", mode[-3:] if mode.startswith("x6-bn") else "")
-    monkeypatch.setenv("DS2_GEMM64", "0" if mode == "bk16" else "1")
-    if mode in ("128", "160", "db128", "db160"):
-        monkeypatch.setenv("DS2_GEMM_BN", mode[-3:])
-        monkeypatch.setenv("DS2_GEMM_DB", "1" if mode.startswith("db") else "0")
-    m, n, k = 128 * 29, 128 * 27 + 52, 2080
+    reduced in a fixed order; alpha/beta/bias applied once.  bf16x6 kernel: 256 x 160 tiles
+    (N >= 256) and 256 x 128 ("-narrow": N < 256); fp32 kernels (DS2_GEMM_X6=0): BK = 64 /
+    16x16x4 with the plan's tile width, and ("unaligned": A one float off 16-B alignment)
+    the BK = 16 / 32x32x2 kernel."""
+    monkeypatch.setenv("DS2_GEMM_X6", "1" if mode.startswith("x6") else "0")
+    m, k = 128 * 29, 2080
+    n = 200 if mode.endswith("narrow") else 128 * 27 + 52
     g = torch.Generator().manual_seed(5)
     a = torch.randn(k, m, generator=g) if ta else torch.randn(m, k, generator=g)
     b = torch.randn(n, k, generator=g) if tb else torch.randn(k, n, generator=g)
@@ -73,8 +68,14 @@ def test_sgemm_full_rounds_plus_split_tail(dev, ta, tb, mode, monkeypatch):
     ref = 0.5 * ((a.t() if ta else a).double() @ (b.t() if tb else b).double()) \
         + 0.25 * c0.double() + bias.double()
     ad, bd, cd = a.to(dev), b.to(dev), c0.to(dev).clone()
+    a_off, lda = 0, ad.shape[1]
+    if mode == "unaligned":
+        buf = torch.empty(ad.numel() + 1, device=dev)
+        buf[1:].copy_(ad.reshape(-1))
+        ad, a_off = buf, 1
     ops.sgemm(ad, bd, cd, m=m, n=n, k=k, trans_a=bool(ta), trans_b=bool(tb),
-              lda=ad.shape[1], ldb=bd.shape[1], ldc=n, alpha=0.5, beta=0.25, bias=bias.to(dev))
+              lda=lda, ldb=bd.shape[1], ldc=n, alpha=0.5, beta=0.25, bias=bias.to(dev),
+              a_off=a_off)
     torch.cuda.synchronize()
     _close(cd, ref, 1e-5, "sgemm main+tail")
 
@@ -136,13 +137,10 @@ def test_sgemm_x6_nonfinite_operands(dev, ta, tb, monkeypatch):
 @pytest.mark.parametrize("m,n,k", [(4, 4, 4), (36, 52, 28), (128, 128, 64), (300, 256, 516),
                                    (516, 2400, 132), (256, 300, 5000),      # split-K tail
                                    (128 * 29, 128 * 27 + 52, 2080)])       # rounds + tail
-@pytest.mark.parametrize("x2", ["0", "1"])
-def test_sgemm_bf16(dev, ta, tb, m, n, k, x2, monkeypatch):
+def test_sgemm_bf16(dev, ta, tb, m, n, k):
     """bf16-operand GEMM (BASELINE cfg4): operands rounded to bf16 (nearest even) on the
     way in, exact products, fp32 accumulation.  Reference: the same bf16 roundings done by
-    torch on the host, multiplied in fp64 -- so only the fp32 summation differs (1e-5).
-    x2 "1": the one-plane sxgemm2 form (DS2_GEMM_BF16_X2=1)."""
-    monkeypatch.setenv("DS2_GEMM_BF16_X2", x2)
+    torch on the host, multiplied in fp64 -- so only the fp32 summation differs (1e-5)."""
     g = torch.Generator().manual_seed(m * 7 + n * 3 + k + 1)
     a = torch.randn(k, m, generator=g) if ta else torch.randn(m, k, generator=g)
     b = torch.randn(n, k, generator=g) if tb else torch.randn(k, n, generator=g)
@@ -194,13 +192,13 @@ CONVS = [  # (n, ci, h, w, co, kh, kw, sh, sw, ph, pw)
 ]
 
 
-@pytest.mark.parametrize("x6", ["1", "2", "0"])
+@pytest.mark.parametrize("x6", ["1", "0"])
 @pytest.mark.parametrize("cfg", CONVS)
 def test_conv_fwd_bwd(dev, cfg, x6, monkeypatch):
     """conv fwd / dgrad / wgrad vs fp64 torch at 1e-5: the bf16x6 direct kernels (default
-    where they fit: width stride 1, <= 24 tap rows, <= 12 kernel columns; DS2_CONV_X6=2 adds
-    the forward's width stride 2 and tap-row chunks) and the fp32 LDS-patch / implicit-GEMM
-    kernels (DS2_CONV_X6=0)."""
+    where they fit: width stride 1, <= 24 tap rows, <= 12 kernel columns) and the fp32
+    LDS-patch / implicit-GEMM kernels (DS2_CONV_X6=0, and every shape the bf16x6 kernels do
+    not cover)."""
     monkeypatch.setenv("DS2_CONV_X6", x6)
     n, ci, h, w, co, kh, kw, sh, sw, ph, pw = cfg
     g = torch.Generator().manual_seed(sum(cfg))
@@ -255,11 +253,13 @@ def test_conv_x6_is_fp32_accurate(dev, monkeypatch):
 
 @pytest.mark.parametrize("cfg", [(2, 32, 81, 200, 32, 21, 11, 2, 1, 10, 5),
                                  (3, 5, 30, 70, 20, 7, 11, 1, 1, 3, 5),
-                                 (4, 32, 81, 70, 32, 21, 11, 2, 1, 10, 5)])
-def test_conv_x6_wgrad_forms(dev, cfg, monkeypatch):
-    """The sliding-window bf16x6 weight gradient (default: sh new x rows per output row into a
-    6-slot ring) and the per-row-restaging form (DS2_CONV_X6W_SW=0) against fp64 torch: splits
-    that start mid-segment and segments of one row (4 x 70 columns = 3 chunks per row)."""
+                                 (4, 32, 81, 70, 32, 21, 11, 2, 1, 10, 5),
+                                 (2, 8, 40, 60, 16, 7, 11, 3, 1, 3, 5)])
+def test_conv_x6_wgrad_forms(dev, cfg):
+    """The bf16x6 weight gradients against fp64 torch: the sliding-window form (row strides
+    <= 2: sh new x rows per output row into a 6-slot ring; splits that start mid-segment and
+    segments of one row, 4 x 70 columns = 3 chunks per row) and the per-row-restaging form
+    (row stride 3)."""
     n, ci, h, w, co, kh, kw, sh, sw, ph, pw = cfg
     g = torch.Generator().manual_seed(sum(cfg) + 1)
     x = torch.randn(n, ci, h, w, generator=g, dtype=torch.float64)
@@ -267,28 +267,9 @@ def test_conv_x6_wgrad_forms(dev, cfg, monkeypatch):
     y = F.conv2d(x, wt, None, stride=(sh, sw), padding=(ph, pw))
     dy = torch.randn(y.shape, generator=g, dtype=torch.float64)
     dwr = torch.nn.grad.conv2d_weight(x, wt.shape, dy, stride=(sh, sw), padding=(ph, pw))
-    for form in ("1", "0"):
-        monkeypatch.setenv("DS2_CONV_X6W_SW", form)
-        dw, _ = ops.conv2d_wgrad(dy.float().to(dev), x.float().to(dev), tuple(wt.shape), (sh, sw),
-                                 (ph, pw), with_bias=False)
-        _close(dw, dwr, 1e-5, "conv wgrad form " + form)
-
-
-def test_conv1_x6_is_fp32_accurate(dev, monkeypatch):
-    """The model's conv1 (1 -> 32 channels, 41 x 11 taps, stride (2, 2): three 16-row tap
-    chunks, stride-2 patch columns) on the opt-in bf16x6 kernel (DS2_CONV_X6=2): error
-    against fp64 of the fp32 kernel's order."""
-    n, ci, h, w, co, kh, kw, sh, sw, ph, pw = 2, 1, 161, 300, 32, 41, 11, 2, 2, 20, 5
-    g = torch.Generator().manual_seed(12)
-    x = torch.randn(n, ci, h, w, generator=g, dtype=torch.float64)
-    wt = torch.randn(co, ci, kh, kw, generator=g, dtype=torch.float64) * 0.1
-    y = F.conv2d(x, wt, None, stride=(sh, sw), padding=(ph, pw))
-    errs = {}
-    for mode in ("2", "0"):
-        monkeypatch.setenv("DS2_CONV_X6", mode)
-        yd = ops.conv2d_fwd(x.float().to(dev), wt.float().to(dev), None, (sh, sw), (ph, pw))
-        errs[mode] = (yd.double().cpu() - y).abs().max().item() / y.abs().max().item()
-    assert errs["2"] <= 2.5 * errs["0"] and errs["2"] < 5e-6, errs
+    dw, _ = ops.conv2d_wgrad(dy.float().to(dev), x.float().to(dev), tuple(wt.shape), (sh, sw),
+                             (ph, pw), with_bias=False)
+    _close(dw, dwr, 1e-5, "conv wgrad")
 
 
 # ---------------------------------------------------------------------------- BN
@@ -414,158 +395,19 @@ def test_gru_persistent_equals_per_step(dev, h, monkeypatch):
         _close(a, b, 1e-5, "persistent vs per-step")
 
 
-@pytest.mark.parametrize("cell", ["gru", "lstm"])
-def test_rnn_flag_handoff_equals_counter_handoff(dev, cell, monkeypatch):
-    """The per-producer-flag and the arrival-counter hand-offs of the persistent kernels
-    synchronise differently but compute the same thing: bit-identical outputs and grads."""
-    n, t, inp, h = 32, 29, 48, 64
-    gm = 3 if cell == "gru" else 4
-    g = torch.Generator().manual_seed(77)
-    weights = [torch.rand(s, generator=g) * 0.4 - 0.2 for s in
-               [(gm * h, inp), (gm * h, h), (gm * h,), (gm * h,)] * 2]
-    lens = torch.tensor(sorted([t - (i % 5) * 4 for i in range(n)], reverse=True), dtype=torch.int32)
-    x = torch.randn(t, n, inp, generator=g)
-    dy = torch.randn(t, n, h, generator=g)
-    fn = ops.GRULayerFn if cell == "gru" else ops.LSTMLayerFn
-    outs = []
-    monkeypatch.setenv("DS2_GRU_DOP", "0")   # both forms of the LDS-staged kernels
-    for flag in ("1", "0"):
-        monkeypatch.setenv("DS2_RNN_FLAGS", flag)
-        ws = [w.to(dev).requires_grad_(True) for w in weights]
-        xd = x.to(dev).requires_grad_(True)
-        y = fn.apply(xd, lens.to(dev), True, h, *ws)
-        y.backward(dy.to(dev))
-        torch.cuda.synchronize()
-        outs.append([y.detach().cpu(), xd.grad.cpu()] + [w.grad.cpu() for w in ws])
-    for a, b in zip(*outs):
-        assert torch.equal(a, b)
-
-
-@pytest.mark.parametrize("n,h,bidir", [(32, 64, True), (20, 800, True), (7, 48, False)])
-def test_gru_direct_operand_equals_staged(dev, n, h, bidir, monkeypatch):
-    """The direct-operand recurrences (per-wave producer polls, A operands loaded straight
-    into registers) and the LDS-staged ones agree; they sum the K range in a different
-    order, so within fp32 rounding."""
-    t, inp = 31, 40
-    nd = 2 if bidir else 1
-    g = torch.Generator().manual_seed(h + n)
-    weights = [torch.rand(s, generator=g) * 0.4 - 0.2 for s in
-               [(3 * h, inp), (3 * h, h), (3 * h,), (3 * h,)] * nd]
-    lens = torch.tensor(sorted([t - (i % 6) * 5 for i in range(n)], reverse=True),
-                        dtype=torch.int32)
-    x = torch.randn(t, n, inp, generator=g)
-    dy = torch.randn(t, n, h, generator=g)
-    outs = []
-    for flag in ("1", "0"):
-        monkeypatch.setenv("DS2_GRU_DOP", flag)
-        ws = [w.to(dev).requires_grad_(True) for w in weights]
-        xd = x.to(dev).requires_grad_(True)
-        y = ops.GRULayerFn.apply(xd, lens.to(dev), True, h, *ws)
-        y.backward(dy.to(dev))
-        torch.cuda.synchronize()
-        outs.append([y.detach().cpu(), xd.grad.cpu()] + [w.grad.cpu() for w in ws])
-    for a, b in zip(*outs):
-        assert torch.isfinite(a).all()
-        _close(a, b, 2e-5, "direct-operand vs staged")
-
-
-@pytest.mark.parametrize("n,h,bidir", [(32, 64, True), (20, 800, True), (7, 48, False),
-                                       (17, 784, True)])
-def test_gru_reduce_scatter_backward(dev, n, h, bidir, monkeypatch):
-    """The reduce-scatter backward (each workgroup multiplies its own gate gradients into
-    partial dh tiles for every unit block; consumers sum them) against the direct-operand
-    backward: the same gradients within fp32 rounding (the K sum is split differently),
-    finite, bias gradients included."""
-    t, inp = 33, 40
-    nd = 2 if bidir else 1
-    g = torch.Generator().manual_seed(h + 5 * n)
-    a = 0.2 if h <= 64 else h ** -0.5
-    weights = [torch.rand(s, generator=g) * 2 * a - a for s in
-               [(3 * h, inp), (3 * h, h), (3 * h,), (3 * h,)] * nd]
-    lens = torch.tensor(sorted([t - (i % 6) * 5 for i in range(n)], reverse=True),
-                        dtype=torch.int32)
-    x = torch.randn(t, n, inp, generator=g)
-    dy = torch.randn(t, n, h, generator=g)
-    outs = []
-    monkeypatch.setenv("DS2_GRU_X6_BWD", "0")
-    for rs in ("0", "1"):
-        monkeypatch.setenv("DS2_GRU_BWD_RS", rs)
-        ws = [w.to(dev).requires_grad_(True) for w in weights]
-        xd = x.to(dev).requires_grad_(True)
-        y = ops.GRULayerFn.apply(xd, lens.to(dev), True, h, *ws)
-        y.backward(dy.to(dev))
-        torch.cuda.synchronize()
-        outs.append([xd.grad.cpu()] + [w.grad.cpu() for w in ws])
-    for a_, b_ in zip(*outs):
-        assert torch.isfinite(b_).all()
-        _close(b_, a_, 2e-5, "reduce-scatter vs direct-operand backward")
-
-
-@pytest.mark.parametrize("n,h,bidir", [(32, 64, True), (20, 800, True), (7, 48, False),
-                                       (16, 1024, True)])
-def test_gru_handoff_forms_agree(dev, n, h, bidir, monkeypatch):
-    """The per-producer-flag, sentinel-ring and hybrid (flag poll + sentinel-validated
-    tiles, no drain before the flag) hand-offs of the direct-operand recurrences
-    synchronise differently but sum in the same order: bit-identical outputs and
-    gradients (ragged lengths, so producers finish their sequences unevenly)."""
-    t, inp = 37, 40
-    nd = 2 if bidir else 1
-    g = torch.Generator().manual_seed(h + 3 * n)
-    weights = [torch.rand(s, generator=g) * 0.4 - 0.2 for s in
-               [(3 * h, inp), (3 * h, h), (3 * h,), (3 * h,)] * nd]
-    lens = torch.tensor(sorted([t - (i % 7) * 5 for i in range(n)], reverse=True),
-                        dtype=torch.int32)
-    x = torch.randn(t, n, inp, generator=g)
-    dy = torch.randn(t, n, h, generator=g)
-    outs = []
-    monkeypatch.setenv("DS2_GRU_DOP", "1")
-    monkeypatch.setenv("DS2_GRU_X6_BWD", "0")   # the fp32-MFMA backward has all three forms
-    for mode in ("flags", "sentinel", "hybrid"):
-        monkeypatch.setenv("DS2_RNN_HANDOFF", mode)
-        ws = [w.to(dev).requires_grad_(True) for w in weights]
-        xd = x.to(dev).requires_grad_(True)
-        y = ops.GRULayerFn.apply(xd, lens.to(dev), True, h, *ws)
-        y.backward(dy.to(dev))
-        torch.cuda.synchronize()
-        outs.append([y.detach().cpu(), xd.grad.cpu()] + [w.grad.cpu() for w in ws])
-    for a, b, c in zip(*outs):
-        assert torch.isfinite(a).all()
-        assert torch.equal(a, b) and torch.equal(a, c)
-
-
 @pytest.mark.parametrize("n,h,bidir", [(32, 800, True), (20, 64, True), (7, 48, False),
-                                       (17, 784, True)])
+                                       (17, 784, True), (16, 1024, True)])
 def test_gru_bf16x6_matches_fp32_mfma(dev, n, h, bidir, monkeypatch):
     """gru_split.hip (W_hh contraction as six bf16 products of three-term splits, fp32
-    accumulation) against the fp32-MFMA direct-operand kernels: equal within fp32 rounding
-    (different summation order); its flag and sentinel hand-offs bit-identical (odd UB = 49
-    included: the last 32-k pair is half empty)."""
-    t, inp = 41, 40
+    accumulation; sentinel-ring forward, pre-split flag backward) against the fp32-MFMA
+    direct-operand kernels (DS2_GRU_X6=0): equal within fp32 rounding (different summation
+    order; odd UB = 49 included: the last 32-k pair is half empty)."""
     nd = 2 if bidir else 1
-    g = torch.Generator().manual_seed(h + 7 * n)
-    a = 0.2 if h <= 64 else h ** -0.5
-    weights = [torch.rand(s, generator=g) * 2 * a - a for s in
-               [(3 * h, inp), (3 * h, h), (3 * h,), (3 * h,)] * nd]
-    lens = torch.tensor(sorted([t - (i % 6) * 5 for i in range(n)], reverse=True),
-                        dtype=torch.int32)
-    x = torch.randn(t, n, inp, generator=g)
-    dy = torch.randn(t, n, h, generator=g)
-    outs = []
-    monkeypatch.setenv("DS2_GRU_DOP", "1")
-    for x6, mode in (("0", ""), ("1", "flags"), ("1", "sentinel")):
-        monkeypatch.setenv("DS2_GRU_X6", x6)
-        monkeypatch.setenv("DS2_GRU_X6_BWD", x6)      # the opt-in bf16x6 backward too
-        monkeypatch.setenv("DS2_RNN_HANDOFF", mode)
-        ws = [w.to(dev).requires_grad_(True) for w in weights]
-        xd = x.to(dev).requires_grad_(True)
-        y = ops.GRULayerFn.apply(xd, lens.to(dev), True, h, *ws)
-        y.backward(dy.to(dev))
-        torch.cuda.synchronize()
-        outs.append([y.detach().cpu(), xd.grad.cpu()] + [w.grad.cpu() for w in ws])
-    for f32, flags, sent in zip(*outs):
-        assert torch.isfinite(flags).all()
-        _close(flags, f32, 2e-5, "bf16x6 vs fp32 MFMA")
-        assert torch.equal(flags, sent)
+    env = [{"DS2_GRU_X6": "0"}, {"DS2_GRU_X6": "1"}]
+    f32, x6 = _gru_run(dev, n, 41, 40, h, nd, h + 7 * n, env, monkeypatch)
+    for a, b in zip(f32, x6):
+        assert torch.isfinite(b).all()
+        _close(b, a, 2e-5, "bf16x6 vs fp32 MFMA")
 
 
 def _gru_run(dev, n, t, inp, h, nd, seed, env, monkeypatch, amp=None):
@@ -591,69 +433,27 @@ def _gru_run(dev, n, t, inp, h, nd, seed, env, monkeypatch, amp=None):
     return outs
 
 
-@pytest.mark.parametrize("n,h,bidir", [(32, 800, True), (20, 800, True), (7, 48, False),
-                                       (17, 784, True), (33, 256, True), (5, 512, False)])
-def test_gru_dh_backward_matches_gate_exchange(dev, n, h, bidir, monkeypatch):
-    """The opt-in dh-exchange backward (DS2_GRU_BWD=dh, gru_bwd_dh.hip: producers publish dh,
-    consumers form dG = dh x the forward's coefficient tiles) against the default gate-exchange
-    backward: equal within fp32 rounding (the gate gradients are dh x c instead of
-    ((dh x a) x b) ...); flag and sentinel hand-offs bit-identical; the 8-wave form (H <= 512)
-    within rounding; with the fp32-MFMA forward the coefficient tiles come from the
-    conversion kernel (gru_coef_kernel) and the same holds."""
-    nd = 2 if bidir else 1
-    base = {"DS2_GRU_DOP": "1", "DS2_GRU_X6_BWD": "0", "DS2_GRU_BWD_WAVES": "4"}
-    env = [dict(base, DS2_GRU_BWD="dg", DS2_RNN_HANDOFF=""),
-           dict(base, DS2_GRU_BWD="dh", DS2_RNN_HANDOFF="flags"),
-           dict(base, DS2_GRU_BWD="dh", DS2_RNN_HANDOFF="sentinel"),
-           dict(base, DS2_GRU_BWD="dh", DS2_RNN_HANDOFF="", DS2_GRU_BWD_WAVES="8")]
-    outs = _gru_run(dev, n, 37, 40, h, nd, h + 11 * n, env, monkeypatch)
-    ref, flags, sent, w8 = outs
-    for r, f, s_, e in zip(ref, flags, sent, w8):
-        assert torch.isfinite(f).all()
-        _close(f, r, 2e-5, "dh vs gate-exchange backward")
-        assert torch.equal(f, s_)
-        _close(e, f, 2e-5, "dh backward 8 vs 4 waves")
-    env32 = [dict(base, DS2_GRU_X6="0", DS2_GRU_BWD="dg", DS2_RNN_HANDOFF=""),
-             dict(base, DS2_GRU_X6="0", DS2_GRU_BWD="dh", DS2_RNN_HANDOFF="")]
-    r32, d32 = _gru_run(dev, n, 37, 40, h, nd, h + 11 * n, env32, monkeypatch)
-    for r, f in zip(r32, d32):
-        _close(f, r, 2e-5, "dh backward after the fp32-MFMA forward (converted coefficients)")
-
-
 @pytest.mark.parametrize("n,h,bidir", [(32, 800, True), (7, 48, False), (17, 784, True),
                                        (33, 256, True), (16, 1024, True), (64, 256, False)])
-def test_gru_presplit_backward(dev, n, h, bidir, monkeypatch):
-    """DS2_GRU_X6_BWD=2 (producers publish their gate-gradient tiles as pre-split bf16 runs,
-    consumers load ready MFMA operands) against the consumer-split bf16x6 backward: the same
-    terms in the same MFMA order, so bit-identical at either wave count; and against the
-    default fp32-MFMA backward within fp32 rounding."""
+def test_gru_xcd_groups_bit_identical(dev, n, h, bidir, monkeypatch):
+    """The same-XCD hand-off groups (default where the groups tile the 8 XCDs: 32 x 800 and
+    16 x 1024 bidirectional, 64 x 256 unidirectional) read the same bytes from plainly stored
+    copies, placed by the XCC id each producer publishes: outputs and gradients bit-identical
+    to the interleaved layout (DS2_GRU_XCD=0), ragged lengths."""
     nd = 2 if bidir else 1
-    base = {"DS2_GRU_DOP": "1", "DS2_GRU_BWD": "dg", "DS2_RNN_HANDOFF": "flags"}
-    env = [dict(base, DS2_GRU_X6_BWD="0", DS2_GRU_X6_BWD_WAVES="8"),
-           dict(base, DS2_GRU_X6_BWD="1", DS2_GRU_X6_BWD_WAVES="8"),
-           dict(base, DS2_GRU_X6_BWD="2", DS2_GRU_X6_BWD_WAVES="8"),
-           dict(base, DS2_GRU_X6_BWD="1", DS2_GRU_X6_BWD_WAVES="4"),
-           dict(base, DS2_GRU_X6_BWD="2", DS2_GRU_X6_BWD_WAVES="4"),
-           dict(base, DS2_GRU_X6_BWD="2", DS2_GRU_X6_BWD_WAVES="8", DS2_GRU_XCD="0")]
-    ref, c8, p8, c4, p4, q8 = _gru_run(dev, n, 37, 40, h, nd, h + 13 * n, env, monkeypatch)
-    for r, a8, b8, a4, b4, x8 in zip(ref, c8, p8, c4, p4, q8):
-        assert torch.isfinite(b8).all() and torch.isfinite(b4).all()
-        # the same-XCD groups (default where the groups tile the XCDs: 32 x 800 and 16 x 1024
-        # bidirectional) read the same bytes from plainly stored copies: bit-identical
-        assert torch.equal(a8, b8) and torch.equal(a4, b4) and torch.equal(b8, x8)
-        _close(b8, r, 2e-5, "pre-split x6 vs fp32-MFMA backward")
-        _close(b4, r, 2e-5, "pre-split x6 (4 waves) vs fp32-MFMA backward")
+    env = [{"DS2_GRU_XCD": "1"}, {"DS2_GRU_XCD": "0"}]
+    xg, il = _gru_run(dev, n, 37, 40, h, nd, h + 13 * n, env, monkeypatch)
+    for a, b in zip(xg, il):
+        assert torch.isfinite(a).all()
+        assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("bwd", ["dg", "dh", "dg32"])
-def test_gru_backward_full_length_vs_torch(dev, bwd, monkeypatch):
+@pytest.mark.parametrize("x6", ["1", "0"])
+def test_gru_backward_full_length_vs_torch(dev, x6, monkeypatch):
     """The cfg2 recurrence shape (bs 32, H 800, both directions) over 201 steps with ragged
-    lengths: the default gate-exchange backward (pre-split bf16x6 tiles), its fp32-MFMA form
-    (DS2_GRU_X6_BWD=0) and the opt-in dh-exchange backward against torch's nn.GRU in fp64."""
-    if bwd == "dg32":
-        monkeypatch.setenv("DS2_GRU_X6_BWD", "0")
-        bwd = "dg"
-    monkeypatch.setenv("DS2_GRU_BWD", bwd)
+    lengths: the default bf16x6 recurrences (pre-split backward tiles) and the fp32-MFMA
+    kernels (DS2_GRU_X6=0) against torch's nn.GRU in fp64."""
+    monkeypatch.setenv("DS2_GRU_X6", x6)
     n, t, inp, h = 32, 201, 64, 800
     g = torch.Generator().manual_seed(3)
     gru = torch.nn.GRU(inp, h, bidirectional=True).double()
@@ -759,58 +559,6 @@ def test_lstm_persistent_equals_per_step(dev, h, n, monkeypatch):
         outs.append([y.detach().cpu(), xd.grad.cpu()] + [w.grad.cpu() for w in ws])
     for a, b in zip(*outs):
         _close(a, b, 1e-5, "lstm persistent vs per-step")
-
-
-@pytest.mark.parametrize("h,n", [(24, 37), (400, 40), (1024, 40)])
-def test_lstm_two_tile_workgroups(dev, h, n, monkeypatch):
-    """32-sample persistent workgroups (DS2_LSTM_BTS=2; cfg4's forward at batch 64) equal
-    16-sample ones: the forward bit for bit (same k split and reduction order per sample),
-    the backward to fp32 rounding (its gate-column chunking differs)."""
-    t, inp = 13, 40
-    lstm, lens, x, g = _lstm_case(n, t, inp, h, True, h + 7)
-    weights = [p.detach().float() for p in lstm.parameters()]
-    x = x.float()
-    dy = torch.randn(t, n, h, generator=g)
-    outs = []
-    for bts in ("1", "2"):
-        monkeypatch.setenv("DS2_LSTM_BTS", bts)
-        ws = [w.to(dev).requires_grad_(True) for w in weights]
-        xd = x.to(dev).requires_grad_(True)
-        y = ops.LSTMLayerFn.apply(xd, lens.to(dev), True, h, *ws)
-        y.backward(dy.to(dev))
-        torch.cuda.synchronize()
-        outs.append([y.detach().cpu(), xd.grad.cpu()] + [w.grad.cpu() for w in ws])
-    assert torch.equal(outs[0][0], outs[1][0]), "lstm forward: 32- vs 16-sample workgroups"
-    for a, b in zip(outs[0][1:], outs[1][1:]):
-        _close(a, b, 1e-5, "lstm 32- vs 16-sample workgroups")
-
-
-@pytest.mark.parametrize("h,n,handoff", [(32, 21, "sentinel"), (32, 21, "flags"),
-                                         (400, 37, "sentinel"), (400, 37, "hybrid"),
-                                         (1024, 40, "flags")])
-def test_lstm_direct_operand_forward(dev, h, n, handoff, monkeypatch):
-    """The direct-operand forward (h tiles loaded straight into MFMA operands; sentinel ring,
-    flags or hybrid hand-off) and the opt-in direct-operand backward equal the LDS-staged
-    persistent kernels to fp32 rounding (their K splits over the waves differ)."""
-    t, inp = 11, 24
-    lstm, lens, x, g = _lstm_case(n, t, inp, h, True, h + 3)
-    weights = [p.detach().float() for p in lstm.parameters()]
-    x = x.float()
-    dy = torch.randn(t, n, h, generator=g)
-    monkeypatch.setenv("DS2_RNN_HANDOFF_FWD", handoff)
-    monkeypatch.setenv("DS2_LSTM_DOP_BWD", "1")     # the opt-in direct-operand backward too
-    outs = []
-    for dop in ("1", "0"):
-        monkeypatch.setenv("DS2_LSTM_DOP", dop)
-        ws = [w.to(dev).requires_grad_(True) for w in weights]
-        xd = x.to(dev).requires_grad_(True)
-        y = ops.LSTMLayerFn.apply(xd, lens.to(dev), True, h, *ws)
-        y.backward(dy.to(dev))
-        torch.cuda.synchronize()
-        assert torch.isfinite(y).all()
-        outs.append([y.detach().cpu(), xd.grad.cpu()] + [w.grad.cpu() for w in ws])
-    for a, b in zip(*outs):
-        _close(a, b, 1e-5, "lstm direct-operand vs staged forward")
 
 
 # ---------------------------------------------------------------------------- Lookahead
