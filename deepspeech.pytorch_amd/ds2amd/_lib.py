@@ -71,6 +71,10 @@ _PROTOS = {
     "ds2_gru_bwd_workspace_size": (_sz, [_c_int, _c_int, _c_int]),
     "ds2_gru_bwd_grid": (_c_int, [_c_int, _c_int, _c_int]),
     "ds2_lstm_bwd_grid": (_c_int, [_c_int, _c_int, _c_int]),
+    "ds2_rnn_fwd": (_c_int, [_c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                             _vp]),
+    "ds2_rnn_bwd": (_c_int, [_c_int, _c_int, _c_int, _c_int, _vp, _c_int, _vp, _vp, _vp, _vp,
+                             _vp, _vp]),
     "ds2_test_occupy": (_c_int, [_c_int, _c_int, _c_int, _vp, _vp]),
     "ds2_test_rnn_launch_lds": (_c_int, [_c_int, _c_int, _vp, _vp]),
     "ds2_test_timestamp": (_c_int, [_vp, _vp]),

@@ -97,8 +97,15 @@ class LSTM(_HipRNN):
     FN = ops.LSTMLayerFn
 
 
+class RNN(_HipRNN):
+    """nn.RNN drop-in (tanh, the reference's rnn_type 'rnn') on the HIP recurrence (rnn.hip)."""
+    GATES = 1
+    FN = ops.RNNLayerFn
+
+
 supported_rnns = {
     'lstm': LSTM,
+    'rnn': RNN,
     'gru': GRU,
 }
 supported_rnns_inv = dict((v, k) for k, v in supported_rnns.items())

@@ -826,6 +826,46 @@ class GRULayerFn(torch.autograd.Function):
         return (dx, None, None, None, *grads)
 
 
+class RNNLayerFn(torch.autograd.Function):
+    """One (bi)directional vanilla tanh RNN layer (nn.RNN, rnn_type 'rnn', model.py:15) over
+    padded [T, N, In] + lengths: pack -> nn.RNN -> pad of model.py:103-105; with sum_dirs the
+    direction sum of model.py:107.  Input projection and every parameter gradient are the
+    GRU's GEMMs with one gate; the recurrence is ds2_rnn_fwd / ds2_rnn_bwd."""
+
+    @staticmethod
+    def forward(ctx, x, lens, sum_dirs, hidden, *weights):
+        x = x.contiguous()
+        t, n, _ = x.shape
+        h = hidden
+        nd = len(weights) // 4
+        dev = x.device
+        bf16 = _RNN_GEMM_BF16[0]
+        xproj = _rnn_input_proj(x, weights, nd, h, bf16)
+        h_all = torch.empty(t, n, nd, h, device=dev, dtype=_F32)
+        _lib.call("ds2_rnn_fwd", t, n, h, nd, xproj.data_ptr(), weights[1].data_ptr(),
+                  _p(weights[5] if nd == 2 else None), weights[3].data_ptr(),
+                  _p(weights[7] if nd == 2 else None), lens.data_ptr(), h_all.data_ptr(),
+                  _stream())
+        ctx.save_for_backward(x, lens, h_all, *weights)
+        ctx.cfg = (sum_dirs, h, nd, bf16)
+        return _rnn_output(h_all, sum_dirs, nd)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, lens, h_all, *weights = ctx.saved_tensors
+        sum_dirs, h, nd, bf16 = ctx.cfg
+        t, n, _ = x.shape
+        dy = dy.contiguous()
+        dy_dirs = 1 if (sum_dirs and nd == 2) else nd
+        dg = torch.empty(t, n, nd, h, device=x.device, dtype=_F32)
+        _lib.call("ds2_rnn_bwd", t, n, h, nd, dy.data_ptr(), dy_dirs, weights[1].data_ptr(),
+                  _p(weights[5] if nd == 2 else None), h_all.data_ptr(), lens.data_ptr(),
+                  dg.data_ptr(), _stream())
+        dx, grads = _rnn_param_grads(x, h_all, dg, dg, weights, nd, h,
+                                     ctx.needs_input_grad[0], bf16)
+        return (dx, None, None, None, *grads)
+
+
 class LSTMLayerFn(torch.autograd.Function):
     """One (bi)directional LSTM layer (nn.LSTM semantics, gates i, f, g, o) over padded
     [T, N, In] + lengths: pack -> nn.LSTM -> pad of model.py:103-105 (rnn_type 'lstm',

@@ -395,6 +395,19 @@ ds2_status_t ds2_ctc_beam_decode_lm(const float* probs, int n, int t_max, int c,
                                     ds2_stream_t stream);
 
 /* ------------------------------------------------------------------------ */
+/* Vanilla tanh RNN recurrence (supported_rnns['rnn'] = nn.RNN, model.py:15; csrc/rnn.hip):
+ * h_t = tanh(xproj_t + b_hh + W_hh h_{t-1}) over packed lengths, xproj / h_all / dy / dgates
+ * laid out as for ds2_gru_fwd / ds2_gru_bwd with one gate ([T][N][D][H]); dgates = the
+ * gradient wrt the pre-activation (= dgx = dgh of the GEMMs).  One launch per step.      */
+ds2_status_t ds2_rnn_fwd(int t_max, int n, int h, int num_dirs, const float* xproj,
+                         const float* w_hh_f, const float* w_hh_r, const float* b_hh_f,
+                         const float* b_hh_r, const int* lens, float* h_all,
+                         ds2_stream_t stream);
+ds2_status_t ds2_rnn_bwd(int t_max, int n, int h, int num_dirs, const float* dy, int dy_dirs,
+                         const float* w_hh_f, const float* w_hh_r, const float* h_all,
+                         const int* lens, float* dgates, ds2_stream_t stream);
+
+/* ------------------------------------------------------------------------ */
 /* Residency test hooks (csrc/residency.hip; not on the training path).  ds2_test_occupy:
  * `ctas` one-wave workgroups with lds_kb KB of dynamic LDS each (> 80: alone on their CU,
  * no recurrence workgroup fits beside), each spinning for max_us microseconds on the

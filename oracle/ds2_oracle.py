@@ -208,11 +208,11 @@ class OracleDS2:
         return x, probs, out_lens, acts
 
     def _gru(self, x, lens, pre):
-        """pack -> nn.GRU / nn.LSTM -> pad -> sum directions (model.py:97-109)."""
+        """pack -> nn.GRU / nn.LSTM / nn.RNN -> pad -> sum directions (model.py:97-109)."""
         p = self.params
         t = x.shape[0]
         inp = x.shape[2]
-        cls = {'gru': torch.nn.GRU, 'lstm': torch.nn.LSTM}[self.rnn_type]
+        cls = {'gru': torch.nn.GRU, 'lstm': torch.nn.LSTM, 'rnn': torch.nn.RNN}[self.rnn_type]
         gru = cls(inp, self.hidden, bidirectional=self.bidirectional, bias=True)
         names = ['weight_ih_l0', 'weight_hh_l0', 'bias_ih_l0', 'bias_hh_l0']
         if self.bidirectional:

@@ -295,6 +295,7 @@ if __name__ == '__main__':
                 context=20)
     golden_tiny(os.path.join(HERE, 'tiny_gru_uni.npz'), seed=2026, rnn_type='gru', bidir=False,
                 context=3)
+    golden_tiny(os.path.join(HERE, 'tiny_rnn_bi.npz'), seed=2027, rnn_type='rnn')
     golden_cfg1(os.path.join(HERE, 'cfg1_ds2.npz'))
     golden_decoder(os.path.join(HERE, 'greedy_decoder.npz'))
     golden_seq_lens(os.path.join(HERE, 'seq_lens.npz'))

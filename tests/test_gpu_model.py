@@ -28,7 +28,8 @@ def _rel(got, ref):
     return (got - ref).abs().max().item() / max(ref.abs().max().item(), 1e-30)
 
 
-TINY = ['tiny_ds2.npz', 'tiny_lstm_bi.npz', 'tiny_lstm_uni.npz', 'tiny_gru_uni.npz']
+TINY = ['tiny_ds2.npz', 'tiny_lstm_bi.npz', 'tiny_lstm_uni.npz', 'tiny_gru_uni.npz',
+        'tiny_rnn_bi.npz']
 
 
 def build(seed, hidden, layers, rnn_type='gru', bidirectional=True, context=20):

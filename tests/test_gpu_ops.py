@@ -500,6 +500,41 @@ def test_gru_per_direction_output(dev):
     _close(xd.grad, xr.grad, 1e-4, "gru dx")
 
 
+# ---------------------------------------------------------------------------- tanh RNN
+@pytest.mark.parametrize("n,t,inp,h,bidir", [(5, 23, 40, 24, True), (19, 9, 33, 100, True),
+                                             (3, 17, 20, 16, False), (33, 40, 64, 800, True)])
+def test_rnn_layer(dev, n, t, inp, h, bidir):
+    """rnn_type 'rnn' (model.py:15, nn.RNN tanh): the ds2amd layer == pack -> nn.RNN -> pad
+    (-> direction sum) in fp64, forward and every gradient; ragged lengths, three batch
+    tiles of 16 at n = 33."""
+    g = torch.Generator().manual_seed(n * 100 + h + 1)
+    rnn = torch.nn.RNN(inp, h, bidirectional=bidir).double()
+    a = 0.3 if h <= 100 else h ** -0.5
+    with torch.no_grad():
+        for p in rnn.parameters():
+            p.copy_((torch.rand(p.shape, generator=g, dtype=torch.float64) * 2 - 1) * a)
+    lens = torch.tensor(sorted([t] + [max(1, t - 3 * i - 1) for i in range(n - 1)], reverse=True),
+                        dtype=torch.int32)
+    x = torch.randn(t, n, inp, generator=g, dtype=torch.float64)
+    for i in range(n):
+        x[int(lens[i]):, i] = 0
+    xr = x.clone().requires_grad_(True)
+    out, _ = rnn(torch.nn.utils.rnn.pack_padded_sequence(xr, lens.numpy()))
+    out, _ = torch.nn.utils.rnn.pad_packed_sequence(out, total_length=t)
+    nd = 2 if bidir else 1
+    summed = out.view(t, n, nd, h).sum(2) if bidir else out
+    dy = torch.randn(summed.shape, generator=g, dtype=torch.float64)
+    summed.backward(dy)
+    weights = [p.detach().float().to(dev).requires_grad_(True) for p in rnn.parameters()]
+    xd = x.float().to(dev).requires_grad_(True)
+    yd = ops.RNNLayerFn.apply(xd, lens.to(dev), True, h, *weights)
+    yd.backward(dy.float().to(dev))
+    _close(yd, summed, 1e-5, "rnn y")
+    _close(xd.grad, xr.grad, 1e-4, "rnn dx")
+    for (name, p), wd in zip(rnn.named_parameters(), weights):
+        _close(wd.grad, p.grad, 1e-4, "rnn " + name)
+
+
 # ---------------------------------------------------------------------------- LSTM
 def _lstm_case(n, t, inp, h, bidir, seed):
     g = torch.Generator().manual_seed(seed)

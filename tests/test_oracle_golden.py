@@ -21,7 +21,8 @@ def _load(golden_dir, name):
     return np.load(os.path.join(golden_dir, name))
 
 
-TINY = ['tiny_ds2.npz', 'tiny_lstm_bi.npz', 'tiny_lstm_uni.npz', 'tiny_gru_uni.npz']
+TINY = ['tiny_ds2.npz', 'tiny_lstm_bi.npz', 'tiny_lstm_uni.npz', 'tiny_gru_uni.npz',
+        'tiny_rnn_bi.npz']
 
 
 def build_model(seed, hidden, layers, rnn_type='gru', bidirectional=True, context=20):
