@@ -71,6 +71,10 @@ _PROTOS = {
     "ds2_gru_bwd_workspace_size": (_sz, [_c_int, _c_int, _c_int]),
     "ds2_gru_bwd_grid": (_c_int, [_c_int, _c_int, _c_int]),
     "ds2_lstm_bwd_grid": (_c_int, [_c_int, _c_int, _c_int]),
+    "ds2_bgemm_workspace_size": (_sz, [_c_int, _c_int, _c_int]),
+    "ds2_bgemm_nt": (_c_int, [_c_int, _c_int, _c_int, _c_f, _vp, _c_i64, _vp, _c_i64, _c_f, _vp,
+                              _c_i64, _vp, _vp, _sz, _vp]),
+    "ds2_cvt_bf16": (_c_int, [_vp, _c_int, _c_int, _c_i64, _vp, _c_i64, _c_int, _vp]),
     "ds2_rnn_fwd": (_c_int, [_c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                              _vp]),
     "ds2_rnn_bwd": (_c_int, [_c_int, _c_int, _c_int, _c_int, _vp, _c_int, _vp, _vp, _vp, _vp,

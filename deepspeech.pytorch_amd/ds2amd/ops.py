@@ -108,6 +108,41 @@ def sgemm(a: torch.Tensor, b: torch.Tensor, c: torch.Tensor, *, m: int, n: int, 
     return c
 
 
+def to_bf16(x: torch.Tensor, transpose: bool = False,
+            out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """fp32 [rows, cols] (row-major, contiguous rows) -> bf16 (round to nearest even) on the
+    device (ds2_cvt_bf16), as is or transposed ([cols, rows]): the k-contiguous bf16 copy an
+    operand of ds2_bgemm_nt needs."""
+    if not x.is_cuda or x.dtype != _F32 or x.dim() != 2 or x.stride(1) != 1:
+        raise _lib.Ds2Error("to_bf16: expected a row-major float32 device matrix")
+    rows, cols = x.shape
+    shape = (cols, rows) if transpose else (rows, cols)
+    if out is None:
+        out = torch.empty(shape, device=x.device, dtype=torch.bfloat16)
+    _lib.call("ds2_cvt_bf16", x.data_ptr(), rows, cols, x.stride(0), out.data_ptr(),
+              out.stride(0), int(transpose), _stream())
+    return out
+
+
+def bgemm_nt(a: torch.Tensor, b: torch.Tensor, c: torch.Tensor, *, alpha: float = 1.0,
+             beta: float = 0.0, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """c[m, n] (fp32) = alpha * a[m, k] @ b[n, k]^T + beta * c (+ bias): bf16 operands
+    (k-contiguous), bf16 MFMA, fp32 accumulation (ds2_bgemm_nt, csrc/bgemm.hip)."""
+    for t in (a, b):
+        if not t.is_cuda or t.dtype != torch.bfloat16 or t.dim() != 2 or t.stride(1) != 1:
+            raise _lib.Ds2Error("bgemm_nt: expected row-major bf16 device matrices")
+    m, k = a.shape
+    n = b.shape[0]
+    if b.shape[1] != k or tuple(c.shape) != (m, n) or c.dtype != _F32:
+        raise _lib.Ds2Error(f"bgemm_nt: shapes a {tuple(a.shape)} b {tuple(b.shape)} c {tuple(c.shape)}")
+    nbytes = _lib.size("ds2_bgemm_workspace_size", m, n, k)
+    ws = _ws(nbytes, c.device) if nbytes > 0 else None
+    _lib.call("ds2_bgemm_nt", m, n, k, float(alpha), a.data_ptr(), a.stride(0), b.data_ptr(),
+              b.stride(0), float(beta), c.data_ptr(), c.stride(0), _p(bias), _p(ws),
+              0 if ws is None else ws.numel(), _stream())
+    return c
+
+
 def matmul_nt(x2d: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None,
               out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """x2d[M,K] @ w[N,K]^T (+bias) -> [M,N] (nn.Linear forward)."""

@@ -394,6 +394,21 @@ ds2_status_t ds2_ctc_beam_decode_lm(const float* probs, int n, int t_max, int c,
                                     float* out_scores, void* ws, size_t ws_bytes,
                                     ds2_stream_t stream);
 
+/* bf16 GEMM on bf16 operands (BASELINE cfg4's bf16 MFMA RNN GEMMs; csrc/bgemm.hip):
+ * C[m x n] (fp32, ldc) = alpha * A . B^T + beta * C + bias, A [m][lda] and B [n][ldb] bf16
+ * (raw 16-bit words, k-contiguous), fp32 accumulation.  A and B 16-B aligned, k, lda, ldb
+ * multiples of 8, each operand < 2 GiB, else DS2_UNSUPPORTED_SHAPE.  Workspace for the
+ * split-K tail: ds2_bgemm_workspace_size (NULL / too small: no split).
+ * ds2_cvt_bf16: fp32 [rows][ld_src] -> bf16 (round to nearest even) as [rows][ld_dst], or
+ * with transpose != 0 as [cols][ld_dst] (the k-contiguous copy of an m- or n-contiguous
+ * operand).                                                                    */
+size_t ds2_bgemm_workspace_size(int m, int n, int k);
+ds2_status_t ds2_bgemm_nt(int m, int n, int k, float alpha, const void* a, int64_t lda,
+                          const void* b, int64_t ldb, float beta, float* c, int64_t ldc,
+                          const float* bias, void* ws, size_t ws_bytes, ds2_stream_t stream);
+ds2_status_t ds2_cvt_bf16(const float* src, int rows, int cols, int64_t ld_src, void* dst,
+                          int64_t ld_dst, int transpose, ds2_stream_t stream);
+
 /* ------------------------------------------------------------------------ */
 /* Vanilla tanh RNN recurrence (supported_rnns['rnn'] = nn.RNN, model.py:15; csrc/rnn.hip):
  * h_t = tanh(xproj_t + b_hh + W_hh h_{t-1}) over packed lengths, xproj / h_all / dy / dgates

@@ -162,6 +162,31 @@ def test_sgemm_bf16(dev, ta, tb, m, n, k):
         assert (cd.double().cpu() - full).abs().max() > 1e-4 * full.abs().max()
 
 
+@pytest.mark.parametrize("m,n,k", [(256, 256, 64), (300, 200, 136), (1000, 520, 1024),
+                                   (513, 777, 4104), (2048, 4096, 1312),
+                                   (4096, 1024, 32064 // 4), (64, 1024, 32064)])
+def test_bgemm_nt(dev, m, n, k):
+    """ds2_bgemm_nt (bf16 operands in HBM, the 256 x 256 LDS-DMA ping-pong kernel): partial
+    tiles in M and N, K not a multiple of 64 (the masked last K-tile), whole rounds plus a
+    split-K tail, one tile row with deep K.  Reference: the same bf16 values multiplied in
+    fp64 -- only the fp32 summation order differs (1e-5).  ds2_cvt_bf16 (RNE) equals torch's
+    bf16 rounding bit for bit, plain and transposed."""
+    g = torch.Generator().manual_seed(m + n + k)
+    a32 = torch.randn(m, k, generator=g).to(dev)
+    b32 = torch.randn(k, n, generator=g).to(dev)          # n-contiguous: the transposing copy
+    c0 = torch.randn(m, n, generator=g).to(dev)
+    bias = torch.randn(n, generator=g).to(dev)
+    a = ops.to_bf16(a32)
+    bt = ops.to_bf16(b32, transpose=True)                  # [n, k]
+    assert torch.equal(a, a32.to(torch.bfloat16))
+    assert torch.equal(bt, b32.t().contiguous().to(torch.bfloat16))
+    c = c0.clone()
+    ops.bgemm_nt(a, bt, c, alpha=0.5, beta=0.25, bias=bias)
+    torch.cuda.synchronize()
+    ref = 0.5 * (a.double() @ bt.double().t()) + 0.25 * c0.double() + bias.double()
+    _close(c, ref, 1e-5, "bgemm_nt")
+
+
 def test_sgemm_bf16_rejects_unaligned(dev):
     a = torch.randn(8, 6, device=dev)
     b = torch.randn(6, 8, device=dev)
