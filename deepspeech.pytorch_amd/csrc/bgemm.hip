@@ -254,12 +254,13 @@ __global__ __launch_bounds__(BG_T, 1) void bgemm_nt_kernel(
 __global__ __launch_bounds__(256) void cvt_bf16_kernel(const float* __restrict__ src, int rows,
                                                        int cols, int64_t ld_src,
                                                        unsigned short* __restrict__ dst,
-                                                       int64_t ld_dst, int transpose) {
+                                                       int64_t ld_dst, int transpose, int vec) {
   __shared__ unsigned short tl[64][66];
   const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
   const int t = threadIdx.x;
   if (!transpose) {
-    // 64 rows x 64 cols: each thread 16 consecutive columns of one row
+    // 64 rows x 64 cols: each thread 16 consecutive columns of one row (pairs when vec: src
+    // 8-B and dst 4-B aligned with even row strides)
     const int r = r0 + (t >> 2), cb = c0 + 16 * (t & 3);
     if (r >= rows) return;
     const float* s = src + (int64_t)r * ld_src;
@@ -267,7 +268,10 @@ __global__ __launch_bounds__(256) void cvt_bf16_kernel(const float* __restrict__
 #pragma unroll
     for (int i = 0; i < 16; i += 2) {
       const int c = cb + i;
-      if (c + 1 < cols) {
+      if (!vec) {
+        if (c < cols) d[c] = __builtin_bit_cast(unsigned short, (__bf16)s[c]);
+        if (c + 1 < cols) d[c + 1] = __builtin_bit_cast(unsigned short, (__bf16)s[c + 1]);
+      } else if (c + 1 < cols) {
         const f32x2v v = *reinterpret_cast<const f32x2v*>(s + c);
         *reinterpret_cast<unsigned*>(d + c) = __builtin_bit_cast(unsigned, __builtin_convertvector(v, bf16x2v));
       } else if (c < cols) {
@@ -433,13 +437,12 @@ ds2_status_t ds2_cvt_bf16(const float* src, int rows, int cols, int64_t ld_src, 
   if (rows < 0 || cols < 0 || src == nullptr || dst == nullptr) return DS2_INVALID_VALUE;
   if (rows == 0 || cols == 0) return DS2_OK;
   if (ld_src < cols || ld_dst < (transpose ? rows : cols)) return DS2_INVALID_VALUE;
-  if (!transpose && ((reinterpret_cast<uintptr_t>(src) & 7) || (reinterpret_cast<uintptr_t>(dst) & 3) ||
-                     (ld_src & 1) || (ld_dst & 1)))
-    return DS2_UNSUPPORTED_SHAPE;
+  const int vec = !((reinterpret_cast<uintptr_t>(src) & 7) || (reinterpret_cast<uintptr_t>(dst) & 3) ||
+                    (ld_src & 1) || (ld_dst & 1));
   const dim3 grid(cdiv(cols, 64), cdiv(rows, 64));
   if (grid.y > 65535) return DS2_UNSUPPORTED_SHAPE;
   hipLaunchKernelGGL(cvt_bf16_kernel, grid, dim3(256), 0, as_stream(stream), src, rows, cols,
-                     ld_src, static_cast<unsigned short*>(dst), ld_dst, transpose);
+                     ld_src, static_cast<unsigned short*>(dst), ld_dst, transpose, vec);
   return launch_status("ds2_cvt_bf16");
 }
 

@@ -98,12 +98,42 @@ def sgemm(a: torch.Tensor, b: torch.Tensor, c: torch.Tensor, *, m: int, n: int, 
     ds2_sgemm_bf16_ws) -- the opt-in precision of BASELINE cfg4's RNN GEMMs.
     """
     es = 4
+    if bf16 and k % 8 == 0 and k > 0 and m > 0 and n > 0:
+        return _sgemm_bf16_bgemm(a, b, c, m, n, k, trans_a, trans_b, lda, ldb, ldc, alpha, beta,
+                                 bias, a_off, b_off, c_off)
     fn = "ds2_sgemm_bf16" if bf16 else "ds2_sgemm"
     nbytes = _lib.size(fn + "_workspace_size", m, n, k, 1)
     ws = _ws(nbytes, c.device) if nbytes > 0 else None
     _lib.call(fn + "_ws", int(trans_a), int(trans_b), m, n, k, float(alpha),
               a.data_ptr() + es * a_off, lda, 0, b.data_ptr() + es * b_off, ldb, 0,
               float(beta), c.data_ptr() + es * c_off, ldc, 0, 1, _p(bias), _p(ws),
+              0 if ws is None else ws.numel(), _stream())
+    return c
+
+
+def _sgemm_bf16_bgemm(a, b, c, m, n, k, trans_a, trans_b, lda, ldb, ldc, alpha, beta, bias,
+                      a_off, b_off, c_off):
+    """The bf16 RNN GEMMs (BASELINE cfg4) on ds2_bgemm_nt: both operands rounded to bf16 into
+    k-contiguous copies (A -> [m][k], B -> [n][k]; ds2_cvt_bf16, transposing where the operand
+    is m- or n-contiguous), then the bf16 MFMA GEMM.  Same rounding (RNE) and products as
+    ds2_sgemm_bf16_ws; only the fp32 summation order differs."""
+    dev = c.device
+    cp = a.data_ptr() + 4 * a_off
+    ab = torch.empty(m, k, device=dev, dtype=torch.bfloat16)
+    if trans_a:   # A stored [k][m]
+        _lib.call("ds2_cvt_bf16", cp, k, m, lda, ab.data_ptr(), k, 1, _stream())
+    else:
+        _lib.call("ds2_cvt_bf16", cp, m, k, lda, ab.data_ptr(), k, 0, _stream())
+    bp = b.data_ptr() + 4 * b_off
+    bb = torch.empty(n, k, device=dev, dtype=torch.bfloat16)
+    if trans_b:   # B stored [n][k]
+        _lib.call("ds2_cvt_bf16", bp, n, k, ldb, bb.data_ptr(), k, 0, _stream())
+    else:         # B stored [k][n]
+        _lib.call("ds2_cvt_bf16", bp, k, n, ldb, bb.data_ptr(), k, 1, _stream())
+    nbytes = _lib.size("ds2_bgemm_workspace_size", m, n, k)
+    ws = _ws(nbytes, dev) if nbytes > 0 else None
+    _lib.call("ds2_bgemm_nt", m, n, k, float(alpha), ab.data_ptr(), k, bb.data_ptr(), k,
+              float(beta), c.data_ptr() + 4 * c_off, ldc, _p(bias), _p(ws),
               0 if ws is None else ws.numel(), _stream())
     return c
 

@@ -1,0 +1,7 @@
+set -o pipefail
+cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest tests/test_gpu_ops.py -k "bgemm" -x -v --timeout 120 --timeout-method thread > gpurun_out/r4c.bg.log 2>&1; rc=$?; tail -3 gpurun_out/r4c.bg.log
+[ $rc -ne 0 ] && exit $rc
+timeout -k 10 300 python -u scripts/bench_bgemm.py > gpurun_out/r4c.bench_bgemm.log 2>&1 || exit 1
+cat gpurun_out/r4c.bench_bgemm.log
+TESTS=tests NOPROF=1 bash scripts/gpu_check.sh r4c
