@@ -362,7 +362,14 @@ struct BeamLm {
   unsigned tmask;
   int fstate, order, start, space;
   double alpha, beta;
+  // test hook (ds2_test_beam_stamps): per-phase shader-clock stamps (s_memtime) of
+  // utterance 0's first BEAM_NSTAMP_T frames, [frame][phase], slot 8 = the frame start on
+  // s_memrealtime (100 MHz); null = off
+  unsigned long long* stamps;
 };
+
+constexpr int BEAM_NSTAMP_T = 256, BEAM_NSTAMP_P = 9;   // 8 phases + s_memrealtime
+static unsigned long long* g_beam_stamps = nullptr;
 
 constexpr int LM_MAX_ORDER = 6;
 
@@ -508,6 +515,10 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
   int* ns = node_ns + (int64_t)n * node_cap;
   unsigned long long* km = node_km + (int64_t)n * node_cap;
   const bool prune = cutoff_prob < 1.0 || cutoff_top_n < C;
+  unsigned long long* const stamps = (L.stamps != nullptr && n == 0) ? L.stamps : nullptr;
+#define BEAM_STAMP(ph)                                                      \
+  if (stamps != nullptr && t < BEAM_NSTAMP_T && lane == 0)                  \
+    stamps[t * BEAM_NSTAMP_P + (ph)] = __builtin_amdgcn_s_memtime();
 
   if (lane == 0) {
     b_node[0][0] = 0; b_last[0][0] = -1; b_pb[0][0] = 0.f; b_pnb[0][0] = -INFINITY;
@@ -527,6 +538,9 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
   for (int t = 0; t < size; ++t) {
     const int nb = s_nb;
     if (nb == 0) break;
+    BEAM_STAMP(0)
+    if (stamps != nullptr && t < BEAM_NSTAMP_T && lane == 0)
+      stamps[t * BEAM_NSTAMP_P + 8] = __builtin_amdgcn_s_memrealtime();
     const int tc = t % BEAM_TCH;
     if (tc == 0) {   // stage the next BEAM_TCH frames (all loads of a lane in flight at once)
       const int nf = min(BEAM_TCH, size - t);
@@ -570,6 +584,7 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
     } else if (lane < C) {
       allowed[lane] = 1;
     }
+    BEAM_STAMP(1)
     // ---- beam bookkeeping: scores, parent index in the beam, child map
 #pragma unroll
     for (int q = 0; q < EPL; ++q) {
@@ -639,6 +654,7 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
       }
     }
     __syncthreads();
+    BEAM_STAMP(2)
     // ---- candidates, scored straight into registers: lane holds k = lane + 64 jj (the
     // selection below scans them there); the unrolled loop lets the LDS reads of several
     // candidates overlap.  (i, c) = divmod(k, C) advanced incrementally.
@@ -702,6 +718,7 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
       }
     }
     __syncthreads();
+    BEAM_STAMP(3)
     // ---- attempted extensions onto pruned-but-alive trie nodes take the log_prob_c rule
     // (get_path_trie updates a found child whether or not it is kept)
     for (int r = lane; r < s_nr; r += 64) {
@@ -713,6 +730,7 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
         tst[x] = t;
       }
     }
+    BEAM_STAMP(4)
     // ---- keep the best `beam` candidates: a selection round is a register scan + a wave
     // arg-best, with no LDS traffic and no barrier
     int nsel = 0;
@@ -732,12 +750,15 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
       if (bs == -INFINITY) break;
       const int k = bkey & 4095;
 #pragma unroll
-      for (int jj = 0; jj < SJ; ++jj)
+      for (int jj = 0; jj < SJ; ++jj) {
+        if (SJ <= 32 && jj >= jn) break;
         if (lane + 64 * jj == k) rs[jj] = -INFINITY;
+      }
       if (lane == 0) sel_k[r] = k;
       ++nsel;
     }
     __syncthreads();
+    BEAM_STAMP(5)
     // ---- new beam: lane r builds entries r, r + 64, ...; new prefixes get trie nodes in
     // rank order (node = first free + the number of extensions ranked before it)
     const int nxt = cur ^ 1;
@@ -834,6 +855,7 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
         run += __popcll(em);
       }
       __syncthreads();
+      BEAM_STAMP(6)
       // pruned entries leave the beam; a node with no alive child left dies and takes its
       // bit and count out of its parent (recursively; the root never dies)
 #pragma unroll
@@ -855,8 +877,10 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
       }
     }
     __syncthreads();
+    BEAM_STAMP(7)
     cur = nxt;
   }
+#undef BEAM_STAMP
   // ---- final ranking and back-tracking (one lane per returned path)
   const int nb = s_nb;
 #pragma unroll
@@ -1136,6 +1160,7 @@ static ds2_status_t beam_decode(const float* probs, int n, int t_max, int c, int
   auto* nkm = reinterpret_cast<unsigned long long*>(w + 7 * plane);
   BeamLm L{};
   if (lm != nullptr) L = *lm;
+  L.stamps = g_beam_stamps;
   auto kern = lm != nullptr
                   ? (small ? ctc_beam_kernel<BEAM_SMALL, BEAM_SMALL_C, true>
                            : ctc_beam_kernel<BEAM_LARGE, BEAM_LARGE_C, true>)
@@ -1191,6 +1216,11 @@ ds2_status_t ds2_ctc_beam_decode_lm(const float* probs, int n, int t_max, int c,
   return beam_decode(probs, n, t_max, c, stride_n, stride_t, sizes, blank, beam_width,
                      cutoff_top_n, cutoff_prob, top_paths, out_ids, out_offsets, out_lens,
                      out_scores, ws, ws_bytes, &L, stream, "ds2_ctc_beam_decode_lm");
+}
+
+ds2_status_t ds2_test_beam_stamps(unsigned long long* buf) {
+  g_beam_stamps = buf;   // [BEAM_NSTAMP_T][BEAM_NSTAMP_P] device buffer, or null
+  return DS2_OK;
 }
 
 ds2_status_t ds2_edit_distance(const int* a_ids, int64_t a_stride, const int* a_lens,

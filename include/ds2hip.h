@@ -436,6 +436,11 @@ ds2_status_t ds2_test_rnn_launch_lds(int ctas, int max_us, unsigned long long* r
                                      ds2_stream_t stream);
 ds2_status_t ds2_test_timestamp(unsigned long long* out, ds2_stream_t stream);
 
+/* ds2_test_beam_stamps: test hook; every later beam decode writes per-phase clock stamps of
+ * utterance 0's first 256 frames into buf ([256][9] uint64: s_memtime at the 8 phase
+ * boundaries of a frame, then s_memrealtime at its start); buf = NULL turns it off.       */
+ds2_status_t ds2_test_beam_stamps(unsigned long long* buf);
+
 /* ------------------------------------------------------------------------ */
 /* Data-parallel gradient exchange over RCCL (SURVEY §8b allreduce_bucket /
  * ds2_comm_t; replaces DistributedDataParallel's bucketed all-reduce, train.py:947-951).

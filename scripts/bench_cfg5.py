@@ -5,7 +5,10 @@ STFT + max_frame normalisation -> DeepSpeech.forward -> prefix beam search (beam
 cutoff_top_n 40: the reference's opts.py defaults; no LM) -> host strings
 (ds2amd.transcribe.transcribe_batch on device arrays).  Greedy decoding is timed beside it.
 
-usage: python scripts/bench_cfg5.py [--batch N] [--seconds S] [--beam W] [--iters K]
+usage: python scripts/bench_cfg5.py [--batch N] [--seconds S] [--beam W] [--iters K] [--stamps]
+
+--stamps: also run one beam decode with the kernel's per-phase clock stamps on (utterance 0,
+frames 1..255; ds2_test_beam_stamps) and print the mean time of each phase of a frame.
 """
 import argparse
 import json
@@ -27,6 +30,7 @@ def main():
     ap.add_argument("--seconds", type=float, default=30.0)
     ap.add_argument("--beam", type=int, default=10)
     ap.add_argument("--iters", type=int, default=3)
+    ap.add_argument("--stamps", action="store_true")
     ap.add_argument("--lm", default=os.path.join(os.path.dirname(os.path.abspath(__file__)), "..",
                                                  "tests", "golden", "tiny_lm.arpa"),
                     help="ARPA model for the beam_lm line (default: the committed 3-gram fixture)")
@@ -71,6 +75,27 @@ def main():
         out[f"{name}_sample"] = strings[0][0][:40]
     out["beam_width"] = args.beam
     print(json.dumps(out), flush=True)
+    if args.stamps:
+        from ds2amd import _lib
+        for name, dec in (("beam", beam), ("beam_lm", beam_lm)):
+            buf = torch.zeros(256 * 9, dtype=torch.int64, device=dev)
+            _lib.call("ds2_test_beam_stamps", buf.data_ptr())
+            run(dec)
+            torch.cuda.synchronize()
+            _lib.call("ds2_test_beam_stamps", None)
+            st = buf.view(256, 9).cpu().double()
+            fr = st[1:255]
+            nxt = st[2:256]
+            ticks = (nxt[:, 0] - fr[:, 0]).mean().item()
+            us = ((nxt[:, 8] - fr[:, 8]).mean() / 100.0).item()   # s_memrealtime: 100 MHz
+            names = ["stage+lp+prune", "bookkeeping", "scoring", "revival", "selection",
+                     "new beam", "deaths", "tail"]
+            ph = [(fr[:, i + 1] - fr[:, i]).mean().item() for i in range(7)]
+            ph.append((nxt[:, 0] - fr[:, 7]).mean().item())
+            print(json.dumps({"decoder": name, "us_per_frame": round(us, 3),
+                              "clock_mhz": round(ticks / us, 1) if us > 0 else None,
+                              "phase_us": {nm: round(v / ticks * us, 3) for nm, v in zip(names, ph)}}),
+                  flush=True)
 
 
 if __name__ == "__main__":

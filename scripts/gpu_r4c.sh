@@ -4,4 +4,6 @@ timeout -k 10 300 python -u -m pytest tests/test_gpu_ops.py -k "bgemm" -x -v --t
 [ $rc -ne 0 ] && exit $rc
 timeout -k 10 300 python -u scripts/bench_bgemm.py > gpurun_out/r4c.bench_bgemm.log 2>&1 || exit 1
 cat gpurun_out/r4c.bench_bgemm.log
-TESTS=tests NOPROF=1 bash scripts/gpu_check.sh r4c
+timeout -k 10 300 python -u scripts/bench_cfg5.py --iters 1 --stamps > gpurun_out/r4c.cfg5.log 2>&1 || exit 1
+cat gpurun_out/r4c.cfg5.log
+TESTS=tests NOPROF=1 BENCH_ARGS="--steps 20 --warmup 5 --no-cpu-baseline" bash scripts/gpu_check.sh r4c
