@@ -16,14 +16,15 @@
 // competing, and the loads hide behind the partner's MFMAs.
 //
 // Hazards (barrier b_i; group 0 phase p = load (b_2p, b_2p+1), MFMA (b_2p+1, b_2p+2); group 1
-// one interval later): each group DMAs its own parts of K-tile t+1 in phases 4t .. 4t+3 --
-// q0: its A rows 0-63, q1/q2: B rows 0-63 / 64-127 of its 128-row B half, q3: its A rows 64-127
-// -- and waits vmcnt(2) at the end of each load segment, so a part is complete one segment
-// after it was issued (RAW: the first reader of every part is at least one barrier later).
-// The buffer a part overwrites held K-tile t-1, whose last reads (group 1, phase 4t-1) were
-// retired by lgkmcnt(0) after b_8t; only group 0's q0 part (its own A rows, never read by group
-// 1) is issued before b_8t+1 (WAR).  All LDS traffic of the loop is LDS-DMA + ds_read; no
-// ordinary global load is pending in the loop (hipcc would drain the DMA queue at it).
+// one interval later): each group DMAs its own parts of K-tile t+1 during K-tile t -- its A rows
+// 0-63 and B rows 0-63 of its 128-row B half in phase 0, B rows 64-127 in phase 1, its A rows
+// 64-127 in phase 2 -- so every part has 2-3 phases to land before the wait that retires it:
+// phase 3's vmcnt (first readers: phase 0 of t+1, both groups for B) and phase 1 of t+1's (A
+// rows 64-127, first read in phase 2), each followed by a barrier before any reader (RAW).  The
+// buffer a part overwrites held K-tile t-1, whose last reads (group 1, phase 3 of t-1) were
+// retired by lgkmcnt(0) BEFORE the barrier that ends that load segment (WAR).  All LDS traffic
+// of the loop is LDS-DMA + ds_read; no ordinary global load is pending in the loop (hipcc would
+// drain the DMA queue at it).
 #include "common.h"
 
 #include <algorithm>
@@ -93,7 +94,7 @@ __global__ __launch_bounds__(BG_T, 1) void bgemm_nt_kernel(
     int M, int N, int K, float alpha, const unsigned short* __restrict__ A, int lda,
     const unsigned short* __restrict__ B, int ldb, float beta, float* __restrict__ C, int64_t ldc,
     const float* __restrict__ bias, int main_wgs, int tail_tile0, int tail_tiles, int nsplit,
-    int kchunk, float* __restrict__ partial) {
+    int kchunk, float* __restrict__ partial, int cvec) {
   __shared__ __attribute__((aligned(16))) unsigned short lds[2 * BG_IMG];   // 128 KB
   int m0, n0, kbeg, kend;
   float* part;
@@ -194,12 +195,30 @@ __global__ __launch_bounds__(BG_T, 1) void bgemm_nt_kernel(
           for (int ks = 0; ks < 2; ++ks)
             af[mi][ks] = *reinterpret_cast<const bf16x8*>(img + a_off(4 * qm + mi, ks));
       }
+      // DMA of K-tile kt + 1 (buffer cur ^ 1): phase 0 its A rows 0-63 and B rows 0-63, phase
+      // 1 B rows 64-127, phase 2 A rows 64-127.  Waits: phase 1 retires A rows 64-127 of THIS
+      // K-tile (issued in phase 2 of the previous one; 6 DMA after it when more), phase 3
+      // retires everything of kt + 1 but its A rows 64-127 (2 DMA after them).
       if (more) {
-        issue(q, knext, cur ^ 1);
-        asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-      } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (q == 0) {
+          issue(0, knext, cur ^ 1);
+          issue(1, knext, cur ^ 1);
+        } else if (q == 1) {
+          issue(2, knext, cur ^ 1);
+        } else if (q == 2) {
+          issue(3, knext, cur ^ 1);
+        }
       }
+      if (q == 1) {
+        if (more) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      } else if (q == 3) {
+        if (more) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      // this segment's fragment reads retire before the barrier, so a DMA the other group issues
+      // right after it may overwrite what they read (WAR)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       bg_barrier();
       // ---- MFMA segment
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -220,29 +239,46 @@ __global__ __launch_bounds__(BG_T, 1) void bgemm_nt_kernel(
   }
   if (wr == 0) bg_barrier();   // equal barrier counts for both groups
 
-  // epilogue (16x16 C map: row 4 (lane >> 4) + r, col lane & 15)
-  const int rbase = 128 * wr + 4 * fk, cbase = 64 * wc + fr;
+  // epilogue: the accumulators (16x16 C map: row 4 (lane >> 4) + r, col lane & 15) go through
+  // the now idle LDS, 64 rows x 64 columns per wave and pass (16 KB per wave, columns XOR 16 by
+  // row bit 2: conflict-free b32 writes and b128 reads), and leave as 16-B row runs -- each
+  // store instruction writes four 256-B row segments instead of sixteen 64-B ones
+  float* const stage = reinterpret_cast<float*>(lds) + wave * 4096;
 #pragma unroll
-  for (int mt = 0; mt < 8; ++mt) {
+  for (int pass = 0; pass < 2; ++pass) {
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt) {
-      const int cl = cbase + 16 * nt;
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int lr = 16 * mt + 4 * fk + r;
+          stage[lr * 64 + ((16 * nt + fr) ^ (((lr >> 2) & 1) << 4))] = acc[4 * pass + mt][nt][r];
+        }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int lr = 4 * i + (lane >> 4), cc = lane & 15;
+      const f32x4 v4 = *reinterpret_cast<const f32x4*>(stage + lr * 64 + 4 * (cc ^ (((lr >> 2) & 1) << 2)));
+      const int rl = 128 * wr + 64 * pass + lr, cl = 64 * wc + 4 * cc;   // within the tile
       if (part != nullptr) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) part[(rbase + 16 * mt + r) * BG_N + cl] = acc[mt][nt][r];
+        *reinterpret_cast<f32x4*>(part + rl * BG_N + cl) = v4;
         continue;
       }
-      const int col = n0 + cl;
-      if (col >= N) continue;
-      const float bv = bias != nullptr ? bias[col] : 0.f;
+      const int row = m0 + rl, col = n0 + cl;
+      if (row >= M || col >= N) continue;
+      float* cp = C + (int64_t)row * ldc + col;
+      if (cvec && col + 3 < N) {
+        f32x4 o = v4 * alpha;
+        if (bias != nullptr) o += *reinterpret_cast<const f32x4*>(bias + col);
+        if (beta != 0.f) o += beta * *reinterpret_cast<const f32x4*>(cp);
+        *reinterpret_cast<f32x4*>(cp) = o;
+      } else {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = m0 + rbase + 16 * mt + r;
-        if (row < M) {
-          float* cp = C + (int64_t)row * ldc + col;
-          float v = alpha * acc[mt][nt][r] + bv;
-          if (beta != 0.f) v += beta * *cp;
-          *cp = v;
+        for (int e = 0; e < 4; ++e) {
+          if (col + e >= N) break;
+          float o = alpha * v4[e] + (bias != nullptr ? bias[col + e] : 0.f);
+          if (beta != 0.f) o += beta * cp[e];
+          cp[e] = o;
         }
       }
     }
@@ -411,18 +447,21 @@ ds2_status_t ds2_bgemm_nt(int m, int n, int k, float alpha, const void* a, int64
   if (nwg > 0x7fffffff) return DS2_UNSUPPORTED_SHAPE;
   hipStream_t st = as_stream(stream);
   const bool kalign = k % BG_K == 0 && p.kchunk % BG_K == 0;
+  // 16-B row runs of C (and of bias) when every row starts 16-B aligned
+  const int cvec = !((reinterpret_cast<uintptr_t>(c) & 15) || (ldc & 3) ||
+                     (bias != nullptr && (reinterpret_cast<uintptr_t>(bias) & 15)));
   const unsigned short* A = static_cast<const unsigned short*>(a);
   const unsigned short* B = static_cast<const unsigned short*>(b);
   if (kalign)
     hipLaunchKernelGGL(bgemm_nt_kernel<false>, dim3(static_cast<unsigned>(nwg)), dim3(BG_T), 0, st,
                        m, n, k, alpha, A, static_cast<int>(lda), B, static_cast<int>(ldb), beta, c,
                        ldc, bias, p.main_wgs, p.tail_tile0, p.tail_tiles, p.nsplit, p.kchunk,
-                       partial);
+                       partial, cvec);
   else
     hipLaunchKernelGGL(bgemm_nt_kernel<true>, dim3(static_cast<unsigned>(nwg)), dim3(BG_T), 0, st,
                        m, n, k, alpha, A, static_cast<int>(lda), B, static_cast<int>(ldb), beta, c,
                        ldc, bias, p.main_wgs, p.tail_tile0, p.tail_tiles, p.nsplit, p.kchunk,
-                       partial);
+                       partial, cvec);
   if (p.nsplit > 1) {
     const int64_t total = (int64_t)p.tail_tiles * BG_M * BG_N;
     const int g = static_cast<int>(std::min<int64_t>(cdiv(total, 256), 4096));

@@ -312,39 +312,105 @@ __device__ __forceinline__ bool beam_better(float s1, int key1, float s2, int ke
   return s1 > s2 || (s1 == s2 && key1 < key2);
 }
 
-// one step of a wave arg-best over (score, key) through a DPP lane pattern (no LDS)
-template <int CTRL>
-__device__ __forceinline__ void beam_dpp_step(float& bs, int& bk) {
-  const float os = __builtin_bit_cast(
-      float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, bs), CTRL, 0xF, 0xF, false));
-  const int ok = __builtin_amdgcn_update_dpp(0, bk, CTRL, 0xF, 0xF, false);
-  if (beam_better(os, ok, bs, bk)) {
-    bs = os;
-    bk = ok;
-  }
+// (score, key) packed so that beam_better is the unsigned 64-bit order: the score's bits made
+// order-preserving in the high word (-0 read as +0, which beam_better calls equal), the key
+// reversed in the low word; -inf and NaN (never selected) pack to 0, below every candidate
+__device__ __forceinline__ unsigned long long beam_pack(float s, int key) {
+  if (!(s > -INFINITY)) return 0ull;
+  unsigned b = __float_as_uint(s + 0.0f);
+  b = (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+  return (static_cast<unsigned long long>(b) << 32) | (0xFFFFFFFFu - static_cast<unsigned>(key));
 }
 
-// the wave's best (score, key) -- a strict order (keys are unique), so any reduction tree
-// gives the same winner: xor 1 and xor 2 within quads, half-row and row mirrors (best of
-// each 16-lane row), then the four row winners through v_readlane
-__device__ __forceinline__ void beam_wave_best(float& bs, int& bk) {
-  beam_dpp_step<0xB1>(bs, bk);    // quad_perm [1,0,3,2]
-  beam_dpp_step<0x4E>(bs, bk);    // quad_perm [2,3,0,1]
-  beam_dpp_step<0x141>(bs, bk);   // row_half_mirror
-  beam_dpp_step<0x140>(bs, bk);   // row_mirror
-  float best = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, bs), 0));
-  int key = __builtin_amdgcn_readlane(bk, 0);
+// one step of a wave max over packed keys through a DPP lane pattern (no LDS)
+template <int CTRL>
+__device__ __forceinline__ void beam_dpp_step(unsigned long long& v) {
+  const unsigned lo = static_cast<unsigned>(
+      __builtin_amdgcn_update_dpp(0, static_cast<int>(static_cast<unsigned>(v)), CTRL, 0xF, 0xF, false));
+  const unsigned hi = static_cast<unsigned>(
+      __builtin_amdgcn_update_dpp(0, static_cast<int>(static_cast<unsigned>(v >> 32)), CTRL, 0xF, 0xF, false));
+  const unsigned long long o = (static_cast<unsigned long long>(hi) << 32) | lo;
+  v = o > v ? o : v;
+}
+
+// beam_dpp_step over the rows in ROW_MASK only (the other lanes keep their value)
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ void beam_dpp_step_rows(unsigned long long& v) {
+  const int vlo = static_cast<int>(static_cast<unsigned>(v));
+  const int vhi = static_cast<int>(static_cast<unsigned>(v >> 32));
+  const unsigned lo = static_cast<unsigned>(__builtin_amdgcn_update_dpp(vlo, vlo, CTRL, ROW_MASK, 0xF, false));
+  const unsigned hi = static_cast<unsigned>(__builtin_amdgcn_update_dpp(vhi, vhi, CTRL, ROW_MASK, 0xF, false));
+  const unsigned long long o = (static_cast<unsigned long long>(hi) << 32) | lo;
+  v = o > v ? o : v;
+}
+
+// the wave's largest packed key (uniform) -- keys are unique, so any reduction tree gives the
+// same winner: xor 1 and xor 2 within quads, half-row and row mirrors (every lane of a 16-lane
+// row holds the row's best), then row_bcast:15 into rows 1 and 3 and row_bcast:31 into rows 2
+// and 3 (lane 63 holds the wave's best) -- all in VALU, one v_readlane pair at the end
+__device__ __forceinline__ unsigned long long beam_wave_best(unsigned long long v) {
+  beam_dpp_step<0xB1>(v);              // quad_perm [1,0,3,2]
+  beam_dpp_step<0x4E>(v);              // quad_perm [2,3,0,1]
+  beam_dpp_step<0x141>(v);             // row_half_mirror
+  beam_dpp_step<0x140>(v);             // row_mirror
+  beam_dpp_step_rows<0x142, 0xA>(v);   // row_bcast:15
+  beam_dpp_step_rows<0x143, 0xC>(v);   // row_bcast:31
+  const unsigned lo = static_cast<unsigned>(__builtin_amdgcn_readlane(static_cast<int>(static_cast<unsigned>(v)), 63));
+  const unsigned hi = static_cast<unsigned>(__builtin_amdgcn_readlane(static_cast<int>(static_cast<unsigned>(v >> 32)), 63));
+  return (static_cast<unsigned long long>(hi) << 32) | lo;
+}
+
+// keep the best `beam` of the tot candidates whose packed keys are ukey[0, tot): lane l holds
+// keys l, l + 64, ... in NJ registers (NJ >= the filled slots; the rest hold 0).  A round is a
+// wave max of the lanes' best keys, then the lane holding the (unique) winner drops it.  For
+// NJ <= 8 a lane's keys are sorted once (odd-even transposition), so its best is always slot
+// 0 and the drop is a shift; wider lanes rescan.  No barrier, no LDS traffic inside the
+// rounds.  Writes the winners' candidate indices to sel_k in rank order.
+template <int NJ>
+__device__ __forceinline__ int beam_select(const unsigned long long* ukey, int tot, int beam,
+                                           int* sel_k, int lane) {
+  unsigned long long ru[NJ];
 #pragma unroll
-  for (int r = 16; r < 64; r += 16) {
-    const float s2 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, bs), r));
-    const int k2 = __builtin_amdgcn_readlane(bk, r);
-    if (beam_better(s2, k2, best, key)) {
-      best = s2;
-      key = k2;
-    }
+  for (int jj = 0; jj < NJ; ++jj) {
+    const int k = lane + 64 * jj;
+    ru[jj] = k < tot ? ukey[k] : 0ull;
   }
-  bs = best;
-  bk = key;
+  constexpr bool kSorted = NJ <= 8;
+  unsigned long long lbest = 0ull;
+  if constexpr (kSorted) {
+#pragma unroll
+    for (int p = 0; p < NJ; ++p)
+#pragma unroll
+      for (int j = p & 1; j + 1 < NJ; j += 2) {
+        const unsigned long long x = ru[j], y = ru[j + 1];
+        ru[j] = x > y ? x : y;
+        ru[j + 1] = x > y ? y : x;
+      }
+  } else {
+#pragma unroll
+    for (int jj = 0; jj < NJ; ++jj) lbest = ru[jj] > lbest ? ru[jj] : lbest;
+  }
+  int nsel = 0;
+  for (int r = 0; r < beam; ++r) {
+    const unsigned long long b = beam_wave_best(kSorted ? ru[0] : lbest);
+    if (b == 0ull) break;
+    if constexpr (kSorted) {
+      const bool own = ru[0] == b;
+#pragma unroll
+      for (int jj = 0; jj + 1 < NJ; ++jj) ru[jj] = own ? ru[jj + 1] : ru[jj];
+      ru[NJ - 1] = own ? 0ull : ru[NJ - 1];
+    } else {
+      lbest = 0ull;
+#pragma unroll
+      for (int jj = 0; jj < NJ; ++jj) {
+        ru[jj] = ru[jj] == b ? 0ull : ru[jj];
+        lbest = ru[jj] > lbest ? ru[jj] : lbest;
+      }
+    }
+    if (lane == 0) sel_k[r] = static_cast<int>((0xFFFFFFFFu - static_cast<unsigned>(b)) & 4095u);
+    ++nsel;
+  }
+  return nsel;
 }
 
 // Word n-gram LM of the beam search (ctcdecode's KenLM Scorer, decoder.py:90-99 with
@@ -491,6 +557,8 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
   __shared__ int pidx[BM];
   __shared__ signed char child_of[BM * CM];
   __shared__ float cpb[BM * CM], cpnb[BM * CM];
+  __shared__ unsigned long long ukey[BM * CM];   // beam_pack(score, key) per candidate k
+  __shared__ float bl_sc[BM], bl_pb[BM], bl_pnb[BM];   // the blank candidate of each entry
   __shared__ int sel_k[BM];
   __shared__ int s_nb, s_nodes, s_nr;
   // trie revival: per entry its node's alive-children chars; the attempted extensions onto
@@ -653,68 +721,76 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
         }
       }
     }
+    // ---- the blank candidate of every entry (one per entry: lane e scores entry e's; its
+    // "stay" terms and the merge of the entry's parent's extension by the entry's last char)
+#pragma unroll
+    for (int q = 0; q < EPL; ++q) {
+      const int i = lane + 64 * q;
+      if (i < nb) {
+        const int last_i = b_last[cur][i];
+        const float sc_i = score[i];
+        // with an LM a (prefix, char) pair below the pruning bound is skipped entirely
+        const float pb = (allowed[blank] && !(lp[blank] + sc_i < cut)) ? lp[blank] + sc_i : -INFINITY;
+        float pnb = (last_i >= 0 && allowed[last_i] && !(lp[last_i] + sc_i < cut))
+                        ? lp[last_i] + b_pnb[cur][i] : -INFINITY;
+        const int jp = pidx[i];
+        if (jp >= 0 && allowed[last_i] && !(lp[last_i] + score[jp] < cut)) {
+          float e = (last_i == b_last[cur][jp])
+                        ? (b_pb[cur][jp] != -INFINITY ? lp[last_i] + b_pb[cur][jp] : -INFINITY)
+                        : lp[last_i] + score[jp];
+          if (LM && last_i == L.space) e = lm_add(e, b_lms[cur][jp], L.beta);
+          pnb = beam_lse(pnb, e);
+          const int nd = b_node[cur][i];
+          if (lp[last_i] > b_lpc[cur][i]) {
+            b_lpc[cur][i] = lp[last_i];
+            lpcv[nd] = lp[last_i];
+            tst[nd] = t;
+          }
+        }
+        bl_pb[i] = pb;
+        bl_pnb[i] = pnb;
+        bl_sc[i] = beam_lse(pb, pnb);
+      }
+    }
     __syncthreads();
     BEAM_STAMP(2)
-    // ---- candidates, scored straight into registers: lane holds k = lane + 64 jj (the
-    // selection below scans them there); the unrolled loop lets the LDS reads of several
-    // candidates overlap.  (i, c) = divmod(k, C) advanced incrementally.
-    constexpr int SJ = BM * CM / 64;
-    const int jn = (nb * C + 63) / 64;                   // wave-uniform
-    float rs[SJ];
-    int rk[SJ];
+    // ---- candidates k = i * C + c: lane (g, c) = divmod(lane, CM) scores char c of the entries
+    // i = G jj + g, so the char's log prob and pruning flag stay in registers and every
+    // per-entry read is one LDS address per lane group (a broadcast); packed keys go to
+    // ukey[k] for the selection
     {
-      int i = lane / C;
-      int c = lane - i * C;
-      const int di = 64 / C, dc = 64 - (64 / C) * C;
+      constexpr int G = 64 / CM, SJ = BM / G;
+      const int c = lane % CM, g = lane / CM;
+      const bool cv = c < C;
+      const float lpc = cv ? lp[c] : 0.f;
+      const bool alc = cv && c != blank && allowed[c];
+      const int jn = (nb + G - 1) / G;                  // wave-uniform
 #pragma unroll
       for (int jj = 0; jj < SJ; ++jj) {
-        rs[jj] = -INFINITY;
-        rk[jj] = 0x7fffffff;
         if (jj >= jn) continue;
-        const int k = lane + 64 * jj;
-        if (k < nb * C) {
-          const int last_i = b_last[cur][i];
-          const float pb_i = b_pb[cur][i];
-          float sc = -INFINITY, pb = -INFINITY, pnb = -INFINITY;
-          // with an LM a (prefix, char) pair below the pruning bound is skipped entirely
+        const int i = G * jj + g;
+        if (!cv || i >= nb) continue;
+        const int k = i * C + c;
+        const int last_i = b_last[cur][i];
+        float sc = -INFINITY, pb = -INFINITY, pnb = -INFINITY;
+        if (c == blank) {
+          pb = bl_pb[i];
+          pnb = bl_pnb[i];
+          sc = bl_sc[i];
+        } else {
           const float sc_i = score[i];
-          if (c == blank) {
-            pb = (allowed[blank] && !(lp[blank] + sc_i < cut)) ? lp[blank] + sc_i : -INFINITY;
-            pnb = (last_i >= 0 && allowed[last_i] && !(lp[last_i] + sc_i < cut))
-                      ? lp[last_i] + b_pnb[cur][i] : -INFINITY;
-            const int jp = pidx[i];
-            if (jp >= 0 && allowed[last_i] && !(lp[last_i] + score[jp] < cut)) {
-              float e = (last_i == b_last[cur][jp])
-                            ? (b_pb[cur][jp] != -INFINITY ? lp[last_i] + b_pb[cur][jp] : -INFINITY)
-                            : lp[last_i] + score[jp];
-              if (LM && last_i == L.space) e = lm_add(e, b_lms[cur][jp], L.beta);
-              pnb = beam_lse(pnb, e);
-              const int nd = b_node[cur][i];
-              if (lp[last_i] > b_lpc[cur][i]) {   // one blank candidate per entry: no race
-                b_lpc[cur][i] = lp[last_i];
-                lpcv[nd] = lp[last_i];
-                tst[nd] = t;
-              }
-            }
-            sc = beam_lse(pb, pnb);
-          } else if (allowed[c] && child_of[k] < 0 &&
-                     (!LM || (!(lp[c] + sc_i < cut) && ((vmask[i] >> c) & 1ull)))) {
-            pnb = (c == last_i) ? (pb_i != -INFINITY ? lp[c] + pb_i : -INFINITY) : lp[c] + sc_i;
+          if (alc && child_of[k] < 0 &&
+              (!LM || (!(lpc + sc_i < cut) && ((vmask[i] >> c) & 1ull)))) {
+            const float pb_i = b_pb[cur][i];
+            pnb = (c == last_i) ? (pb_i != -INFINITY ? lpc + pb_i : -INFINITY) : lpc + sc_i;
             if (LM && c == L.space) pnb = lm_add(pnb, b_lms[cur][i], L.beta);
             sc = pnb;
             if ((b_km[i] >> c) & 1ull) rlist[atomicAdd(&s_nr, 1)] = k;   // revival attempt
           }
-          cpb[k] = pb;
-          cpnb[k] = pnb;
-          rs[jj] = sc;
-          rk[jj] = ((c == blank ? last_i : c) + 1) * 4096 + k;
         }
-        i += di;
-        c += dc;
-        if (c >= C) {
-          c -= C;
-          ++i;
-        }
+        cpb[k] = pb;
+        cpnb[k] = pnb;
+        ukey[k] = beam_pack(sc, ((c == blank ? last_i : c) + 1) * 4096 + k);
       }
     }
     __syncthreads();
@@ -731,32 +807,15 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
       }
     }
     BEAM_STAMP(4)
-    // ---- keep the best `beam` candidates: a selection round is a register scan + a wave
-    // arg-best, with no LDS traffic and no barrier
-    int nsel = 0;
-    for (int r = 0; r < beam; ++r) {
-      float bs = -INFINITY;
-      int bkey = 0x7fffffff;
-#pragma unroll
-      for (int jj = 0; jj < SJ; ++jj) {
-        // slots past jn hold -inf; the early exit only where the unroller accepts it
-        if (SJ <= 32 && jj >= jn) break;
-        if (rs[jj] != -INFINITY && beam_better(rs[jj], rk[jj], bs, bkey)) {
-          bs = rs[jj];
-          bkey = rk[jj];
-        }
-      }
-      beam_wave_best(bs, bkey);
-      if (bs == -INFINITY) break;
-      const int k = bkey & 4095;
-#pragma unroll
-      for (int jj = 0; jj < SJ; ++jj) {
-        if (SJ <= 32 && jj >= jn) break;
-        if (lane + 64 * jj == k) rs[jj] = -INFINITY;
-      }
-      if (lane == 0) sel_k[r] = k;
-      ++nsel;
-    }
+    // ---- keep the best `beam` candidates (beam_select, its registers sized to the filled slots)
+    constexpr int SD = BM * CM / 64;
+    const int tot = nb * C;
+    const int jd = (tot + 63) / 64;
+    const int nsel = jd <= 2    ? beam_select<2>(ukey, tot, beam, sel_k, lane)
+                     : jd <= 4  ? beam_select<4>(ukey, tot, beam, sel_k, lane)
+                     : jd <= 8  ? beam_select<8>(ukey, tot, beam, sel_k, lane)
+                     : jd <= 16 ? beam_select<16>(ukey, tot, beam, sel_k, lane)
+                                : beam_select<SD>(ukey, tot, beam, sel_k, lane);
     __syncthreads();
     BEAM_STAMP(5)
     // ---- new beam: lane r builds entries r, r + 64, ...; new prefixes get trie nodes in

@@ -1,0 +1,124 @@
+"""Where does the bs32 full-step gradient difference come from?  (test_gpu_train.py::
+test_benchmark_batch_train_step_matches_oracle: conv.seq_module.0.weight at 9.2e-4 of its max vs
+the 5e-4 bound, everything else inside it.)
+
+  --mode gpu --tag T    one Trainer.train_batch on the test's batch (bs 32, T = 1001, 150 labels,
+                        seed 13) with whatever DS2_*_X6 switches the environment sets; gradients
+                        to gpurun_out/bs32_T.pt
+  --mode oracle         the same step on the CPU oracle (fp32) -> gpurun_out/bs32_oracle.pt, and
+                        how many hardtanh(0, 20) derivative masks of the two conv blocks differ
+                        between that fp32 forward and an fp64 forward of the same weights
+                        (each flipped element moves its layer's weight gradient by one
+                        position's dy * x)
+  --mode compare        max |a - b| / max |b| per parameter for every pair of saved runs
+"""
+import argparse
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "deepspeech.pytorch_amd"))
+sys.path.insert(0, REPO)
+import torch  # noqa: E402
+import torch.nn.functional as F  # noqa: E402
+
+from oracle import ds2_oracle as orc  # noqa: E402
+
+OUT = os.path.join(REPO, "gpurun_out")
+CONF = dict(sample_rate=16000, window_size=0.02, window_stride=0.01, window='hamming')
+
+
+def batch():
+    g = torch.Generator().manual_seed(13)
+    t_list, lab = [1001] * 32, [150] * 32
+    x = torch.zeros(32, 1, 161, 1001)
+    for i, t in enumerate(t_list):
+        x[i, 0, :, :t] = torch.randn(161, t, generator=g)
+    tg = []
+    for L in lab:
+        prev = -1
+        for _ in range(L):
+            v = int(torch.randint(1, 29, (1,), generator=g))
+            while v == prev:
+                v = int(torch.randint(1, 29, (1,), generator=g))
+            tg.append(v)
+            prev = v
+    pct = torch.tensor([t / 1001.0 for t in t_list], dtype=torch.float32)
+    return x, torch.tensor(tg, dtype=torch.int32), torch.tensor(lab, dtype=torch.int32), pct
+
+
+def build():
+    from ds2amd import model as dsm
+    torch.manual_seed(123456)
+    return dsm.DeepSpeech(rnn_type='gru', labels=orc.LABELS, rnn_hidden_size=800, nb_layers=5,
+                          audio_conf=CONF, bidirectional=True)
+
+
+def conv_masks(o, x, lens, dtype):
+    sd = {k: v.to(dtype) if v.is_floating_point() else v for k, v in o.sd.items()}
+    out_lens = orc.get_seq_lens(lens)
+    masks = []
+    h = x.to(dtype)
+    for conv, bn, stride, pad in (("0", "1", (2, 2), (20, 5)), ("3", "4", (2, 1), (10, 5))):
+        h = F.conv2d(h, sd[f'conv.seq_module.{conv}.weight'], sd[f'conv.seq_module.{conv}.bias'],
+                     stride=stride, padding=pad)
+        h = orc._mask_time(h, out_lens)
+        h = F.batch_norm(h, None, None, sd[f'conv.seq_module.{bn}.weight'],
+                         sd[f'conv.seq_module.{bn}.bias'], training=True, eps=1e-5)
+        h = orc._mask_time(h, out_lens)
+        masks.append((h > 0) & (h < 20))
+        h = orc._mask_time(F.hardtanh(h, 0, 20), out_lens)
+    return masks
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--mode", choices=["gpu", "oracle", "compare"], required=True)
+    ap.add_argument("--tag", default="x6")
+    args = ap.parse_args()
+    os.makedirs(OUT, exist_ok=True)
+    x, tg, tl, pct = batch()
+    if args.mode == "gpu":
+        from ds2amd.trainer import Trainer
+        dev = torch.device("cuda", 0)
+        m = build()
+        tr = Trainer(m, orc.LABELS, lr=3e-4, momentum=0.9, max_norm=100.0, device=dev)
+        loss = tr.train_batch((x, tg, None, pct.clone(), tl), return_item=True)
+        grads = {n: p.grad.detach().cpu().clone() for n, p in m.named_parameters()}
+        torch.save({"loss": loss, "grads": grads}, os.path.join(OUT, f"bs32_{args.tag}.pt"))
+        print(f"{args.tag}: loss {loss:.6f}", flush=True)
+    elif args.mode == "oracle":
+        torch.set_num_threads(16)
+        m = build()
+        o = orc.OracleDS2({k: v.detach().clone() for k, v in m.state_dict().items()}, 5, 800)
+        lens = orc.input_sizes_quirk(pct.clone(), 1001)
+        m32 = conv_masks(o, x, lens, torch.float32)
+        m64 = conv_masks(o, x, lens, torch.float64)
+        for i, (a, b) in enumerate(zip(m32, m64)):
+            print(f"conv block {i + 1}: {int((a != b).sum())} of {a.numel()} hardtanh masks differ "
+                  f"between the fp32 and fp64 forward", flush=True)
+        rloss, _, _, rgrads, _ = orc.train_step(o, x, pct.clone(), tg, tl)
+        torch.save({"loss": float(rloss), "grads": {k: torch.as_tensor(v) for k, v in rgrads.items()}},
+                   os.path.join(OUT, "bs32_oracle.pt"))
+        print(f"oracle: loss {float(rloss):.6f}", flush=True)
+    else:
+        runs = {}
+        for f in sorted(os.listdir(OUT)):
+            if f.startswith("bs32_") and f.endswith(".pt"):
+                runs[f[5:-3]] = torch.load(os.path.join(OUT, f), weights_only=True)
+        names = list(next(iter(runs.values()))["grads"].keys())
+        keys = sorted(runs)
+        for i, a in enumerate(keys):
+            for b in keys[i + 1:]:
+                worst = []
+                for n in names:
+                    ga = runs[a]["grads"][n].double()
+                    gb = runs[b]["grads"][n].double()
+                    worst.append(((ga - gb).abs().max() / gb.abs().max().clamp_min(1e-30)).item())
+                top = sorted(zip(worst, names), reverse=True)[:4]
+                print(f"{a} vs {b}: loss {runs[a]['loss']:.6f} / {runs[b]['loss']:.6f}; worst "
+                      + ", ".join(f"{n} {w:.2e}" for w, n in top), flush=True)
+
+
+if __name__ == "__main__":
+    main()
