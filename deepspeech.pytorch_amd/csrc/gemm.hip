@@ -11,6 +11,8 @@
 // (+2 floats) makes those 8 ds_write_b32 per thread conflict-free.
 #include "common.h"
 
+#include <type_traits>
+
 #include <algorithm>
 #include <cstdlib>
 
@@ -664,6 +666,15 @@ constexpr int XS = 32;                  // k per stage
 // (row >> 2) & 3 left the row-contiguous stores 4-way conflicted (12 % of LDS cycles).
 __device__ __forceinline__ int xswz(int row) { return ((row >> 2) & 1) | ((((row >> 1) ^ (row >> 3)) & 1) << 1); }
 __device__ __forceinline__ int xslot(int row, int s) { return row * XS + 8 * (s ^ xswz(row)); }
+// the v_mfma_f32_16x16x32_bf16 form (M16): a fragment is 16 rows x one 8-k slot per 16-lane
+// quarter (lane (row l & 15, slot l >> 4)); slot s of row r at s ^ ((r >> 1) & 3) keeps its
+// ds_read_b128 lane groups, the 8-lane groups of the (row, slot)-unit stores and those of the
+// 8-consecutive-row stores of row-contiguous operands on distinct banks
+template <bool M16>
+__device__ __forceinline__ int xslot_t(int row, int s) {
+  if constexpr (M16) return row * XS + 8 * (s ^ ((row >> 1) & 3));
+  else return xslot(row, s);
+}
 
 // The default bf16x6 kernel: tile 256 x 128, eight waves (two per SIMD) of 2 x 2 32x32
 // tiles on v_mfma_f32_32x32x16_bf16 (which holds the SIMD's vector issue for 8 of its 32
@@ -771,7 +782,7 @@ __device__ __forceinline__ void x2_split_store(unsigned short* __restrict__ s, i
   }
 }
 
-template <bool KC, int ROWS, int NPL = 3>
+template <bool KC, int ROWS, int NPL = 3, bool M16 = false>
 __device__ __forceinline__ void x2_store(unsigned short* __restrict__ s,
                                          const float (&v)[X2Op<KC, ROWS>::F]) {
   using O = X2Op<KC, ROWS>;
@@ -780,13 +791,13 @@ __device__ __forceinline__ void x2_store(unsigned short* __restrict__ s,
 #pragma unroll
     for (int u = 0; u < O::SL; ++u) {
       const int unit = t + X2T * u;
-      x2_split_store<NPL>(s, O::P, xslot(unit >> 2, unit & 3), v + 8 * u);
+      x2_split_store<NPL>(s, O::P, xslot_t<M16>(unit >> 2, unit & 3), v + 8 * u);
     }
   } else {
     const int r = t % ROWS;
 #pragma unroll
     for (int u = 0; u < O::SL; ++u)
-      x2_split_store<NPL>(s, O::P, xslot(r, O::SL * (t / ROWS) + u), v + 8 * u);
+      x2_split_store<NPL>(s, O::P, xslot_t<M16>(r, O::SL * (t / ROWS) + u), v + 8 * u);
   }
 }
 
@@ -798,6 +809,16 @@ __device__ __forceinline__ void x2_mma6(const bf16x8 (&a)[3], const bf16x8 (&b)[
   c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[0], c, 0, 0, 0);
   c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[1], c, 0, 0, 0);
   c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], c, 0, 0, 0);
+}
+
+// the same on the 16x16x32 form
+__device__ __forceinline__ void x2_mma6_16(const bf16x8 (&a)[3], const bf16x8 (&b)[3], f32x4& c) {
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[1], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], b[0], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[2], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[0], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[1], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[0], c, 0, 0, 0);
 }
 
 // B stages of 160 rows (N = 800 / 2400 without a partial tile column): 640 (row, 8-k slot)
@@ -845,23 +866,23 @@ __device__ __forceinline__ void x2_load160(__amdgpu_buffer_rsrc_t rs, int ld, co
   }
 }
 
-template <bool KC, int NPL = 3>
+template <bool KC, int NPL = 3, bool M16 = false>
 __device__ __forceinline__ void x2_store160(unsigned short* __restrict__ s, const float (&v)[16]) {
   constexpr int P = 160 * XS;
   const int t = threadIdx.x;
   if (KC) {
-    x2_split_store<NPL>(s, P, xslot(t >> 2, t & 3), v);
-    if (t < 128) x2_split_store<NPL>(s, P, xslot((t + X2T) >> 2, (t + X2T) & 3), v + 8);
+    x2_split_store<NPL>(s, P, xslot_t<M16>(t >> 2, t & 3), v);
+    if (t < 128) x2_split_store<NPL>(s, P, xslot_t<M16>((t + X2T) >> 2, (t + X2T) & 3), v + 8);
   } else {
-    x2_split_store<NPL>(s, P, xslot(t & 127, t >> 7), v);
-    if (t < 128) x2_split_store<NPL>(s, P, xslot(128 + (t & 31), (t >> 5) & 3), v + 8);
+    x2_split_store<NPL>(s, P, xslot_t<M16>(t & 127, t >> 7), v);
+    if (t < 128) x2_split_store<NPL>(s, P, xslot_t<M16>(128 + (t & 31), (t >> 5) & 3), v + 8);
   }
 }
 
 // NPL 3: the bf16x6 fp32-accurate GEMM; NPL 1: the bf16-operand GEMM (operands rounded to
 // bf16 while staged, one product per fragment pair, fp32 accumulation -- cfg4's opt-in
 // precision), one LDS plane per operand
-template <int TA, int TB, bool KCHK, int TBN, int NPL = 3>
+template <int TA, int TB, bool KCHK, int TBN, int NPL = 3, bool M16 = false>
 __global__ __launch_bounds__(X2T, 1) void sxgemm2_kernel(
     int M, int N, int K, float alpha, const float* __restrict__ A, int64_t lda, int64_t sA,
     const float* __restrict__ B, int64_t ldb, int64_t sB, float beta, float* __restrict__ C,
@@ -870,8 +891,12 @@ __global__ __launch_bounds__(X2T, 1) void sxgemm2_kernel(
   constexpr bool AK = (TA == 0);
   constexpr bool BKc = (TB == 1);
   static_assert(TBN == 128 || TBN == 160, "tile width");
-  // waves: 4 (M) x 2 (N) of 2 x 2 32x32 tiles (TBN 128) or 8 (M) x 1 (N) of 1 x 5 (TBN 160)
-  constexpr int WMT = TBN == 128 ? 2 : 1, WNT = TBN == 128 ? 2 : 5;
+  // waves: 4 (M) x 2 (N) of 2 x 2 32x32 tiles (TBN 128) or 8 (M) x 1 (N) of 1 x 5 (TBN 160);
+  // M16: the same wave tiles as 4 x 4 / 2 x 10 16x16 tiles
+  constexpr int TS = M16 ? 16 : 32;   // MFMA tile edge
+  constexpr int WMT = (TBN == 128 ? 64 : 32) / TS, WNT = (TBN == 128 ? 64 : 160) / TS;
+  using AccT = typename std::conditional<M16, f32x4, f32x16>::type;
+  constexpr int AR = M16 ? 4 : 16;    // accumulator registers per tile
   constexpr int BP = TBN * XS;             // bf16 per B plane
   constexpr int BF = TBN == 128 ? 8 : 16;  // B floats per thread per stage
   using OA = X2Op<AK, X2M>;
@@ -937,13 +962,13 @@ __global__ __launch_bounds__(X2T, 1) void sxgemm2_kernel(
     }
   }
 
-  f32x16 acc[WMT][WNT];
+  AccT acc[WMT][WNT];
 #pragma unroll
   for (int i = 0; i < WMT; ++i)
 #pragma unroll
     for (int j = 0; j < WNT; ++j)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+      for (int r = 0; r < AR; ++r) acc[i][j][r] = 0.f;
 
   // two register sets: stage kt + 2's loads are issued at the top of stage kt (a whole
   // stage of latency) while the split of stage kt + 1 reads the other set
@@ -957,9 +982,9 @@ __global__ __launch_bounds__(X2T, 1) void sxgemm2_kernel(
   };
   auto bstore = [&](unsigned short* dst, const float (&vb)[BF]) {
     if constexpr (TBN == 128)
-      x2_store<BKc, TBN, NPL>(dst, vb);
+      x2_store<BKc, TBN, NPL, M16>(dst, vb);
     else
-      x2_store160<BKc, NPL>(dst, vb);
+      x2_store160<BKc, NPL, M16>(dst, vb);
   };
   auto body = [&](int kt, int cur, float (&la)[OA::F], float (&lb)[BF],
                   const float (&sa)[OA::F], const float (&sb)[BF]) {
@@ -968,6 +993,47 @@ __global__ __launch_bounds__(X2T, 1) void sxgemm2_kernel(
     load(kbeg + (kt + 2) * XS, la, lb);          // stages past kend load as zeros
     const unsigned short* as = As[cur];
     const unsigned short* bs = Bs[cur];
+    if constexpr (M16) {
+      static_assert(NPL == 3, "M16: bf16x6 only");
+      // one k-step of 32 per stage: the A fragments, then per B fragment (its three planes
+      // read two fragments ahead) the WMT x 6 MFMAs it feeds, with the split VALU of stage
+      // kt + 1 and its LDS stores interleaved
+      const int r16 = lane & 15, s16 = lane >> 4;
+      bf16x8 af[WMT][3];
+#pragma unroll
+      for (int i = 0; i < WMT; ++i) {
+        const int at = xslot_t<true>(wm + 16 * i + r16, s16);
+#pragma unroll
+        for (int p = 0; p < 3; ++p) af[i][p] = *reinterpret_cast<const bf16x8*>(as + p * X2_AP + at);
+      }
+#pragma unroll
+      for (int j = 0; j < WNT; ++j) {
+        bf16x8 bq[3];
+        const int bt = xslot_t<true>(wn + 16 * j + r16, s16);
+#pragma unroll
+        for (int p = 0; p < 3; ++p) bq[p] = *reinterpret_cast<const bf16x8*>(bs + p * BP + bt);
+#pragma unroll
+        for (int i = 0; i < WMT; ++i) x2_mma6_16(af[i], bq, acc[i][j]);
+      }
+      x2_store<AK, X2M, NPL, true>(As[cur ^ 1], sa);
+      bstore(Bs[cur ^ 1], sb);
+      constexpr int MPB = WMT * 6;   // MFMAs per B fragment
+      __builtin_amdgcn_sched_group_barrier(0x020, 32, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 3 * WMT + 6, 0);
+#pragma unroll
+      for (int j = 0; j < WNT; ++j) {
+#pragma unroll
+        for (int q = 0; q < MPB; q += 2) {   // 1.5 VALU per MFMA
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
+        }
+        if (j + 2 < WNT) __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
+        __builtin_amdgcn_sched_group_barrier(0x200, 2, 0);
+      }
+      return;
+    }
     constexpr int NMF = WMT * WNT * (NPL == 3 ? 6 : 1);   // MFMAs per k-step
     constexpr int NRD = (WMT + WNT) * NPL;                 // fragment reads per k-step
 #pragma unroll
@@ -989,14 +1055,15 @@ __global__ __launch_bounds__(X2T, 1) void sxgemm2_kernel(
       for (int i = 0; i < WMT; ++i)
 #pragma unroll
         for (int j = 0; j < WNT; ++j) {
-          if constexpr (NPL == 3)
+          if constexpr (M16) {
+          } else if constexpr (NPL == 3)
             x2_mma6(af[i], bfr[j], acc[i][j]);
           else
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][0], bfr[j][0], acc[i][j], 0, 0, 0);
         }
     }
     // stage kt + 1 -> the other buffer (a stage past the end writes zeros nobody reads)
-    x2_store<AK, X2M, NPL>(As[cur ^ 1], sa);
+    x2_store<AK, X2M, NPL, M16>(As[cur ^ 1], sa);
     bstore(Bs[cur ^ 1], sb);
     // schedule: the loads, the first k-step's fragments, then each MFMA followed by up to
     // three VALU (the split of the next stage), the second k-step's fragments early, the
@@ -1018,7 +1085,7 @@ __global__ __launch_bounds__(X2T, 1) void sxgemm2_kernel(
   };
   const int ktiles = (kend - kbeg + XS - 1) / XS;
   load(kbeg, ra0, rb0);
-  x2_store<AK, X2M, NPL>(As[0], ra0);
+  x2_store<AK, X2M, NPL, M16>(As[0], ra0);
   bstore(Bs[0], rb0);
   load(kbeg + XS, ra1, rb1);
   for (int kt = 0; kt < ktiles; kt += 2) {
@@ -1026,6 +1093,36 @@ __global__ __launch_bounds__(X2T, 1) void sxgemm2_kernel(
     if (kt + 1 < ktiles) body(kt + 1, 1, ra1, rb1, ra0, rb0);
   }
 
+  if constexpr (M16) {
+    // epilogue (16x16 C/D map: col = lane & 15, row = 4 (lane >> 4) + r)
+#pragma unroll
+    for (int i = 0; i < WMT; ++i) {
+#pragma unroll
+      for (int j = 0; j < WNT; ++j) {
+        const int cl = wn + 16 * j + (lane & 15);
+        const int rb = wm + 16 * i + 4 * (lane >> 4);
+        if (part != nullptr) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) part[(rb + r) * TBN + cl] = acc[i][j][r];
+          continue;
+        }
+        const int col = n0 + cl;
+        if (col >= N) continue;
+        const float bv = bias != nullptr ? bias[col] : 0.f;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = m0 + rb + r;
+          if (row < M) {
+            float* cp = C + (int64_t)row * ldc + col;
+            float v = alpha * acc[i][j][r] + bv;
+            if (beta != 0.f) v += beta * *cp;
+            *cp = v;
+          }
+        }
+      }
+    }
+    return;
+  }
   // epilogue (32x32 C/D map: col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5))
 #pragma unroll
   for (int i = 0; i < WMT; ++i) {
@@ -1156,6 +1253,13 @@ static bool x6_enabled(bool va, bool vb) {
   return !(e != nullptr && e[0] == '0');
 }
 
+// A/B switch (experiment): DS2_GEMM_M16=1 runs the bf16x6 kernel on v_mfma_f32_16x16x32_bf16
+// (the same wave tiles as 16x16 tiles) where every stage lies inside K
+static bool m16_enabled() {
+  const char* e = getenv("DS2_GEMM_M16");
+  return e != nullptr && e[0] == '1';
+}
+
 // 32-bit buffer offsets: each operand (one batch entry) must span < 2^31 bytes
 static bool fits_rsrc(int64_t rows, int64_t ld) { return rows * ld * 4 < (1ll << 31); }
 
@@ -1277,15 +1381,19 @@ extern "C" ds2_status_t ds2_sgemm_ws(int trans_a, int trans_b, int m, int n, int
   hipStream_t st = as_stream(stream);
   // every stage of every piece lies wholly inside [0, K): no per-element k check
   const bool kalign = k % XS == 0 && (p.nsplit == 1 || p.kchunk % XS == 0);
-#define DS2_X6(TA_, TB_, KCHK_, BN_)                                                          \
-  hipLaunchKernelGGL((sxgemm2_kernel<TA_, TB_, KCHK_, BN_>), grid, dim3(X2T), 0, st, m, n, k,   \
-                     alpha, a, lda, stride_a, b, ldb, stride_b, beta, c, ldc, stride_c, bias,   \
-                     p.main_wgs, p.tail_tile0, p.tail_tiles, p.nsplit, p.kchunk, partial)
+#define DS2_X6(TA_, TB_, KCHK_, BN_, M16_)                                                    \
+  hipLaunchKernelGGL((sxgemm2_kernel<TA_, TB_, KCHK_, BN_, 3, M16_>), grid, dim3(X2T), 0, st,   \
+                     m, n, k, alpha, a, lda, stride_a, b, ldb, stride_b, beta, c, ldc,          \
+                     stride_c, bias, p.main_wgs, p.tail_tile0, p.tail_tiles, p.nsplit,          \
+                     p.kchunk, partial)
+  const bool m16 = x6 && kalign && m16_enabled();
 #define DS2_G(TA_, TB_)                                                                       \
-  if (x6 && kalign && p.bn == 160) DS2_X6(TA_, TB_, false, 160);                             \
-  else if (x6 && p.bn == 160) DS2_X6(TA_, TB_, true, 160);                                   \
-  else if (x6 && kalign) DS2_X6(TA_, TB_, false, 128);                                       \
-  else if (x6) DS2_X6(TA_, TB_, true, 128);                                                  \
+  if (m16 && p.bn == 160) DS2_X6(TA_, TB_, false, 160, true);                                \
+  else if (m16) DS2_X6(TA_, TB_, false, 128, true);                                          \
+  else if (x6 && kalign && p.bn == 160) DS2_X6(TA_, TB_, false, 160, false);                 \
+  else if (x6 && p.bn == 160) DS2_X6(TA_, TB_, true, 160, false);                            \
+  else if (x6 && kalign) DS2_X6(TA_, TB_, false, 128, false);                                \
+  else if (x6) DS2_X6(TA_, TB_, true, 128, false);                                           \
   else if (k64)                                                                               \
     launch_k64<TA_, TB_>(p.bn, grid, st, m, n, k, alpha, a, lda, stride_a, b, ldb, stride_b,   \
                          beta, c, ldc, stride_c, bias, p.main_wgs, p.tail_tile0, p.tail_tiles,  \

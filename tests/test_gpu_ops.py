@@ -25,16 +25,18 @@ def _close(got, ref, rel=1e-5, name=""):
 
 
 # ---------------------------------------------------------------------------- GEMM
-@pytest.mark.parametrize("x6", ["1", "0"])
+@pytest.mark.parametrize("x6", ["1", "0", "m16"])
 @pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
 @pytest.mark.parametrize("m,n,k", [(1, 1, 1), (37, 53, 29), (128, 128, 16), (300, 257, 513),
                                    (515, 2400, 132), (257, 300, 5000),   # split-K path
-                                   (300, 256, 516), (260, 132, 1000)])   # float4 staging, K % 32 != 0
+                                   (300, 256, 516), (260, 132, 1000),    # float4 staging, K % 32 != 0
+                                   (300, 260, 1024)])                    # K % 32 == 0
 def test_sgemm(dev, ta, tb, m, n, k, x6, monkeypatch):
     """ds2_sgemm_ws vs fp64 at 1e-5: the bf16x6 kernel (default for float4-staged operands;
-    256 x 160 tiles for N >= 256, 256 x 128 below) and the fp32-MFMA kernels
-    (DS2_GEMM_X6=0)."""
-    monkeypatch.setenv("DS2_GEMM_X6", x6)
+    256 x 160 tiles for N >= 256, 256 x 128 below), its 16x16x32 form (DS2_GEMM_M16=1, where
+    every stage lies inside K) and the fp32-MFMA kernels (DS2_GEMM_X6=0)."""
+    monkeypatch.setenv("DS2_GEMM_X6", "0" if x6 == "0" else "1")
+    monkeypatch.setenv("DS2_GEMM_M16", "1" if x6 == "m16" else "0")
     g = torch.Generator().manual_seed(m * 7 + n * 3 + k)
     a = torch.randn(k, m, generator=g) if ta else torch.randn(m, k, generator=g)
     b = torch.randn(n, k, generator=g) if tb else torch.randn(k, n, generator=g)
@@ -49,7 +51,8 @@ def test_sgemm(dev, ta, tb, m, n, k, x6, monkeypatch):
     _close(cd, ref, 1e-5, "sgemm")
 
 
-@pytest.mark.parametrize("mode", ["x6", "x6-narrow", "fp32", "fp32-narrow", "unaligned"])
+@pytest.mark.parametrize("mode", ["x6", "x6-narrow", "x6m16", "x6m16-narrow", "fp32",
+                                  "fp32-narrow", "unaligned"])
 @pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
 def test_sgemm_full_rounds_plus_split_tail(dev, ta, tb, mode, monkeypatch):
     """Whole rounds of resident workgroups + a tail whose K range is split (one launch) and
@@ -58,6 +61,7 @@ def test_sgemm_full_rounds_plus_split_tail(dev, ta, tb, mode, monkeypatch):
     16x16x4 with the plan's tile width, and ("unaligned": A one float off 16-B alignment)
     the BK = 16 / 32x32x2 kernel."""
     monkeypatch.setenv("DS2_GEMM_X6", "1" if mode.startswith("x6") else "0")
+    monkeypatch.setenv("DS2_GEMM_M16", "1" if mode.startswith("x6m16") else "0")
     m, k = 128 * 29, 2080
     n = 200 if mode.endswith("narrow") else 128 * 27 + 52
     g = torch.Generator().manual_seed(5)
@@ -93,13 +97,15 @@ def test_sgemm_x6_is_fp32_accurate(dev, ta, tb, m, n, k, monkeypatch):
     ref = (a.t() if ta else a).double() @ (b.t() if tb else b).double()
     scale = ref.abs().max().item()
     errs = {}
-    for mode in ("1", "0"):
-        monkeypatch.setenv("DS2_GEMM_X6", mode)
+    for mode in ("1", "0", "m16"):
+        monkeypatch.setenv("DS2_GEMM_X6", "0" if mode == "0" else "1")
+        monkeypatch.setenv("DS2_GEMM_M16", "1" if mode == "m16" else "0")
         c = torch.empty(m, n, device=dev)
         ops.sgemm(a, b, c, m=m, n=n, k=k, trans_a=bool(ta), trans_b=bool(tb), lda=a.shape[1],
                   ldb=b.shape[1], ldc=n)
         errs[mode] = (c.double() - ref).abs().max().item() / scale
     assert errs["1"] <= 2.5 * errs["0"] and errs["1"] < 5e-6, errs
+    assert errs["m16"] <= 2.5 * errs["0"] and errs["m16"] < 5e-6, errs
 
 
 @pytest.mark.parametrize("ta,tb", [(0, 1), (1, 0)])
