@@ -603,6 +603,9 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
   }
   __syncthreads();
   int cur = 0;
+  unsigned long long km_next[EPL];   // children masks of the beam's entries' nodes (prefetched)
+#pragma unroll
+  for (int q = 0; q < EPL; ++q) km_next[q] = 0ull;   // the root starts childless
   for (int t = 0; t < size; ++t) {
     const int nb = s_nb;
     if (nb == 0) break;
@@ -660,7 +663,7 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
       if (e < nb) {
         score[e] = beam_lse(b_pb[cur][e], b_pnb[cur][e]);
         const int nd = b_node[cur][e];
-        b_km[e] = __hip_atomic_load(km + nd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        b_km[e] = km_next[q];
         kept[e] = 0;
         const int pnode = nd > 0 ? b_par[cur][e] : -1;
         int j = -1;
@@ -824,6 +827,9 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
     {
       const int nodes0 = s_nodes;
       int run = 0;
+      // a new node's sibling link (the parent's previous first child, returned by the
+      // exchange) is stored after the deaths below, so no lane waits for the exchange here
+      int ns_node[EPL], ns_val[EPL];
       // revived nodes first: every lookup reads only the trie as the previous frame left it
       int rv[EPL];
 #pragma unroll
@@ -840,6 +846,7 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
 #pragma unroll
       for (int q = 0; q < EPL; ++q) {
         const int e = lane + 64 * q;
+        ns_node[q] = -1;
         int k = 0, i = 0, c = blank;
         if (e < nsel) {
           k = sel_k[e];
@@ -900,7 +907,8 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
             cnt[nd] = 1;
             fc[nd] = -1;
             km[nd] = 0ull;
-            ns[nd] = atomicExch(fc + p, nd);
+            ns_node[q] = nd;
+            ns_val[q] = atomicExch(fc + p, nd);
             atomicAdd(cnt + p, 1);
             atomicOr(km + p, 1ull << c);
             b_node[nxt][e] = nd;
@@ -930,9 +938,20 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
           }
         }
       }
+#pragma unroll
+      for (int q = 0; q < EPL; ++q)
+        if (ns_node[q] >= 0) ns[ns_node[q]] = ns_val[q];
       if (lane == 0) {
         s_nodes = nodes0 + run;
         s_nb = nsel;
+      }
+      // the next frame's children masks, loaded now (after this frame's trie updates, in
+      // issue order) and consumed by its bookkeeping
+#pragma unroll
+      for (int q = 0; q < EPL; ++q) {
+        const int e = lane + 64 * q;
+        if (e < nsel)
+          km_next[q] = __hip_atomic_load(km + b_node[nxt][e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
     __syncthreads();
