@@ -1,0 +1,10 @@
+set -o pipefail
+cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
+timeout -k 10 300 python -u scripts/bench_cfg4.py --rnn-gemm bf16 > gpurun_out/r4e.cfg4bf16.log 2>&1 || exit 1
+tail -2 gpurun_out/r4e.cfg4bf16.log
+timeout -k 10 200 python -u scripts/bs32_probe.py --mode gpu --tag x6 > gpurun_out/r4e.probe.log 2>&1 || exit 1
+DS2_GEMM_X6=0 DS2_GRU_X6=0 DS2_CONV_X6=0 timeout -k 10 200 python -u scripts/bs32_probe.py --mode gpu --tag fp32 >> gpurun_out/r4e.probe.log 2>&1 || exit 1
+timeout -k 10 500 python -u scripts/bs32_probe.py --mode oracle >> gpurun_out/r4e.probe.log 2>&1 || exit 1
+python -u scripts/bs32_probe.py --mode compare >> gpurun_out/r4e.probe.log 2>&1
+cat gpurun_out/r4e.probe.log
+rm -f gpurun_out/bs32_*.pt

@@ -472,11 +472,13 @@ def test_gru_xcd_groups_bit_identical(dev, n, h, bidir, monkeypatch):
     copies, placed by the XCC id each producer publishes: outputs and gradients bit-identical
     to the interleaved layout (DS2_GRU_XCD=0), ragged lengths."""
     nd = 2 if bidir else 1
-    env = [{"DS2_GRU_XCD": "1"}, {"DS2_GRU_XCD": "0"}]
-    xg, il = _gru_run(dev, n, 37, 40, h, nd, h + 13 * n, env, monkeypatch)
-    for a, b in zip(xg, il):
+    env = [{"DS2_GRU_XCD": "1", "DS2_GRU_XF": "0"}, {"DS2_GRU_XCD": "0", "DS2_GRU_XF": "0"},
+           {"DS2_GRU_XCD": "1", "DS2_GRU_XF": "1"}]
+    xg, il, xf = _gru_run(dev, n, 37, 40, h, nd, h + 13 * n, env, monkeypatch)
+    for a, b, c in zip(xg, il, xf):
         assert torch.isfinite(a).all()
         assert torch.equal(a, b)
+        assert torch.equal(a, c)   # fp32 cross-XCD copies split by the consumer: same runs
 
 
 @pytest.mark.parametrize("x6", ["1", "0"])
