@@ -745,6 +745,55 @@ def _rnn_output(h_all, sum_dirs, nd):
     return h_all.view(t, n, nd * h)
 
 
+def _rnn_param_grads_bf16(x2d, h_all, dgx, dgh, weights, nd, g, t, n, inp, h, need_dx, dbias):
+    """_rnn_param_grads with bf16 operands (BASELINE cfg4's opt-in) on ds2_bgemm_nt, each
+    operand rounded to bf16 ONCE per layer into the k-contiguous copy the GEMMs share:
+    dgx^T [D g][T N] serves dW_ih (all rows) and, shifted by one step, dW_hh (the LSTM's dgh is
+    dgx); x^T and h^T likewise; dgx as is serves dX.  Same rounding (RNE) and products as the
+    per-GEMM conversions of sgemm(..., bf16=True); only where the copies come from differs."""
+    dev = x2d.device
+    tn = t * n
+    ld = nd * g
+    dgx2 = dgx.view(tn, ld)
+    dgx_t = to_bf16(dgx2, transpose=True)                       # [ld][tn]
+    dgh_t = dgx_t if dgh is dgx else to_bf16(dgh.view(tn, ld), transpose=True)
+    x_t = to_bf16(x2d, transpose=True)                          # [inp][tn]
+    h_t = to_bf16(h_all.view(tn, nd * h), transpose=True)       # [nd h][tn]
+    dx = torch.empty(t, n, inp, device=dev, dtype=_F32) if need_dx else None
+    grads = []
+    if dx is not None:
+        dgx_b = to_bf16(dgx2)                                   # [tn][ld]
+        w_all = torch.cat([weights[4 * d] for d in range(nd)], 0) if nd > 1 else weights[0]
+        w_t = to_bf16(w_all, transpose=True)                    # [inp][ld]
+        bgemm_nt(dgx_b, w_t, dx.view(tn, inp))
+    for d in range(nd):
+        w_ih, w_hh, b_ih, b_hh = weights[4 * d: 4 * d + 4]
+        dw_ih = grad_like(w_ih)
+        bgemm_nt(dgx_t[d * g:(d + 1) * g], x_t, dw_ih)
+        if dbias is not None:
+            db_ih, db_hh = dbias[2 * d], dbias[2 * d + 1]
+        else:
+            db_ih = grad_like(b_ih)
+            colsum(dgx, tn, g, ld, db_ih, off=d * g)
+        # sum_t dgh_t^T h_{t-1} (fwd) / h_{t+1} (rev): k runs over (t - 1) n rows, dgh from
+        # step 1 (fwd) or 0 (rev), h from step 0 (fwd) or 1 (rev)
+        k = (t - 1) * n
+        ka, kb = (n, 0) if d == 0 else (0, n)
+        dw_hh = grad_like(w_hh)
+        bgemm_nt(dgh_t[d * g:(d + 1) * g, ka:ka + k], h_t[d * h:(d + 1) * h, kb:kb + k], dw_hh)
+        if dbias is None:
+            db_hh = grad_like(b_hh)
+            if dgh is dgx:
+                db_hh.copy_(db_ih)
+            elif g == 3 * h:
+                db_hh[:2 * h].copy_(db_ih[:2 * h])
+                colsum(dgh, tn, h, ld, db_hh[2 * h:], off=d * g + 2 * h)
+            else:
+                colsum(dgh, tn, g, ld, db_hh, off=d * g)
+        grads += [dw_ih, dw_hh, db_ih, db_hh]
+    return dx, grads
+
+
 def _rnn_param_grads(x, h_all, dgx, dgh, weights, nd, g, need_dx, bf16=False, dbias=None):
     """Weight/bias/input gradients of one recurrent layer from the gate gradients.
 
@@ -758,6 +807,9 @@ def _rnn_param_grads(x, h_all, dgx, dgh, weights, nd, g, need_dx, bf16=False, db
     x2d = x.view(t * n, inp)
     tn = t * n
     ld = nd * g
+    if bf16 and t > 1 and all(v % 8 == 0 for v in (n, inp, h, g)):
+        return _rnn_param_grads_bf16(x2d, h_all, dgx, dgh, weights, nd, g, t, n, inp, h,
+                                     need_dx, dbias)
     grads = []
     dx = torch.empty(t, n, inp, device=dev, dtype=_F32) if need_dx else None
     # both directions in one GEMM where W_ih (dX) and its gradient slots (dW_ih) are stacked

@@ -1,5 +1,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
+timeout -k 10 400 python -u -m pytest tests/test_gpu_model.py tests/test_gpu_train.py -k "bf16 or cfg4" -x -q --timeout 300 --timeout-method thread > gpurun_out/r4e.bf16.log 2>&1; rc=$?; tail -3 gpurun_out/r4e.bf16.log
+[ $rc -ne 0 ] && exit $rc
 timeout -k 10 300 python -u scripts/bench_cfg4.py --rnn-gemm bf16 > gpurun_out/r4e.cfg4bf16.log 2>&1 || exit 1
 tail -2 gpurun_out/r4e.cfg4bf16.log
 timeout -k 10 200 python -u scripts/bs32_probe.py --mode gpu --tag x6 > gpurun_out/r4e.probe.log 2>&1 || exit 1
