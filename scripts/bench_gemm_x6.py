@@ -18,11 +18,12 @@ dev = torch.device("cuda")
 TN = 501 * 32
 PEAK32, PEAKX6 = 157.3, 2516.6 / 6
 SHAPES = [  # name, ta, tb, m, n, k
-    ("xproj NT L0", 0, 1, TN, 2400, 1312),
-    ("xproj NT", 0, 1, TN, 2400, 800),
-    ("dX NN", 0, 0, TN, 800, 2400),
-    ("dW TN", 1, 0, 2400, 800, TN),
-    ("dW_ih L0 TN", 1, 0, 2400, 1312, TN),
+    ("xproj NT L0", 0, 1, TN, 4800, 1312),      # both directions stacked (as in the step)
+    ("xproj NT", 0, 1, TN, 4800, 800),
+    ("dX NN", 0, 0, TN, 800, 4800),
+    ("dW_ih TN", 1, 0, 4800, 800, TN),
+    ("dW_ih L0 TN", 1, 0, 4800, 1312, TN),
+    ("dW_hh TN", 1, 0, 2400, 800, TN - 32),     # one direction, T - 1 steps
     ("FC NT", 0, 1, TN, 32, 800),
 ]
 
@@ -55,17 +56,21 @@ def main():
         scale = ref.abs().max().item()
         line = f"{name:12s} {m:6d}x{n:5d}x{k:6d} |"
         # x6 and its 16x16x32 form alternate twice (the clock the chip holds differs by body)
-        for tag, env, m16, peak in (("x6", "1", "0", PEAKX6), ("x6m16", "1", "1", PEAKX6),
-                                    ("x6", "1", "0", PEAKX6), ("x6m16", "1", "1", PEAKX6),
-                                    ("fp32", "0", "0", PEAK32)):
+        for tag, env, m16, sk, peak in (("x6", "1", "0", "0", PEAKX6), ("x6m16", "1", "1", "0", PEAKX6),
+                                        ("x6sk", "1", "0", "2", PEAKX6),
+                                        ("x6", "1", "0", "0", PEAKX6), ("x6m16", "1", "1", "0", PEAKX6),
+                                        ("x6sk", "1", "0", "2", PEAKX6),
+                                        ("fp32", "0", "0", "0", PEAK32)):
             os.environ["DS2_GEMM_X6"] = env
             os.environ["DS2_GEMM_M16"] = m16
+            os.environ["DS2_GEMM_SK"] = sk
             t = timeit(lambda: ops.sgemm(a, b, c, **kw), iters=30)
             err = (c.double() - ref).abs().max().item() / scale
             tf = fl / t / 1e9
             line += f" {tag} {tf:6.1f} TF ({tf / peak:4.0%}) {t * 1e3:7.1f} us err {err:.1e} |"
         os.environ.pop("DS2_GEMM_X6", None)
         os.environ.pop("DS2_GEMM_M16", None)
+        os.environ.pop("DS2_GEMM_SK", None)
         print(line, flush=True)
 
 

@@ -84,6 +84,35 @@ def test_sgemm_full_rounds_plus_split_tail(dev, ta, tb, mode, monkeypatch):
     _close(cd, ref, 1e-5, "sgemm main+tail")
 
 
+@pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
+@pytest.mark.parametrize("m,n,k", [(768, 160, 10944), (1024, 800, 4096), (600, 300, 8192)])
+def test_sgemm_stream_k(dev, ta, tb, m, n, k, monkeypatch):
+    """Stream-K plan of the bf16x6 kernel (few tiles, deep K: equal contiguous stage ranges
+    per workgroup, the tiles split between workgroups finished by streamk_reduce_kernel in
+    workgroup order; forced by DS2_GEMM_SK=2) vs fp64 at 1e-5, alpha / beta / bias applied
+    once, and against the tile plan (DS2_GEMM_SK=0)."""
+    monkeypatch.setenv("DS2_GEMM_X6", "1")
+    monkeypatch.setenv("DS2_GEMM_M16", "0")
+    g = torch.Generator().manual_seed(m + n + k)
+    a = torch.randn(k, m, generator=g) if ta else torch.randn(m, k, generator=g)
+    b = torch.randn(n, k, generator=g) if tb else torch.randn(k, n, generator=g)
+    c0 = torch.randn(m, n, generator=g)
+    bias = torch.randn(n, generator=g)
+    ref = 0.5 * ((a.t() if ta else a).double() @ (b.t() if tb else b).double()) \
+        + 0.25 * c0.double() + bias.double()
+    ad, bd = a.to(dev), b.to(dev)
+    out = {}
+    for sk in ("2", "0"):
+        monkeypatch.setenv("DS2_GEMM_SK", sk)
+        cd = c0.to(dev).clone()
+        ops.sgemm(ad, bd, cd, m=m, n=n, k=k, trans_a=bool(ta), trans_b=bool(tb),
+                  lda=ad.shape[1], ldb=bd.shape[1], ldc=n, alpha=0.5, beta=0.25, bias=bias.to(dev))
+        torch.cuda.synchronize()
+        _close(cd, ref, 1e-5, f"sgemm stream-K={sk}")
+        out[sk] = cd.cpu()
+    assert (out["2"] - out["0"]).abs().max().item() <= 1e-5 * ref.abs().max().item()
+
+
 @pytest.mark.parametrize("ta,tb,m,n,k", [(0, 1, 2048, 2400, 800), (0, 0, 2048, 800, 2400),
                                          (1, 0, 2400, 800, 4096), (1, 0, 2400, 1312, 4096)])
 def test_sgemm_x6_is_fp32_accurate(dev, ta, tb, m, n, k, monkeypatch):
