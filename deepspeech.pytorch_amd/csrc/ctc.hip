@@ -499,6 +499,102 @@ __device__ __forceinline__ float lm_term(const BeamLm& L, const int* hist, int w
   return static_cast<float>(lnp * L.alpha);
 }
 
+// lm_term with every lookup's first probe issued at once: the order n-gram keys (n-gram
+// orders order..1 ending in w) in one round of loads, then the back-off contexts (lengths
+// m..order-1 of the history) in a second; a key whose first slot holds another key (a
+// collision) continues with lm_find's linear probing from the next slot.  Same result as
+// lm_term (same keys, same table, same float sums in the same order); two dependent rounds
+// of table loads instead of up to 2 order - 1.
+__device__ __forceinline__ bool lm_first_probe(const BeamLm& L, const int* k, int4& a, int4& b,
+                                               unsigned& slot) {
+  slot = lm_hash(k) & L.tmask;
+  a = L.tab[2 * slot];
+  b = L.tab[2 * slot + 1];
+  return true;
+}
+
+__device__ __forceinline__ int lm_resolve(const BeamLm& L, const int* k, const int4& a,
+                                          const int4& b, unsigned slot, float& prob, float& bo) {
+  if (a.x == -1) return 0;
+  if (a.x == k[0] && a.y == k[1] && a.z == k[2] && a.w == k[3] && b.x == k[4] && b.y == k[5]) {
+    prob = __int_as_float(b.z);
+    bo = __int_as_float(b.w);
+    return 1;
+  }
+  // collision: probe on from the next slot (rare)
+  unsigned sl = (slot + 1) & L.tmask;
+  for (unsigned p = 1; p <= L.tmask; ++p) {
+    const int4 c = L.tab[2 * sl], d = L.tab[2 * sl + 1];
+    if (c.x == -1) return 0;
+    if (c.x == k[0] && c.y == k[1] && c.z == k[2] && c.w == k[3] && d.x == k[4] && d.y == k[5]) {
+      prob = __int_as_float(d.z);
+      bo = __int_as_float(d.w);
+      return 1;
+    }
+    sl = (sl + 1) & L.tmask;
+  }
+  return 0;
+}
+
+__device__ __forceinline__ float lm_term_par(const BeamLm& L, const int* hist, int w) {
+  double lnp = -1000.0;
+  if (w >= 0) {
+    const int n1 = L.order - 1;
+    int h[LM_MAX_ORDER - 1];
+#pragma unroll
+    for (int i = 0; i < LM_MAX_ORDER - 1; ++i) h[i] = i < n1 ? hist[i] : -1;
+    // round 1: the n-grams of orders 1..order ending in w
+    int4 ra[LM_MAX_ORDER], rb[LM_MAX_ORDER];
+    unsigned rs[LM_MAX_ORDER];
+#pragma unroll
+    for (int m = 1; m <= LM_MAX_ORDER; ++m) {
+      if (m > L.order) break;
+      int key[LM_MAX_ORDER];
+#pragma unroll
+      for (int i = 0; i < LM_MAX_ORDER; ++i) key[i] = i < m - 1 ? h[n1 - (m - 1) + i] : (i == m - 1 ? w : -1);
+      lm_first_probe(L, key, ra[m - 1], rb[m - 1], rs[m - 1]);
+    }
+    float p = 0.f, bo = 0.f;
+    int m = L.order;
+    bool found = false;
+#pragma unroll
+    for (int mm = LM_MAX_ORDER; mm >= 1; --mm) {
+      if (mm > L.order || found) continue;
+      int key[LM_MAX_ORDER];
+#pragma unroll
+      for (int i = 0; i < LM_MAX_ORDER; ++i) key[i] = i < mm - 1 ? h[n1 - (mm - 1) + i] : (i == mm - 1 ? w : -1);
+      if (lm_resolve(L, key, ra[mm - 1], rb[mm - 1], rs[mm - 1], p, bo)) {
+        found = true;
+        m = mm;
+      }
+    }
+    if (found) {
+      // round 2: the back-offs of the contexts of lengths m..order-1
+      int4 ca[LM_MAX_ORDER - 1], cb[LM_MAX_ORDER - 1];
+      unsigned cs[LM_MAX_ORDER - 1];
+#pragma unroll
+      for (int ln = 1; ln < LM_MAX_ORDER; ++ln) {
+        if (ln < m || ln > n1) continue;
+        int key[LM_MAX_ORDER];
+#pragma unroll
+        for (int i = 0; i < LM_MAX_ORDER; ++i) key[i] = i < ln ? h[n1 - ln + i] : -1;
+        lm_first_probe(L, key, ca[ln - 1], cb[ln - 1], cs[ln - 1]);
+      }
+#pragma unroll
+      for (int ln = 1; ln < LM_MAX_ORDER; ++ln) {
+        if (ln < m || ln > n1) continue;
+        int key[LM_MAX_ORDER];
+#pragma unroll
+        for (int i = 0; i < LM_MAX_ORDER; ++i) key[i] = i < ln ? h[n1 - ln + i] : -1;
+        float pp, b2;
+        if (lm_resolve(L, key, ca[ln - 1], cb[ln - 1], cs[ln - 1], pp, b2)) p += b2;
+      }
+      lnp = static_cast<double>(p) / static_cast<double>(0.4342944819f);   // NUM_FLT_LOGE
+    }
+  }
+  return static_cast<float>(lnp * L.alpha);
+}
+
 // log_p += score; log_p += beta (float, then a double add rounded to float)
 __device__ __forceinline__ float lm_add(float v, float term, double beta) {
   return static_cast<float>(static_cast<double>(v + term) + beta);
@@ -880,7 +976,7 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
                 if ((unsigned)ns >= (unsigned)L.nstates) ns = L.fstate;   // a malformed arc
                 b_dst[nxt][e] = ns;
                 for (int h = 0; h < n1; ++h) b_hist[nxt][e][h] = b_hist[cur][i][h];
-                b_lms[nxt][e] = lm_term(L, &b_hist[cur][i][0], L.dword[ns]);
+                b_lms[nxt][e] = lm_term_par(L, &b_hist[cur][i][0], L.dword[ns]);
               }
             }
           }
