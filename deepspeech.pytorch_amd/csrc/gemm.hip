@@ -882,7 +882,7 @@ __device__ __forceinline__ void x2_store160(unsigned short* __restrict__ s, cons
 // NPL 3: the bf16x6 fp32-accurate GEMM; NPL 1: the bf16-operand GEMM (operands rounded to
 // bf16 while staged, one product per fragment pair, fp32 accumulation -- cfg4's opt-in
 // precision), one LDS plane per operand
-template <int TA, int TB, bool KCHK, int TBN, int NPL = 3, bool M16 = false, bool SK = false>
+template <int TA, int TB, bool KCHK, int TBN, int NPL = 3, bool M16 = false>
 __global__ __launch_bounds__(X2T, 1) void sxgemm2_kernel(
     int M, int N, int K, float alpha, const float* __restrict__ A, int64_t lda, int64_t sA,
     const float* __restrict__ B, int64_t ldb, int64_t sB, float beta, float* __restrict__ C,
@@ -1147,85 +1147,15 @@ __global__ __launch_bounds__(X2T, 1) void sxgemm2_kernel(
   }
   };   // job
 
-  if constexpr (!SK) {
-    int m0, n0, kbeg, kend, bz;
-    float* part;
-    decode_work(M, N, K, main_wgs, tail_tile0, tail_tiles, nsplit, kchunk, partial, m0, n0, kbeg,
-                kend, bz, part, TBN, X2M);
-    A += bz * sA;
-    B += bz * sB;
-    C += bz * sC;
-    job(m0, n0, kbeg, kend, part);
-  } else {
-    // stream-K (batch 1): the tiles' 32-k stages, U = tiles x S units in tile order, split into
-    // G equal contiguous ranges (numbered so that one XCD's workgroups take consecutive
-    // ranges).  A range spans at most two tiles (the plan checks); workgroup j < G runs the
-    // first segment of range j, workgroup G + j its second (launched 2 G wide: one job per
-    // workgroup, nothing carried between jobs).  A segment that covers part of a tile goes to
-    // partial slab 2 w + segment and streamk_reduce_kernel finishes those tiles.
-    const int G = gridDim.x >> 1;
-    const int sg = blockIdx.x >= G ? 1 : 0;
-    const int orig = blockIdx.x - sg * G;
-    const int q = G >> 3, r = G & 7, xcd = orig & 7;
-    const int w = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
-    const int S = (K + XS - 1) / XS;
-    const int tn = (N + TBN - 1) / TBN, tm = (M + X2M - 1) / X2M;
-    const int64_t U = (int64_t)tm * tn * S;
-    const int64_t u0 = U * w / G, u1 = U * (w + 1) / G;
-    if (u0 >= u1) return;
-    int64_t u = u0;
-    int t = static_cast<int>(u / S);
-    int ks = static_cast<int>(u - (int64_t)t * S);
-    int ke = static_cast<int>(ks + (u1 - u) < S ? ks + (u1 - u) : S);
-    if (sg == 1) {   // the second segment: the rest of the range, from the next tile's start
-      u += ke - ks;
-      if (u >= u1) return;
-      t += 1;
-      ks = 0;
-      ke = static_cast<int>(u1 - u < S ? u1 - u : S);
-    }
-    int tile_m, tile_n;
-    tile_coords(t, tn, tm, tile_m, tile_n);
-    float* const part = (ks == 0 && ke == S) ? nullptr
-                                             : partial + (int64_t)(2 * w + sg) * (X2M * TBN);
-    job(tile_m * X2M, tile_n * TBN, ks * XS, ke * XS < K ? ke * XS : K, part);
-  }
+  int m0, n0, kbeg, kend, bz;
+  float* part;
+  decode_work(M, N, K, main_wgs, tail_tile0, tail_tiles, nsplit, kchunk, partial, m0, n0, kbeg,
+              kend, bz, part, TBN, X2M);
+  A += bz * sA;
+  B += bz * sB;
+  C += bz * sC;
+  job(m0, n0, kbeg, kend, part);
 }
-
-// Stream-K fix-up: a tile whose stages were split between workgroups (a workgroup boundary
-// falls inside it) = alpha * (sum of its slabs in workgroup order) + bias + beta * C
-template <int TBN>
-__global__ void streamk_reduce_kernel(const float* __restrict__ partial, int M, int N, int K,
-                                      int G, float alpha, float beta, float* __restrict__ C,
-                                      int64_t ldc, const float* __restrict__ bias) {
-  const int S = (K + XS - 1) / XS;
-  const int tn = (N + TBN - 1) / TBN, tm = (M + X2M - 1) / X2M;
-  const int64_t U = (int64_t)tm * tn * S;
-  const int t = blockIdx.y;
-  const int64_t ta = (int64_t)t * S, tb = ta + S;
-  // the workgroup whose range holds the tile's first unit
-  int w = static_cast<int>((ta * G) / U);
-  while (w > 0 && U * w / G > ta) --w;
-  while (U * (w + 1) / G <= ta) ++w;
-  if (U * (w + 1) / G >= tb && U * w / G <= ta) return;   // one workgroup did the whole tile
-  int tile_m, tile_n;
-  tile_coords(t, tn, tm, tile_m, tile_n);
-  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < X2M * TBN; e += gridDim.x * blockDim.x) {
-    const int row = tile_m * X2M + e / TBN, col = tile_n * TBN + e % TBN;
-    if (row >= M || col >= N) continue;
-    float acc = 0.f;
-    for (int v = w; v < G && U * v / G < tb; ++v) {
-      if (U * (v + 1) / G == U * v / G) continue;             // an empty range (U < G)
-      const int slab = U * v / G >= ta ? 2 * v : 2 * v + 1;   // the range's first / last segment
-      acc += partial[(int64_t)slab * (X2M * TBN) + e];
-    }
-    float* cp = C + (int64_t)row * ldc + col;
-    float o = alpha * acc + (bias != nullptr ? bias[col] : 0.f);
-    if (beta != 0.f) o += beta * *cp;
-    *cp = o;
-  }
-}
-
 
 // Tail tiles: C[b] = alpha * sum_s partial[b][s][tile] + beta * C[b] + bias (fixed order)
 __global__ void splitk_reduce_kernel(const float* __restrict__ partial, int M, int N, int nsplit,
@@ -1316,7 +1246,6 @@ static int device_cus() {
 // becomes 133 tiles x 5 splits.  Split partials are reduced in a fixed order.
 struct GemmPlan {
   int main_wgs, tail_tile0, tail_tiles, nsplit, kchunk, bn, bm;
-  int sk = 0;   // stream-K (bf16x6 kernel, batch 1): sk workgroups, each an equal stage range
 };
 
 // DS2_GEMM_X6=0 selects the fp32-MFMA kernels (the accuracy cross-check of the tests); the
@@ -1327,13 +1256,6 @@ static bool x6_enabled(bool va, bool vb) {
   if (!va || !vb) return false;
   const char* e = getenv("DS2_GEMM_X6");
   return !(e != nullptr && e[0] == '0');
-}
-
-// A/B switch (experiment): DS2_GEMM_M16=1 runs the bf16x6 kernel on v_mfma_f32_16x16x32_bf16
-// (the same wave tiles as 16x16 tiles) where every stage lies inside K
-static bool m16_enabled() {
-  const char* e = getenv("DS2_GEMM_M16");
-  return e != nullptr && e[0] == '1';
 }
 
 // 32-bit buffer offsets: each operand (one batch entry) must span < 2^31 bytes
@@ -1407,7 +1329,6 @@ static GemmPlan gemm_plan(int m, int n, int k, int batch, bool k64) {
 }
 
 static size_t plan_ws(const GemmPlan& p, int batch) {
-  if (p.sk > 0) return (size_t)2 * p.sk * p.bm * p.bn * sizeof(float) + 256;
   return p.nsplit > 1 ? (size_t)p.nsplit * batch * p.tail_tiles * p.bm * p.bn * sizeof(float) + 256
                       : 0;
 }
@@ -1415,37 +1336,8 @@ static size_t plan_ws(const GemmPlan& p, int batch) {
 // the bf16x6 kernel: 256-row tiles, one workgroup per CU, split-K in 32-k chunks; 160-wide
 // tiles measured faster on every step shape with N >= 800 (scripts/bench_gemm_x6.py: 180-201
 // vs 159-194 TF), 128-wide on narrow N (the FC's 29 columns)
-//
-// Stream-K: with few tiles per CU (the weight gradients: 95 tiles of 501 stages on 256 CUs)
-// whole tiles plus a split tail leave CUs idle; equal contiguous stage ranges per workgroup
-// do not.  Model: ceil(units / CUs) stages + a prologue (2 stages) per extra segment + the
-// slab write / fix-up traffic; taken when 5 % under the tile plan (batch 1, K % 32 == 0).
-// DS2_GEMM_SK=0 keeps the tile plan, =2 takes stream-K wherever a range spans at most two
-// tiles (the A/B and the tests).
-static int sk_mode() {
-  const char* e = getenv("DS2_GEMM_SK");
-  return e == nullptr || e[0] == 0 ? 1 : e[0] - '0';
-}
-
-static GemmPlan x6_plan(int m, int n, int k, int batch, bool allow_sk = true) {
-  const int cus = device_cus();
-  const int bn = n >= 256 ? 160 : 128;
-  const PlanChoice pc = plan_bn(m, n, k, batch, bn, cus, XS, 1.0, X2M);
-  const int mode = sk_mode();
-  if (!allow_sk || batch != 1 || k % XS != 0 || mode == 0) return pc.p;
-  const int64_t tiles = (int64_t)cdiv(m, X2M) * cdiv(n, bn);
-  const int64_t S = k / XS;
-  const int64_t U = tiles * S;
-  if (U < 2 * (int64_t)cus) return pc.p;
-  const double unit = 2.0 * X2M * bn / (157.3e12 / cus);   // one k of one tile on one slot
-  const int64_t per = (U + cus - 1) / cus;
-  if (per > S) return pc.p;   // a range may span at most two tiles (the kernel's two jobs)
-  const double t_sk = (double)(per + 2) * XS * unit +
-                      (double)2 * cus * X2M * bn * 8.0 / 4e12 + 6e-6;
-  if (mode != 2 && t_sk > 0.95 * pc.t) return pc.p;
-  GemmPlan p = pc.p;   // the tile plan stays filled in: the fallback without workspace
-  p.sk = cus;
-  return p;
+static GemmPlan x6_plan(int m, int n, int k, int batch) {
+  return plan_bn(m, n, k, batch, n >= 256 ? 160 : 128, device_cus(), XS, 1.0, X2M).p;
 }
 
 // large enough for any kernel's plan (the choice depends on operand alignment)
@@ -1453,8 +1345,7 @@ extern "C" size_t ds2_sgemm_workspace_size(int m, int n, int k, int batch) {
   if (m <= 0 || n <= 0 || k <= 0 || batch <= 0) return 0;
   return std::max(std::max(plan_ws(gemm_plan(m, n, k, batch, false), batch),
                            plan_ws(gemm_plan(m, n, k, batch, true), batch)),
-                  std::max(plan_ws(x6_plan(m, n, k, batch), batch),
-                           plan_ws(x6_plan(m, n, k, batch, false), batch)));
+                  plan_ws(x6_plan(m, n, k, batch), batch));
 }
 
 extern "C" ds2_status_t ds2_sgemm_ws(int trans_a, int trans_b, int m, int n, int k, float alpha,
@@ -1477,12 +1368,11 @@ extern "C" ds2_status_t ds2_sgemm_ws(int trans_a, int trans_b, int m, int n, int
   const bool x6 = fits && x6_enabled(va, vb);
   const bool k64 = !x6 && va && vb && fits;
   GemmPlan p = x6 ? x6_plan(m, n, k, batch) : gemm_plan(m, n, k, batch, k64);
-  if (p.sk > 0 && (ws == nullptr || ws_bytes < plan_ws(p, batch))) p.sk = 0;   // tile plan
-  if (p.sk == 0 && p.nsplit > 1 && (ws == nullptr || ws_bytes < plan_ws(p, batch))) {
+  if (p.nsplit > 1 && (ws == nullptr || ws_bytes < plan_ws(p, batch))) {
     p.nsplit = 1;                       // no workspace: whole-K pieces
     p.kchunk = std::max(k, 1);
   }
-  float* partial = (p.sk > 0 || p.nsplit > 1) ? static_cast<float*>(ws) : nullptr;
+  float* partial = p.nsplit > 1 ? static_cast<float*>(ws) : nullptr;
   const int64_t nwg = p.main_wgs + (int64_t)p.tail_tiles * batch * p.nsplit;
   if (nwg > 0x7fffffff) return DS2_UNSUPPORTED_SHAPE;
   dim3 grid(static_cast<unsigned>(nwg));
@@ -1494,15 +1384,11 @@ extern "C" ds2_status_t ds2_sgemm_ws(int trans_a, int trans_b, int m, int n, int
                      m, n, k, alpha, a, lda, stride_a, b, ldb, stride_b, beta, c, ldc,          \
                      stride_c, bias, p.main_wgs, p.tail_tile0, p.tail_tiles, p.nsplit,          \
                      p.kchunk, partial)
-  const bool m16 = x6 && kalign && m16_enabled();
-#define DS2_SK(TA_, TB_, BN_)                                                                 \
-  hipLaunchKernelGGL((sxgemm2_kernel<TA_, TB_, false, BN_, 3, false, true>), dim3(2 * p.sk),   \
-                     dim3(X2T), 0, st, m, n, k, alpha, a, lda, stride_a, b, ldb, stride_b,      \
-                     beta, c, ldc, stride_c, bias, 0, 0, 0, 1, k, partial)
+  // the 16x16x32 form wherever every stage lies inside K (r4d: 0-15 % faster on the step's
+  // shapes, profiles/r4d_gemm_x6_m16_sk_ab.txt), the 32x32x16 form for a K tail
+  const bool m16 = x6 && kalign;
 #define DS2_G(TA_, TB_)                                                                       \
-  if (x6 && p.sk > 0 && p.bn == 160) DS2_SK(TA_, TB_, 160);                                  \
-  else if (x6 && p.sk > 0) DS2_SK(TA_, TB_, 128);                                            \
-  else if (m16 && p.bn == 160) DS2_X6(TA_, TB_, false, 160, true);                           \
+  if (m16 && p.bn == 160) DS2_X6(TA_, TB_, false, 160, true);                               \
   else if (m16) DS2_X6(TA_, TB_, false, 128, true);                                          \
   else if (x6 && kalign && p.bn == 160) DS2_X6(TA_, TB_, false, 160, false);                 \
   else if (x6 && p.bn == 160) DS2_X6(TA_, TB_, true, 160, false);                            \
@@ -1527,16 +1413,7 @@ extern "C" ds2_status_t ds2_sgemm_ws(int trans_a, int trans_b, int m, int n, int
   }
 #undef DS2_G
 #undef DS2_X6
-#undef DS2_SK
-  if (x6 && p.sk > 0) {
-    const int tiles = cdiv(m, X2M) * cdiv(n, p.bn);
-    if (p.bn == 160)
-      hipLaunchKernelGGL(streamk_reduce_kernel<160>, dim3(8, tiles), dim3(256), 0, st, partial,
-                         m, n, k, p.sk, alpha, beta, c, ldc, bias);
-    else
-      hipLaunchKernelGGL(streamk_reduce_kernel<128>, dim3(8, tiles), dim3(256), 0, st, partial,
-                         m, n, k, p.sk, alpha, beta, c, ldc, bias);
-  } else if (p.nsplit > 1) {
+  if (p.nsplit > 1) {
     const int64_t total = (int64_t)batch * p.tail_tiles * p.bm * p.bn;
     int g = cdiv(total, 256);
     if (g > 4096) g = 4096;

@@ -375,11 +375,7 @@ __global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
   // xmode: same-XCD groups -- every tile is also stored plainly into ring slots 2-3 (kept in
   // the producer's L2) and a consumer loads the tiles of the producers that share its XCD
   // from there
-  // xmode 2 (xf): the write-through copy -- the one the consumers on the other XCD read --
-  // is the fp32 tile (1 KB, at the start of the tile's slot) and those consumers split it on
-  // arrival; the plain same-XCD copy stays pre-split
   const bool xg = xmode != 0;
-  const bool xf = xmode == 2;
   if (xg ? !map_work_xgrp(UB, BT, D, ub, d, bt) : !map_work(UB * D, BT, UB, ub, d, bt)) return;
   const int n0 = bt * GB;
   const int lane = threadIdx.x & 63;
@@ -479,15 +475,11 @@ __global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
       u32x2 lo[2 * NP];
       auto load_run = [&](int i) {
         const bool ok = i < 2 * np && t_first + i < NB3;
-        const bool same = (tsame >> i) & 1ull;
-        const int to = tb0 + i * TF * 4 + (same ? aoff : 0);
+        const int to = tb0 + i * TF * 4 + (((tsame >> i) & 1ull) ? aoff : 0);
         hm[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
                                               x_rs, ok ? to + lane * 16 : 0x7ffffff0, 0, kSc1));
-        if (!xf || same)
-          lo[i] = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(
+        lo[i] = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(
                                               x_rs, ok ? to + 1024 + lane * 8 : 0x7ffffff0, 0, kSc1));
-        else
-          lo[i] = u32x2{0u, 0u};
       };
 #pragma unroll
       for (int i = 0; i < 2 * LWP; ++i) load_run(i);
@@ -499,8 +491,6 @@ __global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
           load_run(2 * (p + LWP));
           load_run(2 * (p + LWP) + 1);
         }
-        if (xf && !((tsame >> (2 * p)) & 1ull)) split_pk4(__builtin_bit_cast(f32x4, hm[2 * p]), hm[2 * p], lo[2 * p]);
-        if (xf && !((tsame >> (2 * p + 1)) & 1ull)) split_pk4(__builtin_bit_cast(f32x4, hm[2 * p + 1]), hm[2 * p + 1], lo[2 * p + 1]);
         acc = mma6(tri_of(hm[2 * p], lo[2 * p], hm[2 * p + 1], lo[2 * p + 1]), w[p], acc);
       }
       trace_at(s, 2);
@@ -551,15 +541,10 @@ __global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
       for (int g = 0; g < 3; ++g) {
         u32x4 hmv;
         u32x2 lov;
-        const f32x4 tv = *reinterpret_cast<const f32x4*>(tile + g * GB * GU + lane * 4);
-        split_pk4(tv, hmv, lov);
+        split_pk4(*reinterpret_cast<const f32x4*>(tile + g * GB * GU + lane * 4), hmv, lov);
         const int go = so + g * UB * TF * 4;
-        if (xf) {
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, tv), x_rs, go + lane * 16, 0, kSc1);
-        } else {
-          __builtin_amdgcn_raw_buffer_store_b128(hmv, x_rs, go + lane * 16, 0, kSc1);
-          __builtin_amdgcn_raw_buffer_store_b64(lov, x_rs, go + 1024 + lane * 8, 0, kSc1);
-        }
+        __builtin_amdgcn_raw_buffer_store_b128(hmv, x_rs, go + lane * 16, 0, kSc1);
+        __builtin_amdgcn_raw_buffer_store_b64(lov, x_rs, go + 1024 + lane * 8, 0, kSc1);
         if (xg) {   // plain copies: stay in this XCD's L2 for the same-XCD consumers
           __builtin_amdgcn_raw_buffer_store_b128(hmv, x_rs, aoff + go + lane * 16, 0, 0);
           __builtin_amdgcn_raw_buffer_store_b64(lov, x_rs, aoff + go + 1024 + lane * 8, 0, 0);
@@ -678,8 +663,6 @@ bool launch_gru_bwd_x6(int t_max, int n, int h, int num_dirs, const float* dy, i
   const void* fn = bwd_x6_fn((3 * UB + 1) / 2);
   if (fn == nullptr) return false;
   int XM_ = xcd_groups(UB, BT, num_dirs) ? 1 : 0;
-  const char* xfe = getenv("DS2_GRU_XF");   // A/B: fp32 cross-XCD copies (xmode 2)
-  if (XM_ && xfe != nullptr && xfe[0] == '1') XM_ = 2;
   const int grid = XM_ ? xgrp_grid(UB, BT, num_dirs) : mapped_grid(UB * num_dirs, BT);
   int T_ = t_max, N_ = n, H_ = h, D_ = num_dirs, UB_ = UB, BT_ = BT, DYD_ = dy_dirs;
   void* args[] = {&T_, &N_, &H_, &D_, &UB_, &BT_, &dy, &DYD_, &w_hh_f, &w_hh_r, &h_all,

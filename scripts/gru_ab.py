@@ -64,9 +64,6 @@ if len(sys.argv) > 1 and sys.argv[1] == "flagpoll":
     # s_sleep(1) units between the flag hand-off's polls (the pre-split backward's wait)
     variants = {f"bwd-poll-{t}": {"DS2_GRU_X6": "1", "DS2_RNN_TUNE": t}
                 for t in ("1,10,14,1", "1,10,14,0", "1,10,14,2", "1,10,14,4")}
-if len(sys.argv) > 1 and sys.argv[1] == "xf":
-    # the backward's cross-XCD copies as fp32 split by the consumers (DS2_GRU_XF=1) vs pre-split
-    variants = {f"xf{v}": {"DS2_GRU_X6": "1", "DS2_GRU_XF": v} for v in ("0", "1")}
 rounds = int(os.environ.get("AB_ROUNDS", "3"))
 variants = {f"{k}#{r}": v for r in range(rounds) for k, v in variants.items()}
 ref = None
