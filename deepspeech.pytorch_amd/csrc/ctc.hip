@@ -322,93 +322,58 @@ __device__ __forceinline__ unsigned long long beam_pack(float s, int key) {
   return (static_cast<unsigned long long>(b) << 32) | (0xFFFFFFFFu - static_cast<unsigned>(key));
 }
 
-// one step of a wave max over packed keys through a DPP lane pattern (no LDS)
-template <int CTRL>
-__device__ __forceinline__ void beam_dpp_step(unsigned long long& v) {
-  const unsigned lo = static_cast<unsigned>(
-      __builtin_amdgcn_update_dpp(0, static_cast<int>(static_cast<unsigned>(v)), CTRL, 0xF, 0xF, false));
-  const unsigned hi = static_cast<unsigned>(
-      __builtin_amdgcn_update_dpp(0, static_cast<int>(static_cast<unsigned>(v >> 32)), CTRL, 0xF, 0xF, false));
-  const unsigned long long o = (static_cast<unsigned long long>(hi) << 32) | lo;
-  v = o > v ? o : v;
-}
-
-// beam_dpp_step over the rows in ROW_MASK only (the other lanes keep their value)
-template <int CTRL, int ROW_MASK>
-__device__ __forceinline__ void beam_dpp_step_rows(unsigned long long& v) {
-  const int vlo = static_cast<int>(static_cast<unsigned>(v));
-  const int vhi = static_cast<int>(static_cast<unsigned>(v >> 32));
-  const unsigned lo = static_cast<unsigned>(__builtin_amdgcn_update_dpp(vlo, vlo, CTRL, ROW_MASK, 0xF, false));
-  const unsigned hi = static_cast<unsigned>(__builtin_amdgcn_update_dpp(vhi, vhi, CTRL, ROW_MASK, 0xF, false));
-  const unsigned long long o = (static_cast<unsigned long long>(hi) << 32) | lo;
-  v = o > v ? o : v;
-}
-
-// the wave's largest packed key (uniform) -- keys are unique, so any reduction tree gives the
-// same winner: xor 1 and xor 2 within quads, half-row and row mirrors (every lane of a 16-lane
-// row holds the row's best), then row_bcast:15 into rows 1 and 3 and row_bcast:31 into rows 2
-// and 3 (lane 63 holds the wave's best) -- all in VALU, one v_readlane pair at the end
-__device__ __forceinline__ unsigned long long beam_wave_best(unsigned long long v) {
-  beam_dpp_step<0xB1>(v);              // quad_perm [1,0,3,2]
-  beam_dpp_step<0x4E>(v);              // quad_perm [2,3,0,1]
-  beam_dpp_step<0x141>(v);             // row_half_mirror
-  beam_dpp_step<0x140>(v);             // row_mirror
-  beam_dpp_step_rows<0x142, 0xA>(v);   // row_bcast:15
-  beam_dpp_step_rows<0x143, 0xC>(v);   // row_bcast:31
-  const unsigned lo = static_cast<unsigned>(__builtin_amdgcn_readlane(static_cast<int>(static_cast<unsigned>(v)), 63));
-  const unsigned hi = static_cast<unsigned>(__builtin_amdgcn_readlane(static_cast<int>(static_cast<unsigned>(v >> 32)), 63));
-  return (static_cast<unsigned long long>(hi) << 32) | lo;
-}
-
-// keep the best `beam` of the tot candidates whose packed keys are ukey[0, tot): lane l holds
-// keys l, l + 64, ... in NJ registers (NJ >= the filled slots; the rest hold 0).  A round is a
-// wave max of the lanes' best keys, then the lane holding the (unique) winner drops it.  For
-// NJ <= 8 a lane's keys are sorted once (odd-even transposition), so its best is always slot
-// 0 and the drop is a shift; wider lanes rescan.  No barrier, no LDS traffic inside the
-// rounds.  Writes the winners' candidate indices to sel_k in rank order.
+// keep the best `beam` of the tot candidates whose packed keys are ukey[0, tot) (unique;
+// 0 = no candidate): lane l holds keys l, l + 64, ... in NJ registers (NJ >= the filled slots;
+// the rest hold 0).  A radix select finds the threshold: bit by bit from the top, the
+// largest T with at least `beam` keys >= T -- each test is NJ v_cmp ballots and their popcounts,
+// no cross-lane data movement -- stopping early once exactly `beam` keys are >= T.  The
+// selected keys are compacted into sk[] (LDS) and each is ranked by counting the selected
+// keys above it, so sel_k receives the winners' candidate indices in rank order (the order
+// of beam_better: score, then char, then index).  Returns the number selected.
 template <int NJ>
 __device__ __forceinline__ int beam_select(const unsigned long long* ukey, int tot, int beam,
-                                           int* sel_k, int lane) {
+                                           int* sel_k, unsigned long long* sk, int lane) {
   unsigned long long ru[NJ];
 #pragma unroll
   for (int jj = 0; jj < NJ; ++jj) {
     const int k = lane + 64 * jj;
     ru[jj] = k < tot ? ukey[k] : 0ull;
   }
-  constexpr bool kSorted = NJ <= 8;
-  unsigned long long lbest = 0ull;
-  if constexpr (kSorted) {
+  auto count_ge = [&](unsigned long long c) {
+    int n = 0;
 #pragma unroll
-    for (int p = 0; p < NJ; ++p)
-#pragma unroll
-      for (int j = p & 1; j + 1 < NJ; j += 2) {
-        const unsigned long long x = ru[j], y = ru[j + 1];
-        ru[j] = x > y ? x : y;
-        ru[j + 1] = x > y ? y : x;
-      }
-  } else {
-#pragma unroll
-    for (int jj = 0; jj < NJ; ++jj) lbest = ru[jj] > lbest ? ru[jj] : lbest;
-  }
-  int nsel = 0;
-  for (int r = 0; r < beam; ++r) {
-    const unsigned long long b = beam_wave_best(kSorted ? ru[0] : lbest);
-    if (b == 0ull) break;
-    if constexpr (kSorted) {
-      const bool own = ru[0] == b;
-#pragma unroll
-      for (int jj = 0; jj + 1 < NJ; ++jj) ru[jj] = own ? ru[jj + 1] : ru[jj];
-      ru[NJ - 1] = own ? 0ull : ru[NJ - 1];
-    } else {
-      lbest = 0ull;
-#pragma unroll
-      for (int jj = 0; jj < NJ; ++jj) {
-        ru[jj] = ru[jj] == b ? 0ull : ru[jj];
-        lbest = ru[jj] > lbest ? ru[jj] : lbest;
+    for (int jj = 0; jj < NJ; ++jj) n += __popcll(__ballot(ru[jj] >= c));
+    return n;
+  };
+  unsigned long long thr = 1ull;                  // every candidate, when at most `beam`
+  if (count_ge(1ull) > beam) {
+    unsigned long long t = 0ull;
+    for (int bit = 63; bit >= 0; --bit) {
+      const unsigned long long c = t | (1ull << bit);
+      const int n = count_ge(c);
+      if (n >= beam) {
+        t = c;
+        if (n == beam) break;
       }
     }
-    if (lane == 0) sel_k[r] = static_cast<int>((0xFFFFFFFFu - static_cast<unsigned>(b)) & 4095u);
-    ++nsel;
+    thr = t;
+  }
+  int nsel = 0;
+#pragma unroll
+  for (int jj = 0; jj < NJ; ++jj) {
+    const bool sel = ru[jj] >= thr;
+    const unsigned long long m = __ballot(sel);
+    if (sel)
+      sk[nsel + __builtin_amdgcn_mbcnt_hi(static_cast<unsigned>(m >> 32),
+                                          __builtin_amdgcn_mbcnt_lo(static_cast<unsigned>(m), 0))] = ru[jj];
+    nsel += __popcll(m);
+  }
+  __builtin_amdgcn_wave_barrier();
+  for (int r = lane; r < nsel; r += 64) {
+    const unsigned long long kr = sk[r];
+    int rank = 0;
+    for (int j = 0; j < nsel; ++j) rank += sk[j] > kr ? 1 : 0;
+    sel_k[rank] = static_cast<int>((0xFFFFFFFFu - static_cast<unsigned>(kr)) & 4095u);
   }
   return nsel;
 }
@@ -654,6 +619,7 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
   __shared__ signed char child_of[BM * CM];
   __shared__ float cpb[BM * CM], cpnb[BM * CM];
   __shared__ unsigned long long ukey[BM * CM];   // beam_pack(score, key) per candidate k
+  __shared__ unsigned long long sk_sel[BM];       // the selected keys (beam_select)
   __shared__ float bl_sc[BM], bl_pb[BM], bl_pnb[BM];   // the blank candidate of each entry
   __shared__ int sel_k[BM];
   __shared__ int s_nb, s_nodes, s_nr;
@@ -855,41 +821,64 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
     BEAM_STAMP(2)
     // ---- candidates k = i * C + c: lane (g, c) = divmod(lane, CM) scores char c of the entries
     // i = G jj + g, so the char's log prob and pruning flag stay in registers and every
-    // per-entry read is one LDS address per lane group (a broadcast); packed keys go to
-    // ukey[k] for the selection
+    // per-entry read is one LDS address per lane group (a broadcast).  Entries go in groups of
+    // SG: every LDS read of a group is issued before any of its arithmetic, which is
+    // branch-free (the blank lane takes its entry's precomputed blank candidate); packed keys
+    // go to ukey[k] for the selection
     {
-      constexpr int G = 64 / CM, SJ = BM / G;
+      constexpr int G = 64 / CM, SG = 4;
       const int c = lane % CM, g = lane / CM;
       const bool cv = c < C;
-      const float lpc = cv ? lp[c] : 0.f;
-      const bool alc = cv && c != blank && allowed[c];
+      const int cs = cv ? c : 0;                          // an in-range char for idle lanes
+      const float lpc = lp[cs];
+      const bool alc = cv && c != blank && allowed[cs];
+      const bool isb = c == blank;
       const int jn = (nb + G - 1) / G;                  // wave-uniform
+      for (int j0 = 0; j0 < jn; j0 += SG) {
+        int last[SG];
+        float sci[SG], pbi[SG], blp[SG], blnp[SG], bls[SG], lms[SG];
+        int co[SG];
+        unsigned long long kmi[SG], vmi[SG];
 #pragma unroll
-      for (int jj = 0; jj < SJ; ++jj) {
-        if (jj >= jn) continue;
-        const int i = G * jj + g;
-        if (!cv || i >= nb) continue;
-        const int k = i * C + c;
-        const int last_i = b_last[cur][i];
-        float sc = -INFINITY, pb = -INFINITY, pnb = -INFINITY;
-        if (c == blank) {
-          pb = bl_pb[i];
-          pnb = bl_pnb[i];
-          sc = bl_sc[i];
-        } else {
-          const float sc_i = score[i];
-          if (alc && child_of[k] < 0 &&
-              (!LM || (!(lpc + sc_i < cut) && ((vmask[i] >> c) & 1ull)))) {
-            const float pb_i = b_pb[cur][i];
-            pnb = (c == last_i) ? (pb_i != -INFINITY ? lpc + pb_i : -INFINITY) : lpc + sc_i;
-            if (LM && c == L.space) pnb = lm_add(pnb, b_lms[cur][i], L.beta);
-            sc = pnb;
-            if ((b_km[i] >> c) & 1ull) rlist[atomicAdd(&s_nr, 1)] = k;   // revival attempt
+        for (int u = 0; u < SG; ++u) {
+          const int ir = G * (j0 + u) + g;
+          const int i = ir < BM ? ir : BM - 1;            // in-bounds reads; validity below
+          last[u] = b_last[cur][i];
+          sci[u] = score[i];
+          pbi[u] = b_pb[cur][i];
+          co[u] = child_of[i * C + cs];
+          kmi[u] = b_km[i];
+          blp[u] = bl_pb[i];
+          blnp[u] = bl_pnb[i];
+          bls[u] = bl_sc[i];
+          if constexpr (LM) {
+            vmi[u] = vmask[i];
+            lms[u] = b_lms[cur][i];
+          } else {
+            vmi[u] = 0ull;
+            lms[u] = 0.f;
           }
         }
-        cpb[k] = pb;
-        cpnb[k] = pnb;
-        ukey[k] = beam_pack(sc, ((c == blank ? last_i : c) + 1) * 4096 + k);
+#pragma unroll
+        for (int u = 0; u < SG; ++u) {
+          const int i = G * (j0 + u) + g;
+          const int k = i * C + c;
+          // with an LM a (prefix, char) pair below the pruning bound is skipped entirely
+          const bool ext = alc && co[u] < 0 &&
+                           (!LM || (!(lpc + sci[u] < cut) && ((vmi[u] >> cs) & 1ull)));
+          float pe = (c == last[u]) ? (pbi[u] != -INFINITY ? lpc + pbi[u] : -INFINITY)
+                                    : lpc + sci[u];
+          if constexpr (LM) pe = c == L.space ? lm_add(pe, lms[u], L.beta) : pe;
+          const float pb = isb ? blp[u] : -INFINITY;
+          const float pnb = isb ? blnp[u] : (ext ? pe : -INFINITY);
+          const float sc = isb ? bls[u] : (ext ? pe : -INFINITY);
+          if (cv && i < nb) {
+            cpb[k] = pb;
+            cpnb[k] = pnb;
+            ukey[k] = beam_pack(sc, ((isb ? last[u] : c) + 1) * 4096 + k);
+            if (ext && ((kmi[u] >> c) & 1ull)) rlist[atomicAdd(&s_nr, 1)] = k;   // revival attempt
+          }
+        }
       }
     }
     __syncthreads();
@@ -910,11 +899,12 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
     constexpr int SD = BM * CM / 64;
     const int tot = nb * C;
     const int jd = (tot + 63) / 64;
-    const int nsel = jd <= 2    ? beam_select<2>(ukey, tot, beam, sel_k, lane)
-                     : jd <= 4  ? beam_select<4>(ukey, tot, beam, sel_k, lane)
-                     : jd <= 8  ? beam_select<8>(ukey, tot, beam, sel_k, lane)
-                     : jd <= 16 ? beam_select<16>(ukey, tot, beam, sel_k, lane)
-                                : beam_select<SD>(ukey, tot, beam, sel_k, lane);
+    const int nsel = jd <= 2    ? beam_select<2>(ukey, tot, beam, sel_k, sk_sel, lane)
+                     : jd <= 4  ? beam_select<4>(ukey, tot, beam, sel_k, sk_sel, lane)
+                     : jd <= 6  ? beam_select<6>(ukey, tot, beam, sel_k, sk_sel, lane)
+                     : jd <= 8  ? beam_select<8>(ukey, tot, beam, sel_k, sk_sel, lane)
+                     : jd <= 16 ? beam_select<16>(ukey, tot, beam, sel_k, sk_sel, lane)
+                                : beam_select<SD>(ukey, tot, beam, sel_k, sk_sel, lane);
     __syncthreads();
     BEAM_STAMP(5)
     // ---- new beam: lane r builds entries r, r + 64, ...; new prefixes get trie nodes in
