@@ -615,8 +615,7 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
   __shared__ int b_par[2][BM];
   __shared__ float b_lpc[2][BM];
   __shared__ float score[BM];
-  __shared__ int pidx[BM];
-  __shared__ signed char child_of[BM * CM];
+  __shared__ unsigned long long cmask[BM];   // chars of the entry's in-beam children
   __shared__ float cpb[BM * CM], cpnb[BM * CM];
   __shared__ unsigned long long ukey[BM * CM];   // beam_pack(score, key) per candidate k
   __shared__ unsigned long long sk_sel[BM];       // the selected keys (beam_select)
@@ -718,103 +717,116 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
       allowed[lane] = 1;
     }
     BEAM_STAMP(1)
-    // ---- beam bookkeeping: scores, parent index in the beam, child map
-#pragma unroll
-    for (int q = 0; q < EPL; ++q) {
-      const int e = lane + 64 * q;
-      if (e < nb) {
-        score[e] = beam_lse(b_pb[cur][e], b_pnb[cur][e]);
-        const int nd = b_node[cur][e];
-        b_km[e] = km_next[q];
-        kept[e] = 0;
-        const int pnode = nd > 0 ? b_par[cur][e] : -1;
-        int j = -1;
-#pragma unroll
-        for (int i = 0; i < BM; ++i) {   // unrolled: the nb LDS reads overlap
-          if (i >= nb) break;
-          if (pnode >= 0 && b_node[cur][i] == pnode) j = i;
-        }
-        pidx[e] = j;
-      }
-    }
-    for (int e = lane; e < nb * C; e += 64) child_of[e] = -1;
+    // ---- beam bookkeeping, one pass per entry (lane e) over data the previous frame left in
+    // LDS, with no barrier inside: its score, its parent's index in the beam (jp), the chars
+    // of its node's children that are themselves in the beam (cmask: an extension onto one of
+    // them merges into that entry instead), the LM bound and masks, and its blank candidate
+    // ("stay" terms plus the merge of the parent's extension by the entry's last char; the
+    // parent's score recomputed here rather than read after a barrier)
     if (lane == 0) s_nr = 0;
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < EPL; ++q) {
-      const int e = lane + 64 * q;
-      if (e < nb && pidx[e] >= 0) child_of[pidx[e] * C + b_last[cur][e]] = static_cast<signed char>(e);
-    }
-    // ---- LM: the scorer's pruning bound (min_cutoff = worst beam score + log p_blank -
-    // max(0, beta), applied once the beam is full), the dictionary reset of post-space
-    // entries (their first attempted non-blank char is rejected and the trie state goes
-    // back to the start) and each entry's valid-extension mask
-    // cut = min_cutoff once the beam is full, else -inf (nothing is below it); wave-uniform
-    float cut = -INFINITY;
-    if constexpr (LM) {
-      float wv = INFINITY;
-      for (int e = lane; e < nb; e += 64) wv = fminf(wv, score[e]);
-      wv = wave_min(wv);
-      const double pbl = static_cast<double>(pf[blank]);
-      const float mincut = static_cast<float>(
-          static_cast<double>(wv) + (pbl > 0.0 ? log(pbl) : -INFINITY) - fmax(0.0, L.beta));
-      cut = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(
-                                          int, nb == beam ? mincut : -INFINITY)));
+    float cut = -INFINITY;   // LM: min_cutoff once the beam is full, else -inf; wave-uniform
+    {
+      float sce[EPL];
+      int jpe[EPL];
 #pragma unroll
       for (int q = 0; q < EPL; ++q) {
         const int e = lane + 64 * q;
+        sce[q] = INFINITY;
+        jpe[q] = -1;
         if (e < nb) {
-          const int s = b_dst[cur][e];
-          int cs = -1;
-          unsigned long long vm;
-          if (s == L.fstate) {
-            const float se = score[e];
-            for (int r = 0; r < C; ++r) {
-              const int cc = prune ? order[r] : r;
-              if (cc == blank || !allowed[cc]) continue;
-              if (!(lp[cc] + se < cut)) {
-                cs = cc;
-                break;
-              }
-            }
-            vm = L.dmask[0] & ~(cs >= 0 ? (1ull << cs) : 0ull);
-          } else {
-            vm = L.dmask[s];
+          const float sc = beam_lse(b_pb[cur][e], b_pnb[cur][e]);
+          score[e] = sc;
+          sce[q] = sc;
+          const int nd = b_node[cur][e];
+          b_km[e] = km_next[q];
+          kept[e] = 0;
+          const int pnode = nd > 0 ? b_par[cur][e] : -1;
+          int j = -1;
+          unsigned long long cm = 0ull;
+#pragma unroll
+          for (int i = 0; i < BM; ++i) {   // unrolled: the nb LDS reads overlap
+            if (i >= nb) break;
+            const int ni = b_node[cur][i];
+            if (pnode >= 0 && ni == pnode) j = i;
+            if (ni > 0 && b_par[cur][i] == nd) cm |= 1ull << b_last[cur][i];
           }
-          cstar[e] = cs;
-          vmask[e] = vm;
+          jpe[q] = j;
+          cmask[e] = cm;
         }
       }
-    }
-    // ---- the blank candidate of every entry (one per entry: lane e scores entry e's; its
-    // "stay" terms and the merge of the entry's parent's extension by the entry's last char)
+      // ---- LM: the scorer's pruning bound (min_cutoff = worst beam score + log p_blank -
+      // max(0, beta), applied once the beam is full), the dictionary reset of post-space
+      // entries (their first attempted non-blank char is rejected and the trie state goes
+      // back to the start) and each entry's valid-extension mask
+      if constexpr (LM) {
+        float wv = INFINITY;
 #pragma unroll
-    for (int q = 0; q < EPL; ++q) {
-      const int i = lane + 64 * q;
-      if (i < nb) {
-        const int last_i = b_last[cur][i];
-        const float sc_i = score[i];
-        // with an LM a (prefix, char) pair below the pruning bound is skipped entirely
-        const float pb = (allowed[blank] && !(lp[blank] + sc_i < cut)) ? lp[blank] + sc_i : -INFINITY;
-        float pnb = (last_i >= 0 && allowed[last_i] && !(lp[last_i] + sc_i < cut))
-                        ? lp[last_i] + b_pnb[cur][i] : -INFINITY;
-        const int jp = pidx[i];
-        if (jp >= 0 && allowed[last_i] && !(lp[last_i] + score[jp] < cut)) {
-          float e = (last_i == b_last[cur][jp])
-                        ? (b_pb[cur][jp] != -INFINITY ? lp[last_i] + b_pb[cur][jp] : -INFINITY)
-                        : lp[last_i] + score[jp];
-          if (LM && last_i == L.space) e = lm_add(e, b_lms[cur][jp], L.beta);
-          pnb = beam_lse(pnb, e);
-          const int nd = b_node[cur][i];
-          if (lp[last_i] > b_lpc[cur][i]) {
-            b_lpc[cur][i] = lp[last_i];
-            lpcv[nd] = lp[last_i];
-            tst[nd] = t;
+        for (int q = 0; q < EPL; ++q) wv = fminf(wv, sce[q]);
+        wv = wave_min(wv);
+        const double pbl = static_cast<double>(pf[blank]);
+        const float mincut = static_cast<float>(
+            static_cast<double>(wv) + (pbl > 0.0 ? log(pbl) : -INFINITY) - fmax(0.0, L.beta));
+        cut = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(
+                                            int, nb == beam ? mincut : -INFINITY)));
+#pragma unroll
+        for (int q = 0; q < EPL; ++q) {
+          const int e = lane + 64 * q;
+          if (e < nb) {
+            const int s = b_dst[cur][e];
+            int cs = -1;
+            unsigned long long vm;
+            if (s == L.fstate) {
+              const float se = sce[q];
+              for (int r = 0; r < C; ++r) {
+                const int cc = prune ? order[r] : r;
+                if (cc == blank || !allowed[cc]) continue;
+                if (!(lp[cc] + se < cut)) {
+                  cs = cc;
+                  break;
+                }
+              }
+              vm = L.dmask[0] & ~(cs >= 0 ? (1ull << cs) : 0ull);
+            } else {
+              vm = L.dmask[s];
+            }
+            cstar[e] = cs;
+            vmask[e] = vm;
           }
         }
-        bl_pb[i] = pb;
-        bl_pnb[i] = pnb;
-        bl_sc[i] = beam_lse(pb, pnb);
+      }
+      // ---- the blank candidate of every entry
+#pragma unroll
+      for (int q = 0; q < EPL; ++q) {
+        const int i = lane + 64 * q;
+        if (i < nb) {
+          const int last_i = b_last[cur][i];
+          const float sc_i = sce[q];
+          // with an LM a (prefix, char) pair below the pruning bound is skipped entirely
+          const float pb = (allowed[blank] && !(lp[blank] + sc_i < cut)) ? lp[blank] + sc_i : -INFINITY;
+          float pnb = (last_i >= 0 && allowed[last_i] && !(lp[last_i] + sc_i < cut))
+                          ? lp[last_i] + b_pnb[cur][i] : -INFINITY;
+          const int jp = jpe[q];
+          if (jp >= 0) {
+            const float pb_jp = b_pb[cur][jp];
+            const float sc_jp = beam_lse(pb_jp, b_pnb[cur][jp]);
+            if (allowed[last_i] && !(lp[last_i] + sc_jp < cut)) {
+              float e = (last_i == b_last[cur][jp])
+                            ? (pb_jp != -INFINITY ? lp[last_i] + pb_jp : -INFINITY)
+                            : lp[last_i] + sc_jp;
+              if (LM && last_i == L.space) e = lm_add(e, b_lms[cur][jp], L.beta);
+              pnb = beam_lse(pnb, e);
+              const int nd = b_node[cur][i];
+              if (lp[last_i] > b_lpc[cur][i]) {
+                b_lpc[cur][i] = lp[last_i];
+                lpcv[nd] = lp[last_i];
+                tst[nd] = t;
+              }
+            }
+          }
+          bl_pb[i] = pb;
+          bl_pnb[i] = pnb;
+          bl_sc[i] = beam_lse(pb, pnb);
+        }
       }
     }
     __syncthreads();
@@ -837,8 +849,7 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
       for (int j0 = 0; j0 < jn; j0 += SG) {
         int last[SG];
         float sci[SG], pbi[SG], blp[SG], blnp[SG], bls[SG], lms[SG];
-        int co[SG];
-        unsigned long long kmi[SG], vmi[SG];
+        unsigned long long kmi[SG], vmi[SG], cmi[SG];
 #pragma unroll
         for (int u = 0; u < SG; ++u) {
           const int ir = G * (j0 + u) + g;
@@ -846,7 +857,7 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
           last[u] = b_last[cur][i];
           sci[u] = score[i];
           pbi[u] = b_pb[cur][i];
-          co[u] = child_of[i * C + cs];
+          cmi[u] = cmask[i];
           kmi[u] = b_km[i];
           blp[u] = bl_pb[i];
           blnp[u] = bl_pnb[i];
@@ -864,7 +875,7 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
           const int i = G * (j0 + u) + g;
           const int k = i * C + c;
           // with an LM a (prefix, char) pair below the pruning bound is skipped entirely
-          const bool ext = alc && co[u] < 0 &&
+          const bool ext = alc && !((cmi[u] >> cs) & 1ull) &&
                            (!LM || (!(lpc + sci[u] < cut) && ((vmi[u] >> cs) & 1ull)));
           float pe = (c == last[u]) ? (pbi[u] != -INFINITY ? lpc + pbi[u] : -INFINITY)
                                     : lpc + sci[u];
