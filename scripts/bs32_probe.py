@@ -115,9 +115,10 @@ def main():
                     ga = runs[a]["grads"][n].double()
                     gb = runs[b]["grads"][n].double()
                     worst.append(((ga - gb).abs().max() / gb.abs().max().clamp_min(1e-30)).item())
-                top = sorted(zip(worst, names), reverse=True)[:4]
-                print(f"{a} vs {b}: loss {runs[a]['loss']:.6f} / {runs[b]['loss']:.6f}; worst "
-                      + ", ".join(f"{n} {w:.2e}" for w, n in top), flush=True)
+                print(f"{a} vs {b}: loss {runs[a]['loss']:.6f} / {runs[b]['loss']:.6f}", flush=True)
+                for w, n in zip(worst, names):
+                    ref = runs[b]["grads"][n].double()
+                    print(f"   {n:40s} rel {w:.2e}  max|ref| {ref.abs().max().item():.3e}", flush=True)
 
 
 if __name__ == "__main__":
