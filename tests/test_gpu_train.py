@@ -87,12 +87,23 @@ def test_benchmark_batch_train_step_matches_oracle(dev):
     """The bench's own batch (bench.py / BASELINE cfg2): bs 32, all 32 utterances 10 s
     (T = 1001 -> T' = 501), 150-label targets -- the full Trainer.train_batch (both batch tiles
     of the persistent recurrences full, the same-XCD hand-off groups, the stacked W_ih GEMMs,
-    clip, SGD-Nesterov) vs oracle.train_step with the same bounds.  One oracle step at this
-    shape is ~150 s on 16 host threads."""
-    _check_train_step(dev, [1001] * 32, [150] * 32, seed=13)
+    clip, SGD-Nesterov) vs oracle.train_step.  One oracle step at this shape is ~150 s on 16
+    host threads.
+
+    Loss, gradient norm, every recurrent / FC gradient and update: the bounds above.  The conv
+    block (conv.*) is compared at 1e-2: its hardtanh(0, 20) derivative masks flip under
+    last-bit differences -- 4 of 62.6 M between an fp32 and an fp64 forward of the oracle
+    itself -- and each flip moves the block's weight / BN gradients by one position's
+    contribution.  Our own two fp32-accurate paths (bf16x6 and fp32-MFMA) differ by up to
+    5.5e-3 there, the oracle from either by 3.1e-3 / 5.5e-3, while every other gradient
+    agrees within 4.7e-4 (scripts/bs32_probe.py, profiles/r4g_bs32_probe.txt).  With no time
+    step masked, the conv biases' gradients are zero in exact arithmetic (BatchNorm follows
+    each conv): both sides hold rounding noise, bounded against the conv weight gradient's
+    scale."""
+    _check_train_step(dev, [1001] * 32, [150] * 32, seed=13, conv_tol=1e-2, zero_conv_bias=True)
 
 
-def _check_train_step(dev, t_list, label_lens, seed):
+def _check_train_step(dev, t_list, label_lens, seed, conv_tol=5e-4, zero_conv_bias=False):
     _threads()
     g = torch.Generator().manual_seed(seed)
     x = _spect_batch(g, t_list, 1001)
@@ -108,14 +119,24 @@ def _check_train_step(dev, t_list, label_lens, seed):
     assert abs(float(tr.optimizer.norm.item()) - float(rnorm)) <= 1e-4 * float(rnorm)
     worst = {}
     for name, p in m.named_parameters():
-        worst[name] = _rel(p.grad, rgrads[name])
-        assert worst[name] <= 5e-4, (name, worst[name])
-        # the update itself (p_new - p_old), not just p_new (dominated by p_old); both
-        # differences carry the float32 rounding of p_new (half an ulp of |p| each)
+        tol = conv_tol if name.startswith('conv.') else 5e-4
         d = p.detach().cpu() - before[name]
         rd = rnew[name] - before[name]
         ulp = torch.finfo(torch.float32).eps * before[name].abs().max().item()
-        assert (d - rd).abs().max().item() <= 5e-4 * rd.abs().max().item() + ulp, (name, 'update')
+        if zero_conv_bias and name.startswith('conv.') and name.endswith('.bias') \
+                and name.replace('.bias', '.weight') in rgrads \
+                and p.dim() == 1 and rgrads[name.replace('.bias', '.weight')].dim() == 4:
+            # a conv bias (BatchNorm follows): zero up to rounding on both sides
+            scale = torch.as_tensor(rgrads[name.replace('.bias', '.weight')]).abs().max().item()
+            err = (p.grad.detach().double().cpu() - torch.as_tensor(rgrads[name]).double()).abs().max().item()
+            worst[name] = err / scale
+            assert worst[name] <= 5e-4, (name, worst[name])
+            continue
+        worst[name] = _rel(p.grad, rgrads[name])
+        assert worst[name] <= tol, (name, worst[name])
+        # the update itself (p_new - p_old), not just p_new (dominated by p_old); both
+        # differences carry the float32 rounding of p_new (half an ulp of |p| each)
+        assert (d - rd).abs().max().item() <= tol * rd.abs().max().item() + ulp, (name, 'update')
     for k, v in m.state_dict().items():
         if 'running' in k:
             assert _rel(v, o.sd[k]) <= 1e-5, k
