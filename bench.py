@@ -45,7 +45,8 @@ def gemm_peak():
     if os.environ.get("DS2_GEMM_X6", "1")[:1] == "0":
         return PEAK_F32_MFMA_TFLOPS, "fp32 MFMA (v_mfma_f32_16x16x4_f32)"
     return PEAK_X6_TFLOPS, ("fp32 operands split into 3 bf16 terms, 6 products on "
-                            "v_mfma_f32_32x32x16_bf16, fp32 accumulation (bf16 dense peak / 6)")
+                            "v_mfma_f32_16x16x32_bf16 (32x32x16 for a K tail), fp32 "
+                            "accumulation (bf16 dense peak / 6)")
 
 
 def gru_bwd_kernel(x6f: bool):
