@@ -28,10 +28,14 @@ OUT = os.path.join(REPO, "gpurun_out")
 CONF = dict(sample_rate=16000, window_size=0.02, window_stride=0.01, window='hamming')
 
 
-def batch():
-    g = torch.Generator().manual_seed(13)
-    t_list, lab = [1001] * 32, [150] * 32
-    x = torch.zeros(32, 1, 161, 1001)
+BATCHES = {"bs32": ([1001] * 32, [150] * 32, 13),
+           "bs4": ([1001, 877, 508, 254], [150, 120, 80, 40], 11)}   # test_gpu_train's batches
+
+
+def batch(which="bs32"):
+    t_list, lab, seed = BATCHES[which]
+    g = torch.Generator().manual_seed(seed)
+    x = torch.zeros(len(t_list), 1, 161, 1001)
     for i, t in enumerate(t_list):
         x[i, 0, :, :t] = torch.randn(161, t, generator=g)
     tg = []
@@ -75,9 +79,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--mode", choices=["gpu", "oracle", "compare"], required=True)
     ap.add_argument("--tag", default="x6")
+    ap.add_argument("--batch", choices=sorted(BATCHES), default="bs32")
     args = ap.parse_args()
     os.makedirs(OUT, exist_ok=True)
-    x, tg, tl, pct = batch()
+    x, tg, tl, pct = batch(args.batch)
     if args.mode == "gpu":
         from ds2amd.trainer import Trainer
         dev = torch.device("cuda", 0)
@@ -115,7 +120,16 @@ def main():
                     ga = runs[a]["grads"][n].double()
                     gb = runs[b]["grads"][n].double()
                     worst.append(((ga - gb).abs().max() / gb.abs().max().clamp_min(1e-30)).item())
-                print(f"{a} vs {b}: loss {runs[a]['loss']:.6f} / {runs[b]['loss']:.6f}", flush=True)
+                def norms(r):
+                    g = r["grads"]
+                    conv = sum(float(g[n].double().pow(2).sum()) for n in names if n.startswith("conv."))
+                    rest = sum(float(g[n].double().pow(2).sum()) for n in names if not n.startswith("conv."))
+                    return (conv + rest) ** 0.5, conv ** 0.5, rest ** 0.5
+                na, nb_ = norms(runs[a]), norms(runs[b])
+                print(f"{a} vs {b}: loss {runs[a]['loss']:.6f} / {runs[b]['loss']:.6f}; grad norm "
+                      f"{na[0]:.4f} / {nb_[0]:.4f} (rel {abs(na[0] - nb_[0]) / nb_[0]:.2e}); conv block "
+                      f"{na[1]:.4f} / {nb_[1]:.4f} (rel {abs(na[1] - nb_[1]) / nb_[1]:.2e}); rest "
+                      f"{na[2]:.4f} / {nb_[2]:.4f} (rel {abs(na[2] - nb_[2]) / nb_[2]:.2e})", flush=True)
                 for w, n in zip(worst, names):
                     ref = runs[b]["grads"][n].double()
                     print(f"   {n:40s} rel {w:.2e}  max|ref| {ref.abs().max().item():.3e}", flush=True)
