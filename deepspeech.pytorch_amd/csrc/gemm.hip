@@ -771,7 +771,14 @@ __device__ __forceinline__ void x2_split_store(unsigned short* __restrict__ s, i
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       unsigned a, b, c;
+#if defined(DS2_X6_ABL) && DS2_X6_ABL == 3
+      // ablation build: the hi term only (no residual splits)
+      a = __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2{v[2 * j], v[2 * j + 1]}, bf16x2));
+      b = a;
+      c = a;
+#else
       x2_split2(v[2 * j], v[2 * j + 1], a, b, c);
+#endif
       h[j] = a;
       m[j] = b;
       l[j] = c;
@@ -969,11 +976,19 @@ __global__ __launch_bounds__(X2T, 1) void sxgemm2_kernel(
   // stage of latency) while the split of stage kt + 1 reads the other set
   float ra0[OA::F], rb0[BF], ra1[OA::F], rb1[BF];
   auto load = [&](int k0, float (&va)[OA::F], float (&vb)[BF]) {
+#if defined(DS2_X6_ABL) && DS2_X6_ABL == 2
+    // ablation build (scripts/gemm_ablation.sh): no global loads, run-time values instead
+#pragma unroll
+    for (int i = 0; i < OA::F; ++i) va[i] = __builtin_bit_cast(float, (unsigned)(t * 977 + k0 + i) | 0x3f000000u);
+#pragma unroll
+    for (int i = 0; i < BF; ++i) vb[i] = __builtin_bit_cast(float, (unsigned)(t * 613 + k0 + i) | 0x3f000000u);
+#else
     x2_load<AK, X2M, KCHK>(a_rs, ilda, a_voff, K, kend, k0, va);
     if constexpr (TBN == 128)
       x2_load<BKc, TBN, KCHK>(b_rs, ildb, b_voff, K, kend, k0, vb);
     else
       x2_load160<BKc, KCHK>(b_rs, ildb, b_voff, b_ok1, K, kend, k0, vb);
+#endif
   };
   auto bstore = [&](unsigned short* dst, const float (&vb)[BF]) {
     if constexpr (TBN == 128)
@@ -984,7 +999,11 @@ __global__ __launch_bounds__(X2T, 1) void sxgemm2_kernel(
   auto body = [&](int kt, int cur, float (&la)[OA::F], float (&lb)[BF],
                   const float (&sa)[OA::F], const float (&sb)[BF]) {
     // stage kt visible; every wave is done reading the other buffer (stage kt - 1)
+#if defined(DS2_X6_ABL) && DS2_X6_ABL == 4
+    __builtin_amdgcn_wave_barrier();   // ablation build: no workgroup barrier (results invalid)
+#else
     __syncthreads();
+#endif
     load(kbeg + (kt + 2) * XS, la, lb);          // stages past kend load as zeros
     const unsigned short* as = As[cur];
     const unsigned short* bs = Bs[cur];
@@ -1008,7 +1027,14 @@ __global__ __launch_bounds__(X2T, 1) void sxgemm2_kernel(
 #pragma unroll
         for (int p = 0; p < 3; ++p) bq[p] = *reinterpret_cast<const bf16x8*>(bs + p * BP + bt);
 #pragma unroll
-        for (int i = 0; i < WMT; ++i) x2_mma6_16(af[i], bq, acc[i][j]);
+        for (int i = 0; i < WMT; ++i) {
+#if defined(DS2_X6_ABL) && DS2_X6_ABL == 1
+          // ablation build: no MFMA, the fragments kept live
+          asm volatile("" ::"v"(af[i][0]), "v"(af[i][1]), "v"(af[i][2]), "v"(bq[0]), "v"(bq[1]), "v"(bq[2]));
+#else
+          x2_mma6_16(af[i], bq, acc[i][j]);
+#endif
+        }
       }
       x2_store<AK, X2M, NPL, true>(As[cur ^ 1], sa);
       bstore(Bs[cur ^ 1], sb);
