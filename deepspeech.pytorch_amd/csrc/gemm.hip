@@ -1183,6 +1183,286 @@ __global__ __launch_bounds__(X2T, 1) void sxgemm2_kernel(
   job(m0, n0, kbeg, kend, part);
 }
 
+// ---------------------------------------------------------------------------
+// The bf16x6 GEMM with its two halves ping-ponging (256 x 160 tiles, K % 32 == 0, the 16x16x32
+// form).  Ablation builds of sxgemm2_kernel (scripts/gemm_ablation.sh, profiles/
+// r4j_gemm_ablation.txt) showed its MFMA work and everything else -- staging loads, the split,
+// the LDS traffic, the barrier -- running one after the other: without MFMAs it took 52-65 % of
+// the time, the MFMAs alone would take about half.  Here the eight waves form two groups
+// (waves 0-3: tile rows 0-127, waves 4-7: rows 128-255) one barrier interval apart, so in
+// every interval one wave per SIMD issues MFMAs while its partner stages and reads fragments:
+//   stage s, phase 0: [split + store the group's A rows of stage s + 1, issue their loads for
+//                      stage s + 2, read the A fragments and B n-tiles 0-4] barrier
+//                     [60 MFMAs] barrier
+//            phase 1: [split + store the group's B rows (group 0: 0-79, group 1: 80-159) of
+//                      stage s + 1, issue their loads for stage s + 2, read B n-tiles 5-9]
+//                     barrier [60 MFMAs] barrier
+// Every LDS write lands at least one barrier before its first reader, and the buffer it
+// overwrites (stage s - 1's) was last read at least one barrier earlier, with each load
+// segment's LDS operations retired (lgkmcnt(0)) before its barrier.  A thread's staging
+// loads are the same instructions every stage (a stage past the end loads a clamped,
+// unused k), so the counted waits are exact: phase 0 waits for the A loads issued a stage
+// earlier with the B loads after them still in flight, phase 1 the other way round.
+constexpr int PP_BN = 160;
+constexpr int PP_BP = PP_BN * XS;   // bf16 per B plane
+constexpr int kPpOob = 0x7ffffff0;
+
+// a raw s_barrier no memory operation moves across (the counted vmcnt stays in force)
+__device__ __forceinline__ void pp_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("" ::: "memory");
+}
+
+template <int TA, int TB>
+__global__ __launch_bounds__(X2T, 1) void sxgemm_pp_kernel(
+    int M, int N, int K, float alpha, const float* __restrict__ A, int64_t lda, int64_t sA,
+    const float* __restrict__ B, int64_t ldb, int64_t sB, float beta, float* __restrict__ C,
+    int64_t ldc, int64_t sC, const float* __restrict__ bias, int main_wgs, int tail_tile0,
+    int tail_tiles, int nsplit, int kchunk, float* __restrict__ partial) {
+  constexpr bool AK = (TA == 0);    // A stored [m][k]
+  constexpr bool BKc = (TB == 1);   // B stored [n][k]
+  __shared__ __attribute__((aligned(16))) unsigned short As[2][3 * X2_AP];
+  __shared__ __attribute__((aligned(16))) unsigned short Bs[2][3 * PP_BP];
+  int m0, n0, kbeg, kend, bz;
+  float* part;
+  decode_work(M, N, K, main_wgs, tail_tile0, tail_tiles, nsplit, kchunk, partial, m0, n0, kbeg,
+              kend, bz, part, PP_BN, X2M);
+  A += bz * sA;
+  B += bz * sB;
+  C += bz * sC;
+  const int a_rows = AK ? M : K, b_rows = BKc ? N : K;
+  const __amdgpu_buffer_rsrc_t a_rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(A), (short)0, static_cast<int>(a_rows * lda * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t b_rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(B), (short)0, static_cast<int>(b_rows * ldb * 4), 0x00020000);
+  const int ilda = static_cast<int>(lda), ildb = static_cast<int>(ldb);
+  const int t = threadIdx.x;
+  const int lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int grp = wave >> 2;           // 0: tile rows 0-127, 1: rows 128-255
+  const int tg = t & 255;              // thread within the group
+  const int wm = wave * 32;            // the wave's 32 rows
+  const int r16 = lane & 15, s16 = lane >> 4;
+
+  // ---- staging of the group's share: A rows [128 grp, +128) (16 floats per thread),
+  // B rows [80 grp, +80) (two 8-float units; the second real for the group's first wave only,
+  // the other waves issue the same loads out of range so every wave's load count is equal)
+  int a_vo[2] = {kPpOob, kPpOob}, a_row[2] = {0, 0}, a_slot[2] = {0, 0};
+  if (AK) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int u = tg + 256 * j;
+      a_row[j] = 128 * grp + (u >> 2);
+      a_slot[j] = u & 3;
+      const int r = m0 + a_row[j];
+      if (r < M) a_vo[j] = (r * ilda + 8 * a_slot[j]) * 4;
+    }
+  } else {
+    a_row[0] = 128 * grp + (tg & 127);
+    a_slot[0] = 2 * (tg >> 7);         // 16 k from slot 2 (tg >> 7): wave-uniform
+    const int r = m0 + a_row[0];
+    if (r < M) a_vo[0] = r * 4;
+  }
+  int b_vo[2] = {kPpOob, kPpOob}, b_row[2] = {0, 0}, b_slot[2] = {0, 0};
+  const bool b_u1 = tg < 64;           // the second B unit (rows 64-79 of the share)
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int u = j == 0 ? tg : tg + 256;   // 320 units of (row, 8-k slot) per group
+    if (BKc) {
+      b_row[j] = 80 * grp + ((u >> 2) < 80 ? (u >> 2) : 79);
+      b_slot[j] = u & 3;
+      const int r = n0 + b_row[j];
+      if ((j == 0 || b_u1) && r < N) b_vo[j] = (r * ildb + 8 * b_slot[j]) * 4;
+    } else {
+      const int uu = u < 320 ? u : 319;
+      b_row[j] = 80 * grp + uu % 80;
+      b_slot[j] = uu / 80;
+      const int r = n0 + b_row[j];
+      if ((j == 0 || b_u1) && r < N) b_vo[j] = (r + 8 * b_slot[j] * ildb) * 4;
+    }
+  }
+  float va[16], vb[16];
+  auto load_a = [&](int k0) {
+    if (AK) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int kw = k0 + 4 * h;
+          const f32x4 x = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                        a_rs, a_vo[j], kw < K ? kw * 4 : 0, 0));
+#pragma unroll
+          for (int c = 0; c < 4; ++c) va[8 * j + 4 * h + c] = x[c];
+        }
+    } else {
+      // the 16-k run (slot pair a_slot) is wave-uniform: all of k in the scalar offset
+      const int kb = (k0 < K ? k0 : 0) + 8 * __builtin_amdgcn_readfirstlane(a_slot[0]);
+#pragma unroll
+      for (int i = 0; i < 16; ++i)
+        va[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                              a_rs, a_vo[0], (kb + i) * ilda * 4, 0));
+    }
+  };
+  auto load_b = [&](int k0) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      if (BKc) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int kw = k0 + 4 * h;
+          const f32x4 x = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                        b_rs, b_vo[j], kw < K ? kw * 4 : 0, 0));
+#pragma unroll
+          for (int c = 0; c < 4; ++c) vb[8 * j + 4 * h + c] = x[c];
+        }
+      } else {
+        // the unit's slot (8 slot rows of B) is in its vector offset, the stage's k0 + i in the
+        // wave-uniform scalar one (a stage past the end reads stage 0's rows, unused)
+        const int kk = k0 < K ? k0 : 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          vb[8 * j + i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                        b_rs, b_vo[j], (kk + i) * ildb * 4, 0));
+      }
+    }
+  };
+  auto store_a = [&](unsigned short* dst) {
+    if (AK) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) x2_split_store<3>(dst, X2_AP, xslot_t<true>(a_row[j], a_slot[j]), va + 8 * j);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) x2_split_store<3>(dst, X2_AP, xslot_t<true>(a_row[0], a_slot[0] + j), va + 8 * j);
+    }
+  };
+  auto store_b = [&](unsigned short* dst) {
+    x2_split_store<3>(dst, PP_BP, xslot_t<true>(b_row[0], b_slot[0]), vb);
+    if (b_u1) x2_split_store<3>(dst, PP_BP, xslot_t<true>(b_row[1], b_slot[1]), vb + 8);
+  };
+  constexpr int NA = AK ? 4 : 16;      // a thread's A load instructions per stage
+  constexpr int NB = BKc ? 4 : 16;     // its B load instructions per stage
+  // LATE (an operand with scalar loads): each share's loads are issued one phase later --
+  // B's for stage s + 1 in phase 0 of stage s, A's for stage s + 2 in phase 1 -- so only one
+  // share is in flight during a MFMA segment (16 VGPRs fewer; two barrier intervals of
+  // latency per load instead of four)
+  constexpr bool LATE = !(AK && BKc);
+
+  f32x4 acc[2][10];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 10; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int S = (kend - kbeg) / XS;
+  // prologue: stage 0 staged by both groups, stage 1's loads in flight (LATE: A's only)
+  load_a(kbeg);
+  load_b(kbeg);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  store_a(As[0]);
+  store_b(Bs[0]);
+  load_a(kbeg + XS);
+  if (!LATE) load_b(kbeg + XS);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  pp_barrier();
+  if (grp == 1) pp_barrier();          // group 1 runs one interval behind
+
+  bf16x8 af[2][3], bq[5][3];
+  for (int s = 0; s < S; ++s) {
+    const unsigned short* as = As[s & 1];
+    const unsigned short* bs = Bs[s & 1];
+    const bool stage_next = s + 1 < S;
+    // ---- phase 0, load segment: A share of stage s + 1, A fragments, B n-tiles 0-4
+    if (stage_next) {
+      if constexpr (LATE) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      else if constexpr (NB == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+      store_a(As[(s + 1) & 1]);
+    }
+    if constexpr (LATE) load_b(kbeg + (s + 1) * XS);
+    else load_a(kbeg + (s + 2) * XS);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int at = xslot_t<true>(wm + 16 * i + r16, s16);
+#pragma unroll
+      for (int p = 0; p < 3; ++p) af[i][p] = *reinterpret_cast<const bf16x8*>(as + p * X2_AP + at);
+    }
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+      const int bt = xslot_t<true>(16 * j + r16, s16);
+#pragma unroll
+      for (int p = 0; p < 3; ++p) bq[j][p] = *reinterpret_cast<const bf16x8*>(bs + p * PP_BP + bt);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    pp_barrier();
+    // ---- phase 0, MFMA segment
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int j = 0; j < 5; ++j)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) x2_mma6_16(af[i], bq[j], acc[i][j]);
+    __builtin_amdgcn_s_setprio(0);
+    pp_barrier();
+    // ---- phase 1, load segment: B share of stage s + 1, B n-tiles 5-9
+    if (stage_next) {
+      if constexpr (LATE) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      else if constexpr (NA == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+      store_b(Bs[(s + 1) & 1]);
+    }
+    if constexpr (LATE) load_a(kbeg + (s + 2) * XS);
+    else load_b(kbeg + (s + 2) * XS);
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+      const int bt = xslot_t<true>(16 * (j + 5) + r16, s16);
+#pragma unroll
+      for (int p = 0; p < 3; ++p) bq[j][p] = *reinterpret_cast<const bf16x8*>(bs + p * PP_BP + bt);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    pp_barrier();
+    // ---- phase 1, MFMA segment
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int j = 0; j < 5; ++j)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) x2_mma6_16(af[i], bq[j], acc[i][j + 5]);
+    __builtin_amdgcn_s_setprio(0);
+    pp_barrier();
+  }
+  if (grp == 0) pp_barrier();          // equal barrier counts
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the clamped loads past the end
+
+  // epilogue (16x16 C/D map: col = lane & 15, row = 4 (lane >> 4) + r)
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+#pragma unroll
+    for (int j = 0; j < 10; ++j) {
+      const int cl = 16 * j + (lane & 15);
+      const int rb = wm + 16 * i + 4 * (lane >> 4);
+      if (part != nullptr) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) part[(rb + r) * PP_BN + cl] = acc[i][j][r];
+        continue;
+      }
+      const int col = n0 + cl;
+      if (col >= N) continue;
+      const float bv = bias != nullptr ? bias[col] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + rb + r;
+        if (row < M) {
+          float* cp = C + (int64_t)row * ldc + col;
+          float v = alpha * acc[i][j][r] + bv;
+          if (beta != 0.f) v += beta * *cp;
+          *cp = v;
+        }
+      }
+    }
+  }
+}
+
 // Tail tiles: C[b] = alpha * sum_s partial[b][s][tile] + beta * C[b] + bias (fixed order)
 __global__ void splitk_reduce_kernel(const float* __restrict__ partial, int M, int N, int nsplit,
                                      int batch, int tail_tile0, int tail_tiles, float alpha,
@@ -1282,6 +1562,13 @@ static bool x6_enabled(bool va, bool vb) {
   if (!va || !vb) return false;
   const char* e = getenv("DS2_GEMM_X6");
   return !(e != nullptr && e[0] == '0');
+}
+
+// A/B switch: DS2_GEMM_PP=1 runs the ping-pong bf16x6 kernel (sxgemm_pp_kernel) on 160-wide
+// tiles without a K tail
+static bool pp_enabled() {
+  const char* e = getenv("DS2_GEMM_PP");
+  return e != nullptr && e[0] == '1';
 }
 
 // 32-bit buffer offsets: each operand (one batch entry) must span < 2^31 bytes
@@ -1413,8 +1700,13 @@ extern "C" ds2_status_t ds2_sgemm_ws(int trans_a, int trans_b, int m, int n, int
   // the 16x16x32 form wherever every stage lies inside K (r4d: 0-15 % faster on the step's
   // shapes, profiles/r4d_gemm_x6_m16_sk_ab.txt), the 32x32x16 form for a K tail
   const bool m16 = x6 && kalign;
+  const bool pp = m16 && pp_enabled();
 #define DS2_G(TA_, TB_)                                                                       \
-  if (m16 && p.bn == 160) DS2_X6(TA_, TB_, false, 160, true);                               \
+  if (pp && p.bn == 160)                                                                      \
+    hipLaunchKernelGGL((sxgemm_pp_kernel<TA_, TB_>), grid, dim3(X2T), 0, st, m, n, k, alpha, a, \
+                       lda, stride_a, b, ldb, stride_b, beta, c, ldc, stride_c, bias,          \
+                       p.main_wgs, p.tail_tile0, p.tail_tiles, p.nsplit, p.kchunk, partial);   \
+  else if (m16 && p.bn == 160) DS2_X6(TA_, TB_, false, 160, true);                          \
   else if (m16) DS2_X6(TA_, TB_, false, 128, true);                                          \
   else if (x6 && kalign && p.bn == 160) DS2_X6(TA_, TB_, false, 160, false);                 \
   else if (x6 && p.bn == 160) DS2_X6(TA_, TB_, true, 160, false);                            \

@@ -56,14 +56,17 @@ def main():
         scale = ref.abs().max().item()
         line = f"{name:12s} {m:6d}x{n:5d}x{k:6d} |"
         # alternating twice (the clock the chip holds differs by body)
-        for tag, env, peak in (("x6", "1", PEAKX6), ("fp32", "0", PEAK32),
-                               ("x6", "1", PEAKX6), ("fp32", "0", PEAK32)):
+        for tag, env, pp, peak in (("x6", "1", "0", PEAKX6), ("x6pp", "1", "1", PEAKX6),
+                                   ("x6", "1", "0", PEAKX6), ("x6pp", "1", "1", PEAKX6),
+                                   ("fp32", "0", "0", PEAK32)):
             os.environ["DS2_GEMM_X6"] = env
+            os.environ["DS2_GEMM_PP"] = pp
             t = timeit(lambda: ops.sgemm(a, b, c, **kw), iters=30)
             err = (c.double() - ref).abs().max().item() / scale
             tf = fl / t / 1e9
             line += f" {tag} {tf:6.1f} TF ({tf / peak:4.0%}) {t * 1e3:7.1f} us err {err:.1e} |"
         os.environ.pop("DS2_GEMM_X6", None)
+        os.environ.pop("DS2_GEMM_PP", None)
         print(line, flush=True)
 
 
