@@ -1184,31 +1184,35 @@ __global__ __launch_bounds__(X2T, 1) void sxgemm2_kernel(
 }
 
 // ---------------------------------------------------------------------------
-// The bf16x6 GEMM with its two halves ping-ponging (256 x 160 tiles, K % 32 == 0, the 16x16x32
-// form).  Ablation builds of sxgemm2_kernel (scripts/gemm_ablation.sh, profiles/
-// r4j_gemm_ablation.txt) showed its MFMA work and everything else -- staging loads, the split,
-// the LDS traffic, the barrier -- running one after the other: without MFMAs it took 52-65 % of
-// the time, the MFMAs alone would take about half.  Here the eight waves form two groups
-// (waves 0-3: tile rows 0-127, waves 4-7: rows 128-255) one barrier interval apart, so in
-// every interval one wave per SIMD issues MFMAs while its partner stages and reads fragments:
-//   stage s, phase 0: [split + store the group's A rows of stage s + 1, issue their loads for
-//                      stage s + 2, read the A fragments and B n-tiles 0-4] barrier
-//                     [60 MFMAs] barrier
-//            phase 1: [split + store the group's B rows (group 0: 0-79, group 1: 80-159) of
-//                      stage s + 1, issue their loads for stage s + 2, read B n-tiles 5-9]
-//                     barrier [60 MFMAs] barrier
-// Every LDS write lands at least one barrier before its first reader, and the buffer it
-// overwrites (stage s - 1's) was last read at least one barrier earlier, with each load
-// segment's LDS operations retired (lgkmcnt(0)) before its barrier.  A thread's staging
-// loads are the same instructions every stage (a stage past the end loads a clamped,
-// unused k), so the counted waits are exact: phase 0 waits for the A loads issued a stage
-// earlier with the B loads after them still in flight, phase 1 the other way round.
-constexpr int PP_BN = 160;
-constexpr int PP_BP = PP_BN * XS;   // bf16 per B plane
-constexpr int kPpOob = 0x7ffffff0;
+// The bf16x6 GEMM on pre-split operand planes (the default for large batch-1 products).
+// Ablation builds of sxgemm2_kernel (scripts/gemm_ablation.sh, profiles/r4j_gemm_ablation.txt)
+// showed its staging -- the split VALU and, above all, the 80 KB of ds_write_b128 per stage
+// (3 bf16 planes of 416 rows x 32 k) -- running beside the MFMAs, not under them: without
+// MFMAs the kernel still took 52-65 % of its time.  Here each operand is split ONCE by
+// x6_split_kernel into three k-contiguous bf16 planes in HBM,
+//   X3[p][r][kp], p = hi / mid / lo, kp < Kp = K rounded up to 32 (zeros past K),
+// and the GEMM kernel fills its LDS stages by LDS-DMA (buffer_load ... lds, 16 B per lane):
+// no staging VALU, no ds_write, no register round trip.  The split is x2_split2's, so the
+// planes hold exactly the values the in-kernel split produces.
+//
+// Tile 256 x 160 x 32 (k) per workgroup of 8 waves (4 M x 2 N, each 64 x 80 = 4 x 5 tiles of
+// v_mfma_f32_16x16x32_bf16, 6 products per tile and k-step, small terms first); two LDS
+// stages of 3 x (256 + 160) rows x 64 B = 78 KB.  A stage is 78 one-KB DMA blocks (16 rows of
+// one plane, lane-linear in LDS, the xslot_t<true> swizzle applied to the source address);
+// wave w issues blocks w, w + 8, ... .  Per stage: issue the DMA of stage kt + 1 into the
+// other buffer, fragments + MFMAs of stage kt, wait for the own DMA (vmcnt(0)), one barrier
+// (it publishes stage kt + 1 and retires every read of stage kt before its buffer is
+// refilled).
+constexpr int XD_BN = 160;
+constexpr int XD_APL = X2M * XS;                 // bf16 per A plane in LDS
+constexpr int XD_BPL = XD_BN * XS;               // bf16 per B plane
+constexpr int XD_IMG = 3 * (XD_APL + XD_BPL);    // bf16 per stage (79,872 B)
+constexpr int XD_ABLK = 3 * X2M / 16;            // 48 A blocks per stage
+constexpr int XD_NBLK = XD_ABLK + 3 * XD_BN / 16;   // 78
+constexpr int XD_BPW = (XD_NBLK + 7) / 8;        // blocks per wave (waves 6, 7 issue one fewer)
+static_assert(2 * XD_IMG * 2 <= 160 * 1024, "two DMA stages");
 
-// a raw s_barrier no memory operation moves across (the counted vmcnt stays in force)
-__device__ __forceinline__ void pp_barrier() {
+__device__ __forceinline__ void xd_barrier() {
   asm volatile("" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
   __builtin_amdgcn_s_barrier();
@@ -1216,234 +1220,101 @@ __device__ __forceinline__ void pp_barrier() {
   asm volatile("" ::: "memory");
 }
 
-template <int TA, int TB>
-__global__ __launch_bounds__(X2T, 1) void sxgemm_pp_kernel(
-    int M, int N, int K, float alpha, const float* __restrict__ A, int64_t lda, int64_t sA,
-    const float* __restrict__ B, int64_t ldb, int64_t sB, float beta, float* __restrict__ C,
-    int64_t ldc, int64_t sC, const float* __restrict__ bias, int main_wgs, int tail_tile0,
-    int tail_tiles, int nsplit, int kchunk, float* __restrict__ partial) {
-  constexpr bool AK = (TA == 0);    // A stored [m][k]
-  constexpr bool BKc = (TB == 1);   // B stored [n][k]
-  __shared__ __attribute__((aligned(16))) unsigned short As[2][3 * X2_AP];
-  __shared__ __attribute__((aligned(16))) unsigned short Bs[2][3 * PP_BP];
+__global__ __launch_bounds__(X2T, 1) void sxgemm_dma_kernel(
+    int M, int N, int Kp, float alpha, const unsigned short* __restrict__ A3,
+    const unsigned short* __restrict__ B3, float beta, float* __restrict__ C, int64_t ldc,
+    const float* __restrict__ bias, int main_wgs, int tail_tile0, int tail_tiles, int nsplit,
+    int kchunk, float* __restrict__ partial) {
+  __shared__ __attribute__((aligned(16))) unsigned short lds[2 * XD_IMG];
   int m0, n0, kbeg, kend, bz;
   float* part;
-  decode_work(M, N, K, main_wgs, tail_tile0, tail_tiles, nsplit, kchunk, partial, m0, n0, kbeg,
-              kend, bz, part, PP_BN, X2M);
-  A += bz * sA;
-  B += bz * sB;
-  C += bz * sC;
-  const int a_rows = AK ? M : K, b_rows = BKc ? N : K;
-  const __amdgpu_buffer_rsrc_t a_rs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float*>(A), (short)0, static_cast<int>(a_rows * lda * 4), 0x00020000);
-  const __amdgpu_buffer_rsrc_t b_rs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float*>(B), (short)0, static_cast<int>(b_rows * ldb * 4), 0x00020000);
-  const int ilda = static_cast<int>(lda), ildb = static_cast<int>(ldb);
+  decode_work(M, N, Kp, main_wgs, tail_tile0, tail_tiles, nsplit, kchunk, partial, m0, n0, kbeg,
+              kend, bz, part, XD_BN, X2M);
   const int t = threadIdx.x;
   const int lane = t & 63;
   const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int grp = wave >> 2;           // 0: tile rows 0-127, 1: rows 128-255
-  const int tg = t & 255;              // thread within the group
-  const int wm = wave * 32;            // the wave's 32 rows
-  const int r16 = lane & 15, s16 = lane >> 4;
+  const __amdgpu_buffer_rsrc_t a_rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<unsigned short*>(A3), (short)0, static_cast<int>(3ll * M * Kp * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t b_rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<unsigned short*>(B3), (short)0, static_cast<int>(3ll * N * Kp * 2), 0x00020000);
+  constexpr int kOob = 0x7ffffff0;
 
-  // ---- staging of the group's share: A rows [128 grp, +128) (16 floats per thread),
-  // B rows [80 grp, +80) (two 8-float units; the second real for the group's first wave only,
-  // the other waves issue the same loads out of range so every wave's load count is equal)
-  int a_vo[2] = {kPpOob, kPpOob}, a_row[2] = {0, 0}, a_slot[2] = {0, 0};
-  if (AK) {
+  // this wave's DMA blocks: lane L of block b fills LDS chunk L (tile row 16 rb + L / 4, slot
+  // position L & 3) with source slot (L & 3) ^ ((row >> 1) & 3) of its plane row
+  int soff[XD_BPW], loff[XD_BPW];
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int u = tg + 256 * j;
-      a_row[j] = 128 * grp + (u >> 2);
-      a_slot[j] = u & 3;
-      const int r = m0 + a_row[j];
-      if (r < M) a_vo[j] = (r * ilda + 8 * a_slot[j]) * 4;
-    }
-  } else {
-    a_row[0] = 128 * grp + (tg & 127);
-    a_slot[0] = 2 * (tg >> 7);         // 16 k from slot 2 (tg >> 7): wave-uniform
-    const int r = m0 + a_row[0];
-    if (r < M) a_vo[0] = r * 4;
+  for (int i = 0; i < XD_BPW; ++i) {
+    const int b = wave + 8 * i;
+    const bool isa = b < XD_ABLK;
+    const int bb = isa ? b : b - XD_ABLK;
+    const int nrb = isa ? X2M / 16 : XD_BN / 16;
+    const int p = bb / nrb, rb = bb - p * nrb;
+    const int tr = 16 * rb + (lane >> 2);                 // row within the tile
+    const int gr = (isa ? m0 : n0) + tr;
+    const int lim = isa ? M : N;
+    const int gs = (lane & 3) ^ ((tr >> 1) & 3);
+    soff[i] = (b < XD_NBLK && gr < lim) ? (((p * lim + gr) * Kp) + 8 * gs) * 2 : kOob;
+    loff[i] = (isa ? 0 : 3 * XD_APL) + p * (isa ? XD_APL : XD_BPL) + 512 * rb;
   }
-  int b_vo[2] = {kPpOob, kPpOob}, b_row[2] = {0, 0}, b_slot[2] = {0, 0};
-  const bool b_u1 = tg < 64;           // the second B unit (rows 64-79 of the share)
+  auto issue = [&](int k0, int buf) {
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int u = j == 0 ? tg : tg + 256;   // 320 units of (row, 8-k slot) per group
-    if (BKc) {
-      b_row[j] = 80 * grp + ((u >> 2) < 80 ? (u >> 2) : 79);
-      b_slot[j] = u & 3;
-      const int r = n0 + b_row[j];
-      if ((j == 0 || b_u1) && r < N) b_vo[j] = (r * ildb + 8 * b_slot[j]) * 4;
-    } else {
-      const int uu = u < 320 ? u : 319;
-      b_row[j] = 80 * grp + uu % 80;
-      b_slot[j] = uu / 80;
-      const int r = n0 + b_row[j];
-      if ((j == 0 || b_u1) && r < N) b_vo[j] = (r + 8 * b_slot[j] * ildb) * 4;
-    }
-  }
-  float va[16], vb[16];
-  auto load_a = [&](int k0) {
-    if (AK) {
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int kw = k0 + 4 * h;
-          const f32x4 x = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                        a_rs, a_vo[j], kw < K ? kw * 4 : 0, 0));
-#pragma unroll
-          for (int c = 0; c < 4; ++c) va[8 * j + 4 * h + c] = x[c];
-        }
-    } else {
-      // the 16-k run (slot pair a_slot) is wave-uniform: all of k in the scalar offset
-      const int kb = (k0 < K ? k0 : 0) + 8 * __builtin_amdgcn_readfirstlane(a_slot[0]);
-#pragma unroll
-      for (int i = 0; i < 16; ++i)
-        va[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                              a_rs, a_vo[0], (kb + i) * ilda * 4, 0));
-    }
-  };
-  auto load_b = [&](int k0) {
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      if (BKc) {
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int kw = k0 + 4 * h;
-          const f32x4 x = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                        b_rs, b_vo[j], kw < K ? kw * 4 : 0, 0));
-#pragma unroll
-          for (int c = 0; c < 4; ++c) vb[8 * j + 4 * h + c] = x[c];
-        }
-      } else {
-        // the unit's slot (8 slot rows of B) is in its vector offset, the stage's k0 + i in the
-        // wave-uniform scalar one (a stage past the end reads stage 0's rows, unused)
-        const int kk = k0 < K ? k0 : 0;
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-          vb[8 * j + i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                                        b_rs, b_vo[j], (kk + i) * ildb * 4, 0));
+    for (int i = 0; i < XD_BPW; ++i) {
+      if (wave + 8 * i < XD_NBLK) {
+        unsigned short* dst = lds + buf * XD_IMG + loff[i];
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            wave + 8 * i < XD_ABLK ? a_rs : b_rs, (__attribute__((address_space(3))) void*)dst, 16,
+            soff[i], k0 * 2, 0, 0);
       }
     }
   };
-  auto store_a = [&](unsigned short* dst) {
-    if (AK) {
-#pragma unroll
-      for (int j = 0; j < 2; ++j) x2_split_store<3>(dst, X2_AP, xslot_t<true>(a_row[j], a_slot[j]), va + 8 * j);
-    } else {
-#pragma unroll
-      for (int j = 0; j < 2; ++j) x2_split_store<3>(dst, X2_AP, xslot_t<true>(a_row[0], a_slot[0] + j), va + 8 * j);
-    }
-  };
-  auto store_b = [&](unsigned short* dst) {
-    x2_split_store<3>(dst, PP_BP, xslot_t<true>(b_row[0], b_slot[0]), vb);
-    if (b_u1) x2_split_store<3>(dst, PP_BP, xslot_t<true>(b_row[1], b_slot[1]), vb + 8);
-  };
-  constexpr int NA = AK ? 4 : 16;      // a thread's A load instructions per stage
-  constexpr int NB = BKc ? 4 : 16;     // its B load instructions per stage
-  // LATE (an operand with scalar loads): each share's loads are issued one phase later --
-  // B's for stage s + 1 in phase 0 of stage s, A's for stage s + 2 in phase 1 -- so only one
-  // share is in flight during a MFMA segment (16 VGPRs fewer; two barrier intervals of
-  // latency per load instead of four)
-  constexpr bool LATE = !(AK && BKc);
 
-  f32x4 acc[2][10];
+  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 80;
+  const int r16 = lane & 15, s16 = lane >> 4;
+  f32x4 acc[4][5];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 10; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < 5; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int S = (kend - kbeg) / XS;
-  // prologue: stage 0 staged by both groups, stage 1's loads in flight (LATE: A's only)
-  load_a(kbeg);
-  load_b(kbeg);
+  const int KT = (kend - kbeg) / XS;
+  issue(kbeg, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  store_a(As[0]);
-  store_b(Bs[0]);
-  load_a(kbeg + XS);
-  if (!LATE) load_b(kbeg + XS);
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  pp_barrier();
-  if (grp == 1) pp_barrier();          // group 1 runs one interval behind
-
-  bf16x8 af[2][3], bq[5][3];
-  for (int s = 0; s < S; ++s) {
-    const unsigned short* as = As[s & 1];
-    const unsigned short* bs = Bs[s & 1];
-    const bool stage_next = s + 1 < S;
-    // ---- phase 0, load segment: A share of stage s + 1, A fragments, B n-tiles 0-4
-    if (stage_next) {
-      if constexpr (LATE) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      else if constexpr (NB == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-      store_a(As[(s + 1) & 1]);
-    }
-    if constexpr (LATE) load_b(kbeg + (s + 1) * XS);
-    else load_a(kbeg + (s + 2) * XS);
+  xd_barrier();
+  for (int kt = 0; kt < KT; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < KT) issue(kbeg + (kt + 1) * XS, cur ^ 1);
+    const unsigned short* as = lds + cur * XD_IMG;
+    const unsigned short* bs = as + 3 * XD_APL;
+    bf16x8 af[4][3];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < 4; ++i) {
       const int at = xslot_t<true>(wm + 16 * i + r16, s16);
 #pragma unroll
-      for (int p = 0; p < 3; ++p) af[i][p] = *reinterpret_cast<const bf16x8*>(as + p * X2_AP + at);
+      for (int p = 0; p < 3; ++p) af[i][p] = *reinterpret_cast<const bf16x8*>(as + p * XD_APL + at);
     }
 #pragma unroll
     for (int j = 0; j < 5; ++j) {
-      const int bt = xslot_t<true>(16 * j + r16, s16);
+      bf16x8 bq[3];
+      const int bt = xslot_t<true>(wn + 16 * j + r16, s16);
 #pragma unroll
-      for (int p = 0; p < 3; ++p) bq[j][p] = *reinterpret_cast<const bf16x8*>(bs + p * PP_BP + bt);
+      for (int p = 0; p < 3; ++p) bq[p] = *reinterpret_cast<const bf16x8*>(bs + p * XD_BPL + bt);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) x2_mma6_16(af[i], bq, acc[i][j]);
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    pp_barrier();
-    // ---- phase 0, MFMA segment
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int j = 0; j < 5; ++j)
-#pragma unroll
-      for (int i = 0; i < 2; ++i) x2_mma6_16(af[i], bq[j], acc[i][j]);
-    __builtin_amdgcn_s_setprio(0);
-    pp_barrier();
-    // ---- phase 1, load segment: B share of stage s + 1, B n-tiles 5-9
-    if (stage_next) {
-      if constexpr (LATE) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      else if constexpr (NA == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-      store_b(Bs[(s + 1) & 1]);
-    }
-    if constexpr (LATE) load_a(kbeg + (s + 2) * XS);
-    else load_b(kbeg + (s + 2) * XS);
-#pragma unroll
-    for (int j = 0; j < 5; ++j) {
-      const int bt = xslot_t<true>(16 * (j + 5) + r16, s16);
-#pragma unroll
-      for (int p = 0; p < 3; ++p) bq[j][p] = *reinterpret_cast<const bf16x8*>(bs + p * PP_BP + bt);
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    pp_barrier();
-    // ---- phase 1, MFMA segment
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int j = 0; j < 5; ++j)
-#pragma unroll
-      for (int i = 0; i < 2; ++i) x2_mma6_16(af[i], bq[j], acc[i][j + 5]);
-    __builtin_amdgcn_s_setprio(0);
-    pp_barrier();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    xd_barrier();
   }
-  if (grp == 0) pp_barrier();          // equal barrier counts
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the clamped loads past the end
 
   // epilogue (16x16 C/D map: col = lane & 15, row = 4 (lane >> 4) + r)
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < 4; ++i) {
 #pragma unroll
-    for (int j = 0; j < 10; ++j) {
-      const int cl = 16 * j + (lane & 15);
+    for (int j = 0; j < 5; ++j) {
+      const int cl = wn + 16 * j + (lane & 15);
       const int rb = wm + 16 * i + 4 * (lane >> 4);
       if (part != nullptr) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) part[(rb + r) * PP_BN + cl] = acc[i][j][r];
+        for (int r = 0; r < 4; ++r) part[(rb + r) * XD_BN + cl] = acc[i][j][r];
         continue;
       }
       const int col = n0 + cl;
@@ -1459,6 +1330,197 @@ __global__ __launch_bounds__(X2T, 1) void sxgemm_pp_kernel(
           *cp = v;
         }
       }
+    }
+  }
+}
+
+// The same product with the eight waves as two groups one barrier interval apart (waves 0-3:
+// tile rows 0-127, waves 4-7: rows 128-255; per SIMD one wave of each), so in every interval
+// one wave per SIMD issues MFMAs while its partner reads fragments and issues DMA.  Stage s,
+// interval I_n = (barrier n, barrier n + 1), group 0 / group 1:
+//   phase 0  load [A frags i 0-1, B frags j 0-4, DMA of stage s + 1]  I_4s     / I_4s+1
+//            MFMA [60: i 0-1 x j 0-4]                                 I_4s+1   / I_4s+2
+//   phase 1  load [A frags i 2-3, wait for the own DMA]               I_4s+2   / I_4s+3
+//            MFMA [60: i 2-3 x j 0-4]                                 I_4s+3   / I_4s+4
+// Stage s + 1's buffer held stage s - 1, last read by group 1 in I_4s-1 (retired by
+// lgkmcnt(0) before barrier 4s: WAR); its DMA is complete before barrier 4s + 4 (each wave's
+// vmcnt(0) in I_4s+2 / I_4s+3), first read by group 0 in I_4s+4 (RAW).
+__global__ __launch_bounds__(X2T, 1) void sxgemm_dma_pp_kernel(
+    int M, int N, int Kp, float alpha, const unsigned short* __restrict__ A3,
+    const unsigned short* __restrict__ B3, float beta, float* __restrict__ C, int64_t ldc,
+    const float* __restrict__ bias, int main_wgs, int tail_tile0, int tail_tiles, int nsplit,
+    int kchunk, float* __restrict__ partial) {
+  __shared__ __attribute__((aligned(16))) unsigned short lds[2 * XD_IMG];
+  int m0, n0, kbeg, kend, bz;
+  float* part;
+  decode_work(M, N, Kp, main_wgs, tail_tile0, tail_tiles, nsplit, kchunk, partial, m0, n0, kbeg,
+              kend, bz, part, XD_BN, X2M);
+  const int t = threadIdx.x;
+  const int lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int grp = wave >> 2;
+  const __amdgpu_buffer_rsrc_t a_rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<unsigned short*>(A3), (short)0, static_cast<int>(3ll * M * Kp * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t b_rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<unsigned short*>(B3), (short)0, static_cast<int>(3ll * N * Kp * 2), 0x00020000);
+  constexpr int kOob = 0x7ffffff0;
+  int soff[XD_BPW], loff[XD_BPW];
+#pragma unroll
+  for (int i = 0; i < XD_BPW; ++i) {
+    const int b = wave + 8 * i;
+    const bool isa = b < XD_ABLK;
+    const int bb = isa ? b : b - XD_ABLK;
+    const int nrb = isa ? X2M / 16 : XD_BN / 16;
+    const int p = bb / nrb, rb = bb - p * nrb;
+    const int tr = 16 * rb + (lane >> 2);
+    const int gr = (isa ? m0 : n0) + tr;
+    const int lim = isa ? M : N;
+    const int gs = (lane & 3) ^ ((tr >> 1) & 3);
+    soff[i] = (b < XD_NBLK && gr < lim) ? (((p * lim + gr) * Kp) + 8 * gs) * 2 : kOob;
+    loff[i] = (isa ? 0 : 3 * XD_APL) + p * (isa ? XD_APL : XD_BPL) + 512 * rb;
+  }
+  auto issue = [&](int k0, int buf) {
+#pragma unroll
+    for (int i = 0; i < XD_BPW; ++i) {
+      if (wave + 8 * i < XD_NBLK) {
+        unsigned short* dst = lds + buf * XD_IMG + loff[i];
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            wave + 8 * i < XD_ABLK ? a_rs : b_rs, (__attribute__((address_space(3))) void*)dst, 16,
+            soff[i], k0 * 2, 0, 0);
+      }
+    }
+  };
+
+  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 80;
+  const int r16 = lane & 15, s16 = lane >> 4;
+  f32x4 acc[4][5];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 5; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int KT = (kend - kbeg) / XS;
+  issue(kbeg, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  xd_barrier();
+  if (grp == 1) xd_barrier();
+  bf16x8 af[2][3], bq[5][3];
+  for (int kt = 0; kt < KT; ++kt) {
+    const int cur = kt & 1;
+    const unsigned short* as = lds + cur * XD_IMG;
+    const unsigned short* bs = as + 3 * XD_APL;
+#pragma unroll
+    for (int ph = 0; ph < 2; ++ph) {
+      // ---- load segment
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int at = xslot_t<true>(wm + 16 * (2 * ph + i) + r16, s16);
+#pragma unroll
+        for (int p = 0; p < 3; ++p) af[i][p] = *reinterpret_cast<const bf16x8*>(as + p * XD_APL + at);
+      }
+      if (ph == 0) {
+#pragma unroll
+        for (int j = 0; j < 5; ++j) {
+          const int bt = xslot_t<true>(wn + 16 * j + r16, s16);
+#pragma unroll
+          for (int p = 0; p < 3; ++p) bq[j][p] = *reinterpret_cast<const bf16x8*>(bs + p * XD_BPL + bt);
+        }
+        if (kt + 1 < KT) issue(kbeg + (kt + 1) * XS, cur ^ 1);
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      xd_barrier();
+      // ---- MFMA segment
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int j = 0; j < 5; ++j)
+#pragma unroll
+        for (int i = 0; i < 2; ++i) x2_mma6_16(af[i], bq[j], acc[2 * ph + i][j]);
+      __builtin_amdgcn_s_setprio(0);
+      xd_barrier();
+    }
+  }
+  if (grp == 0) xd_barrier();   // equal barrier counts for both groups
+
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+      const int cl = wn + 16 * j + (lane & 15);
+      const int rb = wm + 16 * i + 4 * (lane >> 4);
+      if (part != nullptr) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) part[(rb + r) * XD_BN + cl] = acc[i][j][r];
+        continue;
+      }
+      const int col = n0 + cl;
+      if (col >= N) continue;
+      const float bv = bias != nullptr ? bias[col] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + rb + r;
+        if (row < M) {
+          float* cp = C + (int64_t)row * ldc + col;
+          float v = alpha * acc[i][j][r] + bv;
+          if (beta != 0.f) v += beta * *cp;
+          *cp = v;
+        }
+      }
+    }
+  }
+}
+
+// fp32 operand -> the three k-contiguous bf16 planes X3[p][r][kp] (kp < Kp, zeros past K;
+// the caller keeps 3 R Kp < 2^31).  Source element (r, k): src[r * ld + k] (k-contiguous) or
+// src[k * ld + r] (TRANS).  k-contiguous: one thread per (row, 8-k group), float4 loads when
+// VEC; TRANS: 64 x 64 tiles transposed through LDS, one thread per (row, 16-k run).
+template <bool TRANS, bool VEC>
+__global__ __launch_bounds__(256) void x6_split_kernel(const float* __restrict__ src, int64_t ld,
+                                                       int R, int K, int Kp,
+                                                       unsigned short* __restrict__ dst) {
+  const int plane = R * Kp;
+  if constexpr (!TRANS) {
+    const int64_t gid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    const int kg = Kp / 8;
+    if (gid >= (int64_t)R * kg) return;
+    const int r = static_cast<int>(gid / kg);
+    const int k0 = static_cast<int>(gid - (int64_t)r * kg) * 8;
+    const float* sp = src + (int64_t)r * ld + k0;
+    float v[8];
+    if (VEC && k0 + 8 <= K) {
+      const f32x4 x0 = *reinterpret_cast<const f32x4*>(sp);
+      const f32x4 x1 = *reinterpret_cast<const f32x4*>(sp + 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[e] = x0[e];
+        v[4 + e] = x1[e];
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = k0 + e < K ? sp[e] : 0.f;
+    }
+    x2_split_store<3>(dst, plane, r * Kp + k0, v);
+  } else {
+    __shared__ float tl[64][65];
+    const int r0 = blockIdx.x * 64, k0 = blockIdx.y * 64;
+    const int t = threadIdx.x;
+#pragma unroll 4
+    for (int i = t; i < 64 * 64; i += 256) {
+      const int kk = i >> 6, rr = i & 63;
+      const int k = k0 + kk, r = r0 + rr;
+      tl[kk][rr] = (k < K && r < R) ? src[(int64_t)k * ld + r] : 0.f;
+    }
+    __syncthreads();
+    const int rr = t >> 2, kq = 16 * (t & 3);
+    const int r = r0 + rr;
+    if (r >= R || k0 + kq >= Kp) return;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = tl[kq + 8 * h + e][rr];
+      x2_split_store<3>(dst, plane, r * Kp + k0 + kq + 8 * h, v);
     }
   }
 }
@@ -1564,13 +1626,6 @@ static bool x6_enabled(bool va, bool vb) {
   return !(e != nullptr && e[0] == '0');
 }
 
-// A/B switch: DS2_GEMM_PP=1 runs the ping-pong bf16x6 kernel (sxgemm_pp_kernel) on 160-wide
-// tiles without a K tail
-static bool pp_enabled() {
-  const char* e = getenv("DS2_GEMM_PP");
-  return e != nullptr && e[0] == '1';
-}
-
 // 32-bit buffer offsets: each operand (one batch entry) must span < 2^31 bytes
 static bool fits_rsrc(int64_t rows, int64_t ld) { return rows * ld * 4 < (1ll << 31); }
 
@@ -1653,12 +1708,83 @@ static GemmPlan x6_plan(int m, int n, int k, int batch) {
   return plan_bn(m, n, k, batch, n >= 256 ? 160 : 128, device_cus(), XS, 1.0, X2M).p;
 }
 
+// The pre-split DMA path (x6_split_kernel + sxgemm_dma_kernel): batch 1, N >= 256 (160-wide
+// tiles), every plane within a 32-bit buffer range.  Workspace: the split-K slab, A3, B3.
+static int x6_kp(int k) { return cdiv(k, XS) * XS; }
+static bool dma_shape_ok(int m, int n, int k, int batch) {
+  if (batch != 1 || n < 256) return false;
+  const int64_t kp = x6_kp(k);
+  return 6 * (int64_t)m * kp < (1ll << 31) && 6 * (int64_t)n * kp < (1ll << 31);
+}
+static GemmPlan dma_plan(int m, int n, int k) {
+  return plan_bn(m, n, x6_kp(k), 1, XD_BN, device_cus(), XS, 1.0, X2M).p;
+}
+static size_t al256(size_t v) { return (v + 255) & ~static_cast<size_t>(255); }
+static size_t dma_ws(int m, int n, int k) {
+  const size_t kp = x6_kp(k);
+  return al256(plan_ws(dma_plan(m, n, k), 1)) + al256(6 * (size_t)m * kp) + al256(6 * (size_t)n * kp);
+}
+// opt-in A/B (measured no faster end to end, see DESIGN): DS2_GEMM_DMA=1 the DMA kernel,
+// =2 its ping-pong form, wherever the shape allows
+static bool use_dma(int m, int n, int k, int batch) {
+  if (!dma_shape_ok(m, n, k, batch)) return false;
+  const char* e = getenv("DS2_GEMM_DMA");
+  if (e != nullptr && e[0] == '0') return false;
+  return e != nullptr && (e[0] == '1' || e[0] == '2');
+}
+
 // large enough for any kernel's plan (the choice depends on operand alignment)
 extern "C" size_t ds2_sgemm_workspace_size(int m, int n, int k, int batch) {
   if (m <= 0 || n <= 0 || k <= 0 || batch <= 0) return 0;
-  return std::max(std::max(plan_ws(gemm_plan(m, n, k, batch, false), batch),
-                           plan_ws(gemm_plan(m, n, k, batch, true), batch)),
-                  plan_ws(x6_plan(m, n, k, batch), batch));
+  size_t w = std::max(std::max(plan_ws(gemm_plan(m, n, k, batch, false), batch),
+                               plan_ws(gemm_plan(m, n, k, batch, true), batch)),
+                      plan_ws(x6_plan(m, n, k, batch), batch));
+  if (dma_shape_ok(m, n, k, batch)) w = std::max(w, dma_ws(m, n, k));
+  return w;
+}
+
+// split both operands into their planes, then the DMA kernel (+ the split-K reduce)
+static void launch_dma(int trans_a, int trans_b, int m, int n, int k, float alpha, const float* a,
+                       int64_t lda, const float* b, int64_t ldb, float beta, float* c, int64_t ldc,
+                       const float* bias, void* ws, hipStream_t st) {
+  const GemmPlan p = dma_plan(m, n, k);
+  const int kp = x6_kp(k);
+  char* w = static_cast<char*>(ws);
+  float* partial = p.nsplit > 1 ? reinterpret_cast<float*>(w) : nullptr;
+  w += al256(plan_ws(p, 1));
+  unsigned short* a3 = reinterpret_cast<unsigned short*>(w);
+  w += al256(6 * (size_t)m * kp);
+  unsigned short* b3 = reinterpret_cast<unsigned short*>(w);
+  auto split = [&](const float* src, int64_t ld, int rows, bool kcontig, unsigned short* dst) {
+    if (kcontig) {
+      const int64_t thr = (int64_t)rows * (kp / 8);
+      hipLaunchKernelGGL((x6_split_kernel<false, true>), dim3(static_cast<unsigned>(cdiv(thr, 256))),
+                         dim3(256), 0, st, src, ld, rows, k, kp, dst);
+    } else {
+      hipLaunchKernelGGL((x6_split_kernel<true, false>), dim3(cdiv(rows, 64), cdiv(kp, 64)),
+                         dim3(256), 0, st, src, ld, rows, k, kp, dst);
+    }
+  };
+  split(a, lda, m, !trans_a, a3);
+  split(b, ldb, n, trans_b != 0, b3);
+  const int64_t nwg = p.main_wgs + (int64_t)p.tail_tiles * p.nsplit;
+  const char* e = getenv("DS2_GEMM_DMA");
+  if (e != nullptr && e[0] == '2')
+    hipLaunchKernelGGL(sxgemm_dma_pp_kernel, dim3(static_cast<unsigned>(nwg)), dim3(X2T), 0, st, m,
+                       n, kp, alpha, a3, b3, beta, c, ldc, bias, p.main_wgs, p.tail_tile0,
+                       p.tail_tiles, p.nsplit, p.kchunk, partial);
+  else
+    hipLaunchKernelGGL(sxgemm_dma_kernel, dim3(static_cast<unsigned>(nwg)), dim3(X2T), 0, st, m, n,
+                       kp, alpha, a3, b3, beta, c, ldc, bias, p.main_wgs, p.tail_tile0,
+                       p.tail_tiles, p.nsplit, p.kchunk, partial);
+  if (p.nsplit > 1) {
+    const int64_t total = (int64_t)p.tail_tiles * p.bm * p.bn;
+    int g = cdiv(total, 256);
+    if (g > 4096) g = 4096;
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(g), dim3(256), 0, st, partial, m, n, p.nsplit, 1,
+                       p.tail_tile0, p.tail_tiles, alpha, beta, c, ldc, (int64_t)0, bias, p.bn,
+                       p.bm);
+  }
 }
 
 extern "C" ds2_status_t ds2_sgemm_ws(int trans_a, int trans_b, int m, int n, int k, float alpha,
@@ -1680,6 +1806,11 @@ extern "C" ds2_status_t ds2_sgemm_ws(int trans_a, int trans_b, int m, int n, int
   const bool fits = fits_rsrc(trans_a ? k : m, lda) && fits_rsrc(trans_b ? n : k, ldb);
   const bool x6 = fits && x6_enabled(va, vb);
   const bool k64 = !x6 && va && vb && fits;
+  if (x6 && use_dma(m, n, k, batch) && ws != nullptr && ws_bytes >= dma_ws(m, n, k)) {
+    launch_dma(trans_a, trans_b, m, n, k, alpha, a, lda, b, ldb, beta, c, ldc, bias, ws,
+               as_stream(stream));
+    return launch_status("ds2_sgemm");
+  }
   GemmPlan p = x6 ? x6_plan(m, n, k, batch) : gemm_plan(m, n, k, batch, k64);
   if (p.nsplit > 1 && (ws == nullptr || ws_bytes < plan_ws(p, batch))) {
     p.nsplit = 1;                       // no workspace: whole-K pieces
@@ -1700,13 +1831,8 @@ extern "C" ds2_status_t ds2_sgemm_ws(int trans_a, int trans_b, int m, int n, int
   // the 16x16x32 form wherever every stage lies inside K (r4d: 0-15 % faster on the step's
   // shapes, profiles/r4d_gemm_x6_m16_sk_ab.txt), the 32x32x16 form for a K tail
   const bool m16 = x6 && kalign;
-  const bool pp = m16 && pp_enabled();
 #define DS2_G(TA_, TB_)                                                                       \
-  if (pp && p.bn == 160)                                                                      \
-    hipLaunchKernelGGL((sxgemm_pp_kernel<TA_, TB_>), grid, dim3(X2T), 0, st, m, n, k, alpha, a, \
-                       lda, stride_a, b, ldb, stride_b, beta, c, ldc, stride_c, bias,          \
-                       p.main_wgs, p.tail_tile0, p.tail_tiles, p.nsplit, p.kchunk, partial);   \
-  else if (m16 && p.bn == 160) DS2_X6(TA_, TB_, false, 160, true);                          \
+  if (m16 && p.bn == 160) DS2_X6(TA_, TB_, false, 160, true);                          \
   else if (m16) DS2_X6(TA_, TB_, false, 128, true);                                          \
   else if (x6 && kalign && p.bn == 160) DS2_X6(TA_, TB_, false, 160, false);                 \
   else if (x6 && p.bn == 160) DS2_X6(TA_, TB_, true, 160, false);                            \

@@ -25,7 +25,7 @@ def _close(got, ref, rel=1e-5, name=""):
 
 
 # ---------------------------------------------------------------------------- GEMM
-@pytest.mark.parametrize("x6", ["1", "0"])
+@pytest.mark.parametrize("x6", ["1", "dma", "0"])
 @pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
 @pytest.mark.parametrize("m,n,k", [(1, 1, 1), (37, 53, 29), (128, 128, 16), (300, 257, 513),
                                    (515, 2400, 132), (257, 300, 5000),   # split-K path
@@ -34,8 +34,11 @@ def _close(got, ref, rel=1e-5, name=""):
 def test_sgemm(dev, ta, tb, m, n, k, x6, monkeypatch):
     """ds2_sgemm_ws vs fp64 at 1e-5: the bf16x6 kernel (default for float4-staged operands;
     256 x 160 tiles for N >= 256, 256 x 128 below; its 16x16x32 form where every stage lies
-    inside K, the 32x32x16 form for a K tail) and the fp32-MFMA kernels (DS2_GEMM_X6=0)."""
-    monkeypatch.setenv("DS2_GEMM_X6", x6)
+    inside K, the 32x32x16 form for a K tail), the same product on pre-split planes by LDS-DMA
+    ("dma": DS2_GEMM_DMA=1, every shape with N >= 256; the others run as "1") and the fp32-MFMA
+    kernels (DS2_GEMM_X6=0)."""
+    monkeypatch.setenv("DS2_GEMM_X6", "0" if x6 == "0" else "1")
+    monkeypatch.setenv("DS2_GEMM_DMA", "1" if x6 == "dma" else "0")
     g = torch.Generator().manual_seed(m * 7 + n * 3 + k)
     a = torch.randn(k, m, generator=g) if ta else torch.randn(m, k, generator=g)
     b = torch.randn(n, k, generator=g) if tb else torch.randn(k, n, generator=g)
@@ -50,19 +53,20 @@ def test_sgemm(dev, ta, tb, m, n, k, x6, monkeypatch):
     _close(cd, ref, 1e-5, "sgemm")
 
 
-@pytest.mark.parametrize("mode", ["x6", "x6-narrow", "x6-ktail", "x6-ktail-narrow", "x6pp", "fp32",
+@pytest.mark.parametrize("mode", ["x6", "x6-narrow", "x6-ktail", "x6-ktail-narrow", "x6-dma",
+                                  "x6-dma-ktail", "fp32",
                                   "fp32-narrow", "unaligned"])
 @pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
 def test_sgemm_full_rounds_plus_split_tail(dev, ta, tb, mode, monkeypatch):
     """Whole rounds of resident workgroups + a tail whose K range is split (one launch) and
     reduced in a fixed order; alpha/beta/bias applied once.  bf16x6 kernel: 256 x 160 tiles
-    (N >= 256) and 256 x 128 ("-narrow": N < 256); fp32 kernels (DS2_GEMM_X6=0): BK = 64 /
+    (N >= 256) and 256 x 128 ("-narrow": N < 256), "-dma" the pre-split planes by LDS-DMA
+    (DS2_GEMM_DMA=1; "-ktail": K zero-padded to 32 in the planes); fp32 kernels (DS2_GEMM_X6=0): BK = 64 /
     16x16x4 with the plan's tile width, and ("unaligned": A one float off 16-B alignment)
     the BK = 16 / 32x32x2 kernel."""
     monkeypatch.setenv("DS2_GEMM_X6", "1" if mode.startswith("x6") else "0")
-    monkeypatch.setenv("DS2_GEMM_PP", "1" if mode == "x6pp" else "0")
-    # K % 32 == 0: the 16x16x32 form; "-ktail" (K % 32 == 4): the 32x32x16 form with k checks;
-    # "x6pp": the ping-pong kernel
+    monkeypatch.setenv("DS2_GEMM_DMA", "1" if "dma" in mode else "0")
+    # K % 32 == 0: the 16x16x32 form; "-ktail" (K % 32 == 4): the 32x32x16 form with k checks
     m, k = 128 * 29, 2084 if "ktail" in mode else 2080
     n = 200 if mode.endswith("narrow") else 128 * 27 + 52
     g = torch.Generator().manual_seed(5)
@@ -83,34 +87,6 @@ def test_sgemm_full_rounds_plus_split_tail(dev, ta, tb, mode, monkeypatch):
               a_off=a_off)
     torch.cuda.synchronize()
     _close(cd, ref, 1e-5, "sgemm main+tail")
-
-
-@pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
-@pytest.mark.parametrize("m,n,k", [(1000, 800, 1312), (600, 300, 4096), (300, 257, 2048),
-                                   (130, 1000, 32)])
-def test_sgemm_pingpong(dev, ta, tb, m, n, k, monkeypatch):
-    """The ping-pong bf16x6 kernel (DS2_GEMM_PP=1: two wave groups one barrier interval apart,
-    160-wide tiles, K % 32 == 0; split-K tails on the bigger shapes) vs fp64 at 1e-5 with alpha,
-    beta and bias, and against the default kernel at the same bound."""
-    monkeypatch.setenv("DS2_GEMM_X6", "1")
-    g = torch.Generator().manual_seed(m + 3 * n + k)
-    a = torch.randn(k, m, generator=g) if ta else torch.randn(m, k, generator=g)
-    b = torch.randn(n, k, generator=g) if tb else torch.randn(k, n, generator=g)
-    c0 = torch.randn(m, n, generator=g)
-    bias = torch.randn(n, generator=g)
-    ref = 0.5 * ((a.t() if ta else a).double() @ (b.t() if tb else b).double()) \
-        + 0.25 * c0.double() + bias.double()
-    ad, bd = a.to(dev), b.to(dev)
-    out = {}
-    for pp in ("1", "0"):
-        monkeypatch.setenv("DS2_GEMM_PP", pp)
-        cd = c0.to(dev).clone()
-        ops.sgemm(ad, bd, cd, m=m, n=n, k=k, trans_a=bool(ta), trans_b=bool(tb),
-                  lda=ad.shape[1], ldb=bd.shape[1], ldc=n, alpha=0.5, beta=0.25, bias=bias.to(dev))
-        torch.cuda.synchronize()
-        _close(cd, ref, 1e-5, f"sgemm pp={pp}")
-        out[pp] = cd.cpu().double()
-    assert (out["1"] - out["0"]).abs().max().item() <= 1e-5 * ref.abs().max().item()
 
 
 @pytest.mark.parametrize("ta,tb,m,n,k", [(0, 1, 2048, 2400, 800), (0, 0, 2048, 800, 2400),
