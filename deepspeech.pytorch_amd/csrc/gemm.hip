@@ -1183,348 +1183,6 @@ __global__ __launch_bounds__(X2T, 1) void sxgemm2_kernel(
   job(m0, n0, kbeg, kend, part);
 }
 
-// ---------------------------------------------------------------------------
-// The bf16x6 GEMM on pre-split operand planes (the default for large batch-1 products).
-// Ablation builds of sxgemm2_kernel (scripts/gemm_ablation.sh, profiles/r4j_gemm_ablation.txt)
-// showed its staging -- the split VALU and, above all, the 80 KB of ds_write_b128 per stage
-// (3 bf16 planes of 416 rows x 32 k) -- running beside the MFMAs, not under them: without
-// MFMAs the kernel still took 52-65 % of its time.  Here each operand is split ONCE by
-// x6_split_kernel into three k-contiguous bf16 planes in HBM,
-//   X3[p][r][kp], p = hi / mid / lo, kp < Kp = K rounded up to 32 (zeros past K),
-// and the GEMM kernel fills its LDS stages by LDS-DMA (buffer_load ... lds, 16 B per lane):
-// no staging VALU, no ds_write, no register round trip.  The split is x2_split2's, so the
-// planes hold exactly the values the in-kernel split produces.
-//
-// Tile 256 x 160 x 32 (k) per workgroup of 8 waves (4 M x 2 N, each 64 x 80 = 4 x 5 tiles of
-// v_mfma_f32_16x16x32_bf16, 6 products per tile and k-step, small terms first); two LDS
-// stages of 3 x (256 + 160) rows x 64 B = 78 KB.  A stage is 78 one-KB DMA blocks (16 rows of
-// one plane, lane-linear in LDS, the xslot_t<true> swizzle applied to the source address);
-// wave w issues blocks w, w + 8, ... .  Per stage: issue the DMA of stage kt + 1 into the
-// other buffer, fragments + MFMAs of stage kt, wait for the own DMA (vmcnt(0)), one barrier
-// (it publishes stage kt + 1 and retires every read of stage kt before its buffer is
-// refilled).
-constexpr int XD_BN = 160;
-constexpr int XD_APL = X2M * XS;                 // bf16 per A plane in LDS
-constexpr int XD_BPL = XD_BN * XS;               // bf16 per B plane
-constexpr int XD_IMG = 3 * (XD_APL + XD_BPL);    // bf16 per stage (79,872 B)
-constexpr int XD_ABLK = 3 * X2M / 16;            // 48 A blocks per stage
-constexpr int XD_NBLK = XD_ABLK + 3 * XD_BN / 16;   // 78
-constexpr int XD_BPW = (XD_NBLK + 7) / 8;        // blocks per wave (waves 6, 7 issue one fewer)
-static_assert(2 * XD_IMG * 2 <= 160 * 1024, "two DMA stages");
-
-__device__ __forceinline__ void xd_barrier() {
-  asm volatile("" ::: "memory");
-  __builtin_amdgcn_sched_barrier(0);
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_sched_barrier(0);
-  asm volatile("" ::: "memory");
-}
-
-__global__ __launch_bounds__(X2T, 1) void sxgemm_dma_kernel(
-    int M, int N, int Kp, float alpha, const unsigned short* __restrict__ A3,
-    const unsigned short* __restrict__ B3, float beta, float* __restrict__ C, int64_t ldc,
-    const float* __restrict__ bias, int main_wgs, int tail_tile0, int tail_tiles, int nsplit,
-    int kchunk, float* __restrict__ partial) {
-  __shared__ __attribute__((aligned(16))) unsigned short lds[2 * XD_IMG];
-  int m0, n0, kbeg, kend, bz;
-  float* part;
-  decode_work(M, N, Kp, main_wgs, tail_tile0, tail_tiles, nsplit, kchunk, partial, m0, n0, kbeg,
-              kend, bz, part, XD_BN, X2M);
-  const int t = threadIdx.x;
-  const int lane = t & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
-  const __amdgpu_buffer_rsrc_t a_rs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<unsigned short*>(A3), (short)0, static_cast<int>(3ll * M * Kp * 2), 0x00020000);
-  const __amdgpu_buffer_rsrc_t b_rs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<unsigned short*>(B3), (short)0, static_cast<int>(3ll * N * Kp * 2), 0x00020000);
-  constexpr int kOob = 0x7ffffff0;
-
-  // this wave's DMA blocks: lane L of block b fills LDS chunk L (tile row 16 rb + L / 4, slot
-  // position L & 3) with source slot (L & 3) ^ ((row >> 1) & 3) of its plane row
-  int soff[XD_BPW], loff[XD_BPW];
-#pragma unroll
-  for (int i = 0; i < XD_BPW; ++i) {
-    const int b = wave + 8 * i;
-    const bool isa = b < XD_ABLK;
-    const int bb = isa ? b : b - XD_ABLK;
-    const int nrb = isa ? X2M / 16 : XD_BN / 16;
-    const int p = bb / nrb, rb = bb - p * nrb;
-    const int tr = 16 * rb + (lane >> 2);                 // row within the tile
-    const int gr = (isa ? m0 : n0) + tr;
-    const int lim = isa ? M : N;
-    const int gs = (lane & 3) ^ ((tr >> 1) & 3);
-    soff[i] = (b < XD_NBLK && gr < lim) ? (((p * lim + gr) * Kp) + 8 * gs) * 2 : kOob;
-    loff[i] = (isa ? 0 : 3 * XD_APL) + p * (isa ? XD_APL : XD_BPL) + 512 * rb;
-  }
-  auto issue = [&](int k0, int buf) {
-#pragma unroll
-    for (int i = 0; i < XD_BPW; ++i) {
-      if (wave + 8 * i < XD_NBLK) {
-        unsigned short* dst = lds + buf * XD_IMG + loff[i];
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(
-            wave + 8 * i < XD_ABLK ? a_rs : b_rs, (__attribute__((address_space(3))) void*)dst, 16,
-            soff[i], k0 * 2, 0, 0);
-      }
-    }
-  };
-
-  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 80;
-  const int r16 = lane & 15, s16 = lane >> 4;
-  f32x4 acc[4][5];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 5; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int KT = (kend - kbeg) / XS;
-  issue(kbeg, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  xd_barrier();
-  for (int kt = 0; kt < KT; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < KT) issue(kbeg + (kt + 1) * XS, cur ^ 1);
-    const unsigned short* as = lds + cur * XD_IMG;
-    const unsigned short* bs = as + 3 * XD_APL;
-    bf16x8 af[4][3];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int at = xslot_t<true>(wm + 16 * i + r16, s16);
-#pragma unroll
-      for (int p = 0; p < 3; ++p) af[i][p] = *reinterpret_cast<const bf16x8*>(as + p * XD_APL + at);
-    }
-#pragma unroll
-    for (int j = 0; j < 5; ++j) {
-      bf16x8 bq[3];
-      const int bt = xslot_t<true>(wn + 16 * j + r16, s16);
-#pragma unroll
-      for (int p = 0; p < 3; ++p) bq[p] = *reinterpret_cast<const bf16x8*>(bs + p * XD_BPL + bt);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) x2_mma6_16(af[i], bq, acc[i][j]);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    xd_barrier();
-  }
-
-  // epilogue (16x16 C/D map: col = lane & 15, row = 4 (lane >> 4) + r)
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-#pragma unroll
-    for (int j = 0; j < 5; ++j) {
-      const int cl = wn + 16 * j + (lane & 15);
-      const int rb = wm + 16 * i + 4 * (lane >> 4);
-      if (part != nullptr) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) part[(rb + r) * XD_BN + cl] = acc[i][j][r];
-        continue;
-      }
-      const int col = n0 + cl;
-      if (col >= N) continue;
-      const float bv = bias != nullptr ? bias[col] : 0.f;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = m0 + rb + r;
-        if (row < M) {
-          float* cp = C + (int64_t)row * ldc + col;
-          float v = alpha * acc[i][j][r] + bv;
-          if (beta != 0.f) v += beta * *cp;
-          *cp = v;
-        }
-      }
-    }
-  }
-}
-
-// The same product with the eight waves as two groups one barrier interval apart (waves 0-3:
-// tile rows 0-127, waves 4-7: rows 128-255; per SIMD one wave of each), so in every interval
-// one wave per SIMD issues MFMAs while its partner reads fragments and issues DMA.  Stage s,
-// interval I_n = (barrier n, barrier n + 1), group 0 / group 1:
-//   phase 0  load [A frags i 0-1, B frags j 0-4, DMA of stage s + 1]  I_4s     / I_4s+1
-//            MFMA [60: i 0-1 x j 0-4]                                 I_4s+1   / I_4s+2
-//   phase 1  load [A frags i 2-3, wait for the own DMA]               I_4s+2   / I_4s+3
-//            MFMA [60: i 2-3 x j 0-4]                                 I_4s+3   / I_4s+4
-// Stage s + 1's buffer held stage s - 1, last read by group 1 in I_4s-1 (retired by
-// lgkmcnt(0) before barrier 4s: WAR); its DMA is complete before barrier 4s + 4 (each wave's
-// vmcnt(0) in I_4s+2 / I_4s+3), first read by group 0 in I_4s+4 (RAW).
-__global__ __launch_bounds__(X2T, 1) void sxgemm_dma_pp_kernel(
-    int M, int N, int Kp, float alpha, const unsigned short* __restrict__ A3,
-    const unsigned short* __restrict__ B3, float beta, float* __restrict__ C, int64_t ldc,
-    const float* __restrict__ bias, int main_wgs, int tail_tile0, int tail_tiles, int nsplit,
-    int kchunk, float* __restrict__ partial) {
-  __shared__ __attribute__((aligned(16))) unsigned short lds[2 * XD_IMG];
-  int m0, n0, kbeg, kend, bz;
-  float* part;
-  decode_work(M, N, Kp, main_wgs, tail_tile0, tail_tiles, nsplit, kchunk, partial, m0, n0, kbeg,
-              kend, bz, part, XD_BN, X2M);
-  const int t = threadIdx.x;
-  const int lane = t & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int grp = wave >> 2;
-  const __amdgpu_buffer_rsrc_t a_rs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<unsigned short*>(A3), (short)0, static_cast<int>(3ll * M * Kp * 2), 0x00020000);
-  const __amdgpu_buffer_rsrc_t b_rs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<unsigned short*>(B3), (short)0, static_cast<int>(3ll * N * Kp * 2), 0x00020000);
-  constexpr int kOob = 0x7ffffff0;
-  int soff[XD_BPW], loff[XD_BPW];
-#pragma unroll
-  for (int i = 0; i < XD_BPW; ++i) {
-    const int b = wave + 8 * i;
-    const bool isa = b < XD_ABLK;
-    const int bb = isa ? b : b - XD_ABLK;
-    const int nrb = isa ? X2M / 16 : XD_BN / 16;
-    const int p = bb / nrb, rb = bb - p * nrb;
-    const int tr = 16 * rb + (lane >> 2);
-    const int gr = (isa ? m0 : n0) + tr;
-    const int lim = isa ? M : N;
-    const int gs = (lane & 3) ^ ((tr >> 1) & 3);
-    soff[i] = (b < XD_NBLK && gr < lim) ? (((p * lim + gr) * Kp) + 8 * gs) * 2 : kOob;
-    loff[i] = (isa ? 0 : 3 * XD_APL) + p * (isa ? XD_APL : XD_BPL) + 512 * rb;
-  }
-  auto issue = [&](int k0, int buf) {
-#pragma unroll
-    for (int i = 0; i < XD_BPW; ++i) {
-      if (wave + 8 * i < XD_NBLK) {
-        unsigned short* dst = lds + buf * XD_IMG + loff[i];
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(
-            wave + 8 * i < XD_ABLK ? a_rs : b_rs, (__attribute__((address_space(3))) void*)dst, 16,
-            soff[i], k0 * 2, 0, 0);
-      }
-    }
-  };
-
-  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 80;
-  const int r16 = lane & 15, s16 = lane >> 4;
-  f32x4 acc[4][5];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 5; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int KT = (kend - kbeg) / XS;
-  issue(kbeg, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  xd_barrier();
-  if (grp == 1) xd_barrier();
-  bf16x8 af[2][3], bq[5][3];
-  for (int kt = 0; kt < KT; ++kt) {
-    const int cur = kt & 1;
-    const unsigned short* as = lds + cur * XD_IMG;
-    const unsigned short* bs = as + 3 * XD_APL;
-#pragma unroll
-    for (int ph = 0; ph < 2; ++ph) {
-      // ---- load segment
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int at = xslot_t<true>(wm + 16 * (2 * ph + i) + r16, s16);
-#pragma unroll
-        for (int p = 0; p < 3; ++p) af[i][p] = *reinterpret_cast<const bf16x8*>(as + p * XD_APL + at);
-      }
-      if (ph == 0) {
-#pragma unroll
-        for (int j = 0; j < 5; ++j) {
-          const int bt = xslot_t<true>(wn + 16 * j + r16, s16);
-#pragma unroll
-          for (int p = 0; p < 3; ++p) bq[j][p] = *reinterpret_cast<const bf16x8*>(bs + p * XD_BPL + bt);
-        }
-        if (kt + 1 < KT) issue(kbeg + (kt + 1) * XS, cur ^ 1);
-      } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      xd_barrier();
-      // ---- MFMA segment
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int j = 0; j < 5; ++j)
-#pragma unroll
-        for (int i = 0; i < 2; ++i) x2_mma6_16(af[i], bq[j], acc[2 * ph + i][j]);
-      __builtin_amdgcn_s_setprio(0);
-      xd_barrier();
-    }
-  }
-  if (grp == 0) xd_barrier();   // equal barrier counts for both groups
-
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-#pragma unroll
-    for (int j = 0; j < 5; ++j) {
-      const int cl = wn + 16 * j + (lane & 15);
-      const int rb = wm + 16 * i + 4 * (lane >> 4);
-      if (part != nullptr) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) part[(rb + r) * XD_BN + cl] = acc[i][j][r];
-        continue;
-      }
-      const int col = n0 + cl;
-      if (col >= N) continue;
-      const float bv = bias != nullptr ? bias[col] : 0.f;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = m0 + rb + r;
-        if (row < M) {
-          float* cp = C + (int64_t)row * ldc + col;
-          float v = alpha * acc[i][j][r] + bv;
-          if (beta != 0.f) v += beta * *cp;
-          *cp = v;
-        }
-      }
-    }
-  }
-}
-
-// fp32 operand -> the three k-contiguous bf16 planes X3[p][r][kp] (kp < Kp, zeros past K;
-// the caller keeps 3 R Kp < 2^31).  Source element (r, k): src[r * ld + k] (k-contiguous) or
-// src[k * ld + r] (TRANS).  k-contiguous: one thread per (row, 8-k group), float4 loads when
-// VEC; TRANS: 64 x 64 tiles transposed through LDS, one thread per (row, 16-k run).
-template <bool TRANS, bool VEC>
-__global__ __launch_bounds__(256) void x6_split_kernel(const float* __restrict__ src, int64_t ld,
-                                                       int R, int K, int Kp,
-                                                       unsigned short* __restrict__ dst) {
-  const int plane = R * Kp;
-  if constexpr (!TRANS) {
-    const int64_t gid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    const int kg = Kp / 8;
-    if (gid >= (int64_t)R * kg) return;
-    const int r = static_cast<int>(gid / kg);
-    const int k0 = static_cast<int>(gid - (int64_t)r * kg) * 8;
-    const float* sp = src + (int64_t)r * ld + k0;
-    float v[8];
-    if (VEC && k0 + 8 <= K) {
-      const f32x4 x0 = *reinterpret_cast<const f32x4*>(sp);
-      const f32x4 x1 = *reinterpret_cast<const f32x4*>(sp + 4);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        v[e] = x0[e];
-        v[4 + e] = x1[e];
-      }
-    } else {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = k0 + e < K ? sp[e] : 0.f;
-    }
-    x2_split_store<3>(dst, plane, r * Kp + k0, v);
-  } else {
-    __shared__ float tl[64][65];
-    const int r0 = blockIdx.x * 64, k0 = blockIdx.y * 64;
-    const int t = threadIdx.x;
-#pragma unroll 4
-    for (int i = t; i < 64 * 64; i += 256) {
-      const int kk = i >> 6, rr = i & 63;
-      const int k = k0 + kk, r = r0 + rr;
-      tl[kk][rr] = (k < K && r < R) ? src[(int64_t)k * ld + r] : 0.f;
-    }
-    __syncthreads();
-    const int rr = t >> 2, kq = 16 * (t & 3);
-    const int r = r0 + rr;
-    if (r >= R || k0 + kq >= Kp) return;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      float v[8];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = tl[kq + 8 * h + e][rr];
-      x2_split_store<3>(dst, plane, r * Kp + k0 + kq + 8 * h, v);
-    }
-  }
-}
-
 // Tail tiles: C[b] = alpha * sum_s partial[b][s][tile] + beta * C[b] + bias (fixed order)
 __global__ void splitk_reduce_kernel(const float* __restrict__ partial, int M, int N, int nsplit,
                                      int batch, int tail_tile0, int tail_tiles, float alpha,
@@ -1708,83 +1366,12 @@ static GemmPlan x6_plan(int m, int n, int k, int batch) {
   return plan_bn(m, n, k, batch, n >= 256 ? 160 : 128, device_cus(), XS, 1.0, X2M).p;
 }
 
-// The pre-split DMA path (x6_split_kernel + sxgemm_dma_kernel): batch 1, N >= 256 (160-wide
-// tiles), every plane within a 32-bit buffer range.  Workspace: the split-K slab, A3, B3.
-static int x6_kp(int k) { return cdiv(k, XS) * XS; }
-static bool dma_shape_ok(int m, int n, int k, int batch) {
-  if (batch != 1 || n < 256) return false;
-  const int64_t kp = x6_kp(k);
-  return 6 * (int64_t)m * kp < (1ll << 31) && 6 * (int64_t)n * kp < (1ll << 31);
-}
-static GemmPlan dma_plan(int m, int n, int k) {
-  return plan_bn(m, n, x6_kp(k), 1, XD_BN, device_cus(), XS, 1.0, X2M).p;
-}
-static size_t al256(size_t v) { return (v + 255) & ~static_cast<size_t>(255); }
-static size_t dma_ws(int m, int n, int k) {
-  const size_t kp = x6_kp(k);
-  return al256(plan_ws(dma_plan(m, n, k), 1)) + al256(6 * (size_t)m * kp) + al256(6 * (size_t)n * kp);
-}
-// opt-in A/B (measured no faster end to end, see DESIGN): DS2_GEMM_DMA=1 the DMA kernel,
-// =2 its ping-pong form, wherever the shape allows
-static bool use_dma(int m, int n, int k, int batch) {
-  if (!dma_shape_ok(m, n, k, batch)) return false;
-  const char* e = getenv("DS2_GEMM_DMA");
-  if (e != nullptr && e[0] == '0') return false;
-  return e != nullptr && (e[0] == '1' || e[0] == '2');
-}
-
 // large enough for any kernel's plan (the choice depends on operand alignment)
 extern "C" size_t ds2_sgemm_workspace_size(int m, int n, int k, int batch) {
   if (m <= 0 || n <= 0 || k <= 0 || batch <= 0) return 0;
-  size_t w = std::max(std::max(plan_ws(gemm_plan(m, n, k, batch, false), batch),
-                               plan_ws(gemm_plan(m, n, k, batch, true), batch)),
-                      plan_ws(x6_plan(m, n, k, batch), batch));
-  if (dma_shape_ok(m, n, k, batch)) w = std::max(w, dma_ws(m, n, k));
-  return w;
-}
-
-// split both operands into their planes, then the DMA kernel (+ the split-K reduce)
-static void launch_dma(int trans_a, int trans_b, int m, int n, int k, float alpha, const float* a,
-                       int64_t lda, const float* b, int64_t ldb, float beta, float* c, int64_t ldc,
-                       const float* bias, void* ws, hipStream_t st) {
-  const GemmPlan p = dma_plan(m, n, k);
-  const int kp = x6_kp(k);
-  char* w = static_cast<char*>(ws);
-  float* partial = p.nsplit > 1 ? reinterpret_cast<float*>(w) : nullptr;
-  w += al256(plan_ws(p, 1));
-  unsigned short* a3 = reinterpret_cast<unsigned short*>(w);
-  w += al256(6 * (size_t)m * kp);
-  unsigned short* b3 = reinterpret_cast<unsigned short*>(w);
-  auto split = [&](const float* src, int64_t ld, int rows, bool kcontig, unsigned short* dst) {
-    if (kcontig) {
-      const int64_t thr = (int64_t)rows * (kp / 8);
-      hipLaunchKernelGGL((x6_split_kernel<false, true>), dim3(static_cast<unsigned>(cdiv(thr, 256))),
-                         dim3(256), 0, st, src, ld, rows, k, kp, dst);
-    } else {
-      hipLaunchKernelGGL((x6_split_kernel<true, false>), dim3(cdiv(rows, 64), cdiv(kp, 64)),
-                         dim3(256), 0, st, src, ld, rows, k, kp, dst);
-    }
-  };
-  split(a, lda, m, !trans_a, a3);
-  split(b, ldb, n, trans_b != 0, b3);
-  const int64_t nwg = p.main_wgs + (int64_t)p.tail_tiles * p.nsplit;
-  const char* e = getenv("DS2_GEMM_DMA");
-  if (e != nullptr && e[0] == '2')
-    hipLaunchKernelGGL(sxgemm_dma_pp_kernel, dim3(static_cast<unsigned>(nwg)), dim3(X2T), 0, st, m,
-                       n, kp, alpha, a3, b3, beta, c, ldc, bias, p.main_wgs, p.tail_tile0,
-                       p.tail_tiles, p.nsplit, p.kchunk, partial);
-  else
-    hipLaunchKernelGGL(sxgemm_dma_kernel, dim3(static_cast<unsigned>(nwg)), dim3(X2T), 0, st, m, n,
-                       kp, alpha, a3, b3, beta, c, ldc, bias, p.main_wgs, p.tail_tile0,
-                       p.tail_tiles, p.nsplit, p.kchunk, partial);
-  if (p.nsplit > 1) {
-    const int64_t total = (int64_t)p.tail_tiles * p.bm * p.bn;
-    int g = cdiv(total, 256);
-    if (g > 4096) g = 4096;
-    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(g), dim3(256), 0, st, partial, m, n, p.nsplit, 1,
-                       p.tail_tile0, p.tail_tiles, alpha, beta, c, ldc, (int64_t)0, bias, p.bn,
-                       p.bm);
-  }
+  return std::max(std::max(plan_ws(gemm_plan(m, n, k, batch, false), batch),
+                           plan_ws(gemm_plan(m, n, k, batch, true), batch)),
+                  plan_ws(x6_plan(m, n, k, batch), batch));
 }
 
 extern "C" ds2_status_t ds2_sgemm_ws(int trans_a, int trans_b, int m, int n, int k, float alpha,
@@ -1806,11 +1393,6 @@ extern "C" ds2_status_t ds2_sgemm_ws(int trans_a, int trans_b, int m, int n, int
   const bool fits = fits_rsrc(trans_a ? k : m, lda) && fits_rsrc(trans_b ? n : k, ldb);
   const bool x6 = fits && x6_enabled(va, vb);
   const bool k64 = !x6 && va && vb && fits;
-  if (x6 && use_dma(m, n, k, batch) && ws != nullptr && ws_bytes >= dma_ws(m, n, k)) {
-    launch_dma(trans_a, trans_b, m, n, k, alpha, a, lda, b, ldb, beta, c, ldc, bias, ws,
-               as_stream(stream));
-    return launch_status("ds2_sgemm");
-  }
   GemmPlan p = x6 ? x6_plan(m, n, k, batch) : gemm_plan(m, n, k, batch, k64);
   if (p.nsplit > 1 && (ws == nullptr || ws_bytes < plan_ws(p, batch))) {
     p.nsplit = 1;                       // no workspace: whole-K pieces

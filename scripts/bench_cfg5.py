@@ -74,6 +74,24 @@ def main():
         out[f"{name}_ms_per_batch"] = round(dt * 1e3, 2)
         out[f"{name}_sample"] = strings[0][0][:40]
     out["beam_width"] = args.beam
+    # the decoders alone on one forward's output: device part (kernel + allocations, synced)
+    # and the whole decode (+ the copy back and the strings / offsets on the host)
+    with torch.no_grad():
+        spect = ops.stft_logmag(pcm, ns, n_fft, hop, win, 1, taps, frames).unsqueeze(1)
+        _, probs, out_lens = m(spect, torch.full((args.batch,), frames, dtype=torch.int32))
+    parts = {}
+    for name, fn in (("beam_device", lambda: beam.decode_raw(probs, out_lens)),
+                     ("beam_full", lambda: beam.decode(probs, out_lens)),
+                     ("greedy_device", lambda: greedy.decode_ids(probs, out_lens)),
+                     ("greedy_full", lambda: greedy.decode(probs, out_lens))):
+        fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.iters):
+            fn()
+        torch.cuda.synchronize()
+        parts[name] = round((time.perf_counter() - t0) / args.iters * 1e3, 2)
+    out["decode_ms"] = parts
     print(json.dumps(out), flush=True)
     if args.stamps:
         from ds2amd import _lib

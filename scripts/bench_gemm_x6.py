@@ -45,7 +45,7 @@ def main():
     import argparse
     ap = argparse.ArgumentParser()
     ap.add_argument("--shape", default=None, help="one shape (name prefix), e.g. for rocprofv3")
-    ap.add_argument("--mode", default=None, choices=["x6", "x6dma", "x6dpp", "fp32"])
+    ap.add_argument("--mode", default=None, choices=["x6", "fp32"])
     args = ap.parse_args()
     torch.manual_seed(0)
     for name, ta, tb, m, n, k in SHAPES:
@@ -62,22 +62,16 @@ def main():
         ref = torch.mm(at.double(), bt.double())
         scale = ref.abs().max().item()
         line = f"{name:12s} {m:6d}x{n:5d}x{k:6d} |"
-        # alternating twice (the clock the chip holds differs by body); x6dma includes its
-        # two operand-split launches
-        for tag, env, dma, peak in (("x6", "1", "0", PEAKX6), ("x6dma", "1", "1", PEAKX6),
-                                    ("x6dpp", "1", "2", PEAKX6), ("x6", "1", "0", PEAKX6),
-                                    ("x6dma", "1", "1", PEAKX6), ("x6dpp", "1", "2", PEAKX6),
-                                    ("fp32", "0", "0", PEAK32)):
+        # alternating twice (the clock the chip holds differs by body)
+        for tag, env, peak in (("x6", "1", PEAKX6), ("x6", "1", PEAKX6), ("fp32", "0", PEAK32)):
             if args.mode is not None and tag != args.mode:
                 continue
             os.environ["DS2_GEMM_X6"] = env
-            os.environ["DS2_GEMM_DMA"] = dma
             t = timeit(lambda: ops.sgemm(a, b, c, **kw), iters=30)
             err = (c.double() - ref).abs().max().item() / scale
             tf = fl / t / 1e9
             line += f" {tag} {tf:6.1f} TF ({tf / peak:4.0%}) {t * 1e3:7.1f} us err {err:.1e} |"
         os.environ.pop("DS2_GEMM_X6", None)
-        os.environ.pop("DS2_GEMM_DMA", None)
         print(line, flush=True)
 
 

@@ -25,7 +25,7 @@ def _close(got, ref, rel=1e-5, name=""):
 
 
 # ---------------------------------------------------------------------------- GEMM
-@pytest.mark.parametrize("x6", ["1", "dma", "0"])
+@pytest.mark.parametrize("x6", ["1", "0"])
 @pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
 @pytest.mark.parametrize("m,n,k", [(1, 1, 1), (37, 53, 29), (128, 128, 16), (300, 257, 513),
                                    (515, 2400, 132), (257, 300, 5000),   # split-K path
@@ -34,11 +34,8 @@ def _close(got, ref, rel=1e-5, name=""):
 def test_sgemm(dev, ta, tb, m, n, k, x6, monkeypatch):
     """ds2_sgemm_ws vs fp64 at 1e-5: the bf16x6 kernel (default for float4-staged operands;
     256 x 160 tiles for N >= 256, 256 x 128 below; its 16x16x32 form where every stage lies
-    inside K, the 32x32x16 form for a K tail), the same product on pre-split planes by LDS-DMA
-    ("dma": DS2_GEMM_DMA=1, every shape with N >= 256; the others run as "1") and the fp32-MFMA
-    kernels (DS2_GEMM_X6=0)."""
-    monkeypatch.setenv("DS2_GEMM_X6", "0" if x6 == "0" else "1")
-    monkeypatch.setenv("DS2_GEMM_DMA", "1" if x6 == "dma" else "0")
+    inside K, the 32x32x16 form for a K tail) and the fp32-MFMA kernels (DS2_GEMM_X6=0)."""
+    monkeypatch.setenv("DS2_GEMM_X6", x6)
     g = torch.Generator().manual_seed(m * 7 + n * 3 + k)
     a = torch.randn(k, m, generator=g) if ta else torch.randn(m, k, generator=g)
     b = torch.randn(n, k, generator=g) if tb else torch.randn(k, n, generator=g)
@@ -53,19 +50,16 @@ def test_sgemm(dev, ta, tb, m, n, k, x6, monkeypatch):
     _close(cd, ref, 1e-5, "sgemm")
 
 
-@pytest.mark.parametrize("mode", ["x6", "x6-narrow", "x6-ktail", "x6-ktail-narrow", "x6-dma",
-                                  "x6-dma-ktail", "fp32",
+@pytest.mark.parametrize("mode", ["x6", "x6-narrow", "x6-ktail", "x6-ktail-narrow", "fp32",
                                   "fp32-narrow", "unaligned"])
 @pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
 def test_sgemm_full_rounds_plus_split_tail(dev, ta, tb, mode, monkeypatch):
     """Whole rounds of resident workgroups + a tail whose K range is split (one launch) and
     reduced in a fixed order; alpha/beta/bias applied once.  bf16x6 kernel: 256 x 160 tiles
-    (N >= 256) and 256 x 128 ("-narrow": N < 256), "-dma" the pre-split planes by LDS-DMA
-    (DS2_GEMM_DMA=1; "-ktail": K zero-padded to 32 in the planes); fp32 kernels (DS2_GEMM_X6=0): BK = 64 /
+    (N >= 256) and 256 x 128 ("-narrow": N < 256); fp32 kernels (DS2_GEMM_X6=0): BK = 64 /
     16x16x4 with the plan's tile width, and ("unaligned": A one float off 16-B alignment)
     the BK = 16 / 32x32x2 kernel."""
     monkeypatch.setenv("DS2_GEMM_X6", "1" if mode.startswith("x6") else "0")
-    monkeypatch.setenv("DS2_GEMM_DMA", "1" if "dma" in mode else "0")
     # K % 32 == 0: the 16x16x32 form; "-ktail" (K % 32 == 4): the 32x32x16 form with k checks
     m, k = 128 * 29, 2084 if "ktail" in mode else 2080
     n = 200 if mode.endswith("narrow") else 128 * 27 + 52
