@@ -332,7 +332,8 @@ __device__ __forceinline__ unsigned long long beam_pack(float s, int key) {
 // of beam_better: score, then char, then index).  Returns the number selected.
 template <int NJ>
 __device__ __forceinline__ int beam_select(const unsigned long long* ukey, int tot, int beam,
-                                           int* sel_k, unsigned long long* sk, int lane) {
+                                           int* sel_k, unsigned long long* sk, int lane,
+                                           unsigned long long lb) {
   unsigned long long ru[NJ];
 #pragma unroll
   for (int jj = 0; jj < NJ; ++jj) {
@@ -345,6 +346,37 @@ __device__ __forceinline__ int beam_select(const unsigned long long* ukey, int t
     for (int jj = 0; jj < NJ; ++jj) n += __popcll(__ballot(ru[jj] >= c));
     return n;
   };
+  // fast path: lb (a key such that at least `beam` keys are >= it; 0 = none) usually leaves
+  // at most 64 keys; they are compacted one per lane and ranked against each other by
+  // v_readlane, with no bit-by-bit descent
+  if (lb != 0ull) {
+    const int ns = count_ge(lb);
+    if (ns >= beam && ns <= 64) {
+      int base = 0;
+#pragma unroll
+      for (int jj = 0; jj < NJ; ++jj) {
+        const bool sel = ru[jj] >= lb;
+        const unsigned long long m = __ballot(sel);
+        if (sel)
+          sk[base + __builtin_amdgcn_mbcnt_hi(static_cast<unsigned>(m >> 32),
+                                              __builtin_amdgcn_mbcnt_lo(static_cast<unsigned>(m), 0))] = ru[jj];
+        base += __popcll(m);
+      }
+      __builtin_amdgcn_wave_barrier();
+      const unsigned long long kr = lane < ns ? sk[lane] : 0ull;
+      const unsigned klo = static_cast<unsigned>(kr), khi = static_cast<unsigned>(kr >> 32);
+      int rank = 0;
+      for (int j = 0; j < ns; ++j) {
+        const unsigned long long kj =
+            (static_cast<unsigned long long>(__builtin_amdgcn_readlane(khi, j)) << 32) |
+            static_cast<unsigned>(__builtin_amdgcn_readlane(klo, j));
+        rank += kj > kr ? 1 : 0;
+      }
+      if (lane < ns && rank < beam)
+        sel_k[rank] = static_cast<int>((0xFFFFFFFFu - klo) & 4095u);
+      return beam;
+    }
+  }
   unsigned long long thr = 1ull;                  // every candidate, when at most `beam`
   if (count_ge(1ull) > beam) {
     unsigned long long t = 0ull;
@@ -614,11 +646,12 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
   // until the final back-tracking)
   __shared__ int b_par[2][BM];
   __shared__ float b_lpc[2][BM];
+  __shared__ int b_len[2][BM];   // prefix length (the node's depth): one back-tracking walk
   __shared__ float score[BM];
   __shared__ unsigned long long cmask[BM];   // chars of the entry's in-beam children
   __shared__ float cpb[BM * CM], cpnb[BM * CM];
   __shared__ unsigned long long ukey[BM * CM];   // beam_pack(score, key) per candidate k
-  __shared__ unsigned long long sk_sel[BM];       // the selected keys (beam_select)
+  __shared__ unsigned long long sk_sel[BM > 64 ? BM : 64];   // the selected keys (beam_select)
   __shared__ float bl_sc[BM], bl_pb[BM], bl_pnb[BM];   // the blank candidate of each entry
   __shared__ int sel_k[BM];
   __shared__ int s_nb, s_nodes, s_nr;
@@ -651,7 +684,7 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
 
   if (lane == 0) {
     b_node[0][0] = 0; b_last[0][0] = -1; b_pb[0][0] = 0.f; b_pnb[0][0] = -INFINITY;
-    b_par[0][0] = -1; b_lpc[0][0] = -INFINITY;
+    b_par[0][0] = -1; b_lpc[0][0] = -INFINITY; b_len[0][0] = 0;
     par[0] = -1; chr[0] = -1; tst[0] = -1; lpcv[0] = -INFINITY;
     cnt[0] = 1; fc[0] = -1; ns[0] = -1; km[0] = 0ull;
     s_nb = 1;
@@ -728,28 +761,43 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
     {
       float sce[EPL];
       int jpe[EPL];
+      // every entry's (node, parent, last char) in registers (lane l: entry l + 64 r), so the
+      // scan over the beam below is v_readlane + VALU, not a chain of LDS round trips
+      int bnr[EPL], bpr[EPL], blr[EPL];
+#pragma unroll
+      for (int r = 0; r < EPL; ++r) {
+        const int e = lane + 64 * r;
+        const bool in = e < nb;
+        bnr[r] = in ? b_node[cur][e] : -2;
+        bpr[r] = in ? b_par[cur][e] : -2;
+        blr[r] = in ? b_last[cur][e] : 0;
+      }
 #pragma unroll
       for (int q = 0; q < EPL; ++q) {
         const int e = lane + 64 * q;
         sce[q] = INFINITY;
+        const int nd = bnr[q];
+        const int pnode = nd > 0 ? bpr[q] : -1;
+        int j = -1;
+        unsigned long long cm = 0ull;
+#pragma unroll
+        for (int r = 0; r < EPL; ++r) {
+          const int lim = min(64, nb - 64 * r);          // wave-uniform
+          for (int l = 0; l < lim; ++l) {
+            const int ni = __builtin_amdgcn_readlane(bnr[r], l);
+            const int pi = __builtin_amdgcn_readlane(bpr[r], l);
+            const int li = __builtin_amdgcn_readlane(blr[r], l);
+            if (pnode >= 0 && ni == pnode) j = 64 * r + l;
+            if (ni > 0 && pi == nd) cm |= 1ull << li;
+          }
+        }
         jpe[q] = -1;
         if (e < nb) {
           const float sc = beam_lse(b_pb[cur][e], b_pnb[cur][e]);
           score[e] = sc;
           sce[q] = sc;
-          const int nd = b_node[cur][e];
           b_km[e] = km_next[q];
           kept[e] = 0;
-          const int pnode = nd > 0 ? b_par[cur][e] : -1;
-          int j = -1;
-          unsigned long long cm = 0ull;
-#pragma unroll
-          for (int i = 0; i < BM; ++i) {   // unrolled: the nb LDS reads overlap
-            if (i >= nb) break;
-            const int ni = b_node[cur][i];
-            if (pnode >= 0 && ni == pnode) j = i;
-            if (ni > 0 && b_par[cur][i] == nd) cm |= 1ull << b_last[cur][i];
-          }
           jpe[q] = j;
           cmask[e] = cm;
         }
@@ -799,7 +847,7 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
       for (int q = 0; q < EPL; ++q) {
         const int i = lane + 64 * q;
         if (i < nb) {
-          const int last_i = b_last[cur][i];
+          const int last_i = blr[q];
           const float sc_i = sce[q];
           // with an LM a (prefix, char) pair below the pruning bound is skipped entirely
           const float pb = (allowed[blank] && !(lp[blank] + sc_i < cut)) ? lp[blank] + sc_i : -INFINITY;
@@ -815,7 +863,7 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
                             : lp[last_i] + sc_jp;
               if (LM && last_i == L.space) e = lm_add(e, b_lms[cur][jp], L.beta);
               pnb = beam_lse(pnb, e);
-              const int nd = b_node[cur][i];
+              const int nd = bnr[q];
               if (lp[last_i] > b_lpc[cur][i]) {
                 b_lpc[cur][i] = lp[last_i];
                 lpcv[nd] = lp[last_i];
@@ -910,12 +958,35 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
     constexpr int SD = BM * CM / 64;
     const int tot = nb * C;
     const int jd = (tot + 63) / 64;
-    const int nsel = jd <= 2    ? beam_select<2>(ukey, tot, beam, sel_k, sk_sel, lane)
-                     : jd <= 4  ? beam_select<4>(ukey, tot, beam, sel_k, sk_sel, lane)
-                     : jd <= 6  ? beam_select<6>(ukey, tot, beam, sel_k, sk_sel, lane)
-                     : jd <= 8  ? beam_select<8>(ukey, tot, beam, sel_k, sk_sel, lane)
-                     : jd <= 16 ? beam_select<16>(ukey, tot, beam, sel_k, sk_sel, lane)
-                                : beam_select<SD>(ukey, tot, beam, sel_k, sk_sel, lane);
+    // a lower bound of the selection: the worst of the nb >= beam blank candidates (real
+    // candidates, so at least `beam` keys are >= it); 0 (none) while the beam is not full or
+    // some entry has no blank candidate (its key is 0)
+    unsigned long long lb = 0ull;
+    if (nb >= beam) {
+      unsigned long long v = ~0ull;
+#pragma unroll
+      for (int q = 0; q < EPL; ++q) {
+        const int e = lane + 64 * q;
+        if (e < nb) {
+          const unsigned long long kb = ukey[e * C + blank];
+          v = kb < v ? kb : v;
+        }
+      }
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) {
+        const unsigned long long w =
+            (static_cast<unsigned long long>(static_cast<unsigned>(__shfl_xor(static_cast<int>(v >> 32), o))) << 32) |
+            static_cast<unsigned>(__shfl_xor(static_cast<int>(static_cast<unsigned>(v)), o));
+        v = w < v ? w : v;
+      }
+      lb = v == ~0ull ? 0ull : v;
+    }
+    const int nsel = jd <= 2    ? beam_select<2>(ukey, tot, beam, sel_k, sk_sel, lane, lb)
+                     : jd <= 4  ? beam_select<4>(ukey, tot, beam, sel_k, sk_sel, lane, lb)
+                     : jd <= 6  ? beam_select<6>(ukey, tot, beam, sel_k, sk_sel, lane, lb)
+                     : jd <= 8  ? beam_select<8>(ukey, tot, beam, sel_k, sk_sel, lane, lb)
+                     : jd <= 16 ? beam_select<16>(ukey, tot, beam, sel_k, sk_sel, lane, lb)
+                                : beam_select<SD>(ukey, tot, beam, sel_k, sk_sel, lane, lb);
     __syncthreads();
     BEAM_STAMP(5)
     // ---- new beam: lane r builds entries r, r + 64, ...; new prefixes get trie nodes in
@@ -986,6 +1057,7 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
             b_last[nxt][e] = b_last[cur][i];
             b_par[nxt][e] = b_par[cur][i];
             b_lpc[nxt][e] = b_lpc[cur][i];
+            b_len[nxt][e] = b_len[cur][i];
             kept[i] = 1;
           } else if (revived) {
             const int x = rv[q];
@@ -994,6 +1066,7 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
             b_last[nxt][e] = c;
             b_par[nxt][e] = b_node[cur][i];
             b_lpc[nxt][e] = lpcv[x];
+            b_len[nxt][e] = b_len[cur][i] + 1;
           } else {
             const int nd = nodes0 + run + before;
             const int p = b_node[cur][i];
@@ -1012,6 +1085,7 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
             b_last[nxt][e] = c;
             b_par[nxt][e] = b_node[cur][i];
             b_lpc[nxt][e] = lp[c];
+            b_len[nxt][e] = b_len[cur][i] + 1;
           }
           b_pb[nxt][e] = cpb[k];
           b_pnb[nxt][e] = cpnb[k];
@@ -1077,12 +1151,11 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
     for (int i = 0; i < nb; ++i)
       if (i != e && beam_better(score[i], (b_last[cur][i] + 1) * 4096 + i, s0, key0)) ++rank;
     if (rank < top_paths) {
-      int len = 0;
-      for (int nd = b_node[cur][e]; nd > 0; nd = par[nd]) ++len;
+      const int len = b_len[cur][e];
       int* ids = out_ids + ((int64_t)n * top_paths + rank) * t_max;
       int* tsp = out_ts + ((int64_t)n * top_paths + rank) * t_max;
       int pos = len;
-      for (int nd = b_node[cur][e]; nd > 0; nd = par[nd]) {
+      for (int nd = b_node[cur][e]; nd > 0 && pos > 0; nd = par[nd]) {
         --pos;
         ids[pos] = chr[nd];
         tsp[pos] = tst[nd];
