@@ -610,6 +610,24 @@ __device__ int trie_alive_child(const int* fc, const int* ns, const int* chr, co
   return -1;
 }
 
+// wave minimum in VALU only (DPP: quad permutes, half-row and row mirrors, row_bcast:15 and
+// :31 -- lane 63 ends with the minimum), no LDS round trip; every lane gets it
+template <int CTRL, int RMASK>
+__device__ __forceinline__ float dpp_min_step(float x) {
+  const int y = __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, x), __builtin_bit_cast(int, x),
+                                            CTRL, RMASK, 0xf, false);
+  return fminf(x, __builtin_bit_cast(float, y));
+}
+__device__ __forceinline__ float wave_min_dpp(float v) {
+  v = dpp_min_step<0xB1, 0xf>(v);    // quad_perm [1, 0, 3, 2]
+  v = dpp_min_step<0x4E, 0xf>(v);    // quad_perm [2, 3, 0, 1]
+  v = dpp_min_step<0x141, 0xf>(v);   // row_half_mirror
+  v = dpp_min_step<0x140, 0xf>(v);   // row_mirror
+  v = dpp_min_step<0x142, 0xa>(v);   // row_bcast:15 into rows 1, 3
+  v = dpp_min_step<0x143, 0xc>(v);   // row_bcast:31 into rows 2, 3
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
+}
+
 __device__ __forceinline__ float wave_min(float v) {
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) v = fminf(v, __shfl_xor(v, o));
@@ -758,6 +776,7 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
     // parent's score recomputed here rather than read after a barrier)
     if (lane == 0) s_nr = 0;
     float cut = -INFINITY;   // LM: min_cutoff once the beam is full, else -inf; wave-uniform
+    float blmin = INFINITY;  // the worst blank-candidate score of the beam (wave-uniform)
     {
       float sce[EPL];
       int jpe[EPL];
@@ -843,8 +862,10 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
         }
       }
       // ---- the blank candidate of every entry
+      float blsr[EPL];
 #pragma unroll
       for (int q = 0; q < EPL; ++q) {
+        blsr[q] = INFINITY;
         const int i = lane + 64 * q;
         if (i < nb) {
           const int last_i = blr[q];
@@ -873,21 +894,31 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
           }
           bl_pb[i] = pb;
           bl_pnb[i] = pnb;
-          bl_sc[i] = beam_lse(pb, pnb);
+          const float bs = beam_lse(pb, pnb);
+          bl_sc[i] = bs;
+          blsr[q] = bs;
         }
       }
+      float bm = INFINITY;
+#pragma unroll
+      for (int r = 0; r < EPL; ++r) bm = fminf(bm, blsr[r]);
+      blmin = wave_min_dpp(bm);
     }
     __syncthreads();
     BEAM_STAMP(2)
-    // ---- candidates k = i * C + c: lane (g, c) = divmod(lane, CM) scores char c of the entries
+    // ---- candidates k = i * C + c: lane (g, c) = divmod(lane, CW) scores char c of the entries
     // i = G jj + g, so the char's log prob and pruning flag stay in registers and every
     // per-entry read is one LDS address per lane group (a broadcast).  Entries go in groups of
     // SG: every LDS read of a group is issued before any of its arithmetic, which is
     // branch-free (the blank lane takes its entry's precomputed blank candidate); packed keys
     // go to ukey[k] for the selection
     {
-      constexpr int G = 64 / CM, SG = 4;
-      const int c = lane % CM, g = lane / CM;
+      // lane groups of 32 when the vocabulary fits (the small instantiation's CM = 64 would
+      // leave half the wave idle on the model's 29 labels): G entries per pass
+      constexpr int SG = 4;
+      const int CW = (CM > 32 && C <= 32) ? 32 : CM;     // wave-uniform
+      const int G = 64 / CW;
+      const int c = lane & (CW - 1), g = lane / CW;
       const bool cv = c < C;
       const int cs = cv ? c : 0;                          // an in-range char for idle lanes
       const float lpc = lp[cs];
@@ -958,29 +989,11 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
     constexpr int SD = BM * CM / 64;
     const int tot = nb * C;
     const int jd = (tot + 63) / 64;
-    // a lower bound of the selection: the worst of the nb >= beam blank candidates (real
-    // candidates, so at least `beam` keys are >= it); 0 (none) while the beam is not full or
-    // some entry has no blank candidate (its key is 0)
-    unsigned long long lb = 0ull;
-    if (nb >= beam) {
-      unsigned long long v = ~0ull;
-#pragma unroll
-      for (int q = 0; q < EPL; ++q) {
-        const int e = lane + 64 * q;
-        if (e < nb) {
-          const unsigned long long kb = ukey[e * C + blank];
-          v = kb < v ? kb : v;
-        }
-      }
-#pragma unroll
-      for (int o = 32; o >= 1; o >>= 1) {
-        const unsigned long long w =
-            (static_cast<unsigned long long>(static_cast<unsigned>(__shfl_xor(static_cast<int>(v >> 32), o))) << 32) |
-            static_cast<unsigned>(__shfl_xor(static_cast<int>(static_cast<unsigned>(v)), o));
-        v = w < v ? w : v;
-      }
-      lb = v == ~0ull ? 0ull : v;
-    }
+    // a lower bound of the selection: the score word of the worst of the nb >= beam blank
+    // candidates with an empty key word (they are real candidates, so at least `beam` keys are
+    // >= it); 0 (none) while the beam is not full or some entry has no blank candidate
+    const unsigned long long lb = (nb >= beam && blmin > -INFINITY)
+                                      ? (beam_pack(blmin, 0) & 0xFFFFFFFF00000000ull) : 0ull;
     const int nsel = jd <= 2    ? beam_select<2>(ukey, tot, beam, sel_k, sk_sel, lane, lb)
                      : jd <= 4  ? beam_select<4>(ukey, tot, beam, sel_k, sk_sel, lane, lb)
                      : jd <= 6  ? beam_select<6>(ukey, tot, beam, sel_k, sk_sel, lane, lb)
