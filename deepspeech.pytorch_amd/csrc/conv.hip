@@ -1455,35 +1455,36 @@ __device__ __forceinline__ void cw_split_store(unsigned short* __restrict__ s, i
 // order and scatters into dW[co][ci][a][b].  (The [co][ci][a][b] slab layout had each lane
 // store to its own line: 2.6x the partial bytes in write traffic.)
 constexpr int X6W_BLOCK = 32 * 4 * 32;     // floats per (co, w, ci) plane of one kernel column
-template <int KW>
+                                           // (4 tap rows per group; NW rows: NW / 4 of them)
+template <int KW, int NW = 4>
 __device__ __forceinline__ void x6w_store_block(float* __restrict__ partial, int s, int G, int gi,
                                                 int wave, bool active, int fr, int fh,
                                                 const f32x16 (&acc)[KW]) {
   if (!active) return;   // rows a >= kh: never read by the reduce
-  float* blk = partial + ((int64_t)s * G + gi) * X6W_BLOCK * KW;
+  float* blk = partial + ((int64_t)s * G + gi) * (X6W_BLOCK / 4 * NW) * KW;
 #pragma unroll
   for (int b = 0; b < KW; ++b)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int co = (r & 3) + 8 * (r >> 2) + 4 * fh;
-      blk[((co * 4 + wave) * KW + b) * 32 + fr] = acc[b][r];
+      blk[((co * NW + wave) * KW + b) * 32 + fr] = acc[b][r];
     }
 }
 
 // dW[co][ci][a][b] = sum over the S splits (in order) of the blocks above; thread = one
 // (gi, co, w, b, ci) element in block order (coalesced loads)
 __global__ void wgrad_reduce_x6_kernel(const float* __restrict__ partial, int S, int G, int KW,
-                                       ConvDims g, float* __restrict__ dw) {
-  const int64_t per = (int64_t)G * X6W_BLOCK * KW;
+                                       int NW, ConvDims g, float* __restrict__ dw) {
+  const int64_t per = (int64_t)G * (X6W_BLOCK / 4 * NW) * KW;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < per;
        i += (int64_t)gridDim.x * blockDim.x) {
     int64_t r = i;
     const int ci = static_cast<int>(r % 32); r /= 32;
     const int b = static_cast<int>(r % KW); r /= KW;
-    const int w = static_cast<int>(r % 4); r /= 4;
+    const int w = static_cast<int>(r % NW); r /= NW;
     const int co = static_cast<int>(r % 32);
     const int gi = static_cast<int>(r / 32);
-    const int a = 4 * gi + w;
+    const int a = NW * gi + w;
     if (a >= g.kh || co >= g.co || ci >= g.ci) continue;
     float acc = 0.f;
 #pragma unroll 8
@@ -1626,27 +1627,29 @@ __global__ __launch_bounds__(CW_T, 2) void conv_x6_wgrad_kernel(const float* __r
 // thread -- while the MFMAs of row ho run on the other slots; one barrier per row.  Each x row
 // is staged once per (group, chunk) instead of kh / sh times, and the G groups of a split run on
 // one XCD (consecutive workgroup ids), so they share its L2 for x and dy.
-constexpr int SW_T = 256;
 constexpr int SW_COLS = 32;                 // output columns per row stage (two 16-column k-steps)
 constexpr int SW_XP = 56;                   // x slot row pitch (bf16): columns c0 - 8 .. c0 + 39;
                                             // 7 x 16 B (odd): ds_read_b128's 16-lane groups
                                             // hit 16 distinct 16-B bank slots (48 had 2-way
                                             // conflicts: 34 % of LDS cycles in SQ counters)
 constexpr int SW_DP = 40;                   // dy row pitch (bf16): 32 columns, 5 x 16 B
-constexpr int SW_RING = 6;                  // x slots: 4 window rows + 2 incoming
 constexpr int SW_XSL = 32 * SW_XP;          // bf16 per x slot (32 input channels)
-constexpr int SW_XPL = SW_RING * SW_XSL;    // bf16 per x plane
 constexpr int SW_DPL = 32 * SW_DP;          // bf16 per dy plane
 
-template <int KW, int OFF0>
-__global__ __launch_bounds__(SW_T, 2) void conv_x6_wgrad_sw_kernel(const float* __restrict__ dy,
-                                                                   const float* __restrict__ x,
-                                                                   float* __restrict__ partial,
-                                                                   ConvDims g, int S) {
-  __shared__ __attribute__((aligned(16))) unsigned short xs[3 * SW_XPL];
+// NW = 8: eight waves (tap rows) per group, one 512-thread workgroup per CU with a 10-slot ring
+// (123 KB of LDS): G = 3 groups instead of 6 for conv2's 21 tap rows, so every x and dy row is
+// staged -- and fetched -- half as often
+template <int KW, int OFF0, int NW = 4>
+__global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_x6_wgrad_sw_kernel(
+    const float* __restrict__ dy, const float* __restrict__ x, float* __restrict__ partial,
+    ConvDims g, int S) {
+  static_assert(NW == 4 || NW == 8, "waves per group");
+  constexpr int RING = NW + 2;                // NW window rows + 2 incoming
+  __shared__ __attribute__((aligned(16))) unsigned short xs[3 * RING * SW_XSL];
   __shared__ __attribute__((aligned(16))) unsigned short ds[2][3 * SW_DPL];
+  constexpr int XPL = RING * SW_XSL;
   constexpr int kOob = 0x7ffffff0;
-  const int G = (g.kh + 3) / 4;
+  const int G = (g.kh + NW - 1) / NW;
   int gi, s;
   {
     const int nwg = gridDim.x, o = blockIdx.x;
@@ -1662,18 +1665,23 @@ __global__ __launch_bounds__(SW_T, 2) void conv_x6_wgrad_sw_kernel(const float* 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int a = 4 * gi + wave;
+  const int a = NW * gi + wave;
   const bool active = a < g.kh;
   const int fr = lane & 31, fh = lane >> 5;
   const int dplane = g.ho * g.wo, xplane = g.hi * g.wi;   // host: channel stacks < 2^31 B
-  const int wtop = 4 * gi - g.ph;                           // window row 0 of output row 0
+  const int wtop = NW * gi - g.ph;                          // window row 0 of output row 0
   // staging units (8 values each): 384 x units (incoming row r, channel, 8-column run j) and
-  // 128 dy units (channel, run j); thread t takes units t and t + 256
-  // (unit kinds are wave-uniform: waves 0-2 unit a row 0, wave 3 row 1; waves 0-1 unit b x
-  // row 1, waves 2-3 dy -- so the buffer resources stay scalar)
-  const int u1 = tid + SW_T;
-  const int xr_a = wave == 3 ? 1 : 0, xc_a = (tid / 6) & 31, xj_a = tid % 6;
-  const bool b_is_x = wave < 2;
+  // 128 dy units (channel, run j).  NW = 4: thread t takes units t and t + 256 (unit kinds are
+  // wave-uniform: waves 0-2 unit a row 0, wave 3 row 1; waves 0-1 unit b x row 1, waves 2-3
+  // dy -- so the buffer resources stay scalar).  NW = 8: thread t takes unit t alone (waves
+  // 0-2 x row 0, 3-5 x row 1, 6-7 dy; unit b unused)
+  const int u1 = NW == 4 ? tid + 256 : tid;
+  const int ta = NW == 4 ? tid : (wave < 6 ? tid % 192 : 0);
+  const int xr_a = NW == 4 ? (wave == 3 ? 1 : 0) : (wave >= 3 ? 1 : 0);
+  const int xc_a = NW == 4 ? (ta / 6) & 31 : ta / 6, xj_a = ta % 6;
+  const bool a_is_x = NW == 4 || wave < 6;
+  const bool b_is_x = NW == 4 && wave < 2;
+  const bool b_is_dy = NW == 4 ? wave >= 2 : wave >= 6;
   const int xc_b = (u1 / 6) & 31, xj_b = u1 % 6;             // x unit: incoming row 1
   const int dc_b = (u1 - 384) >> 2, dj_b = (u1 - 384) & 3;   // dy unit
 
@@ -1684,7 +1692,7 @@ __global__ __launch_bounds__(SW_T, 2) void conv_x6_wgrad_sw_kernel(const float* 
     for (int r = 0; r < 16; ++r) acc[b][r] = 0.f;
 
   float va[8], vb[8];
-  auto slot_of = [](int xr) { return ((xr % SW_RING) + SW_RING) % SW_RING; };
+  auto slot_of = [](int xr) { return ((xr % RING) + RING) % RING; };
 
   int row = r0;
   while (row < r1) {
@@ -1696,7 +1704,7 @@ __global__ __launch_bounds__(SW_T, 2) void conv_x6_wgrad_sw_kernel(const float* 
     const __amdgpu_buffer_rsrc_t xrs = conv_rsrc(x + (int64_t)n * g.ci * xplane, (int64_t)g.ci * xplane);
     // loads of x rows xr0 + r (r < nr; r = 0 unit a, r = 1 unit b) and, when hd >= 0, dy row hd
     auto load = [&](int xr0, int nr, int hd) {
-      {
+      if (a_is_x) {
         const int xr = xr0 + xr_a, cb = c0 - 8 + 8 * xj_a;
         const bool ok = xr_a < nr && xc_a < g.ci && xr >= 0 && xr < g.hi;
         const int vo = ok ? (xc_a * xplane + xr * g.wi + cb) * 4 : kOob;
@@ -1713,37 +1721,40 @@ __global__ __launch_bounds__(SW_T, 2) void conv_x6_wgrad_sw_kernel(const float* 
         for (int i = 0; i < 8; ++i)
           vb[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
                                                 xrs, (cb + i >= 0 && cb + i < g.wi) ? vo + 4 * i : kOob, 0, 0));
-      } else {
+      } else if (b_is_dy) {
+        // (NW = 8: the dy waves' unit goes in va, which they use for nothing else)
         const int cb = c0 + 8 * dj_b;
         const int vo = (hd >= 0 && dc_b < g.co) ? (dc_b * dplane + hd * g.wo + cb) * 4 : kOob;
+        float* vd = NW == 8 ? va : vb;
 #pragma unroll
         for (int i = 0; i < 8; ++i)
-          vb[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+          vd[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
                                                 drs, cb + i < g.wo ? vo + 4 * i : kOob, 0, 0));
       }
     };
     auto store = [&](int xr0, int nr, int db) {
-      if (xr_a < nr) cw_split_store(xs, SW_XPL, slot_of(xr0 + xr_a) * SW_XSL + xc_a * SW_XP + 8 * xj_a, va);
+      if (a_is_x && xr_a < nr) cw_split_store(xs, XPL, slot_of(xr0 + xr_a) * SW_XSL + xc_a * SW_XP + 8 * xj_a, va);
       if (b_is_x) {
-        if (nr > 1) cw_split_store(xs, SW_XPL, slot_of(xr0 + 1) * SW_XSL + xc_b * SW_XP + 8 * xj_b, vb);
-      } else if (db >= 0) {
-        cw_split_store(ds[db], SW_DPL, dc_b * SW_DP + 8 * dj_b, vb);
+        if (nr > 1) cw_split_store(xs, XPL, slot_of(xr0 + 1) * SW_XSL + xc_b * SW_XP + 8 * xj_b, vb);
+      } else if (b_is_dy && db >= 0) {
+        cw_split_store(ds[db], SW_DPL, dc_b * SW_DP + 8 * dj_b, NW == 8 ? va : vb);
       }
     };
     // segment start: every slot and dy buffer is free once all waves pass this barrier; the
-    // four window rows of ho0 go in two passes (the first with ho0's dy row)
+    // NW window rows of ho0 go in NW / 2 passes (the first with ho0's dy row)
     const int xb0 = ho0 * g.sh + wtop;
     __syncthreads();
-    load(xb0, 2, ho0);
-    store(xb0, 2, ho0 & 1);
-    load(xb0 + 2, 2, -1);
-    store(xb0 + 2, 2, -1);
+#pragma unroll
+    for (int p = 0; p < NW / 2; ++p) {
+      load(xb0 + 2 * p, 2, p == 0 ? ho0 : -1);
+      store(xb0 + 2 * p, 2, p == 0 ? (ho0 & 1) : -1);
+    }
     __syncthreads();
     for (int k = 0; k < nrow; ++k) {
       const int ho = ho0 + k;
       const bool more = k + 1 < nrow;
       const int xb = ho * g.sh + wtop;                      // window row 0 of this output row
-      const int xin = xb + 4;                               // row ho + 1's incoming rows
+      const int xin = xb + NW;                              // row ho + 1's incoming rows
       if (more) load(xin, g.sh, ho + 1);
       if (active) {
         const unsigned short* dsb = ds[ho & 1];
@@ -1760,7 +1771,7 @@ __global__ __launch_bounds__(SW_T, 2) void conv_x6_wgrad_sw_kernel(const float* 
             unsigned wv[12];
 #pragma unroll
             for (int jj = 0; jj < 3; ++jj) {
-              const u32x4 qv = *reinterpret_cast<const u32x4*>(xsl + pl * SW_XPL + 8 * (2 * kst + fh + jj));
+              const u32x4 qv = *reinterpret_cast<const u32x4*>(xsl + pl * XPL + 8 * (2 * kst + fh + jj));
 #pragma unroll
               for (int e = 0; e < 4; ++e) wv[4 * jj + e] = qv[e];
             }
@@ -1787,7 +1798,7 @@ __global__ __launch_bounds__(SW_T, 2) void conv_x6_wgrad_sw_kernel(const float* 
     }
     row += nrow;
   }
-  x6w_store_block<KW>(partial, s, G, gi, wave, active, fr, fh, acc);
+  x6w_store_block<KW, NW>(partial, s, G, gi, wave, active, fr, fh, acc);
 }
 
 // ---------------------------------------------------------------------------
@@ -1908,34 +1919,40 @@ __global__ __launch_bounds__(CX_T, 1) void conv_x6q_dgrad_kernel(const float* __
     }
   }
 
-  float rp[2][8];
-  u32x4 rw[WR];
-  auto load = [&](int l) {
+  // staging registers: one set per channel parity (DB: channel l + 2 is gathered while channel
+  // l + 1, gathered a whole channel earlier, is split into the free buffer between channel l's
+  // k-steps, so neither the gather latency nor the split stands between two channels)
+  struct Stage {
+    float rp[2][8];
+    u32x4 rw[WR];
+  };
+  Stage sa, sb;
+  auto load = [&](int l, Stage& S) {
     const __amdgpu_buffer_rsrc_t rs = conv_rsrc(inn + (int64_t)l * plane_in, plane_in);
 #pragma unroll
     for (int u = 0; u < 2; ++u)
 #pragma unroll
       for (int x = 0; x < 8; ++x)
-        rp[u][x] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, goff[u][x], 0, 0));
+        S.rp[u][x] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, goff[u][x], 0, 0));
     const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<unsigned short*>(wimg + (int64_t)l * wstride), (short)0, wstride * 2, 0x00020000);
 #pragma unroll
     for (int r = 0; r < WR; ++r) {
       const int i = tid + CX_T * r;
-      rw[r] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                            wr, i < wchunks ? i * 16 : 0x7ffffff0, 0, 0));
+      S.rw[r] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                              wr, i < wchunks ? i * 16 : 0x7ffffff0, 0, 0));
     }
   };
-  auto store = [&](int b) {
+  auto store = [&](int b, const Stage& S) {
     unsigned short* pb = ps + b * (3 * CQ_PPL);
     unsigned short* wb = ws + b * wstride;
 #pragma unroll
     for (int u = 0; u < 2; ++u)
-      if (soff[u] >= 0) cw_split_store(pb, CQ_PPL, soff[u], rp[u]);
+      if (soff[u] >= 0) cw_split_store(pb, CQ_PPL, soff[u], S.rp[u]);
 #pragma unroll
     for (int r = 0; r < WR; ++r) {
       const int i = tid + CX_T * r;
-      if (i < wchunks) *reinterpret_cast<u32x4*>(wb + 8 * i) = rw[r];
+      if (i < wchunks) *reinterpret_cast<u32x4*>(wb + 8 * i) = S.rw[r];
     }
   };
 
@@ -1948,58 +1965,82 @@ __global__ __launch_bounds__(CX_T, 1) void conv_x6q_dgrad_kernel(const float* __
   const bool active = orow < out_h && c0 + 64 * cw < out_w;
   constexpr int H0 = (CQ_NK + 1) / 2;
 
-  load(0);
-  store(0);
-  __syncthreads();
-  for (int l = 0; l < L; ++l) {
+  auto kstep = [&](int st, int cur) {
+    const unsigned short* pc = ps + cur * (3 * CQ_PPL);
+    const unsigned short* wc = ws + cur * wstride;
+    const int rq = st / 3, cq = st - (st / 3) * 3;
+    bf16x8 af[3], bfr[2][3];
+    const int aw = fr * CQ_COP + (st * 2 + fh) * 8;
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl) af[pl] = *reinterpret_cast<const bf16x8*>(wc + pl * WPL + aw);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int sc = 64 * cw + 32 * j + fr + 4 * cq + 2 * fh;   // first patch column
+      const int ap = (sc & 1) * CQ_OFFO + (sc >> 1) * CQ_PP + 8 * rq;
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl)
+        bfr[j][pl] = *reinterpret_cast<const bf16x8*>(pc + pl * CQ_PPL + ap);
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      f32x16 cc = acc[j];
+      cc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1], bfr[j][1], cc, 0, 0, 0);
+      cc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[2], bfr[j][0], cc, 0, 0, 0);
+      cc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bfr[j][2], cc, 0, 0, 0);
+      cc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1], bfr[j][0], cc, 0, 0, 0);
+      cc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bfr[j][1], cc, 0, 0, 0);
+      acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bfr[j][0], cc, 0, 0, 0);
+    }
+  };
+  // channel l from buffer l & 1 (DB) or 0; X holds channel l + 1, Y receives channel l + 2
+  auto channel = [&](int l, Stage& X, Stage& Y) {
     const int cur = DB ? (l & 1) : 0;
-    if (l + 1 < L) load(l + 1);
+    if (DB) {
+      if (l + 2 < L) load(l + 2, Y);
+    } else if (l + 1 < L) {
+      load(l + 1, X);
+    }
+    bool staged = !DB || l + 1 >= L;
     if (active) {
-      const unsigned short* pc = ps + cur * (3 * CQ_PPL);
-      const unsigned short* wc = ws + cur * wstride;
-      auto kstep = [&](int st) {
-        const int rq = st / 3, cq = st - (st / 3) * 3;
-        bf16x8 af[3], bfr[2][3];
-        const int aw = fr * CQ_COP + (st * 2 + fh) * 8;
-#pragma unroll
-        for (int pl = 0; pl < 3; ++pl) af[pl] = *reinterpret_cast<const bf16x8*>(wc + pl * WPL + aw);
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const int sc = 64 * cw + 32 * j + fr + 4 * cq + 2 * fh;   // first patch column
-          const int ap = (sc & 1) * CQ_OFFO + (sc >> 1) * CQ_PP + 8 * rq;
-#pragma unroll
-          for (int pl = 0; pl < 3; ++pl)
-            bfr[j][pl] = *reinterpret_cast<const bf16x8*>(pc + pl * CQ_PPL + ap);
-        }
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          f32x16 cc = acc[j];
-          cc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1], bfr[j][1], cc, 0, 0, 0);
-          cc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[2], bfr[j][0], cc, 0, 0, 0);
-          cc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bfr[j][2], cc, 0, 0, 0);
-          cc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1], bfr[j][0], cc, 0, 0, 0);
-          cc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bfr[j][1], cc, 0, 0, 0);
-          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bfr[j][0], cc, 0, 0, 0);
-        }
-      };
       if (kk == 0) {
 #pragma unroll
-        for (int st = 0; st < H0; ++st) kstep(st);
+        for (int st = 0; st < H0; ++st) {
+          kstep(st, cur);
+          if (!staged) {   // the other buffer was last read in channel l - 1, before the last barrier
+            store(cur ^ 1, X);
+            staged = true;
+          }
+        }
       } else {
 #pragma unroll
-        for (int st = H0; st < CQ_NK; ++st) kstep(st);
+        for (int st = H0; st < CQ_NK; ++st) {
+          kstep(st, cur);
+          if (!staged) {
+            store(cur ^ 1, X);
+            staged = true;
+          }
+        }
       }
     }
+    if (!staged) store(cur ^ 1, X);
+    __syncthreads();
+    if (!DB && l + 1 < L) {
+      store(0, X);
+      __syncthreads();
+    }
+  };
+
+  load(0, sa);
+  store(0, sa);
+  if (DB && L > 1) load(1, sb);
+  __syncthreads();
+  for (int l = 0; l < L; l += 2) {
     if (DB) {
-      // the other buffer was last read in channel l - 1, before the previous barrier
-      if (l + 1 < L) store(cur ^ 1);
-      __syncthreads();
+      channel(l, sb, sa);
+      if (l + 1 < L) channel(l + 1, sa, sb);
     } else {
-      __syncthreads();
-      if (l + 1 < L) {
-        store(0);
-        __syncthreads();
-      }
+      channel(l, sa, sb);
+      if (l + 1 < L) channel(l + 1, sa, sb);
     }
   }
   // the two k halves meet in LDS (the patch area): half 1 writes, half 0 adds (fixed order)
@@ -2252,11 +2293,15 @@ static inline bool x6w_sw(const ConvDims& g) {
   return g.sh <= 2 && R < (1ll << 31) - 1;
 }
 
+// tap rows per group: 8 for the sliding-window form (one workgroup per CU), 4 otherwise
+static inline int x6w_nw(const ConvDims& g) { return x6w_sw(g) ? 8 : 4; }
+
 static inline int x6w_splits(const ConvDims& g) {
-  const int G = (g.kh + 3) / 4;
+  const int nw = x6w_nw(g);
+  const int G = (g.kh + nw - 1) / nw;
   const int64_t R = x6w_sw(g) ? (int64_t)g.n * ((g.wo + SW_COLS - 1) / SW_COLS) * g.ho
                               : (int64_t)g.n * g.ho;
-  int64_t S = CW_SLOTS / G;
+  int64_t S = (nw == 8 ? CW_SLOTS / 2 : CW_SLOTS) / G;
   if (S < 1) S = 1;
   return static_cast<int>(S > R ? R : S);
 }
@@ -2347,8 +2392,10 @@ size_t ds2_conv2d_wgrad_workspace_size(int n, int c_in, int h_in, int w_in, int 
   ConvDims g;
   if (!make_dims(g, n, c_in, h_in, w_in, c_out, kh, kw, sh, sw, ph, pw)) return 0;
   const size_t per = (size_t)c_out * c_in * kh * kw * sizeof(float);
-  if (x6w_ok(g))
-    return (size_t)x6w_splits(g) * ((kh + 3) / 4) * X6W_BLOCK * kw * sizeof(float) + 256;
+  if (x6w_ok(g)) {
+    const int nw = x6w_nw(g);
+    return (size_t)x6w_splits(g) * ((kh + nw - 1) / nw) * (X6W_BLOCK / 4 * nw) * kw * sizeof(float) + 256;
+  }
   const WgradPlan pl = wgrad_plan(g);
   return (size_t)n * (pl.nt > 0 ? pl.bands : 1) * per + 256;
 }
@@ -2370,9 +2417,10 @@ ds2_status_t ds2_conv2d_wgrad(const float* dy, const float* x, float* dw, float*
   int slabs = n;
   if (x6w_ok(g)) {
     slabs = x6w_splits(g);
-    const int G = (kh + 3) / 4;
+    const int nw = x6w_nw(g);
+    const int G = (kh + nw - 1) / nw;
     if (x6w_sw(g))
-      hipLaunchKernelGGL((conv_x6_wgrad_sw_kernel<11, 3>), dim3(G * slabs), dim3(SW_T), 0, st, dy,
+      hipLaunchKernelGGL((conv_x6_wgrad_sw_kernel<11, 3, 8>), dim3(G * slabs), dim3(512), 0, st, dy,
                          x, partial, g, slabs);
     else
       hipLaunchKernelGGL((conv_x6_wgrad_kernel<11, 3>), dim3(G * slabs), dim3(CW_T), 0, st, dy, x,
@@ -2397,11 +2445,12 @@ ds2_status_t ds2_conv2d_wgrad(const float* dy, const float* x, float* dw, float*
   int rg = cdiv(per, 256);
   if (rg > 2048) rg = 2048;
   if (x6w_ok(g)) {
-    const int G = (kh + 3) / 4;
-    const int64_t blk = (int64_t)G * X6W_BLOCK * kw;
+    const int nw = x6w_nw(g);
+    const int G = (kh + nw - 1) / nw;
+    const int64_t blk = (int64_t)G * (X6W_BLOCK / 4 * nw) * kw;
     const int xg = static_cast<int>(std::min<int64_t>(cdiv(blk, 256), 2048));
     hipLaunchKernelGGL(wgrad_reduce_x6_kernel, dim3(xg), dim3(256), 0, st, partial, slabs, G, kw,
-                       g, dw);
+                       nw, g, dw);
   } else {
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(rg), dim3(256), 0, st, partial, slabs, per, dw);
   }
