@@ -1919,40 +1919,34 @@ __global__ __launch_bounds__(CX_T, 1) void conv_x6q_dgrad_kernel(const float* __
     }
   }
 
-  // staging registers: one set per channel parity (DB: channel l + 2 is gathered while channel
-  // l + 1, gathered a whole channel earlier, is split into the free buffer between channel l's
-  // k-steps, so neither the gather latency nor the split stands between two channels)
-  struct Stage {
-    float rp[2][8];
-    u32x4 rw[WR];
-  };
-  Stage sa, sb;
-  auto load = [&](int l, Stage& S) {
+  float rp[2][8];
+  u32x4 rw[WR];
+  auto load = [&](int l) {
     const __amdgpu_buffer_rsrc_t rs = conv_rsrc(inn + (int64_t)l * plane_in, plane_in);
 #pragma unroll
     for (int u = 0; u < 2; ++u)
 #pragma unroll
       for (int x = 0; x < 8; ++x)
-        S.rp[u][x] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, goff[u][x], 0, 0));
+        rp[u][x] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, goff[u][x], 0, 0));
     const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<unsigned short*>(wimg + (int64_t)l * wstride), (short)0, wstride * 2, 0x00020000);
 #pragma unroll
     for (int r = 0; r < WR; ++r) {
       const int i = tid + CX_T * r;
-      S.rw[r] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                              wr, i < wchunks ? i * 16 : 0x7ffffff0, 0, 0));
+      rw[r] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                            wr, i < wchunks ? i * 16 : 0x7ffffff0, 0, 0));
     }
   };
-  auto store = [&](int b, const Stage& S) {
+  auto store = [&](int b) {
     unsigned short* pb = ps + b * (3 * CQ_PPL);
     unsigned short* wb = ws + b * wstride;
 #pragma unroll
     for (int u = 0; u < 2; ++u)
-      if (soff[u] >= 0) cw_split_store(pb, CQ_PPL, soff[u], S.rp[u]);
+      if (soff[u] >= 0) cw_split_store(pb, CQ_PPL, soff[u], rp[u]);
 #pragma unroll
     for (int r = 0; r < WR; ++r) {
       const int i = tid + CX_T * r;
-      if (i < wchunks) *reinterpret_cast<u32x4*>(wb + 8 * i) = S.rw[r];
+      if (i < wchunks) *reinterpret_cast<u32x4*>(wb + 8 * i) = rw[r];
     }
   };
 
@@ -1965,82 +1959,58 @@ __global__ __launch_bounds__(CX_T, 1) void conv_x6q_dgrad_kernel(const float* __
   const bool active = orow < out_h && c0 + 64 * cw < out_w;
   constexpr int H0 = (CQ_NK + 1) / 2;
 
-  auto kstep = [&](int st, int cur) {
-    const unsigned short* pc = ps + cur * (3 * CQ_PPL);
-    const unsigned short* wc = ws + cur * wstride;
-    const int rq = st / 3, cq = st - (st / 3) * 3;
-    bf16x8 af[3], bfr[2][3];
-    const int aw = fr * CQ_COP + (st * 2 + fh) * 8;
-#pragma unroll
-    for (int pl = 0; pl < 3; ++pl) af[pl] = *reinterpret_cast<const bf16x8*>(wc + pl * WPL + aw);
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int sc = 64 * cw + 32 * j + fr + 4 * cq + 2 * fh;   // first patch column
-      const int ap = (sc & 1) * CQ_OFFO + (sc >> 1) * CQ_PP + 8 * rq;
-#pragma unroll
-      for (int pl = 0; pl < 3; ++pl)
-        bfr[j][pl] = *reinterpret_cast<const bf16x8*>(pc + pl * CQ_PPL + ap);
-    }
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      f32x16 cc = acc[j];
-      cc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1], bfr[j][1], cc, 0, 0, 0);
-      cc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[2], bfr[j][0], cc, 0, 0, 0);
-      cc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bfr[j][2], cc, 0, 0, 0);
-      cc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1], bfr[j][0], cc, 0, 0, 0);
-      cc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bfr[j][1], cc, 0, 0, 0);
-      acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bfr[j][0], cc, 0, 0, 0);
-    }
-  };
-  // channel l from buffer l & 1 (DB) or 0; X holds channel l + 1, Y receives channel l + 2
-  auto channel = [&](int l, Stage& X, Stage& Y) {
+  load(0);
+  store(0);
+  __syncthreads();
+  for (int l = 0; l < L; ++l) {
     const int cur = DB ? (l & 1) : 0;
-    if (DB) {
-      if (l + 2 < L) load(l + 2, Y);
-    } else if (l + 1 < L) {
-      load(l + 1, X);
-    }
-    bool staged = !DB || l + 1 >= L;
+    if (l + 1 < L) load(l + 1);
     if (active) {
+      const unsigned short* pc = ps + cur * (3 * CQ_PPL);
+      const unsigned short* wc = ws + cur * wstride;
+      auto kstep = [&](int st) {
+        const int rq = st / 3, cq = st - (st / 3) * 3;
+        bf16x8 af[3], bfr[2][3];
+        const int aw = fr * CQ_COP + (st * 2 + fh) * 8;
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) af[pl] = *reinterpret_cast<const bf16x8*>(wc + pl * WPL + aw);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int sc = 64 * cw + 32 * j + fr + 4 * cq + 2 * fh;   // first patch column
+          const int ap = (sc & 1) * CQ_OFFO + (sc >> 1) * CQ_PP + 8 * rq;
+#pragma unroll
+          for (int pl = 0; pl < 3; ++pl)
+            bfr[j][pl] = *reinterpret_cast<const bf16x8*>(pc + pl * CQ_PPL + ap);
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          f32x16 cc = acc[j];
+          cc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1], bfr[j][1], cc, 0, 0, 0);
+          cc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[2], bfr[j][0], cc, 0, 0, 0);
+          cc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bfr[j][2], cc, 0, 0, 0);
+          cc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1], bfr[j][0], cc, 0, 0, 0);
+          cc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bfr[j][1], cc, 0, 0, 0);
+          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bfr[j][0], cc, 0, 0, 0);
+        }
+      };
       if (kk == 0) {
 #pragma unroll
-        for (int st = 0; st < H0; ++st) {
-          kstep(st, cur);
-          if (!staged) {   // the other buffer was last read in channel l - 1, before the last barrier
-            store(cur ^ 1, X);
-            staged = true;
-          }
-        }
+        for (int st = 0; st < H0; ++st) kstep(st);
       } else {
 #pragma unroll
-        for (int st = H0; st < CQ_NK; ++st) {
-          kstep(st, cur);
-          if (!staged) {
-            store(cur ^ 1, X);
-            staged = true;
-          }
-        }
+        for (int st = H0; st < CQ_NK; ++st) kstep(st);
       }
     }
-    if (!staged) store(cur ^ 1, X);
-    __syncthreads();
-    if (!DB && l + 1 < L) {
-      store(0, X);
-      __syncthreads();
-    }
-  };
-
-  load(0, sa);
-  store(0, sa);
-  if (DB && L > 1) load(1, sb);
-  __syncthreads();
-  for (int l = 0; l < L; l += 2) {
     if (DB) {
-      channel(l, sb, sa);
-      if (l + 1 < L) channel(l + 1, sa, sb);
+      // the other buffer was last read in channel l - 1, before the previous barrier
+      if (l + 1 < L) store(cur ^ 1);
+      __syncthreads();
     } else {
-      channel(l, sa, sb);
-      if (l + 1 < L) channel(l + 1, sa, sb);
+      __syncthreads();
+      if (l + 1 < L) {
+        store(0);
+        __syncthreads();
+      }
     }
   }
   // the two k halves meet in LDS (the patch area): half 1 writes, half 0 adds (fixed order)
