@@ -34,6 +34,7 @@ namespace ds2 {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x2v __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int BG_M = 256, BG_N = 256, BG_K = 64, BG_T = 512;
 constexpr int BG_IMG = (BG_M + BG_N) * BG_K;   // bf16 per LDS buffer (A rows, then B rows)
@@ -286,32 +287,86 @@ __global__ __launch_bounds__(BG_T, 1) void bgemm_nt_kernel(
 }
 
 // fp32 [rows][cols] (row stride ld_src) -> bf16 (RNE), either as is (dst [rows][ld_dst]) or
-// transposed (dst [cols][ld_dst]); 64 x 64 tiles through LDS for the transposed form
+// transposed (dst [cols][ld_dst]); 64 x 64 tiles.  vec (16-B aligned src / dst, ld_src % 4 ==
+// 0, ld_dst % 8 == 0): 16-B loads and 16-B stores of 8 bf16 -- the transposed form goes
+// through an fp32 LDS tile (float4 row loads in, 8-row column runs out); otherwise element
+// loads and 2-B stores
 __global__ __launch_bounds__(256) void cvt_bf16_kernel(const float* __restrict__ src, int rows,
                                                        int cols, int64_t ld_src,
                                                        unsigned short* __restrict__ dst,
                                                        int64_t ld_dst, int transpose, int vec) {
-  __shared__ unsigned short tl[64][66];
+  __shared__ float tf[64][65];
   const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
   const int t = threadIdx.x;
+  auto pack8 = [](const float* v) {
+    u32x4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      o[e] = __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2v{v[2 * e], v[2 * e + 1]}, bf16x2v));
+    return o;
+  };
   if (!transpose) {
-    // 64 rows x 64 cols: each thread 16 consecutive columns of one row (pairs when vec: src
-    // 8-B and dst 4-B aligned with even row strides)
+    // 64 rows x 64 cols: thread = (row t >> 2, 16 columns), two 8-column runs
     const int r = r0 + (t >> 2), cb = c0 + 16 * (t & 3);
     if (r >= rows) return;
-    const float* s = src + (int64_t)r * ld_src;
+    const float* sr = src + (int64_t)r * ld_src;
     unsigned short* d = dst + (int64_t)r * ld_dst;
 #pragma unroll
-    for (int i = 0; i < 16; i += 2) {
-      const int c = cb + i;
-      if (!vec) {
-        if (c < cols) d[c] = __builtin_bit_cast(unsigned short, (__bf16)s[c]);
-        if (c + 1 < cols) d[c + 1] = __builtin_bit_cast(unsigned short, (__bf16)s[c + 1]);
-      } else if (c + 1 < cols) {
-        const f32x2v v = *reinterpret_cast<const f32x2v*>(s + c);
-        *reinterpret_cast<unsigned*>(d + c) = __builtin_bit_cast(unsigned, __builtin_convertvector(v, bf16x2v));
-      } else if (c < cols) {
-        d[c] = __builtin_bit_cast(unsigned short, (__bf16)s[c]);
+    for (int h = 0; h < 2; ++h) {
+      const int c = cb + 8 * h;
+      if (c >= cols) break;
+      float v[8];
+      if (vec && c + 8 <= cols) {
+        const f32x4 x0 = *reinterpret_cast<const f32x4*>(sr + c);
+        const f32x4 x1 = *reinterpret_cast<const f32x4*>(sr + c + 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] = x0[e];
+          v[4 + e] = x1[e];
+        }
+        *reinterpret_cast<u32x4*>(d + c) = pack8(v);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (c + e < cols) d[c + e] = __builtin_bit_cast(unsigned short, (__bf16)sr[c + e]);
+      }
+    }
+    return;
+  }
+  // transposed: in = rows r0.. (64) x cols c0.. (64) as float4 runs (16 threads per row, 16
+  // rows per pass); out = for column c, rows r0 + 8 q .. + 7 as one 16-B store
+  if (vec) {
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int rr = 16 * p + (t >> 4), cc = 4 * (t & 15);
+      const int r = r0 + rr, c = c0 + cc;
+      f32x4 x = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (r < rows) {
+        if (c + 4 <= cols) {
+          x = *reinterpret_cast<const f32x4*>(src + (int64_t)r * ld_src + c);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) x[e] = c + e < cols ? src[(int64_t)r * ld_src + c + e] : 0.f;
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) tf[rr][cc + e] = x[e];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const int o = t + 256 * p;              // 512 outputs: (column, 8-row run)
+      const int cc = o >> 3, q = o & 7;
+      const int c = c0 + cc, rb = r0 + 8 * q;
+      if (c >= cols || rb >= rows) continue;
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = tf[8 * q + e][cc];
+      unsigned short* d = dst + (int64_t)c * ld_dst + rb;
+      if (rb + 8 <= rows) {
+        *reinterpret_cast<u32x4*>(d) = pack8(v);
+      } else {
+        for (int e = 0; e < 8 && rb + e < rows; ++e) d[e] = __builtin_bit_cast(unsigned short, (__bf16)v[e]);
       }
     }
     return;
@@ -319,14 +374,13 @@ __global__ __launch_bounds__(256) void cvt_bf16_kernel(const float* __restrict__
   for (int i = t; i < 64 * 64; i += 256) {
     const int rr = i >> 6, cc = i & 63;
     const int r = r0 + rr, c = c0 + cc;
-    tl[cc][rr] = (r < rows && c < cols) ? __builtin_bit_cast(unsigned short, (__bf16)src[(int64_t)r * ld_src + c])
-                                        : (unsigned short)0;
+    tf[cc][rr] = (r < rows && c < cols) ? src[(int64_t)r * ld_src + c] : 0.f;
   }
   __syncthreads();
   for (int i = t; i < 64 * 64; i += 256) {
     const int cc = i >> 6, rr = i & 63;
     const int r = r0 + rr, c = c0 + cc;
-    if (r < rows && c < cols) dst[(int64_t)c * ld_dst + r] = tl[cc][rr];
+    if (r < rows && c < cols) dst[(int64_t)c * ld_dst + r] = __builtin_bit_cast(unsigned short, (__bf16)tf[cc][rr]);
   }
 }
 
@@ -476,8 +530,8 @@ ds2_status_t ds2_cvt_bf16(const float* src, int rows, int cols, int64_t ld_src, 
   if (rows < 0 || cols < 0 || src == nullptr || dst == nullptr) return DS2_INVALID_VALUE;
   if (rows == 0 || cols == 0) return DS2_OK;
   if (ld_src < cols || ld_dst < (transpose ? rows : cols)) return DS2_INVALID_VALUE;
-  const int vec = !((reinterpret_cast<uintptr_t>(src) & 7) || (reinterpret_cast<uintptr_t>(dst) & 3) ||
-                    (ld_src & 1) || (ld_dst & 1));
+  const int vec = !((reinterpret_cast<uintptr_t>(src) & 15) || (reinterpret_cast<uintptr_t>(dst) & 15) ||
+                    (ld_src & 3) || (ld_dst & 7));
   const dim3 grid(cdiv(cols, 64), cdiv(rows, 64));
   if (grid.y > 65535) return DS2_UNSUPPORTED_SHAPE;
   hipLaunchKernelGGL(cvt_bf16_kernel, grid, dim3(256), 0, as_stream(stream), src, rows, cols,

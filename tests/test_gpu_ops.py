@@ -190,6 +190,20 @@ def test_bgemm_nt(dev, m, n, k):
     _close(c, ref, 1e-5, "bgemm_nt")
 
 
+@pytest.mark.parametrize("rows,cols", [(37, 53), (64, 64), (130, 96), (96, 130), (100, 8),
+                                       (1000, 1312), (65, 4100)])
+@pytest.mark.parametrize("transpose", [False, True])
+def test_cvt_bf16(dev, rows, cols, transpose):
+    """ds2_cvt_bf16 equals torch's bf16 rounding bit for bit on the 16-B vector paths (row
+    runs / LDS-transposed 8-row runs) and the element paths (strides not multiples of 4 / 8),
+    with partial 64 x 64 tiles and run tails in both directions."""
+    g = torch.Generator().manual_seed(rows * 7 + cols)
+    x = torch.randn(rows, cols, generator=g).to(dev)
+    y = ops.to_bf16(x, transpose=transpose)
+    ref = (x.t().contiguous() if transpose else x).to(torch.bfloat16)
+    assert torch.equal(y, ref)
+
+
 def test_sgemm_bf16_rejects_unaligned(dev):
     a = torch.randn(8, 6, device=dev)
     b = torch.randn(6, 8, device=dev)
