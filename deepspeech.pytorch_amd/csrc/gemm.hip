@@ -118,9 +118,9 @@ __device__ __forceinline__ void decode_work(int M, int N, int K, int main_wgs, i
                                             int tail_tiles, int nsplit, int kchunk,
                                             float* partial, int& m0, int& n0, int& kbeg,
                                             int& kend, int& bz, float*& part, int bn = BN,
-                                            int bm = BM, int item = -1) {
+                                            int bm = BM) {
   const int tn = (N + bn - 1) / bn;
-  const int orig = item >= 0 ? item : static_cast<int>(blockIdx.x);
+  const int orig = blockIdx.x;
   int tile, z = 0;
   part = nullptr;
   if (orig < main_wgs) {
@@ -889,10 +889,7 @@ __device__ __forceinline__ void x2_store160(unsigned short* __restrict__ s, cons
 // NPL 3: the bf16x6 fp32-accurate GEMM; NPL 1: the bf16-operand GEMM (operands rounded to
 // bf16 while staged, one product per fragment pair, fp32 accumulation -- cfg4's opt-in
 // precision), one LDS plane per operand
-// PERSIST: a capped grid (ds2_sgemm_slots_ws) -- workgroup b runs the whole tiles b, b + grid,
-// ... (main_wgs = all tiles, no split), one barrier between tiles (the next tile's prologue
-// refills the stage buffers the last one read)
-template <int TA, int TB, bool KCHK, int TBN, int NPL = 3, bool M16 = false, bool PERSIST = false>
+template <int TA, int TB, bool KCHK, int TBN, int NPL = 3, bool M16 = false>
 __global__ __launch_bounds__(X2T, 1) void sxgemm2_kernel(
     int M, int N, int K, float alpha, const float* __restrict__ A, int64_t lda, int64_t sA,
     const float* __restrict__ B, int64_t ldb, int64_t sB, float beta, float* __restrict__ C,
@@ -1178,15 +1175,6 @@ __global__ __launch_bounds__(X2T, 1) void sxgemm2_kernel(
 
   int m0, n0, kbeg, kend, bz;
   float* part;
-  if constexpr (PERSIST) {
-    for (int it = blockIdx.x; it < main_wgs; it += gridDim.x) {
-      if (it != static_cast<int>(blockIdx.x)) __syncthreads();
-      decode_work(M, N, K, main_wgs, tail_tile0, tail_tiles, nsplit, kchunk, partial, m0, n0, kbeg,
-                  kend, bz, part, TBN, X2M, it);
-      job(m0, n0, kbeg, kend, nullptr);
-    }
-    return;
-  }
   decode_work(M, N, K, main_wgs, tail_tile0, tail_tiles, nsplit, kchunk, partial, m0, n0, kbeg,
               kend, bz, part, TBN, X2M);
   A += bz * sA;
@@ -1460,35 +1448,6 @@ extern "C" ds2_status_t ds2_sgemm_ws(int trans_a, int trans_b, int m, int n, int
                        p.bn, p.bm);
   }
   return launch_status("ds2_sgemm");
-}
-
-// ds2_sgemm_ws on at most `slots` resident workgroups (one per CU, persistent over whole tiles):
-// for a GEMM run beside a persistent recurrence on the CUs it leaves free (ops.py side
-// stream).  The bf16x6 16x16x32 form only (float4-staged operands, batch 1, K % 32 == 0,
-// N >= 256); anything else is DS2_UNSUPPORTED_SHAPE (the caller runs it the normal way).
-extern "C" ds2_status_t ds2_sgemm_slots(int trans_a, int trans_b, int m, int n, int k, float alpha,
-                                        const float* a, int64_t lda, const float* b, int64_t ldb,
-                                        float beta, float* c, int64_t ldc, const float* bias,
-                                        int slots, ds2_stream_t stream) {
-  if (m < 0 || n < 0 || k < 0 || slots < 0) return DS2_INVALID_VALUE;
-  if (m == 0 || n == 0) return DS2_OK;
-  if (ldc < n || (trans_a ? lda < m : lda < k) || (trans_b ? ldb < k : ldb < n)) return DS2_INVALID_VALUE;
-  const bool va = aligned16(a) && (lda % 4 == 0) && (trans_a ? (m % 4 == 0) : (k % 4 == 0));
-  const bool vb = aligned16(b) && (ldb % 4 == 0) && (trans_b ? (k % 4 == 0) : (n % 4 == 0));
-  const bool fits = fits_rsrc(trans_a ? k : m, lda) && fits_rsrc(trans_b ? n : k, ldb);
-  if (!(fits && x6_enabled(va, vb)) || k == 0 || k % XS != 0 || n < 256 || slots < 8)
-    return DS2_UNSUPPORTED_SHAPE;
-  const int tiles = cdiv(m, X2M) * cdiv(n, 160);
-  int grid = slots & ~7;
-  if (grid > tiles) grid = tiles;
-  hipStream_t st = as_stream(stream);
-#define DS2_XP(TA_, TB_)                                                                          hipLaunchKernelGGL((sxgemm2_kernel<TA_, TB_, false, 160, 3, true, true>), dim3(grid), dim3(X2T),                      0, st, m, n, k, alpha, a, lda, (int64_t)0, b, ldb, (int64_t)0, beta, c, ldc,                      (int64_t)0, bias, tiles, tiles, 0, 1, k, static_cast<float*>(nullptr))
-  if (!trans_a && !trans_b) DS2_XP(0, 0);
-  else if (!trans_a && trans_b) DS2_XP(0, 1);
-  else if (trans_a && !trans_b) DS2_XP(1, 0);
-  else DS2_XP(1, 1);
-#undef DS2_XP
-  return launch_status("ds2_sgemm_slots");
 }
 
 // bf16-operand GEMM (sbgemm_kernel): same contract as ds2_sgemm_ws; every operand must be

@@ -45,8 +45,6 @@ _PROTOS = {
     "ds2_sgemm_ws": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _c_f, _vp, _c_i64, _c_i64,
                               _vp, _c_i64, _c_i64, _c_f, _vp, _c_i64, _c_i64, _c_int, _vp, _vp,
                               _sz, _vp]),
-    "ds2_sgemm_slots": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _c_f, _vp, _c_i64, _vp,
-                                 _c_i64, _c_f, _vp, _c_i64, _vp, _c_int, _vp]),
     "ds2_sgemm_bf16_workspace_size": (_sz, [_c_int, _c_int, _c_int, _c_int]),
     "ds2_sgemm_bf16_ws": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _c_f, _vp, _c_i64,
                                    _c_i64, _vp, _c_i64, _c_i64, _c_f, _vp, _c_i64, _c_i64, _c_int,

@@ -794,110 +794,6 @@ def _rnn_param_grads_bf16(x2d, h_all, dgx, dgh, weights, nd, g, t, n, inp, h, ne
     return dx, grads
 
 
-# ---- weight gradients beside the next recurrence --------------------------------------------
-# A persistent backward recurrence holds `grid` CUs (200 of 256 at cfg2) for its whole launch;
-# the rest are idle.  With side GEMMs on (Trainer, one rank: no gradient hook reads a gradient
-# before backward ends), the dW_hh products of a recurrent layer -- off the critical path --
-# are deferred and launched on a side stream right before the NEXT layer's recurrence, as
-# ds2_sgemm_slots on at most CUs - grid workgroups, so both kernels stay co-resident (each
-# workgroup of either holds a CU alone: the recurrence's LDS pad, the GEMM's 156 KB of
-# stages).  What no recurrence follows runs on the main stream when backward ends, and the
-# main stream then waits for the side stream (torch's end-of-backward callback).
-_SIDE = {"on": False, "pending": [], "events": [], "streams": {}, "queued": False, "launched": 0}
-
-
-def set_side_gemms(on: bool) -> None:
-    """Deferred side-stream weight gradients (see above); the Trainer turns them on for a
-    single rank."""
-    _SIDE["on"] = bool(on)
-
-
-def side_reset() -> None:
-    """Drop deferred products a failed backward left behind (Trainer, before each backward)."""
-    _SIDE["pending"].clear()
-    _SIDE["queued"] = False
-
-
-def _side_stream(dev):
-    st = _SIDE["streams"].get(dev)
-    if st is None:
-        st = torch.cuda.Stream(device=dev)
-        _SIDE["streams"][dev] = st
-    return st
-
-
-def _defer_gemm(dev, launch, tensors) -> None:
-    """launch(stream, slots) -> bool issues the product (slots > 0: capped, False when the
-    shape is not covered); launch(None, 0) issues it the normal way on the current stream."""
-    _SIDE["pending"].append((dev, launch, tensors))
-    if not _SIDE["queued"]:
-        _SIDE["queued"] = True
-        torch.autograd.Variable._execution_engine.queue_callback(_side_flush)
-
-
-def _side_launch(dev, grid: int) -> None:
-    """Before a persistent recurrence of `grid` workgroups: the deferred products on the side
-    stream, capped to the CUs the recurrence leaves."""
-    if not _SIDE["pending"]:
-        return
-    cus = torch.cuda.get_device_properties(dev).multi_processor_count
-    slots = (cus - grid) // 8 * 8
-    main = torch.cuda.current_stream(dev)
-    side = _side_stream(dev)
-    side.wait_stream(main)
-    keep = []
-    for item in _SIDE["pending"]:
-        d, launch, tensors = item
-        ok = False
-        if d == dev and grid > 0 and slots >= 8:
-            with torch.cuda.stream(side):
-                ok = launch(side, slots)
-            if ok:
-                _SIDE["launched"] += 1
-                for t in tensors:
-                    t.record_stream(side)
-        if not ok:
-            keep.append(item)
-    _SIDE["pending"] = keep
-    ev = torch.cuda.Event()
-    ev.record(side)
-    _SIDE["events"].append((dev, ev))
-
-
-def _side_flush() -> None:
-    """End of backward: what is still deferred runs on the main stream; the main stream waits
-    for every side launch."""
-    _SIDE["queued"] = False
-    pending, _SIDE["pending"] = _SIDE["pending"], []
-    for dev, launch, _ in pending:
-        with torch.cuda.device(dev):
-            launch(None, 0)
-    events, _SIDE["events"] = _SIDE["events"], []
-    for dev, ev in events:
-        torch.cuda.current_stream(dev).wait_event(ev)
-
-
-def _sgemm_deferred(a, b, c_ptr, *, m, n, k, trans_a, trans_b, lda, ldb, ldc, a_off=0, b_off=0,
-                    stream=None, slots=0) -> bool:
-    """C = op(A) op(B) into the raw pointer c_ptr (a gradient slot: holding the tensor itself
-    would keep autograd from adopting it as .grad) -- capped on `stream` (False: shape not
-    covered) or, with stream None, ds2_sgemm_ws on the current stream."""
-    es = 4
-    pa, pb = a.data_ptr() + es * a_off, b.data_ptr() + es * b_off
-    if stream is not None:
-        st = _lib.load().ds2_sgemm_slots(int(trans_a), int(trans_b), m, n, k, 1.0, pa, lda, pb,
-                                         ldb, 0.0, c_ptr, ldc, None, int(slots), stream.cuda_stream)
-        if st == 2:    # DS2_UNSUPPORTED_SHAPE
-            return False
-        _lib.check(st, "ds2_sgemm_slots")
-        return True
-    nbytes = _lib.size("ds2_sgemm_workspace_size", m, n, k, 1)
-    ws = _ws(nbytes, a.device) if nbytes > 0 else None
-    _lib.call("ds2_sgemm_ws", int(trans_a), int(trans_b), m, n, k, 1.0, pa, lda, 0, pb, ldb, 0,
-              0.0, c_ptr, ldc, 0, 1, None, _p(ws), 0 if ws is None else ws.numel(), _stream())
-    return True
-
-
 def _rnn_param_grads(x, h_all, dgx, dgh, weights, nd, g, need_dx, bf16=False, dbias=None):
     """Weight/bias/input gradients of one recurrent layer from the gate gradients.
 
@@ -941,17 +837,8 @@ def _rnn_param_grads(x, h_all, dgx, dgh, weights, nd, g, need_dx, bf16=False, db
             # sum_t dgh_t^T h_{t-1} (fwd) / h_{t+1} (rev); h_prev = 0 at the start
             a_off = (n * ld if d == 0 else 0) + d * g
             b_off = (0 if d == 0 else n * nd * h) + d * h
-            kw = dict(m=g, n=h, k=(t - 1) * n, trans_a=True, trans_b=False, lda=ld, ldb=nd * h,
-                      ldc=h, a_off=a_off, b_off=b_off)
-            # deferred only into a fresh gradient (autograd adopts the tensor as .grad when
-            # backward hands it over; an existing .grad would be accumulated into right then)
-            if _SIDE["on"] and not bf16 and dgh.is_cuda and w_hh.grad is None:
-                def launch(stream, slots, dgh=dgh, h_all=h_all, c_ptr=dw_hh.data_ptr(), kw=kw):
-                    return _sgemm_deferred(dgh, h_all, c_ptr, stream=stream, slots=slots, **kw)
-                _defer_gemm(dgh.device, launch, (dgh, h_all))
-            else:
-                sgemm(dgh, h_all, dw_hh, m=g, n=h, k=(t - 1) * n, trans_a=True, lda=ld,
-                      ldb=nd * h, ldc=h, a_off=a_off, b_off=b_off, bf16=bf16)
+            sgemm(dgh, h_all, dw_hh, m=g, n=h, k=(t - 1) * n, trans_a=True, lda=ld,
+                  ldb=nd * h, ldc=h, a_off=a_off, b_off=b_off, bf16=bf16)
         else:
             dw_hh.zero_()
         if dbias is None:
@@ -1044,8 +931,6 @@ class GRULayerFn(torch.autograd.Function):
         w_hh_r = weights[5] if nd == 2 else None
         ws = _ws(_lib.size("ds2_gru_bwd_workspace_size", n, h, nd), dev)
         _guard_cooperative("gru", n, h, nd)
-        if _SIDE["pending"]:
-            _side_launch(dev, persistent_bwd_grid("gru", n, h, nd))
         # bias gradients straight into their slots, summed by the recurrence kernel
         dbias = [grad_like(weights[4 * d + k]) for d in range(nd) for k in (2, 3)]
         _lib.call("ds2_gru_bwd_bias", t, n, h, nd, dy.data_ptr(), dy_dirs, w_hh_f.data_ptr(),

@@ -123,11 +123,6 @@ class Trainer:
                                      broadcast_buffers=broadcast_buffers)
         if dist.is_initialized():
             ops.set_cooperative_guard(self.reducer.guard_cooperative)
-        # one rank: the recurrent layers' dW_hh products run beside the next layer's backward
-        # recurrence on the CUs it leaves free (ops.set_side_gemms); with several ranks the
-        # bucket hooks read gradients mid-backward, so they stay in order on the main stream
-        ops.set_side_gemms(self.world == 1 and self.device.type == "cuda"
-                           and os.environ.get("DS2_SIDE_GEMMS", "1") != "0")
         self.criterion = CTCLoss()
         self.decoder = GreedyDecoder(labels)
         self.decode = decode
@@ -254,7 +249,6 @@ class Trainer:
 
         self.optimizer.zero_grad()
         self.reducer.begin()
-        ops.side_reset()
         loss.backward()
         self.reducer.finish()
         # clip + SGD; always taken for NaN data (see module docstring).  Skipped on the device

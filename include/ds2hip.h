@@ -133,15 +133,6 @@ ds2_status_t ds2_sgemm_ws(int trans_a, int trans_b, int m, int n, int k, float a
                           const float* b, int64_t ldb, int64_t stride_b, float beta,
                           float* c, int64_t ldc, int64_t stride_c, int batch,
                           const float* bias, void* ws, size_t ws_bytes, ds2_stream_t stream);
-/* The bf16x6 product on at most `slots` resident workgroups (one per CU, each looping over
- * whole tiles; no workspace): a weight gradient run on a side stream beside a persistent
- * recurrence, on the CUs the recurrence leaves free (slots = CUs - its grid - collective
- * CTAs), so both stay co-resident.  float4-staged operands, K % 32 == 0, N >= 256, slots >= 8;
- * DS2_UNSUPPORTED_SHAPE otherwise (the caller then runs ds2_sgemm_ws). */
-ds2_status_t ds2_sgemm_slots(int trans_a, int trans_b, int m, int n, int k, float alpha,
-                             const float* a, int64_t lda, const float* b, int64_t ldb,
-                             float beta, float* c, int64_t ldc, const float* bias, int slots,
-                             ds2_stream_t stream);
 /* bf16-operand variant (BASELINE cfg4 "bf16 MFMA RNN GEMMs", opt-in): same contract, A and
  * B rounded to bf16 (nearest even) as they are staged, v_mfma_f32_16x16x32_bf16, fp32
  * accumulation and fp32 C.  Needs float4-aligned operands (16-B aligned pointers, ld and

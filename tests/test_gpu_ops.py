@@ -475,46 +475,6 @@ def _gru_run(dev, n, t, inp, h, nd, seed, env, monkeypatch, amp=None):
     return outs
 
 
-def test_side_stream_weight_gradients(dev):
-    """ops.set_side_gemms: two stacked BiGRU-800 layers at batch 32 (persistent backward grid
-    200 of the CUs) -- the upper layer's dW_hh products run on the side stream beside the lower
-    layer's backward recurrence, capped to the CUs it leaves (ds2_sgemm_slots), the lower
-    layer's at the end of backward on the main stream.  Every gradient equals the in-order run:
-    dW_hh at 1e-5 of its max (whole tiles instead of the split-K plan: another fp32 summation
-    order), everything else bit for bit; and the side launches really happened."""
-    t, n, h = 60, 32, 800
-    g = torch.Generator().manual_seed(21)
-    a = h ** -0.5
-    layers = [[torch.rand(s, generator=g) * 2 * a - a for s in
-               [(3 * h, h), (3 * h, h), (3 * h,), (3 * h,)] * 2] for _ in range(2)]
-    lens = torch.tensor(sorted([t - (i % 5) * 4 for i in range(n)], reverse=True), dtype=torch.int32)
-    x = torch.randn(t, n, h, generator=g)
-    dy = torch.randn(t, n, h, generator=g)
-    outs = []
-    for side in (False, True):
-        ops.set_side_gemms(side)
-        try:
-            before = ops._SIDE["launched"]
-            ws = [[w.to(dev).requires_grad_(True) for w in lw] for lw in layers]
-            xd = x.to(dev).requires_grad_(True)
-            y = ops.GRULayerFn.apply(xd, lens.to(dev), True, h, *ws[0])
-            y = ops.GRULayerFn.apply(y, lens.to(dev), True, h, *ws[1])
-            y.backward(dy.to(dev))
-            torch.cuda.synchronize()
-            ops.check_rnn_status(dev)
-            launched = ops._SIDE["launched"] - before
-        finally:
-            ops.set_side_gemms(False)
-        outs.append(([xd.grad.cpu()] + [w.grad.cpu() for lw in ws for w in lw], launched))
-    (ref, l0), (got, l1) = outs
-    assert l0 == 0 and l1 == 2, (l0, l1)   # the upper layer's two directions
-    for i, (r, q) in enumerate(zip(ref, got)):
-        if i in (2, 6, 10, 14):      # the four W_hh gradients
-            _close(q, r, 1e-5, f"dW_hh {i}")
-        else:
-            assert torch.equal(q, r), i
-
-
 @pytest.mark.parametrize("n,h,bidir", [(32, 800, True), (7, 48, False), (17, 784, True),
                                        (33, 256, True), (16, 1024, True), (64, 256, False)])
 def test_gru_xcd_groups_bit_identical(dev, n, h, bidir, monkeypatch):
