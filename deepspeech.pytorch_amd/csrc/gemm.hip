@@ -1115,29 +1115,47 @@ __global__ __launch_bounds__(X2T, 1) void sxgemm2_kernel(
   }
 
   if constexpr (M16) {
-    // epilogue (16x16 C/D map: col = lane & 15, row = 4 (lane >> 4) + r)
+    // epilogue through the now idle stage buffers, 16 rows of the wave tile per pass (16x16
+    // C/D map: col = lane & 15, row = 4 (lane >> 4) + r, written row-major with a 4-float pad:
+    // conflict-free), leaving as 16-B row runs -- each store instruction writes 1 KB of whole
+    // row segments instead of sixteen 64-B pieces
+    constexpr int EW = WNT * 16, EP = EW + 4;
+    static_assert(8 * 16 * EP * 4 <= 2 * NPL * X2_AP * 2, "epilogue staging fits the A stages");
+    __syncthreads();   // every wave is done reading the last stage
+    float* const stg = reinterpret_cast<float*>(&As[0][0]) + wave * 16 * EP;
+    const bool cv4 = ((reinterpret_cast<uintptr_t>(C) | static_cast<uintptr_t>(ldc * 4)) & 15) == 0 &&
+                     (bias == nullptr || (reinterpret_cast<uintptr_t>(bias) & 15) == 0);
 #pragma unroll
     for (int i = 0; i < WMT; ++i) {
 #pragma unroll
-      for (int j = 0; j < WNT; ++j) {
-        const int cl = wn + 16 * j + (lane & 15);
-        const int rb = wm + 16 * i + 4 * (lane >> 4);
-        if (part != nullptr) {
+      for (int j = 0; j < WNT; ++j)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) part[(rb + r) * TBN + cl] = acc[i][j][r];
+        for (int r = 0; r < 4; ++r) stg[(4 * (lane >> 4) + r) * EP + 16 * j + (lane & 15)] = acc[i][j][r];
+#pragma unroll
+      for (int q = 0; q < WNT; ++q) {
+        const int idx = lane + 64 * q;
+        const int rr = idx / (EW / 4), c4 = idx - (idx / (EW / 4)) * (EW / 4);
+        const f32x4 v = *reinterpret_cast<const f32x4*>(stg + rr * EP + 4 * c4);
+        const int rl = wm + 16 * i + rr, cl = wn + 4 * c4;
+        if (part != nullptr) {
+          *reinterpret_cast<f32x4*>(part + rl * TBN + cl) = v;
           continue;
         }
-        const int col = n0 + cl;
-        if (col >= N) continue;
-        const float bv = bias != nullptr ? bias[col] : 0.f;
+        const int row = m0 + rl, col = n0 + cl;
+        if (row >= M || col >= N) continue;
+        float* cp = C + (int64_t)row * ldc + col;
+        if (cv4 && col + 3 < N) {
+          f32x4 o = v * alpha;
+          if (bias != nullptr) o += *reinterpret_cast<const f32x4*>(bias + col);
+          if (beta != 0.f) o += beta * *reinterpret_cast<const f32x4*>(cp);
+          *reinterpret_cast<f32x4*>(cp) = o;
+        } else {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = m0 + rb + r;
-          if (row < M) {
-            float* cp = C + (int64_t)row * ldc + col;
-            float v = alpha * acc[i][j][r] + bv;
-            if (beta != 0.f) v += beta * *cp;
-            *cp = v;
+          for (int e = 0; e < 4; ++e) {
+            if (col + e >= N) break;
+            float o = alpha * v[e] + (bias != nullptr ? bias[col + e] : 0.f);
+            if (beta != 0.f) o += beta * cp[e];
+            cp[e] = o;
           }
         }
       }
