@@ -1201,13 +1201,50 @@ __global__ __launch_bounds__(X2T, 1) void sxgemm2_kernel(
   job(m0, n0, kbeg, kend, part);
 }
 
-// Tail tiles: C[b] = alpha * sum_s partial[b][s][tile] + beta * C[b] + bias (fixed order)
+// Tail tiles: C[b] = alpha * sum_s partial[b][s][tile] + beta * C[b] + bias (fixed order).
+// VEC (16-B aligned C rows and bias, bn % 4 == 0): each thread four consecutive columns, 16-B
+// slab loads and C accesses -- the same per-element sums in the same order
+template <bool VEC>
 __global__ void splitk_reduce_kernel(const float* __restrict__ partial, int M, int N, int nsplit,
                                      int batch, int tail_tile0, int tail_tiles, float alpha,
                                      float beta, float* __restrict__ C, int64_t ldc, int64_t sC,
                                      const float* __restrict__ bias, int bn, int bm) {
   const int TE = bm * bn;
   const int tn = (N + bn - 1) / bn;
+  if constexpr (VEC) {
+    const int TE4 = TE / 4;
+    const int64_t total4 = (int64_t)batch * tail_tiles * TE4;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total4;
+         i += (int64_t)gridDim.x * blockDim.x) {
+      const int e = static_cast<int>(i % TE4) * 4;
+      const int64_t bt = i / TE4;
+      const int lt = static_cast<int>(bt % tail_tiles);
+      const int b = static_cast<int>(bt / tail_tiles);
+      int tile_m, tile_n;
+      tile_coords(tail_tile0 + lt, tn, (M + bm - 1) / bm, tile_m, tile_n);
+      const int row = tile_m * bm + e / bn;
+      const int col = tile_n * bn + e % bn;
+      if (row >= M || col >= N) continue;
+      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 8
+      for (int sp = 0; sp < nsplit; ++sp)
+        acc += *reinterpret_cast<const f32x4*>(partial + (((int64_t)b * nsplit + sp) * tail_tiles + lt) * TE + e);
+      float* cp = C + b * sC + (int64_t)row * ldc + col;
+      if (col + 3 < N) {
+        f32x4 v = alpha * acc;
+        if (bias != nullptr) v += *reinterpret_cast<const f32x4*>(bias + col);
+        if (beta != 0.f) v += beta * *reinterpret_cast<const f32x4*>(cp);
+        *reinterpret_cast<f32x4*>(cp) = v;
+      } else {
+        for (int c = 0; c < 4 && col + c < N; ++c) {
+          float v = alpha * acc[c] + (bias != nullptr ? bias[col + c] : 0.f);
+          if (beta != 0.f) v += beta * cp[c];
+          cp[c] = v;
+        }
+      }
+    }
+    return;
+  }
   const int64_t total = (int64_t)batch * tail_tiles * TE;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * blockDim.x) {
@@ -1458,12 +1495,19 @@ extern "C" ds2_status_t ds2_sgemm_ws(int trans_a, int trans_b, int m, int n, int
 #undef DS2_G
 #undef DS2_X6
   if (p.nsplit > 1) {
-    const int64_t total = (int64_t)batch * p.tail_tiles * p.bm * p.bn;
+    const bool vec = p.bn % 4 == 0 && aligned16(c) && ldc % 4 == 0 && stride_c % 4 == 0 &&
+                     (bias == nullptr || aligned16(bias));
+    const int64_t total = (int64_t)batch * p.tail_tiles * p.bm * p.bn / (vec ? 4 : 1);
     int g = cdiv(total, 256);
     if (g > 4096) g = 4096;
-    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(g), dim3(256), 0, st, partial, m, n, p.nsplit,
-                       batch, p.tail_tile0, p.tail_tiles, alpha, beta, c, ldc, stride_c, bias,
-                       p.bn, p.bm);
+    if (vec)
+      hipLaunchKernelGGL(splitk_reduce_kernel<true>, dim3(g), dim3(256), 0, st, partial, m, n,
+                         p.nsplit, batch, p.tail_tile0, p.tail_tiles, alpha, beta, c, ldc,
+                         stride_c, bias, p.bn, p.bm);
+    else
+      hipLaunchKernelGGL(splitk_reduce_kernel<false>, dim3(g), dim3(256), 0, st, partial, m, n,
+                         p.nsplit, batch, p.tail_tile0, p.tail_tiles, alpha, beta, c, ldc,
+                         stride_c, bias, p.bn, p.bm);
   }
   return launch_status("ds2_sgemm");
 }
@@ -1516,7 +1560,7 @@ extern "C" ds2_status_t ds2_sgemm_bf16_ws(int trans_a, int trans_b, int m, int n
     const int64_t total = (int64_t)batch * p.tail_tiles * p.bm * p.bn;
     int g = cdiv(total, 256);
     if (g > 4096) g = 4096;
-    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(g), dim3(256), 0, st, partial, m, n, p.nsplit,
+    hipLaunchKernelGGL(splitk_reduce_kernel<false>, dim3(g), dim3(256), 0, st, partial, m, n, p.nsplit,
                        batch, p.tail_tile0, p.tail_tiles, alpha, beta, c, ldc, stride_c, bias,
                        p.bn, p.bm);
   }
