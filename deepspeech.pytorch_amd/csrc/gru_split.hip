@@ -618,8 +618,7 @@ static const void* bwd_x6_fn(int pairs) {
 // 8 XCDs: cfg2 backward 5.82 -> 5.43 us per step in isolation, 6.14 -> 5.69 in the training
 // step; DS2_GRU_XCD=0 keeps map_work's interleaved layout (bit-identical results)
 static inline bool xcd_groups(int UB, int BT, int num_dirs) {
-  const char* xe = getenv("DS2_GRU_XCD");
-  return !(xe != nullptr && xe[0] == '0') && xgrp_fits(UB, BT, num_dirs);
+  return xcd_groups_on() && xgrp_fits(UB, BT, num_dirs);
 }
 
 bool launch_gru_fwd_x6(int t_max, int n, int h, int num_dirs, const float* xproj,

@@ -388,7 +388,13 @@ __global__ __launch_bounds__(GT) void lstm_fwd_persist_kernel(
 // persistent backward: W_hh^T fragments for NCH chunks of 4*GW*KSWC gate columns in
 // registers; dc carried in a register; gate gradients handed off through sc1 stores.
 // BTS as in the forward (BTS = 2 stages 32 rows per chunk: KSWC = 32 keeps them in LDS).
-template <int KSWC, int NCH, int BTS>
+// XG: the same-XCD group placement of the GRU backward (rnn_common.h map_work_xgrp), each
+// (direction, batch tile) group on its own 8 / G XCDs, same hand-off; bit-identical results.
+// cfg4 bf16 145.8 -> 144.9 ms per step (the forward's too: 143.7).  Measured and not kept on top of it: the GRU's
+// plain same-XCD copies (a two-slot ring stored write-through and plainly, consumers staging
+// the same-XCD producers' pieces from the plain copy): 150.5 ms, with dg's own stores moved
+// after the flag or not (profiles/r4zd_*).
+template <int KSWC, int NCH, int BTS, bool XG>
 __global__ __launch_bounds__(GT) void lstm_bwd_persist_kernel(
     int T, int N, int H, int D, int UB, int BT, const float* __restrict__ dy, int dyd,
     const float* __restrict__ wpt, const float* __restrict__ c_all,
@@ -401,7 +407,7 @@ __global__ __launch_bounds__(GT) void lstm_bwd_persist_kernel(
   float* red = hs;                          // reduction buffer aliases the staged rows
   __shared__ int flag;
   int ub, d, bt;
-  if (!map_work(UB * D, BT, UB, ub, d, bt)) return;
+  if (XG ? !map_work_xgrp(UB, BT, D, ub, d, bt) : !map_work(UB * D, BT, UB, ub, d, bt)) return;
   const int n0 = n_base + bt * RB;     // samples [n_base, ...) of a batch chunk
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -535,14 +541,15 @@ __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     const float* __restrict__ w_f, const float* __restrict__ w_r, const float* __restrict__ b_f,
     const float* __restrict__ b_r, const int* __restrict__ lens, float* __restrict__ h_all,
     float* __restrict__ c_all, float* __restrict__ gates, float* __restrict__ hx,
-    unsigned* __restrict__ counters, unsigned* __restrict__ err, int n_base) {
+    unsigned* __restrict__ counters, unsigned* __restrict__ err, int n_base, int xg) {
   constexpr int RB = GB * BTS;
   __shared__ float red[GW * RB * LRP];
   __shared__ __attribute__((aligned(16))) float tile[RB * GU];
   __shared__ int flag;
   __shared__ int failed;
   int ub, d, bt;
-  if (!map_work(UB * D, BT, UB, ub, d, bt)) return;
+  // xg: the same-XCD group placement (as lstm_bwd_persist_kernel's XG), same hand-off
+  if (xg ? !map_work_xgrp(UB, BT, D, ub, d, bt) : !map_work(UB * D, BT, UB, ub, d, bt)) return;
   const int n0 = n_base + bt * RB;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -853,10 +860,13 @@ ds2_status_t ds2_lstm_fwd(int t_max, int n, int h, int num_dirs, const float* xp
         return launch_status("ds2_lstm counters");
       if (hm != 0 && hipMemsetAsync(ring, 0xFF, lstm_ring_bytes(n, h, num_dirs), st) != hipSuccess)
         return launch_status("ds2_lstm ring");
+      // same-XCD groups (DS2_GRU_XCD) where they tile the XCDs: cfg4 bf16 144.9 -> 143.7 ms
+      int XG_ = xcd_groups_on() && xgrp_fits(UB, BT_, num_dirs) ? 1 : 0;
       void* args[] = {&T_, &N_, &H_, &D_, &UB_, &BT_, &xproj, &w_hh_f, &w_hh_r, &b_hh_f,
-                      &b_hh_r, &lens, &h_all, &c_all, &gates, &ring, &ctrs, &err, &NB_};
-      ok = rnn_launch(fn, dim3(mapped_grid(UB * num_dirs, BT_)), dim3(GT), args,
-                                      kLstmDopPadLds, st) == hipSuccess;
+                      &b_hh_r, &lens, &h_all, &c_all, &gates, &ring, &ctrs, &err, &NB_, &XG_};
+      ok = rnn_launch(fn,
+                      dim3(XG_ ? xgrp_grid(UB, BT_, num_dirs) : mapped_grid(UB * num_dirs, BT_)),
+                      dim3(GT), args, kLstmDopPadLds, st) == hipSuccess;
       if (ok) fold_err(err, err_out, st);
       if (!ok && launched) return launch_status("ds2_lstm_fwd chunk");
       launched = launched || ok;
@@ -984,10 +994,13 @@ ds2_status_t ds2_lstm_bwd(int t_max, int n, int h, int num_dirs, const float* dy
       kswc = 32;
       nch = (4 * h + 4 * GW * 32 - 1) / (4 * GW * 32);
     }
-    const void* fn = nullptr;
-#define DS2_LBP(K, C, B)                                                   \
-  if (kswc == K && nch == C && bts == B)                                   \
-    fn = reinterpret_cast<const void*>(lstm_bwd_persist_kernel<K, C, B>);
+    const void* fn = nullptr;    // the interleaved layout
+    const void* fx = nullptr;    // the same-XCD groups
+#define DS2_LBP(K, C, B)                                                          \
+  if (kswc == K && nch == C && bts == B) {                                        \
+    fn = reinterpret_cast<const void*>(lstm_bwd_persist_kernel<K, C, B, false>);  \
+    fx = reinterpret_cast<const void*>(lstm_bwd_persist_kernel<K, C, B, true>);   \
+  }
     DS2_LBP(8, 1, 1) DS2_LBP(16, 1, 1) DS2_LBP(25, 1, 1) DS2_LBP(32, 1, 1) DS2_LBP(48, 1, 1)
     DS2_LBP(64, 1, 1) DS2_LBP(48, 2, 1) DS2_LBP(64, 2, 1)
     DS2_LBP(32, 1, 2) DS2_LBP(32, 2, 2)
@@ -1001,10 +1014,13 @@ ds2_status_t ds2_lstm_bwd(int t_max, int n, int h, int num_dirs, const float* dy
       unsigned* err = ctrs + num_dirs * BT_;
       if (hipMemsetAsync(ctrs, 0, lstm_counter_bytes(n, num_dirs), st) != hipSuccess)
         return launch_status("ds2_lstm counters");
+      // same-XCD groups (DS2_GRU_XCD, as the GRU backward's) where they tile the XCDs
+      const bool xm = xcd_groups_on() && xgrp_fits(UB, BT_, num_dirs);
       void* args[] = {&T_, &N_, &H_, &D_, &UB_, &BT_, &dy, &DYD_, &wpt, &c_all, &gates, &lens,
                       &dgates, &ctrs, &err, &NB_};
-      ok = rnn_launch(fn, dim3(mapped_grid(UB * num_dirs, BT_)), dim3(GT), args,
-                                      0, st) == hipSuccess;
+      ok = rnn_launch(xm ? fx : fn,
+                      dim3(xm ? xgrp_grid(UB, BT_, num_dirs) : mapped_grid(UB * num_dirs, BT_)),
+                      dim3(GT), args, 0, st) == hipSuccess;
       if (ok) fold_err(err, err_out, st);
       if (!ok && b0 > 0) return launch_status("ds2_lstm_bwd chunk");
     }

@@ -106,6 +106,11 @@ static inline bool xgrp_fits(int UB, int BT, int D) {
   return G >= 1 && G <= 8 && 8 % G == 0 && UB % (8 / G) == 0;
 }
 static inline int xgrp_grid(int UB, int BT, int D) { return 8 * (UB / (8 / (D * BT))); }
+// DS2_GRU_XCD=0 keeps map_work's interleaved layout for every persistent backward
+static inline bool xcd_groups_on() {
+  const char* xe = getenv("DS2_GRU_XCD");
+  return !(xe != nullptr && xe[0] == '0');
+}
 __device__ __forceinline__ bool map_work_xgrp(int UB, int BT, int D, int& ub, int& d, int& bt) {
   const int wg = blockIdx.x;
   const int xcd = wg & 7, slot = wg >> 3;

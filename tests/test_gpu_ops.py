@@ -638,6 +638,33 @@ def test_lstm_persistent_equals_per_step(dev, h, n, monkeypatch):
         _close(a, b, 1e-5, "lstm persistent vs per-step")
 
 
+@pytest.mark.parametrize("n,h,bidir", [(64, 1024, True), (21, 800, True), (16, 256, False),
+                                       (7, 48, False)])
+def test_lstm_xcd_groups_bit_identical(dev, n, h, bidir, monkeypatch):
+    """The persistent LSTM backward's same-XCD group placement (64 x 1024 bidirectional: the
+    cfg4 shape, two 2-tile chunks; 21 x 800 ragged rows; 16 x 256 unidirectional; 7 x 48 does
+    not tile the XCDs and keeps the interleaved layout): outputs and gradients bit-identical to
+    DS2_GRU_XCD=0."""
+    t, inp = 29, 40
+    lstm, lens, x, g = _lstm_case(n, t, inp, h, bidir, h + n)
+    weights = [p.detach().float() for p in lstm.parameters()]
+    x = x.float()
+    dy = torch.randn(t, n, h, generator=g)
+    outs = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("DS2_GRU_XCD", flag)
+        ws = [w.to(dev).requires_grad_(True) for w in weights]
+        xd = x.to(dev).requires_grad_(True)
+        y = ops.LSTMLayerFn.apply(xd, lens.to(dev), True, h, *ws)
+        y.backward(dy.to(dev))
+        torch.cuda.synchronize()
+        ops.check_rnn_status(dev)
+        outs.append([y.detach().cpu(), xd.grad.cpu()] + [w.grad.cpu() for w in ws])
+    for a, b in zip(*outs):
+        assert torch.isfinite(a).all()
+        assert torch.equal(a, b)
+
+
 # ---------------------------------------------------------------------------- Lookahead
 @pytest.mark.parametrize("t,n,h,context", [(37, 3, 20, 20), (7, 2, 33, 20), (50, 5, 130, 3),
                                            (1, 1, 1, 1)])
