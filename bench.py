@@ -115,7 +115,7 @@ class KernelProbe:
         return sum(ms) / len(ms), sum(self.flops) / len(self.flops), len(ms)
 
 
-PMC_SUMMARY = "r4w_pmc_traffic.csv"   # profiles/: PMC passes on the round-4 kernels
+PMC_SUMMARY = "r4zh_pmc_traffic.csv"   # profiles/: PMC passes on the round-4 final tree
 
 
 def pmc_traffic_per_launch(prefix="gemm", extra=("splitk_reduce_kernel",)):
