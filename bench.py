@@ -405,6 +405,13 @@ def main():
                    "bucket_mb": [round((e - s) * 4 / 2**20, 2) for s, e, _ in tr.reducer.buckets],
                    "issued_from_hooks": tr.reducer.issued_from_hooks,
                    "guard_waits": tr.reducer.guard_waits,
+                   "collectives": tr.reducer.collectives,
+                   "issue_policy": tr.reducer.policy,
+                   "status_in_last_bucket": bool(tr.flat.tail.numel()),
+                   "traffic_standin": (None if tr.reducer.standin is None else
+                                       {"busbw_gbps": tr.reducer.standin.busbw,
+                                        "world": tr.reducer.standin.world,
+                                        "ctas": tr.reducer.standin.ctas}),
                    "rccl_cta_cap": tr.reducer.rccl_ctas,
                    "broadcasts": tr.sync.broadcasts,
                    "status_clean": True},

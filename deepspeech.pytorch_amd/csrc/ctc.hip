@@ -14,6 +14,7 @@
 // ballot/mbcnt compaction of the frames that survive blank/repeat removal
 // (ref decoder.py:165-197).
 #include "common.h"
+#include "../../include/ds2hip_test.h"
 
 namespace ds2 {
 
@@ -417,7 +418,7 @@ __device__ __forceinline__ int beam_select(const unsigned long long* ukey, int t
 // trie: dnext [S][C] arcs, dmask [S] the arcs as a char bit mask, dword [S] the word a
 // state spells (-1 none); state 0 = start, fstate = after a word's space (no arcs).
 struct BeamLm {
-  int nstates;   // dict_states: an arc outside [0, nstates) reads as no arc (-1)
+  int nstates;   // dict_states: an arc outside [0, nstates) leads to the post-space state (fstate)
   const int* dnext;
   const unsigned long long* dmask;
   const int* dword;

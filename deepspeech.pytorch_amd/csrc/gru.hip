@@ -1269,8 +1269,10 @@ int ds2_gru_bwd_grid(int n, int h, int num_dirs) {
   const int grid = mapped_grid(UB * num_dirs, BT);
   if (!persistent_enabled() || grid > num_cus()) return 0;
   if ((h % GU) == 0 && UB <= 8 * GW) {
+    // the x6 launch may decline at run time and fall back to the direct-operand kernel at
+    // `grid`: report the larger so the CU guard never budgets for fewer workgroups than run
     const int g = gru_bwd_x6_grid(n, h, num_dirs);
-    return g > 0 ? g : grid;
+    return g > grid ? g : grid;
   }
   return (3 * h <= KC_BWD && (h % 4) == 0) ? grid : 0;
 }

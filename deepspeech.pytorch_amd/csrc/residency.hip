@@ -9,11 +9,15 @@
 //                          max_us (bounded: every wave exits by itself), recording
 //                          [start, end, xcc id, hw id] per workgroup;
 //   ds2_test_timestamp  -- one s_memrealtime stamp on a stream (orders kernels on it);
+//   ds2_test_ring_traffic -- a ring all-reduce's local HBM traffic (read-only on the bucket),
+//                          paced at a bus bandwidth, on `ctas` CUs: the interference of a
+//                          bucket all-reduce with the recurrences, measured on one GPU;
 //   ds2_test_rnn_launch_lds -- the same occupier with 94 KB of STATIC LDS launched through
 //                          rnn_launch with the recurrences' 80 KB pad: the clamp that fixed round
 //                          3's dispatch fault (static + pad over the 160 KB per workgroup) must
 //                          shrink the pad so the launch runs.
 #include "rnn_common.h"
+#include "../../include/ds2hip_test.h"
 
 namespace ds2 {
 
@@ -51,6 +55,36 @@ __global__ __launch_bounds__(64) void occupy_static_kernel(int max_us, unsigned 
   occupy_body(max_us, rec, vb[63 * 367] != 63.f);
 }
 
+// A ring all-reduce's local HBM traffic on ONE GPU (ds2_test_ring_traffic): the
+// 2 (W - 1) phases over W ranks each read one S / W chunk of the bucket and the scratch chunk
+// a peer would have landed here, and write the reduced chunk back to scratch (what is sent
+// on).  Phase p starts no earlier than p * phase_ticks after the workgroup's start (the link
+// pace; 0 = as fast as the CTAs go).  The bucket is only read.
+__global__ __launch_bounds__(256) void ring_traffic_kernel(const float4* __restrict__ bucket,
+                                                           int64_t count4, int world,
+                                                           float4* __restrict__ scratch,
+                                                           int64_t chunk4, long long phase_ticks) {
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  const int phases = 2 * (world - 1);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int p = 0; p < phases; ++p) {
+    if (phase_ticks > 0) {
+      const unsigned long long due = t0 + (unsigned long long)p * phase_ticks;
+      // bounded: at most 2^20 sleeps (~80 ms) per phase whatever the clock says
+      for (int i = 0; i < (1 << 20) && __builtin_amdgcn_s_memrealtime() < due; ++i)
+        __builtin_amdgcn_s_sleep(8);
+    }
+    const int64_t base = (int64_t)(p % world) * chunk4;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < chunk4; i += stride) {
+      const int64_t j = base + i;
+      const float4 a = j < count4 ? bucket[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+      float4 b = scratch[i];
+      b.x += a.x; b.y += a.y; b.z += a.z; b.w += a.w;
+      scratch[i] = b;
+    }
+  }
+}
+
 __global__ void timestamp_kernel(unsigned long long* out) {
   if (threadIdx.x == 0) *out = __builtin_amdgcn_s_memrealtime();
 }
@@ -82,6 +116,24 @@ ds2_status_t ds2_test_rnn_launch_lds(int ctas, int max_us, unsigned long long* r
                  80 * 1024, as_stream(stream)) != hipSuccess)
     return launch_status("ds2_test_rnn_launch_lds");
   return launch_status("ds2_test_rnn_launch_lds");
+}
+
+ds2_status_t ds2_test_ring_traffic(const float* bucket, int64_t count, int world, float* scratch,
+                                   int ctas, double busbw_gbps, ds2_stream_t stream) {
+  if (bucket == nullptr || scratch == nullptr || count < 0 || world < 2 || world > 64 ||
+      ctas < 1 || ctas > 1024 || busbw_gbps < 0 || (reinterpret_cast<uintptr_t>(bucket) & 15) ||
+      (reinterpret_cast<uintptr_t>(scratch) & 15))
+    return DS2_INVALID_VALUE;
+  if (count == 0) return DS2_OK;
+  const int64_t count4 = count / 4;                       // a partial float4 is not streamed
+  const int64_t chunk4 = (count4 + world - 1) / world;
+  // one phase moves chunk bytes over the link: (S / W) / busbw seconds, 100 MHz ticks
+  const long long ticks =
+      busbw_gbps > 0 ? (long long)((double)chunk4 * 16.0 / (busbw_gbps * 1e9) * 1e8) : 0;
+  hipLaunchKernelGGL(ring_traffic_kernel, dim3(ctas), dim3(256), 0, as_stream(stream),
+                     reinterpret_cast<const float4*>(bucket), count4, world,
+                     reinterpret_cast<float4*>(scratch), chunk4, ticks);
+  return launch_status("ds2_test_ring_traffic");
 }
 
 ds2_status_t ds2_test_timestamp(unsigned long long* out, ds2_stream_t stream) {

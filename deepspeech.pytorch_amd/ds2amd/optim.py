@@ -31,11 +31,14 @@ class FlatParams:
 
     ALIGN = 64  # elements; keeps every view 256-byte aligned
 
-    def __init__(self, params: List[torch.nn.Parameter], device, adjacent=()):
+    def __init__(self, params: List[torch.nn.Parameter], device, adjacent=(), tail: int = 0):
         """adjacent: (first, second) parameter pairs laid out back to back (first, then
         second, no padding between when first fills whole 64-element blocks) -- a
         bidirectional recurrent layer's W_ih of both directions, so its input projection,
-        dX and dW_ih GEMMs run as one GEMM over both directions (ops._stacked_rows)."""
+        dX and dW_ih GEMMs run as one GEMM over both directions (ops._stacked_rows).
+        tail: extra fp32 slots after the last parameter's gradient (``self.tail``), outside
+        ``numel`` (no norm, clip or update touches them): the step's status word and loss ride
+        in the last all-reduce bucket there (GradAllReducer, status_slots)."""
         params = [p for p in params if p.requires_grad]
         self.model_params = params                 # model.parameters() order
         order = list(reversed(params))             # backward-completion order
@@ -63,8 +66,10 @@ class FlatParams:
         self.numel = total
         self.offsets = offs
         self.offset_of = {id(p): o for p, o in zip(self.params, offs)}
+        self.tail_alloc = (tail + self.ALIGN - 1) // self.ALIGN * self.ALIGN
         self.flat = torch.zeros(total, dtype=torch.float32, device=device)
-        self.grad = torch.zeros(total, dtype=torch.float32, device=device)
+        self.grad = torch.zeros(total + self.tail_alloc, dtype=torch.float32, device=device)
+        self.tail = self.grad[total:total + tail]
         for p, o in zip(self.params, offs):
             n = p.numel()
             self.flat[o:o + n].copy_(p.data.reshape(-1))
@@ -256,16 +261,27 @@ class ParamBroadcaster:
             self.broadcasts += 1
 
 
+UNKNOWN_CTAS = 1 << 30
+_warned_uncapped = [False]
+
+
 def rccl_channel_cap() -> int:
     """The CTA budget RCCL may hold while a persistent recurrence runs:
     NCCL_MAX_NCHANNELS, which init_distributed() sets to 32 before the communicator exists.
-    Unset (a process group created elsewhere: RCCL then picks its own channel count) the
-    budget is the conservative 64, so the guard waits rather than trusting a count nobody
-    capped."""
+    Unset or unreadable (a process group created elsewhere: RCCL then picks its own channel
+    count, which nothing here can read back) the budget is unknown: ``UNKNOWN_CTAS``, so the
+    guard always waits for the buckets in flight before a persistent recurrence,
+    and a warning says so once."""
     try:
         return int(os.environ["NCCL_MAX_NCHANNELS"])
     except (KeyError, ValueError):
-        return 64
+        if not _warned_uncapped[0]:
+            _warned_uncapped[0] = True
+            import warnings
+            warnings.warn("NCCL_MAX_NCHANNELS is not set: RCCL's CTA count is unknown, so every "
+                          "persistent recurrence waits for the all-reduces in flight "
+                          "(ds2amd.trainer.init_distributed caps it at 32)")
+        return UNKNOWN_CTAS
 
 
 def global_status_word(word: torch.Tensor, group=None) -> torch.Tensor:
@@ -335,6 +351,63 @@ class RcclComm:
             self.handle = ctypes.c_void_p()
 
 
+class _Both:
+    """Two in-flight handles waited as one (the all-reduce and its traffic stand-in)."""
+
+    def __init__(self, a, b):
+        self.a, self.b = a, b
+
+    def wait(self):
+        self.a.wait()
+        self.b.wait()
+
+
+class _Waited:
+    """A handle the compute stream already waited for (the 'gap' policy): later waits on it
+    cost nothing and are not counted again."""
+
+    def __init__(self, h):
+        self.h = h
+
+    def wait(self):
+        pass
+
+
+class RingTrafficStandIn:
+    """One-GPU stand-in for a ring all-reduce's local HBM traffic (DS2_AR_STANDIN=busbw_GBps
+    [,world]): for a bucket of S bytes, ``ds2_test_ring_traffic`` runs the
+    2 (W - 1) ring phases of an all-reduce over W ranks on a side stream, each phase reading
+    an S / W chunk of the bucket and a chunk of scratch and writing the scratch chunk (the
+    received data a peer lands in this GPU's HBM, reduced and passed on), paced so a phase
+    lasts (S / W) / busbw, on ``ctas`` CUs (RCCL's channel cap).  The gradients are only read:
+    results stay bit-identical.  Measurement only -- never on by default."""
+
+    def __init__(self, spec: str, device, ctas: int = 32):
+        parts = spec.split(",")
+        self.busbw = float(parts[0])
+        self.world = int(parts[1]) if len(parts) > 1 else 8
+        self.ctas = ctas
+        self.device = device
+        self.stream = torch.cuda.Stream(device)
+        self.scratch = None
+        self.launches = 0
+
+    def run(self, bucket: torch.Tensor):
+        count = bucket.numel()
+        chunk = (count + self.world - 1) // self.world
+        if self.scratch is None or self.scratch.numel() < chunk:
+            self.scratch = torch.zeros(chunk, dtype=torch.float32, device=self.device)
+        ready = torch.cuda.Event()
+        ready.record()
+        self.stream.wait_event(ready)
+        _lib.call("ds2_test_ring_traffic", bucket.data_ptr(), count, self.world,
+                  self.scratch.data_ptr(), self.ctas, float(self.busbw), self.stream.cuda_stream)
+        self.launches += 1
+        done = torch.cuda.Event()
+        done.record(self.stream)
+        return _StreamDone(done)
+
+
 class GradAllReducer:
     """Bucketed gradient all-reduce (SUM, then /world) overlapped with backward.
 
@@ -358,11 +431,22 @@ class GradAllReducer:
     """
 
     def __init__(self, flat: FlatParams, bucket_mb: float = 40.0, group=None,
-                 comm: Optional[RcclComm] = None, collective_ctas: Optional[int] = None):
+                 comm: Optional[RcclComm] = None, collective_ctas: Optional[int] = None,
+                 policy: Optional[str] = None):
+        """policy: when a bucket's all-reduce may run beside a persistent recurrence --
+        'overlap' (default): issued the moment the bucket is complete, running beside
+        whatever the backward does next; 'gap': each backward recurrence first waits for
+        the all-reduces in flight (DS2_AR_POLICY; DESIGN.md §6 has the measured A/B).
+        The last bucket also carries ``flat.tail`` (the status word and the loss, packed by
+        the function given to ``set_status_packer``) when the flat buffer has one, so a step
+        issues one series of collectives, not three."""
         self.flat = flat
         self.group = group
         self.comm = comm     # None: torch.distributed; else ds2_allreduce_bucket
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.policy = policy or os.environ.get("DS2_AR_POLICY", "overlap")
+        if self.policy not in ("overlap", "gap"):
+            raise ValueError(f"DS2_AR_POLICY must be 'overlap' or 'gap', got {self.policy!r}")
         cap = int(bucket_mb * 1024 * 1024 / 4)
         self.buckets = []          # (start, end, n_params) element ranges
         self.param_bucket = {}
@@ -373,11 +457,14 @@ class GradAllReducer:
             members.append(p)
             nxt = plist[i + 1][1] if i + 1 < len(plist) else flat.numel
             if nxt - start >= cap or i + 1 == len(plist):
+                if i + 1 == len(plist):
+                    nxt = flat.numel + flat.tail_alloc     # the status tail rides along
                 self._close(start, nxt, members)
                 start, members = nxt, []
         self.pending = [0] * len(self.buckets)
         self.handles = [None] * len(self.buckets)
         self.issued_from_hooks = 0
+        self.collectives = 0       # collectives issued in the last step
         self.guard_waits = 0
         self.cus = 0
         if flat.flat.is_cuda:
@@ -386,6 +473,9 @@ class GradAllReducer:
             collective_ctas = rccl_channel_cap() if self.world > 1 else 0
         self.rccl_ctas = int(collective_ctas)
         self.extra = []            # in-flight work registered by track()
+        self._pack = None
+        self._packed = False
+        self.standin = None        # RingTrafficStandIn (DS2_AR_STANDIN), one-GPU measurements
         self._hooks = []
         # hooks whenever a process group exists (world 1 included: that exercises the
         # RCCL path on a single-GPU box; the all-reduce is then a no-op copy)
@@ -399,10 +489,19 @@ class GradAllReducer:
         for p in members:
             self.param_bucket[id(p)] = b
 
+    def set_status_packer(self, fn) -> None:
+        """fn(tail) writes this step's status slots into ``flat.tail`` on the current stream;
+        called right before the last bucket's all-reduce is issued (by then every recurrence
+        of the backward has been enqueued: the last bucket holds the conv block's
+        parameters, whose gradients come last)."""
+        self._pack = fn
+
     def begin(self):
         self.pending = [b[2] for b in self.buckets]
         self.handles = [None] * len(self.buckets)
         self.issued_from_hooks = 0
+        self.collectives = 0
+        self._packed = False
         self.extra = []
 
     def track(self, handle):
@@ -415,9 +514,20 @@ class GradAllReducer:
         b = self.param_bucket[id(p)]
         self.pending[b] -= 1
         if self.pending[b] == 0:
-            s, e, _ = self.buckets[b]
-            self.handles[b] = self._all_reduce(self.flat.grad[s:e])
+            self.handles[b] = self._issue(b)
             self.issued_from_hooks += 1
+
+    def _issue(self, b):
+        s, e, _ = self.buckets[b]
+        if b == len(self.buckets) - 1 and self._pack is not None and not self._packed:
+            self._pack(self.flat.tail)
+            self._packed = True
+        self.collectives += 1
+        bucket = self.flat.grad[s:e]
+        h = self._all_reduce(bucket)
+        if self.standin is not None:
+            h = _Both(h, self.standin.run(bucket))
+        return h
 
     def _all_reduce(self, bucket):
         if self.comm is not None:
@@ -425,14 +535,17 @@ class GradAllReducer:
         return dist.all_reduce(bucket, group=self.group, async_op=True)
 
     def guard_cooperative(self, grid: int):
-        if self.cus <= 0 or self.rccl_ctas <= 0:
-            return
-        if min(grid, self.cus) + self.rccl_ctas <= self.cus:
-            return
-        for h in list(self.handles) + self.extra:
+        if self.policy != "gap":
+            if self.cus <= 0 or self.rccl_ctas <= 0:
+                return
+            if min(grid, self.cus) + self.rccl_ctas <= self.cus:
+                return
+        for i, h in enumerate(list(self.handles) + self.extra):
             if h is not None:
                 h.wait()
                 self.guard_waits += 1
+                if i < len(self.handles):
+                    self.handles[i] = _Waited(h)
 
     def finish(self):
         if not self._hooks:
@@ -440,8 +553,7 @@ class GradAllReducer:
         self.flat.finalize_grads()   # zero the slices no gradient was written to
         for b, h in enumerate(self.handles):
             if h is None:     # a bucket whose params received no gradient this step
-                s, e, _ = self.buckets[b]
-                h = self._all_reduce(self.flat.grad[s:e])
+                h = self._issue(b)
             h.wait()
         if self.world > 1:
             self.flat.grad.mul_(1.0 / self.world)

@@ -28,8 +28,7 @@ from . import _lib, ops
 from .ctc import CTCLoss
 from .decoder import GreedyDecoder
 from .ops import _stream
-from .optim import (FlatParams, FusedSGD, GradAllReducer, ParamBroadcaster, RcclComm,
-                    global_status_word)
+from .optim import FlatParams, FusedSGD, GradAllReducer, ParamBroadcaster, RcclComm
 
 
 def reduce_tensor(tensor, world_size):
@@ -107,7 +106,10 @@ class Trainer:
         # per layer for the input projection, dX and dW_ih (ops._stacked_rows)
         pairs = [(m.weight_ih_l0, m.weight_ih_l0_reverse) for m in self.model.modules()
                  if hasattr(m, 'weight_ih_l0_reverse')]
-        self.flat = FlatParams(list(self.model.parameters()), self.device, adjacent=pairs)
+        # two tail slots after the gradients: (status word, loss), all-reduced with the last
+        # bucket (GradAllReducer.set_status_packer) instead of two collectives of their own
+        self.flat = FlatParams(list(self.model.parameters()), self.device, adjacent=pairs,
+                               tail=2 if dist.is_initialized() else 0)
         self.optimizer = FusedSGD(self.flat, lr=lr, momentum=momentum, max_norm=max_norm)
         # DS2_ALLREDUCE=ds2: the buckets go through the library's own RCCL communicator
         # (ds2_comm_init / ds2_allreduce_bucket) instead of torch.distributed's
@@ -117,6 +119,14 @@ class Trainer:
             comm = RcclComm(group, self.device)
         self.reducer = GradAllReducer(self.flat, bucket_mb=bucket_mb, group=group, comm=comm)
         self.world = self.reducer.world
+        if dist.is_initialized():
+            self.reducer.set_status_packer(self._pack_status)
+            spec = os.environ.get("DS2_AR_STANDIN")
+            if spec and self.device.type == "cuda":
+                from .optim import RingTrafficStandIn
+                self.reducer.standin = RingTrafficStandIn(spec, self.device,
+                                                          ctas=self.reducer.rccl_ctas or 32)
+        self._step_loss = None
         # DDP: rank 0's parameters and buffers everywhere (construction), rank 0's BN running
         # statistics before every forward (broadcast_buffers, train.py:950-951)
         self.sync = ParamBroadcaster(self.model, self.flat, group=group,
@@ -137,12 +147,12 @@ class Trainer:
         # the step ends
         self._side = torch.cuda.Stream(device=self.device) if self.device.type == 'cuda' else None
         self._rnn_word = ops.rnn_status_word(self.device)
-        # pinned ring of (nan flag, rnn status, loss bits) per in-flight step
-        self._ring = [torch.zeros(3, dtype=torch.int32).pin_memory()
+        # pinned ring of (nan flag, rnn status, loss bits, global status bits) per in-flight step
+        self._ring = [torch.zeros(4, dtype=torch.int32).pin_memory()
                       for _ in range(self.STATUS_RING)]
         self._ring_next = 0
         self._inflight = deque()
-        self._status = torch.zeros(3, dtype=torch.int32, device=self.device)
+        self._status = torch.zeros(4, dtype=torch.int32, device=self.device)
         self.warnings = {"nan": 0, "inf_loss": 0}
 
     # train.py:584-587 running sums, read lazily (one device->host copy)
@@ -163,12 +173,23 @@ class Trainer:
         return float(self._score_acc[3])
 
     # ---- deferred status --------------------------------------------------------------
-    def _record_status(self, loss):
-        """Stage (nan flag, recurrence status, loss bits) of this step for the host."""
+    def _pack_status(self, tail):
+        """The last bucket's tail slots (GradAllReducer.set_status_packer): this rank's
+        recurrence status word (as a float: summed over the ranks it is non-zero iff any
+        rank's word is) and its loss (summed, then scaled by 1/world with the gradients:
+        reduce_tensor, data/utils.py:40-44)."""
+        tail[0:1].copy_(self._rnn_word)
+        tail[1:2].copy_(self._step_loss)
+
+    def _record_status(self, loss, global_word=None):
+        """Stage (nan flag, recurrence status, loss bits, global status bits) of this step
+        for the host."""
         st = self._status
         st[0:1].copy_(self.nan_flag)
         st[1:2].copy_(self._rnn_word)
         st[2:3].copy_(loss.detach().reshape(1).view(torch.int32))
+        if global_word is not None:
+            st[3:4].copy_(global_word)
         if len(self._inflight) == self.STATUS_RING:
             self._drain_one(block=True)
         buf = self._ring[self._ring_next]
@@ -184,9 +205,12 @@ class Trainer:
             return False
         ev.synchronize()
         self._inflight.popleft()
-        nan, err, loss_bits = (int(v) for v in buf.tolist())
+        nan, err, loss_bits, global_bits = (int(v) for v in buf.tolist())
         loss = torch.tensor([loss_bits], dtype=torch.int32).view(torch.float32).item()
         msg = ops.rnn_status_error(err)
+        if msg is None and global_bits != 0:
+            msg = ("recurrence kernel failure on another rank (its NaN gradients were "
+                   "all-reduced; every rank skipped the update)")
         if msg is not None:
             self._rnn_word.zero_()
             raise _lib.Ds2Error(msg)
@@ -249,22 +273,28 @@ class Trainer:
 
         self.optimizer.zero_grad()
         self.reducer.begin()
+        self._step_loss = loss.detach().reshape(1)
         loss.backward()
         self.reducer.finish()
         # clip + SGD; always taken for NaN data (see module docstring).  Skipped on the device
         # when a persistent recurrence reported a hand-off failure this step: its outputs are
         # NaN and the update would write NaN into every parameter and momentum slot before the
-        # host sees the error (the word is 0 in a normal step; no host sync).  With several
-        # ranks the word is first made global (MAX over the ranks): the failing rank's NaN
-        # gradients are already in every rank's buckets, so all ranks skip and all raise.
-        if self.world > 1:
-            global_status_word(self._rnn_word, self.reducer.group)
-        self.optimizer.step(skip_flag=self._rnn_word)
+        # host sees the error (the word is 0 in a normal step; no host sync).  With a process
+        # group the decision is global: the status word rode in the last gradient bucket's
+        # tail, summed over the ranks (the failing rank's NaN gradients are already in every
+        # rank's buckets, so all ranks skip and all raise), and so did the loss (reduce_tensor,
+        # data/utils.py:40-44): one series of collectives per step.  A non-zero float sum has
+        # non-zero bits, so the kernel reads the slot as its int skip flag.
+        global_word = None
+        if self.flat.tail.numel():
+            global_word = self.flat.tail[0:1].view(torch.int32)
+            self.optimizer.step(skip_flag=global_word)
+            loss = self.flat.tail[1:2].clone().reshape(())
+        else:
+            self.optimizer.step(skip_flag=self._rnn_word)
         if side is not None:
             torch.cuda.current_stream(self.device).wait_stream(side)
-        if self.world > 1:
-            loss = reduce_tensor(loss.detach(), self.world)
-        self._record_status(loss)
+        self._record_status(loss, global_word)
         if return_item:
             self.poll_status(block=True)
             v = float(loss.item())

@@ -217,9 +217,7 @@ ds2_status_t ds2_bn_backward(const float* dy, int dy_layout, const float* x, int
  *   xproj : [T][N][D][3H]  x @ W_ih^T + b_ih for each direction
  *   h_all : [T][N][D][H]   per-direction hidden states (output)
  *   gates : the backward cache, or NULL: ds2_gru_cache_floats(T, N, H, D) floats =
- *           [T][N][D][4H] (r, z, n, W_hn h + b_hn), then the backward's coefficient tiles
- *           (c_r, c_z, c_hn in hand-off tile order, csrc/rnn_common.h) that let the backward
- *           recurrence exchange dh instead of the 3H gate gradients (csrc/gru_bwd_dh.hip)
+ *           [T][N][D][4H] (r, z, n, W_hn h + b_hn)
  * num_dirs = 1 or 2; w_hh_r / b_hh_r ignored when num_dirs == 1.
  * err_out: NULL, or a caller-owned device status word; the persistent
  * (one-launch-per-layer) kernels OR their hand-off status into it after the
@@ -240,16 +238,17 @@ size_t ds2_gru_bwd_workspace_size(int n, int h, int num_dirs);
  * (model.py:107), dy_dirs = num_dirs: per-direction output gradient.
  * dgates_x: [T][N][D][3H] grad wrt xproj;  dgates_h: [T][N][D][3H] grad wrt
  * W_hh h + b_hh.  Weight gradients are then plain GEMMs (see ds2amd/ops.py). */
-/* Workgroups the persistent backward recurrence holds at once for this shape (one per
- * CU, all resident together: they spin on each other's hand-offs), 0 when the shape runs
- * the per-step kernels.  What a concurrent collective must leave free (DESIGN.md §6;
- * optim.GradAllReducer.guard_cooperative).                                     */
-int ds2_gru_bwd_grid(int n, int h, int num_dirs);
-int ds2_lstm_bwd_grid(int n, int h, int num_dirs);
 ds2_status_t ds2_gru_bwd(int t_max, int n, int h, int num_dirs, const float* dy, int dy_dirs,
                          const float* w_hh_f, const float* w_hh_r, const float* h_all,
                          const float* gates, const int* lens, float* dgates_x, float* dgates_h,
                          unsigned* err_out, void* ws, size_t ws_bytes, ds2_stream_t stream);
+/* Workgroups the persistent backward recurrence holds at once for this shape (one per
+ * CU, all resident together: they spin on each other's hand-offs; an upper bound when the
+ * launch may fall back to another persistent kernel), 0 when the shape runs the per-step
+ * kernels.  What a concurrent collective must leave free (DESIGN.md §6;
+ * optim.GradAllReducer.guard_cooperative).                                     */
+int ds2_gru_bwd_grid(int n, int h, int num_dirs);
+int ds2_lstm_bwd_grid(int n, int h, int num_dirs);
 /* ds2_gru_bwd plus the bias gradients of the layer (replaces the column sums of the
  * reference's autograd over bias_ih_l* / bias_hh_l*, nn.GRU via model.py:97-109):
  * db_ih_{f,r} [3H] = sum over rows of dgates_x, db_hh_{f,r} [3H] = sum over rows of
@@ -421,25 +420,6 @@ ds2_status_t ds2_rnn_fwd(int t_max, int n, int h, int num_dirs, const float* xpr
 ds2_status_t ds2_rnn_bwd(int t_max, int n, int h, int num_dirs, const float* dy, int dy_dirs,
                          const float* w_hh_f, const float* w_hh_r, const float* h_all,
                          const int* lens, float* dgates, ds2_stream_t stream);
-
-/* ------------------------------------------------------------------------ */
-/* Residency test hooks (csrc/residency.hip; not on the training path).  ds2_test_occupy:
- * `ctas` one-wave workgroups with lds_kb KB of dynamic LDS each (> 80: alone on their CU,
- * no recurrence workgroup fits beside), each spinning for max_us microseconds on the
- * device clock, recording rec[4*i..4*i+3] = {start, end (s_memrealtime, 100 MHz),
- * XCC id, HW_ID}.  ds2_test_rnn_launch_lds: the same with 94 KB of static LDS launched
- * through the recurrences' launcher and its 80 KB pad (the pad must be clamped to fit).
- * ds2_test_timestamp: *out = s_memrealtime when the stream reaches it.         */
-ds2_status_t ds2_test_occupy(int ctas, int lds_kb, int max_us, unsigned long long* rec,
-                             ds2_stream_t stream);
-ds2_status_t ds2_test_rnn_launch_lds(int ctas, int max_us, unsigned long long* rec,
-                                     ds2_stream_t stream);
-ds2_status_t ds2_test_timestamp(unsigned long long* out, ds2_stream_t stream);
-
-/* ds2_test_beam_stamps: test hook; every later beam decode writes per-phase clock stamps of
- * utterance 0's first 256 frames into buf ([256][9] uint64: s_memtime at the 8 phase
- * boundaries of a frame, then s_memrealtime at its start); buf = NULL turns it off.       */
-ds2_status_t ds2_test_beam_stamps(unsigned long long* buf);
 
 /* ------------------------------------------------------------------------ */
 /* Data-parallel gradient exchange over RCCL (SURVEY §8b allreduce_bucket /

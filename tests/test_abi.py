@@ -13,12 +13,23 @@ from ds2amd import _lib
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(REPO, "include", "ds2hip.h")
+TEST_HEADER = os.path.join(REPO, "include", "ds2hip_test.h")   # test hooks, not product ABI
 
 
-def declared_symbols():
-    text = open(HEADER).read()
-    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-    return sorted(set(re.findall(r"\b(ds2_[a-z0-9_]+)\s*\(", text)))
+def _header_text(path):
+    return re.sub(r"/\*.*?\*/", "", open(path).read(), flags=re.S)
+
+
+def declared_symbols(paths=(HEADER, TEST_HEADER)):
+    return sorted({s for p in paths
+                   for s in re.findall(r"\b(ds2_[a-z0-9_]+)\s*\(", _header_text(p))})
+
+
+def test_product_header_has_no_test_hooks():
+    """ds2_test_* entry points live in ds2hip_test.h only (VERDICT r4 housekeeping)."""
+    prod = declared_symbols((HEADER,))
+    assert not [s for s in prod if s.startswith("ds2_test_")]
+    assert all(s.startswith("ds2_test_") for s in declared_symbols((TEST_HEADER,)))
 
 
 def test_library_present():
@@ -65,7 +76,7 @@ def test_invalid_args_rejected_without_launch():
 
 def declared_arities():
     """{symbol: number of parameters} from the prototypes in ds2hip.h."""
-    text = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    text = _header_text(HEADER) + _header_text(TEST_HEADER)
     out = {}
     for m in re.finditer(r"\b(ds2_[a-z0-9_]+)\s*\(([^;{]*?)\)\s*;", text):
         args = m.group(2).strip()

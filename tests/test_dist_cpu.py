@@ -342,13 +342,74 @@ def test_skip_decision_is_global():
     assert res == [(0, 1), (1, 1)]
 
 
+def _fold_worker(rank, world, port, out_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    m = _model()
+    flat = FlatParams(list(m.parameters()), "cpu", tail=2)
+    red = GradAllReducer(flat, bucket_mb=0.0005)
+    word = torch.zeros(1, dtype=torch.int32)
+    state = {}
+
+    def pack(tail):
+        tail[0:1].copy_(word)
+        tail[1:2].copy_(state["loss"])
+
+    red.set_status_packer(pack)
+    x, y = _data()
+    xs, ys = x[rank::world], y[rank::world]
+    out = []
+    for step in range(2):
+        word.fill_(1 if (rank == 1 and step == 1) else 0)   # rank 1 fails in step 1
+        flat.zero_grad()
+        red.begin()
+        loss = ((m(xs) - ys) ** 2).sum(1).mean()
+        state["loss"] = loss.detach().reshape(1)
+        loss.backward()
+        red.finish()
+        skip = int(flat.tail[0:1].view(torch.int32).item())
+        out.append((float(loss), float(flat.tail[1]), skip, red.collectives, len(red.buckets),
+                    red.buckets[-1][1], flat.numel, flat.tail_alloc))
+    out_q.put((rank, out))
+    dist.destroy_process_group()
+
+
+def test_status_and_loss_ride_in_the_last_bucket():
+    """the step's status word and loss travel in the last gradient bucket's tail
+    (FlatParams(tail=2)), so a step issues exactly one collective per bucket -- no separate
+    MAX all-reduce of the status word, no reduce_tensor of the loss.  gloo world 2: the tail
+    holds the mean loss (data/utils.py:40-44), and a status word set on rank 1 alone makes the
+    skip flag non-zero on both ranks (every rank skips, every rank raises)."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_fold_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for step in range(2):
+        losses = [res[r][step][0] for r in range(world)]
+        for r in range(world):
+            loss, mean, skip, colls, nb, end, numel, tail_alloc = res[r][step]
+            assert colls == nb, "one collective per bucket, none for status or loss"
+            assert end == numel + tail_alloc, "the last bucket covers the tail"
+            assert mean == pytest.approx(sum(losses) / world, rel=1e-6)
+            assert (skip != 0) == (step == 1), (r, step, skip)
+
+
 def test_rccl_cap_defaults(monkeypatch):
     """The guard's CTA budget: NCCL_MAX_NCHANNELS when set (init_distributed sets 32 before the
-    communicator exists), the conservative 64 when nobody capped RCCL."""
-    from ds2amd.optim import rccl_channel_cap
+    communicator exists); unknown when nobody capped RCCL, so the guard always
+    waits for the buckets in flight."""
+    from ds2amd.optim import rccl_channel_cap, UNKNOWN_CTAS
     monkeypatch.delenv("NCCL_MAX_NCHANNELS", raising=False)
-    assert rccl_channel_cap() == 64
+    assert rccl_channel_cap() == UNKNOWN_CTAS
     monkeypatch.setenv("NCCL_MAX_NCHANNELS", "32")
     assert rccl_channel_cap() == 32
     monkeypatch.setenv("NCCL_MAX_NCHANNELS", "junk")
-    assert rccl_channel_cap() == 64
+    assert rccl_channel_cap() == UNKNOWN_CTAS
