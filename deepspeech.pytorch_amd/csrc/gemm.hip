@@ -756,11 +756,27 @@ __device__ __forceinline__ void x2_split2(float x0, float x1, unsigned& h, unsig
   l = __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2{l0, l1}, bf16x2));
 }
 
-// NPL 3: the hi / mid / lo planes; NPL 1: the bf16 (RNE) rounding alone (the bf16-operand GEMM)
+// NPL 3: the hi / mid / lo planes; NPL 1: the bf16 (RNE) rounding alone (the bf16-operand GEMM);
+// NPL 2: the fp16 two-term split of the scaled value x sc (sc = 2^e, the operand row's scale:
+// hi = f16(x sc), lo = f16(x sc - hi), RNE, the residual exact in fp32), two planes
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 template <int NPL = 3>
 __device__ __forceinline__ void x2_split_store(unsigned short* __restrict__ s, int plane, int at,
-                                               const float* v) {
-  if constexpr (NPL == 1) {
+                                               const float* v, float sc = 1.f) {
+  if constexpr (NPL == 2) {
+    u32x4v h, l;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const f32x2 x = f32x2{v[2 * j], v[2 * j + 1]} * sc;
+      const f16x2 hh = __builtin_convertvector(x, f16x2);
+      const f32x2 r = x - __builtin_convertvector(hh, f32x2);
+      h[j] = __builtin_bit_cast(unsigned, hh);
+      l[j] = __builtin_bit_cast(unsigned, __builtin_convertvector(r, f16x2));
+    }
+    *reinterpret_cast<u32x4v*>(s + at) = h;
+    *reinterpret_cast<u32x4v*>(s + plane + at) = l;
+  } else if constexpr (NPL == 1) {
     u32x4v h;
 #pragma unroll
     for (int j = 0; j < 4; ++j)
@@ -789,22 +805,25 @@ __device__ __forceinline__ void x2_split_store(unsigned short* __restrict__ s, i
   }
 }
 
+// sc: the scales of the thread's staging rows (NPL 2): k-contiguous unit u -> sc[u]; a
+// row-contiguous operand's thread row -> sc[0]
 template <bool KC, int ROWS, int NPL = 3, bool M16 = false>
 __device__ __forceinline__ void x2_store(unsigned short* __restrict__ s,
-                                         const float (&v)[X2Op<KC, ROWS>::F]) {
+                                         const float (&v)[X2Op<KC, ROWS>::F],
+                                         const float (&sc)[2] = {1.f, 1.f}) {
   using O = X2Op<KC, ROWS>;
   const int t = threadIdx.x;
   if (KC) {
 #pragma unroll
     for (int u = 0; u < O::SL; ++u) {
       const int unit = t + X2T * u;
-      x2_split_store<NPL>(s, O::P, xslot_t<M16>(unit >> 2, unit & 3), v + 8 * u);
+      x2_split_store<NPL>(s, O::P, xslot_t<M16>(unit >> 2, unit & 3), v + 8 * u, sc[u]);
     }
   } else {
     const int r = t % ROWS;
 #pragma unroll
     for (int u = 0; u < O::SL; ++u)
-      x2_split_store<NPL>(s, O::P, xslot_t<M16>(r, O::SL * (t / ROWS) + u), v + 8 * u);
+      x2_split_store<NPL>(s, O::P, xslot_t<M16>(r, O::SL * (t / ROWS) + u), v + 8 * u, sc[0]);
   }
 }
 
@@ -874,17 +893,30 @@ __device__ __forceinline__ void x2_load160(__amdgpu_buffer_rsrc_t rs, int ld, co
 }
 
 template <bool KC, int NPL = 3, bool M16 = false>
-__device__ __forceinline__ void x2_store160(unsigned short* __restrict__ s, const float (&v)[16]) {
+__device__ __forceinline__ void x2_store160(unsigned short* __restrict__ s, const float (&v)[16],
+                                            const float (&sc)[2] = {1.f, 1.f}) {
   constexpr int P = 160 * XS;
   const int t = threadIdx.x;
   if (KC) {
-    x2_split_store<NPL>(s, P, xslot_t<M16>(t >> 2, t & 3), v);
-    if (t < 128) x2_split_store<NPL>(s, P, xslot_t<M16>((t + X2T) >> 2, (t + X2T) & 3), v + 8);
+    x2_split_store<NPL>(s, P, xslot_t<M16>(t >> 2, t & 3), v, sc[0]);
+    if (t < 128) x2_split_store<NPL>(s, P, xslot_t<M16>((t + X2T) >> 2, (t + X2T) & 3), v + 8, sc[1]);
   } else {
-    x2_split_store<NPL>(s, P, xslot_t<M16>(t & 127, t >> 7), v);
-    if (t < 128) x2_split_store<NPL>(s, P, xslot_t<M16>(128 + (t & 31), (t >> 5) & 3), v + 8);
+    x2_split_store<NPL>(s, P, xslot_t<M16>(t & 127, t >> 7), v, sc[0]);
+    if (t < 128) x2_split_store<NPL>(s, P, xslot_t<M16>(128 + (t & 31), (t >> 5) & 3), v + 8, sc[1]);
   }
 }
+
+// fp16x3 row scales.  amax: the bit pattern of max |x| over a logical row (non-negative floats
+// order as unsigned).  The row is staged as x 2^e, e = 14 - floor(log2 amax), so its largest
+// element lies in [2^14, 2^15) (fp16 max 65504) and its fp16 (hi, lo) split keeps 22 bits for
+// every element within 2^17 of the row max; a zero, inf or NaN row max keeps e = 0.
+__device__ __forceinline__ int h3_exp(unsigned amax) {
+  const int E = (int)(amax >> 23);                 // biased exponent (sign bit is 0)
+  if (amax == 0u || E >= 255) return 0;
+  int e = 14 - ((E == 0 ? 1 : E) - 127);
+  return e > 127 ? 127 : e;                        // 2^e stays a normal float
+}
+__device__ __forceinline__ float h3_scale(int e) { return __builtin_bit_cast(float, (e + 127) << 23); }
 
 // NPL 3: the bf16x6 fp32-accurate GEMM; NPL 1: the bf16-operand GEMM (operands rounded to
 // bf16 while staged, one product per fragment pair, fp32 accumulation -- cfg4's opt-in
@@ -894,10 +926,12 @@ __global__ __launch_bounds__(X2T, 1) void sxgemm2_kernel(
     int M, int N, int K, float alpha, const float* __restrict__ A, int64_t lda, int64_t sA,
     const float* __restrict__ B, int64_t ldb, int64_t sB, float beta, float* __restrict__ C,
     int64_t ldc, int64_t sC, const float* __restrict__ bias, int main_wgs, int tail_tile0,
-    int tail_tiles, int nsplit, int kchunk, float* __restrict__ partial) {
+    int tail_tiles, int nsplit, int kchunk, float* __restrict__ partial,
+    const unsigned* __restrict__ a_amax, const unsigned* __restrict__ b_amax) {
   constexpr bool AK = (TA == 0);
   constexpr bool BKc = (TB == 1);
   static_assert(TBN == 128 || TBN == 160, "tile width");
+  static_assert(NPL != 2 || M16, "fp16x3: the 16x16x32 form");
   // waves: 4 (M) x 2 (N) of 2 x 2 32x32 tiles (TBN 128) or 8 (M) x 1 (N) of 1 x 5 (TBN 160);
   // M16: the same wave tiles as 4 x 4 / 2 x 10 16x16 tiles
   constexpr int TS = M16 ? 16 : 32;   // MFMA tile edge
@@ -964,6 +998,29 @@ __global__ __launch_bounds__(X2T, 1) void sxgemm2_kernel(
     }
   }
 
+  // fp16x3: the scale of each staging row (loop-invariant; NPL 3 / 1 ignore them)
+  float a_sc[2] = {1.f, 1.f}, b_sc[2] = {1.f, 1.f};
+  if constexpr (NPL == 2) {
+    auto sc_of = [](const unsigned* am, int r, int lim) {
+      return h3_scale(r < lim ? h3_exp(am[r]) : 0);
+    };
+    if (AK) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u) a_sc[u] = sc_of(a_amax, m0 + (t >> 2) + u * (X2T / 4), M);
+    } else {
+      a_sc[0] = sc_of(a_amax, m0 + (t % X2M), M);
+    }
+    if (TBN == 128) {
+      b_sc[0] = sc_of(b_amax, BKc ? n0 + (t >> 2) : n0 + (t % TBN), N);
+    } else if (BKc) {
+      b_sc[0] = sc_of(b_amax, n0 + (t >> 2), N);
+      b_sc[1] = sc_of(b_amax, n0 + ((t + X2T) >> 2), N);
+    } else {
+      b_sc[0] = sc_of(b_amax, n0 + (t & 127), N);
+      b_sc[1] = sc_of(b_amax, n0 + 128 + (t & 31), N);
+    }
+  }
+
   AccT acc[WMT][WNT];
 #pragma unroll
   for (int i = 0; i < WMT; ++i)
@@ -992,9 +1049,9 @@ __global__ __launch_bounds__(X2T, 1) void sxgemm2_kernel(
   };
   auto bstore = [&](unsigned short* dst, const float (&vb)[BF]) {
     if constexpr (TBN == 128)
-      x2_store<BKc, TBN, NPL, M16>(dst, vb);
+      x2_store<BKc, TBN, NPL, M16>(dst, vb, b_sc);
     else
-      x2_store160<BKc, NPL, M16>(dst, vb);
+      x2_store160<BKc, NPL, M16>(dst, vb, b_sc);
   };
   auto body = [&](int kt, int cur, float (&la)[OA::F], float (&lb)[BF],
                   const float (&sa)[OA::F], const float (&sb)[BF]) {
@@ -1007,8 +1064,51 @@ __global__ __launch_bounds__(X2T, 1) void sxgemm2_kernel(
     load(kbeg + (kt + 2) * XS, la, lb);          // stages past kend load as zeros
     const unsigned short* as = As[cur];
     const unsigned short* bs = Bs[cur];
-    if constexpr (M16) {
-      static_assert(NPL == 3, "M16: bf16x6 only");
+    if constexpr (M16 && NPL == 2) {
+      // fp16x3: two planes per operand, three v_mfma_f32_16x16x32_f16 per fragment pair
+      // (lo.hi + hi.lo + hi.hi; lo.lo, below 2^-22 |a b|, dropped), same wave tiles and the
+      // same interleave of the next stage's split and stores as the bf16x6 form below
+      const int r16 = lane & 15, s16 = lane >> 4;
+      f16x8 af[WMT][2];
+#pragma unroll
+      for (int i = 0; i < WMT; ++i) {
+        const int at = xslot_t<true>(wm + 16 * i + r16, s16);
+#pragma unroll
+        for (int p = 0; p < 2; ++p) af[i][p] = *reinterpret_cast<const f16x8*>(as + p * X2_AP + at);
+      }
+#pragma unroll
+      for (int j = 0; j < WNT; ++j) {
+        f16x8 bq[2];
+        const int bt = xslot_t<true>(wn + 16 * j + r16, s16);
+#pragma unroll
+        for (int p = 0; p < 2; ++p) bq[p] = *reinterpret_cast<const f16x8*>(bs + p * BP + bt);
+#pragma unroll
+        for (int i = 0; i < WMT; ++i) {
+          AccT c = acc[i][j];
+          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i][1], bq[0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i][0], bq[1], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i][0], bq[0], c, 0, 0, 0);
+          acc[i][j] = c;
+        }
+      }
+      x2_store<AK, X2M, NPL, true>(As[cur ^ 1], sa, a_sc);
+      bstore(Bs[cur ^ 1], sb);
+      constexpr int MPB = WMT * 3;   // MFMAs per B fragment
+      __builtin_amdgcn_sched_group_barrier(0x020, 32, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 2 * WMT + 4, 0);
+#pragma unroll
+      for (int j = 0; j < WNT; ++j) {
+#pragma unroll
+        for (int q = 0; q < MPB; ++q) {   // 2 VALU per MFMA
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+        }
+        if (j + 2 < WNT) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+        __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+      }
+      return;
+    } else if constexpr (M16) {
+      static_assert(NPL == 3, "M16: bf16x6 or fp16x3 only");
       // one k-step of 32 per stage: the A fragments, then per B fragment (its three planes
       // read two fragments ahead) the WMT x 6 MFMAs it feeds, with the split VALU of stage
       // kt + 1 and its LDS stores interleaved
@@ -1106,7 +1206,7 @@ __global__ __launch_bounds__(X2T, 1) void sxgemm2_kernel(
   };
   const int ktiles = (kend - kbeg + XS - 1) / XS;
   load(kbeg, ra0, rb0);
-  x2_store<AK, X2M, NPL, M16>(As[0], ra0);
+  x2_store<AK, X2M, NPL, M16>(As[0], ra0, a_sc);
   bstore(Bs[0], rb0);
   load(kbeg + XS, ra1, rb1);
   for (int kt = 0; kt < ktiles; kt += 2) {
@@ -1121,6 +1221,26 @@ __global__ __launch_bounds__(X2T, 1) void sxgemm2_kernel(
     // row segments instead of sixteen 64-B pieces
     constexpr int EW = WNT * 16, EP = EW + 4;
     static_assert(8 * 16 * EP * 4 <= 2 * NPL * X2_AP * 2, "epilogue staging fits the A stages");
+    if constexpr (NPL == 2) {
+      // undo the row scales: C = acc 2^-(e_a(row) - e_b(col)), exact unless the result
+      // itself under- or overflows
+#pragma unroll
+      for (int i = 0; i < WMT; ++i) {
+        int ea[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = m0 + wm + 16 * i + 4 * (lane >> 4) + r;
+          ea[r] = row < M ? h3_exp(a_amax[row]) : 0;
+        }
+#pragma unroll
+        for (int j = 0; j < WNT; ++j) {
+          const int col = n0 + wn + 16 * j + (lane & 15);
+          const int eb = col < N ? h3_exp(b_amax[col]) : 0;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[i][j][r] = __builtin_ldexpf(acc[i][j][r], -(ea[r] + eb));
+        }
+      }
+    }
     __syncthreads();   // every wave is done reading the last stage
     float* const stg = reinterpret_cast<float*>(&As[0][0]) + wave * 16 * EP;
     const bool cv4 = ((reinterpret_cast<uintptr_t>(C) | static_cast<uintptr_t>(ldc * 4)) & 15) == 0 &&
@@ -1303,6 +1423,59 @@ static void launch_k64(int bn, dim3 grid, hipStream_t st, int M, int N, int K,
 
 static inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
+// fp16x3 row scales (sxgemm2_kernel NPL 2): max |x| of every logical operand row, as float
+// bits.  A logical row that is a stored row: one wave per row, float4 loads, a wave max.
+__global__ __launch_bounds__(256) void amax_rows_kernel(const float* __restrict__ p, int rows,
+                                                        int cols, int64_t ld,
+                                                        unsigned* __restrict__ out) {
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (r >= rows) return;
+  const f32x4* q = reinterpret_cast<const f32x4*>(p + (int64_t)r * ld);
+  float m = 0.f;
+  for (int c = lane; c < cols / 4; c += 64) {
+    const f32x4 v = q[c];
+    m = fmaxf(m, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  if (lane == 0) out[r] = __builtin_bit_cast(unsigned, m);
+}
+
+// A logical row that is a stored column: a block covers 1024 columns (a float4 per thread) of
+// `rpb` stored rows and folds its maxima in with unsigned atomic max (non-negative float bits
+// order as unsigned; `out` zeroed first).
+__global__ __launch_bounds__(256) void amax_cols_kernel(const float* __restrict__ p, int rows,
+                                                        int cols, int64_t ld, int rpb,
+                                                        unsigned* __restrict__ out) {
+  const int c = (blockIdx.x * 256 + threadIdx.x) * 4;
+  if (c >= cols) return;
+  const int r0 = blockIdx.y * rpb, r1 = min(rows, r0 + rpb);
+  f32x4 m = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int r = r0; r < r1; ++r) {
+    const f32x4 v = *reinterpret_cast<const f32x4*>(p + (int64_t)r * ld + c);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) m[e] = fmaxf(m[e], fabsf(v[e]));
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+    if (m[e] > 0.f || m[e] != m[e]) atomicMax(out + c + e, __builtin_bit_cast(unsigned, m[e]));
+}
+
+// amax of the `lrows` logical rows of an operand stored [lrows][k] (rowwise) or [k][lrows]
+static void launch_amax(const float* p, bool rowwise, int lrows, int k, int64_t ld, unsigned* out,
+                        hipStream_t st) {
+  if (rowwise) {
+    hipLaunchKernelGGL(amax_rows_kernel, dim3(cdiv(lrows, 4)), dim3(256), 0, st, p, lrows, k, ld,
+                       out);
+    return;
+  }
+  (void)hipMemsetAsync(out, 0, (size_t)lrows * 4, st);
+  const int cb = cdiv(lrows, 1024);
+  const int rpb = std::max(16, cdiv((int64_t)k * cb, 1024));
+  hipLaunchKernelGGL(amax_cols_kernel, dim3(cb, cdiv(k, rpb)), dim3(256), 0, st, p, k, lrows, ld,
+                     rpb, out);
+}
+
 }  // namespace ds2
 
 using namespace ds2;
@@ -1421,12 +1594,22 @@ static GemmPlan x6_plan(int m, int n, int k, int batch) {
   return plan_bn(m, n, k, batch, n >= 256 ? 160 : 128, device_cus(), XS, 1.0, X2M).p;
 }
 
+// fp16x3 (DS2_GEMM_H3=1, experimental): the x6 kernel's plan and tiles with the operands
+// split into two fp16 terms of row-scaled values and three products per pair (see
+// x2_split_store); the row maxima come from a pre-pass over each operand into the workspace
+// after the split-K slabs
+static bool h3_enabled() {
+  const char* e = getenv("DS2_GEMM_H3");
+  return e != nullptr && e[0] == '1';
+}
+static size_t h3_ws(int m, int n) { return (size_t)(m + n) * 4 + 512; }
+
 // large enough for any kernel's plan (the choice depends on operand alignment)
 extern "C" size_t ds2_sgemm_workspace_size(int m, int n, int k, int batch) {
   if (m <= 0 || n <= 0 || k <= 0 || batch <= 0) return 0;
   return std::max(std::max(plan_ws(gemm_plan(m, n, k, batch, false), batch),
                            plan_ws(gemm_plan(m, n, k, batch, true), batch)),
-                  plan_ws(x6_plan(m, n, k, batch), batch));
+                  plan_ws(x6_plan(m, n, k, batch), batch) + h3_ws(m, n));
 }
 
 extern "C" ds2_status_t ds2_sgemm_ws(int trans_a, int trans_b, int m, int n, int k, float alpha,
@@ -1464,12 +1647,31 @@ extern "C" ds2_status_t ds2_sgemm_ws(int trans_a, int trans_b, int m, int n, int
   hipLaunchKernelGGL((sxgemm2_kernel<TA_, TB_, KCHK_, BN_, 3, M16_>), grid, dim3(X2T), 0, st,   \
                      m, n, k, alpha, a, lda, stride_a, b, ldb, stride_b, beta, c, ldc,          \
                      stride_c, bias, p.main_wgs, p.tail_tile0, p.tail_tiles, p.nsplit,          \
-                     p.kchunk, partial)
+                     p.kchunk, partial, nullptr, nullptr)
+#define DS2_H3(TA_, TB_, BN_)                                                                   \
+  hipLaunchKernelGGL((sxgemm2_kernel<TA_, TB_, false, BN_, 2, true>), grid, dim3(X2T), 0, st,   \
+                     m, n, k, alpha, a, lda, stride_a, b, ldb, stride_b, beta, c, ldc,          \
+                     stride_c, bias, p.main_wgs, p.tail_tile0, p.tail_tiles, p.nsplit,          \
+                     p.kchunk, partial, a_amax, b_amax)
   // the 16x16x32 form wherever every stage lies inside K (r4d: 0-15 % faster on the step's
   // shapes, profiles/r4d_gemm_x6_m16_sk_ab.txt), the 32x32x16 form for a K tail
   const bool m16 = x6 && kalign;
+  const size_t slabs = p.nsplit > 1 ? plan_ws(p, batch) : 0;
+  const bool h3 = m16 && batch == 1 && h3_enabled() && ws != nullptr &&
+                  ws_bytes >= slabs + h3_ws(m, n);
+  unsigned* a_amax = nullptr;
+  unsigned* b_amax = nullptr;
+  if (h3) {
+    const uintptr_t base = (reinterpret_cast<uintptr_t>(ws) + slabs + 255) & ~uintptr_t(255);
+    a_amax = reinterpret_cast<unsigned*>(base);
+    b_amax = a_amax + m;
+    launch_amax(a, !trans_a, m, k, lda, a_amax, st);
+    launch_amax(b, trans_b != 0, n, k, ldb, b_amax, st);
+  }
 #define DS2_G(TA_, TB_)                                                                       \
-  if (m16 && p.bn == 160) DS2_X6(TA_, TB_, false, 160, true);                          \
+  if (h3 && p.bn == 160) DS2_H3(TA_, TB_, 160);                                               \
+  else if (h3) DS2_H3(TA_, TB_, 128);                                                         \
+  else if (m16 && p.bn == 160) DS2_X6(TA_, TB_, false, 160, true);                          \
   else if (m16) DS2_X6(TA_, TB_, false, 128, true);                                          \
   else if (x6 && kalign && p.bn == 160) DS2_X6(TA_, TB_, false, 160, false);                 \
   else if (x6 && p.bn == 160) DS2_X6(TA_, TB_, true, 160, false);                            \
@@ -1494,6 +1696,7 @@ extern "C" ds2_status_t ds2_sgemm_ws(int trans_a, int trans_b, int m, int n, int
   }
 #undef DS2_G
 #undef DS2_X6
+#undef DS2_H3
   if (p.nsplit > 1) {
     const bool vec = p.bn % 4 == 0 && aligned16(c) && ldc % 4 == 0 && stride_c % 4 == 0 &&
                      (bias == nullptr || aligned16(bias));

@@ -541,7 +541,7 @@ class GradAllReducer:
             if min(grid, self.cus) + self.rccl_ctas <= self.cus:
                 return
         for i, h in enumerate(list(self.handles) + self.extra):
-            if h is not None:
+            if h is not None and not isinstance(h, _Waited):
                 h.wait()
                 self.guard_waits += 1
                 if i < len(self.handles):

@@ -290,9 +290,13 @@ def test_world1_nccl_trainer_hooks_and_bit_identity(dev, golden_dir, tmp_path, m
         tr = Trainer(_build(int(g['seed']), 16, 2), LABELS, device=dev, bucket_mb=0.05)
         assert len(tr.reducer.buckets) > 1 and tr.reducer._hooks
         assert (tr.reducer.comm is not None) == (allreduce == "ds2")
-        tr.train_batch(data(), return_item=True)
+        loss = tr.train_batch(data(), return_item=True)
         assert tr.reducer.issued_from_hooks == len(tr.reducer.buckets)
-        assert torch.equal(tr.flat.grad, ref_grad)
+        # one collective per bucket: the status word and the loss rode in the last one
+        assert tr.reducer.collectives == len(tr.reducer.buckets)
+        nparam = tr.flat.numel
+        assert torch.equal(tr.flat.grad[:nparam], ref_grad)
+        assert tr.flat.tail.tolist() == [0.0, loss]     # status word 0, the loss itself
         assert torch.equal(tr.flat.flat, ref_params)
         tr.close()
         assert tr.reducer.comm is None
