@@ -40,10 +40,30 @@ PEAK_BF16_MFMA_TFLOPS = 16 * PEAK_F32_MFMA_TFLOPS
 PEAK_X6_TFLOPS = PEAK_BF16_MFMA_TFLOPS / 6
 
 
-def gemm_peak():
-    """(peak TFLOP/s, arithmetic) of ds2_sgemm_ws as configured (DS2_GEMM_X6=0: fp32 MFMA)."""
+PEAK_H3_TFLOPS = PEAK_BF16_MFMA_TFLOPS / 3
+# the rate a bare MFMA loop reaches at the GEMM's own wave tile (2 x 10 16x16 tiles, 8 waves,
+# fragments re-read from LDS every k-step, random operands, the clock the chip holds under
+# it): scripts/mfma_ceiling.hip, profiles/r5b_mfma_ceiling.jsonl (fp32-equivalent TFLOP/s)
+MEASURED_CEILING = {"x6": 300.0, "h3": 521.3}
+CEILING_SOURCE = "profiles/r5b_mfma_ceiling.jsonl"
+
+
+def gemm_mode():
     if os.environ.get("DS2_GEMM_X6", "1")[:1] == "0":
+        return "fp32"
+    return "h3" if os.environ.get("DS2_GEMM_H3", "0")[:1] == "1" else "x6"
+
+
+def gemm_peak():
+    """(peak TFLOP/s, arithmetic) of ds2_sgemm_ws as configured (DS2_GEMM_X6=0: fp32 MFMA;
+    DS2_GEMM_H3=1: the fp16x3 kernel)."""
+    mode = gemm_mode()
+    if mode == "fp32":
         return PEAK_F32_MFMA_TFLOPS, "fp32 MFMA (v_mfma_f32_16x16x4_f32)"
+    if mode == "h3":
+        return PEAK_H3_TFLOPS, ("fp32 operands scaled per row by 2^e and split into 2 fp16 "
+                                "terms, 3 products on v_mfma_f32_16x16x32_f16, fp32 accumulation "
+                                "(fp16 dense peak / 3)")
     return PEAK_X6_TFLOPS, ("fp32 operands split into 3 bf16 terms, 6 products on "
                             "v_mfma_f32_16x16x32_bf16 (32x32x16 for a K tail), fp32 "
                             "accumulation (bf16 dense peak / 6)")
@@ -364,6 +384,11 @@ def main():
                  "traffic": None if traffic is None else round(traffic),
                  "traffic_unit": "bytes/launch (HBM, PMC)", "traffic_source": src,
                  "step_achieved_tflops": step_tf}
+            if name == args.probe and gemm_mode() in MEASURED_CEILING:
+                ceil = MEASURED_CEILING[gemm_mode()]
+                e["measured_ceiling"] = ceil
+                e["frac_of_measured_ceiling"] = round(achieved / ceil, 4)
+                e["ceiling_source"] = CEILING_SOURCE
             if name.startswith("ds2_gru"):
                 # latency-bound: T' dependent steps, one cross-CU hand-off each
                 e["us_per_step"] = round(avg_ms * 1e3 / ((T_FRAMES - 1) // 2 + 1), 3)

@@ -941,9 +941,12 @@ __global__ __launch_bounds__(X2T, 1) void sxgemm2_kernel(
   constexpr int BP = TBN * XS;             // bf16 per B plane
   constexpr int BF = TBN == 128 ? 8 : 16;  // B floats per thread per stage
   using OA = X2Op<AK, X2M>;
-  static_assert(NPL == 1 || NPL == 3, "planes");
-  __shared__ __attribute__((aligned(16))) unsigned short As[2][NPL * X2_AP];
-  __shared__ __attribute__((aligned(16))) unsigned short Bs[2][NPL * BP];
+  static_assert(NPL == 1 || NPL == 2 || NPL == 3, "planes");
+  // the A and B stages back to back (the epilogue staging may span both)
+  constexpr int SA = 2 * NPL * X2_AP, SB = 2 * NPL * BP;
+  __shared__ __attribute__((aligned(16))) unsigned short smem[SA + SB];
+  unsigned short (*const As)[NPL * X2_AP] = reinterpret_cast<unsigned short (*)[NPL * X2_AP]>(smem);
+  unsigned short (*const Bs)[NPL * BP] = reinterpret_cast<unsigned short (*)[NPL * BP]>(smem + SA);
 
   // one job: C tile (m0, n0) over k in [kbeg, kend), into C or (part != null) a partial slab
   auto job = [&](const int m0, const int n0, const int kbeg, const int kend, float* const part) {
@@ -1220,7 +1223,7 @@ __global__ __launch_bounds__(X2T, 1) void sxgemm2_kernel(
     // conflict-free), leaving as 16-B row runs -- each store instruction writes 1 KB of whole
     // row segments instead of sixteen 64-B pieces
     constexpr int EW = WNT * 16, EP = EW + 4;
-    static_assert(8 * 16 * EP * 4 <= 2 * NPL * X2_AP * 2, "epilogue staging fits the A stages");
+    static_assert(8 * 16 * EP * 4 <= (SA + SB) * 2, "epilogue staging fits the stages");
     if constexpr (NPL == 2) {
       // undo the row scales: C = acc 2^-(e_a(row) - e_b(col)), exact unless the result
       // itself under- or overflows
@@ -1242,7 +1245,7 @@ __global__ __launch_bounds__(X2T, 1) void sxgemm2_kernel(
       }
     }
     __syncthreads();   // every wave is done reading the last stage
-    float* const stg = reinterpret_cast<float*>(&As[0][0]) + wave * 16 * EP;
+    float* const stg = reinterpret_cast<float*>(smem) + wave * 16 * EP;
     const bool cv4 = ((reinterpret_cast<uintptr_t>(C) | static_cast<uintptr_t>(ldc * 4)) & 15) == 0 &&
                      (bias == nullptr || (reinterpret_cast<uintptr_t>(bias) & 15) == 0);
 #pragma unroll
@@ -1456,9 +1459,43 @@ __global__ __launch_bounds__(256) void amax_cols_kernel(const float* __restrict_
 #pragma unroll
     for (int e = 0; e < 4; ++e) m[e] = fmaxf(m[e], fabsf(v[e]));
   }
+  // (each element copied to a scalar first: hipcc 7.2 bit_cast an ext_vector element
+  // straight into the atomic's data as element 0 for every e)
+  const float me[4] = {m[0], m[1], m[2], m[3]};
 #pragma unroll
   for (int e = 0; e < 4; ++e)
-    if (m[e] > 0.f || m[e] != m[e]) atomicMax(out + c + e, __builtin_bit_cast(unsigned, m[e]));
+    if (me[e] > 0.f) atomicMax(out + c + e, __float_as_uint(me[e]));
+}
+
+// Row AND column maxima in one pass (ds2_amax): a block covers 1024 columns (a float4 per
+// thread) of `rpb` rows; column maxima fold in by unsigned atomic max, row maxima by a wave
+// max per row and one atomic per wave (both outputs zeroed first).
+__global__ __launch_bounds__(256) void amax_both_kernel(const float* __restrict__ p, int rows,
+                                                        int cols, int64_t ld, int rpb,
+                                                        unsigned* __restrict__ rmax,
+                                                        unsigned* __restrict__ cmax) {
+  const int c = (blockIdx.x * 256 + threadIdx.x) * 4;
+  const bool in = c < cols;
+  const int r0 = blockIdx.y * rpb, r1 = min(rows, r0 + rpb);
+  f32x4 m = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int r = r0; r < r1; ++r) {
+    f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (in) v = *reinterpret_cast<const f32x4*>(p + (int64_t)r * ld + c);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) m[e] = fmaxf(m[e], fabsf(v[e]));
+    if (rmax != nullptr) {
+      float w = fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3])));
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) w = fmaxf(w, __shfl_xor(w, o));
+      if ((threadIdx.x & 63) == 0 && w > 0.f) atomicMax(rmax + r, __float_as_uint(w));
+    }
+  }
+  if (cmax != nullptr && in) {
+    const float me[4] = {m[0], m[1], m[2], m[3]};   // see amax_cols_kernel
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      if (me[e] > 0.f) atomicMax(cmax + c + e, __float_as_uint(me[e]));
+  }
 }
 
 // amax of the `lrows` logical rows of an operand stored [lrows][k] (rowwise) or [k][lrows]
@@ -1604,6 +1641,27 @@ static bool h3_enabled() {
 }
 static size_t h3_ws(int m, int n) { return (size_t)(m + n) * 4 + 512; }
 
+extern "C" ds2_status_t ds2_amax(const float* x, int rows, int cols, int64_t ld,
+                                 unsigned* row_amax, unsigned* col_amax, ds2_stream_t stream) {
+  if (rows < 0 || cols < 0 || ld < cols) return DS2_INVALID_VALUE;
+  if (rows == 0 || cols == 0 || (row_amax == nullptr && col_amax == nullptr)) return DS2_OK;
+  if (x == nullptr || !aligned16(x) || (cols % 4) != 0 || (ld % 4) != 0)
+    return DS2_UNSUPPORTED_SHAPE;
+  hipStream_t st = as_stream(stream);
+  if (col_amax == nullptr) {            // rows only: one wave per row, no atomics
+    hipLaunchKernelGGL(amax_rows_kernel, dim3(cdiv(rows, 4)), dim3(256), 0, st, x, rows, cols,
+                       ld, row_amax);
+    return launch_status("ds2_amax");
+  }
+  if (row_amax != nullptr) (void)hipMemsetAsync(row_amax, 0, (size_t)rows * 4, st);
+  (void)hipMemsetAsync(col_amax, 0, (size_t)cols * 4, st);
+  const int cb = cdiv(cols, 1024);
+  const int rpb = std::max(16, cdiv((int64_t)rows * cb, 1024));
+  hipLaunchKernelGGL(amax_both_kernel, dim3(cb, cdiv(rows, rpb)), dim3(256), 0, st, x, rows, cols,
+                     ld, rpb, row_amax, col_amax);
+  return launch_status("ds2_amax");
+}
+
 // large enough for any kernel's plan (the choice depends on operand alignment)
 extern "C" size_t ds2_sgemm_workspace_size(int m, int n, int k, int batch) {
   if (m <= 0 || n <= 0 || k <= 0 || batch <= 0) return 0;
@@ -1612,12 +1670,39 @@ extern "C" size_t ds2_sgemm_workspace_size(int m, int n, int k, int batch) {
                   plan_ws(x6_plan(m, n, k, batch), batch) + h3_ws(m, n));
 }
 
+static ds2_status_t sgemm_run(int trans_a, int trans_b, int m, int n, int k, float alpha,
+                              const float* a, int64_t lda, int64_t stride_a, const float* b,
+                              int64_t ldb, int64_t stride_b, float beta, float* c, int64_t ldc,
+                              int64_t stride_c, int batch, const float* bias, void* ws,
+                              size_t ws_bytes, const unsigned* a_amax_in,
+                              const unsigned* b_amax_in, ds2_stream_t stream);
+
 extern "C" ds2_status_t ds2_sgemm_ws(int trans_a, int trans_b, int m, int n, int k, float alpha,
                                      const float* a, int64_t lda, int64_t stride_a,
                                      const float* b, int64_t ldb, int64_t stride_b, float beta,
                                      float* c, int64_t ldc, int64_t stride_c, int batch,
                                      const float* bias, void* ws, size_t ws_bytes,
                                      ds2_stream_t stream) {
+  return sgemm_run(trans_a, trans_b, m, n, k, alpha, a, lda, stride_a, b, ldb, stride_b, beta, c,
+                   ldc, stride_c, batch, bias, ws, ws_bytes, nullptr, nullptr, stream);
+}
+
+extern "C" ds2_status_t ds2_sgemm_amax_ws(int trans_a, int trans_b, int m, int n, int k,
+                                          float alpha, const float* a, int64_t lda,
+                                          const float* b, int64_t ldb, float beta, float* c,
+                                          int64_t ldc, const float* bias, const unsigned* a_amax,
+                                          const unsigned* b_amax, void* ws, size_t ws_bytes,
+                                          ds2_stream_t stream) {
+  return sgemm_run(trans_a, trans_b, m, n, k, alpha, a, lda, 0, b, ldb, 0, beta, c, ldc, 0, 1,
+                   bias, ws, ws_bytes, a_amax, b_amax, stream);
+}
+
+static ds2_status_t sgemm_run(int trans_a, int trans_b, int m, int n, int k, float alpha,
+                              const float* a, int64_t lda, int64_t stride_a, const float* b,
+                              int64_t ldb, int64_t stride_b, float beta, float* c, int64_t ldc,
+                              int64_t stride_c, int batch, const float* bias, void* ws,
+                              size_t ws_bytes, const unsigned* a_amax_in,
+                              const unsigned* b_amax_in, ds2_stream_t stream) {
   if (m < 0 || n < 0 || k < 0 || batch < 0) return DS2_INVALID_VALUE;
   if (m == 0 || n == 0 || batch == 0) return DS2_OK;
   if (ldc < n) return DS2_INVALID_VALUE;
@@ -1659,14 +1744,20 @@ extern "C" ds2_status_t ds2_sgemm_ws(int trans_a, int trans_b, int m, int n, int
   const size_t slabs = p.nsplit > 1 ? plan_ws(p, batch) : 0;
   const bool h3 = m16 && batch == 1 && h3_enabled() && ws != nullptr &&
                   ws_bytes >= slabs + h3_ws(m, n);
-  unsigned* a_amax = nullptr;
-  unsigned* b_amax = nullptr;
+  const unsigned* a_amax = a_amax_in;
+  const unsigned* b_amax = b_amax_in;
   if (h3) {
     const uintptr_t base = (reinterpret_cast<uintptr_t>(ws) + slabs + 255) & ~uintptr_t(255);
-    a_amax = reinterpret_cast<unsigned*>(base);
-    b_amax = a_amax + m;
-    launch_amax(a, !trans_a, m, k, lda, a_amax, st);
-    launch_amax(b, trans_b != 0, n, k, ldb, b_amax, st);
+    unsigned* wa = reinterpret_cast<unsigned*>(base);
+    unsigned* wb = wa + m;
+    if (a_amax == nullptr) {
+      launch_amax(a, !trans_a, m, k, lda, wa, st);
+      a_amax = wa;
+    }
+    if (b_amax == nullptr) {
+      launch_amax(b, trans_b != 0, n, k, ldb, wb, st);
+      b_amax = wb;
+    }
   }
 #define DS2_G(TA_, TB_)                                                                       \
   if (h3 && p.bn == 160) DS2_H3(TA_, TB_, 160);                                               \

@@ -82,6 +82,9 @@ _PROTOS = {
     "ds2_test_occupy": (_c_int, [_c_int, _c_int, _c_int, _vp, _vp]),
     "ds2_test_rnn_launch_lds": (_c_int, [_c_int, _c_int, _vp, _vp]),
     "ds2_test_timestamp": (_c_int, [_vp, _vp]),
+    "ds2_amax": (_c_int, [_vp, _c_int, _c_int, _c_i64, _vp, _vp, _vp]),
+    "ds2_sgemm_amax_ws": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _c_f, _vp, _c_i64, _vp,
+                                   _c_i64, _c_f, _vp, _c_i64, _vp, _vp, _vp, _vp, _sz, _vp]),
     "ds2_test_ring_traffic": (_c_int, [_vp, _c_i64, _c_int, _vp, _c_int, ctypes.c_double, _vp]),
     "ds2_test_beam_stamps": (_c_int, [_vp]),
     "ds2_gru_bwd": (_c_int, [_c_int, _c_int, _c_int, _c_int, _vp, _c_int, _vp, _vp, _vp, _vp,

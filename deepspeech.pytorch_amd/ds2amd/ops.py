@@ -10,6 +10,7 @@ from __future__ import annotations
 
 from typing import Optional, Tuple
 
+import os
 import numpy as np
 import torch
 
@@ -90,15 +91,31 @@ def check_rnn_status(device=None, reset: bool = True) -> None:
 def sgemm(a: torch.Tensor, b: torch.Tensor, c: torch.Tensor, *, m: int, n: int, k: int,
           trans_a: bool = False, trans_b: bool = False, lda: int, ldb: int, ldc: int,
           alpha: float = 1.0, beta: float = 0.0, bias: Optional[torch.Tensor] = None,
-          a_off: int = 0, b_off: int = 0, c_off: int = 0, bf16: bool = False) -> torch.Tensor:
+          a_off: int = 0, b_off: int = 0, c_off: int = 0, bf16: bool = False,
+          a_amax: Optional[torch.Tensor] = None, b_amax: Optional[torch.Tensor] = None
+          ) -> torch.Tensor:
     """C = alpha*op(A)@op(B) + beta*C (+bias) on raw row-major storage.
 
     ``*_off`` are element offsets into the (contiguous) storage of a/b/c.  ``bf16``: the
     operands are rounded to bf16 and multiplied on the bf16 MFMA (fp32 accumulation,
     ds2_sgemm_bf16_ws) -- the opt-in precision of BASELINE cfg4's RNN GEMMs.
+    ``a_amax`` / ``b_amax``: int32 tensors holding the float bits of max |op(A)[m, :]| /
+    max |op(B)[:, n]| (ds2_amax; an upper bound is valid): the fp16x3 kernel's row scales,
+    shared between GEMMs instead of recomputed by each (ds2_sgemm_amax_ws).
     """
     es = 4
-    if bf16 and k % 8 == 0 and k > 0 and m > 0 and n > 0:
+    if (a_amax is not None or b_amax is not None) and not bf16:
+        nbytes = _lib.size("ds2_sgemm_workspace_size", m, n, k, 1)
+        ws = _ws(nbytes, c.device) if nbytes > 0 else None
+        _lib.call("ds2_sgemm_amax_ws", int(trans_a), int(trans_b), m, n, k, float(alpha),
+                  a.data_ptr() + es * a_off, lda, b.data_ptr() + es * b_off, ldb, float(beta),
+                  c.data_ptr() + es * c_off, ldc, _p(bias), _p(a_amax), _p(b_amax), _p(ws),
+                  0 if ws is None else ws.numel(), _stream())
+        return c
+    # ds2_bgemm_nt takes bf16 copies of < 2 GiB each (ADVICE r4): larger operands stay on the
+    # staged-rounding kernel (ds2_sgemm_bf16_ws), which has no such limit
+    if (bf16 and k % 8 == 0 and k > 0 and m > 0 and n > 0 and 2 * m * k < 2**31
+            and 2 * n * k < 2**31):
         return _sgemm_bf16_bgemm(a, b, c, m, n, k, trans_a, trans_b, lda, ldb, ldc, alpha, beta,
                                  bias, a_off, b_off, c_off)
     fn = "ds2_sgemm_bf16" if bf16 else "ds2_sgemm"
@@ -109,6 +126,40 @@ def sgemm(a: torch.Tensor, b: torch.Tensor, c: torch.Tensor, *, m: int, n: int, 
               float(beta), c.data_ptr() + es * c_off, ldc, 0, 1, _p(bias), _p(ws),
               0 if ws is None else ws.numel(), _stream())
     return c
+
+
+def h3_enabled() -> bool:
+    """The fp16x3 GEMM kernel is in use (DS2_GEMM_H3, read by the library per call)."""
+    return os.environ.get("DS2_GEMM_H3", "0")[:1] == "1" and \
+        os.environ.get("DS2_GEMM_X6", "1")[:1] != "0"
+
+
+def amax(x: torch.Tensor, rows: int, cols: int, ld: int, off: int = 0, want_rows: bool = True,
+         want_cols: bool = True):
+    """(row maxima, column maxima) of |x| over the [rows][cols] matrix at element offset
+    ``off`` of x's storage (leading dimension ld) as int32 float bits (ds2_amax, one pass);
+    None for a part not asked for, or for both when the operand is not float4-aligned."""
+    ptr = x.data_ptr() + 4 * off
+    if ptr % 16 or cols % 4 or ld % 4 or rows <= 0 or cols <= 0:
+        return None, None
+    r = torch.empty(rows, dtype=_I32, device=x.device) if want_rows else None
+    c = torch.empty(cols, dtype=_I32, device=x.device) if want_cols else None
+    _lib.call("ds2_amax", ptr, rows, cols, ld, _p(r), _p(c), _stream())
+    return r, c
+
+
+_ONE_BITS = {}
+
+
+def unit_bound(n: int, device) -> torch.Tensor:
+    """n float bits of 1.0: the fp16x3 scale bound of tanh-bounded operands (the recurrent
+    states h, |h| < 1)."""
+    key = (n, str(device))
+    t = _ONE_BITS.get(key)
+    if t is None:
+        t = torch.full((n,), 0x3F800000, dtype=_I32, device=device)
+        _ONE_BITS[key] = t
+    return t
 
 
 def _sgemm_bf16_bgemm(a, b, c, m, n, k, trans_a, trans_b, lda, ldb, ldc, alpha, beta, bias,
@@ -794,12 +845,15 @@ def _rnn_param_grads_bf16(x2d, h_all, dgx, dgh, weights, nd, g, t, n, inp, h, ne
     return dx, grads
 
 
-def _rnn_param_grads(x, h_all, dgx, dgh, weights, nd, g, need_dx, bf16=False, dbias=None):
+def _rnn_param_grads(x, h_all, dgx, dgh, weights, nd, g, need_dx, bf16=False, dbias=None,
+                     shared_bf16=True):
     """Weight/bias/input gradients of one recurrent layer from the gate gradients.
 
     dgx = d/d(x W_ih^T + b_ih), dgh = d/d(h W_hh^T + b_hh), both [T, N, D, g]
     (the same tensor for LSTM).  All plain GEMMs + column sums; dbias = [db_ih, db_hh] per
     direction already summed (the GRU backward kernel's own sums) skips the column sums.
+    shared_bf16=False keeps bf16 mode on the per-GEMM conversions (the cross-check of
+    _rnn_param_grads_bf16's shared copies, tests/test_gpu_ops.py).
     """
     t, n, inp = x.shape
     h = h_all.shape[-1]
@@ -807,7 +861,7 @@ def _rnn_param_grads(x, h_all, dgx, dgh, weights, nd, g, need_dx, bf16=False, db
     x2d = x.view(t * n, inp)
     tn = t * n
     ld = nd * g
-    if bf16 and t > 1 and all(v % 8 == 0 for v in (n, inp, h, g)):
+    if bf16 and shared_bf16 and t > 1 and all(v % 8 == 0 for v in (n, inp, h, g)):
         return _rnn_param_grads_bf16(x2d, h_all, dgx, dgh, weights, nd, g, t, n, inp, h,
                                      need_dx, dbias)
     grads = []
@@ -816,17 +870,39 @@ def _rnn_param_grads(x, h_all, dgx, dgh, weights, nd, g, need_dx, bf16=False, db
     w_st = _stacked_rows(weights[0], weights[4]) if nd == 2 else None
     dw_ih_all = [grad_like(weights[4 * d]) for d in range(nd)]
     dw_st = _stacked_rows(dw_ih_all[0], dw_ih_all[1]) if w_st is not None else None
+    # fp16x3 operand scales, each operand read once and shared by the GEMMs below: dgx rows
+    # (dX) and columns (dW_ih), dgh columns (dW_hh; a bound over all its rows), x and W_ih
+    # columns, and 1.0 for the tanh-bounded states h
+    am = {}
+    if h3_enabled() and not bf16:
+        am["dgx_r"], am["dgx_c"] = amax(dgx, tn, ld, ld, want_rows=need_dx)
+        am["dgh_c"] = am["dgx_c"] if dgh is dgx else amax(dgh, tn, ld, ld, want_rows=False)[1]
+        am["x_c"] = amax(x2d, tn, inp, inp, want_rows=False)[1]
+        am["h"] = unit_bound(nd * h, dev)
+        if need_dx:
+            if w_st is not None:
+                am["w_c"] = amax(w_st, 2 * g, inp, inp, want_rows=False)[1]
+            else:
+                am["w_c"] = [amax(weights[4 * d], g, inp, inp, want_rows=False)[1]
+                             for d in range(nd)]
+
+    def sl(key, lo, hi):
+        v = am.get(key)
+        return None if v is None else v[lo:hi]
+
     if dw_st is not None:
         sgemm(dgx, x2d, dw_st, m=2 * g, n=inp, k=tn, trans_a=True, lda=ld, ldb=inp, ldc=inp,
-              bf16=bf16)
+              bf16=bf16, a_amax=am.get("dgx_c"), b_amax=am.get("x_c"))
     if dx is not None and w_st is not None:
-        sgemm(dgx, w_st, dx, m=tn, n=inp, k=2 * g, lda=ld, ldb=inp, ldc=inp, bf16=bf16)
+        sgemm(dgx, w_st, dx, m=tn, n=inp, k=2 * g, lda=ld, ldb=inp, ldc=inp, bf16=bf16,
+              a_amax=am.get("dgx_r"), b_amax=am.get("w_c"))
     for d in range(nd):
         w_ih, w_hh, b_ih, b_hh = weights[4 * d: 4 * d + 4]
         dw_ih = dw_ih_all[d]
         if dw_st is None:
             sgemm(dgx, x2d, dw_ih, m=g, n=inp, k=tn, trans_a=True, lda=ld, ldb=inp, ldc=inp,
-                  a_off=d * g, bf16=bf16)
+                  a_off=d * g, bf16=bf16, a_amax=sl("dgx_c", d * g, (d + 1) * g),
+                  b_amax=am.get("x_c"))
         if dbias is not None:
             db_ih, db_hh = dbias[2 * d], dbias[2 * d + 1]
         else:
@@ -838,7 +914,8 @@ def _rnn_param_grads(x, h_all, dgx, dgh, weights, nd, g, need_dx, bf16=False, db
             a_off = (n * ld if d == 0 else 0) + d * g
             b_off = (0 if d == 0 else n * nd * h) + d * h
             sgemm(dgh, h_all, dw_hh, m=g, n=h, k=(t - 1) * n, trans_a=True, lda=ld,
-                  ldb=nd * h, ldc=h, a_off=a_off, b_off=b_off, bf16=bf16)
+                  ldb=nd * h, ldc=h, a_off=a_off, b_off=b_off, bf16=bf16,
+                  a_amax=sl("dgh_c", d * g, (d + 1) * g), b_amax=sl("h", d * h, (d + 1) * h))
         else:
             dw_hh.zero_()
         if dbias is None:
@@ -853,8 +930,10 @@ def _rnn_param_grads(x, h_all, dgx, dgh, weights, nd, g, need_dx, bf16=False, db
             else:
                 colsum(dgh, tn, g, ld, db_hh, off=d * g)
         if dx is not None and w_st is None:
+            # dgx's row maxima span both directions: an upper bound for each direction's slice
             sgemm(dgx, w_ih, dx, m=tn, n=inp, k=g, lda=ld, ldb=inp, ldc=inp,
-                  beta=0.0 if d == 0 else 1.0, a_off=d * g, bf16=bf16)
+                  beta=0.0 if d == 0 else 1.0, a_off=d * g, bf16=bf16,
+                  a_amax=am.get("dgx_r"), b_amax=None if "w_c" not in am else am["w_c"][d])
         grads += [dw_ih, dw_hh, db_ih, db_hh]
     return dx, grads
 

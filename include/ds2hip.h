@@ -133,6 +133,21 @@ ds2_status_t ds2_sgemm_ws(int trans_a, int trans_b, int m, int n, int k, float a
                           const float* b, int64_t ldb, int64_t stride_b, float beta,
                           float* c, int64_t ldc, int64_t stride_c, int batch,
                           const float* bias, void* ws, size_t ws_bytes, ds2_stream_t stream);
+/* fp16x3 operand scales: row_amax[r] / col_amax[c] = the float bits of max |x| over row r /
+ * column c of x [rows][ld] (either output NULL: not computed; non-negative float bits order
+ * as unsigned).  16-B aligned x, cols and ld multiples of 4, else DS2_UNSUPPORTED_SHAPE.  One
+ * pass over x.  A NaN is skipped (max of the other elements), an inf gives inf.            */
+ds2_status_t ds2_amax(const float* x, int rows, int cols, int64_t ld, unsigned* row_amax,
+                      unsigned* col_amax, ds2_stream_t stream);
+/* ds2_sgemm_ws (batch 1) with the fp16x3 scales of the logical operand rows supplied by the
+ * caller: a_amax[m] = max over k of |op(A)[m][k]|, b_amax[n] = max over k of |op(B)[k][n]|
+ * (ds2_amax bits; an upper bound is valid and costs only precision below 2^-17 of it); NULL
+ * = computed here.  Ignored unless the fp16x3 kernel runs.                               */
+ds2_status_t ds2_sgemm_amax_ws(int trans_a, int trans_b, int m, int n, int k, float alpha,
+                               const float* a, int64_t lda, const float* b, int64_t ldb,
+                               float beta, float* c, int64_t ldc, const float* bias,
+                               const unsigned* a_amax, const unsigned* b_amax, void* ws,
+                               size_t ws_bytes, ds2_stream_t stream);
 /* bf16-operand variant (BASELINE cfg4 "bf16 MFMA RNN GEMMs", opt-in): same contract, A and
  * B rounded to bf16 (nearest even) as they are staged, v_mfma_f32_16x16x32_bf16, fp32
  * accumulation and fp32 C.  Needs float4-aligned operands (16-B aligned pointers, ld and

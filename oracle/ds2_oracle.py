@@ -162,21 +162,19 @@ class OracleDS2:
                             self.params[prefix + '.weight'], self.params[prefix + '.bias'],
                             training=training, momentum=self.bnm, eps=1e-5)
 
-    def forward(self, x: torch.Tensor, lengths: torch.Tensor, training: bool = True,
-                params: Optional[Dict[str, torch.Tensor]] = None, keep: bool = False):
-        """Returns (logits [N,T',C], probs, out_lens int32, acts dict)."""
-        self.params = params if params is not None else self.parameters()
+    def conv_block(self, x: torch.Tensor, out_lens: torch.Tensor, training: bool = True,
+                   acts: Optional[dict] = None) -> torch.Tensor:
+        """The conv stack (model.py:208-215) with MaskConv after each module (model.py:63-79)
+        and the T x N x H collapse (model.py:360-362), in the dtype of x and self.params
+        (the parameters: self.params as set by forward, or the caller's)."""
         p = self.params
-        acts = {}
-        out_lens = get_seq_lens(lengths.cpu().int())
-        # conv stack (model.py:208-215) with MaskConv after each module
         x = F.conv2d(x, p['conv.seq_module.0.weight'], p['conv.seq_module.0.bias'], stride=(2, 2),
                      padding=(20, 5))
         x = _mask_time(x, out_lens)
         x = self._bn(x, 'conv.seq_module.1', training)
         x = _mask_time(x, out_lens)
         x = _mask_time(F.hardtanh(x, 0, 20), out_lens)
-        if keep:
+        if acts is not None:
             acts['conv1'] = x
         x = F.conv2d(x, p['conv.seq_module.3.weight'], p['conv.seq_module.3.bias'], stride=(2, 1),
                      padding=(10, 5))
@@ -184,10 +182,19 @@ class OracleDS2:
         x = self._bn(x, 'conv.seq_module.4', training)
         x = _mask_time(x, out_lens)
         x = _mask_time(F.hardtanh(x, 0, 20), out_lens)
-        if keep:
+        if acts is not None:
             acts['conv2'] = x
         n, c, d, t = x.shape
-        x = x.view(n, c * d, t).transpose(1, 2).transpose(0, 1).contiguous()   # T x N x H
+        return x.view(n, c * d, t).transpose(1, 2).transpose(0, 1).contiguous()   # T x N x H
+
+    def forward(self, x: torch.Tensor, lengths: torch.Tensor, training: bool = True,
+                params: Optional[Dict[str, torch.Tensor]] = None, keep: bool = False):
+        """Returns (logits [N,T',C], probs, out_lens int32, acts dict)."""
+        self.params = params if params is not None else self.parameters()
+        p = self.params
+        acts = {}
+        out_lens = get_seq_lens(lengths.cpu().int())
+        x = self.conv_block(x, out_lens, training, acts if keep else None)
         for i in range(self.nb_layers):
             pre = f'rnns.{i}'
             if i > 0:    # SequenceWise(BatchNorm1d) (model.py:100-101)

@@ -25,17 +25,25 @@ def _close(got, ref, rel=1e-5, name=""):
 
 
 # ---------------------------------------------------------------------------- GEMM
-@pytest.mark.parametrize("x6", ["1", "0"])
+def _gemm_mode(monkeypatch, mode):
+    """x6: the bf16x6 kernel; h3: the fp16x3 kernel (DS2_GEMM_H3=1); fp32: DS2_GEMM_X6=0."""
+    monkeypatch.setenv("DS2_GEMM_X6", "0" if mode.startswith("fp32") or mode == "unaligned"
+                       else "1")
+    monkeypatch.setenv("DS2_GEMM_H3", "1" if mode.startswith("h3") else "0")
+
+
+@pytest.mark.parametrize("x6", ["1", "0", "h3"])
 @pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
 @pytest.mark.parametrize("m,n,k", [(1, 1, 1), (37, 53, 29), (128, 128, 16), (300, 257, 513),
                                    (515, 2400, 132), (257, 300, 5000),   # split-K path
                                    (300, 256, 516), (260, 132, 1000),    # float4 staging, K % 32 != 0
                                    (300, 260, 1024)])                    # K % 32 == 0
 def test_sgemm(dev, ta, tb, m, n, k, x6, monkeypatch):
-    """ds2_sgemm_ws vs fp64 at 1e-5: the bf16x6 kernel (default for float4-staged operands;
-    256 x 160 tiles for N >= 256, 256 x 128 below; its 16x16x32 form where every stage lies
-    inside K, the 32x32x16 form for a K tail) and the fp32-MFMA kernels (DS2_GEMM_X6=0)."""
-    monkeypatch.setenv("DS2_GEMM_X6", x6)
+    """ds2_sgemm_ws vs fp64 at 1e-5: the bf16x6 kernel (256 x 160 tiles for N >= 256,
+    256 x 128 below; its 16x16x32 form where every stage lies inside K, the 32x32x16 form for
+    a K tail), the fp16x3 kernel ("h3", the same tiles on v_mfma_f32_16x16x32_f16 where every
+    stage lies inside K, else the bf16x6 kernel) and the fp32-MFMA kernels (DS2_GEMM_X6=0)."""
+    _gemm_mode(monkeypatch, {"1": "x6", "0": "fp32", "h3": "h3"}[x6])
     g = torch.Generator().manual_seed(m * 7 + n * 3 + k)
     a = torch.randn(k, m, generator=g) if ta else torch.randn(m, k, generator=g)
     b = torch.randn(n, k, generator=g) if tb else torch.randn(k, n, generator=g)
@@ -51,7 +59,7 @@ def test_sgemm(dev, ta, tb, m, n, k, x6, monkeypatch):
 
 
 @pytest.mark.parametrize("mode", ["x6", "x6-narrow", "x6-ktail", "x6-ktail-narrow", "fp32",
-                                  "fp32-narrow", "unaligned"])
+                                  "fp32-narrow", "unaligned", "h3", "h3-narrow"])
 @pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
 def test_sgemm_full_rounds_plus_split_tail(dev, ta, tb, mode, monkeypatch):
     """Whole rounds of resident workgroups + a tail whose K range is split (one launch) and
@@ -59,7 +67,7 @@ def test_sgemm_full_rounds_plus_split_tail(dev, ta, tb, mode, monkeypatch):
     (N >= 256) and 256 x 128 ("-narrow": N < 256); fp32 kernels (DS2_GEMM_X6=0): BK = 64 /
     16x16x4 with the plan's tile width, and ("unaligned": A one float off 16-B alignment)
     the BK = 16 / 32x32x2 kernel."""
-    monkeypatch.setenv("DS2_GEMM_X6", "1" if mode.startswith("x6") else "0")
+    _gemm_mode(monkeypatch, mode)
     # K % 32 == 0: the 16x16x32 form; "-ktail" (K % 32 == 4): the 32x32x16 form with k checks
     m, k = 128 * 29, 2084 if "ktail" in mode else 2080
     n = 200 if mode.endswith("narrow") else 128 * 27 + 52
@@ -96,13 +104,89 @@ def test_sgemm_x6_is_fp32_accurate(dev, ta, tb, m, n, k, monkeypatch):
     ref = (a.t() if ta else a).double() @ (b.t() if tb else b).double()
     scale = ref.abs().max().item()
     errs = {}
-    for mode in ("1", "0"):
-        monkeypatch.setenv("DS2_GEMM_X6", mode)
+    for mode in ("x6", "fp32", "h3"):
+        _gemm_mode(monkeypatch, mode)
         c = torch.empty(m, n, device=dev)
         ops.sgemm(a, b, c, m=m, n=n, k=k, trans_a=bool(ta), trans_b=bool(tb), lda=a.shape[1],
                   ldb=b.shape[1], ldc=n)
         errs[mode] = (c.double() - ref).abs().max().item() / scale
-    assert errs["1"] <= 2.5 * errs["0"] and errs["1"] < 5e-6, errs
+    assert errs["x6"] <= 2.5 * errs["fp32"] and errs["x6"] < 5e-6, errs
+    assert errs["h3"] <= 2.5 * errs["fp32"] and errs["h3"] < 5e-6, errs
+
+
+@pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
+def test_sgemm_h3_rows_over_twelve_decades(dev, ta, tb, monkeypatch):
+    """The fp16x3 kernel's per-row scales: rows of op(A) and columns of op(B) scaled by
+    10^U(-6, 6), so one unscaled fp16 range could not hold them.  Componentwise error
+    max |C - C64| / (|A| |B|) (the form of the fp32 GEMM error bound) within 2.5x of the
+    fp32-MFMA kernel's and < 1e-6; the caller-supplied scales (ds2_sgemm_amax_ws, from
+    ds2_amax) give the same bits as the kernel's own pre-pass."""
+    m, n, k = 600, 416, 1088
+    g = torch.Generator().manual_seed(17 + 2 * ta + tb)
+    a = torch.randn(k, m, generator=g) if ta else torch.randn(m, k, generator=g)
+    b = torch.randn(n, k, generator=g) if tb else torch.randn(k, n, generator=g)
+    sa = torch.pow(10.0, torch.rand(m, generator=g) * 12 - 6)
+    sb = torch.pow(10.0, torch.rand(n, generator=g) * 12 - 6)
+    a = (a * sa[None, :] if ta else a * sa[:, None]).to(dev)
+    b = (b * sb[:, None] if tb else b * sb[None, :]).to(dev)
+    at, bt = (a.t() if ta else a).double(), (b.t() if tb else b).double()
+    ref = at @ bt
+    bound = at.abs() @ bt.abs()
+    comp = {}
+    outs = {}
+    for mode in ("fp32", "h3"):
+        _gemm_mode(monkeypatch, mode)
+        c = torch.empty(m, n, device=dev)
+        ops.sgemm(a, b, c, m=m, n=n, k=k, trans_a=bool(ta), trans_b=bool(tb), lda=a.shape[1],
+                  ldb=b.shape[1], ldc=n)
+        torch.cuda.synchronize()
+        assert torch.isfinite(c).all().item(), mode
+        comp[mode] = ((c.double() - ref).abs() / bound).max().item()
+        outs[mode] = c
+    assert comp["h3"] <= 2.5 * comp["fp32"] and comp["h3"] < 1e-6, comp
+    # the same with the scales computed by ds2_amax and handed in
+    am_a = torch.zeros(a.shape[0], dtype=torch.int32, device=dev)
+    am_b = torch.zeros(b.shape[0] if tb else b.shape[1], dtype=torch.int32, device=dev)
+    ca = torch.zeros(a.shape[1], dtype=torch.int32, device=dev)
+    if ta:
+        _lib.call("ds2_amax", a.data_ptr(), k, m, m, None, ca.data_ptr(), ops._stream())
+        am_a = ca
+    else:
+        _lib.call("ds2_amax", a.data_ptr(), m, k, k, am_a.data_ptr(), None, ops._stream())
+    if tb:
+        _lib.call("ds2_amax", b.data_ptr(), n, k, k, am_b.data_ptr(), None, ops._stream())
+    else:
+        _lib.call("ds2_amax", b.data_ptr(), k, n, n, None, am_b.data_ptr(), ops._stream())
+    c2 = torch.empty(m, n, device=dev)
+    ops.sgemm(a, b, c2, m=m, n=n, k=k, trans_a=bool(ta), trans_b=bool(tb), lda=a.shape[1],
+              ldb=b.shape[1], ldc=n, a_amax=am_a, b_amax=am_b)
+    torch.cuda.synchronize()
+    assert torch.equal(c2, outs["h3"])
+
+
+@pytest.mark.parametrize("rows,cols", [(1, 4), (37, 52), (16032, 4800), (300, 4100)])
+def test_amax_rows_and_cols(dev, rows, cols):
+    """ds2_amax: row and column maxima of |x| in one pass, bit-exact against torch (float bits;
+    a NaN is skipped, an inf kept), rows alone through the one-wave-per-row kernel too."""
+    g = torch.Generator().manual_seed(rows + cols)
+    x = torch.randn(rows, cols + 8, generator=g) * torch.pow(10.0, torch.rand(rows, 1, generator=g) * 8 - 4)
+    if rows > 3 and cols > 3:
+        x[1, 2] = float('nan')
+        x[2, 3] = float('-inf')
+    x = x.to(dev)
+    view = x[:, :cols]
+    ref = view.abs().nan_to_num(nan=0.0, posinf=float('inf'))
+    r = torch.zeros(rows, dtype=torch.int32, device=dev)
+    c = torch.zeros(cols, dtype=torch.int32, device=dev)
+    _lib.call("ds2_amax", x.data_ptr(), rows, cols, cols + 8, r.data_ptr(), c.data_ptr(),
+              ops._stream())
+    torch.cuda.synchronize()
+    assert torch.equal(r, ref.amax(1).contiguous().view(torch.int32))
+    assert torch.equal(c, ref.amax(0).contiguous().view(torch.int32))
+    r2 = torch.zeros(rows, dtype=torch.int32, device=dev)
+    _lib.call("ds2_amax", x.data_ptr(), rows, cols, cols + 8, r2.data_ptr(), None, ops._stream())
+    torch.cuda.synchronize()
+    assert torch.equal(r2, r)
 
 
 @pytest.mark.parametrize("ta,tb", [(0, 1), (1, 0)])
@@ -124,16 +208,19 @@ def test_sgemm_x6_nonfinite_operands(dev, ta, tb, monkeypatch):
     b[2, 3] = float('inf')
     a, b = a.to(dev), b.to(dev)
     out = {}
-    for mode in ("1", "0"):
-        monkeypatch.setenv("DS2_GEMM_X6", mode)
+    for mode in ("x6", "fp32", "h3"):
+        _gemm_mode(monkeypatch, mode)
         c = torch.empty(m, n, device=dev)
         ops.sgemm(a, b, c, m=m, n=n, k=k, trans_a=bool(ta), trans_b=bool(tb), lda=a.shape[1],
                   ldb=b.shape[1], ldc=n)
         out[mode] = c.cpu()
-    bad1, bad0 = ~torch.isfinite(out["1"]), ~torch.isfinite(out["0"])
-    assert bad0.any() and torch.equal(bad1, bad0)
+    bad0 = ~torch.isfinite(out["fp32"])
+    assert bad0.any()
     fin = ~bad0
-    assert (out["1"][fin] - out["0"][fin]).abs().max().item() <= 1e-4 * out["0"][fin].abs().max().item()
+    for mode in ("x6", "h3"):   # the fp16x3 split: an inf row keeps scale 1, inf - inf = NaN
+        assert torch.equal(~torch.isfinite(out[mode]), bad0), mode
+        assert (out[mode][fin] - out["fp32"][fin]).abs().max().item() <= \
+            1e-4 * out["fp32"][fin].abs().max().item(), mode
 
 
 @pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
@@ -1204,3 +1291,39 @@ def test_colsum(dev, rows, cols, ld, off, accumulate):
     out = out0.to(dev).clone()
     ops.colsum(x.to(dev), rows, cols, ld, out, accumulate=bool(accumulate), off=off)
     _close(out, ref, 1e-6, "colsum")
+
+
+@pytest.mark.parametrize("cell,nd", [("gru", 1), ("gru", 2), ("lstm", 1), ("lstm", 2),
+                                     ("rnn", 1), ("rnn", 2)])
+def test_rnn_param_grads_bf16_shared_copies(dev, cell, nd):
+    """the cfg4 backward's bf16 parameter gradients from operand copies made ONCE per
+    layer (ops._rnn_param_grads_bf16: dW_ih, dW_hh with the per-direction one-step k shift, dX
+    through the concatenated W_ih, bias sums) against the per-GEMM bf16 conversions of
+    sgemm(bf16=True) -- the same bf16 products, only the fp32 summation order (tile plans)
+    differs: 1e-5 of each gradient's max.  N = 16, every size a multiple of 8 (the fast
+    path's condition)."""
+    torch.manual_seed(5)
+    t, n, inp, h = 9, 16, 64, 32
+    g = {"gru": 3 * h, "lstm": 4 * h, "rnn": h}[cell]
+    x = torch.randn(t, n, inp, device=dev)
+    h_all = torch.randn(t, n, nd, h, device=dev)
+    dgx = torch.randn(t, n, nd, g, device=dev)
+    dgh = dgx if cell == "lstm" else torch.randn(t, n, nd, g, device=dev)
+    if cell == "gru":   # the kernels store the same r, z columns in both
+        dgh[..., :2 * h] = dgx[..., :2 * h]
+    weights = []
+    for _ in range(nd):
+        weights += [torch.randn(g, inp, device=dev), torch.randn(g, h, device=dev),
+                    torch.randn(g, device=dev), torch.randn(g, device=dev)]
+    dx_f, gr_f = ops._rnn_param_grads(x, h_all, dgx, dgh, weights, nd, g, True, bf16=True)
+    dx_p, gr_p = ops._rnn_param_grads(x, h_all, dgx, dgh, weights, nd, g, True, bf16=True,
+                                      shared_bf16=False)
+    torch.cuda.synchronize()
+    _close(dx_f, dx_p, 1e-5, "dx")
+    names = ["dw_ih", "dw_hh", "db_ih", "db_hh"]
+    for i, (a, b) in enumerate(zip(gr_f, gr_p)):
+        _close(a, b, 1e-5, f"{names[i % 4]} dir {i // 4}")
+    # and both really are bf16 products: the fp32 path differs by far more than 1e-5
+    _, gr_32 = ops._rnn_param_grads(x, h_all, dgx, dgh, weights, nd, g, True, bf16=False)
+    d = (gr_32[0] - gr_f[0]).abs().max().item() / gr_32[0].abs().max().item()
+    assert d > 1e-4, d

@@ -100,10 +100,41 @@ def test_benchmark_batch_train_step_matches_oracle(dev):
     step masked, the conv biases' gradients are zero in exact arithmetic (BatchNorm follows
     each conv): both sides hold rounding noise, bounded against the conv weight gradient's
     scale."""
-    _check_train_step(dev, [1001] * 32, [150] * 32, seed=13, conv_tol=1e-2, zero_conv_bias=True)
+    _check_train_step(dev, [1001] * 32, [150] * 32, seed=13, conv_tol=1e-2, zero_conv_bias=True,
+                      conv_fp64=True)
 
 
-def _check_train_step(dev, t_list, label_lens, seed, conv_tol=5e-4, zero_conv_bias=False):
+def _conv_block_grads(sd, x, out_lens, g_out, dtype, masks=None):
+    """The oracle's conv block (model.py:208-215 + MaskConv + collapse) in `dtype` on the CPU,
+    backpropagated from the upstream gradient g_out [T', N, 1312]: {conv param name: grad}.
+    masks: the two Hardtanh derivative masks to use instead of the block's own (NCHW bool:
+    where 0 < pre-activation < 20), so that a comparison measures arithmetic, not which
+    near-kink positions a last-bit difference moved across 0 or 20."""
+    o = orc.OracleDS2(sd, 1, 8)
+    o.sd = {k: (v.to(dtype) if v.is_floating_point() else v) for k, v in o.sd.items()}
+    params = {k: v.clone().requires_grad_(True) for k, v in o.parameters().items()
+              if k.startswith('conv.')}
+    o.params = params
+    if masks is None:
+        y = o.conv_block(x.to(dtype), out_lens, training=True)
+    else:
+        it = iter(masks)
+        real = torch.nn.functional.hardtanh
+
+        def htanh_masked(v, lo, hi):   # value of hardtanh, derivative from the given mask
+            mk = next(it).to(v.dtype)
+            return real(v, lo, hi).detach() + mk * (v - v.detach())
+        orc.F.hardtanh = htanh_masked
+        try:
+            y = o.conv_block(x.to(dtype), out_lens, training=True)
+        finally:
+            orc.F.hardtanh = real
+    y.backward(g_out.to(dtype))
+    return {k: v.grad for k, v in params.items()}
+
+
+def _check_train_step(dev, t_list, label_lens, seed, conv_tol=5e-4, zero_conv_bias=False,
+                      conv_fp64=False):
     _threads()
     g = torch.Generator().manual_seed(seed)
     x = _spect_batch(g, t_list, 1001)
@@ -111,9 +142,61 @@ def _check_train_step(dev, t_list, label_lens, seed, conv_tol=5e-4, zero_conv_bi
     tg, tl = _targets(g, label_lens)
     m = _build(123456, 800, 5)
     o = orc.OracleDS2({k: v.detach().clone() for k, v in m.state_dict().items()}, 5, 800)
+    sd0 = {k: v.detach().clone() for k, v in m.state_dict().items()}
     before = {k: v.detach().clone() for k, v in m.named_parameters()}
-    tr = Trainer(m, LABELS, lr=3e-4, momentum=0.9, max_norm=100.0, device=dev)
-    loss = tr.train_batch((x, tg, None, pct.clone(), tl), return_item=True)
+    captured = {}
+    if conv_fp64:
+        # the gradient our recurrent stack hands the conv block and our two conv blocks'
+        # outputs (their Hardtanh masks), for the fp64 check below
+        orig = m.conv.forward_collapsed
+        orig_apply = ops.ConvBlockFn.apply
+        outs = []
+
+        def rec_apply(*a):
+            y = orig_apply(*a)
+            outs.append(y.detach())
+            return y
+
+        def tapped(xx, lens):
+            y = orig(xx, lens)
+            y.register_hook(lambda gr: captured.__setitem__('g', gr.detach().cpu().clone()))
+            return y
+        m.conv.forward_collapsed = tapped
+        ops.ConvBlockFn.apply = rec_apply
+    try:
+        tr = Trainer(m, LABELS, lr=3e-4, momentum=0.9, max_norm=100.0, device=dev)
+        loss = tr.train_batch((x, tg, None, pct.clone(), tl), return_item=True)
+    finally:
+        if conv_fp64:
+            del ops.ConvBlockFn.apply    # back to the inherited Function.apply
+    if conv_fp64:
+        # VERDICT r4 #5a: the conv block's arithmetic against fp64 on the SAME upstream
+        # gradient (ours) and the SAME Hardtanh masks (ours: 0 < y < 20 of our two block
+        # outputs), so the kinks a last-bit difference moves (1 + 3 of 63 M positions between
+        # an fp32 and an fp64 forward, profiles/r4g_bs32_probe.txt) drop out of both sides:
+        # our conv gradients may be at most 2x as far from that fp64 block as the fp32 oracle
+        # block (same masks) is, with a 1e-6 floor.  Measured with each block's own masks
+        # instead, ours sat at 8.3e-4 of conv1.weight's max against the fp32 oracle's 2.8e-4:
+        # flips, not arithmetic.
+        t_, n_ = captured['g'].shape[:2]
+        m1 = (outs[0] > 0) & (outs[0] < 20)
+        y2 = outs[1].view(t_, n_, 32, -1).permute(1, 2, 3, 0)
+        m2 = (y2 > 0) & (y2 < 20)
+        masks = (m1.cpu(), m2.cpu())
+        del outs
+        out_lens = orc.get_seq_lens(orc.input_sizes_quirk(pct, 1001))
+        g64 = _conv_block_grads(sd0, x, out_lens, captured['g'], torch.float64, masks)
+        g32 = _conv_block_grads(sd0, x, out_lens, captured['g'], torch.float32, masks)
+        for name, p in m.named_parameters():
+            if not name.startswith('conv.') or (zero_conv_bias and name.endswith('.bias')
+                                                and p.dim() == 1 and name.replace('.bias', '.weight') in g64
+                                                and g64[name.replace('.bias', '.weight')].dim() == 4):
+                continue
+            ref = g64[name]
+            ours = _rel(p.grad, ref)
+            own = _rel(g32[name], ref)
+            print(f"conv fp64 check {name}: ours {ours:.2e} fp32 oracle {own:.2e}")
+            assert ours <= 2.0 * own + 1e-6, (name, ours, own)
     rloss, rnew, _, rgrads, rnorm = orc.train_step(o, x, pct.clone(), tg, tl)
     assert abs(loss - float(rloss)) <= 1e-4 * abs(float(rloss))
     # the clip norm within 2e-4: every gradient of ours carries the fp32 CTC's rounding (log-space
@@ -391,3 +474,62 @@ def test_cfg4_lstm1024_bf16_gemms_and_batch64_chunks(dev):
     c32 = CTCLoss()(l32.transpose(0, 1).contiguous(), tg[:80], ol, tl[:4])
     c16 = CTCLoss()(l16.transpose(0, 1).contiguous(), tg[:80], ol, tl[:4])
     assert abs(float(c16) - float(c32)) <= 1e-2 * abs(float(c32))
+
+
+@pytest.mark.timeout(900)
+def test_cfg4_full_shape_bf16_step(dev):
+    """BASELINE cfg4 at its own shape (VERDICT r4 #5b): 7 x BiLSTM-1024, batch 64, 10 s
+    (T = 1001 -> T' = 501), the opt-in bf16 RNN GEMMs, through Trainer.train_batch (forward,
+    CTC, BPTT, clip, SGD-Nesterov): every gradient finite; deterministic (the same step from
+    the same state twice: loss, gradients and updated parameters bit-identical); the loss
+    within 1 % of the fp32 HIP path's on the same batch; and a 2-layer slice of the same
+    weights (conv, rnns.0-1, fc) in bf16 mode against the fp32 oracle forward at full length
+    (logits 2e-2, CTC loss 1 %, the existing bf16 bounds)."""
+    _threads()
+    from ds2amd.ctc import CTCLoss
+    g = torch.Generator().manual_seed(404)
+    x = _spect_batch(g, [1001] * 64, 1001)
+    pct = torch.ones(64)
+    tg, tl = _targets(g, [150] * 64)
+    m0 = _build(4040, 1024, 7, rnn_type='lstm')
+    sd0 = {k: v.detach().clone() for k, v in m0.state_dict().items()}
+
+    def step(precision):
+        m = _build(4040, 1024, 7, rnn_type='lstm')
+        m.load_state_dict(sd0)
+        if precision == 'bf16':
+            m.set_rnn_gemm_precision('bf16')
+        tr = Trainer(m, LABELS, lr=3e-4, momentum=0.9, max_norm=400.0, device=dev, verbose=False)
+        loss = tr.train_batch((x, tg, None, pct.clone(), tl), return_item=True)
+        torch.cuda.synchronize()
+        out = (loss, tr.flat.grad[:tr.flat.numel].clone(), tr.flat.flat.clone())
+        del tr, m
+        return out
+
+    l16a, g16a, p16a = step('bf16')
+    assert np.isfinite(l16a) and torch.isfinite(g16a).all().item()
+    l16b, g16b, p16b = step('bf16')
+    assert l16a == l16b and torch.equal(g16a, g16b) and torch.equal(p16a, p16b)
+    del g16b, p16b
+    l32, g32, _ = step('fp32')
+    assert abs(l16a - l32) <= 1e-2 * abs(l32), (l16a, l32)
+    # the bf16 products move the gradients by about their own rounding, not more
+    assert (g16a - g32).norm().item() <= 5e-2 * g32.norm().item()
+    del g16a, g32, p16a
+    # 2-layer slice vs the fp32 oracle, 4 utterances at full length
+    m2 = _build(4040, 1024, 2, rnn_type='lstm')
+    m2.load_state_dict({k: v for k, v in sd0.items() if k in m2.state_dict()})
+    m2 = m2.to(dev).train()
+    m2.set_rnn_gemm_precision('bf16')
+    o2 = orc.OracleDS2({k: v.detach().cpu().clone() for k, v in m2.state_dict().items()}, 2,
+                       1024, rnn_type='lstm')
+    xb, sb = x[:4], torch.full((4,), 1001, dtype=torch.int32)
+    with torch.no_grad():
+        l2, _, ol = m2(xb.to(dev), sb)
+        rl2, _, ro, _ = o2.forward(xb, sb, training=True)
+    assert ol.cpu().tolist() == ro.tolist() == [501] * 4
+    assert _rel(l2, rl2) < 2e-2
+    c16 = CTCLoss()(l2.transpose(0, 1).contiguous(), tg[:600], ol, tl[:4])
+    rc = torch.nn.functional.ctc_loss(rl2.transpose(0, 1).log_softmax(2), tg[:600].long(),
+                                      ro.long(), tl[:4].long(), reduction='sum')
+    assert abs(float(c16) - float(rc)) <= 1e-2 * abs(float(rc))
