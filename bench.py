@@ -51,12 +51,12 @@ CEILING_SOURCE = "profiles/r5b_mfma_ceiling.jsonl"
 def gemm_mode():
     if os.environ.get("DS2_GEMM_X6", "1")[:1] == "0":
         return "fp32"
-    return "h3" if os.environ.get("DS2_GEMM_H3", "0")[:1] == "1" else "x6"
+    return "x6" if os.environ.get("DS2_GEMM_H3", "1")[:1] == "0" else "h3"
 
 
 def gemm_peak():
-    """(peak TFLOP/s, arithmetic) of ds2_sgemm_ws as configured (DS2_GEMM_X6=0: fp32 MFMA;
-    DS2_GEMM_H3=1: the fp16x3 kernel)."""
+    """(peak TFLOP/s, arithmetic) of ds2_sgemm_ws as configured: the fp16x3 kernel by default,
+    DS2_GEMM_H3=0 the bf16x6 kernel, DS2_GEMM_X6=0 fp32 MFMA."""
     mode = gemm_mode()
     if mode == "fp32":
         return PEAK_F32_MFMA_TFLOPS, "fp32 MFMA (v_mfma_f32_16x16x4_f32)"
@@ -274,7 +274,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=3,
                     help="timed oracle training steps of the CPU baseline (after 1 warm-up)")
-    ap.add_argument("--probe", default="ds2_sgemm_ws")
+    ap.add_argument("--probe", default="ds2_sgemm_ws,ds2_sgemm_amax_ws",
+                    help="comma-separated C-ABI entry points timed as the GEMM family")
     ap.add_argument("--input", choices=["spect", "pcm"], default="spect",
                     help="spect: 10 s spectrograms resident in HBM (the headline metric); "
                          "pcm: raw 16 kHz PCM resident in HBM, the device STFT + max_frame "
@@ -316,13 +317,15 @@ def main():
         def featurize():
             return ops.stft_logmag(pcm, ns, n_fft, hop, win, 1, taps, frames).unsqueeze(1)
 
-    probe = KernelProbe(args.probe, sgemm_flops)
+    probe = KernelProbe(tuple(args.probe.split(",")), sgemm_flops)
     probe.install()
     fprobe = KernelProbe(("ds2_gru_fwd",), gru_recurrence_flops)
     fprobe.install()
     bprobe = KernelProbe(("ds2_gru_bwd", "ds2_gru_bwd_bias"), gru_recurrence_flops)
     bprobe.install()
-    probes = (probe, fprobe, bprobe)
+    aprobe = KernelProbe(("ds2_amax",), lambda a: 4.0 * a[1] * a[2])   # bytes read
+    aprobe.install()
+    probes = (probe, fprobe, bprobe, aprobe)
 
     def step():
         inp = x if featurize is None else featurize()
@@ -357,7 +360,7 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
     final_loss = float(loss.item())
-    pk, fk, bk = (p_.summary() for p_ in probes)
+    pk, fk, bk, ak = (p_.summary() for p_ in probes)
 
     if rank == 0:
         audio = world * BATCH * SECONDS * args.steps
@@ -384,7 +387,7 @@ def main():
                  "traffic": None if traffic is None else round(traffic),
                  "traffic_unit": "bytes/launch (HBM, PMC)", "traffic_source": src,
                  "step_achieved_tflops": step_tf}
-            if name == args.probe and gemm_mode() in MEASURED_CEILING:
+            if name == "ds2_sgemm_ws" and gemm_mode() in MEASURED_CEILING:
                 ceil = MEASURED_CEILING[gemm_mode()]
                 e["measured_ceiling"] = ceil
                 e["frac_of_measured_ceiling"] = round(achieved / ceil, 4)
@@ -395,7 +398,20 @@ def main():
             kernels[name] = e
 
         gpeak, garith = gemm_peak()
-        entry(args.probe, pk, gpeak, garith, "mfma", ("gemm", ("splitk_reduce_kernel",)))
+        # the GEMM family: ds2_sgemm_ws and ds2_sgemm_amax_ws (the RNN gradients with shared
+        # fp16x3 operand scales), keyed "ds2_sgemm_ws"
+        entry("ds2_sgemm_ws", pk, gpeak, garith, "mfma", ("gemm", ("splitk_reduce_kernel",)))
+        kernels["ds2_sgemm_ws"]["entry_points"] = args.probe.split(",")
+        if ak is not None:
+            a_ms, a_bytes, a_n = ak
+            kernels["ds2_amax"] = {
+                "bound": "hbm", "kernel": "ds2_amax", "launches": a_n,
+                "launches_per_step": round(a_n / args.steps, 2),
+                "avg_launch_ms": round(a_ms, 5), "ms_per_step": round(a_ms * a_n / args.steps, 3),
+                "achieved": round(a_bytes / (a_ms * 1e-3) / 1e9, 1), "unit": "GB/s",
+                "peak": 8000.0, "frac": round(a_bytes / (a_ms * 1e-3) / 1e9 / 8000.0, 4),
+                "note": "fp16x3 operand row/column maxima shared by the RNN gradient GEMMs "
+                        "(one read of each operand)"}
         x6f = os.environ.get("DS2_GRU_X6", "1")[:1] != "0"
         entry("ds2_gru_fwd", fk, PEAK_X6_TFLOPS if x6f else PEAK_F32_MFMA_TFLOPS,
               "W_hh contraction, bf16x6 (fp32-accurate) on v_mfma_f32_16x16x32_bf16" if x6f
@@ -454,7 +470,7 @@ def main():
         # (exit-time teardown diagnostics, scripts/prof_exit_probe2.sh)
         import gc
         torch.cuda.synchronize()
-        del tr, m, x, probe, fprobe, bprobe, probes
+        del tr, m, x, probe, fprobe, bprobe, aprobe, probes
         gc.collect()
         torch.cuda.empty_cache()
         torch.cuda.synchronize()

@@ -1631,13 +1631,15 @@ static GemmPlan x6_plan(int m, int n, int k, int batch) {
   return plan_bn(m, n, k, batch, n >= 256 ? 160 : 128, device_cus(), XS, 1.0, X2M).p;
 }
 
-// fp16x3 (DS2_GEMM_H3=1, experimental): the x6 kernel's plan and tiles with the operands
-// split into two fp16 terms of row-scaled values and three products per pair (see
-// x2_split_store); the row maxima come from a pre-pass over each operand into the workspace
-// after the split-K slabs
+// fp16x3 (default since round 5; DS2_GEMM_H3=0 selects the bf16x6 kernel): the x6 kernel's
+// plan and tiles with the operands split into two fp16 terms of row-scaled values and three
+// products per pair (see x2_split_store); the row maxima come from the caller
+// (ds2_sgemm_amax_ws) or from a pre-pass over each operand into the workspace after the
+// split-K slabs.  On the step's shapes 1.4-1.7x the bf16x6 kernel's rate at equal or lower
+// error against fp64 (scripts/bench_gemm_h3.py, profiles/r5b_gemm_h3_vs_x6.txt).
 static bool h3_enabled() {
   const char* e = getenv("DS2_GEMM_H3");
-  return e != nullptr && e[0] == '1';
+  return !(e != nullptr && e[0] == '0');
 }
 static size_t h3_ws(int m, int n) { return (size_t)(m + n) * 4 + 512; }
 

@@ -129,8 +129,9 @@ def sgemm(a: torch.Tensor, b: torch.Tensor, c: torch.Tensor, *, m: int, n: int, 
 
 
 def h3_enabled() -> bool:
-    """The fp16x3 GEMM kernel is in use (DS2_GEMM_H3, read by the library per call)."""
-    return os.environ.get("DS2_GEMM_H3", "0")[:1] == "1" and \
+    """The fp16x3 GEMM kernel is in use (the default; DS2_GEMM_H3=0 or DS2_GEMM_X6=0 turn it
+    off -- the library reads the same variables per call)."""
+    return os.environ.get("DS2_GEMM_H3", "1")[:1] != "0" and \
         os.environ.get("DS2_GEMM_X6", "1")[:1] != "0"
 
 

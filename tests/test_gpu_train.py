@@ -187,6 +187,7 @@ def _check_train_step(dev, t_list, label_lens, seed, conv_tol=5e-4, zero_conv_bi
         out_lens = orc.get_seq_lens(orc.input_sizes_quirk(pct, 1001))
         g64 = _conv_block_grads(sd0, x, out_lens, captured['g'], torch.float64, masks)
         g32 = _conv_block_grads(sd0, x, out_lens, captured['g'], torch.float32, masks)
+        bad = []
         for name, p in m.named_parameters():
             if not name.startswith('conv.') or (zero_conv_bias and name.endswith('.bias')
                                                 and p.dim() == 1 and name.replace('.bias', '.weight') in g64
@@ -196,7 +197,9 @@ def _check_train_step(dev, t_list, label_lens, seed, conv_tol=5e-4, zero_conv_bi
             ours = _rel(p.grad, ref)
             own = _rel(g32[name], ref)
             print(f"conv fp64 check {name}: ours {ours:.2e} fp32 oracle {own:.2e}")
-            assert ours <= 2.0 * own + 1e-6, (name, ours, own)
+            if ours > 2.0 * own + 1e-6:
+                bad.append((name, ours, own))
+        assert not bad, bad
     rloss, rnew, _, rgrads, rnorm = orc.train_step(o, x, pct.clone(), tg, tl)
     assert abs(loss - float(rloss)) <= 1e-4 * abs(float(rloss))
     # the clip norm within 2e-4: every gradient of ours carries the fp32 CTC's rounding (log-space
