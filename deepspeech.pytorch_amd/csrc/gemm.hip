@@ -1468,33 +1468,45 @@ __global__ __launch_bounds__(256) void amax_cols_kernel(const float* __restrict_
 }
 
 // Row AND column maxima in one pass (ds2_amax): a block covers 1024 columns (a float4 per
-// thread) of `rpb` rows; column maxima fold in by unsigned atomic max, row maxima by a wave
-// max per row and one atomic per wave (both outputs zeroed first).
+// thread) of `rpb` (<= 64) rows; each thread folds its 4 columns' maxima over the rows in
+// registers and each row's maximum over the block's columns into an LDS word (ds_max_u32), and
+// the block then folds both into the outputs with unsigned atomic max (both zeroed first).
 __global__ __launch_bounds__(256) void amax_both_kernel(const float* __restrict__ p, int rows,
                                                         int cols, int64_t ld, int rpb,
                                                         unsigned* __restrict__ rmax,
                                                         unsigned* __restrict__ cmax) {
+  __shared__ unsigned rm[64];
   const int c = (blockIdx.x * 256 + threadIdx.x) * 4;
   const bool in = c < cols;
   const int r0 = blockIdx.y * rpb, r1 = min(rows, r0 + rpb);
+  if (threadIdx.x < 64) rm[threadIdx.x] = 0u;
+  __syncthreads();
   f32x4 m = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int r = r0; r < r1; ++r) {
-    f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (in) v = *reinterpret_cast<const f32x4*>(p + (int64_t)r * ld + c);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) m[e] = fmaxf(m[e], fabsf(v[e]));
-    if (rmax != nullptr) {
-      float w = fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3])));
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) w = fmaxf(w, __shfl_xor(w, o));
-      if ((threadIdx.x & 63) == 0 && w > 0.f) atomicMax(rmax + r, __float_as_uint(w));
+  if (in) {
+    for (int r = r0; r < r1; ++r) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(p + (int64_t)r * ld + c);
+      const float a0 = fabsf(v[0]), a1 = fabsf(v[1]), a2 = fabsf(v[2]), a3 = fabsf(v[3]);
+      m[0] = fmaxf(m[0], a0);
+      m[1] = fmaxf(m[1], a1);
+      m[2] = fmaxf(m[2], a2);
+      m[3] = fmaxf(m[3], a3);
+      if (rmax != nullptr) {
+        const float w = fmaxf(fmaxf(a0, a1), fmaxf(a2, a3));
+        if (w > 0.f) atomicMax(&rm[r - r0], __float_as_uint(w));
+      }
     }
   }
   if (cmax != nullptr && in) {
-    const float me[4] = {m[0], m[1], m[2], m[3]};   // see amax_cols_kernel
+    // (each element copied to a scalar first: hipcc 7.2 bit_cast an ext_vector element
+    // straight into the atomic's data as element 0 for every e)
+    const float me[4] = {m[0], m[1], m[2], m[3]};
 #pragma unroll
     for (int e = 0; e < 4; ++e)
       if (me[e] > 0.f) atomicMax(cmax + c + e, __float_as_uint(me[e]));
+  }
+  if (rmax != nullptr) {
+    __syncthreads();
+    if (threadIdx.x < r1 - r0 && rm[threadIdx.x] != 0u) atomicMax(rmax + r0 + threadIdx.x, rm[threadIdx.x]);
   }
 }
 
@@ -1658,7 +1670,7 @@ extern "C" ds2_status_t ds2_amax(const float* x, int rows, int cols, int64_t ld,
   if (row_amax != nullptr) (void)hipMemsetAsync(row_amax, 0, (size_t)rows * 4, st);
   (void)hipMemsetAsync(col_amax, 0, (size_t)cols * 4, st);
   const int cb = cdiv(cols, 1024);
-  const int rpb = std::max(16, cdiv((int64_t)rows * cb, 1024));
+  const int rpb = std::min(64, std::max(16, cdiv((int64_t)rows * cb, 2048)));
   hipLaunchKernelGGL(amax_both_kernel, dim3(cb, cdiv(rows, rpb)), dim3(256), 0, st, x, rows, cols,
                      ld, rpb, row_amax, col_amax);
   return launch_status("ds2_amax");

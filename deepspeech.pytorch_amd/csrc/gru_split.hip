@@ -63,6 +63,52 @@ __device__ __forceinline__ f32x4 mma6(const Tri& a, const Tri& b, f32x4 c) {
   return c;
 }
 
+// fp16x3 (the forward's default since round 5): a value x of a row scaled by 2^e into
+// [2^14, 2^15) splits into hi = f16(x 2^e) and lo = f16(x 2^e - hi) (22 significant bits
+// kept for every element within 2^17 of the row's max), and a.b takes three products
+// lo.hi + hi.lo + hi.hi on v_mfma_f32_16x16x32_f16 (each exact in fp32): half the MFMAs of
+// the bf16x6 form and two operand planes instead of three.  h (|h| <= 1) takes the fixed
+// scale 2^14; each W_hh row (gate, unit) its own, found at kernel start.
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2h __attribute__((ext_vector_type(2)));
+struct Duo {
+  f16x8 hi, lo;
+};
+
+// 8 fp32 values (k slots 0..3 from a, 4..7 from b) times sc -> fp16 (hi, lo)
+__device__ __forceinline__ Duo split2h(const f32x4 a, const f32x4 b, float sc) {
+  typedef float f32x2v __attribute__((ext_vector_type(2)));
+  Duo t;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const f32x2v x = (j < 2 ? f32x2v{a[2 * j], a[2 * j + 1]} : f32x2v{b[2 * j - 4], b[2 * j - 3]}) * sc;
+    const f16x2h h = __builtin_convertvector(x, f16x2h);
+    const f16x2h l = __builtin_convertvector(x - __builtin_convertvector(h, f32x2v), f16x2h);
+    t.hi[2 * j] = h[0];
+    t.hi[2 * j + 1] = h[1];
+    t.lo[2 * j] = l[0];
+    t.lo[2 * j + 1] = l[1];
+  }
+  return t;
+}
+
+// c += a.b from the fp16 terms (small terms first)
+__device__ __forceinline__ f32x4 mma3h(const Duo& a, const Duo& b, f32x4 c) {
+  c = __builtin_amdgcn_mfma_f32_16x16x32_f16(a.lo, b.hi, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_f16(a.hi, b.lo, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_f16(a.hi, b.hi, c, 0, 0, 0);
+  return c;
+}
+
+// 2^e scale of a row whose max |x| is m (m > 0 finite: m 2^e in [2^14, 2^15); else 1)
+__device__ __forceinline__ int h3_row_exp(float m) {
+  const unsigned u = __float_as_uint(m);
+  const int E = (int)(u >> 23);
+  if (u == 0u || E >= 255) return 0;
+  const int e = 14 - ((E == 0 ? 1 : E) - 127);
+  return e > 127 ? 127 : e;
+}
+
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
@@ -103,7 +149,7 @@ __device__ __forceinline__ void pair_split(int pairs, int wave, int& p0, int& np
 // ---------------------------------------------------------------------------------------
 // forward: gh[16 samples x 48] = h_{t-1}[16 x H] . W_hh[r, z, n rows of 16 units]^T, with
 // the sentinel-ring hand-off of gru_fwd_dop_kernel (the data is the flag).
-template <int NP>
+template <int NP, bool H3 = false>
 __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(1, 1))) void gru_fwd_x6_kernel(
     int T, int N, int H, int D, int UB, int BT, const float* __restrict__ xproj,
     const float* __restrict__ w_f, const float* __restrict__ w_r, const float* __restrict__ b_f,
@@ -151,21 +197,69 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
 
   // W_hh split fragments: pair p, gate g, k slot j -> W[g H + 16 ub + (lane & 15)]
   //   [16 (t_first + 2p + (j >> 2)) + 4 (lane >> 4) + (j & 3)]
-  Tri w[3][NP];
+  using WT = typename std::conditional<H3, Duo, Tri>::type;
+  WT w[3][NP];
+  // fp16x3: 2^-(e(g, unit) + 14) undoes the row scale of W_hh and the fixed 2^14 of h; the
+  // owner thread's unit u = threadIdx.x & 15
+  float unscale[3] = {1.f, 1.f, 1.f};
   {
     const float* W = d == 0 ? w_f : w_r;
     const float* wr = W + (int64_t)(ub * GU + (lane & 15)) * H + 4 * (lane >> 4);
-#pragma unroll
-    for (int p = 0; p < NP; ++p) {
+    auto frag = [&](int p, int g, f32x4& a, f32x4& b) {
       const int ta = t_first + 2 * p, tb = ta + 1;
+      const float* wg = wr + (int64_t)g * H * H;
+      const f32x4 z4 = f32x4{0.f, 0.f, 0.f, 0.f};
+      a = (p < np && ta < UB) ? *reinterpret_cast<const f32x4*>(wg + 16 * ta) : z4;
+      b = (p < np && tb < UB) ? *reinterpret_cast<const f32x4*>(wg + 16 * tb) : z4;
+    };
+    if constexpr (H3) {
+      // max |W| of each (gate, unit) row over the whole K: the lane's share, the 4 lanes
+      // of its unit, then the workgroup's waves (LDS, reusing `red`)
+      float mx[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+      for (int p = 0; p < NP; ++p)
+#pragma unroll
+        for (int g = 0; g < 3; ++g) {
+          f32x4 a, b;
+          frag(p, g, a, b);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) mx[g] = fmaxf(mx[g], fmaxf(fabsf(a[j]), fabsf(b[j])));
+        }
 #pragma unroll
       for (int g = 0; g < 3; ++g) {
-        const float* wg = wr + (int64_t)g * H * H;
-        const f32x4 z4 = f32x4{0.f, 0.f, 0.f, 0.f};
-        const f32x4 a = (p < np && ta < UB) ? *reinterpret_cast<const f32x4*>(wg + 16 * ta) : z4;
-        const f32x4 b = (p < np && tb < UB) ? *reinterpret_cast<const f32x4*>(wg + 16 * tb) : z4;
-        w[g][p] = split3(a, b);
+        mx[g] = fmaxf(mx[g], __shfl_xor(mx[g], 16));
+        mx[g] = fmaxf(mx[g], __shfl_xor(mx[g], 32));
+        if (lane < 16) red[(wave * 3 + g) * 16 + lane] = mx[g];
       }
+      __syncthreads();
+      int eg[3];
+#pragma unroll
+      for (int g = 0; g < 3; ++g) {
+        float m = 0.f;
+#pragma unroll
+        for (int w8 = 0; w8 < XW; ++w8) m = fmaxf(m, red[(w8 * 3 + g) * 16 + (lane & 15)]);
+        eg[g] = h3_row_exp(m);
+        // the owner thread's unit is threadIdx.x & 15 = lane & 15: the same row
+        unscale[g] = __builtin_ldexpf(1.f, -(eg[g] + 14));
+      }
+      __syncthreads();
+#pragma unroll
+      for (int p = 0; p < NP; ++p)
+#pragma unroll
+        for (int g = 0; g < 3; ++g) {
+          f32x4 a, b;
+          frag(p, g, a, b);
+          w[g][p] = split2h(a, b, __builtin_ldexpf(1.f, eg[g]));
+        }
+    } else {
+#pragma unroll
+      for (int p = 0; p < NP; ++p)
+#pragma unroll
+        for (int g = 0; g < 3; ++g) {
+          f32x4 a, b;
+          frag(p, g, a, b);
+          w[g][p] = split3(a, b);
+        }
     }
   }
   const float* bh = d == 0 ? b_f : b_r;
@@ -241,9 +335,15 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
 #pragma unroll
         for (int p = 0; p < NP; ++p) {
           if (((pend >> p) & 1u) && wave_ready(hv[2 * p]) && wave_ready(hv[2 * p + 1])) {
-            const Tri a = split3(hv[2 * p], hv[2 * p + 1]);
+            if constexpr (H3) {
+              const Duo a = split2h(hv[2 * p], hv[2 * p + 1], 16384.f);
 #pragma unroll
-            for (int g = 0; g < 3; ++g) pacc[p][g] = mma6(a, w[g][p], pacc[p][g]);
+              for (int g = 0; g < 3; ++g) pacc[p][g] = mma3h(a, w[g][p], pacc[p][g]);
+            } else {
+              const Tri a = split3(hv[2 * p], hv[2 * p + 1]);
+#pragma unroll
+              for (int g = 0; g < 3; ++g) pacc[p][g] = mma6(a, w[g][p], pacc[p][g]);
+            }
             pend &= ~(1u << p);
           }
         }
@@ -292,7 +392,7 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
         float v = 0.f;
 #pragma unroll
         for (int w8 = 0; w8 < XW; ++w8) v += red[(w8 * GB + m) * RP + g * GU + u];
-        gh[g] = v;
+        gh[g] = H3 ? v * unscale[g] : v;
       }
       const float ghr = gh[0] + bias_r;
       const float ghz = gh[1] + bias_z;
@@ -597,9 +697,18 @@ static inline bool x6_enabled() {
   return !(e != nullptr && e[0] == '0');
 }
 
+// the forward's W_hh product on fp16x3 (default since round 5; DS2_GRU_H3=0 keeps bf16x6)
+static inline bool fwd_h3_enabled() {
+  const char* e = getenv("DS2_GRU_H3");
+  return !(e != nullptr && e[0] == '0');
+}
+
 static const void* fwd_x6_fn(int need) {
-#define DS2_FX6(K) \
-  if (need <= K) return reinterpret_cast<const void*>(gru_fwd_x6_kernel<K>);
+  const bool h3 = fwd_h3_enabled();
+#define DS2_FX6(K)                                                                  \
+  if (need <= K)                                                                    \
+    return h3 ? reinterpret_cast<const void*>(gru_fwd_x6_kernel<K, true>)           \
+              : reinterpret_cast<const void*>(gru_fwd_x6_kernel<K, false>);
   DS2_FX6(1) DS2_FX6(2) DS2_FX6(3) DS2_FX6(4) DS2_FX6(5) DS2_FX6(6) DS2_FX6(7)
 #undef DS2_FX6
   return nullptr;
