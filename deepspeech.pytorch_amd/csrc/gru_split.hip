@@ -687,6 +687,307 @@ __global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
 }
 
 // ---------------------------------------------------------------------------------------
+// backward on fp16x3 (default since round 5; DS2_GRU_H3_BWD=0 keeps the bf16x6 kernel
+// above).  The same work, groups and flag hand-off as gru_bwd_x6_kernel, but each producer
+// publishes ONE record per step: its three gate-gradient tiles (dar, daz, dghn of 16
+// samples x 16 units), every sample row scaled by its own 2^e (e from the row's max over
+// the 48 values) and split into fp16 (hi, lo) in the consumers' MFMA operand order, plus the
+// 16 row factors 2^-e:
+//   [0, 1 KB)  hi of r, z: lane L = (m, q) holds r[m][4q..4q+3], z[m][4q..4q+3]
+//   [1, 2 KB)  lo of r, z, same order
+//   [2, 3 KB)  n: lane L holds hi n[m][4q..4q+3], lo n[m][4q..4q+3]
+//   [3 KB, +64 B)  2^-e of the 16 rows
+// (3.06 KB per producer and step instead of 4.5 KB of pre-split bf16 runs).  A consumer
+// multiplies each producer's record with its W_hh^T fragments -- the r, z pair as three
+// v_mfma_f32_16x16x32_f16, the n tile as three v_mfma_f32_16x16x16_f16, one temporary -- and
+// adds the temporary into its sum row-scaled by the producer's 2^-e: the products of one
+// producer share their rows' scales, so the scale applies after the MFMAs.  W_hh^T is
+// scaled per column (unit) by 2^e found at kernel start and undone on the reduced sum.
+constexpr int HBR = 784;   // floats per producer record (3 x 256 + 16)
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+template <int NPW>
+__global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(2, 2))) void gru_bwd_h3_kernel(
+    int T, int N, int H, int D, int UB, int BT, const float* __restrict__ dy, int dyd,
+    const float* __restrict__ w_f, const float* __restrict__ w_r,
+    const float* __restrict__ h_all, const float* __restrict__ gates,
+    const int* __restrict__ lens, float* __restrict__ dgx, float* __restrict__ dgh,
+    float* __restrict__ gx, unsigned* __restrict__ counters, unsigned* __restrict__ err,
+    unsigned long long* __restrict__ stamps, double* __restrict__ dbp, int xmode) {
+  static_assert(NPW <= 8, "producers per wave");
+  constexpr int RP = GU + 1;
+  constexpr int LWP = NPW < 3 ? NPW : 3;        // producers' records in flight per wave
+  constexpr int RED = BW * GB * RP > 8 * GB * GU ? BW * GB * RP : 8 * GB * GU;
+  __shared__ __attribute__((aligned(8))) float red[RED];
+  __shared__ __attribute__((aligned(16))) _Float16 stg[3 * 64 * 8];   // the record published
+  __shared__ __attribute__((aligned(16))) float stsc[GB];
+  __shared__ int flag;
+  int ub, d, bt;
+  const bool xg = xmode != 0;
+  if (xg ? !map_work_xgrp(UB, BT, D, ub, d, bt) : !map_work(UB * D, BT, UB, ub, d, bt)) return;
+  const int n0 = bt * GB;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int H3 = 3 * H;
+  unsigned* xtab = counters + (D * BT + 1) + D * BT * 64 + (d * BT + bt) * 64;
+  const unsigned my_xcc = xcc_id() + 1u;
+  if (xg && threadIdx.x == 0)   // published by the step-0 flag (wave 0 drains before it)
+    __hip_atomic_store(xtab + ub, my_xcc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  uint32_t psame = 0;           // bit p: producer p0 + p shares this XCD
+  const int p0 = (UB * wave) / BW;
+  const int np = (UB * (wave + 1)) / BW - p0;      // host guarantees np <= NPW
+  const unsigned* gflags = counters + (D * BT + 1) + (d * BT + bt) * UB;
+  unsigned* myflag = counters + (D * BT + 1) + (d * BT + bt) * UB + ub;
+  const int slot_floats = D * BT * UB * HBR;
+  const __amdgpu_buffer_rsrc_t x_rs = __builtin_amdgcn_make_buffer_rsrc(
+      gx, (short)0, (xg ? 4 : 2) * slot_floats * 4, 0x00020000);
+  const int grp_off = (d * BT + bt) * UB * HBR;
+  const int aoff = 2 * slot_floats * 4;   // the plain-store copies (xmode)
+  const bool tracing = stamps != nullptr && threadIdx.x == 0;
+  auto trace_at = [&](int s, int p) {
+    if (tracing && s >= kXTraceS0 && s < kXTraceS0 + kXTraceSteps)
+      stamps[((int64_t)(s - kXTraceS0) * gridDim.x + blockIdx.x) * 5 + p] =
+          __builtin_amdgcn_s_memrealtime();
+  };
+
+  // W_hh^T fragments of producer p (unit block pb = p0 + p), lane (u = lane & 15, q = lane >> 4):
+  // pair slot j -> W_hh[(j >> 2) H + 16 pb + 4 q + (j & 3)][16 ub + u] (gates r, z), single
+  // slot j -> W_hh[2 H + 16 pb + 4 q + j][16 ub + u] (gate n); column u scaled by 2^e(u)
+  Duo wrz[NPW];
+  f16x4 wnh[NPW], wnl[NPW];
+  float unscale = 1.f;   // 2^-e(u) of the owner's unit (threadIdx.x & 15 = lane & 15)
+  {
+    const float* W = d == 0 ? w_f : w_r;
+    const float* wc = W + ub * GU + (lane & 15);
+    const int q4 = 4 * (lane >> 4);
+    auto wv = [&](int g, int p, int j) {
+      return p < np ? wc[(int64_t)(g * H + 16 * (p0 + p) + q4 + j) * H] : 0.f;
+    };
+    float mx = 0.f;
+#pragma unroll
+    for (int p = 0; p < NPW; ++p)
+#pragma unroll
+      for (int g = 0; g < 3; ++g)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) mx = fmaxf(mx, fabsf(wv(g, p, j)));
+    mx = fmaxf(mx, __shfl_xor(mx, 16));
+    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    if (lane < 16) red[wave * 16 + lane] = mx;
+    __syncthreads();
+    float m = 0.f;
+#pragma unroll
+    for (int w8 = 0; w8 < BW; ++w8) m = fmaxf(m, red[w8 * 16 + (lane & 15)]);
+    const int eu = h3_row_exp(m);
+    unscale = __builtin_ldexpf(1.f, -eu);
+    const float sc = __builtin_ldexpf(1.f, eu);
+    __syncthreads();
+#pragma unroll
+    for (int p = 0; p < NPW; ++p) {
+      f32x4 a, b, c;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        a[j] = wv(0, p, j);
+        b[j] = wv(1, p, j);
+        c[j] = wv(2, p, j);
+      }
+      wrz[p] = split2h(a, b, sc);
+      const Duo dn = split2h(c, c, sc);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        wnh[p][j] = dn.hi[j];
+        wnl[p][j] = dn.lo[j];
+      }
+    }
+  }
+  const int m = (threadIdx.x >> 4) & 15;
+  const int u = threadIdx.x & 15;
+  const int n = n0 + m;
+  const int j = ub * GU + u;
+  const bool gate_thread = threadIdx.x < GB * GU;
+  const bool owner = gate_thread && n < N;
+  int len = owner ? lens[n] : 0;
+  settle(len);
+  // this thread's slots in the staged record: consumer lane m + 16 (u >> 2), k slot u & 3
+  const int sL = (m + 16 * (u >> 2)) * 8 + (u & 3);
+  float dh_prev = 0.f, z_prev = 0.f;
+  float px_dar = 0.f, px_daz = 0.f, px_dan = 0.f, px_dghn = 0.f;
+  int64_t px_row = -1;
+  double sb_r = 0.0, sb_z = 0.0, sb_n = 0.0, sb_hn = 0.0;
+  for (int s = 0; s < T; ++s) {
+    const int t = d == 0 ? T - 1 - s : s;
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+    float dyv = 0.f, g_r = 0.f, g_z = 0.f, g_n = 0.f, g_hn = 0.f, hp = 0.f;
+    const int64_t row = ((int64_t)t * N + n) * D + d;
+    if (owner && t < len) {
+      dyv = dy[(((int64_t)t * N + n) * dyd + (dyd > 1 ? d : 0)) * H + j];
+      const float* gp = gates + row * 4 * H;
+      g_r = gp[j];
+      g_z = gp[H + j];
+      g_n = gp[2 * H + j];
+      g_hn = gp[3 * H + j];
+      const int tp = d == 0 ? t - 1 : t + 1;
+      if (tp >= 0 && tp < T) hp = h_all[(((int64_t)tp * N + n) * D + d) * H + j];
+    }
+    trace_at(s, 0);
+    if (s > 0) {
+      if (!flags_wait(gflags, UB, (unsigned)s, err, &flag)) {
+        poison_rest(dgx, s, T, d == 0, N, D, n, d, H, j, H3, 3, owner);
+        return;
+      }
+      trace_at(s, 1);
+      if (xg && s == 1) {   // which producers share this XCD (their ids came with step 0)
+        const unsigned v = lane < UB ? __hip_atomic_load(xtab + lane, __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT) : 0u;
+        const unsigned long long same = __ballot(v == my_xcc);
+#pragma unroll
+        for (int p = 0; p < NPW; ++p)
+          if ((same >> (p0 + p)) & 1ull) psame |= 1u << p;
+      }
+      const int rb = ((s - 1) & 1) * slot_floats + grp_off;
+      u32x4 r0[NPW], r1[NPW], r2[NPW];
+      f32x4 rs[NPW];
+      auto load_rec = [&](int p) {
+        const bool ok = p < np;
+        const int base = (rb + (p0 + p) * HBR) * 4 + (((psame >> p) & 1u) ? aoff : 0);
+        r0[p] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                              x_rs, ok ? base + lane * 16 : 0x7ffffff0, 0, kSc1));
+        r1[p] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                              x_rs, ok ? base + 1024 + lane * 16 : 0x7ffffff0, 0, kSc1));
+        r2[p] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                              x_rs, ok ? base + 2048 + lane * 16 : 0x7ffffff0, 0, kSc1));
+        rs[p] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                              x_rs, ok ? base + 3072 + (lane >> 4) * 16 : 0x7ffffff0, 0, kSc1));
+      };
+#pragma unroll
+      for (int p = 0; p < LWP; ++p) load_rec(p);
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int p = 0; p < NPW; ++p) {
+        if (p + LWP < NPW) load_rec(p + LWP);
+        if (p < np) {
+          f32x4 tmp = f32x4{0.f, 0.f, 0.f, 0.f};
+          const f16x8 ahi = __builtin_bit_cast(f16x8, r0[p]);
+          const f16x8 alo = __builtin_bit_cast(f16x8, r1[p]);
+          tmp = __builtin_amdgcn_mfma_f32_16x16x32_f16(alo, wrz[p].hi, tmp, 0, 0, 0);
+          tmp = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, wrz[p].lo, tmp, 0, 0, 0);
+          tmp = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, wrz[p].hi, tmp, 0, 0, 0);
+          const f16x4 nh = __builtin_bit_cast(f16x4, u32x2{r2[p][0], r2[p][1]});
+          const f16x4 nl = __builtin_bit_cast(f16x4, u32x2{r2[p][2], r2[p][3]});
+          tmp = __builtin_amdgcn_mfma_f32_16x16x16f16(nl, wnh[p], tmp, 0, 0, 0);
+          tmp = __builtin_amdgcn_mfma_f32_16x16x16f16(nh, wnl[p], tmp, 0, 0, 0);
+          tmp = __builtin_amdgcn_mfma_f32_16x16x16f16(nh, wnh[p], tmp, 0, 0, 0);
+          acc += tmp * rs[p];   // rows 4 (lane >> 4) + i: the producer's 2^-e of those rows
+        }
+      }
+      trace_at(s, 2);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      red[(wave * GB + (lane >> 4) * 4 + r) * RP + (lane & 15)] = acc[r];
+    settle(dyv);
+    settle(g_r);
+    settle(g_z);
+    settle(g_n);
+    settle(g_hn);
+    settle(hp);
+    __syncthreads();
+    trace_at(s, 3);
+    float dar = 0.f, daz = 0.f, dan = 0.f, dghn = 0.f;
+    if (owner) {
+      float dh = 0.f, zc = 0.f;
+      if (t < len) {
+        float carry = 0.f;
+        if (s > 0) {
+          float rec = 0.f;
+#pragma unroll
+          for (int w8 = 0; w8 < BW; ++w8) rec += red[(w8 * GB + m) * RP + u];
+          carry = dh_prev * z_prev + rec * unscale;
+        }
+        dh = dyv + carry;
+        zc = g_z;
+        dan = dh * (1.f - zc) * (1.f - g_n * g_n);
+        daz = dh * (hp - g_n) * zc * (1.f - zc);
+        dar = dan * g_hn * g_r * (1.f - g_r);
+        dghn = dan * g_r;
+      }
+      dh_prev = dh;
+      z_prev = zc;
+      px_dar = dar; px_daz = daz; px_dan = dan; px_dghn = dghn; px_row = row;
+      sb_r += dar; sb_z += daz; sb_n += dan; sb_hn += dghn;
+    }
+    if (gate_thread) {
+      // the row's scale: max over the sample's 16 units x 3 gates (16 consecutive lanes)
+      float mx = fmaxf(fmaxf(fabsf(dar), fabsf(daz)), fabsf(dghn));
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+      const int e = h3_row_exp(mx);
+      const float sc = __builtin_ldexpf(1.f, e);
+      const float vr = dar * sc, vz = daz * sc, vn = dghn * sc;
+      const _Float16 hr = (_Float16)vr, hz = (_Float16)vz, hn = (_Float16)vn;
+      stg[sL] = hr;
+      stg[sL + 4] = hz;
+      stg[512 + sL] = (_Float16)(vr - (float)hr);
+      stg[512 + sL + 4] = (_Float16)(vz - (float)hz);
+      stg[1024 + sL] = hn;
+      stg[1024 + sL + 4] = (_Float16)(vn - (float)hn);
+      if (u == 0) stsc[m] = __builtin_ldexpf(1.f, -e);
+    }
+    __syncthreads();
+    if (wave == 0) {
+      const int so = ((s & 1) * slot_floats + grp_off + ub * HBR) * 4;
+      const u32x4 v0 = *reinterpret_cast<const u32x4*>(stg + lane * 8);
+      const u32x4 v1 = *reinterpret_cast<const u32x4*>(stg + 512 + lane * 8);
+      const u32x4 v2 = *reinterpret_cast<const u32x4*>(stg + 1024 + lane * 8);
+      __builtin_amdgcn_raw_buffer_store_b128(v0, x_rs, so + lane * 16, 0, kSc1);
+      __builtin_amdgcn_raw_buffer_store_b128(v1, x_rs, so + 1024 + lane * 16, 0, kSc1);
+      __builtin_amdgcn_raw_buffer_store_b128(v2, x_rs, so + 2048 + lane * 16, 0, kSc1);
+      if (xg) {   // plain copies: stay in this XCD's L2 for the same-XCD consumers
+        __builtin_amdgcn_raw_buffer_store_b128(v0, x_rs, aoff + so + lane * 16, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(v1, x_rs, aoff + so + 1024 + lane * 16, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(v2, x_rs, aoff + so + 2048 + lane * 16, 0, 0);
+      }
+      if (lane < 4) {
+        const u32x4 vs = *reinterpret_cast<const u32x4*>(stsc + lane * 4);
+        __builtin_amdgcn_raw_buffer_store_b128(vs, x_rs, so + 3072 + lane * 16, 0, kSc1);
+        if (xg) __builtin_amdgcn_raw_buffer_store_b128(vs, x_rs, aoff + so + 3072 + lane * 16, 0, 0);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0)
+        __hip_atomic_store(myflag, (unsigned)s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    trace_at(s, 4);
+    if (owner) {
+      float* gxr = dgx + px_row * H3;
+      gxr[j] = px_dar;
+      gxr[H + j] = px_daz;
+      gxr[2 * H + j] = px_dan;
+      float* ghr = dgh + px_row * H3;
+      ghr[j] = px_dar;
+      ghr[H + j] = px_daz;
+      ghr[2 * H + j] = px_dghn;
+    }
+  }
+  if (dbp == nullptr) return;
+  // the workgroup's 16 samples summed per unit in sample order -> dbp[bt][d][4][H]
+  double* rd = reinterpret_cast<double*>(red);
+  __syncthreads();
+  if (gate_thread) {
+    rd[(0 * GB + m) * GU + u] = owner ? sb_r : 0.0;
+    rd[(1 * GB + m) * GU + u] = owner ? sb_z : 0.0;
+    rd[(2 * GB + m) * GU + u] = owner ? sb_n : 0.0;
+    rd[(3 * GB + m) * GU + u] = owner ? sb_hn : 0.0;
+  }
+  __syncthreads();
+  if (threadIdx.x < 4 * GU) {
+    const int g = threadIdx.x / GU, uu = threadIdx.x - (threadIdx.x / GU) * GU;
+    double a = 0.0;
+#pragma unroll
+    for (int mm = 0; mm < GB; ++mm) a += rd[(g * GB + mm) * GU + uu];
+    dbp[(((int64_t)bt * D + d) * 4 + g) * H + ub * GU + uu] = a;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 // host launchers (called by ds2_gru_fwd / ds2_gru_bwd in gru.hip with their workspace
 // carve-up); false = shape not covered (caller falls back to the fp32-MFMA kernels)
 
@@ -759,6 +1060,22 @@ int gru_bwd_x6_grid(int n, int h, int num_dirs) {
                                       : mapped_grid(UB * num_dirs, BT);
 }
 
+// the backward's W_hh^T product on fp16x3 (default since round 5; DS2_GRU_H3_BWD=0 keeps
+// the bf16x6 pre-split kernel)
+static inline bool bwd_h3_enabled() {
+  const char* e = getenv("DS2_GRU_H3_BWD");
+  return !(e != nullptr && e[0] == '0');
+}
+
+static const void* bwd_h3_fn(int UB) {
+  const int need = (UB + BW - 1) / BW;
+#define DS2_BH3(K) \
+  if (need <= K) return reinterpret_cast<const void*>(gru_bwd_h3_kernel<K>);
+  DS2_BH3(1) DS2_BH3(2) DS2_BH3(3) DS2_BH3(4) DS2_BH3(5) DS2_BH3(6) DS2_BH3(7) DS2_BH3(8)
+#undef DS2_BH3
+  return nullptr;
+}
+
 bool launch_gru_bwd_x6(int t_max, int n, int h, int num_dirs, const float* dy, int dy_dirs,
                        const float* w_hh_f, const float* w_hh_r, const float* h_all,
                        const float* gates, const int* lens, float* dgates_x, float* dgates_h,
@@ -768,7 +1085,8 @@ bool launch_gru_bwd_x6(int t_max, int n, int h, int num_dirs, const float* dy, i
   apply_spin_limit_env();
   apply_rnn_tune_env();
   const int UB = h / GU, BT = (n + GB - 1) / GB;
-  const void* fn = bwd_x6_fn((3 * UB + 1) / 2);
+  const void* fn = bwd_h3_enabled() ? bwd_h3_fn(UB) : nullptr;
+  if (fn == nullptr) fn = bwd_x6_fn((3 * UB + 1) / 2);
   if (fn == nullptr) return false;
   int XM_ = xcd_groups(UB, BT, num_dirs) ? 1 : 0;
   const int grid = XM_ ? xgrp_grid(UB, BT, num_dirs) : mapped_grid(UB * num_dirs, BT);

@@ -532,13 +532,14 @@ def test_gru_bf16x6_matches_fp32_mfma(dev, n, h, bidir, monkeypatch):
     direct-operand kernels (DS2_GRU_X6=0): equal within fp32 rounding (different summation
     order; odd UB = 49 included: the last 32-k pair is half empty)."""
     nd = 2 if bidir else 1
-    env = [{"DS2_GRU_X6": "0"}, {"DS2_GRU_X6": "1", "DS2_GRU_H3": "0"},
-           {"DS2_GRU_X6": "1", "DS2_GRU_H3": "1"}]
+    env = [{"DS2_GRU_X6": "0"},
+           {"DS2_GRU_X6": "1", "DS2_GRU_H3": "0", "DS2_GRU_H3_BWD": "0"},
+           {"DS2_GRU_X6": "1", "DS2_GRU_H3": "1", "DS2_GRU_H3_BWD": "1"}]
     f32, x6, h3 = _gru_run(dev, n, 41, 40, h, nd, h + 7 * n, env, monkeypatch)
     for a, b, c in zip(f32, x6, h3):
         assert torch.isfinite(b).all() and torch.isfinite(c).all()
         _close(b, a, 2e-5, "bf16x6 vs fp32 MFMA")
-        _close(c, a, 2e-5, "fp16x3 forward vs fp32 MFMA")
+        _close(c, a, 2e-5, "fp16x3 recurrences vs fp32 MFMA")
 
 
 def _gru_run(dev, n, t, inp, h, nd, seed, env, monkeypatch, amp=None):
@@ -564,14 +565,19 @@ def _gru_run(dev, n, t, inp, h, nd, seed, env, monkeypatch, amp=None):
     return outs
 
 
+@pytest.mark.parametrize("kern", ["h3", "x6"])
 @pytest.mark.parametrize("n,h,bidir", [(32, 800, True), (7, 48, False), (17, 784, True),
                                        (33, 256, True), (16, 1024, True), (64, 256, False)])
-def test_gru_xcd_groups_bit_identical(dev, n, h, bidir, monkeypatch):
+def test_gru_xcd_groups_bit_identical(dev, n, h, bidir, kern, monkeypatch):
     """The same-XCD hand-off groups (default where the groups tile the 8 XCDs: 32 x 800 and
     16 x 1024 bidirectional, 64 x 256 unidirectional) read the same bytes from plainly stored
     copies, placed by the XCC id each producer publishes: outputs and gradients bit-identical
-    to the interleaved layout (DS2_GRU_XCD=0), ragged lengths."""
+    to the interleaved layout (DS2_GRU_XCD=0), ragged lengths; for the fp16x3 recurrences
+    (default) and the bf16x6 ones."""
     nd = 2 if bidir else 1
+    f = "1" if kern == "h3" else "0"
+    monkeypatch.setenv("DS2_GRU_H3", f)
+    monkeypatch.setenv("DS2_GRU_H3_BWD", f)
     env = [{"DS2_GRU_XCD": "1"}, {"DS2_GRU_XCD": "0"}]
     xg, il = _gru_run(dev, n, 37, 40, h, nd, h + 13 * n, env, monkeypatch)
     for a, b in zip(xg, il):
@@ -579,14 +585,15 @@ def test_gru_xcd_groups_bit_identical(dev, n, h, bidir, monkeypatch):
         assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("x6", ["1", "0", "x6fwd"])
+@pytest.mark.parametrize("x6", ["1", "0", "x6"])
 def test_gru_backward_full_length_vs_torch(dev, x6, monkeypatch):
     """The cfg2 recurrence shape (bs 32, H 800, both directions) over 201 steps with ragged
-    lengths: the default recurrences (fp16x3 forward, bf16x6 pre-split backward), the bf16x6
-    forward (DS2_GRU_H3=0, "x6fwd") and the fp32-MFMA kernels (DS2_GRU_X6=0) against torch's
-    nn.GRU in fp64."""
+    lengths: the default recurrences (fp16x3 forward and backward), the bf16x6 ones
+    (DS2_GRU_H3=0 DS2_GRU_H3_BWD=0, "x6") and the fp32-MFMA kernels (DS2_GRU_X6=0) against
+    torch's nn.GRU in fp64."""
     monkeypatch.setenv("DS2_GRU_X6", "0" if x6 == "0" else "1")
-    monkeypatch.setenv("DS2_GRU_H3", "0" if x6 == "x6fwd" else "1")
+    monkeypatch.setenv("DS2_GRU_H3", "0" if x6 == "x6" else "1")
+    monkeypatch.setenv("DS2_GRU_H3_BWD", "0" if x6 == "x6" else "1")
     n, t, inp, h = 32, 201, 64, 800
     g = torch.Generator().manual_seed(3)
     gru = torch.nn.GRU(inp, h, bidirectional=True).double()
