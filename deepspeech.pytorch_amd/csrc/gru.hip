@@ -1057,7 +1057,8 @@ bool launch_gru_bwd_x6(int t_max, int n, int h, int num_dirs, const float* dy, i
                        const float* w_hh_f, const float* w_hh_r, const float* h_all,
                        const float* gates, const int* lens, float* dgates_x, float* dgates_h,
                        float* ring, unsigned* ctrs, unsigned* err, unsigned long long* stamps,
-                       double* dbp, size_t lds_pad, hipStream_t st);
+                       double* dbp, size_t lds_pad, hipStream_t st, unsigned* camax,
+                       bool* camax_done);
 int gru_bwd_x6_grid(int n, int h, int num_dirs);
 }  // namespace ds2
 
@@ -1292,7 +1293,15 @@ static ds2_status_t gru_bwd_run(int t_max, int n, int h, int num_dirs, const flo
                                 const float* w_hh_f, const float* w_hh_r, const float* h_all,
                                 const float* gates, const int* lens, float* dgates_x,
                                 float* dgates_h, unsigned* err_out, void* ws, hipStream_t st,
-                                double* dbp, bool& summed);
+                                double* dbp, bool& summed, unsigned* camax, bool& camax_done);
+
+static ds2_status_t gru_bwd_bias_impl(int t_max, int n, int h, int num_dirs, const float* dy,
+                                      int dy_dirs, const float* w_hh_f, const float* w_hh_r,
+                                      const float* h_all, const float* gates, const int* lens,
+                                      float* dgates_x, float* dgates_h, float* db_ih_f,
+                                      float* db_hh_f, float* db_ih_r, float* db_hh_r,
+                                      unsigned* err_out, void* ws, size_t ws_bytes,
+                                      unsigned* camax, ds2_stream_t stream);
 
 ds2_status_t ds2_gru_bwd_bias(int t_max, int n, int h, int num_dirs, const float* dy, int dy_dirs,
                               const float* w_hh_f, const float* w_hh_r, const float* h_all,
@@ -1300,6 +1309,31 @@ ds2_status_t ds2_gru_bwd_bias(int t_max, int n, int h, int num_dirs, const float
                               float* dgates_h, float* db_ih_f, float* db_hh_f, float* db_ih_r,
                               float* db_hh_r, unsigned* err_out, void* ws, size_t ws_bytes,
                               ds2_stream_t stream) {
+  return gru_bwd_bias_impl(t_max, n, h, num_dirs, dy, dy_dirs, w_hh_f, w_hh_r, h_all, gates, lens,
+                           dgates_x, dgates_h, db_ih_f, db_hh_f, db_ih_r, db_hh_r, err_out, ws,
+                           ws_bytes, nullptr, stream);
+}
+
+ds2_status_t ds2_gru_bwd_bias_amax(int t_max, int n, int h, int num_dirs, const float* dy,
+                                   int dy_dirs, const float* w_hh_f, const float* w_hh_r,
+                                   const float* h_all, const float* gates, const int* lens,
+                                   float* dgates_x, float* dgates_h, float* db_ih_f,
+                                   float* db_hh_f, float* db_ih_r, float* db_hh_r,
+                                   unsigned* col_amax, unsigned* err_out, void* ws,
+                                   size_t ws_bytes, ds2_stream_t stream) {
+  if (col_amax == nullptr) return DS2_INVALID_VALUE;
+  return gru_bwd_bias_impl(t_max, n, h, num_dirs, dy, dy_dirs, w_hh_f, w_hh_r, h_all, gates, lens,
+                           dgates_x, dgates_h, db_ih_f, db_hh_f, db_ih_r, db_hh_r, err_out, ws,
+                           ws_bytes, col_amax, stream);
+}
+
+static ds2_status_t gru_bwd_bias_impl(int t_max, int n, int h, int num_dirs, const float* dy,
+                                      int dy_dirs, const float* w_hh_f, const float* w_hh_r,
+                                      const float* h_all, const float* gates, const int* lens,
+                                      float* dgates_x, float* dgates_h, float* db_ih_f,
+                                      float* db_hh_f, float* db_ih_r, float* db_hh_r,
+                                      unsigned* err_out, void* ws, size_t ws_bytes,
+                                      unsigned* camax, ds2_stream_t stream) {
   if (t_max < 0 || n < 0 || h < 1 || (num_dirs != 1 && num_dirs != 2)) return DS2_INVALID_VALUE;
   if (gates == nullptr) return DS2_INVALID_VALUE;
   if (dy_dirs != 1 && dy_dirs != num_dirs) return DS2_INVALID_VALUE;
@@ -1310,6 +1344,9 @@ ds2_status_t ds2_gru_bwd_bias(int t_max, int n, int h, int num_dirs, const float
     return DS2_WORKSPACE_TOO_SMALL;
   hipStream_t st = as_stream(stream);
   double* dbp = reinterpret_cast<double*>(static_cast<char*>(ws) + gru_bwd_ws_base(n, h, num_dirs));
+  const size_t camax_bytes = (size_t)2 * num_dirs * 3 * h * sizeof(unsigned);
+  if (camax != nullptr && hipMemsetAsync(camax, 0, camax_bytes, st) != hipSuccess)
+    return launch_status("ds2_gru_bwd_bias_amax");
   if (t_max == 0 || n == 0) {
     if (!want_db) return DS2_OK;
     // no rows: zero bias gradients
@@ -1319,11 +1356,21 @@ ds2_status_t ds2_gru_bwd_bias(int t_max, int n, int h, int num_dirs, const float
                        dbp, 1, num_dirs, h, db_ih_f, db_hh_f, db_ih_r, db_hh_r);
     return launch_status("ds2_gru_bwd_bias");
   }
-  bool summed = false;
+  bool summed = false, camax_done = false;
   const ds2_status_t rc = gru_bwd_run(t_max, n, h, num_dirs, dy, dy_dirs, w_hh_f, w_hh_r, h_all,
                                       gates, lens, dgates_x, dgates_h, err_out, ws, st,
-                                      want_db ? dbp : nullptr, summed);
-  if (rc != DS2_OK || !want_db) return rc;
+                                      want_db ? dbp : nullptr, summed, camax, camax_done);
+  if (rc != DS2_OK) return rc;
+  if (camax != nullptr && !camax_done) {
+    // a kernel without the fused maxima ran: one column pass over each of dgx, dgh
+    const ds2_status_t ra = ds2_amax(dgates_x, t_max * n, num_dirs * 3 * h, num_dirs * 3 * h,
+                                     nullptr, camax, stream);
+    const ds2_status_t rb = ra != DS2_OK ? ra
+        : ds2_amax(dgates_h, t_max * n, num_dirs * 3 * h, num_dirs * 3 * h, nullptr,
+                   camax + num_dirs * 3 * h, stream);
+    if (rb != DS2_OK) return rb;
+  }
+  if (!want_db) return DS2_OK;
   int bt = (n + GB - 1) / GB;
   if (!summed) {
     hipLaunchKernelGGL(gru_db_cols_kernel, dim3(num_dirs * 4 * h), dim3(256), 0, st, dgates_x,
@@ -1339,7 +1386,7 @@ static ds2_status_t gru_bwd_run(int t_max, int n, int h, int num_dirs, const flo
                                 const float* w_hh_f, const float* w_hh_r, const float* h_all,
                                 const float* gates, const int* lens, float* dgates_x,
                                 float* dgates_h, unsigned* err_out, void* ws, hipStream_t st,
-                                double* dbp, bool& summed) {
+                                double* dbp, bool& summed, unsigned* camax, bool& camax_done) {
   if (num_dirs == 1) w_hh_r = w_hh_f;
   apply_spin_limit_env();
   apply_rnn_tune_env();
@@ -1368,7 +1415,8 @@ static ds2_status_t gru_bwd_run(int t_max, int n, int h, int num_dirs, const flo
     void* args[] = {&T_, &N_, &H_, &D_, &UB_, &BT_, &dy, &DYD_, &w_hh_f, &w_hh_r, &h_all,
                     &gates, &lens, &dgates_x, &dgates_h, &ring, &ctrs, &err, &stamps, &dbp};
     if (launch_gru_bwd_x6(t_max, n, h, num_dirs, dy, dy_dirs, w_hh_f, w_hh_r, h_all, gates,
-                          lens, dgates_x, dgates_h, ring, ctrs, err, stamps, dbp, kDopPadLds, st)) {
+                          lens, dgates_x, dgates_h, ring, ctrs, err, stamps, dbp, kDopPadLds, st,
+                          camax, &camax_done)) {
       fold_err(err, err_out, st);
       summed = dbp != nullptr;
       return launch_status("ds2_gru_bwd");

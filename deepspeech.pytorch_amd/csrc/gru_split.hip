@@ -712,7 +712,8 @@ __global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     const float* __restrict__ h_all, const float* __restrict__ gates,
     const int* __restrict__ lens, float* __restrict__ dgx, float* __restrict__ dgh,
     float* __restrict__ gx, unsigned* __restrict__ counters, unsigned* __restrict__ err,
-    unsigned long long* __restrict__ stamps, double* __restrict__ dbp, int xmode) {
+    unsigned long long* __restrict__ stamps, double* __restrict__ dbp, int xmode,
+    unsigned* __restrict__ camax) {
   static_assert(NPW <= 8, "producers per wave");
   constexpr int RP = GU + 1;
   constexpr int LWP = NPW < 3 ? NPW : 3;        // producers' records in flight per wave
@@ -812,6 +813,9 @@ __global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
   float px_dar = 0.f, px_daz = 0.f, px_dan = 0.f, px_dghn = 0.f;
   int64_t px_row = -1;
   double sb_r = 0.0, sb_z = 0.0, sb_n = 0.0, sb_hn = 0.0;
+  // camax: running max |.| of the unit's dar, daz, dan, dghn over the steps (the fp16x3
+  // GEMMs' column scales of dgx / dgh, published at the end)
+  float cm_r = 0.f, cm_z = 0.f, cm_n = 0.f, cm_hn = 0.f;
   for (int s = 0; s < T; ++s) {
     const int t = d == 0 ? T - 1 - s : s;
     f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -914,6 +918,10 @@ __global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
       z_prev = zc;
       px_dar = dar; px_daz = daz; px_dan = dan; px_dghn = dghn; px_row = row;
       sb_r += dar; sb_z += daz; sb_n += dan; sb_hn += dghn;
+      cm_r = fmaxf(cm_r, fabsf(dar));
+      cm_z = fmaxf(cm_z, fabsf(daz));
+      cm_n = fmaxf(cm_n, fabsf(dan));
+      cm_hn = fmaxf(cm_hn, fabsf(dghn));
     }
     if (gate_thread) {
       // the row's scale: max over the sample's 16 units x 3 gates (16 consecutive lanes)
@@ -965,6 +973,37 @@ __global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
       ghr[j] = px_dar;
       ghr[H + j] = px_daz;
       ghr[2 * H + j] = px_dghn;
+    }
+  }
+  if (camax != nullptr) {
+    // column maxima of dgx [T N][D 3H] and dgh: the 16 samples' running maxima per unit, then
+    // one unsigned atomic max per (gate, unit) into camax[0, D 3H) (dgx) and [D 3H, 2 D 3H)
+    // (dgh; its r, z columns are dgx's, its n column dghn)
+    __syncthreads();
+    if (gate_thread) {
+      red[(0 * GB + m) * GU + u] = cm_r;
+      red[(1 * GB + m) * GU + u] = cm_z;
+      red[(2 * GB + m) * GU + u] = cm_n;
+      red[(3 * GB + m) * GU + u] = cm_hn;
+    }
+    __syncthreads();
+    if (threadIdx.x < 4 * GU) {
+      const int g = threadIdx.x / GU, uu = threadIdx.x - (threadIdx.x / GU) * GU;
+      float a = 0.f;
+#pragma unroll
+      for (int mm = 0; mm < GB; ++mm) a = fmaxf(a, red[(g * GB + mm) * GU + uu]);
+      const unsigned bits = __float_as_uint(a);
+      const int col = d * H3 + ub * GU + uu;
+      if (bits != 0u) {
+        if (g < 2) {
+          atomicMax(camax + col + g * H, bits);
+          atomicMax(camax + D * H3 + col + g * H, bits);
+        } else if (g == 2) {
+          atomicMax(camax + col + 2 * H, bits);
+        } else {
+          atomicMax(camax + D * H3 + col + 2 * H, bits);
+        }
+      }
     }
   }
   if (dbp == nullptr) return;
@@ -1076,24 +1115,32 @@ static const void* bwd_h3_fn(int UB) {
   return nullptr;
 }
 
+// camax (nullable, zeroed by the caller): the fp16x3 backward also leaves the column maxima
+// of dgates_x / dgates_h there; *camax_done says whether the kernel that ran did
 bool launch_gru_bwd_x6(int t_max, int n, int h, int num_dirs, const float* dy, int dy_dirs,
                        const float* w_hh_f, const float* w_hh_r, const float* h_all,
                        const float* gates, const int* lens, float* dgates_x, float* dgates_h,
                        float* ring, unsigned* ctrs, unsigned* err, unsigned long long* stamps,
-                       double* dbp, size_t lds_pad, hipStream_t st) {
+                       double* dbp, size_t lds_pad, hipStream_t st, unsigned* camax,
+                       bool* camax_done) {
+  if (camax_done != nullptr) *camax_done = false;
   if (!x6_enabled() || (h % GU) != 0) return false;
   apply_spin_limit_env();
   apply_rnn_tune_env();
   const int UB = h / GU, BT = (n + GB - 1) / GB;
   const void* fn = bwd_h3_enabled() ? bwd_h3_fn(UB) : nullptr;
+  const bool h3 = fn != nullptr;
   if (fn == nullptr) fn = bwd_x6_fn((3 * UB + 1) / 2);
   if (fn == nullptr) return false;
   int XM_ = xcd_groups(UB, BT, num_dirs) ? 1 : 0;
   const int grid = XM_ ? xgrp_grid(UB, BT, num_dirs) : mapped_grid(UB * num_dirs, BT);
   int T_ = t_max, N_ = n, H_ = h, D_ = num_dirs, UB_ = UB, BT_ = BT, DYD_ = dy_dirs;
   void* args[] = {&T_, &N_, &H_, &D_, &UB_, &BT_, &dy, &DYD_, &w_hh_f, &w_hh_r, &h_all,
-                  &gates, &lens, &dgates_x, &dgates_h, &ring, &ctrs, &err, &stamps, &dbp, &XM_};
-  return rnn_launch(fn, dim3(grid), dim3(BW * 64), args, lds_pad, st) == hipSuccess;
+                  &gates, &lens, &dgates_x, &dgates_h, &ring, &ctrs, &err, &stamps, &dbp, &XM_,
+                  &camax};
+  const bool ok = rnn_launch(fn, dim3(grid), dim3(BW * 64), args, lds_pad, st) == hipSuccess;
+  if (ok && h3 && camax != nullptr && camax_done != nullptr) *camax_done = true;
+  return ok;
 }
 
 }  // namespace ds2

@@ -91,6 +91,9 @@ _PROTOS = {
                              _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
     "ds2_gru_bwd_bias": (_c_int, [_c_int, _c_int, _c_int, _c_int, _vp, _c_int, _vp, _vp, _vp,
                                   _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
+    "ds2_gru_bwd_bias_amax": (_c_int, [_c_int, _c_int, _c_int, _c_int, _vp, _c_int, _vp, _vp,
+                                       _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                       _sz, _vp]),
     "ds2_lstm_fwd_workspace_size": (_sz, [_c_int, _c_int, _c_int]),
     "ds2_lstm_fwd": (_c_int, [_c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                               _vp, _vp, _vp, _vp, _sz, _vp]),

@@ -847,14 +847,15 @@ def _rnn_param_grads_bf16(x2d, h_all, dgx, dgh, weights, nd, g, t, n, inp, h, ne
 
 
 def _rnn_param_grads(x, h_all, dgx, dgh, weights, nd, g, need_dx, bf16=False, dbias=None,
-                     shared_bf16=True):
+                     shared_bf16=True, col_amax=None):
     """Weight/bias/input gradients of one recurrent layer from the gate gradients.
 
     dgx = d/d(x W_ih^T + b_ih), dgh = d/d(h W_hh^T + b_hh), both [T, N, D, g]
     (the same tensor for LSTM).  All plain GEMMs + column sums; dbias = [db_ih, db_hh] per
     direction already summed (the GRU backward kernel's own sums) skips the column sums.
     shared_bf16=False keeps bf16 mode on the per-GEMM conversions (the cross-check of
-    _rnn_param_grads_bf16's shared copies, tests/test_gpu_ops.py).
+    _rnn_param_grads_bf16's shared copies, tests/test_gpu_ops.py).  col_amax: the column
+    maxima of dgx and dgh ([2 D g] float bits) when the recurrence kept them.
     """
     t, n, inp = x.shape
     h = h_all.shape[-1]
@@ -876,8 +877,13 @@ def _rnn_param_grads(x, h_all, dgx, dgh, weights, nd, g, need_dx, bf16=False, db
     # columns, and 1.0 for the tanh-bounded states h
     am = {}
     if h3_enabled() and not bf16:
-        am["dgx_r"], am["dgx_c"] = amax(dgx, tn, ld, ld, want_rows=need_dx)
-        am["dgh_c"] = am["dgx_c"] if dgh is dgx else amax(dgh, tn, ld, ld, want_rows=False)[1]
+        if col_amax is not None:
+            am["dgx_c"], am["dgh_c"] = col_amax[:ld], col_amax[ld:]
+            if need_dx:
+                am["dgx_r"] = amax(dgx, tn, ld, ld, want_cols=False)[0]
+        else:
+            am["dgx_r"], am["dgx_c"] = amax(dgx, tn, ld, ld, want_rows=need_dx)
+            am["dgh_c"] = am["dgx_c"] if dgh is dgx else amax(dgh, tn, ld, ld, want_rows=False)[1]
         am["x_c"] = amax(x2d, tn, inp, inp, want_rows=False)[1]
         am["h"] = unit_bound(nd * h, dev)
         if need_dx:
@@ -1011,15 +1017,24 @@ class GRULayerFn(torch.autograd.Function):
         w_hh_r = weights[5] if nd == 2 else None
         ws = _ws(_lib.size("ds2_gru_bwd_workspace_size", n, h, nd), dev)
         _guard_cooperative("gru", n, h, nd)
-        # bias gradients straight into their slots, summed by the recurrence kernel
+        # bias gradients straight into their slots, summed by the recurrence kernel; with the
+        # fp16x3 GEMMs the kernel also keeps the column maxima of dgx / dgh they scale by
         dbias = [grad_like(weights[4 * d + k]) for d in range(nd) for k in (2, 3)]
-        _lib.call("ds2_gru_bwd_bias", t, n, h, nd, dy.data_ptr(), dy_dirs, w_hh_f.data_ptr(),
-                  _p(w_hh_r), h_all.data_ptr(), gates.data_ptr(), lens.data_ptr(), dgx.data_ptr(),
+        common = (t, n, h, nd, dy.data_ptr(), dy_dirs, w_hh_f.data_ptr(), _p(w_hh_r),
+                  h_all.data_ptr(), gates.data_ptr(), lens.data_ptr(), dgx.data_ptr(),
                   dgh.data_ptr(), dbias[0].data_ptr(), dbias[1].data_ptr(),
-                  _p(dbias[2] if nd == 2 else None), _p(dbias[3] if nd == 2 else None),
-                  rnn_status_word(dev).data_ptr(), ws.data_ptr(), ws.numel(), _stream())
+                  _p(dbias[2] if nd == 2 else None), _p(dbias[3] if nd == 2 else None))
+        col_amax = None
+        if h3_enabled() and not bf16:
+            col_amax = torch.empty(2 * nd * h3, dtype=_I32, device=dev)
+            _lib.call("ds2_gru_bwd_bias_amax", *common, col_amax.data_ptr(),
+                      rnn_status_word(dev).data_ptr(), ws.data_ptr(), ws.numel(), _stream())
+        else:
+            _lib.call("ds2_gru_bwd_bias", *common, rnn_status_word(dev).data_ptr(),
+                      ws.data_ptr(), ws.numel(), _stream())
         dx, grads = _rnn_param_grads(x, h_all, dgx, dgh, weights, nd, h3,
-                                     ctx.needs_input_grad[0], bf16, dbias=dbias)
+                                     ctx.needs_input_grad[0], bf16, dbias=dbias,
+                                     col_amax=col_amax)
         return (dx, None, None, None, *grads)
 
 

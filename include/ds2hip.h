@@ -276,6 +276,17 @@ ds2_status_t ds2_gru_bwd_bias(int t_max, int n, int h, int num_dirs, const float
                               float* dgates_h, float* db_ih_f, float* db_hh_f, float* db_ih_r,
                               float* db_hh_r, unsigned* err_out, void* ws, size_t ws_bytes,
                               ds2_stream_t stream);
+/* ds2_gru_bwd_bias plus the column maxima of the gate gradients for the fp16x3 GEMMs that
+ * follow (ds2_sgemm_amax_ws: dW_ih, dW_hh): col_amax[0, D 3H) = max over rows of |dgates_x|,
+ * [D 3H, 2 D 3H) = the same of dgates_h, as float bits (ds2_amax's format).  The fp16x3
+ * recurrence keeps them as it goes; any other kernel is followed by a column pass. */
+ds2_status_t ds2_gru_bwd_bias_amax(int t_max, int n, int h, int num_dirs, const float* dy,
+                                   int dy_dirs, const float* w_hh_f, const float* w_hh_r,
+                                   const float* h_all, const float* gates, const int* lens,
+                                   float* dgates_x, float* dgates_h, float* db_ih_f,
+                                   float* db_hh_f, float* db_ih_r, float* db_hh_r,
+                                   unsigned* col_amax, unsigned* err_out, void* ws,
+                                   size_t ws_bytes, ds2_stream_t stream);
 
 /* ------------------------------------------------------------------------ */
 /* (Bi)directional LSTM recurrence (torch gate order i, f, g, o), same packed-

@@ -1338,3 +1338,30 @@ def test_rnn_param_grads_bf16_shared_copies(dev, cell, nd):
     _, gr_32 = ops._rnn_param_grads(x, h_all, dgx, dgh, weights, nd, g, True, bf16=False)
     d = (gr_32[0] - gr_f[0]).abs().max().item() / gr_32[0].abs().max().item()
     assert d > 1e-4, d
+
+
+@pytest.mark.parametrize("bwd", ["h3", "x6"])
+@pytest.mark.parametrize("n,h,bidir", [(32, 800, True), (7, 48, False), (20, 256, True)])
+def test_gru_bwd_column_maxima(dev, n, h, bidir, bwd, monkeypatch):
+    """ds2_gru_bwd_bias_amax: the column maxima of dgx / dgh the fp16x3 GEMMs scale by, kept
+    by the fp16x3 backward recurrence as it runs (bwd='h3') or by a column pass after the
+    bf16x6 one (DS2_GRU_H3_BWD=0): bit-exact against torch's amax of the gradients the layer
+    handed to its GEMMs."""
+    monkeypatch.setenv("DS2_GRU_H3_BWD", "1" if bwd == "h3" else "0")
+    nd = 2 if bidir else 1
+    seen = {}
+    orig = ops._rnn_param_grads
+
+    def spy(x, h_all, dgx, dgh, weights, nd_, g, need_dx, bf16=False, dbias=None, **kw):
+        seen["dgx"], seen["dgh"], seen["col"] = dgx.clone(), dgh.clone(), kw.get("col_amax")
+        return orig(x, h_all, dgx, dgh, weights, nd_, g, need_dx, bf16, dbias, **kw)
+
+    monkeypatch.setattr(ops, "_rnn_param_grads", spy)
+    _gru_run(dev, n, 29, 40, h, nd, h + n, [{}], monkeypatch)
+    col = seen["col"]
+    assert col is not None
+    g = nd * 3 * h
+    ref_x = seen["dgx"].view(-1, g).abs().amax(0).contiguous().view(torch.int32)
+    ref_h = seen["dgh"].view(-1, g).abs().amax(0).contiguous().view(torch.int32)
+    assert torch.equal(col[:g], ref_x)
+    assert torch.equal(col[g:], ref_h)
