@@ -69,10 +69,31 @@ def gemm_peak():
                             "accumulation (bf16 dense peak / 6)")
 
 
-def gru_bwd_kernel(x6f: bool):
-    """(peak, arithmetic, kernel name) of the GRU backward recurrence as configured: the
-    pre-split bf16x6 kernel by default (gru_split.hip), the fp32-MFMA kernel with
+def _env_on(name: str) -> bool:
+    return os.environ.get(name, "1")[:1] != "0"
+
+
+def gru_fwd_kernel(x6f: bool):
+    """(peak, arithmetic, kernel name) of the GRU forward recurrence as configured: fp16x3 by
+    default (gru_split.hip), bf16x6 with DS2_GRU_H3=0, the fp32-MFMA kernel with
     DS2_GRU_X6=0."""
+    if x6f and _env_on("DS2_GRU_H3"):
+        return (PEAK_H3_TFLOPS, "W_hh contraction, fp16x3 (fp32-accurate: per-row scaled fp16 "
+                "hi/lo, 3 products) on v_mfma_f32_16x16x32_f16", "gru_fwd_x6_kernel")
+    if x6f:
+        return (PEAK_X6_TFLOPS, "W_hh contraction, bf16x6 (fp32-accurate) on "
+                "v_mfma_f32_16x16x32_bf16", "gru_fwd_x6_kernel")
+    return PEAK_F32_MFMA_TFLOPS, "W_hh contraction, fp32 MFMA", "gru_fwd_dop_kernel"
+
+
+def gru_bwd_kernel(x6f: bool):
+    """(peak, arithmetic, kernel name) of the GRU backward recurrence as configured: fp16x3
+    records by default (gru_bwd_h3_kernel), the pre-split bf16x6 kernel with DS2_GRU_H3_BWD=0,
+    the fp32-MFMA kernel with DS2_GRU_X6=0."""
+    if x6f and _env_on("DS2_GRU_H3_BWD"):
+        return (PEAK_H3_TFLOPS, "W_hh^T contraction, fp16x3 (one per-row scaled fp16 hi/lo "
+                "record per producer and step) on v_mfma_f32_16x16x32_f16 / 16x16x16f16",
+                "gru_bwd_h3_kernel")
     if x6f:
         return (PEAK_X6_TFLOPS, "W_hh^T contraction, bf16x6 (fp32-accurate, pre-split tiles) "
                 "on v_mfma_f32_16x16x32_bf16", "gru_bwd_x6_kernel")
@@ -321,7 +342,8 @@ def main():
     probe.install()
     fprobe = KernelProbe(("ds2_gru_fwd",), gru_recurrence_flops)
     fprobe.install()
-    bprobe = KernelProbe(("ds2_gru_bwd", "ds2_gru_bwd_bias"), gru_recurrence_flops)
+    bprobe = KernelProbe(("ds2_gru_bwd", "ds2_gru_bwd_bias", "ds2_gru_bwd_bias_amax"),
+                         gru_recurrence_flops)
     bprobe.install()
     aprobe = KernelProbe(("ds2_amax",), lambda a: 4.0 * a[1] * a[2])   # bytes read
     aprobe.install()
@@ -412,10 +434,9 @@ def main():
                 "peak": 8000.0, "frac": round(a_bytes / (a_ms * 1e-3) / 1e9 / 8000.0, 4),
                 "note": "fp16x3 operand row/column maxima shared by the RNN gradient GEMMs "
                         "(one read of each operand)"}
-        x6f = os.environ.get("DS2_GRU_X6", "1")[:1] != "0"
-        entry("ds2_gru_fwd", fk, PEAK_X6_TFLOPS if x6f else PEAK_F32_MFMA_TFLOPS,
-              "W_hh contraction, bf16x6 (fp32-accurate) on v_mfma_f32_16x16x32_bf16" if x6f
-              else "W_hh contraction, fp32 MFMA", "mfma", ("gru_fwd_x6_kernel" if x6f else "gru_fwd_dop_kernel", ()))
+        x6f = _env_on("DS2_GRU_X6")
+        fpeak, farith, fkern = gru_fwd_kernel(x6f)
+        entry("ds2_gru_fwd", fk, fpeak, farith, "mfma", (fkern, ()))
         bpeak, barith, bkern = gru_bwd_kernel(x6f)
         entry("ds2_gru_bwd", bk, bpeak, barith, "mfma", (bkern, ()))
         # the roofline object is the dominant kernel family of the step (most ms per step)

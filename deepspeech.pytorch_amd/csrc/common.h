@@ -84,4 +84,16 @@ __device__ __forceinline__ float tanh_fast(float x) {
   return 1.0f - 2.0f * __builtin_amdgcn_rcpf(1.0f + __expf(2.0f * x));
 }
 
+// fp16x3 row scales.  amax: the bit pattern of max |x| over a logical row (non-negative floats
+// order as unsigned).  The row is staged as x 2^e, e = 14 - floor(log2 amax), so its largest
+// element lies in [2^14, 2^15) (fp16 max 65504) and its fp16 (hi, lo) split keeps 22 bits for
+// every element within 2^17 of the row max; a zero, inf or NaN row max keeps e = 0.
+__device__ __forceinline__ int h3_exp(unsigned amax) {
+  const int E = (int)(amax >> 23);                 // biased exponent (sign bit is 0)
+  if (amax == 0u || E >= 255) return 0;
+  int e = 14 - ((E == 0 ? 1 : E) - 127);
+  return e > 127 ? 127 : e;                        // 2^e stays a normal float
+}
+__device__ __forceinline__ float h3_scale(int e) { return __builtin_bit_cast(float, (e + 127) << 23); }
+
 }  // namespace ds2

@@ -1084,6 +1084,126 @@ __device__ __forceinline__ void cx_split_store8(unsigned short* __restrict__ s, 
   *reinterpret_cast<u32x4*>(s + plane + at) = m;
   *reinterpret_cast<u32x4*>(s + 2 * plane + at) = l;
 }
+
+// fp16x3: 8 fp32 values times the power of two sc -> fp16 hi / lo rows of 16 B
+// at s + at, + plane (RNE casts; the residual is exact in fp32)
+typedef _Float16 cf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 cf16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void cx_split_store8h(unsigned short* __restrict__ s, int plane, int at,
+                                                 const float* v, float sc) {
+  u32x4 h, l;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const cf32x2 x = cf32x2{v[2 * e], v[2 * e + 1]} * sc;
+    const cf16x2 hh = __builtin_convertvector(x, cf16x2);
+    const cf16x2 ll = __builtin_convertvector(x - __builtin_convertvector(hh, cf32x2), cf16x2);
+    h[e] = __builtin_bit_cast(unsigned, hh);
+    l[e] = __builtin_bit_cast(unsigned, ll);
+  }
+  *reinterpret_cast<u32x4*>(s + at) = h;
+  *reinterpret_cast<u32x4*>(s + plane + at) = l;
+}
+
+// NPL 3: bf16 hi / mid / lo planes; NPL 2: fp16 hi / lo planes of v sc
+template <int NPL>
+__device__ __forceinline__ void cx_store8(unsigned short* __restrict__ s, int plane, int at,
+                                          const float* v, float sc) {
+  if constexpr (NPL == 2) cx_split_store8h(s, plane, at, v, sc);
+  else cx_split_store8(s, plane, at, v);
+}
+
+// acc += a.b over one 32 x 32 x 16 fragment pair: bf16x6 (6 products, small terms first) or
+// fp16x3 (lo.hi + hi.lo + hi.hi)
+template <int NPL>
+__device__ __forceinline__ f32x16 cx_mma(const bf16x8 (&a)[3], const bf16x8 (&b)[3], f32x16 c) {
+  if constexpr (NPL == 2) {
+    typedef cf16x8 H;
+    c = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(H, a[1]), __builtin_bit_cast(H, b[0]), c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(H, a[0]), __builtin_bit_cast(H, b[1]), c, 0, 0, 0);
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(H, a[0]), __builtin_bit_cast(H, b[0]), c, 0, 0, 0);
+  } else {
+    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[1], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[0], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[2], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[0], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[1], c, 0, 0, 0);
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], c, 0, 0, 0);
+  }
+}
+
+// a weight-image value's fp16x3 / bf16x6 terms (NPL planes, `per` apart from img[base])
+template <int NPL>
+__device__ __forceinline__ void cx_wimg_put(unsigned short* __restrict__ img, int64_t base,
+                                            int64_t per, float v, float sc) {
+  if constexpr (NPL == 2) {
+    const float x = v * sc;
+    const _Float16 hb = (_Float16)x;
+    img[base] = __builtin_bit_cast(unsigned short, hb);
+    img[base + per] = __builtin_bit_cast(unsigned short, (_Float16)(x - (float)hb));
+  } else {
+    const __bf16 hb = (__bf16)v;
+    const float r1 = v - (float)hb;
+    const __bf16 mbf = (__bf16)r1;
+    const __bf16 lb = (__bf16)(r1 - (float)mbf);
+    img[base] = __builtin_bit_cast(unsigned short, hb);
+    img[base + per] = __builtin_bit_cast(unsigned short, mbf);
+    img[base + 2 * per] = __builtin_bit_cast(unsigned short, lb);
+  }
+}
+
+// fp16x3 scales of an implicit-GEMM convolution: m_exp[m] = h3_exp(max |w| over the taps and
+// loop channels of output row m) (fwd: m = co; dgrad: m = ci), one workgroup per m
+template <bool DGRAD>
+__global__ void conv_h3_wexp_kernel(const float* __restrict__ w, ConvDims g, int* __restrict__ m_exp) {
+  __shared__ float red[4];
+  const int m = blockIdx.x;
+  const int KHW = g.kh * g.kw;
+  const int L = DGRAD ? g.co : g.ci;
+  float mx = 0.f;
+  for (int i = threadIdx.x; i < L * KHW; i += blockDim.x) {
+    const int l = i / KHW, t = i - l * KHW;
+    const float v = DGRAD ? w[((int64_t)l * g.ci + m) * KHW + t] : w[((int64_t)m * g.ci + l) * KHW + t];
+    mx = fmaxf(mx, fabsf(v));
+  }
+  mx = wave_max(mx);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int i = 1; i < (int)(blockDim.x >> 6); ++i) mx = fmaxf(mx, red[i]);
+    m_exp[m] = h3_exp(__float_as_uint(mx));
+  }
+}
+
+// per-sample max |x| of an [n][per] tensor (float bits, unsigned atomic max; out zeroed first):
+// grid (chunks, n), 256 threads, 16-B loads where the sample's base is 16-B aligned
+__global__ void conv_h3_samax_kernel(const float* __restrict__ x, int64_t per,
+                                     unsigned* __restrict__ out) {
+  __shared__ float red[4];
+  const int n = blockIdx.y;
+  const float* xs = x + (int64_t)n * per;
+  const int64_t chunk = (per + gridDim.x - 1) / gridDim.x;
+  const int64_t b = (int64_t)blockIdx.x * chunk;
+  const int64_t e = b + chunk < per ? b + chunk : per;
+  float mx = 0.f;
+  if ((reinterpret_cast<uintptr_t>(xs + b) & 15) == 0 && (chunk & 3) == 0) {
+    const int64_t e4 = b + ((e - b) & ~(int64_t)3);
+    for (int64_t i = b + 4 * threadIdx.x; i < e4; i += 4 * blockDim.x) {
+      const float4 v = *reinterpret_cast<const float4*>(xs + i);
+      mx = fmaxf(mx, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+    }
+    for (int64_t i = e4 + threadIdx.x; i < e; i += blockDim.x) mx = fmaxf(mx, fabsf(xs[i]));
+  } else {
+    for (int64_t i = b + threadIdx.x; i < e; i += blockDim.x) mx = fmaxf(mx, fabsf(xs[i]));
+  }
+  mx = wave_max(mx);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int i = 1; i < (int)(blockDim.x >> 6); ++i) mx = fmaxf(mx, red[i]);
+    if (b < e) atomicMax(out + n, __float_as_uint(mx));
+  }
+}
+
 constexpr int CX_T = 512;
 constexpr int CX_COLS = 256;
 constexpr int CX_PATCH = 3 * 522 * 24;   // bf16: 3 planes x columns x pitch (max)
@@ -1130,10 +1250,12 @@ __host__ __device__ inline CxGeom cx_geom(const ConvDims& g, bool dgrad) {
   return c;
 }
 
-// split-weight image: [class][mb][loop channel][plane][32][COP] bf16
-template <bool DGRAD>
+// split-weight image: [class][mb][loop channel][plane][32][COP] bf16 (NPL 3) or fp16 (NPL 2)
+// NPL 2: fp16 hi / lo planes of w 2^m_exp[m] (fp16x3)
+template <bool DGRAD, int NPL = 3>
 __global__ void conv_x6_wimg_kernel(const float* __restrict__ w, ConvDims g, CxGeom c,
-                                    unsigned short* __restrict__ img) {
+                                    unsigned short* __restrict__ img,
+                                    const int* __restrict__ m_exp) {
   const int M = DGRAD ? g.ci : g.co;
   const int L = (DGRAD ? g.co : g.ci) * c.RC;          // (channel, tap-row chunk) pairs
   const int mbn = (M + 31) / 32;
@@ -1161,14 +1283,8 @@ __global__ void conv_x6_wimg_kernel(const float* __restrict__ w, ConvDims g, CxG
         if (a < aq) v = w[((int64_t)ch * g.ci + m) * KHW + (q + g.sh * (aq - 1 - a)) * g.kw + (g.kw - 1 - b)];
       }
     }
-    const __bf16 hb = (__bf16)v;
-    const float r1 = v - (float)hb;
-    const __bf16 mbf = (__bf16)r1;
-    const __bf16 lb = (__bf16)(r1 - (float)mbf);
-    const int64_t base = ((((int64_t)q * mbn + mb) * L + l) * 3) * per + e;
-    img[base] = __builtin_bit_cast(unsigned short, hb);
-    img[base + per] = __builtin_bit_cast(unsigned short, mbf);
-    img[base + 2 * per] = __builtin_bit_cast(unsigned short, lb);
+    const float sc = NPL == 2 && m < M ? h3_scale(m_exp[m]) : 1.f;
+    cx_wimg_put<NPL>(img, ((((int64_t)q * mbn + mb) * L + l) * NPL) * per + e, per, v, sc);
   }
 }
 
@@ -1180,13 +1296,18 @@ __global__ void conv_x6_wimg_kernel(const float* __restrict__ w, ConvDims g, CxG
 // DB: the input patch double-buffered (conv2 fwd): the next channel's patch is split and
 // stored into the other buffer in the middle of this channel's k-steps (its loads were issued
 // at the channel's start), so only the weight image copy stays between the two barriers.
-template <bool DGRAD, int NGA, int NBP_, int PU, int SW, bool RCH, bool DB = false>
+// NPL 2: fp16x3 -- the patch is staged as fp16 hi / lo of x 2^e_n (e_n from the sample's
+// max |x|, n_amax[n]), the image holds w 2^m_exp[m], three products per fragment pair, and the
+// epilogue multiplies by 2^-(m_exp[m] + e_n) (exact) before the bias.
+template <bool DGRAD, int NGA, int NBP_, int PU, int SW, bool RCH, bool DB = false, int NPL = 3>
 __global__ __launch_bounds__(CX_T, 1) void conv_x6_kernel(const float* __restrict__ in,
                                                           const unsigned short* __restrict__ img,
                                                           const float* __restrict__ bias,
                                                           float* __restrict__ out, ConvDims g,
                                                           const int* __restrict__ out_lens,
-                                                          CxGeom c, int gx, int gy) {
+                                                          CxGeom c, int gx, int gy,
+                                                          const int* __restrict__ m_exp,
+                                                          const unsigned* __restrict__ n_amax) {
   __shared__ __attribute__((aligned(16))) unsigned short
       ps[DB ? CX_PATCH_DB : ((SW == 1 && !RCH) ? CX_PATCH1 : CX_PATCH)];
   __shared__ __attribute__((aligned(16))) unsigned short ws[CX_WIMG];
@@ -1239,7 +1360,9 @@ __global__ __launch_bounds__(CX_T, 1) void conv_x6_kernel(const float* __restric
   const int cPCOL = CG ? CC::PCOL : c.PCOL;
   const int PPL = cPCOL * cP;                  // bf16 per patch plane
   const int WPL = 32 * cCOP;                   // bf16 per weight plane
-  const int64_t wstride = (int64_t)3 * WPL;    // one loop channel's image
+  const int64_t wstride = (int64_t)NPL * WPL;  // one loop channel's image
+  const int en = NPL == 2 ? h3_exp(n_amax[n]) : 0;
+  const float nsc = h3_scale(en);
   const unsigned short* wimg = img + ((int64_t)q * mbn + mb) * L * RC * wstride;
   const int ngr = NGA > 0 ? NGA : cKA / 8;
   const int nbp = NBP_ > 0 ? NBP_ : c.NBP;
@@ -1284,7 +1407,7 @@ __global__ __launch_bounds__(CX_T, 1) void conv_x6_kernel(const float* __restric
       const int unit = tid + CX_T * u;
       if (unit < units) {
         const int j = unit / ngr, rg = unit - (unit / ngr) * ngr;
-        cx_split_store8(dst, PPL, j * cP + 8 * rg, rp[u]);
+        cx_store8<NPL>(dst, PPL, j * cP + 8 * rg, rp[u], nsc);
       }
     }
   };
@@ -1317,8 +1440,8 @@ __global__ __launch_bounds__(CX_T, 1) void conv_x6_kernel(const float* __restric
   __syncthreads();
   for (int l = 0; l < LL; ++l) {
     if (l + 1 < LL) load(l + 1);
-    const unsigned short* pcur = DB ? ps + (l & 1) * 3 * PPL : ps;
-    unsigned short* pnext = ps + ((l + 1) & 1) * 3 * PPL;
+    const unsigned short* pcur = DB ? ps + (l & 1) * NPL * PPL : ps;
+    unsigned short* pnext = ps + ((l + 1) & 1) * NPL * PPL;
     bool staged = false;
     if (active) {
       auto kstep = [&](int st) {
@@ -1327,24 +1450,16 @@ __global__ __launch_bounds__(CX_T, 1) void conv_x6_kernel(const float* __restric
         bf16x8 af[3], bfr[2][3];
         const int aw = fr * cCOP + b * cKA + 8 * ga;
 #pragma unroll
-        for (int pl = 0; pl < 3; ++pl) af[pl] = *reinterpret_cast<const bf16x8*>(ws + pl * WPL + aw);
+        for (int pl = 0; pl < NPL; ++pl) af[pl] = *reinterpret_cast<const bf16x8*>(ws + pl * WPL + aw);
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
           const int ap = ((64 * cw + 32 * j + fr) * sw + b) * cP + 8 * ga;
 #pragma unroll
-          for (int pl = 0; pl < 3; ++pl)
+          for (int pl = 0; pl < NPL; ++pl)
             bfr[j][pl] = *reinterpret_cast<const bf16x8*>(pcur + pl * PPL + ap);
         }
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          f32x16 cc = acc[j];
-          cc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1], bfr[j][1], cc, 0, 0, 0);
-          cc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[2], bfr[j][0], cc, 0, 0, 0);
-          cc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bfr[j][2], cc, 0, 0, 0);
-          cc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1], bfr[j][0], cc, 0, 0, 0);
-          cc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bfr[j][1], cc, 0, 0, 0);
-          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bfr[j][0], cc, 0, 0, 0);
-        }
+        for (int j = 0; j < 2; ++j) acc[j] = cx_mma<NPL>(af, bfr[j], acc[j]);
       };
       if (NGA > 0 && NBP_ > 0) {
         constexpr int NK = NGA * NBP_, H0 = (NK + 1) / 2;
@@ -1410,6 +1525,7 @@ __global__ __launch_bounds__(CX_T, 1) void conv_x6_kernel(const float* __restric
       const int m = m0 + (r & 3) + 8 * (r >> 2) + 4 * fh;
       if (m < M) {
         float v = acc[j][r] + red[((cw * 2 + j) * 16 + r) * 64 + lane];
+        if (NPL == 2) v = __builtin_ldexpf(v, -(m_exp[m] + en));
         if (!DGRAD) {
           if (bias != nullptr) v += bias[m];
           if (col >= len) v = 0.f;
@@ -1823,8 +1939,11 @@ static_assert(CQ_OFFO >= CQ_PAIRS * CQ_PP && CQ_OFFO + CQ_PAIRS * CQ_PP <= CQ_PP
 static_assert(CQ_UNITS <= 2 * CX_T, "two staging units per thread");
 
 // pre-split weight image [class][mb][co][plane][32 ci][CQ_COP]: k-step st, half h, element e
+// (NPL 2: fp16 hi / lo planes of w 2^m_exp[ci])
+template <int NPL = 3>
 __global__ void conv_x6q_wimg_kernel(const float* __restrict__ w, ConvDims g,
-                                     unsigned short* __restrict__ img) {
+                                     unsigned short* __restrict__ img,
+                                     const int* __restrict__ m_exp) {
   const int M = g.ci, L = g.co;
   const int mbn = (M + 31) / 32;
   const int64_t per = (int64_t)32 * CQ_COP;
@@ -1847,29 +1966,26 @@ __global__ void conv_x6q_wimg_kernel(const float* __restrict__ w, ConvDims g,
       if (a < aq && b < g.kw)
         v = w[((int64_t)l * g.ci + m) * KHW + (q + g.sh * (aq - 1 - a)) * g.kw + (g.kw - 1 - b)];
     }
-    const __bf16 hb = (__bf16)v;
-    const float r1 = v - (float)hb;
-    const __bf16 mbf = (__bf16)r1;
-    const __bf16 lb = (__bf16)(r1 - (float)mbf);
-    const int64_t base = ((((int64_t)q * mbn + mb) * L + l) * 3) * per + e;
-    img[base] = __builtin_bit_cast(unsigned short, hb);
-    img[base + per] = __builtin_bit_cast(unsigned short, mbf);
-    img[base + 2 * per] = __builtin_bit_cast(unsigned short, lb);
+    const float sc = NPL == 2 && m < M ? h3_scale(m_exp[m]) : 1.f;
+    cx_wimg_put<NPL>(img, ((((int64_t)q * mbn + mb) * L + l) * NPL) * per + e, per, v, sc);
   }
 }
 
 // DB: double-buffered patch and weight chunk (2 x 69 KB of LDS) -- channel l + 1 is staged
 // into the other buffer right after the k-steps of channel l, one barrier per channel.  The
 // patch gather offsets (and their bounds) are the same for every channel and are hoisted.
-template <bool DB>
+// NPL 2: fp16x3, scales as conv_x6_kernel's (e_n from the sample's max |dy|, m = ci)
+template <bool DB, int NPL = 3>
 __global__ __launch_bounds__(CX_T, 1) void conv_x6q_dgrad_kernel(const float* __restrict__ dy,
                                                                  const unsigned short* __restrict__ img,
                                                                  float* __restrict__ dx, ConvDims g,
-                                                                 int gx, int gy) {
+                                                                 int gx, int gy,
+                                                                 const int* __restrict__ m_exp,
+                                                                 const unsigned* __restrict__ n_amax) {
   constexpr int NB = DB ? 2 : 1;
   constexpr int WPL = 32 * CQ_COP;
-  constexpr int wstride = 3 * WPL;
-  __shared__ __attribute__((aligned(16))) unsigned short ps[NB * 3 * CQ_PPL];
+  constexpr int wstride = NPL * WPL;
+  __shared__ __attribute__((aligned(16))) unsigned short ps[NB * NPL * CQ_PPL];
   __shared__ __attribute__((aligned(16))) unsigned short ws[NB * wstride];
   const int M = g.ci, L = g.co;
   const int in_h = g.ho, in_w = g.wo, out_h = g.hi, out_w = g.wi;
@@ -1900,6 +2016,8 @@ __global__ __launch_bounds__(CX_T, 1) void conv_x6q_dgrad_kernel(const float* __
   const unsigned short* wimg = img + ((int64_t)q * mbn + mb) * L * wstride;
   constexpr int wchunks = wstride / 8;
   constexpr int WR = (wchunks + CX_T - 1) / CX_T;
+  const int en = NPL == 2 ? h3_exp(n_amax[n]) : 0;
+  const float nsc = h3_scale(en);
 
   // per-thread gather offsets (bytes; out-of-range elements read the buffer's zero tail)
   int goff[2][8];
@@ -1938,11 +2056,11 @@ __global__ __launch_bounds__(CX_T, 1) void conv_x6q_dgrad_kernel(const float* __
     }
   };
   auto store = [&](int b) {
-    unsigned short* pb = ps + b * (3 * CQ_PPL);
+    unsigned short* pb = ps + b * (NPL * CQ_PPL);
     unsigned short* wb = ws + b * wstride;
 #pragma unroll
     for (int u = 0; u < 2; ++u)
-      if (soff[u] >= 0) cw_split_store(pb, CQ_PPL, soff[u], rp[u]);
+      if (soff[u] >= 0) cx_store8<NPL>(pb, CQ_PPL, soff[u], rp[u], nsc);
 #pragma unroll
     for (int r = 0; r < WR; ++r) {
       const int i = tid + CX_T * r;
@@ -1966,32 +2084,24 @@ __global__ __launch_bounds__(CX_T, 1) void conv_x6q_dgrad_kernel(const float* __
     const int cur = DB ? (l & 1) : 0;
     if (l + 1 < L) load(l + 1);
     if (active) {
-      const unsigned short* pc = ps + cur * (3 * CQ_PPL);
+      const unsigned short* pc = ps + cur * (NPL * CQ_PPL);
       const unsigned short* wc = ws + cur * wstride;
       auto kstep = [&](int st) {
         const int rq = st / 3, cq = st - (st / 3) * 3;
         bf16x8 af[3], bfr[2][3];
         const int aw = fr * CQ_COP + (st * 2 + fh) * 8;
 #pragma unroll
-        for (int pl = 0; pl < 3; ++pl) af[pl] = *reinterpret_cast<const bf16x8*>(wc + pl * WPL + aw);
+        for (int pl = 0; pl < NPL; ++pl) af[pl] = *reinterpret_cast<const bf16x8*>(wc + pl * WPL + aw);
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
           const int sc = 64 * cw + 32 * j + fr + 4 * cq + 2 * fh;   // first patch column
           const int ap = (sc & 1) * CQ_OFFO + (sc >> 1) * CQ_PP + 8 * rq;
 #pragma unroll
-          for (int pl = 0; pl < 3; ++pl)
+          for (int pl = 0; pl < NPL; ++pl)
             bfr[j][pl] = *reinterpret_cast<const bf16x8*>(pc + pl * CQ_PPL + ap);
         }
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          f32x16 cc = acc[j];
-          cc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1], bfr[j][1], cc, 0, 0, 0);
-          cc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[2], bfr[j][0], cc, 0, 0, 0);
-          cc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bfr[j][2], cc, 0, 0, 0);
-          cc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1], bfr[j][0], cc, 0, 0, 0);
-          cc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bfr[j][1], cc, 0, 0, 0);
-          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bfr[j][0], cc, 0, 0, 0);
-        }
+        for (int j = 0; j < 2; ++j) acc[j] = cx_mma<NPL>(af, bfr[j], acc[j]);
       };
       if (kk == 0) {
 #pragma unroll
@@ -2030,9 +2140,11 @@ __global__ __launch_bounds__(CX_T, 1) void conv_x6q_dgrad_kernel(const float* __
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int m = m0 + (r & 3) + 8 * (r >> 2) + 4 * fh;
-      if (m < M)
-        dx[(((int64_t)n * M + m) * out_h + orow) * out_w + col] =
-            acc[j][r] + red[((cw * 2 + j) * 16 + r) * 64 + lane];
+      if (m < M) {
+        float v = acc[j][r] + red[((cw * 2 + j) * 16 + r) * 64 + lane];
+        if (NPL == 2) v = __builtin_ldexpf(v, -(m_exp[m] + en));
+        dx[(((int64_t)n * M + m) * out_h + orow) * out_w + col] = v;
+      }
     }
   }
 }
@@ -2118,32 +2230,86 @@ static inline bool x6q_ok(const ConvDims& g) {
   return plane * 4 < (1ll << 31) - 64 && wimg < (1ll << 31) - 64;
 }
 
+// fp16x3 for the conv2-shaped bf16x6 kernels (the double-buffered forward and the 4 x 2
+// dgrad; DS2_CONV_H3=0 keeps bf16x6): two fp16 planes per image / patch instead of three bf16,
+// three MFMAs per fragment pair instead of six, and per-row power-of-two scales
+static inline bool h3c_on() {
+  const char* e = getenv("DS2_CONV_H3");
+  return !(e != nullptr && e[0] == '0');
+}
+
+// workspace of a split-weight image of `elems` values per plane: NPL 3 planes, or 2 planes +
+// the fp16x3 scales (m_exp[M] int, n_amax[n] unsigned) at the next 256-B boundary
+static size_t cx_ws_bytes(int64_t elems, int M, int n) {
+  const size_t x6 = (size_t)elems * 3 * sizeof(unsigned short);
+  const size_t h3 = ((size_t)elems * 2 * sizeof(unsigned short) + 255) / 256 * 256 +
+                    ((size_t)M + (size_t)n) * 4;
+  return x6 > h3 ? x6 : h3;
+}
+
+// the fp16x3 scales: m_exp (per output row m of the implicit GEMM) and n_amax (per sample of the
+// staged input `in`, [n][L][plane_in])
+template <bool DGRAD>
+static void cx_h3_scales(const float* in, const float* w, const ConvDims& g, int64_t elems,
+                         void* ws, int*& m_exp, unsigned*& n_amax, hipStream_t st) {
+  const int M = DGRAD ? g.ci : g.co;
+  const int L = DGRAD ? g.co : g.ci;
+  const int64_t per = (int64_t)L * (DGRAD ? (int64_t)g.ho * g.wo : (int64_t)g.hi * g.wi);
+  char* base = static_cast<char*>(ws) + ((size_t)elems * 2 * sizeof(unsigned short) + 255) / 256 * 256;
+  m_exp = reinterpret_cast<int*>(base);
+  n_amax = reinterpret_cast<unsigned*>(base + (size_t)M * 4);
+  hipLaunchKernelGGL(conv_h3_wexp_kernel<DGRAD>, dim3(M), dim3(256), 0, st, w, g, m_exp);
+  hipMemsetAsync(n_amax, 0, (size_t)g.n * 4, st);
+  int64_t chunks = cdiv(per, 8192);
+  const int64_t cap = cdiv(2048, g.n);
+  chunks = chunks < 1 ? 1 : (chunks > cap ? cap : chunks);
+  hipLaunchKernelGGL(conv_h3_samax_kernel, dim3(static_cast<unsigned>(chunks), g.n), dim3(256), 0, st,
+                     in, per, n_amax);
+}
+
+static int64_t x6q_img_elems(const ConvDims& g) {
+  return (int64_t)g.sh * ((g.ci + 31) / 32) * g.co * 32 * CQ_COP;
+}
+
 static size_t x6q_ws_bytes(const ConvDims& g) {
   if (!x6q_ok(g)) return 0;
-  return (size_t)g.sh * ((g.ci + 31) / 32) * g.co * 3 * 32 * CQ_COP * sizeof(unsigned short);
+  return cx_ws_bytes(x6q_img_elems(g), g.ci, g.n);
 }
 
 static ds2_status_t launch_x6q(const float* dy, const float* w, float* dx, const ConvDims& g,
                                void* ws, hipStream_t st) {
   unsigned short* img = static_cast<unsigned short*>(ws);
-  const int64_t total = (int64_t)x6q_ws_bytes(g) / 6;
-  hipLaunchKernelGGL(conv_x6q_wimg_kernel, dim3(cdiv(total, 256) > 2048 ? 2048 : cdiv(total, 256)),
-                     dim3(256), 0, st, w, g, img);
+  const int64_t total = x6q_img_elems(g);
+  const int wgrid = cdiv(total, 256) > 2048 ? 2048 : cdiv(total, 256);
   const int gx = cdiv(g.wi, CX_COLS);
   const int64_t nwg = (int64_t)gx * g.hi * g.n * cdiv(g.ci, 32);
   if (nwg > 0x7fffffff) return DS2_UNSUPPORTED_SHAPE;
-  hipLaunchKernelGGL(conv_x6q_dgrad_kernel<true>, dim3(static_cast<unsigned>(nwg)), dim3(CX_T), 0, st,
-                     dy, img, dx, g, gx, g.hi);
+  if (h3c_on()) {
+    int* m_exp;
+    unsigned* n_amax;
+    cx_h3_scales<true>(dy, w, g, total, ws, m_exp, n_amax, st);
+    hipLaunchKernelGGL(conv_x6q_wimg_kernel<2>, dim3(wgrid), dim3(256), 0, st, w, g, img, m_exp);
+    hipLaunchKernelGGL((conv_x6q_dgrad_kernel<true, 2>), dim3(static_cast<unsigned>(nwg)), dim3(CX_T),
+                       0, st, dy, img, dx, g, gx, g.hi, m_exp, n_amax);
+  } else {
+    hipLaunchKernelGGL(conv_x6q_wimg_kernel<3>, dim3(wgrid), dim3(256), 0, st, w, g, img, nullptr);
+    hipLaunchKernelGGL((conv_x6q_dgrad_kernel<true, 3>), dim3(static_cast<unsigned>(nwg)), dim3(CX_T),
+                       0, st, dy, img, dx, g, gx, g.hi, nullptr, nullptr);
+  }
   return launch_status("ds2_conv2d_dgrad");
 }
 
-static size_t x6_ws_bytes(const ConvDims& g, bool dgrad) {
-  if (!x6_ok(g, dgrad)) return 0;
+static int64_t x6_img_elems(const ConvDims& g, bool dgrad) {
   const CxGeom c = cx_geom(g, dgrad);
   const int M = dgrad ? g.ci : g.co;
   const int L = dgrad ? g.co : g.ci;
   const int classes = dgrad ? g.sh : 1;
-  return (size_t)classes * ((M + 31) / 32) * L * c.RC * 3 * 32 * c.COP * sizeof(unsigned short);
+  return (int64_t)classes * ((M + 31) / 32) * L * c.RC * 32 * c.COP;
+}
+
+static size_t x6_ws_bytes(const ConvDims& g, bool dgrad) {
+  if (!x6_ok(g, dgrad)) return 0;
+  return cx_ws_bytes(x6_img_elems(g, dgrad), dgrad ? g.ci : g.co, g.n);
 }
 
 template <bool DGRAD>
@@ -2151,9 +2317,8 @@ static ds2_status_t launch_x6(const float* in, const float* w, const float* bias
                               const ConvDims& g, const int* out_lens, void* ws, hipStream_t st) {
   const CxGeom c = cx_geom(g, DGRAD);
   unsigned short* img = static_cast<unsigned short*>(ws);
-  const int64_t total = (int64_t)x6_ws_bytes(g, DGRAD) / 6;   // elements of one plane set
-  hipLaunchKernelGGL(conv_x6_wimg_kernel<DGRAD>, dim3(cdiv(total, 256) > 2048 ? 2048 : cdiv(total, 256)),
-                     dim3(256), 0, st, w, g, c, img);
+  const int64_t total = x6_img_elems(g, DGRAD);   // elements of one plane
+  const int wgrid = cdiv(total, 256) > 2048 ? 2048 : cdiv(total, 256);
   const int M = DGRAD ? g.ci : g.co;
   const int gy = DGRAD ? g.hi : g.ho;
   const int gx = cdiv(DGRAD ? g.wi : g.wo, CX_COLS);
@@ -2164,7 +2329,7 @@ static ds2_status_t launch_x6(const float* in, const float* w, const float* bias
   bool small = g.sw == 1 && c.RC == 1 && 3 * c.PCOL * c.P <= CX_PATCH1 && c.PCOL * nga <= 2 * CX_T;
 #define DS2_CX(NG, NB, PU, SW, RCH)                                                          \
   hipLaunchKernelGGL((conv_x6_kernel<DGRAD, NG, NB, PU, SW, RCH>), grid, dim3(CX_T), 0, st, in, \
-                     img, bias, out, g, out_lens, c, gx, gy)
+                     img, bias, out, g, out_lens, c, gx, gy, nullptr, nullptr)
   // the compile-time-geometry instantiations must see the geometry cx_geom computed
   const bool c36 = c.KA == CxConst<3, 6>::KA && c.P == CxConst<3, 6>::P &&
                    c.COP == CxConst<3, 6>::COP && c.PCOL == CxConst<3, 6>::PCOL && c.NBP == 6;
@@ -2172,9 +2337,20 @@ static ds2_status_t launch_x6(const float* in, const float* w, const float* bias
                    c.COP == CxConst<2, 6>::COP && c.PCOL == CxConst<2, 6>::PCOL && c.NBP == 6;
   small = small && (DGRAD ? c26 : c36);
   const bool db = small && 2 * 3 * c.PCOL * c.P <= CX_PATCH_DB;
-  if (small && !DGRAD && nga == 3 && c.NBP == 6 && db)
+  const bool conv2f = small && !DGRAD && nga == 3 && c.NBP == 6 && db;
+  if (conv2f && h3c_on()) {                              // conv2 fwd, fp16x3
+    int* m_exp;
+    unsigned* n_amax;
+    cx_h3_scales<DGRAD>(in, w, g, total, ws, m_exp, n_amax, st);
+    hipLaunchKernelGGL((conv_x6_wimg_kernel<DGRAD, 2>), dim3(wgrid), dim3(256), 0, st, w, g, c, img, m_exp);
+    hipLaunchKernelGGL((conv_x6_kernel<DGRAD, 3, 6, 2, 1, false, true, 2>), grid, dim3(CX_T), 0, st,
+                       in, img, bias, out, g, out_lens, c, gx, gy, m_exp, n_amax);
+    return launch_status("ds2_conv2d_fwd");
+  }
+  hipLaunchKernelGGL((conv_x6_wimg_kernel<DGRAD, 3>), dim3(wgrid), dim3(256), 0, st, w, g, c, img, nullptr);
+  if (conv2f)
     hipLaunchKernelGGL((conv_x6_kernel<DGRAD, 3, 6, 2, 1, false, true>), grid, dim3(CX_T), 0, st,
-                       in, img, bias, out, g, out_lens, c, gx, gy);   // conv2 fwd, double-buffered
+                       in, img, bias, out, g, out_lens, c, gx, gy, nullptr, nullptr);   // conv2 fwd, double-buffered
   else if (small && !DGRAD && nga == 3 && c.NBP == 6)
     DS2_CX(3, 6, 2, 1, false);                           // conv2 fwd
   else if (small && DGRAD && nga == 2 && c.NBP == 6)

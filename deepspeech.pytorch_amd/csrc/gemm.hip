@@ -906,18 +906,6 @@ __device__ __forceinline__ void x2_store160(unsigned short* __restrict__ s, cons
   }
 }
 
-// fp16x3 row scales.  amax: the bit pattern of max |x| over a logical row (non-negative floats
-// order as unsigned).  The row is staged as x 2^e, e = 14 - floor(log2 amax), so its largest
-// element lies in [2^14, 2^15) (fp16 max 65504) and its fp16 (hi, lo) split keeps 22 bits for
-// every element within 2^17 of the row max; a zero, inf or NaN row max keeps e = 0.
-__device__ __forceinline__ int h3_exp(unsigned amax) {
-  const int E = (int)(amax >> 23);                 // biased exponent (sign bit is 0)
-  if (amax == 0u || E >= 255) return 0;
-  int e = 14 - ((E == 0 ? 1 : E) - 127);
-  return e > 127 ? 127 : e;                        // 2^e stays a normal float
-}
-__device__ __forceinline__ float h3_scale(int e) { return __builtin_bit_cast(float, (e + 127) << 23); }
-
 // NPL 3: the bf16x6 fp32-accurate GEMM; NPL 1: the bf16-operand GEMM (operands rounded to
 // bf16 while staged, one product per fragment pair, fp32 accumulation -- cfg4's opt-in
 // precision), one LDS plane per operand

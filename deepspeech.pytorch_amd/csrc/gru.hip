@@ -1060,6 +1060,17 @@ bool launch_gru_bwd_x6(int t_max, int n, int h, int num_dirs, const float* dy, i
                        double* dbp, size_t lds_pad, hipStream_t st, unsigned* camax,
                        bool* camax_done);
 int gru_bwd_x6_grid(int n, int h, int num_dirs);
+bool launch_rnn_fwd_h3(int t_max, int n, int h, int num_dirs, const float* xproj,
+                       const float* w_hh_f, const float* w_hh_r, const float* b_hh_f,
+                       const float* b_hh_r, const int* lens, float* h_all, float* ring,
+                       unsigned* ctrs, unsigned* err, unsigned long long* stamps, size_t lds_pad,
+                       hipStream_t st);
+bool launch_rnn_bwd_h3(int t_max, int n, int h, int num_dirs, const float* dy, int dy_dirs,
+                       const float* w_hh_f, const float* w_hh_r, const float* h_all,
+                       const int* lens, float* dgates, float* ring, unsigned* ctrs, unsigned* err,
+                       unsigned long long* stamps, size_t lds_pad, hipStream_t st,
+                       unsigned* camax);
+int rnn_h3_grid(int n, int h, int num_dirs);
 }  // namespace ds2
 
 using namespace ds2;
@@ -1466,6 +1477,105 @@ static ds2_status_t gru_bwd_run(int t_max, int n, int h, int num_dirs, const flo
     }
   }
   return launch_status("ds2_gru_bwd");
+}
+
+// ---------------------------------------------------------------------------------------
+// supported_rnns['rnn'] (nn.RNN, tanh; model.py:15) on the persistent machinery: the
+// one-gate fp16x3 instantiations of the GRU recurrences (gru_split.hip), falling back to the
+// per-step kernels of rnn.hip (ds2_rnn_fwd / ds2_rnn_bwd) where they decline the shape or
+// DS2_RNN_PERSISTENT=0.  Workspace: the counters and the hand-off ring.
+static bool rnn_persistent_ok(int t_max, int n, int h, int num_dirs) {
+  const int g = rnn_h3_grid(n, h, num_dirs);
+  return persistent_enabled() && g > 0 && g <= num_cus() &&
+         (int64_t)t_max * n * num_dirs * h * 4 < (1ll << 31);
+}
+
+size_t ds2_rnn_fwd_workspace_size(int n, int h, int num_dirs) {
+  if (n < 1 || h < 1 || num_dirs < 1) return 256;
+  return align256(counter_bytes(n, num_dirs)) + ring_bytes(n, h, num_dirs, 1) + 256;
+}
+
+ds2_status_t ds2_rnn_fwd_ws(int t_max, int n, int h, int num_dirs, const float* xproj,
+                            const float* w_hh_f, const float* w_hh_r, const float* b_hh_f,
+                            const float* b_hh_r, const int* lens, float* h_all, unsigned* err_out,
+                            void* ws, size_t ws_bytes, ds2_stream_t stream) {
+  if (t_max < 0 || n < 0 || h < 1 || (num_dirs != 1 && num_dirs != 2)) return DS2_INVALID_VALUE;
+  if (t_max == 0 || n == 0) return DS2_OK;
+  if (xproj == nullptr || w_hh_f == nullptr || b_hh_f == nullptr || lens == nullptr ||
+      h_all == nullptr || (num_dirs == 2 && (w_hh_r == nullptr || b_hh_r == nullptr)))
+    return DS2_INVALID_VALUE;
+  if (ws == nullptr || ws_bytes < ds2_rnn_fwd_workspace_size(n, h, num_dirs))
+    return DS2_WORKSPACE_TOO_SMALL;
+  if (num_dirs == 1) {
+    w_hh_r = w_hh_f;
+    b_hh_r = b_hh_f;
+  }
+  hipStream_t st = as_stream(stream);
+  if (rnn_persistent_ok(t_max, n, h, num_dirs)) {
+    unsigned* ctrs = static_cast<unsigned*>(ws);
+    unsigned* err = ctrs + num_dirs * ((n + GB - 1) / GB);
+    float* ring = reinterpret_cast<float*>(static_cast<char*>(ws) + align256(counter_bytes(n, num_dirs)));
+    if (hipMemsetAsync(ctrs, 0, counter_bytes(n, num_dirs), st) != hipSuccess)
+      return launch_status("ds2_rnn counters");
+    if (ring_reset(ring, n, h, num_dirs, st) != hipSuccess) return launch_status("ds2_rnn ring");
+    unsigned long long* stamps = stamp_mode() == 2 ? stamp_slots(ctrs, n, num_dirs) : nullptr;
+    if (launch_rnn_fwd_h3(t_max, n, h, num_dirs, xproj, w_hh_f, w_hh_r, b_hh_f, b_hh_r, lens,
+                          h_all, ring, ctrs, err, stamps, kDopPadLds, st)) {
+      fold_err(err, err_out, st);
+      return launch_status("ds2_rnn_fwd");
+    }
+    (void)hipGetLastError();
+  }
+  return ds2_rnn_fwd(t_max, n, h, num_dirs, xproj, w_hh_f, w_hh_r, b_hh_f, b_hh_r, lens, h_all,
+                     stream);
+}
+
+size_t ds2_rnn_bwd_workspace_size(int n, int h, int num_dirs) {
+  if (n < 1 || h < 1 || num_dirs < 1) return 256;
+  return align256(counter_bytes(n, num_dirs)) + ring_bytes(n, h, num_dirs, 3) + 256;
+}
+
+int ds2_rnn_bwd_grid(int n, int h, int num_dirs) {
+  if (n < 1 || h < 1 || (num_dirs != 1 && num_dirs != 2)) return 0;
+  const int g = rnn_h3_grid(n, h, num_dirs);
+  return persistent_enabled() && g > 0 && g <= num_cus() ? g : 0;
+}
+
+ds2_status_t ds2_rnn_bwd_ws(int t_max, int n, int h, int num_dirs, const float* dy, int dy_dirs,
+                            const float* w_hh_f, const float* w_hh_r, const float* h_all,
+                            const int* lens, float* dgates, unsigned* col_amax, unsigned* err_out,
+                            void* ws, size_t ws_bytes, ds2_stream_t stream) {
+  if (t_max < 0 || n < 0 || h < 1 || (num_dirs != 1 && num_dirs != 2)) return DS2_INVALID_VALUE;
+  if (dy_dirs != 1 && dy_dirs != num_dirs) return DS2_INVALID_VALUE;
+  if (ws == nullptr || ws_bytes < ds2_rnn_bwd_workspace_size(n, h, num_dirs))
+    return DS2_WORKSPACE_TOO_SMALL;
+  hipStream_t st = as_stream(stream);
+  if (col_amax != nullptr &&
+      hipMemsetAsync(col_amax, 0, (size_t)num_dirs * h * sizeof(unsigned), st) != hipSuccess)
+    return launch_status("ds2_rnn_bwd_ws");
+  if (t_max == 0 || n == 0) return DS2_OK;
+  if (dy == nullptr || w_hh_f == nullptr || h_all == nullptr || lens == nullptr ||
+      dgates == nullptr || (num_dirs == 2 && w_hh_r == nullptr))
+    return DS2_INVALID_VALUE;
+  if (num_dirs == 1) w_hh_r = w_hh_f;
+  if (rnn_persistent_ok(t_max, n, h, num_dirs)) {
+    unsigned* ctrs = static_cast<unsigned*>(ws);
+    unsigned* err = ctrs + num_dirs * ((n + GB - 1) / GB);
+    float* ring = reinterpret_cast<float*>(static_cast<char*>(ws) + align256(counter_bytes(n, num_dirs)));
+    if (hipMemsetAsync(ctrs, 0, counter_bytes(n, num_dirs), st) != hipSuccess)
+      return launch_status("ds2_rnn counters");
+    unsigned long long* stamps = stamp_mode() == 2 ? stamp_slots(ctrs, n, num_dirs) : nullptr;
+    if (launch_rnn_bwd_h3(t_max, n, h, num_dirs, dy, dy_dirs, w_hh_f, w_hh_r, h_all, lens, dgates,
+                          ring, ctrs, err, stamps, kDopPadLds, st, col_amax)) {
+      fold_err(err, err_out, st);
+      return launch_status("ds2_rnn_bwd");
+    }
+    (void)hipGetLastError();
+  }
+  const ds2_status_t rc = ds2_rnn_bwd(t_max, n, h, num_dirs, dy, dy_dirs, w_hh_f, w_hh_r, h_all,
+                                      lens, dgates, stream);
+  if (rc != DS2_OK || col_amax == nullptr) return rc;
+  return ds2_amax(dgates, t_max * n, num_dirs * h, num_dirs * h, nullptr, col_amax, stream);
 }
 
 }  // extern "C"

@@ -63,52 +63,6 @@ __device__ __forceinline__ f32x4 mma6(const Tri& a, const Tri& b, f32x4 c) {
   return c;
 }
 
-// fp16x3 (the forward's default since round 5): a value x of a row scaled by 2^e into
-// [2^14, 2^15) splits into hi = f16(x 2^e) and lo = f16(x 2^e - hi) (22 significant bits
-// kept for every element within 2^17 of the row's max), and a.b takes three products
-// lo.hi + hi.lo + hi.hi on v_mfma_f32_16x16x32_f16 (each exact in fp32): half the MFMAs of
-// the bf16x6 form and two operand planes instead of three.  h (|h| <= 1) takes the fixed
-// scale 2^14; each W_hh row (gate, unit) its own, found at kernel start.
-typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
-typedef _Float16 f16x2h __attribute__((ext_vector_type(2)));
-struct Duo {
-  f16x8 hi, lo;
-};
-
-// 8 fp32 values (k slots 0..3 from a, 4..7 from b) times sc -> fp16 (hi, lo)
-__device__ __forceinline__ Duo split2h(const f32x4 a, const f32x4 b, float sc) {
-  typedef float f32x2v __attribute__((ext_vector_type(2)));
-  Duo t;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const f32x2v x = (j < 2 ? f32x2v{a[2 * j], a[2 * j + 1]} : f32x2v{b[2 * j - 4], b[2 * j - 3]}) * sc;
-    const f16x2h h = __builtin_convertvector(x, f16x2h);
-    const f16x2h l = __builtin_convertvector(x - __builtin_convertvector(h, f32x2v), f16x2h);
-    t.hi[2 * j] = h[0];
-    t.hi[2 * j + 1] = h[1];
-    t.lo[2 * j] = l[0];
-    t.lo[2 * j + 1] = l[1];
-  }
-  return t;
-}
-
-// c += a.b from the fp16 terms (small terms first)
-__device__ __forceinline__ f32x4 mma3h(const Duo& a, const Duo& b, f32x4 c) {
-  c = __builtin_amdgcn_mfma_f32_16x16x32_f16(a.lo, b.hi, c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_16x16x32_f16(a.hi, b.lo, c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_16x16x32_f16(a.hi, b.hi, c, 0, 0, 0);
-  return c;
-}
-
-// 2^e scale of a row whose max |x| is m (m > 0 finite: m 2^e in [2^14, 2^15); else 1)
-__device__ __forceinline__ int h3_row_exp(float m) {
-  const unsigned u = __float_as_uint(m);
-  const int E = (int)(u >> 23);
-  if (u == 0u || E >= 255) return 0;
-  const int e = 14 - ((E == 0 ? 1 : E) - 127);
-  return e > 127 ? 127 : e;
-}
-
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
@@ -149,7 +103,9 @@ __device__ __forceinline__ void pair_split(int pairs, int wave, int& p0, int& np
 // ---------------------------------------------------------------------------------------
 // forward: gh[16 samples x 48] = h_{t-1}[16 x H] . W_hh[r, z, n rows of 16 units]^T, with
 // the sentinel-ring hand-off of gru_fwd_dop_kernel (the data is the flag).
-template <int NP, bool H3 = false>
+// NG = 1: the one-gate instantiation for supported_rnns['rnn'] (nn.RNN, tanh; model.py:15):
+// gh[16 x 16] = h_{t-1} . W_hh[16 units]^T and h_t = tanh(xproj_t + gh + b_hh), no gate cache.
+template <int NP, bool H3 = false, int NG = 3>
 __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(1, 1))) void gru_fwd_x6_kernel(
     int T, int N, int H, int D, int UB, int BT, const float* __restrict__ xproj,
     const float* __restrict__ w_f, const float* __restrict__ w_r, const float* __restrict__ b_f,
@@ -157,7 +113,8 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     float* __restrict__ gates, float* __restrict__ hx, unsigned* __restrict__ counters,
     unsigned* __restrict__ err, unsigned long long* __restrict__ stamps, int xmode) {
   static_assert(2 * NP <= 64, "tsame holds a wave's tiles");
-  constexpr int RP = 3 * GU + 1;
+  static_assert(NG == 3 || (NG == 1 && H3), "the one-gate form is fp16x3 only");
+  constexpr int RP = NG * GU + 1;
   constexpr int NSLOT = kRingSlots;
   __shared__ float red[XW * GB * RP];
   __shared__ __attribute__((aligned(16))) float tile[GB * GU];
@@ -198,10 +155,12 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   // W_hh split fragments: pair p, gate g, k slot j -> W[g H + 16 ub + (lane & 15)]
   //   [16 (t_first + 2p + (j >> 2)) + 4 (lane >> 4) + (j & 3)]
   using WT = typename std::conditional<H3, Duo, Tri>::type;
-  WT w[3][NP];
+  WT w[NG][NP];
   // fp16x3: 2^-(e(g, unit) + 14) undoes the row scale of W_hh and the fixed 2^14 of h; the
   // owner thread's unit u = threadIdx.x & 15
-  float unscale[3] = {1.f, 1.f, 1.f};
+  float unscale[NG];
+#pragma unroll
+  for (int g = 0; g < NG; ++g) unscale[g] = 1.f;
   {
     const float* W = d == 0 ? w_f : w_r;
     const float* wr = W + (int64_t)(ub * GU + (lane & 15)) * H + 4 * (lane >> 4);
@@ -215,29 +174,31 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     if constexpr (H3) {
       // max |W| of each (gate, unit) row over the whole K: the lane's share, the 4 lanes
       // of its unit, then the workgroup's waves (LDS, reusing `red`)
-      float mx[3] = {0.f, 0.f, 0.f};
+      float mx[NG];
+#pragma unroll
+      for (int g = 0; g < NG; ++g) mx[g] = 0.f;
 #pragma unroll
       for (int p = 0; p < NP; ++p)
 #pragma unroll
-        for (int g = 0; g < 3; ++g) {
+        for (int g = 0; g < NG; ++g) {
           f32x4 a, b;
           frag(p, g, a, b);
 #pragma unroll
           for (int j = 0; j < 4; ++j) mx[g] = fmaxf(mx[g], fmaxf(fabsf(a[j]), fabsf(b[j])));
         }
 #pragma unroll
-      for (int g = 0; g < 3; ++g) {
+      for (int g = 0; g < NG; ++g) {
         mx[g] = fmaxf(mx[g], __shfl_xor(mx[g], 16));
         mx[g] = fmaxf(mx[g], __shfl_xor(mx[g], 32));
-        if (lane < 16) red[(wave * 3 + g) * 16 + lane] = mx[g];
+        if (lane < 16) red[(wave * NG + g) * 16 + lane] = mx[g];
       }
       __syncthreads();
-      int eg[3];
+      int eg[NG];
 #pragma unroll
-      for (int g = 0; g < 3; ++g) {
+      for (int g = 0; g < NG; ++g) {
         float m = 0.f;
 #pragma unroll
-        for (int w8 = 0; w8 < XW; ++w8) m = fmaxf(m, red[(w8 * 3 + g) * 16 + (lane & 15)]);
+        for (int w8 = 0; w8 < XW; ++w8) m = fmaxf(m, red[(w8 * NG + g) * 16 + (lane & 15)]);
         eg[g] = h3_row_exp(m);
         // the owner thread's unit is threadIdx.x & 15 = lane & 15: the same row
         unscale[g] = __builtin_ldexpf(1.f, -(eg[g] + 14));
@@ -246,7 +207,7 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
 #pragma unroll
       for (int p = 0; p < NP; ++p)
 #pragma unroll
-        for (int g = 0; g < 3; ++g) {
+        for (int g = 0; g < NG; ++g) {
           f32x4 a, b;
           frag(p, g, a, b);
           w[g][p] = split2h(a, b, __builtin_ldexpf(1.f, eg[g]));
@@ -272,8 +233,10 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   int len = 0;
   if (owner) {
     bias_r = bh[j];
-    bias_z = bh[H + j];
-    bias_n = bh[2 * H + j];
+    if constexpr (NG == 3) {
+      bias_z = bh[H + j];
+      bias_n = bh[2 * H + j];
+    }
     len = lens[n];
   }
   settle(bias_r);
@@ -288,14 +251,16 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     const int64_t row = ((int64_t)t * N + n) * D + d;
     float xr = 0.f, xz = 0.f, xn = 0.f;
     if (owner && t < len) {
-      const float* xp = xproj + row * 3 * H;
+      const float* xp = xproj + row * NG * H;
       xr = xp[j];
-      xz = xp[H + j];
-      xn = xp[2 * H + j];
+      if constexpr (NG == 3) {
+        xz = xp[H + j];
+        xn = xp[2 * H + j];
+      }
     }
-    f32x4 acc[3];
+    f32x4 acc[NG];
 #pragma unroll
-    for (int g = 0; g < 3; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int g = 0; g < NG; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
     trace_at(s, 0);
     if (s > 0) {
       trace_at(s, 1);
@@ -325,11 +290,11 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
       __builtin_amdgcn_sched_barrier(0);
       // per-pair partials summed in a fixed order afterwards: pairs are multiplied in
       // arrival order (one re-load round trip per pass), the result is deterministic
-      f32x4 pacc[NP][3];
+      f32x4 pacc[NP][NG];
 #pragma unroll
       for (int p = 0; p < NP; ++p)
 #pragma unroll
-        for (int g = 0; g < 3; ++g) pacc[p][g] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int g = 0; g < NG; ++g) pacc[p][g] = f32x4{0.f, 0.f, 0.f, 0.f};
       unsigned pend = (1u << np) - 1u;
       for (unsigned spins = 0;; ++spins) {
 #pragma unroll
@@ -338,11 +303,11 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
             if constexpr (H3) {
               const Duo a = split2h(hv[2 * p], hv[2 * p + 1], 16384.f);
 #pragma unroll
-              for (int g = 0; g < 3; ++g) pacc[p][g] = mma3h(a, w[g][p], pacc[p][g]);
+              for (int g = 0; g < NG; ++g) pacc[p][g] = mma3h(a, w[g][p], pacc[p][g]);
             } else {
               const Tri a = split3(hv[2 * p], hv[2 * p + 1]);
 #pragma unroll
-              for (int g = 0; g < 3; ++g) pacc[p][g] = mma6(a, w[g][p], pacc[p][g]);
+              for (int g = 0; g < NG; ++g) pacc[p][g] = mma6(a, w[g][p], pacc[p][g]);
             }
             pend &= ~(1u << p);
           }
@@ -363,7 +328,7 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
                            x_rs, base + i * 1024 + (((tsame >> i) & 1ull) ? aoff : 0), 0, kSc1));
       }
 #pragma unroll
-      for (int g = 0; g < 3; ++g) {
+      for (int g = 0; g < NG; ++g) {
         acc[g] = pacc[0][g];
 #pragma unroll
         for (int p = 1; p < NP; ++p) acc[g] += pacc[p][g];
@@ -371,7 +336,7 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
       trace_at(s, 2);
     }
 #pragma unroll
-    for (int g = 0; g < 3; ++g)
+    for (int g = 0; g < NG; ++g)
 #pragma unroll
       for (int r = 0; r < 4; ++r)
         red[(wave * GB + (lane >> 4) * 4 + r) * RP + g * GU + (lane & 15)] = acc[g][r];
@@ -385,10 +350,18 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     }
     trace_at(s, 3);
     float hout = 0.f;
-    if (owner) {
-      float gh[3];
+    if constexpr (NG == 1) {
+      if (owner) {
+        float v = 0.f;
 #pragma unroll
-      for (int g = 0; g < 3; ++g) {
+        for (int w8 = 0; w8 < XW; ++w8) v += red[(w8 * GB + m) * RP + u];
+        if (t < len) hout = tanh_fast(xr + (v * unscale[0] + bias_r));
+        h_own = hout;
+      }
+    } else if (owner) {
+      float gh[NG];
+#pragma unroll
+      for (int g = 0; g < NG; ++g) {
         float v = 0.f;
 #pragma unroll
         for (int w8 = 0; w8 < XW; ++w8) v += red[(w8 * GB + m) * RP + g * GU + u];
@@ -429,7 +402,7 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     trace_at(s, 4);
     if (owner) {
       h_all[row * H + j] = h_own;
-      if (gates != nullptr) {
+      if (NG == 3 && gates != nullptr) {
         float* gp = gates + g_row * 4 * H;
         gp[j] = g_r;
         gp[H + j] = g_z;
@@ -703,9 +676,22 @@ __global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
 // adds the temporary into its sum row-scaled by the producer's 2^-e: the products of one
 // producer share their rows' scales, so the scale applies after the MFMAs.  W_hh^T is
 // scaled per column (unit) by 2^e found at kernel start and undone on the reduced sum.
+// NG = 1: the one-gate instantiation for supported_rnns['rnn'] (nn.RNN, tanh): the record is
+// the pre-activation gradient da = (dy + W_hh^T da_next) (1 - h^2) of 16 samples x 16 units
+// in the n tile's layout, [0, 1 KB), and the 16 row factors at 1 KB (272 floats); gates = NULL,
+// h_all supplies h_t; dgx receives da ([T][N][D][H]); dgh and dbp are unused.
+// NG = 4: the LSTM (supported_rnns['lstm'], model.py:14; gate order i, f, g, o): the record
+// holds dai, daf as the first pair and dag, dao as the second, [0, 1 KB) hi (i, f), [1, 2 KB)
+// lo (i, f), [2, 3 KB) hi (g, o), [3, 4 KB) lo (g, o), row factors at 4 KB (1040 floats);
+// `h_all` is c_all ([T][N][D][H] cell states), `gates` the [T][N][D][4H] activation cache,
+// dgx receives dgates ([T][N][D][4H]); dgh and dbp are unused; the carried dc lives in a
+// register.  n_base: the first sample of this launch (the batch runs as consecutive chunks of
+// 16-sample tiles when one launch of all of them would not fit the chip).
 constexpr int HBR = 784;   // floats per producer record (3 x 256 + 16)
+constexpr int HBR1 = 272;  // the one-gate record (256 + 16)
+constexpr int HBR4 = 1040; // the LSTM record (4 x 256 + 16)
 typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
-template <int NPW>
+template <int NPW, int NG = 3>
 __global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(2, 2))) void gru_bwd_h3_kernel(
     int T, int N, int H, int D, int UB, int BT, const float* __restrict__ dy, int dyd,
     const float* __restrict__ w_f, const float* __restrict__ w_r,
@@ -713,22 +699,27 @@ __global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     const int* __restrict__ lens, float* __restrict__ dgx, float* __restrict__ dgh,
     float* __restrict__ gx, unsigned* __restrict__ counters, unsigned* __restrict__ err,
     unsigned long long* __restrict__ stamps, double* __restrict__ dbp, int xmode,
-    unsigned* __restrict__ camax) {
+    unsigned* __restrict__ camax, int n_base) {
   static_assert(NPW <= 8, "producers per wave");
+  static_assert(NG == 3 || NG == 1 || NG == 4, "GRU, one-gate RNN or LSTM");
   constexpr int RP = GU + 1;
-  constexpr int LWP = NPW < 3 ? NPW : 3;        // producers' records in flight per wave
+  constexpr int HB = NG == 3 ? HBR : (NG == 4 ? HBR4 : HBR1);   // record floats
+  constexpr int NO = NG >= 3 ? 2048 : 0;       // byte offset of the n-layout tile (LSTM: hi (g, o))
+  constexpr int SO = NG == 3 ? 3072 : (NG == 4 ? 4096 : 1024);  // ... of the row factors
+  // producers' records in flight per wave (the LSTM's 4-KB records: 2, within 256 VGPRs)
+  constexpr int LWP = NG == 4 ? (NPW < 2 ? NPW : 2) : (NPW < 3 ? NPW : 3);
   constexpr int RED = BW * GB * RP > 8 * GB * GU ? BW * GB * RP : 8 * GB * GU;
   __shared__ __attribute__((aligned(8))) float red[RED];
-  __shared__ __attribute__((aligned(16))) _Float16 stg[3 * 64 * 8];   // the record published
+  __shared__ __attribute__((aligned(16))) _Float16 stg[4 * 64 * 8];   // the record published
   __shared__ __attribute__((aligned(16))) float stsc[GB];
   __shared__ int flag;
   int ub, d, bt;
   const bool xg = xmode != 0;
   if (xg ? !map_work_xgrp(UB, BT, D, ub, d, bt) : !map_work(UB * D, BT, UB, ub, d, bt)) return;
-  const int n0 = bt * GB;
+  const int n0 = n_base + bt * GB;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int H3 = 3 * H;
+  const int H3 = NG * H;
   unsigned* xtab = counters + (D * BT + 1) + D * BT * 64 + (d * BT + bt) * 64;
   const unsigned my_xcc = xcc_id() + 1u;
   if (xg && threadIdx.x == 0)   // published by the step-0 flag (wave 0 drains before it)
@@ -738,10 +729,10 @@ __global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
   const int np = (UB * (wave + 1)) / BW - p0;      // host guarantees np <= NPW
   const unsigned* gflags = counters + (D * BT + 1) + (d * BT + bt) * UB;
   unsigned* myflag = counters + (D * BT + 1) + (d * BT + bt) * UB + ub;
-  const int slot_floats = D * BT * UB * HBR;
+  const int slot_floats = D * BT * UB * HB;
   const __amdgpu_buffer_rsrc_t x_rs = __builtin_amdgcn_make_buffer_rsrc(
       gx, (short)0, (xg ? 4 : 2) * slot_floats * 4, 0x00020000);
-  const int grp_off = (d * BT + bt) * UB * HBR;
+  const int grp_off = (d * BT + bt) * UB * HB;
   const int aoff = 2 * slot_floats * 4;   // the plain-store copies (xmode)
   const bool tracing = stamps != nullptr && threadIdx.x == 0;
   auto trace_at = [&](int s, int p) {
@@ -753,7 +744,8 @@ __global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
   // W_hh^T fragments of producer p (unit block pb = p0 + p), lane (u = lane & 15, q = lane >> 4):
   // pair slot j -> W_hh[(j >> 2) H + 16 pb + 4 q + (j & 3)][16 ub + u] (gates r, z), single
   // slot j -> W_hh[2 H + 16 pb + 4 q + j][16 ub + u] (gate n); column u scaled by 2^e(u)
-  Duo wrz[NPW];
+  Duo wrz[NPW];                 // GRU: (r, z); LSTM: (i, f)
+  Duo wgo[NPW];                 // LSTM: (g, o)
   f16x4 wnh[NPW], wnl[NPW];
   float unscale = 1.f;   // 2^-e(u) of the owner's unit (threadIdx.x & 15 = lane & 15)
   {
@@ -767,7 +759,7 @@ __global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
 #pragma unroll
     for (int p = 0; p < NPW; ++p)
 #pragma unroll
-      for (int g = 0; g < 3; ++g)
+      for (int g = 0; g < NG; ++g)
 #pragma unroll
         for (int j = 0; j < 4; ++j) mx = fmaxf(mx, fabsf(wv(g, p, j)));
     mx = fmaxf(mx, __shfl_xor(mx, 16));
@@ -784,13 +776,26 @@ __global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
 #pragma unroll
     for (int p = 0; p < NPW; ++p) {
       f32x4 a, b, c;
+      if constexpr (NG == 4) {
+        f32x4 e, f;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          a[j] = wv(0, p, j);
+          b[j] = wv(1, p, j);
+          e[j] = wv(2, p, j);
+          f[j] = wv(3, p, j);
+        }
+        wrz[p] = split2h(a, b, sc);
+        wgo[p] = split2h(e, f, sc);
+        continue;
+      }
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        a[j] = wv(0, p, j);
-        b[j] = wv(1, p, j);
-        c[j] = wv(2, p, j);
+        a[j] = NG == 3 ? wv(0, p, j) : 0.f;
+        b[j] = NG == 3 ? wv(1, p, j) : 0.f;
+        c[j] = wv(NG - 1, p, j);
       }
-      wrz[p] = split2h(a, b, sc);
+      if constexpr (NG == 3) wrz[p] = split2h(a, b, sc);
       const Duo dn = split2h(c, c, sc);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -810,6 +815,8 @@ __global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
   // this thread's slots in the staged record: consumer lane m + 16 (u >> 2), k slot u & 3
   const int sL = (m + 16 * (u >> 2)) * 8 + (u & 3);
   float dh_prev = 0.f, z_prev = 0.f;
+  float dc_carry = 0.f;   // LSTM: dc_{t+1} f_{t+1}
+  float g_o = 0.f, c_t = 0.f;
   float px_dar = 0.f, px_daz = 0.f, px_dan = 0.f, px_dghn = 0.f;
   int64_t px_row = -1;
   double sb_r = 0.0, sb_z = 0.0, sb_n = 0.0, sb_hn = 0.0;
@@ -823,18 +830,31 @@ __global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     const int64_t row = ((int64_t)t * N + n) * D + d;
     if (owner && t < len) {
       dyv = dy[(((int64_t)t * N + n) * dyd + (dyd > 1 ? d : 0)) * H + j];
-      const float* gp = gates + row * 4 * H;
-      g_r = gp[j];
-      g_z = gp[H + j];
-      g_n = gp[2 * H + j];
-      g_hn = gp[3 * H + j];
-      const int tp = d == 0 ? t - 1 : t + 1;
-      if (tp >= 0 && tp < T) hp = h_all[(((int64_t)tp * N + n) * D + d) * H + j];
+      if constexpr (NG == 3) {
+        const float* gp = gates + row * 4 * H;
+        g_r = gp[j];
+        g_z = gp[H + j];
+        g_n = gp[2 * H + j];
+        g_hn = gp[3 * H + j];
+        const int tp = d == 0 ? t - 1 : t + 1;
+        if (tp >= 0 && tp < T) hp = h_all[(((int64_t)tp * N + n) * D + d) * H + j];
+      } else if constexpr (NG == 4) {
+        const float* gp = gates + row * 4 * H;
+        g_r = gp[j];                // i
+        g_z = gp[H + j];            // f
+        g_n = gp[2 * H + j];        // g
+        g_o = gp[3 * H + j];        // o
+        c_t = h_all[row * H + j];   // c_t (h_all is c_all)
+        const int tp = d == 0 ? t - 1 : t + 1;
+        if (tp >= 0 && tp < T) hp = h_all[(((int64_t)tp * N + n) * D + d) * H + j];   // c_{t-1}
+      } else {
+        g_n = h_all[row * H + j];   // h_t
+      }
     }
     trace_at(s, 0);
     if (s > 0) {
       if (!flags_wait(gflags, UB, (unsigned)s, err, &flag)) {
-        poison_rest(dgx, s, T, d == 0, N, D, n, d, H, j, H3, 3, owner);
+        poison_rest(dgx, s, T, d == 0, N, D, n, d, H, j, H3, NG, owner);
         return;
       }
       trace_at(s, 1);
@@ -847,19 +867,24 @@ __global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
           if ((same >> (p0 + p)) & 1ull) psame |= 1u << p;
       }
       const int rb = ((s - 1) & 1) * slot_floats + grp_off;
-      u32x4 r0[NPW], r1[NPW], r2[NPW];
+      u32x4 r0[NPW], r1[NPW], r2[NPW], r3[NPW];
       f32x4 rs[NPW];
       auto load_rec = [&](int p) {
         const bool ok = p < np;
-        const int base = (rb + (p0 + p) * HBR) * 4 + (((psame >> p) & 1u) ? aoff : 0);
-        r0[p] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                              x_rs, ok ? base + lane * 16 : 0x7ffffff0, 0, kSc1));
-        r1[p] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                              x_rs, ok ? base + 1024 + lane * 16 : 0x7ffffff0, 0, kSc1));
+        const int base = (rb + (p0 + p) * HB) * 4 + (((psame >> p) & 1u) ? aoff : 0);
+        if constexpr (NG >= 3) {
+          r0[p] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                x_rs, ok ? base + lane * 16 : 0x7ffffff0, 0, kSc1));
+          r1[p] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                x_rs, ok ? base + 1024 + lane * 16 : 0x7ffffff0, 0, kSc1));
+        }
+        if constexpr (NG == 4)
+          r3[p] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                x_rs, ok ? base + 3072 + lane * 16 : 0x7ffffff0, 0, kSc1));
         r2[p] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                              x_rs, ok ? base + 2048 + lane * 16 : 0x7ffffff0, 0, kSc1));
+                                              x_rs, ok ? base + NO + lane * 16 : 0x7ffffff0, 0, kSc1));
         rs[p] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                              x_rs, ok ? base + 3072 + (lane >> 4) * 16 : 0x7ffffff0, 0, kSc1));
+                                              x_rs, ok ? base + SO + (lane >> 4) * 16 : 0x7ffffff0, 0, kSc1));
       };
 #pragma unroll
       for (int p = 0; p < LWP; ++p) load_rec(p);
@@ -870,16 +895,27 @@ __global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
         if (p + LWP < NPW) load_rec(p + LWP);
         if (p < np) {
           f32x4 tmp = f32x4{0.f, 0.f, 0.f, 0.f};
-          const f16x8 ahi = __builtin_bit_cast(f16x8, r0[p]);
-          const f16x8 alo = __builtin_bit_cast(f16x8, r1[p]);
-          tmp = __builtin_amdgcn_mfma_f32_16x16x32_f16(alo, wrz[p].hi, tmp, 0, 0, 0);
-          tmp = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, wrz[p].lo, tmp, 0, 0, 0);
-          tmp = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, wrz[p].hi, tmp, 0, 0, 0);
-          const f16x4 nh = __builtin_bit_cast(f16x4, u32x2{r2[p][0], r2[p][1]});
-          const f16x4 nl = __builtin_bit_cast(f16x4, u32x2{r2[p][2], r2[p][3]});
-          tmp = __builtin_amdgcn_mfma_f32_16x16x16f16(nl, wnh[p], tmp, 0, 0, 0);
-          tmp = __builtin_amdgcn_mfma_f32_16x16x16f16(nh, wnl[p], tmp, 0, 0, 0);
-          tmp = __builtin_amdgcn_mfma_f32_16x16x16f16(nh, wnh[p], tmp, 0, 0, 0);
+          if constexpr (NG >= 3) {
+            const f16x8 ahi = __builtin_bit_cast(f16x8, r0[p]);
+            const f16x8 alo = __builtin_bit_cast(f16x8, r1[p]);
+            tmp = __builtin_amdgcn_mfma_f32_16x16x32_f16(alo, wrz[p].hi, tmp, 0, 0, 0);
+            tmp = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, wrz[p].lo, tmp, 0, 0, 0);
+            tmp = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, wrz[p].hi, tmp, 0, 0, 0);
+          }
+          if constexpr (NG == 4) {
+            const f16x8 bhi = __builtin_bit_cast(f16x8, r2[p]);
+            const f16x8 blo = __builtin_bit_cast(f16x8, r3[p]);
+            tmp = __builtin_amdgcn_mfma_f32_16x16x32_f16(blo, wgo[p].hi, tmp, 0, 0, 0);
+            tmp = __builtin_amdgcn_mfma_f32_16x16x32_f16(bhi, wgo[p].lo, tmp, 0, 0, 0);
+            tmp = __builtin_amdgcn_mfma_f32_16x16x32_f16(bhi, wgo[p].hi, tmp, 0, 0, 0);
+          }
+          if constexpr (NG != 4) {
+            const f16x4 nh = __builtin_bit_cast(f16x4, u32x2{r2[p][0], r2[p][1]});
+            const f16x4 nl = __builtin_bit_cast(f16x4, u32x2{r2[p][2], r2[p][3]});
+            tmp = __builtin_amdgcn_mfma_f32_16x16x16f16(nl, wnh[p], tmp, 0, 0, 0);
+            tmp = __builtin_amdgcn_mfma_f32_16x16x16f16(nh, wnl[p], tmp, 0, 0, 0);
+            tmp = __builtin_amdgcn_mfma_f32_16x16x16f16(nh, wnh[p], tmp, 0, 0, 0);
+          }
           acc += tmp * rs[p];   // rows 4 (lane >> 4) + i: the producer's 2^-e of those rows
         }
       }
@@ -894,10 +930,53 @@ __global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     settle(g_n);
     settle(g_hn);
     settle(hp);
+    if constexpr (NG == 4) {
+      settle(g_o);
+      settle(c_t);
+    }
     __syncthreads();
     trace_at(s, 3);
     float dar = 0.f, daz = 0.f, dan = 0.f, dghn = 0.f;
-    if (owner) {
+    if (NG == 4 && owner) {
+      // the LSTM cell: (dai, daf, dag, dao) carried in (dar, daz, dan, dghn)
+      if (t < len) {
+        float rec = 0.f;
+        if (s > 0) {
+#pragma unroll
+          for (int w8 = 0; w8 < BW; ++w8) rec += red[(w8 * GB + m) * RP + u];
+        }
+        const float tc = tanh_fast(c_t);
+        const float dh = dyv + rec * unscale;
+        const float dc = dc_carry + dh * g_o * (1.f - tc * tc);
+        dghn = dh * tc * g_o * (1.f - g_o);
+        dar = dc * g_n * g_r * (1.f - g_r);
+        dan = dc * g_r * (1.f - g_n * g_n);
+        daz = dc * hp * g_z * (1.f - g_z);
+        dc_carry = dc * g_z;
+      } else {
+        dc_carry = 0.f;
+      }
+      px_dar = dar; px_daz = daz; px_dan = dan; px_dghn = dghn; px_row = row;
+      cm_r = fmaxf(cm_r, fabsf(dar));
+      cm_z = fmaxf(cm_z, fabsf(daz));
+      cm_n = fmaxf(cm_n, fabsf(dan));
+      cm_hn = fmaxf(cm_hn, fabsf(dghn));
+    } else if (NG == 1 && owner) {
+      // the one-gate cell: da = (dy + W_hh^T da_next) (1 - h_t^2), carried in dghn
+      float da = 0.f;
+      if (t < len) {
+        float rec = 0.f;
+        if (s > 0) {
+#pragma unroll
+          for (int w8 = 0; w8 < BW; ++w8) rec += red[(w8 * GB + m) * RP + u];
+        }
+        da = (dyv + rec * unscale) * (1.f - g_n * g_n);
+      }
+      dghn = da;
+      px_dan = da;
+      px_row = row;
+      cm_n = fmaxf(cm_n, fabsf(da));
+    } else if (owner) {
       float dh = 0.f, zc = 0.f;
       if (t < len) {
         float carry = 0.f;
@@ -926,45 +1005,65 @@ __global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     if (gate_thread) {
       // the row's scale: max over the sample's 16 units x 3 gates (16 consecutive lanes)
       float mx = fmaxf(fmaxf(fabsf(dar), fabsf(daz)), fabsf(dghn));
+      if constexpr (NG == 4) mx = fmaxf(mx, fabsf(dan));
 #pragma unroll
       for (int o = 1; o < 16; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
       const int e = h3_row_exp(mx);
       const float sc = __builtin_ldexpf(1.f, e);
       const float vr = dar * sc, vz = daz * sc, vn = dghn * sc;
       const _Float16 hr = (_Float16)vr, hz = (_Float16)vz, hn = (_Float16)vn;
-      stg[sL] = hr;
-      stg[sL + 4] = hz;
-      stg[512 + sL] = (_Float16)(vr - (float)hr);
-      stg[512 + sL + 4] = (_Float16)(vz - (float)hz);
-      stg[1024 + sL] = hn;
-      stg[1024 + sL + 4] = (_Float16)(vn - (float)hn);
+      if constexpr (NG >= 3) {
+        stg[sL] = hr;
+        stg[sL + 4] = hz;
+        stg[512 + sL] = (_Float16)(vr - (float)hr);
+        stg[512 + sL + 4] = (_Float16)(vz - (float)hz);
+      }
+      if constexpr (NG == 4) {   // second pair (g, o): dan, dghn
+        const float vg = dan * sc;
+        const _Float16 hg = (_Float16)vg;
+        stg[1024 + sL] = hg;
+        stg[1024 + sL + 4] = hn;
+        stg[1536 + sL] = (_Float16)(vg - (float)hg);
+        stg[1536 + sL + 4] = (_Float16)(vn - (float)hn);
+      } else {
+        stg[NO / 2 + sL] = hn;   // the n-layout tile (fp16 offset)
+        stg[NO / 2 + sL + 4] = (_Float16)(vn - (float)hn);
+      }
       if (u == 0) stsc[m] = __builtin_ldexpf(1.f, -e);
     }
     __syncthreads();
     if (wave == 0) {
-      const int so = ((s & 1) * slot_floats + grp_off + ub * HBR) * 4;
-      const u32x4 v0 = *reinterpret_cast<const u32x4*>(stg + lane * 8);
-      const u32x4 v1 = *reinterpret_cast<const u32x4*>(stg + 512 + lane * 8);
-      const u32x4 v2 = *reinterpret_cast<const u32x4*>(stg + 1024 + lane * 8);
-      __builtin_amdgcn_raw_buffer_store_b128(v0, x_rs, so + lane * 16, 0, kSc1);
-      __builtin_amdgcn_raw_buffer_store_b128(v1, x_rs, so + 1024 + lane * 16, 0, kSc1);
-      __builtin_amdgcn_raw_buffer_store_b128(v2, x_rs, so + 2048 + lane * 16, 0, kSc1);
-      if (xg) {   // plain copies: stay in this XCD's L2 for the same-XCD consumers
-        __builtin_amdgcn_raw_buffer_store_b128(v0, x_rs, aoff + so + lane * 16, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b128(v1, x_rs, aoff + so + 1024 + lane * 16, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b128(v2, x_rs, aoff + so + 2048 + lane * 16, 0, 0);
+      const int so = ((s & 1) * slot_floats + grp_off + ub * HB) * 4;
+      // the record's 1-KB tiles: NG 3: (rz hi, rz lo, n); NG 4: (if hi, if lo, go hi, go lo);
+      // NG 1: (n)
+      constexpr int NT = NG == 4 ? 4 : (NG == 3 ? 3 : 1);
+#pragma unroll
+      for (int k = 0; k < NT; ++k) {
+        const int tk = NG == 1 ? 0 : k;          // stg / record tile index
+        const u32x4 v = *reinterpret_cast<const u32x4*>(stg + tk * 512 + lane * 8);
+        __builtin_amdgcn_raw_buffer_store_b128(v, x_rs, so + tk * 1024 + lane * 16, 0, kSc1);
+        // plain copies: stay in this XCD's L2 for the same-XCD consumers
+        if (xg) __builtin_amdgcn_raw_buffer_store_b128(v, x_rs, aoff + so + tk * 1024 + lane * 16, 0, 0);
       }
       if (lane < 4) {
         const u32x4 vs = *reinterpret_cast<const u32x4*>(stsc + lane * 4);
-        __builtin_amdgcn_raw_buffer_store_b128(vs, x_rs, so + 3072 + lane * 16, 0, kSc1);
-        if (xg) __builtin_amdgcn_raw_buffer_store_b128(vs, x_rs, aoff + so + 3072 + lane * 16, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(vs, x_rs, so + SO + lane * 16, 0, kSc1);
+        if (xg) __builtin_amdgcn_raw_buffer_store_b128(vs, x_rs, aoff + so + SO + lane * 16, 0, 0);
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (lane == 0)
         __hip_atomic_store(myflag, (unsigned)s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     trace_at(s, 4);
-    if (owner) {
+    if (NG == 1 && owner) {
+      dgx[px_row * H + j] = px_dan;
+    } else if (NG == 4 && owner) {
+      float* gr = dgx + px_row * H3;
+      gr[j] = px_dar;
+      gr[H + j] = px_daz;
+      gr[2 * H + j] = px_dan;
+      gr[3 * H + j] = px_dghn;
+    } else if (owner) {
       float* gxr = dgx + px_row * H3;
       gxr[j] = px_dar;
       gxr[H + j] = px_daz;
@@ -974,6 +1073,42 @@ __global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
       ghr[H + j] = px_daz;
       ghr[2 * H + j] = px_dghn;
     }
+  }
+  if constexpr (NG == 1) {
+    // the one-gate cell: column maxima of da [T N][D H] into camax[0, D H)
+    if (camax == nullptr) return;
+    __syncthreads();
+    if (gate_thread) red[m * GU + u] = cm_n;
+    __syncthreads();
+    if (threadIdx.x < GU) {
+      float a = 0.f;
+#pragma unroll
+      for (int mm = 0; mm < GB; ++mm) a = fmaxf(a, red[mm * GU + threadIdx.x]);
+      const unsigned bits = __float_as_uint(a);
+      if (bits != 0u) atomicMax(camax + d * H + ub * GU + threadIdx.x, bits);
+    }
+    return;
+  }
+  if constexpr (NG == 4) {
+    // column maxima of dgates [T N][D 4H] into camax[0, D 4H)
+    if (camax == nullptr) return;
+    __syncthreads();
+    if (gate_thread) {
+      red[(0 * GB + m) * GU + u] = cm_r;
+      red[(1 * GB + m) * GU + u] = cm_z;
+      red[(2 * GB + m) * GU + u] = cm_n;
+      red[(3 * GB + m) * GU + u] = cm_hn;
+    }
+    __syncthreads();
+    if (threadIdx.x < 4 * GU) {
+      const int g = threadIdx.x / GU, uu = threadIdx.x - (threadIdx.x / GU) * GU;
+      float a = 0.f;
+#pragma unroll
+      for (int mm = 0; mm < GB; ++mm) a = fmaxf(a, red[(g * GB + mm) * GU + uu]);
+      const unsigned bits = __float_as_uint(a);
+      if (bits != 0u) atomicMax(camax + d * H3 + g * H + ub * GU + uu, bits);
+    }
+    return;
   }
   if (camax != nullptr) {
     // column maxima of dgx [T N][D 3H] and dgh: the 16 samples' running maxima per unit, then
@@ -1134,13 +1269,142 @@ bool launch_gru_bwd_x6(int t_max, int n, int h, int num_dirs, const float* dy, i
   if (fn == nullptr) return false;
   int XM_ = xcd_groups(UB, BT, num_dirs) ? 1 : 0;
   const int grid = XM_ ? xgrp_grid(UB, BT, num_dirs) : mapped_grid(UB * num_dirs, BT);
-  int T_ = t_max, N_ = n, H_ = h, D_ = num_dirs, UB_ = UB, BT_ = BT, DYD_ = dy_dirs;
+  int T_ = t_max, N_ = n, H_ = h, D_ = num_dirs, UB_ = UB, BT_ = BT, DYD_ = dy_dirs, NB_ = 0;
   void* args[] = {&T_, &N_, &H_, &D_, &UB_, &BT_, &dy, &DYD_, &w_hh_f, &w_hh_r, &h_all,
                   &gates, &lens, &dgates_x, &dgates_h, &ring, &ctrs, &err, &stamps, &dbp, &XM_,
-                  &camax};
+                  &camax, &NB_};
   const bool ok = rnn_launch(fn, dim3(grid), dim3(BW * 64), args, lds_pad, st) == hipSuccess;
   if (ok && h3 && camax != nullptr && camax_done != nullptr) *camax_done = true;
   return ok;
+}
+
+
+// ---------------------------------------------------------------------------------------
+// supported_rnns['rnn'] (nn.RNN, tanh) on the same machinery: the one-gate instantiations of
+// the fp16x3 forward / backward (NG = 1), same groups, hand-offs and rings (ds2_rnn_fwd_ws /
+// ds2_rnn_bwd_ws in gru.hip carve the workspace).  false = not covered (caller falls back to
+// the per-step kernels of rnn.hip).
+static const void* rnn_fwd_fn(int need) {
+#define DS2_RF(K) \
+  if (need <= K) return reinterpret_cast<const void*>(gru_fwd_x6_kernel<K, true, 1>);
+  DS2_RF(1) DS2_RF(2) DS2_RF(3) DS2_RF(4) DS2_RF(5) DS2_RF(6) DS2_RF(7)
+#undef DS2_RF
+  return nullptr;
+}
+
+static const void* rnn_bwd_fn(int UB) {
+  const int need = (UB + BW - 1) / BW;
+#define DS2_RB(K) \
+  if (need <= K) return reinterpret_cast<const void*>(gru_bwd_h3_kernel<K, 1>);
+  DS2_RB(1) DS2_RB(2) DS2_RB(3) DS2_RB(4) DS2_RB(5) DS2_RB(6) DS2_RB(7) DS2_RB(8)
+#undef DS2_RB
+  return nullptr;
+}
+
+bool launch_rnn_fwd_h3(int t_max, int n, int h, int num_dirs, const float* xproj,
+                       const float* w_hh_f, const float* w_hh_r, const float* b_hh_f,
+                       const float* b_hh_r, const int* lens, float* h_all, float* ring,
+                       unsigned* ctrs, unsigned* err, unsigned long long* stamps, size_t lds_pad,
+                       hipStream_t st) {
+  if ((h % GU) != 0) return false;
+  apply_spin_limit_env();
+  apply_rnn_tune_env();
+  const int UB = h / GU, BT = (n + GB - 1) / GB;
+  const void* fn = rnn_fwd_fn(((UB + 1) / 2 + XW - 1) / XW);
+  if (fn == nullptr) return false;
+  int XM_ = xcd_groups(UB, BT, num_dirs) ? 1 : 0;
+  const int grid = XM_ ? xgrp_grid(UB, BT, num_dirs) : mapped_grid(UB * num_dirs, BT);
+  int T_ = t_max, N_ = n, H_ = h, D_ = num_dirs, UB_ = UB, BT_ = BT;
+  float* gates = nullptr;
+  void* args[] = {&T_, &N_, &H_, &D_, &UB_, &BT_, &xproj, &w_hh_f, &w_hh_r, &b_hh_f,
+                  &b_hh_r, &lens, &h_all, &gates, &ring, &ctrs, &err, &stamps, &XM_};
+  return rnn_launch(fn, dim3(grid), dim3(XT), args, lds_pad, st) == hipSuccess;
+}
+
+// dgates: [T][N][D][H] gradient wrt the pre-activation; camax (nullable, zeroed by the
+// caller): its column maxima
+bool launch_rnn_bwd_h3(int t_max, int n, int h, int num_dirs, const float* dy, int dy_dirs,
+                       const float* w_hh_f, const float* w_hh_r, const float* h_all,
+                       const int* lens, float* dgates, float* ring, unsigned* ctrs, unsigned* err,
+                       unsigned long long* stamps, size_t lds_pad, hipStream_t st,
+                       unsigned* camax) {
+  if ((h % GU) != 0) return false;
+  apply_spin_limit_env();
+  apply_rnn_tune_env();
+  const int UB = h / GU, BT = (n + GB - 1) / GB;
+  const void* fn = rnn_bwd_fn(UB);
+  if (fn == nullptr) return false;
+  int XM_ = xcd_groups(UB, BT, num_dirs) ? 1 : 0;
+  const int grid = XM_ ? xgrp_grid(UB, BT, num_dirs) : mapped_grid(UB * num_dirs, BT);
+  int T_ = t_max, N_ = n, H_ = h, D_ = num_dirs, UB_ = UB, BT_ = BT, DYD_ = dy_dirs, NB_ = 0;
+  const float* gates = nullptr;
+  float* dgh = nullptr;
+  double* dbp = nullptr;
+  void* args[] = {&T_, &N_, &H_, &D_, &UB_, &BT_, &dy, &DYD_, &w_hh_f, &w_hh_r, &h_all,
+                  &gates, &lens, &dgates, &dgh, &ring, &ctrs, &err, &stamps, &dbp, &XM_,
+                  &camax, &NB_};
+  return rnn_launch(fn, dim3(grid), dim3(BW * 64), args, lds_pad, st) == hipSuccess;
+}
+
+// grid of the one-gate launches, -1 if they decline the shape
+int rnn_h3_grid(int n, int h, int num_dirs) {
+  if ((h % GU) != 0) return -1;
+  const int UB = h / GU, BT = (n + GB - 1) / GB;
+  if (rnn_bwd_fn(UB) == nullptr || rnn_fwd_fn(((UB + 1) / 2 + XW - 1) / XW) == nullptr) return -1;
+  return xcd_groups(UB, BT, num_dirs) ? xgrp_grid(UB, BT, num_dirs) : mapped_grid(UB * num_dirs, BT);
+}
+
+// supported_rnns['lstm'] backward on the same machinery (NG = 4): one launch over the
+// 16-sample tiles [tile0, tile0 + BT_launch) of the batch (the caller runs consecutive chunks
+// when all tiles would not fit the chip); ring and counters sized for BT_launch groups.
+// camax (nullable, zeroed by the caller): column maxima of dgates over every launch.
+static const void* lstm_bwd_fn(int UB) {
+  const int need = (UB + BW - 1) / BW;
+#define DS2_LB(K) \
+  if (need <= K) return reinterpret_cast<const void*>(gru_bwd_h3_kernel<K, 4>);
+  DS2_LB(1) DS2_LB(2) DS2_LB(3) DS2_LB(4) DS2_LB(5) DS2_LB(6) DS2_LB(7) DS2_LB(8)
+#undef DS2_LB
+  return nullptr;
+}
+
+// grid of one LSTM fp16x3 backward launch over bt_launch tiles, -1 if it declines the shape
+int lstm_h3_grid(int h, int num_dirs, int bt_launch) {
+  if ((h % GU) != 0) return -1;
+  const int UB = h / GU;
+  if (lstm_bwd_fn(UB) == nullptr) return -1;
+  return xcd_groups(UB, bt_launch, num_dirs) ? xgrp_grid(UB, bt_launch, num_dirs)
+                                            : mapped_grid(UB * num_dirs, bt_launch);
+}
+
+bool launch_lstm_bwd_h3(int t_max, int n, int h, int num_dirs, const float* dy, int dy_dirs,
+                        const float* w_hh_f, const float* w_hh_r, const float* c_all,
+                        const float* gates, const int* lens, float* dgates, float* ring,
+                        unsigned* ctrs, unsigned* err, size_t lds_pad, hipStream_t st,
+                        unsigned* camax, int tile0, int bt_launch) {
+  if ((h % GU) != 0) return false;
+  apply_spin_limit_env();
+  apply_rnn_tune_env();
+  const int UB = h / GU;
+  const void* fn = lstm_bwd_fn(UB);
+  if (fn == nullptr) return false;
+  int XM_ = xcd_groups(UB, bt_launch, num_dirs) ? 1 : 0;
+  const int grid = XM_ ? xgrp_grid(UB, bt_launch, num_dirs) : mapped_grid(UB * num_dirs, bt_launch);
+  int T_ = t_max, N_ = n, H_ = h, D_ = num_dirs, UB_ = UB, BT_ = bt_launch, DYD_ = dy_dirs;
+  int NB_ = tile0 * GB;
+  float* dgh = nullptr;
+  double* dbp = nullptr;
+  unsigned long long* stamps = nullptr;
+  void* args[] = {&T_, &N_, &H_, &D_, &UB_, &BT_, &dy, &DYD_, &w_hh_f, &w_hh_r, &c_all,
+                  &gates, &lens, &dgates, &dgh, &ring, &ctrs, &err, &stamps, &dbp, &XM_,
+                  &camax, &NB_};
+  return rnn_launch(fn, dim3(grid), dim3(BW * 64), args, lds_pad, st) == hipSuccess;
+}
+
+// ring bytes of the fp16x3 backward records (2 slots, doubled for the same-XCD plain copies)
+size_t h3_bwd_ring_bytes(int n_tiles, int h, int num_dirs, int ng) {
+  const size_t UB = (h + GU - 1) / GU;
+  const size_t hb = ng == 4 ? HBR4 : (ng == 3 ? HBR : HBR1);
+  return 4 * (size_t)num_dirs * n_tiles * UB * hb * sizeof(float);
 }
 
 }  // namespace ds2

@@ -534,7 +534,12 @@ __global__ __launch_bounds__(GT) void lstm_bwd_persist_kernel(
 // the MFMAs.  HM: 1 the sentinel ring of gru_fwd_dop_kernel, 0 per-producer flags (the 8-tile
 // shapes, H > 512: W_hh's 128 fragment registers leave no room for the sentinel spin's live
 // state); BTS as in lstm_fwd_persist_kernel.  h_all, c_all and the gate cache are written after the publish.
-template <int NBW, int HM, int BTS>
+// H3: the W_hh product on fp16x3 (rnn_common.h; default since round 5, DS2_LSTM_H3=0 keeps fp32
+// MFMA): the wave's blocks are taken in pairs (one v_mfma_f32_16x16x32_f16 k-step: slots 0..3
+// of lane (r, q) from block 2p, 4..7 from 2p + 1, the 16 B the lane loads from each tile),
+// W_hh rows (gate, unit) scaled by their own 2^e, h (|h| < 1) by 2^14; three products per
+// pair instead of sixteen v_mfma_f32_16x16x4_f32 (each 4x the cycles of one f16 product).
+template <int NBW, int HM, int BTS, bool H3 = false>
 __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void lstm_fwd_dop_kernel(
     int T, int N, int H, int D, int UB, int BT, const float* __restrict__ xproj,
     const float* __restrict__ w_f, const float* __restrict__ w_r, const float* __restrict__ b_f,
@@ -570,20 +575,63 @@ __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   }
 
   // W_hh fragments: w[g][i][c] = W_hh[g H + ub 16 + (lane & 15)][16 (b0 + i) + 4 (lane >> 4) + c]
-  f32x4 w[4][NBW];
+  // (fp32), or their fp16x3 pairs w3[g][p] (blocks 2p, 2p + 1) with the row scales undone by
+  // unscale[g] (the owner thread's unit is threadIdx.x & 15 = lane & 15: the same row)
+  constexpr int NW32 = H3 ? 1 : NBW;
+  constexpr int NPR = H3 ? (NBW + 1) / 2 : 1;
+  f32x4 w[4][NW32];
+  Duo w3[4][NPR];
+  float unscale[4] = {1.f, 1.f, 1.f, 1.f};
   {
     const float* W = d == 0 ? w_f : w_r;
     const float* wr = W + (int64_t)(ub * GU + (lane & 15)) * H + 16 * b0 + 4 * (lane >> 4);
+    auto wblk = [&](int g, int i) {
+      return i < nb ? *reinterpret_cast<const f32x4*>(wr + (int64_t)g * H * H + 16 * i)
+                    : f32x4{0.f, 0.f, 0.f, 0.f};
+    };
+    if constexpr (H3) {
+      float mx[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int i = 0; i < NBW; ++i)
+      for (int i = 0; i < NBW; ++i)
 #pragma unroll
-      for (int g = 0; g < 4; ++g)
-        w[g][i] = i < nb ? *reinterpret_cast<const f32x4*>(wr + (int64_t)g * H * H + 16 * i)
-                         : f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int g = 0; g < 4; ++g) {
+          const f32x4 v = wblk(g, i);
 #pragma unroll
-    for (int i = 0; i < NBW; ++i)
+          for (int q = 0; q < 4; ++q) mx[g] = fmaxf(mx[g], fabsf(v[q]));
+        }
+      // the row's max over the lane's 4 k quads, then over the 8 waves (LDS, before `red` is used)
 #pragma unroll
-      for (int g = 0; g < 4; ++g) settle(w[g][i]);
+      for (int g = 0; g < 4; ++g) {
+        mx[g] = fmaxf(mx[g], __shfl_xor(mx[g], 16));
+        mx[g] = fmaxf(mx[g], __shfl_xor(mx[g], 32));
+        if (lane < 16) red[(wave * 4 + g) * 16 + lane] = mx[g];
+      }
+      __syncthreads();
+      float sc[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        float m8 = 0.f;
+#pragma unroll
+        for (int w8 = 0; w8 < GW; ++w8) m8 = fmaxf(m8, red[(w8 * 4 + g) * 16 + (lane & 15)]);
+        const int e = h3_row_exp(m8);
+        sc[g] = __builtin_ldexpf(1.f, e);
+        unscale[g] = __builtin_ldexpf(1.f, -(e + 14));
+      }
+      __syncthreads();
+#pragma unroll
+      for (int p = 0; p < NPR; ++p)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) w3[g][p] = split2h(wblk(g, 2 * p), wblk(g, 2 * p + 1), sc[g]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < NBW; ++i)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) w[g][i] = wblk(g, i);
+#pragma unroll
+      for (int i = 0; i < NBW; ++i)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) settle(w[g][i]);
+    }
   }
   const float* bh = d == 0 ? b_f : b_r;
   const int m = threadIdx.x >> 4;               // sample within the workgroup (< RB)
@@ -638,18 +686,33 @@ __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
       asm volatile("" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int b = 0; b < BTS; ++b)
+      for (int b = 0; b < BTS; ++b) {
+        if constexpr (H3) {
 #pragma unroll
-        for (int i = 0; i < NBW; ++i) {
-          if (SENT && i < nb && !spin_tile(hv[b][i], x_rs, base + (b * UB + i) * 1024, err))
-            failed = 1;
+          for (int i = 0; i < NBW; ++i)
+            if (SENT && i < nb && !spin_tile(hv[b][i], x_rs, base + (b * UB + i) * 1024, err))
+              failed = 1;
 #pragma unroll
-          for (int cc = 0; cc < 4; ++cc)
+          for (int p = 0; p < NPR; ++p) {
+            const f32x4 z4 = f32x4{0.f, 0.f, 0.f, 0.f};
+            const Duo a = split2h(hv[b][2 * p], 2 * p + 1 < NBW ? hv[b][2 * p + 1] : z4, 16384.f);
 #pragma unroll
-            for (int g = 0; g < 4; ++g)
-              acc[b][g] = __builtin_amdgcn_mfma_f32_16x16x4f32(hv[b][i][cc], w[g][i][cc],
-                                                               acc[b][g], 0, 0, 0);
+            for (int g = 0; g < 4; ++g) acc[b][g] = mma3h(a, w3[g][p], acc[b][g]);
+          }
+        } else {
+#pragma unroll
+          for (int i = 0; i < NBW; ++i) {
+            if (SENT && i < nb && !spin_tile(hv[b][i], x_rs, base + (b * UB + i) * 1024, err))
+              failed = 1;
+#pragma unroll
+            for (int cc = 0; cc < 4; ++cc)
+#pragma unroll
+              for (int g = 0; g < 4; ++g)
+                acc[b][g] = __builtin_amdgcn_mfma_f32_16x16x4f32(hv[b][i][cc], w[g][i][cc],
+                                                                 acc[b][g], 0, 0, 0);
+          }
         }
+      }
     }
 #pragma unroll
     for (int b = 0; b < BTS; ++b)
@@ -676,7 +739,7 @@ __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
             float v = 0.f;
 #pragma unroll
             for (int w8 = 0; w8 < GW; ++w8) v += red[(w8 * RB + m) * LRP + g * GU + u];
-            gh[g] = v + bias[g] + xg[g];
+            gh[g] = (H3 ? v * unscale[g] : v) + bias[g] + xg[g];
           }
           o = lstm_cell(gh[0], gh[1], gh[2], gh[3], c);
         }
@@ -739,6 +802,15 @@ static int lstm_pick_ksw(int per) {
   return -1;
 }
 
+// gru_split.hip: the fp16x3 backward with the LSTM cell (gru_bwd_h3_kernel<., 4>)
+int lstm_h3_grid(int h, int num_dirs, int bt_launch);
+bool launch_lstm_bwd_h3(int t_max, int n, int h, int num_dirs, const float* dy, int dy_dirs,
+                        const float* w_hh_f, const float* w_hh_r, const float* c_all,
+                        const float* gates, const int* lens, float* dgates, float* ring,
+                        unsigned* ctrs, unsigned* err, size_t lds_pad, hipStream_t st,
+                        unsigned* camax, int tile0, int bt_launch);
+size_t h3_bwd_ring_bytes(int n_tiles, int h, int num_dirs, int ng);
+
 }  // namespace ds2
 
 using namespace ds2;
@@ -776,6 +848,13 @@ static inline size_t lstm_ring_bytes(int n, int h, int num_dirs) {
   return align256(kRingSlots * (size_t)num_dirs * BT2 * UB * 256 * sizeof(float));
 }
 constexpr unsigned kLstmDopPadLds = 80 * 1024;   // dynamic LDS: one workgroup per CU
+
+// the recurrences' W_hh products on fp16x3 (default since round 5; DS2_LSTM_H3=0 keeps the
+// fp32-MFMA kernels)
+static inline bool lstm_h3_on() {
+  const char* e = getenv("DS2_LSTM_H3");
+  return !(e != nullptr && e[0] == '0');
+}
 
 size_t ds2_lstm_fwd_workspace_size(int n, int h, int num_dirs) {
   const int64_t UB = (h + GU - 1) / GU;
@@ -835,17 +914,18 @@ ds2_status_t ds2_lstm_fwd(int t_max, int n, int h, int num_dirs, const float* xp
     // sentinel spin's live state (it spills), so those run the flag hand-off
     if (nbw == 8) hm = 0;
     const void* fn = nullptr;
-#define DS2_LDOP(K)                                                                          \
-  case K:                                                                                    \
-    fn = bts == 2 ? reinterpret_cast<const void*>(lstm_fwd_dop_kernel<K, 1, 2>)              \
-                  : reinterpret_cast<const void*>(lstm_fwd_dop_kernel<K, 1, 1>);             \
+    const bool h3 = lstm_h3_on();
+#define DS2_LDOP(K, HM)                                                                       \
+  case K:                                                                                     \
+    if (h3)                                                                                   \
+      fn = bts == 2 ? reinterpret_cast<const void*>(lstm_fwd_dop_kernel<K, HM, 2, true>)      \
+                    : reinterpret_cast<const void*>(lstm_fwd_dop_kernel<K, HM, 1, true>);     \
+    else                                                                                      \
+      fn = bts == 2 ? reinterpret_cast<const void*>(lstm_fwd_dop_kernel<K, HM, 2>)            \
+                    : reinterpret_cast<const void*>(lstm_fwd_dop_kernel<K, HM, 1>);           \
     break;
     switch (nbw) {
-      DS2_LDOP(1) DS2_LDOP(2) DS2_LDOP(4)
-      case 8:
-        fn = bts == 2 ? reinterpret_cast<const void*>(lstm_fwd_dop_kernel<8, 0, 2>)
-                      : reinterpret_cast<const void*>(lstm_fwd_dop_kernel<8, 0, 1>);
-        break;
+      DS2_LDOP(1, 1) DS2_LDOP(2, 1) DS2_LDOP(4, 1) DS2_LDOP(8, 0)
       default: break;
     }
 #undef DS2_LDOP
@@ -918,12 +998,34 @@ ds2_status_t ds2_lstm_fwd(int t_max, int n, int h, int num_dirs, const float* xp
   return launch_status("ds2_lstm_fwd");
 }
 
-size_t ds2_lstm_bwd_workspace_size(int n, int h, int num_dirs) {
+// the fp16x3 backward's counters (as the GRU's: group counters, error word, 64 flags and 64
+// XCC ids per group) and record ring, after the fp32 kernels' regions
+static inline size_t lstm_h3_ctr_bytes(int n, int num_dirs) {
+  const size_t groups = (size_t)num_dirs * ((n + GB - 1) / GB);
+  return align256((groups + 1 + groups * 128) * sizeof(unsigned));
+}
+static size_t lstm_bwd_ws_base(int n, int h, int num_dirs) {
   const int64_t UB = (h + GU - 1) / GU;
   const int64_t KS = h;
   return align256((size_t)(num_dirs * UB * KS * 64) * sizeof(float)) +
-         align256((size_t)2 * n * num_dirs * h * sizeof(float)) + lstm_counter_bytes(n, num_dirs) +
-         256;
+         align256((size_t)2 * n * num_dirs * h * sizeof(float)) + lstm_counter_bytes(n, num_dirs);
+}
+
+size_t ds2_lstm_bwd_workspace_size(int n, int h, int num_dirs) {
+  if (n < 1 || h < 1 || num_dirs < 1) return 256;
+  return lstm_bwd_ws_base(n, h, num_dirs) + lstm_h3_ctr_bytes(n, num_dirs) +
+         align256(h3_bwd_ring_bytes((n + GB - 1) / GB, h, num_dirs, 4)) + 256;
+}
+
+// the fp16x3 backward's launch: 16-sample tiles per launch (consecutive launches cover the
+// batch), 0 when it declines the shape
+static int lstm_h3_tiles(int t_max, int n, int h, int num_dirs) {
+  if (!lstm_h3_on() || !persistent_enabled() || (h % GU) != 0) return 0;
+  if ((int64_t)t_max * n * num_dirs * 4 * h * 4 >= (1ll << 31)) return 0;
+  const int UB = h / GU, BT = (n + GB - 1) / GB;
+  const int ct = lstm_chunk_tiles(UB, num_dirs, BT);
+  const int g = lstm_h3_grid(h, num_dirs, ct);
+  return g > 0 && g <= num_cus() ? ct : 0;
 }
 
 #define DS2_LBWD_CASE(K)                                                                    \
@@ -936,6 +1038,9 @@ size_t ds2_lstm_bwd_workspace_size(int n, int h, int num_dirs) {
 // runs as consecutive launches of at most this many), 0 for the per-step kernels
 int ds2_lstm_bwd_grid(int n, int h, int num_dirs) {
   if (n < 1 || h < 1 || (num_dirs != 1 && num_dirs != 2)) return 0;
+  // t_max only bounds 32-bit offsets; 1 asks about the launch shape
+  const int ct = lstm_h3_tiles(1, n, h, num_dirs);
+  if (ct > 0) return lstm_h3_grid(h, num_dirs, ct);
   if (!persistent_enabled() || (h % 4) != 0) return 0;
   const int UB = (h + GU - 1) / GU, BT = (n + GB - 1) / GB;
   int bts = lstm_bts(UB, num_dirs, BT);
@@ -969,6 +1074,28 @@ ds2_status_t ds2_lstm_bwd(int t_max, int n, int h, int num_dirs, const float* dy
   float* dcs = reinterpret_cast<float*>(static_cast<char*>(ws) + off);
   off += align256((size_t)2 * n * num_dirs * h * sizeof(float));
   unsigned* ctrs = reinterpret_cast<unsigned*>(static_cast<char*>(ws) + off);
+  // the fp16x3 backward (gru_split.hip, NG = 4): W_hh read directly, gate gradients handed
+  // off as one scaled fp16 hi / lo record per producer and step
+  const int ct3 = lstm_h3_tiles(t_max, n, h, num_dirs);
+  if (ct3 > 0) {
+    char* base3 = static_cast<char*>(ws) + lstm_bwd_ws_base(n, h, num_dirs);
+    unsigned* ctrs3 = reinterpret_cast<unsigned*>(base3);
+    float* ring3 = reinterpret_cast<float*>(base3 + lstm_h3_ctr_bytes(n, num_dirs));
+    bool ok = true, launched = false;
+    for (int b0 = 0; ok && b0 < BT; b0 += ct3) {
+      const int bt = std::min(ct3, BT - b0);
+      unsigned* err = ctrs3 + num_dirs * bt;
+      if (hipMemsetAsync(ctrs3, 0, lstm_h3_ctr_bytes(n, num_dirs), st) != hipSuccess)
+        return launch_status("ds2_lstm counters");
+      ok = launch_lstm_bwd_h3(t_max, n, h, num_dirs, dy, dy_dirs, w_hh_f, w_hh_r, c_all, gates,
+                              lens, dgates, ring3, ctrs3, err, kLstmDopPadLds, st, nullptr, b0, bt);
+      if (ok) fold_err(err, err_out, st);
+      if (!ok && launched) return launch_status("ds2_lstm_bwd chunk");
+      launched = launched || ok;
+    }
+    if (ok) return launch_status("ds2_lstm_bwd");
+    (void)hipGetLastError();
+  }
   hipLaunchKernelGGL(pack_bwd_kernel<4>, dim3(grid_cap((int64_t)num_dirs * UB * KS * 64)),
                      dim3(256), 0, st, w_hh_f, w_hh_r, h, num_dirs, UB, KS, wpt);
   const int grid = mapped_grid(UB * num_dirs, BT);

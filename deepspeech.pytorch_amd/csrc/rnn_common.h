@@ -434,4 +434,50 @@ static inline int grid_cap(int64_t work) {
 
 static inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
+// fp16x3 (the recurrences' default since round 5): a value x of a row scaled by 2^e into
+// [2^14, 2^15) splits into hi = f16(x 2^e) and lo = f16(x 2^e - hi) (22 significant bits
+// kept for every element within 2^17 of the row's max), and a.b takes three products
+// lo.hi + hi.lo + hi.hi on v_mfma_f32_16x16x32_f16 (each exact in fp32): half the MFMAs of
+// the bf16x6 form and two operand planes instead of three.  h (|h| <= 1) takes the fixed
+// scale 2^14; each W_hh row (gate, unit) its own, found at kernel start.
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2h __attribute__((ext_vector_type(2)));
+struct Duo {
+  f16x8 hi, lo;
+};
+
+// 8 fp32 values (k slots 0..3 from a, 4..7 from b) times sc -> fp16 (hi, lo)
+__device__ __forceinline__ Duo split2h(const f32x4 a, const f32x4 b, float sc) {
+  typedef float f32x2v __attribute__((ext_vector_type(2)));
+  Duo t;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const f32x2v x = (j < 2 ? f32x2v{a[2 * j], a[2 * j + 1]} : f32x2v{b[2 * j - 4], b[2 * j - 3]}) * sc;
+    const f16x2h h = __builtin_convertvector(x, f16x2h);
+    const f16x2h l = __builtin_convertvector(x - __builtin_convertvector(h, f32x2v), f16x2h);
+    t.hi[2 * j] = h[0];
+    t.hi[2 * j + 1] = h[1];
+    t.lo[2 * j] = l[0];
+    t.lo[2 * j + 1] = l[1];
+  }
+  return t;
+}
+
+// c += a.b from the fp16 terms (small terms first)
+__device__ __forceinline__ f32x4 mma3h(const Duo& a, const Duo& b, f32x4 c) {
+  c = __builtin_amdgcn_mfma_f32_16x16x32_f16(a.lo, b.hi, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_f16(a.hi, b.lo, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_f16(a.hi, b.hi, c, 0, 0, 0);
+  return c;
+}
+
+// 2^e scale of a row whose max |x| is m (m > 0 finite: m 2^e in [2^14, 2^15); else 1)
+__device__ __forceinline__ int h3_row_exp(float m) {
+  const unsigned u = __float_as_uint(m);
+  const int E = (int)(u >> 23);
+  if (u == 0u || E >= 255) return 0;
+  const int e = 14 - ((E == 0 ? 1 : E) - 127);
+  return e > 127 ? 127 : e;
+}
+
 }  // namespace ds2

@@ -79,6 +79,13 @@ _PROTOS = {
                              _vp]),
     "ds2_rnn_bwd": (_c_int, [_c_int, _c_int, _c_int, _c_int, _vp, _c_int, _vp, _vp, _vp, _vp,
                              _vp, _vp]),
+    "ds2_rnn_fwd_workspace_size": (_sz, [_c_int, _c_int, _c_int]),
+    "ds2_rnn_fwd_ws": (_c_int, [_c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                _vp, _vp, _sz, _vp]),
+    "ds2_rnn_bwd_workspace_size": (_sz, [_c_int, _c_int, _c_int]),
+    "ds2_rnn_bwd_grid": (_c_int, [_c_int, _c_int, _c_int]),
+    "ds2_rnn_bwd_ws": (_c_int, [_c_int, _c_int, _c_int, _c_int, _vp, _c_int, _vp, _vp, _vp, _vp,
+                                _vp, _vp, _vp, _vp, _sz, _vp]),
     "ds2_test_occupy": (_c_int, [_c_int, _c_int, _c_int, _vp, _vp]),
     "ds2_test_rnn_launch_lds": (_c_int, [_c_int, _c_int, _vp, _vp]),
     "ds2_test_timestamp": (_c_int, [_vp, _vp]),

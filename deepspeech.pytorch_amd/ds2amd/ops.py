@@ -878,7 +878,9 @@ def _rnn_param_grads(x, h_all, dgx, dgh, weights, nd, g, need_dx, bf16=False, db
     am = {}
     if h3_enabled() and not bf16:
         if col_amax is not None:
-            am["dgx_c"], am["dgh_c"] = col_amax[:ld], col_amax[ld:]
+            # [2 D g] (dgx, dgh), or [D g] when dgh is dgx (the one-gate RNN)
+            am["dgx_c"] = col_amax[:ld]
+            am["dgh_c"] = col_amax[ld:] if col_amax.numel() == 2 * ld else am["dgx_c"]
             if need_dx:
                 am["dgx_r"] = amax(dgx, tn, ld, ld, want_cols=False)[0]
         else:
@@ -957,9 +959,10 @@ def set_cooperative_guard(fn) -> None:
 
 def persistent_bwd_grid(cell: str, n: int, h: int, nd: int) -> int:
     """Workgroups the persistent backward recurrence of this shape holds at once, as the
-    library will launch it (ds2_gru_bwd_grid / ds2_lstm_bwd_grid; 0 for the per-step
+    library will launch it (ds2_gru_bwd_grid / ds2_lstm_bwd_grid / ds2_rnn_bwd_grid; 0 for the per-step
     kernels, which need no co-residency)."""
-    return _lib.size("ds2_gru_bwd_grid" if cell == "gru" else "ds2_lstm_bwd_grid", n, h, nd)
+    fn = {"gru": "ds2_gru_bwd_grid", "lstm": "ds2_lstm_bwd_grid", "rnn": "ds2_rnn_bwd_grid"}[cell]
+    return _lib.size(fn, n, h, nd)
 
 
 def _guard_cooperative(cell, n, h, nd):
@@ -1042,7 +1045,8 @@ class RNNLayerFn(torch.autograd.Function):
     """One (bi)directional vanilla tanh RNN layer (nn.RNN, rnn_type 'rnn', model.py:15) over
     padded [T, N, In] + lengths: pack -> nn.RNN -> pad of model.py:103-105; with sum_dirs the
     direction sum of model.py:107.  Input projection and every parameter gradient are the
-    GRU's GEMMs with one gate; the recurrence is ds2_rnn_fwd / ds2_rnn_bwd."""
+    GRU's GEMMs with one gate; the recurrence is ds2_rnn_fwd_ws / ds2_rnn_bwd_ws (the GRU's
+    persistent fp16x3 machinery with one gate; per-step kernels where it declines)."""
 
     @staticmethod
     def forward(ctx, x, lens, sum_dirs, hidden, *weights):
@@ -1054,10 +1058,11 @@ class RNNLayerFn(torch.autograd.Function):
         bf16 = _RNN_GEMM_BF16[0]
         xproj = _rnn_input_proj(x, weights, nd, h, bf16)
         h_all = torch.empty(t, n, nd, h, device=dev, dtype=_F32)
-        _lib.call("ds2_rnn_fwd", t, n, h, nd, xproj.data_ptr(), weights[1].data_ptr(),
+        ws = _ws(_lib.size("ds2_rnn_fwd_workspace_size", n, h, nd), dev)
+        _lib.call("ds2_rnn_fwd_ws", t, n, h, nd, xproj.data_ptr(), weights[1].data_ptr(),
                   _p(weights[5] if nd == 2 else None), weights[3].data_ptr(),
                   _p(weights[7] if nd == 2 else None), lens.data_ptr(), h_all.data_ptr(),
-                  _stream())
+                  rnn_status_word(dev).data_ptr(), ws.data_ptr(), ws.numel(), _stream())
         ctx.save_for_backward(x, lens, h_all, *weights)
         ctx.cfg = (sum_dirs, h, nd, bf16)
         return _rnn_output(h_all, sum_dirs, nd)
@@ -1069,12 +1074,18 @@ class RNNLayerFn(torch.autograd.Function):
         t, n, _ = x.shape
         dy = dy.contiguous()
         dy_dirs = 1 if (sum_dirs and nd == 2) else nd
-        dg = torch.empty(t, n, nd, h, device=x.device, dtype=_F32)
-        _lib.call("ds2_rnn_bwd", t, n, h, nd, dy.data_ptr(), dy_dirs, weights[1].data_ptr(),
+        dev = x.device
+        dg = torch.empty(t, n, nd, h, device=dev, dtype=_F32)
+        ws = _ws(_lib.size("ds2_rnn_bwd_workspace_size", n, h, nd), dev)
+        _guard_cooperative("rnn", n, h, nd)
+        col_amax = (torch.empty(nd * h, dtype=_I32, device=dev)
+                    if h3_enabled() and not bf16 else None)
+        _lib.call("ds2_rnn_bwd_ws", t, n, h, nd, dy.data_ptr(), dy_dirs, weights[1].data_ptr(),
                   _p(weights[5] if nd == 2 else None), h_all.data_ptr(), lens.data_ptr(),
-                  dg.data_ptr(), _stream())
+                  dg.data_ptr(), _p(col_amax), rnn_status_word(dev).data_ptr(), ws.data_ptr(),
+                  ws.numel(), _stream())
         dx, grads = _rnn_param_grads(x, h_all, dg, dg, weights, nd, h,
-                                     ctx.needs_input_grad[0], bf16)
+                                     ctx.needs_input_grad[0], bf16, col_amax=col_amax)
         return (dx, None, None, None, *grads)
 
 

@@ -446,6 +446,23 @@ ds2_status_t ds2_rnn_fwd(int t_max, int n, int h, int num_dirs, const float* xpr
 ds2_status_t ds2_rnn_bwd(int t_max, int n, int h, int num_dirs, const float* dy, int dy_dirs,
                          const float* w_hh_f, const float* w_hh_r, const float* h_all,
                          const int* lens, float* dgates, ds2_stream_t stream);
+/* The same recurrences on the GRU's persistent machinery (one launch per layer and pass: the
+ * one-gate fp16x3 instantiations of the GRU kernels, csrc/gru_split.hip), with the per-step
+ * kernels above as the fallback for shapes they decline (H % 16 != 0, a grid past the CUs)
+ * and DS2_RNN_PERSISTENT=0.  err_out as for ds2_gru_fwd.  col_amax (nullable): [D H] column
+ * maxima of |dgates| as float bits (ds2_amax's format) for the fp16x3 weight-gradient GEMMs.
+ * ds2_rnn_bwd_grid: workgroups the persistent backward holds at once (0: per-step kernels). */
+size_t ds2_rnn_fwd_workspace_size(int n, int h, int num_dirs);
+ds2_status_t ds2_rnn_fwd_ws(int t_max, int n, int h, int num_dirs, const float* xproj,
+                            const float* w_hh_f, const float* w_hh_r, const float* b_hh_f,
+                            const float* b_hh_r, const int* lens, float* h_all, unsigned* err_out,
+                            void* ws, size_t ws_bytes, ds2_stream_t stream);
+size_t ds2_rnn_bwd_workspace_size(int n, int h, int num_dirs);
+int ds2_rnn_bwd_grid(int n, int h, int num_dirs);
+ds2_status_t ds2_rnn_bwd_ws(int t_max, int n, int h, int num_dirs, const float* dy, int dy_dirs,
+                            const float* w_hh_f, const float* w_hh_r, const float* h_all,
+                            const int* lens, float* dgates, unsigned* col_amax, unsigned* err_out,
+                            void* ws, size_t ws_bytes, ds2_stream_t stream);
 
 /* ------------------------------------------------------------------------ */
 /* Data-parallel gradient exchange over RCCL (SURVEY §8b allreduce_bucket /

@@ -321,14 +321,22 @@ CONVS = [  # (n, ci, h, w, co, kh, kw, sh, sw, ph, pw)
 ]
 
 
-@pytest.mark.parametrize("x6", ["1", "0"])
+def _conv_mode(monkeypatch, mode):
+    """h3: the default (fp16x3 conv2-shaped fwd / dgrad, bf16x6 elsewhere); x6: bf16x6
+    (DS2_CONV_H3=0); fp32: the fp32 LDS-patch / implicit-GEMM kernels (DS2_CONV_X6=0)."""
+    monkeypatch.setenv("DS2_CONV_X6", "0" if mode == "fp32" else "1")
+    monkeypatch.setenv("DS2_CONV_H3", "1" if mode == "h3" else "0")
+
+
+@pytest.mark.parametrize("mode", ["h3", "x6", "fp32"])
 @pytest.mark.parametrize("cfg", CONVS)
-def test_conv_fwd_bwd(dev, cfg, x6, monkeypatch):
-    """conv fwd / dgrad / wgrad vs fp64 torch at 1e-5: the bf16x6 direct kernels (default
-    where they fit: width stride 1, <= 24 tap rows, <= 12 kernel columns) and the fp32
-    LDS-patch / implicit-GEMM kernels (DS2_CONV_X6=0, and every shape the bf16x6 kernels do
-    not cover)."""
-    monkeypatch.setenv("DS2_CONV_X6", x6)
+def test_conv_fwd_bwd(dev, cfg, mode, monkeypatch):
+    """conv fwd / dgrad / wgrad vs fp64 torch at 1e-5: the fp16x3 kernels (default for the
+    conv2-shaped forward -- 3 tap-row groups, 11-12 kernel columns, width stride 1 -- and the
+    4 x 2-fragment dgrad), the bf16x6 direct kernels (DS2_CONV_H3=0, and where fp16x3 does not
+    apply: width stride 1, <= 24 tap rows, <= 12 kernel columns) and the fp32 LDS-patch /
+    implicit-GEMM kernels (DS2_CONV_X6=0, and every shape the bf16x6 kernels do not cover)."""
+    _conv_mode(monkeypatch, mode)
     n, ci, h, w, co, kh, kw, sh, sw, ph, pw = cfg
     g = torch.Generator().manual_seed(sum(cfg))
     x = torch.randn(n, ci, h, w, generator=g, dtype=torch.float64)
@@ -357,8 +365,8 @@ def test_conv_fwd_bwd(dev, cfg, x6, monkeypatch):
 
 
 def test_conv_x6_is_fp32_accurate(dev, monkeypatch):
-    """On the model's conv2 (32 -> 32 channels, 21 x 11 taps, stride (2, 1)) the bf16x6
-    kernels' error against fp64 is of the fp32 kernels' order (fwd, dgrad and wgrad)."""
+    """On the model's conv2 (32 -> 32 channels, 21 x 11 taps, stride (2, 1)) the fp16x3 and
+    bf16x6 kernels' error against fp64 is of the fp32 kernels' order (fwd, dgrad and wgrad)."""
     n, ci, h, w, co, kh, kw, sh, sw, ph, pw = 2, 32, 81, 300, 32, 21, 11, 2, 1, 10, 5
     g = torch.Generator().manual_seed(11)
     x = torch.randn(n, ci, h, w, generator=g, dtype=torch.float64)
@@ -368,16 +376,47 @@ def test_conv_x6_is_fp32_accurate(dev, monkeypatch):
     dxr = torch.nn.grad.conv2d_input(x.shape, wt, dy, stride=(sh, sw), padding=(ph, pw))
     dwr = torch.nn.grad.conv2d_weight(x, wt.shape, dy, stride=(sh, sw), padding=(ph, pw))
     errs = {}
-    for mode in ("1", "0"):
-        monkeypatch.setenv("DS2_CONV_X6", mode)
+    for mode in ("h3", "x6", "fp32"):
+        _conv_mode(monkeypatch, mode)
         yd = ops.conv2d_fwd(x.float().to(dev), wt.float().to(dev), None, (sh, sw), (ph, pw))
         dx = ops.conv2d_dgrad(dy.float().to(dev), wt.float().to(dev), x.shape, (sh, sw), (ph, pw))
         dw, _ = ops.conv2d_wgrad(dy.float().to(dev), x.float().to(dev), tuple(wt.shape), (sh, sw),
                                  (ph, pw), with_bias=False)
         errs[mode] = tuple((a.double().cpu() - r).abs().max().item() / r.abs().max().item()
                            for a, r in ((yd, y), (dx, dxr), (dw, dwr)))
-    assert all(e1 <= 2.5 * e0 for e1, e0 in zip(errs["1"], errs["0"])), errs
-    assert max(errs["1"]) < 5e-6, errs
+    for mode in ("h3", "x6"):
+        assert all(e1 <= 2.5 * e0 for e1, e0 in zip(errs[mode], errs["fp32"])), errs
+        assert max(errs[mode]) < 5e-6, errs
+
+
+def test_conv_h3_scales_over_twelve_decades(dev, monkeypatch):
+    """fp16x3 conv2 forward / dgrad with samples and output channels spread over 10^+-6: the
+    per-sample input scale and per-row weight scale keep every output at the fp32 error bound's
+    form, max |y - y64| / (|w| * |x|) (the same convolution of absolute values), within 2.5x of
+    bf16x6's and below 2e-6."""
+    n, ci, h, w, co, kh, kw, sh, sw, ph, pw = 4, 32, 81, 90, 32, 21, 11, 2, 1, 10, 5
+    g = torch.Generator().manual_seed(23)
+    sx = torch.pow(10.0, torch.linspace(-6, 6, n, dtype=torch.float64))
+    sw_ = torch.pow(10.0, torch.empty(co, dtype=torch.float64).uniform_(-6, 6, generator=g))
+    x = torch.randn(n, ci, h, w, generator=g, dtype=torch.float64) * sx[:, None, None, None]
+    wt = torch.randn(co, ci, kh, kw, generator=g, dtype=torch.float64) * 0.1 * sw_[:, None, None, None]
+    y = F.conv2d(x, wt, None, stride=(sh, sw), padding=(ph, pw))
+    yb = F.conv2d(x.abs(), wt.abs(), None, stride=(sh, sw), padding=(ph, pw))
+    # dgrad: dy samples spread the same way, the weight rows of the dgrad GEMM are ci
+    swi = torch.pow(10.0, torch.empty(ci, dtype=torch.float64).uniform_(-6, 6, generator=g))
+    wt2 = torch.randn(co, ci, kh, kw, generator=g, dtype=torch.float64) * 0.1 * swi[None, :, None, None]
+    dy = torch.randn(y.shape, generator=g, dtype=torch.float64) * sx[:, None, None, None]
+    dxr = torch.nn.grad.conv2d_input(x.shape, wt2, dy, stride=(sh, sw), padding=(ph, pw))
+    dxb = torch.nn.grad.conv2d_input(x.shape, wt2.abs(), dy.abs(), stride=(sh, sw), padding=(ph, pw))
+    errs = {}
+    for mode in ("h3", "x6"):
+        _conv_mode(monkeypatch, mode)
+        yd = ops.conv2d_fwd(x.float().to(dev), wt.float().to(dev), None, (sh, sw), (ph, pw))
+        dx = ops.conv2d_dgrad(dy.float().to(dev), wt2.float().to(dev), x.shape, (sh, sw), (ph, pw))
+        errs[mode] = tuple(((a.double().cpu() - r).abs() / b.clamp_min(1e-300)).max().item()
+                           for a, r, b in ((yd, y, yb), (dx, dxr, dxb)))
+    assert all(e3 <= 2.5 * e6 + 1e-7 for e3, e6 in zip(errs["h3"], errs["x6"])), errs
+    assert max(errs["h3"]) < 2e-6, errs
 
 
 @pytest.mark.parametrize("cfg", [(2, 32, 81, 200, 32, 21, 11, 2, 1, 10, 5),
@@ -641,12 +680,17 @@ def test_gru_per_direction_output(dev):
 
 
 # ---------------------------------------------------------------------------- tanh RNN
+@pytest.mark.parametrize("persistent", ["1", "0"])
 @pytest.mark.parametrize("n,t,inp,h,bidir", [(5, 23, 40, 24, True), (19, 9, 33, 100, True),
-                                             (3, 17, 20, 16, False), (33, 40, 64, 800, True)])
-def test_rnn_layer(dev, n, t, inp, h, bidir):
+                                             (3, 17, 20, 16, False), (33, 40, 64, 800, True),
+                                             (20, 31, 24, 48, True), (32, 120, 96, 800, False)])
+def test_rnn_layer(dev, n, t, inp, h, bidir, persistent, monkeypatch):
     """rnn_type 'rnn' (model.py:15, nn.RNN tanh): the ds2amd layer == pack -> nn.RNN -> pad
     (-> direction sum) in fp64, forward and every gradient; ragged lengths, three batch
-    tiles of 16 at n = 33."""
+    tiles of 16 at n = 33.  Both recurrence paths: the one-gate fp16x3 persistent kernels
+    (H % 16 == 0: 16, 48, 800; the others fall back) and the per-step kernels
+    (DS2_RNN_PERSISTENT=0)."""
+    monkeypatch.setenv("DS2_RNN_PERSISTENT", persistent)
     g = torch.Generator().manual_seed(n * 100 + h + 1)
     rnn = torch.nn.RNN(inp, h, bidirectional=bidir).double()
     a = 0.3 if h <= 100 else h ** -0.5
@@ -690,12 +734,16 @@ def _lstm_case(n, t, inp, h, bidir, seed):
     return lstm, lens, x, g
 
 
+@pytest.mark.parametrize("h3", ["1", "0"])
 @pytest.mark.parametrize("n,t,inp,h,bidir", [(5, 23, 40, 24, True), (19, 9, 33, 400, True),
                                              (3, 17, 20, 16, False),
                                              (64, 5, 64, 1024, True),     # cfg4 shape: 2 batch chunks
-                                             (32, 6, 48, 1024, False)])   # persistent, 2 bwd chunks
-def test_lstm_layer(dev, n, t, inp, h, bidir):
-    """ds2amd LSTM layer == pack -> nn.LSTM -> pad (-> direction sum), fwd and bwd."""
+                                             (32, 6, 48, 1024, False),    # persistent, 2 bwd chunks
+                                             (40, 150, 32, 1024, True)])  # long: 3 tiles, 2 chunks
+def test_lstm_layer(dev, n, t, inp, h, bidir, h3, monkeypatch):
+    """ds2amd LSTM layer == pack -> nn.LSTM -> pad (-> direction sum), fwd and bwd: the
+    fp16x3 recurrences (default; H % 16 == 0) and the fp32-MFMA ones (DS2_LSTM_H3=0)."""
+    monkeypatch.setenv("DS2_LSTM_H3", h3)
     lstm, lens, x, g = _lstm_case(n, t, inp, h, bidir, n * 100 + h)
     xr = x.clone().requires_grad_(True)
     out, _ = lstm(torch.nn.utils.rnn.pack_padded_sequence(xr, lens.numpy()))
