@@ -910,11 +910,16 @@ __global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
             tmp = __builtin_amdgcn_mfma_f32_16x16x32_f16(bhi, wgo[p].hi, tmp, 0, 0, 0);
           }
           if constexpr (NG != 4) {
+            // its own accumulator: a 16x16x16 MFMA taking a 16x16x32 MFMA's result as srcC
+            // back to back got rows 0-1 of every 4 wrong on gfx950 (hipcc 7.2 inserts no wait
+            // states between the two opcodes; scripts/gru_bwd_h3_debug.py)
             const f16x4 nh = __builtin_bit_cast(f16x4, u32x2{r2[p][0], r2[p][1]});
             const f16x4 nl = __builtin_bit_cast(f16x4, u32x2{r2[p][2], r2[p][3]});
-            tmp = __builtin_amdgcn_mfma_f32_16x16x16f16(nl, wnh[p], tmp, 0, 0, 0);
-            tmp = __builtin_amdgcn_mfma_f32_16x16x16f16(nh, wnl[p], tmp, 0, 0, 0);
-            tmp = __builtin_amdgcn_mfma_f32_16x16x16f16(nh, wnh[p], tmp, 0, 0, 0);
+            f32x4 tn = f32x4{0.f, 0.f, 0.f, 0.f};
+            tn = __builtin_amdgcn_mfma_f32_16x16x16f16(nl, wnh[p], tn, 0, 0, 0);
+            tn = __builtin_amdgcn_mfma_f32_16x16x16f16(nh, wnl[p], tn, 0, 0, 0);
+            tn = __builtin_amdgcn_mfma_f32_16x16x16f16(nh, wnh[p], tn, 0, 0, 0);
+            tmp += tn;
           }
           acc += tmp * rs[p];   // rows 4 (lane >> 4) + i: the producer's 2^-e of those rows
         }

@@ -1,0 +1,95 @@
+// MFMA accumulation rounding probe: how the fp32 result of one MFMA is rounded when the
+// exact value C + sum(a b) is not representable, for the instructions the fp32-accurate
+// split kernels use (f16 / bf16 16x16x32, 32x32x16) and the fp32 one (16x16x4f32).
+// Case "tie+": C = 2^24, products sum to 1.5 (exact 2^24 + 1.5): RNE 2^24 + 2, RZ / RD 2^24.
+// Case "tie-": the same negated: RNE -(2^24 + 2), RZ / RU -2^24.
+// Case "sum": C = 0, products 2^24, 1, 1 in one instruction: exact 2^24 + 2 (one rounding of
+// the exact sum) vs 2^24 (sequential fp32 adds, each tie to even).
+// build: hipcc -O3 --offload-arch=gfx950 -o scripts/mfma_rounding scripts/mfma_rounding.hip
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// lane 0..15 hold row i = lane, k = 0..7 (16x16x32: k = 8 (lane / 16) + j); products placed at
+// k = 0, 1, 2 of row/column 0 only
+__global__ void probe(float* out) {
+  const int lane = threadIdx.x;
+  const int cases = 3;
+  for (int cs = 0; cs < cases; ++cs) {
+    float pa[3] = {0.f, 0.f, 0.f}, c0 = 0.f;
+    if (cs == 0) { pa[0] = 1.5f; c0 = 16777216.f; }
+    if (cs == 1) { pa[0] = -1.5f; c0 = -16777216.f; }
+    if (cs == 2) { pa[0] = 16777216.f; pa[1] = 1.f; pa[2] = 1.f; c0 = 0.f; }
+    // f16 16x16x32: a = value (f16 holds 2^24? no: max 65504) -> use a = v / 2^12, b = 2^12
+    {
+      f16x8 a = {}, b = {};
+      if (lane == 0)
+        for (int j = 0; j < 3; ++j) { a[j] = (_Float16)(pa[j] / 4096.f); b[j] = (_Float16)4096.f; }
+      f32x4 c = {c0, c0, c0, c0};
+      c = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+      if (lane == 0) out[cs * 8 + 0] = c[0];
+    }
+    {
+      bf16x8 a = {}, b = {};
+      if (lane == 0)
+        for (int j = 0; j < 3; ++j) { a[j] = (__bf16)(pa[j] / 4096.f); b[j] = (__bf16)4096.f; }
+      f32x4 c = {c0, c0, c0, c0};
+      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+      if (lane == 0) out[cs * 8 + 1] = c[0];
+    }
+    {
+      // 32x32x16 bf16: lane L holds row L % 32, k = 8 (L / 32) + j
+      bf16x8 a = {}, b = {};
+      if (lane == 0)
+        for (int j = 0; j < 3; ++j) { a[j] = (__bf16)(pa[j] / 4096.f); b[j] = (__bf16)4096.f; }
+      f32x16 c;
+      for (int r = 0; r < 16; ++r) c[r] = c0;
+      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+      if (lane == 0) out[cs * 8 + 2] = c[0];
+    }
+    {
+      f16x8 a = {}, b = {};
+      if (lane == 0)
+        for (int j = 0; j < 3; ++j) { a[j] = (_Float16)(pa[j] / 4096.f); b[j] = (_Float16)4096.f; }
+      f32x16 c;
+      for (int r = 0; r < 16; ++r) c[r] = c0;
+      c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+      if (lane == 0) out[cs * 8 + 3] = c[0];
+    }
+    {
+      // 16x16x4 f32: lane L holds row L % 16, k = L / 16: three MFMAs, one product each
+      // (k = 0 only), so this is three sequential accumulations
+      f32x4 c = {c0, c0, c0, c0};
+      for (int j = 0; j < 3; ++j) {
+        const float a = lane == 0 ? pa[j] : 0.f, b = lane == 0 ? 1.f : 0.f;
+        c = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+      }
+      if (lane == 0) out[cs * 8 + 4] = c[0];
+    }
+  }
+}
+
+int main() {
+  float* d;
+  hipMalloc(&d, 64 * sizeof(float));
+  hipMemset(d, 0, 64 * sizeof(float));
+  hipLaunchKernelGGL(probe, dim3(1), dim3(64), 0, 0, d);
+  float h[64];
+  hipMemcpy(h, d, sizeof(h), hipMemcpyDeviceToHost);
+  const char* names[5] = {"f16 16x16x32", "bf16 16x16x32", "bf16 32x32x16", "f16 32x32x16",
+                          "f32 16x16x4 (3 MFMAs)"};
+  const char* cases[3] = {"tie+ (2^24 + 1.5: RNE +2, RZ +0)", "tie- (-(2^24 + 1.5): RNE -2, RZ -0)",
+                          "sum (2^24 + 1 + 1 in one MFMA: exact +2, sequential +0)"};
+  for (int cs = 0; cs < 3; ++cs)
+    for (int i = 0; i < 5; ++i) {
+      const double base = cs == 1 ? -16777216.0 : 16777216.0;
+      printf("{\"instr\": \"%s\", \"case\": \"%s\", \"result_minus_2^24\": %.1f}\n", names[i],
+             cases[cs], (double)h[cs * 8 + i] - base);
+    }
+  hipFree(d);
+  return 0;
+}
