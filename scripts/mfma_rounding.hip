@@ -73,6 +73,64 @@ __global__ void probe(float* out) {
   }
 }
 
+// Width of the exact window: C = 2^20 (even lsb, ulp 2^-3) or 2^20 + 2^-3 (odd lsb); products
+// {2^-4 (half an ulp: a tie), +-2^(-4-d)} in ONE instruction.  T1 (C even, +tiny): exact
+// rounds UP (+2^-3); tiny dropped -> tie -> even (+0).  T2 (C odd, -tiny): exact rounds DOWN
+// (+2^-3 kept); tiny dropped toward zero -> tie -> even (+2^-2); floor-truncated -> down (+2^-3).
+__global__ void window(float* out) {
+  const int lane = threadIdx.x;
+  for (int d = 0; d < 8; ++d) {
+    const int dd = 2 + 3 * d;                         // tiny = 2^(-4 - dd)
+    const float tiny = ldexpf(1.f, -4 - dd);
+    for (int t = 0; t < 2; ++t) {
+      const float c0 = t == 0 ? 1048576.f : 1048576.f + 0.125f;
+      const float p1 = t == 0 ? tiny : -tiny;
+      {
+        f16x8 a = {}, b = {};
+        if (lane == 0) {
+          a[0] = (_Float16)0.25f; b[0] = (_Float16)0.25f;                 // 2^-4
+          a[1] = (_Float16)ldexpf(p1, (4 + dd) / 2); b[1] = (_Float16)ldexpf(1.f, -(4 + dd) + (4 + dd) / 2);
+        }
+        f32x4 c = {c0, c0, c0, c0};
+        c = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+        if (lane == 0) out[(d * 2 + t) * 4 + 0] = c[0] - 1048576.f;
+      }
+      {
+        bf16x8 a = {}, b = {};
+        if (lane == 0) {
+          a[0] = (__bf16)0.25f; b[0] = (__bf16)0.25f;
+          a[1] = (__bf16)p1; b[1] = (__bf16)1.f;
+        }
+        f32x4 c = {c0, c0, c0, c0};
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+        if (lane == 0) out[(d * 2 + t) * 4 + 1] = c[0] - 1048576.f;
+      }
+      {
+        bf16x8 a = {}, b = {};
+        if (lane == 0) {
+          a[0] = (__bf16)0.25f; b[0] = (__bf16)0.25f;
+          a[1] = (__bf16)p1; b[1] = (__bf16)1.f;
+        }
+        f32x16 c;
+        for (int r = 0; r < 16; ++r) c[r] = c0;
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+        if (lane == 0) out[(d * 2 + t) * 4 + 2] = c[0] - 1048576.f;
+      }
+      {
+        f16x8 a = {}, b = {};
+        if (lane == 0) {
+          a[0] = (_Float16)0.25f; b[0] = (_Float16)0.25f;
+          a[1] = (_Float16)ldexpf(p1, (4 + dd) / 2); b[1] = (_Float16)ldexpf(1.f, -(4 + dd) + (4 + dd) / 2);
+        }
+        f32x16 c;
+        for (int r = 0; r < 16; ++r) c[r] = c0;
+        c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+        if (lane == 0) out[(d * 2 + t) * 4 + 3] = c[0] - 1048576.f;
+      }
+    }
+  }
+}
+
 int main() {
   float* d;
   hipMalloc(&d, 64 * sizeof(float));
@@ -90,6 +148,21 @@ int main() {
       printf("{\"instr\": \"%s\", \"case\": \"%s\", \"result_minus_2^24\": %.1f}\n", names[i],
              cases[cs], (double)h[cs * 8 + i] - base);
     }
+  float* w;
+  hipMalloc(&w, 128 * sizeof(float));
+  hipMemset(w, 0, 128 * sizeof(float));
+  hipLaunchKernelGGL(window, dim3(1), dim3(64), 0, 0, w);
+  float hw[128];
+  hipMemcpy(hw, w, sizeof(hw), hipMemcpyDeviceToHost);
+  const char* wn[4] = {"f16 16x16x32", "bf16 16x16x32", "bf16 32x32x16", "f16 32x32x16"};
+  for (int dd = 0; dd < 8; ++dd)
+    for (int i = 0; i < 4; ++i)
+      printf("{\"instr\": \"%s\", \"tiny_rel_to_C\": \"2^-%d\", \"T1_even_plus\": %.4f, "
+             "\"T2_odd_minus\": %.4f}\n", wn[i], 24 + 2 + 3 * dd, (double)hw[(dd * 2) * 4 + i],
+             (double)hw[(dd * 2 + 1) * 4 + i]);
+  printf("T1: 0.125 = tiny kept (exact RNE), 0 = tiny dropped; T2: 0.125 = exact or floor, "
+         "0.25 = tiny dropped toward zero\n");
+  hipFree(w);
   hipFree(d);
   return 0;
 }

@@ -40,8 +40,30 @@ for it in range(3):
     torch.cuda.synchronize()
 
 
+# Floors of each phase from MI355X_MICROARCH.md (persistent-kernel price list, per-instruction
+# table) for the fp16x3 kernels at this shape, printed beside the measured phases:
+#  forward  -- sentinel ring (data-tagged: handoff-1to1, 1.0-1.4 us idle/loaded for <= 4 KB);
+#              stage = UB 1-KB h tiles per workgroup per step at the handoff-payload rate
+#              (62-70 GB/s per block cross-XCD, 104-122 same-XCD plain); MFMA = per wave 7
+#              pairs x 3 gates x 3 v_mfma_f32_16x16x32_f16 (16 cycles/SIMD each), one wave/SIMD
+#  backward -- flag hand-off (handoff-flag, drained sc1: 1.3 idle ... 1.7-1.9x handoff-1to1);
+#              stage = UB records of 3.06 KB; MFMA = per wave 7 producers x (3 x 16 + 3 x 8)
+#              cycles, two waves per SIMD
+CLK_GHZ = 2.0
+FLOORS = {
+    "forward": {"wait": (1.0, 1.4), "stage": (UB * 1024 / 122e3, UB * 1024 / 62e3),
+                "mfma": (7 * 3 * 3 * 16 / (CLK_GHZ * 1e3),) * 2},
+    "backward": {"wait": (1.3, 2.5), "stage": (UB * 3136 / 122e3, UB * 3136 / 62e3),
+                 "mfma": (2 * 7 * (3 * 16 + 3 * 8) / (CLK_GHZ * 1e3),) * 2},
+}
+
+
 def analyse(tr, label):
     print(f"--- {label}")
+    fl = FLOORS.get(label)
+    if fl is not None:
+        print("floors (us, MI355X_MICROARCH): " + ", ".join(
+            f"{k} {a:.2f}-{b:.2f}" for k, (a, b) in fl.items()))
     groups = {}
     for wg in range(grid):
         xcd, slot = wg & 7, wg >> 3
