@@ -1131,6 +1131,24 @@ __device__ __forceinline__ f32x16 cx_mma(const bf16x8 (&a)[3], const bf16x8 (&b)
   }
 }
 
+// acc += a.b with the pair's products summed from zero and added into acc by VALU (RNE).  The
+// matrix cores floor each addend's bits below ~2^-31 of the largest operand of the instruction,
+// C included (scripts/mfma_rounding.hip, profiles/r5l_mfma_rounding.jsonl): chained into a
+// long accumulator, every MFMA loses a floor of ~2^-31 |C| -- a negative bias that sums of
+// the outputs (the BatchNorm parameter gradients after the conv block) amplify.  From a zero
+// C the window sits at the pair's own products.
+template <int NPL, bool FRESH>
+__device__ __forceinline__ void cx_mma_acc(const bf16x8 (&a)[3], const bf16x8 (&b)[3], f32x16& acc) {
+  if constexpr (FRESH) {
+    f32x16 z;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) z[r] = 0.f;
+    acc += cx_mma<NPL>(a, b, z);
+  } else {
+    acc = cx_mma<NPL>(a, b, acc);
+  }
+}
+
 // a weight-image value's fp16x3 / bf16x6 terms (NPL planes, `per` apart from img[base])
 template <int NPL>
 __device__ __forceinline__ void cx_wimg_put(unsigned short* __restrict__ img, int64_t base,
@@ -1201,6 +1219,33 @@ __global__ void conv_h3_samax_kernel(const float* __restrict__ x, int64_t per,
   if (threadIdx.x == 0) {
     for (int i = 1; i < (int)(blockDim.x >> 6); ++i) mx = fmaxf(mx, red[i]);
     if (b < e) atomicMax(out + n, __float_as_uint(mx));
+  }
+}
+
+// per-channel max |t| of an [N][C][plane] tensor (float bits, unsigned atomic max; out zeroed
+// first): grid (chunks, C), 256 threads striding the channel's N x plane elements
+__global__ void conv_h3_chamax_kernel(const float* __restrict__ t, int N, int C, int64_t plane,
+                                      unsigned* __restrict__ out) {
+  __shared__ float red[4];
+  const int ch = blockIdx.y;
+  const int64_t total = (int64_t)N * plane;
+  const int64_t chunk = (total + gridDim.x - 1) / gridDim.x;
+  const int64_t b = (int64_t)blockIdx.x * chunk;
+  const int64_t e = b + chunk < total ? b + chunk : total;
+  float mx = 0.f;
+  int64_t i = b + threadIdx.x;
+  int64_t n = i / plane, pp = i - n * plane;
+  for (; i < e; i += blockDim.x) {
+    mx = fmaxf(mx, fabsf(t[(n * C + ch) * plane + pp]));
+    pp += blockDim.x;
+    while (pp >= plane) { pp -= plane; ++n; }
+  }
+  mx = wave_max(mx);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int k = 1; k < (int)(blockDim.x >> 6); ++k) mx = fmaxf(mx, red[k]);
+    if (b < e && mx > 0.f) atomicMax(out + ch, __float_as_uint(mx));
   }
 }
 
@@ -1299,7 +1344,8 @@ __global__ void conv_x6_wimg_kernel(const float* __restrict__ w, ConvDims g, CxG
 // NPL 2: fp16x3 -- the patch is staged as fp16 hi / lo of x 2^e_n (e_n from the sample's
 // max |x|, n_amax[n]), the image holds w 2^m_exp[m], three products per fragment pair, and the
 // epilogue multiplies by 2^-(m_exp[m] + e_n) (exact) before the bias.
-template <bool DGRAD, int NGA, int NBP_, int PU, int SW, bool RCH, bool DB = false, int NPL = 3>
+template <bool DGRAD, int NGA, int NBP_, int PU, int SW, bool RCH, bool DB = false, int NPL = 3,
+          bool FRESH = false>
 __global__ __launch_bounds__(CX_T, 1) void conv_x6_kernel(const float* __restrict__ in,
                                                           const unsigned short* __restrict__ img,
                                                           const float* __restrict__ bias,
@@ -1444,6 +1490,16 @@ __global__ __launch_bounds__(CX_T, 1) void conv_x6_kernel(const float* __restric
     unsigned short* pnext = ps + ((l + 1) & 1) * NPL * PPL;
     bool staged = false;
     if (active) {
+      // FRESH: this channel's MFMA chain starts from zero C and joins acc by VALU (RNE), so
+      // the matrix cores' floor of addend bits below ~2^-31 of C (cx_mma_acc) acts at one
+      // channel's magnitude instead of the whole sum's
+      f32x16 tac[2];
+      if constexpr (FRESH) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) tac[j][r] = 0.f;
+      }
       auto kstep = [&](int st) {
         const int ga = st / nbp, p = st - (st / nbp) * nbp;
         const int b = 2 * p + fh;
@@ -1459,7 +1515,10 @@ __global__ __launch_bounds__(CX_T, 1) void conv_x6_kernel(const float* __restric
             bfr[j][pl] = *reinterpret_cast<const bf16x8*>(pcur + pl * PPL + ap);
         }
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[j] = cx_mma<NPL>(af, bfr[j], acc[j]);
+        for (int j = 0; j < 2; ++j) {
+          if constexpr (FRESH) tac[j] = cx_mma<NPL>(af, bfr[j], tac[j]);
+          else acc[j] = cx_mma<NPL>(af, bfr[j], acc[j]);
+        }
       };
       if (NGA > 0 && NBP_ > 0) {
         constexpr int NK = NGA * NBP_, H0 = (NK + 1) / 2;
@@ -1489,6 +1548,10 @@ __global__ __launch_bounds__(CX_T, 1) void conv_x6_kernel(const float* __restric
         }
       } else {
         for (int st = s_beg; st < s_end; ++st) kstep(st);
+      }
+      if constexpr (FRESH) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[j] += tac[j];
       }
     }
     if (DB && !staged && l + 1 < LL) {
@@ -1589,8 +1652,11 @@ __device__ __forceinline__ void x6w_store_block(float* __restrict__ partial, int
 
 // dW[co][ci][a][b] = sum over the S splits (in order) of the blocks above; thread = one
 // (gi, co, w, b, ci) element in block order (coalesced loads)
+// co_amax / ci_amax (fp16x3 partials, else NULL): the sums are scaled by 2^(e_co + e_ci)
 __global__ void wgrad_reduce_x6_kernel(const float* __restrict__ partial, int S, int G, int KW,
-                                       int NW, ConvDims g, float* __restrict__ dw) {
+                                       int NW, ConvDims g, float* __restrict__ dw,
+                                       const unsigned* __restrict__ co_amax,
+                                       const unsigned* __restrict__ ci_amax) {
   const int64_t per = (int64_t)G * (X6W_BLOCK / 4 * NW) * KW;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < per;
        i += (int64_t)gridDim.x * blockDim.x) {
@@ -1605,6 +1671,7 @@ __global__ void wgrad_reduce_x6_kernel(const float* __restrict__ partial, int S,
     float acc = 0.f;
 #pragma unroll 8
     for (int s = 0; s < S; ++s) acc += partial[(int64_t)s * per + i];   // order kept
+    if (co_amax != nullptr) acc = __builtin_ldexpf(acc, -(h3_exp(co_amax[co]) + h3_exp(ci_amax[ci])));
     dw[((int64_t)co * g.ci + ci) * g.kh * KW + a * KW + b] = acc;
   }
 }
@@ -1755,10 +1822,13 @@ constexpr int SW_DPL = 32 * SW_DP;          // bf16 per dy plane
 // NW = 8: eight waves (tap rows) per group, one 512-thread workgroup per CU with a 10-slot ring
 // (123 KB of LDS): G = 3 groups instead of 6 for conv2's 21 tap rows, so every x and dy row is
 // staged -- and fetched -- half as often
-template <int KW, int OFF0, int NW = 4>
+// NPL 2: fp16x3 -- dy staged as fp16 hi / lo of dy 2^e_co (co_amax: max |dy| of each output
+// channel over the batch), x as hi / lo of x 2^e_ci (ci_amax), three products per fragment pair;
+// wgrad_reduce_x6_kernel undoes 2^-(e_co + e_ci) on the summed partials
+template <int KW, int OFF0, int NW = 4, int NPL = 3>
 __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_x6_wgrad_sw_kernel(
     const float* __restrict__ dy, const float* __restrict__ x, float* __restrict__ partial,
-    ConvDims g, int S) {
+    ConvDims g, int S, const unsigned* __restrict__ co_amax, const unsigned* __restrict__ ci_amax) {
   static_assert(NW == 4 || NW == 8, "waves per group");
   constexpr int RING = NW + 2;                // NW window rows + 2 incoming
   __shared__ __attribute__((aligned(16))) unsigned short xs[3 * RING * SW_XSL];
@@ -1800,7 +1870,16 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_x6_wgrad_sw_ker
   const bool b_is_dy = NW == 4 ? wave >= 2 : wave >= 6;
   const int xc_b = (u1 / 6) & 31, xj_b = u1 % 6;             // x unit: incoming row 1
   const int dc_b = (u1 - 384) >> 2, dj_b = (u1 - 384) & 3;   // dy unit
-
+  // fp16x3 staging scales of this thread's units (channels fixed for the whole launch)
+  float sc_a = 1.f, sc_b = 1.f;
+  if constexpr (NPL == 2) {
+    if (a_is_x && xc_a < g.ci) sc_a = h3_scale(h3_exp(ci_amax[xc_a]));
+    if (b_is_x && xc_b < g.ci) sc_b = h3_scale(h3_exp(ci_amax[xc_b]));
+    if (b_is_dy && dc_b >= 0 && dc_b < g.co) {
+      const float s = h3_scale(h3_exp(co_amax[dc_b]));
+      if (NW == 8) sc_a = s; else sc_b = s;
+    }
+  }
   f32x16 acc[KW];
 #pragma unroll
   for (int b = 0; b < KW; ++b)
@@ -1849,11 +1928,12 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_x6_wgrad_sw_ker
       }
     };
     auto store = [&](int xr0, int nr, int db) {
-      if (a_is_x && xr_a < nr) cw_split_store(xs, XPL, slot_of(xr0 + xr_a) * SW_XSL + xc_a * SW_XP + 8 * xj_a, va);
+      if (a_is_x && xr_a < nr)
+        cx_store8<NPL>(xs, XPL, slot_of(xr0 + xr_a) * SW_XSL + xc_a * SW_XP + 8 * xj_a, va, sc_a);
       if (b_is_x) {
-        if (nr > 1) cw_split_store(xs, XPL, slot_of(xr0 + 1) * SW_XSL + xc_b * SW_XP + 8 * xj_b, vb);
+        if (nr > 1) cx_store8<NPL>(xs, XPL, slot_of(xr0 + 1) * SW_XSL + xc_b * SW_XP + 8 * xj_b, vb, sc_b);
       } else if (b_is_dy && db >= 0) {
-        cw_split_store(ds[db], SW_DPL, dc_b * SW_DP + 8 * dj_b, NW == 8 ? va : vb);
+        cx_store8<NPL>(ds[db], SW_DPL, dc_b * SW_DP + 8 * dj_b, NW == 8 ? va : vb, NW == 8 ? sc_a : sc_b);
       }
     };
     // segment start: every slot and dy buffer is free once all waves pass this barrier; the
@@ -1879,11 +1959,11 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_x6_wgrad_sw_ker
         for (int kst = 0; kst < SW_COLS / 16; ++kst) {
           bf16x8 af[3];
 #pragma unroll
-          for (int pl = 0; pl < 3; ++pl)
+          for (int pl = 0; pl < NPL; ++pl)
             af[pl] = *reinterpret_cast<const bf16x8*>(dsb + pl * SW_DPL + fr * SW_DP + 16 * kst + 8 * fh);
 #pragma unroll
-          for (int pi = 0; pi < 3; ++pi) {
-            const int pl = 2 - pi;
+          for (int pi = 0; pi < NPL; ++pi) {
+            const int pl = NPL - 1 - pi;
             unsigned wv[12];
 #pragma unroll
             for (int jj = 0; jj < 3; ++jj) {
@@ -1901,8 +1981,14 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_x6_wgrad_sw_ker
                                 : wv[o / 2 + e];
               const bf16x8 bx = __builtin_bit_cast(bf16x8, qb);
 #pragma unroll
-              for (int i = 2 - pl; i >= 0; --i)
-                acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bx, acc[b], 0, 0, 0);
+              for (int i = NPL - 1 - pl; i >= 0; --i) {
+                if constexpr (NPL == 2)
+                  acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(cf16x8, af[i]),
+                                                                  __builtin_bit_cast(cf16x8, bx),
+                                                                  acc[b], 0, 0, 0);
+                else
+                  acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bx, acc[b], 0, 0, 0);
+              }
             }
           }
         }
@@ -1975,7 +2061,7 @@ __global__ void conv_x6q_wimg_kernel(const float* __restrict__ w, ConvDims g,
 // into the other buffer right after the k-steps of channel l, one barrier per channel.  The
 // patch gather offsets (and their bounds) are the same for every channel and are hoisted.
 // NPL 2: fp16x3, scales as conv_x6_kernel's (e_n from the sample's max |dy|, m = ci)
-template <bool DB, int NPL = 3>
+template <bool DB, int NPL = 3, bool FRESH = false>
 __global__ __launch_bounds__(CX_T, 1) void conv_x6q_dgrad_kernel(const float* __restrict__ dy,
                                                                  const unsigned short* __restrict__ img,
                                                                  float* __restrict__ dx, ConvDims g,
@@ -2101,7 +2187,7 @@ __global__ __launch_bounds__(CX_T, 1) void conv_x6q_dgrad_kernel(const float* __
             bfr[j][pl] = *reinterpret_cast<const bf16x8*>(pc + pl * CQ_PPL + ap);
         }
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[j] = cx_mma<NPL>(af, bfr[j], acc[j]);
+        for (int j = 0; j < 2; ++j) cx_mma_acc<NPL, FRESH>(af, bfr[j], acc[j]);
       };
       if (kk == 0) {
 #pragma unroll
@@ -2237,6 +2323,12 @@ static inline bool h3c_on() {
   const char* e = getenv("DS2_CONV_H3");
   return !(e != nullptr && e[0] == '0');
 }
+// fp16x3 conv kernels' per-k-step zero-C MFMA chains added by VALU (cx_mma_acc; default on,
+// DS2_CONV_FRESH=0 chains every MFMA into the running accumulator)
+static inline bool fresh_on() {
+  const char* e = getenv("DS2_CONV_FRESH");
+  return !(e != nullptr && e[0] == '0');
+}
 
 // workspace of a split-weight image of `elems` values per plane: NPL 3 planes, or 2 planes +
 // the fp16x3 scales (m_exp[M] int, n_amax[n] unsigned) at the next 256-B boundary
@@ -2259,7 +2351,7 @@ static void cx_h3_scales(const float* in, const float* w, const ConvDims& g, int
   m_exp = reinterpret_cast<int*>(base);
   n_amax = reinterpret_cast<unsigned*>(base + (size_t)M * 4);
   hipLaunchKernelGGL(conv_h3_wexp_kernel<DGRAD>, dim3(M), dim3(256), 0, st, w, g, m_exp);
-  hipMemsetAsync(n_amax, 0, (size_t)g.n * 4, st);
+  (void)hipMemsetAsync(n_amax, 0, (size_t)g.n * 4, st);
   int64_t chunks = cdiv(per, 8192);
   const int64_t cap = cdiv(2048, g.n);
   chunks = chunks < 1 ? 1 : (chunks > cap ? cap : chunks);
@@ -2289,8 +2381,12 @@ static ds2_status_t launch_x6q(const float* dy, const float* w, float* dx, const
     unsigned* n_amax;
     cx_h3_scales<true>(dy, w, g, total, ws, m_exp, n_amax, st);
     hipLaunchKernelGGL(conv_x6q_wimg_kernel<2>, dim3(wgrid), dim3(256), 0, st, w, g, img, m_exp);
-    hipLaunchKernelGGL((conv_x6q_dgrad_kernel<true, 2>), dim3(static_cast<unsigned>(nwg)), dim3(CX_T),
-                       0, st, dy, img, dx, g, gx, g.hi, m_exp, n_amax);
+    if (fresh_on())
+      hipLaunchKernelGGL((conv_x6q_dgrad_kernel<true, 2, true>), dim3(static_cast<unsigned>(nwg)),
+                         dim3(CX_T), 0, st, dy, img, dx, g, gx, g.hi, m_exp, n_amax);
+    else
+      hipLaunchKernelGGL((conv_x6q_dgrad_kernel<true, 2>), dim3(static_cast<unsigned>(nwg)), dim3(CX_T),
+                         0, st, dy, img, dx, g, gx, g.hi, m_exp, n_amax);
   } else {
     hipLaunchKernelGGL(conv_x6q_wimg_kernel<3>, dim3(wgrid), dim3(256), 0, st, w, g, img, nullptr);
     hipLaunchKernelGGL((conv_x6q_dgrad_kernel<true, 3>), dim3(static_cast<unsigned>(nwg)), dim3(CX_T),
@@ -2343,8 +2439,12 @@ static ds2_status_t launch_x6(const float* in, const float* w, const float* bias
     unsigned* n_amax;
     cx_h3_scales<DGRAD>(in, w, g, total, ws, m_exp, n_amax, st);
     hipLaunchKernelGGL((conv_x6_wimg_kernel<DGRAD, 2>), dim3(wgrid), dim3(256), 0, st, w, g, c, img, m_exp);
-    hipLaunchKernelGGL((conv_x6_kernel<DGRAD, 3, 6, 2, 1, false, true, 2>), grid, dim3(CX_T), 0, st,
-                       in, img, bias, out, g, out_lens, c, gx, gy, m_exp, n_amax);
+    if (fresh_on())
+      hipLaunchKernelGGL((conv_x6_kernel<DGRAD, 3, 6, 2, 1, false, true, 2, true>), grid, dim3(CX_T), 0,
+                         st, in, img, bias, out, g, out_lens, c, gx, gy, m_exp, n_amax);
+    else
+      hipLaunchKernelGGL((conv_x6_kernel<DGRAD, 3, 6, 2, 1, false, true, 2>), grid, dim3(CX_T), 0, st,
+                         in, img, bias, out, g, out_lens, c, gx, gy, m_exp, n_amax);
     return launch_status("ds2_conv2d_fwd");
   }
   hipLaunchKernelGGL((conv_x6_wimg_kernel<DGRAD, 3>), dim3(wgrid), dim3(256), 0, st, w, g, c, img, nullptr);
@@ -2442,6 +2542,21 @@ static inline bool x6w_sw(const ConvDims& g) {
 // tap rows per group: 8 for the sliding-window form (one workgroup per CU), 4 otherwise
 static inline int x6w_nw(const ConvDims& g) { return x6w_sw(g) ? 8 : 4; }
 
+// the sliding-window wgrad on fp16x3 (default; DS2_CONV_H3W=0 keeps bf16x6)
+static inline bool h3w_on() {
+  const char* e = getenv("DS2_CONV_H3W");
+  return !(e != nullptr && e[0] == '0');
+}
+
+static inline int x6w_splits(const ConvDims& g);
+// bytes of the x6 wgrad partial blocks (the fp16x3 channel maxima follow, 256-B aligned)
+static inline size_t x6w_part_bytes(const ConvDims& g) {
+  const int nw = x6w_nw(g);
+  const size_t b = (size_t)x6w_splits(g) * ((g.kh + nw - 1) / nw) * (X6W_BLOCK / 4 * nw) * g.kw *
+                   sizeof(float);
+  return (b + 255) / 256 * 256;
+}
+
 static inline int x6w_splits(const ConvDims& g) {
   const int nw = x6w_nw(g);
   const int G = (g.kh + nw - 1) / nw;
@@ -2538,10 +2653,7 @@ size_t ds2_conv2d_wgrad_workspace_size(int n, int c_in, int h_in, int w_in, int 
   ConvDims g;
   if (!make_dims(g, n, c_in, h_in, w_in, c_out, kh, kw, sh, sw, ph, pw)) return 0;
   const size_t per = (size_t)c_out * c_in * kh * kw * sizeof(float);
-  if (x6w_ok(g)) {
-    const int nw = x6w_nw(g);
-    return (size_t)x6w_splits(g) * ((kh + nw - 1) / nw) * (X6W_BLOCK / 4 * nw) * kw * sizeof(float) + 256;
-  }
+  if (x6w_ok(g)) return x6w_part_bytes(g) + ((size_t)c_out + c_in) * 4 + 512;
   const WgradPlan pl = wgrad_plan(g);
   return (size_t)n * (pl.nt > 0 ? pl.bands : 1) * per + 256;
 }
@@ -2561,13 +2673,29 @@ ds2_status_t ds2_conv2d_wgrad(const float* dy, const float* x, float* dw, float*
   float* partial = static_cast<float*>(ws);
   const WgradPlan pl = wgrad_plan(g);
   int slabs = n;
+  unsigned* co_am = nullptr;   // fp16x3 channel maxima (the sliding-window wgrad)
+  unsigned* ci_am = nullptr;
   if (x6w_ok(g)) {
     slabs = x6w_splits(g);
     const int nw = x6w_nw(g);
     const int G = (kh + nw - 1) / nw;
-    if (x6w_sw(g))
+    if (x6w_sw(g) && h3w_on()) {
+      co_am = reinterpret_cast<unsigned*>(static_cast<char*>(ws) + x6w_part_bytes(g));
+      ci_am = co_am + c_out;
+      if (hipMemsetAsync(co_am, 0, ((size_t)c_out + c_in) * 4, st) != hipSuccess)
+        return launch_status("ds2_conv2d_wgrad");
+      const int64_t dpl = (int64_t)g.ho * g.wo, xpl = (int64_t)g.hi * g.wi;
+      const int cd = static_cast<int>(std::min<int64_t>(64, cdiv((int64_t)n * dpl, 16384)));
+      const int cx = static_cast<int>(std::min<int64_t>(64, cdiv((int64_t)n * xpl, 16384)));
+      hipLaunchKernelGGL(conv_h3_chamax_kernel, dim3(cd, c_out), dim3(256), 0, st, dy, n, c_out,
+                         dpl, co_am);
+      hipLaunchKernelGGL(conv_h3_chamax_kernel, dim3(cx, c_in), dim3(256), 0, st, x, n, c_in, xpl,
+                         ci_am);
+      hipLaunchKernelGGL((conv_x6_wgrad_sw_kernel<11, 3, 8, 2>), dim3(G * slabs), dim3(512), 0, st,
+                         dy, x, partial, g, slabs, co_am, ci_am);
+    } else if (x6w_sw(g))
       hipLaunchKernelGGL((conv_x6_wgrad_sw_kernel<11, 3, 8>), dim3(G * slabs), dim3(512), 0, st, dy,
-                         x, partial, g, slabs);
+                         x, partial, g, slabs, nullptr, nullptr);
     else
       hipLaunchKernelGGL((conv_x6_wgrad_kernel<11, 3>), dim3(G * slabs), dim3(CW_T), 0, st, dy, x,
                          partial, g, slabs);
@@ -2596,7 +2724,7 @@ ds2_status_t ds2_conv2d_wgrad(const float* dy, const float* x, float* dw, float*
     const int64_t blk = (int64_t)G * (X6W_BLOCK / 4 * nw) * kw;
     const int xg = static_cast<int>(std::min<int64_t>(cdiv(blk, 256), 2048));
     hipLaunchKernelGGL(wgrad_reduce_x6_kernel, dim3(xg), dim3(256), 0, st, partial, slabs, G, kw,
-                       nw, g, dw);
+                       nw, g, dw, co_am, ci_am);
   } else {
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(rg), dim3(256), 0, st, partial, slabs, per, dw);
   }

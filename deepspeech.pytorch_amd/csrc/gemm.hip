@@ -1423,7 +1423,16 @@ __global__ __launch_bounds__(256) void amax_rows_kernel(const float* __restrict_
   if (r >= rows) return;
   const f32x4* q = reinterpret_cast<const f32x4*>(p + (int64_t)r * ld);
   float m = 0.f;
-  for (int c = lane; c < cols / 4; c += 64) {
+  const int c4 = cols / 4;
+  int c = lane;
+  // 4 loads in flight per lane (a 4800-column row is 19 per lane)
+  for (; c + 192 < c4; c += 256) {
+    const f32x4 v0 = q[c], v1 = q[c + 64], v2 = q[c + 128], v3 = q[c + 192];
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      m = fmaxf(m, fmaxf(fmaxf(fabsf(v0[e]), fabsf(v1[e])), fmaxf(fabsf(v2[e]), fabsf(v3[e]))));
+  }
+  for (; c < c4; c += 64) {
     const f32x4 v = q[c];
     m = fmaxf(m, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
   }
@@ -1432,18 +1441,29 @@ __global__ __launch_bounds__(256) void amax_rows_kernel(const float* __restrict_
   if (lane == 0) out[r] = __builtin_bit_cast(unsigned, m);
 }
 
-// A logical row that is a stored column: a block covers 1024 columns (a float4 per thread) of
-// `rpb` stored rows and folds its maxima in with unsigned atomic max (non-negative float bits
-// order as unsigned; `out` zeroed first).
-__global__ __launch_bounds__(256) void amax_cols_kernel(const float* __restrict__ p, int rows,
+// Column maxima only (ds2_amax with row_amax NULL): one wave per block, a float4 column group
+// per lane, `rpb` rows per block with 8 loads in flight per lane, then one unsigned atomic max
+// per column (`out` zeroed first).
+__global__ __launch_bounds__(64) void amax_cols8_kernel(const float* __restrict__ p, int rows,
                                                         int cols, int64_t ld, int rpb,
                                                         unsigned* __restrict__ out) {
-  const int c = (blockIdx.x * 256 + threadIdx.x) * 4;
+  const int c = (blockIdx.x * 64 + threadIdx.x) * 4;
   if (c >= cols) return;
   const int r0 = blockIdx.y * rpb, r1 = min(rows, r0 + rpb);
+  const float* base = p + c;
   f32x4 m = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int r = r0; r < r1; ++r) {
-    const f32x4 v = *reinterpret_cast<const f32x4*>(p + (int64_t)r * ld + c);
+  int r = r0;
+  for (; r + 8 <= r1; r += 8) {
+    f32x4 v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = *reinterpret_cast<const f32x4*>(base + (int64_t)(r + i) * ld);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) m[e] = fmaxf(m[e], fabsf(v[i][e]));
+  }
+  for (; r < r1; ++r) {
+    const f32x4 v = *reinterpret_cast<const f32x4*>(base + (int64_t)r * ld);
 #pragma unroll
     for (int e = 0; e < 4; ++e) m[e] = fmaxf(m[e], fabsf(v[e]));
   }
@@ -1507,10 +1527,8 @@ static void launch_amax(const float* p, bool rowwise, int lrows, int k, int64_t 
     return;
   }
   (void)hipMemsetAsync(out, 0, (size_t)lrows * 4, st);
-  const int cb = cdiv(lrows, 1024);
-  const int rpb = std::max(16, cdiv((int64_t)k * cb, 1024));
-  hipLaunchKernelGGL(amax_cols_kernel, dim3(cb, cdiv(k, rpb)), dim3(256), 0, st, p, k, lrows, ld,
-                     rpb, out);
+  hipLaunchKernelGGL(amax_cols8_kernel, dim3(cdiv(lrows, 256), cdiv(k, 64)), dim3(64), 0, st, p, k,
+                     lrows, ld, 64, out);
 }
 
 }  // namespace ds2
@@ -1655,8 +1673,13 @@ extern "C" ds2_status_t ds2_amax(const float* x, int rows, int cols, int64_t ld,
                        ld, row_amax);
     return launch_status("ds2_amax");
   }
-  if (row_amax != nullptr) (void)hipMemsetAsync(row_amax, 0, (size_t)rows * 4, st);
   (void)hipMemsetAsync(col_amax, 0, (size_t)cols * 4, st);
+  if (row_amax == nullptr) {            // columns only: one wave per 256 columns x 64 rows
+    hipLaunchKernelGGL(amax_cols8_kernel, dim3(cdiv(cols, 256), cdiv(rows, 64)), dim3(64), 0, st,
+                       x, rows, cols, ld, 64, col_amax);
+    return launch_status("ds2_amax");
+  }
+  (void)hipMemsetAsync(row_amax, 0, (size_t)rows * 4, st);
   const int cb = cdiv(cols, 1024);
   const int rpb = std::min(64, std::max(16, cdiv((int64_t)rows * cb, 2048)));
   hipLaunchKernelGGL(amax_both_kernel, dim3(cb, cdiv(rows, rpb)), dim3(256), 0, st, x, rows, cols,

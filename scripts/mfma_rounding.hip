@@ -131,6 +131,23 @@ __global__ void window(float* out) {
   }
 }
 
+// Conversion rounding of the split code's packed converts (v_cvt_pk_f16_f32 /
+// v_cvt_pk_bf16_f32 via __builtin_convertvector) and the scalar casts: x = 1 + 0.75 ulp
+// (RNE: up, RZ / RD: down) and its negation, for fp16 (ulp 2^-10 at 1) and bf16 (ulp 2^-7)
+typedef float cvf2 __attribute__((ext_vector_type(2)));
+typedef _Float16 cvh2 __attribute__((ext_vector_type(2)));
+typedef __bf16 cvb2 __attribute__((ext_vector_type(2)));
+__global__ void convs(const float* in, float* out) {
+  if (threadIdx.x != 0) return;
+  const float xh = in[0], xb = in[1];
+  const cvh2 ph = __builtin_convertvector(cvf2{xh, -xh}, cvh2);
+  const cvb2 pb = __builtin_convertvector(cvf2{xb, -xb}, cvb2);
+  out[0] = (float)ph[0]; out[1] = (float)ph[1];
+  out[2] = (float)pb[0]; out[3] = (float)pb[1];
+  out[4] = (float)(_Float16)xh; out[5] = (float)(_Float16)(-xh);
+  out[6] = (float)(__bf16)xb; out[7] = (float)(__bf16)(-xb);
+}
+
 int main() {
   float* d;
   hipMalloc(&d, 64 * sizeof(float));
@@ -163,6 +180,24 @@ int main() {
   printf("T1: 0.125 = tiny kept (exact RNE), 0 = tiny dropped; T2: 0.125 = exact or floor, "
          "0.25 = tiny dropped toward zero\n");
   hipFree(w);
+  {
+    float hin[2] = {1.f + 0.75f * 0x1p-10f, 1.f + 0.75f * 0x1p-7f}, *din, *dout, hout[8];
+    hipMalloc(&din, sizeof(hin));
+    hipMalloc(&dout, sizeof(hout));
+    hipMemcpy(din, hin, sizeof(hin), hipMemcpyHostToDevice);
+    hipLaunchKernelGGL(convs, dim3(1), dim3(64), 0, 0, din, dout);
+    hipMemcpy(hout, dout, sizeof(hout), hipMemcpyDeviceToHost);
+    const char* cn[8] = {"pk f16 +", "pk f16 -", "pk bf16 +", "pk bf16 -", "cast f16 +",
+                         "cast f16 -", "cast bf16 +", "cast bf16 -"};
+    for (int i = 0; i < 8; ++i) {
+      const double ulp = i % 4 < 2 ? 0x1p-10 : 0x1p-7;
+      const double got = (i & 1) ? -(double)hout[i] : (double)hout[i];
+      printf("{\"convert\": \"%s\", \"|result| - 1 in ulps\": %.2f, \"RNE\": 1, \"RZ\": 0}\n",
+             cn[i], (got - 1.0) / ulp);
+    }
+    hipFree(din);
+    hipFree(dout);
+  }
   hipFree(d);
   return 0;
 }
