@@ -1131,22 +1131,20 @@ __device__ __forceinline__ f32x16 cx_mma(const bf16x8 (&a)[3], const bf16x8 (&b)
   }
 }
 
-// acc += a.b with the pair's products summed from zero and added into acc by VALU (RNE).  The
-// matrix cores floor each addend's bits below ~2^-31 of the largest operand of the instruction,
-// C included (scripts/mfma_rounding.hip, profiles/r5l_mfma_rounding.jsonl): chained into a
-// long accumulator, every MFMA loses a floor of ~2^-31 |C| -- a negative bias that sums of
-// the outputs (the BatchNorm parameter gradients after the conv block) amplify.  From a zero
-// C the window sits at the pair's own products.
-template <int NPL, bool FRESH>
-__device__ __forceinline__ void cx_mma_acc(const bf16x8 (&a)[3], const bf16x8 (&b)[3], f32x16& acc) {
-  if constexpr (FRESH) {
-    f32x16 z;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) z[r] = 0.f;
-    acc += cx_mma<NPL>(a, b, z);
-  } else {
-    acc = cx_mma<NPL>(a, b, acc);
-  }
+// acc += a.b, fp16x3 with the small products in their own chain: big += hi.hi, small +=
+// lo.hi + hi.lo.  The matrix cores floor (truncate toward -inf) each addend's bits below
+// ~2^-31 of the largest operand of the instruction, C included (scripts/mfma_rounding.hip,
+// profiles/r5n_mfma_rounding.txt).  Chained with hi.hi and a large C, every lo.hi product
+// lost its low bits to that floor: a small NEGATIVE bias per product that sums of the outputs
+// (the conv block's BatchNorm parameter gradients: 1.3 M nearly cancelling terms) amplify.  In
+// their own chain the small products keep every bit (their C stays ~2^-11 of the big one's);
+// the two sums meet by a VALU add (RNE).
+__device__ __forceinline__ void cx_mma_h3s(const bf16x8 (&a)[3], const bf16x8 (&b)[3], f32x16& big,
+                                           f32x16& small) {
+  typedef cf16x8 H;
+  small = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(H, a[1]), __builtin_bit_cast(H, b[0]), small, 0, 0, 0);
+  small = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(H, a[0]), __builtin_bit_cast(H, b[1]), small, 0, 0, 0);
+  big = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(H, a[0]), __builtin_bit_cast(H, b[0]), big, 0, 0, 0);
 }
 
 // a weight-image value's fp16x3 / bf16x6 terms (NPL planes, `per` apart from img[base])
@@ -1344,8 +1342,7 @@ __global__ void conv_x6_wimg_kernel(const float* __restrict__ w, ConvDims g, CxG
 // NPL 2: fp16x3 -- the patch is staged as fp16 hi / lo of x 2^e_n (e_n from the sample's
 // max |x|, n_amax[n]), the image holds w 2^m_exp[m], three products per fragment pair, and the
 // epilogue multiplies by 2^-(m_exp[m] + e_n) (exact) before the bias.
-template <bool DGRAD, int NGA, int NBP_, int PU, int SW, bool RCH, bool DB = false, int NPL = 3,
-          bool FRESH = false>
+template <bool DGRAD, int NGA, int NBP_, int PU, int SW, bool RCH, bool DB = false, int NPL = 3>
 __global__ __launch_bounds__(CX_T, 1) void conv_x6_kernel(const float* __restrict__ in,
                                                           const unsigned short* __restrict__ img,
                                                           const float* __restrict__ bias,
@@ -1469,11 +1466,11 @@ __global__ __launch_bounds__(CX_T, 1) void conv_x6_kernel(const float* __restric
     store_w();
   };
 
-  f32x16 acc[2];
+  f32x16 acc[2], acs[2];   // acs: fp16x3's small products (cx_mma_h3s)
 #pragma unroll
   for (int j = 0; j < 2; ++j)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+    for (int r = 0; r < 16; ++r) acc[j][r] = acs[j][r] = 0.f;
   const int nks = ngr * nbp;
   const int s_beg = kk == 0 ? 0 : (nks + 1) / 2;
   const int s_end = kk == 0 ? (nks + 1) / 2 : nks;
@@ -1490,16 +1487,6 @@ __global__ __launch_bounds__(CX_T, 1) void conv_x6_kernel(const float* __restric
     unsigned short* pnext = ps + ((l + 1) & 1) * NPL * PPL;
     bool staged = false;
     if (active) {
-      // FRESH: this channel's MFMA chain starts from zero C and joins acc by VALU (RNE), so
-      // the matrix cores' floor of addend bits below ~2^-31 of C (cx_mma_acc) acts at one
-      // channel's magnitude instead of the whole sum's
-      f32x16 tac[2];
-      if constexpr (FRESH) {
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) tac[j][r] = 0.f;
-      }
       auto kstep = [&](int st) {
         const int ga = st / nbp, p = st - (st / nbp) * nbp;
         const int b = 2 * p + fh;
@@ -1516,7 +1503,7 @@ __global__ __launch_bounds__(CX_T, 1) void conv_x6_kernel(const float* __restric
         }
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
-          if constexpr (FRESH) tac[j] = cx_mma<NPL>(af, bfr[j], tac[j]);
+          if constexpr (NPL == 2) cx_mma_h3s(af, bfr[j], acc[j], acs[j]);
           else acc[j] = cx_mma<NPL>(af, bfr[j], acc[j]);
         }
       };
@@ -1549,10 +1536,6 @@ __global__ __launch_bounds__(CX_T, 1) void conv_x6_kernel(const float* __restric
       } else {
         for (int st = s_beg; st < s_end; ++st) kstep(st);
       }
-      if constexpr (FRESH) {
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[j] += tac[j];
-      }
     }
     if (DB && !staged && l + 1 < LL) {
       store_patch(pnext);
@@ -1567,6 +1550,10 @@ __global__ __launch_bounds__(CX_T, 1) void conv_x6_kernel(const float* __restric
       }
       __syncthreads();
     }
+  }
+  if constexpr (NPL == 2) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[j] += acs[j];
   }
   // the two k halves meet in LDS (the patch area): half 1 writes, half 0 adds (fixed order)
   float* red = reinterpret_cast<float*>(ps);
@@ -2061,7 +2048,7 @@ __global__ void conv_x6q_wimg_kernel(const float* __restrict__ w, ConvDims g,
 // into the other buffer right after the k-steps of channel l, one barrier per channel.  The
 // patch gather offsets (and their bounds) are the same for every channel and are hoisted.
 // NPL 2: fp16x3, scales as conv_x6_kernel's (e_n from the sample's max |dy|, m = ci)
-template <bool DB, int NPL = 3, bool FRESH = false>
+template <bool DB, int NPL = 3>
 __global__ __launch_bounds__(CX_T, 1) void conv_x6q_dgrad_kernel(const float* __restrict__ dy,
                                                                  const unsigned short* __restrict__ img,
                                                                  float* __restrict__ dx, ConvDims g,
@@ -2154,11 +2141,11 @@ __global__ __launch_bounds__(CX_T, 1) void conv_x6q_dgrad_kernel(const float* __
     }
   };
 
-  f32x16 acc[2];
+  f32x16 acc[2], acs[2];   // acs: fp16x3's small products (cx_mma_h3s)
 #pragma unroll
   for (int j = 0; j < 2; ++j)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+    for (int r = 0; r < 16; ++r) acc[j][r] = acs[j][r] = 0.f;
   const int fr = lane & 31, fh = lane >> 5;
   const bool active = orow < out_h && c0 + 64 * cw < out_w;
   constexpr int H0 = (CQ_NK + 1) / 2;
@@ -2187,7 +2174,10 @@ __global__ __launch_bounds__(CX_T, 1) void conv_x6q_dgrad_kernel(const float* __
             bfr[j][pl] = *reinterpret_cast<const bf16x8*>(pc + pl * CQ_PPL + ap);
         }
 #pragma unroll
-        for (int j = 0; j < 2; ++j) cx_mma_acc<NPL, FRESH>(af, bfr[j], acc[j]);
+        for (int j = 0; j < 2; ++j) {
+          if constexpr (NPL == 2) cx_mma_h3s(af, bfr[j], acc[j], acs[j]);
+          else acc[j] = cx_mma<NPL>(af, bfr[j], acc[j]);
+        }
       };
       if (kk == 0) {
 #pragma unroll
@@ -2208,6 +2198,10 @@ __global__ __launch_bounds__(CX_T, 1) void conv_x6q_dgrad_kernel(const float* __
         __syncthreads();
       }
     }
+  }
+  if constexpr (NPL == 2) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[j] += acs[j];
   }
   // the two k halves meet in LDS (the patch area): half 1 writes, half 0 adds (fixed order)
   float* red = reinterpret_cast<float*>(ps);
@@ -2323,12 +2317,7 @@ static inline bool h3c_on() {
   const char* e = getenv("DS2_CONV_H3");
   return !(e != nullptr && e[0] == '0');
 }
-// fp16x3 conv kernels' per-k-step zero-C MFMA chains added by VALU (cx_mma_acc; default on,
-// DS2_CONV_FRESH=0 chains every MFMA into the running accumulator)
-static inline bool fresh_on() {
-  const char* e = getenv("DS2_CONV_FRESH");
-  return !(e != nullptr && e[0] == '0');
-}
+
 
 // workspace of a split-weight image of `elems` values per plane: NPL 3 planes, or 2 planes +
 // the fp16x3 scales (m_exp[M] int, n_amax[n] unsigned) at the next 256-B boundary
@@ -2381,12 +2370,8 @@ static ds2_status_t launch_x6q(const float* dy, const float* w, float* dx, const
     unsigned* n_amax;
     cx_h3_scales<true>(dy, w, g, total, ws, m_exp, n_amax, st);
     hipLaunchKernelGGL(conv_x6q_wimg_kernel<2>, dim3(wgrid), dim3(256), 0, st, w, g, img, m_exp);
-    if (fresh_on())
-      hipLaunchKernelGGL((conv_x6q_dgrad_kernel<true, 2, true>), dim3(static_cast<unsigned>(nwg)),
-                         dim3(CX_T), 0, st, dy, img, dx, g, gx, g.hi, m_exp, n_amax);
-    else
-      hipLaunchKernelGGL((conv_x6q_dgrad_kernel<true, 2>), dim3(static_cast<unsigned>(nwg)), dim3(CX_T),
-                         0, st, dy, img, dx, g, gx, g.hi, m_exp, n_amax);
+    hipLaunchKernelGGL((conv_x6q_dgrad_kernel<true, 2>), dim3(static_cast<unsigned>(nwg)), dim3(CX_T),
+                       0, st, dy, img, dx, g, gx, g.hi, m_exp, n_amax);
   } else {
     hipLaunchKernelGGL(conv_x6q_wimg_kernel<3>, dim3(wgrid), dim3(256), 0, st, w, g, img, nullptr);
     hipLaunchKernelGGL((conv_x6q_dgrad_kernel<true, 3>), dim3(static_cast<unsigned>(nwg)), dim3(CX_T),
@@ -2439,12 +2424,8 @@ static ds2_status_t launch_x6(const float* in, const float* w, const float* bias
     unsigned* n_amax;
     cx_h3_scales<DGRAD>(in, w, g, total, ws, m_exp, n_amax, st);
     hipLaunchKernelGGL((conv_x6_wimg_kernel<DGRAD, 2>), dim3(wgrid), dim3(256), 0, st, w, g, c, img, m_exp);
-    if (fresh_on())
-      hipLaunchKernelGGL((conv_x6_kernel<DGRAD, 3, 6, 2, 1, false, true, 2, true>), grid, dim3(CX_T), 0,
-                         st, in, img, bias, out, g, out_lens, c, gx, gy, m_exp, n_amax);
-    else
-      hipLaunchKernelGGL((conv_x6_kernel<DGRAD, 3, 6, 2, 1, false, true, 2>), grid, dim3(CX_T), 0, st,
-                         in, img, bias, out, g, out_lens, c, gx, gy, m_exp, n_amax);
+    hipLaunchKernelGGL((conv_x6_kernel<DGRAD, 3, 6, 2, 1, false, true, 2>), grid, dim3(CX_T), 0, st,
+                       in, img, bias, out, g, out_lens, c, gx, gy, m_exp, n_amax);
     return launch_status("ds2_conv2d_fwd");
   }
   hipLaunchKernelGGL((conv_x6_wimg_kernel<DGRAD, 3>), dim3(wgrid), dim3(256), 0, st, w, g, c, img, nullptr);

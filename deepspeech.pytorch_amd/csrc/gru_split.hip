@@ -894,33 +894,36 @@ __global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
       for (int p = 0; p < NPW; ++p) {
         if (p + LWP < NPW) load_rec(p + LWP);
         if (p < np) {
-          f32x4 tmp = f32x4{0.f, 0.f, 0.f, 0.f};
+          // big (hi.hi) and small (lo.hi + hi.lo) products in separate zero-C chains, and the
+          // 16x16x16 n-gate products apart from the 16x16x32 ones (see mma3h; a 16x16x16 MFMA
+          // taking a 16x16x32 result as srcC back to back also got rows 0-1 of every 4 wrong
+          // on gfx950: hipcc 7.2 inserts no wait states between the two opcodes)
+          const f32x4 z4 = f32x4{0.f, 0.f, 0.f, 0.f};
+          f32x4 tb = z4, ts = z4;
           if constexpr (NG >= 3) {
             const f16x8 ahi = __builtin_bit_cast(f16x8, r0[p]);
             const f16x8 alo = __builtin_bit_cast(f16x8, r1[p]);
-            tmp = __builtin_amdgcn_mfma_f32_16x16x32_f16(alo, wrz[p].hi, tmp, 0, 0, 0);
-            tmp = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, wrz[p].lo, tmp, 0, 0, 0);
-            tmp = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, wrz[p].hi, tmp, 0, 0, 0);
+            ts = __builtin_amdgcn_mfma_f32_16x16x32_f16(alo, wrz[p].hi, ts, 0, 0, 0);
+            ts = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, wrz[p].lo, ts, 0, 0, 0);
+            tb = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, wrz[p].hi, tb, 0, 0, 0);
           }
           if constexpr (NG == 4) {
             const f16x8 bhi = __builtin_bit_cast(f16x8, r2[p]);
             const f16x8 blo = __builtin_bit_cast(f16x8, r3[p]);
-            tmp = __builtin_amdgcn_mfma_f32_16x16x32_f16(blo, wgo[p].hi, tmp, 0, 0, 0);
-            tmp = __builtin_amdgcn_mfma_f32_16x16x32_f16(bhi, wgo[p].lo, tmp, 0, 0, 0);
-            tmp = __builtin_amdgcn_mfma_f32_16x16x32_f16(bhi, wgo[p].hi, tmp, 0, 0, 0);
+            ts = __builtin_amdgcn_mfma_f32_16x16x32_f16(blo, wgo[p].hi, ts, 0, 0, 0);
+            ts = __builtin_amdgcn_mfma_f32_16x16x32_f16(bhi, wgo[p].lo, ts, 0, 0, 0);
+            tb = __builtin_amdgcn_mfma_f32_16x16x32_f16(bhi, wgo[p].hi, tb, 0, 0, 0);
           }
           if constexpr (NG != 4) {
-            // its own accumulator: a 16x16x16 MFMA taking a 16x16x32 MFMA's result as srcC
-            // back to back got rows 0-1 of every 4 wrong on gfx950 (hipcc 7.2 inserts no wait
-            // states between the two opcodes; scripts/gru_bwd_h3_debug.py)
             const f16x4 nh = __builtin_bit_cast(f16x4, u32x2{r2[p][0], r2[p][1]});
             const f16x4 nl = __builtin_bit_cast(f16x4, u32x2{r2[p][2], r2[p][3]});
-            f32x4 tn = f32x4{0.f, 0.f, 0.f, 0.f};
-            tn = __builtin_amdgcn_mfma_f32_16x16x16f16(nl, wnh[p], tn, 0, 0, 0);
-            tn = __builtin_amdgcn_mfma_f32_16x16x16f16(nh, wnl[p], tn, 0, 0, 0);
-            tn = __builtin_amdgcn_mfma_f32_16x16x16f16(nh, wnh[p], tn, 0, 0, 0);
-            tmp += tn;
+            f32x4 ns = __builtin_amdgcn_mfma_f32_16x16x16f16(nl, wnh[p], z4, 0, 0, 0);
+            ns = __builtin_amdgcn_mfma_f32_16x16x16f16(nh, wnl[p], ns, 0, 0, 0);
+            const f32x4 nb = __builtin_amdgcn_mfma_f32_16x16x16f16(nh, wnh[p], z4, 0, 0, 0);
+            tb += nb;
+            ts += ns;
           }
+          const f32x4 tmp = tb + ts;
           acc += tmp * rs[p];   // rows 4 (lane >> 4) + i: the producer's 2^-e of those rows
         }
       }
@@ -1163,6 +1166,263 @@ __global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
 #pragma unroll
     for (int mm = 0; mm < GB; ++mm) a += rd[(g * GB + mm) * GU + uu];
     dbp[(((int64_t)bt * D + d) * 4 + g) * H + ub * GU + uu] = a;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// LSTM backward for cfg4's bf16 mode (BASELINE cfg4: "bf16 MFMA RNN GEMMs"; opt-in, the
+// model's rnn_gemm_precision='bf16'): the W_hh^T product with ONE fp16 term per operand
+// (per-row scaled gate gradients, per-column scaled W_hh^T, 11 significant bits each instead of
+// 22), so a producer's record per 16-sample tile is 2 KB and a workgroup takes 32 samples:
+// cfg4's batch 64 runs as ONE launch of 2 x 2 x 64 = 256 workgroups instead of two 16-sample
+// chunk launches.  Record per producer and step: [b][(i, f) hi 1 KB, (g, o) hi 1 KB] for the
+// two 16-sample tiles b, then 32 row factors 2^-e (4224 B).  Flag hand-off and groups as
+// gru_bwd_h3_kernel; `c_all` / `gates` / `dg` as ds2_lstm_bwd.
+constexpr int L1B = 32;        // samples per workgroup
+constexpr int HBL1 = 1056;     // floats per producer record (2 x 512 + 32)
+template <int NPW>
+__global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(2, 2))) void lstm_bwd_h1_kernel(
+    int T, int N, int H, int D, int UB, int BT, const float* __restrict__ dy, int dyd,
+    const float* __restrict__ w_f, const float* __restrict__ w_r,
+    const float* __restrict__ c_all, const float* __restrict__ gates,
+    const int* __restrict__ lens, float* __restrict__ dg, float* __restrict__ gx,
+    unsigned* __restrict__ counters, unsigned* __restrict__ err, int xmode,
+    unsigned* __restrict__ camax) {
+  static_assert(NPW <= 8, "producers per wave");
+  static_assert(BW * 64 == L1B * GU, "one thread per (sample, unit)");
+  constexpr int RP = GU + 1;
+  constexpr int LWP = NPW < 2 ? NPW : 2;       // producers' records in flight per wave
+  __shared__ __attribute__((aligned(8))) float red[BW * L1B * RP];
+  __shared__ __attribute__((aligned(16))) _Float16 stg[4 * 512];   // the record published
+  __shared__ __attribute__((aligned(16))) float stsc[L1B];
+  __shared__ int flag;
+  int ub, d, bt;
+  const bool xg = xmode != 0;
+  if (xg ? !map_work_xgrp(UB, BT, D, ub, d, bt) : !map_work(UB * D, BT, UB, ub, d, bt)) return;
+  const int n0 = bt * L1B;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int H4 = 4 * H;
+  unsigned* xtab = counters + (D * BT + 1) + D * BT * 64 + (d * BT + bt) * 64;
+  const unsigned my_xcc = xcc_id() + 1u;
+  if (xg && threadIdx.x == 0)
+    __hip_atomic_store(xtab + ub, my_xcc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  uint32_t psame = 0;
+  const int p0 = (UB * wave) / BW;
+  const int np = (UB * (wave + 1)) / BW - p0;      // host guarantees np <= NPW
+  const unsigned* gflags = counters + (D * BT + 1) + (d * BT + bt) * UB;
+  unsigned* myflag = counters + (D * BT + 1) + (d * BT + bt) * UB + ub;
+  const int slot_floats = D * BT * UB * HBL1;
+  const __amdgpu_buffer_rsrc_t x_rs = __builtin_amdgcn_make_buffer_rsrc(
+      gx, (short)0, (xg ? 4 : 2) * slot_floats * 4, 0x00020000);
+  const int grp_off = (d * BT + bt) * UB * HBL1;
+  const int aoff = 2 * slot_floats * 4;   // the plain-store copies (xmode)
+
+  // W_hh^T fragments of producer p, lane (u = lane & 15, q = lane >> 4), hi terms only:
+  // slot j -> W_hh[(g0 + (j >> 2)) H + 16 pb + 4 q + (j & 3)][16 ub + u], g0 = 0 (i, f) / 2 (g, o)
+  f16x8 wif[NPW], wgo[NPW];
+  float unscale = 1.f;   // 2^-e(u) of the owner's unit (threadIdx.x & 15 = lane & 15)
+  {
+    const float* W = d == 0 ? w_f : w_r;
+    const float* wc = W + ub * GU + (lane & 15);
+    const int q4 = 4 * (lane >> 4);
+    auto wv = [&](int g, int p, int j) {
+      return p < np ? wc[(int64_t)(g * H + 16 * (p0 + p) + q4 + j) * H] : 0.f;
+    };
+    float mx = 0.f;
+#pragma unroll
+    for (int p = 0; p < NPW; ++p)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) mx = fmaxf(mx, fabsf(wv(g, p, j)));
+    mx = fmaxf(mx, __shfl_xor(mx, 16));
+    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    if (lane < 16) red[wave * 16 + lane] = mx;
+    __syncthreads();
+    float m = 0.f;
+#pragma unroll
+    for (int w8 = 0; w8 < BW; ++w8) m = fmaxf(m, red[w8 * 16 + (lane & 15)]);
+    const int eu = h3_row_exp(m);
+    unscale = __builtin_ldexpf(1.f, -eu);
+    const float sc = __builtin_ldexpf(1.f, eu);
+    __syncthreads();
+#pragma unroll
+    for (int p = 0; p < NPW; ++p)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        wif[p][j] = (_Float16)(wv(j >> 2, p, j & 3) * sc);
+        wgo[p][j] = (_Float16)(wv(2 + (j >> 2), p, j & 3) * sc);
+      }
+  }
+  const int m = threadIdx.x >> 4;        // sample of the workgroup (0 .. 31)
+  const int u = threadIdx.x & 15;
+  const int n = n0 + m;
+  const int j = ub * GU + u;
+  const bool owner = n < N;
+  int len = owner ? lens[n] : 0;
+  settle(len);
+  // this thread's slots in the staged record: tile b = m >> 4, consumer lane (m & 15) + 16 (u >> 2)
+  const int sL = (m >> 4) * 1024 + ((m & 15) + 16 * (u >> 2)) * 8 + (u & 3);
+  float dc_carry = 0.f;
+  float p_i = 0.f, p_f = 0.f, p_g = 0.f, p_o = 0.f;
+  int64_t px_row = -1;
+  float cm_i = 0.f, cm_f = 0.f, cm_g = 0.f, cm_o = 0.f;
+  for (int s = 0; s < T; ++s) {
+    const int t = d == 0 ? T - 1 - s : s;
+    f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+    float dyv = 0.f, gi = 0.f, gf = 0.f, gg = 0.f, go = 0.f, ct = 0.f, cp = 0.f;
+    const int64_t row = ((int64_t)t * N + n) * D + d;
+    if (owner && t < len) {
+      dyv = dy[(((int64_t)t * N + n) * dyd + (dyd > 1 ? d : 0)) * H + j];
+      const float* gp = gates + row * 4 * H;
+      gi = gp[j];
+      gf = gp[H + j];
+      gg = gp[2 * H + j];
+      go = gp[3 * H + j];
+      ct = c_all[row * H + j];
+      const int tp = d == 0 ? t - 1 : t + 1;
+      if (tp >= 0 && tp < T) cp = c_all[(((int64_t)tp * N + n) * D + d) * H + j];
+    }
+    if (s > 0) {
+      if (!flags_wait(gflags, UB, (unsigned)s, err, &flag)) {
+        poison_rest(dg, s, T, d == 0, N, D, n, d, H, j, H4, 4, owner);
+        return;
+      }
+      if (xg && s == 1) {
+        const unsigned v = lane < UB ? __hip_atomic_load(xtab + lane, __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT) : 0u;
+        const unsigned long long same = __ballot(v == my_xcc);
+#pragma unroll
+        for (int p = 0; p < NPW; ++p)
+          if ((same >> (p0 + p)) & 1ull) psame |= 1u << p;
+      }
+      const int rb = ((s - 1) & 1) * slot_floats + grp_off;
+      u32x4 ra[NPW][2], rg[NPW][2];
+      f32x4 rs[NPW][2];
+      auto load_rec = [&](int p) {
+        const bool ok = p < np;
+        const int base = (rb + (p0 + p) * HBL1) * 4 + (((psame >> p) & 1u) ? aoff : 0);
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          ra[p][b] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                   x_rs, ok ? base + b * 2048 + lane * 16 : 0x7ffffff0, 0, kSc1));
+          rg[p][b] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                   x_rs, ok ? base + b * 2048 + 1024 + lane * 16 : 0x7ffffff0, 0, kSc1));
+          rs[p][b] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                   x_rs, ok ? base + 4096 + b * 64 + (lane >> 4) * 16 : 0x7ffffff0, 0, kSc1));
+        }
+      };
+#pragma unroll
+      for (int p = 0; p < LWP; ++p) load_rec(p);
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int p = 0; p < NPW; ++p) {
+        if (p + LWP < NPW) load_rec(p + LWP);
+        if (p < np) {
+#pragma unroll
+          for (int b = 0; b < 2; ++b) {
+            f32x4 tb = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, ra[p][b]), wif[p],
+                                                              f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+            tb = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, rg[p][b]), wgo[p], tb, 0, 0, 0);
+            acc[b] += tb * rs[p][b];
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        red[(wave * L1B + b * GB + (lane >> 4) * 4 + r) * RP + (lane & 15)] = acc[b][r];
+    settle(dyv);
+    settle(gi);
+    settle(gf);
+    settle(gg);
+    settle(go);
+    settle(ct);
+    settle(cp);
+    __syncthreads();
+    float dai = 0.f, daf = 0.f, dag = 0.f, dao = 0.f;
+    if (owner) {
+      if (t < len) {
+        float rec = 0.f;
+        if (s > 0) {
+#pragma unroll
+          for (int w8 = 0; w8 < BW; ++w8) rec += red[(w8 * L1B + m) * RP + u];
+        }
+        const float tc = tanh_fast(ct);
+        const float dh = dyv + rec * unscale;
+        const float dc = dc_carry + dh * go * (1.f - tc * tc);
+        dao = dh * tc * go * (1.f - go);
+        dai = dc * gg * gi * (1.f - gi);
+        dag = dc * gi * (1.f - gg * gg);
+        daf = dc * cp * gf * (1.f - gf);
+        dc_carry = dc * gf;
+      } else {
+        dc_carry = 0.f;
+      }
+      p_i = dai; p_f = daf; p_g = dag; p_o = dao; px_row = row;
+      cm_i = fmaxf(cm_i, fabsf(dai));
+      cm_f = fmaxf(cm_f, fabsf(daf));
+      cm_g = fmaxf(cm_g, fabsf(dag));
+      cm_o = fmaxf(cm_o, fabsf(dao));
+    }
+    {
+      // the row's scale: max over the sample's 16 units x 4 gates (16 consecutive lanes)
+      float mx = fmaxf(fmaxf(fabsf(dai), fabsf(daf)), fmaxf(fabsf(dag), fabsf(dao)));
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+      const int e = h3_row_exp(mx);
+      const float sc = __builtin_ldexpf(1.f, e);
+      stg[sL] = (_Float16)(dai * sc);
+      stg[sL + 4] = (_Float16)(daf * sc);
+      stg[sL + 512] = (_Float16)(dag * sc);
+      stg[sL + 516] = (_Float16)(dao * sc);
+      if (u == 0) stsc[m] = __builtin_ldexpf(1.f, -e);
+    }
+    __syncthreads();
+    if (wave == 0) {
+      const int so = ((s & 1) * slot_floats + grp_off + ub * HBL1) * 4;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const u32x4 v = *reinterpret_cast<const u32x4*>(stg + k * 512 + lane * 8);
+        __builtin_amdgcn_raw_buffer_store_b128(v, x_rs, so + k * 1024 + lane * 16, 0, kSc1);
+        if (xg) __builtin_amdgcn_raw_buffer_store_b128(v, x_rs, aoff + so + k * 1024 + lane * 16, 0, 0);
+      }
+      if (lane < 8) {
+        const u32x4 vs = *reinterpret_cast<const u32x4*>(stsc + lane * 4);
+        __builtin_amdgcn_raw_buffer_store_b128(vs, x_rs, so + 4096 + lane * 16, 0, kSc1);
+        if (xg) __builtin_amdgcn_raw_buffer_store_b128(vs, x_rs, aoff + so + 4096 + lane * 16, 0, 0);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0)
+        __hip_atomic_store(myflag, (unsigned)s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (owner) {
+      float* gr = dg + px_row * H4;
+      gr[j] = p_i;
+      gr[H + j] = p_f;
+      gr[2 * H + j] = p_g;
+      gr[3 * H + j] = p_o;
+    }
+  }
+  if (camax == nullptr) return;
+  // column maxima of dg [T N][D 4H]: the 32 samples' running maxima per (gate, unit)
+  __syncthreads();
+  red[(0 * L1B + m) * GU + u] = cm_i;
+  red[(1 * L1B + m) * GU + u] = cm_f;
+  red[(2 * L1B + m) * GU + u] = cm_g;
+  red[(3 * L1B + m) * GU + u] = cm_o;
+  __syncthreads();
+  if (threadIdx.x < 4 * GU) {
+    const int g = threadIdx.x / GU, uu = threadIdx.x - (threadIdx.x / GU) * GU;
+    float a = 0.f;
+#pragma unroll
+    for (int mm = 0; mm < L1B; ++mm) a = fmaxf(a, red[(g * L1B + mm) * GU + uu]);
+    const unsigned bits = __float_as_uint(a);
+    if (bits != 0u) atomicMax(camax + d * H4 + g * H + ub * GU + uu, bits);
   }
 }
 
@@ -1410,6 +1670,48 @@ size_t h3_bwd_ring_bytes(int n_tiles, int h, int num_dirs, int ng) {
   const size_t UB = (h + GU - 1) / GU;
   const size_t hb = ng == 4 ? HBR4 : (ng == 3 ? HBR : HBR1);
   return 4 * (size_t)num_dirs * n_tiles * UB * hb * sizeof(float);
+}
+
+// the single-term LSTM backward (cfg4's bf16 mode): one launch over ceil(n / 32) 32-sample
+// tiles; false = not covered
+static const void* lstm_bwd_h1_fn(int UB) {
+  const int need = (UB + BW - 1) / BW;
+#define DS2_L1(K) \
+  if (need <= K) return reinterpret_cast<const void*>(lstm_bwd_h1_kernel<K>);
+  DS2_L1(1) DS2_L1(2) DS2_L1(4) DS2_L1(8)
+#undef DS2_L1
+  return nullptr;
+}
+
+int lstm_h1_grid(int n, int h, int num_dirs) {
+  if ((h % GU) != 0) return -1;
+  const int UB = h / GU, BT = (n + L1B - 1) / L1B;
+  if (lstm_bwd_h1_fn(UB) == nullptr) return -1;
+  return xcd_groups(UB, BT, num_dirs) ? xgrp_grid(UB, BT, num_dirs) : mapped_grid(UB * num_dirs, BT);
+}
+
+size_t lstm_h1_ring_bytes(int n, int h, int num_dirs) {
+  const size_t UB = (h + GU - 1) / GU, BT = (n + L1B - 1) / L1B;
+  return 4 * (size_t)num_dirs * BT * UB * HBL1 * sizeof(float);
+}
+
+bool launch_lstm_bwd_h1(int t_max, int n, int h, int num_dirs, const float* dy, int dy_dirs,
+                        const float* w_hh_f, const float* w_hh_r, const float* c_all,
+                        const float* gates, const int* lens, float* dgates, float* ring,
+                        unsigned* ctrs, unsigned* err, size_t lds_pad, hipStream_t st,
+                        unsigned* camax) {
+  if ((h % GU) != 0) return false;
+  apply_spin_limit_env();
+  apply_rnn_tune_env();
+  const int UB = h / GU, BT = (n + L1B - 1) / L1B;
+  const void* fn = lstm_bwd_h1_fn(UB);
+  if (fn == nullptr) return false;
+  int XM_ = xcd_groups(UB, BT, num_dirs) ? 1 : 0;
+  const int grid = XM_ ? xgrp_grid(UB, BT, num_dirs) : mapped_grid(UB * num_dirs, BT);
+  int T_ = t_max, N_ = n, H_ = h, D_ = num_dirs, UB_ = UB, BT_ = BT, DYD_ = dy_dirs;
+  void* args[] = {&T_, &N_, &H_, &D_, &UB_, &BT_, &dy, &DYD_, &w_hh_f, &w_hh_r, &c_all,
+                  &gates, &lens, &dgates, &ring, &ctrs, &err, &XM_, &camax};
+  return rnn_launch(fn, dim3(grid), dim3(BW * 64), args, lds_pad, st) == hipSuccess;
 }
 
 }  // namespace ds2

@@ -810,6 +810,14 @@ bool launch_lstm_bwd_h3(int t_max, int n, int h, int num_dirs, const float* dy, 
                         unsigned* ctrs, unsigned* err, size_t lds_pad, hipStream_t st,
                         unsigned* camax, int tile0, int bt_launch);
 size_t h3_bwd_ring_bytes(int n_tiles, int h, int num_dirs, int ng);
+// gru_split.hip: the single-term backward of cfg4's bf16 mode (lstm_bwd_h1_kernel)
+int lstm_h1_grid(int n, int h, int num_dirs);
+size_t lstm_h1_ring_bytes(int n, int h, int num_dirs);
+bool launch_lstm_bwd_h1(int t_max, int n, int h, int num_dirs, const float* dy, int dy_dirs,
+                        const float* w_hh_f, const float* w_hh_r, const float* c_all,
+                        const float* gates, const int* lens, float* dgates, float* ring,
+                        unsigned* ctrs, unsigned* err, size_t lds_pad, hipStream_t st,
+                        unsigned* camax);
 
 }  // namespace ds2
 
@@ -1013,8 +1021,56 @@ static size_t lstm_bwd_ws_base(int n, int h, int num_dirs) {
 
 size_t ds2_lstm_bwd_workspace_size(int n, int h, int num_dirs) {
   if (n < 1 || h < 1 || num_dirs < 1) return 256;
+  const size_t r3 = h3_bwd_ring_bytes((n + GB - 1) / GB, h, num_dirs, 4);
+  const size_t r1 = lstm_h1_ring_bytes(n, h, num_dirs);
   return lstm_bwd_ws_base(n, h, num_dirs) + lstm_h3_ctr_bytes(n, num_dirs) +
-         align256(h3_bwd_ring_bytes((n + GB - 1) / GB, h, num_dirs, 4)) + 256;
+         align256(r3 > r1 ? r3 : r1) + 256;
+}
+
+// the single-term backward (cfg4's bf16 mode) as launched: its grid, 0 when it declines
+static int lstm_h1_launch_grid(int t_max, int n, int h, int num_dirs) {
+  if (!persistent_enabled() || (h % GU) != 0) return 0;
+  if ((int64_t)t_max * n * num_dirs * 4 * h * 4 >= (1ll << 31)) return 0;
+  const int g = lstm_h1_grid(n, h, num_dirs);
+  return g > 0 && g <= num_cus() ? g : 0;
+}
+
+int ds2_lstm_bwd_half_grid(int n, int h, int num_dirs) {
+  if (n < 1 || h < 1 || (num_dirs != 1 && num_dirs != 2)) return 0;
+  const int g = lstm_h1_launch_grid(1, n, h, num_dirs);
+  return g > 0 ? g : ds2_lstm_bwd_grid(n, h, num_dirs);
+}
+
+ds2_status_t ds2_lstm_bwd_half(int t_max, int n, int h, int num_dirs, const float* dy, int dy_dirs,
+                               const float* w_hh_f, const float* w_hh_r, const float* c_all,
+                               const float* gates, const int* lens, float* dgates,
+                               unsigned* err_out, void* ws, size_t ws_bytes, ds2_stream_t stream) {
+  if (t_max < 0 || n < 0 || h < 1 || (num_dirs != 1 && num_dirs != 2)) return DS2_INVALID_VALUE;
+  if (t_max == 0 || n == 0) return DS2_OK;
+  if (gates == nullptr || c_all == nullptr) return DS2_INVALID_VALUE;
+  if (dy_dirs != 1 && dy_dirs != num_dirs) return DS2_INVALID_VALUE;
+  if (ws == nullptr || ws_bytes < ds2_lstm_bwd_workspace_size(n, h, num_dirs))
+    return DS2_WORKSPACE_TOO_SMALL;
+  if (lstm_h1_launch_grid(t_max, n, h, num_dirs) > 0) {
+    hipStream_t st = as_stream(stream);
+    apply_spin_limit_env();
+    char* base3 = static_cast<char*>(ws) + lstm_bwd_ws_base(n, h, num_dirs);
+    unsigned* ctrs3 = reinterpret_cast<unsigned*>(base3);
+    float* ring3 = reinterpret_cast<float*>(base3 + lstm_h3_ctr_bytes(n, num_dirs));
+    const int BT32 = (n + 31) / 32;
+    unsigned* err = ctrs3 + num_dirs * BT32;
+    if (hipMemsetAsync(ctrs3, 0, lstm_h3_ctr_bytes(n, num_dirs), st) != hipSuccess)
+      return launch_status("ds2_lstm counters");
+    if (launch_lstm_bwd_h1(t_max, n, h, num_dirs, dy, dy_dirs, w_hh_f,
+                           num_dirs == 2 ? w_hh_r : w_hh_f, c_all, gates, lens, dgates, ring3,
+                           ctrs3, err, kLstmDopPadLds, st, nullptr)) {
+      fold_err(err, err_out, st);
+      return launch_status("ds2_lstm_bwd_half");
+    }
+    (void)hipGetLastError();
+  }
+  return ds2_lstm_bwd(t_max, n, h, num_dirs, dy, dy_dirs, w_hh_f, w_hh_r, c_all, gates, lens,
+                      dgates, err_out, ws, ws_bytes, stream);
 }
 
 // the fp16x3 backward's launch: 16-sample tiles per launch (consecutive launches cover the

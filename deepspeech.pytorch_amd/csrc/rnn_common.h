@@ -463,7 +463,14 @@ __device__ __forceinline__ Duo split2h(const f32x4 a, const f32x4 b, float sc) {
   return t;
 }
 
-// c += a.b from the fp16 terms (small terms first)
+// c += a.b from the fp16 terms in one MFMA chain (small terms first): the forward
+// recurrences' form.  The matrix cores floor an addend's bits below ~2^-31 of the largest
+// operand of one instruction, C included (scripts/mfma_rounding.hip), so the small products
+// chained beside hi.hi lose their lowest bits downward: ~1e-7 relative per result, which the
+// forward's state update does not sum up (the backward kernels, whose gate gradients feed the
+// bias-gradient sums, keep the small products in a chain of their own).  Splitting the chains
+// here cost the GRU forward 1.95 -> 2.32 ms per launch (the join is a VALU add on the
+// critical path of every hand-off step).
 __device__ __forceinline__ f32x4 mma3h(const Duo& a, const Duo& b, f32x4 c) {
   c = __builtin_amdgcn_mfma_f32_16x16x32_f16(a.lo, b.hi, c, 0, 0, 0);
   c = __builtin_amdgcn_mfma_f32_16x16x32_f16(a.hi, b.lo, c, 0, 0, 0);

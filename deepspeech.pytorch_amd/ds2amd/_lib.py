@@ -107,6 +107,9 @@ _PROTOS = {
     "ds2_lstm_bwd_workspace_size": (_sz, [_c_int, _c_int, _c_int]),
     "ds2_lstm_bwd": (_c_int, [_c_int, _c_int, _c_int, _c_int, _vp, _c_int, _vp, _vp, _vp, _vp,
                               _vp, _vp, _vp, _vp, _sz, _vp]),
+    "ds2_lstm_bwd_half_grid": (_c_int, [_c_int, _c_int, _c_int]),
+    "ds2_lstm_bwd_half": (_c_int, [_c_int, _c_int, _c_int, _c_int, _vp, _c_int, _vp, _vp, _vp,
+                                   _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
     "ds2_lookahead_fwd": (_c_int, [_vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_f,
                                    _c_f, _vp, _vp]),
     "ds2_lookahead_bwd_workspace_size": (_sz, [_c_int, _c_int, _c_int, _c_int]),

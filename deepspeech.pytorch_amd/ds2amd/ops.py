@@ -961,7 +961,8 @@ def persistent_bwd_grid(cell: str, n: int, h: int, nd: int) -> int:
     """Workgroups the persistent backward recurrence of this shape holds at once, as the
     library will launch it (ds2_gru_bwd_grid / ds2_lstm_bwd_grid / ds2_rnn_bwd_grid; 0 for the per-step
     kernels, which need no co-residency)."""
-    fn = {"gru": "ds2_gru_bwd_grid", "lstm": "ds2_lstm_bwd_grid", "rnn": "ds2_rnn_bwd_grid"}[cell]
+    fn = {"gru": "ds2_gru_bwd_grid", "lstm": "ds2_lstm_bwd_grid", "rnn": "ds2_rnn_bwd_grid",
+          "lstm_half": "ds2_lstm_bwd_half_grid"}[cell]
     return _lib.size(fn, n, h, nd)
 
 
@@ -1130,8 +1131,11 @@ class LSTMLayerFn(torch.autograd.Function):
         w_hh_f = weights[1]
         w_hh_r = weights[5] if nd == 2 else None
         ws = _ws(_lib.size("ds2_lstm_bwd_workspace_size", n, h, nd), dev)
-        _guard_cooperative("lstm", n, h, nd)
-        _lib.call("ds2_lstm_bwd", t, n, h, nd, dy.data_ptr(), dy_dirs, w_hh_f.data_ptr(),
+        # bf16 mode (BASELINE cfg4): the recurrence's W_hh^T product on one fp16 term too
+        half = bf16 and os.environ.get("DS2_LSTM_HALF", "1")[:1] != "0"
+        _guard_cooperative("lstm_half" if half else "lstm", n, h, nd)
+        _lib.call("ds2_lstm_bwd_half" if half else "ds2_lstm_bwd", t, n, h, nd, dy.data_ptr(),
+                  dy_dirs, w_hh_f.data_ptr(),
                   _p(w_hh_r), c_all.data_ptr(), gates.data_ptr(), lens.data_ptr(), dg.data_ptr(),
                   rnn_status_word(dev).data_ptr(), ws.data_ptr(), ws.numel(), _stream())
         dx, grads = _rnn_param_grads(x, h_all, dg, dg, weights, nd, 4 * h,

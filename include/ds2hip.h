@@ -309,6 +309,17 @@ ds2_status_t ds2_lstm_bwd(int t_max, int n, int h, int num_dirs, const float* dy
                           const float* w_hh_f, const float* w_hh_r, const float* c_all,
                           const float* gates, const int* lens, float* dgates, unsigned* err_out,
                           void* ws, size_t ws_bytes, ds2_stream_t stream);
+/* ds2_lstm_bwd for BASELINE cfg4's opt-in bf16 mode (rnn_gemm_precision='bf16'): the W_hh^T
+ * product of the backward recurrence on ONE fp16 term per operand (per-row scaled gate
+ * gradients, per-column scaled W_hh^T: 11 significant bits each), so a workgroup takes 32
+ * samples and cfg4's batch 64 runs as one launch.  Same arguments and workspace as
+ * ds2_lstm_bwd, which it falls back to where it declines the shape.
+ * ds2_lstm_bwd_half_grid: workgroups that launch holds at once.                          */
+int ds2_lstm_bwd_half_grid(int n, int h, int num_dirs);
+ds2_status_t ds2_lstm_bwd_half(int t_max, int n, int h, int num_dirs, const float* dy, int dy_dirs,
+                               const float* w_hh_f, const float* w_hh_r, const float* c_all,
+                               const float* gates, const int* lens, float* dgates,
+                               unsigned* err_out, void* ws, size_t ws_bytes, ds2_stream_t stream);
 
 /* ------------------------------------------------------------------------ */
 /* Lookahead convolution, ref model.py:140-177 (Lookahead.forward), optionally

@@ -5,8 +5,8 @@ BatchNorm's backward, zero-mean per channel), so per-element errors that share a
 the sum while random ones cancel.
 
 For conv2's shape (32 -> 32 channels, 21 x 11 taps, stride (2, 1)) at a reduced batch this
-prints, per kernel mode (h3: fp16x3 with zero-C MFMA chains per channel / k-step; h3-chain:
-DS2_CONV_FRESH=0; x6; fp32 -- DS2_CONV_H3 / DS2_CONV_X6) and direction (forward
+prints, per kernel mode (h3: fp16x3, its small products in their own MFMA chain; x6: bf16x6;
+fp32 -- DS2_CONV_H3 / DS2_CONV_X6) and direction (forward
 y, dgrad dx), the max elementwise error relative to max |ref| and the per-channel SUM error
 relative to the channel's sum of |ref|, against an fp64 torch reference on the same fp32
 inputs.  dy is made zero-mean per channel, as a BatchNorm backward leaves it.
@@ -39,10 +39,9 @@ def main():
     dy = (dy - dy.mean((0, 2, 3), keepdim=True)).float()
     dx64 = torch.nn.grad.conv2d_input(x.shape, wt.double(), dy.double(), stride=(sh, sw),
                                       padding=(ph, pw))
-    for mode in ("h3", "h3-chain", "x6", "fp32"):
+    for mode in ("h3", "x6", "fp32"):
         os.environ["DS2_CONV_X6"] = "0" if mode == "fp32" else "1"
-        os.environ["DS2_CONV_H3"] = "1" if mode.startswith("h3") else "0"
-        os.environ["DS2_CONV_FRESH"] = "0" if mode == "h3-chain" else "1"
+        os.environ["DS2_CONV_H3"] = "1" if mode == "h3" else "0"
         yd = ops.conv2d_fwd(x.to(dev), wt.to(dev), None, (sh, sw), (ph, pw)).double().cpu()
         dx = ops.conv2d_dgrad(dy.to(dev), wt.to(dev), x.shape, (sh, sw), (ph, pw)).double().cpu()
         for name, a, r in (("fwd y", yd, y64), ("dgrad dx", dx, dx64)):

@@ -784,6 +784,52 @@ def test_lstm_persistent_equals_per_step(dev, h, n, monkeypatch):
         _close(a, b, 1e-5, "lstm persistent vs per-step")
 
 
+@pytest.mark.parametrize("n,t,h,bidir", [(64, 60, 1024, True), (40, 37, 256, False), (7, 9, 48, True),
+                                         (5, 8, 40, True)])
+def test_lstm_bwd_half_vs_fp32(dev, n, t, h, bidir):
+    """ds2_lstm_bwd_half (cfg4's bf16 mode: the backward recurrence's W_hh^T product on one
+    fp16 term per operand, 32-sample workgroups, one launch for batch 64) against ds2_lstm_bwd
+    (fp32-accurate) on the same forward cache: the gate gradients within 4e-3 of their max
+    (11-bit operands, per-row / per-column power-of-two scales), every step finite, ragged
+    lengths; a shape it declines falls back to ds2_lstm_bwd exactly."""
+    nd = 2 if bidir else 1
+    g = torch.Generator().manual_seed(n + t + h)
+    xproj = (torch.randn(t, n, nd, 4 * h, generator=g) * 0.5).to(dev)
+    w = [((torch.rand(4 * h, h, generator=g) * 2 - 1) * h ** -0.5).to(dev) for _ in range(nd)]
+    b = [(torch.rand(4 * h, generator=g) * 0.2 - 0.1).to(dev) for _ in range(nd)]
+    lens = torch.tensor(sorted([max(1, t - (i * 5) % t) for i in range(n)], reverse=True),
+                        dtype=torch.int32, device=dev)
+    h_all = torch.empty(t, n, nd, h, device=dev)
+    c_all = torch.empty(t, n, nd, h, device=dev)
+    gates = torch.empty(t, n, nd, 4 * h, device=dev)
+    st = ops.rnn_status_word(dev)
+    ws = ops._ws(_lib.size("ds2_lstm_fwd_workspace_size", n, h, nd), dev)
+    wr = w[1].data_ptr() if bidir else None
+    br = b[1].data_ptr() if bidir else None
+    _lib.call("ds2_lstm_fwd", t, n, h, nd, xproj.data_ptr(), w[0].data_ptr(), wr, b[0].data_ptr(),
+              br, lens.data_ptr(), h_all.data_ptr(), c_all.data_ptr(), gates.data_ptr(),
+              st.data_ptr(), ws.data_ptr(), ws.numel(), ops._stream())
+    dy = torch.randn(t, n, nd, h, generator=g).to(dev)
+    out = {}
+    for fn in ("ds2_lstm_bwd", "ds2_lstm_bwd_half"):
+        dg = torch.full((t, n, nd, 4 * h), 7.0, device=dev)
+        wsb = ops._ws(_lib.size("ds2_lstm_bwd_workspace_size", n, h, nd), dev)
+        _lib.call(fn, t, n, h, nd, dy.data_ptr(), nd, w[0].data_ptr(), wr, c_all.data_ptr(),
+                  gates.data_ptr(), lens.data_ptr(), dg.data_ptr(), st.data_ptr(), wsb.data_ptr(),
+                  wsb.numel(), ops._stream())
+        torch.cuda.synchronize()
+        out[fn] = dg.cpu()
+    ops.check_rnn_status(dev)
+    ref, got = out["ds2_lstm_bwd"], out["ds2_lstm_bwd_half"]
+    assert torch.isfinite(got).all()
+    for i in range(n):   # rows past a sample's length are zero on both sides
+        assert (got[int(lens[i]):, i] == 0).all()
+    err = (got - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 4e-3, err
+    if h % 16 != 0:
+        assert torch.equal(got, ref)
+
+
 @pytest.mark.parametrize("n,h,bidir", [(64, 1024, True), (21, 800, True), (16, 256, False),
                                        (7, 48, False)])
 def test_lstm_xcd_groups_bit_identical(dev, n, h, bidir, monkeypatch):

@@ -208,6 +208,7 @@ def _check_train_step(dev, t_list, label_lens, seed, conv_tol=5e-4, zero_conv_bi
     # default, 2.6e-5 between the two; profiles/r4i_bs4_norm_probe.txt)
     assert abs(float(tr.optimizer.norm.item()) - float(rnorm)) <= 2e-4 * float(rnorm)
     worst = {}
+    bad_grads = []
     for name, p in m.named_parameters():
         tol = conv_tol if name.startswith('conv.') else 5e-4
         d = p.detach().cpu() - before[name]
@@ -220,13 +221,19 @@ def _check_train_step(dev, t_list, label_lens, seed, conv_tol=5e-4, zero_conv_bi
             scale = torch.as_tensor(rgrads[name.replace('.bias', '.weight')]).abs().max().item()
             err = (p.grad.detach().double().cpu() - torch.as_tensor(rgrads[name]).double()).abs().max().item()
             worst[name] = err / scale
-            assert worst[name] <= 5e-4, (name, worst[name])
+            if worst[name] > 5e-4:
+                bad_grads.append((name, worst[name]))
             continue
         worst[name] = _rel(p.grad, rgrads[name])
-        assert worst[name] <= tol, (name, worst[name])
+        if worst[name] > tol:
+            bad_grads.append((name, worst[name]))
         # the update itself (p_new - p_old), not just p_new (dominated by p_old); both
         # differences carry the float32 rounding of p_new (half an ulp of |p| each)
-        assert (d - rd).abs().max().item() <= tol * rd.abs().max().item() + ulp, (name, 'update')
+        if (d - rd).abs().max().item() > tol * rd.abs().max().item() + ulp:
+            bad_grads.append((name, 'update'))
+    print("gradient distances from the oracle (max-abs / max-abs), largest first:",
+          sorted(((round(v, 7), k) for k, v in worst.items()), reverse=True)[:12])
+    assert not bad_grads, bad_grads
     for k, v in m.state_dict().items():
         if 'running' in k:
             assert _rel(v, o.sd[k]) <= 1e-5, k
