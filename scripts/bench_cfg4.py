@@ -20,6 +20,15 @@ import torch  # noqa: E402
 import bench  # noqa: E402  (synthetic batch + labels of the headline bench)
 
 
+def recurrence_label(rnn_gemm):
+    """The LSTM recurrences' arithmetic as ops.LSTMLayerFn will run it."""
+    h3 = os.environ.get("DS2_LSTM_H3", "1")[:1] != "0"
+    fwd = "fp16x3" if h3 else "fp32 MFMA"
+    if rnn_gemm == "bf16" and os.environ.get("DS2_LSTM_HALF", "1")[:1] != "0":
+        return f"recurrence fwd {fwd}, bwd single-term fp16"
+    return f"recurrence {fwd}"
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--bidir", type=int, default=1)
@@ -57,7 +66,7 @@ def main():
     print(json.dumps({
         "config": f"cfg4: {args.layers}x{'Bi' if args.bidir else ''}LSTM-{args.hidden}"
                   f"{'' if args.bidir else ' + lookahead(20)'}, batch {args.batch}, 10 s, "
-                  f"RNN GEMMs {args.rnn_gemm}, recurrence + rest fp32",
+                  f"RNN GEMMs {args.rnn_gemm}, " + recurrence_label(args.rnn_gemm) + ", rest fp32",
         "audio_seconds_per_sec": round(args.batch * bench.SECONDS * args.steps / dt, 2),
         "ms_per_step": round(dt * 1e3 / args.steps, 2), "loss": round(float(loss), 4),
         "steps": args.steps}), flush=True)

@@ -322,10 +322,12 @@ CONVS = [  # (n, ci, h, w, co, kh, kw, sh, sw, ph, pw)
 
 
 def _conv_mode(monkeypatch, mode):
-    """h3: the default (fp16x3 conv2-shaped fwd / dgrad, bf16x6 elsewhere); x6: bf16x6
-    (DS2_CONV_H3=0); fp32: the fp32 LDS-patch / implicit-GEMM kernels (DS2_CONV_X6=0)."""
+    """h3: the default (fp16x3 conv2-shaped fwd / dgrad and sliding-window wgrad, bf16x6
+    elsewhere); x6: bf16x6 (DS2_CONV_H3=0, DS2_CONV_H3W=0); fp32: the fp32 LDS-patch /
+    implicit-GEMM kernels (DS2_CONV_X6=0)."""
     monkeypatch.setenv("DS2_CONV_X6", "0" if mode == "fp32" else "1")
     monkeypatch.setenv("DS2_CONV_H3", "1" if mode == "h3" else "0")
+    monkeypatch.setenv("DS2_CONV_H3W", "1" if mode == "h3" else "0")
 
 
 @pytest.mark.parametrize("mode", ["h3", "x6", "fp32"])
@@ -390,10 +392,11 @@ def test_conv_x6_is_fp32_accurate(dev, monkeypatch):
 
 
 def test_conv_h3_scales_over_twelve_decades(dev, monkeypatch):
-    """fp16x3 conv2 forward / dgrad with samples and output channels spread over 10^+-6: the
-    per-sample input scale and per-row weight scale keep every output at the fp32 error bound's
-    form, max |y - y64| / (|w| * |x|) (the same convolution of absolute values), within 2.5x of
-    bf16x6's and below 2e-6."""
+    """fp16x3 conv2 forward / dgrad with samples and output channels spread over 10^+-6, and
+    the weight gradient with input and output channels spread likewise: the per-sample input
+    scale, per-row weight scale and per-channel wgrad scales keep every output at the fp32
+    error bound's form, max |y - y64| / (|w| * |x|) (the same convolution of absolute values),
+    within 2.5x of bf16x6's and below 2e-6."""
     n, ci, h, w, co, kh, kw, sh, sw, ph, pw = 4, 32, 81, 90, 32, 21, 11, 2, 1, 10, 5
     g = torch.Generator().manual_seed(23)
     sx = torch.pow(10.0, torch.linspace(-6, 6, n, dtype=torch.float64))
@@ -408,13 +411,21 @@ def test_conv_h3_scales_over_twelve_decades(dev, monkeypatch):
     dy = torch.randn(y.shape, generator=g, dtype=torch.float64) * sx[:, None, None, None]
     dxr = torch.nn.grad.conv2d_input(x.shape, wt2, dy, stride=(sh, sw), padding=(ph, pw))
     dxb = torch.nn.grad.conv2d_input(x.shape, wt2.abs(), dy.abs(), stride=(sh, sw), padding=(ph, pw))
+    # wgrad: x channels (ci) and dy channels (co) spread over 10^+-6 -- the fp16x3 weight
+    # gradient scales each by its own channel maximum over the batch
+    xw = torch.randn(n, ci, h, w, generator=g, dtype=torch.float64) * swi[None, :, None, None]
+    dyw = torch.randn(y.shape, generator=g, dtype=torch.float64) * sw_[None, :, None, None]
+    dwr = torch.nn.grad.conv2d_weight(xw, wt.shape, dyw, stride=(sh, sw), padding=(ph, pw))
+    dwb = torch.nn.grad.conv2d_weight(xw.abs(), wt.shape, dyw.abs(), stride=(sh, sw), padding=(ph, pw))
     errs = {}
     for mode in ("h3", "x6"):
         _conv_mode(monkeypatch, mode)
         yd = ops.conv2d_fwd(x.float().to(dev), wt.float().to(dev), None, (sh, sw), (ph, pw))
         dx = ops.conv2d_dgrad(dy.float().to(dev), wt2.float().to(dev), x.shape, (sh, sw), (ph, pw))
+        dwd, _ = ops.conv2d_wgrad(dyw.float().to(dev), xw.float().to(dev), tuple(wt.shape), (sh, sw),
+                                  (ph, pw), with_bias=False)
         errs[mode] = tuple(((a.double().cpu() - r).abs() / b.clamp_min(1e-300)).max().item()
-                           for a, r, b in ((yd, y, yb), (dx, dxr, dxb)))
+                           for a, r, b in ((yd, y, yb), (dx, dxr, dxb), (dwd, dwr, dwb)))
     assert all(e3 <= 2.5 * e6 + 1e-7 for e3, e6 in zip(errs["h3"], errs["x6"])), errs
     assert max(errs["h3"]) < 2e-6, errs
 
