@@ -2,7 +2,13 @@
 // NCDT -> T,N,(C*D) collapse) and their backward passes.  HBM-bound.
 //
 // Reductions accumulate in fp64 per workgroup and combine the partials in a
-// fixed order (deterministic; no atomics).  Two reduction shapes:
+// fixed order (deterministic; no atomics).  The backward re-sums x beside g and g*x,
+// so its coefficients use the batch mean exactly (the forward keeps only the
+// fp32-rounded mean): sum(g*xhat) = invstd*(sum(g*x) - mean*sum(g)), and the
+// apply dx = k1*g - k2 - k3*xhat runs in fp64 with xhat from that mean.  With the
+// fp32 mean, every dx of a channel carried the same -k3*invstd*(mean32 - mean)
+// shift, which the next layer's per-channel sums (the conv biases' BatchNorm
+// gradients) add up 1.3 M times.  Two reduction shapes:
 //   rows   : x is [R][C] (SequenceWise BatchNorm1d, model.py:28-43,89,336)
 //            block = 64 columns x 4 row groups, grid = column blocks x row chunks
 //   planes : x is [outer][C][D][T] (BatchNorm2d, model.py:210,213)
@@ -15,6 +21,11 @@ constexpr int kRowChunks = 256;   // row chunks for the [R][C] reduction (>= 4 w
 constexpr int kPlaneSplit = 4;    // slices per (outer, channel) plane
 
 enum RedMode { RED_STATS = 0, RED_BWD = 1 };
+// doubles per (part, channel) partial: stats (sum x, sum x^2, -), backward
+// (sum g, sum g*x, sum x)
+constexpr int kParts = 3;
+// doubles per channel of backward coefficients: k1, k2, k3, exact mean
+constexpr int kCoef = 4;
 
 struct BnBwdArgs {
   const float* mean;
@@ -44,7 +55,7 @@ __global__ __launch_bounds__(256) void reduce_rows_kernel(const float* __restric
                                                           const float* __restrict__ dy, int R,
                                                           int C, BnBwdArgs a,
                                                           double* __restrict__ partial) {
-  __shared__ double s0[4][64], s1[4][64];
+  __shared__ double s0[4][64], s1[4][64], s2[4][64];
   const int lane = threadIdx.x & 63;
   const int grp = threadIdx.x >> 6;
   const int col = blockIdx.x * 64 + lane;
@@ -52,7 +63,7 @@ __global__ __launch_bounds__(256) void reduce_rows_kernel(const float* __restric
   const int per = (R + gridDim.y - 1) / gridDim.y;
   const int r0 = chunk * per;
   const int r1 = min(R, r0 + per);
-  double acc0 = 0.0, acc1 = 0.0;
+  double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0;
   if (col < C) {
     for (int r = r0 + grp; r < r1; r += 4) {
       const float v = x[(int64_t)r * C + col];
@@ -63,18 +74,20 @@ __global__ __launch_bounds__(256) void reduce_rows_kernel(const float* __restric
         float xhat;
         const float g = bwd_g(dy[(int64_t)r * C + col], v, col, 0, 1, a, &xhat);
         acc0 += g;
-        acc1 += (double)g * xhat;
+        acc1 += (double)g * v;
+        acc2 += v;
       }
     }
   }
   s0[grp][lane] = acc0;
   s1[grp][lane] = acc1;
+  s2[grp][lane] = acc2;
   __syncthreads();
   if (grp == 0 && col < C) {
-    double t0 = s0[0][lane] + s0[1][lane] + s0[2][lane] + s0[3][lane];
-    double t1 = s1[0][lane] + s1[1][lane] + s1[2][lane] + s1[3][lane];
-    partial[((int64_t)chunk * C + col) * 2 + 0] = t0;
-    partial[((int64_t)chunk * C + col) * 2 + 1] = t1;
+    double* pp = partial + ((int64_t)chunk * C + col) * kParts;
+    pp[0] = s0[0][lane] + s0[1][lane] + s0[2][lane] + s0[3][lane];
+    pp[1] = s1[0][lane] + s1[1][lane] + s1[2][lane] + s1[3][lane];
+    pp[2] = s2[0][lane] + s2[1][lane] + s2[2][lane] + s2[3][lane];
   }
 }
 
@@ -86,7 +99,7 @@ __global__ __launch_bounds__(256) void reduce_rows4_kernel(const float* __restri
                                                            const float* __restrict__ dy, int R,
                                                            int C, BnBwdArgs a,
                                                            double* __restrict__ partial) {
-  __shared__ double s0[4][256], s1[4][256];
+  __shared__ double s0[4][256], s1[4][256], s2[4][256];
   const int lane = threadIdx.x & 63;
   const int grp = threadIdx.x >> 6;
   const int col = blockIdx.x * 256 + lane * 4;
@@ -95,6 +108,7 @@ __global__ __launch_bounds__(256) void reduce_rows4_kernel(const float* __restri
   const int r0 = chunk * per;
   const int r1 = min(R, r0 + per);
   double acc0[4] = {0.0, 0.0, 0.0, 0.0}, acc1[4] = {0.0, 0.0, 0.0, 0.0};
+  double acc2[4] = {0.0, 0.0, 0.0, 0.0};
   if (col < C) {
     float mu[4] = {0.f, 0.f, 0.f, 0.f}, is[4] = {0.f, 0.f, 0.f, 0.f};
     float ga[4] = {0.f, 0.f, 0.f, 0.f}, be[4] = {0.f, 0.f, 0.f, 0.f};
@@ -130,7 +144,8 @@ __global__ __launch_bounds__(256) void reduce_rows4_kernel(const float* __restri
             g = (y2 > a.lo && y2 < a.hi) ? g : 0.f;
           }
           acc0[e] += g;
-          acc1[e] += (double)g * xhat;
+          acc1[e] += (double)g * vv[e];
+          acc2[e] += vv[e];
         }
       }
     };
@@ -145,13 +160,16 @@ __global__ __launch_bounds__(256) void reduce_rows4_kernel(const float* __restri
   for (int e = 0; e < 4; ++e) {
     s0[grp][lane * 4 + e] = acc0[e];
     s1[grp][lane * 4 + e] = acc1[e];
+    s2[grp][lane * 4 + e] = acc2[e];
   }
   __syncthreads();
   const int c = blockIdx.x * 256 + threadIdx.x;
   if (c < C) {
     const int t = threadIdx.x;
-    partial[((int64_t)chunk * C + c) * 2 + 0] = s0[0][t] + s0[1][t] + s0[2][t] + s0[3][t];
-    partial[((int64_t)chunk * C + c) * 2 + 1] = s1[0][t] + s1[1][t] + s1[2][t] + s1[3][t];
+    double* pp = partial + ((int64_t)chunk * C + c) * kParts;
+    pp[0] = s0[0][t] + s0[1][t] + s0[2][t] + s0[3][t];
+    pp[1] = s1[0][t] + s1[1][t] + s1[2][t] + s1[3][t];
+    pp[2] = s2[0][t] + s2[1][t] + s2[2][t] + s2[3][t];
   }
 }
 
@@ -175,7 +193,7 @@ __global__ __launch_bounds__(256) void reduce_planes_kernel(const float* __restr
   const int d1 = min(D, d0 + per);
   const int64_t base = ((int64_t)o * C + c) * D * T;
   const int len = (MODE == RED_BWD && a.masked) ? a.lens[o] : T;
-  double acc0 = 0.0, acc1 = 0.0;
+  double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0;
   for (int d = d0; d < d1; ++d) {
     const int64_t rb = base + (int64_t)d * T;
     for (int t = threadIdx.x; t < T; t += blockDim.x) {
@@ -187,51 +205,59 @@ __global__ __launch_bounds__(256) void reduce_planes_kernel(const float* __restr
         float xhat;
         const float g = bwd_g(dy[rb + t], v, c, t, len, a, &xhat);
         acc0 += g;
-        acc1 += (double)g * xhat;
+        acc1 += (double)g * v;
+        acc2 += v;
       }
     }
   }
-  __shared__ double r0[4], r1[4];
+  __shared__ double r0[4], r1[4], r2[4];
   acc0 = wave_sum_d(acc0);
   acc1 = wave_sum_d(acc1);
+  acc2 = wave_sum_d(acc2);
   if ((threadIdx.x & 63) == 0) {
     r0[threadIdx.x >> 6] = acc0;
     r1[threadIdx.x >> 6] = acc1;
+    r2[threadIdx.x >> 6] = acc2;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
     const int64_t pidx = ((int64_t)o * gridDim.z + sl) * C + c;
-    partial[pidx * 2 + 0] = r0[0] + r0[1] + r0[2] + r0[3];
-    partial[pidx * 2 + 1] = r1[0] + r1[1] + r1[2] + r1[3];
+    partial[pidx * kParts + 0] = r0[0] + r0[1] + r0[2] + r0[3];
+    partial[pidx * kParts + 1] = r1[0] + r1[1] + r1[2] + r1[3];
+    partial[pidx * kParts + 2] = r2[0] + r2[1] + r2[2] + r2[3];
   }
 }
 
 // ---- finalize ---------------------------------------------------------------
-// Fixed-order sum of the (s, ss) partial pairs of column c = blockIdx.x * 64 + lane:
+// Fixed-order sum of the kParts-wide partials of column c = blockIdx.x * 64 + lane:
 // the 4 waves of a 256-thread block sum interleaved part subsets, wave 0 combines.
 // Returns false for the threads that do not finish a column.
-__device__ __forceinline__ bool sum_pairs(const double* __restrict__ partial, int nparts, int C,
-                                          int& c, double& s, double& ss) {
-  __shared__ double red[2][4][64];
+template <int K>
+__device__ __forceinline__ bool sum_parts(const double* __restrict__ partial, int nparts, int C,
+                                          int& c, double (&out)[K]) {
+  __shared__ double red[K][4][64];
   const int lane = threadIdx.x & 63;
   const int grp = threadIdx.x >> 6;
   c = blockIdx.x * 64 + lane;
-  double a = 0.0, b = 0.0;
+  double acc[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) acc[k] = 0.0;
   // unrolled so that 8 partials' loads are in flight at once (the sums keep their order):
   // one dependent load per iteration made these finals latency-bound (~18 us each)
   if (c < C) {
 #pragma unroll 8
     for (int p = grp; p < nparts; p += 4) {
-      a += partial[((int64_t)p * C + c) * 2 + 0];
-      b += partial[((int64_t)p * C + c) * 2 + 1];
+#pragma unroll
+      for (int k = 0; k < K; ++k) acc[k] += partial[((int64_t)p * C + c) * kParts + k];
     }
   }
-  red[0][grp][lane] = a;
-  red[1][grp][lane] = b;
+#pragma unroll
+  for (int k = 0; k < K; ++k) red[k][grp][lane] = acc[k];
   __syncthreads();
   if (grp != 0 || c >= C) return false;
-  s = (red[0][0][lane] + red[0][1][lane]) + (red[0][2][lane] + red[0][3][lane]);
-  ss = (red[1][0][lane] + red[1][1][lane]) + (red[1][2][lane] + red[1][3][lane]);
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+    out[k] = (red[k][0][lane] + red[k][1][lane]) + (red[k][2][lane] + red[k][3][lane]);
   return true;
 }
 
@@ -240,8 +266,9 @@ __global__ __launch_bounds__(256) void stats_final_kernel(
     float momentum, float* __restrict__ save_mean, float* __restrict__ save_invstd,
     float* __restrict__ running_mean, float* __restrict__ running_var) {
   int c;
-  double s = 0.0, ss = 0.0;
-  if (!sum_pairs(partial, nparts, C, c, s, ss)) return;
+  double sum[2];
+  if (!sum_parts<2>(partial, nparts, C, c, sum)) return;
+  const double s = sum[0], ss = sum[1];
   const double mean = s / count;
   double var = ss / count - mean * mean;
   if (var < 0.0) var = 0.0;
@@ -263,23 +290,29 @@ __global__ void eval_stats_kernel(const float* __restrict__ rm, const float* __r
   invstd[c] = static_cast<float>(1.0 / sqrt((double)rv[c] + (double)eps));
 }
 
-// sums -> per-channel coefficients for the backward apply:
+// sums -> per-channel coefficients for the backward apply (fp64):
 //   dx = k1 * g - k2 - k3 * xhat  with k1 = gamma*invstd, k2 = k1*mean(g),
-//   k3 = k1*mean(g*xhat); also dgamma = sum(g*xhat), dbeta = sum(g) and the
-//   closed-form bias gradient (see ds2_bn_backward).
+//   k3 = k1*mean(g*xhat), xhat = (x - mean)*invstd with the exact batch mean
+//   sum(x)/count; also dgamma = sum(g*xhat), dbeta = sum(g) and the closed-form
+//   bias gradient (see ds2_bn_backward).
 __global__ __launch_bounds__(256) void bwd_final_kernel(
     const double* __restrict__ partial, int nparts, int C, double count, BnBwdArgs a,
-    int n_outer, int D, int T, float* __restrict__ coef, float* __restrict__ dgamma,
+    int n_outer, int D, int T, double* __restrict__ coef, float* __restrict__ dgamma,
     float* __restrict__ dbeta, float* __restrict__ dbias) {
   int c;
-  double sg = 0.0, sgx = 0.0;
-  if (!sum_pairs(partial, nparts, C, c, sg, sgx)) return;
+  double sum[3];
+  if (!sum_parts<3>(partial, nparts, C, c, sum)) return;
+  const double sg = sum[0];
+  const double mean = sum[2] / count;
+  const double is = (double)a.invstd[c];
+  const double sgx = is * (sum[1] - mean * sg);     // sum(g * xhat)
   const double gbar = sg / count;
   const double gxbar = sgx / count;
-  const double k1 = (double)a.gamma[c] * a.invstd[c];
-  coef[c * 3 + 0] = static_cast<float>(k1);
-  coef[c * 3 + 1] = static_cast<float>(k1 * gbar);
-  coef[c * 3 + 2] = static_cast<float>(k1 * gxbar);
+  const double k1 = (double)a.gamma[c] * is;
+  coef[c * kCoef + 0] = k1;
+  coef[c * kCoef + 1] = k1 * gbar;
+  coef[c * kCoef + 2] = k1 * gxbar;
+  coef[c * kCoef + 3] = mean;
   if (dgamma != nullptr) dgamma[c] = static_cast<float>(sgx);
   if (dbeta != nullptr) dbeta[c] = static_cast<float>(sg);
   if (dbias != nullptr) {
@@ -291,7 +324,7 @@ __global__ __launch_bounds__(256) void bwd_final_kernel(
     } else {
       cnt_u = count;
     }
-    const double v = k1 * (count - cnt_u) * (gbar - gxbar * (double)a.invstd[c] * a.mean[c]);
+    const double v = k1 * (count - cnt_u) * (gbar - gxbar * is * mean);
     dbias[c] = static_cast<float>(v);
   }
 }
@@ -420,7 +453,7 @@ __global__ __launch_bounds__(256) void tnf_to_nft_kernel(const float* __restrict
 // backward apply over [outer][C][D][T] (rows case: D = T = 1 -> inner = 1)
 __global__ void bwd_apply_planes_kernel(const float* __restrict__ dy, const float* __restrict__ x,
                                         int C, int D, int T, BnBwdArgs a,
-                                        const float* __restrict__ coef, float* __restrict__ dx) {
+                                        const double* __restrict__ coef, float* __restrict__ dx) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   const int d = blockIdx.y;
   const int oc = blockIdx.z;
@@ -429,22 +462,26 @@ __global__ void bwd_apply_planes_kernel(const float* __restrict__ dy, const floa
   if (t >= T) return;
   const int64_t idx = ((int64_t)oc * D + d) * T + t;
   const int len = a.masked ? a.lens[o] : T;
-  float xhat;
-  const float g = bwd_g(dy[idx], x[idx], c, t, len, a, &xhat);
-  float v = coef[c * 3 + 0] * g - coef[c * 3 + 1] - coef[c * 3 + 2] * xhat;
+  const float xv = x[idx];
+  float xhat32;
+  const float g = bwd_g(dy[idx], xv, c, t, len, a, &xhat32);   // mask as the forward's
+  const double* k = coef + c * kCoef;
+  const double xhat = ((double)xv - k[3]) * (double)a.invstd[c];
+  float v = static_cast<float>(k[0] * g - k[1] - k[2] * xhat);
   if (a.masked && t >= len) v = 0.f;
   dx[idx] = v;
 }
 
 __global__ void bwd_apply_rows_kernel(const float* __restrict__ dy, const float* __restrict__ x,
                                       int64_t R, int C, BnBwdArgs a,
-                                      const float* __restrict__ coef, float* __restrict__ dx) {
+                                      const double* __restrict__ coef, float* __restrict__ dx) {
   const int64_t total = R * C;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * blockDim.x) {
     const int c = static_cast<int>(i % C);
-    const float xhat = (x[i] - a.mean[c]) * a.invstd[c];
-    dx[i] = coef[c * 3 + 0] * dy[i] - coef[c * 3 + 1] - coef[c * 3 + 2] * xhat;
+    const double* k = coef + c * kCoef;
+    const double xhat = ((double)x[i] - k[3]) * (double)a.invstd[c];
+    dx[i] = static_cast<float>(k[0] * dy[i] - k[1] - k[2] * xhat);
   }
 }
 
@@ -466,8 +503,8 @@ using namespace ds2;
 extern "C" {
 
 size_t ds2_bn_workspace_size(int outer, int c, int inner) {
-  return partial_parts(outer, c, inner) * (size_t)c * 2 * sizeof(double) +
-         (size_t)c * 3 * sizeof(float) + 256;
+  return partial_parts(outer, c, inner) * (size_t)c * kParts * sizeof(double) +
+         (size_t)c * kCoef * sizeof(double) + 256;
 }
 
 ds2_status_t ds2_bn_train_stats(const float* x, int outer, int c, int inner, float eps,
@@ -562,7 +599,7 @@ ds2_status_t ds2_bn_backward(const float* dy, int dy_layout, const float* x, int
   hipStream_t st = as_stream(stream);
   const size_t nparts = partial_parts(outer, c, inner);
   double* partial = static_cast<double*>(ws);
-  float* coef = reinterpret_cast<float*>(partial + nparts * c * 2);
+  double* coef = partial + nparts * c * kParts;
   BnBwdArgs a{mean, invstd, gamma, beta, lens, lo, hi, masked};
 
   const float* g_src = dy;
