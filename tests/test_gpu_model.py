@@ -9,6 +9,7 @@ import os
 import numpy as np
 import pytest
 import torch
+import torch.nn.functional as F
 
 from ds2amd import model as dsm
 from ds2amd.decoder import GreedyDecoder
@@ -158,11 +159,20 @@ def test_lstm_1024_forward_matches_oracle(dev, bidir):
 @pytest.mark.parametrize("rnn_type,bidir", [('lstm', True), ('lstm', False), ('gru', True)])
 def test_bf16_rnn_gemms_track_the_fp32_oracle(dev, rnn_type, bidir):
     """BASELINE cfg4's opt-in precision: the recurrent layers' GEMMs (input projection,
-    dX, dW_ih, dW_hh) on bf16 operands with fp32 accumulation.  Same weights, same batch:
-    logits within 2e-2 (relative to max |logit|) of the fp32 oracle, loss within 1 %,
-    recurrent-layer weight gradients within 1e-1 (bf16 activations and gate gradients
-    compound over the 3 layers; a layout error would be O(1)); the fp32 model is bit-for-bit unaffected by the switch
-    being available (rnn_gemm_precision defaults to 'fp32')."""
+    dX, dW_ih, dW_hh) on bf16 operands with fp32 accumulation (and, for the LSTM, the
+    backward recurrence's single-term fp16 W_hh^T product).  Same weights, same batch:
+    logits within 2e-2 (relative to max |logit|) of the fp32 oracle, loss within 1 %.
+    Recurrent-layer gradients, each against the oracle's own autograd gradients:
+      - the fp32 model within 1e-3 (measured 1e-4);
+      - the bf16 model within 5e-2 of the oracle run with the same bf16 rounding of its
+        recurrent layers' input x and W_ih (straight-through; measured <= 2.5e-2): the
+        arithmetic itself;
+      - the bf16 model within 2e-1 of the plain fp32 oracle, a layout error would be O(1).
+        bf16 input projections alone move the unidirectional LSTM's last-layer bias
+        gradients by 0.111 in the oracle itself (Lookahead + Hardtanh follows that layer),
+        and ours by 0.111 (profiles/r6f_bf16_rnn_gemms.txt).
+    The fp32 model is bit-for-bit unaffected by the switch being available
+    (rnn_gemm_precision defaults to 'fp32')."""
     from ds2amd.ctc import CTCLoss
     m = build(91, 256, 3, rnn_type=rnn_type, bidirectional=bidir).to(dev).train()
     m16 = build(91, 256, 3, rnn_type=rnn_type, bidirectional=bidir).to(dev).train()
@@ -192,9 +202,49 @@ def test_bf16_rnn_gemms_track_the_fp32_oracle(dev, rnn_type, bidir):
         losses.append(float(loss))
         grads.append({k: p.grad.detach().cpu().clone() for k, p in mm.named_parameters()})
     assert abs(losses[1] - losses[0]) <= 1e-2 * abs(losses[0])
-    for k, g32 in grads[0].items():
-        if k.startswith('rnns.'):
-            assert _rel(grads[1][k], g32) < 1e-1, k
+    dist = {k: _rel(grads[1][k], g32) for k, g32 in grads[0].items() if k.startswith('rnns.')}
+    print("bf16 vs fp32 recurrent-layer gradient distances, largest first:",
+          sorted(((round(v, 4), k) for k, v in dist.items()), reverse=True)[:8])
+    # both against the oracle's own autograd gradients (CTC summed, as CTCLoss() above)
+    params = {k: v.detach().clone().requires_grad_(True) for k, v in o.parameters().items()}
+    ol, _, oo, _ = o.forward(x, sizes, training=True, params=params)
+    lp = F.log_softmax(ol.transpose(0, 1).double(), dim=2).float()
+    F.ctc_loss(lp, tg.long(), oo.long(), tl.long(), blank=0, reduction='sum').backward()
+    d32 = {k: _rel(grads[0][k], params[k].grad) for k in dist}
+    print("fp32 model vs oracle, largest first:",
+          sorted(((round(v, 5), k) for k, v in d32.items()), reverse=True)[:6])
+
+    # the oracle with its recurrent layers' input x and W_ih rounded to bf16 in the forward
+    # (straight-through, fp32 otherwise)
+    class _Bf16In(orc.OracleDS2):
+        def _gru(self, x, lens, pre):
+            saved = self.params
+            self.params = dict(saved)
+            try:
+                for k in list(self.params):
+                    if k.startswith(pre + '.weight_ih'):
+                        w = self.params[k]
+                        self.params[k] = w + (w.bfloat16().float() - w).detach()
+                x = x + (x.bfloat16().float() - x).detach()
+                return super()._gru(x, lens, pre)
+            finally:
+                self.params = saved
+    ob = _Bf16In({k: v.detach().cpu() for k, v in m.state_dict().items()}, 3, 256,
+                 bidirectional=bidir, rnn_type=rnn_type)
+    pb = {k: v.detach().clone().requires_grad_(True) for k, v in ob.parameters().items()}
+    bl, _, bo, _ = ob.forward(x, sizes, training=True, params=pb)
+    lpb = F.log_softmax(bl.transpose(0, 1).double(), dim=2).float()
+    F.ctc_loss(lpb, tg.long(), bo.long(), tl.long(), blank=0, reduction='sum').backward()
+    d_emu = {k: _rel(pb[k].grad, params[k].grad) for k in dist}
+    print("oracle with bf16 input projections vs oracle, largest first:",
+          sorted(((round(v, 4), k) for k, v in d_emu.items()), reverse=True)[:6])
+    d16 = {k: _rel(grads[1][k], pb[k].grad) for k in dist}
+    print("bf16 model vs that oracle, largest first:",
+          sorted(((round(v, 4), k) for k, v in d16.items()), reverse=True)[:6])
+    for k in dist:
+        assert d32[k] < 1e-3, (k, d32[k])
+        assert d16[k] < 5e-2, (k, d16[k])
+        assert dist[k] < 2e-1, (k, dist[k])
 
 
 def test_cfg2_shape_step_properties(dev):

@@ -514,6 +514,47 @@ def test_conv_block_fwd_bwd(dev, layout):
         _close(pd.grad, pr.grad, 2e-4, name)
 
 
+@pytest.mark.parametrize("mode", ["h3", "x6", "fp32"])
+def test_conv_block_model_conv2_ragged(dev, mode, monkeypatch):
+    """ConvBlockFn at the model's conv2 (32 -> 32 channels, 21 x 11 taps, stride (2, 1), the
+    input a Hardtanh(0, 20) output) with ragged lengths -- the kernels the bs32 benchmark uses
+    (fp16x3 forward / dgrad, sliding-window wgrad), with the time mask of model.py:69-78 --
+    vs fp64: output 1e-5, gradients 2e-4 (relative to max), in each conv mode."""
+    _conv_mode(monkeypatch, mode)
+    g = torch.Generator().manual_seed(23)
+    n, ci, h, w = 3, 32, 41, 150
+    co, kh, kw, sh, sw, ph, pw = 32, 21, 11, 2, 1, 10, 5
+    lens = torch.tensor([w, w - 31, 62], dtype=torch.int32)
+    x = (torch.rand(n, ci, h, w, generator=g, dtype=torch.float64) * 24 - 2).clamp(0, 20)
+    for i in range(n):
+        x[i, :, :, int(lens[i]):] = 0
+    wt = torch.randn(co, ci, kh, kw, generator=g, dtype=torch.float64) * (ci * kh * kw) ** -0.5
+    b = torch.randn(co, generator=g, dtype=torch.float64) * 0.1
+    gamma = torch.rand(co, generator=g, dtype=torch.float64) + 0.5
+    beta = torch.randn(co, generator=g, dtype=torch.float64) * 0.2
+    params = [t.clone().requires_grad_(True) for t in (x, wt, b, gamma, beta)]
+    xr, wr, brr, gr, ber = params
+    rm, rv = torch.zeros(co, dtype=torch.float64), torch.ones(co, dtype=torch.float64)
+
+    def mask(t):
+        m = torch.arange(t.shape[-1])[None, :] >= lens[:, None].long()
+        return t.masked_fill(m[:, None, None, :], 0)
+    z = mask(F.conv2d(xr, wr, brr, stride=(sh, sw), padding=(ph, pw)))
+    z = mask(F.batch_norm(z, rm, rv, gr, ber, training=True, momentum=0.1, eps=1e-5))
+    y = mask(F.hardtanh(z, 0, 20))
+    dy = torch.randn(y.shape, generator=g, dtype=torch.float64)
+    y.backward(dy)
+    dparams = [p.detach().float().to(dev).requires_grad_(True) for p in params]
+    xd, wd, bd, gd, bed = dparams
+    rm_d, rv_d = torch.zeros(co, device=dev), torch.ones(co, device=dev)
+    yd = ops.ConvBlockFn.apply(xd, lens.to(dev), wd, bd, gd, bed, rm_d, rv_d, True, 0.1, 1e-5,
+                               (sh, sw), (ph, pw), 0.0, 20.0, 0)
+    yd.backward(dy.float().to(dev))
+    _close(yd, y, 1e-5, "block y")
+    for name, pd, pr in zip(["dx", "dw", "dbias", "dgamma", "dbeta"], dparams, params):
+        _close(pd.grad, pr.grad, 2e-4, name)
+
+
 # ---------------------------------------------------------------------------- GRU
 @pytest.mark.parametrize("n,t,inp,h,bidir", [(5, 23, 40, 24, True), (19, 9, 33, 400, True),
                                              (3, 17, 20, 16, False), (20, 30, 64, 800, True),
