@@ -164,24 +164,32 @@ static void apply_spin_limit_env() {
 // scripts/gru_ab.py sweeps (the forward's first-poll delay 14 -> 10 with the same-XCD groups,
 // whose same-XCD tiles arrive sooner: 4.32-4.40 -> 4.26 us per step, `ftune`,
 // profiles/r3fa_fwd_tune.txt); [3] s_sleep(1) units between the flag hand-off's polls.
-// DS2_RNN_TUNE="a,b,c,d" overrides them (diagnostic; checked at every recurrence entry point).
+// [4]: the flag hand-off's second poll in flight, issued this many s_sleep(1) units after the
+// first (0: one poll at a time, each after the previous one returned).
+// DS2_RNN_TUNE="a,b,c,d,e" overrides them (diagnostic; checked at every recurrence entry point).
 constexpr unsigned kRepollSleep = 1u, kFirstPollDelay = 10u, kFirstPollDelayBwd = 14u,
-                   kFlagPollSleep = 1u;
-static __constant__ unsigned g_rnn_tune[4] = {kRepollSleep, kFirstPollDelay, kFirstPollDelayBwd,
-                                              kFlagPollSleep};
+                   kFlagPollSleep = 1u, kFlagPollGap = 0u;
+constexpr int kTuneN = 5;
+static __constant__ unsigned g_rnn_tune[kTuneN] = {kRepollSleep, kFirstPollDelay,
+                                                   kFirstPollDelayBwd, kFlagPollSleep,
+                                                   kFlagPollGap};
 
 static void apply_rnn_tune_env() {
-  static unsigned applied[4] = {kRepollSleep, kFirstPollDelay, kFirstPollDelayBwd, kFlagPollSleep};
-  unsigned v[4] = {kRepollSleep, kFirstPollDelay, kFirstPollDelayBwd, kFlagPollSleep};
+  static unsigned applied[kTuneN] = {kRepollSleep, kFirstPollDelay, kFirstPollDelayBwd,
+                                     kFlagPollSleep, kFlagPollGap};
+  unsigned v[kTuneN] = {kRepollSleep, kFirstPollDelay, kFirstPollDelayBwd, kFlagPollSleep,
+                        kFlagPollGap};
   const char* e = getenv("DS2_RNN_TUNE");
-  for (int i = 0; e != nullptr && e[0] != 0 && i < 4; ++i) {
+  for (int i = 0; e != nullptr && e[0] != 0 && i < kTuneN; ++i) {
     char* end = nullptr;
     v[i] = static_cast<unsigned>(strtoul(e, &end, 10));
     e = (end != nullptr && *end == ',') ? end + 1 : nullptr;
   }
-  if (v[0] == applied[0] && v[1] == applied[1] && v[2] == applied[2] && v[3] == applied[3]) return;
+  bool same = true;
+  for (int i = 0; i < kTuneN; ++i) same = same && v[i] == applied[i];
+  if (same) return;
   if (hipMemcpyToSymbol(HIP_SYMBOL(g_rnn_tune), v, sizeof(v)) == hipSuccess)
-    for (int i = 0; i < 4; ++i) applied[i] = v[i];
+    for (int i = 0; i < kTuneN; ++i) applied[i] = v[i];
 }
 
 __device__ __forceinline__ void sleep_units(unsigned k) {
@@ -230,10 +238,33 @@ __device__ __forceinline__ bool flags_wait(const unsigned* flags, int count, uns
       if (lane == 0) __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       ok = 0;
     }
-    for (; ok;) {
-      const unsigned v = lane < count ? __hip_atomic_load(flags + lane, __ATOMIC_RELAXED,
-                                                          __HIP_MEMORY_SCOPE_AGENT)
-                                      : target;
+    auto poll = [&]() {
+      return lane < count ? __hip_atomic_load(flags + lane, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT)
+                          : target;
+    };
+    const unsigned gap = g_rnn_tune[4];
+    if (gap != 0u && ok) {
+      // two polls in flight, `gap` apart: a flag set just after one poll passed the L2 is
+      // seen by the other about half a round trip later instead of a full one
+      unsigned a = poll();
+      sleep_units(gap);
+      unsigned b = poll();
+      for (;;) {
+        if (__ballot(a < target) == 0ull) break;
+        a = poll();
+        if (__ballot(b < target) == 0ull) break;
+        b = poll();
+        if (++spins > g_spin_limit) {
+          if (lane == 0) __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          ok = 0;
+          break;
+        }
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the poll left in flight
+    }
+    for (; ok && gap == 0u;) {
+      const unsigned v = poll();
       if (__ballot(v < target) == 0ull) break;
       sleep_units(g_rnn_tune[3]);
       if (++spins > g_spin_limit) {

@@ -64,6 +64,10 @@ if len(sys.argv) > 1 and sys.argv[1] == "flagpoll":
     # s_sleep(1) units between the flag hand-off's polls (the pre-split backward's wait)
     variants = {f"bwd-poll-{t}": {"DS2_GRU_X6": "1", "DS2_RNN_TUNE": t}
                 for t in ("1,10,14,1", "1,10,14,0", "1,10,14,2", "1,10,14,4")}
+if len(sys.argv) > 1 and sys.argv[1] == "flagpipe":
+    # the flag hand-off with a second poll in flight, issued G s_sleep(1) units after the first
+    # (0: one poll at a time)
+    variants = {f"bwd-pipe-{g}": {"DS2_RNN_TUNE": f"1,10,14,1,{g}"} for g in ("0", "4", "8", "14", "20")}
 rounds = int(os.environ.get("AB_ROUNDS", "3"))
 variants = {f"{k}#{r}": v for r in range(rounds) for k, v in variants.items()}
 ref = None
