@@ -99,7 +99,7 @@ __global__ __launch_bounds__(256) void reduce_rows4_kernel(const float* __restri
                                                            const float* __restrict__ dy, int R,
                                                            int C, BnBwdArgs a,
                                                            double* __restrict__ partial) {
-  __shared__ double s0[4][256], s1[4][256], s2[4][256];
+  __shared__ double sh[4][256];   // one sum at a time (8 KB: occupancy of this HBM-bound pass)
   const int lane = threadIdx.x & 63;
   const int grp = threadIdx.x >> 6;
   const int col = blockIdx.x * 256 + lane * 4;
@@ -156,20 +156,17 @@ __global__ __launch_bounds__(256) void reduce_rows4_kernel(const float* __restri
     }
     if (r < r1) add(r);
   }
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    s0[grp][lane * 4 + e] = acc0[e];
-    s1[grp][lane * 4 + e] = acc1[e];
-    s2[grp][lane * 4 + e] = acc2[e];
-  }
-  __syncthreads();
   const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c < C) {
-    const int t = threadIdx.x;
-    double* pp = partial + ((int64_t)chunk * C + c) * kParts;
-    pp[0] = s0[0][t] + s0[1][t] + s0[2][t] + s0[3][t];
-    pp[1] = s1[0][t] + s1[1][t] + s1[2][t] + s1[3][t];
-    pp[2] = s2[0][t] + s2[1][t] + s2[2][t] + s2[3][t];
+  const int t = threadIdx.x;
+  double* pp = partial + ((int64_t)chunk * C + c) * kParts;
+#pragma unroll
+  for (int k = 0; k < (MODE == RED_BWD ? 3 : 2); ++k) {
+    const double* a = k == 0 ? acc0 : (k == 1 ? acc1 : acc2);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) sh[grp][lane * 4 + e] = a[e];
+    __syncthreads();
+    if (c < C) pp[k] = sh[0][t] + sh[1][t] + sh[2][t] + sh[3][t];
+    __syncthreads();
   }
 }
 
