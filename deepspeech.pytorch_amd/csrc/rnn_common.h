@@ -165,20 +165,26 @@ static void apply_spin_limit_env() {
 // whose same-XCD tiles arrive sooner: 4.32-4.40 -> 4.26 us per step, `ftune`,
 // profiles/r3fa_fwd_tune.txt); [3] s_sleep(1) units between the flag hand-off's polls.
 // [4]: the flag hand-off's second poll in flight, issued this many s_sleep(1) units after the
-// first (0: one poll at a time, each after the previous one returned).
+// first (0: one poll at a time, each after the previous one returned).  [5]: s_sleep(1) units
+// before the flag hand-off's first poll of a step (polls before the group's last producer can
+// have published only load the flag lines that producers are writing).  [6]: s_sleep(1) units
+// before the tagged-record backward's first record loads of a step.
 // DS2_RNN_TUNE="a,b,c,d,e" overrides them (diagnostic; checked at every recurrence entry point).
 constexpr unsigned kRepollSleep = 1u, kFirstPollDelay = 10u, kFirstPollDelayBwd = 14u,
-                   kFlagPollSleep = 1u, kFlagPollGap = 0u;
-constexpr int kTuneN = 5;
+                   kFlagPollSleep = 1u, kFlagPollGap = 0u, kFlagFirstDelay = 0u,
+                   kTagFirstDelay = 0u;
+constexpr int kTuneN = 7;
 static __constant__ unsigned g_rnn_tune[kTuneN] = {kRepollSleep, kFirstPollDelay,
                                                    kFirstPollDelayBwd, kFlagPollSleep,
-                                                   kFlagPollGap};
+                                                   kFlagPollGap, kFlagFirstDelay,
+                                                   kTagFirstDelay};
 
 static void apply_rnn_tune_env() {
   static unsigned applied[kTuneN] = {kRepollSleep, kFirstPollDelay, kFirstPollDelayBwd,
-                                     kFlagPollSleep, kFlagPollGap};
+                                     kFlagPollSleep, kFlagPollGap, kFlagFirstDelay,
+                                     kTagFirstDelay};
   unsigned v[kTuneN] = {kRepollSleep, kFirstPollDelay, kFirstPollDelayBwd, kFlagPollSleep,
-                        kFlagPollGap};
+                        kFlagPollGap, kFlagFirstDelay, kTagFirstDelay};
   const char* e = getenv("DS2_RNN_TUNE");
   for (int i = 0; e != nullptr && e[0] != 0 && i < kTuneN; ++i) {
     char* end = nullptr;
@@ -228,10 +234,13 @@ __device__ __forceinline__ float ld_sc1(const float* p) {
 // group's UB flags sit in one or two cache lines; wave 0 polls them with one vector sc1
 // load (lane i <- producer i) and a ballot, so no atomic read-modify-write serialises
 // the arrivals.  flags[i] holds the number of steps producer i has published.
+// poll_wave: the wave that polls.  Its loads return in order, so any global load it issued
+// before the poll (a step's dy / gate-cache loads) holds the poll's first answer back until
+// that load is served; a wave that loads nothing else polls unhindered.
 __device__ __forceinline__ bool flags_wait(const unsigned* flags, int count, unsigned target,
-                                           unsigned* err, int* lds_flag) {
-  if (threadIdx.x < 64) {
-    const int lane = threadIdx.x;
+                                           unsigned* err, int* lds_flag, int poll_wave = 0) {
+  if ((threadIdx.x >> 6) == poll_wave) {
+    const int lane = threadIdx.x & 63;
     unsigned spins = 0;
     int ok = 1;
     if (g_spin_limit == 0) {   // fault injection
@@ -244,6 +253,7 @@ __device__ __forceinline__ bool flags_wait(const unsigned* flags, int count, uns
                           : target;
     };
     const unsigned gap = g_rnn_tune[4];
+    sleep_units(g_rnn_tune[5]);
     if (gap != 0u && ok) {
       // two polls in flight, `gap` apart: a flag set just after one poll passed the L2 is
       // seen by the other about half a round trip later instead of a full one
