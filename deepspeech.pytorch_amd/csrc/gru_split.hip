@@ -734,14 +734,15 @@ __global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
   int ub, d, bt;
   // xmode bit 0: same-XCD groups; bits 1 / 2: timing diagnostics only (DS2_GRU_BWD_DIAG,
   // results wrong): 2 skips the producer's store drain before its flag, 4 also every wait
-  const bool xg = !TAG && (xmode & 1) != 0;
+  const bool xgrp = (xmode & 1) != 0;   // the launch's workgroup -> (ub, d, bt) mapping
+  const bool xg = !TAG && xgrp;          // the same-XCD plain copies (not with TAG)
   const bool no_drain = (xmode & 2) != 0, no_wait = (xmode & 4) != 0;
   // the flags are polled by wave 0, which reaches the poll last (it publishes the record);
   // bit 3 (diagnostic) polls from the last wave instead, which starts polling as soon as its
   // step is done: 6.02 vs 4.99 us per step (profiles/r6j_gru_bwd_poll_ab.txt) -- early polls
   // only load the flag lines the producers are writing
   const int poll_wave = (xmode & 8) != 0 ? BW - 1 : 0;
-  if (xg ? !map_work_xgrp(UB, BT, D, ub, d, bt) : !map_work(UB * D, BT, UB, ub, d, bt)) return;
+  if (xgrp ? !map_work_xgrp(UB, BT, D, ub, d, bt) : !map_work(UB * D, BT, UB, ub, d, bt)) return;
   const int n0 = n_base + bt * GB;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -949,7 +950,12 @@ __global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
               }
               sleep_units(g_rnn_tune[0]);
               asm volatile("" ::: "memory");
+              // re-load p and every other stale record of the window in one pass, so their
+              // round trips overlap instead of following one another
               load_rec(p);
+#pragma unroll
+              for (int q = p + 1; q < NPW && q < p + LWP; ++q)
+                if (q < np && !rec_ready(q)) load_rec(q);
             }
           }
         }
