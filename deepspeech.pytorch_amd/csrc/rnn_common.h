@@ -163,14 +163,15 @@ static void apply_spin_limit_env() {
 // from every workgroup crowd the fabric that carries the real tiles).  Defaults from
 // scripts/gru_ab.py sweeps (the forward's first-poll delay 14 -> 10 with the same-XCD groups,
 // whose same-XCD tiles arrive sooner: 4.32-4.40 -> 4.26 us per step, `ftune`,
-// profiles/r3fa_fwd_tune.txt); [3] s_sleep(1) units between the flag hand-off's polls.
+// profiles/r3fa_fwd_tune.txt; the fp16x3 forward: 10 -> 7, 3.74-3.83 -> 3.74-3.75 us,
+// profiles/r6p_fwd_tune.txt); [3] s_sleep(1) units between the flag hand-off's polls.
 // [4]: the flag hand-off's second poll in flight, issued this many s_sleep(1) units after the
 // first (0: one poll at a time, each after the previous one returned).  [5]: s_sleep(1) units
 // before the flag hand-off's first poll of a step (polls before the group's last producer can
 // have published only load the flag lines that producers are writing).  [6]: s_sleep(1) units
 // before the tagged-record backward's first record loads of a step.
 // DS2_RNN_TUNE="a,b,c,d,e" overrides them (diagnostic; checked at every recurrence entry point).
-constexpr unsigned kRepollSleep = 1u, kFirstPollDelay = 10u, kFirstPollDelayBwd = 14u,
+constexpr unsigned kRepollSleep = 1u, kFirstPollDelay = 7u, kFirstPollDelayBwd = 14u,
                    kFlagPollSleep = 1u, kFlagPollGap = 0u, kFlagFirstDelay = 0u,
                    kTagFirstDelay = 0u;
 constexpr int kTuneN = 7;

@@ -59,7 +59,7 @@ if len(sys.argv) > 1 and sys.argv[1] == "xcd":
 if len(sys.argv) > 1 and sys.argv[1] == "ftune":
     # the sentinel forward's first-poll delay / re-poll sleep (s_sleep units)
     variants = {f"fwd-tune-{t}": {"DS2_GRU_X6": "1", "DS2_RNN_TUNE": t}
-                for t in ("1,14,14", "1,6,14", "1,10,14", "1,18,14", "0,10,14", "2,10,14")}
+                for t in ("1,10,14", "1,0,14", "1,4,14", "1,7,14", "1,14,14", "0,7,14", "2,7,14")}
 if len(sys.argv) > 1 and sys.argv[1] == "flagpoll":
     # s_sleep(1) units between the flag hand-off's polls (the pre-split backward's wait)
     variants = {f"bwd-poll-{t}": {"DS2_GRU_X6": "1", "DS2_RNN_TUNE": t}
