@@ -723,8 +723,10 @@ __global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
   constexpr int HB = NG == 3 ? HBR : (NG == 4 ? HBR4 : HBR1);   // record floats
   constexpr int NO = NG >= 3 ? 2048 : 0;       // byte offset of the n-layout tile (LSTM: hi (g, o))
   constexpr int SO = NG == 3 ? 3072 : (NG == 4 ? 4096 : 1024);  // ... of the row factors
-  // producers' records in flight per wave (the LSTM's 4-KB records: 2, within 256 VGPRs)
-  constexpr int LWP = NG == 4 ? (NPW < 2 ? NPW : 2) : (NPW < 3 ? NPW : 3);
+  // producers' records in flight per wave: 2 (GRU at cfg2: 4.84 us per step against 4.86
+  // with 1, 5.00 with 3 and 5.11 with 4 -- more loads in flight crowd the fabric the records
+  // cross; profiles/r6t_gru_bwd_window.txt; the LSTM's 4-KB records: 2 fit 256 VGPRs)
+  constexpr int LWP = NPW < 2 ? NPW : 2;
   constexpr int RED = BW * GB * RP > 8 * GB * GU ? BW * GB * RP : 8 * GB * GU;
   __shared__ __attribute__((aligned(8))) float red[RED];
   __shared__ __attribute__((aligned(16))) _Float16 stg[4 * 64 * 8];   // the record published
