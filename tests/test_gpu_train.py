@@ -78,6 +78,18 @@ def test_benchmark_train_step_matches_oracle(dev):
 
 
 @pytest.mark.timeout(600)
+@pytest.mark.parametrize("rnn_type", ["rnn", "lstm"])
+def test_benchmark_shape_train_step_other_rnn_types(dev, rnn_type):
+    """supported_rnns['rnn'] and ['lstm'] (model.py:14-15) at the benchmark shape: 5 x Bi-800,
+    T = 1001 (501 recurrent steps), bs 4 with the ragged quirk lengths -- the full train step
+    through the persistent fp16x3 one-gate / four-gate recurrences vs oracle.train_step, with
+    the bounds and the same-mask fp64 conv check of the GRU test above, and the float64 step as
+    the arbiter of recurrent gradients past 5e-4 (the LSTM's last layers: 5.2-5.6e-4)."""
+    _check_train_step(dev, [1001, 877, 508, 254], [150, 120, 80, 40], seed=11, conv_fp64=True,
+                      conv_tol=5e-2, rnn_type=rnn_type, rnn_fp64=True)
+
+
+@pytest.mark.timeout(600)
 def test_benchmark_train_step_two_batch_tiles(dev):
     """As above at bs 20: the persistent recurrences run TWO batch tiles (samples 0-15 and
     16-19, the second one partly empty) per direction, so the hand-off groups of both tiles,
@@ -140,15 +152,28 @@ def _conv_block_grads(sd, x, out_lens, g_out, dtype, masks=None):
     return {k: v.grad for k, v in params.items()}
 
 
+class _OracleF64(orc.OracleDS2):
+    """The oracle with its state in float64 (its ops follow the dtype of x and the state)."""
+
+    def __init__(self, *a, **k):
+        super().__init__(*a, **k)
+        self.sd = {kk: (v.double() if v.is_floating_point() else v) for kk, v in self.sd.items()}
+
+
 def _check_train_step(dev, t_list, label_lens, seed, conv_tol=5e-4, zero_conv_bias=False,
-                      conv_fp64=False):
+                      conv_fp64=False, rnn_type='gru', rnn_fp64=False):
+    """rnn_fp64: a recurrent / FC gradient past 5e-4 from the fp32 oracle still passes when it
+    sits within 2x (+1e-5) of the fp32 oracle's own distance from the same step in float64
+    (the oracle's state and input in float64): both are fp32 approximations of one exact
+    step, and over 501 recurrent steps the reference's own fp32 drifts."""
     _threads()
     g = torch.Generator().manual_seed(seed)
     x = _spect_batch(g, t_list, 1001)
     pct = torch.tensor([t / 1001.0 for t in t_list], dtype=torch.float32)
     tg, tl = _targets(g, label_lens)
-    m = _build(123456, 800, 5)
-    o = orc.OracleDS2({k: v.detach().clone() for k, v in m.state_dict().items()}, 5, 800)
+    m = _build(123456, 800, 5, rnn_type=rnn_type)
+    o = orc.OracleDS2({k: v.detach().clone() for k, v in m.state_dict().items()}, 5, 800,
+                      rnn_type=rnn_type)
     sd0 = {k: v.detach().clone() for k, v in m.state_dict().items()}
     before = {k: v.detach().clone() for k, v in m.named_parameters()}
     captured = {}
@@ -223,6 +248,10 @@ def _check_train_step(dev, t_list, label_lens, seed, conv_tol=5e-4, zero_conv_bi
     # (the conv fp64 verdict is asserted after the oracle comparison, so one run prints both)
     rloss, rnew, _, rgrads, rnorm = orc.train_step(o, x, pct.clone(), tg, tl)
     assert abs(loss - float(rloss)) <= 1e-4 * abs(float(rloss))
+    g64 = None
+    if rnn_fp64:
+        o64 = _OracleF64({k: v.detach().clone() for k, v in sd0.items()}, 5, 800, rnn_type=rnn_type)
+        _, _, _, g64, _ = orc.train_step(o64, x.double(), pct.clone(), tg, tl)
     # the clip norm within 2e-4: every gradient of ours carries the fp32 CTC's rounding (log-space
     # alpha / beta of magnitude ~nll, as warp-ctc's), the oracle's CTC runs in fp64 -- a uniform
     # ~1e-4 shift of all gradients (bs 4: norm 7.9e-5 for our fp32-MFMA path, 1.06e-4 for the
@@ -246,11 +275,16 @@ def _check_train_step(dev, t_list, label_lens, seed, conv_tol=5e-4, zero_conv_bi
                 bad_grads.append((name, worst[name]))
             continue
         worst[name] = _rel(p.grad, rgrads[name])
-        if worst[name] > tol:
+        exact_ok = False
+        if g64 is not None and not name.startswith('conv.') and worst[name] > tol:
+            ours64, own64 = _rel(p.grad, g64[name]), _rel(rgrads[name], g64[name])
+            exact_ok = ours64 <= 2.0 * own64 + 1e-5
+            print(f"fp64 check {name}: ours {ours64:.2e} fp32 oracle {own64:.2e}")
+        if worst[name] > tol and not exact_ok:
             bad_grads.append((name, worst[name]))
         # the update itself (p_new - p_old), not just p_new (dominated by p_old); both
         # differences carry the float32 rounding of p_new (half an ulp of |p| each)
-        if (d - rd).abs().max().item() > tol * rd.abs().max().item() + ulp:
+        if (d - rd).abs().max().item() > tol * rd.abs().max().item() + ulp and not exact_ok:
             bad_grads.append((name, 'update'))
     print("gradient distances from the oracle (max-abs / max-abs), largest first:",
           sorted(((round(v, 7), k) for k, v in worst.items()), reverse=True)[:12])
