@@ -90,6 +90,16 @@ def test_benchmark_shape_train_step_other_rnn_types(dev, rnn_type):
 
 
 @pytest.mark.timeout(600)
+@pytest.mark.parametrize("rnn_type", ["gru", "lstm"])
+def test_benchmark_shape_train_step_unidirectional_lookahead(dev, rnn_type):
+    """Unidirectional 5 x GRU / LSTM-800 with the Lookahead (context 20) + Hardtanh head of
+    model.py:329-333 at the benchmark shape (T = 1001, bs 4 ragged): the full train step vs
+    oracle.train_step, bounds and arbiters as above."""
+    _check_train_step(dev, [1001, 877, 508, 254], [150, 120, 80, 40], seed=11, conv_fp64=True,
+                      conv_tol=5e-2, rnn_type=rnn_type, rnn_fp64=True, bidirectional=False)
+
+
+@pytest.mark.timeout(600)
 def test_benchmark_train_step_two_batch_tiles(dev):
     """As above at bs 20: the persistent recurrences run TWO batch tiles (samples 0-15 and
     16-19, the second one partly empty) per direction, so the hand-off groups of both tiles,
@@ -161,7 +171,7 @@ class _OracleF64(orc.OracleDS2):
 
 
 def _check_train_step(dev, t_list, label_lens, seed, conv_tol=5e-4, zero_conv_bias=False,
-                      conv_fp64=False, rnn_type='gru', rnn_fp64=False):
+                      conv_fp64=False, rnn_type='gru', rnn_fp64=False, bidirectional=True):
     """rnn_fp64: a recurrent / FC gradient past 5e-4 from the fp32 oracle still passes when it
     sits within 2x (+1e-5) of the fp32 oracle's own distance from the same step in float64
     (the oracle's state and input in float64): both are fp32 approximations of one exact
@@ -171,9 +181,9 @@ def _check_train_step(dev, t_list, label_lens, seed, conv_tol=5e-4, zero_conv_bi
     x = _spect_batch(g, t_list, 1001)
     pct = torch.tensor([t / 1001.0 for t in t_list], dtype=torch.float32)
     tg, tl = _targets(g, label_lens)
-    m = _build(123456, 800, 5, rnn_type=rnn_type)
+    m = _build(123456, 800, 5, rnn_type=rnn_type, bidirectional=bidirectional)
     o = orc.OracleDS2({k: v.detach().clone() for k, v in m.state_dict().items()}, 5, 800,
-                      rnn_type=rnn_type)
+                      rnn_type=rnn_type, bidirectional=bidirectional)
     sd0 = {k: v.detach().clone() for k, v in m.state_dict().items()}
     before = {k: v.detach().clone() for k, v in m.named_parameters()}
     captured = {}
@@ -250,7 +260,8 @@ def _check_train_step(dev, t_list, label_lens, seed, conv_tol=5e-4, zero_conv_bi
     assert abs(loss - float(rloss)) <= 1e-4 * abs(float(rloss))
     g64 = None
     if rnn_fp64:
-        o64 = _OracleF64({k: v.detach().clone() for k, v in sd0.items()}, 5, 800, rnn_type=rnn_type)
+        o64 = _OracleF64({k: v.detach().clone() for k, v in sd0.items()}, 5, 800, rnn_type=rnn_type,
+                         bidirectional=bidirectional)
         _, _, _, g64, _ = orc.train_step(o64, x.double(), pct.clone(), tg, tl)
     # the clip norm within 2e-4: every gradient of ours carries the fp32 CTC's rounding (log-space
     # alpha / beta of magnitude ~nll, as warp-ctc's), the oracle's CTC runs in fp64 -- a uniform
