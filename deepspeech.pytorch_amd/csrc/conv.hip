@@ -1197,18 +1197,23 @@ __global__ void conv_h3_samax_kernel(const float* __restrict__ x, int64_t per,
   __shared__ float red[4];
   const int n = blockIdx.y;
   const float* xs = x + (int64_t)n * per;
-  const int64_t chunk = (per + gridDim.x - 1) / gridDim.x;
+  // chunks of a multiple of 4 elements, so that 16-B aligned samples take the float4 path
+  const int64_t chunk = (((per + gridDim.x - 1) / gridDim.x) + 3) & ~(int64_t)3;
   const int64_t b = (int64_t)blockIdx.x * chunk;
   const int64_t e = b + chunk < per ? b + chunk : per;
+  if (b >= e) return;   // block-uniform: past the sample's end after the rounding up
   float mx = 0.f;
-  if ((reinterpret_cast<uintptr_t>(xs + b) & 15) == 0 && (chunk & 3) == 0) {
+  if ((reinterpret_cast<uintptr_t>(xs + b) & 15) == 0) {
     const int64_t e4 = b + ((e - b) & ~(int64_t)3);
+    // unrolled: 8 loads in flight per thread (one at a time ran at ~2.5 TB/s)
+#pragma unroll 8
     for (int64_t i = b + 4 * threadIdx.x; i < e4; i += 4 * blockDim.x) {
       const float4 v = *reinterpret_cast<const float4*>(xs + i);
       mx = fmaxf(mx, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
     }
     for (int64_t i = e4 + threadIdx.x; i < e; i += blockDim.x) mx = fmaxf(mx, fabsf(xs[i]));
   } else {
+#pragma unroll 8
     for (int64_t i = b + threadIdx.x; i < e; i += blockDim.x) mx = fmaxf(mx, fabsf(xs[i]));
   }
   mx = wave_max(mx);
@@ -1231,12 +1236,15 @@ __global__ void conv_h3_chamax_kernel(const float* __restrict__ t, int N, int C,
   const int64_t b = (int64_t)blockIdx.x * chunk;
   const int64_t e = b + chunk < total ? b + chunk : total;
   float mx = 0.f;
-  int64_t i = b + threadIdx.x;
-  int64_t n = i / plane, pp = i - n * plane;
-  for (; i < e; i += blockDim.x) {
-    mx = fmaxf(mx, fabsf(t[(n * C + ch) * plane + pp]));
-    pp += blockDim.x;
-    while (pp >= plane) { pp -= plane; ++n; }
+  // the chunk walked sample by sample: inside one sample the channel's plane is contiguous,
+  // so the loop is a plain strided sweep with 8 loads in flight per thread
+  for (int64_t i = b; i < e;) {
+    const int64_t n = i / plane;
+    const int64_t seg = (n + 1) * plane < e ? (n + 1) * plane : e;
+    const float* base = t + (n * C + ch) * plane - n * plane;   // base[k]: element k
+#pragma unroll 8
+    for (int64_t k = i + threadIdx.x; k < seg; k += blockDim.x) mx = fmaxf(mx, fabsf(base[k]));
+    i = seg;
   }
   mx = wave_max(mx);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
