@@ -687,27 +687,11 @@ __global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
 // dgx receives dgates ([T][N][D][4H]); dgh and dbp are unused; the carried dc lives in a
 // register.  n_base: the first sample of this launch (the batch runs as consecutive chunks of
 // 16-sample tiles when one launch of all of them would not fit the chip).
-// TAG: RNE of an fp16 lo term, then moved one ulp toward the exact residual if its last bit is
-// not the tag's (tag 2: unconstrained).  |error| <= 1 ulp of lo (2^-21 of the value); +-0 with
-// tag 1 becomes +-2^-24.
-__device__ __forceinline__ _Float16 lo_tagged(float resid, unsigned tag) {
-  const _Float16 l = (_Float16)resid;
-  unsigned short b = __builtin_bit_cast(unsigned short, l);
-  if (tag < 2u && (b & 1u) != tag) {
-    if ((b & 0x7fffu) == 0u) {
-      b |= 1u;
-    } else {
-      const bool away = (resid - (float)l >= 0.f) == ((b & 0x8000u) == 0u);
-      b = away ? (unsigned short)(b + 1u) : (unsigned short)(b - 1u);
-    }
-  }
-  return __builtin_bit_cast(_Float16, b);
-}
 constexpr int HBR = 784;   // floats per producer record (3 x 256 + 16)
 constexpr int HBR1 = 272;  // the one-gate record (256 + 16)
 constexpr int HBR4 = 1040; // the LSTM record (4 x 256 + 16)
 typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
-template <int NPW, int NG = 3, bool TAG = false>
+template <int NPW, int NG = 3>
 __global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(2, 2))) void gru_bwd_h3_kernel(
     int T, int N, int H, int D, int UB, int BT, const float* __restrict__ dy, int dyd,
     const float* __restrict__ w_f, const float* __restrict__ w_r,
@@ -718,7 +702,6 @@ __global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     unsigned* __restrict__ camax, int n_base) {
   static_assert(NPW <= 8, "producers per wave");
   static_assert(NG == 3 || NG == 1 || NG == 4, "GRU, one-gate RNN or LSTM");
-  static_assert(!TAG || NG == 3, "the tagged-record hand-off is the GRU's");
   constexpr int RP = GU + 1;
   constexpr int HB = NG == 3 ? HBR : (NG == 4 ? HBR4 : HBR1);   // record floats
   constexpr int NO = NG >= 3 ? 2048 : 0;       // byte offset of the n-layout tile (LSTM: hi (g, o))
@@ -732,18 +715,16 @@ __global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
   __shared__ __attribute__((aligned(16))) _Float16 stg[4 * 64 * 8];   // the record published
   __shared__ __attribute__((aligned(16))) float stsc[GB];
   __shared__ int flag;
-  __shared__ int tfail;   // TAG: a wave's record poll timed out
   int ub, d, bt;
-  // xmode bit 0: same-XCD groups; bits 1 / 2: timing diagnostics only (DS2_GRU_BWD_DIAG,
-  // results wrong): 2 skips the producer's store drain before its flag, 4 also every wait
-  const bool xgrp = (xmode & 1) != 0;   // the launch's workgroup -> (ub, d, bt) mapping
-  const bool xg = !TAG && xgrp;          // the same-XCD plain copies (not with TAG)
-  const bool no_drain = (xmode & 2) != 0, no_wait = (xmode & 4) != 0;
-  // the flags are polled by wave 0, which reaches the poll last (it publishes the record);
-  // bit 3 (diagnostic) polls from the last wave instead, which starts polling as soon as its
-  // step is done: 6.02 vs 4.99 us per step (profiles/r6j_gru_bwd_poll_ab.txt) -- early polls
-  // only load the flag lines the producers are writing
-  const int poll_wave = (xmode & 8) != 0 ? BW - 1 : 0;
+  // xmode bit 0: same-XCD groups (the workgroup -> (ub, d, bt) mapping and the plain copies).
+  // The flags are polled by wave 0, which reaches the poll last (it publishes the record);
+  // polling from the last wave, which is done first, measured slower (6.02 vs 4.99 us per
+  // step, profiles/r6j_gru_bwd_poll_ab.txt): early polls only load the flag lines the
+  // producers are writing.  The round-5 timing diagnostics (no store drain, no wait:
+  // profiles/r6i_gru_bwd_handoff_bounds.txt) and the tagged-record hand-off (5.27-5.53 vs
+  // 5.00 us per step, profiles/r6m_gru_bwd_tagged_records_ab.txt) were removed in round 6.
+  const bool xgrp = (xmode & 1) != 0;
+  const bool xg = xgrp;
   if (xgrp ? !map_work_xgrp(UB, BT, D, ub, d, bt) : !map_work(UB * D, BT, UB, ub, d, bt)) return;
   const int n0 = n_base + bt * GB;
   const int lane = threadIdx.x & 63;
@@ -759,10 +740,9 @@ __global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
   const unsigned* gflags = counters + (D * BT + 1) + (d * BT + bt) * UB;
   unsigned* myflag = counters + (D * BT + 1) + (d * BT + bt) * UB + ub;
   const int slot_floats = D * BT * UB * HB;
-  // TAG: a 4-slot ring of tagged records (no flags, no plain copies); else 2 slots (+ 2 of
-  // plain copies with xmode)
+  // 2 slots (+ 2 of plain copies with xmode)
   const __amdgpu_buffer_rsrc_t x_rs = __builtin_amdgcn_make_buffer_rsrc(
-      gx, (short)0, (TAG ? 4 : (xg ? 4 : 2)) * slot_floats * 4, 0x00020000);
+      gx, (short)0, (xg ? 4 : 2) * slot_floats * 4, 0x00020000);
   const int grp_off = (d * BT + bt) * UB * HB;
   const int aoff = 2 * slot_floats * 4;   // the plain-store copies (xmode)
   const bool tracing = stamps != nullptr && threadIdx.x == 0;
@@ -854,10 +834,6 @@ __global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
   // camax: running max |.| of the unit's dar, daz, dan, dghn over the steps (the fp16x3
   // GEMMs' column scales of dgx / dgh, published at the end)
   float cm_r = 0.f, cm_z = 0.f, cm_n = 0.f, cm_hn = 0.f;
-  if (TAG) {
-    if (threadIdx.x == 0) tfail = 0;
-    __syncthreads();
-  }
   for (int s = 0; s < T; ++s) {
     const int t = d == 0 ? T - 1 - s : s;
     f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -888,7 +864,7 @@ __global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     }
     trace_at(s, 0);
     if (s > 0) {
-      if (!TAG && !no_wait && !flags_wait(gflags, UB, (unsigned)s, err, &flag, poll_wave)) {
+      if (!flags_wait(gflags, UB, (unsigned)s, err, &flag)) {
         poison_rest(dgx, s, T, d == 0, N, D, n, d, H, j, H3, NG, owner);
         return;
       }
@@ -901,9 +877,7 @@ __global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
         for (int p = 0; p < NPW; ++p)
           if ((same >> (p0 + p)) & 1ull) psame |= 1u << p;
       }
-      const int rb = ((s - 1) & (TAG ? 3 : 1)) * slot_floats + grp_off;
-      // TAG: the tag bit every 16-B run of a step s - 1 record carries
-      [[maybe_unused]] const unsigned want = ((unsigned)(s - 1) >> 2) & 1u;
+      const int rb = ((s - 1) & 1) * slot_floats + grp_off;
       u32x4 r0[NPW], r1[NPW], r2[NPW], r3[NPW];
       f32x4 rs[NPW];
       auto load_rec = [&](int p) {
@@ -923,16 +897,6 @@ __global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
         rs[p] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
                                               x_rs, ok ? base + SO + (lane >> 4) * 16 : 0x7ffffff0, 0, kSc1));
       };
-      // TAG: every run of producer p's record carries step s - 1's tag (lanes of producers past
-      // np count as ready)
-      auto rec_ready = [&](int p) {
-        const bool ok = p >= np ||
-                        (((r0[p][3] >> 16) & 1u) == want && ((r1[p][3] >> 16) & 1u) == want &&
-                         ((r2[p][3] >> 16) & 1u) == want &&
-                         (__builtin_bit_cast(u32x4, rs[p])[0] & 1u) == want);
-        return __ballot(!ok) == 0ull;
-      };
-      if (TAG) sleep_units(g_rnn_tune[6]);
 #pragma unroll
       for (int p = 0; p < LWP; ++p) load_rec(p);
       asm volatile("" ::: "memory");
@@ -940,27 +904,6 @@ __global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
 #pragma unroll
       for (int p = 0; p < NPW; ++p) {
         if (p + LWP < NPW) load_rec(p + LWP);
-        if constexpr (TAG) {
-          if (p < np) {
-            for (unsigned spins = 0; !rec_ready(p); ++spins) {
-              if (spins > g_spin_limit || g_spin_limit == 0) {
-                if (lane == 0) {
-                  __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                  tfail = 1;
-                }
-                break;
-              }
-              sleep_units(g_rnn_tune[0]);
-              asm volatile("" ::: "memory");
-              // re-load p and every other stale record of the window in one pass, so their
-              // round trips overlap instead of following one another
-              load_rec(p);
-#pragma unroll
-              for (int q = p + 1; q < NPW && q < p + LWP; ++q)
-                if (q < np && !rec_ready(q)) load_rec(q);
-            }
-          }
-        }
         if (p < np) {
           // big (hi.hi) and small (lo.hi + hi.lo) products in separate zero-C chains, and the
           // 16x16x16 n-gate products apart from the 16x16x32 ones (see mma3h; a 16x16x16 MFMA
@@ -969,11 +912,9 @@ __global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
           const f32x4 z4 = f32x4{0.f, 0.f, 0.f, 0.f};
           f32x4 tb = z4, ts = z4;
           if constexpr (NG >= 3) {
-            // TAG runs are {hi r, lo r} and {hi z, lo z}; else {hi r, hi z} and {lo r, lo z}
-            const f16x8 ahi = __builtin_bit_cast(
-                f16x8, TAG ? u32x4{r0[p][0], r0[p][1], r1[p][0], r1[p][1]} : r0[p]);
-            const f16x8 alo = __builtin_bit_cast(
-                f16x8, TAG ? u32x4{r0[p][2], r0[p][3], r1[p][2], r1[p][3]} : r1[p]);
+            // runs {hi r, hi z} and {lo r, lo z}
+            const f16x8 ahi = __builtin_bit_cast(f16x8, r0[p]);
+            const f16x8 alo = __builtin_bit_cast(f16x8, r1[p]);
             ts = __builtin_amdgcn_mfma_f32_16x16x32_f16(alo, wrz[p].hi, ts, 0, 0, 0);
             ts = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, wrz[p].lo, ts, 0, 0, 0);
             tb = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, wrz[p].hi, tb, 0, 0, 0);
@@ -995,12 +936,7 @@ __global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
             ts += ns;
           }
           const f32x4 tmp = tb + ts;
-          f32x4 sc4 = rs[p];
-          if constexpr (TAG) {   // the tag rides in bit 0 of the 2^-e words
-            const u32x4 sb = __builtin_bit_cast(u32x4, sc4);
-            sc4 = __builtin_bit_cast(f32x4, u32x4{sb[0] & ~1u, sb[1] & ~1u, sb[2] & ~1u, sb[3] & ~1u});
-          }
-          acc += tmp * sc4;   // rows 4 (lane >> 4) + i: the producer's 2^-e of those rows
+          acc += tmp * rs[p];   // rows 4 (lane >> 4) + i: the producer's 2^-e of those rows
         }
       }
       trace_at(s, 2);
@@ -1019,10 +955,6 @@ __global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
       settle(c_t);
     }
     __syncthreads();
-    if (TAG && tfail) {
-      poison_rest(dgx, s, T, d == 0, N, D, n, d, H, j, H3, NG, owner);
-      return;
-    }
     trace_at(s, 3);
     float dar = 0.f, daz = 0.f, dan = 0.f, dghn = 0.f;
     if (NG == 4 && owner) {
@@ -1096,23 +1028,11 @@ __global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
       if constexpr (NG == 4) mx = fmaxf(mx, fabsf(dan));
 #pragma unroll
       for (int o = 1; o < 16; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
-      // TAG: an all-zero row still carries the tag (a lo of +-2^-24); its factor 2^-127 sends
-      // that to zero in the consumer's sum
-      const int e = (TAG && mx == 0.f) ? 127 : h3_row_exp(mx);
+      const int e = h3_row_exp(mx);
       const float sc = __builtin_ldexpf(1.f, e);
       const float vr = dar * sc, vz = daz * sc, vn = dghn * sc;
       const _Float16 hr = (_Float16)vr, hz = (_Float16)vz, hn = (_Float16)vn;
-      if constexpr (TAG) {
-        // runs {hi r, lo r}, {hi z, lo z}, {hi n, lo n}; the lo in each run's last slot
-        // (k slot 3: u & 3 == 3) is rounded to the step's tag parity
-        const unsigned tg = (u & 3) == 3 ? (((unsigned)s >> 2) & 1u) : 2u;
-        stg[sL] = hr;
-        stg[sL + 4] = lo_tagged(vr - (float)hr, tg);
-        stg[512 + sL] = hz;
-        stg[512 + sL + 4] = lo_tagged(vz - (float)hz, tg);
-        stg[NO / 2 + sL] = hn;
-        stg[NO / 2 + sL + 4] = lo_tagged(vn - (float)hn, tg);
-      } else if constexpr (NG >= 3) {
+      if constexpr (NG >= 3) {
         stg[sL] = hr;
         stg[sL + 4] = hz;
         stg[512 + sL] = (_Float16)(vr - (float)hr);
@@ -1125,20 +1045,17 @@ __global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
         stg[1024 + sL + 4] = hn;
         stg[1536 + sL] = (_Float16)(vg - (float)hg);
         stg[1536 + sL + 4] = (_Float16)(vn - (float)hn);
-      } else if constexpr (!TAG) {
+      } else {
         stg[NO / 2 + sL] = hn;   // the n-layout tile (fp16 offset)
         stg[NO / 2 + sL + 4] = (_Float16)(vn - (float)hn);
       }
       if (u == 0) {
-        const float f = __builtin_ldexpf(1.f, -e);   // a power of two: bit 0 is free
-        stsc[m] = TAG ? __builtin_bit_cast(float, __builtin_bit_cast(unsigned, f) |
-                                                      (((unsigned)s >> 2) & 1u))
-                      : f;
+        stsc[m] = __builtin_ldexpf(1.f, -e);
       }
     }
     __syncthreads();
     if (wave == 0) {
-      const int so = ((s & (TAG ? 3 : 1)) * slot_floats + grp_off + ub * HB) * 4;
+      const int so = ((s & 1) * slot_floats + grp_off + ub * HB) * 4;
       // the record's 1-KB tiles: NG 3: (rz hi, rz lo, n); NG 4: (if hi, if lo, go hi, go lo);
       // NG 1: (n)
       constexpr int NT = NG == 4 ? 4 : (NG == 3 ? 3 : 1);
@@ -1155,11 +1072,9 @@ __global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
         __builtin_amdgcn_raw_buffer_store_b128(vs, x_rs, so + SO + lane * 16, 0, kSc1);
         if (xg) __builtin_amdgcn_raw_buffer_store_b128(vs, x_rs, aoff + so + SO + lane * 16, 0, 0);
       }
-      if constexpr (!TAG) {   // TAG: the runs are their own flags (no drain, no flag)
-        if (!no_drain) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (lane == 0)
-          __hip_atomic_store(myflag, (unsigned)s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0)
+        __hip_atomic_store(myflag, (unsigned)s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     trace_at(s, 4);
     if (NG == 1 && owner) {
@@ -1605,20 +1520,10 @@ static inline bool bwd_h3_enabled() {
   return !(e != nullptr && e[0] == '0');
 }
 
-// the tagged-record hand-off (DS2_GRU_BWD_TAG=1): every 16-B run of a record carries its
-// step's tag, so a producer publishes without a store drain or a flag and a consumer polls
-// the records themselves
-static inline bool bwd_tag_enabled() {
-  const char* e = getenv("DS2_GRU_BWD_TAG");
-  return e != nullptr && e[0] == '1';
-}
-
-static const void* bwd_h3_fn(int UB, bool tag) {
+static const void* bwd_h3_fn(int UB) {
   const int need = (UB + BW - 1) / BW;
-#define DS2_BH3(K)                                                                         \
-  if (need <= K)                                                                           \
-    return tag ? reinterpret_cast<const void*>(gru_bwd_h3_kernel<K, 3, true>)              \
-               : reinterpret_cast<const void*>(gru_bwd_h3_kernel<K>);
+#define DS2_BH3(K) \
+  if (need <= K) return reinterpret_cast<const void*>(gru_bwd_h3_kernel<K>);
   DS2_BH3(1) DS2_BH3(2) DS2_BH3(3) DS2_BH3(4) DS2_BH3(5) DS2_BH3(6) DS2_BH3(7) DS2_BH3(8)
 #undef DS2_BH3
   return nullptr;
@@ -1637,22 +1542,12 @@ bool launch_gru_bwd_x6(int t_max, int n, int h, int num_dirs, const float* dy, i
   apply_spin_limit_env();
   apply_rnn_tune_env();
   const int UB = h / GU, BT = (n + GB - 1) / GB;
-  const bool tag = bwd_tag_enabled();
-  const void* fn = bwd_h3_enabled() ? bwd_h3_fn(UB, tag) : nullptr;
+  const void* fn = bwd_h3_enabled() ? bwd_h3_fn(UB) : nullptr;
   const bool h3 = fn != nullptr;
-  if (h3 && tag) {
-    // every run starts with tag bit 1: records of steps 0-3 carry 0, so none reads as published
-    const size_t slot = (size_t)num_dirs * BT * UB * HBR * sizeof(float);
-    if (hipMemsetAsync(ring, 0xFF, 4 * slot, st) != hipSuccess) return false;
-  }
   if (fn == nullptr) fn = bwd_x6_fn((3 * UB + 1) / 2);
   if (fn == nullptr) return false;
   int XM_ = xcd_groups(UB, BT, num_dirs) ? 1 : 0;
   const int grid = XM_ ? xgrp_grid(UB, BT, num_dirs) : mapped_grid(UB * num_dirs, BT);
-  if (h3) {   // timing diagnostics (gru_bwd_h3_kernel's xmode bits 1-2; results wrong)
-    const char* dg = getenv("DS2_GRU_BWD_DIAG");
-    if (dg != nullptr) XM_ |= (atoi(dg) & 7) << 1;
-  }
   int T_ = t_max, N_ = n, H_ = h, D_ = num_dirs, UB_ = UB, BT_ = BT, DYD_ = dy_dirs, NB_ = 0;
   void* args[] = {&T_, &N_, &H_, &D_, &UB_, &BT_, &dy, &DYD_, &w_hh_f, &w_hh_r, &h_all,
                   &gates, &lens, &dgates_x, &dgates_h, &ring, &ctrs, &err, &stamps, &dbp, &XM_,

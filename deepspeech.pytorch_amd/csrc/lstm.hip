@@ -1035,10 +1035,14 @@ static int lstm_h1_launch_grid(int t_max, int n, int h, int num_dirs) {
   return g > 0 && g <= num_cus() ? g : 0;
 }
 
+// ds2_lstm_bwd_half falls back to ds2_lstm_bwd when the single-term launch declines at run time
+// (t_max past the 32-bit offset bound, a failed launch); that kernel's 16-sample tiles can hold
+// more workgroups, so report the larger grid: the CU guard never budgets for fewer than run
 int ds2_lstm_bwd_half_grid(int n, int h, int num_dirs) {
   if (n < 1 || h < 1 || (num_dirs != 1 && num_dirs != 2)) return 0;
   const int g = lstm_h1_launch_grid(1, n, h, num_dirs);
-  return g > 0 ? g : ds2_lstm_bwd_grid(n, h, num_dirs);
+  const int f = ds2_lstm_bwd_grid(n, h, num_dirs);
+  return g > f ? g : f;
 }
 
 ds2_status_t ds2_lstm_bwd_half(int t_max, int n, int h, int num_dirs, const float* dy, int dy_dirs,

@@ -168,24 +168,20 @@ static void apply_spin_limit_env() {
 // [4]: the flag hand-off's second poll in flight, issued this many s_sleep(1) units after the
 // first (0: one poll at a time, each after the previous one returned).  [5]: s_sleep(1) units
 // before the flag hand-off's first poll of a step (polls before the group's last producer can
-// have published only load the flag lines that producers are writing).  [6]: s_sleep(1) units
-// before the tagged-record backward's first record loads of a step.
+// have published only load the flag lines that producers are writing).
 // DS2_RNN_TUNE="a,b,c,d,e" overrides them (diagnostic; checked at every recurrence entry point).
 constexpr unsigned kRepollSleep = 1u, kFirstPollDelay = 7u, kFirstPollDelayBwd = 14u,
-                   kFlagPollSleep = 1u, kFlagPollGap = 0u, kFlagFirstDelay = 0u,
-                   kTagFirstDelay = 0u;
-constexpr int kTuneN = 7;
+                   kFlagPollSleep = 1u, kFlagPollGap = 0u, kFlagFirstDelay = 0u;
+constexpr int kTuneN = 6;
 static __constant__ unsigned g_rnn_tune[kTuneN] = {kRepollSleep, kFirstPollDelay,
                                                    kFirstPollDelayBwd, kFlagPollSleep,
-                                                   kFlagPollGap, kFlagFirstDelay,
-                                                   kTagFirstDelay};
+                                                   kFlagPollGap, kFlagFirstDelay};
 
 static void apply_rnn_tune_env() {
   static unsigned applied[kTuneN] = {kRepollSleep, kFirstPollDelay, kFirstPollDelayBwd,
-                                     kFlagPollSleep, kFlagPollGap, kFlagFirstDelay,
-                                     kTagFirstDelay};
+                                     kFlagPollSleep, kFlagPollGap, kFlagFirstDelay};
   unsigned v[kTuneN] = {kRepollSleep, kFirstPollDelay, kFirstPollDelayBwd, kFlagPollSleep,
-                        kFlagPollGap, kFlagFirstDelay, kTagFirstDelay};
+                        kFlagPollGap, kFlagFirstDelay};
   const char* e = getenv("DS2_RNN_TUNE");
   for (int i = 0; e != nullptr && e[0] != 0 && i < kTuneN; ++i) {
     char* end = nullptr;

@@ -109,21 +109,44 @@ class BeamCTCDecoder(Decoder):
                                        blank=self.blank_index, cutoff_top_n=self.cutoff_top_n,
                                        cutoff_prob=self.cutoff_prob)
 
+    def convert_to_strings(self, out, seq_len):
+        """[batch][beam][T] label ids (ctcdecode's ``beam_results``) and [batch][beam]
+        lengths -> [batch][beam] strings; a beam of length <= 0 is ''.  Ref
+        decoder.py:101-113 (tensors, numpy arrays or nested lists)."""
+        results = []
+        for b, batch in enumerate(out):
+            utterances = []
+            for p, utt in enumerate(batch):
+                size = int(seq_len[b][p])
+                row = np.asarray(utt[0:size] if size > 0 else [], dtype=np.int64)
+                utterances.append(self._row_string(row) if size > 0 else '')
+            results.append(utterances)
+        return results
+
+    def convert_tensor(self, offsets, sizes):
+        """[batch][beam][T] frame offsets and [batch][beam] lengths -> per beam the first
+        ``size`` offsets (an empty int tensor for size <= 0).  Ref decoder.py:115-126."""
+        results = []
+        for b, batch in enumerate(offsets):
+            utterances = []
+            for p, utt in enumerate(batch):
+                size = int(sizes[b][p])
+                if size > 0:
+                    utterances.append(utt[0:size])
+                else:
+                    utterances.append(torch.tensor([], dtype=torch.int))
+            results.append(utterances)
+        return results
+
     def decode(self, probs, sizes=None):
+        """Ref decoder.py:128-143: (strings, offsets) per utterance and beam, best first;
+        the reference's ``convert_to_strings`` / ``convert_tensor`` over the device search's
+        (ids, offsets, lens), with one device->host copy and vectorised id->char lookups (a
+        per-element tensor loop cost more than the beam search itself on 30 s utterances)."""
         ids, offs, lens, _ = self.decode_raw(probs, sizes)
-        # one device->host copy, then vectorised id->char lookups (a per-element tensor
-        # loop here cost more than the beam search itself on 30 s utterances)
         ids, offs, lens = ids.cpu().numpy(), offs.cpu().numpy(), lens.cpu().numpy()
-        strings, offsets = [], []
-        for b in range(ids.shape[0]):
-            sb, ob = [], []
-            for p in range(ids.shape[1]):
-                k = int(lens[b, p])
-                sb.append(self._row_string(ids[b, p, :k]))
-                ob.append(torch.from_numpy(offs[b, p, :k].copy()) if k > 0
-                          else torch.tensor([], dtype=torch.int))
-            strings.append(sb)
-            offsets.append(ob)
+        strings = self.convert_to_strings(ids, lens)
+        offsets = self.convert_tensor(torch.from_numpy(offs), lens)
         return strings, offsets
 
 

@@ -394,9 +394,14 @@ class RingTrafficStandIn:
 
     def run(self, bucket: torch.Tensor):
         count = bucket.numel()
-        chunk = (count + self.world - 1) // self.world
+        # the kernel's chunk: ceil(floor(count / 4) / world) float4s (ds2_test_ring_traffic)
+        chunk = 4 * ((count // 4 + self.world - 1) // self.world)
         if self.scratch is None or self.scratch.numel() < chunk:
+            if self.scratch is not None:
+                # the side stream may still be reading the old buffer
+                torch.cuda.current_stream(self.device).wait_stream(self.stream)
             self.scratch = torch.zeros(chunk, dtype=torch.float32, device=self.device)
+            self.scratch.record_stream(self.stream)
         ready = torch.cuda.Event()
         ready.record()
         self.stream.wait_event(ready)

@@ -174,11 +174,12 @@ class Trainer:
 
     # ---- deferred status --------------------------------------------------------------
     def _pack_status(self, tail):
-        """The last bucket's tail slots (GradAllReducer.set_status_packer): this rank's
-        recurrence status word (as a float: summed over the ranks it is non-zero iff any
-        rank's word is) and its loss (summed, then scaled by 1/world with the gradients:
-        reduce_tensor, data/utils.py:40-44)."""
-        tail[0:1].copy_(self._rnn_word)
+        """The last bucket's tail slots (GradAllReducer.set_status_packer): whether this
+        rank's recurrence status word is non-zero (a FLAG, 1.0 or 0.0, not the bitmask: summed
+        over the ranks it is non-zero iff any rank failed, whatever bits a word carries; each
+        rank decodes its own word from ``_rnn_word``) and its loss (summed, then scaled by
+        1/world with the gradients: reduce_tensor, data/utils.py:40-44)."""
+        tail[0:1].copy_(self._rnn_word != 0)
         tail[1:2].copy_(self._step_loss)
 
     def _record_status(self, loss, global_word=None):

@@ -68,24 +68,10 @@ if len(sys.argv) > 1 and sys.argv[1] == "flagpipe":
     # the flag hand-off with a second poll in flight, issued G s_sleep(1) units after the first
     # (0: one poll at a time)
     variants = {f"bwd-pipe-{g}": {"DS2_RNN_TUNE": f"1,10,14,1,{g}"} for g in ("0", "4", "8", "14", "20")}
-if len(sys.argv) > 1 and sys.argv[1] == "bwddiag":
-    # timing diagnostics of the fp16x3 backward's flag hand-off (results wrong for 1 and 3):
-    # 1 = no store drain before the producer's flag, 3 = no drain and no consumer wait
-    variants = {f"bwd-diag-{v}": {"DS2_GRU_BWD_DIAG": v} for v in ("0", "1", "3")}
-if len(sys.argv) > 1 and sys.argv[1] == "pollwave":
-    # the backward's flag poll on the last wave (0, default) vs wave 0, which also issues the
-    # step's dy / gate-cache loads (4)
-    variants = {f"bwd-pollwave-{v}": {"DS2_GRU_BWD_DIAG": v} for v in ("4", "0")}
 if len(sys.argv) > 1 and sys.argv[1] == "flagdelay":
     # s_sleep(1) units before the backward's first flag poll of a step ([5]) and between polls ([3])
     variants = {f"bwd-flagdelay-{t}": {"DS2_RNN_TUNE": f"1,10,14,{t}"}
                 for t in ("1,0,0", "1,0,8", "1,0,16", "1,0,24", "2,0,16", "4,0,16")}
-if len(sys.argv) > 1 and sys.argv[1] == "tag":
-    # the fp16x3 backward's flag hand-off vs tagged records (DS2_GRU_BWD_TAG=1), the latter with
-    # s_sleep(1) units before a step's first record loads (DS2_RNN_TUNE [6])
-    variants = {"bwd-flag": {"DS2_GRU_BWD_TAG": "0", "DS2_RNN_TUNE": ""}}
-    for t in ("0", "4", "8", "14"):
-        variants[f"bwd-tag-{t}"] = {"DS2_GRU_BWD_TAG": "1", "DS2_RNN_TUNE": f"1,10,14,1,0,0,{t}"}
 rounds = int(os.environ.get("AB_ROUNDS", "3"))
 variants = {f"{k}#{r}": v for r in range(rounds) for k, v in variants.items()}
 ref = None

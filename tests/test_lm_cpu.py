@@ -270,3 +270,25 @@ def test_beam_trie_revival_keeps_prefixes_unique():
             strings = [tuple(ids) for _, ids, _ in out]
             assert len(set(strings)) == len(strings)
         assert ctc_beam.STATS["revived"] > 0, use_lm
+
+
+def test_beam_decoder_convert_helpers():
+    """BeamCTCDecoder.convert_to_strings / convert_tensor (ref decoder.py:101-126): ctcdecode's
+    [batch][beam][T] ids / offsets cut at [batch][beam] lengths; a beam of length <= 0 gives
+    '' and an empty int tensor.  Host-only: the constructor touches no device."""
+    import torch
+    from ds2amd.decoder import BeamCTCDecoder
+    dec = BeamCTCDecoder(LABELS, beam_width=4)
+    out = torch.tensor([[[2, 3, 4, 0], [5, 0, 0, 0]], [[1, 1, 7, 8], [9, 9, 9, 9]]])
+    lens = torch.tensor([[3, 0], [4, 2]])
+    want = [[''.join(LABELS[i] for i in (2, 3, 4)), ''],
+            [''.join(LABELS[i] for i in (1, 1, 7, 8)), LABELS[9] * 2]]
+    assert dec.convert_to_strings(out, lens) == want
+    # nested lists and numpy arrays, as ctcdecode callers pass them, give the same strings
+    assert dec.convert_to_strings(out.tolist(), lens.tolist()) == want
+    assert dec.convert_to_strings(out.numpy(), lens.numpy()) == want
+    offs = torch.arange(16, dtype=torch.int32).reshape(2, 2, 4)
+    got = dec.convert_tensor(offs, lens)
+    assert got[0][0].tolist() == [0, 1, 2] and got[1][0].tolist() == [8, 9, 10, 11]
+    assert got[1][1].tolist() == [12, 13]
+    assert got[0][1].numel() == 0 and got[0][1].dtype == torch.int
