@@ -1071,6 +1071,21 @@ bool launch_rnn_bwd_h3(int t_max, int n, int h, int num_dirs, const float* dy, i
                        unsigned long long* stamps, size_t lds_pad, hipStream_t st,
                        unsigned* camax);
 int rnn_h3_grid(int n, int h, int num_dirs);
+// gru_xl.hip: the XCD-local groups (default where the shape fits: 32 units x 8 samples per
+// workgroup, a group of H / 32 workgroups in one XCD)
+int gru_xl_groups(int n, int h, int num_dirs);
+int gru_xl_active(int n, int h, int num_dirs);
+size_t gru_xl_ctr_words();
+bool launch_gru_fwd_xl(int t_max, int n, int h, int num_dirs, const float* xproj,
+                       const float* w_hh_f, const float* w_hh_r, const float* b_hh_f,
+                       const float* b_hh_r, const int* lens, float* h_all, float* gates,
+                       float* ring, unsigned* xl, unsigned* err, unsigned long long* stamps,
+                       size_t lds_pad, hipStream_t st);
+bool launch_gru_bwd_xl(int t_max, int n, int h, int num_dirs, const float* dy, int dy_dirs,
+                       const float* w_hh_f, const float* w_hh_r, const float* h_all,
+                       const float* gates, const int* lens, float* dgates_x, float* dgates_h,
+                       float* ring, unsigned* xl, unsigned* err, unsigned long long* stamps,
+                       double* dbp, size_t lds_pad, hipStream_t st, unsigned* camax);
 }  // namespace ds2
 
 using namespace ds2;
@@ -1093,10 +1108,12 @@ static const void* bwd_dop_fn(int need) {
   return nullptr;
 }
 // group counters, the error word, 64 per-producer flags per group, then 64 per-producer XCC
-// ids per group (the same-XCD groups of gru_split.hip)
+// ids per group (the same-XCD groups of gru_split.hip); the XCD-local kernels (gru_xl.hip) use
+// gru_xl_ctr_words() words after the error word instead
 static inline size_t ctr_words(int n, int num_dirs) {
   const int groups = num_dirs * ((n + GB - 1) / GB);
-  return (size_t)groups + 1 + (size_t)groups * 128;
+  const size_t a = (size_t)groups * 128, b = gru_xl_ctr_words();
+  return (size_t)groups + 1 + (a > b ? a : b);
 }
 static inline size_t counter_bytes(int n, int num_dirs) {
   const size_t trace = stamp_mode() == 2 ? (size_t)kTraceSteps * 1024 * 5 : 16;
@@ -1191,6 +1208,12 @@ ds2_status_t ds2_gru_fwd(int t_max, int n, int h, int num_dirs, const float* xpr
     void* args[] = {&T_, &N_, &H_, &D_, &UB_, &BT_, &xproj, &w_hh_f, &w_hh_r, &b_hh_f,
                     &b_hh_r, &lens, &h_all, &gates, &ring, &ctrs, &err, &stamps};
     if (ring_reset(ring, n, h, num_dirs, st) != hipSuccess) return launch_status("ds2_gru ring");
+    if (launch_gru_fwd_xl(t_max, n, h, num_dirs, xproj, w_hh_f, w_hh_r, b_hh_f, b_hh_r, lens,
+                          h_all, gates, ring, err + 1, err, stamps, kDopPadLds, st)) {
+      fold_err(err, err_out, st);
+      return launch_status("ds2_gru_fwd");
+    }
+    (void)hipGetLastError();
     if (launch_gru_fwd_x6(t_max, n, h, num_dirs, xproj, w_hh_f, w_hh_r, b_hh_f, b_hh_r, lens,
                           h_all, gates, ring, ctrs, err, stamps, kDopPadLds, st)) {
       fold_err(err, err_out, st);
@@ -1258,8 +1281,9 @@ static size_t gru_bwd_ws_base(int n, int h, int num_dirs) {
 }
 
 // bias-gradient partial sums [batch tile][direction][4][H] fp64, at the end of the workspace
+// (8-sample tiles: the XCD-local kernel's; the 16-sample kernels use the first half)
 static size_t gru_db_bytes(int n, int h, int num_dirs) {
-  return align256((size_t)((n + GB - 1) / GB) * num_dirs * 4 * h * sizeof(double));
+  return align256((size_t)((n + 7) / 8) * num_dirs * 4 * h * sizeof(double));
 }
 
 size_t ds2_gru_bwd_workspace_size(int n, int h, int num_dirs) {
@@ -1281,10 +1305,13 @@ int ds2_gru_bwd_grid(int n, int h, int num_dirs) {
   const int grid = mapped_grid(UB * num_dirs, BT);
   if (!persistent_enabled() || grid > num_cus()) return 0;
   if ((h % GU) == 0 && UB <= 8 * GW) {
-    // the x6 launch may decline at run time and fall back to the direct-operand kernel at
-    // `grid`: report the larger so the CU guard never budgets for fewer workgroups than run
+    // the XCD-local or x6 launch may decline at run time and fall back to the direct-operand
+    // kernel at `grid`: report the largest so the CU guard never budgets for fewer workgroups
+    // than run
     const int g = gru_bwd_x6_grid(n, h, num_dirs);
-    return g > grid ? g : grid;
+    const int x = gru_xl_active(n, h, num_dirs);
+    const int m = g > x ? g : x;
+    return m > grid ? m : grid;
   }
   return (3 * h <= KC_BWD && (h % 4) == 0) ? grid : 0;
 }
@@ -1304,7 +1331,8 @@ static ds2_status_t gru_bwd_run(int t_max, int n, int h, int num_dirs, const flo
                                 const float* w_hh_f, const float* w_hh_r, const float* h_all,
                                 const float* gates, const int* lens, float* dgates_x,
                                 float* dgates_h, unsigned* err_out, void* ws, hipStream_t st,
-                                double* dbp, bool& summed, unsigned* camax, bool& camax_done);
+                                double* dbp, bool& summed, unsigned* camax, bool& camax_done,
+                                int& db_tiles);
 
 static ds2_status_t gru_bwd_bias_impl(int t_max, int n, int h, int num_dirs, const float* dy,
                                       int dy_dirs, const float* w_hh_f, const float* w_hh_r,
@@ -1368,9 +1396,10 @@ static ds2_status_t gru_bwd_bias_impl(int t_max, int n, int h, int num_dirs, con
     return launch_status("ds2_gru_bwd_bias");
   }
   bool summed = false, camax_done = false;
+  int db_tiles = (n + GB - 1) / GB;
   const ds2_status_t rc = gru_bwd_run(t_max, n, h, num_dirs, dy, dy_dirs, w_hh_f, w_hh_r, h_all,
                                       gates, lens, dgates_x, dgates_h, err_out, ws, st,
-                                      want_db ? dbp : nullptr, summed, camax, camax_done);
+                                      want_db ? dbp : nullptr, summed, camax, camax_done, db_tiles);
   if (rc != DS2_OK) return rc;
   if (camax != nullptr && !camax_done) {
     // a kernel without the fused maxima ran: one column pass over each of dgx, dgh
@@ -1382,7 +1411,7 @@ static ds2_status_t gru_bwd_bias_impl(int t_max, int n, int h, int num_dirs, con
     if (rb != DS2_OK) return rb;
   }
   if (!want_db) return DS2_OK;
-  int bt = (n + GB - 1) / GB;
+  int bt = db_tiles;
   if (!summed) {
     hipLaunchKernelGGL(gru_db_cols_kernel, dim3(num_dirs * 4 * h), dim3(256), 0, st, dgates_x,
                        dgates_h, t_max * n, num_dirs, h, dbp);
@@ -1397,7 +1426,8 @@ static ds2_status_t gru_bwd_run(int t_max, int n, int h, int num_dirs, const flo
                                 const float* w_hh_f, const float* w_hh_r, const float* h_all,
                                 const float* gates, const int* lens, float* dgates_x,
                                 float* dgates_h, unsigned* err_out, void* ws, hipStream_t st,
-                                double* dbp, bool& summed, unsigned* camax, bool& camax_done) {
+                                double* dbp, bool& summed, unsigned* camax, bool& camax_done,
+                                int& db_tiles) {
   if (num_dirs == 1) w_hh_r = w_hh_f;
   apply_spin_limit_env();
   apply_rnn_tune_env();
@@ -1425,6 +1455,16 @@ static ds2_status_t gru_bwd_run(int t_max, int n, int h, int num_dirs, const flo
                                            align256(counter_bytes(n, num_dirs)));
     void* args[] = {&T_, &N_, &H_, &D_, &UB_, &BT_, &dy, &DYD_, &w_hh_f, &w_hh_r, &h_all,
                     &gates, &lens, &dgates_x, &dgates_h, &ring, &ctrs, &err, &stamps, &dbp};
+    if (launch_gru_bwd_xl(t_max, n, h, num_dirs, dy, dy_dirs, w_hh_f, w_hh_r, h_all, gates,
+                          lens, dgates_x, dgates_h, ring, err + 1, err, stamps, dbp, kDopPadLds,
+                          st, camax)) {
+      fold_err(err, err_out, st);
+      summed = dbp != nullptr;
+      camax_done = camax != nullptr;
+      db_tiles = (n + 7) / 8;
+      return launch_status("ds2_gru_bwd");
+    }
+    (void)hipGetLastError();
     if (launch_gru_bwd_x6(t_max, n, h, num_dirs, dy, dy_dirs, w_hh_f, w_hh_r, h_all, gates,
                           lens, dgates_x, dgates_h, ring, ctrs, err, stamps, dbp, kDopPadLds, st,
                           camax, &camax_done)) {

@@ -38,6 +38,22 @@ def bwd():
               dgh.data_ptr(), None, wsb.data_ptr(), wsb.numel(), ops._stream())
 
 
+def xl_modes():
+    """The XCD-local kernels' per-group mode words (1 LOCAL, 2 GLOBAL, 3 mixed) of the last
+    forward and backward launches, read from the workspaces' counter area."""
+    if os.environ.get("DS2_GRU_XL", "1")[:1] == "0":
+        return ""
+    al = lambda x: (x + 255) & ~255
+    UB, BT = (H + 15) // 16, (N + 15) // 16
+    cf = al(D * UB * ((H + 3) // 4) * 3 * 64 * 4)
+    cb = al(D * UB * ((3 * H + 3) // 4) * 64 * 4) + al(2 * N * D * H * 4)
+    out = []
+    for ws, c in ((wsf, cf), (wsb, cb)):
+        words = ws[c:c + 4 * (D * BT + 1 + 520)].view(torch.int32).cpu()
+        out.append(words[D * BT + 1 + 512: D * BT + 1 + 520].tolist())
+    return f"  modes fwd {out[0]} bwd {out[1]}"
+
+
 def timed(fn, reps=5):
     fn()
     torch.cuda.synchronize()
@@ -72,6 +88,18 @@ if len(sys.argv) > 1 and sys.argv[1] == "flagdelay":
     # s_sleep(1) units before the backward's first flag poll of a step ([5]) and between polls ([3])
     variants = {f"bwd-flagdelay-{t}": {"DS2_RNN_TUNE": f"1,10,14,{t}"}
                 for t in ("1,0,0", "1,0,8", "1,0,16", "1,0,24", "2,0,16", "4,0,16")}
+if len(sys.argv) > 1 and sys.argv[1] == "xl":
+    # the XCD-local kernels (gru_xl.hip) LOCAL (plain stores, default), forced GLOBAL (sc1), and
+    # the 16-unit fp16x3 kernels they replace
+    variants = {"xl-local": {"DS2_GRU_XL": "1", "DS2_RNN_TUNE": ""},
+                "xl-global": {"DS2_GRU_XL": "2", "DS2_RNN_TUNE": ""},
+                "16unit": {"DS2_GRU_XL": "0", "DS2_RNN_TUNE": ""}}
+if len(sys.argv) > 1 and sys.argv[1] == "xlonly":
+    variants = {"xl-local": {"DS2_GRU_XL": "1", "DS2_RNN_TUNE": ""}}
+if len(sys.argv) > 1 and sys.argv[1] == "xltune":
+    # the XCD-local forward's first-poll delay / re-poll sleep (s_sleep units)
+    variants = {f"xl-tune-{t}": {"DS2_GRU_XL": "1", "DS2_RNN_TUNE": t}
+                for t in ("1,7,14", "1,0,14", "1,3,14", "0,0,14", "0,3,14", "2,3,14")}
 rounds = int(os.environ.get("AB_ROUNDS", "3"))
 variants = {f"{k}#{r}": v for r in range(rounds) for k, v in variants.items()}
 ref = None
@@ -86,4 +114,4 @@ for name, env in variants.items():
     dh = (out_h - ref[0]).abs().max().item()
     dg = (out_g - ref[1]).abs().max().item() / max(ref[1].abs().max().item(), 1e-30)
     print(f"{name:12s} fwd {tf * 1e3:8.1f} us ({tf * 1e3 / T:5.2f}/step)  bwd {tb * 1e3:8.1f} us "
-          f"({tb * 1e3 / T:5.2f}/step)  max|dh| {dh:.2e} rel|ddgx| {dg:.2e}", flush=True)
+          f"({tb * 1e3 / T:5.2f}/step)  max|dh| {dh:.2e} rel|ddgx| {dg:.2e}{xl_modes()}", flush=True)

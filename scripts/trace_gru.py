@@ -33,6 +33,11 @@ G = D * BT
 # same-XCD groups (the default where they tile the XCDs; DS2_GRU_XCD=0 the interleaved layout)
 XG = os.environ.get("DS2_GRU_XCD", "1")[:1] != "0" and 8 % G == 0 and UB % (8 // G) == 0
 grid = 8 * (UB // (8 // G)) if XG else 8 * ((P + 7) // 8) * BT
+# the XCD-local kernels (gru_xl.hip, the default at this shape; DS2_GRU_XL=0 the 16-unit ones):
+# 32 units x 8 samples per workgroup, group = blocks with equal b % 8, grid 8 x H / 32
+XL = os.environ.get("DS2_GRU_XL", "1")[:1] != "0" and H % 32 == 0 and D * ((N + 7) // 8) <= 8
+if XL:
+    grid = 8 * (H // 32)
 for it in range(3):
     _lib.call("ds2_gru_fwd", T, N, H, D, xproj.data_ptr(), w[0].data_ptr(), w[1].data_ptr(),
               b[0].data_ptr(), b[1].data_ptr(), lens.data_ptr(), h_all.data_ptr(),
@@ -50,12 +55,25 @@ for it in range(3):
 #              stage = UB records of 3.06 KB; MFMA = per wave 7 producers x (3 x 16 + 3 x 8)
 #              cycles, two waves per SIMD
 CLK_GHZ = 2.0
-FLOORS = {
+if XL:
+    # stage: UBX tiles of 1 KB (forward) / records of 3.1 KB (backward) from the XCD's own L2
+    # (handoff-payload same-XCD 104-122 GB/s per block); MFMA: per wave 7 producers x 12
+    # v_mfma_f32_16x16x32_f16 (16 cycles each), one wave per SIMD
+    UBX = H // 32
+    FLOORS = {
+        "forward": {"wait": (1.0, 1.4), "stage": (UBX * 1024 / 122e3, UBX * 1024 / 104e3),
+                    "mfma": (7 * 12 * 16 / (CLK_GHZ * 1e3),) * 2},
+        "backward": {"wait": (1.3, 2.5), "stage": (UBX * 3136 / 122e3, UBX * 3136 / 104e3),
+                     "mfma": (7 * 12 * 16 / (CLK_GHZ * 1e3),) * 2},
+    }
+FLOORS_16 = {
     "forward": {"wait": (1.0, 1.4), "stage": (UB * 1024 / 122e3, UB * 1024 / 62e3),
                 "mfma": (7 * 3 * 3 * 16 / (CLK_GHZ * 1e3),) * 2},
     "backward": {"wait": (1.3, 2.5), "stage": (UB * 3136 / 122e3, UB * 3136 / 62e3),
                  "mfma": (2 * 7 * (3 * 16 + 3 * 8) / (CLK_GHZ * 1e3),) * 2},
 }
+if not XL:
+    FLOORS = FLOORS_16
 
 
 def analyse(tr, label):
@@ -67,6 +85,10 @@ def analyse(tr, label):
     groups = {}
     for wg in range(grid):
         xcd, slot = wg & 7, wg >> 3
+        if XL:
+            if xcd < D * ((N + 7) // 8):
+                groups.setdefault((xcd // ((N + 7) // 8), xcd % ((N + 7) // 8)), []).append(wg)
+            continue
         if XG:
             q = xcd // (8 // G)
             groups.setdefault((q // BT, q % BT), []).append(wg)
@@ -114,7 +136,43 @@ def analyse(tr, label):
         print(f"xcd {x}: stage {st[:, cols].mean():.2f} us, mfma {((ph[..., 3] - ph[..., 2]) * ticks_us)[:, cols].mean():.2f} us, wait {((ph[..., 1] - ph[..., 0]) * ticks_us)[:, cols].mean():.2f}")
 
 
-analyse(ws[off:off + NS * grid * 5 * 8].view(torch.int64).cpu().numpy().reshape(NS, grid, 5), "forward")
+def analyse_xl(tr, label):
+    """The XCD-local kernels' per-wave stamps [step][block][wave][6]: step start, hand-off wait
+    done, products done, io done, reduction barrier done, published."""
+    print(f"--- {label} (XCD-local, per wave)")
+    fl = FLOORS.get(label)
+    if fl is not None:
+        print("floors (us, MI355X_MICROARCH): " + ", ".join(
+            f"{k} {a:.2f}-{b:.2f}" for k, (a, b) in fl.items()))
+    G = D * ((N + 7) // 8)
+    act = [b for b in range(grid) if (b & 7) < G]
+    t = tr[:, act].astype(np.float64) * 0.01          # us
+    ph = t[1:NS - 1]
+    names = ["wait", "products", "io", "reduction barrier", "pointwise+publish"]
+    for w in range(4):
+        d_ = np.diff(ph[:, :, w, :], axis=-1)
+        print(f"wave {w}: " + ", ".join(f"{nm} {d_[..., i].mean():.2f}" for i, nm in enumerate(names)))
+    step = (t[2:NS, :, 0, 0] - t[1:NS - 1, :, 0, 0]).mean()
+    print("step length (us): mean %.2f" % step)
+    # per group: the last publish of step s -> each consumer's products done at s + 1
+    rows = []
+    for gq in range(G):
+        bl = [i for i, b in enumerate(act) if (b & 7) == gq]
+        for s_ in range(1, NS - 2):
+            pub = t[s_, bl, 0, 5]
+            nxt = t[s_ + 1, bl, :, 2].max(axis=1)
+            rows.append(((pub.max() - pub.min()), (nxt.mean() - pub.max())))
+    r = np.array(rows)
+    print("publish skew within a group %.2f us; last publish -> consumers' products done %.2f us"
+          % tuple(r.mean(0)))
+
+
+if XL:
+    analyse_xl(ws[off:off + NS * grid * 24 * 8].view(torch.int64).cpu().numpy().reshape(NS, grid, 4, 6),
+               "forward")
+else:
+    analyse(ws[off:off + NS * grid * 5 * 8].view(torch.int64).cpu().numpy().reshape(NS, grid, 5),
+            "forward")
 dy = torch.randn(T, N, H, device=dev)
 dgx = torch.empty(T, N, D, 3 * H, device=dev)
 dgh = torch.empty(T, N, D, 3 * H, device=dev)
@@ -126,4 +184,9 @@ for it in range(3):
     torch.cuda.synchronize()
 KS3 = (3 * H + 3) // 4
 offb = al(D * UB * KS3 * 64 * 4) + al(2 * N * D * H * 4) + al((D * BT + 1 + D * BT * 128) * 4)
-analyse(wsb[offb:offb + NS * grid * 5 * 8].view(torch.int64).cpu().numpy().reshape(NS, grid, 5), "backward")
+if XL:
+    analyse_xl(wsb[offb:offb + NS * grid * 24 * 8].view(torch.int64).cpu().numpy().reshape(NS, grid, 4, 6),
+               "backward")
+else:
+    analyse(wsb[offb:offb + NS * grid * 5 * 8].view(torch.int64).cpu().numpy().reshape(NS, grid, 5),
+            "backward")

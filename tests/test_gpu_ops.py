@@ -667,11 +667,45 @@ def test_gru_xcd_groups_bit_identical(dev, n, h, bidir, kern, monkeypatch):
     (default) and the bf16x6 ones."""
     nd = 2 if bidir else 1
     f = "1" if kern == "h3" else "0"
+    monkeypatch.setenv("DS2_GRU_XL", "0")    # the 16-unit kernels' groups
     monkeypatch.setenv("DS2_GRU_H3", f)
     monkeypatch.setenv("DS2_GRU_H3_BWD", f)
     env = [{"DS2_GRU_XCD": "1"}, {"DS2_GRU_XCD": "0"}]
     xg, il = _gru_run(dev, n, 37, 40, h, nd, h + 13 * n, env, monkeypatch)
     for a, b in zip(xg, il):
+        assert torch.isfinite(a).all()
+        assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("n,h,bidir", [(32, 800, True), (13, 800, True), (20, 64, True),
+                                       (64, 256, False), (8, 32, False), (3, 96, True)])
+def test_gru_xl_matches_16unit_kernels(dev, n, h, bidir, monkeypatch):
+    """The XCD-local recurrences (gru_xl.hip: 32 units x 8 samples per workgroup, a group of
+    H / 32 workgroups in one XCD, stacked (hi; lo) fp16 fragments; the default where they fit)
+    against the 16-unit fp16x3 kernels (DS2_GRU_XL=0) and the fp32-MFMA ones (DS2_GRU_X6=0):
+    equal within fp32 rounding, ragged lengths, partial batch tiles (13, 3 samples), one and
+    two directions, 1 to 25 producers per group; a second XL run is bit-identical (the sums
+    run in a fixed producer order whatever the arrival order)."""
+    nd = 2 if bidir else 1
+    env = [{"DS2_GRU_XL": "1"}, {"DS2_GRU_XL": "1"}, {"DS2_GRU_XL": "0"},
+           {"DS2_GRU_XL": "1", "DS2_GRU_X6": "0"}]
+    xl, xl2, h3, f32 = _gru_run(dev, n, 41, 40, h, nd, h + 11 * n, env, monkeypatch)
+    for a, b, c, d in zip(xl, xl2, h3, f32):
+        assert torch.isfinite(a).all()
+        assert torch.equal(a, b)
+        _close(a, c, 2e-5, "XCD-local vs 16-unit fp16x3")
+        _close(a, d, 2e-5, "XCD-local vs fp32 MFMA")
+
+
+@pytest.mark.parametrize("n,h,bidir", [(32, 800, True), (64, 256, False)])
+def test_gru_xl_local_equals_global(dev, n, h, bidir, monkeypatch):
+    """A group whose workgroups share one XCD publishes with plain stores (kept in that XCD's
+    L2); DS2_GRU_XL=2 makes every group publish write-through (sc1), the placement-independent
+    form it falls back to when its members' XCC ids differ: same bytes, bit-identical."""
+    nd = 2 if bidir else 1
+    env = [{"DS2_GRU_XL": "1"}, {"DS2_GRU_XL": "2"}]
+    loc, glob = _gru_run(dev, n, 37, 40, h, nd, h + 5 * n, env, monkeypatch)
+    for a, b in zip(loc, glob):
         assert torch.isfinite(a).all()
         assert torch.equal(a, b)
 

@@ -465,6 +465,107 @@ def test_world1_nccl_trainer_hooks_and_bit_identity(dev, golden_dir, tmp_path, m
         dist.destroy_process_group()
 
 
+def _dp_batch(rank):
+    """The world-2 test's 4-utterance batch (2 per rank), as the collate function gives it."""
+    g = torch.Generator().manual_seed(77)
+    x = _spect_batch(g, [64, 60, 52, 40], 64)
+    targets, tsz = _targets(g, [9, 7, 6, 4])
+    pct = torch.tensor([64, 60, 52, 40], dtype=torch.float32) / 64
+    lo, hi = 2 * rank, 2 * rank + 2
+    off = int(tsz[:lo].sum())
+    return (x[lo:hi].clone(), targets[off:off + int(tsz[lo:hi].sum())].clone(), None,
+            pct[lo:hi].clone(), tsz[lo:hi].clone())
+
+
+def _dp_worker(rank, world, port, out_q):
+    """One rank of test_world2_gloo_hip_trainer: the HIP Trainer on cuda:0 under a gloo process
+    group (device tensors), two steps on its half of the batch."""
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda:0")
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        tr = Trainer(_build(1234, 32, 2), LABELS, device=dev, bucket_mb=0.05)
+        nparam = tr.flat.numel
+        out = {"buckets": len(tr.reducer.buckets), "hooks": bool(tr.reducer._hooks),
+               "bcast0": tr.sync.broadcasts, "steps": []}
+        for step in range(2):
+            loss = tr.train_batch(_dp_batch(rank), return_item=True)
+            rec = {"loss": loss, "grad": tr.flat.grad[:nparam].cpu().numpy().copy(),
+                   "tail": tr.flat.tail.cpu().tolist(),
+                   "params": tr.flat.flat[:nparam].cpu().numpy().copy(),
+                   "issued": tr.reducer.issued_from_hooks, "colls": tr.reducer.collectives,
+                   "bufs_before": tr.sync.flat_buffers.cpu().numpy().copy()}
+            # DDP's broadcast_buffers: the next forward starts from rank 0's BN running stats
+            tr.sync.before_forward()
+            rec["bufs_after"] = tr.sync.flat_buffers.cpu().numpy().copy()
+            rec["bcast"] = tr.sync.broadcasts
+            out["steps"].append(rec)
+        torch.cuda.synchronize()
+        out_q.put((rank, out))
+    finally:
+        ops.set_cooperative_guard(None)
+        dist.destroy_process_group()
+
+
+def test_world2_gloo_hip_trainer(dev):
+    """the HIP Trainer at world 2 -- two spawned processes on cuda:0, a gloo
+    process group carrying the device gradient buckets (the closest to cfg3 one GPU allows;
+    train.py:804-809, 947-951, data/utils.py:40-44).  Each rank steps a 2-layer BiGRU-32 DS2
+    on its 2 utterances.  Checked against single-process Trainers on each half: the reduced
+    gradient equals (g0 + g1) / 2 bit for bit (DDP's average; BatchNorm statistics stay local
+    as in DDP), every bucket's all-reduce was issued from the backward hooks, one collective
+    per bucket (the status flag and the loss ride in the last one's tail: flag 0, the mean of
+    the two ranks' losses), the parameters agree across ranks after both steps, and rank 0's
+    BN running statistics reach rank 1 before the next forward."""
+    import torch.multiprocessing as mp
+    import socket
+    refs = []
+    for r in range(2):
+        tr = Trainer(_build(1234, 32, 2), LABELS, device=dev, bucket_mb=0.05)
+        lr = tr.train_batch(_dp_batch(r), return_item=True)
+        refs.append((lr, tr.flat.grad[:tr.flat.numel].cpu().clone()))
+    want = ((refs[0][1] + refs[1][1]) * 0.5).numpy()
+    sock = socket.socket()
+    sock.bind(("127.0.0.1", 0))
+    port = sock.getsockname()[1]
+    sock.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_dp_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    try:
+        res = dict(q.get(timeout=240) for _ in range(2))
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    assert all(p.exitcode == 0 for p in procs)
+    for r in range(2):
+        o = res[r]
+        assert o["hooks"] and o["buckets"] > 1
+        for k, st in enumerate(o["steps"]):
+            assert st["issued"] == o["buckets"], "every bucket issued from a backward hook"
+            assert st["colls"] == o["buckets"], "one collective per bucket"
+            assert st["tail"][0] == 0.0, "status flag clean"
+            assert st["tail"][1] == st["loss"], "the returned loss is the tail's mean"
+            assert st["loss"] == res[1 - r]["steps"][k]["loss"]
+            assert st["bcast"] == o["bcast0"] + 2 * k + 2
+            np.testing.assert_array_equal(st["bufs_after"], res[0]["steps"][k]["bufs_before"])
+        np.testing.assert_array_equal(o["steps"][0]["grad"], want)
+        # reduce_tensor: the mean of the two ranks' batch-mean losses
+        assert o["steps"][0]["loss"] == pytest.approx((refs[0][0] + refs[1][0]) / 2, rel=1e-6)
+    for k in range(2):
+        np.testing.assert_array_equal(res[0]["steps"][k]["params"], res[1]["steps"][k]["params"])
+        np.testing.assert_array_equal(res[0]["steps"][k]["grad"], res[1]["steps"][k]["grad"])
+    # local BN: the two ranks' running statistics differ after a step, until the broadcast
+    assert not np.array_equal(res[0]["steps"][0]["bufs_before"], res[1]["steps"][0]["bufs_before"])
+
+
 # --------------------------------------------------------------------------- cfg4 / cfg5 shapes
 def test_cfg5_30s_eval_forward_and_beam10(dev):
     """cfg5's defining shape: 30 s utterances (T = 3001, T' = 1501) through 5 x BiGRU-800 in
@@ -554,25 +655,28 @@ def test_cfg4_lstm1024_bf16_gemms_and_batch64_chunks(dev):
 
 
 @pytest.mark.timeout(900)
-def test_cfg4_full_shape_bf16_step(dev):
+@pytest.mark.parametrize("bidir", [True, False])
+def test_cfg4_full_shape_bf16_step(dev, bidir):
     """BASELINE cfg4 at its own shape (VERDICT r4 #5b): 7 x BiLSTM-1024, batch 64, 10 s
     (T = 1001 -> T' = 501), the opt-in bf16 RNN GEMMs, through Trainer.train_batch (forward,
     CTC, BPTT, clip, SGD-Nesterov): every gradient finite; deterministic (the same step from
     the same state twice: loss, gradients and updated parameters bit-identical); the loss
     within 1 % of the fp32 HIP path's on the same batch; and a 2-layer slice of the same
     weights (conv, rnns.0-1, fc) in bf16 mode against the fp32 oracle forward at full length
-    (logits 2e-2, CTC loss 1 %, the existing bf16 bounds)."""
+    (logits 2e-2, CTC loss 1 %, the existing bf16 bounds).  bidir=False: cfg4's
+    unidirectional variant, 7 x LSTM-1024 + Lookahead (+ Hardtanh) before the FC
+    (model.py:140-177, 329-333; VERDICT r5 missing #4), same checks."""
     _threads()
     from ds2amd.ctc import CTCLoss
     g = torch.Generator().manual_seed(404)
     x = _spect_batch(g, [1001] * 64, 1001)
     pct = torch.ones(64)
     tg, tl = _targets(g, [150] * 64)
-    m0 = _build(4040, 1024, 7, rnn_type='lstm')
+    m0 = _build(4040, 1024, 7, rnn_type='lstm', bidirectional=bidir)
     sd0 = {k: v.detach().clone() for k, v in m0.state_dict().items()}
 
     def step(precision):
-        m = _build(4040, 1024, 7, rnn_type='lstm')
+        m = _build(4040, 1024, 7, rnn_type='lstm', bidirectional=bidir)
         m.load_state_dict(sd0)
         if precision == 'bf16':
             m.set_rnn_gemm_precision('bf16')
@@ -594,12 +698,12 @@ def test_cfg4_full_shape_bf16_step(dev):
     assert (g16a - g32).norm().item() <= 5e-2 * g32.norm().item()
     del g16a, g32, p16a
     # 2-layer slice vs the fp32 oracle, 4 utterances at full length
-    m2 = _build(4040, 1024, 2, rnn_type='lstm')
+    m2 = _build(4040, 1024, 2, rnn_type='lstm', bidirectional=bidir)
     m2.load_state_dict({k: v for k, v in sd0.items() if k in m2.state_dict()})
     m2 = m2.to(dev).train()
     m2.set_rnn_gemm_precision('bf16')
     o2 = orc.OracleDS2({k: v.detach().cpu().clone() for k, v in m2.state_dict().items()}, 2,
-                       1024, rnn_type='lstm')
+                       1024, rnn_type='lstm', bidirectional=bidir)
     xb, sb = x[:4], torch.full((4,), 1001, dtype=torch.int32)
     with torch.no_grad():
         l2, _, ol = m2(xb.to(dev), sb)
