@@ -77,6 +77,11 @@ def gru_fwd_kernel(x6f: bool):
     """(peak, arithmetic, kernel name) of the GRU forward recurrence as configured: fp16x3 by
     default (gru_split.hip), bf16x6 with DS2_GRU_H3=0, the fp32-MFMA kernel with
     DS2_GRU_X6=0."""
+    if x6f and _env_on("DS2_GRU_H3") and _env_on("DS2_GRU_XL"):
+        return (PEAK_H3_TFLOPS, "W_hh contraction, fp16x3 (fp32-accurate: per-row scaled fp16 "
+                "hi/lo, the 8 samples' hi and lo stacked in one 16-row fragment: 2 "
+                "v_mfma_f32_16x16x32_f16 per k-step and column tile), XCD-local groups of "
+                "32-unit x 8-sample workgroups (gru_xl.hip)", "gru_fwd_xl_kernel")
     if x6f and _env_on("DS2_GRU_H3"):
         return (PEAK_H3_TFLOPS, "W_hh contraction, fp16x3 (fp32-accurate: per-row scaled fp16 "
                 "hi/lo, 3 products) on v_mfma_f32_16x16x32_f16", "gru_fwd_x6_kernel")
@@ -90,6 +95,11 @@ def gru_bwd_kernel(x6f: bool):
     """(peak, arithmetic, kernel name) of the GRU backward recurrence as configured: fp16x3
     records by default (gru_bwd_h3_kernel), the pre-split bf16x6 kernel with DS2_GRU_H3_BWD=0,
     the fp32-MFMA kernel with DS2_GRU_X6=0."""
+    if x6f and _env_on("DS2_GRU_H3_BWD") and _env_on("DS2_GRU_XL"):
+        return (PEAK_H3_TFLOPS, "W_hh^T contraction, fp16x3 (one record of stacked per-row "
+                "scaled fp16 hi/lo fragments per producer and step; 4 v_mfma_f32_16x16x32_f16 "
+                "per gate and 16 columns), XCD-local groups of 32-unit x 8-sample workgroups "
+                "(gru_xl.hip)", "gru_bwd_xl_kernel")
     if x6f and _env_on("DS2_GRU_H3_BWD"):
         return (PEAK_H3_TFLOPS, "W_hh^T contraction, fp16x3 (one per-row scaled fp16 hi/lo "
                 "record per producer and step) on v_mfma_f32_16x16x32_f16 / 16x16x16f16",

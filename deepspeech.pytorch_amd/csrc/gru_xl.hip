@@ -327,7 +327,7 @@ __global__ __launch_bounds__(LT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     if (s > 0) {
       trace_at(s, 1);
       const int base = (((s - 1) % LSLOTS) * slot_floats + grp_off + p0 * 256 + lane * 4) * 4;
-      sleep_units(g_rnn_tune[1]);
+      sleep_units(g_rnn_tune[7]);
       u32x4 hv[NPW + 1];
 #pragma unroll
       for (int p = 0; p < NPW + 1; ++p)
@@ -353,11 +353,15 @@ __global__ __launch_bounds__(LT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
             asm volatile("" ::: "memory");
 #pragma unroll
             for (int q = p; q < NPW + 1; ++q)
-              if (q < np) hv[q] = __builtin_amdgcn_raw_buffer_load_b128(x_rs, base + q * 1024, 0, kSc1);
+              if (q < np && (unsigned)(q - p) < g_rnn_tune[6])
+                hv[q] = __builtin_amdgcn_raw_buffer_load_b128(x_rs, base + q * 1024, 0, kSc1);
           }
           const f16x8 a = __builtin_bit_cast(f16x8, hv[p]);
 #pragma unroll
-          for (int ct = 0; ct < NCT; ++ct) {   // small products first (mma3h's order)
+          for (int ct = 0; ct < NCT; ++ct) {
+            // one chain over the producers, small products first (mma3h's order).  Per-producer
+            // zero-C chains joined by the VALU (the backward's form) moved the bs-32 step's
+            // bias gradients by 3 % and cost 0.6 us per step: the adds wait on each MFMA
             const Duo wf = wfr(p, ct);
             acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, wf.lo, acc[ct], 0, 0, 0);
             acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, wf.hi, acc[ct], 0, 0, 0);
@@ -438,6 +442,8 @@ __global__ __launch_bounds__(LT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
 // 32 rows of that gate block in the consumer's 16 columns, each column scaled by 2^e(unit)
 // (its max over the whole 3H).  Per record: 12 MFMAs from zero C, (C1 + C2) scaled per row and
 // added to the wave's partial in producer order.
+// Per-producer flags: the records as their own flags (the forward's sentinel ring over 3.1-KB
+// records, no drain and no flag) measured 5.3-5.5 vs 3.8 us per step and was removed.
 template <int NPW>
 __global__ __launch_bounds__(LT) __attribute__((amdgpu_waves_per_eu(1, 1))) void gru_bwd_xl_kernel(
     int T, int N, int H, int D, int UBX, int BTX, const float* __restrict__ dy, int dyd,
@@ -471,14 +477,14 @@ __global__ __launch_bounds__(LT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   const int p0 = wave * (UBX / LW) + min(wave, UBX % LW);
   const int np = UBX / LW + (wave < UBX % LW ? 1 : 0);   // host guarantees np <= NPW + 1
   const int H3 = 3 * H;
-  const bool local = xl_group_local(xl + g * 32, ub, UBX, err, &sh_local, xl + 512 + g, force_global);
-  unsigned* flags = xl + 256 + g * 32;
-  const __amdgpu_buffer_rsrc_t f_rs =
-      __builtin_amdgcn_make_buffer_rsrc(xl + 256, (short)0, 8 * 32 * 4, 0x00020000);
   const int slot_floats = G * UBX * LRB;
   const __amdgpu_buffer_rsrc_t x_rs =
       __builtin_amdgcn_make_buffer_rsrc(ring, (short)0, 2 * slot_floats * 4, 0x00020000);
   const int grp_off = g * UBX * LRB;
+  const bool local = xl_group_local(xl + g * 32, ub, UBX, err, &sh_local, xl + 512 + g, force_global);
+  unsigned* flags = xl + 256 + g * 32;
+  const __amdgpu_buffer_rsrc_t f_rs =
+      __builtin_amdgcn_make_buffer_rsrc(xl + 256, (short)0, 8 * 32 * 4, 0x00020000);
   // per-wave timeline (DS2_GRU_STAMPS=2): [step][block][wave][6] = step start, hand-off wait
   // done, products done, io done (waves 1-3), reduction barrier done, published; lane 0 of
   // every wave (scripts/trace_gru.py)
@@ -895,7 +901,8 @@ static const void* bwd_xl_fn(int UBX) {
   return nullptr;
 }
 
-// ring bytes: forward 4 slots of 1-KB tiles, backward 2 slots of records
+// ring bytes: forward 4 slots of 1-KB tiles, backward 2 slots of records (both within the
+// rings ds2_gru_fwd / ds2_gru_bwd carve for the 16-unit kernels)
 size_t gru_xl_ring_bytes(int n, int h, int num_dirs, bool bwd) {
   const size_t UBX = h / LU, G = (size_t)num_dirs * ((n + LB - 1) / LB);
   return bwd ? 2 * G * UBX * LRB * sizeof(float) : LSLOTS * G * UBX * 256 * sizeof(float);

@@ -168,20 +168,26 @@ static void apply_spin_limit_env() {
 // [4]: the flag hand-off's second poll in flight, issued this many s_sleep(1) units after the
 // first (0: one poll at a time, each after the previous one returned).  [5]: s_sleep(1) units
 // before the flag hand-off's first poll of a step (polls before the group's last producer can
-// have published only load the flag lines that producers are writing).
+// have published only load the flag lines that producers are writing).  [6]: tiles the
+// XCD-local forward re-loads per stale pass, from the one it waits on, and [7] its first-poll
+// delay (gru_xl.hip; scripts/gru_ab.py xlrepoll: every pending tile with no delay 3.38 us per
+// step, one tile 3.46, every tile after 7 units 3.62).
 // DS2_RNN_TUNE="a,b,c,d,e" overrides them (diagnostic; checked at every recurrence entry point).
 constexpr unsigned kRepollSleep = 1u, kFirstPollDelay = 7u, kFirstPollDelayBwd = 14u,
-                   kFlagPollSleep = 1u, kFlagPollGap = 0u, kFlagFirstDelay = 0u;
-constexpr int kTuneN = 6;
+                   kFlagPollSleep = 1u, kFlagPollGap = 0u, kFlagFirstDelay = 0u, kXlRepoll = 8u,
+                   kXlFirstDelay = 0u;
+constexpr int kTuneN = 8;
 static __constant__ unsigned g_rnn_tune[kTuneN] = {kRepollSleep, kFirstPollDelay,
                                                    kFirstPollDelayBwd, kFlagPollSleep,
-                                                   kFlagPollGap, kFlagFirstDelay};
+                                                   kFlagPollGap, kFlagFirstDelay, kXlRepoll,
+                                                   kXlFirstDelay};
 
 static void apply_rnn_tune_env() {
   static unsigned applied[kTuneN] = {kRepollSleep, kFirstPollDelay, kFirstPollDelayBwd,
-                                     kFlagPollSleep, kFlagPollGap, kFlagFirstDelay};
+                                     kFlagPollSleep, kFlagPollGap, kFlagFirstDelay, kXlRepoll,
+                                     kXlFirstDelay};
   unsigned v[kTuneN] = {kRepollSleep, kFirstPollDelay, kFirstPollDelayBwd, kFlagPollSleep,
-                        kFlagPollGap, kFlagFirstDelay};
+                        kFlagPollGap, kFlagFirstDelay, kXlRepoll, kXlFirstDelay};
   const char* e = getenv("DS2_RNN_TUNE");
   for (int i = 0; e != nullptr && e[0] != 0 && i < kTuneN; ++i) {
     char* end = nullptr;

@@ -135,7 +135,7 @@ def input_sizes_quirk(input_percentages: torch.Tensor, t_max: int) -> torch.Tens
 def _mask_time(x: torch.Tensor, lens: torch.Tensor) -> torch.Tensor:
     """MaskConv mask (model.py:69-78) as a bool mask."""
     t = x.shape[-1]
-    m = torch.arange(t)[None, :] >= lens[:, None].long()
+    m = torch.arange(t, device=x.device)[None, :] >= lens.to(x.device)[:, None].long()
     return x.masked_fill(m[:, None, None, :], 0)
 
 
@@ -314,8 +314,8 @@ def train_step(model: OracleDS2, x, input_percentages, targets, target_sizes, lr
         acts = acts.clone()
         acts[torch.isnan(acts)] = 0
     lp = F.log_softmax(acts, dim=2)
-    loss = F.ctc_loss(lp, targets.long(), out_lens.long(), target_sizes.long(), blank=0,
-                      reduction='sum') / x.shape[0]
+    loss = F.ctc_loss(lp, targets.long().to(lp.device), out_lens.long(), target_sizes.long(),
+                      blank=0, reduction='sum') / x.shape[0]
     loss.backward()
     grads = {k: v.grad.detach().clone() for k, v in params.items()}
     # clip_grad_norm_ (train.py:622-623)

@@ -94,6 +94,11 @@ if len(sys.argv) > 1 and sys.argv[1] == "xl":
     variants = {"xl-local": {"DS2_GRU_XL": "1", "DS2_RNN_TUNE": ""},
                 "xl-global": {"DS2_GRU_XL": "2", "DS2_RNN_TUNE": ""},
                 "16unit": {"DS2_GRU_XL": "0", "DS2_RNN_TUNE": ""}}
+if len(sys.argv) > 1 and sys.argv[1] == "xlrepoll":
+    # the XCD-local forward: tiles re-loaded per stale pass (DS2_RNN_TUNE [6]) x first-poll delay
+    variants = {f"xl-rp-{t}": {"DS2_GRU_XL": "1", "DS2_RNN_TUNE": t}
+                for t in ("1,7,14,1,0,0,8,7", "1,7,14,1,0,0,1,0", "1,7,14,1,0,0,2,0",
+                          "1,7,14,1,0,0,1,3", "0,7,14,1,0,0,1,0", "1,7,14,1,0,0,8,0")}
 if len(sys.argv) > 1 and sys.argv[1] == "xlonly":
     variants = {"xl-local": {"DS2_GRU_XL": "1", "DS2_RNN_TUNE": ""}}
 if len(sys.argv) > 1 and sys.argv[1] == "xltune":
