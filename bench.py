@@ -166,7 +166,7 @@ class KernelProbe:
         return sum(ms) / len(ms), sum(self.flops) / len(self.flops), len(ms)
 
 
-PMC_SUMMARY = "r7a_pmc_traffic.csv"   # profiles/: PMC passes on the round-5 final tree
+PMC_SUMMARY = "r8o_pmc_traffic.csv"   # profiles/: PMC passes on the XCD-local GRU tree (round 6)
 
 
 def pmc_traffic_per_launch(prefix="gemm", extra=("splitk_reduce_kernel",)):
