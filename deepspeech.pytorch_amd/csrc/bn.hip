@@ -14,6 +14,7 @@
 //   planes : x is [outer][C][D][T] (BatchNorm2d, model.py:210,213)
 //            block = one (outer, channel) plane slice, threads stride along T
 #include "common.h"
+#include "amax_rc.h"
 
 namespace ds2 {
 
@@ -582,6 +583,22 @@ ds2_status_t ds2_bn_apply(const float* x, int outer, int c, int inner, const flo
     hipLaunchKernelGGL(apply_generic_kernel, dim3(grid_cap(total, 256)), dim3(256), 0, st, x,
                        total, c, (int64_t)inner, mean, invstd, gamma, beta, y);
   return launch_status("ds2_bn_apply");
+}
+
+ds2_status_t ds2_bn_apply_amax(const float* x, int rows, int c, const float* mean,
+                               const float* invstd, const float* gamma, const float* beta,
+                               float* y, unsigned* row_amax, unsigned* col_amax,
+                               ds2_stream_t stream) {
+  if (rows < 0 || c < 1 || row_amax == nullptr || col_amax == nullptr) return DS2_INVALID_VALUE;
+  if (rows == 0) return DS2_OK;
+  const uintptr_t al = reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y) |
+                       reinterpret_cast<uintptr_t>(mean) | reinterpret_cast<uintptr_t>(invstd) |
+                       reinterpret_cast<uintptr_t>(gamma) | reinterpret_cast<uintptr_t>(beta);
+  if ((c % 4) != 0 || (al & 15) != 0 || c > 2048) return DS2_UNSUPPORTED_SHAPE;
+  hipStream_t st = as_stream(stream);
+  (void)hipMemsetAsync(col_amax, 0, (size_t)c * 4, st);
+  launch_rows_amax<true>(x, rows, c, c, mean, invstd, gamma, beta, y, row_amax, col_amax, st);
+  return launch_status("ds2_bn_apply_amax");
 }
 
 ds2_status_t ds2_bn_apply_mask_htanh(const float* x, int n, int c, int d, int t,

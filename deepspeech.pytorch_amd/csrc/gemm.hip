@@ -10,6 +10,7 @@
 // Operands that are k-contiguous are transposed on the LDS write; the row pad
 // (+2 floats) makes those 8 ds_write_b32 per thread conflict-free.
 #include "common.h"
+#include "amax_rc.h"
 
 #include <type_traits>
 
@@ -1677,6 +1678,11 @@ extern "C" ds2_status_t ds2_amax(const float* x, int rows, int cols, int64_t ld,
   if (row_amax == nullptr) {            // columns only: one wave per 256 columns x 64 rows
     hipLaunchKernelGGL(amax_cols8_kernel, dim3(cdiv(cols, 256), cdiv(rows, 64)), dim3(64), 0, st,
                        x, rows, cols, ld, 64, col_amax);
+    return launch_status("ds2_amax");
+  }
+  if (cols <= 2048) {                   // narrow (a weight matrix): one wave per row
+    launch_rows_amax<false>(x, rows, cols, ld, nullptr, nullptr, nullptr, nullptr, nullptr,
+                            row_amax, col_amax, st);
     return launch_status("ds2_amax");
   }
   (void)hipMemsetAsync(row_amax, 0, (size_t)rows * 4, st);

@@ -59,6 +59,7 @@ _PROTOS = {
                                     _vp, _sz, _vp]),
     "ds2_bn_eval_stats": (_c_int, [_vp, _vp, _c_int, _c_f, _vp, _vp, _vp]),
     "ds2_bn_apply": (_c_int, [_vp, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "ds2_bn_apply_amax": (_c_int, [_vp, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "ds2_bn_apply_mask_htanh": (_c_int, [_vp, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp,
                                          _vp, _c_f, _c_f, _vp, _c_int, _vp]),
     "ds2_bn_backward": (_c_int, [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp,

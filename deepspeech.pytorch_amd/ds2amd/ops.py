@@ -323,6 +323,45 @@ def bn_apply(x, outer, c, inner, mean, invstd, gamma, beta):
     return y
 
 
+# fp16x3 GEMM scales written by the kernel that produced an operand (ds2_bn_apply_amax), handed
+# to the GEMMs that read it next (the input projection: row maxima; dW_ih: column maxima).  An
+# entry holds the operand itself, so its storage cannot be reused while the entry lives, and is
+# valid only for the same storage, element count and version (views share the base's version
+# counter); the consumer pops it.  A few entries at most: an unconsumed one is dropped.
+_OPERAND_AMAX = []
+
+
+def _tag_amax(y, rows, cols, rmax, cmax):
+    _OPERAND_AMAX.append((y, y.data_ptr(), rows, cols, y._version, rmax, cmax))
+    del _OPERAND_AMAX[:-4]
+
+
+def _take_amax(x, rows, cols):
+    """(row maxima, column maxima) of the [rows][cols] operand x if its producer left them."""
+    for i, (y, ptr, r, c, ver, rmax, cmax) in enumerate(_OPERAND_AMAX):
+        if ptr == x.data_ptr() and (r, c) == (rows, cols) and x.numel() == rows * cols \
+                and x._version == ver == y._version and x.is_contiguous():
+            del _OPERAND_AMAX[i]
+            return rmax, cmax
+    return None, None
+
+
+def bn_apply_amax(x, rows, c, mean, invstd, gamma, beta):
+    """bn_apply over [rows][c] that also keeps y's row / column maxima for the fp16x3 GEMMs
+    reading it next (ds2_bn_apply_amax); plain bn_apply where its shape conditions fail."""
+    ptrs = (x.data_ptr(), mean.data_ptr(), invstd.data_ptr(), gamma.data_ptr(), beta.data_ptr())
+    if c % 4 or c > 2048 or rows <= 0 or any(p % 16 for p in ptrs):
+        return bn_apply(x, rows, c, 1, mean, invstd, gamma, beta)
+    y = torch.empty_like(x)
+    rmax = torch.empty(rows, dtype=_I32, device=x.device)
+    cmax = torch.empty(c, dtype=_I32, device=x.device)
+    _lib.call("ds2_bn_apply_amax", x.data_ptr(), rows, c, mean.data_ptr(), invstd.data_ptr(),
+              gamma.data_ptr(), beta.data_ptr(), y.data_ptr(), rmax.data_ptr(), cmax.data_ptr(),
+              _stream())
+    _tag_amax(y, rows, c, rmax, cmax)
+    return y
+
+
 def bn_backward(dy, dy_layout, x, outer, c, d, t, mean, invstd, gamma, beta, masked=False,
                 lens=None, lo=0.0, hi=20.0, want_dbias=False, bias=None):
     """dgamma / dbeta (/ dbias of the preceding conv) land in the parameters' gradient
@@ -690,7 +729,9 @@ class SeqBatchNormFn(torch.autograd.Function):
         x2d = x2d.contiguous()
         r, c = x2d.shape
         mean, invstd = bn_stats(x2d, r, c, 1, eps, momentum, running_mean, running_var, training)
-        y = bn_apply(x2d, r, c, 1, mean, invstd, gamma, beta)
+        # with the fp16x3 GEMMs, y's row / column maxima for the input projection and dW_ih
+        y = (bn_apply_amax(x2d, r, c, mean, invstd, gamma, beta) if h3_enabled()
+             else bn_apply(x2d, r, c, 1, mean, invstd, gamma, beta))
         ctx.save_for_backward(x2d, gamma, beta, mean, invstd)
         ctx.training = training
         return y
@@ -713,7 +754,13 @@ class LinearFn(torch.autograd.Function):
     def forward(ctx, x2d, weight):
         x2d = x2d.contiguous()
         ctx.save_for_backward(x2d, weight)
-        return matmul_nt(x2d, weight)
+        # the fp16x3 scales of x the BatchNorm before it kept (the FC's SequenceWise BN): rows
+        # for this GEMM, columns for dW's
+        m, k = x2d.shape
+        x_r, ctx.x_c = _take_amax(x2d, m, k) if h3_enabled() else (None, None)
+        out = torch.empty(m, weight.shape[0], device=x2d.device, dtype=_F32)
+        return sgemm(x2d, weight, out, m=m, n=weight.shape[0], k=k, trans_b=True, lda=k, ldb=k,
+                     ldc=weight.shape[0], a_amax=x_r)
 
     @staticmethod
     def backward(ctx, dy):
@@ -726,7 +773,7 @@ class LinearFn(torch.autograd.Function):
             dx = torch.empty_like(x2d)
             sgemm(dy, weight, dx, m=m, n=k, k=n, lda=n, ldb=k, ldc=k)
         dw = grad_like(weight)
-        sgemm(dy, x2d, dw, m=n, n=k, k=m, trans_a=True, lda=n, ldb=k, ldc=k)
+        sgemm(dy, x2d, dw, m=n, n=k, k=m, trans_a=True, lda=n, ldb=k, ldc=k, b_amax=ctx.x_c)
         return dx, dw
 
 
@@ -769,23 +816,37 @@ def _stacked_rows(a: torch.Tensor, b: torch.Tensor):
     return a.as_strided((2 * a.shape[0], a.shape[1]), (a.shape[1], 1))
 
 
-def _rnn_input_proj(x, weights, nd, g, bf16=False):
-    """xproj[T, N, D, g] = x @ W_ih^T + b_ih for every direction: one GEMM over both
-    directions when their W_ih lie back to back (N = 2g), else one GEMM each."""
+def _rnn_input_proj(x, weights, nd, g, bf16=False, need_dx=False):
+    """(xproj, pre): xproj[T, N, D, g] = x @ W_ih^T + b_ih for every direction, one GEMM over
+    both directions when their W_ih lie back to back (N = 2g), else one GEMM each.  With the
+    fp16x3 GEMMs, x's row maxima come from the kernel that produced x where it kept them
+    (ds2_bn_apply_amax) and the stacked W_ih's row maxima from one pass that also takes its
+    column maxima when the backward's dX GEMM will need them; ``pre`` hands the column maxima
+    of x and W_ih to _rnn_param_grads, which would otherwise re-read both operands."""
     t, n, inp = x.shape
     x2d = x.view(t * n, inp)
     xproj = torch.empty(t, n, nd, g, device=x.device, dtype=_F32)
     ws = _stacked_rows(weights[0], weights[4]) if nd == 2 else None
+    pre = {}
+    x_r = w_r = None
+    if h3_enabled() and not bf16:
+        x_r, pre["x_c"] = _take_amax(x2d, t * n, inp)
+        if pre["x_c"] is None:
+            del pre["x_c"]
+        elif ws is not None:
+            w_r, w_c = amax(ws, 2 * g, inp, inp, want_cols=need_dx)
+            if w_c is not None:
+                pre["w_c"] = w_c
     if ws is not None:
         bias = torch.cat([weights[2], weights[6]])
         sgemm(x2d, ws, xproj, m=t * n, n=2 * g, k=inp, trans_b=True, lda=inp, ldb=inp,
-              ldc=2 * g, bias=bias, bf16=bf16)
-        return xproj
+              ldc=2 * g, bias=bias, bf16=bf16, a_amax=x_r, b_amax=w_r)
+        return xproj, pre
     for d in range(nd):
         w_ih, _, b_ih, _ = weights[4 * d: 4 * d + 4]
         sgemm(x2d, w_ih, xproj, m=t * n, n=g, k=inp, trans_b=True, lda=inp, ldb=inp,
-              ldc=nd * g, bias=b_ih, c_off=d * g, bf16=bf16)
-    return xproj
+              ldc=nd * g, bias=b_ih, c_off=d * g, bf16=bf16, a_amax=x_r)
+    return xproj, pre
 
 
 def _rnn_output(h_all, sum_dirs, nd):
@@ -846,8 +907,36 @@ def _rnn_param_grads_bf16(x2d, h_all, dgx, dgh, weights, nd, g, t, n, inp, h, ne
     return dx, grads
 
 
-def _rnn_param_grads(x, h_all, dgx, dgh, weights, nd, g, need_dx, bf16=False, dbias=None,
-                     shared_bf16=True, col_amax=None):
+_SIDE = {}
+
+
+def _side_stream(dev) -> torch.cuda.Stream:
+    """A second stream per device for HBM-bound passes that may overlap the MFMA-bound GEMMs."""
+    st = _SIDE.get(dev)
+    if st is None:
+        st = _SIDE[dev] = torch.cuda.Stream(dev)
+    return st
+
+
+def _rows_amax_beside(x, rows, cols, ld):
+    """(row maxima of x, event) computed on the side stream, after the work queued so far on the
+    current stream: the pass reads x while the current stream runs the GEMMs that do not need
+    it (the dX GEMM waits on the event).  The allocator is told about both streams' uses."""
+    cur = torch.cuda.current_stream(x.device)
+    side = _side_stream(x.device)
+    side.wait_stream(cur)
+    with torch.cuda.stream(side):
+        r = amax(x, rows, cols, ld, want_cols=False)[0]
+        ev = torch.cuda.Event()
+        ev.record(side)
+    x.record_stream(side)
+    if r is not None:
+        r.record_stream(cur)
+    return r, ev
+
+
+def _rnn_param_grads(x, h_all, dgx, dgh, weights, nd, g, need_dx, bf16=False, pre=None,
+                     dbias=None, shared_bf16=True, col_amax=None):
     """Weight/bias/input gradients of one recurrent layer from the gate gradients.
 
     dgx = d/d(x W_ih^T + b_ih), dgh = d/d(h W_hh^T + b_hh), both [T, N, D, g]
@@ -855,7 +944,9 @@ def _rnn_param_grads(x, h_all, dgx, dgh, weights, nd, g, need_dx, bf16=False, db
     direction already summed (the GRU backward kernel's own sums) skips the column sums.
     shared_bf16=False keeps bf16 mode on the per-GEMM conversions (the cross-check of
     _rnn_param_grads_bf16's shared copies, tests/test_gpu_ops.py).  col_amax: the column
-    maxima of dgx and dgh ([2 D g] float bits) when the recurrence kept them.
+    maxima of dgx and dgh ([2 D g] float bits) when the recurrence kept them (dgx's row maxima,
+    which only the dX GEMM needs, then come from a pass beside the dW GEMMs).  pre: the column
+    maxima of x and of the stacked W_ih the forward's input projection took (_rnn_input_proj).
     """
     t, n, inp = x.shape
     h = h_all.shape[-1]
@@ -876,21 +967,24 @@ def _rnn_param_grads(x, h_all, dgx, dgh, weights, nd, g, need_dx, bf16=False, db
     # (dX) and columns (dW_ih), dgh columns (dW_hh; a bound over all its rows), x and W_ih
     # columns, and 1.0 for the tanh-bounded states h
     am = {}
+    r_ev = None
     if h3_enabled() and not bf16:
         if col_amax is not None:
             # [2 D g] (dgx, dgh), or [D g] when dgh is dgx (the one-gate RNN)
             am["dgx_c"] = col_amax[:ld]
             am["dgh_c"] = col_amax[ld:] if col_amax.numel() == 2 * ld else am["dgx_c"]
             if need_dx:
-                am["dgx_r"] = amax(dgx, tn, ld, ld, want_cols=False)[0]
+                am["dgx_r"], r_ev = _rows_amax_beside(dgx, tn, ld, ld)
         else:
             am["dgx_r"], am["dgx_c"] = amax(dgx, tn, ld, ld, want_rows=need_dx)
             am["dgh_c"] = am["dgx_c"] if dgh is dgx else amax(dgh, tn, ld, ld, want_rows=False)[1]
-        am["x_c"] = amax(x2d, tn, inp, inp, want_rows=False)[1]
+        pre = pre or {}
+        am["x_c"] = pre["x_c"] if "x_c" in pre else amax(x2d, tn, inp, inp, want_rows=False)[1]
         am["h"] = unit_bound(nd * h, dev)
         if need_dx:
             if w_st is not None:
-                am["w_c"] = amax(w_st, 2 * g, inp, inp, want_rows=False)[1]
+                am["w_c"] = (pre["w_c"] if "w_c" in pre
+                             else amax(w_st, 2 * g, inp, inp, want_rows=False)[1])
             else:
                 am["w_c"] = [amax(weights[4 * d], g, inp, inp, want_rows=False)[1]
                              for d in range(nd)]
@@ -903,6 +997,8 @@ def _rnn_param_grads(x, h_all, dgx, dgh, weights, nd, g, need_dx, bf16=False, db
         sgemm(dgx, x2d, dw_st, m=2 * g, n=inp, k=tn, trans_a=True, lda=ld, ldb=inp, ldc=inp,
               bf16=bf16, a_amax=am.get("dgx_c"), b_amax=am.get("x_c"))
     if dx is not None and w_st is not None:
+        if r_ev is not None:
+            torch.cuda.current_stream(dev).wait_event(r_ev)
         sgemm(dgx, w_st, dx, m=tn, n=inp, k=2 * g, lda=ld, ldb=inp, ldc=inp, bf16=bf16,
               a_amax=am.get("dgx_r"), b_amax=am.get("w_c"))
     for d in range(nd):
@@ -939,6 +1035,8 @@ def _rnn_param_grads(x, h_all, dgx, dgh, weights, nd, g, need_dx, bf16=False, db
             else:
                 colsum(dgh, tn, g, ld, db_hh, off=d * g)
         if dx is not None and w_st is None:
+            if r_ev is not None:
+                torch.cuda.current_stream(dev).wait_event(r_ev)
             # dgx's row maxima span both directions: an upper bound for each direction's slice
             sgemm(dgx, w_ih, dx, m=tn, n=inp, k=g, lda=ld, ldb=inp, ldc=inp,
                   beta=0.0 if d == 0 else 1.0, a_off=d * g, bf16=bf16,
@@ -989,7 +1087,7 @@ class GRULayerFn(torch.autograd.Function):
         nd = len(weights) // 4
         dev = x.device
         bf16 = _RNN_GEMM_BF16[0]
-        xproj = _rnn_input_proj(x, weights, nd, 3 * h, bf16)
+        xproj, ctx.pre = _rnn_input_proj(x, weights, nd, 3 * h, bf16, ctx.needs_input_grad[0])
         h_all = torch.empty(t, n, nd, h, device=dev, dtype=_F32)
         need_grad = any(ctx.needs_input_grad)   # forward() itself runs under no_grad
         # backward cache: [T][N][D][4H] gates + the dh-exchange backward's coefficient tiles
@@ -1037,7 +1135,7 @@ class GRULayerFn(torch.autograd.Function):
             _lib.call("ds2_gru_bwd_bias", *common, rnn_status_word(dev).data_ptr(),
                       ws.data_ptr(), ws.numel(), _stream())
         dx, grads = _rnn_param_grads(x, h_all, dgx, dgh, weights, nd, h3,
-                                     ctx.needs_input_grad[0], bf16, dbias=dbias,
+                                     ctx.needs_input_grad[0], bf16, ctx.pre, dbias=dbias,
                                      col_amax=col_amax)
         return (dx, None, None, None, *grads)
 
@@ -1057,7 +1155,7 @@ class RNNLayerFn(torch.autograd.Function):
         nd = len(weights) // 4
         dev = x.device
         bf16 = _RNN_GEMM_BF16[0]
-        xproj = _rnn_input_proj(x, weights, nd, h, bf16)
+        xproj, ctx.pre = _rnn_input_proj(x, weights, nd, h, bf16, ctx.needs_input_grad[0])
         h_all = torch.empty(t, n, nd, h, device=dev, dtype=_F32)
         ws = _ws(_lib.size("ds2_rnn_fwd_workspace_size", n, h, nd), dev)
         _lib.call("ds2_rnn_fwd_ws", t, n, h, nd, xproj.data_ptr(), weights[1].data_ptr(),
@@ -1086,7 +1184,7 @@ class RNNLayerFn(torch.autograd.Function):
                   dg.data_ptr(), _p(col_amax), rnn_status_word(dev).data_ptr(), ws.data_ptr(),
                   ws.numel(), _stream())
         dx, grads = _rnn_param_grads(x, h_all, dg, dg, weights, nd, h,
-                                     ctx.needs_input_grad[0], bf16, col_amax=col_amax)
+                                     ctx.needs_input_grad[0], bf16, ctx.pre, col_amax=col_amax)
         return (dx, None, None, None, *grads)
 
 
@@ -1103,7 +1201,7 @@ class LSTMLayerFn(torch.autograd.Function):
         nd = len(weights) // 4
         dev = x.device
         bf16 = _RNN_GEMM_BF16[0]
-        xproj = _rnn_input_proj(x, weights, nd, 4 * h, bf16)
+        xproj, ctx.pre = _rnn_input_proj(x, weights, nd, 4 * h, bf16, ctx.needs_input_grad[0])
         h_all = torch.empty(t, n, nd, h, device=dev, dtype=_F32)
         need_grad = any(ctx.needs_input_grad)
         c_all = torch.empty(t, n, nd, h, device=dev, dtype=_F32) if need_grad else None
@@ -1139,7 +1237,7 @@ class LSTMLayerFn(torch.autograd.Function):
                   _p(w_hh_r), c_all.data_ptr(), gates.data_ptr(), lens.data_ptr(), dg.data_ptr(),
                   rnn_status_word(dev).data_ptr(), ws.data_ptr(), ws.numel(), _stream())
         dx, grads = _rnn_param_grads(x, h_all, dg, dg, weights, nd, 4 * h,
-                                     ctx.needs_input_grad[0], bf16)
+                                     ctx.needs_input_grad[0], bf16, ctx.pre)
         return (dx, None, None, None, *grads)
 
 

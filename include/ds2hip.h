@@ -202,6 +202,15 @@ ds2_status_t ds2_bn_eval_stats(const float* running_mean, const float* running_v
 ds2_status_t ds2_bn_apply(const float* x, int outer, int c, int inner, const float* mean,
                           const float* invstd, const float* gamma, const float* beta, float* y,
                           ds2_stream_t stream);
+/* ds2_bn_apply over [rows][c] (inner 1) that also writes the fp16x3 GEMM scales of y: the
+ * float bits of max |y| per row (row_amax[rows]) and per column (col_amax[c]), the next
+ * input projection's A-row and dW_ih's B-column maxima (ds2_sgemm_amax_ws).  Needs c % 4 == 0,
+ * c <= 2048 and 16-B aligned x / y / mean / invstd / gamma / beta (DS2_UNSUPPORTED_SHAPE
+ * otherwise).  Replaces the same SequenceWise BatchNorm1d as ds2_bn_apply (model.py:89). */
+ds2_status_t ds2_bn_apply_amax(const float* x, int rows, int c, const float* mean,
+                               const float* invstd, const float* gamma, const float* beta,
+                               float* y, unsigned* row_amax, unsigned* col_amax,
+                               ds2_stream_t stream);
 /* Conv-block epilogue (MaskConv, model.py:69-78): x is [n][c][d][t];
  * y = mask(hardtanh(mask(bn(x)), lo, hi)) where mask zeroes t >= lens[n].
  * out_layout 0: y is [n][c][d][t];  1: y is [t][n][c*d] (the TxNxH collapse of

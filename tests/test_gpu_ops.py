@@ -164,10 +164,13 @@ def test_sgemm_h3_rows_over_twelve_decades(dev, ta, tb, monkeypatch):
     assert torch.equal(c2, outs["h3"])
 
 
-@pytest.mark.parametrize("rows,cols", [(1, 4), (37, 52), (16032, 4800), (300, 4100)])
+@pytest.mark.parametrize("rows,cols", [(1, 4), (37, 52), (4800, 800), (5, 2048), (16032, 4800),
+                                       (300, 4100)])
 def test_amax_rows_and_cols(dev, rows, cols):
     """ds2_amax: row and column maxima of |x| in one pass, bit-exact against torch (float bits;
-    a NaN is skipped, an inf kept), rows alone through the one-wave-per-row kernel too."""
+    a NaN is skipped, an inf kept) -- one wave per row up to 2048 columns (the stacked W_ih the
+    input projection and dX share), row-block tiles beyond -- and rows alone through the
+    one-wave-per-row kernel too."""
     g = torch.Generator().manual_seed(rows + cols)
     x = torch.randn(rows, cols + 8, generator=g) * torch.pow(10.0, torch.rand(rows, 1, generator=g) * 8 - 4)
     if rows > 3 and cols > 3:
@@ -475,6 +478,29 @@ def test_seq_bn_fwd_bwd(dev):
     _close(bd.grad, br.grad, 1e-5, "bn dbeta")
     _close(rm_d, 0.1 * x.mean(0), 1e-5, "running_mean")
     _close(rv_d, 0.9 + 0.1 * x.var(0, unbiased=True), 1e-5, "running_var")
+
+
+@pytest.mark.parametrize("rows,c", [(32032, 800), (777, 96), (5, 1600), (130, 260), (64, 4)])
+def test_bn_apply_amax(dev, rows, c):
+    """ds2_bn_apply_amax: y bit-identical to ds2_bn_apply, and its row / column maxima equal to
+    |y|'s (the fp16x3 scales the next input projection and dW_ih take from it), for every
+    columns-per-lane instantiation and ragged row counts."""
+    g = torch.Generator().manual_seed(rows + c)
+    x = (torch.randn(rows, c, generator=g) * 3 + 1).to(dev)
+    mean, invstd = (torch.randn(c, generator=g).to(dev), (torch.rand(c, generator=g) + .5).to(dev))
+    gamma, beta = (torch.randn(c, generator=g).to(dev), torch.randn(c, generator=g).to(dev))
+    y0 = ops.bn_apply(x, rows, c, 1, mean, invstd, gamma, beta)
+    y1 = ops.bn_apply_amax(x, rows, c, mean, invstd, gamma, beta)
+    assert torch.equal(y0, y1)
+    rmax, cmax = ops._take_amax(y1, rows, c)
+    assert rmax is not None and all(v is None for v in ops._take_amax(y1, rows, c))
+    ay = y1.abs()
+    assert torch.equal(rmax, ay.amax(1).contiguous().view(torch.int32))
+    assert torch.equal(cmax, ay.amax(0).contiguous().view(torch.int32))
+    # an in-place change of y invalidates the maxima
+    y2 = ops.bn_apply_amax(x, rows, c, mean, invstd, gamma, beta)
+    y2.mul_(2)
+    assert all(v is None for v in ops._take_amax(y2, rows, c))
 
 
 @pytest.mark.parametrize("layout", [0, 1])
@@ -1532,9 +1558,9 @@ def test_gru_bwd_column_maxima(dev, n, h, bidir, bwd, monkeypatch):
     seen = {}
     orig = ops._rnn_param_grads
 
-    def spy(x, h_all, dgx, dgh, weights, nd_, g, need_dx, bf16=False, dbias=None, **kw):
+    def spy(x, h_all, dgx, dgh, weights, nd_, g, need_dx, bf16=False, pre=None, dbias=None, **kw):
         seen["dgx"], seen["dgh"], seen["col"] = dgx.clone(), dgh.clone(), kw.get("col_amax")
-        return orig(x, h_all, dgx, dgh, weights, nd_, g, need_dx, bf16, dbias, **kw)
+        return orig(x, h_all, dgx, dgh, weights, nd_, g, need_dx, bf16, pre, dbias, **kw)
 
     monkeypatch.setattr(ops, "_rnn_param_grads", spy)
     _gru_run(dev, n, 29, 40, h, nd, h + n, [{}], monkeypatch)
