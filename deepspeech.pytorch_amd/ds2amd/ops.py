@@ -907,34 +907,6 @@ def _rnn_param_grads_bf16(x2d, h_all, dgx, dgh, weights, nd, g, t, n, inp, h, ne
     return dx, grads
 
 
-_SIDE = {}
-
-
-def _side_stream(dev) -> torch.cuda.Stream:
-    """A second stream per device for HBM-bound passes that may overlap the MFMA-bound GEMMs."""
-    st = _SIDE.get(dev)
-    if st is None:
-        st = _SIDE[dev] = torch.cuda.Stream(dev)
-    return st
-
-
-def _rows_amax_beside(x, rows, cols, ld):
-    """(row maxima of x, event) computed on the side stream, after the work queued so far on the
-    current stream: the pass reads x while the current stream runs the GEMMs that do not need
-    it (the dX GEMM waits on the event).  The allocator is told about both streams' uses."""
-    cur = torch.cuda.current_stream(x.device)
-    side = _side_stream(x.device)
-    side.wait_stream(cur)
-    with torch.cuda.stream(side):
-        r = amax(x, rows, cols, ld, want_cols=False)[0]
-        ev = torch.cuda.Event()
-        ev.record(side)
-    x.record_stream(side)
-    if r is not None:
-        r.record_stream(cur)
-    return r, ev
-
-
 def _rnn_param_grads(x, h_all, dgx, dgh, weights, nd, g, need_dx, bf16=False, pre=None,
                      dbias=None, shared_bf16=True, col_amax=None):
     """Weight/bias/input gradients of one recurrent layer from the gate gradients.
@@ -944,8 +916,7 @@ def _rnn_param_grads(x, h_all, dgx, dgh, weights, nd, g, need_dx, bf16=False, pr
     direction already summed (the GRU backward kernel's own sums) skips the column sums.
     shared_bf16=False keeps bf16 mode on the per-GEMM conversions (the cross-check of
     _rnn_param_grads_bf16's shared copies, tests/test_gpu_ops.py).  col_amax: the column
-    maxima of dgx and dgh ([2 D g] float bits) when the recurrence kept them (dgx's row maxima,
-    which only the dX GEMM needs, then come from a pass beside the dW GEMMs).  pre: the column
+    maxima of dgx and dgh ([2 D g] float bits) when the recurrence kept them.  pre: the column
     maxima of x and of the stacked W_ih the forward's input projection took (_rnn_input_proj).
     """
     t, n, inp = x.shape
@@ -967,14 +938,13 @@ def _rnn_param_grads(x, h_all, dgx, dgh, weights, nd, g, need_dx, bf16=False, pr
     # (dX) and columns (dW_ih), dgh columns (dW_hh; a bound over all its rows), x and W_ih
     # columns, and 1.0 for the tanh-bounded states h
     am = {}
-    r_ev = None
     if h3_enabled() and not bf16:
         if col_amax is not None:
             # [2 D g] (dgx, dgh), or [D g] when dgh is dgx (the one-gate RNN)
             am["dgx_c"] = col_amax[:ld]
             am["dgh_c"] = col_amax[ld:] if col_amax.numel() == 2 * ld else am["dgx_c"]
             if need_dx:
-                am["dgx_r"], r_ev = _rows_amax_beside(dgx, tn, ld, ld)
+                am["dgx_r"] = amax(dgx, tn, ld, ld, want_cols=False)[0]
         else:
             am["dgx_r"], am["dgx_c"] = amax(dgx, tn, ld, ld, want_rows=need_dx)
             am["dgh_c"] = am["dgx_c"] if dgh is dgx else amax(dgh, tn, ld, ld, want_rows=False)[1]
@@ -997,8 +967,6 @@ def _rnn_param_grads(x, h_all, dgx, dgh, weights, nd, g, need_dx, bf16=False, pr
         sgemm(dgx, x2d, dw_st, m=2 * g, n=inp, k=tn, trans_a=True, lda=ld, ldb=inp, ldc=inp,
               bf16=bf16, a_amax=am.get("dgx_c"), b_amax=am.get("x_c"))
     if dx is not None and w_st is not None:
-        if r_ev is not None:
-            torch.cuda.current_stream(dev).wait_event(r_ev)
         sgemm(dgx, w_st, dx, m=tn, n=inp, k=2 * g, lda=ld, ldb=inp, ldc=inp, bf16=bf16,
               a_amax=am.get("dgx_r"), b_amax=am.get("w_c"))
     for d in range(nd):
@@ -1035,8 +1003,6 @@ def _rnn_param_grads(x, h_all, dgx, dgh, weights, nd, g, need_dx, bf16=False, pr
             else:
                 colsum(dgh, tn, g, ld, db_hh, off=d * g)
         if dx is not None and w_st is None:
-            if r_ev is not None:
-                torch.cuda.current_stream(dev).wait_event(r_ev)
             # dgx's row maxima span both directions: an upper bound for each direction's slice
             sgemm(dgx, w_ih, dx, m=tn, n=inp, k=g, lda=ld, ldb=inp, ldc=inp,
                   beta=0.0 if d == 0 else 1.0, a_off=d * g, bf16=bf16,

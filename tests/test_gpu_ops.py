@@ -1571,3 +1571,14 @@ def test_gru_bwd_column_maxima(dev, n, h, bidir, bwd, monkeypatch):
     ref_h = seen["dgh"].view(-1, g).abs().amax(0).contiguous().view(torch.int32)
     assert torch.equal(col[:g], ref_x)
     assert torch.equal(col[g:], ref_h)
+
+
+@pytest.mark.parametrize("n,h,nd", [(64, 1024, 2), (64, 1024, 1), (32, 800, 2), (16, 256, 1)])
+def test_lstm_half_grid_covers_its_fallback(dev, n, h, nd):
+    """ds2_lstm_bwd_half_grid budgets the co-residency guard for ds2_lstm_bwd_half, which falls
+    back to ds2_lstm_bwd (16-sample tiles, up to twice the workgroups) when its own kernel
+    declines: the reported grid must cover both, as ds2_gru_bwd_grid covers the
+    XCD-local kernel and its fallbacks."""
+    half = ops.persistent_bwd_grid("lstm_half", n, h, nd)
+    full = ops.persistent_bwd_grid("lstm", n, h, nd)
+    assert half >= full
