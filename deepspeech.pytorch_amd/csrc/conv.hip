@@ -1306,7 +1306,7 @@ __host__ __device__ inline CxGeom cx_geom(const ConvDims& g, bool dgrad) {
 template <bool DGRAD, int NPL = 3>
 __global__ void conv_x6_wimg_kernel(const float* __restrict__ w, ConvDims g, CxGeom c,
                                     unsigned short* __restrict__ img,
-                                    const int* __restrict__ m_exp) {
+                                    const int* __restrict__ m_exp, int flip_odd = 0) {
   const int M = DGRAD ? g.ci : g.co;
   const int L = (DGRAD ? g.co : g.ci) * c.RC;          // (channel, tap-row chunk) pairs
   const int mbn = (M + 31) / 32;
@@ -1334,9 +1334,10 @@ __global__ void conv_x6_wimg_kernel(const float* __restrict__ w, ConvDims g, CxG
         if (a < aq) v = w[((int64_t)ch * g.ci + m) * KHW + (q + g.sh * (aq - 1 - a)) * g.kw + (g.kw - 1 - b)];
       }
       // k-step st = (tap-row group, column pair); the second half of the k-steps (the kk = 1
-      // waves' share) is stored negated: see conv_x6_kernel's epilogue
+      // waves' share) is stored negated: see conv_x6_kernel's epilogue.  flip_odd 1: the odd
+      // loop channels instead; 2: nothing negated (conv_h3_fwd2r_kernel)
       const int st = (al >> 3) * c.NBP + (b >> 1), nks = (c.KA / 8) * c.NBP;
-      if (st >= (nks + 1) / 2) v = -v;
+      if (flip_odd == 0 ? st >= (nks + 1) / 2 : (flip_odd == 1 && (l & 1) != 0)) v = -v;
     }
     const float sc = NPL == 2 && m < M ? h3_scale(m_exp[m]) : 1.f;
     cx_wimg_put<NPL>(img, ((((int64_t)q * mbn + mb) * L + l) * NPL) * per + e, per, v, sc);
@@ -1596,6 +1597,218 @@ __global__ __launch_bounds__(CX_T, 1) void conv_x6_kernel(const float* __restric
           if (col >= len) v = 0.f;
         }
         out[(((int64_t)n * M + m) * out_h + orow) * out_w + col] = v;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// conv2 forward on fp16x3, two output rows per workgroup (height stride 2, width stride 1,
+// <= 24 tap rows, 6 kernel-column pairs: the model's 21 x 11 conv2).  With stride 2, output
+// rows r and r + 4 read input rows 8 apart -- exactly one 8-row fragment group -- so ONE
+// column-major patch of 32 input rows serves both: row r's B fragments are patch row groups
+// 0..2, row r + 4's are groups 1..3, and both multiply the SAME weight fragments (tap row group
+// ga).  Per loop channel a workgroup then stages 32 patch rows and one weight image for two
+// output rows (conv_x6_kernel: 24 rows and one image for one row), and every weight fragment
+// read feeds six MFMAs instead of three.  Rows r, r + 4 with r = 8 b + j (j < 4) tile the
+// output rows in pairs; a row past the output is computed and not stored.
+// Waves: 8 x 32 columns, each all 18 k-steps of both rows (no k halves).  The sign split of
+// conv_x6_kernel (one k half on negated weights) becomes a flip per loop channel: the weight
+// image stores odd channels negated and the accumulators are negated between channels, so the
+// MFMAs' floor of low addend bits drifts one way in even channels and the other in odd ones
+// (same cancellation, DESIGN.md §4 "MFMA rounding").  Small products in their own chain
+// (cx_mma_h3s), the next channel's patch double-buffered as in conv_x6_kernel.
+#ifndef DS2_C2R_MODE
+#define DS2_C2R_MODE 2
+#endif
+constexpr int C2_KAP = 32;                                  // patch rows
+constexpr int C2_P = cx_pitch8odd(C2_KAP);                  // 40: 8 x odd bf16
+constexpr int C2_PCOL = CxConst<3, 6>::PCOL;                // 267
+constexpr int C2_PPL = C2_PCOL * C2_P;                      // fp16 per patch plane
+constexpr int C2_WPL = 32 * CxConst<3, 6>::COP;             // fp16 per weight plane
+constexpr int C2_WQ = (2 * C2_WPL / 8 + CX_T - 1) / CX_T;   // 16-B image chunks per thread
+constexpr int C2_PU = (C2_PCOL * (C2_KAP / 8) + CX_T - 1) / CX_T;   // patch units per thread
+
+__global__ __launch_bounds__(CX_T, 1) void conv_h3_fwd2r_kernel(
+    const float* __restrict__ in, const unsigned short* __restrict__ img,
+    const float* __restrict__ bias, float* __restrict__ out, ConvDims g,
+    const int* __restrict__ out_lens, int gx, int gy, const int* __restrict__ m_exp,
+    const unsigned* __restrict__ n_amax) {
+  using CC = CxConst<3, 6>;
+  __shared__ __attribute__((aligned(16))) unsigned short ps[2 * 2 * C2_PPL];
+  __shared__ __attribute__((aligned(16))) unsigned short ws[2 * C2_WPL];
+  const int M = g.co, L = g.ci;
+  const int mbn = (M + 31) / 32;
+  int bx, by, bz;
+  xcd_tile(gx, gy, bx, by, bz);
+  const int n = bz / mbn;
+  const int mb = bz - n * mbn;
+  const int m0 = mb * 32;
+  const int c0 = bx * CX_COLS;
+  const int orow = 8 * (by >> 2) + (by & 3);          // and orow + 4
+  const int prow0 = orow * 2 - g.ph;                   // the patch's first input row
+  const int pcol0 = c0 - g.pw;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int plane_in = g.hi * g.wi;
+  const float* inn = in + (int64_t)n * L * plane_in;
+  const int en = h3_exp(n_amax[n]);
+  const float nsc = h3_scale(en);
+  constexpr int wstride = 2 * C2_WPL;                  // one loop channel's image (fp16)
+  const unsigned short* wimg = img + (int64_t)mb * L * wstride;
+  constexpr int wchunks = wstride / 8;
+  constexpr int units = C2_PCOL * (C2_KAP / 8);
+  const int last_row = 2 * 4 + 20;                     // rows a >= 29 feed no tap of either row
+
+  float rp[C2_PU][8];
+  u32x4 rw[C2_WQ];
+  auto load_w = [&](int l) __attribute__((always_inline)) {
+    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<unsigned short*>(wimg + (int64_t)l * wstride), (short)0, wstride * 2, 0x00020000);
+#pragma unroll
+    for (int r = 0; r < C2_WQ; ++r) {
+      const int i = tid + CX_T * r;
+      rw[r] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                            wr, i < wchunks ? i * 16 : 0x7ffffff0, 0, 0));
+    }
+  };
+  auto load = [&](int l) __attribute__((always_inline)) {
+    const __amdgpu_buffer_rsrc_t rs = conv_rsrc(inn + (int64_t)l * plane_in, plane_in);
+#pragma unroll
+    for (int u = 0; u < C2_PU; ++u) {
+      const int unit = tid + CX_T * u;
+      const int j = unit >> 2, rg = unit & 3;
+      const int ic = pcol0 + j;
+      const bool cok = unit < units && ic >= 0 && ic < g.wi;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int a = 8 * rg + i, ir = prow0 + a;
+        const bool ok = cok && a <= last_row && ir >= 0 && ir < g.hi;
+        rp[u][i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                 rs, ok ? (ir * g.wi + ic) * 4 : 0x7ffffff0, 0, 0));
+      }
+    }
+  };
+  auto store_patch = [&](unsigned short* dst) __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < C2_PU; ++u) {
+      const int unit = tid + CX_T * u;
+      if (unit < units) cx_store8<2>(dst, C2_PPL, (unit >> 2) * C2_P + 8 * (unit & 3), rp[u], nsc);
+    }
+  };
+  auto store_w = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int r = 0; r < C2_WQ; ++r) {
+      const int i = tid + CX_T * r;
+      if (i < wchunks) *reinterpret_cast<u32x4*>(ws + 8 * i) = rw[r];
+    }
+  };
+
+  f32x16 acc[2], acs[2];
+#if DS2_C2R_MODE == 2
+  f32x16 tot[2];
+#endif
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      acc[j][r] = acs[j][r] = 0.f;
+#if DS2_C2R_MODE == 2
+      tot[j][r] = 0.f;
+#endif
+    }
+  const int fr = lane & 31, fh = lane >> 5;
+  const bool active = c0 + 32 * wave < g.wo;
+
+  load(0);
+  load_w(0);
+  store_patch(ps);
+  store_w();
+  __syncthreads();
+  for (int l = 0; l < L; ++l) {
+    if (l + 1 < L) load(l + 1);
+    const unsigned short* pcur = ps + (l & 1) * 2 * C2_PPL;
+    unsigned short* pnext = ps + ((l + 1) & 1) * 2 * C2_PPL;
+    bool staged = false;
+    if (active) {
+      constexpr int NK = 3 * 6, MID = 6;
+#pragma unroll
+      for (int st = 0; st < NK; ++st) {
+        if (st == MID && l + 1 < L) {
+          store_patch(pnext);
+          load_w(l + 1);
+          staged = true;
+        }
+        const int ga = st / 6, p = st - (st / 6) * 6;
+        const int b = 2 * p + fh;
+        bf16x8 af[3], b0[3], b1[3];
+        const int aw = fr * CC::COP + b * CC::KA + 8 * ga;
+        const int ap = (32 * wave + fr + b) * C2_P + 8 * ga;
+#pragma unroll
+        for (int pl = 0; pl < 2; ++pl) {
+          af[pl] = *reinterpret_cast<const bf16x8*>(ws + pl * C2_WPL + aw);
+          b0[pl] = *reinterpret_cast<const bf16x8*>(pcur + pl * C2_PPL + ap);
+          b1[pl] = *reinterpret_cast<const bf16x8*>(pcur + pl * C2_PPL + ap + 8);
+        }
+        cx_mma_h3s(af, b0, acc[0], acs[0]);
+        cx_mma_h3s(af, b1, acc[1], acs[1]);
+        __builtin_amdgcn_sched_barrier(0);   // bound the fragment-read hoisting
+      }
+    }
+    if (!staged && l + 1 < L) {
+      store_patch(pnext);
+      load_w(l + 1);
+    }
+#if DS2_C2R_MODE == 1
+    if (l + 1 < L) {
+      // the next channel's weights are stored negated when this one's were not (and back)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        acc[j] = -acc[j];
+        acs[j] = -acs[j];
+      }
+    }
+#elif DS2_C2R_MODE == 2
+    // the big chain restarts every channel and is summed by the VALU (RNE)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      tot[j] += acc[j];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+    }
+#endif
+    __syncthreads();
+    if (l + 1 < L) {
+      store_w();
+      __syncthreads();
+    }
+  }
+  if (!active) return;
+#if DS2_C2R_MODE == 1
+  const float sgn = ((L - 1) & 1) ? -1.f : 1.f;        // the last channel's sign
+#else
+  const float sgn = 1.f;
+#endif
+#if DS2_C2R_MODE == 2
+#pragma unroll
+  for (int j = 0; j < 2; ++j) acc[j] = tot[j];
+#endif
+  const int len = out_lens != nullptr ? out_lens[n] : g.wo;
+  const int col = c0 + 32 * wave + fr;
+  if (col >= g.wo) return;
+#pragma unroll
+  for (int rr = 0; rr < 2; ++rr) {
+    const int row = orow + 4 * rr;
+    if (row >= g.ho) continue;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int m = m0 + (r & 3) + 8 * (r >> 2) + 4 * fh;
+      if (m < M) {
+        float v = __builtin_ldexpf((acc[rr][r] + acs[rr][r]) * sgn, -(m_exp[m] + en));
+        if (bias != nullptr) v += bias[m];
+        if (col >= len) v = 0.f;
+        out[(((int64_t)n * M + m) * g.ho + row) * g.wo + col] = v;
       }
     }
   }
@@ -2355,6 +2568,11 @@ static inline bool h3c_on() {
   const char* e = getenv("DS2_CONV_H3");
   return !(e != nullptr && e[0] == '0');
 }
+// DS2_CONV_2R=0 keeps conv2's fp16x3 forward on one output row per workgroup (conv_x6_kernel)
+static inline bool c2r_on() {
+  const char* e = getenv("DS2_CONV_2R");
+  return !(e != nullptr && e[0] == '0');
+}
 
 
 // workspace of a split-weight image of `elems` values per plane: NPL 3 planes, or 2 planes +
@@ -2466,6 +2684,16 @@ static ds2_status_t launch_x6(const float* in, const float* w, const float* bias
     int* m_exp;
     unsigned* n_amax;
     cx_h3_scales<DGRAD>(in, w, g, total, ws, m_exp, n_amax, st);
+    // two output rows per workgroup where the height stride is 2 (conv_h3_fwd2r_kernel)
+    if (!DGRAD && g.sh == 2 && c.RC == 1 && c2r_on()) {
+      hipLaunchKernelGGL((conv_x6_wimg_kernel<DGRAD, 2>), dim3(wgrid), dim3(256), 0, st, w, g, c, img,
+                         m_exp, DS2_C2R_MODE == 1 ? 1 : 2);
+      const int pairs = 4 * (g.ho / 8) + std::min(4, g.ho % 8);
+      const int64_t nwg2 = (int64_t)gx * pairs * g.n * cdiv(M, 32);
+      hipLaunchKernelGGL(conv_h3_fwd2r_kernel, dim3(static_cast<unsigned>(nwg2)), dim3(CX_T), 0, st,
+                         in, img, bias, out, g, out_lens, gx, pairs, m_exp, n_amax);
+      return launch_status("ds2_conv2d_fwd");
+    }
     hipLaunchKernelGGL((conv_x6_wimg_kernel<DGRAD, 2>), dim3(wgrid), dim3(256), 0, st, w, g, c, img, m_exp);
     hipLaunchKernelGGL((conv_x6_kernel<DGRAD, 3, 6, 2, 1, false, true, 2>), grid, dim3(CX_T), 0, st,
                        in, img, bias, out, g, out_lens, c, gx, gy, m_exp, n_amax);

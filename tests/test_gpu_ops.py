@@ -394,6 +394,40 @@ def test_conv_x6_is_fp32_accurate(dev, monkeypatch):
         assert max(errs[mode]) < 5e-6, errs
 
 
+@pytest.mark.parametrize("h,w,n,lens", [(81, 300, 2, None), (81, 501, 3, (501, 377, 120)),
+                                        (17, 90, 2, None), (9, 40, 1, None), (31, 260, 2, (200, 260))])
+def test_conv2_two_row_forward(dev, h, w, n, lens, monkeypatch):
+    """conv_h3_fwd2r_kernel (conv2's fp16x3 forward, output rows r and r + 4 per workgroup from
+    one 32-row patch, sign flip per input channel) against the one-row conv_x6_kernel
+    (DS2_CONV_2R=0) and fp64: the same fp32-level error (ragged output rows 41 / 9 / 5 / 16,
+    partial column blocks, bias, MaskConv lengths), and no systematic drift -- the mean of the
+    signed error stays a small fraction of the mean absolute error, as the sign split keeps
+    it for the one-row kernel ("MFMA rounding")."""
+    ci, co, kh, kw, sh, sw, ph, pw = 32, 32, 21, 11, 2, 1, 10, 5
+    g = torch.Generator().manual_seed(h * 1000 + w)
+    x = torch.randn(n, ci, h, w, generator=g, dtype=torch.float64).abs() * 3   # conv1 block: >= 0
+    wt = torch.randn(co, ci, kh, kw, generator=g, dtype=torch.float64) * 0.05
+    b = torch.randn(co, generator=g, dtype=torch.float64)
+    ref = F.conv2d(x, wt, b, stride=(sh, sw), padding=(ph, pw))
+    ld = None
+    if lens is not None:
+        ld = torch.tensor(lens, dtype=torch.int32, device=dev)
+        for i, L in enumerate(lens):
+            ref[i, :, :, L:] = 0.0
+    outs = {}
+    for two in ("1", "0"):
+        monkeypatch.setenv("DS2_CONV_2R", two)
+        outs[two] = ops.conv2d_fwd(x.float().to(dev), wt.float().to(dev), b.float().to(dev),
+                                   (sh, sw), (ph, pw), out_lens=ld).double().cpu()
+    scale = ref.abs().max().item()
+    e2 = (outs["1"] - ref).abs().max().item() / scale
+    e1 = (outs["0"] - ref).abs().max().item() / scale
+    assert e2 < 2e-6 and e2 <= 2.5 * e1 + 1e-7, (e2, e1)
+    err = (outs["1"] - ref)[ref != 0]
+    drift = (err.mean() / err.abs().mean()).item()
+    assert abs(drift) < 0.1, drift
+
+
 def test_conv_h3_scales_over_twelve_decades(dev, monkeypatch):
     """fp16x3 conv2 forward / dgrad with samples and output channels spread over 10^+-6, and
     the weight gradient with input and output channels spread likewise: the per-sample input
