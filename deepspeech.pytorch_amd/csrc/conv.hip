@@ -2244,7 +2244,7 @@ static_assert(CQ_UNITS <= 2 * CX_T, "two staging units per thread");
 template <int NPL = 3>
 __global__ void conv_x6q_wimg_kernel(const float* __restrict__ w, ConvDims g,
                                      unsigned short* __restrict__ img,
-                                     const int* __restrict__ m_exp) {
+                                     const int* __restrict__ m_exp, int no_split = 0) {
   const int M = g.ci, L = g.co;
   const int mbn = (M + 31) / 32;
   const int64_t per = (int64_t)32 * CQ_COP;
@@ -2268,8 +2268,8 @@ __global__ void conv_x6q_wimg_kernel(const float* __restrict__ w, ConvDims g,
         v = w[((int64_t)l * g.ci + m) * KHW + (q + g.sh * (aq - 1 - a)) * g.kw + (g.kw - 1 - b)];
     }
     // the second half of the k-steps (the kk = 1 waves' share) is stored negated: see the
-    // dgrad kernel's epilogue
-    if (slot >= ((CQ_NK + 1) / 2) * 16) v = -v;
+    // dgrad kernel's epilogue (no_split: nothing negated, conv_h3_dgrad2r_kernel)
+    if (!no_split && slot >= ((CQ_NK + 1) / 2) * 16) v = -v;
     const float sc = NPL == 2 && m < M ? h3_scale(m_exp[m]) : 1.f;
     cx_wimg_put<NPL>(img, ((((int64_t)q * mbn + mb) * L + l) * NPL) * per + e, per, v, sc);
   }
@@ -2480,6 +2480,178 @@ __global__ __launch_bounds__(CX_T, 1) void conv_x6q_dgrad_kernel(const float* __
   }
 }
 
+// ---------------------------------------------------------------------------
+// conv2 dgrad on fp16x3, two dx rows per workgroup: rows t and t + 4 of one stride class (dx
+// rows hq + sh t) read dy rows 4 apart -- exactly one row quad of the 4 x 2 fragments -- so ONE
+// column-pair patch of 16 dy rows serves both (row t's B fragments are quads 0..2, row t + 4's
+// quads 1..3) and both multiply the SAME weight fragments.  Per loop channel a workgroup then
+// stages 16 patch rows and one weight image for two dx rows (conv_x6q_dgrad_kernel: 12 rows and
+// one image for one row).  Waves: 8 x 32 columns, all 9 k-steps of both rows; the k-half sign
+// split becomes unnecessary because the big chain restarts every input channel (VALU-summed,
+// as conv_x6q_dgrad_kernel's FL form), so no chain is longer than 9 MFMAs.  Pair pitch 40 fp16
+// (5 x 16 B, odd) and the O copy 128 B off the E copy's bank phase keep the b128 fragment reads
+// conflict-free as in conv_x6q_dgrad_kernel.
+constexpr int C2Q_ROWS = 16;                          // patch rows: 12 class taps + one quad
+constexpr int C2Q_PP = 40;                            // fp16 per column pair
+constexpr int C2Q_OFFO = 5440;                        // O copy: 10880 B = 128 mod 256
+constexpr int C2Q_PPL = 10880;                        // fp16 per plane: 21760 B = 0 mod 256
+constexpr int C2Q_UNITS = 2 * CQ_PAIRS * (C2Q_ROWS / 4);   // (copy, pair, row quad) units
+constexpr int C2Q_PU = (C2Q_UNITS + CX_T - 1) / CX_T;
+static_assert(C2Q_OFFO >= CQ_PAIRS * C2Q_PP && C2Q_OFFO + CQ_PAIRS * C2Q_PP <= C2Q_PPL, "patch plane");
+
+__global__ __launch_bounds__(CX_T, 1) void conv_h3_dgrad2r_kernel(
+    const float* __restrict__ dy, const unsigned short* __restrict__ img, float* __restrict__ dx,
+    ConvDims g, int gx, int gy, const int* __restrict__ m_exp,
+    const unsigned* __restrict__ n_amax) {
+  constexpr int WPL = 32 * CQ_COP;
+  constexpr int wstride = 2 * WPL;
+  __shared__ __attribute__((aligned(16))) unsigned short ps[2 * 2 * C2Q_PPL];
+  __shared__ __attribute__((aligned(16))) unsigned short ws[2 * wstride];
+  const int M = g.ci, L = g.co;
+  const int in_h = g.ho, in_w = g.wo, out_h = g.hi, out_w = g.wi;
+  const int mbn = (M + 31) / 32;
+  int bx, by, bz;
+  xcd_tile(gx, gy, bx, by, bz);
+  const int n = bz / mbn;
+  const int mb = bz - n * mbn;
+  const int m0 = mb * 32;
+  const int c0 = bx * CX_COLS;
+  // (class q, row pair) of this workgroup: rows t and t + 4 with t = 8 b + j, j < 4
+  int pr = by, hq = 0, q, cnt = 0;
+  for (q = 0; q < g.sh; ++q) {
+    hq = ((q - g.ph) % g.sh + g.sh) % g.sh;
+    cnt = hq < g.hi ? (g.hi - 1 - hq) / g.sh + 1 : 0;
+    const int pairs = 4 * (cnt / 8) + min(4, cnt % 8);
+    if (pr < pairs) break;
+    pr -= pairs;
+  }
+  const int t = 8 * (pr >> 2) + (pr & 3);
+  const int A = class_taps(g, q);
+  const int orow = hq + g.sh * t;                      // and orow + 4 sh (class row t + 4)
+  const bool second = t + 4 < cnt;
+  const int prow0 = (orow + g.ph - q) / g.sh - (A - 1);
+  const int pcol0 = c0 + g.pw - g.kw + 1;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int plane_in = in_h * in_w;
+  const float* inn = dy + (int64_t)n * L * plane_in;
+  const unsigned short* wimg = img + ((int64_t)q * mbn + mb) * L * wstride;
+  constexpr int wchunks = wstride / 8;
+  constexpr int WR = (wchunks + CX_T - 1) / CX_T;
+  const int en = h3_exp(n_amax[n]);
+  const float nsc = h3_scale(en);
+
+  int goff[C2Q_PU][8];
+  int soff[C2Q_PU];
+#pragma unroll
+  for (int u = 0; u < C2Q_PU; ++u) {
+    const int unit = tid + CX_T * u;
+    const int cp = unit / (CQ_PAIRS * 4), rem = unit - cp * (CQ_PAIRS * 4);
+    const int j = rem >> 2, rq = rem & 3;
+    const int col = pcol0 + 2 * j + cp;
+    soff[u] = unit < C2Q_UNITS ? cp * C2Q_OFFO + j * C2Q_PP + 8 * rq : -1;
+#pragma unroll
+    for (int x = 0; x < 8; ++x) {
+      const int a = 4 * rq + (x >> 1), ir = prow0 + a, ic = col + (x & 1);
+      const bool ok = unit < C2Q_UNITS && a < A + 4 && ir >= 0 && ir < in_h && ic >= 0 && ic < in_w;
+      goff[u][x] = ok ? (ir * in_w + ic) * 4 : 0x7ffffff0;
+    }
+  }
+
+  float rp[C2Q_PU][8];
+  u32x4 rw[WR];
+  auto load = [&](int l) __attribute__((always_inline)) {
+    const __amdgpu_buffer_rsrc_t rs = conv_rsrc(inn + (int64_t)l * plane_in, plane_in);
+#pragma unroll
+    for (int u = 0; u < C2Q_PU; ++u)
+#pragma unroll
+      for (int x = 0; x < 8; ++x)
+        rp[u][x] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, goff[u][x], 0, 0));
+    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<unsigned short*>(wimg + (int64_t)l * wstride), (short)0, wstride * 2, 0x00020000);
+#pragma unroll
+    for (int r = 0; r < WR; ++r) {
+      const int i = tid + CX_T * r;
+      rw[r] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                            wr, i < wchunks ? i * 16 : 0x7ffffff0, 0, 0));
+    }
+  };
+  auto store = [&](int b) __attribute__((always_inline)) {
+    unsigned short* pb = ps + b * (2 * C2Q_PPL);
+    unsigned short* wb = ws + b * wstride;
+#pragma unroll
+    for (int u = 0; u < C2Q_PU; ++u)
+      if (soff[u] >= 0) cx_store8<2>(pb, C2Q_PPL, soff[u], rp[u], nsc);
+#pragma unroll
+    for (int r = 0; r < WR; ++r) {
+      const int i = tid + CX_T * r;
+      if (i < wchunks) *reinterpret_cast<u32x4*>(wb + 8 * i) = rw[r];
+    }
+  };
+
+  f32x16 acc[2], acs[2], acf[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[j][r] = acs[j][r] = acf[j][r] = 0.f;
+  const int fr = lane & 31, fh = lane >> 5;
+  const bool active = c0 + 32 * wave < out_w;
+
+  load(0);
+  store(0);
+  __syncthreads();
+  for (int l = 0; l < L; ++l) {
+    const int cur = l & 1;
+    if (l + 1 < L) load(l + 1);
+    if (active) {
+      const unsigned short* pc = ps + cur * (2 * C2Q_PPL);
+      const unsigned short* wc = ws + cur * wstride;
+#pragma unroll
+      for (int st = 0; st < CQ_NK; ++st) {
+        const int rq = st / 3, cq = st - (st / 3) * 3;
+        bf16x8 af[3], b0[3], b1[3];
+        const int aw = fr * CQ_COP + (st * 2 + fh) * 8;
+        const int sc = 32 * wave + fr + 4 * cq + 2 * fh;   // the lane's first patch column
+        const int ap = (sc & 1) * C2Q_OFFO + (sc >> 1) * C2Q_PP + 8 * rq;
+#pragma unroll
+        for (int pl = 0; pl < 2; ++pl) {
+          af[pl] = *reinterpret_cast<const bf16x8*>(wc + pl * WPL + aw);
+          b0[pl] = *reinterpret_cast<const bf16x8*>(pc + pl * C2Q_PPL + ap);
+          b1[pl] = *reinterpret_cast<const bf16x8*>(pc + pl * C2Q_PPL + ap + 8);
+        }
+        cx_mma_h3s(af, b0, acc[0], acs[0]);
+        cx_mma_h3s(af, b1, acc[1], acs[1]);
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        acf[j] += acc[j];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+      }
+    }
+    // the other buffer was last read in channel l - 1, before the previous barrier
+    if (l + 1 < L) store(cur ^ 1);
+    __syncthreads();
+  }
+  if (!active) return;
+  const int col = c0 + 32 * wave + fr;
+  if (col >= out_w) return;
+#pragma unroll
+  for (int rr = 0; rr < 2; ++rr) {
+    if (rr == 1 && !second) continue;
+    const int row = orow + 4 * g.sh * rr;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int m = m0 + (r & 3) + 8 * (r >> 2) + 4 * fh;
+      if (m < M) {
+        const float v = __builtin_ldexpf(acf[rr][r] + acs[rr][r], -(m_exp[m] + en));
+        dx[(((int64_t)n * M + m) * out_h + row) * out_w + col] = v;
+      }
+    }
+  }
+}
+
 static inline bool make_dims(ConvDims& g, int n, int c_in, int h_in, int w_in, int c_out, int kh,
                              int kw, int sh, int sw, int ph, int pw) {
   if (n < 0 || c_in < 1 || h_in < 1 || w_in < 1 || c_out < 1 || kh < 1 || kw < 1 || sh < 1 ||
@@ -2625,6 +2797,20 @@ static ds2_status_t launch_x6q(const float* dy, const float* w, float* dx, const
     int* m_exp;
     unsigned* n_amax;
     cx_h3_scales<true>(dy, w, g, total, ws, m_exp, n_amax, st);
+    if (c2r_on()) {
+      // two dx rows per workgroup (conv_h3_dgrad2r_kernel)
+      hipLaunchKernelGGL(conv_x6q_wimg_kernel<2>, dim3(wgrid), dim3(256), 0, st, w, g, img, m_exp, 1);
+      int pairs = 0;
+      for (int q = 0; q < g.sh; ++q) {
+        const int hq = ((q - g.ph) % g.sh + g.sh) % g.sh;
+        const int cnt = hq < g.hi ? (g.hi - 1 - hq) / g.sh + 1 : 0;
+        pairs += 4 * (cnt / 8) + std::min(4, cnt % 8);
+      }
+      const int64_t nwg2 = (int64_t)gx * pairs * g.n * cdiv(g.ci, 32);
+      hipLaunchKernelGGL(conv_h3_dgrad2r_kernel, dim3(static_cast<unsigned>(nwg2)), dim3(CX_T), 0, st,
+                         dy, img, dx, g, gx, pairs, m_exp, n_amax);
+      return launch_status("ds2_conv2d_dgrad");
+    }
     hipLaunchKernelGGL(conv_x6q_wimg_kernel<2>, dim3(wgrid), dim3(256), 0, st, w, g, img, m_exp);
     static const bool flush = !(getenv("DS2_CONV_DG_FLUSH") && atoi(getenv("DS2_CONV_DG_FLUSH")) == 0);
     if (flush)

@@ -1,5 +1,6 @@
-"""A/B: conv2's fp16x3 forward with two output rows per workgroup (conv_h3_fwd2r_kernel,
-default) vs one (conv_x6_kernel, DS2_CONV_2R=0), the headline shape (32 x [32, 81, 501] -> 32
+"""A/B: conv2's fp16x3 forward and dgrad with two output rows per workgroup
+(conv_h3_fwd2r_kernel / conv_h3_dgrad2r_kernel, default) vs one (conv_x6_kernel /
+conv_x6q_dgrad_kernel, DS2_CONV_2R=0), the headline shape (32 x [32, 81, 501] -> 32
 channels, 21 x 11 taps, stride (2, 1)), alternating in one process.
 usage: python scripts/bench_conv2_2r.py [rounds]"""
 import os
@@ -32,13 +33,17 @@ def timeit(fn, iters=20):
 
 
 rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 3
-ys = {}
-for r in range(rounds):
-    for mode in ("1", "0"):
-        os.environ["DS2_CONV_2R"] = mode
-        ms = timeit(lambda: ops.conv2d_fwd(x, wt, b, (sh, sw), (ph, pw)))
-        ys[mode] = ops.conv2d_fwd(x, wt, b, (sh, sw), (ph, pw))
-        print(f"round {r} {'two-row' if mode == '1' else 'one-row'}: {ms * 1e3:8.1f} us "
-              f"({flop / ms / 1e9:6.1f} TF, {flop / ms / 1e9 / 838.9:.3f} of 838.9)", flush=True)
-d = (ys["1"] - ys["0"]).abs().max().item() / ys["0"].abs().max().item()
-print(f"max |two - one| / max |one| = {d:.2e}")
+dy = torch.randn(n, co, ho, wo, device=dev)
+ops_ = {"fwd": lambda: ops.conv2d_fwd(x, wt, b, (sh, sw), (ph, pw)),
+        "dgrad": lambda: ops.conv2d_dgrad(dy, wt, (n, ci, h, w), (sh, sw), (ph, pw))}
+for name, fn in ops_.items():
+    ys = {}
+    for r in range(rounds):
+        for mode in ("1", "0"):
+            os.environ["DS2_CONV_2R"] = mode
+            ms = timeit(fn)
+            ys[mode] = fn()
+            print(f"{name} round {r} {'two-row' if mode == '1' else 'one-row'}: {ms * 1e3:8.1f} us "
+                  f"({flop / ms / 1e9:6.1f} TF, {flop / ms / 1e9 / 838.9:.3f} of 838.9)", flush=True)
+    d = (ys["1"] - ys["0"]).abs().max().item() / ys["0"].abs().max().item()
+    print(f"{name}: max |two - one| / max |one| = {d:.2e}")

@@ -428,6 +428,33 @@ def test_conv2_two_row_forward(dev, h, w, n, lens, monkeypatch):
     assert abs(drift) < 0.1, drift
 
 
+@pytest.mark.parametrize("h,w,n", [(81, 300, 2), (81, 501, 1), (17, 90, 2), (9, 40, 1), (31, 260, 2),
+                                   (2, 30, 1)])
+def test_conv2_two_row_dgrad(dev, h, w, n, monkeypatch):
+    """conv_h3_dgrad2r_kernel (conv2's fp16x3 dgrad, dx rows t and t + 4 of a stride class per
+    workgroup from one 16-row dy patch, the big chain restarted per output channel) against the
+    one-row conv_x6q_dgrad_kernel (DS2_CONV_2R=0) and fp64: fp32-level error on ragged class row
+    counts (41 + 40, 9 + 8, 16 + 15, 5 + 4, 1 + 1 rows), and no systematic drift."""
+    ci, co, kh, kw, sh, sw, ph, pw = 32, 32, 21, 11, 2, 1, 10, 5
+    g = torch.Generator().manual_seed(h * 1000 + w + 7)
+    ho, wo = (h + 2 * ph - kh) // sh + 1, (w + 2 * pw - kw) // sw + 1
+    wt = torch.randn(co, ci, kh, kw, generator=g, dtype=torch.float64) * 0.05
+    dy = torch.randn(n, co, ho, wo, generator=g, dtype=torch.float64)
+    ref = torch.nn.grad.conv2d_input((n, ci, h, w), wt, dy, stride=(sh, sw), padding=(ph, pw))
+    outs = {}
+    for two in ("1", "0"):
+        monkeypatch.setenv("DS2_CONV_2R", two)
+        outs[two] = ops.conv2d_dgrad(dy.float().to(dev), wt.float().to(dev), (n, ci, h, w), (sh, sw),
+                                     (ph, pw)).double().cpu()
+    scale = ref.abs().max().item()
+    e2 = (outs["1"] - ref).abs().max().item() / scale
+    e1 = (outs["0"] - ref).abs().max().item() / scale
+    assert e2 < 2e-6 and e2 <= 2.5 * e1 + 1e-7, (e2, e1)
+    err = (outs["1"] - ref)[ref != 0]
+    drift = (err.mean() / err.abs().mean()).item()
+    assert abs(drift) < 0.1, drift
+
+
 def test_conv_h3_scales_over_twelve_decades(dev, monkeypatch):
     """fp16x3 conv2 forward / dgrad with samples and output channels spread over 10^+-6, and
     the weight gradient with input and output channels spread likewise: the per-sample input
