@@ -1770,12 +1770,14 @@ __global__ __launch_bounds__(CX_T, 1) void conv_h3_fwd2r_kernel(
       }
     }
 #elif DS2_C2R_MODE == 2
-    // the big chain restarts every channel and is summed by the VALU (RNE)
+    // both chains restart every channel and are folded into a VALU sum (RNE); odd channels
+    // ran on the negated weight image, so they are subtracted
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      tot[j] += acc[j];
+      if (l & 1) tot[j] -= acc[j] + acs[j];
+      else tot[j] += acc[j] + acs[j];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+      for (int r = 0; r < 16; ++r) acc[j][r] = acs[j][r] = 0.f;
     }
 #endif
     __syncthreads();
@@ -1792,7 +1794,11 @@ __global__ __launch_bounds__(CX_T, 1) void conv_h3_fwd2r_kernel(
 #endif
 #if DS2_C2R_MODE == 2
 #pragma unroll
-  for (int j = 0; j < 2; ++j) acc[j] = tot[j];
+  for (int j = 0; j < 2; ++j) {
+    acc[j] = tot[j];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acs[j][r] = 0.f;
+  }
 #endif
   const int len = out_lens != nullptr ? out_lens[n] : g.wo;
   const int col = c0 + 32 * wave + fr;
@@ -2244,7 +2250,7 @@ static_assert(CQ_UNITS <= 2 * CX_T, "two staging units per thread");
 template <int NPL = 3>
 __global__ void conv_x6q_wimg_kernel(const float* __restrict__ w, ConvDims g,
                                      unsigned short* __restrict__ img,
-                                     const int* __restrict__ m_exp, int no_split = 0) {
+                                     const int* __restrict__ m_exp, int flip_odd = 0) {
   const int M = g.ci, L = g.co;
   const int mbn = (M + 31) / 32;
   const int64_t per = (int64_t)32 * CQ_COP;
@@ -2268,8 +2274,8 @@ __global__ void conv_x6q_wimg_kernel(const float* __restrict__ w, ConvDims g,
         v = w[((int64_t)l * g.ci + m) * KHW + (q + g.sh * (aq - 1 - a)) * g.kw + (g.kw - 1 - b)];
     }
     // the second half of the k-steps (the kk = 1 waves' share) is stored negated: see the
-    // dgrad kernel's epilogue (no_split: nothing negated, conv_h3_dgrad2r_kernel)
-    if (!no_split && slot >= ((CQ_NK + 1) / 2) * 16) v = -v;
+    // dgrad kernel's epilogue (flip_odd: the odd loop channels instead, conv_h3_dgrad2r_kernel)
+    if (flip_odd ? (l & 1) != 0 : slot >= ((CQ_NK + 1) / 2) * 16) v = -v;
     const float sc = NPL == 2 && m < M ? h3_scale(m_exp[m]) : 1.f;
     cx_wimg_put<NPL>(img, ((((int64_t)q * mbn + mb) * L + l) * NPL) * per + e, per, v, sc);
   }
@@ -2486,9 +2492,11 @@ __global__ __launch_bounds__(CX_T, 1) void conv_x6q_dgrad_kernel(const float* __
 // column-pair patch of 16 dy rows serves both (row t's B fragments are quads 0..2, row t + 4's
 // quads 1..3) and both multiply the SAME weight fragments.  Per loop channel a workgroup then
 // stages 16 patch rows and one weight image for two dx rows (conv_x6q_dgrad_kernel: 12 rows and
-// one image for one row).  Waves: 8 x 32 columns, all 9 k-steps of both rows; the k-half sign
-// split becomes unnecessary because the big chain restarts every input channel (VALU-summed,
-// as conv_x6q_dgrad_kernel's FL form), so no chain is longer than 9 MFMAs.  Pair pitch 40 fp16
+// one image for one row).  Waves: 8 x 32 columns, all 9 k-steps of both rows.  Both MFMA chains
+// (big and small products) restart every channel and are folded into a VALU sum (RNE), so no
+// chain is longer than 9 MFMAs; and the k-half sign split becomes a split by channel parity: odd
+// channels run on the negated weight image and are subtracted, so the MFMAs' floor of low
+// addend bits drifts the even and the odd channels' terms in opposite directions.  Pair pitch 40 fp16
 // (5 x 16 B, odd) and the O copy 128 B off the E copy's bank phase keep the b128 fragment reads
 // conflict-free as in conv_x6q_dgrad_kernel.
 constexpr int C2Q_ROWS = 16;                          // patch rows: 12 class taps + one quad
@@ -2623,11 +2631,14 @@ __global__ __launch_bounds__(CX_T, 1) void conv_h3_dgrad2r_kernel(
         cx_mma_h3s(af, b0, acc[0], acs[0]);
         cx_mma_h3s(af, b1, acc[1], acs[1]);
       }
+      // both chains restart every channel; odd channels ran on negated weights, so their
+      // chains hold -(their sum) and drift the other way in the true sum
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        acf[j] += acc[j];
+        if (l & 1) acf[j] -= acc[j] + acs[j];
+        else acf[j] += acc[j] + acs[j];
 #pragma unroll
-        for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+        for (int r = 0; r < 16; ++r) acc[j][r] = acs[j][r] = 0.f;
       }
     }
     // the other buffer was last read in channel l - 1, before the previous barrier
@@ -2645,7 +2656,7 @@ __global__ __launch_bounds__(CX_T, 1) void conv_h3_dgrad2r_kernel(
     for (int r = 0; r < 16; ++r) {
       const int m = m0 + (r & 3) + 8 * (r >> 2) + 4 * fh;
       if (m < M) {
-        const float v = __builtin_ldexpf(acf[rr][r] + acs[rr][r], -(m_exp[m] + en));
+        const float v = __builtin_ldexpf(acf[rr][r], -(m_exp[m] + en));
         dx[(((int64_t)n * M + m) * out_h + row) * out_w + col] = v;
       }
     }
@@ -2873,7 +2884,7 @@ static ds2_status_t launch_x6(const float* in, const float* w, const float* bias
     // two output rows per workgroup where the height stride is 2 (conv_h3_fwd2r_kernel)
     if (!DGRAD && g.sh == 2 && c.RC == 1 && c2r_on()) {
       hipLaunchKernelGGL((conv_x6_wimg_kernel<DGRAD, 2>), dim3(wgrid), dim3(256), 0, st, w, g, c, img,
-                         m_exp, DS2_C2R_MODE == 1 ? 1 : 2);
+                         m_exp, DS2_C2R_MODE == 0 ? 2 : 1);
       const int pairs = 4 * (g.ho / 8) + std::min(4, g.ho % 8);
       const int64_t nwg2 = (int64_t)gx * pairs * g.n * cdiv(M, 32);
       hipLaunchKernelGGL(conv_h3_fwd2r_kernel, dim3(static_cast<unsigned>(nwg2)), dim3(CX_T), 0, st,
