@@ -30,7 +30,8 @@ struct CtcWs {
   float* lp;         // [n][t_max][c]       log-softmax
   float* alpha;      // [n][t_max][s_max]
   float* beta;       // [n][t_max][s_max]
-  float* nll;        // [n]
+  double* nll;       // [n]
+  double* shift;     // [2][n][t_max]       the row maxima subtracted by the alpha / beta scans
   int* offs;         // [n]                 label offsets
   int* cls_start;    // [n][65]             per-class start into cls_pos
   int* cls_pos;      // [n][max_label_len]  label positions grouped by class
@@ -92,7 +93,11 @@ __global__ __launch_bounds__(64) void ctc_prep_kernel(
 //    loop issues no global loads: a load there made the waitcnt pass wait for the
 //    previous steps' alpha/beta row stores every step (1.1-1.3 us per step).  A thread
 //    owns the states s = tid + kScanThreads * k; their labels and skip-transition flags
-//    are computed once.
+//    are computed once.  Each row is stored minus the previous row's maximum (a one-step-
+//    delayed rescaling: the per-wave maxima meet in LDS behind the step's barrier, so no extra
+//    barrier), and the subtracted amounts are summed in fp64 per frame (`shift`).  The stored
+//    values stay O(1-10) instead of growing to ~|log p| (~1e3 at T' = 501), whose fp32 ulp
+//    (~1e-4) was a uniform relative error of every gradient term exp(alpha + beta + nll - lp).
 constexpr int kScanPer = (kCtcMaxS + kScanThreads - 1) / kScanThreads;
 constexpr int kScanChunk = 256;        // frames of log probs per LDS stage (C <= 64)
 
@@ -100,8 +105,9 @@ __global__ __launch_bounds__(kScanThreads) void ctc_scan_kernel(
     const float* __restrict__ lp_all, int t_max, int c, const int* __restrict__ labels,
     const int* __restrict__ label_lens, const int* __restrict__ act_lens,
     const int* __restrict__ offs, int blank, int s_max, float* __restrict__ alpha_all,
-    float* __restrict__ beta_all, float* __restrict__ nll_out) {
+    float* __restrict__ beta_all, double* __restrict__ shift_all, double* __restrict__ nll_out) {
   __shared__ float rows[2][kCtcMaxS];
+  __shared__ float wmax[2][kScanThreads / 64];
   __shared__ int lab_s[kMaxLabel];
   __shared__ float lpc[kScanChunk * 64];
   const int b = blockIdx.x;
@@ -115,6 +121,7 @@ __global__ __launch_bounds__(kScanThreads) void ctc_scan_kernel(
   __syncthreads();
   const float* lp = lp_all + (int64_t)b * t_max * c;
   float* out = (is_beta ? beta_all : alpha_all) + (int64_t)b * t_max * s_max;
+  double* shift = shift_all + ((int64_t)blockIdx.y * gridDim.x + b) * t_max;
   int ls[kScanPer];
   bool skip[kScanPer];
 #pragma unroll
@@ -126,6 +133,7 @@ __global__ __launch_bounds__(kScanThreads) void ctc_scan_kernel(
   }
   int cur = 0;
   int f0 = 0, f1 = 0;                  // frames [f0, f1) staged in lpc
+  double off = 0.0;                    // the row maxima subtracted so far (true = stored + off)
   for (int step = 0; step < T; ++step) {
     const int t = is_beta ? T - 1 - step : step;
     if (t < f0 || t >= f1) {           // uniform: stage the next chunk of frames
@@ -137,6 +145,15 @@ __global__ __launch_bounds__(kScanThreads) void ctc_scan_kernel(
     }
     const float* lpt = lpc + (t - f0) * c;
     const float* prv = rows[cur ^ 1];
+    float msub = 0.f;                  // the previous row's maximum, subtracted from this row
+    if (step > 0) {
+      float m = wmax[cur ^ 1][0];
+#pragma unroll
+      for (int w = 1; w < kScanThreads / 64; ++w) m = fmaxf(m, wmax[cur ^ 1][w]);
+      msub = m == -INFINITY ? 0.f : m;
+      off += msub;
+    }
+    float lm = -INFINITY;
 #pragma unroll
     for (int k = 0; k < kScanPer; ++k) {
       const int st = tid + kScanThreads * k;
@@ -149,22 +166,27 @@ __global__ __launch_bounds__(kScanThreads) void ctc_scan_kernel(
         v = prv[st];
         if (st + d >= 0 && st + d < S) v = log_add_fast(v, prv[st + d]);
         if (skip[k]) v = log_add_fast(v, prv[st + 2 * d]);
-        v = (v == -INFINITY) ? -INFINITY : v + lpt[ls[k]];
+        v = (v == -INFINITY) ? -INFINITY : v + (lpt[ls[k]] - msub);
       }
+      lm = fmaxf(lm, v);
       rows[cur][st] = v;
       out[(int64_t)t * s_max + st] = v;
     }
+    lm = wave_max(lm);
+    if ((tid & 63) == 0) wmax[cur][tid >> 6] = lm;
+    if (tid == 0) shift[t] = off;
     __syncthreads();
     cur ^= 1;
   }
   if (!is_beta && tid == 0) {
-    float ll;
+    double ll;
     if (T == 0) {
-      ll = (L == 0) ? 0.f : -INFINITY;
+      ll = (L == 0) ? 0.0 : -INFINITY;
     } else {
       const float* last = rows[cur ^ 1];
-      ll = last[S - 1];
-      if (S >= 2) ll = log_add(ll, last[S - 2]);
+      float v = last[S - 1];
+      if (S >= 2) v = log_add(v, last[S - 2]);
+      ll = v == -INFINITY ? -INFINITY : (double)v + off;
     }
     nll_out[b] = -ll;
   }
@@ -176,7 +198,8 @@ __global__ __launch_bounds__(kScanThreads) void ctc_scan_kernel(
 __global__ void ctc_grad_kernel(int t_max, int n, int c, int blank, int zero_infinity,
                                 const int* __restrict__ act_lens, const int* __restrict__ label_lens,
                                 const float* __restrict__ lp_all, const float* __restrict__ alpha_all,
-                                const float* __restrict__ beta_all, const float* __restrict__ nll_all,
+                                const float* __restrict__ beta_all, const double* __restrict__ shift_all,
+                                const double* __restrict__ nll_all,
                                 const int* __restrict__ cls_start, const int* __restrict__ cls_pos,
                                 int s_max, int max_l, float* __restrict__ costs,
                                 float* __restrict__ grads) {
@@ -187,10 +210,10 @@ __global__ void ctc_grad_kernel(int t_max, int n, int c, int blank, int zero_inf
   const int b = row - t * n;
   int T = act_lens[b];
   T = T > t_max ? t_max : (T < 0 ? 0 : T);
-  const float nll = nll_all[b];
-  const bool feasible = (nll != INFINITY) && (nll == nll);
+  const double nll_d = nll_all[b];
+  const bool feasible = (nll_d != INFINITY) && (nll_d == nll_d);
   if (t == 0 && lane == 0 && costs != nullptr)
-    costs[b] = feasible ? nll : (zero_infinity ? 0.f : INFINITY);
+    costs[b] = feasible ? (float)nll_d : (zero_infinity ? 0.f : INFINITY);
   if (grads == nullptr) return;
   float* g = grads + (int64_t)row * c;
   if (t >= T || !feasible) {
@@ -202,6 +225,10 @@ __global__ void ctc_grad_kernel(int t_max, int n, int c, int blank, int zero_inf
   const float* lpt = lp_all + ((int64_t)b * t_max + t) * c;
   const float* al = alpha_all + ((int64_t)b * t_max + t) * s_max;
   const float* be = beta_all + ((int64_t)b * t_max + t) * s_max;
+  // alpha_t + beta_t + nll = stored alpha + stored beta + (both row shifts + nll): the large
+  // parts cancel in fp64, so the exponent's fp32 error is that of O(1) values
+  const float nll = (float)(shift_all[(int64_t)b * t_max + t] +
+                            shift_all[((int64_t)n + b) * t_max + t] + nll_d);
   const float lpb = lpt[blank];
   float accb = 0.f;
   for (int s = 2 * lane; s < S; s += 128) {
@@ -1337,7 +1364,8 @@ size_t ds2_ctc_workspace_size(int t_max, int n, int max_label_len) {
   const size_t s_max = 2 * (size_t)max_label_len + 1;
   const size_t ml = max_label_len > 0 ? max_label_len : 1;
   return al256((size_t)n * t_max * 64 * sizeof(float)) +
-         2 * al256((size_t)n * t_max * s_max * sizeof(float)) + al256((size_t)n * sizeof(float)) +
+         2 * al256((size_t)n * t_max * s_max * sizeof(float)) + al256((size_t)n * sizeof(double)) +
+         al256(2 * (size_t)n * t_max * sizeof(double)) +
          al256((size_t)n * sizeof(int)) + al256((size_t)n * 65 * sizeof(int)) +
          al256((size_t)n * ml * sizeof(int)) + 256;
 }
@@ -1358,7 +1386,8 @@ ds2_status_t ds2_ctc_loss(const float* acts, int t_max, int n, int c, const int*
   float* lp = reinterpret_cast<float*>(p); p += al256((size_t)n * t_max * 64 * sizeof(float));
   float* alpha = reinterpret_cast<float*>(p); p += al256((size_t)n * t_max * s_max * sizeof(float));
   float* beta = reinterpret_cast<float*>(p); p += al256((size_t)n * t_max * s_max * sizeof(float));
-  float* nll = reinterpret_cast<float*>(p); p += al256((size_t)n * sizeof(float));
+  double* nll = reinterpret_cast<double*>(p); p += al256((size_t)n * sizeof(double));
+  double* shift = reinterpret_cast<double*>(p); p += al256(2 * (size_t)n * t_max * sizeof(double));
   int* offs = reinterpret_cast<int*>(p); p += al256((size_t)n * sizeof(int));
   int* cls_start = reinterpret_cast<int*>(p); p += al256((size_t)n * 65 * sizeof(int));
   int* cls_pos = reinterpret_cast<int*>(p);
@@ -1369,9 +1398,9 @@ ds2_status_t ds2_ctc_loss(const float* acts, int t_max, int n, int c, const int*
   hipLaunchKernelGGL(ctc_prep_kernel, dim3(n), dim3(64), 0, st, labels, label_lens, n, c,
                      ml, offs, cls_start, cls_pos);
   hipLaunchKernelGGL(ctc_scan_kernel, dim3(n, 2), dim3(kScanThreads), 0, st, lp, t_max, c, labels,
-                     label_lens, act_lens, offs, blank, s_max, alpha, beta, nll);
+                     label_lens, act_lens, offs, blank, s_max, alpha, beta, shift, nll);
   hipLaunchKernelGGL(ctc_grad_kernel, dim3(cdiv(rows > 0 ? rows : 1, 4)), dim3(256), 0, st, t_max,
-                     n, c, blank, zero_infinity, act_lens, label_lens, lp, alpha, beta, nll,
+                     n, c, blank, zero_infinity, act_lens, label_lens, lp, alpha, beta, shift, nll,
                      cls_start, cls_pos, s_max, ml, costs, grads);
   return launch_status("ds2_ctc_loss");
 }

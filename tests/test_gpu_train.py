@@ -262,21 +262,32 @@ def _check_train_step(dev, t_list, label_lens, seed, conv_tol=5e-4, zero_conv_bi
     # (the conv fp64 verdict is asserted after the oracle comparison, so one run prints both)
     rloss, rnew, _, rgrads, rnorm = orc.train_step(o, x, pct.clone(), tg, tl)
     assert abs(loss - float(rloss)) <= 1e-4 * abs(float(rloss))
-    g64 = None
+    g64 = n64 = None
     past = [name for name, p in m.named_parameters()
             if not name.startswith('conv.') and _rel(p.grad, rgrads[name]) > 5e-4]
-    if rnn_fp64 and past:
+    norm = float(tr.optimizer.norm.item())
+    norm_off = abs(norm - float(rnorm)) > 2e-4 * float(rnorm)
+    if rnn_fp64 and (past or norm_off):
         where = dev if rnn_fp64 == 'gpu' else torch.device('cpu')
         o64 = _OracleF64({k: v.detach().clone() for k, v in sd0.items()}, 5, 800, rnn_type=rnn_type,
                          bidirectional=bidirectional)
         o64.sd = {k: v.to(where) for k, v in o64.sd.items()}
-        _, _, _, g64, _ = orc.train_step(o64, x.double().to(where), pct.clone(), tg, tl)
+        _, _, _, g64, n64 = orc.train_step(o64, x.double().to(where), pct.clone(), tg, tl)
         g64 = {k: v.cpu() for k, v in g64.items()}
-    # the clip norm within 2e-4: every gradient of ours carries the fp32 CTC's rounding (log-space
-    # alpha / beta of magnitude ~nll, as warp-ctc's), the oracle's CTC runs in fp64 -- a uniform
-    # ~1e-4 shift of all gradients (bs 4: norm 7.9e-5 for our fp32-MFMA path, 1.06e-4 for the
-    # default, 2.6e-5 between the two; profiles/r4i_bs4_norm_probe.txt)
-    assert abs(float(tr.optimizer.norm.item()) - float(rnorm)) <= 2e-4 * float(rnorm)
+        n64 = float(n64)
+    # the clip norm within 2e-4 of the oracle's, or (rnn_fp64) no farther from the float64
+    # step's than 2x the oracle's own distance (+1e-5 relative).  The oracle's CTC is torch's
+    # CPU ctc_loss in fp32: log-space alpha / beta of magnitude ~|log p| (~1.5e3 at T' = 501)
+    # put ~7e-4 (max-abs / max-abs) on its CTC gradient at the bench length, where our
+    # rescaled scans sit at 5e-5 (test_ctc_rescaled_scan_at_the_benchmark_length); before
+    # them our norm sat ~1e-4 from the oracle's through the same effect
+    # (profiles/r4i_bs4_norm_probe.txt).
+    if n64 is not None and norm_off:
+        print(f"fp64 check clip norm: ours {abs(norm - n64) / n64:.2e} "
+              f"fp32 oracle {abs(float(rnorm) - n64) / n64:.2e}")
+        assert abs(norm - n64) <= 2.0 * abs(float(rnorm) - n64) + 1e-5 * n64
+    else:
+        assert not norm_off, (norm, float(rnorm))
     worst = {}
     bad_grads = []
     for name, p in m.named_parameters():
