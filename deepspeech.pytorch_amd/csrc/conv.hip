@@ -1613,11 +1613,14 @@ __global__ __launch_bounds__(CX_T, 1) void conv_x6_kernel(const float* __restric
 // read feeds six MFMAs instead of three.  Rows r, r + 4 with r = 8 b + j (j < 4) tile the
 // output rows in pairs; a row past the output is computed and not stored.
 // Waves: 8 x 32 columns, each all 18 k-steps of both rows (no k halves).  The sign split of
-// conv_x6_kernel (one k half on negated weights) becomes a flip per loop channel: the weight
-// image stores odd channels negated and the accumulators are negated between channels, so the
-// MFMAs' floor of low addend bits drifts one way in even channels and the other in odd ones
-// (same cancellation, DESIGN.md §4 "MFMA rounding").  Small products in their own chain
-// (cx_mma_h3s), the next channel's patch double-buffered as in conv_x6_kernel.
+// conv_x6_kernel (one k half on negated weights) becomes a sign per loop channel: the weight
+// image stores odd channels negated, both MFMA chains (hi.hi and the small products,
+// cx_mma_h3s) restart from zero every channel and are folded into a VALU total with the
+// channel's sign (DS2_C2R_MODE 2, the default), so the MFMAs' floor of low addend bits drifts
+// one way in even channels and the other in odd ones and cancels in the total (DESIGN.md §4
+// "MFMA rounding").  Mode 1 (negate the running accumulators between channels, no restart)
+// spilled 46 VGPRs; mode 0 keeps no sign split.  The next channel's patch is double-buffered as
+// in conv_x6_kernel.
 #ifndef DS2_C2R_MODE
 #define DS2_C2R_MODE 2
 #endif

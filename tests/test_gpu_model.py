@@ -166,7 +166,11 @@ def test_bf16_rnn_gemms_track_the_fp32_oracle(dev, rnn_type, bidir):
       - the fp32 model within 1e-3 (measured 1e-4);
       - the bf16 model within 5e-2 of the oracle run with the same bf16 rounding of its
         recurrent layers' input x and W_ih (straight-through; measured <= 2.5e-2): the
-        arithmetic itself;
+        arithmetic itself -- or within 2x of how far that oracle moves when its layer inputs
+        move by one ulp first (bf16 rounding decisions flip; two jitter draws), where that is
+        larger: the unidirectional LSTM's last layer (Lookahead + Hardtanh follows it) moves
+        by up to ~0.1 under such flips, so an ulp-level change upstream (conv2's two-row
+        kernels) took it from 0.025 to 0.091 against the same oracle;
       - the bf16 model within 2e-1 of the plain fp32 oracle, a layout error would be O(1).
         bf16 input projections alone move the unidirectional LSTM's last-layer bias
         gradients by 0.111 in the oracle itself (Lookahead + Hardtanh follows that layer),
@@ -216,7 +220,11 @@ def test_bf16_rnn_gemms_track_the_fp32_oracle(dev, rnn_type, bidir):
 
     # the oracle with its recurrent layers' input x and W_ih rounded to bf16 in the forward
     # (straight-through, fp32 otherwise)
+    # (jitter: the layer input moved by up to one ulp first, so that some bf16 rounding
+    # decisions flip -- what any fp32-level difference upstream of a bf16 rounding does)
     class _Bf16In(orc.OracleDS2):
+        jitter = None
+
         def _gru(self, x, lens, pre):
             saved = self.params
             self.params = dict(saved)
@@ -225,25 +233,39 @@ def test_bf16_rnn_gemms_track_the_fp32_oracle(dev, rnn_type, bidir):
                     if k.startswith(pre + '.weight_ih'):
                         w = self.params[k]
                         self.params[k] = w + (w.bfloat16().float() - w).detach()
+                if self.jitter is not None:
+                    u = torch.rand(x.shape, generator=torch.Generator().manual_seed(self.jitter))
+                    x = x * (1 + 2.0 ** -23 * (2 * u - 1))
                 x = x + (x.bfloat16().float() - x).detach()
                 return super()._gru(x, lens, pre)
             finally:
                 self.params = saved
-    ob = _Bf16In({k: v.detach().cpu() for k, v in m.state_dict().items()}, 3, 256,
-                 bidirectional=bidir, rnn_type=rnn_type)
-    pb = {k: v.detach().clone().requires_grad_(True) for k, v in ob.parameters().items()}
-    bl, _, bo, _ = ob.forward(x, sizes, training=True, params=pb)
-    lpb = F.log_softmax(bl.transpose(0, 1).double(), dim=2).float()
-    F.ctc_loss(lpb, tg.long(), bo.long(), tl.long(), blank=0, reduction='sum').backward()
+
+    def _bf16_oracle_grads(jitter):
+        ob = _Bf16In({k: v.detach().cpu() for k, v in m.state_dict().items()}, 3, 256,
+                     bidirectional=bidir, rnn_type=rnn_type)
+        ob.jitter = jitter
+        pb = {k: v.detach().clone().requires_grad_(True) for k, v in ob.parameters().items()}
+        bl, _, bo, _ = ob.forward(x, sizes, training=True, params=pb)
+        lpb = F.log_softmax(bl.transpose(0, 1).double(), dim=2).float()
+        F.ctc_loss(lpb, tg.long(), bo.long(), tl.long(), blank=0, reduction='sum').backward()
+        return pb
+    pb = _bf16_oracle_grads(None)
     d_emu = {k: _rel(pb[k].grad, params[k].grad) for k in dist}
     print("oracle with bf16 input projections vs oracle, largest first:",
           sorted(((round(v, 4), k) for k, v in d_emu.items()), reverse=True)[:6])
     d16 = {k: _rel(grads[1][k], pb[k].grad) for k in dist}
     print("bf16 model vs that oracle, largest first:",
           sorted(((round(v, 4), k) for k, v in d16.items()), reverse=True)[:6])
+    # the same oracle with its layer inputs one ulp away: how far bf16 rounding-decision flips
+    # alone move each gradient (the resolution of the comparison above)
+    pj = [_bf16_oracle_grads(j) for j in (1, 2)]
+    d_flip = {k: max(_rel(q[k].grad, pb[k].grad) for q in pj) for k in dist}
+    print("that oracle vs itself with one-ulp input jitter, largest first:",
+          sorted(((round(v, 4), k) for k, v in d_flip.items()), reverse=True)[:6])
     for k in dist:
         assert d32[k] < 1e-3, (k, d32[k])
-        assert d16[k] < 5e-2, (k, d16[k])
+        assert d16[k] < max(5e-2, 2.0 * d_flip[k]), (k, d16[k], d_flip[k])
         assert dist[k] < 2e-1, (k, dist[k])
 
 
