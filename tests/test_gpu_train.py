@@ -69,12 +69,15 @@ def test_benchmark_train_step_matches_oracle(dev):
     Two batch tiles at this shape: test_benchmark_train_step_two_batch_tiles.
 
     The conv block's arithmetic is checked against fp64 with our own Hardtanh masks (the
-    conv_fp64 check: every conv gradient within 2x of the fp32 oracle's distance).  End to end
+    conv_fp64 check: every conv gradient within 1.25x of the fp32 oracle's distance).  End to end
     against the oracle its gradients get 5e-2: ONE of the 2.6 M conv2 masks sits on the other
     side of a kink in the oracle's fp32 forward, and that one position moves conv2's weight
-    gradient by 1.8e-2 (profiles/r6e_bs4_conv_flip.txt)."""
+    gradient by 1.8e-2 (profiles/r6e_bs4_conv_flip.txt).  Recurrent / FC gradients past 5e-4
+    from the fp32 oracle go to the float64 arbiter: since the rescaled CTC scans ours sit
+    ~5e-6 from fp64, the oracle (torch's fp32 CPU CTC) up to 7e-4, so the oracle's own error
+    sets the distance between the two (4.1e-4 at the last run)."""
     _check_train_step(dev, [1001, 877, 508, 254], [150, 120, 80, 40], seed=11, conv_fp64=True,
-                      conv_tol=5e-2)
+                      conv_tol=5e-2, rnn_fp64=True)
 
 
 @pytest.mark.timeout(600)
@@ -108,7 +111,7 @@ def test_benchmark_train_step_two_batch_tiles(dev):
     t_list = [1001, 1001, 990, 950, 901, 877, 820, 760, 700, 640, 600, 508, 470, 400, 333,
               300, 254, 200, 150, 101]
     lab = [max(10, t // 7) for t in t_list]
-    _check_train_step(dev, t_list, lab, seed=12)
+    _check_train_step(dev, t_list, lab, seed=12, rnn_fp64='gpu')
 
 
 @pytest.mark.timeout(900)
@@ -173,7 +176,7 @@ class _OracleF64(orc.OracleDS2):
 def _check_train_step(dev, t_list, label_lens, seed, conv_tol=5e-4, zero_conv_bias=False,
                       conv_fp64=False, rnn_type='gru', rnn_fp64=False, bidirectional=True):
     """rnn_fp64: a recurrent / FC gradient past 5e-4 from the fp32 oracle still passes when it
-    sits within 2x (+1e-5) of the fp32 oracle's own distance from the same step in float64
+    sits within 1.25x (+1e-5) of the fp32 oracle's own distance from the same step in float64
     (the oracle's state and input in float64): both are fp32 approximations of one exact
     step, and over 501 recurrent steps the reference's own fp32 drifts.  The float64 step runs
     only when some gradient is past 5e-4; rnn_fp64='gpu' runs it on the GPU (the oracle's own
@@ -220,7 +223,7 @@ def _check_train_step(dev, t_list, label_lens, seed, conv_tol=5e-4, zero_conv_bi
         # gradient (ours) and the SAME Hardtanh masks (ours: 0 < y < 20 of our two block
         # outputs), so the kinks a last-bit difference moves (1 + 3 of 63 M positions between
         # an fp32 and an fp64 forward, profiles/r4g_bs32_probe.txt) drop out of both sides:
-        # our conv gradients may be at most 2x as far from that fp64 block as the fp32 oracle
+        # our conv gradients may be at most 1.25x as far from that fp64 block as the fp32 oracle
         # block (same masks) is, with a 1e-6 floor.  Measured with each block's own masks
         # instead, ours sat at 8.3e-4 of conv1.weight's max against the fp32 oracle's 2.8e-4:
         # flips, not arithmetic.
@@ -255,7 +258,7 @@ def _check_train_step(dev, t_list, label_lens, seed, conv_tol=5e-4, zero_conv_bi
             ours = _rel(p.grad, ref)
             own = _rel(g32[name], ref)
             print(f"conv fp64 check {name}: ours {ours:.2e} fp32 oracle {own:.2e}")
-            if ours > 2.0 * own + 1e-6:
+            if ours > 1.25 * own + 1e-6:
                 bad.append((name, ours, own))
     else:
         bad = []
@@ -276,7 +279,7 @@ def _check_train_step(dev, t_list, label_lens, seed, conv_tol=5e-4, zero_conv_bi
         g64 = {k: v.cpu() for k, v in g64.items()}
         n64 = float(n64)
     # the clip norm within 2e-4 of the oracle's, or (rnn_fp64) no farther from the float64
-    # step's than 2x the oracle's own distance (+1e-5 relative).  The oracle's CTC is torch's
+    # step's than 1.25x the oracle's own distance (+1e-5 relative).  The oracle's CTC is torch's
     # CPU ctc_loss in fp32: log-space alpha / beta of magnitude ~|log p| (~1.5e3 at T' = 501)
     # put ~7e-4 (max-abs / max-abs) on its CTC gradient at the bench length, where our
     # rescaled scans sit at 5e-5 (test_ctc_rescaled_scan_at_the_benchmark_length); before
@@ -285,7 +288,7 @@ def _check_train_step(dev, t_list, label_lens, seed, conv_tol=5e-4, zero_conv_bi
     if n64 is not None and norm_off:
         print(f"fp64 check clip norm: ours {abs(norm - n64) / n64:.2e} "
               f"fp32 oracle {abs(float(rnorm) - n64) / n64:.2e}")
-        assert abs(norm - n64) <= 2.0 * abs(float(rnorm) - n64) + 1e-5 * n64
+        assert abs(norm - n64) <= 1.25 * abs(float(rnorm) - n64) + 1e-5 * n64
     else:
         assert not norm_off, (norm, float(rnorm))
     worst = {}
@@ -309,7 +312,7 @@ def _check_train_step(dev, t_list, label_lens, seed, conv_tol=5e-4, zero_conv_bi
         exact_ok = False
         if g64 is not None and not name.startswith('conv.') and worst[name] > tol:
             ours64, own64 = _rel(p.grad, g64[name]), _rel(rgrads[name], g64[name])
-            exact_ok = ours64 <= 2.0 * own64 + 1e-5
+            exact_ok = ours64 <= 1.25 * own64 + 1e-5
             print(f"fp64 check {name}: ours {ours64:.2e} fp32 oracle {own64:.2e}")
         if worst[name] > tol and not exact_ok:
             bad_grads.append((name, worst[name]))
