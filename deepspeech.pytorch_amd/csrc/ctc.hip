@@ -1249,13 +1249,21 @@ __global__ __launch_bounds__(64) void ctc_beam_kernel(
 constexpr int ED_MAXC = 2048;   // ids per sequence
 constexpr int ED_MAXW = 1024;   // words per sequence
 
+// inclusive prefix minimum over the wave in VALU only: Hillis-Steele row shifts 1, 2, 4, 8
+// (lanes without a source keep their value -- min is idempotent), then row_bcast:15 / :31 carry
+// the rows' minima forward.  A __shfl_up chain (six ds_bpermute round trips) made the DP row
+// loop latency-bound (139 us per batch in the step)
+template <int CTRL, int RMASK, int BMASK>
+__device__ __forceinline__ int dpp_min_i(int v) {
+  return min(v, __builtin_amdgcn_update_dpp(v, v, CTRL, RMASK, BMASK, false));
+}
 __device__ __forceinline__ int wave_incl_min(int v) {
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const int o = __shfl_up(v, off, 64);
-    if (lane >= off) v = min(v, o);
-  }
+  v = dpp_min_i<0x111, 0xf, 0xf>(v);   // row_shr:1
+  v = dpp_min_i<0x112, 0xf, 0xf>(v);   // row_shr:2
+  v = dpp_min_i<0x114, 0xf, 0xf>(v);   // row_shr:4
+  v = dpp_min_i<0x118, 0xf, 0xf>(v);   // row_shr:8
+  v = dpp_min_i<0x142, 0xa, 0xf>(v);   // row_bcast:15 into rows 1, 3
+  v = dpp_min_i<0x143, 0xc, 0xf>(v);   // row_bcast:31 into rows 2, 3
   return v;
 }
 
@@ -1283,7 +1291,7 @@ __device__ int ed_levenshtein(const int* x, int m, const int* y, int n, int* r0,
       int v = wave_incl_min(j <= n ? e - j : 0x3fffffff);
       v = min(v, carry);
       if (j <= n) cur[j] = v + j;
-      carry = __shfl(v, 63, 64);
+      carry = __builtin_amdgcn_readlane(v, 63);
     }
     __syncthreads();
     int* tmp = prev;
@@ -1291,6 +1299,54 @@ __device__ int ed_levenshtein(const int* x, int m, const int* y, int n, int* r0,
     cur = tmp;
   }
   return prev[n];
+}
+
+// the same DP with the row in registers for n < 64 NC: lane l holds columns l + 64 c, D[i-1][j-1]
+// comes from the next-lower lane by DPP wave_shr:1 (lane 0: column 64 c - 1 by v_readlane), so
+// a row has no LDS round trip and no barrier; identical integer results
+template <int NC>
+__device__ int ed_levenshtein_reg(const int* x, int m, const int* y, int n) {
+  const int lane = threadIdx.x;
+  constexpr int BIG = 0x3fffffff;
+  int prev[NC], yv[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int j = lane + 64 * c;
+    prev[c] = j;
+    yv[c] = (j >= 1 && j <= n) ? y[j - 1] : -1;
+  }
+  for (int i = 1; i <= m; ++i) {
+    const int xi = x[i - 1];
+    int carry = BIG;
+    int cur[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int j = lane + 64 * c;
+      const int lo = c == 0 ? BIG : __builtin_amdgcn_readlane(prev[c > 0 ? c - 1 : 0], 63);
+      const int pj1 = __builtin_amdgcn_update_dpp(lo, prev[c], 0x138, 0xf, 0xf, false);  // wave_shr:1
+      int e = BIG;
+      if (j <= n) e = j == 0 ? i : min(prev[c] + 1, pj1 + (xi != yv[c] ? 1 : 0));
+      int v = wave_incl_min(j <= n ? e - j : BIG);
+      v = min(v, carry);
+      cur[c] = v + j;
+      carry = __builtin_amdgcn_readlane(v, 63);
+    }
+#pragma unroll
+    for (int c = 0; c < NC; ++c) prev[c] = cur[c];
+  }
+  int r = 0;
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+    if (c == (n >> 6)) r = __builtin_amdgcn_readlane(prev[c], n & 63);
+  return r;
+}
+
+__device__ __forceinline__ int ed_distance(const int* x, int m, const int* y, int n, int* r0, int* r1) {
+  if (n < 64) return ed_levenshtein_reg<1>(x, m, y, n);
+  if (n < 128) return ed_levenshtein_reg<2>(x, m, y, n);
+  if (n < 192) return ed_levenshtein_reg<3>(x, m, y, n);
+  if (n < 256) return ed_levenshtein_reg<4>(x, m, y, n);
+  return ed_levenshtein(x, m, y, n, r0, r1);
 }
 
 // compact non-space ids and word starts of one sequence into LDS
@@ -1366,9 +1422,9 @@ __global__ __launch_bounds__(64) void edit_distance_kernel(
     if (in_a) wida[w] = id; else widb[w - nwa] = id;
   }
   __syncthreads();
-  const int wer = ed_levenshtein(wida, nwa, widb, nwb, r0, r1);
+  const int wer = ed_distance(wida, nwa, widb, nwb, r0, r1);
   __syncthreads();
-  const int cer = ed_levenshtein(ca, nca, cb, ncb, r0, r1);
+  const int cer = ed_distance(ca, nca, cb, ncb, r0, r1);
   if (lane == 0) {
     out[4 * n + 0] = wer;
     out[4 * n + 1] = cer;

@@ -1570,6 +1570,11 @@ def test_edit_distance_vs_reference_semantics(dev):
     b_rows.append(list(range(1, 29)) * 35)
     a_rows.append([5, space, 6, space, space, 5])   # identical after strip / split
     b_rows.append([space, 5, space, 6, space, 5, space])
+    # reference lengths on both sides of the register-row DP's 64-column chunks (1-4 chunks
+    # in registers below 256 columns, the LDS-row DP from 256 on)
+    for lb in (63, 64, 127, 128, 191, 192, 255, 256):
+        a_rows.append([int(k) for k in g.integers(1, space, 300)])   # no spaces: n = lb
+        b_rows.append([int(k) for k in g.integers(1, space, lb)])
     n = len(a_rows)
     width = max(len(r) for r in a_rows)
     a = torch.zeros(n, width, dtype=torch.int32)
