@@ -1426,6 +1426,18 @@ __global__ __launch_bounds__(256) void amax_rows_kernel(const float* __restrict_
   float m = 0.f;
   const int c4 = cols / 4;
   int c = lane;
+  // up to 10 loads in flight per lane at once for rows up to 2560 columns (one batch instead of
+  // two of 4 and two single loads; 22.6 -> 22.1 us on 16032 x 2400, 6.98 TB/s)
+  if (c4 <= 640) {
+    f32x4 v[10];
+#pragma unroll
+    for (int k = 0; k < 10; ++k)
+      v[k] = c + 64 * k < c4 ? q[c + 64 * k] : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < 10; ++k)
+      m = fmaxf(m, fmaxf(fmaxf(fabsf(v[k][0]), fabsf(v[k][1])), fmaxf(fabsf(v[k][2]), fabsf(v[k][3]))));
+    c = c4;
+  }
   // 4 loads in flight per lane (a 4800-column row is 19 per lane)
   for (; c + 192 < c4; c += 256) {
     const f32x4 v0 = q[c], v1 = q[c + 64], v2 = q[c + 128], v3 = q[c + 192];

@@ -164,7 +164,7 @@ def test_sgemm_h3_rows_over_twelve_decades(dev, ta, tb, monkeypatch):
     assert torch.equal(c2, outs["h3"])
 
 
-@pytest.mark.parametrize("rows,cols", [(1, 4), (37, 52), (4800, 800), (5, 2048), (16032, 4800),
+@pytest.mark.parametrize("rows,cols", [(1, 4), (37, 52), (4800, 800), (5, 2048), (16032, 4800), (16032, 2400),
                                        (300, 4100)])
 def test_amax_rows_and_cols(dev, rows, cols):
     """ds2_amax: row and column maxima of |x| in one pass, bit-exact against torch (float bits;
