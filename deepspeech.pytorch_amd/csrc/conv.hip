@@ -2049,15 +2049,25 @@ constexpr int SW_DPL = 32 * SW_DP;          // bf16 per dy plane
 // NPL 2: fp16x3 -- dy staged as fp16 hi / lo of dy 2^e_co (co_amax: max |dy| of each output
 // channel over the batch), x as hi / lo of x 2^e_ci (ci_amax), three products per fragment pair;
 // wgrad_reduce_x6_kernel undoes 2^-(e_co + e_ci) on the summed partials
-template <int KW, int OFF0, int NW = 4, int NPL = 3>
+// SWC = 64 (NW 8, fp16x3): 64-column row stages -- x slot pitch 88 (11 x 16 B), dy pitch 72
+// (9 x 16 B), 80 x columns staged per 64 output columns instead of 48 per 32, half the stages
+// and barriers per MFMA; 131 KB of LDS.  Staging units (x: 32 channels x 10 runs per row, dy: 32
+// x 8): unit a = tid (waves 0-4 x row 0, waves 5-7 x row 1 units 0-191), unit b = waves 0-1 x
+// row 1 units 192-319, waves 2-5 dy, waves 6-7 none (kinds wave-uniform)
+template <int KW, int OFF0, int NW = 4, int NPL = 3, int SWC = SW_COLS>
 __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_x6_wgrad_sw_kernel(
     const float* __restrict__ dy, const float* __restrict__ x, float* __restrict__ partial,
     ConvDims g, int S, const unsigned* __restrict__ co_amax, const unsigned* __restrict__ ci_amax) {
   static_assert(NW == 4 || NW == 8, "waves per group");
+  static_assert(SWC == SW_COLS || (SWC == 64 && NW == 8 && NPL == 2), "64-column stages: NW 8, fp16x3");
   constexpr int RING = NW + 2;                // NW window rows + 2 incoming
-  __shared__ __attribute__((aligned(16))) unsigned short xs[3 * RING * SW_XSL];
-  __shared__ __attribute__((aligned(16))) unsigned short ds[2][3 * SW_DPL];
-  constexpr int XPL = RING * SW_XSL;
+  constexpr int XP = SWC == 64 ? 88 : SW_XP, DP = SWC == 64 ? 72 : SW_DP;
+  constexpr int XSL = 32 * XP, DPL = 32 * DP;
+  constexpr int XRUNS = (SWC + 16) / 8, DRUNS = SWC / 8;
+  constexpr bool DY_IN_A = NW == 8 && SWC == SW_COLS;   // the dy waves' unit rides in va
+  __shared__ __attribute__((aligned(16))) unsigned short xs[(SWC == 64 ? 2 : 3) * RING * XSL];
+  __shared__ __attribute__((aligned(16))) unsigned short ds[2][(SWC == 64 ? 2 : 3) * DPL];
+  constexpr int XPL = RING * XSL;
   constexpr int kOob = 0x7ffffff0;
   const int G = (g.kh + NW - 1) / NW;
   int gi, s;
@@ -2068,7 +2078,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_x6_wgrad_sw_ker
     gi = id % G;
     s = id / G;
   }
-  const int nch = (g.wo + SW_COLS - 1) / SW_COLS;
+  const int nch = (g.wo + SWC - 1) / SWC;
   const int R = g.n * nch * g.ho;                           // host: < 2^31
   const int r0 = static_cast<int>((int64_t)s * R / S);
   const int r1 = static_cast<int>((int64_t)(s + 1) * R / S);
@@ -2086,14 +2096,21 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_x6_wgrad_sw_ker
   // dy -- so the buffer resources stay scalar).  NW = 8: thread t takes unit t alone (waves
   // 0-2 x row 0, 3-5 x row 1, 6-7 dy; unit b unused)
   const int u1 = NW == 4 ? tid + 256 : tid;
-  const int ta = NW == 4 ? tid : (wave < 6 ? tid % 192 : 0);
-  const int xr_a = NW == 4 ? (wave == 3 ? 1 : 0) : (wave >= 3 ? 1 : 0);
-  const int xc_a = NW == 4 ? (ta / 6) & 31 : ta / 6, xj_a = ta % 6;
-  const bool a_is_x = NW == 4 || wave < 6;
-  const bool b_is_x = NW == 4 && wave < 2;
-  const bool b_is_dy = NW == 4 ? wave >= 2 : wave >= 6;
-  const int xc_b = (u1 / 6) & 31, xj_b = u1 % 6;             // x unit: incoming row 1
-  const int dc_b = (u1 - 384) >> 2, dj_b = (u1 - 384) & 3;   // dy unit
+  // (const initialisers, as in the 32-column form: assigning these inside if-constexpr branches
+  // made hipcc 7.2 pack sc_a / sc_b into one register pair and apply them with v_pk_mul_f32
+  // op_sel swapped -- wrong scales, test_conv_x6_wgrad_forms)
+  constexpr bool W64 = SWC == 64;
+  const int ta = W64 ? (wave < 5 ? tid : tid - 320) : (NW == 4 ? tid : (wave < 6 ? tid % 192 : 0));
+  const int xr_a = W64 ? (wave >= 5 ? 1 : 0) : NW == 4 ? (wave == 3 ? 1 : 0) : (wave >= 3 ? 1 : 0);
+  const int xc_a = W64 ? ta / XRUNS : NW == 4 ? (ta / 6) & 31 : ta / 6;
+  const int xj_a = W64 ? ta % XRUNS : ta % 6;
+  const bool a_is_x = W64 || NW == 4 || wave < 6;
+  const bool b_is_x = W64 ? wave < 2 : NW == 4 && wave < 2;
+  const bool b_is_dy = W64 ? (wave >= 2 && wave < 6) : NW == 4 ? wave >= 2 : wave >= 6;
+  const int xc_b = W64 ? (192 + tid) / XRUNS : (u1 / 6) & 31;      // x unit: incoming row 1
+  const int xj_b = W64 ? (192 + tid) % XRUNS : u1 % 6;
+  const int dc_b = W64 ? (tid - 128) / DRUNS : (u1 - 384) >> 2;    // dy unit
+  const int dj_b = W64 ? (tid - 128) % DRUNS : (u1 - 384) & 3;
   // fp16x3 staging scales of this thread's units (channels fixed for the whole launch)
   float sc_a = 1.f, sc_b = 1.f;
   if constexpr (NPL == 2) {
@@ -2101,7 +2118,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_x6_wgrad_sw_ker
     if (b_is_x && xc_b < g.ci) sc_b = h3_scale(h3_exp(ci_amax[xc_b]));
     if (b_is_dy && dc_b >= 0 && dc_b < g.co) {
       const float s = h3_scale(h3_exp(co_amax[dc_b]));
-      if (NW == 8) sc_a = s; else sc_b = s;
+      if (DY_IN_A) sc_a = s; else sc_b = s;
     }
   }
   f32x16 acc[KW];
@@ -2118,7 +2135,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_x6_wgrad_sw_ker
     const int ho0 = row % g.ho, q = row / g.ho;
     const int ch = q % nch, n = q / nch;
     const int nrow = min(r1 - row, g.ho - ho0);              // rows of this (n, chunk) segment
-    const int c0 = ch * SW_COLS;
+    const int c0 = ch * SWC;
     const __amdgpu_buffer_rsrc_t drs = conv_rsrc(dy + (int64_t)n * g.co * dplane, (int64_t)g.co * dplane);
     const __amdgpu_buffer_rsrc_t xrs = conv_rsrc(x + (int64_t)n * g.ci * xplane, (int64_t)g.ci * xplane);
     // loads of x rows xr0 + r (r < nr; r = 0 unit a, r = 1 unit b) and, when hd >= 0, dy row hd
@@ -2141,10 +2158,10 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_x6_wgrad_sw_ker
           vb[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
                                                 xrs, (cb + i >= 0 && cb + i < g.wi) ? vo + 4 * i : kOob, 0, 0));
       } else if (b_is_dy) {
-        // (NW = 8: the dy waves' unit goes in va, which they use for nothing else)
+        // (NW = 8, 32 columns: the dy waves' unit goes in va, which they use for nothing else)
         const int cb = c0 + 8 * dj_b;
         const int vo = (hd >= 0 && dc_b < g.co) ? (dc_b * dplane + hd * g.wo + cb) * 4 : kOob;
-        float* vd = NW == 8 ? va : vb;
+        float* vd = DY_IN_A ? va : vb;
 #pragma unroll
         for (int i = 0; i < 8; ++i)
           vd[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
@@ -2153,11 +2170,11 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_x6_wgrad_sw_ker
     };
     auto store = [&](int xr0, int nr, int db) {
       if (a_is_x && xr_a < nr)
-        cx_store8<NPL>(xs, XPL, slot_of(xr0 + xr_a) * SW_XSL + xc_a * SW_XP + 8 * xj_a, va, sc_a);
+        cx_store8<NPL>(xs, XPL, slot_of(xr0 + xr_a) * XSL + xc_a * XP + 8 * xj_a, va, sc_a);
       if (b_is_x) {
-        if (nr > 1) cx_store8<NPL>(xs, XPL, slot_of(xr0 + 1) * SW_XSL + xc_b * SW_XP + 8 * xj_b, vb, sc_b);
+        if (nr > 1) cx_store8<NPL>(xs, XPL, slot_of(xr0 + 1) * XSL + xc_b * XP + 8 * xj_b, vb, sc_b);
       } else if (b_is_dy && db >= 0) {
-        cx_store8<NPL>(ds[db], SW_DPL, dc_b * SW_DP + 8 * dj_b, NW == 8 ? va : vb, NW == 8 ? sc_a : sc_b);
+        cx_store8<NPL>(ds[db], DPL, dc_b * DP + 8 * dj_b, DY_IN_A ? va : vb, DY_IN_A ? sc_a : sc_b);
       }
     };
     // segment start: every slot and dy buffer is free once all waves pass this barrier; the
@@ -2178,13 +2195,15 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_x6_wgrad_sw_ker
       if (more) load(xin, g.sh, ho + 1);
       if (active) {
         const unsigned short* dsb = ds[ho & 1];
-        const unsigned short* xsl = xs + slot_of(xb + wave) * SW_XSL + fr * SW_XP;
-#pragma unroll
-        for (int kst = 0; kst < SW_COLS / 16; ++kst) {
+        const unsigned short* xsl = xs + slot_of(xb + wave) * XSL + fr * XP;
+        // (SWC 64: unrolled by 2, 8 VGPRs spilled, 905 us in isolation; not unrolled, 1 spilled,
+        // 943 us; fully unrolled, 10 spilled)
+#pragma unroll(SWC == 64 ? 2 : SWC / 16)
+        for (int kst = 0; kst < SWC / 16; ++kst) {
           bf16x8 af[3];
 #pragma unroll
           for (int pl = 0; pl < NPL; ++pl)
-            af[pl] = *reinterpret_cast<const bf16x8*>(dsb + pl * SW_DPL + fr * SW_DP + 16 * kst + 8 * fh);
+            af[pl] = *reinterpret_cast<const bf16x8*>(dsb + pl * DPL + fr * DP + 16 * kst + 8 * fh);
 #pragma unroll
           for (int pi = 0; pi < NPL; ++pi) {
             const int pl = NPL - 1 - pi;
@@ -3000,6 +3019,15 @@ static inline bool h3w_on() {
   return !(e != nullptr && e[0] == '0');
 }
 
+// DS2_CONV_W64=1: the fp16x3 sliding-window wgrad on 64-column row stages (read per call).
+// Opt-in: 0.70 GB of HBM per launch against 0.93 GB (PMC, FETCH_SIZE x 2 + WRITE_SIZE), but
+// 905 vs 860-880 us at the model's conv2 shape (scripts/bench_conv2_wgrad.py): the second
+// staging unit per thread pushes it past 256 VGPRs (8 spilled)
+static inline bool w64_on() {
+  const char* e = getenv("DS2_CONV_W64");
+  return e != nullptr && e[0] == '1';
+}
+
 static inline int x6w_splits(const ConvDims& g);
 // bytes of the x6 wgrad partial blocks (the fp16x3 channel maxima follow, 256-B aligned)
 static inline size_t x6w_part_bytes(const ConvDims& g) {
@@ -3143,8 +3171,12 @@ ds2_status_t ds2_conv2d_wgrad(const float* dy, const float* x, float* dw, float*
                          dpl, co_am);
       hipLaunchKernelGGL(conv_h3_chamax_kernel, dim3(cx, c_in), dim3(256), 0, st, x, n, c_in, xpl,
                          ci_am);
-      hipLaunchKernelGGL((conv_x6_wgrad_sw_kernel<11, 3, 8, 2>), dim3(G * slabs), dim3(512), 0, st,
-                         dy, x, partial, g, slabs, co_am, ci_am);
+      if (w64_on())
+        hipLaunchKernelGGL((conv_x6_wgrad_sw_kernel<11, 3, 8, 2, 64>), dim3(G * slabs), dim3(512), 0,
+                           st, dy, x, partial, g, slabs, co_am, ci_am);
+      else
+        hipLaunchKernelGGL((conv_x6_wgrad_sw_kernel<11, 3, 8, 2>), dim3(G * slabs), dim3(512), 0, st,
+                           dy, x, partial, g, slabs, co_am, ci_am);
     } else if (x6w_sw(g))
       hipLaunchKernelGGL((conv_x6_wgrad_sw_kernel<11, 3, 8>), dim3(G * slabs), dim3(512), 0, st, dy,
                          x, partial, g, slabs, nullptr, nullptr);

@@ -498,11 +498,14 @@ def test_conv_h3_scales_over_twelve_decades(dev, monkeypatch):
                                  (3, 5, 30, 70, 20, 7, 11, 1, 1, 3, 5),
                                  (4, 32, 81, 70, 32, 21, 11, 2, 1, 10, 5),
                                  (2, 8, 40, 60, 16, 7, 11, 3, 1, 3, 5)])
-def test_conv_x6_wgrad_forms(dev, cfg):
+@pytest.mark.parametrize("w64", ["0", "1"])
+def test_conv_x6_wgrad_forms(dev, cfg, w64, monkeypatch):
     """The bf16x6 weight gradients against fp64 torch: the sliding-window form (row strides
     <= 2: sh new x rows per output row into a 6-slot ring; splits that start mid-segment and
     segments of one row, 4 x 70 columns = 3 chunks per row) and the per-row-restaging form
-    (row stride 3)."""
+    (row stride 3).  w64 = 1: the fp16x3 sliding window on 64-column stages (DS2_CONV_W64;
+    200 columns = 4 chunks with a partial last one, 70 = 2)."""
+    monkeypatch.setenv("DS2_CONV_W64", w64)
     n, ci, h, w, co, kh, kw, sh, sw, ph, pw = cfg
     g = torch.Generator().manual_seed(sum(cfg) + 1)
     x = torch.randn(n, ci, h, w, generator=g, dtype=torch.float64)
