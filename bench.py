@@ -166,7 +166,7 @@ class KernelProbe:
         return sum(ms) / len(ms), sum(self.flops) / len(self.flops), len(ms)
 
 
-PMC_SUMMARY = "r9r_pmc_traffic.csv"   # profiles/: PMC passes on the final round-6 tree
+PMC_SUMMARY = "r9z_pmc_traffic.csv"   # profiles/: PMC passes on the final round-6 tree
 
 
 def pmc_traffic_per_launch(prefix="gemm", extra=("splitk_reduce_kernel",)):
